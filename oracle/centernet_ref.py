@@ -1,0 +1,175 @@
+"""Numpy restatement of the CenterNet targets, splat, loss and decode (TEST INFRASTRUCTURE).
+
+Follows /root/reference/CenterNet/tf_centernet_hourglass.py (format_data :379-456, model_loss
+:492-505, nms :44-85, bboxes_iou :22-42) and CenterNet/tf_centernet.py (center_dist_1d/2d :6-19,
+format_data :152-342).  fp32 coordinate math as TF2 eager gives it with an fp32 `img_dim` tensor.
+"""
+import numpy as np
+
+from .fcos_ref import focal_loss, smooth_l1_loss
+
+f32 = np.float32
+
+
+def _sorted_by_area(gt, H, W):
+    if len(gt) <= 1:
+        return gt
+    area = (gt[:, 2] * H) * (gt[:, 3] * W)
+    return gt[np.argsort(area, kind="stable")]
+
+
+def _coords(row, H, W):
+    yc, xc, h, w = row[0], row[1], row[2], row[3]
+    return (f32(f32(yc - f32(0.5) * h) * H), f32(f32(xc - f32(0.5) * w) * W),
+            f32(f32(yc + f32(0.5) * h) * H), f32(f32(xc + f32(0.5) * w) * W))
+
+
+def hourglass_format_data(gt_labels, img_dim, num_classes, img_pad=None, stride=8):
+    """tf_centernet_hourglass.py:379-456: hard one-hot at the centroid cell (Q30)."""
+    gt = np.asarray(gt_labels, dtype=f32)
+    H, W = f32(img_dim[0]), f32(img_dim[1])
+    if img_pad is None:
+        img_pad = (float(H), float(W))
+    hm, wm = int(img_pad[1] / stride), int(img_pad[0] / stride)   # swapped, harmless if square
+    pad_y = int(f32(f32(f32(img_pad[1]) - W) / f32(2.0)))
+    pad_x = int(f32(f32(f32(img_pad[0]) - H) / f32(2.0)))
+    out = np.zeros((hm, wm, num_classes + 4))
+    if len(gt) == 0:
+        return out, 0
+    sf = f32(stride)
+    for row in _sorted_by_area(gt, H, W):
+        c0, c1, c2, c3 = _coords(row, H, W)
+        ycf = f32(f32(c0 + c2) / f32(2.0))
+        xcf = f32(f32(c1 + c3) / f32(2.0))
+        yc = int(f32(f32(f32(pad_y) + ycf) / sf))
+        xc = int(f32(f32(f32(pad_x) + xcf) / sf))
+        off = [f32(f32(yc + 0.5) - f32(f32(f32(pad_y) + c0) / sf)),
+               f32(f32(f32(f32(f32(pad_y) + c2) / sf) - f32(yc)) - f32(0.5)),
+               f32(f32(xc + 0.5) - f32(f32(f32(pad_x) + c1) / sf)),
+               f32(f32(f32(f32(f32(pad_x) + c3) / sf) - f32(xc)) - f32(0.5))]
+        out[yc, xc, :4] = off
+        out[yc, xc, 4 + int(row[4])] = 1.0
+    return out, len(gt)
+
+
+def hourglass_model_loss(y_true, y_pred):
+    """tf_centernet_hourglass.py:492-505 -> (cls, reg)."""
+    y = np.asarray(y_true)
+    p = np.asarray(y_pred)
+    mask = (y[..., 4:].max(-1) > 0).astype(np.float64)
+    return focal_loss(y[..., 4:], p[..., 4:]), smooth_l1_loss(y[..., :4], p[..., :4], mask)
+
+
+def center_dist_1d(grid_x, mu_x=0.0, spread=2.0):
+    """tf_centernet.py:6-10 (inverse power, Q32)."""
+    g = 1.0 / np.power(np.asarray(grid_x, np.float64) - mu_x, spread)
+    return g / g.max()
+
+
+def center_dist_2d(grid_x, grid_y, mu_x=0.0, mu_y=0.0, spread=2.0):
+    """tf_centernet.py:12-19."""
+    gx = 1.0 / np.power(np.asarray(grid_x, np.float64) - mu_x, spread)
+    gy = 1.0 / np.power(np.asarray(grid_y, np.float64) - mu_y, spread)
+    return gx * gy / (gx * gy).max()
+
+
+def splat_format_data(gt_labels, img_dim, num_classes, img_pad=None, stride=8, sigma=0.25):
+    """tf_centernet.py:152-342: ltrb over the sigma sub-box + inverse-power centre splat in ch4."""
+    gt = np.asarray(gt_labels, dtype=f32)
+    H, W = f32(img_dim[0]), f32(img_dim[1])
+    if img_pad is None:
+        img_pad = (float(H), float(W))
+    sf = f32(stride)
+    hr, wr = f32(H / sf), f32(W / sf)
+    Hs, Ws = int(img_pad[0] / stride), int(img_pad[1] / stride)
+    ylim, xlim = int(f32(H / sf)), int(f32(W / sf))
+    out = np.zeros((Hs, Ws, num_classes + 5))
+    spread = 8.0                                                # :206-207 (tmp_std forced to 8)
+    sg = f32(sigma)
+    for row in _sorted_by_area(gt, H, W):
+        c0, c1, c2, c3 = _coords(row, H, W)
+        t0, t1, t2, t3 = f32(c0 / sf), f32(c1 / sf), f32(c2 / sf), f32(c3 / sf)
+        ycen = int(f32(row[0] * hr))
+        xcen = int(f32(row[1] * wr))
+        ylo = max(0, 1 + int(f32(f32(row[0] - f32(sg * row[2]) / f32(2)) * hr)))
+        xlo = max(0, 1 + int(f32(f32(row[1] - f32(sg * row[3]) / f32(2)) * wr)))
+        yup = min(1 + int(f32(f32(row[0] + f32(sg * row[2]) / f32(2)) * hr)), ylim)
+        xup = min(1 + int(f32(f32(row[1] + f32(sg * row[3]) / f32(2)) * wr)), xlim)
+        k = 5 + int(row[4])
+        if yup - ylo > 0 and xup - xlo > 0:
+            gyd = np.arange(ylo, yup, dtype=np.float64) + 0.5
+            gxd = np.arange(xlo, xup, dtype=np.float64) + 0.5
+            gx, gy = np.meshgrid(gxd, gyd)
+            gy32, gx32 = gy.astype(f32), gx.astype(f32)
+            reg = out[ylo:yup, xlo:xup]
+            reg[..., 0] = np.maximum(f32(0), gy32 - t0)
+            reg[..., 1] = np.maximum(f32(0), t2 - gy32)
+            reg[..., 2] = np.maximum(f32(0), gx32 - t1)
+            reg[..., 3] = np.maximum(f32(0), t3 - gx32)
+            nx, ny = int(0.5 * (xlo + xup)), int(0.5 * (ylo + yup))
+            reg[..., 4] = center_dist_2d(gx, gy, nx, ny, spread)
+            out[ny, nx, 4] = 1.0
+            reg[..., k] = 1
+        elif yup - ylo > 0:
+            gyd = np.arange(ylo, yup, dtype=np.float64) + 0.5
+            col = out[ylo:yup, xcen]
+            col[:, 0] = np.maximum(f32(0), gyd.astype(f32) - t0)
+            col[:, 1] = np.maximum(f32(0), t2 - gyd.astype(f32))
+            col[:, 2] = max(f32(0), f32(f32(xcen + 0.5) - t1))
+            col[:, 3] = max(f32(0), f32(f32(t3 - f32(xcen)) - f32(0.5)))
+            ny = int(0.5 * (ylo + yup))
+            col[:, 4] = center_dist_1d(gyd, ny, spread)
+            out[ny, xcen, 4] = 1.0
+            col[:, k] = 1
+        elif xup - xlo > 0:
+            gxd = np.arange(xlo, xup, dtype=np.float64) + 0.5
+            rw = out[ycen, xlo:xup]
+            rw[:, 0] = max(f32(0), f32(f32(ycen + 0.5) - t0))
+            rw[:, 1] = max(f32(0), f32(f32(t2 - f32(ycen)) - f32(0.5)))
+            rw[:, 2] = np.maximum(f32(0), gxd.astype(f32) - t1)
+            rw[:, 3] = np.maximum(f32(0), t3 - gxd.astype(f32))
+            nx = int(0.5 * (xlo + xup))
+            rw[:, 4] = center_dist_1d(gxd, nx, spread)
+            out[ycen, nx, 4] = 1.0
+            rw[:, k] = 1
+        else:
+            cell = out[ycen, xcen]
+            cell[0] = max(f32(0), f32(f32(ycen + 0.5) - t0))
+            cell[1] = max(f32(0), f32(f32(t2 - f32(ycen)) - f32(0.5)))
+            cell[2] = max(f32(0), f32(f32(xcen + 0.5) - t1))
+            cell[3] = max(f32(0), f32(f32(t3 - f32(xcen)) - f32(0.5)))
+            cell[4] = 1
+            cell[k] = 1
+    return out
+
+
+def bboxes_iou(b1, b2):
+    """tf_centernet_hourglass.py:22-42 (corner format, float64, floor at fp32 eps)."""
+    b1 = np.asarray(b1, np.float64)
+    b2 = np.asarray(b2, np.float64)
+    a1 = (b1[..., 2] - b1[..., 0]) * (b1[..., 3] - b1[..., 1])
+    a2 = (b2[..., 2] - b2[..., 0]) * (b2[..., 3] - b2[..., 1])
+    lu = np.maximum(b1[..., :2], b2[..., :2])
+    rd = np.minimum(b1[..., 2:], b2[..., 2:])
+    it = np.maximum(rd - lu, 0.0)
+    inter = it[..., 0] * it[..., 1]
+    return np.maximum(inter / (a1 + a2 - inter), np.finfo(np.float32).eps)
+
+
+def nms(bboxes, iou_threshold):
+    """tf_centernet_hourglass.py:44-85, method='nms'. Input rows (x, y, w, h, score, cls)."""
+    bb = np.array(bboxes, np.float64)
+    bb[:, 2] = bb[:, 0] + bb[:, 2]
+    bb[:, 3] = bb[:, 1] + bb[:, 3]
+    best = []
+    for c in list(set(bb[:, 5])):                 # python set order, as the reference
+        cb = bb[bb[:, 5] == c]
+        while len(cb) > 0:
+            i = int(np.argmax(cb[:, 4]))
+            b = cb[i]
+            best.append(b.copy())
+            cb = np.concatenate([cb[:i], cb[i + 1:]])
+            iou = bboxes_iou(b[np.newaxis, :4], cb[:, :4])
+            keep = ~(iou > iou_threshold)
+            cb = cb[keep & (cb[:, 4] > 0)]
+    return np.array(best, np.float64).reshape(-1, 6)

@@ -1,0 +1,254 @@
+#!/usr/bin/env python3
+"""Generate golden input/output vectors by executing the REFERENCE's own numpy-level functions.
+
+TEST INFRASTRUCTURE ONLY — run in the build container, where /root/reference exists:
+
+    python tests/golden/make_golden.py            # writes tests/golden/*.npz
+
+What runs: the reference's `FCOS/fcos.py` (`format_data`, `model_loss`, `focal_loss`,
+`smooth_l1_loss`, `iou_loss`), `RetinaNet/retinanet_module.py` (`RetinaNet.__init__` anchor dims,
+`get_anchors`, `format_data`), `RetinaNet/utils.py:compute_iou`,
+`CenterNet/tf_centernet_hourglass.py` (`format_data`, `model_loss`, `nms`, `bboxes_iou`) and
+`CenterNet/tf_centernet.py` (`center_dist_1d/2d`, `format_data`), imported from /root/reference with
+`tests/golden/tfstub` (numpy stand-ins for TF's elementwise ops, see its docstring) first on
+sys.path.  TensorFlow itself is not installed in this image (ordinary ModuleNotFoundError, see
+SURVEY.md §8c).  No reference source is copied: only inputs/outputs are written.
+
+Each detector family runs in its own subprocess because FCOS/ and RetinaNet/ both ship modules
+named `utils` / `data_preprocess`.
+"""
+import json
+import os
+import subprocess
+import sys
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+STUB = os.path.join(HERE, "tfstub")
+REF = os.environ.get("CVL_REFERENCE", "/root/reference")
+
+
+# ----------------------------------------------------------------------------------------------
+# synthetic VOC/COCO-shaped boxes (SURVEY.md §8d generator, widened to cover edge cases)
+# ----------------------------------------------------------------------------------------------
+def synth_boxes(rng, img_h, img_w, n_classes, lam=1.4, nmax=16, side_lo=2.0, side_hi=480.0,
+                edge_frac=0.15):
+    """Normalised (yc, xc, h, w, cls) float32 rows, distinct areas, optional border-touching."""
+    n = int(min(max(1 + rng.poisson(lam), 1), nmax))
+    rows, areas = [], set()
+    while len(rows) < n:
+        h = float(np.exp(rng.uniform(np.log(side_lo), np.log(min(side_hi, img_h)))))
+        w = float(np.exp(rng.uniform(np.log(side_lo), np.log(min(side_hi, img_w)))))
+        if rng.uniform() < edge_frac:      # touch a border exactly / straddle it slightly
+            yc = h / 2.0 if rng.uniform() < 0.5 else img_h - h / 2.0
+            xc = rng.uniform(w / 2.0, img_w - w / 2.0)
+            if rng.uniform() < 0.3:
+                yc -= rng.uniform(0.0, 6.0)
+        else:
+            yc = rng.uniform(h / 2.0, img_h - h / 2.0)
+            xc = rng.uniform(w / 2.0, img_w - w / 2.0)
+        r = np.array([yc / img_h, xc / img_w, h / img_h, w / img_w,
+                      rng.integers(0, n_classes)], dtype=np.float32)
+        a = float(np.float32(r[2] * np.float32(img_h)) * np.float32(r[3] * np.float32(img_w)))
+        if a in areas:
+            continue
+        areas.add(a)
+        rows.append(r)
+    return np.stack(rows).astype(np.float32)
+
+
+# ----------------------------------------------------------------------------------------------
+# child-process workers (run with the stub + one reference family dir on sys.path)
+# ----------------------------------------------------------------------------------------------
+def _child_setup(family):
+    sys.path.insert(0, os.path.join(REF, family))
+    sys.path.insert(0, STUB)
+    np.int = int  # reference RetinaNet/retinanet_module.py:303 uses np.int (removed in numpy>=1.24)
+    import tensorflow as tf  # the stub
+    return tf
+
+
+def work_fcos(out_path):
+    tf = _child_setup("FCOS")
+    import fcos as ref
+    rng = np.random.default_rng(20250218)
+    C = 20
+    # (img_dim, img_pad): square bench case, jittered non-square cases padded to x128 squares
+    dims = [((512.0, 512.0), (512, 512))] * 24 + [
+        ((300.0, 384.0), (384, 384)), ((384.0, 256.0), (384, 384)), ((240.0, 320.0), (384, 384)),
+        ((384.0, 384.0), (384, 384)), ((256.0, 256.0), (256, 256)), ((200.0, 256.0), (256, 256)),
+        ((128.0, 128.0), (128, 128)), ((333.0, 251.0), (384, 384))] * 4
+    assign = {"n_images": len(dims), "C": C}
+    arrays = {}
+    for i, (dim, pad) in enumerate(dims):
+        H, W = dim
+        boxes = synth_boxes(rng, H, W, C)
+        img_dim = tf.constant(np.array(dim, dtype=np.float32))
+        gt = tf.constant(boxes)
+        outs, ntgt = ref.format_data(gt, img_dim, C, img_pad=list(pad))
+        arrays["assign_%d_boxes" % i] = boxes
+        arrays["assign_%d_img_dim" % i] = np.array(dim, dtype=np.float32)
+        arrays["assign_%d_img_pad" % i] = np.array(pad, dtype=np.int32)
+        arrays["assign_%d_ntgt" % i] = np.array(ntgt, dtype=np.int32)
+        for l, o in enumerate(outs):
+            arrays["assign_%d_L%d" % (i, l)] = np.asarray(o)
+    # losses on reference targets + random logits (fp32), l1 and iou
+    loss_imgs = [0, 1, 28, 30, 36, 38, 44, 46]
+    assign["loss_imgs"] = loss_imgs
+    for i in loss_imgs:
+        tgt = [arrays["assign_%d_L%d" % (i, l)] for l in range(5)]
+        preds = []
+        for l in range(5):
+            S = tgt[l].shape
+            p = rng.normal(0.0, 1.5, size=(1, S[0], S[1], 5 + C)).astype(np.float32)
+            p[..., :4] = np.abs(p[..., :4]) * 3.0
+            preds.append(p)
+        res = {}
+        for reg_type in ("l1", "iou"):
+            cls, reg, cen = ref.model_loss(tgt, [tf.constant(p) for p in preds],
+                                           [8, 16, 32, 64, 128], reg_type=reg_type, cls_lambda=1.0)
+            res[reg_type] = np.array([float(cls), float(reg), float(cen)], dtype=np.float64)
+        for l in range(5):
+            arrays["loss_%d_pred_L%d" % (i, l)] = preds[l]
+        arrays["loss_%d_l1" % i] = res["l1"]
+        arrays["loss_%d_iou" % i] = res["iou"]
+    # elementwise loss functions on random inputs
+    x = rng.normal(0, 3, size=(7, 9, 11)).astype(np.float32)
+    y = (rng.uniform(size=(7, 9, 11)) < 0.2).astype(np.float64)
+    arrays["focal_x"] = x
+    arrays["focal_y"] = y
+    arrays["focal_out"] = np.float64(float(ref.focal_loss(y, tf.constant(x))))
+    a = rng.normal(0, 1.5, size=(6, 5, 4)).astype(np.float32)
+    b = rng.normal(0, 1.5, size=(6, 5, 4)).astype(np.float64)
+    m = (rng.uniform(size=(6, 5)) < 0.5).astype(np.float32)
+    arrays["sl1_pred"] = a
+    arrays["sl1_true"] = b
+    arrays["sl1_mask"] = m
+    arrays["sl1_out"] = np.float64(float(ref.smooth_l1_loss(b, tf.constant(a),
+                                                            mask=tf.constant(m))))
+    arrays["sl1_out_nomask"] = np.float64(float(ref.smooth_l1_loss(b, tf.constant(a))))
+    # decode helper (fcos.py:112-134)
+    xy = np.abs(rng.normal(0, 2, size=(6, 7, 4))).astype(np.float32)
+    arrays["p2c_in"] = xy
+    arrays["p2c_out"] = np.asarray(ref.prediction_to_corners(tf.constant(xy), 16))
+    np.savez_compressed(out_path, meta=json.dumps(assign), **arrays)
+
+
+def work_retina(out_path):
+    tf = _child_setup("RetinaNet")
+    import retinanet_module as rm
+    import utils as rutils
+    rm.build_model = lambda *a, **k: None      # model layers are not part of the golden
+    rng = np.random.default_rng(77)
+    C = 80
+    arrays = {}
+    cases = [(640, [20.0, 40.0, 80.0, 160.0, 320.0])] * 3 + \
+            [(512, None)] * 2 + [(256, [20.0, 40.0, 80.0, 160.0, 320.0])] * 8 + \
+            [(320, [20.0, 40.0, 80.0, 160.0, 320.0])] * 4
+    for i, (D, sizes) in enumerate(cases):
+        net = rm.RetinaNet(C, {k: str(k) for k in range(C)}, anchor_sizes=sizes)
+        dims = np.array([[float(np.asarray(v)) for v in np.asarray(ab, dtype=np.float64)]
+                         for lev in net.anchor_boxes for ab in lev], dtype=np.float64)
+        boxes = synth_boxes(rng, float(D), float(D), C, lam=6.3, nmax=50, side_lo=8.0,
+                            side_hi=float(D), edge_frac=0.1)
+        img_dim = tf.constant(np.array([D, D], dtype=np.float32))
+        outs, ntgt = net.format_data(tf.constant(boxes), img_dim, iou_thresh=0.5, img_pad=[D, D])
+        arrays["case_%d_D" % i] = np.int32(D)
+        arrays["case_%d_sizes" % i] = np.array(net.anchor_sizes, dtype=np.float64)
+        arrays["case_%d_anchor_dims" % i] = dims.reshape(5, 9, 2)
+        arrays["case_%d_boxes" % i] = boxes
+        arrays["case_%d_ntgt" % i] = np.int64(ntgt)
+        for l in range(5):
+            arrays["case_%d_L%d" % (i, l)] = np.stack([np.asarray(o) for o in outs[l]])
+        if i == 0:
+            anc = net.get_anchors([5, 5], 4)
+            arrays["get_anchors_5x5_L4"] = np.stack([np.asarray(a) for a in anc])
+    b1 = np.abs(rng.normal(50, 20, size=(7, 4))).astype(np.float32)
+    b2 = np.abs(rng.normal(50, 20, size=(13, 4))).astype(np.float32)
+    arrays["iou_b1"] = b1
+    arrays["iou_b2"] = b2
+    arrays["iou_out"] = np.asarray(rutils.compute_iou(b1, b2))
+    np.savez_compressed(out_path, **arrays)
+
+
+def work_centernet(out_path):
+    tf = _child_setup("CenterNet")
+    import tf_centernet_hourglass as hg
+    import tf_centernet as cs
+    rng = np.random.default_rng(4242)
+    C = 20
+    arrays = {}
+    for i in range(16):
+        D = 512.0 if i < 10 else 384.0
+        stride = 4 if i % 2 == 0 else 8
+        boxes = synth_boxes(rng, D, D, C, lam=2.4, nmax=20, side_lo=3.0, side_hi=D)
+        out, n = hg.format_data(tf.constant(boxes), tf.constant(np.array([D, D], np.float32)), C,
+                                img_pad=[int(D), int(D)], stride=stride)
+        arrays["hg_%d_boxes" % i] = boxes
+        arrays["hg_%d_D" % i] = np.float32(D)
+        arrays["hg_%d_stride" % i] = np.int32(stride)
+        arrays["hg_%d_out" % i] = np.asarray(out)
+        arrays["hg_%d_n" % i] = np.int32(n)
+    for i in range(6):
+        S = 32 if i < 3 else 16
+        y = np.zeros((2, S, S, 4 + C), np.float64)
+        y[..., :4] = rng.uniform(0, 3, size=(2, S, S, 4))
+        cls_on = rng.uniform(size=(2, S, S)) < 0.05
+        y[..., 4:][cls_on, 0] = 1.0
+        p = rng.normal(0, 1.5, size=(2, S, S, 4 + C)).astype(np.float32)
+        c, r = hg.model_loss(y, tf.constant(p))
+        arrays["hgloss_%d_y" % i] = y
+        arrays["hgloss_%d_p" % i] = p
+        arrays["hgloss_%d_out" % i] = np.array([float(c), float(r)], np.float64)
+    for i in range(12):
+        D = 512.0 if i < 8 else 384.0
+        boxes = synth_boxes(rng, D, D, C, lam=2.4, nmax=20, side_lo=3.0, side_hi=D)
+        out = cs.format_data(tf.constant(boxes), tf.constant(np.array([D, D], np.float32)), C,
+                             img_pad=[int(D), int(D)], stride=8)
+        arrays["splat_%d_boxes" % i] = boxes
+        arrays["splat_%d_D" % i] = np.float32(D)
+        arrays["splat_%d_out" % i] = np.asarray(out)
+    gx = np.arange(3, 9, dtype=np.float64) + 0.5
+    gy = np.arange(10, 14, dtype=np.float64) + 0.5
+    mx, my = np.meshgrid(gx, gy)
+    arrays["cd2_gx"] = mx
+    arrays["cd2_gy"] = my
+    arrays["cd2_out"] = np.asarray(cs.center_dist_2d(mx, my, mu_x=5, mu_y=12, spread=8.0))
+    arrays["cd1_out"] = np.asarray(cs.center_dist_1d(gx, mu_x=6, spread=8.0))
+    # nms on random (x, y, w, h, score%, cls) rows: reference nms mutates its input
+    for i in range(8):
+        n = 40
+        xy = rng.uniform(0, 300, size=(n, 2))
+        wh = rng.uniform(10, 120, size=(n, 2))
+        sc = rng.integers(50, 100, size=(n, 1)).astype(np.float64)
+        cl = rng.integers(0, 3, size=(n, 1)).astype(np.float64)
+        bb = np.concatenate([xy, wh, sc, cl], axis=1)
+        arrays["nms_%d_in" % i] = bb.copy()
+        res = hg.nms(bb.copy(), 0.213, method="nms")
+        arrays["nms_%d_out" % i] = np.array(res, dtype=np.float64).reshape(-1, 6)
+    np.savez_compressed(out_path, **arrays)
+
+
+WORKERS = {"fcos": work_fcos, "retinanet": work_retina, "centernet": work_centernet}
+
+
+def main():
+    if len(sys.argv) == 3 and sys.argv[1] in WORKERS:
+        WORKERS[sys.argv[1]](sys.argv[2])
+        return
+    if not os.path.isdir(REF):
+        print("reference not present at %s: nothing to do" % REF)
+        return
+    for fam in WORKERS:
+        out = os.path.join(HERE, "golden_%s.npz" % fam)
+        subprocess.check_call([sys.executable, os.path.abspath(__file__), fam, out])
+        print("wrote", out, os.path.getsize(out), "bytes")
+    with open(os.path.join(HERE, "GOLDEN_INFO.json"), "w") as f:
+        json.dump({"numpy": np.__version__, "python": sys.version.split()[0],
+                   "generator": "tests/golden/make_golden.py",
+                   "reference": "WD-Leong/CV-Lite-Object-Detection @ 2025-02-18"}, f, indent=1)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,81 @@
+"""Pin the CPU oracle (oracle/*.py) to golden vectors produced by the reference's own functions
+(tests/golden/make_golden.py).  Bit-exact for targets / indices / anchors; 1e-6 relative for
+float losses (the goldens were computed with fp32 numpy elementwise ops, the oracle in float64)."""
+import json
+
+import numpy as np
+import pytest
+
+from oracle import centernet_ref, fcos_ref, retina_ref
+
+
+def test_fcos_format_data_bit_exact(golden):
+    d = golden("fcos")
+    meta = json.loads(str(d["meta"]))
+    branches = 0
+    for i in range(meta["n_images"]):
+        outs, nt = fcos_ref.format_data(d["assign_%d_boxes" % i], d["assign_%d_img_dim" % i],
+                                        meta["C"], img_pad=tuple(int(x) for x in d["assign_%d_img_pad" % i]))
+        assert list(nt) == list(d["assign_%d_ntgt" % i])
+        for l in range(5):
+            np.testing.assert_array_equal(outs[l], d["assign_%d_L%d" % (i, l)])
+        branches += sum(int(o[..., 5:].sum() > 0) for o in outs)
+    assert branches > 40
+
+
+def test_fcos_losses(golden):
+    d = golden("fcos")
+    meta = json.loads(str(d["meta"]))
+    for i in meta["loss_imgs"]:
+        tgt = [d["assign_%d_L%d" % (i, l)] for l in range(5)]
+        pr = [d["loss_%d_pred_L%d" % (i, l)] for l in range(5)]
+        for rt in ("l1", "iou"):
+            np.testing.assert_allclose(fcos_ref.model_loss(tgt, pr, reg_type=rt), d["loss_%d_%s" % (i, rt)],
+                                       rtol=1e-6)
+    np.testing.assert_allclose(fcos_ref.focal_loss(d["focal_y"], d["focal_x"]), d["focal_out"], rtol=1e-6)
+    np.testing.assert_allclose(fcos_ref.smooth_l1_loss(d["sl1_true"], d["sl1_pred"], d["sl1_mask"]),
+                               d["sl1_out"], rtol=1e-6)
+    np.testing.assert_allclose(fcos_ref.smooth_l1_loss(d["sl1_true"], d["sl1_pred"]), d["sl1_out_nomask"],
+                               rtol=1e-6)
+    np.testing.assert_array_equal(fcos_ref.prediction_to_corners(d["p2c_in"], 16), d["p2c_out"])
+
+
+def test_retinanet_anchor_and_match_bit_exact(golden):
+    d = golden("retinanet")
+    i = 0
+    while "case_%d_D" % i in d:
+        D = int(d["case_%d_D" % i])
+        dims = retina_ref.anchor_dims(list(d["case_%d_sizes" % i]))
+        np.testing.assert_array_equal(dims.astype(np.float64), d["case_%d_anchor_dims" % i])
+        outs, n = retina_ref.format_data(d["case_%d_boxes" % i], np.array([D, D], np.float32), dims, 80,
+                                         img_pad=[D, D])
+        assert n == int(d["case_%d_ntgt" % i])
+        for l in range(5):
+            np.testing.assert_array_equal(np.stack(outs[l]), d["case_%d_L%d" % (i, l)])
+        i += 1
+    assert i >= 10
+    dims = retina_ref.anchor_dims([20.0, 40.0, 80.0, 160.0, 320.0])
+    np.testing.assert_array_equal(np.stack(retina_ref.get_anchors(dims, [5, 5], 4)), d["get_anchors_5x5_L4"])
+    np.testing.assert_array_equal(retina_ref.compute_iou(d["iou_b1"], d["iou_b2"]), d["iou_out"])
+
+
+def test_centernet_targets_splat_nms(golden):
+    d = golden("centernet")
+    for i in range(16):
+        D = float(d["hg_%d_D" % i])
+        o, n = centernet_ref.hourglass_format_data(d["hg_%d_boxes" % i], np.array([D, D], np.float32), 20,
+                                                   img_pad=[int(D), int(D)], stride=int(d["hg_%d_stride" % i]))
+        np.testing.assert_array_equal(o, d["hg_%d_out" % i])
+        assert n == int(d["hg_%d_n" % i])
+    for i in range(6):
+        np.testing.assert_allclose(centernet_ref.hourglass_model_loss(d["hgloss_%d_y" % i], d["hgloss_%d_p" % i]),
+                                   d["hgloss_%d_out" % i], rtol=1e-6)
+    for i in range(12):
+        D = float(d["splat_%d_D" % i])
+        o = centernet_ref.splat_format_data(d["splat_%d_boxes" % i], np.array([D, D], np.float32), 20,
+                                            img_pad=[int(D), int(D)])
+        np.testing.assert_array_equal(o, d["splat_%d_out" % i])
+    np.testing.assert_array_equal(centernet_ref.center_dist_2d(d["cd2_gx"], d["cd2_gy"], 5, 12, 8.0), d["cd2_out"])
+    np.testing.assert_array_equal(centernet_ref.center_dist_1d(np.arange(3, 9) + 0.5, 6, 8.0), d["cd1_out"])
+    for i in range(8):
+        np.testing.assert_array_equal(centernet_ref.nms(d["nms_%d_in" % i], 0.213), d["nms_%d_out" % i])
