@@ -1,0 +1,43 @@
+// cvlite — shared helpers for the gfx950 kernels behind include/cvlite.h.
+// Internal header: not part of the C ABI.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/cvlite.h"
+
+#define CVL_CHECK_ARG(cond) \
+  do {                      \
+    if (!(cond)) return CVL_EINVAL; \
+  } while (0)
+
+static inline int cvl_launch_status() {
+  hipError_t e = hipGetLastError();
+  return e == hipSuccess ? CVL_OK : (CVL_EHIP + (int)e);
+}
+
+// ---- bf16 helpers (bit-level; round-to-nearest-even, NaN-preserving) ------------------------
+typedef uint16_t cvl_bf16;
+
+__device__ __forceinline__ float bf16_to_f32(cvl_bf16 h) {
+  return __uint_as_float(((uint32_t)h) << 16);
+}
+
+__device__ __forceinline__ cvl_bf16 f32_to_bf16(float f) {
+  uint32_t u = __float_as_uint(f);
+  if ((u & 0x7f800000u) == 0x7f800000u && (u & 0x007fffffu)) return (cvl_bf16)((u >> 16) | 0x40);
+  u += 0x7fffu + ((u >> 16) & 1u);
+  return (cvl_bf16)(u >> 16);
+}
+
+__device__ __forceinline__ float warp_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+__device__ __forceinline__ double warp_sum_d(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}

@@ -1,0 +1,172 @@
+// Fused FCOS loss forward + backward on gfx950 — restates FCOS/fcos.py:380-496.
+//
+//   cls = sum focal(targets[5:], cls_logits)            (fcos.py:443-462, alpha .25, gamma 2)
+//   cen = sum smoothL1(targets[4], sigmoid(reg[4]))     over ALL cells (fcos.py:483-486, Q10)
+//   reg = sum mask * smoothL1(targets[:4], reg[:4])     (l1)  or  -log IoU (iou, fcos.py:393-441)
+//   mask = max(targets[5:]) >= 1                        (fcos.py:475-477)
+// "smooth L1" is the reference's discontinuous 0.5 d^2 (|d|<1) / |d| (Q8).  One pass reads the
+// predictions and targets once and writes the gradients once (HBM-bound); per-image sums are
+// reduced deterministically (per-tile partials in float64, then a fixed-order second pass).
+#include "cvl_common.h"
+
+namespace {
+
+constexpr int kThreads = 256;
+
+struct LossArgs {
+  const float* reg;
+  const float* cls;
+  const float* tgt;
+  float* losses;
+  void* dreg;
+  void* dcls;
+  double* partial;   // [B, tiles, 3]
+  int ld_reg, ld_cls, ld_dreg, ld_dcls, dreg_bf16, dcls_bf16;
+  int P, C, reg_type, tiles;
+  float grad_scale;
+};
+
+__device__ __forceinline__ void store_g(void* base, size_t idx, float v, int is_bf16) {
+  if (is_bf16) reinterpret_cast<cvl_bf16*>(base)[idx] = f32_to_bf16(v);
+  else reinterpret_cast<float*>(base)[idx] = v;
+}
+
+__device__ __forceinline__ float sl1(float d, float* g) {
+  // loss of d = t - x and its derivative w.r.t. x (TF gradient of the tf.where form)
+  const float ad = fabsf(d);
+  if (ad < 1.0f) { *g = -d; return 0.5f * d * d; }
+  *g = d > 0.f ? -1.0f : (d < 0.f ? 1.0f : 0.0f);
+  return ad;
+}
+
+__global__ void __launch_bounds__(kThreads) fcos_loss_kernel(LossArgs a) {
+  const int b = blockIdx.y;
+  const int p = blockIdx.x * kThreads + threadIdx.x;
+  float s_cls = 0.f, s_reg = 0.f, s_cen = 0.f;
+  if (p < a.P) {
+    const size_t cell = (size_t)b * a.P + p;
+    const float* t = a.tgt + cell * (5 + a.C);
+    const float* xr = a.reg + cell * a.ld_reg;
+    const float* xc = a.cls + cell * a.ld_cls;
+    const float alpha = 0.25f;
+    float tmax = 0.f;
+    for (int c = 0; c < a.C; ++c) {
+      const float y = t[5 + c];
+      tmax = fmaxf(tmax, y);
+      const float x = xc[c];
+      const float e = expf(-fabsf(x));
+      const float L = log1pf(e);                       // log(1 + exp(-|x|))
+      const float p1 = x >= 0.f ? 1.0f / (1.0f + e) : e / (1.0f + e);   // sigmoid(x)
+      const float q1 = x >= 0.f ? e / (1.0f + e) : 1.0f / (1.0f + e);   // 1 - sigmoid(x)
+      const float nlp = L - fminf(x, 0.f);             // -log p
+      const float nlq = L + fmaxf(x, 0.f);             // -log(1-p)
+      const float wpos = y * alpha * q1 * q1;
+      const float wneg = (1.0f - y) * (1.0f - alpha) * p1 * p1;
+      s_cls += wpos * nlp + wneg * nlq;
+      if (a.dcls) {
+        const float g = -y * alpha * q1 * q1 * (2.0f * p1 * nlp + q1) +
+                        (1.0f - y) * (1.0f - alpha) * p1 * p1 * (2.0f * q1 * nlq + p1);
+        store_g(a.dcls, cell * a.ld_dcls + c, g * a.grad_scale, a.dcls_bf16);
+      }
+    }
+    if (a.dcls)
+      for (int c = a.C; c < a.ld_dcls; ++c) store_g(a.dcls, cell * a.ld_dcls + c, 0.f, a.dcls_bf16);
+    const float mask = tmax >= 1.0f ? 1.0f : 0.0f;
+    float g[5] = {0.f, 0.f, 0.f, 0.f, 0.f};
+    // centerness: smooth-L1 on sigmoid(logit), all cells
+    {
+      const float x = xr[4];
+      const float sg = 1.0f / (1.0f + expf(-x));
+      float gd;
+      s_cen += sl1(t[4] - sg, &gd);
+      g[4] = gd * sg * (1.0f - sg);
+    }
+    if (a.reg_type == 0) {
+      for (int j = 0; j < 4; ++j) {
+        float gd;
+        const float l = sl1(t[j] - xr[j], &gd);
+        s_reg += mask * l;
+        g[j] = mask * gd;
+      }
+    } else if (mask != 0.f) {
+      // IoU of ltrb boxes about the same grid point (grid offsets cancel)
+      const float t0 = t[0], t1 = t[1], t2 = t[2], t3 = t[3];
+      const float p0 = xr[0], p1 = xr[1], p2 = xr[2], p3 = xr[3];
+      const float th = t0 + t1, tw = t2 + t3, ph = p0 + p1, pw = p2 + p3;
+      const float ihr = fminf(t1, p1) + fminf(t0, p0);
+      const float iwr = fminf(t3, p3) + fminf(t2, p2);
+      const float ih = fmaxf(ihr, 0.f), iw = fmaxf(iwr, 0.f);
+      const float I = ih * iw;
+      const float Ue = th * tw + ph * pw - I + 1.0e-12f;
+      const float iou = I / Ue;
+      s_reg += -logf(iou + 1.0e-12f);
+      const float dL = -1.0f / (iou + 1.0e-12f);
+      const float dI = (Ue + I) / (Ue * Ue);            // d iou / d I (U depends on -I)
+      const float dph = -I * pw / (Ue * Ue), dpw = -I * ph / (Ue * Ue);
+      const float gih = ihr > 0.f ? dI * iw : 0.f;
+      const float giw = iwr > 0.f ? dI * ih : 0.f;
+      g[0] = dL * ((p0 < t0 ? gih : 0.f) + dph);
+      g[1] = dL * ((p1 < t1 ? gih : 0.f) + dph);
+      g[2] = dL * ((p2 < t2 ? giw : 0.f) + dpw);
+      g[3] = dL * ((p3 < t3 ? giw : 0.f) + dpw);
+    }
+    if (a.dreg) {
+      for (int j = 0; j < 5; ++j) store_g(a.dreg, cell * a.ld_dreg + j, g[j] * a.grad_scale, a.dreg_bf16);
+      for (int j = 5; j < a.ld_dreg; ++j) store_g(a.dreg, cell * a.ld_dreg + j, 0.f, a.dreg_bf16);
+    }
+  }
+  // deterministic block reduction in float64
+  __shared__ double red[3][kThreads / 64];
+  double v0 = warp_sum_d((double)s_cls), v1 = warp_sum_d((double)s_reg), v2 = warp_sum_d((double)s_cen);
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  if (lane == 0) { red[0][w] = v0; red[1][w] = v1; red[2][w] = v2; }
+  __syncthreads();
+  if (threadIdx.x < 3) {
+    double s = 0.0;
+    for (int k = 0; k < kThreads / 64; ++k) s += red[threadIdx.x][k];
+    a.partial[((size_t)b * a.tiles + blockIdx.x) * 3 + threadIdx.x] = s;
+  }
+}
+
+__global__ void fcos_loss_finalize(const double* partial, float* losses, int tiles) {
+  const int b = blockIdx.x;
+  const int k = threadIdx.x;   // 0..2
+  if (k < 3) {
+    double s = 0.0;
+    for (int i = 0; i < tiles; ++i) s += partial[((size_t)b * tiles + i) * 3 + k];
+    losses[b * 3 + k] = (float)s;
+  }
+}
+
+}  // namespace
+
+extern "C" size_t cvl_fcos_loss_workspace_size(int B, int P) {
+  const size_t tiles = (size_t)(P + kThreads - 1) / kThreads;
+  return (size_t)B * tiles * 3 * sizeof(double);
+}
+
+extern "C" int cvl_fcos_loss(const float* reg_pred, int ld_reg, const float* cls_pred, int ld_cls,
+                             const float* targets, int B, int P, int num_classes, int reg_type,
+                             float grad_scale, float* losses, void* d_reg, int ld_dreg,
+                             int dreg_dtype, void* d_cls, int ld_dcls, int dcls_dtype,
+                             void* workspace, cvl_stream_t stream) {
+  CVL_CHECK_ARG(reg_pred && cls_pred && targets && losses && workspace);
+  CVL_CHECK_ARG(B > 0 && P > 0 && num_classes > 0 && ld_reg >= 5 && ld_cls >= num_classes);
+  CVL_CHECK_ARG(reg_type == 0 || reg_type == 1);
+  CVL_CHECK_ARG(!d_reg || ld_dreg >= 5);
+  CVL_CHECK_ARG(!d_cls || ld_dcls >= num_classes);
+  CVL_CHECK_ARG((dreg_dtype == 0 || dreg_dtype == 1) && (dcls_dtype == 0 || dcls_dtype == 1));
+  LossArgs a;
+  a.reg = reg_pred; a.cls = cls_pred; a.tgt = targets; a.losses = losses;
+  a.dreg = d_reg; a.dcls = d_cls; a.partial = (double*)workspace;
+  a.ld_reg = ld_reg; a.ld_cls = ld_cls; a.ld_dreg = ld_dreg; a.ld_dcls = ld_dcls;
+  a.dreg_bf16 = dreg_dtype; a.dcls_bf16 = dcls_dtype;
+  a.P = P; a.C = num_classes; a.reg_type = reg_type; a.grad_scale = grad_scale;
+  a.tiles = (P + kThreads - 1) / kThreads;
+  hipLaunchKernelGGL(fcos_loss_kernel, dim3(a.tiles, B), dim3(kThreads), 0, (hipStream_t)stream, a);
+  int st = cvl_launch_status();
+  if (st) return st;
+  hipLaunchKernelGGL(fcos_loss_finalize, dim3(B), dim3(64), 0, (hipStream_t)stream,
+                     (const double*)workspace, losses, a.tiles);
+  return cvl_launch_status();
+}

@@ -1,0 +1,74 @@
+"""ctypes binding of the cvlite C ABI (include/cvlite.h) -> libcvlite_hip.so (built in-tree).
+
+torch is imported first on purpose: it loads its bundled HIP runtime (soname libamdhip64.so.7),
+and the library then binds to that same runtime instance, so torch's hipStream_t handles and
+device pointers are valid inside it.  There is no CPU fallback: every op fails loudly when the
+library or the GPU is missing.
+"""
+import ctypes
+import os
+
+import torch  # noqa: F401  (must precede the CDLL load, see module docstring)
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libcvlite_hip.so")
+
+c_int, c_float, c_size_t, c_void_p = ctypes.c_int, ctypes.c_float, ctypes.c_size_t, ctypes.c_void_p
+P = c_void_p
+
+# name -> (restype, argtypes); must match include/cvlite.h exactly
+SIGNATURES = {
+    "cvl_version": (c_int, []),
+    "cvl_fcos_assign": (c_int, [P, P, P, c_int, c_int, c_int, c_int, c_int, P, P, P, P, P]),
+    "cvl_fcos_loss_workspace_size": (c_size_t, [c_int, c_int]),
+    "cvl_fcos_loss": (c_int, [P, c_int, P, c_int, P, c_int, c_int, c_int, c_int, c_float, P,
+                              P, c_int, c_int, P, c_int, c_int, P, P]),
+}
+
+
+class CvlError(RuntimeError):
+    pass
+
+
+_lib = None
+
+
+def load():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise CvlError("cvlite native library not built (%s): run __graft_entry__.build() or "
+                           "make -C cv-lite-object-detection_amd/csrc" % LIB_PATH)
+        lib = ctypes.CDLL(LIB_PATH)
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(lib, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = lib
+    return _lib
+
+
+def call(name, *args):
+    st = getattr(load(), name)(*args)
+    if st != 0:
+        if st >= 1000:
+            raise CvlError("%s failed: hipError %d" % (name, st - 1000))
+        raise CvlError("%s: invalid argument (status %d)" % (name, st))
+
+
+def ptr(t):
+    return None if t is None else c_void_p(t.data_ptr())
+
+
+def stream():
+    return c_void_p(torch.cuda.current_stream().cuda_stream)
+
+
+def require_cuda(*tensors):
+    if not torch.cuda.is_available():
+        raise CvlError("cvlite ops need an MI355X GPU (no CPU fallback)")
+    for t in tensors:
+        if t is not None and not t.is_cuda:
+            raise CvlError("cvlite ops take device tensors")
+        if t is not None and not t.is_contiguous():
+            raise CvlError("cvlite ops take contiguous tensors")

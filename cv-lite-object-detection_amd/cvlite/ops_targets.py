@@ -1,0 +1,58 @@
+"""Device ops for target assignment and the fused detection losses (C ABI: include/cvlite.h)."""
+import torch
+
+from . import _lib
+from ._lib import ptr
+
+FCOS_STRIDES = (8, 16, 32, 64, 128)      # FCOS/fcos.py:142-143
+FCOS_BOUNDS = (32.0, 64.0, 128.0, 256.0)  # FCOS/fcos.py:145-147
+
+
+def fcos_level_shapes(pad_h, pad_w, strides=FCOS_STRIDES):
+    return [(int(pad_h // s), int(pad_w // s)) for s in strides]
+
+
+def fcos_assign(boxes, nbox, img_dim, pad_hw, num_classes, strides=FCOS_STRIDES, bounds=FCOS_BOUNDS,
+                out=None, num_targets=None):
+    """Batched FCOS targets.  boxes [B,Nmax,5] f32, nbox [B] i32, img_dim [B,2] f32 (device).
+    Returns targets [B, P, 5+C] f32 (level-major cells) and num_targets [B,5] i32."""
+    _lib.require_cuda(boxes, nbox, img_dim)
+    assert boxes.dtype == torch.float32 and nbox.dtype == torch.int32 and img_dim.dtype == torch.float32
+    B, nmax = int(boxes.shape[0]), int(boxes.shape[1])
+    P = sum(h * w for h, w in fcos_level_shapes(pad_hw[0], pad_hw[1], strides))
+    if out is None:
+        out = torch.empty((B, P, 5 + num_classes), device=boxes.device, dtype=torch.float32)
+    if num_targets is None:
+        num_targets = torch.empty((B, 5), device=boxes.device, dtype=torch.int32)
+    st = (_lib.ctypes.c_int32 * 5)(*[int(s) for s in strides])
+    bd = (_lib.ctypes.c_float * 4)(*[float(x) for x in bounds])
+    _lib.call("cvl_fcos_assign", ptr(boxes), ptr(nbox), ptr(img_dim), B, nmax, int(pad_hw[0]),
+              int(pad_hw[1]), int(num_classes), _lib.ctypes.cast(st, _lib.c_void_p),
+              _lib.ctypes.cast(bd, _lib.c_void_p), ptr(out), ptr(num_targets), _lib.stream())
+    return out, num_targets
+
+
+def fcos_loss(reg_pred, cls_pred, targets, num_classes, reg_type="l1", grad_scale=1.0,
+              with_grad=True, grad_dtype=torch.float32, d_reg=None, d_cls=None):
+    """Fused focal + smooth-L1/IoU + centerness forward and backward.
+    reg_pred [B,P,ld_reg>=5] f32, cls_pred [B,P,ld_cls>=C] f32, targets [B,P,5+C] f32.
+    Returns (losses [B,3] f32 = (cls, reg, cen) per image, d_reg, d_cls)."""
+    _lib.require_cuda(reg_pred, cls_pred, targets)
+    B, P = int(targets.shape[0]), int(targets.shape[1])
+    assert reg_pred.shape[:2] == (B, P) and cls_pred.shape[:2] == (B, P)
+    rt = {"l1": 0, "iou": 1}[reg_type]
+    dev = targets.device
+    losses = torch.empty((B, 3), device=dev, dtype=torch.float32)
+    ws = torch.empty(int(_lib.load().cvl_fcos_loss_workspace_size(B, P)), device=dev, dtype=torch.uint8)
+    if with_grad:
+        if d_reg is None:
+            d_reg = torch.empty((B, P, reg_pred.shape[2]), device=dev, dtype=grad_dtype)
+        if d_cls is None:
+            d_cls = torch.empty((B, P, cls_pred.shape[2]), device=dev, dtype=grad_dtype)
+    dt = lambda t: 0 if t is None or t.dtype == torch.float32 else 1  # noqa: E731
+    _lib.call("cvl_fcos_loss", ptr(reg_pred), int(reg_pred.shape[2]), ptr(cls_pred), int(cls_pred.shape[2]),
+              ptr(targets), B, P, int(num_classes), rt, float(grad_scale), ptr(losses),
+              ptr(d_reg), int(d_reg.shape[2]) if d_reg is not None else 0, dt(d_reg),
+              ptr(d_cls), int(d_cls.shape[2]) if d_cls is not None else 0, dt(d_cls),
+              ptr(ws), _lib.stream())
+    return losses, d_reg, d_cls

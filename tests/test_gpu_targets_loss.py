@@ -1,0 +1,104 @@
+"""GPU parity of the FCOS target-assignment and fused-loss kernels (through the C ABI)."""
+import json
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import fcos_ref, fcos_torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _batches(d, meta):
+    groups = {}
+    for i in range(meta["n_images"]):
+        key = tuple(int(x) for x in d["assign_%d_img_pad" % i])
+        groups.setdefault(key, []).append(i)
+    return groups
+
+
+def test_fcos_assign_bit_exact_vs_reference_goldens(golden):
+    from cvlite import ops_targets as ot
+    d = golden("fcos")
+    meta = json.loads(str(d["meta"]))
+    C = meta["C"]
+    for pad, idx in _batches(d, meta).items():
+        nmax = max(len(d["assign_%d_boxes" % i]) for i in idx)
+        boxes = np.zeros((len(idx), nmax, 5), np.float32)
+        nbox = np.zeros(len(idx), np.int32)
+        dims = np.zeros((len(idx), 2), np.float32)
+        for k, i in enumerate(idx):
+            bx = d["assign_%d_boxes" % i]
+            boxes[k, :len(bx)] = bx
+            nbox[k] = len(bx)
+            dims[k] = d["assign_%d_img_dim" % i]
+        tg, nt = ot.fcos_assign(torch.from_numpy(boxes).cuda(), torch.from_numpy(nbox).cuda(),
+                                torch.from_numpy(dims).cuda(), pad, C)
+        tg, nt = tg.cpu().numpy(), nt.cpu().numpy()
+        for k, i in enumerate(idx):
+            ref = fcos_ref.pack_targets([d["assign_%d_L%d" % (i, l)] for l in range(5)])
+            np.testing.assert_array_equal(tg[k], ref)
+            np.testing.assert_array_equal(nt[k], d["assign_%d_ntgt" % i])
+
+
+def test_fcos_assign_edge_cases():
+    from cvlite import ops_targets as ot
+    C = 20
+    rng = np.random.default_rng(5)
+    cases = [np.zeros((0, 5), np.float32),                                    # empty image
+             np.array([[0.5, 0.5, 1.0, 1.0, 3]], np.float32),                 # whole-image box
+             np.array([[0.001, 0.999, 0.002, 0.002, 19]], np.float32),        # tiny corner box
+             np.array([[0.0, 0.5, 0.1, 0.2, 0], [0.5, 0.5, 0.1, 0.2, 1]], np.float32),  # border straddle
+             np.array([[0.5, 0.5, 0.25, 0.25, 2], [0.5, 0.5, 0.2, 0.3, 5],    # overlaps, multi-hot
+                       [0.52, 0.48, 0.3, 0.22, 7]], np.float32)]
+    for _ in range(40):                                                      # many overlapping boxes
+        n = 64
+        r = np.zeros((n, 5), np.float32)
+        r[:, 2:4] = np.exp(rng.uniform(np.log(2 / 512), 0, (n, 2)))
+        r[:, 0] = rng.uniform(r[:, 2] / 2, 1 - r[:, 2] / 2)
+        r[:, 1] = rng.uniform(r[:, 3] / 2, 1 - r[:, 3] / 2)
+        r[:, 4] = rng.integers(0, C, n)
+        area = (r[:, 2] * np.float32(512)) * (r[:, 3] * np.float32(512))
+        _, first = np.unique(area, return_index=True)
+        cases.append(r[np.sort(first)])
+    nmax = max(1, max(len(c) for c in cases))
+    boxes = np.zeros((len(cases), nmax, 5), np.float32)
+    nbox = np.array([len(c) for c in cases], np.int32)
+    for k, c in enumerate(cases):
+        boxes[k, :len(c)] = c
+    dims = np.tile(np.array([[512.0, 512.0]], np.float32), (len(cases), 1))
+    tg, nt = ot.fcos_assign(torch.from_numpy(boxes).cuda(), torch.from_numpy(nbox).cuda(),
+                            torch.from_numpy(dims).cuda(), (512, 512), C)
+    tg, nt = tg.cpu().numpy(), nt.cpu().numpy()
+    for k, c in enumerate(cases):
+        outs, n = fcos_ref.format_data(c, dims[k], C, img_pad=(512, 512))
+        np.testing.assert_array_equal(tg[k], fcos_ref.pack_targets(outs))
+        np.testing.assert_array_equal(nt[k], n)
+
+
+@pytest.mark.parametrize("reg_type", ["l1", "iou"])
+def test_fcos_loss_matches_reference_and_grad(golden, reg_type):
+    from cvlite import ops_targets as ot
+    d = golden("fcos")
+    meta = json.loads(str(d["meta"]))
+    C = meta["C"]
+    for i in meta["loss_imgs"]:
+        tgt = fcos_ref.pack_targets([d["assign_%d_L%d" % (i, l)] for l in range(5)])
+        pred = np.concatenate([d["loss_%d_pred_L%d" % (i, l)][0].reshape(-1, 5 + C) for l in range(5)], 0)
+        reg = np.zeros((pred.shape[0], 8), np.float32)
+        reg[:, :5] = pred[:, :5]
+        cls = np.zeros((pred.shape[0], 32), np.float32)
+        cls[:, :C] = pred[:, 5:]
+        losses, dreg, dcls = ot.fcos_loss(torch.from_numpy(reg)[None].cuda(), torch.from_numpy(cls)[None].cuda(),
+                                          torch.from_numpy(tgt)[None].cuda(), C, reg_type=reg_type,
+                                          grad_scale=0.5)
+        got = losses.cpu().numpy()[0]
+        np.testing.assert_allclose(got, d["loss_%d_%s" % (i, reg_type)], rtol=2e-5)  # reference golden
+        tr = torch.from_numpy(reg).double().requires_grad_()
+        tc = torch.from_numpy(cls).double().requires_grad_()
+        lc, lr, le = fcos_torch.packed_loss(tr, tc, torch.from_numpy(tgt).double(), C, reg_type)
+        (0.5 * (lc + lr + le)).backward()
+        np.testing.assert_allclose(dreg.cpu().numpy()[0], tr.grad.numpy(), rtol=1e-4, atol=1e-6)
+        np.testing.assert_allclose(dcls.cpu().numpy()[0], tc.grad.numpy(), rtol=1e-4, atol=1e-6)
+        assert not dreg[0, :, 5:].any() and not dcls[0, :, C:].any()
