@@ -1,0 +1,69 @@
+// Internal: segmented-conv argument block shared by the fwd/dgrad and wgrad kernels.
+#pragma once
+#include "cvl_common.h"
+
+typedef short s16x8 __attribute__((ext_vector_type(8)));
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+constexpr int kMaxSeg = CVL_CONV_MAX_SEG;
+
+struct ConvSeg {
+  int Hr, Wr, Hs, Ws;
+  long src_base, src_img, dst_base, dst_img;
+  int m_start;   // first row of this segment in the BM-padded M space
+  int rows;      // valid rows = B * Hr * Wr
+  const cvl_bf16* w;
+  const float* bias;
+};
+
+struct ConvArgs {
+  const cvl_bf16* src;
+  void* dst;
+  double* stats;
+  int nseg, B;
+  ConvSeg seg[kMaxSeg];
+  int Cin, KH, KW, stride, pad_t, pad_l;
+  int K, Npad, n_store, ld_dst, dst_coff, dst_f32, relu_out, relu_in;
+  float beta;
+  int m_tiles, m_total;
+};
+
+// Validate a public descriptor and lay its segments out in a BM-padded M space.
+static inline int cvl_conv_prepare(const cvl_conv_desc* d, int bm, ConvArgs* a) {
+  CVL_CHECK_ARG(d);
+  CVL_CHECK_ARG(d->nseg >= 1 && d->nseg <= kMaxSeg && d->B >= 1);
+  CVL_CHECK_ARG(d->Cin > 0 && d->KH > 0 && d->KW > 0 && d->stride > 0);
+  CVL_CHECK_ARG(d->mode == CVL_CONV_FWD || d->mode == CVL_CONV_DGRAD);
+  CVL_CHECK_ARG(d->Npad > 0 && d->n_store > 0 && d->n_store <= d->Npad);
+  CVL_CHECK_ARG(d->ld_dst >= d->dst_coff + d->n_store);
+  a->nseg = d->nseg;
+  a->B = d->B;
+  a->Cin = d->Cin; a->KH = d->KH; a->KW = d->KW; a->stride = d->stride;
+  a->pad_t = d->pad_t; a->pad_l = d->pad_l;
+  a->K = d->KH * d->KW * d->Cin;
+  a->Npad = d->Npad; a->n_store = d->n_store; a->ld_dst = d->ld_dst; a->dst_coff = d->dst_coff;
+  a->dst_f32 = d->dst_f32; a->relu_out = d->relu_out; a->relu_in = d->relu_in; a->beta = d->beta;
+  int m = 0;
+  for (int i = 0; i < kMaxSeg; ++i) {
+    ConvSeg& s = a->seg[i];
+    if (i >= d->nseg) {
+      s = a->seg[0];
+      s.m_start = 0x7fffffff;
+      continue;
+    }
+    const cvl_conv_seg& q = d->seg[i];
+    CVL_CHECK_ARG(q.Hr > 0 && q.Wr > 0 && q.Hs > 0 && q.Ws > 0 && q.w);
+    s.Hr = q.Hr; s.Wr = q.Wr; s.Hs = q.Hs; s.Ws = q.Ws;
+    s.src_base = q.src_base; s.src_img = q.src_img; s.dst_base = q.dst_base; s.dst_img = q.dst_img;
+    s.w = reinterpret_cast<const cvl_bf16*>(q.w);
+    s.bias = q.bias;
+    s.m_start = m;
+    s.rows = d->B * q.Hr * q.Wr;
+    m += ((s.rows + bm - 1) / bm) * bm;
+  }
+  a->m_total = m;
+  a->m_tiles = m / bm;
+  return CVL_OK;
+}

@@ -1,0 +1,257 @@
+// Convolution weight gradient for gfx950, bf16 MFMA with fp32 accumulation.
+//
+// Replaces the TF2 Conv2DBackpropFilter of the reference graph and the per-image Python gradient
+// accumulation of FCOS/train_fcos.py:173-176 (one reduction over all images of the batch, and —
+// for the FCOS towers shared by the five FPN levels — over all levels at once):
+//   dW[(r, s, c), co] = sum_m  A[m, (r, s, c)] * dY[m, co]      (HWIO layout, fp32)
+// where A is the forward conv's implicit im2col and m runs over the forward GEMM rows.
+// The reduction index m is the row (slow) index of both operands, so both are staged in LDS
+// row-major (16-byte coalesced loads along channels) and read back column-wise with gfx950's
+// ds_read_b64_tr_b16 transpose reads into v_mfma_f32_16x16x32_bf16 fragments.
+// The M range is split over `splits` workgroups per output tile (chosen so the grid fills the
+// 256 CUs); partial tiles go to fp32 slabs, summed in a fixed order by a second pass
+// (deterministic), or straight into dW when splits == 1.
+#include "conv_common.h"
+
+namespace {
+
+constexpr int NT = 256;
+constexpr int BR = 32;     // reduction rows per step (one MFMA K)
+constexpr int BKK = 128;   // k columns per tile
+constexpr int BM = 128;    // segment padding granule (must match conv_igemm)
+
+struct WgArgs {
+  ConvArgs a;
+  const cvl_bf16* dy;
+  float* out;
+  int ld_dy, dy_coff, Cout, co_tiles, k_tiles, chunk;
+  float beta;
+  int direct;
+};
+
+__device__ __forceinline__ int fdiv(int x, int d, float rd) {
+  int q = (int)((float)x * rd);
+  if (q * d > x) --q;
+  else if ((q + 1) * d <= x) ++q;
+  return q;
+}
+
+typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+
+__device__ __forceinline__ s16x8 tr_frag(const cvl_bf16* base_lo, const cvl_bf16* base_hi) {
+  s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(base_lo));
+  s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(base_hi));
+  return s16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+}
+
+template <int BCO>
+__global__ void __launch_bounds__(NT) conv_wgrad_kernel(WgArgs g) {
+  constexpr int PITCH_Y = BCO + 16;
+  constexpr int PITCH_A = BKK + 16;
+  constexpr int WCO = BCO / 2, WK = BKK / 2;
+  constexpr int TM = WCO / 16, TN = WK / 16;
+  constexpr int YCPR = BCO / 8;                 // dY 16-byte chunks per row
+  constexpr int YCH = BR * YCPR;                // dY chunks per step
+  __shared__ __attribute__((aligned(16))) cvl_bf16 Ys[BR * PITCH_Y];
+  __shared__ __attribute__((aligned(16))) cvl_bf16 As[BR * PITCH_A];
+
+  const ConvArgs& a = g.a;
+  const int tid = threadIdx.x;
+  const int co_tile = blockIdx.x % g.co_tiles, k_tile = blockIdx.x / g.co_tiles;
+  const int co0 = co_tile * BCO, k0 = k_tile * BKK;
+  const int m_lo = blockIdx.y * g.chunk;
+  const int m_hi = min(m_lo + g.chunk, a.m_total);
+
+  // fixed per-thread k chunk for A (16 chunks of 8 channels per 128-wide k tile)
+  const int ach = tid & 15, arow = tid >> 4;     // rows arow and arow + 16
+  const int kc = k0 + ach * 8;
+  const bool k_ok = kc < a.K;
+  const int tap = k_ok ? kc / a.Cin : 0;
+  const int ci = kc - tap * a.Cin;
+  const int tr_ = tap / a.KW, ts_ = tap - (tap / a.KW) * a.KW;
+  // dY chunk mapping
+  const int ych = tid % YCPR, yrow = tid / YCPR;
+
+  const int wave = tid >> 6, lane = tid & 63;
+  const int wco = wave >> 1, wk = wave & 1;
+  const int lr = lane & 15, lg = lane >> 4;
+  const int q = lr >> 2, p = lr & 3;
+  f32x4 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  for (int m = m_lo; m < m_hi; m += BR) {
+    int sg = 0;
+#pragma unroll
+    for (int i = 1; i < kMaxSeg; ++i)
+      if (i < a.nseg && m >= a.seg[i].m_start) sg = i;
+    const ConvSeg& S = a.seg[sg];
+    const int mloc = m - S.m_start;
+    if (mloc >= S.rows) continue;                   // whole step is segment padding (uniform)
+    const int HWr = S.Hr * S.Wr;
+    const float rHW = 1.0f / (float)HWr, rW = 1.0f / (float)S.Wr;
+    // ---- A: two rows per thread, fixed k chunk -------------------------------------------------
+    s16x8 va[2];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int ml = mloc + arow + h * 16;
+      va[h] = s16x8{0, 0, 0, 0, 0, 0, 0, 0};
+      if (k_ok && ml < S.rows) {
+        const int img = fdiv(ml, HWr, rHW);
+        const int qq = ml - img * HWr;
+        const int oy = fdiv(qq, S.Wr, rW), ox = qq - oy * S.Wr;
+        const int iy = oy * a.stride - a.pad_t + tr_, ix = ox * a.stride - a.pad_l + ts_;
+        if (iy >= 0 && ix >= 0 && iy < S.Hs && ix < S.Ws) {
+          const long row = S.src_base + (long)img * S.src_img + (long)iy * S.Ws + ix;
+          va[h] = *reinterpret_cast<const s16x8*>(a.src + row * a.Cin + ci);
+          if (a.relu_in) {
+#pragma unroll
+            for (int u = 0; u < 8; ++u) va[h][u] = va[h][u] < 0 ? (short)0 : va[h][u];
+          }
+        }
+      }
+    }
+    // ---- dY -------------------------------------------------------------------------------------
+    constexpr int YPT = (YCH + NT - 1) / NT;
+    s16x8 vy[YPT];
+#pragma unroll
+    for (int h = 0; h < YPT; ++h) {
+      const int idx = tid + h * NT;
+      const int r = idx / YCPR;
+      vy[h] = s16x8{0, 0, 0, 0, 0, 0, 0, 0};
+      const int ml = mloc + r;
+      if (idx < YCH && ml < S.rows) {
+        const int img = fdiv(ml, HWr, rHW);
+        const long drow = S.dst_base + (long)img * S.dst_img + (ml - img * HWr);
+        vy[h] = *reinterpret_cast<const s16x8*>(g.dy + drow * g.ld_dy + g.dy_coff + co0 + ych * 8);
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+      *reinterpret_cast<s16x8*>(As + (arow + h * 16) * PITCH_A + ach * 8) = va[h];
+#pragma unroll
+    for (int h = 0; h < YPT; ++h) {
+      const int idx = tid + h * NT;
+      if (idx < YCH) *reinterpret_cast<s16x8*>(Ys + (idx / YCPR) * PITCH_Y + ych * 8) = vy[h];
+    }
+    __syncthreads();
+    // ---- MFMA over the 32-row step ----------------------------------------------------------------
+    s16x8 fa[TM], fb[TN];
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      const int col = wco * WCO + i * 16 + 4 * p;
+      fa[i] = tr_frag(Ys + (8 * lg + q) * PITCH_Y + col, Ys + (8 * lg + 4 + q) * PITCH_Y + col);
+    }
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int col = wk * WK + j * 16 + 4 * p;
+      fb[j] = tr_frag(As + (8 * lg + q) * PITCH_A + col, As + (8 * lg + 4 + q) * PITCH_A + col);
+    }
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+            __builtin_bit_cast(bf16x8, fa[i]), __builtin_bit_cast(bf16x8, fb[j]), acc[i][j], 0, 0, 0);
+  }
+
+  // ---- epilogue: C[co][k] -> out[k][co] (HWIO), 4 consecutive co per lane ------------------------
+  float* out = g.direct ? g.out : g.out + (size_t)blockIdx.y * a.K * g.Cout;
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int k = k0 + wk * WK + j * 16 + lr;
+      const int co = co0 + wco * WCO + i * 16 + 4 * lg;
+      if (k >= a.K || co >= g.Cout) continue;
+      f32x4 v = acc[i][j];
+      if (co + 3 < g.Cout && (g.Cout & 3) == 0) {
+        f32x4* po = reinterpret_cast<f32x4*>(out + (size_t)k * g.Cout + co);
+        if (g.direct && g.beta != 0.f) v += g.beta * *po;
+        *po = v;
+      } else {
+        for (int e = 0; e < 4 && co + e < g.Cout; ++e) {
+          float* po = out + (size_t)k * g.Cout + co + e;
+          *po = (g.direct && g.beta != 0.f) ? v[e] + g.beta * *po : v[e];
+        }
+      }
+    }
+}
+
+__global__ void wgrad_reduce_kernel(const float* slab, float* dw, long n, int splits, float beta) {
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+    float s = slab[i];
+    for (int k = 1; k < splits; ++k) s += slab[(long)k * n + i];
+    if (beta != 0.f) s += beta * dw[i];
+    dw[i] = s;
+  }
+}
+
+int pick_splits(int tiles, int m_total) {
+  // fill ~256 CUs with >= 1 tile each, but keep >= 2048 reduction rows per workgroup
+  int s = (256 + tiles - 1) / tiles;
+  const int max_s = m_total / 2048;
+  if (s > max_s) s = max_s;
+  return s < 1 ? 1 : s;
+}
+
+}  // namespace
+
+extern "C" size_t cvl_conv_wgrad_workspace_size(const cvl_conv_desc* d) {
+  ConvArgs a;
+  if (cvl_conv_prepare(d, BM, &a)) return 0;
+  const int bco = a.Npad % 128 == 0 ? 128 : (a.Npad % 64 == 0 ? 64 : 32);
+  const int tiles = (a.Npad / bco) * ((a.K + BKK - 1) / BKK);
+  const int splits = pick_splits(tiles, a.m_total);
+  return splits > 1 ? (size_t)splits * a.K * a.n_store * sizeof(float) : 16;
+}
+
+extern "C" int cvl_conv_wgrad(const cvl_conv_desc* d, const void* x, const void* dy, float* dw,
+                              float beta, void* workspace, size_t workspace_bytes,
+                              cvl_stream_t stream) {
+  WgArgs g;
+  int st = cvl_conv_prepare(d, BM, &g.a);
+  if (st) return st;
+  CVL_CHECK_ARG(d->mode == CVL_CONV_FWD && x && dy && dw);
+  CVL_CHECK_ARG(d->Cin % 8 == 0 && g.a.Npad % 32 == 0);
+  CVL_CHECK_ARG(d->ld_dst % 8 == 0 && d->dst_coff % 8 == 0 && d->ld_dst >= d->dst_coff + g.a.Npad);
+  for (int i = 1; i < d->nseg; ++i) CVL_CHECK_ARG(d->seg[i].w == d->seg[0].w);  // shared weights
+  g.a.src = reinterpret_cast<const cvl_bf16*>(x);
+  g.dy = reinterpret_cast<const cvl_bf16*>(dy);
+  g.ld_dy = d->ld_dst;
+  g.dy_coff = d->dst_coff;
+  g.Cout = d->n_store;
+  g.beta = beta;
+  const int bco = g.a.Npad % 128 == 0 ? 128 : (g.a.Npad % 64 == 0 ? 64 : 32);
+  g.co_tiles = g.a.Npad / bco;
+  g.k_tiles = (g.a.K + BKK - 1) / BKK;
+  const int tiles = g.co_tiles * g.k_tiles;
+  const int splits = pick_splits(tiles, g.a.m_total);
+  int chunk = (g.a.m_total + splits - 1) / splits;
+  chunk = ((chunk + BM - 1) / BM) * BM;
+  const int nsplit = (g.a.m_total + chunk - 1) / chunk;
+  g.chunk = chunk;
+  g.direct = nsplit == 1;
+  if (!g.direct) {
+    CVL_CHECK_ARG(workspace && workspace_bytes >= (size_t)nsplit * g.a.K * g.Cout * sizeof(float));
+    g.out = reinterpret_cast<float*>(workspace);
+  } else {
+    g.out = dw;
+  }
+  hipStream_t s = (hipStream_t)stream;
+  dim3 grid(tiles, nsplit);
+  if (bco == 128) hipLaunchKernelGGL(conv_wgrad_kernel<128>, grid, dim3(NT), 0, s, g);
+  else if (bco == 64) hipLaunchKernelGGL(conv_wgrad_kernel<64>, grid, dim3(NT), 0, s, g);
+  else hipLaunchKernelGGL(conv_wgrad_kernel<32>, grid, dim3(NT), 0, s, g);
+  st = cvl_launch_status();
+  if (st || g.direct) return st;
+  const long n = (long)g.a.K * g.Cout;
+  int blocks = (int)((n + 255) / 256);
+  blocks = blocks > 4096 ? 4096 : blocks;
+  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(blocks), dim3(256), 0, s,
+                     (const float*)g.out, dw, n, nsplit, beta);
+  return cvl_launch_status();
+}

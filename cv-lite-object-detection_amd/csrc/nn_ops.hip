@@ -1,0 +1,607 @@
+// Memory-bound kernels of the detector training step on gfx950 (all 16-byte vectorised):
+// weight packing, stem im2col, per-image BatchNorm forward/backward, max-pool, FPN upsample-add,
+// ReLU backward, bias gradient, and the fused global-norm clip + Keras-SGD update.
+// Reference semantics: Keras ResNet50 v1 layers used by FCOS/fcos.py:30-46 (BN eps 1.001e-5,
+// momentum 0.99, batch-1 forwards => per-image statistics, Q12), fcos.py:57-72 (FPN),
+// train_fcos.py:173-185 (sum of per-image grads / bs, clip_by_global_norm, SGD momentum, Q16/Q17).
+#include "conv_common.h"
+
+namespace {
+
+constexpr int NT = 256;
+
+__device__ __forceinline__ void unpack8(s16x8 v, float* f) {
+#pragma unroll
+  for (int i = 0; i < 8; ++i) f[i] = bf16_to_f32((cvl_bf16)v[i]);
+}
+__device__ __forceinline__ s16x8 pack8(const float* f) {
+  s16x8 v;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) v[i] = (short)f32_to_bf16(f[i]);
+  return v;
+}
+
+inline int grid_for(long n, int per_block = NT, int cap = 8192) {
+  long b = (n + per_block - 1) / per_block;
+  return (int)(b > cap ? cap : (b < 1 ? 1 : b));
+}
+
+// ---------------------------------------------------------------------------------------------
+// weight packing: fp32 HWIO [KH][KW][Cin][Cout] -> bf16 fwd [Npad][KH*KW*Cin_k] (zero rows >= Cout,
+// zero k-channels >= Cin), and dgrad [Cin_pad][KH*KW*Cout_pad] (zero beyond Cin / Cout)
+// ---------------------------------------------------------------------------------------------
+__global__ void pack_fwd_kernel(const float* w, cvl_bf16* wf, int KHW, int Cin, int Cin_k, int Cout,
+                                int Npad) {
+  const long K = (long)KHW * Cin_k;
+  const long total = (long)Npad * K;
+  for (long i = blockIdx.x * (long)NT + threadIdx.x; i < total; i += (long)gridDim.x * NT) {
+    const int co = (int)(i / K);
+    const long k = i - (long)co * K;
+    const int tap = (int)(k / Cin_k), ci = (int)(k - (long)tap * Cin_k);
+    float v = 0.f;
+    if (co < Cout && ci < Cin) v = w[((long)tap * Cin + ci) * Cout + co];
+    wf[i] = f32_to_bf16(v);
+  }
+}
+
+__global__ void pack_dgrad_kernel(const float* w, cvl_bf16* wd, int KHW, int Cin, int Cout,
+                                  int Cin_pad, int Cout_pad) {
+  const long K = (long)KHW * Cout_pad;
+  const long total = (long)Cin_pad * K;
+  for (long i = blockIdx.x * (long)NT + threadIdx.x; i < total; i += (long)gridDim.x * NT) {
+    const int ci = (int)(i / K);
+    const long k = i - (long)ci * K;
+    const int tap = (int)(k / Cout_pad), co = (int)(k - (long)tap * Cout_pad);
+    float v = 0.f;
+    if (ci < Cin && co < Cout) v = w[((long)tap * Cin + ci) * Cout + co];
+    wd[i] = f32_to_bf16(v);
+  }
+}
+
+// stem: fp32 NHWC image -> bf16 im2col rows [B*Ho*Wo][Kp], k = (r*KW + s)*C + c, zero pad
+__global__ void im2col_kernel(const float* x, cvl_bf16* out, int B, int H, int W, int C, int KH,
+                              int KW, int stride, int pad_t, int pad_l, int Ho, int Wo, int Kp) {
+  const long total = (long)B * Ho * Wo * Kp;
+  for (long i = blockIdx.x * (long)NT + threadIdx.x; i < total; i += (long)gridDim.x * NT) {
+    const long row = i / Kp;
+    const int k = (int)(i - row * Kp);
+    float v = 0.f;
+    if (k < KH * KW * C) {
+      const int tap = k / C, c = k - (k / C) * C;
+      const int r = tap / KW, s = tap - (tap / KW) * KW;
+      const int b = (int)(row / ((long)Ho * Wo));
+      const int q = (int)(row - (long)b * Ho * Wo);
+      const int oy = q / Wo, ox = q - (q / Wo) * Wo;
+      const int iy = oy * stride - pad_t + r, ix = ox * stride - pad_l + s;
+      if (iy >= 0 && ix >= 0 && iy < H && ix < W) v = x[(((long)b * H + iy) * W + ix) * C + c];
+    }
+    out[i] = f32_to_bf16(v);
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// BatchNorm (per-image statistics over H*W, Keras fused-BN semantics)
+// ---------------------------------------------------------------------------------------------
+// stats[b][c] = (sum, sumsq) -> mr[b][c] = (mean, rstd); running stats EMA, images in order.
+__global__ void bn_finalize_kernel(const double* stats, float* mr, float* run_mean, float* run_var,
+                                   int B, int C, int HW, float eps, float momentum) {
+  const int c = blockIdx.x * NT + threadIdx.x;
+  if (c >= C) return;
+  float rm = run_mean ? run_mean[c] : 0.f, rv = run_var ? run_var[c] : 0.f;
+  for (int b = 0; b < B; ++b) {
+    const double s1 = stats[((long)b * C + c) * 2], s2 = stats[((long)b * C + c) * 2 + 1];
+    const double mean = s1 / HW;
+    double var = s2 / HW - mean * mean;
+    var = var > 0.0 ? var : 0.0;
+    mr[((long)b * C + c) * 2] = (float)mean;
+    mr[((long)b * C + c) * 2 + 1] = (float)(1.0 / sqrt(var + (double)eps));
+    const double uvar = HW > 1 ? var * HW / (HW - 1.0) : var;   // TF fused BN: unbiased for EMA
+    rm = rm * momentum + (float)mean * (1.f - momentum);
+    rv = rv * momentum + (float)uvar * (1.f - momentum);
+  }
+  if (run_mean) { run_mean[c] = rm; run_var[c] = rv; }
+}
+
+// y = act(gamma * (z - mean) * rstd + beta [+ residual])
+__global__ void bn_apply_kernel(const cvl_bf16* z, const float* mr, const float* gamma, const float* beta,
+                                const cvl_bf16* res, cvl_bf16* y, long rows, int C, int HW, int relu) {
+  const int C8 = C / 8;
+  const long total = rows * C8;
+  for (long i = blockIdx.x * (long)NT + threadIdx.x; i < total; i += (long)gridDim.x * NT) {
+    const long row = i / C8;
+    const int c0 = (int)(i - row * C8) * 8;
+    const int b = (int)(row / HW);
+    float v[8], r[8];
+    unpack8(*reinterpret_cast<const s16x8*>(z + row * C + c0), v);
+    if (res) unpack8(*reinterpret_cast<const s16x8*>(res + row * C + c0), r);
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int c = c0 + u;
+      const float m = mr[((long)b * C + c) * 2], rs = mr[((long)b * C + c) * 2 + 1];
+      float o = gamma[c] * ((v[u] - m) * rs) + beta[c];
+      if (res) o += r[u];
+      if (relu) o = o > 0.f ? o : 0.f;
+      v[u] = o;
+    }
+    *reinterpret_cast<s16x8*>(y + row * C + c0) = pack8(v);
+  }
+}
+
+// per-(image, channel): sums[b][c] += (sum g, sum g*xhat), g = dy * (y > 0 if relu)
+// block = (image b, row chunk); threads: 8 channels each
+__global__ void bn_bwd_reduce_kernel(const cvl_bf16* dy, const cvl_bf16* y, const cvl_bf16* z,
+                                     const float* mr, double* sums, int C, int HW, int rows_per_blk) {
+  const int b = blockIdx.y;
+  const int C8 = C / 8;
+  const int tpr = C8 < NT ? C8 : NT;            // threads per row
+  const int rpp = NT / tpr;                     // rows per pass
+  const int cg = threadIdx.x % tpr, rsub = threadIdx.x / tpr;
+  const int r0 = blockIdx.x * rows_per_blk;
+  const int r1 = min(r0 + rows_per_blk, HW);
+  __shared__ float red[NT * 8 * 2 / 8];         // reused per channel group pass
+  for (int cgb = cg; cgb < C8; cgb += tpr) {
+    const int c0 = cgb * 8;
+    float m[8], rs[8], s1[8], s2[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      m[u] = mr[((long)b * C + c0 + u) * 2];
+      rs[u] = mr[((long)b * C + c0 + u) * 2 + 1];
+      s1[u] = 0.f; s2[u] = 0.f;
+    }
+    if (rsub < rpp) {
+      for (int r = r0 + rsub; r < r1; r += rpp) {
+        const long off = ((long)b * HW + r) * C + c0;
+        float g[8], zz[8];
+        unpack8(*reinterpret_cast<const s16x8*>(dy + off), g);
+        unpack8(*reinterpret_cast<const s16x8*>(z + off), zz);
+        if (y) {
+          float yy[8];
+          unpack8(*reinterpret_cast<const s16x8*>(y + off), yy);
+#pragma unroll
+          for (int u = 0; u < 8; ++u) g[u] = yy[u] > 0.f ? g[u] : 0.f;
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          s1[u] += g[u];
+          s2[u] += g[u] * ((zz[u] - m[u]) * rs[u]);
+        }
+      }
+    }
+    // reduce over rsub (threads with the same cg) through LDS, 8 channels x 2 values at a time
+    for (int u = 0; u < 8; ++u) {
+      __syncthreads();
+      red[threadIdx.x] = s1[u];
+      red[NT + threadIdx.x] = s2[u];
+      __syncthreads();
+      if (rsub == 0) {
+        double a1 = 0.0, a2 = 0.0;
+        for (int k = 0; k < rpp; ++k) { a1 += red[k * tpr + cg]; a2 += red[NT + k * tpr + cg]; }
+        atomicAdd(&sums[((long)b * C + c0 + u) * 2], a1);
+        atomicAdd(&sums[((long)b * C + c0 + u) * 2 + 1], a2);
+      }
+    }
+  }
+}
+
+// dz = gamma*rstd*(g - mean(g) - xhat*mean(g*xhat)); optional g_out = g (for the residual path)
+__global__ void bn_bwd_apply_kernel(const cvl_bf16* dy, const cvl_bf16* y, const cvl_bf16* z,
+                                    const float* mr, const float* gamma, const double* sums,
+                                    cvl_bf16* dz, cvl_bf16* g_out, long rows, int C, int HW) {
+  const int C8 = C / 8;
+  const long total = rows * C8;
+  const float inv = 1.0f / (float)HW;
+  for (long i = blockIdx.x * (long)NT + threadIdx.x; i < total; i += (long)gridDim.x * NT) {
+    const long row = i / C8;
+    const int c0 = (int)(i - row * C8) * 8;
+    const int b = (int)(row / HW);
+    float g[8], zz[8];
+    unpack8(*reinterpret_cast<const s16x8*>(dy + row * C + c0), g);
+    unpack8(*reinterpret_cast<const s16x8*>(z + row * C + c0), zz);
+    if (y) {
+      float yy[8];
+      unpack8(*reinterpret_cast<const s16x8*>(y + row * C + c0), yy);
+#pragma unroll
+      for (int u = 0; u < 8; ++u) g[u] = yy[u] > 0.f ? g[u] : 0.f;
+    }
+    if (g_out) *reinterpret_cast<s16x8*>(g_out + row * C + c0) = pack8(g);
+    float o[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const long bc = (long)b * C + c0 + u;
+      const float m = mr[bc * 2], rs = mr[bc * 2 + 1];
+      const float mg = (float)sums[bc * 2] * inv, mgx = (float)sums[bc * 2 + 1] * inv;
+      const float xh = (zz[u] - m) * rs;
+      o[u] = gamma[c0 + u] * rs * (g[u] - mg - xh * mgx);
+    }
+    *reinterpret_cast<s16x8*>(dz + row * C + c0) = pack8(o);
+  }
+}
+
+// dgamma[c] = beta_acc*dgamma + sum_b sum g*xhat ; dbeta[c] = ... + sum_b sum g
+__global__ void bn_param_grad_kernel(const double* sums, float* dgamma, float* dbeta, int B, int C,
+                                     float beta_acc) {
+  const int c = blockIdx.x * NT + threadIdx.x;
+  if (c >= C) return;
+  double a1 = 0.0, a2 = 0.0;
+  for (int b = 0; b < B; ++b) { a1 += sums[((long)b * C + c) * 2]; a2 += sums[((long)b * C + c) * 2 + 1]; }
+  dbeta[c] = (float)a1 + (beta_acc != 0.f ? beta_acc * dbeta[c] : 0.f);
+  dgamma[c] = (float)a2 + (beta_acc != 0.f ? beta_acc * dgamma[c] : 0.f);
+}
+
+// ---------------------------------------------------------------------------------------------
+// max-pool 3x3 / 2 after ZeroPadding2D(1) (Keras ResNet50 pool1): zero padding is a real input
+// value; the gradient goes to the first maximum in row-major window order (TF MaxPoolGrad).
+// ---------------------------------------------------------------------------------------------
+__global__ void maxpool_fwd_kernel(const cvl_bf16* x, cvl_bf16* y, uint8_t* arg, int B, int H, int W,
+                                   int C, int Ho, int Wo) {
+  const int C8 = C / 8;
+  const long total = (long)B * Ho * Wo * C8;
+  for (long i = blockIdx.x * (long)NT + threadIdx.x; i < total; i += (long)gridDim.x * NT) {
+    const long pix = i / C8;
+    const int c0 = (int)(i - pix * C8) * 8;
+    const int b = (int)(pix / ((long)Ho * Wo));
+    const int q = (int)(pix - (long)b * Ho * Wo);
+    const int oy = q / Wo, ox = q - (q / Wo) * Wo;
+    float best[8];
+    uint8_t bi[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) { best[u] = -INFINITY; bi[u] = 0; }
+    for (int t = 0; t < 9; ++t) {
+      const int iy = oy * 2 - 1 + t / 3, ix = ox * 2 - 1 + t % 3;
+      float v[8];
+      if (iy >= 0 && ix >= 0 && iy < H && ix < W) {
+        unpack8(*reinterpret_cast<const s16x8*>(x + (((long)b * H + iy) * W + ix) * C + c0), v);
+      } else {
+#pragma unroll
+        for (int u = 0; u < 8; ++u) v[u] = 0.f;
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+        if (v[u] > best[u]) { best[u] = v[u]; bi[u] = (uint8_t)t; }
+    }
+    *reinterpret_cast<s16x8*>(y + pix * C + c0) = pack8(best);
+#pragma unroll
+    for (int u = 0; u < 8; ++u) arg[pix * C + c0 + u] = bi[u];
+  }
+}
+
+__global__ void maxpool_bwd_kernel(const cvl_bf16* dy, const uint8_t* arg, cvl_bf16* dx, int B, int H,
+                                   int W, int C, int Ho, int Wo) {
+  const int C8 = C / 8;
+  const long total = (long)B * H * W * C8;
+  for (long i = blockIdx.x * (long)NT + threadIdx.x; i < total; i += (long)gridDim.x * NT) {
+    const long pix = i / C8;
+    const int c0 = (int)(i - pix * C8) * 8;
+    const int b = (int)(pix / ((long)H * W));
+    const int q = (int)(pix - (long)b * H * W);
+    const int iy = q / W, ix = q - (q / W) * W;
+    float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    // outputs whose window [2o-1, 2o+1] contains (iy, ix): o in [i>>1, (i+1)>>1]
+    for (int oy = iy >> 1; oy <= ((iy + 1) >> 1) && oy < Ho; ++oy) {
+      for (int ox = ix >> 1; ox <= ((ix + 1) >> 1) && ox < Wo; ++ox) {
+        const int t = (iy - (oy * 2 - 1)) * 3 + (ix - (ox * 2 - 1));
+        const long o = (((long)b * Ho + oy) * Wo + ox) * C + c0;
+        float g[8];
+        unpack8(*reinterpret_cast<const s16x8*>(dy + o), g);
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+          if (arg[o + u] == t) acc[u] += g[u];
+      }
+    }
+    *reinterpret_cast<s16x8*>(dx + pix * C + c0) = pack8(acc);
+  }
+}
+
+// FPN top-down: out = a + nearest_up2(b)   (fcos.py:57-60)
+__global__ void upsample_add_kernel(const cvl_bf16* a, const cvl_bf16* b, cvl_bf16* out, int B, int H,
+                                    int W, int C) {
+  const int C8 = C / 8;
+  const long total = (long)B * H * W * C8;
+  const int Hb = H / 2, Wb = W / 2;
+  for (long i = blockIdx.x * (long)NT + threadIdx.x; i < total; i += (long)gridDim.x * NT) {
+    const long pix = i / C8;
+    const int c0 = (int)(i - pix * C8) * 8;
+    const int n = (int)(pix / ((long)H * W));
+    const int q = (int)(pix - (long)n * H * W);
+    const int y = q / W, x = q - (q / W) * W;
+    float va[8], vb[8];
+    unpack8(*reinterpret_cast<const s16x8*>(a + pix * C + c0), va);
+    unpack8(*reinterpret_cast<const s16x8*>(b + (((long)n * Hb + y / 2) * Wb + x / 2) * C + c0), vb);
+#pragma unroll
+    for (int u = 0; u < 8; ++u) va[u] += vb[u];
+    *reinterpret_cast<s16x8*>(out + pix * C + c0) = pack8(va);
+  }
+}
+
+// d_b (+)= sum over each 2x2 block of d_out   (backward of nearest_up2)
+__global__ void upsample_bwd_kernel(const cvl_bf16* dout, cvl_bf16* db, int B, int H, int W, int C,
+                                    float beta) {
+  const int C8 = C / 8;
+  const int Hb = H / 2, Wb = W / 2;
+  const long total = (long)B * Hb * Wb * C8;
+  for (long i = blockIdx.x * (long)NT + threadIdx.x; i < total; i += (long)gridDim.x * NT) {
+    const long pix = i / C8;
+    const int c0 = (int)(i - pix * C8) * 8;
+    const int n = (int)(pix / ((long)Hb * Wb));
+    const int q = (int)(pix - (long)n * Hb * Wb);
+    const int y = q / Wb, x = q - (q / Wb) * Wb;
+    float s[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    for (int dy = 0; dy < 2; ++dy)
+      for (int dx = 0; dx < 2; ++dx) {
+        float v[8];
+        unpack8(*reinterpret_cast<const s16x8*>(dout + (((long)n * H + 2 * y + dy) * W + 2 * x + dx) * C + c0), v);
+#pragma unroll
+        for (int u = 0; u < 8; ++u) s[u] += v[u];
+      }
+    if (beta != 0.f) {
+      float o[8];
+      unpack8(*reinterpret_cast<const s16x8*>(db + pix * C + c0), o);
+#pragma unroll
+      for (int u = 0; u < 8; ++u) s[u] += beta * o[u];
+    }
+    *reinterpret_cast<s16x8*>(db + pix * C + c0) = pack8(s);
+  }
+}
+
+// dx = dy * (y > 0)  [+ beta * dx]
+__global__ void relu_bwd_kernel(const cvl_bf16* dy, const cvl_bf16* y, cvl_bf16* dx, long n8, float beta) {
+  for (long i = blockIdx.x * (long)NT + threadIdx.x; i < n8; i += (long)gridDim.x * NT) {
+    float g[8], yy[8];
+    unpack8(reinterpret_cast<const s16x8*>(dy)[i], g);
+    unpack8(reinterpret_cast<const s16x8*>(y)[i], yy);
+    if (beta != 0.f) {
+      float o[8];
+      unpack8(reinterpret_cast<const s16x8*>(dx)[i], o);
+#pragma unroll
+      for (int u = 0; u < 8; ++u) g[u] = (yy[u] > 0.f ? g[u] : 0.f) + beta * o[u];
+    } else {
+#pragma unroll
+      for (int u = 0; u < 8; ++u) g[u] = yy[u] > 0.f ? g[u] : 0.f;
+    }
+    reinterpret_cast<s16x8*>(dx)[i] = pack8(g);
+  }
+}
+
+// out = a + b (bf16), n8 groups of 8
+__global__ void add_kernel(const cvl_bf16* a, const cvl_bf16* b, cvl_bf16* out, long n8) {
+  for (long i = blockIdx.x * (long)NT + threadIdx.x; i < n8; i += (long)gridDim.x * NT) {
+    float x[8], y[8];
+    unpack8(reinterpret_cast<const s16x8*>(a)[i], x);
+    unpack8(reinterpret_cast<const s16x8*>(b)[i], y);
+#pragma unroll
+    for (int u = 0; u < 8; ++u) x[u] += y[u];
+    reinterpret_cast<s16x8*>(out)[i] = pack8(x);
+  }
+}
+
+// bias gradient: acc[c] += sum over rows of dY[row][c] (rows: base + b*img_stride + q, q < HW)
+__global__ void colsum_kernel(const cvl_bf16* dy, int ld, int coff, int ncol, long base, long img_stride,
+                              int HW, int B, int rows_per_blk, double* acc) {
+  const int col = threadIdx.x % 64 + blockIdx.y * 64;
+  const int rsub = threadIdx.x / 64;
+  const long nrows = (long)B * HW;
+  const long r0 = (long)blockIdx.x * rows_per_blk;
+  const long r1 = r0 + rows_per_blk < nrows ? r0 + rows_per_blk : nrows;
+  float s = 0.f;
+  if (col < ncol) {
+    for (long r = r0 + rsub; r < r1; r += NT / 64) {
+      const int b = (int)(r / HW);
+      const long row = base + (long)b * img_stride + (r - (long)b * HW);
+      s += bf16_to_f32(dy[row * ld + coff + col]);
+    }
+  }
+  __shared__ float red[NT];
+  red[threadIdx.x] = s;
+  __syncthreads();
+  if (rsub == 0 && col < ncol) {
+    double t = 0.0;
+    for (int k = 0; k < NT / 64; ++k) t += red[k * 64 + threadIdx.x];
+    atomicAdd(&acc[col], t);
+  }
+}
+
+__global__ void colsum_finish_kernel(const double* acc, float* db, int ncol, float beta) {
+  const int c = blockIdx.x * NT + threadIdx.x;
+  if (c < ncol) db[c] = (float)acc[c] + (beta != 0.f ? beta * db[c] : 0.f);
+}
+
+// ---------------------------------------------------------------------------------------------
+// optimizer: clip_by_global_norm(g * inv_bs, clip) + Keras SGD momentum, flat fp32 buffers
+// ---------------------------------------------------------------------------------------------
+__global__ void sumsq_kernel(const float* g, long n, double* out) {
+  float s = 0.f;
+  for (long i = blockIdx.x * (long)NT + threadIdx.x; i < n; i += (long)gridDim.x * NT) s += g[i] * g[i];
+  double d = warp_sum_d((double)s);
+  __shared__ double red[NT / 64];
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = d;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double t = 0.0;
+    for (int k = 0; k < NT / 64; ++k) t += red[k];
+    atomicAdd(out, t);
+  }
+}
+
+__global__ void sgd_kernel(float* w, const float* g, float* v, long n, const float* lr_dev,
+                           float momentum, float inv_bs, float clip, const double* gsumsq) {
+  // gsumsq holds sum((g)^2) of the UNscaled grads: norm of (g * inv_bs) = sqrt(gsumsq) * inv_bs
+  const double norm = sqrt(*gsumsq) * (double)inv_bs;
+  const float scale = inv_bs * (float)(clip > 0.f ? (double)clip / (norm > clip ? norm : (double)clip) : 1.0);
+  const float lr = *lr_dev;
+  for (long i = blockIdx.x * (long)NT + threadIdx.x; i < n; i += (long)gridDim.x * NT) {
+    const float gg = g[i] * scale;
+    const float vv = momentum * v[i] - lr * gg;
+    v[i] = vv;
+    w[i] = w[i] + vv;
+  }
+}
+
+// lr = max(init * rate^floor(step / decay_step), min_lr); step += 1   (train_fcos.py:108-110)
+__global__ void lr_schedule_kernel(int* step, float* lr, double init_lr, double min_lr, double rate,
+                                   int decay_step) {
+  const int s = *step;
+  const double l = init_lr * pow(rate, (double)(s / decay_step));
+  *lr = (float)(l > min_lr ? l : min_lr);
+  *step = s + 1;
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------------------------------------
+// C ABI
+// ---------------------------------------------------------------------------------------------
+#define S_ ((hipStream_t)stream)
+
+extern "C" int cvl_pack_conv_weights(const float* w_hwio, int KH, int KW, int Cin, int Cout, int Cin_k,
+                                     int Npad, void* w_fwd, int Cin_pad, int Cout_pad, void* w_dgrad,
+                                     cvl_stream_t stream) {
+  CVL_CHECK_ARG(w_hwio && KH > 0 && KW > 0 && Cin > 0 && Cout > 0 && Cin_k >= Cin && Npad >= Cout);
+  if (w_fwd) {
+    const long total = (long)Npad * KH * KW * Cin_k;
+    hipLaunchKernelGGL(pack_fwd_kernel, dim3(grid_for(total)), dim3(NT), 0, S_, w_hwio, (cvl_bf16*)w_fwd,
+                       KH * KW, Cin, Cin_k, Cout, Npad);
+  }
+  if (w_dgrad) {
+    CVL_CHECK_ARG(Cin_pad >= Cin && Cout_pad >= Cout);
+    const long total = (long)Cin_pad * KH * KW * Cout_pad;
+    hipLaunchKernelGGL(pack_dgrad_kernel, dim3(grid_for(total)), dim3(NT), 0, S_, w_hwio,
+                       (cvl_bf16*)w_dgrad, KH * KW, Cin, Cout, Cin_pad, Cout_pad);
+  }
+  return cvl_launch_status();
+}
+
+extern "C" int cvl_im2col(const float* x, int B, int H, int W, int C, int KH, int KW, int stride, int pad_t,
+                          int pad_l, int Ho, int Wo, int Kp, void* out, cvl_stream_t stream) {
+  CVL_CHECK_ARG(x && out && B > 0 && Kp >= KH * KW * C);
+  const long total = (long)B * Ho * Wo * Kp;
+  hipLaunchKernelGGL(im2col_kernel, dim3(grid_for(total)), dim3(NT), 0, S_, x, (cvl_bf16*)out, B, H, W,
+                     C, KH, KW, stride, pad_t, pad_l, Ho, Wo, Kp);
+  return cvl_launch_status();
+}
+
+extern "C" int cvl_bn_finalize(const double* stats, float* mean_rstd, float* run_mean, float* run_var,
+                               int B, int C, int HW, float eps, float momentum, cvl_stream_t stream) {
+  CVL_CHECK_ARG(stats && mean_rstd && B > 0 && C > 0 && HW > 0);
+  hipLaunchKernelGGL(bn_finalize_kernel, dim3((C + NT - 1) / NT), dim3(NT), 0, S_, stats, mean_rstd,
+                     run_mean, run_var, B, C, HW, eps, momentum);
+  return cvl_launch_status();
+}
+
+extern "C" int cvl_bn_apply(const void* z, const float* mean_rstd, const float* gamma, const float* beta,
+                            const void* residual, void* y, int B, int HW, int C, int relu,
+                            cvl_stream_t stream) {
+  CVL_CHECK_ARG(z && mean_rstd && gamma && beta && y && C % 8 == 0);
+  const long rows = (long)B * HW;
+  hipLaunchKernelGGL(bn_apply_kernel, dim3(grid_for(rows * (C / 8))), dim3(NT), 0, S_, (const cvl_bf16*)z,
+                     mean_rstd, gamma, beta, (const cvl_bf16*)residual, (cvl_bf16*)y, rows, C, HW, relu);
+  return cvl_launch_status();
+}
+
+extern "C" int cvl_bn_backward(const void* dy, const void* y_relu, const void* z, const float* mean_rstd,
+                               const float* gamma, double* sums_ws, void* dz, void* g_out, float* dgamma,
+                               float* dbeta, float beta_acc, int B, int HW, int C, cvl_stream_t stream) {
+  CVL_CHECK_ARG(dy && z && mean_rstd && gamma && sums_ws && dz && dgamma && dbeta && C % 8 == 0);
+  hipError_t e = hipMemsetAsync(sums_ws, 0, sizeof(double) * 2 * B * C, S_);
+  if (e != hipSuccess) return CVL_EHIP + (int)e;
+  int rows_per_blk = 256;
+  while ((long)B * ((HW + rows_per_blk - 1) / rows_per_blk) > 2048 && rows_per_blk < HW) rows_per_blk *= 2;
+  dim3 g1((HW + rows_per_blk - 1) / rows_per_blk, B);
+  hipLaunchKernelGGL(bn_bwd_reduce_kernel, g1, dim3(NT), 0, S_, (const cvl_bf16*)dy, (const cvl_bf16*)y_relu,
+                     (const cvl_bf16*)z, mean_rstd, sums_ws, C, HW, rows_per_blk);
+  const long rows = (long)B * HW;
+  hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(grid_for(rows * (C / 8))), dim3(NT), 0, S_,
+                     (const cvl_bf16*)dy, (const cvl_bf16*)y_relu, (const cvl_bf16*)z, mean_rstd, gamma,
+                     (const double*)sums_ws, (cvl_bf16*)dz, (cvl_bf16*)g_out, rows, C, HW);
+  hipLaunchKernelGGL(bn_param_grad_kernel, dim3((C + NT - 1) / NT), dim3(NT), 0, S_, (const double*)sums_ws,
+                     dgamma, dbeta, B, C, beta_acc);
+  return cvl_launch_status();
+}
+
+extern "C" int cvl_maxpool3x3s2(const void* x, void* y, uint8_t* argmax, int B, int H, int W, int C,
+                                cvl_stream_t stream) {
+  CVL_CHECK_ARG(x && y && argmax && C % 8 == 0);
+  const int Ho = (H + 2 - 3) / 2 + 1, Wo = (W + 2 - 3) / 2 + 1;
+  const long total = (long)B * Ho * Wo * (C / 8);
+  hipLaunchKernelGGL(maxpool_fwd_kernel, dim3(grid_for(total)), dim3(NT), 0, S_, (const cvl_bf16*)x,
+                     (cvl_bf16*)y, argmax, B, H, W, C, Ho, Wo);
+  return cvl_launch_status();
+}
+
+extern "C" int cvl_maxpool3x3s2_backward(const void* dy, const uint8_t* argmax, void* dx, int B, int H,
+                                         int W, int C, cvl_stream_t stream) {
+  CVL_CHECK_ARG(dy && dx && argmax && C % 8 == 0);
+  const int Ho = (H + 2 - 3) / 2 + 1, Wo = (W + 2 - 3) / 2 + 1;
+  const long total = (long)B * H * W * (C / 8);
+  hipLaunchKernelGGL(maxpool_bwd_kernel, dim3(grid_for(total)), dim3(NT), 0, S_, (const cvl_bf16*)dy,
+                     argmax, (cvl_bf16*)dx, B, H, W, C, Ho, Wo);
+  return cvl_launch_status();
+}
+
+extern "C" int cvl_upsample2x_add(const void* a, const void* b, void* out, int B, int H, int W, int C,
+                                  cvl_stream_t stream) {
+  CVL_CHECK_ARG(a && b && out && C % 8 == 0 && H % 2 == 0 && W % 2 == 0);
+  const long total = (long)B * H * W * (C / 8);
+  hipLaunchKernelGGL(upsample_add_kernel, dim3(grid_for(total)), dim3(NT), 0, S_, (const cvl_bf16*)a,
+                     (const cvl_bf16*)b, (cvl_bf16*)out, B, H, W, C);
+  return cvl_launch_status();
+}
+
+extern "C" int cvl_upsample2x_backward(const void* dout, void* db, int B, int H, int W, int C, float beta,
+                                       cvl_stream_t stream) {
+  CVL_CHECK_ARG(dout && db && C % 8 == 0 && H % 2 == 0 && W % 2 == 0);
+  const long total = (long)B * (H / 2) * (W / 2) * (C / 8);
+  hipLaunchKernelGGL(upsample_bwd_kernel, dim3(grid_for(total)), dim3(NT), 0, S_, (const cvl_bf16*)dout,
+                     (cvl_bf16*)db, B, H, W, C, beta);
+  return cvl_launch_status();
+}
+
+extern "C" int cvl_relu_backward(const void* dy, const void* y, void* dx, long n, float beta,
+                                 cvl_stream_t stream) {
+  CVL_CHECK_ARG(dy && y && dx && n % 8 == 0);
+  hipLaunchKernelGGL(relu_bwd_kernel, dim3(grid_for(n / 8)), dim3(NT), 0, S_, (const cvl_bf16*)dy,
+                     (const cvl_bf16*)y, (cvl_bf16*)dx, n / 8, beta);
+  return cvl_launch_status();
+}
+
+extern "C" int cvl_add(const void* a, const void* b, void* out, long n, cvl_stream_t stream) {
+  CVL_CHECK_ARG(a && b && out && n % 8 == 0);
+  hipLaunchKernelGGL(add_kernel, dim3(grid_for(n / 8)), dim3(NT), 0, S_, (const cvl_bf16*)a,
+                     (const cvl_bf16*)b, (cvl_bf16*)out, n / 8);
+  return cvl_launch_status();
+}
+
+extern "C" int cvl_bias_grad(const void* dy, int ld, int coff, int ncol, int64_t base, int64_t img_stride,
+                             int HW, int B, double* acc_ws, float* db, float beta, cvl_stream_t stream) {
+  CVL_CHECK_ARG(dy && acc_ws && db && ncol > 0 && HW > 0 && B > 0);
+  hipError_t e = hipMemsetAsync(acc_ws, 0, sizeof(double) * ncol, S_);
+  if (e != hipSuccess) return CVL_EHIP + (int)e;
+  const long nrows = (long)B * HW;
+  int rows_per_blk = 512;
+  while ((nrows + rows_per_blk - 1) / rows_per_blk > 1024) rows_per_blk *= 2;
+  dim3 g((int)((nrows + rows_per_blk - 1) / rows_per_blk), (ncol + 63) / 64);
+  hipLaunchKernelGGL(colsum_kernel, g, dim3(NT), 0, S_, (const cvl_bf16*)dy, ld, coff, ncol, (long)base,
+                     (long)img_stride, HW, B, rows_per_blk, acc_ws);
+  hipLaunchKernelGGL(colsum_finish_kernel, dim3((ncol + NT - 1) / NT), dim3(NT), 0, S_, (const double*)acc_ws,
+                     db, ncol, beta);
+  return cvl_launch_status();
+}
+
+extern "C" int cvl_sgd_clip_update(float* w, const float* g, float* v, int64_t n, const float* lr_dev,
+                                   float momentum, float inv_bs, float clip, double* sumsq_ws,
+                                   cvl_stream_t stream) {
+  CVL_CHECK_ARG(w && g && v && n > 0 && lr_dev && sumsq_ws);
+  hipError_t e = hipMemsetAsync(sumsq_ws, 0, sizeof(double), S_);
+  if (e != hipSuccess) return CVL_EHIP + (int)e;
+  hipLaunchKernelGGL(sumsq_kernel, dim3(grid_for(n, NT * 8, 2048)), dim3(NT), 0, S_, g, (long)n, sumsq_ws);
+  hipLaunchKernelGGL(sgd_kernel, dim3(grid_for(n, NT * 4, 4096)), dim3(NT), 0, S_, w, g, v, (long)n, lr_dev,
+                     momentum, inv_bs, clip, (const double*)sumsq_ws);
+  return cvl_launch_status();
+}
+
+extern "C" int cvl_lr_schedule(int32_t* step, float* lr, double init_lr, double min_lr, double decay_rate,
+                               int decay_step, cvl_stream_t stream) {
+  CVL_CHECK_ARG(step && lr && decay_step > 0);
+  hipLaunchKernelGGL(lr_schedule_kernel, dim3(1), dim3(1), 0, S_, step, lr, init_lr, min_lr, decay_rate,
+                     decay_step);
+  return cvl_launch_status();
+}

@@ -23,6 +23,25 @@ SIGNATURES = {
     "cvl_fcos_loss_workspace_size": (c_size_t, [c_int, c_int]),
     "cvl_fcos_loss": (c_int, [P, c_int, P, c_int, P, c_int, c_int, c_int, c_int, c_float, P,
                               P, c_int, c_int, P, c_int, c_int, P, P]),
+    "cvl_conv_igemm": (c_int, [P, P, P, P, P]),
+    "cvl_conv_wgrad_workspace_size": (c_size_t, [P]),
+    "cvl_conv_wgrad": (c_int, [P, P, P, P, c_float, P, c_size_t, P]),
+    "cvl_pack_conv_weights": (c_int, [P, c_int, c_int, c_int, c_int, c_int, c_int, P, c_int, c_int, P, P]),
+    "cvl_im2col": (c_int, [P, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int,
+                           c_int, c_int, P, P]),
+    "cvl_bn_finalize": (c_int, [P, P, P, P, c_int, c_int, c_int, c_float, c_float, P]),
+    "cvl_bn_apply": (c_int, [P, P, P, P, P, P, c_int, c_int, c_int, c_int, P]),
+    "cvl_bn_backward": (c_int, [P, P, P, P, P, P, P, P, P, P, c_float, c_int, c_int, c_int, P]),
+    "cvl_maxpool3x3s2": (c_int, [P, P, P, c_int, c_int, c_int, c_int, P]),
+    "cvl_maxpool3x3s2_backward": (c_int, [P, P, P, c_int, c_int, c_int, c_int, P]),
+    "cvl_upsample2x_add": (c_int, [P, P, P, c_int, c_int, c_int, c_int, P]),
+    "cvl_upsample2x_backward": (c_int, [P, P, c_int, c_int, c_int, c_int, c_float, P]),
+    "cvl_relu_backward": (c_int, [P, P, P, ctypes.c_long, c_float, P]),
+    "cvl_add": (c_int, [P, P, P, ctypes.c_long, P]),
+    "cvl_bias_grad": (c_int, [P, c_int, c_int, c_int, ctypes.c_int64, ctypes.c_int64, c_int, c_int, P, P,
+                              c_float, P]),
+    "cvl_sgd_clip_update": (c_int, [P, P, P, ctypes.c_int64, P, c_float, c_float, c_float, P, P]),
+    "cvl_lr_schedule": (c_int, [P, P, ctypes.c_double, ctypes.c_double, ctypes.c_double, c_int, P]),
 }
 
 

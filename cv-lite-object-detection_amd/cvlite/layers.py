@@ -1,0 +1,264 @@
+"""Parameter store and layer objects of the explicit (tape-free) training graph.
+
+All trainable fp32 parameters live in ONE flat device buffer (and so do their gradients and the
+SGD momentum): the optimizer is one fused launch, data-parallel all-reduce is one bucketed
+collective, and checkpoints are one tensor.  Each conv keeps bf16 packed copies of its weights
+(forward and data-gradient layouts) refreshed after every update.  Names follow the Keras layer
+names of the reference graph (e.g. `conv2_block1_1_conv/kernel`, `cls_layer_1/kernel`,
+`logits_output_1/bias`) so a TF checkpoint can be mapped onto the store.
+"""
+import math
+
+import torch
+
+from . import ops_nn as nn
+
+BF16 = torch.bfloat16
+
+
+def glorot_uniform(fan_in, fan_out):
+    lim = math.sqrt(6.0 / (fan_in + fan_out))
+
+    def init(gen, shape):
+        return (torch.rand(shape, generator=gen, dtype=torch.float64) * 2 - 1).mul_(lim).float()
+    return init
+
+
+def constant(v):
+    def init(gen, shape):
+        return torch.full(shape, float(v), dtype=torch.float32)
+    return init
+
+
+def same_pad(n, k, s):
+    """TF 'same': output size and leading pad (asymmetric: extra pad goes bottom/right)."""
+    out = -(-n // s)
+    total = max((out - 1) * s + k - n, 0)
+    return out, total // 2
+
+
+class ParamStore(object):
+    """Flat fp32 parameter / gradient / momentum buffers with named views."""
+
+    def __init__(self):
+        self.specs = []      # (name, shape, init)
+        self.index = {}
+        self.finalized = False
+
+    def add(self, name, shape, init):
+        assert not self.finalized and name not in self.index
+        self.index[name] = len(self.specs)
+        self.specs.append((name, tuple(shape), init))
+        return name
+
+    def finalize(self, device, seed=0):
+        sizes = [int(math.prod(s)) for _, s, _ in self.specs]
+        # 16-element alignment keeps every view 64-byte aligned
+        offs, o = [], 0
+        for n in sizes:
+            offs.append(o)
+            o += (n + 15) // 16 * 16
+        self.numel = o
+        self.flat = torch.zeros(o, dtype=torch.float32, device=device)
+        self.grad = torch.zeros(o, dtype=torch.float32, device=device)
+        self.mom = torch.zeros(o, dtype=torch.float32, device=device)
+        gen = torch.Generator().manual_seed(seed)
+        host = torch.zeros(o, dtype=torch.float32)
+        self.offsets = {}
+        for (name, shape, init), off, n in zip(self.specs, offs, sizes):
+            host[off:off + n] = init(gen, shape).reshape(-1)
+            self.offsets[name] = (off, n, shape)
+        self.flat.copy_(host.to(device))
+        self.finalized = True
+
+    def p(self, name):
+        off, n, shape = self.offsets[name]
+        return self.flat[off:off + n].view(shape)
+
+    def g(self, name):
+        off, n, shape = self.offsets[name]
+        return self.grad[off:off + n].view(shape)
+
+    @property
+    def n_params(self):
+        return sum(n for (off, n, _) in self.offsets.values())
+
+    def state_dict(self):
+        return {name: self.p(name).detach().cpu().clone() for name in self.offsets}
+
+    def load_state_dict(self, sd):
+        for name, t in sd.items():
+            self.p(name).copy_(t.to(self.flat.device))
+
+
+class Conv(object):
+    """Keras Conv2D (HWIO kernel, glorot-uniform init, zero bias) on the segmented MFMA conv.
+
+    pad: 'same' (TF padding), 'valid', or an explicit leading pad int (ZeroPadding2D + valid)."""
+
+    def __init__(self, store, name, k, cin, cout, stride=1, pad="same", bias=True, bias_init=0.0,
+                 cin_k=None, npad=None, cout_pad=None, dgrad=True):
+        self.name, self.k, self.cin, self.cout, self.stride, self.pad = name, k, cin, cout, stride, pad
+        self.cin_k = cin if cin_k is None else cin_k       # channels per tap in the forward pack
+        self.npad = npad if npad is not None else max(32, (cout + 31) // 32 * 32)
+        self.cout_pad = cout_pad if cout_pad is not None else self.npad   # dgrad pack K-channels
+        self.cin_pad = (cin + 31) // 32 * 32
+        self.has_bias = bias
+        self.need_dgrad = dgrad
+        self.wname = store.add(name + "/kernel", (k, k, cin, cout), glorot_uniform(k * k * cin, k * k * cout))
+        self.bname = store.add(name + "/bias", (cout,), constant(bias_init)) if bias else None
+        self.store = store
+        self.wf = self.wd = None
+        self._bias_pad = None
+
+    # ---- geometry -----------------------------------------------------------------------------
+    def out_hw(self, H, W):
+        if self.pad == "same":
+            (Ho, pt), (Wo, pl) = same_pad(H, self.k, self.stride), same_pad(W, self.k, self.stride)
+        elif self.pad == "valid":
+            Ho, Wo, pt, pl = (H - self.k) // self.stride + 1, (W - self.k) // self.stride + 1, 0, 0
+        else:
+            p = int(self.pad)
+            Ho, Wo = (H + 2 * p - self.k) // self.stride + 1, (W + 2 * p - self.k) // self.stride + 1
+            pt = pl = p
+        return Ho, Wo, pt, pl
+
+    # ---- parameters ---------------------------------------------------------------------------
+    @property
+    def w(self):
+        return self.store.p(self.wname)
+
+    @property
+    def b(self):
+        return self.store.p(self.bname) if self.bname else None
+
+    @property
+    def dw(self):
+        return self.store.g(self.wname)
+
+    @property
+    def db(self):
+        return self.store.g(self.bname) if self.bname else None
+
+    def bias_arg(self):
+        if not self.has_bias:
+            return None
+        if self.npad == self.cout:
+            return self.b
+        assert self._bias_pad is not None, "pack() before use"
+        return self._bias_pad
+
+    def pack(self):
+        dev = self.store.flat.device
+        K = self.k * self.k * self.cin_k
+        if self.wf is None:
+            self.wf = torch.empty((self.npad, K), dtype=BF16, device=dev)
+            if self.need_dgrad:
+                self.wd = torch.empty((self.cin_pad, self.k * self.k * self.cout_pad), dtype=BF16, device=dev)
+        nn.pack_conv_weights(self.w, self.k, self.k, self.cin, self.cout, self.cin_k, self.npad, self.wf,
+                             self.cin_pad, self.cout_pad, self.wd if self.need_dgrad else None)
+        if self.has_bias and self.npad != self.cout:
+            if self._bias_pad is None:
+                self._bias_pad = torch.zeros(self.npad, dtype=torch.float32, device=dev)
+            self._bias_pad[:self.cout].copy_(self.b)
+
+    # ---- descriptors ----------------------------------------------------------------------------
+    def fwd_desc(self, B, segs, ld_dst=None, dst_coff=0, dst_f32=False, relu_out=False, relu_in=False,
+                 beta=0.0, n_store=None):
+        _, _, pt, pl = self.out_hw(segs[0]["Hs"], segs[0]["Ws"])
+        return nn.make_desc(nn.FWD, B, self.cin_k, self.k, self.k, self.stride, pt, pl, self.npad,
+                            self.cout if n_store is None else n_store,
+                            self.npad if ld_dst is None else ld_dst, segs, dst_coff=dst_coff,
+                            dst_f32=dst_f32, relu_out=relu_out, relu_in=relu_in, beta=beta)
+
+    def dgrad_desc(self, B, segs, ld_dst=None, beta=0.0):
+        """segs in dgrad form: Hr/Wr = input map (dX), Hs/Ws = output map (dY)."""
+        Ho, Wo = segs[0]["Hs"], segs[0]["Ws"]
+        _, _, pt, pl = self.out_hw(segs[0]["Hr"], segs[0]["Wr"])
+        return nn.make_desc(nn.DGRAD, B, self.cout_pad, self.k, self.k, self.stride, pt, pl, self.cin_pad,
+                            self.cin, self.cin if ld_dst is None else ld_dst, segs, beta=beta)
+
+    # ---- plain single-map helpers -----------------------------------------------------------------
+    def fwd(self, x, B, H, W, out=None, stats=None, relu_out=False, relu_in=False):
+        Ho, Wo, _, _ = self.out_hw(H, W)
+        if out is None:
+            out = torch.empty((B, Ho, Wo, self.cout), dtype=BF16, device=x.device)
+        d = self.fwd_desc(B, [nn.seg(Ho, Wo, H, W, self.wf, self.bias_arg())], ld_dst=self.cout,
+                          relu_out=relu_out, relu_in=relu_in)
+        nn.conv_igemm(d, x, out, stats)
+        return out, Ho, Wo
+
+    def wgrad(self, x, dy, B, H, W, relu_in=False, dw=None, beta=0.0):
+        Ho, Wo, _, _ = self.out_hw(H, W)
+        d = self.fwd_desc(B, [nn.seg(Ho, Wo, H, W, self.wf, None)], ld_dst=self.cout_pad_ld(dy),
+                          relu_in=relu_in)
+        nn.conv_wgrad(d, x, dy, self.dw if dw is None else dw, beta)
+        if self.has_bias:
+            nn.bias_grad(dy, self.cout_pad_ld(dy), 0, self.cout, 0, Ho * Wo, Ho * Wo, B, self.db)
+
+    def cout_pad_ld(self, dy):
+        return int(dy.shape[-1])
+
+    def dgrad(self, dy, B, H, W, out=None, beta=0.0):
+        Ho, Wo, _, _ = self.out_hw(H, W)
+        if out is None:
+            out = torch.empty((B, H, W, self.cin), dtype=BF16, device=dy.device)
+        d = self.dgrad_desc(B, [nn.seg(H, W, Ho, Wo, self.wd)], ld_dst=self.cin, beta=beta)
+        nn.conv_igemm(d, dy, out)
+        return out
+
+
+class BatchNorm(object):
+    """Keras BatchNormalization(axis=-1) in training mode with per-image statistics."""
+
+    def __init__(self, store, name, c, eps=1.001e-5, momentum=0.99):
+        self.name, self.c, self.eps, self.momentum = name, c, eps, momentum
+        self.gname = store.add(name + "/gamma", (c,), constant(1.0))
+        self.bname = store.add(name + "/beta", (c,), constant(0.0))
+        self.store = store
+        self.run_mean = self.run_var = None
+
+    def init_buffers(self, device):
+        self.run_mean = torch.zeros(self.c, dtype=torch.float32, device=device)
+        self.run_var = torch.ones(self.c, dtype=torch.float32, device=device)
+
+    @property
+    def gamma(self):
+        return self.store.p(self.gname)
+
+    @property
+    def beta(self):
+        return self.store.p(self.bname)
+
+
+class ConvBN(object):
+    """conv -> BN (-> + residual) (-> ReLU): the Keras ResNet50 unit."""
+
+    def __init__(self, store, name, k, cin, cout, stride=1, pad="same", dgrad=True, cin_k=None,
+                 bn_name=None):
+        self.conv = Conv(store, name + "_conv" if bn_name is None else name, k, cin, cout, stride, pad,
+                         bias=True, dgrad=dgrad, cin_k=cin_k)
+        self.bn = BatchNorm(store, (name + "_bn") if bn_name is None else bn_name, cout)
+
+    def forward(self, x, B, H, W, relu=True, residual=None, train=True):
+        c = self.conv.cout
+        Ho, Wo, _, _ = self.conv.out_hw(H, W)
+        stats = torch.zeros((B, c, 2), dtype=torch.float64, device=x.device)
+        z, _, _ = self.conv.fwd(x, B, H, W, stats=stats)
+        mr = torch.empty((B, c, 2), dtype=torch.float32, device=x.device)
+        nn.bn_finalize(stats, mr, self.bn.run_mean if train else None, self.bn.run_var if train else None,
+                       B, c, Ho * Wo, self.bn.eps, self.bn.momentum)
+        y = torch.empty_like(z)
+        nn.bn_apply(z, mr, self.bn.gamma, self.bn.beta, residual, y, B, Ho * Wo, c, relu)
+        return y, (x, z, y, mr, B, H, W, Ho, Wo, relu)
+
+    def backward(self, dy, saved, dx_out=None, dx_beta=0.0, g_out=None, need_dx=True):
+        x, z, y, mr, B, H, W, Ho, Wo, relu = saved
+        c = self.conv.cout
+        dz = torch.empty_like(z)
+        nn.bn_backward(dy, y if relu else None, z, mr, self.bn.gamma, dz, g_out,
+                       self.bn.store.g(self.bn.gname), self.bn.store.g(self.bn.bname), B, Ho * Wo, c)
+        self.conv.wgrad(x, dz, B, H, W)
+        if not need_dx:
+            return None
+        return self.conv.dgrad(dz, B, H, W, out=dx_out, beta=dx_beta)

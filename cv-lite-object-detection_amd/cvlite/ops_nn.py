@@ -1,0 +1,134 @@
+"""Device ops of the conv/BN/FPN training graph: thin torch-tensor wrappers over the C ABI
+(include/cvlite.h).  Tensors are raw storage (bf16 activations NHWC, fp32 params); no autograd."""
+import ctypes
+
+import torch
+
+from . import _lib
+from ._lib import ptr, stream
+
+c_int, c_int64, c_float, c_void_p = ctypes.c_int, ctypes.c_int64, ctypes.c_float, ctypes.c_void_p
+BF16 = torch.bfloat16
+FWD, DGRAD = 0, 1
+
+
+class ConvSeg(ctypes.Structure):
+    _fields_ = [("Hr", c_int), ("Wr", c_int), ("Hs", c_int), ("Ws", c_int),
+                ("src_base", c_int64), ("src_img", c_int64), ("dst_base", c_int64), ("dst_img", c_int64),
+                ("w", c_void_p), ("bias", c_void_p)]
+
+
+class ConvDesc(ctypes.Structure):
+    _fields_ = [("mode", c_int), ("B", c_int), ("Cin", c_int), ("KH", c_int), ("KW", c_int),
+                ("stride", c_int), ("pad_t", c_int), ("pad_l", c_int), ("Npad", c_int),
+                ("n_store", c_int), ("ld_dst", c_int), ("dst_coff", c_int), ("dst_f32", c_int),
+                ("relu_out", c_int), ("relu_in", c_int), ("beta", c_float), ("nseg", c_int),
+                ("seg", ConvSeg * 5)]
+
+
+def seg(Hr, Wr, Hs, Ws, w, bias=None, src_base=0, src_img=None, dst_base=0, dst_img=None):
+    return dict(Hr=Hr, Wr=Wr, Hs=Hs, Ws=Ws, w=w, bias=bias, src_base=src_base,
+                src_img=Hs * Ws if src_img is None else src_img, dst_base=dst_base,
+                dst_img=Hr * Wr if dst_img is None else dst_img)
+
+
+def make_desc(mode, B, Cin, KH, KW, stride, pad_t, pad_l, Npad, n_store, ld_dst, segs, dst_coff=0,
+              dst_f32=False, relu_out=False, relu_in=False, beta=0.0):
+    d = ConvDesc()
+    d.mode, d.B, d.Cin, d.KH, d.KW = mode, B, Cin, KH, KW
+    d.stride, d.pad_t, d.pad_l, d.Npad, d.n_store = stride, pad_t, pad_l, Npad, n_store
+    d.ld_dst, d.dst_coff, d.dst_f32 = ld_dst, dst_coff, int(bool(dst_f32))
+    d.relu_out, d.relu_in, d.beta = int(bool(relu_out)), int(bool(relu_in)), float(beta)
+    d.nseg = len(segs)
+    keep = []
+    for i, s in enumerate(segs):
+        q = d.seg[i]
+        q.Hr, q.Wr, q.Hs, q.Ws = s["Hr"], s["Wr"], s["Hs"], s["Ws"]
+        q.src_base, q.src_img, q.dst_base, q.dst_img = s["src_base"], s["src_img"], s["dst_base"], s["dst_img"]
+        q.w = s["w"].data_ptr()
+        q.bias = s["bias"].data_ptr() if s["bias"] is not None else None
+        keep.append((s["w"], s["bias"]))
+    d._keep = keep   # keep weight tensors alive as long as the descriptor
+    return d
+
+
+def conv_igemm(desc, src, dst, stats=None):
+    _lib.call("cvl_conv_igemm", ctypes.byref(desc), ptr(src), ptr(dst), ptr(stats), stream())
+
+
+def conv_wgrad(desc, x, dy, dw, beta=0.0):
+    lib = _lib.load()
+    n = int(lib.cvl_conv_wgrad_workspace_size(ctypes.byref(desc)))
+    ws = torch.empty(max(n, 16), dtype=torch.uint8, device=x.device)
+    _lib.call("cvl_conv_wgrad", ctypes.byref(desc), ptr(x), ptr(dy), ptr(dw), float(beta), ptr(ws),
+              ws.numel(), stream())
+
+
+def pack_conv_weights(w_hwio, KH, KW, Cin, Cout, Cin_k, Npad, w_fwd, Cin_pad=0, Cout_pad=0, w_dgrad=None):
+    _lib.call("cvl_pack_conv_weights", ptr(w_hwio), KH, KW, Cin, Cout, Cin_k, Npad, ptr(w_fwd),
+              Cin_pad, Cout_pad, ptr(w_dgrad), stream())
+
+
+def im2col(x, KH, KW, stride, pad_t, pad_l, Ho, Wo, Kp, out):
+    B, H, W, C = x.shape
+    _lib.call("cvl_im2col", ptr(x), B, H, W, C, KH, KW, stride, pad_t, pad_l, Ho, Wo, Kp, ptr(out), stream())
+
+
+def bn_finalize(stats, mean_rstd, run_mean, run_var, B, C, HW, eps, momentum):
+    _lib.call("cvl_bn_finalize", ptr(stats), ptr(mean_rstd), ptr(run_mean), ptr(run_var), B, C, HW,
+              float(eps), float(momentum), stream())
+
+
+def bn_apply(z, mean_rstd, gamma, beta, residual, y, B, HW, C, relu):
+    _lib.call("cvl_bn_apply", ptr(z), ptr(mean_rstd), ptr(gamma), ptr(beta), ptr(residual), ptr(y),
+              B, HW, C, int(bool(relu)), stream())
+
+
+def bn_backward(dy, y_relu, z, mean_rstd, gamma, dz, g_out, dgamma, dbeta, B, HW, C, beta_acc=0.0):
+    ws = torch.empty((B, C, 2), dtype=torch.float64, device=dy.device)
+    _lib.call("cvl_bn_backward", ptr(dy), ptr(y_relu), ptr(z), ptr(mean_rstd), ptr(gamma), ptr(ws),
+              ptr(dz), ptr(g_out), ptr(dgamma), ptr(dbeta), float(beta_acc), B, HW, C, stream())
+
+
+def maxpool3x3s2(x, y, argmax):
+    B, H, W, C = x.shape
+    _lib.call("cvl_maxpool3x3s2", ptr(x), ptr(y), ptr(argmax), B, H, W, C, stream())
+
+
+def maxpool3x3s2_backward(dy, argmax, dx):
+    B, H, W, C = dx.shape
+    _lib.call("cvl_maxpool3x3s2_backward", ptr(dy), ptr(argmax), ptr(dx), B, H, W, C, stream())
+
+
+def upsample2x_add(a, b, out, B, H, W, C):
+    _lib.call("cvl_upsample2x_add", ptr(a), ptr(b), ptr(out), B, H, W, C, stream())
+
+
+def upsample2x_backward(dout, db, B, H, W, C, beta=0.0):
+    _lib.call("cvl_upsample2x_backward", ptr(dout), ptr(db), B, H, W, C, float(beta), stream())
+
+
+def relu_backward(dy, y, dx, beta=0.0):
+    _lib.call("cvl_relu_backward", ptr(dy), ptr(y), ptr(dx), dy.numel(), float(beta), stream())
+
+
+def add(a, b, out):
+    _lib.call("cvl_add", ptr(a), ptr(b), ptr(out), a.numel(), stream())
+
+
+def bias_grad(dy, ld, coff, ncol, base, img_stride, HW, B, db, beta=0.0):
+    ws = torch.empty(ncol, dtype=torch.float64, device=dy.device)
+    _lib.call("cvl_bias_grad", ptr(dy), ld, coff, ncol, int(base), int(img_stride), HW, B, ptr(ws), ptr(db),
+              float(beta), stream())
+
+
+def sgd_clip_update(w, g, v, lr_dev, momentum, inv_bs, clip, ws=None):
+    if ws is None:
+        ws = torch.empty(1, dtype=torch.float64, device=w.device)
+    _lib.call("cvl_sgd_clip_update", ptr(w), ptr(g), ptr(v), w.numel(), ptr(lr_dev), float(momentum),
+              float(inv_bs), float(clip), ptr(ws), stream())
+
+
+def lr_schedule(step_dev, lr_dev, init_lr, min_lr, decay_rate, decay_step):
+    _lib.call("cvl_lr_schedule", ptr(step_dev), ptr(lr_dev), float(init_lr), float(min_lr),
+              float(decay_rate), int(decay_step), stream())

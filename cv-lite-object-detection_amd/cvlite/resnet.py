@@ -1,0 +1,180 @@
+"""ResNet-50 v1 backbone (the Keras `tf.keras.applications.ResNet50` graph tapped by
+FCOS/fcos.py:30-46 and RetinaNet/retinanet_module.py:32-38), explicit forward/backward on the
+cvlite kernels.  Keras layer names are kept (`conv1_conv`, `conv2_block1_0_conv`, ...).
+
+Keras ResNet50 v1 structure (third-party, restated): ZeroPadding2D(3) -> conv1 7x7/2 (+bias)
+-> BN -> ReLU -> ZeroPadding2D(1) -> MaxPool 3x3/2 -> stacks of bottleneck blocks
+(filters 64/128/256/512, blocks 3/4/6/3, stride on the first 1x1 and on the projection
+shortcut of each stack's first block, BN eps 1.001e-5) -> C3 = conv3_block4_out,
+C4 = conv4_block6_out, C5 = conv5_block3_out.
+"""
+import torch
+
+from . import ops_nn as nn
+from .layers import BF16, BatchNorm, Conv, ConvBN
+
+STEM_K = 7
+STEM_KP = 160      # im2col K = 7*7*3 = 147 padded to a multiple of 32
+
+
+class Stem(object):
+    """conv1_conv (7x7/2 after ZeroPadding2D(3)) as im2col + 1x1 MFMA GEMM, conv1_bn, ReLU, pool1."""
+
+    def __init__(self, store):
+        self.conv = Conv(store, "conv1_conv", STEM_K, 3, 64, stride=2, pad=3, bias=True, dgrad=False,
+                         cin_k=STEM_KP)
+        self.bn = BatchNorm(store, "conv1_bn", 64)
+
+    def pack(self):
+        c = self.conv
+        if c.wf is None:
+            c.wf = torch.empty((64, STEM_KP), dtype=BF16, device=c.store.flat.device)
+        # HWIO [7][7][3][64] == [1][1][147][64]: pack as a 1x1 conv with 147 -> 160 channels
+        nn.pack_conv_weights(c.w, 1, 1, 147, 64, STEM_KP, 64, c.wf)
+
+    def _desc(self, B, Ho, Wo):
+        return nn.make_desc(nn.FWD, B, STEM_KP, 1, 1, 1, 0, 0, 64, 64, 64,
+                            [nn.seg(Ho, Wo, Ho, Wo, self.conv.wf, self.conv.b)])
+
+    def forward(self, x, train=True):
+        B, H, W, _ = x.shape
+        Ho, Wo, pt, pl = self.conv.out_hw(H, W)
+        A = torch.empty((B * Ho * Wo, STEM_KP), dtype=BF16, device=x.device)
+        nn.im2col(x, STEM_K, STEM_K, 2, pt, pl, Ho, Wo, STEM_KP, A)
+        stats = torch.zeros((B, 64, 2), dtype=torch.float64, device=x.device)
+        z = torch.empty((B, Ho, Wo, 64), dtype=BF16, device=x.device)
+        nn.conv_igemm(self._desc(B, Ho, Wo), A, z, stats)
+        mr = torch.empty((B, 64, 2), dtype=torch.float32, device=x.device)
+        nn.bn_finalize(stats, mr, self.bn.run_mean if train else None, self.bn.run_var if train else None,
+                       B, 64, Ho * Wo, self.bn.eps, self.bn.momentum)
+        y = torch.empty_like(z)
+        nn.bn_apply(z, mr, self.bn.gamma, self.bn.beta, None, y, B, Ho * Wo, 64, True)
+        Hp, Wp = (Ho + 2 - 3) // 2 + 1, (Wo + 2 - 3) // 2 + 1
+        p = torch.empty((B, Hp, Wp, 64), dtype=BF16, device=x.device)
+        arg = torch.empty((B, Hp, Wp, 64), dtype=torch.uint8, device=x.device)
+        nn.maxpool3x3s2(y, p, arg)
+        return p, (A, z, y, mr, arg, B, Ho, Wo)
+
+    def backward(self, dp, saved):
+        A, z, y, mr, arg, B, Ho, Wo = saved
+        dy = torch.empty_like(y)
+        nn.maxpool3x3s2_backward(dp, arg, dy)
+        dz = torch.empty_like(z)
+        st = self.bn.store
+        nn.bn_backward(dy, y, z, mr, self.bn.gamma, dz, None, st.g(self.bn.gname), st.g(self.bn.bname),
+                       B, Ho * Wo, 64)
+        dw = torch.empty((STEM_KP, 64), dtype=torch.float32, device=dp.device)
+        nn.conv_wgrad(self._desc(B, Ho, Wo), A, dz, dw)
+        self.conv.dw.view(147, 64).copy_(dw[:147])
+        nn.bias_grad(dz, 64, 0, 64, 0, Ho * Wo, Ho * Wo, B, self.conv.db)
+
+
+class Bottleneck(object):
+    """Keras `block1` (resnet.py): [1x1/s -> BN -> ReLU] [3x3 -> BN -> ReLU] [1x1 -> BN] + shortcut -> ReLU."""
+
+    def __init__(self, store, name, cin, filters, stride, conv_shortcut):
+        self.sc = ConvBN(store, name + "_0", 1, cin, 4 * filters, stride) if conv_shortcut else None
+        self.c1 = ConvBN(store, name + "_1", 1, cin, filters, stride)
+        self.c2 = ConvBN(store, name + "_2", 3, filters, filters, 1)
+        self.c3 = ConvBN(store, name + "_3", 1, filters, 4 * filters, 1)
+        self.cout = 4 * filters
+
+    def units(self):
+        return [u for u in (self.sc, self.c1, self.c2, self.c3) if u is not None]
+
+    def forward(self, x, B, H, W, train=True):
+        sv_s = None
+        if self.sc is not None:
+            s, sv_s = self.sc.forward(x, B, H, W, relu=False, train=train)
+        else:
+            s = x
+        y1, sv1 = self.c1.forward(x, B, H, W, relu=True, train=train)
+        H1, W1 = sv1[7], sv1[8]
+        y2, sv2 = self.c2.forward(y1, B, H1, W1, relu=True, train=train)
+        y3, sv3 = self.c3.forward(y2, B, H1, W1, relu=True, residual=s, train=train)
+        return y3, H1, W1, (sv_s, sv1, sv2, sv3)
+
+    def backward(self, dy, saved, dx_out=None, dx_beta=0.0):
+        sv_s, sv1, sv2, sv3 = saved
+        x = sv1[0]
+        if dx_out is None:
+            dx_out = torch.empty_like(x)
+        if self.sc is None:
+            assert dx_beta == 0.0, "identity blocks own their input gradient buffer"
+            g = dx_out                     # residual gradient lands directly in dx
+        else:
+            g = torch.empty_like(dy)
+        dy2 = self.c3.backward(dy, sv3, g_out=g)
+        dy1 = self.c2.backward(dy2, sv2)
+        if self.sc is not None:
+            self.sc.backward(g, sv_s, dx_out=dx_out, dx_beta=dx_beta)
+        self.c1.backward(dy1, sv1, dx_out=dx_out, dx_beta=1.0)
+        return dx_out
+
+
+class ResNet50(object):
+    STACKS = ((64, 3, 1), (128, 4, 2), (256, 6, 2), (512, 3, 2))
+
+    def __init__(self, store):
+        self.stem = Stem(store)
+        self.stages = []
+        cin = 64
+        for si, (f, nb, stride) in enumerate(self.STACKS):
+            stage = []
+            for bi in range(nb):
+                stage.append(Bottleneck(store, "conv%d_block%d" % (si + 2, bi + 1), cin, f,
+                                        stride if bi == 0 else 1, bi == 0))
+                cin = 4 * f
+            self.stages.append(stage)
+
+    def convs(self):
+        out = [self.stem.conv]
+        for st in self.stages:
+            for b in st:
+                out += [u.conv for u in b.units()]
+        return out
+
+    def bns(self):
+        out = [self.stem.bn]
+        for st in self.stages:
+            for b in st:
+                out += [u.bn for u in b.units()]
+        return out
+
+    def pack(self):
+        self.stem.pack()
+        for st in self.stages:
+            for b in st:
+                for u in b.units():
+                    u.conv.pack()
+
+    def forward(self, x, train=True):
+        """x: fp32 NHWC [B,H,W,3] in [-1,1].  Returns [C3, C4, C5] bf16 NHWC and saved state."""
+        B = x.shape[0]
+        h, sv_stem = self.stem.forward(x, train)
+        H, W = h.shape[1], h.shape[2]
+        saved, taps = [], []
+        for st in self.stages:
+            ssv = []
+            for b in st:
+                h, H, W, sv = b.forward(h, B, H, W, train)
+                ssv.append(sv)
+            saved.append(ssv)
+            taps.append((h, H, W))
+        return taps[1:], (sv_stem, saved)
+
+    def backward(self, d_taps, saved):
+        """d_taps: gradients of [C3, C4, C5]; they are used in place as stage-output buffers."""
+        sv_stem, ssv = saved
+        dC = {1: d_taps[0], 2: d_taps[1], 3: d_taps[2]}
+        dh = dC[3]
+        for si in range(3, -1, -1):
+            st = self.stages[si]
+            for bi in range(len(st) - 1, -1, -1):
+                if bi == 0 and (si - 1) in dC:
+                    # this block's input is the previous stage's tap (C3 / C4), whose buffer
+                    # already holds the FPN lateral's gradient: accumulate into it
+                    dh = st[bi].backward(dh, ssv[si][bi], dx_out=dC[si - 1], dx_beta=1.0)
+                else:
+                    dh = st[bi].backward(dh, ssv[si][bi])
+        self.stem.backward(dh, sv_stem)

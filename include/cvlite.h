@@ -63,6 +63,114 @@ int cvl_fcos_loss(const float* reg_pred, int ld_reg, const float* cls_pred, int 
                   float grad_scale, float* losses, void* d_reg, int ld_dreg, int dreg_dtype,
                   void* d_cls, int ld_dcls, int dcls_dtype, void* workspace, cvl_stream_t stream);
 
+
+/* ------------------------------------------------------------------------------------------
+ * Segmented implicit-GEMM convolution (bf16 MFMA, fp32 accumulate).  Replaces every Conv2D of
+ * the reference graphs (Keras ResNet50 backbone; FCOS/fcos.py:49-101 FPN, towers and heads;
+ * RetinaNet/retinanet_module.py:74-148) forward (mode FWD) and backward-input (mode DGRAD).
+ * A "segment" is one feature map of B images: rows of image b live at source/destination rows
+ * base + b*img_stride + (y*W + x), each row holding `Cin` (source) / `ld_dst` (dest) channels.
+ * Several segments in one call share the forward geometry (kernel/stride/pad) but may each have
+ * their own packed weights and bias: the five FPN levels through a shared tower, or the five
+ * per-level heads, are one launch.
+ * Weights: FWD  -> packed [Npad][KH*KW*Cin]   (cvl_pack_conv_weights w_fwd)
+ *          DGRAD-> packed [Npad=Cin_pad][KH*KW*Cout_pad] (w_dgrad); then `Cin` = Cout_pad.
+ * TF "same" padding: pad_t/pad_l = floor(total/2) (asymmetric for stride 2).
+ * bn_stats (nullable) receives per-(image, out channel) (sum, sumsq) in float64 (atomic adds;
+ * zero it first), which requires H*W % 128 == 0 or H*W dividing 128 (and H*W % 4 == 0).
+ * ---------------------------------------------------------------------------------------- */
+#define CVL_CONV_MAX_SEG 5
+enum { CVL_CONV_FWD = 0, CVL_CONV_DGRAD = 1 };
+
+typedef struct {
+  int Hr, Wr;          /* spatial size of the GEMM rows: FWD output map / DGRAD input map */
+  int Hs, Ws;          /* spatial size of the gathered source: FWD input map / DGRAD dY map */
+  int64_t src_base, src_img;  /* source row of image 0 and rows per image */
+  int64_t dst_base, dst_img;  /* destination row of image 0 and rows per image */
+  const void* w;       /* packed bf16 weights for this segment */
+  const float* bias;   /* per output channel, or NULL */
+} cvl_conv_seg;
+
+typedef struct {
+  int mode;            /* CVL_CONV_FWD / CVL_CONV_DGRAD */
+  int B;               /* images per segment */
+  int Cin;             /* channels of each gathered source row (multiple of 32) */
+  int KH, KW, stride, pad_t, pad_l;   /* FORWARD conv geometry */
+  int Npad;            /* GEMM columns = packed weight rows (multiple of 32) */
+  int n_store;         /* columns written (<= Npad) */
+  int ld_dst, dst_coff;/* destination row pitch and channel offset (elements) */
+  int dst_f32;         /* 1: fp32 destination, 0: bf16 */
+  int relu_out;        /* ReLU on the result */
+  int relu_in;         /* ReLU on the gathered source values */
+  float beta;          /* dst = result + beta * dst */
+  int nseg;
+  cvl_conv_seg seg[CVL_CONV_MAX_SEG];
+} cvl_conv_desc;
+
+int cvl_conv_igemm(const cvl_conv_desc* d, const void* src, void* dst, double* bn_stats,
+                   cvl_stream_t stream);
+
+/* Weight gradient (replaces Conv2DBackpropFilter + the per-image gradient accumulation of
+ * FCOS/train_fcos.py:173-176): dw[KH][KW][Cin][n_store] (HWIO fp32) = beta*dw + sum over all
+ * rows of all segments of im2col(x) * dy.  `d` is the FORWARD descriptor (its ld_dst/dst_coff
+ * address dy; all segments must share one weight pointer).  workspace >= *_workspace_size(d). */
+size_t cvl_conv_wgrad_workspace_size(const cvl_conv_desc* d);
+int cvl_conv_wgrad(const cvl_conv_desc* d, const void* x, const void* dy, float* dw, float beta,
+                   void* workspace, size_t workspace_bytes, cvl_stream_t stream);
+
+/* fp32 HWIO [KH][KW][Cin][Cout] master weights -> bf16 forward pack [Npad][KH*KW*Cin_k]
+ * (zero rows >= Cout and channels >= Cin) and/or dgrad pack [Cin_pad][KH*KW*Cout_pad]. */
+int cvl_pack_conv_weights(const float* w_hwio, int KH, int KW, int Cin, int Cout, int Cin_k, int Npad,
+                          void* w_fwd, int Cin_pad, int Cout_pad, void* w_dgrad, cvl_stream_t stream);
+
+/* fp32 NHWC image -> bf16 im2col rows [B*Ho*Wo][Kp] (ResNet50 conv1 after ZeroPadding2D(3)). */
+int cvl_im2col(const float* x, int B, int H, int W, int C, int KH, int KW, int stride, int pad_t,
+               int pad_l, int Ho, int Wo, int Kp, void* out, cvl_stream_t stream);
+
+/* ------------------------------------------------------------------------------------------
+ * BatchNormalization in training mode with per-image statistics (the reference forwards one
+ * image at a time, train_fcos.py:137-153; Keras eps 1.001e-5, momentum 0.99, running variance
+ * unbiased as TF's fused kernel).  stats from cvl_conv_igemm(bn_stats); mean_rstd [B][C][2].
+ * ---------------------------------------------------------------------------------------- */
+int cvl_bn_finalize(const double* stats, float* mean_rstd, float* run_mean, float* run_var, int B,
+                    int C, int HW, float eps, float momentum, cvl_stream_t stream);
+int cvl_bn_apply(const void* z, const float* mean_rstd, const float* gamma, const float* beta,
+                 const void* residual, void* y, int B, int HW, int C, int relu, cvl_stream_t stream);
+/* dy: grad of y; y_relu: y when the unit ends in ReLU (mask), else NULL; writes dz (bf16),
+ * optionally g_out = masked dy (the residual branch's gradient), dgamma/dbeta (= + beta_acc*old).
+ * sums_ws: float64 [B][C][2] workspace. */
+int cvl_bn_backward(const void* dy, const void* y_relu, const void* z, const float* mean_rstd,
+                    const float* gamma, double* sums_ws, void* dz, void* g_out, float* dgamma,
+                    float* dbeta, float beta_acc, int B, int HW, int C, cvl_stream_t stream);
+
+/* ResNet50 pool1: ZeroPadding2D(1) + MaxPooling2D(3, 2); argmax [B][Ho][Wo][C] uint8 (0..8). */
+int cvl_maxpool3x3s2(const void* x, void* y, uint8_t* argmax, int B, int H, int W, int C,
+                     cvl_stream_t stream);
+int cvl_maxpool3x3s2_backward(const void* dy, const uint8_t* argmax, void* dx, int B, int H, int W,
+                              int C, cvl_stream_t stream);
+/* FPN top-down (fcos.py:57-60): out[B,H,W,C] = a + nearest_up2(b[B,H/2,W/2,C]); backward:
+ * db = sum of dout over each 2x2 block (+ beta*db). */
+int cvl_upsample2x_add(const void* a, const void* b, void* out, int B, int H, int W, int C,
+                       cvl_stream_t stream);
+int cvl_upsample2x_backward(const void* dout, void* db, int B, int H, int W, int C, float beta,
+                            cvl_stream_t stream);
+int cvl_relu_backward(const void* dy, const void* y, void* dx, long n, float beta, cvl_stream_t stream);
+int cvl_add(const void* a, const void* b, void* out, long n, cvl_stream_t stream);
+/* bias gradient over a segment's rows: db[c] = beta*db + sum dy[row][coff + c], acc_ws float64[ncol] */
+int cvl_bias_grad(const void* dy, int ld, int coff, int ncol, int64_t base, int64_t img_stride, int HW,
+                  int B, double* acc_ws, float* db, float beta, cvl_stream_t stream);
+
+/* ------------------------------------------------------------------------------------------
+ * Optimizer (train_fcos.py:179-185): g <- (g * inv_bs) clipped by global norm `clip`
+ * (tf.clip_by_global_norm), then Keras SGD momentum v = m*v - lr*g; w += v.  Flat fp32 buffers;
+ * lr read from device memory (graph-capturable); sumsq_ws: one float64.
+ * cvl_lr_schedule: lr = max(init*rate^floor(step/decay_step), min_lr); step += 1 (device ints).
+ * ---------------------------------------------------------------------------------------- */
+int cvl_sgd_clip_update(float* w, const float* g, float* v, int64_t n, const float* lr_dev,
+                        float momentum, float inv_bs, float clip, double* sumsq_ws, cvl_stream_t stream);
+int cvl_lr_schedule(int32_t* step, float* lr, double init_lr, double min_lr, double decay_rate,
+                    int decay_step, cvl_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

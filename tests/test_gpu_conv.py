@@ -1,0 +1,194 @@
+"""GPU parity of the segmented implicit-GEMM conv (fwd / dgrad / wgrad) against a torch fp64
+reference of the same TF-padded convolution on the same bf16-rounded operands.
+Tolerances: bf16 outputs rtol/atol 1e-2 (one bf16 rounding of the result); fp32 outputs 1e-4."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+BF = torch.bfloat16
+
+
+def _pads(n, k, s, mode):
+    if mode == "same":
+        out = -(-n // s)
+        t = max((out - 1) * s + k - n, 0)
+        return out, t // 2, t - t // 2
+    p = int(mode)
+    return (n + 2 * p - k) // s + 1, p, p
+
+
+def ref_conv(x, w, b, stride, pad):
+    """x NHWC, w HWIO (fp64) -> NHWC fp64, TF 'same' or explicit pad."""
+    k = w.shape[0]
+    Ho, pt, pb = _pads(x.shape[1], k, stride, pad)
+    Wo, pl, pr = _pads(x.shape[2], k, stride, pad)
+    xn = F.pad(x.permute(0, 3, 1, 2), (pl, pr, pt, pb))
+    y = F.conv2d(xn, w.permute(3, 2, 0, 1), b, stride)
+    return y.permute(0, 2, 3, 1)
+
+
+def rnd(*shape, scale=1.0, gen=None):
+    return (torch.randn(*shape, generator=gen, dtype=torch.float64) * scale).to(BF).to(torch.float64)
+
+
+def packs(w, cin_k=None, npad=None, cout_pad=None):
+    from cvlite import ops_nn as nn
+    k, _, cin, cout = w.shape
+    cin_k = cin if cin_k is None else cin_k
+    npad = npad or max(32, (cout + 31) // 32 * 32)
+    cout_pad = cout_pad or npad
+    cin_pad = (cin + 31) // 32 * 32
+    wf = torch.empty((npad, k * k * cin_k), dtype=BF, device="cuda")
+    wd = torch.empty((cin_pad, k * k * cout_pad), dtype=BF, device="cuda")
+    nn.pack_conv_weights(w.float().cuda().contiguous(), k, k, cin, cout, cin_k, npad, wf, cin_pad, cout_pad, wd)
+    return wf, wd, npad, cout_pad, cin_pad
+
+
+CASES = [  # (B, H, W, Cin, Cout, k, stride, pad)
+    (2, 16, 16, 64, 64, 3, 1, "same"),
+    (2, 16, 16, 128, 256, 1, 2, "same"),
+    (1, 9, 7, 32, 32, 3, 2, "same"),
+    (3, 8, 8, 256, 96, 3, 1, "same"),
+    (2, 12, 10, 64, 128, 1, 1, "same"),
+    (1, 16, 16, 2048 // 8, 256, 3, 2, "same"),
+    (2, 19, 21, 32, 64, 7, 2, 3),
+]
+
+
+@pytest.mark.parametrize("case", CASES)
+def test_conv_fwd(case):
+    from cvlite import ops_nn as nn
+    B, H, W, Cin, Cout, k, s, pad = case
+    g = torch.Generator().manual_seed(sum(c for c in case if isinstance(c, int)))
+    x = rnd(B, H, W, Cin, gen=g)
+    w = rnd(k, k, Cin, Cout, scale=(k * k * Cin) ** -0.5, gen=g)
+    b = torch.randn(Cout, generator=g, dtype=torch.float64)
+    ref = ref_conv(x, w, b, s, pad)
+    Ho, Wo = ref.shape[1], ref.shape[2]
+    _, pt, _ = _pads(H, k, s, pad)
+    _, pl, _ = _pads(W, k, s, pad)
+    wf, _, npad, _, _ = packs(w)
+    bias = torch.zeros(npad, dtype=torch.float32, device="cuda")
+    bias[:Cout] = b.float().cuda()
+    xg = x.to(BF).cuda()
+    # bf16 output + relu + BN stats
+    out = torch.zeros((B, Ho, Wo, Cout), dtype=BF, device="cuda")
+    stats = torch.zeros((B, Cout, 2), dtype=torch.float64, device="cuda")
+    d = nn.make_desc(nn.FWD, B, Cin, k, k, s, pt, pl, npad, Cout, Cout, [nn.seg(Ho, Wo, H, W, wf, bias)],
+                     relu_out=True)
+    hw = Ho * Wo
+    stats_ok = hw % 128 == 0 or (128 % hw == 0 and hw % 4 == 0)
+    nn.conv_igemm(d, xg, out, stats if stats_ok else None)
+    torch.testing.assert_close(out.double().cpu(), ref.clamp(min=0), rtol=1e-2, atol=1e-2)
+    if stats_ok:
+        o = out.double().cpu()
+        st = torch.stack([o.sum((1, 2)), (o * o).sum((1, 2))], -1)
+        torch.testing.assert_close(stats.cpu(), st, rtol=1e-5, atol=1e-3)
+    # fp32 output into a wider buffer at a channel offset, accumulate (beta = 1), relu on load
+    ld = Cout + 16
+    out32 = torch.randn((B, Ho, Wo, ld), dtype=torch.float32, device="cuda")
+    before = out32.clone()
+    d = nn.make_desc(nn.FWD, B, Cin, k, k, s, pt, pl, npad, Cout, ld, [nn.seg(Ho, Wo, H, W, wf, bias)],
+                     dst_coff=8, dst_f32=True, relu_in=True, beta=1.0)
+    nn.conv_igemm(d, xg, out32)
+    ref2 = ref_conv(x.clamp(min=0), w, b, s, pad)
+    exp = before.double().cpu()
+    exp[..., 8:8 + Cout] += ref2
+    torch.testing.assert_close(out32.double().cpu(), exp, rtol=1e-4, atol=1e-4)
+
+
+@pytest.mark.parametrize("case", CASES[:6])
+def test_conv_dgrad_wgrad(case):
+    from cvlite import ops_nn as nn
+    B, H, W, Cin, Cout, k, s, pad = case
+    g = torch.Generator().manual_seed(7 + sum(c for c in case if isinstance(c, int)))
+    x = rnd(B, H, W, Cin, gen=g).requires_grad_(True)
+    w = rnd(k, k, Cin, Cout, scale=(k * k * Cin) ** -0.5, gen=g).requires_grad_(True)
+    y = ref_conv(x, w, None, s, pad)
+    dy = rnd(*y.shape, gen=g)
+    y.backward(dy)
+    Ho, Wo = y.shape[1], y.shape[2]
+    _, pt, _ = _pads(H, k, s, pad)
+    _, pl, _ = _pads(W, k, s, pad)
+    wf, wd, npad, cout_pad, cin_pad = packs(w.detach())
+    dyg = torch.zeros((B, Ho, Wo, cout_pad), dtype=BF, device="cuda")
+    dyg[..., :Cout] = dy.to(BF).cuda()
+    # dgrad
+    dx = torch.empty((B, H, W, Cin), dtype=BF, device="cuda")
+    d = nn.make_desc(nn.DGRAD, B, cout_pad, k, k, s, pt, pl, cin_pad, Cin, Cin, [nn.seg(H, W, Ho, Wo, wd)])
+    nn.conv_igemm(d, dyg, dx)
+    torch.testing.assert_close(dx.double().cpu(), x.grad, rtol=1e-2, atol=2e-2)
+    # wgrad
+    dw = torch.zeros((k, k, Cin, Cout), dtype=torch.float32, device="cuda")
+    d = nn.make_desc(nn.FWD, B, Cin, k, k, s, pt, pl, npad, Cout, cout_pad, [nn.seg(Ho, Wo, H, W, wf)])
+    nn.conv_wgrad(d, x.detach().to(BF).cuda(), dyg, dw)
+    scale = w.grad.abs().max().item()
+    torch.testing.assert_close(dw.double().cpu(), w.grad, rtol=1e-4, atol=1e-5 * scale)
+
+
+def test_conv_segments_packed_levels():
+    """Five level maps in one packed level-major buffer through one shared-weight launch, and the
+    per-level-weights head form writing an image-major [B, P, ld] fp32 buffer."""
+    from cvlite import ops_nn as nn
+    B, C = 3, 64
+    shapes = [(16, 16), (8, 8), (4, 4), (2, 2), (1, 1)]
+    off, o = [], 0
+    for h, w in shapes:
+        off.append(o)
+        o += h * w
+    P = o
+    g = torch.Generator().manual_seed(3)
+    maps = [rnd(B, h, w, C, gen=g) for h, w in shapes]
+    packed = torch.cat([m.reshape(-1, C) for m in maps], 0).to(BF).cuda()
+    w = rnd(3, 3, C, C, scale=(9 * C) ** -0.5, gen=g)
+    wf, wd, npad, _, _ = packs(w)
+    segs = [nn.seg(h, ww, h, ww, wf, None, src_base=B * off[l], dst_base=B * off[l]) for l, (h, ww) in enumerate(shapes)]
+    out = torch.empty_like(packed)
+    nn.conv_igemm(nn.make_desc(nn.FWD, B, C, 3, 3, 1, 1, 1, npad, C, C, segs), packed, out)
+    for l, (h, ww) in enumerate(shapes):
+        got = out[B * off[l]:B * off[l] + B * h * ww].reshape(B, h, ww, C).double().cpu()
+        torch.testing.assert_close(got, ref_conv(maps[l], w, None, 1, "same"), rtol=1e-2, atol=1e-2)
+    # wgrad over all levels == sum of per-level wgrads
+    dy = rnd(B * P, C, gen=g).to(BF).cuda()
+    dw = torch.zeros((3, 3, C, C), dtype=torch.float32, device="cuda")
+    nn.conv_wgrad(nn.make_desc(nn.FWD, B, C, 3, 3, 1, 1, 1, npad, C, C, segs), packed, dy, dw)
+    ref = torch.zeros(3, 3, C, C, dtype=torch.float64)
+    for l, (h, ww) in enumerate(shapes):
+        wl = w.clone().requires_grad_(True)
+        y = ref_conv(maps[l], wl, None, 1, "same")
+        y.backward(dy[B * off[l]:B * off[l] + B * h * ww].reshape(B, h, ww, C).double().cpu())
+        ref += wl.grad
+    torch.testing.assert_close(dw.double().cpu(), ref, rtol=1e-4, atol=1e-4)
+    # heads: per-level weights, fp32 into [B, P, 32] (n_store 20)
+    Cn = 20
+    hw_ = [rnd(3, 3, C, Cn, scale=0.05, gen=g) for _ in shapes]
+    hb = [torch.randn(Cn, generator=g, dtype=torch.float64) for _ in shapes]
+    pk = [packs(x) for x in hw_]
+    biases = []
+    for b in hb:
+        t = torch.zeros(32, dtype=torch.float32, device="cuda")
+        t[:Cn] = b.float().cuda()
+        biases.append(t)
+    segs = [nn.seg(h, ww, h, ww, pk[l][0], biases[l], src_base=B * off[l], dst_base=off[l], dst_img=P)
+            for l, (h, ww) in enumerate(shapes)]
+    res = torch.zeros((B, P, 32), dtype=torch.float32, device="cuda")
+    nn.conv_igemm(nn.make_desc(nn.FWD, B, C, 3, 3, 1, 1, 1, 32, Cn, 32, segs, dst_f32=True), packed, res)
+    for l, (h, ww) in enumerate(shapes):
+        got = res[:, off[l]:off[l] + h * ww, :Cn].reshape(B, h, ww, Cn).double().cpu()
+        torch.testing.assert_close(got, ref_conv(maps[l], hw_[l], hb[l], 1, "same"), rtol=1e-4, atol=1e-4)
+    assert not res[..., Cn:].any()
+    # head dgrad with per-level dgrad packs back into the packed level-major buffer
+    dres = torch.zeros((B, P, 32), dtype=BF, device="cuda")
+    dres[..., :Cn] = torch.randn((B, P, Cn), generator=g).to(BF).cuda()
+    segs = [nn.seg(h, ww, h, ww, pk[l][1], None, src_base=off[l], src_img=P, dst_base=B * off[l])
+            for l, (h, ww) in enumerate(shapes)]
+    dpk = torch.empty_like(packed)
+    nn.conv_igemm(nn.make_desc(nn.DGRAD, B, 32, 3, 3, 1, 1, 1, C, C, C, segs), dres, dpk)
+    for l, (h, ww) in enumerate(shapes):
+        xl = maps[l].clone().requires_grad_(True)
+        y = ref_conv(xl, hw_[l], None, 1, "same")
+        y.backward(dres[:, off[l]:off[l] + h * ww, :Cn].reshape(B, h, ww, Cn).double().cpu())
+        got = dpk[B * off[l]:B * off[l] + B * h * ww].reshape(B, h, ww, C).double().cpu()
+        torch.testing.assert_close(got, xl.grad, rtol=1e-2, atol=1e-2)

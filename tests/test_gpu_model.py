@@ -1,0 +1,144 @@
+"""End-to-end parity of the FCOS ResNet-50-FPN forward / loss / backward on the GPU (bf16 MFMA
+convs, fp32 accumulation and master weights) against the torch-CPU restatement
+(oracle/model_ref.py) on identical weights, images and reference targets, with the oracle storing
+activations/gradients in bf16 at the same points (fp32 arithmetic).  At random init this graph is
+chaotic (a 0.4% per-layer perturbation grows to ~55% at C5 — measured on the oracle alone, fp32
+vs bf16 storage), so the bf16 path is compared with the bf16-storage oracle; the per-block test
+below compares each block against the plain fp32 oracle with synchronised inputs.
+Tolerances (bf16 activations through ~70 conv+BN layers): predictions and losses rel-L2 <= 3e-2;
+gradients rel-L2 <= 6e-2 over all parameters, <= 0.2 per tensor (tensors with non-negligible
+gradient; the conv biases in front of a BatchNorm have a mathematically-zero gradient)."""
+import numpy as np
+import pytest
+import torch
+
+from oracle import fcos_ref, model_ref
+
+pytestmark = pytest.mark.gpu
+
+
+def synth_batch(B, D, C, seed):
+    rng = np.random.default_rng(seed)
+    nmax = 6
+    boxes = np.zeros((B, nmax, 5), np.float32)
+    nbox = np.zeros(B, np.int32)
+    for b in range(B):
+        n = int(rng.integers(1, nmax + 1))
+        nbox[b] = n
+        for i in range(n):
+            h, w = np.exp(rng.uniform(np.log(8 / D), np.log(0.9), 2))
+            boxes[b, i] = [rng.uniform(h / 2, 1 - h / 2), rng.uniform(w / 2, 1 - w / 2), h, w, rng.integers(0, C)]
+    x = (rng.uniform(-1, 1, size=(B, D, D, 3))).astype(np.float32)
+    return x, boxes, nbox
+
+
+def rel(a, b):
+    return float((a - b).norm() / max(b.norm(), 1e-30))
+
+
+def _run_gpu(net, x, boxes, nbox, C, B, D):
+    from cvlite import ops_targets as ot
+    xg = torch.from_numpy(x).cuda()
+    dims = torch.full((B, 2), float(D), device="cuda")
+    tg, _ = ot.fcos_assign(torch.from_numpy(boxes).cuda(), torch.from_numpy(nbox).cuda(), dims, (D, D), C)
+    for b in range(B):   # device targets are the reference's (bit-exact)
+        outs, _ = fcos_ref.format_data(boxes[b, :nbox[b]], np.array([D, D], np.float32), C, img_pad=(D, D))
+        np.testing.assert_array_equal(tg[b].cpu().numpy(), fcos_ref.pack_targets(outs))
+    reg, cls = net.forward(xg)
+    P = reg.shape[1]
+    d_reg = torch.zeros((B, P, 32), dtype=torch.bfloat16, device="cuda")
+    d_cls = torch.zeros((B, P, 32), dtype=torch.bfloat16, device="cuda")
+    losses, _, _ = ot.fcos_loss(reg, cls, tg, C, grad_scale=1.0 / B, d_reg=d_reg, d_cls=d_cls)
+    net.backward(d_reg, d_cls)
+    torch.cuda.synchronize()
+    return tg.cpu(), reg[..., :5].cpu(), cls[..., :C].cpu(), losses.cpu().double()
+
+
+def _damp_residual_gammas(net, factor):
+    for k in net.store.offsets:
+        if k.endswith("_3_bn/gamma"):
+            net.store.p(k).mul_(factor)
+
+
+def test_fcos_train_graph_matches_cpu_oracle():
+    """Damped residual-branch gammas (x0.25, so the graph is not chaotic) -> the whole forward,
+    loss and backward must match the bf16-storage oracle tightly: this checks every kernel and
+    every connection of the training graph, gradients included."""
+    from cvlite.fcos_net import FCOSNet
+    C, B, D = 20, 2, 256
+    net = FCOSNet(C, seed=1)
+    _damp_residual_gammas(net, 0.25)
+    params = net.store.state_dict()
+    x, boxes, nbox = synth_batch(B, D, C, 3)
+    tg, reg, cls, losses = _run_gpu(net, x, boxes, nbox, C, B, D)
+    with model_ref.emulate_bf16():
+        l_ref, g_ref, reg_ref, cls_ref = model_ref.fcos_loss_and_grads(params, torch.from_numpy(x), tg, C,
+                                                                        grad_scale=1.0 / B)
+    print("reg %.4f cls %.4f loss %.4f" % (rel(reg, reg_ref), rel(cls, cls_ref), rel(losses, l_ref.double())))
+    assert rel(reg, reg_ref) < 2e-2
+    assert rel(cls, cls_ref) < 2e-2
+    assert rel(losses, l_ref.double()) < 2e-2
+    gnorm = {k: float(v.norm()) for k, v in g_ref.items()}
+    big = max(gnorm.values())
+    tot_num = tot_den = 0.0
+    worst = []
+    for k, gr in g_ref.items():
+        gg = net.store.g(k).cpu()
+        tot_num += float((gg - gr).norm() ** 2)
+        tot_den += float(gr.norm() ** 2)
+        if gnorm[k] > 1e-3 * big:
+            worst.append((rel(gg, gr), k))
+    worst.sort(reverse=True)
+    print("grad rel-L2 overall %.4f; worst tensors %s" % ((tot_num / tot_den) ** 0.5, worst[:5]))
+    assert (tot_num / tot_den) ** 0.5 < 5e-2
+    assert worst[0][0] < 0.2, worst[:5]
+
+
+def test_reference_init_deviation_bounded_by_bf16_storage():
+    """Reference (Keras glorot) init: the graph is chaotic, so compare how far the GPU result is
+    from the fp32 oracle with how far bf16 storage alone moves the oracle itself."""
+    from cvlite.fcos_net import FCOSNet
+    C, B, D = 20, 2, 256
+    net = FCOSNet(C, seed=1)
+    params = net.store.state_dict()
+    x, boxes, nbox = synth_batch(B, D, C, 3)
+    tg, reg, cls, _ = _run_gpu(net, x, boxes, nbox, C, B, D)
+    with torch.no_grad():
+        reg32, cls32 = model_ref.fcos_forward(torch.from_numpy(x), params, C)
+        with model_ref.emulate_bf16():
+            reg16, cls16 = model_ref.fcos_forward(torch.from_numpy(x), params, C)
+    for g, r32, r16 in ((reg, reg32, reg16), (cls, cls32, cls16)):
+        e_gpu, e_emu = rel(g, r32), rel(r16, r32)
+        print("gpu-vs-fp32 %.4f  bf16-oracle-vs-fp32 %.4f" % (e_gpu, e_emu))
+        assert e_gpu <= 1.5 * e_emu + 0.02
+
+
+def test_backbone_blocks_match_fp32_oracle_with_synced_inputs():
+    """Every ResNet-50 block (conv + per-image BN + residual + ReLU, fwd) vs the plain fp32 oracle,
+    each fed the oracle's own input: isolates kernel error from the graph's chaotic amplification."""
+    import torch.nn.functional as F
+    from cvlite.fcos_net import FCOSNet
+    C, B, D = 20, 2, 256
+    net = FCOSNet(C, seed=1)
+    p = net.store.state_dict()
+    rng = np.random.default_rng(3)
+    x = torch.from_numpy(rng.uniform(-1, 1, size=(B, D, D, 3)).astype(np.float32))
+    pool, _ = net.backbone.stem.forward(x.cuda())
+    xn = x.permute(0, 3, 1, 2)
+    hr = F.max_pool2d(F.pad(F.relu(model_ref.bn(model_ref.conv(xn, p, "conv1_conv", 2, pad=3), p, "conv1_bn")),
+                            (1, 1, 1, 1)), 3, 2)
+    assert rel(pool.float().cpu().permute(0, 3, 1, 2), hr) < 1e-2
+    H = W = hr.shape[2]
+    for si, stage in enumerate(net.backbone.stages):
+        for bi, blk in enumerate(stage):
+            n = "conv%d_block%d" % (si + 2, bi + 1)
+            s = blk.c1.conv.stride
+            hin = hr.permute(0, 2, 3, 1).contiguous().to(torch.bfloat16).cuda()
+            out, H, W, _ = blk.forward(hin, B, H, W)
+            hb = hin.float().cpu().permute(0, 3, 1, 2)
+            sc = model_ref.bn(model_ref.conv(hb, p, n + "_0_conv", s), p, n + "_0_bn") if bi == 0 else hb
+            y = F.relu(model_ref.bn(model_ref.conv(hb, p, n + "_1_conv", s), p, n + "_1_bn"))
+            y = F.relu(model_ref.bn(model_ref.conv(y, p, n + "_2_conv"), p, n + "_2_bn"))
+            hr = F.relu(model_ref.bn(model_ref.conv(y, p, n + "_3_conv"), p, n + "_3_bn") + sc)
+            e = rel(out.float().cpu().permute(0, 3, 1, 2), hr)
+            assert e < 1.5e-2, (n, e)

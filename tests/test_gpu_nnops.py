@@ -1,0 +1,140 @@
+"""GPU parity of the memory-bound ops (BN fwd/bwd with per-image stats, max-pool, FPN upsample,
+ReLU backward, bias grad, clip+SGD, LR schedule) against torch fp64 references."""
+import math
+
+import numpy as np
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+BF = torch.bfloat16
+
+
+def bfr(t):
+    return t.to(BF).to(torch.float64)
+
+
+@pytest.mark.parametrize("B,HW,C,relu,res", [(2, 64, 64, True, False), (3, 16, 256, False, True),
+                                             (1, 256, 32, True, True)])
+def test_bn_forward_backward(B, HW, C, relu, res):
+    from cvlite import ops_nn as nn
+    g = torch.Generator().manual_seed(B * 100 + C)
+    z = bfr(torch.randn(B, HW, C, generator=g, dtype=torch.float64) * 2 + 0.5)
+    gamma = torch.rand(C, generator=g, dtype=torch.float64) + 0.5
+    beta = torch.randn(C, generator=g, dtype=torch.float64)
+    r = bfr(torch.randn(B, HW, C, generator=g, dtype=torch.float64)) if res else None
+    eps = 1.001e-5
+    stats = torch.stack([z.sum(1), (z * z).sum(1)], -1).cuda()
+    mr = torch.empty((B, C, 2), dtype=torch.float32, device="cuda")
+    rm = torch.zeros(C, device="cuda")
+    rv = torch.ones(C, device="cuda")
+    nn.bn_finalize(stats, mr, rm, rv, B, C, HW, eps, 0.99)
+    y = torch.empty((B, HW, C), dtype=BF, device="cuda")
+    zg = z.to(BF).cuda()
+    nn.bn_apply(zg, mr, gamma.float().cuda(), beta.float().cuda(), r.to(BF).cuda() if res else None, y, B, HW,
+                C, relu)
+    zz = z.clone().requires_grad_(True)
+    gg = gamma.clone().requires_grad_(True)
+    bb = beta.clone().requires_grad_(True)
+    m = zz.mean(1, keepdim=True)
+    v = ((zz - m) ** 2).mean(1, keepdim=True)
+    out = (zz - m) / torch.sqrt(v + eps) * gg + bb
+    if res:
+        out = out + r
+    if relu:
+        out = F.relu(out)
+    torch.testing.assert_close(y.double().cpu(), out.detach(), rtol=1e-2, atol=2e-2)
+    # running stats: sequential EMA over images, unbiased variance
+    erm, erv = torch.zeros(C, dtype=torch.float64), torch.ones(C, dtype=torch.float64)
+    for b in range(B):
+        erm = erm * 0.99 + m[b, 0] * 0.01
+        erv = erv * 0.99 + v[b, 0] * HW / (HW - 1) * 0.01
+    torch.testing.assert_close(rm.double().cpu(), erm.detach(), rtol=1e-5, atol=1e-6)
+    torch.testing.assert_close(rv.double().cpu(), erv.detach(), rtol=1e-5, atol=1e-6)
+    # backward
+    dy = bfr(torch.randn(B, HW, C, generator=g, dtype=torch.float64))
+    out.backward(dy)
+    dz = torch.empty_like(zg)
+    gout = torch.empty_like(zg)
+    dgam = torch.zeros(C, device="cuda")
+    dbet = torch.zeros(C, device="cuda")
+    nn.bn_backward(dy.to(BF).cuda(), y if relu else None, zg, mr, gamma.float().cuda(), dz, gout, dgam, dbet,
+                   B, HW, C)
+    scale = zz.grad.abs().max().item()
+    torch.testing.assert_close(dz.double().cpu(), zz.grad, rtol=2e-2, atol=2e-2 * scale)
+    torch.testing.assert_close(dgam.double().cpu(), gg.grad, rtol=2e-2, atol=2e-2 * gg.grad.abs().max().item())
+    torch.testing.assert_close(dbet.double().cpu(), bb.grad, rtol=2e-2, atol=2e-2 * bb.grad.abs().max().item())
+
+
+def test_maxpool_and_upsample():
+    from cvlite import ops_nn as nn
+    g = torch.Generator().manual_seed(11)
+    B, H, W, C = 2, 14, 10, 64
+    x = bfr(torch.relu(torch.randn(B, H, W, C, generator=g, dtype=torch.float64)))
+    x[0, :3, :3, :8] = 0.0                         # ties with the zero padding
+    xx = x.clone().requires_grad_(True)
+    ref = F.max_pool2d(F.pad(xx.permute(0, 3, 1, 2), (1, 1, 1, 1)), 3, 2).permute(0, 2, 3, 1)
+    Ho, Wo = ref.shape[1], ref.shape[2]
+    y = torch.empty((B, Ho, Wo, C), dtype=BF, device="cuda")
+    arg = torch.empty((B, Ho, Wo, C), dtype=torch.uint8, device="cuda")
+    nn.maxpool3x3s2(x.to(BF).cuda(), y, arg)
+    torch.testing.assert_close(y.double().cpu(), ref.detach())
+    dy = bfr(torch.randn(B, Ho, Wo, C, generator=g, dtype=torch.float64))
+    ref.backward(dy)
+    dx = torch.empty((B, H, W, C), dtype=BF, device="cuda")
+    nn.maxpool3x3s2_backward(dy.to(BF).cuda(), arg, dx)
+    torch.testing.assert_close(dx.double().cpu(), xx.grad, rtol=1e-2, atol=1e-2)
+    # upsample-add and its backward
+    a = bfr(torch.randn(B, 8, 6, C, generator=g, dtype=torch.float64))
+    b = bfr(torch.randn(B, 4, 3, C, generator=g, dtype=torch.float64))
+    o = torch.empty((B, 8, 6, C), dtype=BF, device="cuda")
+    nn.upsample2x_add(a.to(BF).cuda(), b.to(BF).cuda(), o, B, 8, 6, C)
+    up = b.repeat_interleave(2, 1).repeat_interleave(2, 2)
+    torch.testing.assert_close(o.double().cpu(), a + up, rtol=1e-2, atol=1e-2)
+    do = bfr(torch.randn(B, 8, 6, C, generator=g, dtype=torch.float64))
+    db = b.to(BF).cuda()
+    nn.upsample2x_backward(do.to(BF).cuda(), db, B, 8, 6, C, beta=1.0)
+    exp = b + do.reshape(B, 4, 2, 3, 2, C).sum((2, 4))
+    torch.testing.assert_close(db.double().cpu(), exp, rtol=1e-2, atol=2e-2)
+
+
+def test_relu_bwd_bias_grad_sgd_lr():
+    from cvlite import ops_nn as nn
+    g = torch.Generator().manual_seed(5)
+    dy = bfr(torch.randn(4096, generator=g, dtype=torch.float64))
+    y = bfr(torch.randn(4096, generator=g, dtype=torch.float64))
+    dx = torch.empty(4096, dtype=BF, device="cuda")
+    nn.relu_backward(dy.to(BF).cuda(), y.to(BF).cuda(), dx)
+    torch.testing.assert_close(dx.double().cpu(), dy * (y > 0))
+    # bias grad over a segment of an image-major [B, P, ld] buffer
+    B, P, ld = 3, 50, 32
+    t = bfr(torch.randn(B, P, ld, generator=g, dtype=torch.float64))
+    db = torch.ones(20, device="cuda")
+    nn.bias_grad(t.to(BF).cuda(), ld, 0, 20, 10, P, 16, B, db, beta=1.0)
+    torch.testing.assert_close(db.double().cpu(), 1 + t[:, 10:26, :20].sum((0, 1)), rtol=1e-5, atol=1e-4)
+    # clip + SGD (Keras form), lr from device memory
+    n = 100003
+    w = torch.randn(n, generator=g)
+    gr = torch.randn(n, generator=g) * 3
+    v = torch.randn(n, generator=g) * 0.1
+    lr = 5e-4
+    wd, gd, vd = w.cuda(), gr.cuda(), v.cuda()
+    lr_dev = torch.tensor([lr], device="cuda")
+    nn.sgd_clip_update(wd, gd, vd, lr_dev, 0.9, 1.0 / 16, 1.0)
+    gg = gr.double() / 16
+    norm = gg.norm().item()
+    gg = gg * (1.0 / max(norm, 1.0))
+    ev = 0.9 * v.double() - lr * gg
+    torch.testing.assert_close(vd.double().cpu(), ev, rtol=1e-5, atol=1e-7)
+    torch.testing.assert_close(wd.double().cpu(), w.double() + ev, rtol=1e-5, atol=1e-6)
+    # lr schedule (train_fcos.py:108-110)
+    step = torch.tensor([0], dtype=torch.int32, device="cuda")
+    lrd = torch.zeros(1, device="cuda")
+    for s in (0, 999, 1000, 2500, 60000):
+        step.fill_(s)
+        nn.lr_schedule(step, lrd, 5e-4, 1e-5, 0.9, 1000)
+        exp = max(5e-4 * math.pow(0.9, int(s / 1000)), 1e-5)
+        assert abs(lrd.item() - np.float32(exp)) == 0, (s, lrd.item(), exp)
+        assert step.item() == s + 1

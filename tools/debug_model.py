@@ -1,0 +1,117 @@
+"""Layer-by-layer comparison of the GPU FCOS graph with the torch-CPU oracle (debug aid)."""
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "cv-lite-object-detection_amd")]
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+import torch.nn.functional as F  # noqa: E402
+
+from cvlite.fcos_net import FCOSNet  # noqa: E402
+from oracle import model_ref as M  # noqa: E402
+
+
+def rel(a, b):
+    return float((a.double() - b.double()).norm() / max(b.double().norm(), 1e-30))
+
+
+def main():
+    C, B, D = 20, 2, 256
+    net = FCOSNet(C, seed=1)
+    p = net.store.state_dict()
+    rng = np.random.default_rng(3)
+    x = torch.from_numpy(rng.uniform(-1, 1, size=(B, D, D, 3)).astype(np.float32))
+    xg = x.cuda()
+    # stem
+    st = net.backbone.stem
+    pool, sv = st.forward(xg)
+    A, z, y, mr, arg, _, Ho, Wo = sv
+    xn = x.permute(0, 3, 1, 2)
+    zr = M.conv(xn, p, "conv1_conv", 2, pad=3)
+    print("stem z", rel(z.float().cpu().permute(0, 3, 1, 2), zr))
+    yr = F.relu(M.bn(zr, p, "conv1_bn"))
+    print("stem y", rel(y.float().cpu().permute(0, 3, 1, 2), yr))
+    pr = F.max_pool2d(F.pad(yr, (1, 1, 1, 1)), 3, 2)
+    print("pool", rel(pool.float().cpu().permute(0, 3, 1, 2), pr))
+    h = pool
+    H, W = h.shape[1], h.shape[2]
+    hr = pr
+    for si, stage in enumerate(net.backbone.stages):
+        for bi, blk in enumerate(stage):
+            n = "conv%d_block%d" % (si + 2, bi + 1)
+            s = blk.c1.conv.stride
+            # GPU block with the oracle's input to isolate errors
+            hin = hr.permute(0, 2, 3, 1).contiguous().to(torch.bfloat16).cuda()
+            out, H1, W1, svb = blk.forward(hin, B, H, W)
+            hb = hin.float().cpu().permute(0, 3, 1, 2)
+            if bi == 0:
+                sc = M.bn(M.conv(hb, p, n + "_0_conv", s), p, n + "_0_bn")
+            else:
+                sc = hb
+            y1 = F.relu(M.bn(M.conv(hb, p, n + "_1_conv", s), p, n + "_1_bn"))
+            y2 = F.relu(M.bn(M.conv(y1, p, n + "_2_conv"), p, n + "_2_bn"))
+            y3 = M.bn(M.conv(y2, p, n + "_3_conv"), p, n + "_3_bn")
+            o = F.relu(y3 + sc)
+            g1 = svb[1][2].float().cpu().permute(0, 3, 1, 2)
+            g2 = svb[2][2].float().cpu().permute(0, 3, 1, 2)
+            print(n, "y1 %.4f y2 %.4f out %.4f" % (rel(g1, y1), rel(g2, y2), rel(out.float().cpu().permute(0, 3, 1, 2), o)),
+                  "shape", tuple(out.shape))
+            hr = o
+            H, W = H1, W1
+
+
+if __name__ == "__main__" and len(sys.argv) == 1:
+    main()
+
+
+def fpn_check():
+    C, B, D = 20, 2, 256
+    net = FCOSNet(C, seed=1)
+    p = net.store.state_dict()
+    rng = np.random.default_rng(3)
+    x = torch.from_numpy(rng.uniform(-1, 1, size=(B, D, D, 3)).astype(np.float32))
+    reg, cls = net.forward(x.cuda())
+    s = net._saved
+    c3r, c4r, c5r = M.resnet50(x.permute(0, 3, 1, 2), p)
+    (c3, _, _), (c4, _, _), (c5, _, _) = s["C"]
+    g = lambda t: t.float().cpu().permute(0, 3, 1, 2)  # noqa: E731
+    print("chain C3 %.4f C4 %.4f C5 %.4f" % (rel(g(c3), c3r), rel(g(c4), c4r), rel(g(c5), c5r)))
+    # oracle FPN from the GPU's C3..C5
+    c3r, c4r, c5r = g(c3), g(c4), g(c5)
+    l3 = M.conv(c3r, p, "c3_1x1"); l4 = M.conv(c4r, p, "c4_1x1"); l5 = M.conv(c5r, p, "c5_1x1")
+    gl3, gl4, gl5 = s["l"]
+    print("lateral", rel(g(gl3), l3), rel(g(gl4), l4), rel(g(gl5), l5))
+    up = lambda t: t.repeat_interleave(2, 2).repeat_interleave(2, 3)  # noqa: E731
+    p4r = l4 + up(l5); p3r = l3 + up(l4)
+    gp3, gp4 = s["p"]
+    print("p3r/p4r", rel(g(gp3), p3r), rel(g(gp4), p4r))
+    p6 = M.conv(c5r, p, "c6_3x3", 2)
+    fpn = [M.conv(p3r, p, "c3_3x3"), M.conv(p4r, p, "c4_3x3"), M.conv(l5, p, "c5_3x3"), p6,
+           M.conv(F.relu(p6), p, "c7_3x3", 2)]
+    Fp = s["F"]
+    off, shapes = s["off"], s["shapes"]
+    for l, (h, w) in enumerate(shapes):
+        gl = Fp[B * off[l]:B * off[l] + B * h * w].reshape(B, h, w, 256)
+        print("P%d" % (l + 3), rel(g(gl), fpn[l]))
+    # towers from the GPU's F
+    for ti, name in enumerate(("cls", "reg")):
+        acts = s["towers"][ti]
+        for l, (h, w) in enumerate(shapes):
+            t = g(acts[0][B * off[l]:B * off[l] + B * h * w].reshape(B, h, w, 256))
+            for i in range(4):
+                t = M.conv(t, p, "%s_layer_%d" % (name, i + 1), bias=False)
+                gt = g(acts[i + 1][B * off[l]:B * off[l] + B * h * w].reshape(B, h, w, 256))
+                if i == 3:
+                    t = F.relu(t)
+                e = rel(gt, t)
+                if e > 0.02:
+                    print("  tower", name, "level", l, "layer", i + 1, "rel", e)
+            hd = M.conv(g(acts[4][B * off[l]:B * off[l] + B * h * w].reshape(B, h, w, 256)), p,
+                        ("logits_output_%d" if ti == 0 else "reg_output_%d") % (l + 1))
+            out = (cls[:, off[l]:off[l] + h * w, :C] if ti == 0 else reg[:, off[l]:off[l] + h * w, :5]).cpu()
+            print("head", name, l, rel(out.reshape(B, h, w, -1).permute(0, 3, 1, 2), hd))
+
+
+if __name__ == "__main__" and len(sys.argv) > 1:
+    fpn_check()
