@@ -113,5 +113,47 @@ def fpn_check():
             print("head", name, l, rel(out.reshape(B, h, w, -1).permute(0, 3, 1, 2), hd))
 
 
-if __name__ == "__main__" and len(sys.argv) > 1:
+if __name__ == "__main__" and len(sys.argv) > 1 and sys.argv[1] == "fpn":
     fpn_check()
+
+
+def block_bwd_check():
+    """Each backbone block's backward in isolation: oracle input + oracle upstream gradient."""
+    C, B, D = 20, 2, 256
+    net = FCOSNet(C, seed=1)
+    p = net.store.state_dict()
+    rng = np.random.default_rng(3)
+    H = W = 64
+    for si, stage in enumerate(net.backbone.stages):
+        cin = stage[0].c1.conv.cin
+        for bi, blk in enumerate(stage[:2]):
+            n = "conv%d_block%d" % (si + 2, bi + 1)
+            s = blk.c1.conv.stride
+            cb = blk.c1.conv.cin
+            xin = torch.relu(torch.from_numpy(rng.normal(size=(B, H, W, cb)).astype(np.float32)))
+            xin = xin.to(torch.bfloat16).float()
+            hin = xin.cuda().to(torch.bfloat16)
+            out, H1, W1, sv = blk.forward(hin, B, H, W)
+            dy = torch.from_numpy(rng.normal(size=tuple(out.shape)).astype(np.float32)).to(torch.bfloat16)
+            net.store.grad.zero_()
+            dx = blk.backward(dy.cuda(), sv)
+            pp = {k: v.clone().requires_grad_(True) for k, v in p.items() if k.startswith(n + "_")}
+            xb = xin.permute(0, 3, 1, 2).clone().requires_grad_(True)
+            sc = M.bn(M.conv(xb, pp, n + "_0_conv", s), pp, n + "_0_bn") if bi == 0 else xb
+            y = F.relu(M.bn(M.conv(xb, pp, n + "_1_conv", s), pp, n + "_1_bn"))
+            y = F.relu(M.bn(M.conv(y, pp, n + "_2_conv"), pp, n + "_2_bn"))
+            o = F.relu(M.bn(M.conv(y, pp, n + "_3_conv"), pp, n + "_3_bn") + sc)
+            o.backward(dy.float().permute(0, 3, 1, 2))
+            res = ["out %.4f dx %.4f" % (rel(out.float().cpu().permute(0, 3, 1, 2), o.detach()),
+                                           rel(dx.float().cpu().permute(0, 3, 1, 2), xb.grad))]
+            for k, v in pp.items():
+                if v.grad is not None and float(v.grad.norm()) > 1e-6:
+                    e = rel(net.store.g(k).cpu(), v.grad)
+                    if e > 0.02 or "beta" in k:
+                        res.append("%s %.4f" % (k[len(n) + 1:], e))
+            print(n, " ".join(res))
+            H, W = H1, W1
+
+
+if __name__ == "__main__" and len(sys.argv) > 1 and sys.argv[1] == "bwd":
+    block_bwd_check()
