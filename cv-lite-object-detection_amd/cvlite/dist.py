@@ -1,0 +1,61 @@
+"""Data parallelism over RCCL/xGMI (one process per GPU, torch.distributed backend "nccl" = RCCL).
+
+The reference trains on one device (FCOS/train_fcos.py:128-185); SURVEY.md §8e: images are
+independent and BatchNorm statistics are per image, so sharding the batch across ranks changes no
+training-mode math.  Rank r processes its own bs images; the step's gradient is
+    g = (sum over all ranks' images of grad loss_i) / (world * bs)
+= one SUM all-reduce of the flat fp32 gradient buffer, then every rank runs the identical fused
+clip + SGD update (the global norm is computed from the reduced gradient, so no extra collective).
+"""
+import os
+
+import torch
+import torch.distributed as tdist
+
+# 64 MiB buckets: few, large collectives (each RCCL ring step is xGMI-link bound; ~146 MB of fp32
+# gradients per FCOS-R50 step -> 3 buckets)
+BUCKET_BYTES = 64 << 20
+
+
+def init_from_env(backend=None):
+    """torchrun-style env (RANK, WORLD_SIZE, LOCAL_RANK, MASTER_ADDR/PORT).  Returns (rank, world, local)."""
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1 and not tdist.is_initialized():
+        if backend is None:
+            backend = "nccl" if torch.cuda.is_available() else "gloo"
+        if backend == "nccl":
+            torch.cuda.set_device(local)
+        tdist.init_process_group(backend=backend)
+    return rank, world, local
+
+
+def bucket_views(flat, bucket_bytes=BUCKET_BYTES):
+    n = flat.numel()
+    per = max(1, bucket_bytes // flat.element_size())
+    return [flat[i:i + per] for i in range(0, n, per)]
+
+
+def allreduce_grads(flat_grad, group=None, bucket_bytes=BUCKET_BYTES):
+    """SUM all-reduce of the flat gradient buffer in large buckets (in place)."""
+    if not tdist.is_initialized() or tdist.get_world_size(group) == 1:
+        return flat_grad
+    works = [tdist.all_reduce(v, op=tdist.ReduceOp.SUM, group=group, async_op=True)
+             for v in bucket_views(flat_grad, bucket_bytes)]
+    for w in works:
+        w.wait()
+    return flat_grad
+
+
+def max_over_ranks(value, device):
+    if not tdist.is_initialized():
+        return value
+    t = torch.tensor([float(value)], dtype=torch.float64, device=device)
+    tdist.all_reduce(t, op=tdist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def barrier():
+    if tdist.is_initialized():
+        tdist.barrier()
