@@ -170,3 +170,28 @@ extern "C" int cvl_fcos_loss(const float* reg_pred, int ld_reg, const float* cls
                      (const double*)workspace, losses, a.tiles);
   return cvl_launch_status();
 }
+
+// ---------------------------------------------------------------------------------------------
+// fcos.py:112-134 prediction_to_corners: fp32 (cell centre -/+ ltrb), then float64 * stride
+// ---------------------------------------------------------------------------------------------
+namespace {
+__global__ void fcos_decode_kernel(const float* p, int ld, int S0, int S1, double stride, double* out) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= S0 * S1) return;
+  const int y = i / S1, x = i - (i / S1) * S1;
+  const float gy = (float)y + 0.5f, gx = (float)x + 0.5f;
+  const float* q = p + (size_t)i * ld;
+  out[i * 4 + 0] = stride * (double)(gy - q[0]);
+  out[i * 4 + 1] = stride * (double)(gx - q[2]);
+  out[i * 4 + 2] = stride * (double)(gy + q[1]);
+  out[i * 4 + 3] = stride * (double)(gx + q[3]);
+}
+}  // namespace
+
+extern "C" int cvl_fcos_decode(const float* pred, int ld, int S0, int S1, double stride, double* out,
+                               cvl_stream_t stream) {
+  CVL_CHECK_ARG(pred && out && ld >= 4 && S0 > 0 && S1 > 0);
+  hipLaunchKernelGGL(fcos_decode_kernel, dim3((S0 * S1 + 255) / 256), dim3(256), 0, (hipStream_t)stream, pred,
+                     ld, S0, S1, stride, out);
+  return cvl_launch_status();
+}

@@ -23,6 +23,7 @@ SIGNATURES = {
     "cvl_fcos_loss_workspace_size": (c_size_t, [c_int, c_int]),
     "cvl_fcos_loss": (c_int, [P, c_int, P, c_int, P, c_int, c_int, c_int, c_int, c_float, P,
                               P, c_int, c_int, P, c_int, c_int, P, P]),
+    "cvl_fcos_decode": (c_int, [P, c_int, c_int, c_int, ctypes.c_double, P, P]),
     "cvl_conv_igemm": (c_int, [P, P, P, P, P]),
     "cvl_conv_wgrad_workspace_size": (c_size_t, [P]),
     "cvl_conv_wgrad": (c_int, [P, P, P, P, c_float, P, c_size_t, P]),

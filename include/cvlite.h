@@ -63,6 +63,11 @@ int cvl_fcos_loss(const float* reg_pred, int ld_reg, const float* cls_pred, int 
                   float grad_scale, float* losses, void* d_reg, int ld_dreg, int dreg_dtype,
                   void* d_cls, int ld_dcls, int dcls_dtype, void* workspace, cvl_stream_t stream);
 
+/* FCOS/fcos.py:112-134 prediction_to_corners: pred [S0][S1][ld>=4] (t, b, l, r) fp32 ->
+ * out [S0][S1][4] float64 = stride * (y_lo, x_lo, y_hi, x_hi) around cell centres (fp32 math). */
+int cvl_fcos_decode(const float* pred, int ld, int S0, int S1, double stride, double* out,
+                    cvl_stream_t stream);
+
 
 /* ------------------------------------------------------------------------------------------
  * Segmented implicit-GEMM convolution (bf16 MFMA, fp32 accumulate).  Replaces every Conv2D of
