@@ -16,7 +16,7 @@
 namespace {
 
 constexpr int NT = 256;
-constexpr int BR = 32;     // reduction rows per step (one MFMA K)
+constexpr int BR = 64;     // reduction rows per step (two MFMA K-steps)
 constexpr int BKK = 128;   // k columns per tile
 constexpr int BM = 128;    // segment padding granule (must match conv_igemm)
 
@@ -29,19 +29,45 @@ struct WgArgs {
   int direct;
 };
 
-__device__ __forceinline__ int fdiv(int x, int d, float rd) {
-  int q = (int)((float)x * rd);
-  if (q * d > x) --q;
-  else if ((q + 1) * d <= x) ++q;
-  return q;
-}
-
 typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
 
 __device__ __forceinline__ s16x8 tr_frag(const cvl_bf16* base_lo, const cvl_bf16* base_hi) {
   s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(base_lo));
   s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(base_hi));
   return s16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+}
+
+// Row cursor: (image, y, x) of one GEMM row inside the current segment, advanced by a fixed
+// stride each step without divisions.  A reduction step never straddles two segments (steps and
+// split chunks are aligned to the segments' BM padding), so the segment is uniform per step.
+struct RowCursor {
+  int ml, img, oy, ox;
+};
+
+__device__ __forceinline__ int seg_of(const ConvArgs& a, int m) {
+  int sg = 0;
+#pragma unroll
+  for (int i = 1; i < kMaxSeg; ++i)
+    if (i < a.nseg && m >= a.seg[i].m_start) sg = i;
+  return sg;
+}
+
+__device__ __forceinline__ void cursor_seek(const ConvSeg& S, RowCursor& c, int ml) {
+  c.ml = ml;
+  const int HW = S.Hr * S.Wr;
+  c.img = ml / HW;
+  const int q = ml - c.img * HW;
+  c.oy = q / S.Wr;
+  c.ox = q - c.oy * S.Wr;
+}
+
+__device__ __forceinline__ void cursor_advance(const ConvSeg& S, RowCursor& c, int step) {
+  c.ml += step;
+  c.ox += step;
+  while (c.ox >= S.Wr) {
+    c.ox -= S.Wr;
+    if (++c.oy >= S.Hr) { c.oy = 0; ++c.img; }
+  }
 }
 
 template <int BCO>
@@ -51,7 +77,9 @@ __global__ void __launch_bounds__(NT) conv_wgrad_kernel(WgArgs g) {
   constexpr int WCO = BCO / 2, WK = BKK / 2;
   constexpr int TM = WCO / 16, TN = WK / 16;
   constexpr int YCPR = BCO / 8;                 // dY 16-byte chunks per row
-  constexpr int YCH = BR * YCPR;                // dY chunks per step
+  constexpr int YRPP = NT / YCPR;               // dY rows per pass
+  constexpr int YP = BR / YRPP;                 // dY passes per step
+  constexpr int AP = BR / 16;                   // A rows per thread (16 threads per 128-wide row)
   __shared__ __attribute__((aligned(16))) cvl_bf16 Ys[BR * PITCH_Y];
   __shared__ __attribute__((aligned(16))) cvl_bf16 As[BR * PITCH_A];
 
@@ -62,15 +90,55 @@ __global__ void __launch_bounds__(NT) conv_wgrad_kernel(WgArgs g) {
   const int m_lo = blockIdx.y * g.chunk;
   const int m_hi = min(m_lo + g.chunk, a.m_total);
 
-  // fixed per-thread k chunk for A (16 chunks of 8 channels per 128-wide k tile)
-  const int ach = tid & 15, arow = tid >> 4;     // rows arow and arow + 16
+  // A operand: each thread owns one 8-channel k chunk (fixed tap) and rows arow + 16 h
+  const int ach = tid & 15, arow = tid >> 4;
   const int kc = k0 + ach * 8;
   const bool k_ok = kc < a.K;
   const int tap = k_ok ? kc / a.Cin : 0;
   const int ci = kc - tap * a.Cin;
   const int tr_ = tap / a.KW, ts_ = tap - (tap / a.KW) * a.KW;
-  // dY chunk mapping
+  // dY operand: chunk ych of rows yrow + YRPP p
   const int ych = tid % YCPR, yrow = tid / YCPR;
+
+  RowCursor ca[AP], cy[YP];
+  int sg = seg_of(a, m_lo);
+  auto seek_all = [&](int m) {
+    const ConvSeg& S = a.seg[sg];
+    const int ml = m - S.m_start;
+#pragma unroll
+    for (int h = 0; h < AP; ++h) cursor_seek(S, ca[h], ml + arow + 16 * h);
+#pragma unroll
+    for (int h = 0; h < YP; ++h) cursor_seek(S, cy[h], ml + yrow + YRPP * h);
+  };
+  seek_all(m_lo);
+
+  s16x8 va[AP], vy[YP];
+  auto load_step = [&]() {
+    const ConvSeg& S = a.seg[sg];
+#pragma unroll
+    for (int h = 0; h < AP; ++h) {
+      const RowCursor& c = ca[h];
+      va[h] = s16x8{0, 0, 0, 0, 0, 0, 0, 0};
+      const int iy = c.oy * a.stride - a.pad_t + tr_, ix = c.ox * a.stride - a.pad_l + ts_;
+      if (k_ok && c.ml < S.rows && iy >= 0 && ix >= 0 && iy < S.Hs && ix < S.Ws) {
+        const long row = S.src_base + (long)c.img * S.src_img + (long)iy * S.Ws + ix;
+        va[h] = *reinterpret_cast<const s16x8*>(a.src + row * a.Cin + ci);
+        if (a.relu_in) {
+#pragma unroll
+          for (int u = 0; u < 8; ++u) va[h][u] = va[h][u] < 0 ? (short)0 : va[h][u];
+        }
+      }
+    }
+#pragma unroll
+    for (int h = 0; h < YP; ++h) {
+      const RowCursor& c = cy[h];
+      vy[h] = s16x8{0, 0, 0, 0, 0, 0, 0, 0};
+      if (c.ml < S.rows) {
+        const long drow = S.dst_base + (long)c.img * S.dst_img + (long)c.oy * S.Wr + c.ox;
+        vy[h] = *reinterpret_cast<const s16x8*>(g.dy + drow * g.ld_dy + g.dy_coff + co0 + ych * 8);
+      }
+    }
+  };
 
   const int wave = tid >> 6, lane = tid & 63;
   const int wco = wave >> 1, wk = wave & 1;
@@ -82,80 +150,51 @@ __global__ void __launch_bounds__(NT) conv_wgrad_kernel(WgArgs g) {
 #pragma unroll
     for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
+  if (m_lo < m_hi) load_step();
   for (int m = m_lo; m < m_hi; m += BR) {
-    int sg = 0;
-#pragma unroll
-    for (int i = 1; i < kMaxSeg; ++i)
-      if (i < a.nseg && m >= a.seg[i].m_start) sg = i;
-    const ConvSeg& S = a.seg[sg];
-    const int mloc = m - S.m_start;
-    if (mloc >= S.rows) continue;                   // whole step is segment padding (uniform)
-    const int HWr = S.Hr * S.Wr;
-    const float rHW = 1.0f / (float)HWr, rW = 1.0f / (float)S.Wr;
-    // ---- A: two rows per thread, fixed k chunk -------------------------------------------------
-    s16x8 va[2];
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      const int ml = mloc + arow + h * 16;
-      va[h] = s16x8{0, 0, 0, 0, 0, 0, 0, 0};
-      if (k_ok && ml < S.rows) {
-        const int img = fdiv(ml, HWr, rHW);
-        const int qq = ml - img * HWr;
-        const int oy = fdiv(qq, S.Wr, rW), ox = qq - oy * S.Wr;
-        const int iy = oy * a.stride - a.pad_t + tr_, ix = ox * a.stride - a.pad_l + ts_;
-        if (iy >= 0 && ix >= 0 && iy < S.Hs && ix < S.Ws) {
-          const long row = S.src_base + (long)img * S.src_img + (long)iy * S.Ws + ix;
-          va[h] = *reinterpret_cast<const s16x8*>(a.src + row * a.Cin + ci);
-          if (a.relu_in) {
-#pragma unroll
-            for (int u = 0; u < 8; ++u) va[h][u] = va[h][u] < 0 ? (short)0 : va[h][u];
-          }
-        }
-      }
-    }
-    // ---- dY -------------------------------------------------------------------------------------
-    constexpr int YPT = (YCH + NT - 1) / NT;
-    s16x8 vy[YPT];
-#pragma unroll
-    for (int h = 0; h < YPT; ++h) {
-      const int idx = tid + h * NT;
-      const int r = idx / YCPR;
-      vy[h] = s16x8{0, 0, 0, 0, 0, 0, 0, 0};
-      const int ml = mloc + r;
-      if (idx < YCH && ml < S.rows) {
-        const int img = fdiv(ml, HWr, rHW);
-        const long drow = S.dst_base + (long)img * S.dst_img + (ml - img * HWr);
-        vy[h] = *reinterpret_cast<const s16x8*>(g.dy + drow * g.ld_dy + g.dy_coff + co0 + ych * 8);
-      }
-    }
     __syncthreads();
 #pragma unroll
-    for (int h = 0; h < 2; ++h)
-      *reinterpret_cast<s16x8*>(As + (arow + h * 16) * PITCH_A + ach * 8) = va[h];
+    for (int h = 0; h < AP; ++h)
+      *reinterpret_cast<s16x8*>(As + (arow + 16 * h) * PITCH_A + ach * 8) = va[h];
 #pragma unroll
-    for (int h = 0; h < YPT; ++h) {
-      const int idx = tid + h * NT;
-      if (idx < YCH) *reinterpret_cast<s16x8*>(Ys + (idx / YCPR) * PITCH_Y + ych * 8) = vy[h];
-    }
+    for (int h = 0; h < YP; ++h)
+      *reinterpret_cast<s16x8*>(Ys + (yrow + YRPP * h) * PITCH_Y + ych * 8) = vy[h];
     __syncthreads();
-    // ---- MFMA over the 32-row step ----------------------------------------------------------------
-    s16x8 fa[TM], fb[TN];
+    if (m + BR < m_hi) {             // prefetch the next step while this one computes
+      const int nsg = seg_of(a, m + BR);
+      if (nsg != sg) {
+        sg = nsg;
+        seek_all(m + BR);
+      } else {
+        const ConvSeg& S = a.seg[sg];
 #pragma unroll
-    for (int i = 0; i < TM; ++i) {
-      const int col = wco * WCO + i * 16 + 4 * p;
-      fa[i] = tr_frag(Ys + (8 * lg + q) * PITCH_Y + col, Ys + (8 * lg + 4 + q) * PITCH_Y + col);
+        for (int h = 0; h < AP; ++h) cursor_advance(S, ca[h], BR);
+#pragma unroll
+        for (int h = 0; h < YP; ++h) cursor_advance(S, cy[h], BR);
+      }
+      load_step();
     }
 #pragma unroll
-    for (int j = 0; j < TN; ++j) {
-      const int col = wk * WK + j * 16 + 4 * p;
-      fb[j] = tr_frag(As + (8 * lg + q) * PITCH_A + col, As + (8 * lg + 4 + q) * PITCH_A + col);
+    for (int ks = 0; ks < BR / 32; ++ks) {
+      s16x8 fa[TM], fb[TN];
+      const int r0 = ks * 32 + 8 * lg;
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const int col = wco * WCO + i * 16 + 4 * p;
+        fa[i] = tr_frag(Ys + (r0 + q) * PITCH_Y + col, Ys + (r0 + 4 + q) * PITCH_Y + col);
+      }
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int col = wk * WK + j * 16 + 4 * p;
+        fb[j] = tr_frag(As + (r0 + q) * PITCH_A + col, As + (r0 + 4 + q) * PITCH_A + col);
+      }
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+              __builtin_bit_cast(bf16x8, fa[i]), __builtin_bit_cast(bf16x8, fb[j]), acc[i][j], 0, 0, 0);
     }
-#pragma unroll
-    for (int i = 0; i < TM; ++i)
-#pragma unroll
-      for (int j = 0; j < TN; ++j)
-        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
-            __builtin_bit_cast(bf16x8, fa[i]), __builtin_bit_cast(bf16x8, fb[j]), acc[i][j], 0, 0, 0);
   }
 
   // ---- epilogue: C[co][k] -> out[k][co] (HWIO), 4 consecutive co per lane ------------------------
@@ -191,9 +230,9 @@ __global__ void wgrad_reduce_kernel(const float* slab, float* dw, long n, int sp
 }
 
 int pick_splits(int tiles, int m_total) {
-  // fill ~256 CUs with >= 1 tile each, but keep >= 2048 reduction rows per workgroup
-  int s = (256 + tiles - 1) / tiles;
-  const int max_s = m_total / 2048;
+  // ~512 workgroups (2 per CU at this kernel's occupancy), >= 1024 reduction rows each
+  int s = (512 + tiles - 1) / tiles;
+  const int max_s = m_total / 1024;
   if (s > max_s) s = max_s;
   return s < 1 ? 1 : s;
 }

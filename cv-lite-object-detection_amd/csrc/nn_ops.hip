@@ -127,26 +127,37 @@ __global__ void bn_apply_kernel(const cvl_bf16* z, const float* mr, const float*
   }
 }
 
-// per-(image, channel): sums[b][c] += (sum g, sum g*xhat), g = dy * (y > 0 if relu)
-// block = (image b, row chunk); threads: 8 channels each
-__global__ void bn_bwd_reduce_kernel(const cvl_bf16* dy, const cvl_bf16* y, const cvl_bf16* z,
-                                     const float* mr, double* sums, int C, int HW, int rows_per_blk) {
+// BN backward over one (image, row-chunk) block; threads own 8 channels (tpr threads per row,
+// rpp rows per pass).  PASS 0: sums[b][c] += (sum g, sum g*xhat), g = dy * (y > 0 if relu).
+// PASS 1: dz = gamma*rstd*(g - mean(g) - xhat*mean(g*xhat)) (+ g_out = g), and the conv-bias
+// gradient sum_rows dz accumulated per channel (fused column sum).
+template <int PASS>
+__global__ void bn_bwd_kernel(const cvl_bf16* dy, const cvl_bf16* y, const cvl_bf16* z, const float* mr,
+                              const float* gamma, double* sums, cvl_bf16* dz, cvl_bf16* g_out,
+                              double* dbias_acc, int C, int HW, int rows_per_blk) {
   const int b = blockIdx.y;
   const int C8 = C / 8;
-  const int tpr = C8 < NT ? C8 : NT;            // threads per row
-  const int rpp = NT / tpr;                     // rows per pass
+  const int tpr = C8 < NT ? C8 : NT;
+  const int rpp = NT / tpr;
   const int cg = threadIdx.x % tpr, rsub = threadIdx.x / tpr;
   const int r0 = blockIdx.x * rows_per_blk;
   const int r1 = min(r0 + rows_per_blk, HW);
-  __shared__ float red[NT * 8 * 2 / 8];         // reused per channel group pass
+  const float inv = 1.0f / (float)HW;
+  __shared__ float red[NT][17];
   for (int cgb = cg; cgb < C8; cgb += tpr) {
     const int c0 = cgb * 8;
-    float m[8], rs[8], s1[8], s2[8];
+    float m[8], rs[8], s1[8], s2[8], k1[8], k2[8], gm[8];
 #pragma unroll
     for (int u = 0; u < 8; ++u) {
-      m[u] = mr[((long)b * C + c0 + u) * 2];
-      rs[u] = mr[((long)b * C + c0 + u) * 2 + 1];
+      const long bc = (long)b * C + c0 + u;
+      m[u] = mr[bc * 2];
+      rs[u] = mr[bc * 2 + 1];
       s1[u] = 0.f; s2[u] = 0.f;
+      if (PASS == 1) {
+        k1[u] = (float)sums[bc * 2] * inv;          // mean(g)
+        k2[u] = (float)sums[bc * 2 + 1] * inv;      // mean(g * xhat)
+        gm[u] = gamma[c0 + u] * rs[u];
+      }
     }
     if (rsub < rpp) {
       for (int r = r0 + rsub; r < r1; r += rpp) {
@@ -160,68 +171,54 @@ __global__ void bn_bwd_reduce_kernel(const cvl_bf16* dy, const cvl_bf16* y, cons
 #pragma unroll
           for (int u = 0; u < 8; ++u) g[u] = yy[u] > 0.f ? g[u] : 0.f;
         }
+        if (PASS == 0) {
 #pragma unroll
-        for (int u = 0; u < 8; ++u) {
-          s1[u] += g[u];
-          s2[u] += g[u] * ((zz[u] - m[u]) * rs[u]);
+          for (int u = 0; u < 8; ++u) {
+            s1[u] += g[u];
+            s2[u] += g[u] * ((zz[u] - m[u]) * rs[u]);
+          }
+        } else {
+          if (g_out) *reinterpret_cast<s16x8*>(g_out + off) = pack8(g);
+          float o[8];
+#pragma unroll
+          for (int u = 0; u < 8; ++u) {
+            const float xh = (zz[u] - m[u]) * rs[u];
+            o[u] = gm[u] * (g[u] - k1[u] - xh * k2[u]);
+          }
+          const s16x8 ov = pack8(o);
+          *reinterpret_cast<s16x8*>(dz + off) = ov;
+          float orr[8];
+          unpack8(ov, orr);                       // the bias gradient sums the stored bf16 dz
+#pragma unroll
+          for (int u = 0; u < 8; ++u) s1[u] += orr[u];
         }
       }
     }
-    // reduce over rsub (threads with the same cg) through LDS, 8 channels x 2 values at a time
-    for (int u = 0; u < 8; ++u) {
-      __syncthreads();
-      red[threadIdx.x] = s1[u];
-      red[NT + threadIdx.x] = s2[u];
-      __syncthreads();
-      if (rsub == 0) {
+    __syncthreads();
+#pragma unroll
+    for (int u = 0; u < 8; ++u) { red[threadIdx.x][u] = s1[u]; red[threadIdx.x][8 + u] = s2[u]; }
+    __syncthreads();
+    if (rsub == 0) {
+      for (int u = 0; u < 8; ++u) {
         double a1 = 0.0, a2 = 0.0;
-        for (int k = 0; k < rpp; ++k) { a1 += red[k * tpr + cg]; a2 += red[NT + k * tpr + cg]; }
-        atomicAdd(&sums[((long)b * C + c0 + u) * 2], a1);
-        atomicAdd(&sums[((long)b * C + c0 + u) * 2 + 1], a2);
+        for (int k = 0; k < rpp; ++k) { a1 += red[k * tpr + cg][u]; a2 += red[k * tpr + cg][8 + u]; }
+        if (PASS == 0) {
+          atomicAdd(&sums[((long)b * C + c0 + u) * 2], a1);
+          atomicAdd(&sums[((long)b * C + c0 + u) * 2 + 1], a2);
+        } else if (dbias_acc) {
+          atomicAdd(&dbias_acc[c0 + u], a1);
+        }
       }
     }
-  }
-}
-
-// dz = gamma*rstd*(g - mean(g) - xhat*mean(g*xhat)); optional g_out = g (for the residual path)
-__global__ void bn_bwd_apply_kernel(const cvl_bf16* dy, const cvl_bf16* y, const cvl_bf16* z,
-                                    const float* mr, const float* gamma, const double* sums,
-                                    cvl_bf16* dz, cvl_bf16* g_out, long rows, int C, int HW) {
-  const int C8 = C / 8;
-  const long total = rows * C8;
-  const float inv = 1.0f / (float)HW;
-  for (long i = blockIdx.x * (long)NT + threadIdx.x; i < total; i += (long)gridDim.x * NT) {
-    const long row = i / C8;
-    const int c0 = (int)(i - row * C8) * 8;
-    const int b = (int)(row / HW);
-    float g[8], zz[8];
-    unpack8(*reinterpret_cast<const s16x8*>(dy + row * C + c0), g);
-    unpack8(*reinterpret_cast<const s16x8*>(z + row * C + c0), zz);
-    if (y) {
-      float yy[8];
-      unpack8(*reinterpret_cast<const s16x8*>(y + row * C + c0), yy);
-#pragma unroll
-      for (int u = 0; u < 8; ++u) g[u] = yy[u] > 0.f ? g[u] : 0.f;
-    }
-    if (g_out) *reinterpret_cast<s16x8*>(g_out + row * C + c0) = pack8(g);
-    float o[8];
-#pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      const long bc = (long)b * C + c0 + u;
-      const float m = mr[bc * 2], rs = mr[bc * 2 + 1];
-      const float mg = (float)sums[bc * 2] * inv, mgx = (float)sums[bc * 2 + 1] * inv;
-      const float xh = (zz[u] - m) * rs;
-      o[u] = gamma[c0 + u] * rs * (g[u] - mg - xh * mgx);
-    }
-    *reinterpret_cast<s16x8*>(dz + row * C + c0) = pack8(o);
   }
 }
 
 // dgamma[c] = beta_acc*dgamma + sum_b sum g*xhat ; dbeta[c] = ... + sum_b sum g
 __global__ void bn_param_grad_kernel(const double* sums, float* dgamma, float* dbeta, int B, int C,
-                                     float beta_acc) {
+                                     float beta_acc, const double* dbias_acc, float* conv_dbias) {
   const int c = blockIdx.x * NT + threadIdx.x;
   if (c >= C) return;
+  if (conv_dbias) conv_dbias[c] = (float)dbias_acc[c];
   double a1 = 0.0, a2 = 0.0;
   for (int b = 0; b < B; ++b) { a1 += sums[((long)b * C + c) * 2]; a2 += sums[((long)b * C + c) * 2 + 1]; }
   dbeta[c] = (float)a1 + (beta_acc != 0.f ? beta_acc * dbeta[c] : 0.f);
@@ -499,21 +496,27 @@ extern "C" int cvl_bn_apply(const void* z, const float* mean_rstd, const float* 
 
 extern "C" int cvl_bn_backward(const void* dy, const void* y_relu, const void* z, const float* mean_rstd,
                                const float* gamma, double* sums_ws, void* dz, void* g_out, float* dgamma,
-                               float* dbeta, float beta_acc, int B, int HW, int C, cvl_stream_t stream) {
+                               float* dbeta, float beta_acc, float* conv_dbias, int B, int HW, int C,
+                               cvl_stream_t stream) {
   CVL_CHECK_ARG(dy && z && mean_rstd && gamma && sums_ws && dz && dgamma && dbeta && C % 8 == 0);
-  hipError_t e = hipMemsetAsync(sums_ws, 0, sizeof(double) * 2 * B * C, S_);
+  // workspace: [B][C][2] sums followed by [C] conv-bias accumulators (float64)
+  hipError_t e = hipMemsetAsync(sums_ws, 0, sizeof(double) * (2 * (size_t)B * C + C), S_);
   if (e != hipSuccess) return CVL_EHIP + (int)e;
-  int rows_per_blk = 256;
-  while ((long)B * ((HW + rows_per_blk - 1) / rows_per_blk) > 2048 && rows_per_blk < HW) rows_per_blk *= 2;
+  double* dbias_acc = sums_ws + 2 * (size_t)B * C;
+  // ~512 workgroups whatever the layer shape (conv5 maps are only 16x16 per image)
+  const int C8 = C / 8, rpp = NT / (C8 < NT ? C8 : NT);
+  const int chunks = (512 + B - 1) / B;
+  int rows_per_blk = (HW + chunks - 1) / chunks;
+  rows_per_blk = ((rows_per_blk + rpp - 1) / rpp) * rpp;
   dim3 g1((HW + rows_per_blk - 1) / rows_per_blk, B);
-  hipLaunchKernelGGL(bn_bwd_reduce_kernel, g1, dim3(NT), 0, S_, (const cvl_bf16*)dy, (const cvl_bf16*)y_relu,
-                     (const cvl_bf16*)z, mean_rstd, sums_ws, C, HW, rows_per_blk);
-  const long rows = (long)B * HW;
-  hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(grid_for(rows * (C / 8))), dim3(NT), 0, S_,
-                     (const cvl_bf16*)dy, (const cvl_bf16*)y_relu, (const cvl_bf16*)z, mean_rstd, gamma,
-                     (const double*)sums_ws, (cvl_bf16*)dz, (cvl_bf16*)g_out, rows, C, HW);
+  hipLaunchKernelGGL(bn_bwd_kernel<0>, g1, dim3(NT), 0, S_, (const cvl_bf16*)dy, (const cvl_bf16*)y_relu,
+                     (const cvl_bf16*)z, mean_rstd, gamma, sums_ws, (cvl_bf16*)nullptr, (cvl_bf16*)nullptr,
+                     (double*)nullptr, C, HW, rows_per_blk);
+  hipLaunchKernelGGL(bn_bwd_kernel<1>, g1, dim3(NT), 0, S_, (const cvl_bf16*)dy, (const cvl_bf16*)y_relu,
+                     (const cvl_bf16*)z, mean_rstd, gamma, sums_ws, (cvl_bf16*)dz, (cvl_bf16*)g_out,
+                     conv_dbias ? dbias_acc : (double*)nullptr, C, HW, rows_per_blk);
   hipLaunchKernelGGL(bn_param_grad_kernel, dim3((C + NT - 1) / NT), dim3(NT), 0, S_, (const double*)sums_ws,
-                     dgamma, dbeta, B, C, beta_acc);
+                     dgamma, dbeta, B, C, beta_acc, (const double*)dbias_acc, conv_dbias);
   return cvl_launch_status();
 }
 

@@ -32,7 +32,7 @@ SIGNATURES = {
                            c_int, c_int, P, P]),
     "cvl_bn_finalize": (c_int, [P, P, P, P, c_int, c_int, c_int, c_float, c_float, P]),
     "cvl_bn_apply": (c_int, [P, P, P, P, P, P, c_int, c_int, c_int, c_int, P]),
-    "cvl_bn_backward": (c_int, [P, P, P, P, P, P, P, P, P, P, c_float, c_int, c_int, c_int, P]),
+    "cvl_bn_backward": (c_int, [P, P, P, P, P, P, P, P, P, P, c_float, P, c_int, c_int, c_int, P]),
     "cvl_maxpool3x3s2": (c_int, [P, P, P, c_int, c_int, c_int, c_int, P]),
     "cvl_maxpool3x3s2_backward": (c_int, [P, P, P, c_int, c_int, c_int, c_int, P]),
     "cvl_upsample2x_add": (c_int, [P, P, P, c_int, c_int, c_int, c_int, P]),

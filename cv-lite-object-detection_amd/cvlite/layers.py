@@ -188,12 +188,12 @@ class Conv(object):
         nn.conv_igemm(d, x, out, stats)
         return out, Ho, Wo
 
-    def wgrad(self, x, dy, B, H, W, relu_in=False, dw=None, beta=0.0):
+    def wgrad(self, x, dy, B, H, W, relu_in=False, dw=None, beta=0.0, bias=True):
         Ho, Wo, _, _ = self.out_hw(H, W)
         d = self.fwd_desc(B, [nn.seg(Ho, Wo, H, W, self.wf, None)], ld_dst=self.cout_pad_ld(dy),
                           relu_in=relu_in)
         nn.conv_wgrad(d, x, dy, self.dw if dw is None else dw, beta)
-        if self.has_bias:
+        if self.has_bias and bias:
             nn.bias_grad(dy, self.cout_pad_ld(dy), 0, self.cout, 0, Ho * Wo, Ho * Wo, B, self.db)
 
     def cout_pad_ld(self, dy):
@@ -257,8 +257,9 @@ class ConvBN(object):
         c = self.conv.cout
         dz = torch.empty_like(z)
         nn.bn_backward(dy, y if relu else None, z, mr, self.bn.gamma, dz, g_out,
-                       self.bn.store.g(self.bn.gname), self.bn.store.g(self.bn.bname), B, Ho * Wo, c)
-        self.conv.wgrad(x, dz, B, H, W)
+                       self.bn.store.g(self.bn.gname), self.bn.store.g(self.bn.bname), B, Ho * Wo, c,
+                       conv_dbias=self.conv.db)
+        self.conv.wgrad(x, dz, B, H, W, bias=False)
         if not need_dx:
             return None
         return self.conv.dgrad(dz, B, H, W, out=dx_out, beta=dx_beta)

@@ -84,10 +84,12 @@ def bn_apply(z, mean_rstd, gamma, beta, residual, y, B, HW, C, relu):
               B, HW, C, int(bool(relu)), stream())
 
 
-def bn_backward(dy, y_relu, z, mean_rstd, gamma, dz, g_out, dgamma, dbeta, B, HW, C, beta_acc=0.0):
-    ws = torch.empty((B, C, 2), dtype=torch.float64, device=dy.device)
+def bn_backward(dy, y_relu, z, mean_rstd, gamma, dz, g_out, dgamma, dbeta, B, HW, C, beta_acc=0.0,
+                conv_dbias=None):
+    ws = torch.empty(2 * B * C + C, dtype=torch.float64, device=dy.device)
     _lib.call("cvl_bn_backward", ptr(dy), ptr(y_relu), ptr(z), ptr(mean_rstd), ptr(gamma), ptr(ws),
-              ptr(dz), ptr(g_out), ptr(dgamma), ptr(dbeta), float(beta_acc), B, HW, C, stream())
+              ptr(dz), ptr(g_out), ptr(dgamma), ptr(dbeta), float(beta_acc), ptr(conv_dbias), B, HW, C,
+              stream())
 
 
 def maxpool3x3s2(x, y, argmax):

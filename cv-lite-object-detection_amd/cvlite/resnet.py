@@ -62,11 +62,10 @@ class Stem(object):
         dz = torch.empty_like(z)
         st = self.bn.store
         nn.bn_backward(dy, y, z, mr, self.bn.gamma, dz, None, st.g(self.bn.gname), st.g(self.bn.bname),
-                       B, Ho * Wo, 64)
+                       B, Ho * Wo, 64, conv_dbias=self.conv.db)
         dw = torch.empty((STEM_KP, 64), dtype=torch.float32, device=dp.device)
         nn.conv_wgrad(self._desc(B, Ho, Wo), A, dz, dw)
         self.conv.dw.view(147, 64).copy_(dw[:147])
-        nn.bias_grad(dz, 64, 0, 64, 0, Ho * Wo, Ho * Wo, B, self.conv.db)
 
 
 class Bottleneck(object):

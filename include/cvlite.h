@@ -142,11 +142,13 @@ int cvl_bn_finalize(const double* stats, float* mean_rstd, float* run_mean, floa
 int cvl_bn_apply(const void* z, const float* mean_rstd, const float* gamma, const float* beta,
                  const void* residual, void* y, int B, int HW, int C, int relu, cvl_stream_t stream);
 /* dy: grad of y; y_relu: y when the unit ends in ReLU (mask), else NULL; writes dz (bf16),
- * optionally g_out = masked dy (the residual branch's gradient), dgamma/dbeta (= + beta_acc*old).
- * sums_ws: float64 [B][C][2] workspace. */
+ * optionally g_out = masked dy (the residual branch's gradient), dgamma/dbeta (= + beta_acc*old)
+ * and, if conv_dbias != NULL, the gradient of the preceding conv's bias (= column sum of dz,
+ * fused).  sums_ws: float64 workspace of 2*B*C + C elements. */
 int cvl_bn_backward(const void* dy, const void* y_relu, const void* z, const float* mean_rstd,
                     const float* gamma, double* sums_ws, void* dz, void* g_out, float* dgamma,
-                    float* dbeta, float beta_acc, int B, int HW, int C, cvl_stream_t stream);
+                    float* dbeta, float beta_acc, float* conv_dbias, int B, int HW, int C,
+                    cvl_stream_t stream);
 
 /* ResNet50 pool1: ZeroPadding2D(1) + MaxPooling2D(3, 2); argmax [B][Ho][Wo][C] uint8 (0..8). */
 int cvl_maxpool3x3s2(const void* x, void* y, uint8_t* argmax, int B, int H, int W, int C,

@@ -60,10 +60,15 @@ def test_bn_forward_backward(B, HW, C, relu, res):
     gout = torch.empty_like(zg)
     dgam = torch.zeros(C, device="cuda")
     dbet = torch.zeros(C, device="cuda")
+    cdb = torch.full((C,), 7.0, device="cuda")
     nn.bn_backward(dy.to(BF).cuda(), y if relu else None, zg, mr, gamma.float().cuda(), dz, gout, dgam, dbet,
-                   B, HW, C)
+                   B, HW, C, conv_dbias=cdb)
     scale = zz.grad.abs().max().item()
     torch.testing.assert_close(dz.double().cpu(), zz.grad, rtol=2e-2, atol=2e-2 * scale)
+    # fused conv-bias gradient = column sum of the stored dz (mathematically ~0 behind BN)
+    torch.testing.assert_close(cdb.double().cpu(), dz.double().cpu().sum((0, 1)), rtol=1e-4, atol=1e-4 * scale)
+    if relu:
+        torch.testing.assert_close(gout.double().cpu(), dy * (y.double().cpu() > 0))
     torch.testing.assert_close(dgam.double().cpu(), gg.grad, rtol=2e-2, atol=2e-2 * gg.grad.abs().max().item())
     torch.testing.assert_close(dbet.double().cpu(), bb.grad, rtol=2e-2, atol=2e-2 * bb.grad.abs().max().item())
 
