@@ -1,0 +1,538 @@
+// RetinaNet anchor matching, CenterNet centroid targets and centre splat, the shared
+// focal + masked smooth-L1 loss, and greedy per-class NMS on gfx950.
+//
+//   cvl_retina_assign    RetinaNet/retinanet_module.py:205-365 + RetinaNet/utils.py:42-83
+//   cvl_centernet_assign CenterNet/tf_centernet_hourglass.py:379-456
+//   cvl_centernet_splat  CenterNet/tf_centernet.py:6-19, 152-342
+//   cvl_det_loss         tf_centernet_hourglass.py:458-505 / retinanet_module.py:367-426
+//   cvl_nms              tf_centernet_hourglass.py:22-85 (method 'nms')
+// Index/target kernels follow the reference's fp32 operation sequences exactly (this file is
+// compiled with -ffp-contract=off) and keep float64 where the reference computes in float64.
+#include "cvl_common.h"
+
+namespace {
+
+constexpr int NT = 256;
+constexpr int RT = 128;                   // retina_assign block (LDS stage of 128 rows x (4+C))
+constexpr int kMaxBox = 256;
+constexpr int kWords = 8;                  // class bitmask words (C <= 256)
+
+__device__ __forceinline__ float relu0(float v) { return v > 0.f ? v : 0.f; }
+
+// ------------------------------------------------------------------------------------------------
+// RetinaNet: output [B][sum_l A*S_l^2][4+C] ordered (level, anchor, u, v); cell (u, v) of level l
+// is the anchor centred at (u*s, v*s) with dims (h_a, w_a) (the reference builds its grid as
+// (col, row) and writes it back transposed, Q21: self-consistent for square maps).
+// ------------------------------------------------------------------------------------------------
+struct RetinaArgs {
+  const float* boxes;
+  const int32_t* nbox;
+  const float* img_dim;
+  const float* adims;      // [5][A][2] fp32 (h, w)
+  float* out;
+  int32_t* ntgt;
+  int n_max, C, A, P, pad;
+  float thresh;
+  int S[5], stride[5], off[6];
+};
+
+__global__ void __launch_bounds__(RT) retina_assign_kernel(RetinaArgs a) {
+  const int b = blockIdx.y;
+  const int p0 = blockIdx.x * RT;
+  const int tid = threadIdx.x;
+  const int row = 4 + a.C;
+  __shared__ float gy[kMaxBox], gx[kMaxBox], gh[kMaxBox], gw[kMaxBox], ga[kMaxBox], lo0[kMaxBox],
+      lo1[kMaxBox], hi0[kMaxBox], hi1[kMaxBox];
+  __shared__ int gc[kMaxBox];
+  __shared__ int cnt;
+  extern __shared__ __attribute__((aligned(16))) float stage[];
+  int n = a.nbox[b];
+  n = n < 0 ? 0 : (n > a.n_max ? a.n_max : n);
+  const float H = a.img_dim[2 * b], W = a.img_dim[2 * b + 1];
+  if (tid == 0) cnt = 0;
+  for (int i = tid; i < n; i += RT) {
+    const float* r = a.boxes + ((size_t)b * a.n_max + i) * 5;
+    // gt_boxes[:, :4] * [H, W, H, W]  (retinanet_module.py:274-278, fp32)
+    const float y = r[0] * H, x = r[1] * W, h = r[2] * H, w = r[3] * W;
+    gy[i] = y; gx[i] = x; gh[i] = h; gw[i] = w;
+    ga[i] = h * w;                                       // boxes1_area (utils.py:73)
+    lo0[i] = y - h / 2.0f; lo1[i] = x - w / 2.0f;       // convert to corners (utils.py:62-67)
+    hi0[i] = y + h / 2.0f; hi1[i] = x + w / 2.0f;
+    gc[i] = (int)r[4];
+  }
+  __syncthreads();
+  const int p = p0 + tid;
+  int matches = 0;
+  if (p < a.P) {
+    int l = 0;
+    while (l < 4 && p >= a.off[l + 1]) ++l;
+    const int S = a.S[l], s = a.stride[l];
+    const int q = p - a.off[l];
+    const int an = q / (S * S);
+    const int cell = q - an * S * S;
+    const int u = cell / S, v = cell - (cell / S) * S;
+    const float ah = a.adims[(l * a.A + an) * 2], aw = a.adims[(l * a.A + an) * 2 + 1];
+    const float c0 = (float)(u * s), c1 = (float)(v * s);
+    const float alo0 = c0 - ah / 2.0f, alo1 = c1 - aw / 2.0f;
+    const float ahi0 = c0 + ah / 2.0f, ahi1 = c1 + aw / 2.0f;
+    const float aa = ah * aw;
+    uint32_t bits[kWords];
+#pragma unroll
+    for (int k = 0; k < kWords; ++k) bits[k] = 0u;
+    int last = -1;
+    for (int i = 0; i < n; ++i) {
+      const float i0 = relu0(fminf(hi0[i], ahi0) - fmaxf(lo0[i], alo0));
+      const float i1 = relu0(fminf(hi1[i], ahi1) - fmaxf(lo1[i], alo1));
+      const float inter = i0 * i1;
+      float uni = (ga[i] + aa) - inter;
+      uni = uni > 1e-8f ? uni : 1e-8f;
+      float iou = inter / uni;
+      iou = iou < 0.f ? 0.f : (iou > 1.f ? 1.f : iou);
+      if (iou > a.thresh) {                               // strict > (retinanet_module.py:301)
+        ++matches;
+        last = i;
+        const int c = gc[i];
+        if (c >= 0 && c < a.C) bits[c >> 5] |= 1u << (c & 31);
+      }
+    }
+    float* st = stage + (size_t)tid * row;
+    if (last >= 0) {                                      // linear box targets in float64 (Q24)
+      st[0] = (float)(((double)u * s - (double)gy[last]) / (double)ah);
+      st[1] = (float)(((double)v * s - (double)gx[last]) / (double)aw);
+      st[2] = (float)((double)gh[last] / (double)ah);
+      st[3] = (float)((double)gw[last] / (double)aw);
+    } else {
+      st[0] = st[1] = st[2] = st[3] = 0.f;
+    }
+    for (int c = 0; c < a.C; ++c) st[4 + c] = ((bits[c >> 5] >> (c & 31)) & 1u) ? 1.0f : 0.0f;
+  }
+  if (matches) atomicAdd(&cnt, matches);
+  __syncthreads();
+  if (tid == 0 && cnt) atomicAdd(&a.ntgt[b], cnt);
+  const int ncell = min(RT, a.P - p0);
+  float* out = a.out + ((size_t)b * a.P + p0) * row;
+  for (int e = tid; e < ncell * row; e += RT) out[e] = stage[e];
+}
+
+// ------------------------------------------------------------------------------------------------
+// CenterNet hourglass centroid targets: one-hot at the centroid cell, ascending-area order
+// (tf_centernet_hourglass.py:403-453).  Output [B][hm][wm][4+C].
+// ------------------------------------------------------------------------------------------------
+struct CenterArgs {
+  const float* boxes;
+  const int32_t* nbox;
+  const float* img_dim;
+  float* out;
+  int n_max, C, hm, wm, stride;
+  float pad_h, pad_w;
+};
+
+__device__ void sort_by_area(const float* boxes, int n, float H, float W, int* order, float* area) {
+  // stable ascending rank (np.argsort on distinct areas)
+  for (int i = threadIdx.x; i < n; i += blockDim.x) area[i] = (boxes[i * 5 + 2] * H) * (boxes[i * 5 + 3] * W);
+  __syncthreads();
+  for (int i = threadIdx.x; i < n; i += blockDim.x) {
+    int r = 0;
+    for (int j = 0; j < n; ++j) r += (area[j] < area[i]) || (area[j] == area[i] && j < i);
+    order[r] = i;
+  }
+  __syncthreads();
+}
+
+__global__ void __launch_bounds__(NT) centernet_assign_kernel(CenterArgs a) {
+  const int b = blockIdx.y;
+  const int tid = threadIdx.x;
+  __shared__ int order[kMaxBox];
+  __shared__ float area[kMaxBox];
+  __shared__ int cy[kMaxBox], cx[kMaxBox], cc[kMaxBox];
+  __shared__ float off4[kMaxBox][4];
+  int n = a.nbox[b];
+  n = n < 0 ? 0 : (n > a.n_max ? a.n_max : n);
+  const float H = a.img_dim[2 * b], W = a.img_dim[2 * b + 1];
+  const float* bx = a.boxes + (size_t)b * a.n_max * 5;
+  sort_by_area(bx, n, H, W, order, area);
+  const float sf = (float)a.stride;
+  // pad_y = int((img_pad[1] - img_dim[1]) / 2.0), pad_x from index 0 (:397-398, fp32)
+  const float py = (float)(int)((a.pad_w - W) / 2.0f), px = (float)(int)((a.pad_h - H) / 2.0f);
+  for (int k = tid; k < n; k += NT) {
+    const float* r = bx + order[k] * 5;
+    const float c0 = (r[0] - 0.5f * r[2]) * H, c1 = (r[1] - 0.5f * r[3]) * W;   // :431-435
+    const float c2 = (r[0] + 0.5f * r[2]) * H, c3 = (r[1] + 0.5f * r[3]) * W;
+    const float ycf = (c0 + c2) / 2.0f, xcf = (c1 + c3) / 2.0f;                  // :437-438
+    const int yc = (int)((py + ycf) / sf), xc = (int)((px + xcf) / sf);          // :439-440
+    cy[k] = yc; cx[k] = xc; cc[k] = (int)r[4];
+    off4[k][0] = (float)((double)yc + 0.5) - (py + c0) / sf;                     // :444-448
+    off4[k][1] = ((py + c2) / sf - (float)yc) - 0.5f;
+    off4[k][2] = (float)((double)xc + 0.5) - (px + c1) / sf;
+    off4[k][3] = ((px + c3) / sf - (float)xc) - 0.5f;
+  }
+  __syncthreads();
+  const int row = 4 + a.C;
+  const int cells = a.hm * a.wm;
+  for (int cell = blockIdx.x * NT + tid; cell < cells; cell += gridDim.x * NT) {
+    const int y = cell / a.wm, x = cell - (cell / a.wm) * a.wm;
+    float v[4] = {0.f, 0.f, 0.f, 0.f};
+    uint32_t bits[kWords];
+#pragma unroll
+    for (int k = 0; k < kWords; ++k) bits[k] = 0u;
+    for (int k = 0; k < n; ++k) {
+      if (cy[k] == y && cx[k] == x) {
+        v[0] = off4[k][0]; v[1] = off4[k][1]; v[2] = off4[k][2]; v[3] = off4[k][3];
+        if (cc[k] >= 0 && cc[k] < a.C) bits[cc[k] >> 5] |= 1u << (cc[k] & 31);
+      }
+    }
+    float* o = a.out + ((size_t)b * cells + cell) * row;
+    o[0] = v[0]; o[1] = v[1]; o[2] = v[2]; o[3] = v[3];
+    for (int c = 0; c < a.C; ++c) o[4 + c] = ((bits[c >> 5] >> (c & 31)) & 1u) ? 1.0f : 0.0f;
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// CenterNet centre splat (tf_centernet.py:152-342): FCOS-style ltrb over the sigma sub-box, an
+// inverse-power (spread 8) centre kernel normalised by its maximum in ch4, class bits.
+// Output [B][Hs][Ws][5+C].  Last covering box (ascending area) wins ch0..4.
+// ------------------------------------------------------------------------------------------------
+struct SplatArgs {
+  const float* boxes;
+  const int32_t* nbox;
+  const float* img_dim;
+  float* out;
+  int n_max, C, Hs, Ws, stride;
+  float sigma, spread;
+};
+
+struct SplatBox {
+  int ylo, yup, xlo, xup, ycen, xcen, ny, nx, br, cls;
+  float t0, t1, t2, t3;
+  double zy, zx;   // per-axis maxima of the inverse-power kernel over the region
+};
+
+__device__ __forceinline__ double ipow_kernel(double g, double mu, double spread) {
+  return 1.0 / pow(g - mu, spread);
+}
+
+__global__ void __launch_bounds__(NT) centernet_splat_kernel(SplatArgs a) {
+  const int b = blockIdx.y;
+  const int tid = threadIdx.x;
+  __shared__ int order[kMaxBox];
+  __shared__ float area[kMaxBox];
+  __shared__ SplatBox bs[kMaxBox];
+  int n = a.nbox[b];
+  n = n < 0 ? 0 : (n > a.n_max ? a.n_max : n);
+  const float H = a.img_dim[2 * b], W = a.img_dim[2 * b + 1];
+  const float* bx = a.boxes + (size_t)b * a.n_max * 5;
+  sort_by_area(bx, n, H, W, order, area);
+  const float sf = (float)a.stride;
+  const float hr = H / sf, wr = W / sf;
+  const int ylim = (int)(H / sf), xlim = (int)(W / sf);
+  for (int k = tid; k < n; k += NT) {
+    const float* r = bx + order[k] * 5;
+    SplatBox q;
+    const float c0 = (r[0] - 0.5f * r[2]) * H, c1 = (r[1] - 0.5f * r[3]) * W;
+    const float c2 = (r[0] + 0.5f * r[2]) * H, c3 = (r[1] + 0.5f * r[3]) * W;
+    q.t0 = c0 / sf; q.t1 = c1 / sf; q.t2 = c2 / sf; q.t3 = c3 / sf;
+    q.ycen = (int)(r[0] * hr);                                                   // :208-209
+    q.xcen = (int)(r[1] * wr);
+    int ylo = 1 + (int)((r[0] - a.sigma * r[2] / 2.0f) * hr);                   // :211-218
+    int xlo = 1 + (int)((r[1] - a.sigma * r[3] / 2.0f) * wr);
+    int yup = 1 + (int)((r[0] + a.sigma * r[2] / 2.0f) * hr);
+    int xup = 1 + (int)((r[1] + a.sigma * r[3] / 2.0f) * wr);
+    ylo = ylo > 0 ? ylo : 0;
+    xlo = xlo > 0 ? xlo : 0;
+    yup = yup < ylim ? yup : ylim;                                               // upper clamp: img_dim (Q32)
+    xup = xup < xlim ? xup : xlim;
+    q.ylo = ylo; q.yup = yup; q.xlo = xlo; q.xup = xup;
+    q.br = ((yup - ylo) > 0 ? 1 : 0) | ((xup - xlo) > 0 ? 2 : 0);
+    q.ny = (int)(0.5 * (double)(ylo + yup));
+    q.nx = (int)(0.5 * (double)(xlo + xup));
+    q.cls = (int)r[4];
+    // maxima over the region of 1/|g - mu|^spread (the normaliser, separable: tf_centernet.py:17)
+    double zy = 0.0, zx = 0.0;
+    if (q.br & 1)
+      for (int z = ylo; z < yup; ++z) { const double g = ipow_kernel(z + 0.5, q.ny, a.spread); zy = g > zy ? g : zy; }
+    if (q.br & 2)
+      for (int z = xlo; z < xup; ++z) { const double g = ipow_kernel(z + 0.5, q.nx, a.spread); zx = g > zx ? g : zx; }
+    q.zy = zy; q.zx = zx;
+    bs[k] = q;
+  }
+  __syncthreads();
+  const int row = 5 + a.C;
+  const int cells = a.Hs * a.Ws;
+  for (int cell = blockIdx.x * NT + tid; cell < cells; cell += gridDim.x * NT) {
+    const int y = cell / a.Ws, x = cell - (cell / a.Ws) * a.Ws;
+    uint32_t bits[kWords];
+#pragma unroll
+    for (int k = 0; k < kWords; ++k) bits[k] = 0u;
+    int last = -1;
+    for (int k = 0; k < n; ++k) {
+      const SplatBox& q = bs[k];
+      bool cov;
+      switch (q.br) {
+        case 3: cov = y >= q.ylo && y < q.yup && x >= q.xlo && x < q.xup; break;
+        case 1: cov = y >= q.ylo && y < q.yup && x == q.xcen; break;
+        case 2: cov = y == q.ycen && x >= q.xlo && x < q.xup; break;
+        default: cov = y == q.ycen && x == q.xcen; break;
+      }
+      if (cov) {
+        last = k;
+        if (q.cls >= 0 && q.cls < a.C) bits[q.cls >> 5] |= 1u << (q.cls & 31);
+      }
+    }
+    float v[5] = {0.f, 0.f, 0.f, 0.f, 0.f};
+    if (last >= 0) {
+      const SplatBox& q = bs[last];
+      const float gy = (float)y + 0.5f, gx = (float)x + 0.5f;
+      if (q.br & 1) { v[0] = relu0(gy - q.t0); v[1] = relu0(q.t2 - gy); }
+      else { v[0] = relu0((float)((double)q.ycen + 0.5) - q.t0); v[1] = relu0((q.t2 - (float)q.ycen) - 0.5f); }
+      if (q.br & 2) { v[2] = relu0(gx - q.t1); v[3] = relu0(q.t3 - gx); }
+      else { v[2] = relu0((float)((double)q.xcen + 0.5) - q.t1); v[3] = relu0((q.t3 - (float)q.xcen) - 0.5f); }
+      double c;
+      if (q.br == 3) {
+        if (y == q.ny && x == q.nx) c = 1.0;
+        else {
+          const double gg = ipow_kernel(y + 0.5, q.ny, a.spread) * ipow_kernel(x + 0.5, q.nx, a.spread);
+          c = gg / (q.zy * q.zx);
+        }
+      } else if (q.br == 1) {
+        c = (y == q.ny) ? 1.0 : ipow_kernel(y + 0.5, q.ny, a.spread) / q.zy;
+      } else if (q.br == 2) {
+        c = (x == q.nx) ? 1.0 : ipow_kernel(x + 0.5, q.nx, a.spread) / q.zx;
+      } else {
+        c = 1.0;
+      }
+      v[4] = (float)c;
+    }
+    float* o = a.out + ((size_t)b * cells + cell) * row;
+#pragma unroll
+    for (int k = 0; k < 5; ++k) o[k] = v[k];
+    for (int c = 0; c < a.C; ++c) o[5 + c] = ((bits[c >> 5] >> (c & 31)) & 1u) ? 1.0f : 0.0f;
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// focal (alpha .25, gamma 2) on classes + smooth-L1 on 4 box channels masked by max(class) > 0,
+// per image sums and gradients (CenterNet model_loss, RetinaNet train_loss per (level, anchor)).
+// ------------------------------------------------------------------------------------------------
+struct DetLossArgs {
+  const float* reg;
+  const float* cls;
+  const float* tgt;
+  double* partial;
+  float* dreg;
+  float* dcls;
+  int ld_reg, ld_cls, P, C, tiles;
+  float grad_scale_cls, grad_scale_reg;
+};
+
+__global__ void __launch_bounds__(NT) det_loss_kernel(DetLossArgs a) {
+  const int b = blockIdx.y;
+  const int p = blockIdx.x * NT + threadIdx.x;
+  float s_cls = 0.f, s_reg = 0.f;
+  if (p < a.P) {
+    const size_t cell = (size_t)b * a.P + p;
+    const float* t = a.tgt + cell * (4 + a.C);
+    const float* xr = a.reg + cell * a.ld_reg;
+    const float* xc = a.cls + cell * a.ld_cls;
+    float tmax = 0.f;
+    for (int c = 0; c < a.C; ++c) {
+      const float y = t[4 + c];
+      tmax = fmaxf(tmax, y);
+      const float x = xc[c];
+      const float e = expf(-fabsf(x));
+      const float L = log1pf(e);
+      const float p1 = x >= 0.f ? 1.0f / (1.0f + e) : e / (1.0f + e);
+      const float q1 = x >= 0.f ? e / (1.0f + e) : 1.0f / (1.0f + e);
+      const float nlp = L - fminf(x, 0.f), nlq = L + fmaxf(x, 0.f);
+      s_cls += y * 0.25f * q1 * q1 * nlp + (1.0f - y) * 0.75f * p1 * p1 * nlq;
+      if (a.dcls) {
+        const float g = -y * 0.25f * q1 * q1 * (2.0f * p1 * nlp + q1) + (1.0f - y) * 0.75f * p1 * p1 * (2.0f * q1 * nlq + p1);
+        a.dcls[cell * a.ld_cls + c] = g * a.grad_scale_cls;
+      }
+    }
+    const float mask = tmax > 0.f ? 1.0f : 0.0f;                 // max(class) > 0
+    for (int j = 0; j < 4; ++j) {
+      const float d = t[j] - xr[j];
+      const float ad = fabsf(d);
+      float g;
+      if (ad < 1.0f) { s_reg += mask * 0.5f * d * d; g = -d; }
+      else { s_reg += mask * ad; g = d > 0.f ? -1.0f : (d < 0.f ? 1.0f : 0.0f); }
+      if (a.dreg) a.dreg[cell * a.ld_reg + j] = mask * g * a.grad_scale_reg;
+    }
+  }
+  __shared__ double red[2][NT / 64];
+  double v0 = warp_sum_d((double)s_cls), v1 = warp_sum_d((double)s_reg);
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  if (lane == 0) { red[0][w] = v0; red[1][w] = v1; }
+  __syncthreads();
+  if (threadIdx.x < 2) {
+    double s = 0.0;
+    for (int k = 0; k < NT / 64; ++k) s += red[threadIdx.x][k];
+    a.partial[((size_t)b * a.tiles + blockIdx.x) * 2 + threadIdx.x] = s;
+  }
+}
+
+__global__ void det_loss_finalize(const double* partial, float* losses, int tiles) {
+  const int b = blockIdx.x, k = threadIdx.x;
+  if (k < 2) {
+    double s = 0.0;
+    for (int i = 0; i < tiles; ++i) s += partial[((size_t)b * tiles + i) * 2 + k];
+    losses[b * 2 + k] = (float)s;
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// Greedy per-class NMS with the reference's selection order: within a class, repeatedly take the
+// first maximum score among the survivors and drop survivors with IoU > thr (bboxes_iou: float64,
+// floor at fp32 eps).  One workgroup per class; candidates in input order; output = kept indices
+// in the reference's emission order (classes in the caller-given order).
+// ------------------------------------------------------------------------------------------------
+__global__ void nms_kernel(const double* boxes /*[n][6] x1 y1 x2 y2 score cls*/, int n, const double* classes,
+                           int ncls, double thr, int32_t* keep /*[ncls][n]*/, int32_t* nkeep /*[ncls]*/,
+                           uint8_t* alive_ws /*[ncls][n]*/) {
+  const int ci = blockIdx.x;
+  if (ci >= ncls) return;
+  const double cval = classes[ci];
+  uint8_t* alive = alive_ws + (size_t)ci * n;
+  for (int i = threadIdx.x; i < n; i += blockDim.x) alive[i] = boxes[i * 6 + 5] == cval ? 1 : 0;
+  __shared__ double best_s[NT];
+  __shared__ int best_i[NT];
+  __shared__ int sel;
+  int count = 0;
+  __syncthreads();
+  for (;;) {
+    double bsc = -INFINITY;
+    int bi = 0x7fffffff;
+    for (int i = threadIdx.x; i < n; i += blockDim.x) {
+      if (!alive[i]) continue;
+      const double sc = boxes[i * 6 + 4];
+      if (sc > bsc || (sc == bsc && i < bi)) { bsc = sc; bi = i; }
+    }
+    best_s[threadIdx.x] = bsc;
+    best_i[threadIdx.x] = bi;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      double s0 = -INFINITY;
+      int i0 = 0x7fffffff;
+      for (int k = 0; k < (int)blockDim.x; ++k)
+        if (best_s[k] > s0 || (best_s[k] == s0 && best_i[k] < i0)) { s0 = best_s[k]; i0 = best_i[k]; }
+      sel = (i0 == 0x7fffffff) ? -1 : i0;
+      if (sel >= 0) { keep[(size_t)ci * n + count] = sel; alive[sel] = 0; }
+    }
+    __syncthreads();
+    const int s = sel;
+    if (s < 0) break;
+    ++count;
+    const double* q = boxes + s * 6;
+    const double qa = (q[2] - q[0]) * (q[3] - q[1]);
+    for (int i = threadIdx.x; i < n; i += blockDim.x) {
+      if (!alive[i]) continue;
+      const double* r = boxes + i * 6;
+      const double ra = (r[2] - r[0]) * (r[3] - r[1]);
+      const double l0 = q[0] > r[0] ? q[0] : r[0], l1 = q[1] > r[1] ? q[1] : r[1];
+      const double h0 = q[2] < r[2] ? q[2] : r[2], h1 = q[3] < r[3] ? q[3] : r[3];
+      const double w0 = h0 - l0 > 0.0 ? h0 - l0 : 0.0, w1 = h1 - l1 > 0.0 ? h1 - l1 : 0.0;
+      const double inter = w0 * w1;
+      double iou = 1.0 * inter / (qa + ra - inter);
+      const double eps = 1.1920928955078125e-07;        // np.finfo(np.float32).eps
+      iou = iou > eps ? iou : eps;
+      if (iou > thr || !(r[4] * (iou > thr ? 0.0 : 1.0) > 0.0)) alive[i] = 0;
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) nkeep[ci] = count;
+}
+
+}  // namespace
+
+#define S_ ((hipStream_t)stream)
+
+extern "C" int cvl_retina_assign(const float* boxes, const int32_t* nbox, const float* img_dim, int B, int n_max,
+                                 int pad, int num_classes, const float* anchor_dims, int n_anchors,
+                                 const int32_t* strides, float iou_thresh, float* targets, int32_t* num_targets,
+                                 cvl_stream_t stream) {
+  CVL_CHECK_ARG(boxes && nbox && img_dim && anchor_dims && strides && targets && num_targets);
+  CVL_CHECK_ARG(B > 0 && n_max > 0 && n_max <= kMaxBox && pad > 0 && num_classes > 0 &&
+                num_classes <= 32 * kWords && n_anchors > 0);
+  RetinaArgs a;
+  a.boxes = boxes; a.nbox = nbox; a.img_dim = img_dim; a.adims = anchor_dims; a.out = targets;
+  a.ntgt = num_targets; a.n_max = n_max; a.C = num_classes; a.A = n_anchors; a.pad = pad;
+  a.thresh = iou_thresh;
+  a.off[0] = 0;
+  for (int l = 0; l < 5; ++l) {
+    CVL_CHECK_ARG(strides[l] > 0);
+    a.stride[l] = strides[l];
+    a.S[l] = pad / strides[l];
+    a.off[l + 1] = a.off[l] + n_anchors * a.S[l] * a.S[l];
+  }
+  a.P = a.off[5];
+  const size_t lds = (size_t)RT * (4 + num_classes) * sizeof(float);
+  CVL_CHECK_ARG(lds <= 60 * 1024);
+  hipError_t e = hipMemsetAsync(num_targets, 0, sizeof(int32_t) * B, S_);
+  if (e != hipSuccess) return CVL_EHIP + (int)e;
+  hipLaunchKernelGGL(retina_assign_kernel, dim3((a.P + RT - 1) / RT, B), dim3(RT), lds, S_, a);
+  return cvl_launch_status();
+}
+
+extern "C" int cvl_centernet_assign(const float* boxes, const int32_t* nbox, const float* img_dim, int B,
+                                    int n_max, int pad_h, int pad_w, int num_classes, int stride,
+                                    float* targets, cvl_stream_t stream) {
+  CVL_CHECK_ARG(boxes && nbox && img_dim && targets && B > 0 && n_max > 0 && n_max <= kMaxBox);
+  CVL_CHECK_ARG(num_classes > 0 && num_classes <= 32 * kWords && stride > 0 && pad_h > 0 && pad_w > 0);
+  CenterArgs a;
+  a.boxes = boxes; a.nbox = nbox; a.img_dim = img_dim; a.out = targets; a.n_max = n_max;
+  a.C = num_classes; a.stride = stride;
+  // tf_centernet_hourglass.py:395-398: h_max uses img_pad[1], w_max img_pad[0] (swapped)
+  a.hm = pad_w / stride;
+  a.wm = pad_h / stride;
+  a.pad_h = (float)pad_h; a.pad_w = (float)pad_w;
+  const int cells = a.hm * a.wm;
+  int gx = (cells + NT - 1) / NT;
+  gx = gx > 64 ? 64 : gx;
+  hipLaunchKernelGGL(centernet_assign_kernel, dim3(gx, B), dim3(NT), 0, S_, a);
+  return cvl_launch_status();
+}
+
+extern "C" int cvl_centernet_splat(const float* boxes, const int32_t* nbox, const float* img_dim, int B,
+                                   int n_max, int pad_h, int pad_w, int num_classes, int stride, float sigma,
+                                   float* targets, cvl_stream_t stream) {
+  CVL_CHECK_ARG(boxes && nbox && img_dim && targets && B > 0 && n_max > 0 && n_max <= kMaxBox);
+  CVL_CHECK_ARG(num_classes > 0 && num_classes <= 32 * kWords && stride > 0);
+  SplatArgs a;
+  a.boxes = boxes; a.nbox = nbox; a.img_dim = img_dim; a.out = targets; a.n_max = n_max;
+  a.C = num_classes; a.Hs = pad_h / stride; a.Ws = pad_w / stride; a.stride = stride;
+  a.sigma = sigma; a.spread = 8.0f;              // tmp_std forced to 8.0 (tf_centernet.py:206-207)
+  const int cells = a.Hs * a.Ws;
+  int gx = (cells + NT - 1) / NT;
+  gx = gx > 64 ? 64 : gx;
+  hipLaunchKernelGGL(centernet_splat_kernel, dim3(gx, B), dim3(NT), 0, S_, a);
+  return cvl_launch_status();
+}
+
+extern "C" size_t cvl_det_loss_workspace_size(int B, int P) {
+  return (size_t)B * ((P + NT - 1) / NT) * 2 * sizeof(double);
+}
+
+extern "C" int cvl_det_loss(const float* reg_pred, int ld_reg, const float* cls_pred, int ld_cls,
+                            const float* targets, int B, int P, int num_classes, float grad_scale_cls,
+                            float grad_scale_reg, float* losses, float* d_reg, float* d_cls, void* workspace,
+                            cvl_stream_t stream) {
+  CVL_CHECK_ARG(reg_pred && cls_pred && targets && losses && workspace && ld_reg >= 4 && ld_cls >= num_classes);
+  DetLossArgs a;
+  a.reg = reg_pred; a.cls = cls_pred; a.tgt = targets; a.partial = (double*)workspace;
+  a.dreg = d_reg; a.dcls = d_cls; a.ld_reg = ld_reg; a.ld_cls = ld_cls; a.P = P; a.C = num_classes;
+  a.tiles = (P + NT - 1) / NT;
+  a.grad_scale_cls = grad_scale_cls; a.grad_scale_reg = grad_scale_reg;
+  hipLaunchKernelGGL(det_loss_kernel, dim3(a.tiles, B), dim3(NT), 0, S_, a);
+  hipLaunchKernelGGL(det_loss_finalize, dim3(B), dim3(64), 0, S_, (const double*)workspace, losses, a.tiles);
+  return cvl_launch_status();
+}
+
+extern "C" size_t cvl_nms_workspace_size(int n, int ncls) { return (size_t)n * ncls + 16; }
+
+extern "C" int cvl_nms(const double* boxes, int n, const double* classes, int ncls, double iou_threshold,
+                       int32_t* keep, int32_t* nkeep, void* workspace, cvl_stream_t stream) {
+  CVL_CHECK_ARG(boxes && classes && keep && nkeep && workspace && n > 0 && ncls > 0);
+  hipLaunchKernelGGL(nms_kernel, dim3(ncls), dim3(NT), 0, S_, boxes, n, classes, ncls, iou_threshold, keep,
+                     nkeep, (uint8_t*)workspace);
+  return cvl_launch_status();
+}

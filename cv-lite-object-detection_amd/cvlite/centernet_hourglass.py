@@ -1,0 +1,53 @@
+"""Drop-in mirror of CenterNet/tf_centernet_hourglass.py's target / loss / decode functions on
+MI355X: `format_data` (cvl_centernet_assign), `model_loss` (cvl_det_loss), `nms` (cvl_nms),
+`prediction_to_corners` (cvl_fcos_decode: same formula, tf_centernet_hourglass.py:355-377)."""
+import numpy as np
+import torch
+
+from . import _lib
+from . import ops_targets as ot
+from .fcos import prediction_to_corners  # noqa: F401  (identical formula)
+
+
+def format_data(gt_labels, img_dim, num_classes, img_pad=None, stride=8):
+    """tf_centernet_hourglass.py:379-456 -> (float32 [pad_w/s, pad_h/s, 4+C], num_targets)."""
+    if img_pad is None:
+        img_pad = [int(float(v)) for v in np.asarray(img_dim, np.float32)]
+    gt = np.asarray(gt_labels, dtype=np.float32).reshape(-1, 5)
+    n = len(gt)
+    boxes = np.zeros((1, max(n, 1), 5), np.float32)
+    boxes[0, :n] = gt
+    _lib.require_cuda()
+    out = ot.centernet_assign(torch.tensor(boxes, device="cuda"), torch.tensor([n], dtype=torch.int32, device="cuda"),
+                              torch.tensor(np.asarray(img_dim, np.float32).reshape(1, 2), device="cuda"),
+                              (int(img_pad[0]), int(img_pad[1])), num_classes, stride=stride)
+    return out[0].cpu().numpy(), n
+
+
+def model_loss(y_true, y_pred):
+    """tf_centernet_hourglass.py:492-505: (cls, reg) summed over the batch."""
+    _lib.require_cuda()
+    yt = torch.as_tensor(np.asarray(y_true, np.float32) if not torch.is_tensor(y_true) else y_true,
+                         dtype=torch.float32).cuda()
+    yp = torch.as_tensor(np.asarray(y_pred, np.float32) if not torch.is_tensor(y_pred) else y_pred,
+                         dtype=torch.float32).cuda()
+    C = yt.shape[-1] - 4
+    t = yt.reshape(1, -1, 4 + C).contiguous()
+    p = yp.reshape(1, -1, 4 + C)
+    losses, _, _ = ot.det_loss(p[..., :4].contiguous(), p[..., 4:].contiguous(), t, C, with_grad=False)
+    return losses[0, 0], losses[0, 1]
+
+
+def nms(bboxes, iou_threshold, sigma=0.3, method="nms"):
+    """tf_centernet_hourglass.py:44-85 with method 'nms': rows (xmin, ymin, w, h, score, cls) ->
+    list of kept rows (x1, y1, x2, y2, score, cls), classes in python-set order."""
+    assert method in ["nms", "soft-nms"]
+    if method != "nms":
+        raise NotImplementedError("soft-nms is outside the measured path")
+    b = np.array(bboxes, dtype=np.float64)
+    classes = list(set(b[:, 5]))
+    b[:, 2] = b[:, 0] + b[:, 2]
+    b[:, 3] = b[:, 1] + b[:, 3]
+    _lib.require_cuda()
+    kept = ot.nms(torch.tensor(b, device="cuda"), classes, iou_threshold)
+    return [row for row in kept.cpu().numpy()]

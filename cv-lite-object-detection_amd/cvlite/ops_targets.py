@@ -56,3 +56,82 @@ def fcos_loss(reg_pred, cls_pred, targets, num_classes, reg_type="l1", grad_scal
               ptr(d_cls), int(d_cls.shape[2]) if d_cls is not None else 0, dt(d_cls),
               ptr(ws), _lib.stream())
     return losses, d_reg, d_cls
+
+
+def _boxes_args(boxes, nbox, img_dim):
+    _lib.require_cuda(boxes, nbox, img_dim)
+    assert boxes.dtype == torch.float32 and nbox.dtype == torch.int32 and img_dim.dtype == torch.float32
+    return int(boxes.shape[0]), int(boxes.shape[1])
+
+
+RETINA_STRIDES = (8, 16, 32, 64, 128)    # RetinaNet/retinanet_module.py:197
+
+
+def retina_assign(boxes, nbox, img_dim, pad, anchor_dims, num_classes, iou_thresh=0.5,
+                  strides=RETINA_STRIDES, out=None):
+    """Batched RetinaNet targets.  anchor_dims: device fp32 [5, A, 2].  Returns (targets
+    [B, sum_l A*S_l^2, 4+C] f32 ordered (level, anchor, u, v), num_targets [B] i32)."""
+    B, nmax = _boxes_args(boxes, nbox, img_dim)
+    A = int(anchor_dims.shape[1])
+    P = sum(A * (pad // s) ** 2 for s in strides)
+    if out is None:
+        out = torch.empty((B, P, 4 + num_classes), device=boxes.device, dtype=torch.float32)
+    nt = torch.empty((B,), device=boxes.device, dtype=torch.int32)
+    st = (_lib.ctypes.c_int32 * 5)(*[int(s) for s in strides])
+    _lib.call("cvl_retina_assign", ptr(boxes), ptr(nbox), ptr(img_dim), B, nmax, int(pad), int(num_classes),
+              ptr(anchor_dims.contiguous()), A, _lib.ctypes.cast(st, _lib.c_void_p), float(iou_thresh), ptr(out),
+              ptr(nt), _lib.stream())
+    return out, nt
+
+
+def centernet_assign(boxes, nbox, img_dim, pad_hw, num_classes, stride=8):
+    """CenterNet hourglass centroid targets -> [B, pad_w/s, pad_h/s, 4+C]."""
+    B, nmax = _boxes_args(boxes, nbox, img_dim)
+    out = torch.empty((B, pad_hw[1] // stride, pad_hw[0] // stride, 4 + num_classes), device=boxes.device,
+                      dtype=torch.float32)
+    _lib.call("cvl_centernet_assign", ptr(boxes), ptr(nbox), ptr(img_dim), B, nmax, int(pad_hw[0]),
+              int(pad_hw[1]), int(num_classes), int(stride), ptr(out), _lib.stream())
+    return out
+
+
+def centernet_splat(boxes, nbox, img_dim, pad_hw, num_classes, stride=8, sigma=0.25):
+    """CenterNet centre splat targets -> [B, pad_h/s, pad_w/s, 5+C]."""
+    B, nmax = _boxes_args(boxes, nbox, img_dim)
+    out = torch.empty((B, pad_hw[0] // stride, pad_hw[1] // stride, 5 + num_classes), device=boxes.device,
+                      dtype=torch.float32)
+    _lib.call("cvl_centernet_splat", ptr(boxes), ptr(nbox), ptr(img_dim), B, nmax, int(pad_hw[0]),
+              int(pad_hw[1]), int(num_classes), int(stride), float(sigma), ptr(out), _lib.stream())
+    return out
+
+
+def det_loss(reg_pred, cls_pred, targets, num_classes, grad_scale_cls=1.0, grad_scale_reg=1.0, with_grad=True):
+    """Focal + masked smooth-L1 (CenterNet / RetinaNet).  reg [B,P,>=4], cls [B,P,>=C], targets
+    [B,P,4+C] (f32).  Returns (losses [B,2] = (cls, reg), d_reg, d_cls)."""
+    _lib.require_cuda(reg_pred, cls_pred, targets)
+    B, P = int(targets.shape[0]), int(targets.shape[1])
+    dev = targets.device
+    losses = torch.empty((B, 2), device=dev, dtype=torch.float32)
+    ws = torch.empty(int(_lib.load().cvl_det_loss_workspace_size(B, P)), device=dev, dtype=torch.uint8)
+    d_reg = torch.zeros_like(reg_pred) if with_grad else None
+    d_cls = torch.zeros_like(cls_pred) if with_grad else None
+    _lib.call("cvl_det_loss", ptr(reg_pred), int(reg_pred.shape[-1]), ptr(cls_pred), int(cls_pred.shape[-1]),
+              ptr(targets), B, P, int(num_classes), float(grad_scale_cls), float(grad_scale_reg), ptr(losses),
+              ptr(d_reg), ptr(d_cls), ptr(ws), _lib.stream())
+    return losses, d_reg, d_cls
+
+
+def nms(boxes_xyxy, classes, iou_threshold):
+    """boxes [n, 6] float64 (x1, y1, x2, y2, score, cls) device; classes: iterable of class values
+    in processing order.  Returns the kept rows in the reference's emission order."""
+    _lib.require_cuda(boxes_xyxy)
+    n = int(boxes_xyxy.shape[0])
+    cls = torch.tensor(list(classes), dtype=torch.float64, device=boxes_xyxy.device)
+    ncls = int(cls.numel())
+    keep = torch.empty((ncls, n), dtype=torch.int32, device=boxes_xyxy.device)
+    nkeep = torch.empty((ncls,), dtype=torch.int32, device=boxes_xyxy.device)
+    ws = torch.empty(int(_lib.load().cvl_nms_workspace_size(n, ncls)), dtype=torch.uint8, device=boxes_xyxy.device)
+    _lib.call("cvl_nms", ptr(boxes_xyxy), n, ptr(cls), ncls, float(iou_threshold), ptr(keep), ptr(nkeep),
+              ptr(ws), _lib.stream())
+    nk = nkeep.cpu().tolist()
+    idx = torch.cat([keep[c, :nk[c]] for c in range(ncls)]) if ncls else keep.new_zeros(0)
+    return boxes_xyxy[idx.long()]

@@ -1,0 +1,106 @@
+"""Drop-in mirror of RetinaNet/retinanet_module.py's `RetinaNet` target interface on MI355X.
+
+`RetinaNet(n_classes, id_2_label, aspect_ratios, anchor_scales, anchor_sizes, backbone_model)`
+keeps the reference attributes (`anchor_sizes`, `aspect_ratios`, `anchor_scales`, `strides`,
+`n_anchors`, `box_areas`, `anchor_boxes`) and methods `get_anchors`, `format_data` (device kernel
+cvl_retina_assign: anchor generation + IoU matching per output cell), `focal_loss`,
+`smooth_l1_loss`.  The anchor dimensions are the 45 numbers of retinanet_module.py:205-219,
+computed once on the host with the reference's fp32 operation order.
+"""
+import numpy as np
+import torch
+
+from . import _lib
+from . import ops_targets as ot
+
+f32 = np.float32
+
+
+class RetinaNet(object):
+    def __init__(self, n_classes, id_2_label, aspect_ratios=None, anchor_scales=None, anchor_sizes=None,
+                 backbone_model="resnet50", **kwargs):
+        if anchor_sizes is None:
+            self.anchor_sizes = [32.0, 64.0, 128.0, 256.0, 512.0]
+        elif len(anchor_sizes) != 5:
+            raise ValueError("anchor_sizes must be of dimension 5.")
+        else:
+            self.anchor_sizes = anchor_sizes
+        self.aspect_ratios = [0.5, 1.0, 2.0] if aspect_ratios is None else aspect_ratios
+        if anchor_scales is None:
+            self.anchor_scales = [2 ** x for x in [0, 1 / 3, 2 / 3]]
+        elif len(anchor_scales) != 3:
+            raise ValueError("anchor_scales must be of dimension 3.")
+        else:
+            self.anchor_scales = anchor_scales
+        self.n_class = n_classes
+        self.strides = [8, 16, 32, 64, 128]
+        self.n_anchors = len(self.anchor_scales) * len(self.aspect_ratios)
+        self.box_areas = list(sorted([x ** 2 for x in self.anchor_sizes]))
+        self.id_2_label = id_2_label
+        self.backbone_model = backbone_model
+        # retinanet_module.py:205-216: h = sqrt(area / ratio), w = area / h (fp32 tensor ops),
+        # scale * (h, w) (fp32); ratio outer loop, scale inner loop (Q22)
+        boxes = []
+        for area in self.box_areas:
+            lev = []
+            for ratio in self.aspect_ratios:
+                h = np.sqrt(f32(area / ratio))
+                w = f32(f32(area) / h)
+                for sc in self.anchor_scales:
+                    lev.append(np.array([f32(f32(sc) * h), f32(f32(sc) * w)], dtype=f32))
+            boxes.append(lev)
+        self.anchor_boxes = boxes
+        self._dims_dev = None
+
+    def anchor_dims_device(self):
+        if self._dims_dev is None:
+            _lib.require_cuda()
+            self._dims_dev = torch.tensor(np.array(self.anchor_boxes, dtype=f32), device="cuda")
+        return self._dims_dev
+
+    def get_anchors(self, cnn_shape, level):
+        """retinanet_module.py:221-246 (host helper): 9 arrays [S0, S1, 4] = (col, row, h, w)."""
+        if level >= 5 or level < 0:
+            raise ValueError("level has to be between 0 and 4.")
+        gx, gy = np.meshgrid(np.arange(cnn_shape[1], dtype=f32), np.arange(cnn_shape[0], dtype=f32))
+        base = np.stack([gx, gy, np.ones_like(gx), np.ones_like(gx)], -1).astype(np.float64)
+        return [base * np.array([1, 1, d[0], d[1]], np.float64).reshape(1, 1, 4) for d in self.anchor_boxes[level]]
+
+    def format_data_batched(self, boxes, nbox, img_dim, pad, iou_thresh=0.50):
+        """Device form: boxes [B,Nmax,5], nbox [B], img_dim [B,2] -> targets [B, P, 4+C], counts [B]."""
+        return ot.retina_assign(boxes, nbox, img_dim, pad, self.anchor_dims_device(), self.n_class,
+                                iou_thresh=iou_thresh, strides=self.strides)
+
+    def format_data(self, gt_labels, img_dim, iou_thresh=0.50, img_pad=None):
+        """retinanet_module.py:251-365 -> (nested [5][A] float32 [S,S,4+C] maps, num_targets)."""
+        if img_pad is None:
+            img_pad = img_dim
+        pad = int(float(np.asarray(img_pad, dtype=np.float32)[0]))
+        if int(float(np.asarray(img_pad, dtype=np.float32)[1])) != pad:
+            raise ValueError("the reference's transposed anchor grid is consistent only for square maps")
+        gt = np.asarray(gt_labels, dtype=f32).reshape(-1, 5)
+        n = len(gt)
+        boxes = np.zeros((1, max(n, 1), 5), f32)
+        boxes[0, :n] = gt
+        dev = "cuda"
+        tg, nt = self.format_data_batched(torch.tensor(boxes, device=dev), torch.tensor([n], dtype=torch.int32, device=dev),
+                                          torch.tensor(np.asarray(img_dim, f32).reshape(1, 2), device=dev), pad,
+                                          iou_thresh)
+        tg = tg[0].cpu().numpy()
+        outs, o = [], 0
+        for s in self.strides:
+            S = pad // s
+            lev = []
+            for _ in range(self.n_anchors):
+                lev.append(tg[o:o + S * S].reshape(S, S, 4 + self.n_class))
+                o += S * S
+            outs.append(lev)
+        return outs, int(nt[0].item())
+
+    def focal_loss(self, labels, logits, alpha=0.25, gamma=2.0):
+        from .fcos import focal_loss
+        return focal_loss(labels, logits, alpha, gamma)
+
+    def smooth_l1_loss(self, xy_true, xy_pred, mask=1.0, delta=1.0):
+        from .fcos import smooth_l1_loss
+        return smooth_l1_loss(xy_true, xy_pred, mask, delta)

@@ -178,6 +178,46 @@ int cvl_sgd_clip_update(float* w, const float* g, float* v, int64_t n, const flo
 int cvl_lr_schedule(int32_t* step, float* lr, double init_lr, double min_lr, double decay_rate,
                     int decay_step, cvl_stream_t stream);
 
+/* ------------------------------------------------------------------------------------------
+ * RetinaNet target assignment.  Replaces RetinaNet/retinanet_module.py:205-365
+ * (`RetinaNet.__init__` anchor dims are passed in; `get_anchors` + `format_data` + utils.compute_iou
+ * run per output cell): anchor_dims [5][n_anchors][2] fp32 (h, w); square pad (pad x pad);
+ * output targets [B][sum_l n_anchors*S_l^2][4+C] ordered (level, anchor, u, v), the reference's
+ * nested [5][9] maps of [S,S,4+C] (float64 there) rounded to fp32, bit-exact; match iff fp32
+ * IoU > iou_thresh; num_targets[b] = number of (box, anchor) matches. */
+int cvl_retina_assign(const float* boxes, const int32_t* nbox, const float* img_dim, int B, int n_max,
+                      int pad, int num_classes, const float* anchor_dims, int n_anchors,
+                      const int32_t* strides /*host[5]*/, float iou_thresh, float* targets,
+                      int32_t* num_targets, cvl_stream_t stream);
+
+/* CenterNet (hourglass) centroid targets: CenterNet/tf_centernet_hourglass.py:379-456.
+ * Output [B][pad_w/stride][pad_h/stride][4+C] (the reference's h_max/w_max swap kept). */
+int cvl_centernet_assign(const float* boxes, const int32_t* nbox, const float* img_dim, int B, int n_max,
+                         int pad_h, int pad_w, int num_classes, int stride, float* targets,
+                         cvl_stream_t stream);
+
+/* CenterNet centre "splat": CenterNet/tf_centernet.py:152-342 (inverse-power kernel, spread 8,
+ * sigma sub-box).  Output [B][pad_h/stride][pad_w/stride][5+C]. */
+int cvl_centernet_splat(const float* boxes, const int32_t* nbox, const float* img_dim, int B, int n_max,
+                        int pad_h, int pad_w, int num_classes, int stride, float sigma, float* targets,
+                        cvl_stream_t stream);
+
+/* Focal (alpha .25, gamma 2) on C class logits + smooth-L1 on 4 box channels masked by
+ * max(class target) > 0: CenterNet model_loss (tf_centernet_hourglass.py:492-505) and one
+ * (level, anchor) term of RetinaNet.train_loss (retinanet_module.py:403-426).  targets
+ * [B][P][4+C]; losses [B][2] = (cls, reg); d_reg / d_cls (fp32, same strides) nullable. */
+size_t cvl_det_loss_workspace_size(int B, int P);
+int cvl_det_loss(const float* reg_pred, int ld_reg, const float* cls_pred, int ld_cls, const float* targets,
+                 int B, int P, int num_classes, float grad_scale_cls, float grad_scale_reg, float* losses,
+                 float* d_reg, float* d_cls, void* workspace, cvl_stream_t stream);
+
+/* Greedy per-class NMS (CenterNet/tf_centernet_hourglass.py:44-85, method 'nms'): boxes [n][6] =
+ * (x1, y1, x2, y2, score, cls) float64; classes [ncls] processed in the given order; keep
+ * [ncls][n] indices in selection order (first maximum among survivors), nkeep [ncls]. */
+size_t cvl_nms_workspace_size(int n, int ncls);
+int cvl_nms(const double* boxes, int n, const double* classes, int ncls, double iou_threshold,
+            int32_t* keep, int32_t* nkeep, void* workspace, cvl_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,0 +1,116 @@
+"""GPU parity of the RetinaNet anchor matcher, CenterNet centroid targets, centre splat, the
+focal + masked smooth-L1 loss and NMS against the reference golden vectors (bit-exact for maps /
+indices; losses 2e-5; gradients vs float64 autograd 1e-4)."""
+import numpy as np
+import pytest
+import torch
+
+from oracle import centernet_ref, retina_ref
+
+pytestmark = pytest.mark.gpu
+
+
+def test_retina_assign_bit_exact(golden):
+    from cvlite.retinanet import RetinaNet
+    d = golden("retinanet")
+    i = 0
+    while "case_%d_D" % i in d:
+        D = int(d["case_%d_D" % i])
+        net = RetinaNet(80, {}, anchor_sizes=list(d["case_%d_sizes" % i]))
+        np.testing.assert_array_equal(np.array(net.anchor_boxes, np.float64), d["case_%d_anchor_dims" % i])
+        outs, n = net.format_data(d["case_%d_boxes" % i], np.array([D, D], np.float32), iou_thresh=0.5, img_pad=[D, D])
+        assert n == int(d["case_%d_ntgt" % i])
+        for l in range(5):
+            np.testing.assert_array_equal(np.stack(outs[l]), d["case_%d_L%d" % (i, l)].astype(np.float32))
+        i += 1
+    assert i >= 10
+
+
+def test_retina_assign_batched_matches_oracle():
+    from cvlite.retinanet import RetinaNet
+    rng = np.random.default_rng(9)
+    B, D, C, nmax = 4, 640, 80, 50
+    net = RetinaNet(C, {}, anchor_sizes=[20.0, 40.0, 80.0, 160.0, 320.0])
+    boxes = np.zeros((B, nmax, 5), np.float32)
+    nbox = rng.integers(1, nmax + 1, B).astype(np.int32)
+    for b in range(B):
+        n = nbox[b]
+        hw = np.exp(rng.uniform(np.log(8 / D), np.log(0.9), (n, 2)))
+        boxes[b, :n, 2:4] = hw
+        boxes[b, :n, 0] = rng.uniform(hw[:, 0] / 2, 1 - hw[:, 0] / 2)
+        boxes[b, :n, 1] = rng.uniform(hw[:, 1] / 2, 1 - hw[:, 1] / 2)
+        boxes[b, :n, 4] = rng.integers(0, C, n)
+    dims = np.full((B, 2), D, np.float32)
+    tg, nt = net.format_data_batched(torch.tensor(boxes).cuda(), torch.tensor(nbox).cuda(), torch.tensor(dims).cuda(), D)
+    tg = tg.cpu().numpy()
+    ad = retina_ref.anchor_dims([20.0, 40.0, 80.0, 160.0, 320.0])
+    for b in range(B):
+        outs, n = retina_ref.format_data(boxes[b, :nbox[b]], dims[b], ad, C, img_pad=[D, D])
+        ref = np.concatenate([np.stack(outs[l]).reshape(-1, 4 + C) for l in range(5)], 0)
+        np.testing.assert_array_equal(tg[b], ref.astype(np.float32))
+        assert int(nt[b]) == n
+
+
+def test_centernet_assign_and_splat_bit_exact(golden):
+    from cvlite import centernet_hourglass as hg
+    from cvlite import centernet_splat as cs
+    d = golden("centernet")
+    for i in range(16):
+        D = float(d["hg_%d_D" % i])
+        out, n = hg.format_data(d["hg_%d_boxes" % i], np.array([D, D], np.float32), 20, img_pad=[int(D), int(D)],
+                                stride=int(d["hg_%d_stride" % i]))
+        np.testing.assert_array_equal(out, d["hg_%d_out" % i].astype(np.float32))
+        assert n == int(d["hg_%d_n" % i])
+    for i in range(12):
+        D = float(d["splat_%d_D" % i])
+        out = cs.format_data(d["splat_%d_boxes" % i], np.array([D, D], np.float32), 20, img_pad=[int(D), int(D)])
+        np.testing.assert_array_equal(out, d["splat_%d_out" % i].astype(np.float32))
+
+
+def test_centernet_splat_edge_cases():
+    from cvlite import centernet_splat as cs
+    rng = np.random.default_rng(17)
+    for k in range(20):
+        D = 512.0
+        n = int(rng.integers(1, 30))
+        hw = np.exp(rng.uniform(np.log(2 / D), np.log(1.0), (n, 2))).astype(np.float32)
+        yc = rng.uniform(hw[:, 0] / 2, 1 - hw[:, 0] / 2)
+        xc = rng.uniform(hw[:, 1] / 2, 1 - hw[:, 1] / 2)
+        g = np.stack([yc, xc, hw[:, 0], hw[:, 1], rng.integers(0, 20, n)], 1).astype(np.float32)
+        area = (g[:, 2] * np.float32(D)) * (g[:, 3] * np.float32(D))
+        _, first = np.unique(area, return_index=True)
+        g = g[np.sort(first)]
+        out = cs.format_data(g, np.array([D, D], np.float32), 20, img_pad=[512, 512])
+        np.testing.assert_array_equal(out, centernet_ref.splat_format_data(g, np.array([D, D], np.float32), 20,
+                                                                           img_pad=[512, 512]).astype(np.float32))
+
+
+def test_det_loss_matches_reference_and_grad(golden):
+    from cvlite import centernet_hourglass as hg
+    from cvlite import ops_targets as ot
+    from oracle import fcos_torch
+    d = golden("centernet")
+    for i in range(6):
+        y, p = d["hgloss_%d_y" % i], d["hgloss_%d_p" % i]
+        c, r = hg.model_loss(y, p)
+        np.testing.assert_allclose([float(c), float(r)], d["hgloss_%d_out" % i], rtol=2e-5)
+        C = y.shape[-1] - 4
+        t = torch.tensor(y.reshape(1, -1, 4 + C), dtype=torch.float32)
+        pp = torch.tensor(p.reshape(1, -1, 4 + C))
+        _, dr, dc = ot.det_loss(pp[..., :4].contiguous().cuda(), pp[..., 4:].contiguous().cuda(), t.cuda(), C,
+                                grad_scale_cls=2.5, grad_scale_reg=1.0)
+        pr = pp[0, :, :4].double().requires_grad_()
+        pc = pp[0, :, 4:].double().requires_grad_()
+        tt = t[0].double()
+        mask = (tt[:, 4:].max(-1).values > 0).double()
+        (2.5 * fcos_torch.focal(tt[:, 4:], pc) + fcos_torch.smooth_l1(tt[:, :4], pr, mask)).backward()
+        np.testing.assert_allclose(dr[0].cpu().numpy(), pr.grad.numpy(), rtol=1e-4, atol=1e-6)
+        np.testing.assert_allclose(dc[0].cpu().numpy(), pc.grad.numpy(), rtol=1e-4, atol=1e-6)
+
+
+def test_nms_matches_reference(golden):
+    from cvlite import centernet_hourglass as hg
+    d = golden("centernet")
+    for i in range(8):
+        got = np.array(hg.nms(d["nms_%d_in" % i], 0.213), np.float64).reshape(-1, 6)
+        np.testing.assert_array_equal(got, d["nms_%d_out" % i])
