@@ -28,6 +28,8 @@ struct ConvArgs {
   int K, Npad, n_store, ld_dst, dst_coff, dst_f32, relu_out, relu_in;
   float beta;
   int m_tiles, m_total;
+  float* slab;      // split-K partial sums [splits][m_total][Npad] (fp32) or null
+  int splits, ksteps_per_split;
 };
 
 // Validate a public descriptor and lay its segments out in a BM-padded M space.
@@ -38,6 +40,9 @@ static inline int cvl_conv_prepare(const cvl_conv_desc* d, int bm, ConvArgs* a) 
   CVL_CHECK_ARG(d->mode == CVL_CONV_FWD || d->mode == CVL_CONV_DGRAD);
   CVL_CHECK_ARG(d->Npad > 0 && d->n_store > 0 && d->n_store <= d->Npad);
   CVL_CHECK_ARG(d->ld_dst >= d->dst_coff + d->n_store);
+  a->slab = nullptr;
+  a->splits = 1;
+  a->ksteps_per_split = 0;
   a->nseg = d->nseg;
   a->B = d->B;
   a->Cin = d->Cin; a->KH = d->KH; a->KW = d->KW; a->stride = d->stride;

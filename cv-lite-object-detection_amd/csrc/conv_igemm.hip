@@ -34,7 +34,18 @@ __device__ __forceinline__ s16x8 relu_bf16x8(s16x8 v) {
   return v;
 }
 
-template <int BN, int BK, bool DGRAD>
+// 16 zero bytes: the LDS-DMA source of padding taps / rows past the end of a segment
+__device__ __attribute__((aligned(16))) cvl_bf16 g_zero16[8];
+
+__device__ __forceinline__ void glds16(const void* g, void* l) {
+  __builtin_amdgcn_global_load_lds((const void __attribute__((address_space(1)))*)g,
+                                   (void __attribute__((address_space(3)))*)l, 16, 0, 0);
+}
+
+// GLDS: operands go global->LDS by LDS-DMA (global_load_lds_dwordx4: no VGPR staging, no
+// ds_write), double-buffered so the next K step's DMA overlaps this step's MFMAs; the XOR swizzle
+// moves to the per-lane source address (each wave-instruction writes 1 KiB lane-linearly).
+template <int BN, int BK, bool DGRAD, bool GLDS>
 __global__ void __launch_bounds__(NT) conv_igemm_kernel(ConvArgs a) {
   constexpr int WM = BM / 2, WN = BN / 2;
   constexpr int TM = WM / 16, TN = WN / 16;
@@ -43,7 +54,8 @@ __global__ void __launch_bounds__(NT) conv_igemm_kernel(ConvArgs a) {
   constexpr int AP = BM / RPP;
   constexpr int BROWS = BN < RPP ? BN : RPP;
   constexpr int BP = BN / BROWS;
-  constexpr int LDS_AB = (BM + BN) * BK;
+  constexpr int NBUF = GLDS ? 2 : 1;
+  constexpr int LDS_AB = NBUF * (BM + BN) * BK;
   constexpr int LDS_C = BM * (BN + 8);
   constexpr int LDS_EL = LDS_AB > LDS_C ? LDS_AB : LDS_C;
   __shared__ __attribute__((aligned(16))) cvl_bf16 lds[LDS_EL];
@@ -113,6 +125,42 @@ __global__ void __launch_bounds__(NT) conv_igemm_kernel(ConvArgs a) {
         rb[p] = *reinterpret_cast<const s16x8*>(wsrc + (long)n * a.K + k0 + ch * 8);
     }
   };
+  // LDS-DMA form of load_tile + store_tile: lane (rr, ch) of the lane-linear image holds global
+  // chunk ch ^ swz(row), so the fragment reads below are unchanged
+  auto glds_tile = [&](int kt, int buf) {
+    cvl_bf16* Ab = lds + buf * (BM + BN) * BK;
+    cvl_bf16* Bb = Ab + BM * BK;
+    const int k0 = kt * BK;
+    const int tap = k0 / Cin;
+    const int cb = k0 - tap * Cin;
+    const int r = tap / a.KW, s = tap - (tap / a.KW) * a.KW;
+    const int wbase = (tid >> 6) * (64 / CPR);    // first row of this wave's 1 KiB piece
+#pragma unroll
+    for (int p = 0; p < AP; ++p) {
+      int iy, ix;
+      bool ok = a_ok[p];
+      if (DGRAD) {
+        const int ty = a_y[p] - r, tx = a_x[p] - s;
+        ok = ok && ty >= 0 && tx >= 0 && (ty % a.stride) == 0 && (tx % a.stride) == 0;
+        iy = ty / a.stride; ix = tx / a.stride;
+      } else {
+        iy = a_y[p] + r; ix = a_x[p] + s;
+      }
+      ok = ok && iy >= 0 && ix >= 0 && iy < S.Hs && ix < S.Ws;
+      const int row = p * RPP + rr;
+      const cvl_bf16* g = g_zero16;
+      if (ok) {
+        const long grow = S.src_base + (long)a_img[p] * S.src_img + (long)iy * S.Ws + ix;
+        g = src + grow * Cin + cb + ((ch ^ swz<BK>(row)) * 8);
+      }
+      glds16(g, Ab + (p * RPP + wbase) * BK);
+    }
+#pragma unroll
+    for (int p = 0; p < BP; ++p) {
+      const int row = p * BROWS + tid / CPR;
+      glds16(wsrc + (long)(n0 + row) * a.K + k0 + ((ch ^ swz<BK>(row)) * 8), Bb + (p * BROWS + wbase) * BK);
+    }
+  };
   auto store_tile = [&]() {
 #pragma unroll
     for (int p = 0; p < AP; ++p) {
@@ -135,13 +183,31 @@ __global__ void __launch_bounds__(NT) conv_igemm_kernel(ConvArgs a) {
 #pragma unroll
     for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  const int nk = a.K / BK;
-  load_tile(0);
-  for (int kt = 0; kt < nk; ++kt) {
-    __syncthreads();
-    store_tile();
-    __syncthreads();
-    if (kt + 1 < nk) load_tile(kt + 1);
+  // split-K: this workgroup reduces K-steps [kt0, kt1)
+  int kt0 = 0, kt1 = a.K / BK;
+  if (a.splits > 1) {
+    kt0 = blockIdx.z * a.ksteps_per_split;
+    kt1 = min(kt1, kt0 + a.ksteps_per_split);
+  }
+  const int nk = kt1;
+  if (GLDS) glds_tile(kt0, 0);
+  else load_tile(kt0);
+  for (int kt = kt0; kt < nk; ++kt) {
+    const cvl_bf16* Ac = As;
+    const cvl_bf16* Bc = Bs;
+    if (GLDS) {
+      const int buf = (kt - kt0) & 1;
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();                          // step kt landed; buffer buf^1 no longer read
+      if (kt + 1 < nk) glds_tile(kt + 1, buf ^ 1);
+      Ac = lds + buf * (BM + BN) * BK;
+      Bc = Ac + BM * BK;
+    } else {
+      __syncthreads();
+      store_tile();
+      __syncthreads();
+      if (kt + 1 < nk) load_tile(kt + 1);
+    }
 #pragma unroll
     for (int ks = 0; ks < BK / 32; ++ks) {
       const int chunk = ks * 4 + lg;
@@ -149,12 +215,12 @@ __global__ void __launch_bounds__(NT) conv_igemm_kernel(ConvArgs a) {
 #pragma unroll
       for (int i = 0; i < TM; ++i) {
         const int r = wm * WM + i * 16 + lr;
-        fa[i] = *reinterpret_cast<const s16x8*>(As + r * BK + ((chunk ^ swz<BK>(r)) * 8));
+        fa[i] = *reinterpret_cast<const s16x8*>(Ac + r * BK + ((chunk ^ swz<BK>(r)) * 8));
       }
 #pragma unroll
       for (int j = 0; j < TN; ++j) {
         const int r = wn * WN + j * 16 + lr;
-        fb[j] = *reinterpret_cast<const s16x8*>(Bs + r * BK + ((chunk ^ swz<BK>(r)) * 8));
+        fb[j] = *reinterpret_cast<const s16x8*>(Bc + r * BK + ((chunk ^ swz<BK>(r)) * 8));
       }
 #pragma unroll
       for (int i = 0; i < TM; ++i)
@@ -166,6 +232,20 @@ __global__ void __launch_bounds__(NT) conv_igemm_kernel(ConvArgs a) {
   }
 
   // ---- epilogue -------------------------------------------------------------------------------
+  if (a.splits > 1) {   // raw fp32 partials; conv_splitk_finish applies the epilogue
+    float* slab = a.slab + (size_t)blockIdx.z * a.m_total * a.Npad;
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int r = m0 + wm * WM + i * 16 + lg * 4 + e;
+          const int c = n0 + wn * WN + j * 16 + lr;
+          slab[(size_t)r * a.Npad + c] = acc[i][j][e];
+        }
+    return;
+  }
   const float* bias = S.bias;
   float bcol[TN];
 #pragma unroll
@@ -286,11 +366,120 @@ __global__ void __launch_bounds__(NT) conv_igemm_kernel(ConvArgs a) {
   }
 }
 
+// Split-K epilogue for single-segment convs: sum the partial slabs, + bias, ReLU, beta*old,
+// BN statistics (per image: a workgroup owns rows of one image), bf16/fp32 store.
+__global__ void __launch_bounds__(NT) conv_splitk_finish(ConvArgs a, int rows_per_blk) {
+  const ConvSeg& S = a.seg[0];
+  const int HW = S.Hr * S.Wr;
+  const int img = blockIdx.y;
+  const int C8 = a.n_store / 8;
+  const int tpr = C8 < NT ? C8 : NT;
+  const int rpp = NT / tpr;
+  const int cg = threadIdx.x % tpr, rsub = threadIdx.x / tpr;
+  const int q0 = blockIdx.x * rows_per_blk;
+  const int q1 = min(q0 + rows_per_blk, HW);
+  __shared__ float red[NT][17];
+  for (int cgb = cg; cgb < C8; cgb += tpr) {
+    const int c0 = cgb * 8;
+    float s1[8], s2[8], bb[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) { s1[u] = 0.f; s2[u] = 0.f; bb[u] = S.bias ? S.bias[c0 + u] : 0.f; }
+    if (rsub < rpp) {
+      for (int q = q0 + rsub; q < q1; q += rpp) {
+        const long ml = (long)img * HW + q;
+        float v[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) v[u] = bb[u];
+        for (int z = 0; z < a.splits; ++z) {
+          const f32x4* p = reinterpret_cast<const f32x4*>(a.slab + ((size_t)z * a.m_total + ml) * a.Npad + c0);
+          const f32x4 x0 = p[0], x1 = p[1];
+          v[0] += x0[0]; v[1] += x0[1]; v[2] += x0[2]; v[3] += x0[3];
+          v[4] += x1[0]; v[5] += x1[1]; v[6] += x1[2]; v[7] += x1[3];
+        }
+        const long drow = S.dst_base + (long)img * S.dst_img + q;
+        if (a.dst_f32) {
+          float* pd = reinterpret_cast<float*>(a.dst) + drow * a.ld_dst + a.dst_coff + c0;
+#pragma unroll
+          for (int u = 0; u < 8; ++u) {
+            float o = v[u];
+            if (a.relu_out) o = o > 0.f ? o : 0.f;
+            s1[u] += o; s2[u] += o * o;
+            if (a.beta != 0.f) o += a.beta * pd[u];
+            pd[u] = o;
+          }
+        } else {
+          s16x8* pd = reinterpret_cast<s16x8*>(reinterpret_cast<cvl_bf16*>(a.dst) + drow * a.ld_dst + a.dst_coff + c0);
+          s16x8 old;
+          if (a.beta != 0.f) old = *pd;
+          s16x8 o;
+#pragma unroll
+          for (int u = 0; u < 8; ++u) {
+            float x = v[u];
+            if (a.relu_out) x = x > 0.f ? x : 0.f;
+            x = bf16_to_f32(f32_to_bf16(x));
+            s1[u] += x; s2[u] += x * x;
+            if (a.beta != 0.f) x += a.beta * bf16_to_f32((cvl_bf16)old[u]);
+            o[u] = (short)f32_to_bf16(x);
+          }
+          *pd = o;
+        }
+      }
+    }
+    if (a.stats) {
+      __syncthreads();
+#pragma unroll
+      for (int u = 0; u < 8; ++u) { red[threadIdx.x][u] = s1[u]; red[threadIdx.x][8 + u] = s2[u]; }
+      __syncthreads();
+      if (rsub == 0) {
+        for (int u = 0; u < 8; ++u) {
+          double t1 = 0.0, t2 = 0.0;
+          for (int k = 0; k < rpp; ++k) { t1 += red[k * tpr + cg][u]; t2 += red[k * tpr + cg][8 + u]; }
+          double* st = a.stats + ((long)img * a.n_store + c0 + u) * 2;
+          atomicAdd(st, t1);
+          atomicAdd(st + 1, t2);
+        }
+      }
+    }
+  }
+}
+
+// split-K factor: only for grids that cannot fill the chip (small M, e.g. conv5 / c6 at 16x16)
+static inline int pick_ksplit(const ConvArgs& a, int BN_, int BK_) {
+  if (a.nseg != 1) return 1;
+  const int tiles = a.m_tiles * (a.Npad / BN_);
+  const int nk = a.K / BK_;
+  if (tiles >= 192 || nk < 8) return 1;
+  int s = (384 + tiles - 1) / tiles;
+  if (s > nk / 4) s = nk / 4;
+  return s < 1 ? 1 : s;
+}
+
 template <int BN, int BK>
-int launch_bn_bk(const ConvArgs& a, bool dgrad, hipStream_t s) {
-  dim3 grid(a.m_tiles, a.Npad / BN);
-  if (dgrad) hipLaunchKernelGGL((conv_igemm_kernel<BN, BK, true>), grid, dim3(NT), 0, s, a);
-  else hipLaunchKernelGGL((conv_igemm_kernel<BN, BK, false>), grid, dim3(NT), 0, s, a);
+int launch_bn_bk(const ConvArgs& a0, bool dgrad, hipStream_t s) {
+  ConvArgs a = a0;
+  if (a.splits > 1) {
+    const int nk = a.K / BK;
+    a.ksteps_per_split = (nk + a.splits - 1) / a.splits;
+    a.splits = (nk + a.ksteps_per_split - 1) / a.ksteps_per_split;
+  }
+  dim3 grid(a.m_tiles, a.Npad / BN, a.splits);
+  // LDS-DMA staging measured no faster than register staging at this tile (2 blocks/CU): opt-in
+  const bool glds = BK == 64 && !a.relu_in && cvl_env_flag("CVL_CONV_GLDS");
+  if (glds) {
+    if (dgrad) hipLaunchKernelGGL((conv_igemm_kernel<BN, BK, true, true>), grid, dim3(NT), 0, s, a);
+    else hipLaunchKernelGGL((conv_igemm_kernel<BN, BK, false, true>), grid, dim3(NT), 0, s, a);
+  } else {
+    if (dgrad) hipLaunchKernelGGL((conv_igemm_kernel<BN, BK, true, false>), grid, dim3(NT), 0, s, a);
+    else hipLaunchKernelGGL((conv_igemm_kernel<BN, BK, false, false>), grid, dim3(NT), 0, s, a);
+  }
+  int st = cvl_launch_status();
+  if (st || a.splits <= 1) return st;
+  const ConvSeg& S = a.seg[0];
+  const int HW = S.Hr * S.Wr;
+  int chunks = (512 + a.B - 1) / a.B;
+  int rpb = (HW + chunks - 1) / chunks;
+  rpb = rpb < 4 ? 4 : rpb;
+  hipLaunchKernelGGL(conv_splitk_finish, dim3((HW + rpb - 1) / rpb, a.B), dim3(NT), 0, s, a, rpb);
   return cvl_launch_status();
 }
 
@@ -300,10 +489,21 @@ int launch_bn(const ConvArgs& a, bool dgrad, hipStream_t s) {
   return launch_bn_bk<BN, 32>(a, dgrad, s);
 }
 
+static inline int pick_bn(int npad) { return npad % 128 == 0 ? 128 : (npad % 64 == 0 ? 64 : 32); }
+
 }  // namespace
 
+int cvl_conv_igemm_l(const cvl_conv_desc* d, const void* src, void* dst, double* bn_stats, hipStream_t s);
+
+extern "C" size_t cvl_conv_igemm_workspace_size(const cvl_conv_desc* d) {
+  ConvArgs a;
+  if (cvl_conv_prepare(d, BM, &a)) return 0;
+  const int sp = pick_ksplit(a, pick_bn(a.Npad), a.Cin % 64 == 0 ? 64 : 32);
+  return sp > 1 ? (size_t)sp * a.m_total * a.Npad * sizeof(float) : 16;
+}
+
 extern "C" int cvl_conv_igemm(const cvl_conv_desc* d, const void* src, void* dst, double* bn_stats,
-                              cvl_stream_t stream) {
+                              void* workspace, size_t workspace_bytes, cvl_stream_t stream) {
   ConvArgs a;
   int st = cvl_conv_prepare(d, BM, &a);
   if (st) return st;
@@ -316,11 +516,23 @@ extern "C" int cvl_conv_igemm(const cvl_conv_desc* d, const void* src, void* dst
       CVL_CHECK_ARG(hw % BM == 0 || (BM % hw == 0 && hw % 4 == 0));
     }
   }
+  {
+    const int lst = cvl_conv_igemm_l(d, src, dst, bn_stats, (hipStream_t)stream);
+    if (lst >= 0) return lst;          // the 256-row LDS-DMA kernel took the launch
+  }
   a.src = reinterpret_cast<const cvl_bf16*>(src);
   a.dst = dst;
   a.stats = bn_stats;
+  const int bn = pick_bn(a.Npad);
+  const int sp = pick_ksplit(a, bn, a.Cin % 64 == 0 ? 64 : 32);
+  if (sp > 1 && workspace && (d->n_store / 8 <= NT) && workspace_bytes >= (size_t)sp * a.m_total * a.Npad * sizeof(float) &&
+      d->n_store % 8 == 0 && d->dst_coff % 8 == 0 && (d->dst_f32 || d->ld_dst % 8 == 0)) {
+    a.splits = sp;
+    a.slab = reinterpret_cast<float*>(workspace);
+  }
   hipStream_t s = (hipStream_t)stream;
-  if (a.Npad % 128 == 0) return launch_bn<128>(a, d->mode == CVL_CONV_DGRAD, s);
-  if (a.Npad % 64 == 0) return launch_bn<64>(a, d->mode == CVL_CONV_DGRAD, s);
-  return launch_bn<32>(a, d->mode == CVL_CONV_DGRAD, s);
+  const bool dg = d->mode == CVL_CONV_DGRAD;
+  if (bn == 128) return launch_bn<128>(a, dg, s);
+  if (bn == 64) return launch_bn<64>(a, dg, s);
+  return launch_bn<32>(a, dg, s);
 }

@@ -1,0 +1,293 @@
+// Large-tile segmented implicit-GEMM convolution (forward / data-gradient) for gfx950.
+//
+// Same contract and math as conv_igemm.hip (see there; FCOS/fcos.py:6-110 Conv2D forward and
+// backward-input), specialised for the launches that carry most of the step's FLOPs: the shared
+// FCOS towers over all five FPN levels (M = 87,296 rows at bs 16, N = 256, K = 2,304), the FPN
+// output convs and the wide ResNet stages — many M tiles, Npad % BN == 0, Cin % 64 == 0.
+//
+// Tile 256 x BN (128 or 64) x 64, 8 waves as 4 (M) x 2 (N), each a 64 x BN/2 block of
+// v_mfma_f32_16x16x32_bf16 accumulators.  Both operands move global -> LDS by LDS-DMA
+// (global_load_lds_dwordx4, 1 KiB lane-linear per wave-instruction; the XOR swizzle that keeps the
+// ds_read_b128 fragment reads conflict-free is applied to the per-lane SOURCE address) through a
+// 3-deep ring: tile k+2 is in flight while tile k is multiplied, the wait is a counted vmcnt (never
+// 0 in steady state) and the barrier a raw s_barrier, so the DMA stays outstanding across it.
+// Padding taps and rows past a segment's end read a 16-byte zero block.
+#include "conv_common.h"
+
+namespace {
+
+constexpr int BM = 256;
+constexpr int BK = 64;
+constexpr int NT = 512;
+constexpr int NST = 3;
+
+__device__ __attribute__((aligned(16))) cvl_bf16 g_zero_l[8];
+
+__device__ __forceinline__ int swz(int r) { return (r >> 1) & 7; }
+
+__device__ __forceinline__ void glds16(const void* g, void* l) {
+  __builtin_amdgcn_global_load_lds((const void __attribute__((address_space(1)))*)g,
+                                   (void __attribute__((address_space(3)))*)l, 16, 0, 0);
+}
+
+// s_waitcnt with only vmcnt constrained (gfx9 encoding: vmcnt[3:0] + vmcnt[5:4] at [15:14],
+// expcnt [6:4] and lgkmcnt [11:8] left at their maxima)
+template <int N>
+__device__ __forceinline__ void wait_vm() {
+  __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | (7 << 4) | (15 << 8));
+}
+
+template <int BN, bool DGRAD>
+__global__ void __launch_bounds__(NT) conv_igemm_l_kernel(ConvArgs a) {
+  constexpr int WM = BM / 4, WN = BN / 2;
+  constexpr int TM = WM / 16, TN = WN / 16;
+  constexpr int AP = BM * BK / (NT * 8);        // A pieces (16 B) per thread per K step: 4
+  constexpr int BP = BN * BK / (NT * 8);        // B pieces per thread: 2 (BN 128) or 1 (BN 64)
+  constexpr int GPW = AP + BP;                   // LDS-DMA instructions per wave per K step
+  constexpr int STAGE = (BM + BN) * BK;          // bf16 elements per ring slot
+  constexpr int LDS_C = BM * (BN + 8);
+  constexpr int LDS_EL = NST * STAGE > LDS_C ? NST * STAGE : LDS_C;
+  __shared__ __attribute__((aligned(16))) cvl_bf16 lds[LDS_EL];
+
+  const int tid = threadIdx.x;
+  const int wave = tid >> 6, lane = tid & 63;
+  const int m_tile = blockIdx.x, n_tile = blockIdx.y;
+  const int m0 = m_tile * BM, n0 = n_tile * BN;
+  int sg = 0;
+#pragma unroll
+  for (int i = 1; i < kMaxSeg; ++i)
+    if (i < a.nseg && m0 >= a.seg[i].m_start) sg = i;
+  const ConvSeg& S = a.seg[sg];
+  const int HWr = S.Hr * S.Wr;
+  const int mloc0 = m0 - S.m_start;
+  if (mloc0 >= S.rows) return;
+
+  // piece p of this thread: row p*64 + wave*8 + lane/8, chunk lane%8 (lane-linear 1 KiB image)
+  const int prow = wave * 8 + (lane >> 3), ch = lane & 7;
+  int a_img[AP], a_y[AP], a_x[AP];
+  bool a_ok[AP];
+#pragma unroll
+  for (int p = 0; p < AP; ++p) {
+    const int ml = mloc0 + p * 64 + prow;
+    a_ok[p] = ml < S.rows;
+    const int img = ml / HWr, q = ml - img * HWr;
+    const int oy = q / S.Wr, ox = q - (q / S.Wr) * S.Wr;
+    a_img[p] = img;
+    if (DGRAD) { a_y[p] = oy + a.pad_t; a_x[p] = ox + a.pad_l; }
+    else { a_y[p] = oy * a.stride - a.pad_t; a_x[p] = ox * a.stride - a.pad_l; }
+  }
+  const cvl_bf16* __restrict__ wsrc = S.w;
+  const int Cin = a.Cin, KW = a.KW, Kdim = a.K, stride = a.stride;
+  const int Hs = S.Hs, Ws = S.Ws;
+  // per-piece source row pointers at tap (0, 0) (64-bit math once, 32-bit offsets in the loop)
+  const cvl_bf16* a_base[AP];
+#pragma unroll
+  for (int p = 0; p < AP; ++p)
+    a_base[p] = a.src + (S.src_base + (long)a_img[p] * S.src_img) * Cin + ((ch ^ swz(p * 64 + prow)) * 8);
+  const cvl_bf16* b_base[BP];
+#pragma unroll
+  for (int p = 0; p < BP; ++p) {
+    const int row = p * 64 + prow;
+    b_base[p] = wsrc + (long)(n0 + row) * Kdim + ((ch ^ swz(row)) * 8);
+  }
+
+  auto issue = [&](int kt, int slot) {
+    cvl_bf16* Ab = lds + slot * STAGE;
+    cvl_bf16* Bb = Ab + BM * BK;
+    const int k0 = kt * BK;
+    const int tap = k0 / Cin;
+    const int cb = k0 - tap * Cin;
+    const int r = tap / KW, s = tap - (tap / KW) * KW;
+#pragma unroll
+    for (int p = 0; p < AP; ++p) {
+      int iy, ix;
+      bool ok = a_ok[p];
+      if (DGRAD) {
+        const int ty = a_y[p] - r, tx = a_x[p] - s;
+        if (stride == 1) {
+          iy = ty; ix = tx;
+        } else {
+          ok = ok && ty >= 0 && tx >= 0 && (ty % stride) == 0 && (tx % stride) == 0;
+          iy = ty / stride; ix = tx / stride;
+        }
+      } else {
+        iy = a_y[p] + r; ix = a_x[p] + s;
+      }
+      ok = ok && iy >= 0 && ix >= 0 && iy < Hs && ix < Ws;
+      const int off = (iy * Ws + ix) * Cin + cb;
+      const cvl_bf16* g = ok ? a_base[p] + off : g_zero_l;
+      glds16(g, Ab + (p * 64 + wave * 8) * BK);
+    }
+#pragma unroll
+    for (int p = 0; p < BP; ++p) glds16(b_base[p] + k0, Bb + (p * 64 + wave * 8) * BK);
+  };
+
+  const int wm = wave >> 1, wn = wave & 1;
+  const int lr = lane & 15, lg = lane >> 4;
+  f32x4 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int nk = a.K / BK;
+  issue(0, 0);
+  if (nk > 1) issue(1, 1);
+  int slot = 0;
+  for (int kt = 0; kt < nk; ++kt) {
+    // tile kt landed (this wave's DMA), tile kt+1 may stay in flight; then every wave's
+    if (kt + 1 < nk) wait_vm<GPW>();
+    else wait_vm<0>();
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    if (kt + 2 < nk) issue(kt + 2, slot == 0 ? 2 : slot - 1);   // the slot read in step kt-1
+    const cvl_bf16* Ac = lds + slot * STAGE;
+    const cvl_bf16* Bc = Ac + BM * BK;
+#pragma unroll
+    for (int ks = 0; ks < BK / 32; ++ks) {
+      const int chunk = ks * 4 + lg;
+      s16x8 fa[TM], fb[TN];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const int r = wm * WM + i * 16 + lr;
+        fa[i] = *reinterpret_cast<const s16x8*>(Ac + r * BK + ((chunk ^ swz(r)) * 8));
+      }
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int r = wn * WN + j * 16 + lr;
+        fb[j] = *reinterpret_cast<const s16x8*>(Bc + r * BK + ((chunk ^ swz(r)) * 8));
+      }
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+              __builtin_bit_cast(bf16x8, fa[i]), __builtin_bit_cast(bf16x8, fb[j]), acc[i][j], 0, 0, 0);
+    }
+    asm volatile("" ::: "memory");
+    slot = slot == NST - 1 ? 0 : slot + 1;
+  }
+
+  // ---- epilogue: +bias, ReLU, bf16 rounding, BN statistics, beta*old, 16-byte stores ----------
+  float bcol[TN];
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    const int n = n0 + wn * WN + j * 16 + lr;
+    bcol[j] = (S.bias && n < a.n_store) ? S.bias[n] : 0.f;
+  }
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        float v = acc[i][j][e] + bcol[j];
+        if (a.relu_out) v = v > 0.f ? v : 0.f;
+        acc[i][j][e] = bf16_to_f32(f32_to_bf16(v));
+      }
+
+  if (a.stats && HWr % BM == 0) {   // one image per tile: reduce the wave's rows first
+    const int img = mloc0 / HWr;
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) { const float v = acc[i][j][e]; s1 += v; s2 += v * v; }
+      s1 += __shfl_xor(s1, 16, 64); s1 += __shfl_xor(s1, 32, 64);
+      s2 += __shfl_xor(s2, 16, 64); s2 += __shfl_xor(s2, 32, 64);
+      const int n = n0 + wn * WN + j * 16 + lr;
+      if (lg == 0 && n < a.n_store) {
+        double* st = a.stats + ((long)img * a.n_store + n) * 2;
+        atomicAdd(st, (double)s1);
+        atomicAdd(st + 1, (double)s2);
+      }
+    }
+  } else if (a.stats) {
+    // the 4 rows of an accumulator quad share one image (host: H*W % 4 == 0)
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      const int ml0 = mloc0 + wm * WM + i * 16 + lg * 4;
+      if (ml0 >= S.rows) continue;
+      const int img = ml0 / HWr;
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int n = n0 + wn * WN + j * 16 + lr;
+        if (n >= a.n_store) continue;
+        float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) { const float v = acc[i][j][e]; s1 += v; s2 += v * v; }
+        double* st = a.stats + ((long)img * a.n_store + n) * 2;
+        atomicAdd(st, (double)s1);
+        atomicAdd(st + 1, (double)s2);
+      }
+    }
+  }
+
+  wait_vm<0>();
+  __syncthreads();
+  constexpr int CP = BN + 8;
+  cvl_bf16* Cs = lds;
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int r = wm * WM + i * 16 + lg * 4 + e;
+        const int c = wn * WN + j * 16 + lr;
+        Cs[r * CP + c] = f32_to_bf16(acc[i][j][e]);
+      }
+  __syncthreads();
+  constexpr int CCH = BN / 8;
+  cvl_bf16* dst = reinterpret_cast<cvl_bf16*>(a.dst);
+  for (int idx = tid; idx < BM * CCH; idx += NT) {
+    const int r = idx / CCH, c8 = (idx - (idx / CCH) * CCH) * 8;
+    const int ml = mloc0 + r;
+    if (ml >= S.rows || n0 + c8 >= a.n_store) continue;
+    const int img = ml / HWr, q = ml - img * HWr;
+    const long drow = S.dst_base + (long)img * S.dst_img + q;
+    s16x8 v = *reinterpret_cast<const s16x8*>(Cs + r * CP + c8);
+    s16x8* pd = reinterpret_cast<s16x8*>(dst + drow * a.ld_dst + a.dst_coff + n0 + c8);
+    if (a.beta != 0.f) {
+      const s16x8 o = *pd;
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+        v[u] = (short)f32_to_bf16(bf16_to_f32((cvl_bf16)v[u]) + a.beta * bf16_to_f32((cvl_bf16)o[u]));
+    }
+    *pd = v;
+  }
+}
+
+}  // namespace
+
+// Called by cvl_conv_igemm when the launch qualifies (see cvl_conv_igemm_l_ok); returns -1 when
+// it does not, so the caller falls back to the 128-row kernel.
+int cvl_conv_igemm_l(const cvl_conv_desc* d, const void* src, void* dst, double* bn_stats, hipStream_t s) {
+  if (cvl_env_flag("CVL_CONV_NO_L")) return -1;
+  if (d->Cin % 64 != 0 || d->relu_in || d->dst_f32 || d->n_store % 8 || d->ld_dst % 8 || d->dst_coff % 8)
+    return -1;
+  const int bn = d->Npad % 128 == 0 ? 128 : (d->Npad % 64 == 0 ? 64 : 0);
+  if (!bn) return -1;
+  ConvArgs a;
+  if (cvl_conv_prepare(d, BM, &a)) return -1;
+  // too few tiles to fill 256 CUs at one 8-wave workgroup each (tests lower the bar)
+  if ((long)a.m_tiles * (a.Npad / bn) < cvl_env_int("CVL_CONV_L_MIN_TILES", 384)) return -1;
+  if (bn_stats)
+    for (int i = 0; i < a.nseg; ++i)
+      if ((a.seg[i].Hr * a.seg[i].Wr) % 4) return -1;
+  a.src = reinterpret_cast<const cvl_bf16*>(src);
+  a.dst = dst;
+  a.stats = bn_stats;
+  dim3 grid(a.m_tiles, a.Npad / bn);
+  const bool dg = d->mode == CVL_CONV_DGRAD;
+  if (bn == 128) {
+    if (dg) hipLaunchKernelGGL((conv_igemm_l_kernel<128, true>), grid, dim3(NT), 0, s, a);
+    else hipLaunchKernelGGL((conv_igemm_l_kernel<128, false>), grid, dim3(NT), 0, s, a);
+  } else {
+    if (dg) hipLaunchKernelGGL((conv_igemm_l_kernel<64, true>), grid, dim3(NT), 0, s, a);
+    else hipLaunchKernelGGL((conv_igemm_l_kernel<64, false>), grid, dim3(NT), 0, s, a);
+  }
+  return cvl_launch_status();
+}

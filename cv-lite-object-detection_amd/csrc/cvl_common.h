@@ -3,6 +3,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #include "../../include/cvlite.h"
 
@@ -14,6 +15,17 @@
 static inline int cvl_launch_status() {
   hipError_t e = hipGetLastError();
   return e == hipSuccess ? CVL_OK : (CVL_EHIP + (int)e);
+}
+
+// Kernel-variant switches for A/B measurement (e.g. CVL_CONV_GLDS=1); read per launch.
+static inline bool cvl_env_flag(const char* name) {
+  const char* v = getenv(name);
+  return v && v[0] && v[0] != '0';
+}
+
+static inline int cvl_env_int(const char* name, int dflt) {
+  const char* v = getenv(name);
+  return (v && v[0]) ? atoi(v) : dflt;
 }
 
 // ---- bf16 helpers (bit-level; round-to-nearest-even, NaN-preserving) ------------------------

@@ -128,13 +128,20 @@ __global__ void bn_apply_kernel(const cvl_bf16* z, const float* mr, const float*
 }
 
 // BN backward over one (image, row-chunk) block; threads own 8 channels (tpr threads per row,
-// rpp rows per pass).  PASS 0: sums[b][c] += (sum g, sum g*xhat), g = dy * (y > 0 if relu).
-// PASS 1: dz = gamma*rstd*(g - mean(g) - xhat*mean(g*xhat)) (+ g_out = g), and the conv-bias
-// gradient sum_rows dz accumulated per channel (fused column sum).
+// rpp rows per pass), rows taken UNR at a time with all loads issued before any use (the loop is
+// latency-bound otherwise).  No atomics: each block writes its per-channel partial sums to
+// part[b][chunk][C][2]; small follow-up kernels reduce them in a fixed order (deterministic).
+// PASS 0: (sum g, sum g*xhat), g = dy * (y > 0 if relu).
+// PASS 1: dz = gamma*rstd*(g - mean(g) - xhat*mean(g*xhat)) (+ g_out = g), and sum dz (the
+// preceding conv's bias gradient, fused column sum of the stored bf16 dz).
+constexpr int BN_UNR = 4;
+
 template <int PASS>
-__global__ void bn_bwd_kernel(const cvl_bf16* dy, const cvl_bf16* y, const cvl_bf16* z, const float* mr,
-                              const float* gamma, double* sums, cvl_bf16* dz, cvl_bf16* g_out,
-                              double* dbias_acc, int C, int HW, int rows_per_blk) {
+__global__ void __launch_bounds__(NT) bn_bwd_kernel(const cvl_bf16* __restrict__ dy, const cvl_bf16* __restrict__ y,
+                                                    const cvl_bf16* __restrict__ z, const float* __restrict__ mr,
+                                                    const float* __restrict__ gamma, const double* __restrict__ sums,
+                                                    cvl_bf16* __restrict__ dz, cvl_bf16* __restrict__ g_out,
+                                                    float* __restrict__ part, int C, int HW, int rows_per_blk) {
   const int b = blockIdx.y;
   const int C8 = C / 8;
   const int tpr = C8 < NT ? C8 : NT;
@@ -160,69 +167,130 @@ __global__ void bn_bwd_kernel(const cvl_bf16* dy, const cvl_bf16* y, const cvl_b
       }
     }
     if (rsub < rpp) {
-      for (int r = r0 + rsub; r < r1; r += rpp) {
-        const long off = ((long)b * HW + r) * C + c0;
-        float g[8], zz[8];
-        unpack8(*reinterpret_cast<const s16x8*>(dy + off), g);
-        unpack8(*reinterpret_cast<const s16x8*>(z + off), zz);
-        if (y) {
-          float yy[8];
-          unpack8(*reinterpret_cast<const s16x8*>(y + off), yy);
+      for (int r = r0 + rsub; r < r1; r += rpp * BN_UNR) {
+        s16x8 vg[BN_UNR], vz[BN_UNR], vy[BN_UNR];
+        long off[BN_UNR];
 #pragma unroll
-          for (int u = 0; u < 8; ++u) g[u] = yy[u] > 0.f ? g[u] : 0.f;
+        for (int q = 0; q < BN_UNR; ++q) {
+          const int rq = min(r + q * rpp, r1 - 1);       // clamped: loads stay unconditional
+          off[q] = ((long)b * HW + rq) * C + c0;
+          vg[q] = *reinterpret_cast<const s16x8*>(dy + off[q]);
+          vz[q] = *reinterpret_cast<const s16x8*>(z + off[q]);
+          if (y) vy[q] = *reinterpret_cast<const s16x8*>(y + off[q]);
         }
-        if (PASS == 0) {
 #pragma unroll
-          for (int u = 0; u < 8; ++u) {
-            s1[u] += g[u];
-            s2[u] += g[u] * ((zz[u] - m[u]) * rs[u]);
+        for (int q = 0; q < BN_UNR; ++q) {
+          const bool ok = r + q * rpp < r1;
+          float g[8], zz[8];
+          unpack8(vg[q], g);
+          unpack8(vz[q], zz);
+          if (y) {
+            float yy[8];
+            unpack8(vy[q], yy);
+#pragma unroll
+            for (int u = 0; u < 8; ++u) g[u] = yy[u] > 0.f ? g[u] : 0.f;
           }
-        } else {
-          if (g_out) *reinterpret_cast<s16x8*>(g_out + off) = pack8(g);
-          float o[8];
+          if (PASS == 0) {
+            if (ok) {
 #pragma unroll
-          for (int u = 0; u < 8; ++u) {
-            const float xh = (zz[u] - m[u]) * rs[u];
-            o[u] = gm[u] * (g[u] - k1[u] - xh * k2[u]);
+              for (int u = 0; u < 8; ++u) {
+                s1[u] += g[u];
+                s2[u] += g[u] * ((zz[u] - m[u]) * rs[u]);
+              }
+            }
+          } else if (ok) {
+            if (g_out) *reinterpret_cast<s16x8*>(g_out + off[q]) = pack8(g);
+            float o[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+              const float xh = (zz[u] - m[u]) * rs[u];
+              o[u] = gm[u] * (g[u] - k1[u] - xh * k2[u]);
+            }
+            const s16x8 ov = pack8(o);
+            *reinterpret_cast<s16x8*>(dz + off[q]) = ov;
+            float orr[8];
+            unpack8(ov, orr);                       // the bias gradient sums the stored bf16 dz
+#pragma unroll
+            for (int u = 0; u < 8; ++u) s1[u] += orr[u];
           }
-          const s16x8 ov = pack8(o);
-          *reinterpret_cast<s16x8*>(dz + off) = ov;
-          float orr[8];
-          unpack8(ov, orr);                       // the bias gradient sums the stored bf16 dz
-#pragma unroll
-          for (int u = 0; u < 8; ++u) s1[u] += orr[u];
         }
       }
     }
+    if (PASS == 1 && !part) continue;                // uniform: no bias gradient wanted
     __syncthreads();
 #pragma unroll
     for (int u = 0; u < 8; ++u) { red[threadIdx.x][u] = s1[u]; red[threadIdx.x][8 + u] = s2[u]; }
     __syncthreads();
     if (rsub == 0) {
+      float* pp = part + (((long)b * gridDim.x + blockIdx.x) * C + c0) * 2;
       for (int u = 0; u < 8; ++u) {
-        double a1 = 0.0, a2 = 0.0;
+        float a1 = 0.f, a2 = 0.f;
         for (int k = 0; k < rpp; ++k) { a1 += red[k * tpr + cg][u]; a2 += red[k * tpr + cg][8 + u]; }
-        if (PASS == 0) {
-          atomicAdd(&sums[((long)b * C + c0 + u) * 2], a1);
-          atomicAdd(&sums[((long)b * C + c0 + u) * 2 + 1], a2);
-        } else if (dbias_acc) {
-          atomicAdd(&dbias_acc[c0 + u], a1);
-        }
+        pp[2 * u] = a1;
+        pp[2 * u + 1] = a2;
       }
     }
   }
 }
 
-// dgamma[c] = beta_acc*dgamma + sum_b sum g*xhat ; dbeta[c] = ... + sum_b sum g
+// out[y][c][0..1] = sum_r part[y][r][c][0..1]: a block owns 32 channels (256 contiguous bytes per
+// row) and 8 row groups; the row groups are combined in a fixed order (deterministic, float64)
+__global__ void __launch_bounds__(NT) bn_colsum_kernel(const float* __restrict__ part, int R, int C,
+                                                       double* __restrict__ out) {
+  const int y = blockIdx.y;
+  const int cl = threadIdx.x & 31, rg = threadIdx.x >> 5;
+  const int c = blockIdx.x * 32 + cl;
+  __shared__ double red[8][32][2];
+  double a1 = 0.0, a2 = 0.0;
+  if (c < C) {
+    const float2* p = reinterpret_cast<const float2*>(part) + (long)y * R * C + c;
+    int r = rg;
+    for (; r + 24 < R; r += 32) {           // 4 independent loads in flight per thread
+      const float2 v0 = p[(long)r * C], v1 = p[(long)(r + 8) * C];
+      const float2 v2 = p[(long)(r + 16) * C], v3 = p[(long)(r + 24) * C];
+      a1 += ((double)v0.x + v1.x) + ((double)v2.x + v3.x);
+      a2 += ((double)v0.y + v1.y) + ((double)v2.y + v3.y);
+    }
+    for (; r < R; r += 8) {
+      const float2 v = p[(long)r * C];
+      a1 += v.x;
+      a2 += v.y;
+    }
+  }
+  red[rg][cl][0] = a1;
+  red[rg][cl][1] = a2;
+  __syncthreads();
+  if (rg == 0 && c < C) {
+    double t1 = 0.0, t2 = 0.0;
+    for (int k = 0; k < 8; ++k) { t1 += red[k][cl][0]; t2 += red[k][cl][1]; }
+    out[((long)y * C + c) * 2] = t1;
+    out[((long)y * C + c) * 2 + 1] = t2;
+  }
+}
+
+// dgamma[c] = beta_acc*dgamma + sum_b sum g*xhat ; dbeta[c] = ... + sum_b sum g ;
+// conv_dbias[c] = the reduced sum of dz
 __global__ void bn_param_grad_kernel(const double* sums, float* dgamma, float* dbeta, int B, int C,
-                                     float beta_acc, const double* dbias_acc, float* conv_dbias) {
+                                     float beta_acc, const double* dbias_sum, float* conv_dbias) {
   const int c = blockIdx.x * NT + threadIdx.x;
   if (c >= C) return;
-  if (conv_dbias) conv_dbias[c] = (float)dbias_acc[c];
+  if (conv_dbias) conv_dbias[c] = (float)dbias_sum[(long)c * 2];
   double a1 = 0.0, a2 = 0.0;
   for (int b = 0; b < B; ++b) { a1 += sums[((long)b * C + c) * 2]; a2 += sums[((long)b * C + c) * 2 + 1]; }
   dbeta[c] = (float)a1 + (beta_acc != 0.f ? beta_acc * dbeta[c] : 0.f);
   dgamma[c] = (float)a2 + (beta_acc != 0.f ? beta_acc * dgamma[c] : 0.f);
+}
+
+// row chunking shared by the launcher and the workspace query: 512..2048 blocks over the batch,
+// >= 16 rows per thread where the maps allow (fewer partials for the column reduction)
+inline int bn_bwd_rows_per_blk(int B, int HW, int C) {
+  const int C8 = C / 8, rpp = NT / (C8 < NT ? C8 : NT);
+  long want = (long)B * HW * (C8 < NT ? C8 : NT) / (NT * 16);
+  want = want < 512 ? 512 : (want > 2048 ? 2048 : want);
+  const int chunks = (int)((want + B - 1) / B);
+  int rpb = (HW + chunks - 1) / chunks;
+  rpb = ((rpb + rpp - 1) / rpp) * rpp;
+  return rpb;
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -494,29 +562,42 @@ extern "C" int cvl_bn_apply(const void* z, const float* mean_rstd, const float* 
   return cvl_launch_status();
 }
 
+extern "C" size_t cvl_bn_backward_workspace_size(int B, int HW, int C) {
+  if (B <= 0 || HW <= 0 || C <= 0) return 0;
+  const int rpb = bn_bwd_rows_per_blk(B, HW, C);
+  const int nchunk = (HW + rpb - 1) / rpb;
+  return sizeof(double) * 2 * ((size_t)B * C + C) + sizeof(float) * 2 * 2 * (size_t)B * nchunk * C;
+}
+
 extern "C" int cvl_bn_backward(const void* dy, const void* y_relu, const void* z, const float* mean_rstd,
-                               const float* gamma, double* sums_ws, void* dz, void* g_out, float* dgamma,
-                               float* dbeta, float beta_acc, float* conv_dbias, int B, int HW, int C,
-                               cvl_stream_t stream) {
-  CVL_CHECK_ARG(dy && z && mean_rstd && gamma && sums_ws && dz && dgamma && dbeta && C % 8 == 0);
-  // workspace: [B][C][2] sums followed by [C] conv-bias accumulators (float64)
-  hipError_t e = hipMemsetAsync(sums_ws, 0, sizeof(double) * (2 * (size_t)B * C + C), S_);
-  if (e != hipSuccess) return CVL_EHIP + (int)e;
-  double* dbias_acc = sums_ws + 2 * (size_t)B * C;
-  // ~512 workgroups whatever the layer shape (conv5 maps are only 16x16 per image)
-  const int C8 = C / 8, rpp = NT / (C8 < NT ? C8 : NT);
-  const int chunks = (512 + B - 1) / B;
-  int rows_per_blk = (HW + chunks - 1) / chunks;
-  rows_per_blk = ((rows_per_blk + rpp - 1) / rpp) * rpp;
-  dim3 g1((HW + rows_per_blk - 1) / rows_per_blk, B);
+                               const float* gamma, void* workspace, size_t workspace_bytes, void* dz, void* g_out,
+                               float* dgamma, float* dbeta, float beta_acc, float* conv_dbias, int B, int HW,
+                               int C, cvl_stream_t stream) {
+  CVL_CHECK_ARG(dy && z && mean_rstd && gamma && workspace && dz && dgamma && dbeta && C % 8 == 0);
+  CVL_CHECK_ARG(B > 0 && HW > 0 && (C / 8 <= NT || (C / 8) % NT == 0));
+  CVL_CHECK_ARG(workspace_bytes >= cvl_bn_backward_workspace_size(B, HW, C));
+  const int rpb = bn_bwd_rows_per_blk(B, HW, C);
+  const int nchunk = (HW + rpb - 1) / rpb;
+  // workspace: sums [B][C][2] f64 | dbias sums [C][2] f64 | pass-0 partials [B][nchunk][C][2] f32 |
+  // pass-1 partials (same)
+  double* sums = reinterpret_cast<double*>(workspace);
+  double* dbsum = sums + 2 * (size_t)B * C;
+  float* part0 = reinterpret_cast<float*>(dbsum + 2 * (size_t)C);
+  float* part1 = part0 + 2 * (size_t)B * nchunk * C;
+  dim3 g1(nchunk, B);
   hipLaunchKernelGGL(bn_bwd_kernel<0>, g1, dim3(NT), 0, S_, (const cvl_bf16*)dy, (const cvl_bf16*)y_relu,
-                     (const cvl_bf16*)z, mean_rstd, gamma, sums_ws, (cvl_bf16*)nullptr, (cvl_bf16*)nullptr,
-                     (double*)nullptr, C, HW, rows_per_blk);
+                     (const cvl_bf16*)z, mean_rstd, gamma, (const double*)nullptr, (cvl_bf16*)nullptr,
+                     (cvl_bf16*)nullptr, part0, C, HW, rpb);
+  hipLaunchKernelGGL(bn_colsum_kernel, dim3((C + 31) / 32, B), dim3(NT), 0, S_, (const float*)part0, nchunk, C,
+                     sums);
   hipLaunchKernelGGL(bn_bwd_kernel<1>, g1, dim3(NT), 0, S_, (const cvl_bf16*)dy, (const cvl_bf16*)y_relu,
-                     (const cvl_bf16*)z, mean_rstd, gamma, sums_ws, (cvl_bf16*)dz, (cvl_bf16*)g_out,
-                     conv_dbias ? dbias_acc : (double*)nullptr, C, HW, rows_per_blk);
-  hipLaunchKernelGGL(bn_param_grad_kernel, dim3((C + NT - 1) / NT), dim3(NT), 0, S_, (const double*)sums_ws,
-                     dgamma, dbeta, B, C, beta_acc, (const double*)dbias_acc, conv_dbias);
+                     (const cvl_bf16*)z, mean_rstd, gamma, (const double*)sums, (cvl_bf16*)dz, (cvl_bf16*)g_out,
+                     conv_dbias ? part1 : (float*)nullptr, C, HW, rpb);
+  if (conv_dbias)
+    hipLaunchKernelGGL(bn_colsum_kernel, dim3((C + 31) / 32, 1), dim3(NT), 0, S_, (const float*)part1,
+                       B * nchunk, C, dbsum);
+  hipLaunchKernelGGL(bn_param_grad_kernel, dim3((C + NT - 1) / NT), dim3(NT), 0, S_, (const double*)sums,
+                     dgamma, dbeta, B, C, beta_acc, (const double*)dbsum, conv_dbias);
   return cvl_launch_status();
 }
 

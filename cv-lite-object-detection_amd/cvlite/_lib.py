@@ -24,7 +24,8 @@ SIGNATURES = {
     "cvl_fcos_loss": (c_int, [P, c_int, P, c_int, P, c_int, c_int, c_int, c_int, c_float, P,
                               P, c_int, c_int, P, c_int, c_int, P, P]),
     "cvl_fcos_decode": (c_int, [P, c_int, c_int, c_int, ctypes.c_double, P, P]),
-    "cvl_conv_igemm": (c_int, [P, P, P, P, P]),
+    "cvl_conv_igemm_workspace_size": (c_size_t, [P]),
+    "cvl_conv_igemm": (c_int, [P, P, P, P, P, c_size_t, P]),
     "cvl_conv_wgrad_workspace_size": (c_size_t, [P]),
     "cvl_conv_wgrad": (c_int, [P, P, P, P, c_float, P, c_size_t, P]),
     "cvl_pack_conv_weights": (c_int, [P, c_int, c_int, c_int, c_int, c_int, c_int, P, c_int, c_int, P, P]),
@@ -32,7 +33,8 @@ SIGNATURES = {
                            c_int, c_int, P, P]),
     "cvl_bn_finalize": (c_int, [P, P, P, P, c_int, c_int, c_int, c_float, c_float, P]),
     "cvl_bn_apply": (c_int, [P, P, P, P, P, P, c_int, c_int, c_int, c_int, P]),
-    "cvl_bn_backward": (c_int, [P, P, P, P, P, P, P, P, P, P, c_float, P, c_int, c_int, c_int, P]),
+    "cvl_bn_backward_workspace_size": (c_size_t, [c_int, c_int, c_int]),
+    "cvl_bn_backward": (c_int, [P, P, P, P, P, P, c_size_t, P, P, P, P, c_float, P, c_int, c_int, c_int, P]),
     "cvl_maxpool3x3s2": (c_int, [P, P, P, c_int, c_int, c_int, c_int, P]),
     "cvl_maxpool3x3s2_backward": (c_int, [P, P, P, c_int, c_int, c_int, c_int, P]),
     "cvl_upsample2x_add": (c_int, [P, P, P, c_int, c_int, c_int, c_int, P]),

@@ -53,7 +53,10 @@ def make_desc(mode, B, Cin, KH, KW, stride, pad_t, pad_l, Npad, n_store, ld_dst,
 
 
 def conv_igemm(desc, src, dst, stats=None):
-    _lib.call("cvl_conv_igemm", ctypes.byref(desc), ptr(src), ptr(dst), ptr(stats), stream())
+    n = int(_lib.load().cvl_conv_igemm_workspace_size(ctypes.byref(desc)))
+    ws = torch.empty(n, dtype=torch.uint8, device=src.device) if n > 16 else None
+    _lib.call("cvl_conv_igemm", ctypes.byref(desc), ptr(src), ptr(dst), ptr(stats), ptr(ws),
+              n if ws is not None else 0, stream())
 
 
 def conv_wgrad(desc, x, dy, dw, beta=0.0):
@@ -86,8 +89,9 @@ def bn_apply(z, mean_rstd, gamma, beta, residual, y, B, HW, C, relu):
 
 def bn_backward(dy, y_relu, z, mean_rstd, gamma, dz, g_out, dgamma, dbeta, B, HW, C, beta_acc=0.0,
                 conv_dbias=None):
-    ws = torch.empty(2 * B * C + C, dtype=torch.float64, device=dy.device)
-    _lib.call("cvl_bn_backward", ptr(dy), ptr(y_relu), ptr(z), ptr(mean_rstd), ptr(gamma), ptr(ws),
+    n = int(_lib.load().cvl_bn_backward_workspace_size(B, HW, C))
+    ws = torch.empty(n, dtype=torch.uint8, device=dy.device)
+    _lib.call("cvl_bn_backward", ptr(dy), ptr(y_relu), ptr(z), ptr(mean_rstd), ptr(gamma), ptr(ws), n,
               ptr(dz), ptr(g_out), ptr(dgamma), ptr(dbeta), float(beta_acc), ptr(conv_dbias), B, HW, C,
               stream())
 

@@ -112,8 +112,11 @@ typedef struct {
   cvl_conv_seg seg[CVL_CONV_MAX_SEG];
 } cvl_conv_desc;
 
+/* workspace (optional, >= cvl_conv_igemm_workspace_size(d) bytes) enables split-K for grids too
+ * small to fill the GPU (fp32 partial slabs + a finishing pass); NULL = no split. */
+size_t cvl_conv_igemm_workspace_size(const cvl_conv_desc* d);
 int cvl_conv_igemm(const cvl_conv_desc* d, const void* src, void* dst, double* bn_stats,
-                   cvl_stream_t stream);
+                   void* workspace, size_t workspace_bytes, cvl_stream_t stream);
 
 /* Weight gradient (replaces Conv2DBackpropFilter + the per-image gradient accumulation of
  * FCOS/train_fcos.py:173-176): dw[KH][KW][Cin][n_store] (HWIO fp32) = beta*dw + sum over all
@@ -144,10 +147,12 @@ int cvl_bn_apply(const void* z, const float* mean_rstd, const float* gamma, cons
 /* dy: grad of y; y_relu: y when the unit ends in ReLU (mask), else NULL; writes dz (bf16),
  * optionally g_out = masked dy (the residual branch's gradient), dgamma/dbeta (= + beta_acc*old)
  * and, if conv_dbias != NULL, the gradient of the preceding conv's bias (= column sum of dz,
- * fused).  sums_ws: float64 workspace of 2*B*C + C elements. */
+ * fused).  workspace >= cvl_bn_backward_workspace_size(B, HW, C) bytes; reductions are
+ * deterministic (per-block partials summed in a fixed order, no atomics). */
+size_t cvl_bn_backward_workspace_size(int B, int HW, int C);
 int cvl_bn_backward(const void* dy, const void* y_relu, const void* z, const float* mean_rstd,
-                    const float* gamma, double* sums_ws, void* dz, void* g_out, float* dgamma,
-                    float* dbeta, float beta_acc, float* conv_dbias, int B, int HW, int C,
+                    const float* gamma, void* workspace, size_t workspace_bytes, void* dz, void* g_out,
+                    float* dgamma, float* dbeta, float beta_acc, float* conv_dbias, int B, int HW, int C,
                     cvl_stream_t stream);
 
 /* ResNet50 pool1: ZeroPadding2D(1) + MaxPooling2D(3, 2); argmax [B][Ho][Wo][C] uint8 (0..8). */

@@ -29,6 +29,17 @@ def ref_conv(x, w, b, stride, pad):
     return y.permute(0, 2, 3, 1)
 
 
+@pytest.fixture(params=["base", "l"])
+def kern(request, monkeypatch):
+    """Run a test through the 128-row register-staged kernel ("base") and through the 256-row
+    LDS-DMA kernel ("l", normally taken only by launches with >= 384 tiles)."""
+    if request.param == "l":
+        monkeypatch.setenv("CVL_CONV_L_MIN_TILES", "1")
+    else:
+        monkeypatch.setenv("CVL_CONV_NO_L", "1")
+    return request.param
+
+
 def rnd(*shape, scale=1.0, gen=None):
     return (torch.randn(*shape, generator=gen, dtype=torch.float64) * scale).to(BF).to(torch.float64)
 
@@ -58,7 +69,7 @@ CASES = [  # (B, H, W, Cin, Cout, k, stride, pad)
 
 
 @pytest.mark.parametrize("case", CASES)
-def test_conv_fwd(case):
+def test_conv_fwd(case, kern):
     from cvlite import ops_nn as nn
     B, H, W, Cin, Cout, k, s, pad = case
     g = torch.Generator().manual_seed(sum(c for c in case if isinstance(c, int)))
@@ -100,7 +111,7 @@ def test_conv_fwd(case):
 
 
 @pytest.mark.parametrize("case", CASES[:6])
-def test_conv_dgrad_wgrad(case):
+def test_conv_dgrad_wgrad(case, kern):
     from cvlite import ops_nn as nn
     B, H, W, Cin, Cout, k, s, pad = case
     g = torch.Generator().manual_seed(7 + sum(c for c in case if isinstance(c, int)))
@@ -128,7 +139,7 @@ def test_conv_dgrad_wgrad(case):
     torch.testing.assert_close(dw.double().cpu(), w.grad, rtol=1e-4, atol=1e-5 * scale)
 
 
-def test_conv_segments_packed_levels():
+def test_conv_segments_packed_levels(kern):
     """Five level maps in one packed level-major buffer through one shared-weight launch, and the
     per-level-weights head form writing an image-major [B, P, ld] fp32 buffer."""
     from cvlite import ops_nn as nn
@@ -192,3 +203,46 @@ def test_conv_segments_packed_levels():
         y.backward(dres[:, off[l]:off[l] + h * ww, :Cn].reshape(B, h, ww, Cn).double().cpu())
         got = dpk[B * off[l]:B * off[l] + B * h * ww].reshape(B, h, ww, C).double().cpu()
         torch.testing.assert_close(got, xl.grad, rtol=1e-2, atol=1e-2)
+
+
+@pytest.mark.parametrize("case", [  # (B, H, W, Cin, Cout, k, stride): c6 and conv5-stage shapes
+    (16, 16, 16, 2048, 256, 3, 2),
+    (16, 16, 16, 512, 512, 3, 1),
+    (16, 16, 16, 2048, 512, 1, 1),
+])
+def test_conv_splitk_matches_unsplit(case):
+    """Small-M / large-K launches take the split-K path (fp32 partial slabs + finishing pass) when
+    a workspace is given; without one the single-pass kernel runs.  Both must agree (and with fp64)."""
+    import ctypes
+    from cvlite import _lib, ops_nn as nn
+    B, H, W, Cin, Cout, k, s = case
+    g = torch.Generator().manual_seed(Cin + Cout + k)
+    x = rnd(B, H, W, Cin, gen=g)
+    w = rnd(k, k, Cin, Cout, scale=(k * k * Cin) ** -0.5, gen=g)
+    b = torch.randn(Cout, generator=g, dtype=torch.float64)
+    ref = ref_conv(x, w, b, s, "same")
+    Ho, Wo = ref.shape[1], ref.shape[2]
+    _, pt, _ = _pads(H, k, s, "same")
+    wf, _, npad, _, _ = packs(w)
+    bias = b.float().cuda()
+    xg = x.to(BF).cuda()
+    d = nn.make_desc(nn.FWD, B, Cin, k, k, s, pt, pt, npad, Cout, Cout, [nn.seg(Ho, Wo, H, W, wf, bias)],
+                     relu_out=True)
+    assert _lib.load().cvl_conv_igemm_workspace_size(ctypes.byref(d)) > 16, "shape should split"
+    outs, stats = [], []
+    for split in (True, False):
+        out = torch.zeros((B, Ho, Wo, Cout), dtype=BF, device="cuda")
+        st = torch.zeros((B, Cout, 2), dtype=torch.float64, device="cuda")
+        if split:
+            nn.conv_igemm(d, xg, out, st)
+        else:
+            _lib.call("cvl_conv_igemm", ctypes.byref(d), nn.ptr(xg), nn.ptr(out), nn.ptr(st), None, 0,
+                      nn.stream())
+        outs.append(out.double().cpu())
+        stats.append(st.cpu())
+    torch.testing.assert_close(outs[0], ref.clamp(min=0), rtol=1e-2, atol=1e-2)
+    torch.testing.assert_close(outs[0], outs[1], rtol=1e-2, atol=1e-2)
+    torch.testing.assert_close(stats[0], stats[1], rtol=5e-3, atol=1e-1)  # bf16 ulp flips
+    o = outs[0]
+    torch.testing.assert_close(stats[0], torch.stack([o.sum((1, 2)), (o * o).sum((1, 2))], -1),
+                               rtol=1e-5, atol=1e-3)

@@ -17,7 +17,8 @@ def bfr(t):
 
 
 @pytest.mark.parametrize("B,HW,C,relu,res", [(2, 64, 64, True, False), (3, 16, 256, False, True),
-                                             (1, 256, 32, True, True)])
+                                             (1, 256, 32, True, True), (2, 1000, 64, True, False),
+                                             (1, 300, 2048, True, True), (2, 4096, 256, True, False)])
 def test_bn_forward_backward(B, HW, C, relu, res):
     from cvlite import ops_nn as nn
     g = torch.Generator().manual_seed(B * 100 + C)
