@@ -229,22 +229,38 @@ __global__ void wgrad_reduce_kernel(const float* slab, float* dw, long n, int sp
   }
 }
 
-int pick_splits(int tiles, int m_total) {
-  // ~512 workgroups (2 per CU at this kernel's occupancy), >= 1024 reduction rows each
-  int s = (512 + tiles - 1) / tiles;
-  const int max_s = m_total / 1024;
-  if (s > max_s) s = max_s;
-  return s < 1 ? 1 : s;
+int pick_splits(int tiles, int m_total, int bco) {
+  // 2 workgroups per CU at this kernel's occupancy (512 slots); modelled time = rounds x steps
+  // per workgroup (~0.8 us per 64-row step) + the fp32 slab round trip; the cheapest split wins
+  int max_s = m_total / 512;
+  if (max_s < 1) max_s = 1;
+  if (max_s > 8192 / tiles) max_s = 8192 / tiles > 1 ? 8192 / tiles : 1;
+  const double slab_us = (double)bco * BKK * 4 * 2 / 5.0e6;
+  int best = 1;
+  double best_t = 1e30;
+  for (int s = 1; s <= max_s; ++s) {
+    const int rounds = (tiles * s + 511) / 512;
+    const int steps = (m_total / s + BR - 1) / BR;
+    const double t = rounds * steps * 0.8 * bco / 128.0 + (s > 1 ? tiles * s * slab_us : 0.0);
+    if (t < best_t) { best_t = t; best = s; }
+  }
+  return best;
 }
 
 }  // namespace
 
+long cvl_conv_wgrad_l_workspace(const cvl_conv_desc* d);
+int cvl_conv_wgrad_l(const cvl_conv_desc* d, const void* x, const void* dy, float* dw, float beta,
+                     void* workspace, size_t workspace_bytes, hipStream_t s);
+
 extern "C" size_t cvl_conv_wgrad_workspace_size(const cvl_conv_desc* d) {
+  const long wl = cvl_conv_wgrad_l_workspace(d);     // the 128x256 LDS-DMA kernel takes the launch
+  if (wl >= 0) return (size_t)wl;
   ConvArgs a;
   if (cvl_conv_prepare(d, BM, &a)) return 0;
   const int bco = a.Npad % 128 == 0 ? 128 : (a.Npad % 64 == 0 ? 64 : 32);
   const int tiles = (a.Npad / bco) * ((a.K + BKK - 1) / BKK);
-  const int splits = pick_splits(tiles, a.m_total);
+  const int splits = pick_splits(tiles, a.m_total, bco);
   return splits > 1 ? (size_t)splits * a.K * a.n_store * sizeof(float) : 16;
 }
 
@@ -258,6 +274,10 @@ extern "C" int cvl_conv_wgrad(const cvl_conv_desc* d, const void* x, const void*
   CVL_CHECK_ARG(d->Cin % 8 == 0 && g.a.Npad % 32 == 0);
   CVL_CHECK_ARG(d->ld_dst % 8 == 0 && d->dst_coff % 8 == 0 && d->ld_dst >= d->dst_coff + g.a.Npad);
   for (int i = 1; i < d->nseg; ++i) CVL_CHECK_ARG(d->seg[i].w == d->seg[0].w);  // shared weights
+  {
+    const int lst = cvl_conv_wgrad_l(d, x, dy, dw, beta, workspace, workspace_bytes, (hipStream_t)stream);
+    if (lst >= 0) return lst;
+  }
   g.a.src = reinterpret_cast<const cvl_bf16*>(x);
   g.dy = reinterpret_cast<const cvl_bf16*>(dy);
   g.ld_dy = d->ld_dst;
@@ -268,7 +288,7 @@ extern "C" int cvl_conv_wgrad(const cvl_conv_desc* d, const void* x, const void*
   g.co_tiles = g.a.Npad / bco;
   g.k_tiles = (g.a.K + BKK - 1) / BKK;
   const int tiles = g.co_tiles * g.k_tiles;
-  const int splits = pick_splits(tiles, g.a.m_total);
+  const int splits = pick_splits(tiles, g.a.m_total, bco);
   int chunk = (g.a.m_total + splits - 1) / splits;
   chunk = ((chunk + BM - 1) / BM) * BM;
   const int nsplit = (g.a.m_total + chunk - 1) / chunk;

@@ -37,6 +37,7 @@ def kern(request, monkeypatch):
         monkeypatch.setenv("CVL_CONV_L_MIN_TILES", "1")
     else:
         monkeypatch.setenv("CVL_CONV_NO_L", "1")
+        monkeypatch.setenv("CVL_WGRAD_NO_L", "1")
     return request.param
 
 
@@ -246,3 +247,64 @@ def test_conv_splitk_matches_unsplit(case):
     o = outs[0]
     torch.testing.assert_close(stats[0], torch.stack([o.sum((1, 2)), (o * o).sum((1, 2))], -1),
                                rtol=1e-5, atol=1e-3)
+
+
+@pytest.mark.parametrize("case", [  # (B, H, W, Cin, Cout, k, stride): >= 1024 reduction rows
+    (4, 32, 32, 64, 128, 3, 1),       # K = 576: partial 256-wide k tile, taps straddle a tile
+    (4, 32, 32, 256, 256, 3, 2),
+    (2, 64, 64, 256, 512, 1, 2),
+    (3, 40, 24, 128, 128, 3, 1),      # rows not a multiple of the 128-row granule
+])
+def test_conv_wgrad_large(case, kern):
+    """Weight gradient at sizes that take the 128x256 LDS-DMA kernel (and, with kern == "base",
+    the 128x128 one) vs torch fp64; split-M slabs and beta accumulation."""
+    from cvlite import ops_nn as nn
+    B, H, W, Cin, Cout, k, s = case
+    g = torch.Generator().manual_seed(B + H + Cin + Cout + k)
+    x = rnd(B, H, W, Cin, gen=g)
+    w = rnd(k, k, Cin, Cout, scale=(k * k * Cin) ** -0.5, gen=g).requires_grad_(True)
+    y = ref_conv(x, w, None, s, "same")
+    dy = rnd(*y.shape, gen=g)
+    y.backward(dy)
+    Ho, Wo = y.shape[1], y.shape[2]
+    _, pt, _ = _pads(H, k, s, "same")
+    _, pl, _ = _pads(W, k, s, "same")
+    wf, _, npad, cout_pad, _ = packs(w.detach())
+    dyg = torch.zeros((B, Ho, Wo, cout_pad), dtype=BF, device="cuda")
+    dyg[..., :Cout] = dy.to(BF).cuda()
+    old = torch.randn((k, k, Cin, Cout), generator=g).float().cuda()
+    dw = old.clone()
+    d = nn.make_desc(nn.FWD, B, Cin, k, k, s, pt, pl, npad, Cout, cout_pad, [nn.seg(Ho, Wo, H, W, wf)])
+    nn.conv_wgrad(d, x.to(BF).cuda(), dyg, dw, beta=0.5)
+    exp = w.grad + 0.5 * old.double().cpu()
+    scale = w.grad.abs().max().item()
+    torch.testing.assert_close(dw.double().cpu(), exp, rtol=1e-4, atol=1e-5 * scale)
+
+
+def test_conv_wgrad_large_segments(kern):
+    """Shared-weight wgrad over five packed levels (the FCOS tower form) at a size that takes the
+    large kernel: equals the sum of the per-level weight gradients."""
+    from cvlite import ops_nn as nn
+    B, C = 4, 128
+    shapes = [(16, 16), (8, 8), (4, 4), (2, 2), (1, 1)]
+    off, o = [], 0
+    for h, w in shapes:
+        off.append(o)
+        o += h * w
+    P = o
+    g = torch.Generator().manual_seed(5)
+    maps = [rnd(B, h, w, C, gen=g) for h, w in shapes]
+    packed = torch.cat([m.reshape(-1, C) for m in maps], 0).to(BF).cuda()
+    w = rnd(3, 3, C, C, scale=(9 * C) ** -0.5, gen=g)
+    wf, _, npad, _, _ = packs(w)
+    segs = [nn.seg(h, ww, h, ww, wf, None, src_base=B * off[l], dst_base=B * off[l]) for l, (h, ww) in enumerate(shapes)]
+    dy = rnd(B * P, C, gen=g).to(BF).cuda()
+    dw = torch.zeros((3, 3, C, C), dtype=torch.float32, device="cuda")
+    nn.conv_wgrad(nn.make_desc(nn.FWD, B, C, 3, 3, 1, 1, 1, npad, C, C, segs), packed, dy, dw)
+    ref = torch.zeros(3, 3, C, C, dtype=torch.float64)
+    for l, (h, ww) in enumerate(shapes):
+        wl = w.clone().requires_grad_(True)
+        y = ref_conv(maps[l], wl, None, 1, "same")
+        y.backward(dy[B * off[l]:B * off[l] + B * h * ww].reshape(B, h, ww, C).double().cpu())
+        ref += wl.grad
+    torch.testing.assert_close(dw.double().cpu(), ref, rtol=1e-4, atol=1e-4)
