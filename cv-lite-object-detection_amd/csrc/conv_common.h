@@ -9,6 +9,15 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 constexpr int kMaxSeg = CVL_CONV_MAX_SEG;
 
+// Workgroups are dispatched round-robin over the 8 XCDs (hardware id b runs on XCD b % 8).  This
+// bijective remap gives consecutive LOGICAL ids to the workgroups of one XCD, so tiles that read
+// the same rows (the N tiles of an M tile, the (co, k) tiles of one reduction chunk) share that
+// XCD's L2.
+__device__ __forceinline__ int xcd_remap(int b, int nwg) {
+  const int q = nwg / 8, r = nwg % 8, x = b % 8;
+  return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + b / 8;
+}
+
 struct ConvSeg {
   int Hr, Wr, Hs, Ws;
   long src_base, src_img, dst_base, dst_img;
@@ -30,7 +39,19 @@ struct ConvArgs {
   int m_tiles, m_total;
   float* slab;      // split-K partial sums [splits][m_total][Npad] (fp32) or null
   int splits, ksteps_per_split;
+  int dst_up, dst_w;  // output pixel (y, x) of the GEMM grid lands at (y*dst_up, x*dst_up) of a
+                      // dst_w-wide map (1x1 strided data-gradient as a dense GEMM); 1 = identity
 };
+
+// destination row of GEMM row q (within image img) of segment S
+__device__ __forceinline__ long conv_dst_row(const ConvArgs& a, const ConvSeg& S, int img, int q) {
+  long r = q;
+  if (a.dst_up != 1) {
+    const int y = q / S.Wr, x = q - (q / S.Wr) * S.Wr;
+    r = (long)y * a.dst_up * a.dst_w + (long)x * a.dst_up;
+  }
+  return S.dst_base + (long)img * S.dst_img + r;
+}
 
 // Validate a public descriptor and lay its segments out in a BM-padded M space.
 static inline int cvl_conv_prepare(const cvl_conv_desc* d, int bm, ConvArgs* a) {
@@ -43,6 +64,8 @@ static inline int cvl_conv_prepare(const cvl_conv_desc* d, int bm, ConvArgs* a) 
   a->slab = nullptr;
   a->splits = 1;
   a->ksteps_per_split = 0;
+  a->dst_up = 1;
+  a->dst_w = 0;
   a->nseg = d->nseg;
   a->B = d->B;
   a->Cin = d->Cin; a->KH = d->KH; a->KW = d->KW; a->stride = d->stride;

@@ -319,7 +319,7 @@ __global__ void __launch_bounds__(NT) conv_igemm_kernel(ConvArgs a) {
         const int ml = mloc0 + wm * WM + i * 16 + lg * 4 + e;
         if (ml >= S.rows) continue;
         const int img = ml / HWr, q = ml - img * HWr;
-        const long drow = S.dst_base + (long)img * S.dst_img + q;
+        const long drow = conv_dst_row(a, S, img, q);
 #pragma unroll
         for (int j = 0; j < TN; ++j) {
           const int n = n0 + wn * WN + j * 16 + lr;
@@ -353,7 +353,7 @@ __global__ void __launch_bounds__(NT) conv_igemm_kernel(ConvArgs a) {
     const int ml = mloc0 + r;
     if (ml >= S.rows || n0 + c8 >= a.n_store) continue;
     const int img = ml / HWr, q = ml - img * HWr;
-    const long drow = S.dst_base + (long)img * S.dst_img + q;
+    const long drow = conv_dst_row(a, S, img, q);
     s16x8 v = *reinterpret_cast<const s16x8*>(Cs + r * CP + c8);
     s16x8* pd = reinterpret_cast<s16x8*>(dst + drow * a.ld_dst + a.dst_coff + n0 + c8);
     if (a.beta != 0.f) {
@@ -396,7 +396,7 @@ __global__ void __launch_bounds__(NT) conv_splitk_finish(ConvArgs a, int rows_pe
           v[0] += x0[0]; v[1] += x0[1]; v[2] += x0[2]; v[3] += x0[3];
           v[4] += x1[0]; v[5] += x1[1]; v[6] += x1[2]; v[7] += x1[3];
         }
-        const long drow = S.dst_base + (long)img * S.dst_img + q;
+        const long drow = conv_dst_row(a, S, img, q);
         if (a.dst_f32) {
           float* pd = reinterpret_cast<float*>(a.dst) + drow * a.ld_dst + a.dst_coff + c0;
 #pragma unroll
@@ -493,9 +493,50 @@ static inline int pick_bn(int npad) { return npad % 128 == 0 ? 128 : (npad % 64 
 
 }  // namespace
 
-int cvl_conv_igemm_l(const cvl_conv_desc* d, const void* src, void* dst, double* bn_stats, hipStream_t s);
+int cvl_conv_igemm_l(const cvl_conv_desc* d, int dst_up, int dst_w, const void* src, void* dst, double* bn_stats,
+                     hipStream_t s);
+
+// 1x1 strided data-gradient: only every stride-th dX pixel receives a gradient, so instead of a
+// DGRAD gather that finds no valid tap for (s^2-1)/s^2 of the rows, run a dense 1x1 GEMM over the
+// dY pixels whose epilogue writes row (y, x) to dX pixel (y*s, x*s); the other pixels are zeroed
+// (beta == 0) or keep their accumulated value (beta != 0: they receive + 0).
+static bool s2dgrad_transform(const cvl_conv_desc* d, cvl_conv_desc* out, int* up, int* upw) {
+  if (d->mode != CVL_CONV_DGRAD || d->KH != 1 || d->KW != 1 || d->stride < 2 || d->nseg != 1 ||
+      d->pad_t != 0 || d->pad_l != 0 || d->relu_in || cvl_env_flag("CVL_CONV_NO_S2DG"))
+    return false;
+  const cvl_conv_seg& q = d->seg[0];
+  if ((q.Hs - 1) * d->stride >= q.Hr || (q.Ws - 1) * d->stride >= q.Wr) return false;
+  *out = *d;
+  out->mode = CVL_CONV_FWD;
+  out->stride = 1;
+  out->seg[0].Hr = q.Hs;
+  out->seg[0].Wr = q.Ws;
+  *up = d->stride;
+  *upw = q.Wr;
+  return true;
+}
+
+__global__ void zero_gaps_kernel(void* dst, int is_f32, long dst_base, long dst_img, int ld, int coff, int n,
+                                 int B, int H, int W, int s) {
+  const long rows = (long)B * H * W;
+  const int n8 = is_f32 ? n : n / 8;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < rows * n8; i += (long)gridDim.x * blockDim.x) {
+    const long r = i / n8;
+    const int c = (int)(i - r * n8);
+    const int img = (int)(r / ((long)H * W));
+    const int q = (int)(r - (long)img * H * W);
+    const int y = q / W, x = q - (q / W) * W;
+    if (y % s == 0 && x % s == 0) continue;
+    const long row = dst_base + (long)img * dst_img + q;
+    if (is_f32) reinterpret_cast<float*>(dst)[row * ld + coff + c] = 0.f;
+    else *reinterpret_cast<s16x8*>(reinterpret_cast<cvl_bf16*>(dst) + row * ld + coff + c * 8) = s16x8{0, 0, 0, 0, 0, 0, 0, 0};
+  }
+}
 
 extern "C" size_t cvl_conv_igemm_workspace_size(const cvl_conv_desc* d) {
+  cvl_conv_desc dd;
+  int up = 1, upw = 0;
+  if (s2dgrad_transform(d, &dd, &up, &upw)) d = &dd;
   ConvArgs a;
   if (cvl_conv_prepare(d, BM, &a)) return 0;
   const int sp = pick_ksplit(a, pick_bn(a.Npad), a.Cin % 64 == 0 ? 64 : 32);
@@ -504,9 +545,29 @@ extern "C" size_t cvl_conv_igemm_workspace_size(const cvl_conv_desc* d) {
 
 extern "C" int cvl_conv_igemm(const cvl_conv_desc* d, const void* src, void* dst, double* bn_stats,
                               void* workspace, size_t workspace_bytes, cvl_stream_t stream) {
+  hipStream_t s = (hipStream_t)stream;
+  cvl_conv_desc dd;
+  int up = 1, upw = 0;
+  if (s2dgrad_transform(d, &dd, &up, &upw)) {
+    CVL_CHECK_ARG(src && dst && !bn_stats);
+    CVL_CHECK_ARG(d->dst_f32 || (d->ld_dst % 8 == 0 && d->dst_coff % 8 == 0 && d->n_store % 8 == 0));
+    if (d->beta == 0.f) {
+      const cvl_conv_seg& q = d->seg[0];
+      const long work = (long)d->B * q.Hr * q.Wr * (d->dst_f32 ? d->n_store : d->n_store / 8);
+      int blocks = (int)((work + NT - 1) / NT);
+      blocks = blocks > 8192 ? 8192 : (blocks < 1 ? 1 : blocks);
+      hipLaunchKernelGGL(zero_gaps_kernel, dim3(blocks), dim3(NT), 0, s, dst, d->dst_f32, q.dst_base, q.dst_img,
+                         d->ld_dst, d->dst_coff, d->n_store, d->B, q.Hr, q.Wr, d->stride);
+      const int zst = cvl_launch_status();
+      if (zst) return zst;
+    }
+    d = &dd;
+  }
   ConvArgs a;
   int st = cvl_conv_prepare(d, BM, &a);
   if (st) return st;
+  a.dst_up = up;
+  a.dst_w = upw;
   CVL_CHECK_ARG(src && dst);
   CVL_CHECK_ARG(d->Cin % 32 == 0 && a.Npad % 32 == 0);
   if (!d->dst_f32) CVL_CHECK_ARG(d->ld_dst % 8 == 0 && d->dst_coff % 8 == 0 && d->n_store % 8 == 0);
@@ -517,7 +578,7 @@ extern "C" int cvl_conv_igemm(const cvl_conv_desc* d, const void* src, void* dst
     }
   }
   {
-    const int lst = cvl_conv_igemm_l(d, src, dst, bn_stats, (hipStream_t)stream);
+    const int lst = cvl_conv_igemm_l(d, up, upw, src, dst, bn_stats, s);
     if (lst >= 0) return lst;          // the 256-row LDS-DMA kernel took the launch
   }
   a.src = reinterpret_cast<const cvl_bf16*>(src);
@@ -530,7 +591,6 @@ extern "C" int cvl_conv_igemm(const cvl_conv_desc* d, const void* src, void* dst
     a.splits = sp;
     a.slab = reinterpret_cast<float*>(workspace);
   }
-  hipStream_t s = (hipStream_t)stream;
   const bool dg = d->mode == CVL_CONV_DGRAD;
   if (bn == 128) return launch_bn<128>(a, dg, s);
   if (bn == 64) return launch_bn<64>(a, dg, s);

@@ -51,7 +51,11 @@ __global__ void __launch_bounds__(NT) conv_igemm_l_kernel(ConvArgs a) {
 
   const int tid = threadIdx.x;
   const int wave = tid >> 6, lane = tid & 63;
-  const int m_tile = blockIdx.x, n_tile = blockIdx.y;
+  // 1-D grid, XCD-remapped: the N tiles of an M tile and neighbouring M tiles (3x3 halos) share
+  // an XCD's L2
+  const int ntn = a.Npad / BN;
+  const int L = xcd_remap(blockIdx.x, gridDim.x);
+  const int m_tile = L / ntn, n_tile = L % ntn;
   const int m0 = m_tile * BM, n0 = n_tile * BN;
   int sg = 0;
 #pragma unroll
@@ -247,7 +251,7 @@ __global__ void __launch_bounds__(NT) conv_igemm_l_kernel(ConvArgs a) {
     const int ml = mloc0 + r;
     if (ml >= S.rows || n0 + c8 >= a.n_store) continue;
     const int img = ml / HWr, q = ml - img * HWr;
-    const long drow = S.dst_base + (long)img * S.dst_img + q;
+    const long drow = conv_dst_row(a, S, img, q);
     s16x8 v = *reinterpret_cast<const s16x8*>(Cs + r * CP + c8);
     s16x8* pd = reinterpret_cast<s16x8*>(dst + drow * a.ld_dst + a.dst_coff + n0 + c8);
     if (a.beta != 0.f) {
@@ -264,7 +268,8 @@ __global__ void __launch_bounds__(NT) conv_igemm_l_kernel(ConvArgs a) {
 
 // Called by cvl_conv_igemm when the launch qualifies (see cvl_conv_igemm_l_ok); returns -1 when
 // it does not, so the caller falls back to the 128-row kernel.
-int cvl_conv_igemm_l(const cvl_conv_desc* d, const void* src, void* dst, double* bn_stats, hipStream_t s) {
+int cvl_conv_igemm_l(const cvl_conv_desc* d, int dst_up, int dst_w, const void* src, void* dst, double* bn_stats,
+                     hipStream_t s) {
   if (cvl_env_flag("CVL_CONV_NO_L")) return -1;
   if (d->Cin % 64 != 0 || d->relu_in || d->dst_f32 || d->n_store % 8 || d->ld_dst % 8 || d->dst_coff % 8)
     return -1;
@@ -272,6 +277,8 @@ int cvl_conv_igemm_l(const cvl_conv_desc* d, const void* src, void* dst, double*
   if (!bn) return -1;
   ConvArgs a;
   if (cvl_conv_prepare(d, BM, &a)) return -1;
+  a.dst_up = dst_up;
+  a.dst_w = dst_w;
   // too few tiles to fill 256 CUs at one 8-wave workgroup each (tests lower the bar)
   if ((long)a.m_tiles * (a.Npad / bn) < cvl_env_int("CVL_CONV_L_MIN_TILES", 384)) return -1;
   if (bn_stats)
@@ -280,7 +287,7 @@ int cvl_conv_igemm_l(const cvl_conv_desc* d, const void* src, void* dst, double*
   a.src = reinterpret_cast<const cvl_bf16*>(src);
   a.dst = dst;
   a.stats = bn_stats;
-  dim3 grid(a.m_tiles, a.Npad / bn);
+  dim3 grid(a.m_tiles * (a.Npad / bn));
   const bool dg = d->mode == CVL_CONV_DGRAD;
   if (bn == 128) {
     if (dg) hipLaunchKernelGGL((conv_igemm_l_kernel<128, true>), grid, dim3(NT), 0, s, a);

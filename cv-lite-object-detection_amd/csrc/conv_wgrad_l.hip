@@ -30,7 +30,7 @@ struct WgLArgs {
   ConvArgs a;
   const cvl_bf16* dy;
   float* out;
-  int ld_dy, dy_coff, Cout, co_tiles, chunk;
+  int ld_dy, dy_coff, Cout, co_tiles, chunk, nsplit;
   float beta;
   int direct;
 };
@@ -88,9 +88,13 @@ __global__ void __launch_bounds__(NT) conv_wgrad_l_kernel(WgLArgs g) {
 
   const ConvArgs& a = g.a;
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-  const int co_tile = blockIdx.x % g.co_tiles, k_tile = blockIdx.x / g.co_tiles;
+  // 1-D grid of tiles x splits, XCD-remapped: the tiles of one reduction chunk run on one XCD
+  const int L = xcd_remap(blockIdx.x, gridDim.x);
+  const int tiles = gridDim.x / g.nsplit;
+  const int tile = L % tiles, split = L / tiles;
+  const int co_tile = tile % g.co_tiles, k_tile = tile / g.co_tiles;
   const int co0 = co_tile * BCO, k0 = k_tile * BKK;
-  const int m_lo = blockIdx.y * g.chunk;
+  const int m_lo = split * g.chunk;
   const int m_hi = min(m_lo + g.chunk, a.m_total);
 
   // ---- per-lane constant piece geometry -------------------------------------------------------
@@ -224,7 +228,7 @@ __global__ void __launch_bounds__(NT) conv_wgrad_l_kernel(WgLArgs g) {
   }
 
   // ---- epilogue: C[co][k] -> out[k][co] (HWIO), 4 consecutive co per lane ----------------------
-  float* out = g.direct ? g.out : g.out + (size_t)blockIdx.y * a.K * g.Cout;
+  float* out = g.direct ? g.out : g.out + (size_t)split * a.K * g.Cout;
 #pragma unroll
   for (int i = 0; i < 4; ++i)
 #pragma unroll
@@ -319,7 +323,8 @@ int cvl_conv_wgrad_l(const cvl_conv_desc* d, const void* x, const void* dy, floa
   } else {
     g.out = dw;
   }
-  hipLaunchKernelGGL(conv_wgrad_l_kernel, dim3(tiles, nsplit), dim3(NT), 0, s, g);
+  g.nsplit = nsplit;
+  hipLaunchKernelGGL(conv_wgrad_l_kernel, dim3(tiles * nsplit), dim3(NT), 0, s, g);
   int st = cvl_launch_status();
   if (st || g.direct) return st;
   const long n4 = (long)g.a.K * g.Cout / 4;

@@ -132,6 +132,12 @@ def test_conv_dgrad_wgrad(case, kern):
     d = nn.make_desc(nn.DGRAD, B, cout_pad, k, k, s, pt, pl, cin_pad, Cin, Cin, [nn.seg(H, W, Ho, Wo, wd)])
     nn.conv_igemm(d, dyg, dx)
     torch.testing.assert_close(dx.double().cpu(), x.grad, rtol=1e-2, atol=2e-2)
+    # accumulate (beta = 1) into an existing gradient (residual-branch form)
+    old = torch.randn((B, H, W, Cin), generator=g).to(BF)
+    dx2 = old.cuda()
+    d = nn.make_desc(nn.DGRAD, B, cout_pad, k, k, s, pt, pl, cin_pad, Cin, Cin, [nn.seg(H, W, Ho, Wo, wd)], beta=1.0)
+    nn.conv_igemm(d, dyg, dx2)
+    torch.testing.assert_close(dx2.double().cpu(), x.grad + old.double(), rtol=1e-2, atol=3e-2)
     # wgrad
     dw = torch.zeros((k, k, Cin, Cout), dtype=torch.float32, device="cuda")
     d = nn.make_desc(nn.FWD, B, Cin, k, k, s, pt, pl, npad, Cout, cout_pad, [nn.seg(Ho, Wo, H, W, wf)])
