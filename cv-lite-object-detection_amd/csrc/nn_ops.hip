@@ -58,6 +58,53 @@ __global__ void pack_dgrad_kernel(const float* w, cvl_bf16* wd, int KHW, int Cin
   }
 }
 
+// batched weight packing: one launch re-packs every conv of the network after the update.  A
+// workgroup owns one 64 (ci) x 64 (co) block of one tap of one item: coalesced fp32 reads of the
+// HWIO slab [ci][co] into LDS, then 16-byte bf16 stores of the forward image (transposed:
+// [co][tap*Cin_k + ci]) and of the data-gradient image (as is: [ci][tap*Cout_pad + co]).
+__global__ void __launch_bounds__(NT) pack_multi_kernel(const cvl_pack_item* __restrict__ items,
+                                                        const int4* __restrict__ tiles) {
+  const int4 t = tiles[blockIdx.x];
+  const cvl_pack_item it = items[t.x];
+  const int tap = t.y, ci0 = t.z, co0 = t.w;
+  __shared__ float tile[64][65];
+  const int col = threadIdx.x & 63, r0 = threadIdx.x >> 6;
+  const float* src = it.w + (long)tap * it.Cin * it.Cout;
+#pragma unroll 4
+  for (int j = 0; j < 16; ++j) {
+    const int r = r0 + 4 * j, ci = ci0 + r, co = co0 + col;
+    tile[r][col] = (ci < it.Cin && co < it.Cout) ? src[(long)ci * it.Cout + co] : 0.f;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int idx = threadIdx.x + j * NT;
+    const int r = idx >> 3, c8 = (idx & 7) * 8;
+    if (it.w_fwd) {       // row co0 + r, channels ci0 + c8 .. +7 of tap
+      const int co = co0 + r, ci = ci0 + c8;
+      if (co < it.Npad && ci < it.Cin_k) {
+        float f[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) f[u] = tile[c8 + u][r];
+        const long K = (long)it.KHW * it.Cin_k;
+        *reinterpret_cast<s16x8*>(reinterpret_cast<cvl_bf16*>(it.w_fwd) + co * K + (long)tap * it.Cin_k + ci) =
+            pack8(f);
+      }
+    }
+    if (it.w_dgrad) {     // row ci0 + r, channels co0 + c8 .. +7 of tap
+      const int ci = ci0 + r, co = co0 + c8;
+      if (ci < it.Cin_pad && co < it.Cout_pad) {
+        float f[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) f[u] = tile[r][c8 + u];
+        const long K = (long)it.KHW * it.Cout_pad;
+        *reinterpret_cast<s16x8*>(reinterpret_cast<cvl_bf16*>(it.w_dgrad) + ci * K + (long)tap * it.Cout_pad + co) =
+            pack8(f);
+      }
+    }
+  }
+}
+
 // stem: fp32 NHWC image -> bf16 im2col rows [B*Ho*Wo][Kp], k = (r*KW + s)*C + c, zero pad
 __global__ void im2col_kernel(const float* x, cvl_bf16* out, int B, int H, int W, int C, int KH,
                               int KW, int stride, int pad_t, int pad_l, int Ho, int Wo, int Kp) {
@@ -102,29 +149,70 @@ __global__ void bn_finalize_kernel(const double* stats, float* mr, float* run_me
   if (run_mean) { run_mean[c] = rm; run_var[c] = rv; }
 }
 
-// y = act(gamma * (z - mean) * rstd + beta [+ residual])
-__global__ void bn_apply_kernel(const cvl_bf16* z, const float* mr, const float* gamma, const float* beta,
-                                const cvl_bf16* res, cvl_bf16* y, long rows, int C, int HW, int relu) {
+// y = act(gamma * (z - mean) * rstd + beta [+ residual]).  Grid (row chunk, image); a thread owns
+// 8 channels for the whole chunk (scale/shift loaded once) and streams rows UNR at a time with
+// all 16-byte loads issued before use.
+constexpr int BNA_UNR = 4;
+__global__ void __launch_bounds__(NT) bn_apply_kernel(const cvl_bf16* __restrict__ z, const float* __restrict__ mr,
+                                                      const float* __restrict__ gamma, const float* __restrict__ beta,
+                                                      const cvl_bf16* __restrict__ res, cvl_bf16* __restrict__ y,
+                                                      int C, int HW, int relu, int rows_per_blk) {
+  const int b = blockIdx.y;
   const int C8 = C / 8;
-  const long total = rows * C8;
-  for (long i = blockIdx.x * (long)NT + threadIdx.x; i < total; i += (long)gridDim.x * NT) {
-    const long row = i / C8;
-    const int c0 = (int)(i - row * C8) * 8;
-    const int b = (int)(row / HW);
-    float v[8], r[8];
-    unpack8(*reinterpret_cast<const s16x8*>(z + row * C + c0), v);
-    if (res) unpack8(*reinterpret_cast<const s16x8*>(res + row * C + c0), r);
+  const int tpr = C8 < NT ? C8 : NT;
+  const int rpp = NT / tpr;
+  const int cg = threadIdx.x % tpr, rsub = threadIdx.x / tpr;
+  if (rsub >= rpp) return;
+  const int r0 = blockIdx.x * rows_per_blk;
+  const int r1 = min(r0 + rows_per_blk, HW);
+  for (int cgb = cg; cgb < C8; cgb += tpr) {
+    const int c0 = cgb * 8;
+    float m[8], rs[8], ga[8], be[8];
 #pragma unroll
     for (int u = 0; u < 8; ++u) {
-      const int c = c0 + u;
-      const float m = mr[((long)b * C + c) * 2], rs = mr[((long)b * C + c) * 2 + 1];
-      float o = gamma[c] * ((v[u] - m) * rs) + beta[c];
-      if (res) o += r[u];
-      if (relu) o = o > 0.f ? o : 0.f;
-      v[u] = o;
+      const long bc = (long)b * C + c0 + u;
+      m[u] = mr[bc * 2];
+      rs[u] = mr[bc * 2 + 1];
+      ga[u] = gamma[c0 + u];
+      be[u] = beta[c0 + u];
     }
-    *reinterpret_cast<s16x8*>(y + row * C + c0) = pack8(v);
+    for (int r = r0 + rsub; r < r1; r += rpp * BNA_UNR) {
+      s16x8 vz[BNA_UNR], vr[BNA_UNR];
+      long off[BNA_UNR];
+#pragma unroll
+      for (int q = 0; q < BNA_UNR; ++q) {
+        const int rq = min(r + q * rpp, r1 - 1);
+        off[q] = ((long)b * HW + rq) * C + c0;
+        vz[q] = *reinterpret_cast<const s16x8*>(z + off[q]);
+        if (res) vr[q] = *reinterpret_cast<const s16x8*>(res + off[q]);
+      }
+#pragma unroll
+      for (int q = 0; q < BNA_UNR; ++q) {
+        if (r + q * rpp >= r1) break;
+        float v[8], rr[8];
+        unpack8(vz[q], v);
+        if (res) unpack8(vr[q], rr);
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          float o = ga[u] * ((v[u] - m[u]) * rs[u]) + be[u];
+          if (res) o += rr[u];
+          if (relu) o = o > 0.f ? o : 0.f;
+          v[u] = o;
+        }
+        *reinterpret_cast<s16x8*>(y + off[q]) = pack8(v);
+      }
+    }
   }
+}
+
+// rows per block of the (row chunk, image) grids: ~2048 blocks in total, >= 4 passes per thread
+inline int bn_rows_per_blk(int B, int HW, int C) {
+  const int C8 = C / 8, tpr = C8 < NT ? C8 : NT, rpp = NT / tpr;
+  const int chunks = (2048 + B - 1) / B;
+  int rpb = (HW + chunks - 1) / chunks;
+  const int lo = rpp * 4 * (C8 > NT ? 1 : 1);
+  rpb = rpb < lo ? lo : rpb;
+  return (rpb + rpp - 1) / rpp * rpp;
 }
 
 // BN backward over one (image, row-chunk) block; threads own 8 channels (tpr threads per row,
@@ -132,8 +220,7 @@ __global__ void bn_apply_kernel(const cvl_bf16* z, const float* mr, const float*
 // latency-bound otherwise).  No atomics: each block writes its per-channel partial sums to
 // part[b][chunk][C][2]; small follow-up kernels reduce them in a fixed order (deterministic).
 // PASS 0: (sum g, sum g*xhat), g = dy * (y > 0 if relu).
-// PASS 1: dz = gamma*rstd*(g - mean(g) - xhat*mean(g*xhat)) (+ g_out = g), and sum dz (the
-// preceding conv's bias gradient, fused column sum of the stored bf16 dz).
+// PASS 1: dz = gamma*rstd*(g - mean(g) - xhat*mean(g*xhat)) (+ g_out = g).
 constexpr int BN_UNR = 4;
 
 template <int PASS>
@@ -206,17 +293,12 @@ __global__ void __launch_bounds__(NT) bn_bwd_kernel(const cvl_bf16* __restrict__
               const float xh = (zz[u] - m[u]) * rs[u];
               o[u] = gm[u] * (g[u] - k1[u] - xh * k2[u]);
             }
-            const s16x8 ov = pack8(o);
-            *reinterpret_cast<s16x8*>(dz + off[q]) = ov;
-            float orr[8];
-            unpack8(ov, orr);                       // the bias gradient sums the stored bf16 dz
-#pragma unroll
-            for (int u = 0; u < 8; ++u) s1[u] += orr[u];
+            *reinterpret_cast<s16x8*>(dz + off[q]) = pack8(o);
           }
         }
       }
     }
-    if (PASS == 1 && !part) continue;                // uniform: no bias gradient wanted
+    if (PASS == 1) continue;                         // pass 1 only writes dz
     __syncthreads();
 #pragma unroll
     for (int u = 0; u < 8; ++u) { red[threadIdx.x][u] = s1[u]; red[threadIdx.x][8 + u] = s2[u]; }
@@ -269,12 +351,14 @@ __global__ void __launch_bounds__(NT) bn_colsum_kernel(const float* __restrict__
 }
 
 // dgamma[c] = beta_acc*dgamma + sum_b sum g*xhat ; dbeta[c] = ... + sum_b sum g ;
-// conv_dbias[c] = the reduced sum of dz
+// conv_dbias[c] = 0: training-mode BN subtracts the per-image mean of z, so a constant added to z
+// (the preceding conv's bias) cannot change the loss -- sum_rows dz = gamma*rstd*(S_g - S_g -
+// mean(g xhat) * sum xhat) = 0 exactly (TF's fp32 value is rounding noise around this 0)
 __global__ void bn_param_grad_kernel(const double* sums, float* dgamma, float* dbeta, int B, int C,
-                                     float beta_acc, const double* dbias_sum, float* conv_dbias) {
+                                     float beta_acc, float* conv_dbias) {
   const int c = blockIdx.x * NT + threadIdx.x;
   if (c >= C) return;
-  if (conv_dbias) conv_dbias[c] = (float)dbias_sum[(long)c * 2];
+  if (conv_dbias) conv_dbias[c] = 0.f;
   double a1 = 0.0, a2 = 0.0;
   for (int b = 0; b < B; ++b) { a1 += sums[((long)b * C + c) * 2]; a2 += sums[((long)b * C + c) * 2 + 1]; }
   dbeta[c] = (float)a1 + (beta_acc != 0.f ? beta_acc * dbeta[c] : 0.f);
@@ -439,35 +523,82 @@ __global__ void add_kernel(const cvl_bf16* a, const cvl_bf16* b, cvl_bf16* out, 
   }
 }
 
-// bias gradient: acc[c] += sum over rows of dY[row][c] (rows: base + b*img_stride + q, q < HW)
-__global__ void colsum_kernel(const cvl_bf16* dy, int ld, int coff, int ncol, long base, long img_stride,
-                              int HW, int B, int rows_per_blk, double* acc) {
-  const int col = threadIdx.x % 64 + blockIdx.y * 64;
-  const int rsub = threadIdx.x / 64;
-  const long nrows = (long)B * HW;
+// bias gradient, pass 1: a block sums rows [r0, r1) of the segment; a thread owns 8 columns (one
+// 16-byte load per row), rows UNR at a time with the loads issued first; per-block partials
+// part[blk][ncol8*8] (no atomics: deterministic)
+constexpr int CS_UNR = 4;
+__global__ void __launch_bounds__(NT) colsum8_kernel(const cvl_bf16* __restrict__ dy, int ld, int coff, int ncol8,
+                                                     long base, long img_stride, int HW, long nrows,
+                                                     int rows_per_blk, float* __restrict__ part) {
+  const int tpr = ncol8;
+  const int rpp = NT / tpr;
+  const int cg = threadIdx.x % tpr, rsub = threadIdx.x / tpr;
   const long r0 = (long)blockIdx.x * rows_per_blk;
   const long r1 = r0 + rows_per_blk < nrows ? r0 + rows_per_blk : nrows;
-  float s = 0.f;
-  if (col < ncol) {
-    for (long r = r0 + rsub; r < r1; r += NT / 64) {
-      const int b = (int)(r / HW);
-      const long row = base + (long)b * img_stride + (r - (long)b * HW);
-      s += bf16_to_f32(dy[row * ld + coff + col]);
+  float s[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  if (rsub < rpp) {
+    for (long r = r0 + rsub; r < r1; r += (long)rpp * CS_UNR) {
+      s16x8 v[CS_UNR];
+#pragma unroll
+      for (int q = 0; q < CS_UNR; ++q) {
+        long rq = r + (long)q * rpp;
+        rq = rq < r1 ? rq : r1 - 1;                 // clamped: loads stay unconditional
+        const int b = (int)(rq / HW);
+        const long row = base + (long)b * img_stride + (rq - (long)b * HW);
+        v[q] = *reinterpret_cast<const s16x8*>(dy + row * ld + coff + cg * 8);
+      }
+#pragma unroll
+      for (int q = 0; q < CS_UNR; ++q) {
+        if (r + (long)q * rpp >= r1) break;
+        float f[8];
+        unpack8(v[q], f);
+#pragma unroll
+        for (int u = 0; u < 8; ++u) s[u] += f[u];
+      }
     }
   }
-  __shared__ float red[NT];
-  red[threadIdx.x] = s;
+  __shared__ float red[NT][9];
+#pragma unroll
+  for (int u = 0; u < 8; ++u) red[threadIdx.x][u] = s[u];
   __syncthreads();
-  if (rsub == 0 && col < ncol) {
-    double t = 0.0;
-    for (int k = 0; k < NT / 64; ++k) t += red[k * 64 + threadIdx.x];
-    atomicAdd(&acc[col], t);
+  if (rsub == 0) {
+    float* pp = part + (long)blockIdx.x * ncol8 * 8 + cg * 8;
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      float a = 0.f;
+      for (int k = 0; k < rpp; ++k) a += red[k * tpr + cg][u];
+      pp[u] = a;
+    }
   }
 }
 
-__global__ void colsum_finish_kernel(const double* acc, float* db, int ncol, float beta) {
-  const int c = blockIdx.x * NT + threadIdx.x;
-  if (c < ncol) db[c] = (float)acc[c] + (beta != 0.f ? beta * db[c] : 0.f);
+// pass 2: db[c] = beta*db + sum_blk part[blk][c] (float64, fixed order); 32 columns x 8 row groups
+__global__ void __launch_bounds__(NT) colsum8_finish_kernel(const float* __restrict__ part, int nblk, int ldp,
+                                                            int ncol, float* db, float beta) {
+  const int cl = threadIdx.x & 31, rg = threadIdx.x >> 5;
+  const int c = blockIdx.x * 32 + cl;
+  __shared__ double red[8][32];
+  double a = 0.0;
+  if (c < ncol)
+    for (int r = rg; r < nblk; r += 8) a += part[(long)r * ldp + c];
+  red[rg][cl] = a;
+  __syncthreads();
+  if (rg == 0 && c < ncol) {
+    double t = 0.0;
+    for (int k = 0; k < 8; ++k) t += red[k][cl];
+    db[c] = (float)t + (beta != 0.f ? beta * db[c] : 0.f);
+  }
+}
+
+inline void colsum8_geometry(int ncol, long nrows, int* ncol8, int* rows_per_blk, int* nblk) {
+  *ncol8 = (ncol + 7) / 8;
+  const int rpp = NT / *ncol8;
+  long rpb = (nrows + 511) / 512;                       // <= 512 partial rows
+  const long lo = (long)rpp * CS_UNR * 2;
+  rpb = rpb < lo ? lo : rpb;
+  rpb = (rpb + rpp - 1) / rpp * rpp;
+  *rows_per_blk = (int)rpb;
+  *nblk = (int)((nrows + rpb - 1) / rpb);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -535,6 +666,15 @@ extern "C" int cvl_pack_conv_weights(const float* w_hwio, int KH, int KW, int Ci
   return cvl_launch_status();
 }
 
+extern "C" int cvl_pack_conv_weights_multi(const cvl_pack_item* items, const int32_t* tiles, int ntiles,
+                                           cvl_stream_t stream) {
+  CVL_CHECK_ARG(items && tiles && ntiles >= 0);
+  if (ntiles == 0) return CVL_OK;
+  hipLaunchKernelGGL(pack_multi_kernel, dim3(ntiles), dim3(NT), 0, S_, items,
+                     reinterpret_cast<const int4*>(tiles));
+  return cvl_launch_status();
+}
+
 extern "C" int cvl_im2col(const float* x, int B, int H, int W, int C, int KH, int KW, int stride, int pad_t,
                           int pad_l, int Ho, int Wo, int Kp, void* out, cvl_stream_t stream) {
   CVL_CHECK_ARG(x && out && B > 0 && Kp >= KH * KW * C);
@@ -555,10 +695,11 @@ extern "C" int cvl_bn_finalize(const double* stats, float* mean_rstd, float* run
 extern "C" int cvl_bn_apply(const void* z, const float* mean_rstd, const float* gamma, const float* beta,
                             const void* residual, void* y, int B, int HW, int C, int relu,
                             cvl_stream_t stream) {
-  CVL_CHECK_ARG(z && mean_rstd && gamma && beta && y && C % 8 == 0);
-  const long rows = (long)B * HW;
-  hipLaunchKernelGGL(bn_apply_kernel, dim3(grid_for(rows * (C / 8))), dim3(NT), 0, S_, (const cvl_bf16*)z,
-                     mean_rstd, gamma, beta, (const cvl_bf16*)residual, (cvl_bf16*)y, rows, C, HW, relu);
+  CVL_CHECK_ARG(z && mean_rstd && gamma && beta && y && C % 8 == 0 && B > 0 && HW > 0);
+  CVL_CHECK_ARG(C / 8 <= NT || (C / 8) % NT == 0);
+  const int rpb = bn_rows_per_blk(B, HW, C);
+  hipLaunchKernelGGL(bn_apply_kernel, dim3((HW + rpb - 1) / rpb, B), dim3(NT), 0, S_, (const cvl_bf16*)z,
+                     mean_rstd, gamma, beta, (const cvl_bf16*)residual, (cvl_bf16*)y, C, HW, relu, rpb);
   return cvl_launch_status();
 }
 
@@ -578,12 +719,10 @@ extern "C" int cvl_bn_backward(const void* dy, const void* y_relu, const void* z
   CVL_CHECK_ARG(workspace_bytes >= cvl_bn_backward_workspace_size(B, HW, C));
   const int rpb = bn_bwd_rows_per_blk(B, HW, C);
   const int nchunk = (HW + rpb - 1) / rpb;
-  // workspace: sums [B][C][2] f64 | dbias sums [C][2] f64 | pass-0 partials [B][nchunk][C][2] f32 |
-  // pass-1 partials (same)
+  // workspace: sums [B][C][2] f64 | (unused [C][2] f64) | pass-0 partials [B][nchunk][C][2] f32
   double* sums = reinterpret_cast<double*>(workspace);
   double* dbsum = sums + 2 * (size_t)B * C;
   float* part0 = reinterpret_cast<float*>(dbsum + 2 * (size_t)C);
-  float* part1 = part0 + 2 * (size_t)B * nchunk * C;
   dim3 g1(nchunk, B);
   hipLaunchKernelGGL(bn_bwd_kernel<0>, g1, dim3(NT), 0, S_, (const cvl_bf16*)dy, (const cvl_bf16*)y_relu,
                      (const cvl_bf16*)z, mean_rstd, gamma, (const double*)nullptr, (cvl_bf16*)nullptr,
@@ -592,12 +731,9 @@ extern "C" int cvl_bn_backward(const void* dy, const void* y_relu, const void* z
                      sums);
   hipLaunchKernelGGL(bn_bwd_kernel<1>, g1, dim3(NT), 0, S_, (const cvl_bf16*)dy, (const cvl_bf16*)y_relu,
                      (const cvl_bf16*)z, mean_rstd, gamma, (const double*)sums, (cvl_bf16*)dz, (cvl_bf16*)g_out,
-                     conv_dbias ? part1 : (float*)nullptr, C, HW, rpb);
-  if (conv_dbias)
-    hipLaunchKernelGGL(bn_colsum_kernel, dim3((C + 31) / 32, 1), dim3(NT), 0, S_, (const float*)part1,
-                       B * nchunk, C, dbsum);
+                     (float*)nullptr, C, HW, rpb);
   hipLaunchKernelGGL(bn_param_grad_kernel, dim3((C + NT - 1) / NT), dim3(NT), 0, S_, (const double*)sums,
-                     dgamma, dbeta, B, C, beta_acc, (const double*)dbsum, conv_dbias);
+                     dgamma, dbeta, B, C, beta_acc, conv_dbias);
   return cvl_launch_status();
 }
 
@@ -654,19 +790,27 @@ extern "C" int cvl_add(const void* a, const void* b, void* out, long n, cvl_stre
   return cvl_launch_status();
 }
 
+extern "C" size_t cvl_bias_grad_workspace_size(int ncol, int HW, int B) {
+  if (ncol <= 0 || HW <= 0 || B <= 0) return 0;
+  int ncol8, rpb, nblk;
+  colsum8_geometry(ncol, (long)B * HW, &ncol8, &rpb, &nblk);
+  return sizeof(float) * (size_t)nblk * ncol8 * 8;
+}
+
 extern "C" int cvl_bias_grad(const void* dy, int ld, int coff, int ncol, int64_t base, int64_t img_stride,
-                             int HW, int B, double* acc_ws, float* db, float beta, cvl_stream_t stream) {
-  CVL_CHECK_ARG(dy && acc_ws && db && ncol > 0 && HW > 0 && B > 0);
-  hipError_t e = hipMemsetAsync(acc_ws, 0, sizeof(double) * ncol, S_);
-  if (e != hipSuccess) return CVL_EHIP + (int)e;
+                             int HW, int B, void* workspace, size_t workspace_bytes, float* db, float beta,
+                             cvl_stream_t stream) {
+  CVL_CHECK_ARG(dy && workspace && db && ncol > 0 && ncol <= 8 * NT && HW > 0 && B > 0);
+  CVL_CHECK_ARG(ld % 8 == 0 && coff % 8 == 0 && coff + (ncol + 7) / 8 * 8 <= ld);
+  CVL_CHECK_ARG(workspace_bytes >= cvl_bias_grad_workspace_size(ncol, HW, B));
+  int ncol8, rpb, nblk;
   const long nrows = (long)B * HW;
-  int rows_per_blk = 512;
-  while ((nrows + rows_per_blk - 1) / rows_per_blk > 1024) rows_per_blk *= 2;
-  dim3 g((int)((nrows + rows_per_blk - 1) / rows_per_blk), (ncol + 63) / 64);
-  hipLaunchKernelGGL(colsum_kernel, g, dim3(NT), 0, S_, (const cvl_bf16*)dy, ld, coff, ncol, (long)base,
-                     (long)img_stride, HW, B, rows_per_blk, acc_ws);
-  hipLaunchKernelGGL(colsum_finish_kernel, dim3((ncol + NT - 1) / NT), dim3(NT), 0, S_, (const double*)acc_ws,
-                     db, ncol, beta);
+  colsum8_geometry(ncol, nrows, &ncol8, &rpb, &nblk);
+  float* part = reinterpret_cast<float*>(workspace);
+  hipLaunchKernelGGL(colsum8_kernel, dim3(nblk), dim3(NT), 0, S_, (const cvl_bf16*)dy, ld, coff, ncol8,
+                     (long)base, (long)img_stride, HW, nrows, rpb, part);
+  hipLaunchKernelGGL(colsum8_finish_kernel, dim3((ncol + 31) / 32), dim3(NT), 0, S_, (const float*)part, nblk,
+                     ncol8 * 8, ncol, db, beta);
   return cvl_launch_status();
 }
 

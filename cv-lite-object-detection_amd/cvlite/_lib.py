@@ -29,6 +29,7 @@ SIGNATURES = {
     "cvl_conv_wgrad_workspace_size": (c_size_t, [P]),
     "cvl_conv_wgrad": (c_int, [P, P, P, P, c_float, P, c_size_t, P]),
     "cvl_pack_conv_weights": (c_int, [P, c_int, c_int, c_int, c_int, c_int, c_int, P, c_int, c_int, P, P]),
+    "cvl_pack_conv_weights_multi": (c_int, [P, P, c_int, P]),
     "cvl_im2col": (c_int, [P, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int,
                            c_int, c_int, P, P]),
     "cvl_bn_finalize": (c_int, [P, P, P, P, c_int, c_int, c_int, c_float, c_float, P]),
@@ -41,8 +42,9 @@ SIGNATURES = {
     "cvl_upsample2x_backward": (c_int, [P, P, c_int, c_int, c_int, c_int, c_float, P]),
     "cvl_relu_backward": (c_int, [P, P, P, ctypes.c_long, c_float, P]),
     "cvl_add": (c_int, [P, P, P, ctypes.c_long, P]),
-    "cvl_bias_grad": (c_int, [P, c_int, c_int, c_int, ctypes.c_int64, ctypes.c_int64, c_int, c_int, P, P,
-                              c_float, P]),
+    "cvl_bias_grad_workspace_size": (c_size_t, [c_int, c_int, c_int]),
+    "cvl_bias_grad": (c_int, [P, c_int, c_int, c_int, ctypes.c_int64, ctypes.c_int64, c_int, c_int, P, c_size_t,
+                              P, c_float, P]),
     "cvl_sgd_clip_update": (c_int, [P, P, P, ctypes.c_int64, P, c_float, c_float, c_float, P, P]),
     "cvl_lr_schedule": (c_int, [P, P, ctypes.c_double, ctypes.c_double, ctypes.c_double, c_int, P]),
     "cvl_retina_assign": (c_int, [P, P, P, c_int, c_int, c_int, c_int, P, c_int, P, c_float, P, P, P]),

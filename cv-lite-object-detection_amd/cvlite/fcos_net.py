@@ -35,6 +35,7 @@ class FCOSNet(object):
         for bn in self.backbone.bns():
             bn.init_buffers(device)
         self.device = device
+        self._pack_plan = None
         self.pack()
 
 
@@ -72,11 +73,13 @@ class FCOSNet(object):
                  self.c6_3x3, self.c7_3x3] + self.cls_heads + self.reg_heads)
 
     def pack(self):
-        """Refresh the bf16 packed weights from the fp32 masters (after every update)."""
-        self.backbone.pack()
-        for c in self.all_convs():
-            if c is not self.backbone.stem.conv:
-                c.pack()
+        """Refresh the bf16 packed weights from the fp32 masters (after every update): one
+        batched launch over every conv (ops_nn.PackPlan)."""
+        if self._pack_plan is None:
+            entries = self.backbone.pack_entries()
+            entries += [c.pack_entry() for c in self.all_convs() if c not in self.backbone.convs()]
+            self._pack_plan = nn.PackPlan(entries, self.device)
+        self._pack_plan.run()
 
     # ---- geometry ---------------------------------------------------------------------------------
     @staticmethod

@@ -109,7 +109,6 @@ class Conv(object):
         self.bname = store.add(name + "/bias", (cout,), constant(bias_init)) if bias else None
         self.store = store
         self.wf = self.wd = None
-        self._bias_pad = None
 
     # ---- geometry -----------------------------------------------------------------------------
     def out_hw(self, H, W):
@@ -141,26 +140,27 @@ class Conv(object):
         return self.store.g(self.bname) if self.bname else None
 
     def bias_arg(self):
-        if not self.has_bias:
-            return None
-        if self.npad == self.cout:
-            return self.b
-        assert self._bias_pad is not None, "pack() before use"
-        return self._bias_pad
+        # every conv kernel reads bias[n] only for n < n_store (= cout): no padded copy needed
+        return self.b if self.has_bias else None
 
-    def pack(self):
+    def alloc_packed(self):
         dev = self.store.flat.device
         K = self.k * self.k * self.cin_k
         if self.wf is None:
             self.wf = torch.empty((self.npad, K), dtype=BF16, device=dev)
             if self.need_dgrad:
                 self.wd = torch.empty((self.cin_pad, self.k * self.k * self.cout_pad), dtype=BF16, device=dev)
+
+    def pack_entry(self):
+        """Row of an ops_nn.PackPlan (the batched re-pack of every conv)."""
+        self.alloc_packed()
+        return (self.w, self.k * self.k, self.cin, self.cout, self.cin_k, self.npad, self.wf,
+                self.cin_pad, self.cout_pad, self.wd if self.need_dgrad else None)
+
+    def pack(self):
+        self.alloc_packed()
         nn.pack_conv_weights(self.w, self.k, self.k, self.cin, self.cout, self.cin_k, self.npad, self.wf,
                              self.cin_pad, self.cout_pad, self.wd if self.need_dgrad else None)
-        if self.has_bias and self.npad != self.cout:
-            if self._bias_pad is None:
-                self._bias_pad = torch.zeros(self.npad, dtype=torch.float32, device=dev)
-            self._bias_pad[:self.cout].copy_(self.b)
 
     # ---- descriptors ----------------------------------------------------------------------------
     def fwd_desc(self, B, segs, ld_dst=None, dst_coff=0, dst_f32=False, relu_out=False, relu_in=False,
@@ -208,6 +208,22 @@ class Conv(object):
         return out
 
 
+class StatsArena(object):
+    """One zeroed float64 buffer holding the (sum, sumsq) BN statistics of every conv of a forward
+    pass (one memset per step instead of one per BN)."""
+
+    def __init__(self, n_doubles, device):
+        self.buf = torch.zeros(n_doubles, dtype=torch.float64, device=device)
+        self.off = 0
+
+    def take(self, B, c):
+        n = B * c * 2
+        assert self.off + n <= self.buf.numel(), "stats arena too small"
+        v = self.buf[self.off:self.off + n].view(B, c, 2)
+        self.off += n
+        return v
+
+
 class BatchNorm(object):
     """Keras BatchNormalization(axis=-1) in training mode with per-image statistics."""
 
@@ -240,10 +256,11 @@ class ConvBN(object):
                          bias=True, dgrad=dgrad, cin_k=cin_k)
         self.bn = BatchNorm(store, (name + "_bn") if bn_name is None else bn_name, cout)
 
-    def forward(self, x, B, H, W, relu=True, residual=None, train=True):
+    def forward(self, x, B, H, W, relu=True, residual=None, train=True, arena=None):
         c = self.conv.cout
         Ho, Wo, _, _ = self.conv.out_hw(H, W)
-        stats = torch.zeros((B, c, 2), dtype=torch.float64, device=x.device)
+        stats = arena.take(B, c) if arena is not None else torch.zeros((B, c, 2), dtype=torch.float64,
+                                                                         device=x.device)
         z, _, _ = self.conv.fwd(x, B, H, W, stats=stats)
         mr = torch.empty((B, c, 2), dtype=torch.float32, device=x.device)
         nn.bn_finalize(stats, mr, self.bn.run_mean if train else None, self.bn.run_var if train else None,

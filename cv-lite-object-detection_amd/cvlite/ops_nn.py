@@ -72,6 +72,43 @@ def pack_conv_weights(w_hwio, KH, KW, Cin, Cout, Cin_k, Npad, w_fwd, Cin_pad=0, 
               Cin_pad, Cout_pad, ptr(w_dgrad), stream())
 
 
+class PackItem(ctypes.Structure):
+    _fields_ = [("w", c_void_p), ("w_fwd", c_void_p), ("w_dgrad", c_void_p), ("KHW", c_int), ("Cin", c_int),
+                ("Cout", c_int), ("Cin_k", c_int), ("Npad", c_int), ("Cin_pad", c_int), ("Cout_pad", c_int),
+                ("pad_", c_int)]
+
+
+class PackPlan(object):
+    """Device tables for cvl_pack_conv_weights_multi: every conv's fwd/dgrad bf16 re-pack in one
+    launch.  entries: (w_hwio fp32, KHW, Cin, Cout, Cin_k, Npad, w_fwd, Cin_pad, Cout_pad, w_dgrad)."""
+
+    def __init__(self, entries, device):
+        items = (PackItem * len(entries))()
+        tiles = []
+        self._keep = []
+        for i, (w, khw, cin, cout, cin_k, npad, wf, cin_pad, cout_pad, wd) in enumerate(entries):
+            it = items[i]
+            it.w = w.data_ptr()
+            it.w_fwd = wf.data_ptr() if wf is not None else None
+            it.w_dgrad = wd.data_ptr() if wd is not None else None
+            it.KHW, it.Cin, it.Cout, it.Cin_k, it.Npad = khw, cin, cout, cin_k, npad
+            it.Cin_pad, it.Cout_pad = (cin_pad, cout_pad) if wd is not None else (0, 0)
+            self._keep.append((w, wf, wd))
+            ci_hi = max(cin_k, it.Cin_pad)
+            co_hi = max(npad, it.Cout_pad)
+            for tap in range(khw):
+                for ci0 in range(0, ci_hi, 64):
+                    for co0 in range(0, co_hi, 64):
+                        tiles.append((i, tap, ci0, co0))
+        raw = bytes(items)
+        self.items = torch.frombuffer(bytearray(raw), dtype=torch.uint8).to(device)
+        self.tiles = torch.tensor(tiles, dtype=torch.int32, device=device)
+        self.ntiles = len(tiles)
+
+    def run(self):
+        _lib.call("cvl_pack_conv_weights_multi", ptr(self.items), ptr(self.tiles), self.ntiles, stream())
+
+
 def im2col(x, KH, KW, stride, pad_t, pad_l, Ho, Wo, Kp, out):
     B, H, W, C = x.shape
     _lib.call("cvl_im2col", ptr(x), B, H, W, C, KH, KW, stride, pad_t, pad_l, Ho, Wo, Kp, ptr(out), stream())
@@ -123,9 +160,10 @@ def add(a, b, out):
 
 
 def bias_grad(dy, ld, coff, ncol, base, img_stride, HW, B, db, beta=0.0):
-    ws = torch.empty(ncol, dtype=torch.float64, device=dy.device)
-    _lib.call("cvl_bias_grad", ptr(dy), ld, coff, ncol, int(base), int(img_stride), HW, B, ptr(ws), ptr(db),
-              float(beta), stream())
+    n = int(_lib.load().cvl_bias_grad_workspace_size(ncol, HW, B))
+    ws = torch.empty(max(n, 16), dtype=torch.uint8, device=dy.device)
+    _lib.call("cvl_bias_grad", ptr(dy), ld, coff, ncol, int(base), int(img_stride), HW, B, ptr(ws), ws.numel(),
+              ptr(db), float(beta), stream())
 
 
 def sgd_clip_update(w, g, v, lr_dev, momentum, inv_bs, clip, ws=None):

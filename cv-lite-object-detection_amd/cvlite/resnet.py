@@ -11,7 +11,7 @@ C4 = conv4_block6_out, C5 = conv5_block3_out.
 import torch
 
 from . import ops_nn as nn
-from .layers import BF16, BatchNorm, Conv, ConvBN
+from .layers import BF16, BatchNorm, Conv, ConvBN, StatsArena
 
 STEM_K = 7
 STEM_KP = 160      # im2col K = 7*7*3 = 147 padded to a multiple of 32
@@ -25,23 +25,29 @@ class Stem(object):
                          cin_k=STEM_KP)
         self.bn = BatchNorm(store, "conv1_bn", 64)
 
-    def pack(self):
+    def pack_entry(self):
+        # HWIO [7][7][3][64] == [1][1][147][64]: pack as a 1x1 conv with 147 -> 160 channels
         c = self.conv
         if c.wf is None:
             c.wf = torch.empty((64, STEM_KP), dtype=BF16, device=c.store.flat.device)
-        # HWIO [7][7][3][64] == [1][1][147][64]: pack as a 1x1 conv with 147 -> 160 channels
+        return (c.w, 1, 147, 64, STEM_KP, 64, c.wf, 0, 0, None)
+
+    def pack(self):
+        c = self.conv
+        self.pack_entry()
         nn.pack_conv_weights(c.w, 1, 1, 147, 64, STEM_KP, 64, c.wf)
 
     def _desc(self, B, Ho, Wo):
         return nn.make_desc(nn.FWD, B, STEM_KP, 1, 1, 1, 0, 0, 64, 64, 64,
                             [nn.seg(Ho, Wo, Ho, Wo, self.conv.wf, self.conv.b)])
 
-    def forward(self, x, train=True):
+    def forward(self, x, train=True, arena=None):
         B, H, W, _ = x.shape
         Ho, Wo, pt, pl = self.conv.out_hw(H, W)
         A = torch.empty((B * Ho * Wo, STEM_KP), dtype=BF16, device=x.device)
         nn.im2col(x, STEM_K, STEM_K, 2, pt, pl, Ho, Wo, STEM_KP, A)
-        stats = torch.zeros((B, 64, 2), dtype=torch.float64, device=x.device)
+        stats = arena.take(B, 64) if arena is not None else torch.zeros((B, 64, 2), dtype=torch.float64,
+                                                                          device=x.device)
         z = torch.empty((B, Ho, Wo, 64), dtype=BF16, device=x.device)
         nn.conv_igemm(self._desc(B, Ho, Wo), A, z, stats)
         mr = torch.empty((B, 64, 2), dtype=torch.float32, device=x.device)
@@ -81,16 +87,16 @@ class Bottleneck(object):
     def units(self):
         return [u for u in (self.sc, self.c1, self.c2, self.c3) if u is not None]
 
-    def forward(self, x, B, H, W, train=True):
+    def forward(self, x, B, H, W, train=True, arena=None):
         sv_s = None
         if self.sc is not None:
-            s, sv_s = self.sc.forward(x, B, H, W, relu=False, train=train)
+            s, sv_s = self.sc.forward(x, B, H, W, relu=False, train=train, arena=arena)
         else:
             s = x
-        y1, sv1 = self.c1.forward(x, B, H, W, relu=True, train=train)
+        y1, sv1 = self.c1.forward(x, B, H, W, relu=True, train=train, arena=arena)
         H1, W1 = sv1[7], sv1[8]
-        y2, sv2 = self.c2.forward(y1, B, H1, W1, relu=True, train=train)
-        y3, sv3 = self.c3.forward(y2, B, H1, W1, relu=True, residual=s, train=train)
+        y2, sv2 = self.c2.forward(y1, B, H1, W1, relu=True, train=train, arena=arena)
+        y3, sv3 = self.c3.forward(y2, B, H1, W1, relu=True, residual=s, train=train, arena=arena)
         return y3, H1, W1, (sv_s, sv1, sv2, sv3)
 
     def backward(self, dy, saved, dx_out=None, dx_beta=0.0):
@@ -140,6 +146,13 @@ class ResNet50(object):
                 out += [u.bn for u in b.units()]
         return out
 
+    def pack_entries(self):
+        out = [self.stem.pack_entry()]
+        for st in self.stages:
+            for b in st:
+                out += [u.conv.pack_entry() for u in b.units()]
+        return out
+
     def pack(self):
         self.stem.pack()
         for st in self.stages:
@@ -150,13 +163,14 @@ class ResNet50(object):
     def forward(self, x, train=True):
         """x: fp32 NHWC [B,H,W,3] in [-1,1].  Returns [C3, C4, C5] bf16 NHWC and saved state."""
         B = x.shape[0]
-        h, sv_stem = self.stem.forward(x, train)
+        arena = StatsArena(2 * B * sum(bn.c for bn in self.bns()), x.device)
+        h, sv_stem = self.stem.forward(x, train, arena)
         H, W = h.shape[1], h.shape[2]
         saved, taps = [], []
         for st in self.stages:
             ssv = []
             for b in st:
-                h, H, W, sv = b.forward(h, B, H, W, train)
+                h, H, W, sv = b.forward(h, B, H, W, train, arena)
                 ssv.append(sv)
             saved.append(ssv)
             taps.append((h, H, W))

@@ -131,6 +131,19 @@ int cvl_conv_wgrad(const cvl_conv_desc* d, const void* x, const void* dy, float*
 int cvl_pack_conv_weights(const float* w_hwio, int KH, int KW, int Cin, int Cout, int Cin_k, int Npad,
                           void* w_fwd, int Cin_pad, int Cout_pad, void* w_dgrad, cvl_stream_t stream);
 
+/* Batched form of cvl_pack_conv_weights: every conv of a network in ONE launch (run after each
+ * optimizer step).  items: DEVICE array of cvl_pack_item; tiles: DEVICE int32 [ntiles][4] =
+ * (item, tap, ci0, co0), one per 64x64 (Cin x Cout) block of each tap, covering ci < max(Cin_k,
+ * Cin_pad) and co < max(Npad, Cout_pad) (multiples of 64 from 0).  Cin_k, Cin_pad, Cout_pad % 8 == 0. */
+typedef struct {
+  const float* w;      /* HWIO fp32 master [KH*KW][Cin][Cout] */
+  void* w_fwd;         /* bf16 [Npad][KHW*Cin_k] or NULL */
+  void* w_dgrad;       /* bf16 [Cin_pad][KHW*Cout_pad] or NULL */
+  int KHW, Cin, Cout, Cin_k, Npad, Cin_pad, Cout_pad, pad_;
+} cvl_pack_item;
+int cvl_pack_conv_weights_multi(const cvl_pack_item* items, const int32_t* tiles, int ntiles,
+                                cvl_stream_t stream);
+
 /* fp32 NHWC image -> bf16 im2col rows [B*Ho*Wo][Kp] (ResNet50 conv1 after ZeroPadding2D(3)). */
 int cvl_im2col(const float* x, int B, int H, int W, int C, int KH, int KW, int stride, int pad_t,
                int pad_l, int Ho, int Wo, int Kp, void* out, cvl_stream_t stream);
@@ -146,8 +159,8 @@ int cvl_bn_apply(const void* z, const float* mean_rstd, const float* gamma, cons
                  const void* residual, void* y, int B, int HW, int C, int relu, cvl_stream_t stream);
 /* dy: grad of y; y_relu: y when the unit ends in ReLU (mask), else NULL; writes dz (bf16),
  * optionally g_out = masked dy (the residual branch's gradient), dgamma/dbeta (= + beta_acc*old)
- * and, if conv_dbias != NULL, the gradient of the preceding conv's bias (= column sum of dz,
- * fused).  workspace >= cvl_bn_backward_workspace_size(B, HW, C) bytes; reductions are
+ * and, if conv_dbias != NULL, the gradient of the preceding conv's bias, which is exactly 0
+ * behind training-mode BN (the per-image mean subtraction cancels any constant shift of z).  workspace >= cvl_bn_backward_workspace_size(B, HW, C) bytes; reductions are
  * deterministic (per-block partials summed in a fixed order, no atomics). */
 size_t cvl_bn_backward_workspace_size(int B, int HW, int C);
 int cvl_bn_backward(const void* dy, const void* y_relu, const void* z, const float* mean_rstd,
@@ -168,9 +181,12 @@ int cvl_upsample2x_backward(const void* dout, void* db, int B, int H, int W, int
                             cvl_stream_t stream);
 int cvl_relu_backward(const void* dy, const void* y, void* dx, long n, float beta, cvl_stream_t stream);
 int cvl_add(const void* a, const void* b, void* out, long n, cvl_stream_t stream);
-/* bias gradient over a segment's rows: db[c] = beta*db + sum dy[row][coff + c], acc_ws float64[ncol] */
+/* bias gradient over a segment's rows: db[c] = beta*db + sum dy[row][coff + c] (rows base +
+ * b*img_stride + q, q < HW); deterministic (per-block partials summed in a fixed order).  Needs
+ * ld, coff % 8 == 0 and coff + round_up(ncol, 8) <= ld; workspace >= *_workspace_size bytes. */
+size_t cvl_bias_grad_workspace_size(int ncol, int HW, int B);
 int cvl_bias_grad(const void* dy, int ld, int coff, int ncol, int64_t base, int64_t img_stride, int HW,
-                  int B, double* acc_ws, float* db, float beta, cvl_stream_t stream);
+                  int B, void* workspace, size_t workspace_bytes, float* db, float beta, cvl_stream_t stream);
 
 /* ------------------------------------------------------------------------------------------
  * Optimizer (train_fcos.py:179-185): g <- (g * inv_bs) clipped by global norm `clip`

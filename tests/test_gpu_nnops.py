@@ -66,8 +66,9 @@ def test_bn_forward_backward(B, HW, C, relu, res):
                    B, HW, C, conv_dbias=cdb)
     scale = zz.grad.abs().max().item()
     torch.testing.assert_close(dz.double().cpu(), zz.grad, rtol=2e-2, atol=2e-2 * scale)
-    # fused conv-bias gradient = column sum of the stored dz (mathematically ~0 behind BN)
-    torch.testing.assert_close(cdb.double().cpu(), dz.double().cpu().sum((0, 1)), rtol=1e-4, atol=1e-4 * scale)
+    # gradient of the preceding conv's bias: exactly 0 behind training-mode BN (fp64 autograd agrees)
+    assert torch.count_nonzero(cdb).item() == 0
+    torch.testing.assert_close(cdb.double().cpu(), zz.grad.sum((0, 1)), rtol=0, atol=1e-8 * scale * B * HW)
     if relu:
         torch.testing.assert_close(gout.double().cpu(), dy * (y.double().cpu() > 0))
     torch.testing.assert_close(dgam.double().cpu(), gg.grad, rtol=2e-2, atol=2e-2 * gg.grad.abs().max().item())
@@ -120,6 +121,13 @@ def test_relu_bwd_bias_grad_sgd_lr():
     db = torch.ones(20, device="cuda")
     nn.bias_grad(t.to(BF).cuda(), ld, 0, 20, 10, P, 16, B, db, beta=1.0)
     torch.testing.assert_close(db.double().cpu(), 1 + t[:, 10:26, :20].sum((0, 1)), rtol=1e-5, atol=1e-4)
+    for (B, P, ld, coff, ncol, base, HW) in ((16, 5456, 32, 0, 5, 4096, 1024), (16, 5456, 256, 0, 256, 0, 4096),
+                                             (2, 777, 64, 8, 40, 3, 700)):
+        t = bfr(torch.randn(B, P, ld, generator=g, dtype=torch.float64))
+        db = torch.zeros(ncol, device="cuda")
+        nn.bias_grad(t.to(BF).cuda(), ld, coff, ncol, base, P, HW, B, db)
+        exp = t[:, base:base + HW, coff:coff + ncol].sum((0, 1))
+        torch.testing.assert_close(db.double().cpu(), exp, rtol=1e-5, atol=1e-3)
     # clip + SGD (Keras form), lr from device memory
     n = 100003
     w = torch.randn(n, generator=g)
@@ -144,3 +152,30 @@ def test_relu_bwd_bias_grad_sgd_lr():
         exp = max(5e-4 * math.pow(0.9, int(s / 1000)), 1e-5)
         assert abs(lrd.item() - np.float32(exp)) == 0, (s, lrd.item(), exp)
         assert step.item() == s + 1
+
+
+def test_pack_multi_matches_single():
+    """cvl_pack_conv_weights_multi (one launch for every conv) == per-conv cvl_pack_conv_weights."""
+    from cvlite import ops_nn as nn
+    g = torch.Generator().manual_seed(11)
+    specs = [(3, 256, 256, 256, 256, 256, 256), (1, 1024, 256, 1024, 256, 1024, 256), (3, 256, 20, 256, 32, 256, 32),
+             (3, 256, 5, 256, 32, 256, 32), (1, 147, 64, 160, 64, 0, 0), (3, 2048, 256, 2048, 256, 2048, 256),
+             (7, 96, 40, 96, 64, 96, 64)]
+    entries, ref = [], []
+    for (k, cin, cout, cin_k, npad, cin_pad, cout_pad) in specs:
+        w = torch.randn(k, k, cin, cout, generator=g).cuda()
+        khw = k * k
+        wf = torch.full((npad, khw * cin_k), 7.0, dtype=BF, device="cuda")
+        wd = torch.full((cin_pad, khw * cout_pad), 7.0, dtype=BF, device="cuda") if cin_pad else None
+        entries.append((w, khw, cin, cout, cin_k, npad, wf, cin_pad, cout_pad, wd))
+        rf = torch.empty_like(wf)
+        rd = torch.empty_like(wd) if wd is not None else None
+        nn.pack_conv_weights(w, k, k, cin, cout, cin_k, npad, rf, cin_pad, cout_pad, rd)
+        ref.append((rf, rd))
+    plan = nn.PackPlan(entries, "cuda")
+    plan.run()
+    torch.cuda.synchronize()
+    for e, (rf, rd) in zip(entries, ref):
+        assert torch.equal(e[6], rf)
+        if rd is not None:
+            assert torch.equal(e[9], rd)
