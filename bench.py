@@ -94,6 +94,22 @@ def measure_tower_conv(net, B, H, W, iters=20):
     return ms, flops
 
 
+PMC_FILE = "profiles/r01_pmc_tower_conv.json"
+
+
+def pmc_traffic():
+    """Per-launch HBM bytes of the dominant kernel, measured by tools/pmc_tower.sh (committed)."""
+    p = os.path.join(ROOT, PMC_FILE)
+    if not os.path.exists(p):
+        return None
+    return int(json.load(open(p))["hbm_bytes"])
+
+
+def tower_alg_bytes(B, net, H, W):
+    P = net.layout(B, H, W)[2]
+    return 2 * (2 * B * P * 256) + 2 * 256 * 9 * 256
+
+
 def cpu_baseline(H, W, n_img=2):
     """The torch-CPU restatement of the reference step (oracle/model_ref.py: batch-1 forwards,
     per-image BN, gradient sum, /bs, clip, Keras SGD) on a bounded sample."""
@@ -179,7 +195,10 @@ def main():
                    "model": "FCOS-ResNet50-FPN", "global_batch": B * world, "image_size": H,
                    "parallelism": "dp%d" % world},
         "roofline": {"bound": "mfma", "achieved": round(achieved, 2), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
-                     "frac": round(achieved / PEAK_BF16_TFLOPS, 4), "traffic": None,
+                     "frac": round(achieved / PEAK_BF16_TFLOPS, 4), "traffic": pmc_traffic(),
+                     "traffic_note": "HBM bytes per launch from rocprofv3 --pmc FETCH_SIZE (x2, gfx950) + "
+                                     "WRITE_SIZE, separate passes (tools/pmc_tower.sh -> %s); algorithmic "
+                                     "bytes per launch %d (src + dst bf16 + weights)" % (PMC_FILE, tower_alg_bytes(B, net, H, W)),
                      "kernel": "conv_igemm_kernel fwd, shared FCOS tower 3x3 256->256 over all 5 levels "
                                "(M=%d, N=256, K=2304), %.3f ms/launch" % (B * net.layout(B, H, W)[2], k_ms)},
         "model_flops_per_image": fl_img,

@@ -1,0 +1,24 @@
+"""Run the bench's dominant kernel (shared FCOS tower 3x3 conv fwd over all five FPN levels,
+bs=16, 512x512) N times on its own -- the target of the rocprofv3 --pmc passes whose HBM
+byte counts become bench.py's roofline.traffic.  usage: tower_conv.py [iters]"""
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "cv-lite-object-detection_amd")]
+import torch  # noqa: E402
+
+import bench  # noqa: E402
+from cvlite.fcos_net import FCOSNet  # noqa: E402
+
+
+def main():
+    iters = int(sys.argv[1]) if len(sys.argv) > 1 else 20
+    net = FCOSNet(bench.NUM_CLASSES, device="cuda", seed=0)
+    ms, fl = bench.measure_tower_conv(net, 16, 512, 512, iters=iters)
+    torch.cuda.synchronize()
+    print("tower conv %.4f ms/launch, %.1f TFLOP/s" % (ms, fl / ms / 1e9))
+
+
+if __name__ == "__main__":
+    main()
