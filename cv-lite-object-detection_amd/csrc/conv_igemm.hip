@@ -574,7 +574,7 @@ extern "C" int cvl_conv_igemm(const cvl_conv_desc* d, const void* src, void* dst
   if (bn_stats) {
     for (int i = 0; i < a.nseg; ++i) {
       const int hw = a.seg[i].Hr * a.seg[i].Wr;
-      CVL_CHECK_ARG(hw % BM == 0 || (BM % hw == 0 && hw % 4 == 0));
+      CVL_CHECK_ARG(hw % BM == 0 || hw % 4 == 0);   // quads of rows never straddle images
     }
   }
   {

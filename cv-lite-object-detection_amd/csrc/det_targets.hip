@@ -324,6 +324,27 @@ struct DetLossArgs {
   float grad_scale_cls, grad_scale_reg;
 };
 
+// one focal-loss element (alpha .25, gamma 2, the stable form of retinanet_module.py:367-386 /
+// fcos.py:443-462): returns the loss, *g = d loss / d logit
+__device__ __forceinline__ float focal_elem(float y, float x, float* g) {
+  const float e = expf(-fabsf(x));
+  const float L = log1pf(e);
+  const float p1 = x >= 0.f ? 1.0f / (1.0f + e) : e / (1.0f + e);
+  const float q1 = x >= 0.f ? e / (1.0f + e) : 1.0f / (1.0f + e);
+  const float nlp = L - fminf(x, 0.f), nlq = L + fmaxf(x, 0.f);
+  *g = -y * 0.25f * q1 * q1 * (2.0f * p1 * nlp + q1) + (1.0f - y) * 0.75f * p1 * p1 * (2.0f * q1 * nlq + p1);
+  return y * 0.25f * q1 * q1 * nlp + (1.0f - y) * 0.75f * p1 * p1 * nlq;
+}
+
+// one (discontinuous, Q8) smooth-L1 element, delta 1: returns the loss, *g = d loss / d pred
+__device__ __forceinline__ float sl1_elem(float t, float x, float* g) {
+  const float d = t - x;
+  const float ad = fabsf(d);
+  if (ad < 1.0f) { *g = -d; return 0.5f * d * d; }
+  *g = d > 0.f ? -1.0f : (d < 0.f ? 1.0f : 0.0f);
+  return ad;
+}
+
 __global__ void __launch_bounds__(NT) det_loss_kernel(DetLossArgs a) {
   const int b = blockIdx.y;
   const int p = blockIdx.x * NT + threadIdx.x;
@@ -337,25 +358,14 @@ __global__ void __launch_bounds__(NT) det_loss_kernel(DetLossArgs a) {
     for (int c = 0; c < a.C; ++c) {
       const float y = t[4 + c];
       tmax = fmaxf(tmax, y);
-      const float x = xc[c];
-      const float e = expf(-fabsf(x));
-      const float L = log1pf(e);
-      const float p1 = x >= 0.f ? 1.0f / (1.0f + e) : e / (1.0f + e);
-      const float q1 = x >= 0.f ? e / (1.0f + e) : 1.0f / (1.0f + e);
-      const float nlp = L - fminf(x, 0.f), nlq = L + fmaxf(x, 0.f);
-      s_cls += y * 0.25f * q1 * q1 * nlp + (1.0f - y) * 0.75f * p1 * p1 * nlq;
-      if (a.dcls) {
-        const float g = -y * 0.25f * q1 * q1 * (2.0f * p1 * nlp + q1) + (1.0f - y) * 0.75f * p1 * p1 * (2.0f * q1 * nlq + p1);
-        a.dcls[cell * a.ld_cls + c] = g * a.grad_scale_cls;
-      }
+      float g;
+      s_cls += focal_elem(y, xc[c], &g);
+      if (a.dcls) a.dcls[cell * a.ld_cls + c] = g * a.grad_scale_cls;
     }
     const float mask = tmax > 0.f ? 1.0f : 0.0f;                 // max(class) > 0
     for (int j = 0; j < 4; ++j) {
-      const float d = t[j] - xr[j];
-      const float ad = fabsf(d);
       float g;
-      if (ad < 1.0f) { s_reg += mask * 0.5f * d * d; g = -d; }
-      else { s_reg += mask * ad; g = d > 0.f ? -1.0f : (d < 0.f ? 1.0f : 0.0f); }
+      s_reg += mask * sl1_elem(t[j], xr[j], &g);
       if (a.dreg) a.dreg[cell * a.ld_reg + j] = mask * g * a.grad_scale_reg;
     }
   }
@@ -368,6 +378,70 @@ __global__ void __launch_bounds__(NT) det_loss_kernel(DetLossArgs a) {
     double s = 0.0;
     for (int k = 0; k < NT / 64; ++k) s += red[threadIdx.x][k];
     a.partial[((size_t)b * a.tiles + blockIdx.x) * 2 + threadIdx.x] = s;
+  }
+}
+
+// RetinaNet.train_loss (retinanet_module.py:403-426) over every (level, anchor) at once, fwd + bwd.
+// Predictions come straight from the grouped head convs: row (level offset + cell) of [B][P][ld],
+// class channels a*C + c, box channels a*4 + j.  Targets are cvl_retina_assign's [B][A*P][4+C] in
+// (level, anchor, cell) order.  Gradients are written as bf16 (the head backward's operand);
+// img_weight[b] (0/1, nullable) drops images the reference loop skipped (no matches,
+// train_retinanet_coco.py:203-208) from both the loss and the gradient.
+struct RetinaLossArgs {
+  const float* reg;
+  const float* cls;
+  const float* tgt;
+  const float* img_w;
+  double* partial;
+  cvl_bf16* dreg;
+  cvl_bf16* dcls;
+  int ld_reg, ld_cls, ld_dreg, ld_dcls, P, A, C, tiles;
+  int off[6];          // per-image cell offsets of the 5 levels (+ P)
+  float grad_scale;
+};
+
+__global__ void __launch_bounds__(NT) retina_loss_kernel(RetinaLossArgs a) {
+  const int b = blockIdx.y;
+  const int i = blockIdx.x * NT + threadIdx.x;
+  float s_cls = 0.f, s_reg = 0.f;
+  const float wb = a.img_w ? a.img_w[b] : 1.0f;
+  if (i < a.P * a.A) {
+    const int cell = i / a.A, an = i - (i / a.A) * a.A;
+    int l = 0;
+#pragma unroll
+    for (int k = 1; k < 5; ++k)
+      if (cell >= a.off[k]) l = k;
+    const int S2 = a.off[l + 1] - a.off[l];
+    const size_t t_row = (size_t)b * a.P * a.A + (size_t)a.A * a.off[l] + (size_t)an * S2 + (cell - a.off[l]);
+    const float* t = a.tgt + t_row * (4 + a.C);
+    const size_t prow = (size_t)b * a.P + cell;
+    const float* xr = a.reg + prow * a.ld_reg + an * 4;
+    const float* xc = a.cls + prow * a.ld_cls + (size_t)an * a.C;
+    const float gs = a.grad_scale * wb;
+    float tmax = 0.f;
+    for (int c = 0; c < a.C; ++c) {
+      const float y = t[4 + c];
+      tmax = fmaxf(tmax, y);
+      float g;
+      s_cls += focal_elem(y, xc[c], &g);
+      if (a.dcls) a.dcls[prow * a.ld_dcls + (size_t)an * a.C + c] = f32_to_bf16(g * gs);
+    }
+    const float mask = tmax > 0.f ? 1.0f : 0.0f;
+    for (int j = 0; j < 4; ++j) {
+      float g;
+      s_reg += mask * sl1_elem(t[j], xr[j], &g);
+      if (a.dreg) a.dreg[prow * a.ld_dreg + an * 4 + j] = f32_to_bf16(mask * g * gs);
+    }
+  }
+  __shared__ double red[2][NT / 64];
+  double v0 = warp_sum_d((double)s_cls), v1 = warp_sum_d((double)s_reg);
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  if (lane == 0) { red[0][w] = v0; red[1][w] = v1; }
+  __syncthreads();
+  if (threadIdx.x < 2) {
+    double s = 0.0;
+    for (int k = 0; k < NT / 64; ++k) s += red[threadIdx.x][k];
+    a.partial[((size_t)b * a.tiles + blockIdx.x) * 2 + threadIdx.x] = s * (double)wb;
   }
 }
 
@@ -523,6 +597,39 @@ extern "C" int cvl_det_loss(const float* reg_pred, int ld_reg, const float* cls_
   a.tiles = (P + NT - 1) / NT;
   a.grad_scale_cls = grad_scale_cls; a.grad_scale_reg = grad_scale_reg;
   hipLaunchKernelGGL(det_loss_kernel, dim3(a.tiles, B), dim3(NT), 0, S_, a);
+  hipLaunchKernelGGL(det_loss_finalize, dim3(B), dim3(64), 0, S_, (const double*)workspace, losses, a.tiles);
+  return cvl_launch_status();
+}
+
+extern "C" size_t cvl_retina_loss_workspace_size(int B, int P, int n_anchors) {
+  return (size_t)B * (((size_t)P * n_anchors + NT - 1) / NT) * 2 * sizeof(double);
+}
+
+extern "C" int cvl_retina_loss(const float* reg_pred, int ld_reg, const float* cls_pred, int ld_cls,
+                               const float* targets, int B, const int32_t* level_cells, int n_anchors,
+                               int num_classes, const float* img_weight, float grad_scale, float* losses,
+                               void* d_reg, int ld_dreg, void* d_cls, int ld_dcls, void* workspace,
+                               cvl_stream_t stream) {
+  CVL_CHECK_ARG(reg_pred && cls_pred && targets && losses && workspace && level_cells && B > 0);
+  CVL_CHECK_ARG(n_anchors > 0 && num_classes > 0 && ld_reg >= 4 * n_anchors && ld_cls >= n_anchors * num_classes);
+  CVL_CHECK_ARG(!d_reg || ld_dreg >= 4 * n_anchors);
+  CVL_CHECK_ARG(!d_cls || ld_dcls >= n_anchors * num_classes);
+  RetinaLossArgs a;
+  a.reg = reg_pred; a.cls = cls_pred; a.tgt = targets; a.img_w = img_weight;
+  a.partial = (double*)workspace;
+  a.dreg = (cvl_bf16*)d_reg; a.dcls = (cvl_bf16*)d_cls;
+  a.ld_reg = ld_reg; a.ld_cls = ld_cls; a.ld_dreg = ld_dreg; a.ld_dcls = ld_dcls;
+  a.A = n_anchors; a.C = num_classes; a.grad_scale = grad_scale;
+  int o = 0;
+  for (int l = 0; l < 5; ++l) {
+    CVL_CHECK_ARG(level_cells[l] > 0);
+    a.off[l] = o;
+    o += level_cells[l];
+  }
+  a.off[5] = o;
+  a.P = o;
+  a.tiles = (int)(((long)a.P * a.A + NT - 1) / NT);
+  hipLaunchKernelGGL(retina_loss_kernel, dim3(a.tiles, B), dim3(NT), 0, S_, a);
   hipLaunchKernelGGL(det_loss_finalize, dim3(B), dim3(64), 0, S_, (const double*)workspace, losses, a.tiles);
   return cvl_launch_status();
 }

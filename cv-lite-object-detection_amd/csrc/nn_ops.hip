@@ -641,6 +641,24 @@ __global__ void lr_schedule_kernel(int* step, float* lr, double init_lr, double 
   *step = s + 1;
 }
 
+// RetinaNet candidate selection (train_retinanet_coco.py:190-209): the first k of n candidates
+// (in order) whose target count is non-zero; slots left empty get weight 0 (and index 0)
+__global__ void select_first_nonzero_kernel(const int32_t* counts, int n, int k, int32_t* idx, float* w) {
+  if (threadIdx.x != 0) return;
+  int j = 0;
+  for (int i = 0; i < n && j < k; ++i)
+    if (counts[i] > 0) { idx[j] = i; w[j] = 1.0f; ++j; }
+  for (; j < k; ++j) { idx[j] = 0; w[j] = 0.0f; }
+}
+
+// dst row i = src row idx[i] (16-byte vectors; one workgroup row-slice per (chunk, row))
+__global__ void gather_rows_kernel(const int4* src, long row16, const int32_t* idx, int4* dst) {
+  const int r = blockIdx.y;
+  const int4* s = src + (long)idx[r] * row16;
+  int4* d = dst + (long)r * row16;
+  for (long i = blockIdx.x * (long)NT + threadIdx.x; i < row16; i += (long)gridDim.x * NT) d[i] = s[i];
+}
+
 }  // namespace
 
 // ---------------------------------------------------------------------------------------------
@@ -831,5 +849,21 @@ extern "C" int cvl_lr_schedule(int32_t* step, float* lr, double init_lr, double 
   CVL_CHECK_ARG(step && lr && decay_step > 0);
   hipLaunchKernelGGL(lr_schedule_kernel, dim3(1), dim3(1), 0, S_, step, lr, init_lr, min_lr, decay_rate,
                      decay_step);
+  return cvl_launch_status();
+}
+
+extern "C" int cvl_select_first_nonzero(const int32_t* counts, int n, int k, int32_t* idx, float* weight,
+                                        cvl_stream_t stream) {
+  CVL_CHECK_ARG(counts && idx && weight && n > 0 && k > 0);
+  hipLaunchKernelGGL(select_first_nonzero_kernel, dim3(1), dim3(64), 0, S_, counts, n, k, idx, weight);
+  return cvl_launch_status();
+}
+
+extern "C" int cvl_gather_rows(const void* src, int64_t row_bytes, const int32_t* idx, int n, void* dst,
+                               cvl_stream_t stream) {
+  CVL_CHECK_ARG(src && dst && idx && n > 0 && row_bytes > 0 && row_bytes % 16 == 0);
+  const long row16 = row_bytes / 16;
+  hipLaunchKernelGGL(gather_rows_kernel, dim3(grid_for(row16, NT, 1024), n), dim3(NT), 0, S_,
+                     reinterpret_cast<const int4*>(src), row16, idx, reinterpret_cast<int4*>(dst));
   return cvl_launch_status();
 }

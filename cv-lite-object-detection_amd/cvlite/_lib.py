@@ -47,11 +47,16 @@ SIGNATURES = {
                               P, c_float, P]),
     "cvl_sgd_clip_update": (c_int, [P, P, P, ctypes.c_int64, P, c_float, c_float, c_float, P, P]),
     "cvl_lr_schedule": (c_int, [P, P, ctypes.c_double, ctypes.c_double, ctypes.c_double, c_int, P]),
+    "cvl_select_first_nonzero": (c_int, [P, c_int, c_int, P, P, P]),
+    "cvl_gather_rows": (c_int, [P, ctypes.c_int64, P, c_int, P, P]),
     "cvl_retina_assign": (c_int, [P, P, P, c_int, c_int, c_int, c_int, P, c_int, P, c_float, P, P, P]),
     "cvl_centernet_assign": (c_int, [P, P, P, c_int, c_int, c_int, c_int, c_int, c_int, P, P]),
     "cvl_centernet_splat": (c_int, [P, P, P, c_int, c_int, c_int, c_int, c_int, c_int, c_float, P, P]),
     "cvl_det_loss_workspace_size": (c_size_t, [c_int, c_int]),
     "cvl_det_loss": (c_int, [P, c_int, P, c_int, P, c_int, c_int, c_int, c_float, c_float, P, P, P, P, P]),
+    "cvl_retina_loss_workspace_size": (c_size_t, [c_int, c_int, c_int]),
+    "cvl_retina_loss": (c_int, [P, c_int, P, c_int, P, c_int, P, c_int, c_int, P, c_float, P, P, c_int, P, c_int,
+                                P, P]),
     "cvl_nms_workspace_size": (c_size_t, [c_int, c_int]),
     "cvl_nms": (c_int, [P, c_int, P, c_int, ctypes.c_double, P, P, P, P]),
 }

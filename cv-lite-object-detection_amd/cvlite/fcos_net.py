@@ -1,141 +1,37 @@
 """FCOS ResNet-50-FPN network (FCOS/fcos.py:6-110) on the cvlite kernels, explicit fwd/bwd.
 
-MI355X layout decisions:
-* P3..P7 live in ONE packed, level-major bf16 buffer [sum_l B*S_l^2, 256]; each shared tower
-  layer (`cls_layer_k` / `reg_layer_k`, fcos.py:16-27) is one segmented MFMA launch over all five
-  levels (shared weights), forward, data-gradient and weight-gradient (the weight gradient reduces
-  over all levels and images at once — the reference loops levels in Python, fcos.py:78-101).
-* The per-level heads (`logits_output_l`, `reg_output_l`, fcos.py:85-101) are one segmented launch
-  each (per-segment weights) writing fp32 straight into the loss layout [B, P, ld] (P = sum S^2,
-  level-major cells), so the concat of fcos.py:104-108 disappears.
-* c7_3x3 reads relu(P6) through the conv's relu-on-load flag (fcos.py:70-72).
+Trunk (backbone, FPN, shared towers): fpn_det.FPNDetector.  The per-level heads
+(`logits_output_l`, `reg_output_l`, fcos.py:85-101) are one segmented launch each (per-segment
+weights) writing fp32 straight into the loss layout [B, P, ld] (P = sum S^2, level-major cells),
+so the concat of fcos.py:104-108 disappears.
 """
 import math
 
 import torch
 
 from . import ops_nn as nn
-from .layers import BF16, Conv, ParamStore
-from .resnet import ResNet50
-
-FPN_C = 256
-STRIDES = (8, 16, 32, 64, 128)
+from .fpn_det import FPN_C, STRIDES, FPNDetector  # noqa: F401
+from .layers import Conv
 
 
-class FCOSNet(object):
+class FCOSNet(FPNDetector):
     def __init__(self, num_classes, backbone_model="resnet50", device="cuda", seed=0):
-        if backbone_model.lower() != "resnet50":
-            raise NotImplementedError("cvlite implements the resnet50 backbone of fcos.build_model")
-        self.C = num_classes
-        self.store = st = ParamStore()
-        self._build_layers(st, num_classes)
+        self._init_common(num_classes, backbone_model, device, seed)
         self.cls_ld = self.cls_heads[0].npad          # >= C, multiple of 32
         self.reg_ld = 8
-        st.finalize(device, seed)
-        for bn in self.backbone.bns():
-            bn.init_buffers(device)
-        self.device = device
-        self._pack_plan = None
-        self.pack()
 
-
-    def _build_layers(self, st, num_classes):
-        # creation order follows fcos.build_model: towers, backbone, FPN, heads
-        self.cls_tower = [Conv(st, "cls_layer_%d" % (i + 1), 3, FPN_C, FPN_C, bias=False) for i in range(4)]
-        self.reg_tower = [Conv(st, "reg_layer_%d" % (i + 1), 3, FPN_C, FPN_C, bias=False) for i in range(4)]
-        self.backbone = ResNet50(st)
-        self.c3_1x1 = Conv(st, "c3_1x1", 1, 512, FPN_C)
-        self.c4_1x1 = Conv(st, "c4_1x1", 1, 1024, FPN_C)
-        self.c5_1x1 = Conv(st, "c5_1x1", 1, 2048, FPN_C)
-        self.c3_3x3 = Conv(st, "c3_3x3", 3, FPN_C, FPN_C)
-        self.c4_3x3 = Conv(st, "c4_3x3", 3, FPN_C, FPN_C)
-        self.c5_3x3 = Conv(st, "c5_3x3", 3, FPN_C, FPN_C)
-        self.c6_3x3 = Conv(st, "c6_3x3", 3, 2048, FPN_C, stride=2)
-        self.c7_3x3 = Conv(st, "c7_3x3", 3, FPN_C, FPN_C, stride=2)
+    def _build_heads(self, st, num_classes):
         b_focal = math.log(0.01 / 0.99)
         self.cls_heads = [Conv(st, "logits_output_%d" % (l + 1), 3, FPN_C, num_classes, bias_init=b_focal)
                           for l in range(5)]
         self.reg_heads = [Conv(st, "reg_output_%d" % (l + 1), 3, FPN_C, 5) for l in range(5)]
 
-    @classmethod
-    def param_dict(cls, num_classes, seed=0):
-        """The initial parameters (Keras names -> CPU fp32) without touching a GPU."""
-        obj = cls.__new__(cls)
-        st = ParamStore()
-        obj._build_layers(st, num_classes)
-        st.finalize("cpu", seed)
-        return st.state_dict()
+    def head_convs(self):
+        return self.cls_heads + self.reg_heads
 
-    # ---- parameters ------------------------------------------------------------------------------
-    def all_convs(self):
-        return (self.cls_tower + self.reg_tower + self.backbone.convs()[1:] +
-                [self.c3_1x1, self.c4_1x1, self.c5_1x1, self.c3_3x3, self.c4_3x3, self.c5_3x3,
-                 self.c6_3x3, self.c7_3x3] + self.cls_heads + self.reg_heads)
-
-    def pack(self):
-        """Refresh the bf16 packed weights from the fp32 masters (after every update): one
-        batched launch over every conv (ops_nn.PackPlan)."""
-        if self._pack_plan is None:
-            entries = self.backbone.pack_entries()
-            entries += [c.pack_entry() for c in self.all_convs() if c not in self.backbone.convs()]
-            self._pack_plan = nn.PackPlan(entries, self.device)
-        self._pack_plan.run()
-
-    # ---- geometry ---------------------------------------------------------------------------------
-    @staticmethod
-    def level_shapes(H, W):
-        return [(-(-H // s), -(-W // s)) for s in STRIDES]
-
-    def layout(self, B, H, W):
-        shapes = self.level_shapes(H, W)
-        off, o = [], 0
-        for (h, w) in shapes:
-            off.append(o)
-            o += h * w
-        return shapes, off, o     # per-image cell offsets, P
-
-    def _tower_segs(self, conv, B, shapes, off, wf=True):
-        return [nn.seg(h, w, h, w, conv.wf if wf else conv.wd, None, src_base=B * off[l], src_img=h * w,
-                       dst_base=B * off[l], dst_img=h * w) for l, (h, w) in enumerate(shapes)]
-
-    # ---- forward -------------------------------------------------------------------------------------
-    def forward(self, x, train=True):
-        """x fp32 [B,H,W,3].  Returns reg [B,P,8] fp32 (t,b,l,r,centerness), cls [B,P,ld] fp32."""
-        B, H, W, _ = x.shape
-        dev = x.device
-        (C3, C4, C5), bsv = self.backbone.forward(x, train)
-        (c3, H3, W3), (c4, H4, W4), (c5, H5, W5) = C3, C4, C5
-        l3, _, _ = self.c3_1x1.fwd(c3, B, H3, W3)
-        l4, _, _ = self.c4_1x1.fwd(c4, B, H4, W4)
-        l5, _, _ = self.c5_1x1.fwd(c5, B, H5, W5)
-        p4r = torch.empty_like(l4)
-        nn.upsample2x_add(l4, l5, p4r, B, H4, W4, FPN_C)          # fcos.py:57-58
-        p3r = torch.empty_like(l3)
-        nn.upsample2x_add(l3, l4, p3r, B, H3, W3, FPN_C)          # fcos.py:59-60 (up2 of P4_1x1, Q13)
-        shapes, off, P = self.layout(B, H, W)
-        F = torch.empty((B * P, FPN_C), dtype=BF16, device=dev)
-        srcs = [(self.c3_3x3, p3r, H3, W3), (self.c4_3x3, p4r, H4, W4), (self.c5_3x3, l5, H5, W5),
-                (self.c6_3x3, c5, H5, W5)]
-        for l, (conv, src, h, w) in enumerate(srcs):
-            Ho, Wo = shapes[l]
-            d = conv.fwd_desc(B, [nn.seg(Ho, Wo, h, w, conv.wf, conv.bias_arg(), dst_base=B * off[l])],
-                              ld_dst=FPN_C)
-            nn.conv_igemm(d, src, F)
-        h6, w6 = shapes[3]
-        d = self.c7_3x3.fwd_desc(B, [nn.seg(shapes[4][0], shapes[4][1], h6, w6, self.c7_3x3.wf,
-                                            self.c7_3x3.bias_arg(), src_base=B * off[3], dst_base=B * off[4])],
-                                 ld_dst=FPN_C, relu_in=True)
-        nn.conv_igemm(d, F, F)                                      # P7 = conv(relu(P6))
-        # towers over all levels at once
-        towers = []
-        for tw in (self.cls_tower, self.reg_tower):
-            acts = [F]
-            for i, conv in enumerate(tw):
-                out = torch.empty((B * P, FPN_C), dtype=BF16, device=dev)
-                d = conv.fwd_desc(B, self._tower_segs(conv, B, shapes, off), ld_dst=FPN_C, relu_out=(i == 3))
-                nn.conv_igemm(d, acts[-1], out)
-                acts.append(out)
-            towers.append(acts)
+    def _heads_forward(self, towers, B, shapes, off, P):
+        """Returns reg [B,P,8] fp32 (t,b,l,r,centerness), cls [B,P,ld] fp32."""
+        dev = towers[0][0].device
         cls_out = torch.zeros((B, P, self.cls_ld), dtype=torch.float32, device=dev)
         reg_out = torch.zeros((B, P, self.reg_ld), dtype=torch.float32, device=dev)
         for heads, acts, out, ld in ((self.cls_heads, towers[0], cls_out, self.cls_ld),
@@ -144,20 +40,13 @@ class FCOSNet(object):
                            dst_base=off[l], dst_img=P) for l, (h, w) in enumerate(shapes)]
             d = heads[0].fwd_desc(B, segs, ld_dst=ld, dst_f32=True, n_store=heads[0].cout)
             nn.conv_igemm(d, acts[-1], out)
-        self._saved = dict(bsv=bsv, C=(C3, C4, C5), l=(l3, l4, l5), p=(p3r, p4r), F=F, towers=towers,
-                           B=B, H=H, W=W, shapes=shapes, off=off, P=P)
         return reg_out, cls_out
 
-    # ---- backward ------------------------------------------------------------------------------------
-    def backward(self, d_reg, d_cls):
-        """d_reg, d_cls: bf16 [B, P, 32] (padding channels zero) from the fused loss."""
-        s = self._saved
-        B, shapes, off, P = s["B"], s["shapes"], s["off"], s["P"]
-        dev = d_reg.device
-        F, towers = s["F"], s["towers"]
-        dF = torch.empty_like(F)
-        for ti, (heads, acts, dout) in enumerate(((self.cls_heads, towers[0], d_cls),
-                                                  (self.reg_heads, towers[1], d_reg))):
+    def _heads_backward(self, grads, towers, B, shapes, off, P):
+        """grads = (d_reg, d_cls): bf16 [B, P, 32] (padding channels zero) from the fused loss."""
+        d_reg, d_cls = grads
+        dAs = []
+        for heads, acts, dout in ((self.cls_heads, towers[0], d_cls), (self.reg_heads, towers[1], d_reg)):
             ld = int(dout.shape[-1])
             # heads: weight/bias grads per level, data grad for all levels in one launch
             for l, (h, w) in enumerate(shapes):
@@ -166,68 +55,10 @@ class FCOSNet(object):
                                            dst_base=off[l], dst_img=P)], ld_dst=ld)
                 nn.conv_wgrad(d, acts[-1], dout, hd.dw)
                 nn.bias_grad(dout, ld, 0, hd.cout, off[l], P, h * w, B, hd.db)
-            dA = torch.empty_like(F)
+            dA = torch.empty_like(acts[0])
             segs = [nn.seg(h, w, h, w, heads[l].wd, None, src_base=off[l], src_img=P, dst_base=B * off[l],
                            dst_img=h * w) for l, (h, w) in enumerate(shapes)]
             d = heads[0].dgrad_desc(B, segs, ld_dst=FPN_C)
             nn.conv_igemm(d, dout, dA)
-            nn.relu_backward(dA, acts[-1], dA)                      # the tower's final ReLU
-            tw = self.cls_tower if ti == 0 else self.reg_tower
-            for i in range(3, -1, -1):
-                conv = tw[i]
-                d = conv.fwd_desc(B, self._tower_segs(conv, B, shapes, off), ld_dst=FPN_C)
-                nn.conv_wgrad(d, acts[i], dA, conv.dw)
-                dd = conv.dgrad_desc(B, self._tower_segs(conv, B, shapes, off, wf=False), ld_dst=FPN_C,
-                                     beta=(1.0 if (i == 0 and ti == 1) else 0.0))
-                dst = dF if i == 0 else torch.empty_like(F)
-                nn.conv_igemm(dd, dA, dst)
-                dA = dst
-        # ---- FPN backward (fcos.py:49-72) ----
-        (C3, C4, C5) = s["C"]
-        (c3, H3, W3), (c4, H4, W4), (c5, H5, W5) = C3, C4, C5
-        l3, l4, l5 = s["l"]
-        p3r, p4r = s["p"]
-        h6, w6 = shapes[3]
-        h7, w7 = shapes[4]
-        # P7 = c7(relu(P6)): weights (relu on load), then d relu(P6) -> dP6 (masked, accumulated)
-        d = self.c7_3x3.fwd_desc(B, [nn.seg(h7, w7, h6, w6, self.c7_3x3.wf, None, src_base=B * off[3],
-                                            dst_base=B * off[4])], ld_dst=FPN_C, relu_in=True)
-        nn.conv_wgrad(d, F, dF, self.c7_3x3.dw)
-        nn.bias_grad(dF, FPN_C, 0, FPN_C, B * off[4], h7 * w7, h7 * w7, B, self.c7_3x3.db)
-        dr6 = torch.empty((B, h6, w6, FPN_C), dtype=BF16, device=dev)
-        dd = self.c7_3x3.dgrad_desc(B, [nn.seg(h6, w6, h7, w7, self.c7_3x3.wd, None, src_base=B * off[4])],
-                                    ld_dst=FPN_C)
-        nn.conv_igemm(dd, dF, dr6)
-        dP6 = dF[B * off[3]:B * off[4]]
-        P6 = F[B * off[3]:B * off[4]]
-        nn.relu_backward(dr6, P6, dP6, beta=1.0)
-        # c6 (stride 2 on C5), c5_3x3, c4_3x3, c3_3x3: weight/bias grads and data grads
-        dC5 = torch.empty_like(c5)
-        dl5 = torch.empty_like(l5)
-        dp4r = torch.empty_like(p4r)
-        dp3r = torch.empty_like(p3r)
-        for l, (conv, src, h, w, dsrc) in enumerate(((self.c3_3x3, p3r, H3, W3, dp3r),
-                                                     (self.c4_3x3, p4r, H4, W4, dp4r),
-                                                     (self.c5_3x3, l5, H5, W5, dl5),
-                                                     (self.c6_3x3, c5, H5, W5, dC5))):
-            Ho, Wo = shapes[l]
-            d = conv.fwd_desc(B, [nn.seg(Ho, Wo, h, w, conv.wf, None, dst_base=B * off[l])], ld_dst=FPN_C)
-            nn.conv_wgrad(d, src, dF, conv.dw)
-            nn.bias_grad(dF, FPN_C, 0, FPN_C, B * off[l], Ho * Wo, Ho * Wo, B, conv.db)
-            dd = conv.dgrad_desc(B, [nn.seg(h, w, Ho, Wo, conv.wd, None, src_base=B * off[l])],
-                                 ld_dst=conv.cin)
-            nn.conv_igemm(dd, dF, dsrc)
-        # top-down adds: p4r = l4 + up(l5); p3r = l3 + up(l4)
-        nn.upsample2x_backward(dp4r, dl5, B, H4, W4, FPN_C, beta=1.0)   # dl5 += up^T(dp4r)
-        dl4 = dp4r
-        nn.upsample2x_backward(dp3r, dl4, B, H3, W3, FPN_C, beta=1.0)   # dl4 += up^T(dp3r)
-        dl3 = dp3r
-        dC3 = torch.empty_like(c3)
-        dC4 = torch.empty_like(c4)
-        for conv, src, h, w, dl, dC, beta in ((self.c3_1x1, c3, H3, W3, dl3, dC3, 0.0),
-                                              (self.c4_1x1, c4, H4, W4, dl4, dC4, 0.0),
-                                              (self.c5_1x1, c5, H5, W5, dl5, dC5, 1.0)):
-            conv.wgrad(src, dl, B, h, w)
-            conv.dgrad(dl, B, h, w, out=dC, beta=beta)
-        self.backbone.backward([dC3, dC4, dC5], s["bsv"])
-        self._saved = None
+            dAs.append(dA)
+        return dAs

@@ -176,3 +176,14 @@ def sgd_clip_update(w, g, v, lr_dev, momentum, inv_bs, clip, ws=None):
 def lr_schedule(step_dev, lr_dev, init_lr, min_lr, decay_rate, decay_step):
     _lib.call("cvl_lr_schedule", ptr(step_dev), ptr(lr_dev), float(init_lr), float(min_lr),
               float(decay_rate), int(decay_step), stream())
+
+
+def select_first_nonzero(counts, k, idx, weight):
+    _lib.call("cvl_select_first_nonzero", ptr(counts), int(counts.numel()), int(k), ptr(idx), ptr(weight), stream())
+
+
+def gather_rows(src, idx, dst):
+    """dst[i] = src[idx[i]] along dim 0 (contiguous tensors, same row size)."""
+    row_bytes = src[0].numel() * src.element_size()
+    assert dst[0].numel() * dst.element_size() == row_bytes and src.is_contiguous() and dst.is_contiguous()
+    _lib.call("cvl_gather_rows", ptr(src), int(row_bytes), ptr(idx), int(idx.numel()), ptr(dst), stream())

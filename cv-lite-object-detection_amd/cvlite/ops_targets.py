@@ -68,7 +68,7 @@ RETINA_STRIDES = (8, 16, 32, 64, 128)    # RetinaNet/retinanet_module.py:197
 
 
 def retina_assign(boxes, nbox, img_dim, pad, anchor_dims, num_classes, iou_thresh=0.5,
-                  strides=RETINA_STRIDES, out=None):
+                  strides=RETINA_STRIDES, out=None, num_targets=None):
     """Batched RetinaNet targets.  anchor_dims: device fp32 [5, A, 2].  Returns (targets
     [B, sum_l A*S_l^2, 4+C] f32 ordered (level, anchor, u, v), num_targets [B] i32)."""
     B, nmax = _boxes_args(boxes, nbox, img_dim)
@@ -76,7 +76,7 @@ def retina_assign(boxes, nbox, img_dim, pad, anchor_dims, num_classes, iou_thres
     P = sum(A * (pad // s) ** 2 for s in strides)
     if out is None:
         out = torch.empty((B, P, 4 + num_classes), device=boxes.device, dtype=torch.float32)
-    nt = torch.empty((B,), device=boxes.device, dtype=torch.int32)
+    nt = torch.empty((B,), device=boxes.device, dtype=torch.int32) if num_targets is None else num_targets
     st = (_lib.ctypes.c_int32 * 5)(*[int(s) for s in strides])
     _lib.call("cvl_retina_assign", ptr(boxes), ptr(nbox), ptr(img_dim), B, nmax, int(pad), int(num_classes),
               ptr(anchor_dims.contiguous()), A, _lib.ctypes.cast(st, _lib.c_void_p), float(iou_thresh), ptr(out),
@@ -118,6 +118,28 @@ def det_loss(reg_pred, cls_pred, targets, num_classes, grad_scale_cls=1.0, grad_
               ptr(targets), B, P, int(num_classes), float(grad_scale_cls), float(grad_scale_reg), ptr(losses),
               ptr(d_reg), ptr(d_cls), ptr(ws), _lib.stream())
     return losses, d_reg, d_cls
+
+
+def retina_loss(reg_pred, cls_pred, targets, level_cells, n_anchors, num_classes, img_weight=None,
+                grad_scale=1.0, d_reg=None, d_cls=None, losses=None):
+    """RetinaNet.train_loss fwd+bwd (cvl_retina_loss).  reg_pred [B,P,ld>=4A] / cls_pred [B,P,ld>=AC] f32
+    from the grouped heads, targets [B, A*P, 4+C] (cvl_retina_assign order).  d_reg / d_cls: bf16
+    buffers written at the prediction positions (None = no gradient).  Returns losses [B,2]."""
+    _lib.require_cuda(reg_pred, cls_pred, targets)
+    B, P = int(reg_pred.shape[0]), int(reg_pred.shape[1])
+    assert sum(level_cells) == P and int(targets.shape[1]) == n_anchors * P
+    dev = targets.device
+    if losses is None:
+        losses = torch.empty((B, 2), device=dev, dtype=torch.float32)
+    ws = torch.empty(int(_lib.load().cvl_retina_loss_workspace_size(B, P, n_anchors)), device=dev, dtype=torch.uint8)
+    lc = (_lib.ctypes.c_int32 * 5)(*[int(c) for c in level_cells])
+    for t in (d_reg, d_cls):
+        assert t is None or t.dtype == torch.bfloat16
+    _lib.call("cvl_retina_loss", ptr(reg_pred), int(reg_pred.shape[-1]), ptr(cls_pred), int(cls_pred.shape[-1]),
+              ptr(targets), B, _lib.ctypes.cast(lc, _lib.c_void_p), int(n_anchors), int(num_classes), ptr(img_weight),
+              float(grad_scale), ptr(losses), ptr(d_reg), int(d_reg.shape[-1]) if d_reg is not None else 0,
+              ptr(d_cls), int(d_cls.shape[-1]) if d_cls is not None else 0, ptr(ws), _lib.stream())
+    return losses
 
 
 def nms(boxes_xyxy, classes, iou_threshold):

@@ -51,6 +51,39 @@ class RetinaNet(object):
             boxes.append(lev)
         self.anchor_boxes = boxes
         self._dims_dev = None
+        self._model = None
+
+    @property
+    def model(self):
+        """retinanet_module.py:199-200 `self.model = build_model(...)`: the MI355X network
+        (built on first use, so target-only users need no weights)."""
+        if self._model is None:
+            from .retina_net import RetinaNetNet
+            _lib.require_cuda()
+            self._model = RetinaNetNet(self.n_class, n_anchors=self.n_anchors, backbone_model=self.backbone_model)
+        return self._model
+
+    def train_loss(self, x_image, x_label, img_weight=None):
+        """retinanet_module.py:403-426: forward (training-mode BN, per-image statistics) and
+        (cls, reg) summed over levels, anchors and images.  x_image [B,H,W,3] (square);
+        x_label: the device targets [B, A*P, 4+C] of format_data_batched, or (B = 1) the nested
+        [5][A] list format_data returns.  Returns float32 scalars; gradients come from the
+        trainer (cvlite.train_retinanet.RetinaTrainer), which runs the same fused loss."""
+        net = self.model
+        x = torch.as_tensor(x_image, dtype=torch.float32, device="cuda")
+        if x.dim() == 3:
+            x = x.unsqueeze(0)
+        B, H, W = int(x.shape[0]), int(x.shape[1]), int(x.shape[2])
+        if isinstance(x_label, (list, tuple)):
+            flat = [torch.as_tensor(np.asarray(m, np.float32)).reshape(-1, 4 + self.n_class)
+                    for lev in x_label for m in lev]
+            x_label = torch.cat(flat, 0).unsqueeze(0).cuda()
+        shapes, _, _ = net.layout(B, H, W)
+        reg, cls = net.forward(x.contiguous())
+        losses = ot.retina_loss(reg, cls, x_label.contiguous(), [h * w for h, w in shapes], self.n_anchors,
+                                self.n_class, img_weight=img_weight)
+        s = losses.sum(0)
+        return s[0], s[1]
 
     def anchor_dims_device(self):
         if self._dims_dev is None:
@@ -66,10 +99,10 @@ class RetinaNet(object):
         base = np.stack([gx, gy, np.ones_like(gx), np.ones_like(gx)], -1).astype(np.float64)
         return [base * np.array([1, 1, d[0], d[1]], np.float64).reshape(1, 1, 4) for d in self.anchor_boxes[level]]
 
-    def format_data_batched(self, boxes, nbox, img_dim, pad, iou_thresh=0.50):
+    def format_data_batched(self, boxes, nbox, img_dim, pad, iou_thresh=0.50, out=None, num_targets=None):
         """Device form: boxes [B,Nmax,5], nbox [B], img_dim [B,2] -> targets [B, P, 4+C], counts [B]."""
         return ot.retina_assign(boxes, nbox, img_dim, pad, self.anchor_dims_device(), self.n_class,
-                                iou_thresh=iou_thresh, strides=self.strides)
+                                iou_thresh=iou_thresh, strides=self.strides, out=out, num_targets=num_targets)
 
     def format_data(self, gt_labels, img_dim, iou_thresh=0.50, img_pad=None):
         """retinanet_module.py:251-365 -> (nested [5][A] float32 [S,S,4+C] maps, num_targets)."""

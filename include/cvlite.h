@@ -82,7 +82,7 @@ int cvl_fcos_decode(const float* pred, int ld, int S0, int S1, double stride, do
  *          DGRAD-> packed [Npad=Cin_pad][KH*KW*Cout_pad] (w_dgrad); then `Cin` = Cout_pad.
  * TF "same" padding: pad_t/pad_l = floor(total/2) (asymmetric for stride 2).
  * bn_stats (nullable) receives per-(image, out channel) (sum, sumsq) in float64 (atomic adds;
- * zero it first), which requires H*W % 128 == 0 or H*W dividing 128 (and H*W % 4 == 0).
+ * zero it first), which requires H*W % 4 == 0.
  * ---------------------------------------------------------------------------------------- */
 #define CVL_CONV_MAX_SEG 5
 enum { CVL_CONV_FWD = 0, CVL_CONV_DGRAD = 1 };
@@ -199,6 +199,14 @@ int cvl_sgd_clip_update(float* w, const float* g, float* v, int64_t n, const flo
 int cvl_lr_schedule(int32_t* step, float* lr, double init_lr, double min_lr, double decay_rate,
                     int decay_step, cvl_stream_t stream);
 
+/* RetinaNet candidate selection (train_retinanet_coco.py:190-209: images without matches are
+ * skipped, the first batch_size usable candidates are trained on): idx[k] = the first k indices
+ * i < n (in order) with counts[i] > 0, weight[k] = 1 for a filled slot and 0 for an empty one.
+ * cvl_gather_rows: dst row i = src row idx[i], rows of row_bytes (multiple of 16). */
+int cvl_select_first_nonzero(const int32_t* counts, int n, int k, int32_t* idx, float* weight,
+                             cvl_stream_t stream);
+int cvl_gather_rows(const void* src, int64_t row_bytes, const int32_t* idx, int n, void* dst, cvl_stream_t stream);
+
 /* ------------------------------------------------------------------------------------------
  * RetinaNet target assignment.  Replaces RetinaNet/retinanet_module.py:205-365
  * (`RetinaNet.__init__` anchor dims are passed in; `get_anchors` + `format_data` + utils.compute_iou
@@ -231,6 +239,19 @@ size_t cvl_det_loss_workspace_size(int B, int P);
 int cvl_det_loss(const float* reg_pred, int ld_reg, const float* cls_pred, int ld_cls, const float* targets,
                  int B, int P, int num_classes, float grad_scale_cls, float grad_scale_reg, float* losses,
                  float* d_reg, float* d_cls, void* workspace, cvl_stream_t stream);
+
+/* RetinaNet.train_loss fwd + bwd over all (level, anchor) terms (retinanet_module.py:367-426) in
+ * one launch.  reg_pred / cls_pred: the grouped head outputs [B][P][ld] fp32 (P = sum of
+ * level_cells, level-major cells; anchor a's boxes at channels 4a..4a+3, its classes at
+ * aC..aC+C-1); targets: cvl_retina_assign's [B][n_anchors*P][4+C] in (level, anchor, cell) order.
+ * losses [B][2] = (cls, reg) sums; d_reg / d_cls (nullable): bf16 grad_scale * dloss/dpred at the
+ * prediction positions (other channels untouched).  img_weight [B] (nullable) multiplies image b's
+ * loss and gradient (0 = an image the reference loop skipped for having no matches). */
+size_t cvl_retina_loss_workspace_size(int B, int P, int n_anchors);
+int cvl_retina_loss(const float* reg_pred, int ld_reg, const float* cls_pred, int ld_cls, const float* targets,
+                    int B, const int32_t* level_cells /*host[5]*/, int n_anchors, int num_classes,
+                    const float* img_weight, float grad_scale, float* losses, void* d_reg, int ld_dreg,
+                    void* d_cls, int ld_dcls, void* workspace, cvl_stream_t stream);
 
 /* Greedy per-class NMS (CenterNet/tf_centernet_hourglass.py:44-85, method 'nms'): boxes [n][6] =
  * (x1, y1, x2, y2, score, cls) float64; classes [ncls] processed in the given order; keep

@@ -139,9 +139,8 @@ def resnet50(x, p):
     return taps[1:]
 
 
-def fcos_forward(x_nhwc, p, num_classes):
-    """Returns reg [B, P, 5] and cls [B, P, C] (level-major cells) like cvlite's FCOSNet."""
-    x = x_nhwc.permute(0, 3, 1, 2)
+def fpn_levels(x, p):
+    """Backbone + FPN (fcos.py:49-72 == retinanet_module.py:74-105): [P3..P7] NCHW."""
     c3, c4, c5 = resnet50(x, p)
     l3 = conv(c3, p, "c3_1x1")
     l4 = conv(c4, p, "c4_1x1")
@@ -150,8 +149,14 @@ def fcos_forward(x_nhwc, p, num_classes):
     p4r = q(l4 + up(l5))
     p3r = q(l3 + up(l4))
     p6 = conv(c5, p, "c6_3x3", 2)
-    fpn = [conv(p3r, p, "c3_3x3"), conv(p4r, p, "c4_3x3"), conv(l5, p, "c5_3x3"), p6,
-           conv(F.relu(p6), p, "c7_3x3", 2)]
+    return [conv(p3r, p, "c3_3x3"), conv(p4r, p, "c4_3x3"), conv(l5, p, "c5_3x3"), p6,
+            conv(F.relu(p6), p, "c7_3x3", 2)]
+
+
+def fcos_forward(x_nhwc, p, num_classes):
+    """Returns reg [B, P, 5] and cls [B, P, C] (level-major cells) like cvlite's FCOSNet."""
+    x = x_nhwc.permute(0, 3, 1, 2)
+    fpn = fpn_levels(x, p)
     regs, clss = [], []
     for l, f in enumerate(fpn):
         c = f
@@ -200,3 +205,61 @@ def train_step_reference(params, moms, images, targets, num_classes, lr, momentu
         moms[k].mul_(momentum).sub_(lr * g)
         params[k].add_(moms[k])
     return norm
+
+
+def retina_forward(x_nhwc, p, num_classes, n_anchors=9):
+    """retinanet_module.py:8-159: shared towers, then per (level, anchor) 3x3 heads.  The params hold
+    each level's 9 anchor kernels concatenated on the output axis (`cls_output_{l}` = the Keras
+    `cls_output_{l}_anchor_{a}` kernels side by side); returns reg [B, P, 4A] and cls [B, P, AC]
+    (level-major cells, anchor a at channels 4a.. / aC..), cvlite's RetinaNetNet layout."""
+    x = x_nhwc.permute(0, 3, 1, 2)
+    fpn = fpn_levels(x, p)
+    regs, clss = [], []
+    B = x.shape[0]
+    for l, f in enumerate(fpn):
+        c = f
+        r = f
+        for i in range(4):
+            c = conv(c, p, "cls_layer_%d" % (i + 1), bias=False)
+            r = conv(r, p, "reg_layer_%d" % (i + 1), bias=False)
+        c = head_conv(F.relu(c), p, "cls_output_%d" % (l + 1))
+        r = head_conv(F.relu(r), p, "reg_output_%d" % (l + 1))
+        clss.append(c.permute(0, 2, 3, 1).reshape(B, -1, n_anchors * num_classes))
+        regs.append(r.permute(0, 2, 3, 1).reshape(B, -1, n_anchors * 4))
+    return torch.cat(regs, 1), torch.cat(clss, 1)
+
+
+def retina_unpack_targets(tg, level_cells, n_anchors):
+    """[B, A*P, 4+C] in (level, anchor, cell) order -> [B, P, A, 4+C] (cell-major, like the preds)."""
+    B = tg.shape[0]
+    out, o = [], 0
+    for S2 in level_cells:
+        t = tg[:, o:o + n_anchors * S2].reshape(B, n_anchors, S2, -1).permute(0, 2, 1, 3)
+        out.append(t)
+        o += n_anchors * S2
+    return torch.cat(out, 1)
+
+
+def retina_loss_and_grads(params, x, targets, num_classes, level_cells, n_anchors=9, img_weight=None,
+                          dtype=torch.float32):
+    """Forward + RetinaNet.train_loss (retinanet_module.py:403-426: focal over classes, smooth-L1 on
+    boxes masked by any class > 0, summed over all levels and anchors) per image; backward of
+    sum_b w_b (cls_b + reg_b).  Returns losses [B,2], grads, reg, cls."""
+    p = {k: v.detach().to(dtype).requires_grad_(True) for k, v in params.items()}
+    reg, cls = retina_forward(x.to(dtype), p, num_classes, n_anchors)
+    B, P = reg.shape[0], reg.shape[1]
+    t = retina_unpack_targets(targets.to(dtype), level_cells, n_anchors)      # [B, P, A, 4+C]
+    losses, total = [], 0.0
+    for b in range(B):
+        tb = t[b].reshape(P * n_anchors, 4 + num_classes)
+        rb = reg[b].reshape(P * n_anchors, 4)
+        cb = cls[b].reshape(P * n_anchors, num_classes)
+        mask = (tb[:, 4:].max(-1).values > 0).to(tb.dtype)
+        lc = fcos_torch.focal(tb[:, 4:], cb)
+        lr = fcos_torch.smooth_l1(tb[:, :4], rb, mask)
+        w = 1.0 if img_weight is None else float(img_weight[b])
+        losses.append(torch.stack([lc, lr]) * w)
+        total = total + w * (lc + lr)
+    total.backward()
+    grads = {k: v.grad.detach() for k, v in p.items() if v.grad is not None}
+    return torch.stack(losses).detach(), grads, reg.detach(), cls.detach()
