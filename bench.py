@@ -134,6 +134,51 @@ def cpu_baseline(H, W, n_img=2):
                       "%d-image step at %dx%d (per-image fwd+bwd, clip, SGD), after a 1-image warm-up" % (n_img, H, W)}
 
 
+def bench_retinanet(args):
+    """configs[4]: RetinaNet ResNet-50-FPN 640x640 COCO-80, bs=8/GPU (3*bs candidates per step,
+    anchor sizes 20..320 as train_retinanet_coco.py:343)."""
+    from cvlite.retinanet import RetinaNet
+    from cvlite.train_retinanet import RetinaTrainer, synthetic_coco_batch
+    rank, world, local = dist.init_from_env()
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    B = args.bs if args.bs != 16 else 8
+    S = args.size if args.size != 512 else 640
+    rn = RetinaNet(80, {}, anchor_sizes=[20.0, 40.0, 80.0, 160.0, 320.0])
+    net = rn.model
+    tr = RetinaTrainer(net, rn, B, S, n_max=50, world=world, use_graph=not args.no_graph)
+    pool = [synthetic_coco_batch(3 * B, S, 80, n_max=50, seed=4321 + 97 * rank + i, device=dev) for i in range(2)]
+    for i in range(args.warmup):
+        tr.load_candidates(*pool[i % 2])
+        tr.step()
+    torch.cuda.synchronize()
+    dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        tr.load_candidates(*pool[i % 2])
+        tr.step()
+    torch.cuda.synchronize()
+    dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = dist.max_over_ranks(time.perf_counter() - t0, dev)
+    if rank != 0:
+        dist.barrier()
+        return
+    out = {"metric": "training images/sec (whole node), RetinaNet-R50-FPN COCO 640x640 bs=8/GPU",
+           "value": round(world * B * args.steps / elapsed, 3), "unit": "images/s", "n_gpus": world,
+           "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(1000.0 * elapsed / args.steps, 3),
+           "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "bf16",
+           "data": "synthetic COCO-shaped: 3*bs candidates/step, 1+Poisson(6.3) boxes, C=80; random init",
+           "config": {"workload": "RetinaNet R50-FPN train step (assign 3bs candidates + select + fwd + loss + "
+                                  "bwd + clip/SGD)", "model": "RetinaNet-ResNet50-FPN", "global_batch": B * world,
+                      "image_size": S, "parallelism": "dp%d" % world},
+           "last_step_losses_cls_reg": [round(x, 3) for x in tr.losses.double().sum(0).cpu().tolist()]}
+    print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.barrier()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -143,7 +188,12 @@ def main():
     ap.add_argument("--size", type=int, default=512)
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--model", default="fcos", choices=["fcos", "retinanet"],
+                    help="fcos = the headline metric (configs[1]/[2]); retinanet = configs[4] "
+                         "(R50-FPN 640x640 COCO-80 bs=8/GPU), a side line")
     args = ap.parse_args()
+    if args.model == "retinanet":
+        return bench_retinanet(args)
     rank, world, local = dist.init_from_env()
     if world > 1 and args.gpus != world:
         print("warning: --gpus %d but WORLD_SIZE %d" % (args.gpus, world), file=sys.stderr)

@@ -400,37 +400,62 @@ struct RetinaLossArgs {
   float grad_scale;
 };
 
+// A workgroup owns RL_ROWS consecutive target rows of one image (a contiguous [rows][4+C] slab):
+// the slab is staged through LDS with coalesced loads, each row's (mask, prediction row, anchor)
+// is resolved once, then the workgroup walks the slab element by element so that consecutive
+// lanes touch consecutive classes of one prediction row (coalesced logit reads / gradient writes).
+constexpr int RL_ROWS = 32;
+constexpr int RL_MAXW = 4 + 128;     // row width bound held in LDS (C <= 128)
+
 __global__ void __launch_bounds__(NT) retina_loss_kernel(RetinaLossArgs a) {
   const int b = blockIdx.y;
-  const int i = blockIdx.x * NT + threadIdx.x;
-  float s_cls = 0.f, s_reg = 0.f;
-  const float wb = a.img_w ? a.img_w[b] : 1.0f;
-  if (i < a.P * a.A) {
-    const int cell = i / a.A, an = i - (i / a.A) * a.A;
+  const int W = 4 + a.C;
+  const long T = (long)a.P * a.A;
+  const long t0 = (long)blockIdx.x * RL_ROWS;
+  const int nrow = (int)min((long)RL_ROWS, T - t0);
+  __shared__ float tile[RL_ROWS * RL_MAXW];
+  __shared__ long prow_s[RL_ROWS];
+  __shared__ int an_s[RL_ROWS];
+  __shared__ float mask_s[RL_ROWS];
+  const float* src = a.tgt + ((size_t)b * T + t0) * W;
+  for (int i = threadIdx.x; i < nrow * W; i += NT) tile[i] = src[i];
+  if (threadIdx.x < nrow) {
+    const long t = t0 + threadIdx.x;
+    // (level, anchor, cell) of target row t
     int l = 0;
 #pragma unroll
     for (int k = 1; k < 5; ++k)
-      if (cell >= a.off[k]) l = k;
+      if (t >= (long)a.A * a.off[k]) l = k;
     const int S2 = a.off[l + 1] - a.off[l];
-    const size_t t_row = (size_t)b * a.P * a.A + (size_t)a.A * a.off[l] + (size_t)an * S2 + (cell - a.off[l]);
-    const float* t = a.tgt + t_row * (4 + a.C);
-    const size_t prow = (size_t)b * a.P + cell;
-    const float* xr = a.reg + prow * a.ld_reg + an * 4;
-    const float* xc = a.cls + prow * a.ld_cls + (size_t)an * a.C;
-    const float gs = a.grad_scale * wb;
+    const long r = t - (long)a.A * a.off[l];
+    const int an = (int)(r / S2), cell = a.off[l] + (int)(r - (long)(r / S2) * S2);
+    prow_s[threadIdx.x] = (long)b * a.P + cell;
+    an_s[threadIdx.x] = an;
+  }
+  __syncthreads();
+  if (threadIdx.x < nrow) {
     float tmax = 0.f;
-    for (int c = 0; c < a.C; ++c) {
-      const float y = t[4 + c];
-      tmax = fmaxf(tmax, y);
-      float g;
-      s_cls += focal_elem(y, xc[c], &g);
-      if (a.dcls) a.dcls[prow * a.ld_dcls + (size_t)an * a.C + c] = f32_to_bf16(g * gs);
-    }
-    const float mask = tmax > 0.f ? 1.0f : 0.0f;
-    for (int j = 0; j < 4; ++j) {
-      float g;
-      s_reg += mask * sl1_elem(t[j], xr[j], &g);
-      if (a.dreg) a.dreg[prow * a.ld_dreg + an * 4 + j] = f32_to_bf16(mask * g * gs);
+    for (int c = 0; c < a.C; ++c) tmax = fmaxf(tmax, tile[threadIdx.x * W + 4 + c]);
+    mask_s[threadIdx.x] = tmax > 0.f ? 1.0f : 0.0f;      // max(class) > 0
+  }
+  __syncthreads();
+  const float wb = a.img_w ? a.img_w[b] : 1.0f;
+  const float gs = a.grad_scale * wb;
+  float s_cls = 0.f, s_reg = 0.f;
+  for (int i = threadIdx.x; i < nrow * W; i += NT) {
+    const int row = i / W, ch = i - (i / W) * W;
+    const long prow = prow_s[row];
+    const int an = an_s[row];
+    const float y = tile[i];
+    float g;
+    if (ch < 4) {
+      const float m = mask_s[row];
+      s_reg += m * sl1_elem(y, a.reg[prow * a.ld_reg + an * 4 + ch], &g);
+      if (a.dreg) a.dreg[prow * a.ld_dreg + an * 4 + ch] = f32_to_bf16(m * g * gs);
+    } else {
+      const int c = ch - 4;
+      s_cls += focal_elem(y, a.cls[prow * a.ld_cls + (long)an * a.C + c], &g);
+      if (a.dcls) a.dcls[prow * a.ld_dcls + (long)an * a.C + c] = f32_to_bf16(g * gs);
     }
   }
   __shared__ double red[2][NT / 64];
@@ -602,7 +627,7 @@ extern "C" int cvl_det_loss(const float* reg_pred, int ld_reg, const float* cls_
 }
 
 extern "C" size_t cvl_retina_loss_workspace_size(int B, int P, int n_anchors) {
-  return (size_t)B * (((size_t)P * n_anchors + NT - 1) / NT) * 2 * sizeof(double);
+  return (size_t)B * (((size_t)P * n_anchors + RL_ROWS - 1) / RL_ROWS) * 2 * sizeof(double);
 }
 
 extern "C" int cvl_retina_loss(const float* reg_pred, int ld_reg, const float* cls_pred, int ld_cls,
@@ -628,7 +653,8 @@ extern "C" int cvl_retina_loss(const float* reg_pred, int ld_reg, const float* c
   }
   a.off[5] = o;
   a.P = o;
-  a.tiles = (int)(((long)a.P * a.A + NT - 1) / NT);
+  CVL_CHECK_ARG(4 + num_classes <= RL_MAXW);
+  a.tiles = (int)(((long)a.P * a.A + RL_ROWS - 1) / RL_ROWS);
   hipLaunchKernelGGL(retina_loss_kernel, dim3(a.tiles, B), dim3(NT), 0, S_, a);
   hipLaunchKernelGGL(det_loss_finalize, dim3(B), dim3(64), 0, S_, (const double*)workspace, losses, a.tiles);
   return cvl_launch_status();
