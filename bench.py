@@ -179,6 +179,51 @@ def bench_retinanet(args):
         dist.barrier()
 
 
+def bench_centernet(args):
+    """configs[3]: CenterNet hourglass (tf_centernet_hourglass.build_model defaults: separable,
+    n_filters 128, 1 stack, 2 repeats) 512x512 VOC-20, bs=8/GPU, BN sub-batches of 2
+    (train_hourglass_voc.py:317), Keras Adam."""
+    from cvlite.hourglass_net import HourglassNet
+    from cvlite.train_centernet import CenterNetTrainer, synthetic_batch as cn_batch
+    rank, world, local = dist.init_from_env()
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    B = args.bs if args.bs != 16 else 8
+    S = args.size
+    net = HourglassNet(NUM_CLASSES, device=dev, seed=0)
+    tr = CenterNetTrainer(net, B, (S, S), sub_batch_sz=2, n_max=16, world=world, use_graph=not args.no_graph)
+    pool = [cn_batch(B, S, S, NUM_CLASSES, n_max=16, seed=777 + 97 * rank + i, device=dev) for i in range(2)]
+    for i in range(args.warmup):
+        tr.load_batch(*pool[i % 2])
+        tr.step()
+    torch.cuda.synchronize()
+    dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        tr.load_batch(*pool[i % 2])
+        tr.step()
+    torch.cuda.synchronize()
+    dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = dist.max_over_ranks(time.perf_counter() - t0, dev)
+    if rank != 0:
+        dist.barrier()
+        return
+    out = {"metric": "training images/sec (whole node), CenterNet-hourglass VOC 512x512 bs=8/GPU",
+           "value": round(world * B * args.steps / elapsed, 3), "unit": "images/s", "n_gpus": world,
+           "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(1000.0 * elapsed / args.steps, 3),
+           "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "bf16",
+           "data": "synthetic VOC-shaped: U[-1,1) images, 1+Poisson(1.4) boxes, C=20; random init",
+           "config": {"workload": "CenterNet hourglass train step (centroid targets + fwd + loss + bwd + clip/Adam), "
+                                  "BN sub-batch 2", "model": "CenterNet-separable-hourglass-nf128",
+                      "global_batch": B * world, "image_size": S, "parallelism": "dp%d" % world},
+           "last_step_losses_cls_reg": [round(x, 3) for x in tr.losses.double().sum(0).cpu().tolist()]}
+    print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.barrier()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -188,12 +233,14 @@ def main():
     ap.add_argument("--size", type=int, default=512)
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--model", default="fcos", choices=["fcos", "retinanet"],
+    ap.add_argument("--model", default="fcos", choices=["fcos", "retinanet", "centernet"],
                     help="fcos = the headline metric (configs[1]/[2]); retinanet = configs[4] "
                          "(R50-FPN 640x640 COCO-80 bs=8/GPU), a side line")
     args = ap.parse_args()
     if args.model == "retinanet":
         return bench_retinanet(args)
+    if args.model == "centernet":
+        return bench_centernet(args)
     rank, world, local = dist.init_from_env()
     if world > 1 and args.gpus != world:
         print("warning: --gpus %d but WORLD_SIZE %d" % (args.gpus, world), file=sys.stderr)

@@ -381,6 +381,56 @@ __global__ void __launch_bounds__(NT) det_loss_kernel(DetLossArgs a) {
   }
 }
 
+// CenterNet training loss (tf_centernet_hourglass.py:492-505 inside train_step :537-545) straight
+// off the output conv: pred [B*P][ld_pred] fp32 = [reg 0..3 | cls 4..4+C) (b_focal already in the
+// conv bias), targets [B*P][4+C].  Writes the bf16 gradient of cls_scale*cls + reg_scale*reg as
+// the output conv's backward operand [B*P][ld_d] (channels >= 4+C zeroed) and per-image sums.
+struct CnLossArgs {
+  const float* pred;
+  const float* tgt;
+  double* partial;
+  cvl_bf16* d;
+  int ld_pred, ld_d, P, C, tiles;
+  float cls_scale, reg_scale;
+};
+
+__global__ void __launch_bounds__(NT) centernet_loss_kernel(CnLossArgs a) {
+  const int b = blockIdx.y;
+  const int p = blockIdx.x * NT + threadIdx.x;
+  float s_cls = 0.f, s_reg = 0.f;
+  if (p < a.P) {
+    const size_t cell = (size_t)b * a.P + p;
+    const float* t = a.tgt + cell * (4 + a.C);
+    const float* x = a.pred + cell * a.ld_pred;
+    cvl_bf16* d = a.d + cell * a.ld_d;
+    float tmax = 0.f;
+    for (int c = 0; c < a.C; ++c) {
+      const float y = t[4 + c];
+      tmax = fmaxf(tmax, y);
+      float g;
+      s_cls += focal_elem(y, x[4 + c], &g);
+      d[4 + c] = f32_to_bf16(g * a.cls_scale);
+    }
+    const float mask = tmax > 0.f ? 1.0f : 0.0f;
+    for (int j = 0; j < 4; ++j) {
+      float g;
+      s_reg += mask * sl1_elem(t[j], x[j], &g);
+      d[j] = f32_to_bf16(mask * g * a.reg_scale);
+    }
+    for (int c = 4 + a.C; c < a.ld_d; ++c) d[c] = 0;
+  }
+  __shared__ double red[2][NT / 64];
+  double v0 = warp_sum_d((double)s_cls), v1 = warp_sum_d((double)s_reg);
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  if (lane == 0) { red[0][w] = v0; red[1][w] = v1; }
+  __syncthreads();
+  if (threadIdx.x < 2) {
+    double s = 0.0;
+    for (int k = 0; k < NT / 64; ++k) s += red[threadIdx.x][k];
+    a.partial[((size_t)b * a.tiles + blockIdx.x) * 2 + threadIdx.x] = s;
+  }
+}
+
 // RetinaNet.train_loss (retinanet_module.py:403-426) over every (level, anchor) at once, fwd + bwd.
 // Predictions come straight from the grouped head convs: row (level offset + cell) of [B][P][ld],
 // class channels a*C + c, box channels a*4 + j.  Targets are cvl_retina_assign's [B][A*P][4+C] in
@@ -667,5 +717,19 @@ extern "C" int cvl_nms(const double* boxes, int n, const double* classes, int nc
   CVL_CHECK_ARG(boxes && classes && keep && nkeep && workspace && n > 0 && ncls > 0);
   hipLaunchKernelGGL(nms_kernel, dim3(ncls), dim3(NT), 0, S_, boxes, n, classes, ncls, iou_threshold, keep,
                      nkeep, (uint8_t*)workspace);
+  return cvl_launch_status();
+}
+
+extern "C" int cvl_centernet_loss(const float* pred, int ld_pred, const float* targets, int B, int P, int num_classes,
+                                  float cls_scale, float reg_scale, float* losses, void* d_pred, int ld_d,
+                                  void* workspace, cvl_stream_t stream) {
+  CVL_CHECK_ARG(pred && targets && losses && d_pred && workspace && B > 0 && P > 0 && num_classes > 0);
+  CVL_CHECK_ARG(ld_pred >= 4 + num_classes && ld_d >= 4 + num_classes);
+  CnLossArgs a;
+  a.pred = pred; a.tgt = targets; a.partial = (double*)workspace; a.d = (cvl_bf16*)d_pred;
+  a.ld_pred = ld_pred; a.ld_d = ld_d; a.P = P; a.C = num_classes; a.tiles = (P + NT - 1) / NT;
+  a.cls_scale = cls_scale; a.reg_scale = reg_scale;
+  hipLaunchKernelGGL(centernet_loss_kernel, dim3(a.tiles, B), dim3(NT), 0, S_, a);
+  hipLaunchKernelGGL(det_loss_finalize, dim3(B), dim3(64), 0, S_, (const double*)workspace, losses, a.tiles);
   return cvl_launch_status();
 }

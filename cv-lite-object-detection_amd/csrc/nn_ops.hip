@@ -228,7 +228,8 @@ __global__ void __launch_bounds__(NT) bn_bwd_kernel(const cvl_bf16* __restrict__
                                                     const cvl_bf16* __restrict__ z, const float* __restrict__ mr,
                                                     const float* __restrict__ gamma, const double* __restrict__ sums,
                                                     cvl_bf16* __restrict__ dz, cvl_bf16* __restrict__ g_out,
-                                                    float* __restrict__ part, int C, int HW, int rows_per_blk) {
+                                                    float* __restrict__ part, int C, int HW, int rows_per_blk,
+                                                    int group, float dz_beta) {
   const int b = blockIdx.y;
   const int C8 = C / 8;
   const int tpr = C8 < NT ? C8 : NT;
@@ -236,7 +237,10 @@ __global__ void __launch_bounds__(NT) bn_bwd_kernel(const cvl_bf16* __restrict__
   const int cg = threadIdx.x % tpr, rsub = threadIdx.x / tpr;
   const int r0 = blockIdx.x * rows_per_blk;
   const int r1 = min(r0 + rows_per_blk, HW);
-  const float inv = 1.0f / (float)HW;
+  // BN over a sub-batch of `group` images (the last group may be short): sums hold group totals
+  const int g0 = (b / group) * group;
+  const int gsz = min(g0 + group, (int)gridDim.y) - g0;
+  const float inv = 1.0f / ((float)HW * (float)gsz);
   __shared__ float red[NT][17];
   for (int cgb = cg; cgb < C8; cgb += tpr) {
     const int c0 = cgb * 8;
@@ -244,8 +248,8 @@ __global__ void __launch_bounds__(NT) bn_bwd_kernel(const cvl_bf16* __restrict__
 #pragma unroll
     for (int u = 0; u < 8; ++u) {
       const long bc = (long)b * C + c0 + u;
-      m[u] = mr[bc * 2];
-      rs[u] = mr[bc * 2 + 1];
+      m[u] = PASS == 2 ? 0.f : mr[bc * 2];
+      rs[u] = PASS == 2 ? 1.f : mr[bc * 2 + 1];
       s1[u] = 0.f; s2[u] = 0.f;
       if (PASS == 1) {
         k1[u] = (float)sums[bc * 2] * inv;          // mean(g)
@@ -262,7 +266,7 @@ __global__ void __launch_bounds__(NT) bn_bwd_kernel(const cvl_bf16* __restrict__
           const int rq = min(r + q * rpp, r1 - 1);       // clamped: loads stay unconditional
           off[q] = ((long)b * HW + rq) * C + c0;
           vg[q] = *reinterpret_cast<const s16x8*>(dy + off[q]);
-          vz[q] = *reinterpret_cast<const s16x8*>(z + off[q]);
+          if (PASS != 2) vz[q] = *reinterpret_cast<const s16x8*>(z + off[q]);
           if (y) vy[q] = *reinterpret_cast<const s16x8*>(y + off[q]);
         }
 #pragma unroll
@@ -270,6 +274,13 @@ __global__ void __launch_bounds__(NT) bn_bwd_kernel(const cvl_bf16* __restrict__
           const bool ok = r + q * rpp < r1;
           float g[8], zz[8];
           unpack8(vg[q], g);
+          if (PASS == 2) {                                // statistics of x = dy: (sum x, sum x^2)
+            if (ok) {
+#pragma unroll
+              for (int u = 0; u < 8; ++u) { s1[u] += g[u]; s2[u] += g[u] * g[u]; }
+            }
+            continue;
+          }
           unpack8(vz[q], zz);
           if (y) {
             float yy[8];
@@ -292,6 +303,12 @@ __global__ void __launch_bounds__(NT) bn_bwd_kernel(const cvl_bf16* __restrict__
             for (int u = 0; u < 8; ++u) {
               const float xh = (zz[u] - m[u]) * rs[u];
               o[u] = gm[u] * (g[u] - k1[u] - xh * k2[u]);
+            }
+            if (dz_beta != 0.f) {
+              float old[8];
+              unpack8(*reinterpret_cast<const s16x8*>(dz + off[q]), old);
+#pragma unroll
+              for (int u = 0; u < 8; ++u) o[u] += dz_beta * old[u];
             }
             *reinterpret_cast<s16x8*>(dz + off[q]) = pack8(o);
           }
@@ -659,6 +676,47 @@ __global__ void gather_rows_kernel(const int4* src, long row16, const int32_t* i
   for (long i = blockIdx.x * (long)NT + threadIdx.x; i < row16; i += (long)gridDim.x * NT) d[i] = s[i];
 }
 
+
+// ---------------------------------------------------------------------------------------------
+// BatchNorm over sub-batches of `group` images (CenterNet/tf_centernet_hourglass.py:507-553: each
+// sub-batch is one Keras training-mode forward, so its statistics span the sub-batch; groups are
+// [g*G, min((g+1)*G, B)), the last may be short).  Running stats are updated once per group, in
+// group order, as the reference's sequential sub-batch forwards do.
+// ---------------------------------------------------------------------------------------------
+__global__ void bn_finalize_grouped_kernel(const double* stats, float* mr, float* run_mean, float* run_var,
+                                           int B, int C, int HW, int group, float eps, float momentum) {
+  const int c = blockIdx.x * NT + threadIdx.x;
+  if (c >= C) return;
+  float rm = run_mean ? run_mean[c] : 0.f, rv = run_var ? run_var[c] : 0.f;
+  for (int g0 = 0; g0 < B; g0 += group) {
+    const int g1 = min(g0 + group, B);
+    double s1 = 0.0, s2 = 0.0;
+    for (int b = g0; b < g1; ++b) { s1 += stats[((long)b * C + c) * 2]; s2 += stats[((long)b * C + c) * 2 + 1]; }
+    const double n = (double)(g1 - g0) * HW;
+    const double mean = s1 / n;
+    double var = s2 / n - mean * mean;
+    var = var > 0.0 ? var : 0.0;
+    const float fm = (float)mean, frs = (float)(1.0 / sqrt(var + (double)eps));
+    for (int b = g0; b < g1; ++b) { mr[((long)b * C + c) * 2] = fm; mr[((long)b * C + c) * 2 + 1] = frs; }
+    const double uvar = n > 1.0 ? var * n / (n - 1.0) : var;     // TF fused BN: unbiased for EMA
+    rm = rm * momentum + fm * (1.f - momentum);
+    rv = rv * momentum + (float)uvar * (1.f - momentum);
+  }
+  if (run_mean) { run_mean[c] = rm; run_var[c] = rv; }
+}
+
+// gs[b][c] = sum over b's group of s[b'][c] (fixed order: deterministic)
+__global__ void bn_group_sum_kernel(const double* s, double* gs, int B, int C, int group) {
+  const long i = blockIdx.x * (long)NT + threadIdx.x;
+  if (i >= (long)B * C) return;
+  const int b = (int)(i / C), c = (int)(i - (long)b * C);
+  const int g0 = (b / group) * group, g1 = min(g0 + group, B);
+  double a1 = 0.0, a2 = 0.0;
+  for (int k = g0; k < g1; ++k) { a1 += s[((long)k * C + c) * 2]; a2 += s[((long)k * C + c) * 2 + 1]; }
+  gs[i * 2] = a1;
+  gs[i * 2 + 1] = a2;
+}
+
 }  // namespace
 
 // ---------------------------------------------------------------------------------------------
@@ -744,12 +802,12 @@ extern "C" int cvl_bn_backward(const void* dy, const void* y_relu, const void* z
   dim3 g1(nchunk, B);
   hipLaunchKernelGGL(bn_bwd_kernel<0>, g1, dim3(NT), 0, S_, (const cvl_bf16*)dy, (const cvl_bf16*)y_relu,
                      (const cvl_bf16*)z, mean_rstd, gamma, (const double*)nullptr, (cvl_bf16*)nullptr,
-                     (cvl_bf16*)nullptr, part0, C, HW, rpb);
+                     (cvl_bf16*)nullptr, part0, C, HW, rpb, 1, 0.f);
   hipLaunchKernelGGL(bn_colsum_kernel, dim3((C + 31) / 32, B), dim3(NT), 0, S_, (const float*)part0, nchunk, C,
                      sums);
   hipLaunchKernelGGL(bn_bwd_kernel<1>, g1, dim3(NT), 0, S_, (const cvl_bf16*)dy, (const cvl_bf16*)y_relu,
                      (const cvl_bf16*)z, mean_rstd, gamma, (const double*)sums, (cvl_bf16*)dz, (cvl_bf16*)g_out,
-                     (float*)nullptr, C, HW, rpb);
+                     (float*)nullptr, C, HW, rpb, 1, 0.f);
   hipLaunchKernelGGL(bn_param_grad_kernel, dim3((C + NT - 1) / NT), dim3(NT), 0, S_, (const double*)sums,
                      dgamma, dbeta, B, C, beta_acc, conv_dbias);
   return cvl_launch_status();
@@ -865,5 +923,77 @@ extern "C" int cvl_gather_rows(const void* src, int64_t row_bytes, const int32_t
   const long row16 = row_bytes / 16;
   hipLaunchKernelGGL(gather_rows_kernel, dim3(grid_for(row16, NT, 1024), n), dim3(NT), 0, S_,
                      reinterpret_cast<const int4*>(src), row16, idx, reinterpret_cast<int4*>(dst));
+  return cvl_launch_status();
+}
+
+// ---- grouped BatchNorm (sub-batch statistics) + standalone statistics -----------------------------
+extern "C" size_t cvl_bn_stats_workspace_size(int B, int HW, int C) {
+  if (B <= 0 || HW <= 0 || C <= 0) return 0;
+  const int nchunk = (HW + bn_bwd_rows_per_blk(B, HW, C) - 1) / bn_bwd_rows_per_blk(B, HW, C);
+  return sizeof(float) * 2 * (size_t)B * nchunk * C;
+}
+
+extern "C" int cvl_bn_stats(const void* x, int B, int HW, int C, double* stats, void* workspace,
+                            size_t workspace_bytes, cvl_stream_t stream) {
+  CVL_CHECK_ARG(x && stats && workspace && C % 8 == 0 && B > 0 && HW > 0);
+  CVL_CHECK_ARG(C / 8 <= NT || (C / 8) % NT == 0);
+  CVL_CHECK_ARG(workspace_bytes >= cvl_bn_stats_workspace_size(B, HW, C));
+  const int rpb = bn_bwd_rows_per_blk(B, HW, C);
+  const int nchunk = (HW + rpb - 1) / rpb;
+  float* part = reinterpret_cast<float*>(workspace);
+  hipLaunchKernelGGL(bn_bwd_kernel<2>, dim3(nchunk, B), dim3(NT), 0, S_, (const cvl_bf16*)x,
+                     (const cvl_bf16*)nullptr, (const cvl_bf16*)nullptr, (const float*)nullptr, (const float*)nullptr,
+                     (const double*)nullptr, (cvl_bf16*)nullptr, (cvl_bf16*)nullptr, part, C, HW, rpb, 1, 0.f);
+  hipLaunchKernelGGL(bn_colsum_kernel, dim3((C + 31) / 32, B), dim3(NT), 0, S_, (const float*)part, nchunk, C,
+                     stats);
+  return cvl_launch_status();
+}
+
+extern "C" int cvl_bn_finalize_grouped(const double* stats, float* mean_rstd, float* run_mean, float* run_var,
+                                       int B, int C, int HW, int group, float eps, float momentum,
+                                       cvl_stream_t stream) {
+  CVL_CHECK_ARG(stats && mean_rstd && B > 0 && C > 0 && HW > 0 && group > 0);
+  hipLaunchKernelGGL(bn_finalize_grouped_kernel, dim3((C + NT - 1) / NT), dim3(NT), 0, S_, stats, mean_rstd,
+                     run_mean, run_var, B, C, HW, group, eps, momentum);
+  return cvl_launch_status();
+}
+
+extern "C" size_t cvl_bn_backward_grouped_workspace_size(int B, int HW, int C) {
+  if (B <= 0 || HW <= 0 || C <= 0) return 0;
+  return cvl_bn_backward_workspace_size(B, HW, C) + sizeof(double) * 2 * (size_t)B * C;
+}
+
+extern "C" int cvl_bn_backward_grouped(const void* dy, const void* y_relu, const void* z, const float* mean_rstd,
+                                       const float* gamma, void* workspace, size_t workspace_bytes, void* dz,
+                                       float dz_beta, float* dgamma, float* dbeta, int B, int HW, int C, int group,
+                                       cvl_stream_t stream) {
+  CVL_CHECK_ARG(dy && z && mean_rstd && gamma && workspace && dz && dgamma && dbeta && C % 8 == 0 && group > 0);
+  CVL_CHECK_ARG(B > 0 && HW > 0 && (C / 8 <= NT || (C / 8) % NT == 0));
+  CVL_CHECK_ARG(workspace_bytes >= cvl_bn_backward_grouped_workspace_size(B, HW, C));
+  const int rpb = bn_bwd_rows_per_blk(B, HW, C);
+  const int nchunk = (HW + rpb - 1) / rpb;
+  // workspace: sums [B][C][2] f64 | [C][2] f64 | partials [B][nchunk][C][2] f32 | group sums [B][C][2] f64
+  double* sums = reinterpret_cast<double*>(workspace);
+  double* dbsum = sums + 2 * (size_t)B * C;
+  float* part0 = reinterpret_cast<float*>(dbsum + 2 * (size_t)C);
+  double* gsums = reinterpret_cast<double*>(reinterpret_cast<char*>(workspace) +
+                                            cvl_bn_backward_workspace_size(B, HW, C));
+  dim3 g1(nchunk, B);
+  hipLaunchKernelGGL(bn_bwd_kernel<0>, g1, dim3(NT), 0, S_, (const cvl_bf16*)dy, (const cvl_bf16*)y_relu,
+                     (const cvl_bf16*)z, mean_rstd, gamma, (const double*)nullptr, (cvl_bf16*)nullptr,
+                     (cvl_bf16*)nullptr, part0, C, HW, rpb, group, 0.f);
+  hipLaunchKernelGGL(bn_colsum_kernel, dim3((C + 31) / 32, B), dim3(NT), 0, S_, (const float*)part0, nchunk, C,
+                     sums);
+  hipLaunchKernelGGL(bn_param_grad_kernel, dim3((C + NT - 1) / NT), dim3(NT), 0, S_, (const double*)sums,
+                     dgamma, dbeta, B, C, 0.f, (float*)nullptr);
+  const double* use = sums;
+  if (group > 1) {
+    hipLaunchKernelGGL(bn_group_sum_kernel, dim3((int)(((long)B * C + NT - 1) / NT)), dim3(NT), 0, S_,
+                       (const double*)sums, gsums, B, C, group);
+    use = gsums;
+  }
+  hipLaunchKernelGGL(bn_bwd_kernel<1>, g1, dim3(NT), 0, S_, (const cvl_bf16*)dy, (const cvl_bf16*)y_relu,
+                     (const cvl_bf16*)z, mean_rstd, gamma, use, (cvl_bf16*)dz, (cvl_bf16*)nullptr,
+                     (float*)nullptr, C, HW, rpb, group, dz_beta);
   return cvl_launch_status();
 }

@@ -57,6 +57,22 @@ SIGNATURES = {
     "cvl_retina_loss_workspace_size": (c_size_t, [c_int, c_int, c_int]),
     "cvl_retina_loss": (c_int, [P, c_int, P, c_int, P, c_int, P, c_int, c_int, P, c_float, P, P, c_int, P, c_int,
                                 P, P]),
+    "cvl_bn_stats_workspace_size": (c_size_t, [c_int, c_int, c_int]),
+    "cvl_bn_stats": (c_int, [P, c_int, c_int, c_int, P, P, c_size_t, P]),
+    "cvl_bn_finalize_grouped": (c_int, [P, P, P, P, c_int, c_int, c_int, c_int, c_float, c_float, P]),
+    "cvl_bn_backward_grouped_workspace_size": (c_size_t, [c_int, c_int, c_int]),
+    "cvl_bn_backward_grouped": (c_int, [P, P, P, P, P, P, c_size_t, P, c_float, P, P, c_int, c_int, c_int, c_int, P]),
+    "cvl_maxpool2x2": (c_int, [P, P, P, c_int, c_int, c_int, c_int, P]),
+    "cvl_maxpool2x2_backward": (c_int, [P, P, P, c_int, c_int, c_int, c_int, P]),
+    "cvl_upsample_bilinear2x_add": (c_int, [P, P, P, c_int, c_int, c_int, c_int, P]),
+    "cvl_upsample_bilinear2x_backward": (c_int, [P, P, c_int, c_int, c_int, c_int, c_float, P]),
+    "cvl_sep_fold_multi": (c_int, [P, P, c_int, P]),
+    "cvl_sep_unfold_multi": (c_int, [P, P, c_int, P]),
+    "cvl_bias_scalar_fold": (c_int, [P, P, P, c_int, c_int, P]),
+    "cvl_bias_scalar_unfold": (c_int, [P, P, P, c_int, c_int, P]),
+    "cvl_centernet_loss": (c_int, [P, c_int, P, c_int, c_int, c_int, c_float, c_float, P, P, c_int, P, P]),
+    "cvl_adam_clip_update": (c_int, [P, P, P, P, ctypes.c_int64, P, P, c_float, c_float, c_float, c_float, c_float,
+                                     P, P]),
     "cvl_nms_workspace_size": (c_size_t, [c_int, c_int]),
     "cvl_nms": (c_int, [P, c_int, P, c_int, ctypes.c_double, P, P, P, P]),
 }

@@ -1,6 +1,7 @@
-"""Drop-in mirror of CenterNet/tf_centernet_hourglass.py's target / loss / decode functions on
-MI355X: `format_data` (cvl_centernet_assign), `model_loss` (cvl_det_loss), `nms` (cvl_nms),
-`prediction_to_corners` (cvl_fcos_decode: same formula, tf_centernet_hourglass.py:355-377)."""
+"""Drop-in mirror of CenterNet/tf_centernet_hourglass.py on MI355X: `build_model` (the separable
+hourglass, cvlite.hourglass_net), `train_step` (cvlite.train_centernet: sub-batch BN, fused loss,
+clip + Adam, HIP graphs), `format_data` (cvl_centernet_assign), `model_loss` (cvl_det_loss), `nms`
+(cvl_nms), `prediction_to_corners` (cvl_fcos_decode: same formula, :355-377)."""
 import numpy as np
 import torch
 
@@ -51,3 +52,39 @@ def nms(bboxes, iou_threshold, sigma=0.3, method="nms"):
     _lib.require_cuda()
     kept = ot.nms(torch.tensor(b, device="cuda"), classes, iou_threshold)
     return [row for row in kept.cpu().numpy()]
+
+
+def build_model(n_classes, tmp_pi=0.99, n_filters=128, n_stacks=1, n_repeats=2, seperable=True, batch_norm=True,
+                norm_order="norm_first"):
+    """tf_centernet_hourglass.py:163-353 -> cvlite HourglassNet (callable: model(x) -> [B,H/4,W/4,4+C])."""
+    from .hourglass_net import HourglassNet
+    if not (seperable and batch_norm and norm_order == "norm_first"):
+        raise NotImplementedError("the MI355X path builds the reference default (seperable=True, batch_norm=True, "
+                                  "norm_order='norm_first')")
+    if n_stacks != 1:
+        raise NotImplementedError("n_stacks > 1 backward wiring is not built (reference default is 1)")
+    _lib.require_cuda()
+    return HourglassNet(n_classes, tmp_pi=tmp_pi, n_filters=n_filters, n_stacks=n_stacks, n_repeats=n_repeats)
+
+
+def train_step(voc_model, sub_batch_sz, images, bboxes, optimizer, cls_lambda=2.5, reg_lambda=1.0,
+               learning_rate=1.0e-3, grad_clip=1.0):
+    """tf_centernet_hourglass.py:507-564.  images [B,H,W,3] fp32, bboxes = formatted targets
+    [B,H/4,W/4,4+C]; optimizer = cvlite.train_centernet.Adam (tf.keras.optimizers.Adam stand-in).
+    Returns (avg_cls_loss, avg_reg_loss) = per-batch sums / batch_size."""
+    from .train_centernet import CenterNetTrainer
+    _lib.require_cuda()
+    images = torch.as_tensor(images, dtype=torch.float32).cuda()
+    bboxes = torch.as_tensor(bboxes, dtype=torch.float32).cuda()
+    B, H, W, _ = images.shape
+    key = (B, H, W, int(sub_batch_sz), id(optimizer), float(cls_lambda), float(reg_lambda), float(grad_clip))
+    tr = getattr(voc_model, "_trainers", {}).get(key)
+    if tr is None:
+        tr = CenterNetTrainer(voc_model, B, (H, W), sub_batch_sz=sub_batch_sz, optimizer=optimizer,
+                              cls_lambda=cls_lambda, reg_lambda=reg_lambda, grad_clip=grad_clip)
+        voc_model._trainers = getattr(voc_model, "_trainers", {})
+        voc_model._trainers[key] = tr
+    tr.opt.lr_dev.fill_(float(learning_rate))                    # optimizer.lr.assign(learning_rate)
+    tr.load_targets(images, bboxes)
+    losses = tr.step().double().sum(0).cpu().numpy()
+    return float(losses[0]) / B, float(losses[1]) / B

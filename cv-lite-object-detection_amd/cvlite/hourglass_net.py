@@ -1,0 +1,431 @@
+"""CenterNet hourglass (CenterNet/tf_centernet_hourglass.py:87-353, defaults n_filters=128,
+n_stacks=1, n_repeats=2, seperable=True, batch_norm=True, norm_order="norm_first") as an explicit
+forward/backward graph on the cvlite MFMA conv and HIP memory-bound kernels.
+
+MI355X mapping:
+  * every SeparableConv2D (depthwise D, no bias; pointwise P + bias) runs as ONE dense conv on the
+    implicit-GEMM MFMA kernels with the folded kernel W = D x P (exact for 1x1 — a per-channel
+    scale of the GEMM's K rows — and a rank-structured 3x3 / 7x7 kernel otherwise); the fold and
+    the gradient unfold of all 91 separable convs are one launch each (cvl_sep_fold_multi /
+    cvl_sep_unfold_multi), the fold feeding the batched bf16 re-pack;
+  * the 7x7/2 stem (3 channels) is im2col + one K=160 GEMM, like the ResNet stem;
+  * BatchNorm statistics span a sub-batch of `group` images (one Keras forward per sub-batch in
+    train_step :527-545), computed by a deterministic column-sum kernel;
+  * the bilinear x2 up-sampling is fused with the decoder's skip add;
+  * b_focal (tf_bias_layer.py) is folded into the output conv's bias.
+Keras names are kept: `cnn_block_0`, `<blk>_bn_<r>`, `<blk>_{bot,cnn,out}_<r>`
+(`/depthwise_kernel`, `/pointwise_kernel`, `/bias`), `cnn_out`, `b_focal`.
+Reference quirk kept (cnn_block :103-155): from the second repeat on the residual adds the BN
+OUTPUT (`tmp_input` is rebound to the normalised tensor before the convs).
+"""
+import math
+
+import torch
+
+from . import ops_nn as nn
+from .layers import BF16, BatchNorm, Conv, ParamStore, constant, glorot_uniform
+
+STEM_K = 7
+STEM_KP = 160          # im2col K = 7*7*3 = 147 padded to a multiple of 32
+BN_EPS = 1e-3          # Keras BatchNormalization default (the hourglass passes no epsilon)
+BN_MOMENTUM = 0.99
+
+
+def block_graph(n_stacks=1):
+    """(name, input, output) of every cnn_block in graph order (tf_centernet_hourglass.py:189-333)."""
+    out = [("cnn_block_1", "blk0", "cnn1")]
+    for s in range(n_stacks):
+        st = "stack_%d_" % (s + 1)
+        out += [(st + "enc_block_1", "stack_in", "enc1"), (st + "enc_block_2", "e1", "enc2"),
+                (st + "enc_block_3", "e2", "enc3"), (st + "enc_block_4a", "e3", "enc4a"),
+                (st + "enc_block_4b", "enc4a", "enc4b"), (st + "enc_block_4", "enc4b", "enc4"),
+                (st + "dec_block_1", "e3", "dec1"), (st + "dec_out_1", "d1res", "o1"),
+                (st + "dec_block_2", "e2", "dec2"), (st + "dec_out_2", "d2res", "o2"),
+                (st + "dec_block_3", "e1", "dec3"), (st + "dec_out_3", "d3res", "o3"),
+                (st + "dec_block_4", "stack_in", "dec4"), (st + "dec_out_4", "d4res", "o4")]
+    return out
+
+
+class SepConv(object):
+    """Keras SeparableConv2D(cout, k, stride, "same") = dense conv with the folded kernel D x P.
+    The trainable D / P / bias live in the model store; the folded kernel and its gradient in
+    the `eff` store (not optimised)."""
+
+    def __init__(self, store, eff, name, k, cin, cout, stride=1, cin_k=None, dgrad=True):
+        self.name, self.k, self.cin, self.cout = name, k, cin, cout
+        self.dwname = store.add(name + "/depthwise_kernel", (k, k, cin, 1), glorot_uniform(k * k * cin, k * k))
+        self.pwname = store.add(name + "/pointwise_kernel", (1, 1, cin, cout), glorot_uniform(cin, cout))
+        self.bname = store.add(name + "/bias", (cout,), constant(0.0))
+        self.store = store
+        self.conv = Conv(eff, name, k, cin, cout, stride, "same", bias=False, cin_k=cin_k, dgrad=dgrad)
+
+    @property
+    def b(self):
+        return self.store.p(self.bname)
+
+    @property
+    def db(self):
+        return self.store.g(self.bname)
+
+    def sep_entry(self):
+        st = self.store
+        return (st.p(self.dwname), st.p(self.pwname), self.conv.w, self.conv.dw, st.g(self.dwname),
+                st.g(self.pwname))
+
+    def fwd(self, x, B, H, W, relu_out=False):
+        c = self.conv
+        Ho, Wo, _, _ = c.out_hw(H, W)
+        out = torch.empty((B, Ho, Wo, self.cout), dtype=BF16, device=x.device)
+        d = c.fwd_desc(B, [nn.seg(Ho, Wo, H, W, c.wf, self.b)], ld_dst=self.cout, relu_out=relu_out)
+        nn.conv_igemm(d, x, out)
+        return out
+
+    def wgrad(self, x, dy, B, H, W):
+        self.conv.wgrad(x, dy, B, H, W, bias=False)
+        HW = H * W
+        nn.bias_grad(dy, int(dy.shape[-1]), 0, self.cout, 0, HW, HW, B, self.db)
+
+    def dgrad(self, dy, B, H, W, out=None, beta=0.0):
+        return self.conv.dgrad(dy, B, H, W, out=out, beta=beta)
+
+
+class Stem(object):
+    """cnn_block_0: SeparableConv2D(n_filters, 7x7, stride 2, "same") on the 3-channel image as
+    im2col (TF-same pads) + one K=160 GEMM with the folded kernel [7][7][3][nf]."""
+
+    def __init__(self, store, eff, nf):
+        self.sep = SepConv(store, eff, "cnn_block_0", STEM_K, 3, nf, stride=2, cin_k=STEM_KP, dgrad=False)
+        self.nf = nf
+
+    def pack_entry(self):
+        c = self.sep.conv
+        if c.wf is None:
+            c.wf = torch.empty((self.nf, STEM_KP), dtype=BF16, device=c.store.flat.device)
+        return (c.w, 1, 147, self.nf, STEM_KP, self.nf, c.wf, 0, 0, None)
+
+    def _desc(self, B, Ho, Wo):
+        return nn.make_desc(nn.FWD, B, STEM_KP, 1, 1, 1, 0, 0, self.nf, self.nf, self.nf,
+                            [nn.seg(Ho, Wo, Ho, Wo, self.sep.conv.wf, self.sep.b)])
+
+    def forward(self, x):
+        B, H, W, _ = x.shape
+        Ho, Wo, pt, pl = self.sep.conv.out_hw(H, W)
+        A = torch.empty((B * Ho * Wo, STEM_KP), dtype=BF16, device=x.device)
+        nn.im2col(x, STEM_K, STEM_K, 2, pt, pl, Ho, Wo, STEM_KP, A)
+        z = torch.empty((B, Ho, Wo, self.nf), dtype=BF16, device=x.device)
+        nn.conv_igemm(self._desc(B, Ho, Wo), A, z)
+        return z, (A, B, Ho, Wo)
+
+    def backward(self, dz, saved):
+        A, B, Ho, Wo = saved
+        dw = torch.empty((STEM_KP, self.nf), dtype=torch.float32, device=dz.device)
+        nn.conv_wgrad(self._desc(B, Ho, Wo), A, dz, dw)
+        self.sep.conv.dw.view(147, self.nf).copy_(dw[:147])
+        HW = Ho * Wo
+        nn.bias_grad(dz, self.nf, 0, self.nf, 0, HW, HW, B, self.sep.db)
+
+
+class Repeat(object):
+    """One cnn_block repeat: BN -> sep 1x1 (nf) -> sep 3x3 (nf) -> sep 1x1 (2nf) -> ReLU (+ BN out)."""
+
+    def __init__(self, store, eff, blk, r, cin, nf):
+        self.r = r
+        self.bn = BatchNorm(store, "%s_bn_%d" % (blk, r), cin, eps=BN_EPS, momentum=BN_MOMENTUM)
+        self.bot = SepConv(store, eff, "%s_bot_%d" % (blk, r), 1, cin, nf)
+        self.cnn = SepConv(store, eff, "%s_cnn_%d" % (blk, r), 3, nf, nf)
+        self.out = SepConv(store, eff, "%s_out_%d" % (blk, r), 1, nf, 2 * nf)
+        self.cin, self.cout = cin, 2 * nf
+
+    def seps(self):
+        return [self.bot, self.cnn, self.out]
+
+    def forward(self, t, B, H, W, group, train=True):
+        c, HW = self.cin, H * W
+        dev = t.device
+        bn = self.bn
+        mr = torch.empty((B, c, 2), dtype=torch.float32, device=dev)
+        if train:
+            stats = torch.empty((B, c, 2), dtype=torch.float64, device=dev)
+            nn.bn_stats(t, B, HW, c, stats)
+            nn.bn_finalize_grouped(stats, mr, bn.run_mean, bn.run_var, B, c, HW, group, bn.eps, bn.momentum)
+        else:                                     # Keras inference: moving statistics
+            mr[:, :, 0] = bn.run_mean
+            mr[:, :, 1] = torch.rsqrt(bn.run_var + bn.eps)
+        a = torch.empty_like(t)
+        nn.bn_apply(t, mr, bn.gamma, bn.beta, None, a, B, HW, c, False)
+        u = self.bot.fwd(a, B, H, W)
+        v = self.cnn.fwd(u, B, H, W)
+        y = self.out.fwd(v, B, H, W, relu_out=True)
+        if self.r == 0:
+            o = y
+        else:
+            o = torch.empty_like(y)
+            nn.add(y, a, o)
+        return o, (t, mr, a, u, v, y, B, H, W, group)
+
+    def backward(self, dout, saved, dx_out, dx_beta=0.0):
+        """dout: grad of this repeat's output (clobbered when r >= 1: it becomes the BN-output
+        gradient); writes / accumulates (dx_beta) the grad of its input into dx_out."""
+        t, mr, a, u, v, y, B, H, W, group = saved
+        st = self.bn.store
+        dz3 = torch.empty_like(y)
+        nn.relu_backward(dout, y, dz3)
+        self.out.wgrad(v, dz3, B, H, W)
+        dv = self.out.dgrad(dz3, B, H, W)
+        self.cnn.wgrad(u, dv, B, H, W)
+        du = self.cnn.dgrad(dv, B, H, W)
+        self.bot.wgrad(a, du, B, H, W)
+        if self.r == 0:
+            da = self.bot.dgrad(du, B, H, W)
+        else:
+            da = self.bot.dgrad(du, B, H, W, out=dout, beta=1.0)     # + residual branch (BN output)
+        nn.bn_backward_grouped(da, t, mr, self.bn.gamma, dx_out, st.g(self.bn.gname), st.g(self.bn.bname),
+                               B, H * W, self.cin, group, dz_beta=dx_beta)
+        return dx_out
+
+
+class CnnBlock(object):
+    def __init__(self, store, eff, name, cin, nf, n_repeats):
+        self.name = name
+        self.reps = []
+        c = cin
+        for r in range(n_repeats):
+            self.reps.append(Repeat(store, eff, name, r, c, nf))
+            c = 2 * nf
+        self.cout = c
+
+    def seps(self):
+        return [s for r in self.reps for s in r.seps()]
+
+    def bns(self):
+        return [r.bn for r in self.reps]
+
+    def forward(self, x, B, H, W, group, train=True):
+        h, saved = x, []
+        for rep in self.reps:
+            h, sv = rep.forward(h, B, H, W, group, train)
+            saved.append(sv)
+        return h, saved
+
+    def backward(self, dy, saved, dx_out, dx_beta=0.0):
+        """dy is clobbered; the block-input gradient is written/accumulated into dx_out."""
+        g = dy
+        for i in range(len(self.reps) - 1, -1, -1):
+            tgt = dx_out if i == 0 else torch.empty_like(saved[i][0])
+            self.reps[i].backward(g, saved[i], tgt, dx_beta if i == 0 else 0.0)
+            g = tgt
+        return dx_out
+
+
+class HourglassNet(object):
+    """tf_centernet_hourglass.build_model(n_classes, tmp_pi, n_filters, n_stacks, n_repeats) on
+    MI355X.  forward(x [B,H,W,3] fp32) -> [B,H/4,W/4,4+C] fp32; backward(d_out bf16)."""
+
+    def __init__(self, n_classes, tmp_pi=0.99, n_filters=128, n_stacks=1, n_repeats=2, device="cuda", seed=0):
+        self.C = n_classes
+        self.nf = n_filters
+        self.n_stacks = n_stacks
+        self.device = torch.device(device)
+        store, eff = ParamStore(), ParamStore()
+        self._build(store, eff, n_classes, tmp_pi, n_filters, n_stacks, n_repeats)
+        store.finalize(self.device, seed)
+        eff.finalize(self.device, seed + 1)
+        self.store, self.eff = store, eff
+        for bn in self.bns():
+            bn.init_buffers(self.device)
+        self.cout_ld = (4 + n_classes + 31) // 32 * 32
+        self.b_eff = torch.zeros(4 + n_classes, dtype=torch.float32, device=self.device)
+        self.g_beff = torch.zeros(4 + n_classes, dtype=torch.float32, device=self.device)
+        self._plan = None
+        self.pack()
+
+    def _build(self, store, eff, C, tmp_pi, nf, n_stacks, n_repeats):
+        self.stem = Stem(store, eff, nf)
+        self.blocks = {}
+        for name, i, o in block_graph(n_stacks):       # only cnn_block_1 sees the stem's nf channels
+            self.blocks[name] = CnnBlock(store, eff, name, nf if i == "blk0" else 2 * nf, nf, n_repeats)
+        self.cnn_out = Conv(store, "cnn_out", 3, 2 * nf, 4 + C, bias=True)
+        self.bfocal = store.add("b_focal", (1,), constant(math.log((1.0 - tmp_pi) / tmp_pi)))
+
+    # ---- parameters ---------------------------------------------------------------------------
+    def seps(self):
+        out = [self.stem.sep]
+        for b in self.blocks.values():
+            out += b.seps()
+        return out
+
+    def bns(self):
+        return [bn for b in self.blocks.values() for bn in b.bns()]
+
+    def _make_plan(self):
+        entries = [self.stem.pack_entry()] + [s.conv.pack_entry() for s in self.seps()[1:]]
+        entries.append(self.cnn_out.pack_entry())
+        self._plan = (nn.SepPlan([s.sep_entry() for s in self.seps()], self.device),
+                      nn.PackPlan(entries, self.device))
+
+    def pack(self):
+        """fold every separable conv, fold b_focal, re-pack all bf16 conv weights (3 launches)."""
+        if self._plan is None:
+            self._make_plan()
+        sep, pk = self._plan
+        sep.fold()
+        pk.run()
+        nn.bias_scalar_fold(self.cnn_out.b, self.store.p(self.bfocal), self.b_eff, 4)
+
+    def unfold_grads(self):
+        self._plan[0].unfold()
+
+    @staticmethod
+    def out_hw(H, W):
+        s2 = lambda n: -(-n // 2)    # noqa: E731  (SAME stride 2 / pool 2 "same")
+        return s2(s2(H)), s2(s2(W))
+
+    # ---- forward / backward -----------------------------------------------------------------
+    def __call__(self, x, training=False, group=None):
+        """Keras-style call: x [B,H,W,3] (array or tensor) -> [B,H/4,W/4,4+C] fp32."""
+        x = torch.as_tensor(x, dtype=torch.float32).to(self.device).contiguous()
+        return self.forward(x, group=group, train=training)
+
+    def forward(self, x, group=None, train=True):
+        """x fp32 NHWC [B,H,W,3]; group = BN sub-batch size (default: the whole batch)."""
+        B, H, W, _ = x.shape
+        group = B if group is None else int(group)
+        dev = x.device
+        v, hw, saved = {}, {}, {}
+        v["blk0"], sv_stem = self.stem.forward(x)
+        H0, W0 = v["blk0"].shape[1], v["blk0"].shape[2]
+        hw["blk0"] = (H0, W0)
+
+        def run(name):
+            _, i, o = self._graph[name]
+            h, w_ = hw[i]
+            v[o], saved[name] = self.blocks[name].forward(v[i], B, h, w_, group, train)
+            hw[o] = (h, w_)
+            return v[o]
+
+        def pool(src, key):
+            h, w_ = hw[src]
+            Ho, Wo = -(-h // 2), -(-w_ // 2)
+            t = v[src]
+            y = torch.empty((B, Ho, Wo, t.shape[3]), dtype=BF16, device=dev)
+            arg = torch.empty((B, Ho, Wo, t.shape[3]), dtype=torch.uint8, device=dev)
+            nn.maxpool2x2(t, y, arg)
+            v[key], hw[key] = y, (Ho, Wo)
+            saved["pool_" + key] = arg
+
+        def res_add(a, b, key):
+            o = torch.empty_like(v[a])
+            nn.add(v[a], v[b], o)
+            v[key], hw[key] = o, hw[a]
+
+        def up_add(prev, other, key):
+            o = torch.empty_like(v[other])
+            nn.upsample_bilinear2x_add(v[prev], v[other], o)
+            v[key], hw[key] = o, hw[other]
+
+        self._graph = dict((b[0], b) for b in block_graph(self.n_stacks))
+        run("cnn_block_1")
+        pool("cnn1", "stack_in")
+        for s in range(self.n_stacks):
+            st = "stack_%d_" % (s + 1)
+            run(st + "enc_block_1"); res_add("stack_in", "enc1", "e1res"); pool("e1res", "e1")   # noqa: E702
+            run(st + "enc_block_2"); res_add("e1", "enc2", "e2res"); pool("e2res", "e2")         # noqa: E702
+            run(st + "enc_block_3"); res_add("e2", "enc3", "e3res"); pool("e3res", "e3")         # noqa: E702
+            run(st + "enc_block_4a"); run(st + "enc_block_4b"); run(st + "enc_block_4")          # noqa: E702
+            res_add("e3", "enc4", "e4res"); pool("e4res", "e4")                                   # noqa: E702
+            run(st + "dec_block_1"); up_add("e4", "dec1", "d1res"); run(st + "dec_out_1")         # noqa: E702
+            run(st + "dec_block_2"); up_add("o1", "dec2", "d2res"); run(st + "dec_out_2")         # noqa: E702
+            run(st + "dec_block_3"); up_add("o2", "dec3", "d3res"); run(st + "dec_out_3")         # noqa: E702
+            run(st + "dec_block_4"); up_add("o3", "dec4", "d4res"); run(st + "dec_out_4")         # noqa: E702
+            if s + 1 < self.n_stacks:
+                v["stack_in"], hw["stack_in"] = v["o4"], hw["o4"]
+        Ho, Wo = hw["o4"]
+        c = self.cnn_out
+        out = torch.empty((B, Ho, Wo, 4 + self.C), dtype=torch.float32, device=dev)
+        d = c.fwd_desc(B, [nn.seg(Ho, Wo, Ho, Wo, c.wf, self.b_eff)], ld_dst=4 + self.C, dst_f32=True)
+        nn.conv_igemm(d, v["o4"], out)
+        self._saved = (sv_stem, saved, v, hw, B, group)
+        return out
+
+    def backward(self, d_out):
+        """d_out: bf16 [B,Ho,Wo,cout_ld] gradient of the output (cvl_centernet_loss).  Writes every
+        parameter gradient of the store (overwrite semantics)."""
+        assert self.n_stacks == 1, "backward wiring is written for one stack (the reference default)"
+        sv_stem, saved, v, hw, B, group = self._saved
+        st = "stack_1_"
+        c = self.cnn_out
+        Ho, Wo = hw["o4"]
+        HW = Ho * Wo
+        c.wgrad(v["o4"], d_out, B, Ho, Wo, bias=False)
+        nn.bias_grad(d_out, int(d_out.shape[-1]), 0, 4 + self.C, 0, HW, HW, B, self.g_beff)
+        nn.bias_scalar_unfold(self.g_beff, c.db, self.store.g(self.bfocal), 4)
+        g = {}
+        g["o4"] = c.dgrad(d_out, B, Ho, Wo)
+
+        def blk(name, dy, dx_key, beta):
+            _, i, _ = self._graph[name]
+            if dx_key not in g:
+                g[dx_key] = torch.empty_like(v[i])
+                beta = 0.0
+            self.blocks[name].backward(dy, saved[name], g[dx_key], beta)
+
+        def unpool(key, src):                 # g[src] = maxpool backward of g[key]
+            t = torch.empty_like(v[src])
+            nn.maxpool2x2_backward(g[key], saved["pool_" + key], t)
+            g[src] = t
+
+        def upb(res, prev):                   # grad of the up-sampled input of a decoder merge
+            t = torch.empty_like(v[prev])
+            nn.upsample_bilinear2x_backward(g[res], t)
+            g[prev] = t
+
+        def acc(dst, src):                    # g[dst] += g[src] (or alias)
+            if dst in g:
+                nn.add(g[dst], g[src], g[dst])
+            else:
+                g[dst] = g[src].clone()
+
+        # decoder, last merge first: dX_res feeds both the dec block and the up-sampled input
+        blk(st + "dec_out_4", g["o4"], "d4res", 0.0)
+        upb("d4res", "o3")
+        blk(st + "dec_block_4", g["d4res"], "stack_in", 0.0)
+        blk(st + "dec_out_3", g["o3"], "d3res", 0.0)
+        upb("d3res", "o2")
+        blk(st + "dec_block_3", g["d3res"], "e1", 0.0)
+        blk(st + "dec_out_2", g["o2"], "d2res", 0.0)
+        upb("d2res", "o1")
+        blk(st + "dec_block_2", g["d2res"], "e2", 0.0)
+        blk(st + "dec_out_1", g["o1"], "d1res", 0.0)
+        upb("d1res", "e4")
+        blk(st + "dec_block_1", g["d1res"], "e3", 0.0)
+        # encoder: x_res = x + cnn(x) -> pool
+        unpool("e4", "e4res")
+        acc("e3", "e4res")
+        blk(st + "enc_block_4", g["e4res"], "enc4b", 0.0)
+        blk(st + "enc_block_4b", g["enc4b"], "enc4a", 0.0)
+        blk(st + "enc_block_4a", g["enc4a"], "e3", 1.0)
+        unpool("e3", "e3res")
+        acc("e2", "e3res")
+        blk(st + "enc_block_3", g["e3res"], "e2", 1.0)
+        unpool("e2", "e2res")
+        acc("e1", "e2res")
+        blk(st + "enc_block_2", g["e2res"], "e1", 1.0)
+        unpool("e1", "e1res")
+        acc("stack_in", "e1res")
+        blk(st + "enc_block_1", g["e1res"], "stack_in", 1.0)
+        unpool("stack_in", "cnn1")
+        blk("cnn_block_1", g["cnn1"], "blk0", 0.0)
+        self.stem.backward(g["blk0"], sv_stem)
+        self.unfold_grads()
+        self._saved = None
+
+    @staticmethod
+    def param_dict(n_classes, seed=0, **kw):
+        """Initial parameters (Keras names -> CPU fp32) without a GPU (for the CPU oracle)."""
+        net = HourglassNet.__new__(HourglassNet)
+        net.C = n_classes
+        store, eff = ParamStore(), ParamStore()
+        net._build(store, eff, n_classes, kw.get("tmp_pi", 0.99), kw.get("n_filters", 128),
+                   kw.get("n_stacks", 1), kw.get("n_repeats", 2))
+        store.finalize("cpu", seed)
+        return {k: store.p(k).clone() for k in store.offsets}

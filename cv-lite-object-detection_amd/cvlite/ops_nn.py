@@ -187,3 +187,94 @@ def gather_rows(src, idx, dst):
     row_bytes = src[0].numel() * src.element_size()
     assert dst[0].numel() * dst.element_size() == row_bytes and src.is_contiguous() and dst.is_contiguous()
     _lib.call("cvl_gather_rows", ptr(src), int(row_bytes), ptr(idx), int(idx.numel()), ptr(dst), stream())
+
+
+# ---- CenterNet hourglass ops (include/cvlite.h "CenterNet hourglass training path") -------------
+def bn_stats(x, B, HW, C, stats):
+    n = int(_lib.load().cvl_bn_stats_workspace_size(B, HW, C))
+    ws = torch.empty(max(n, 16), dtype=torch.uint8, device=x.device)
+    _lib.call("cvl_bn_stats", ptr(x), B, HW, C, ptr(stats), ptr(ws), ws.numel(), stream())
+
+
+def bn_finalize_grouped(stats, mean_rstd, run_mean, run_var, B, C, HW, group, eps, momentum):
+    _lib.call("cvl_bn_finalize_grouped", ptr(stats), ptr(mean_rstd), ptr(run_mean), ptr(run_var), B, C, HW,
+              int(group), float(eps), float(momentum), stream())
+
+
+def bn_backward_grouped(dy, z, mean_rstd, gamma, dz, dgamma, dbeta, B, HW, C, group, dz_beta=0.0, y_relu=None):
+    n = int(_lib.load().cvl_bn_backward_grouped_workspace_size(B, HW, C))
+    ws = torch.empty(n, dtype=torch.uint8, device=dy.device)
+    _lib.call("cvl_bn_backward_grouped", ptr(dy), ptr(y_relu), ptr(z), ptr(mean_rstd), ptr(gamma), ptr(ws), n,
+              ptr(dz), float(dz_beta), ptr(dgamma), ptr(dbeta), B, HW, C, int(group), stream())
+
+
+def maxpool2x2(x, y, argmax):
+    B, H, W, C = x.shape
+    _lib.call("cvl_maxpool2x2", ptr(x), ptr(y), ptr(argmax), B, H, W, C, stream())
+
+
+def maxpool2x2_backward(dy, argmax, dx):
+    B, H, W, C = dx.shape
+    _lib.call("cvl_maxpool2x2_backward", ptr(dy), ptr(argmax), ptr(dx), B, H, W, C, stream())
+
+
+def upsample_bilinear2x_add(prev, other, out):
+    B, h, w, C = prev.shape
+    assert tuple(other.shape) == (B, 2 * h, 2 * w, C) and out.shape == other.shape
+    _lib.call("cvl_upsample_bilinear2x_add", ptr(prev), ptr(other), ptr(out), B, h, w, C, stream())
+
+
+def upsample_bilinear2x_backward(dout, dprev, beta=0.0):
+    B, h, w, C = dprev.shape
+    assert tuple(dout.shape) == (B, 2 * h, 2 * w, C)
+    _lib.call("cvl_upsample_bilinear2x_backward", ptr(dout), ptr(dprev), B, h, w, C, float(beta), stream())
+
+
+class SepItem(ctypes.Structure):
+    _fields_ = [("dw", c_void_p), ("pw", c_void_p), ("weff", c_void_p), ("gweff", c_void_p), ("gdw", c_void_p),
+                ("gpw", c_void_p), ("taps", c_int), ("cin", c_int), ("cout", c_int), ("pad_", c_int)]
+
+
+class SepPlan(object):
+    """Device tables of cvl_sep_fold_multi / cvl_sep_unfold_multi: every SeparableConv2D's dense
+    fold (forward) and gradient unfold (backward) in one launch each.
+    entries: (dw [kh,kw,Cin,1], pw [1,1,Cin,Cout], weff, gweff, gdw, gpw) fp32 device tensors."""
+
+    def __init__(self, entries, device):
+        items = (SepItem * len(entries))()
+        rows = []
+        self._keep = []
+        for i, (dw, pw, weff, gweff, gdw, gpw) in enumerate(entries):
+            kh, kw, cin, _ = dw.shape
+            cout = pw.shape[3]
+            assert tuple(weff.shape) == (kh, kw, cin, cout) and gweff.shape == weff.shape
+            it = items[i]
+            it.dw, it.pw, it.weff = dw.data_ptr(), pw.data_ptr(), weff.data_ptr()
+            it.gweff, it.gdw, it.gpw = gweff.data_ptr(), gdw.data_ptr(), gpw.data_ptr()
+            it.taps, it.cin, it.cout = kh * kw, cin, cout
+            self._keep.append((dw, pw, weff, gweff, gdw, gpw))
+            rows += [(i, ci) for ci in range(cin)]
+        self.items = torch.frombuffer(bytearray(bytes(items)), dtype=torch.uint8).to(device)
+        self.rows = torch.tensor(rows, dtype=torch.int32, device=device)
+        self.nrows = len(rows)
+
+    def fold(self):
+        _lib.call("cvl_sep_fold_multi", ptr(self.items), ptr(self.rows), self.nrows, stream())
+
+    def unfold(self):
+        _lib.call("cvl_sep_unfold_multi", ptr(self.items), ptr(self.rows), self.nrows, stream())
+
+
+def bias_scalar_fold(bias, scalar, b_eff, c0):
+    _lib.call("cvl_bias_scalar_fold", ptr(bias), ptr(scalar), ptr(b_eff), int(bias.numel()), int(c0), stream())
+
+
+def bias_scalar_unfold(g_eff, g_bias, g_scalar, c0):
+    _lib.call("cvl_bias_scalar_unfold", ptr(g_eff), ptr(g_bias), ptr(g_scalar), int(g_eff.numel()), int(c0), stream())
+
+
+def adam_clip_update(w, g, m, v, lr_dev, iterations, beta1, beta2, eps, inv_bs, clip, ws=None):
+    if ws is None:
+        ws = torch.empty(1, dtype=torch.float64, device=w.device)
+    _lib.call("cvl_adam_clip_update", ptr(w), ptr(g), ptr(m), ptr(v), w.numel(), ptr(lr_dev), ptr(iterations),
+              float(beta1), float(beta2), float(eps), float(inv_bs), float(clip), ptr(ws), stream())

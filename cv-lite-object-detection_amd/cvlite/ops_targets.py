@@ -84,10 +84,11 @@ def retina_assign(boxes, nbox, img_dim, pad, anchor_dims, num_classes, iou_thres
     return out, nt
 
 
-def centernet_assign(boxes, nbox, img_dim, pad_hw, num_classes, stride=8):
+def centernet_assign(boxes, nbox, img_dim, pad_hw, num_classes, stride=8, out=None):
     """CenterNet hourglass centroid targets -> [B, pad_w/s, pad_h/s, 4+C]."""
     B, nmax = _boxes_args(boxes, nbox, img_dim)
-    out = torch.empty((B, pad_hw[1] // stride, pad_hw[0] // stride, 4 + num_classes), device=boxes.device,
+    if out is None:
+        out = torch.empty((B, pad_hw[1] // stride, pad_hw[0] // stride, 4 + num_classes), device=boxes.device,
                       dtype=torch.float32)
     _lib.call("cvl_centernet_assign", ptr(boxes), ptr(nbox), ptr(img_dim), B, nmax, int(pad_hw[0]),
               int(pad_hw[1]), int(num_classes), int(stride), ptr(out), _lib.stream())
@@ -157,3 +158,21 @@ def nms(boxes_xyxy, classes, iou_threshold):
     nk = nkeep.cpu().tolist()
     idx = torch.cat([keep[c, :nk[c]] for c in range(ncls)]) if ncls else keep.new_zeros(0)
     return boxes_xyxy[idx.long()]
+
+
+def centernet_loss(pred, targets, num_classes, cls_scale=2.5, reg_scale=1.0, d_pred=None, losses=None):
+    """CenterNet model_loss fwd+bwd (tf_centernet_hourglass.py:492-505 in train_step :537-549) off
+    the output conv.  pred [B,P,ld] f32 (reg 0..3, cls 4..), targets [B,P,4+C] f32.
+    Returns (losses [B,2] = (cls, reg), d_pred bf16 [B,P,ld_d] of cls_scale*cls + reg_scale*reg)."""
+    _lib.require_cuda(pred, targets)
+    B, P = int(targets.shape[0]), int(targets.shape[1])
+    dev = targets.device
+    if losses is None:
+        losses = torch.empty((B, 2), device=dev, dtype=torch.float32)
+    if d_pred is None:
+        d_pred = torch.empty((B, P, (4 + num_classes + 7) // 8 * 8), device=dev, dtype=torch.bfloat16)
+    ws = torch.empty(int(_lib.load().cvl_det_loss_workspace_size(B, P)), device=dev, dtype=torch.uint8)
+    _lib.call("cvl_centernet_loss", ptr(pred), int(pred.shape[-1]), ptr(targets), B, P, int(num_classes),
+              float(cls_scale), float(reg_scale), ptr(losses), ptr(d_pred), int(d_pred.shape[-1]), ptr(ws),
+              _lib.stream())
+    return losses, d_pred

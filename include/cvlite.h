@@ -260,6 +260,80 @@ size_t cvl_nms_workspace_size(int n, int ncls);
 int cvl_nms(const double* boxes, int n, const double* classes, int ncls, double iou_threshold,
             int32_t* keep, int32_t* nkeep, void* workspace, cvl_stream_t stream);
 
+/* ==========================================================================================
+ * CenterNet hourglass training path (CenterNet/tf_centernet_hourglass.py:87-353 build_model,
+ * :492-564 model_loss / train_step).
+ * ========================================================================================== */
+
+/* BatchNormalization over sub-batches: train_step (:527-545) runs one Keras training-mode forward
+ * per sub-batch of `group` images, so statistics span the sub-batch (groups [g*G, min(g*G+G, B)),
+ * the last may be short); running stats are updated once per group, in order.
+ * cvl_bn_stats: stats[b][c] = (sum, sum of squares) over H*W of a bf16 NHWC tensor (float64,
+ *   deterministic), the input of cvl_bn_finalize[_grouped].
+ * cvl_bn_backward_grouped: as cvl_bn_backward (no ReLU output / conv bias terms) with group
+ *   statistics; dz = BN-backward + dz_beta * dz (accumulate into an existing gradient). */
+size_t cvl_bn_stats_workspace_size(int B, int HW, int C);
+int cvl_bn_stats(const void* x, int B, int HW, int C, double* stats, void* workspace, size_t workspace_bytes,
+                 cvl_stream_t stream);
+int cvl_bn_finalize_grouped(const double* stats, float* mean_rstd, float* run_mean, float* run_var, int B, int C,
+                            int HW, int group, float eps, float momentum, cvl_stream_t stream);
+size_t cvl_bn_backward_grouped_workspace_size(int B, int HW, int C);
+int cvl_bn_backward_grouped(const void* dy, const void* y_relu, const void* z, const float* mean_rstd,
+                            const float* gamma, void* workspace, size_t workspace_bytes, void* dz, float dz_beta,
+                            float* dgamma, float* dbeta, int B, int HW, int C, int group, cvl_stream_t stream);
+
+/* downsample_block (:158-161): MaxPooling2D(2, 2, "same") -> [B][ceil(H/2)][ceil(W/2)][C];
+ * argmax [B][Ho][Wo][C] uint8 (0..3, first maximum in window order). */
+int cvl_maxpool2x2(const void* x, void* y, uint8_t* argmax, int B, int H, int W, int C, cvl_stream_t stream);
+int cvl_maxpool2x2_backward(const void* dy, const uint8_t* argmax, void* dx, int B, int H, int W, int C,
+                            cvl_stream_t stream);
+
+/* Decoder merge (:276-284): out[B][2h][2w][C] = other + UpSampling2D(bilinear)(prev[B][h][w][C]),
+ * TF resize_bilinear with half-pixel centres.  Backward: dprev = adjoint(dout) (+ beta * dprev). */
+int cvl_upsample_bilinear2x_add(const void* prev, const void* other, void* out, int B, int h, int w, int C,
+                                cvl_stream_t stream);
+int cvl_upsample_bilinear2x_backward(const void* dout, void* dprev, int B, int h, int w, int C, float beta,
+                                     cvl_stream_t stream);
+
+/* SeparableConv2D (:110-123, :178-181; depth_multiplier 1) runs as ONE dense conv on the MFMA
+ * conv kernels with the folded kernel W[t][ci][co] = D[t][ci] * P[ci][co] (t = kh*kw taps; D =
+ * Keras depthwise_kernel [kh][kw][Cin][1], P = pointwise_kernel [1][1][Cin][Cout]).
+ * cvl_sep_fold_multi writes weff (fp32 HWIO) for every item; cvl_sep_unfold_multi turns the dense
+ * kernel gradient gweff into gdw / gpw.  rows: DEVICE int32 [nrows][2] = (item, ci), one row per
+ * input channel of every item.  items: DEVICE array. */
+typedef struct {
+  const float* dw;
+  const float* pw;
+  float* weff;
+  const float* gweff;
+  float* gdw;
+  float* gpw;
+  int taps, cin, cout, pad_;
+} cvl_sep_item;
+int cvl_sep_fold_multi(const cvl_sep_item* items, const int32_t* rows, int nrows, cvl_stream_t stream);
+int cvl_sep_unfold_multi(const cvl_sep_item* items, const int32_t* rows, int nrows, cvl_stream_t stream);
+
+/* BiasLayer b_focal (tf_bias_layer.py:4-14; :347) folded into the output conv bias:
+ * b_eff[c] = bias[c] + (c >= c0 ? *scalar : 0); unfold: g_bias = g_eff, *g_scalar = sum_{c>=c0} g_eff. */
+int cvl_bias_scalar_fold(const float* bias, const float* scalar, float* b_eff, int n, int c0, cvl_stream_t stream);
+int cvl_bias_scalar_unfold(const float* g_eff, float* g_bias, float* g_scalar, int n, int c0, cvl_stream_t stream);
+
+/* model_loss (:492-505) fwd + bwd off the output conv: pred [B*P][ld_pred] fp32 (reg 0..3, class
+ * logits 4..4+C), targets [B*P][4+C] (cvl_centernet_assign); losses [B][2] = (cls, reg) sums;
+ * d_pred bf16 [B*P][ld_d] = d(cls_scale*cls + reg_scale*reg)/d(pred), channels >= 4+C zeroed.
+ * workspace >= cvl_det_loss_workspace_size(B, P). */
+int cvl_centernet_loss(const float* pred, int ld_pred, const float* targets, int B, int P, int num_classes,
+                       float cls_scale, float reg_scale, float* losses, void* d_pred, int ld_d, void* workspace,
+                       cvl_stream_t stream);
+
+/* train_step update (:555-563) with tf.keras.optimizers.Adam (train_hourglass_voc.py:330):
+ * g <- clip_by_global_norm(g * inv_bs, clip); t = *iterations + 1;
+ * m += (g - m)(1 - b1); v += (g^2 - v)(1 - b2); w -= lr sqrt(1 - b2^t) / (1 - b1^t) * m / (sqrt(v) + eps);
+ * then *iterations += 1.  lr read from device memory; sumsq_ws: one float64. */
+int cvl_adam_clip_update(float* w, const float* g, float* m, float* v, int64_t n, const float* lr_dev,
+                         int32_t* iterations, float beta1, float beta2, float eps, float inv_bs, float clip,
+                         double* sumsq_ws, cvl_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif
