@@ -48,6 +48,60 @@ def allreduce_grads(flat_grad, group=None, bucket_bytes=BUCKET_BYTES):
     return flat_grad
 
 
+def param_ranges(store, names, bucket_bytes=BUCKET_BYTES):
+    """Contiguous [start, end) element ranges of the flat buffer covering `names` (alignment gaps
+    between neighbouring tensors are included: their gradients stay 0), split at bucket_bytes."""
+    spans = sorted((store.offsets[n][0], store.offsets[n][0] + store.offsets[n][1]) for n in names)
+    merged = []
+    for a, b in spans:
+        if merged and a <= (merged[-1][1] + 15) // 16 * 16:
+            merged[-1][1] = max(merged[-1][1], b)
+        else:
+            merged.append([a, b])
+    per = max(1, bucket_bytes // 4)
+    out = []
+    for a, b in merged:
+        for s in range(a, b, per):
+            out.append((s, min(s + per, b)))
+    return out
+
+
+class GradSync(object):
+    """All-reduce of the flat fp32 gradient buffer overlapped with the backward pass.
+
+    `groups` = [(name, [param names])] in the order the backward pass finalises them; the model's
+    backward calls `ready(name)` as soon as a group's gradients are final, which launches that
+    group's buckets as async RCCL all-reduces (ProcessGroupNCCL runs them on its own HIP stream,
+    ordered after the work already queued on the compute stream), so the collectives of the late
+    layers run while the backward of the early layers computes.  `finish()` makes the compute
+    stream wait for all of them (no host sync) before the optimizer step.  HIP-graph trainers
+    capture the backward in segments split at the ready points and call ready() between replays.
+    With world size 1 every call is a no-op."""
+
+    def __init__(self, store, groups, group=None, bucket_bytes=BUCKET_BYTES):
+        self.grad = store.grad
+        self.pg = group
+        self.order = [n for n, _ in groups]
+        self.ranges = {n: param_ranges(store, names, bucket_bytes) for n, names in groups}
+        names = [k for _, ns in groups for k in ns]
+        assert len(names) == len(set(names)) == len(store.offsets), \
+            "gradient groups must cover every parameter exactly once"
+        self.works = []
+        self.active = tdist.is_initialized() and tdist.get_world_size(group) > 1
+
+    def ready(self, name):
+        if not self.active:
+            return
+        for a, b in self.ranges[name]:
+            self.works.append(tdist.all_reduce(self.grad[a:b], op=tdist.ReduceOp.SUM, group=self.pg,
+                                               async_op=True))
+
+    def finish(self):
+        for w in self.works:
+            w.wait()
+        self.works = []
+
+
 def max_over_ranks(value, device):
     if not tdist.is_initialized():
         return value

@@ -144,14 +144,35 @@ class FPNDetector(object):
         s = self._saved
         return self._heads_forward(towers, s["B"], s["shapes"], s["off"], s["P"])
 
+    # ---- gradient groups (data-parallel overlap, dist.GradSync) ---------------------------------------
+    def grad_groups(self):
+        """[(name, param names)] in the order backward() finalises them; backward(hook=) calls
+        hook(name) at each of these points."""
+        def names(convs):
+            return [n for c in convs for n in (c.wname, c.bname) if n]
+
+        def units(us):
+            return [n for u in us for n in (u.conv.wname, u.conv.bname, u.bn.gname, u.bn.bname)]
+        bb = self.backbone
+        g = [("heads_towers", names(self.head_convs() + self.cls_tower + self.reg_tower)),
+             ("fpn", names([self.c3_1x1, self.c4_1x1, self.c5_1x1, self.c3_3x3, self.c4_3x3, self.c5_3x3,
+                            self.c6_3x3, self.c7_3x3]))]
+        for si in (3, 2, 1):
+            g.append(("conv%d" % (si + 2), units([u for b in bb.stages[si] for u in b.units()])))
+        stem = [bb.stem.conv.wname, bb.stem.conv.bname, bb.stem.bn.gname, bb.stem.bn.bname]
+        g.append(("conv2_stem", units([u for b in bb.stages[0] for u in b.units()]) + stem))
+        return g
+
     # ---- backward ------------------------------------------------------------------------------------
-    def backward(self, *head_grads):
+    def backward(self, *head_grads, hook=None):
         s = self._saved
         dA = self._heads_backward(head_grads, s["towers"], s["B"], s["shapes"], s["off"], s["P"])
-        self.trunk_backward(dA)
+        self.trunk_backward(dA, hook=hook)
 
-    def trunk_backward(self, dA_top):
-        """dA_top: per tower, the gradient w.r.t. its ReLU output (buffer reused in place)."""
+    def trunk_backward(self, dA_top, hook=None):
+        """dA_top: per tower, the gradient w.r.t. its ReLU output (buffer reused in place).
+        hook(name) fires as each grad_groups() group becomes final."""
+        hook = hook or (lambda name: None)
         s = self._saved
         B, shapes, off, P = s["B"], s["shapes"], s["off"], s["P"]
         dev = s["F"].device
@@ -169,6 +190,7 @@ class FPNDetector(object):
                 dst = dF if i == 0 else torch.empty_like(F)
                 nn.conv_igemm(dd, dA, dst)
                 dA = dst
+        hook("heads_towers")
         # ---- FPN backward (fcos.py:49-72) ----
         (C3, C4, C5) = s["C"]
         (c3, H3, W3), (c4, H4, W4), (c5, H5, W5) = C3, C4, C5
@@ -216,5 +238,6 @@ class FPNDetector(object):
                                               (self.c5_1x1, c5, H5, W5, dl5, dC5, 1.0)):
             conv.wgrad(src, dl, B, h, w)
             conv.dgrad(dl, B, h, w, out=dC, beta=beta)
-        self.backbone.backward([dC3, dC4, dC5], s["bsv"])
+        hook("fpn")
+        self.backbone.backward([dC3, dC4, dC5], s["bsv"], hook=hook)
         self._saved = None

@@ -176,8 +176,11 @@ class ResNet50(object):
             taps.append((h, H, W))
         return taps[1:], (sv_stem, saved)
 
-    def backward(self, d_taps, saved):
-        """d_taps: gradients of [C3, C4, C5]; they are used in place as stage-output buffers."""
+    def backward(self, d_taps, saved, hook=None):
+        """d_taps: gradients of [C3, C4, C5]; they are used in place as stage-output buffers.
+        hook(name) fires when a stage's parameter gradients are final ("conv5" .. "conv3", then
+        "conv2_stem")."""
+        hook = hook or (lambda name: None)
         sv_stem, ssv = saved
         dC = {1: d_taps[0], 2: d_taps[1], 3: d_taps[2]}
         dh = dC[3]
@@ -190,4 +193,7 @@ class ResNet50(object):
                     dh = st[bi].backward(dh, ssv[si][bi], dx_out=dC[si - 1], dx_beta=1.0)
                 else:
                     dh = st[bi].backward(dh, ssv[si][bi])
+            if si > 0:
+                hook("conv%d" % (si + 2))
         self.stem.backward(dh, sv_stem)
+        hook("conv2_stem")

@@ -13,6 +13,7 @@ import numpy as np
 import torch
 
 from . import dist
+from .stepper import GraphStepper
 from . import ops_nn as nn
 from . import ops_targets as ot
 
@@ -42,7 +43,7 @@ class Adam(object):
                             self.beta_2, self.epsilon, inv_bs, clip, ws=self.ws)
 
 
-class CenterNetTrainer(object):
+class CenterNetTrainer(GraphStepper):
     def __init__(self, net, batch_size, image_hw, sub_batch_sz=2, n_max=64, optimizer=None, cls_lambda=2.5,
                  reg_lambda=1.0, grad_clip=1.0, world=1, use_graph=True):
         self.net = net
@@ -65,11 +66,10 @@ class CenterNetTrainer(object):
         self.targets = torch.zeros((B, self.Ho, self.Wo, 4 + self.C), dtype=torch.float32, device=dev)
         self.d_out = torch.zeros((B, self.Ho, self.Wo, net.cout_ld), dtype=torch.bfloat16, device=dev)
         self.losses = torch.zeros((B, 2), dtype=torch.float32, device=dev)
-        self.use_graph = use_graph
         self.assign = True
-        self.g_fb = self.g_up = None
+        self._init_stepper(net, world, use_graph)
 
-    def _fwd_bwd(self):
+    def _fwd_bwd(self, hook=None):
         if self.assign:
             ot.centernet_assign(self.boxes, self.nbox, self.img_dim, (self.H, self.W), self.C, stride=self.stride,
                                 out=self.targets)
@@ -78,27 +78,11 @@ class CenterNetTrainer(object):
                           self.cls_lambda, self.reg_lambda, d_pred=self.d_out.view(self.B, self.P, -1),
                           losses=self.losses)
         self.out = out
-        self.net.backward(self.d_out)
+        self.net.backward(self.d_out, hook=hook)
 
     def _update(self):
         self.opt.apply(self.net.store, 1.0 / (self.B * self.world), self.clip)
         self.net.pack()
-
-    def capture(self):
-        s = torch.cuda.Stream()
-        s.wait_stream(torch.cuda.current_stream())
-        with torch.cuda.stream(s):
-            for _ in range(2):
-                self._fwd_bwd()
-        torch.cuda.current_stream().wait_stream(s)
-        torch.cuda.synchronize()
-        self.g_fb = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(self.g_fb):
-            self._fwd_bwd()
-        self.g_up = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(self.g_up):
-            self._update()
-        torch.cuda.synchronize()
 
     def load_batch(self, images, boxes, nbox):
         self.images.copy_(images, non_blocking=True)
@@ -111,22 +95,8 @@ class CenterNetTrainer(object):
         self.targets.copy_(targets, non_blocking=True)
         if self.assign:
             self.assign = False
-            self.g_fb = None                      # re-capture without the assign launch
+            self.invalidate()                     # re-capture without the assign launch
 
-    def step(self):
-        if self.use_graph:
-            if self.g_fb is None:
-                self.capture()
-            self.g_fb.replay()
-        else:
-            self._fwd_bwd()
-        if self.world > 1:
-            dist.allreduce_grads(self.net.store.grad)
-        if self.use_graph:
-            self.g_up.replay()
-        else:
-            self._update()
-        return self.losses
 
 
 def synthetic_batch(B, H, W, n_classes, n_max=64, seed=1234, device="cuda", mean_boxes=2.4):

@@ -20,6 +20,7 @@ import numpy as np
 import torch
 
 from . import dist
+from .stepper import GraphStepper
 from . import ops_nn as nn
 from . import ops_targets as ot
 
@@ -34,7 +35,7 @@ class SGD(object):
         self.momentum = float(momentum)
 
 
-class FCOSTrainer(object):
+class FCOSTrainer(GraphStepper):
     def __init__(self, net, batch_size, image_hw, n_max=16, init_lr=5e-4, min_lr=1e-5, decay_step=1000,
                  decay_rate=0.9, momentum=0.9, gradient_clip=1.0, reg_type="l1", weight_decay=0.0,
                  world=1, use_graph=True, st_step=0):
@@ -64,18 +65,17 @@ class FCOSTrainer(object):
         self.lr = torch.tensor([init_lr], dtype=torch.float32, device=dev)
         self.step_dev = torch.tensor([st_step], dtype=torch.int32, device=dev)
         self.sumsq = torch.zeros(1, dtype=torch.float64, device=dev)
-        self.use_graph = use_graph
-        self.g_fb = self.g_up = None
+        self._init_stepper(net, world, use_graph)
 
     # ---- the two device phases -------------------------------------------------------------------
-    def _fwd_bwd(self):
+    def _fwd_bwd(self, hook=None):
         tg, _ = ot.fcos_assign(self.boxes, self.nbox, self.img_dim, (self.H, self.W), self.C,
                                out=self.targets, num_targets=self.ntgt)
         reg, cls = self.net.forward(self.images)
         losses, _, _ = ot.fcos_loss(reg, cls, tg, self.C, reg_type=self.reg_type, grad_scale=1.0,
                                     d_reg=self.d_reg, d_cls=self.d_cls)
         self.losses.copy_(losses)
-        self.net.backward(self.d_reg, self.d_cls)
+        self.net.backward(self.d_reg, self.d_cls, hook=hook)
 
     def _update(self):
         init_lr, min_lr, rate, dstep = self.sched
@@ -85,43 +85,12 @@ class FCOSTrainer(object):
                            self.clip, ws=self.sumsq)
         self.net.pack()
 
-    def capture(self):
-        """Warm the allocator on a side stream, then capture both phases into HIP graphs."""
-        s = torch.cuda.Stream()
-        s.wait_stream(torch.cuda.current_stream())
-        with torch.cuda.stream(s):
-            for _ in range(2):
-                self._fwd_bwd()
-        torch.cuda.current_stream().wait_stream(s)
-        torch.cuda.synchronize()
-        self.g_fb = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(self.g_fb):
-            self._fwd_bwd()
-        self.g_up = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(self.g_up):
-            self._update()
-        torch.cuda.synchronize()
-
     def load_batch(self, images, boxes, nbox):
         """Device-to-device copy of one batch into the static input buffers."""
         self.images.copy_(images, non_blocking=True)
         self.boxes.copy_(boxes, non_blocking=True)
         self.nbox.copy_(nbox, non_blocking=True)
 
-    def step(self):
-        if self.use_graph:
-            if self.g_fb is None:
-                self.capture()
-            self.g_fb.replay()
-        else:
-            self._fwd_bwd()
-        if self.world > 1:
-            dist.allreduce_grads(self.net.store.grad)
-        if self.use_graph:
-            self.g_up.replay()
-        else:
-            self._update()
-        return self.losses
 
 
 # -------------------------------------------------------------------------------------------------

@@ -17,6 +17,7 @@ import numpy as np
 import torch
 
 from . import dist
+from .stepper import GraphStepper
 from . import ops_nn as nn
 from . import ops_targets as ot
 from .retina_net import RetinaNetNet
@@ -24,7 +25,7 @@ from .retina_net import RetinaNetNet
 BF16 = torch.bfloat16
 
 
-class RetinaTrainer(object):
+class RetinaTrainer(GraphStepper):
     def __init__(self, net, anchors, batch_size, img_size, n_max=64, init_lr=0.01, min_lr=1e-5,
                  momentum=0.9, gradient_clip=1.0, candidates=3, world=1, use_graph=True, st_step=0):
         assert isinstance(net, RetinaNetNet)
@@ -57,10 +58,9 @@ class RetinaTrainer(object):
         self.lr = torch.tensor([init_lr], dtype=torch.float32, device=dev)
         self.step_dev = torch.tensor([st_step], dtype=torch.int32, device=dev)
         self.sumsq = torch.zeros(1, dtype=torch.float64, device=dev)
-        self.use_graph = use_graph
-        self.g_fb = self.g_up = None
+        self._init_stepper(net, world, use_graph)
 
-    def _fwd_bwd(self):
+    def _fwd_bwd(self, hook=None):
         self.anchors.format_data_batched(self.cand_boxes, self.cand_nbox, self.cand_dim, self.S,
                                          out=self.cand_targets, num_targets=self.cand_counts)
         nn.select_first_nonzero(self.cand_counts, self.B, self.sel, self.img_w)
@@ -69,7 +69,7 @@ class RetinaTrainer(object):
         reg, cls = self.net.forward(self.images)
         ot.retina_loss(reg, cls, self.targets, self.level_cells, self.A, self.C, img_weight=self.img_w,
                        d_reg=self.d_reg, d_cls=self.d_cls, losses=self.losses)
-        self.net.backward(self.d_reg, self.d_cls)
+        self.net.backward(self.d_reg, self.d_cls, hook=hook)
 
     def _update(self):
         init_lr, min_lr, rate, dstep = self.sched
@@ -79,22 +79,6 @@ class RetinaTrainer(object):
                            self.clip, ws=self.sumsq)
         self.net.pack()
 
-    def capture(self):
-        s = torch.cuda.Stream()
-        s.wait_stream(torch.cuda.current_stream())
-        with torch.cuda.stream(s):
-            for _ in range(2):
-                self._fwd_bwd()
-        torch.cuda.current_stream().wait_stream(s)
-        torch.cuda.synchronize()
-        self.g_fb = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(self.g_fb):
-            self._fwd_bwd()
-        self.g_up = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(self.g_up):
-            self._update()
-        torch.cuda.synchronize()
-
     def load_candidates(self, images, boxes, nbox):
         """Device-to-device copy of the 3*bs candidate images and their boxes."""
         self.cand_images.copy_(images, non_blocking=True)
@@ -102,20 +86,6 @@ class RetinaTrainer(object):
         self.cand_boxes[:, :boxes.shape[1]].copy_(boxes, non_blocking=True)
         self.cand_nbox.copy_(nbox, non_blocking=True)
 
-    def step(self):
-        if self.use_graph:
-            if self.g_fb is None:
-                self.capture()
-            self.g_fb.replay()
-        else:
-            self._fwd_bwd()
-        if self.world > 1:
-            dist.allreduce_grads(self.net.store.grad)
-        if self.use_graph:
-            self.g_up.replay()
-        else:
-            self._update()
-        return self.losses
 
 
 def synthetic_coco_batch(n, S, n_classes=80, n_max=50, seed=1234, device="cuda"):

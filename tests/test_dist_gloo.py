@@ -51,7 +51,25 @@ def _worker(rank, world, port, out_path):
     x = torch.arange(1000, dtype=torch.float32) * (rank + 1)
     dist.allreduce_grads(x, bucket_bytes=256)
     assert torch.equal(x, torch.arange(1000, dtype=torch.float32) * 3)
-    # 2) DP training step
+    # 2) overlapped per-group all-reduce (GradSync) over the real FCOS parameter layout, fired in
+    #    backward order, equals one all-reduce of the whole flat buffer
+    from cvlite.layers import ParamStore
+    net = FCOSNet.__new__(FCOSNet)
+    st = ParamStore()
+    net._build_layers(st, C)
+    st.finalize("cpu", 0)
+    g = torch.Generator().manual_seed(100 + rank)
+    for k in st.offsets:
+        st.g(k).copy_(torch.randn(st.g(k).shape, generator=g))
+    expect = st.grad.clone()
+    dist.allreduce_grads(expect)
+    sync = dist.GradSync(st, net.grad_groups(), bucket_bytes=1 << 20)
+    assert sync.order == ["heads_towers", "fpn", "conv5", "conv4", "conv3", "conv2_stem"]
+    for name in sync.order:
+        sync.ready(name)
+    sync.finish()
+    assert torch.equal(st.grad, expect)
+    # 3) DP training step
     params = FCOSNet.param_dict(C, seed=0)                 # identical init on every rank
     imgs, tg = _batch(world * BS, seed=11)
     shard = slice(rank * BS, (rank + 1) * BS)
