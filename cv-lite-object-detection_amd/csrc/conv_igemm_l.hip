@@ -19,7 +19,6 @@ namespace {
 constexpr int BM = 256;
 constexpr int BK = 64;
 constexpr int NT = 512;
-constexpr int NST = 3;
 
 __device__ __attribute__((aligned(16))) cvl_bf16 g_zero_l[8];
 
@@ -37,9 +36,13 @@ __device__ __forceinline__ void wait_vm() {
   __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | (7 << 4) | (15 << 8));
 }
 
-template <int BN, bool DGRAD>
+// BN x WGM x NST: 128/64-wide tiles run 8 waves as 4 (M) x 2 (N) with a 3-deep ring; the
+// 256-wide tile runs them as 2 x 4 (each wave 128 x 64: a quarter fewer LDS bytes per MFMA and
+// half the DMA issues per FLOP) with a 2-deep ring (2 x 64 KiB).
+template <int BN, int WGM, int NST, bool DGRAD, bool PRIO>
 __global__ void __launch_bounds__(NT) conv_igemm_l_kernel(ConvArgs a) {
-  constexpr int WM = BM / 4, WN = BN / 2;
+  constexpr int WGN = 8 / WGM;
+  constexpr int WM = BM / WGM, WN = BN / WGN;
   constexpr int TM = WM / 16, TN = WN / 16;
   constexpr int AP = BM * BK / (NT * 8);        // A pieces (16 B) per thread per K step: 4
   constexpr int BP = BN * BK / (NT * 8);        // B pieces per thread: 2 (BN 128) or 1 (BN 64)
@@ -126,7 +129,7 @@ __global__ void __launch_bounds__(NT) conv_igemm_l_kernel(ConvArgs a) {
     for (int p = 0; p < BP; ++p) glds16(b_base[p] + k0, Bb + (p * 64 + wave * 8) * BK);
   };
 
-  const int wm = wave >> 1, wn = wave & 1;
+  const int wm = wave / WGN, wn = wave % WGN;
   const int lr = lane & 15, lg = lane >> 4;
   f32x4 acc[TM][TN];
 #pragma unroll
@@ -135,16 +138,18 @@ __global__ void __launch_bounds__(NT) conv_igemm_l_kernel(ConvArgs a) {
     for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   const int nk = a.K / BK;
-  issue(0, 0);
-  if (nk > 1) issue(1, 1);
+#pragma unroll
+  for (int t = 0; t < NST - 1; ++t)
+    if (t < nk) issue(t, t);
   int slot = 0;
   for (int kt = 0; kt < nk; ++kt) {
-    // tile kt landed (this wave's DMA), tile kt+1 may stay in flight; then every wave's
-    if (kt + 1 < nk) wait_vm<GPW>();
+    // tile kt landed (this wave's DMA; with a 3-deep ring tile kt+1 may stay in flight), then
+    // every wave's
+    if (NST == 3 && kt + 1 < nk) wait_vm<GPW>();
     else wait_vm<0>();
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
-    if (kt + 2 < nk) issue(kt + 2, slot == 0 ? 2 : slot - 1);   // the slot read in step kt-1
+    if (kt + NST - 1 < nk) issue(kt + NST - 1, slot == 0 ? NST - 1 : slot - 1);   // slot read in step kt-1
     const cvl_bf16* Ac = lds + slot * STAGE;
     const cvl_bf16* Bc = Ac + BM * BK;
 #pragma unroll
@@ -164,9 +169,20 @@ __global__ void __launch_bounds__(NT) conv_igemm_l_kernel(ConvArgs a) {
 #pragma unroll
       for (int i = 0; i < TM; ++i)
 #pragma unroll
-        for (int j = 0; j < TN; ++j)
+        for (int j = 0; j < TN; ++j) {
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
               __builtin_bit_cast(bf16x8, fa[i]), __builtin_bit_cast(bf16x8, fb[j]), acc[i][j], 0, 0, 0);
+          if (PRIO && i == 0 && j == 0) {            // keep the MFMA cluster together (T5)
+            __builtin_amdgcn_sched_barrier(0);
+            __builtin_amdgcn_s_setprio(1);
+            __builtin_amdgcn_sched_barrier(0);
+          }
+        }
+      if (PRIO) {
+        __builtin_amdgcn_sched_barrier(0);
+        __builtin_amdgcn_s_setprio(0);
+        __builtin_amdgcn_sched_barrier(0);
+      }
     }
     asm volatile("" ::: "memory");
     slot = slot == NST - 1 ? 0 : slot + 1;
@@ -273,28 +289,44 @@ int cvl_conv_igemm_l(const cvl_conv_desc* d, int dst_up, int dst_w, const void* 
   if (cvl_env_flag("CVL_CONV_NO_L")) return -1;
   if (d->Cin % 64 != 0 || d->relu_in || d->dst_f32 || d->n_store % 8 || d->ld_dst % 8 || d->dst_coff % 8)
     return -1;
-  const int bn = d->Npad % 128 == 0 ? 128 : (d->Npad % 64 == 0 ? 64 : 0);
+  // 256-wide tiles for forward launches only (measured on the FCOS tower shape: forward +17 % per
+  // tile, data-gradient -35 %, tools/conv_ab.py)
+  const bool w256 = d->Npad % 256 == 0 && !cvl_env_flag("CVL_CONV_NO_256") &&
+                    (d->mode == CVL_CONV_FWD || cvl_env_flag("CVL_CONV_DGRAD_256"));
+  const int bn = w256 ? 256 : (d->Npad % 128 == 0 ? 128 : (d->Npad % 64 == 0 ? 64 : 0));
   if (!bn) return -1;
   ConvArgs a;
   if (cvl_conv_prepare(d, BM, &a)) return -1;
   a.dst_up = dst_up;
   a.dst_w = dst_w;
-  // too few tiles to fill 256 CUs at one 8-wave workgroup each (tests lower the bar)
-  if ((long)a.m_tiles * (a.Npad / bn) < cvl_env_int("CVL_CONV_L_MIN_TILES", 384)) return -1;
+  // too few tiles to fill 256 CUs at one 8-wave workgroup each (tests lower the bar); a launch
+  // with too few 256-wide tiles drops to the 128-wide tile first
+  const long min_tiles = cvl_env_int("CVL_CONV_L_MIN_TILES", 384);
+  int use_bn = bn;
+  if (use_bn == 256 && (long)a.m_tiles * (a.Npad / 256) < cvl_env_int("CVL_CONV_L256_MIN_TILES", 512)) use_bn = 128;
+  if ((long)a.m_tiles * (a.Npad / use_bn) < min_tiles) return -1;
   if (bn_stats)
     for (int i = 0; i < a.nseg; ++i)
       if ((a.seg[i].Hr * a.seg[i].Wr) % 4) return -1;
   a.src = reinterpret_cast<const cvl_bf16*>(src);
   a.dst = dst;
   a.stats = bn_stats;
-  dim3 grid(a.m_tiles * (a.Npad / bn));
+  dim3 grid(a.m_tiles * (a.Npad / use_bn));
   const bool dg = d->mode == CVL_CONV_DGRAD;
-  if (bn == 128) {
-    if (dg) hipLaunchKernelGGL((conv_igemm_l_kernel<128, true>), grid, dim3(NT), 0, s, a);
-    else hipLaunchKernelGGL((conv_igemm_l_kernel<128, false>), grid, dim3(NT), 0, s, a);
-  } else {
-    if (dg) hipLaunchKernelGGL((conv_igemm_l_kernel<64, true>), grid, dim3(NT), 0, s, a);
-    else hipLaunchKernelGGL((conv_igemm_l_kernel<64, false>), grid, dim3(NT), 0, s, a);
-  }
+  const bool prio = !cvl_env_flag("CVL_CONV_NO_PRIO");
+#define CVL_L_LAUNCH(BN_, WGM_, NST_)                                                                          \
+  do {                                                                                                         \
+    if (dg) {                                                                                                  \
+      if (prio) hipLaunchKernelGGL((conv_igemm_l_kernel<BN_, WGM_, NST_, true, true>), grid, dim3(NT), 0, s, a);   \
+      else hipLaunchKernelGGL((conv_igemm_l_kernel<BN_, WGM_, NST_, true, false>), grid, dim3(NT), 0, s, a);       \
+    } else {                                                                                                   \
+      if (prio) hipLaunchKernelGGL((conv_igemm_l_kernel<BN_, WGM_, NST_, false, true>), grid, dim3(NT), 0, s, a);  \
+      else hipLaunchKernelGGL((conv_igemm_l_kernel<BN_, WGM_, NST_, false, false>), grid, dim3(NT), 0, s, a);      \
+    }                                                                                                          \
+  } while (0)
+  if (use_bn == 256) CVL_L_LAUNCH(256, 2, 2);
+  else if (use_bn == 128) CVL_L_LAUNCH(128, 4, 3);
+  else CVL_L_LAUNCH(64, 4, 3);
+#undef CVL_L_LAUNCH
   return cvl_launch_status();
 }
