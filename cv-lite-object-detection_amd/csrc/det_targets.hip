@@ -431,6 +431,68 @@ __global__ void __launch_bounds__(NT) centernet_loss_kernel(CnLossArgs a) {
   }
 }
 
+// ------------------------------------------------------------------------------------------------
+// CenterNet detection decode (tf_centernet_hourglass.py:576-650, the part before `nms`): corners
+// from prediction_to_corners (:355-377: fp32 grid +- ltrb, then stride * in float64), sigmoid class
+// probabilities (fp32; evaluated in float64 and rounded), per-cell max / first argmax, threshold,
+// the image-ratio scaling, w/h clamps and x/y floors of :630-650, int(prob * 100).  Rows are
+// emitted in np.nonzero (row-major cell) order: one 1024-thread workgroup scans the cells in
+// chunks with a ballot prefix sum.
+// ------------------------------------------------------------------------------------------------
+__global__ void __launch_bounds__(1024) centernet_decode_kernel(const float* pred, int ld, int H, int W, int C,
+                                                                double stride, float thresh, double w_ratio,
+                                                                double h_ratio, double img_w, double img_h,
+                                                                double* rows, int32_t* count) {
+  __shared__ int wtot[16];
+  __shared__ int base_s;
+  if (threadIdx.x == 0) base_s = 0;
+  __syncthreads();
+  const int n = H * W;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  for (int c0 = 0; c0 < n; c0 += 1024) {
+    const int cell = c0 + threadIdx.x;
+    bool keep = false;
+    float pmax = 0.f;
+    int lab = 0;
+    if (cell < n) {
+      const float* p = pred + (size_t)cell * ld;
+      for (int c = 0; c < C; ++c) {
+        const float pr = (float)(1.0 / (1.0 + exp(-(double)p[4 + c])));
+        if (c == 0 || pr > pmax) { pmax = pr; lab = c; }
+      }
+      keep = pmax >= thresh;
+    }
+    const unsigned long long m = __ballot(keep);
+    const int pre = __popcll(m & ((1ull << lane) - 1ull));
+    if (lane == 0) wtot[wv] = __popcll(m);
+    __syncthreads();
+    int off = 0, tot = 0;
+    for (int k = 0; k < 16; ++k) { off += k < wv ? wtot[k] : 0; tot += wtot[k]; }
+    if (keep) {
+      const float* p = pred + (size_t)cell * ld;
+      const int y = cell / W, x = cell - (cell / W) * W;
+      const float gy = (float)y + 0.5f, gx = (float)x + 0.5f;
+      const double b0 = stride * (double)(gy - p[0]), b1 = stride * (double)(gx - p[2]);
+      const double b2 = stride * (double)(gy + p[1]), b3 = stride * (double)(gx + p[3]);
+      double x_low = h_ratio * b1, y_low = w_ratio * b0;
+      const double x_upp = h_ratio * b3, y_upp = w_ratio * b2;
+      double bw = x_upp - x_low, bh = y_upp - y_low;
+      if (bw > img_w) bw = img_w;
+      if (bh > img_h) bh = img_h;
+      if (x_low < 0.0) x_low = 0.0;
+      if (y_low < 0.0) y_low = 0.0;
+      double* r = rows + (size_t)(base_s + off + pre) * 6;
+      r[0] = x_low; r[1] = y_low; r[2] = bw; r[3] = bh;
+      r[4] = (double)(int)(pmax * 100.0f);
+      r[5] = (double)lab;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) base_s += tot;
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) *count = base_s;
+}
+
 // RetinaNet.train_loss (retinanet_module.py:403-426) over every (level, anchor) at once, fwd + bwd.
 // Predictions come straight from the grouped head convs: row (level offset + cell) of [B][P][ld],
 // class channels a*C + c, box channels a*4 + j.  Targets are cvl_retina_assign's [B][A*P][4+C] in
@@ -731,5 +793,14 @@ extern "C" int cvl_centernet_loss(const float* pred, int ld_pred, const float* t
   a.cls_scale = cls_scale; a.reg_scale = reg_scale;
   hipLaunchKernelGGL(centernet_loss_kernel, dim3(a.tiles, B), dim3(NT), 0, S_, a);
   hipLaunchKernelGGL(det_loss_finalize, dim3(B), dim3(64), 0, S_, (const double*)workspace, losses, a.tiles);
+  return cvl_launch_status();
+}
+
+extern "C" int cvl_centernet_decode(const float* pred, int ld, int H, int W, int num_classes, double stride,
+                                    float thresh, double w_ratio, double h_ratio, double img_width,
+                                    double img_height, double* rows, int32_t* count, cvl_stream_t stream) {
+  CVL_CHECK_ARG(pred && rows && count && H > 0 && W > 0 && num_classes > 0 && ld >= 4 + num_classes);
+  hipLaunchKernelGGL(centernet_decode_kernel, dim3(1), dim3(1024), 0, S_, pred, ld, H, W, num_classes, stride, thresh,
+                     w_ratio, h_ratio, img_width, img_height, rows, count);
   return cvl_launch_status();
 }

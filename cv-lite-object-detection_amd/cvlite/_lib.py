@@ -73,6 +73,8 @@ SIGNATURES = {
     "cvl_centernet_loss": (c_int, [P, c_int, P, c_int, c_int, c_int, c_float, c_float, P, P, c_int, P, P]),
     "cvl_adam_clip_update": (c_int, [P, P, P, P, ctypes.c_int64, P, P, c_float, c_float, c_float, c_float, c_float,
                                      P, P]),
+    "cvl_centernet_decode": (c_int, [P, c_int, c_int, c_int, c_int, ctypes.c_double, c_float, ctypes.c_double,
+                                     ctypes.c_double, ctypes.c_double, ctypes.c_double, P, P, P]),
     "cvl_nms_workspace_size": (c_size_t, [c_int, c_int]),
     "cvl_nms": (c_int, [P, c_int, P, c_int, ctypes.c_double, P, P, P, P]),
 }

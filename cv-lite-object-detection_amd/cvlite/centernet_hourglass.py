@@ -88,3 +88,26 @@ def train_step(voc_model, sub_batch_sz, images, bboxes, optimizer, cls_lambda=2.
     tr.load_targets(images, bboxes)
     losses = tr.step().double().sum(0).cpu().numpy()
     return float(losses[0]) / B, float(losses[1]) / B
+
+
+def decode_detections(pred, thresh=0.50, downsample=8, iou_thresh=0.213, img_rows=448, img_cols=448,
+                      img_shape=None):
+    """The numeric part of obj_detect_results (tf_centernet_hourglass.py:576-656) for one image:
+    pred [H,W,4+C] (the model output, device or host) -> (bboxes_raw [n,6] = (x, y, w, h, score%,
+    cls), bboxes_nms [m,6] corner rows) via cvl_centernet_decode + cvl_nms.  img_shape = the
+    source image's (shape[0], shape[1]) (defaults to (img_rows, img_cols)).  Plotting is outside
+    this path."""
+    _lib.require_cuda()
+    p = torch.as_tensor(pred, dtype=torch.float32).cuda().contiguous()
+    H, W, ld = int(p.shape[0]), int(p.shape[1]), int(p.shape[2])
+    img_w, img_h = (img_rows, img_cols) if img_shape is None else (img_shape[0], img_shape[1])
+    rows = torch.empty((H * W, 6), dtype=torch.float64, device="cuda")
+    cnt = torch.zeros(1, dtype=torch.int32, device="cuda")
+    _lib.call("cvl_centernet_decode", _lib.ptr(p), ld, H, W, ld - 4, float(downsample), float(thresh),
+              float(img_w / img_rows), float(img_h / img_cols), float(img_w), float(img_h), _lib.ptr(rows),
+              _lib.ptr(cnt), _lib.stream())
+    n = int(cnt.item())
+    raw = rows[:n].cpu().numpy()
+    if n == 0:
+        return raw, np.zeros((0, 6))
+    return raw, np.array(nms(raw.copy(), iou_thresh), np.float64).reshape(-1, 6)

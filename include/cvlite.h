@@ -326,6 +326,16 @@ int cvl_centernet_loss(const float* pred, int ld_pred, const float* targets, int
                        float cls_scale, float reg_scale, float* losses, void* d_pred, int ld_d, void* workspace,
                        cvl_stream_t stream);
 
+/* obj_detect_results decode (tf_centernet_hourglass.py:576-650, before `nms`): pred [H][W][ld] fp32
+ * (one image of the model output: ltrb 0..3, class logits 4..4+C) -> rows [n][6] float64 =
+ * (x_low, y_low, w, h, int(100 * max prob), argmax class) for every cell whose max sigmoid
+ * probability >= thresh, in np.nonzero (row-major) order; *count = n (<= H*W).  stride = the
+ * reference's `downsample`; w_ratio = img_width / img_rows, h_ratio = img_height / img_cols with
+ * img_width/img_height the source image's shape[0]/shape[1] (as the reference names them). */
+int cvl_centernet_decode(const float* pred, int ld, int H, int W, int num_classes, double stride, float thresh,
+                         double w_ratio, double h_ratio, double img_width, double img_height, double* rows,
+                         int32_t* count, cvl_stream_t stream);
+
 /* train_step update (:555-563) with tf.keras.optimizers.Adam (train_hourglass_voc.py:330):
  * g <- clip_by_global_norm(g * inv_bs, clip); t = *iterations + 1;
  * m += (g - m)(1 - b1); v += (g^2 - v)(1 - b2); w -= lr sqrt(1 - b2^t) / (1 - b1^t) * m / (sqrt(v) + eps);

@@ -173,3 +173,55 @@ def nms(bboxes, iou_threshold):
             keep = ~(iou > iou_threshold)
             cb = cb[keep & (cb[:, 4] > 0)]
     return np.array(best, np.float64).reshape(-1, 6)
+
+
+def prediction_to_corners(xy_pred, stride):
+    """tf_centernet_hourglass.py:355-377: fp32 grid (cell + 0.5) -+ ltrb, stored float64, * stride."""
+    xy = np.asarray(xy_pred, np.float32)
+    H, W = xy.shape[:2]
+    ch = np.arange(H, dtype=np.float32) + np.float32(0.5)
+    cw = np.arange(W, dtype=np.float32) + np.float32(0.5)
+    gx, gy = np.meshgrid(cw, ch)
+    out = np.zeros((H, W, 4))
+    out[:, :, 0] = gy - xy[..., 0]
+    out[:, :, 2] = gy + xy[..., 1]
+    out[:, :, 1] = gx - xy[..., 2]
+    out[:, :, 3] = gx + xy[..., 3]
+    return stride * out
+
+
+def sigmoid32(x):
+    """fp32 sigmoid (tf.nn.sigmoid): evaluated in float64, rounded to fp32 (TF's own fp32 kernel
+    is an implementation detail not available here: parity unpinned at the ulp level)."""
+    return (1.0 / (1.0 + np.exp(-np.asarray(x, np.float64)))).astype(np.float32)
+
+
+def decode_cells(pred, thresh=0.5, downsample=8, img_rows=448, img_cols=448, img_width=448, img_height=448):
+    """The per-cell part of obj_detect_results (tf_centernet_hourglass.py:576-650): rows
+    (x_low, y_low, w, h, int(100 p), label) of the cells with max class probability >= thresh, in
+    np.nonzero order -> the input of `nms`."""
+    pred = np.asarray(pred, np.float32)
+    reg = prediction_to_corners(pred[:, :, :4], downsample)
+    probs = sigmoid32(pred[:, :, 4:])
+    pmax = probs.max(axis=2)
+    lab = probs.argmax(axis=2)
+    w_ratio = img_width / img_rows
+    h_ratio = img_height / img_cols
+    rows = []
+    xs, ys = np.nonzero(np.where(pmax >= thresh, 1, 0))
+    for xc, yc in zip(xs, ys):
+        b = reg[xc, yc, :]
+        p = int(pmax[xc, yc] * 100)
+        x_low, y_low = h_ratio * b[1], w_ratio * b[0]
+        x_upp, y_upp = h_ratio * b[3], w_ratio * b[2]
+        bw, bh = x_upp - x_low, y_upp - y_low
+        if bw > img_width:
+            bw = img_width
+        if bh > img_height:
+            bh = img_height
+        if x_low < 0:
+            x_low = 0
+        if y_low < 0:
+            y_low = 0
+        rows.append(np.array([x_low, y_low, bw, bh, p, lab[xc, yc]], np.float64))
+    return np.array(rows, np.float64).reshape(-1, 6)

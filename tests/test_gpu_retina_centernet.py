@@ -114,3 +114,25 @@ def test_nms_matches_reference(golden):
     for i in range(8):
         got = np.array(hg.nms(d["nms_%d_in" % i], 0.213), np.float64).reshape(-1, 6)
         np.testing.assert_array_equal(got, d["nms_%d_out" % i])
+
+
+def test_centernet_decode_matches_restatement():
+    """cvl_centernet_decode + cvl_nms vs the numpy restatement of obj_detect_results' decode
+    (oracle/centernet_ref.py) on random heads: bit-exact rows, including boxes clamped at the image
+    border / size limits and an empty result."""
+    from cvlite import centernet_hourglass as hg
+    rng = np.random.default_rng(11)
+    for (H, C, thr, ds, shape) in [(128, 20, 0.5, 4, (500, 375)), (64, 3, 0.3, 8, None), (32, 80, 0.99, 4, None)]:
+        pred = np.zeros((H, H, 4 + C), np.float32)
+        pred[..., :4] = rng.uniform(-2, 40, size=(H, H, 4)).astype(np.float32)
+        pred[..., 4:] = rng.normal(-4.0, 2.5, size=(H, H, C)).astype(np.float32)
+        raw, kept = hg.decode_detections(pred, thresh=thr, downsample=ds, img_rows=448, img_cols=448,
+                                         img_shape=shape)
+        sh = shape or (448, 448)
+        ref = centernet_ref.decode_cells(pred, thr, ds, 448, 448, sh[0], sh[1])
+        np.testing.assert_array_equal(raw, ref)
+        if len(ref):
+            np.testing.assert_array_equal(kept, centernet_ref.nms(ref.copy(), 0.213))
+    pred = np.full((16, 16, 24), -9.0, np.float32)
+    raw, kept = hg.decode_detections(pred)
+    assert raw.shape == (0, 6) and kept.shape == (0, 6)
