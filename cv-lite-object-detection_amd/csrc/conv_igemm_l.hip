@@ -48,7 +48,7 @@ __global__ void __launch_bounds__(NT) conv_igemm_l_kernel(ConvArgs a) {
   constexpr int BP = BN * BK / (NT * 8);        // B pieces per thread: 2 (BN 128) or 1 (BN 64)
   constexpr int GPW = AP + BP;                   // LDS-DMA instructions per wave per K step
   constexpr int STAGE = (BM + BN) * BK;          // bf16 elements per ring slot
-  constexpr int LDS_C = BM * (BN + 8);
+  constexpr int LDS_C = BM * (BN + 8) + (WGM > 2 ? WGM * BN * 2 * 2 : 0);   // C image + per-wave stats
   constexpr int LDS_EL = NST * STAGE > LDS_C ? NST * STAGE : LDS_C;
   __shared__ __attribute__((aligned(16))) cvl_bf16 lds[LDS_EL];
 
@@ -206,7 +206,11 @@ __global__ void __launch_bounds__(NT) conv_igemm_l_kernel(ConvArgs a) {
         acc[i][j][e] = bf16_to_f32(f32_to_bf16(v));
       }
 
-  if (a.stats && HWr % BM == 0) {   // one image per tile: reduce the wave's rows first
+  // one image per tile: each wave reduces its rows (registers + lane shuffles), the WGM waves of a
+  // column are combined through LDS below, then ONE atomic pair per (tile, column)
+  // (the 2-wave-tall 256-wide tile keeps the per-wave atomics: it runs at the register limit)
+  const bool tile_stats = a.stats && HWr % BM == 0;
+  if (WGM == 2 && tile_stats) {
     const int img = mloc0 / HWr;
 #pragma unroll
     for (int j = 0; j < TN; ++j) {
@@ -224,7 +228,7 @@ __global__ void __launch_bounds__(NT) conv_igemm_l_kernel(ConvArgs a) {
         atomicAdd(st + 1, (double)s2);
       }
     }
-  } else if (a.stats) {
+  } else if (a.stats && !tile_stats) {
     // the 4 rows of an accumulator quad share one image (host: H*W % 4 == 0)
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
@@ -259,7 +263,33 @@ __global__ void __launch_bounds__(NT) conv_igemm_l_kernel(ConvArgs a) {
         const int c = wn * WN + j * 16 + lr;
         Cs[r * CP + c] = f32_to_bf16(acc[i][j][e]);
       }
+  float* sred = reinterpret_cast<float*>(lds + BM * CP);     // [WGM][BN][2]
+  if (WGM > 2 && tile_stats) {
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) { const float v = acc[i][j][e]; s1 += v; s2 += v * v; }
+      s1 += __shfl_xor(s1, 16, 64); s1 += __shfl_xor(s1, 32, 64);
+      s2 += __shfl_xor(s2, 16, 64); s2 += __shfl_xor(s2, 32, 64);
+      if (lg == 0) {
+        const int c = wn * WN + j * 16 + lr;
+        sred[(wm * BN + c) * 2] = s1;
+        sred[(wm * BN + c) * 2 + 1] = s2;
+      }
+    }
+  }
   __syncthreads();
+  if (WGM > 2 && tile_stats && tid < BN && n0 + tid < a.n_store) {
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int w = 0; w < WGM; ++w) { s1 += sred[(w * BN + tid) * 2]; s2 += sred[(w * BN + tid) * 2 + 1]; }
+    double* st = a.stats + ((long)(mloc0 / HWr) * a.n_store + n0 + tid) * 2;
+    atomicAdd(st, (double)s1);
+    atomicAdd(st + 1, (double)s2);
+  }
   constexpr int CCH = BN / 8;
   cvl_bf16* dst = reinterpret_cast<cvl_bf16*>(a.dst);
   for (int idx = tid; idx < BM * CCH; idx += NT) {

@@ -220,10 +220,33 @@ __global__ void __launch_bounds__(NT) conv_wgrad_kernel(WgArgs g) {
     }
 }
 
-__global__ void wgrad_reduce_kernel(const float* slab, float* dw, long n, int splits, float beta) {
-  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
-    float s = slab[i];
-    for (int k = 1; k < splits; ++k) s += slab[(long)k * n + i];
+// dw[i] = sum_k slab[k][i] (+ beta*dw[i]).  A block owns 32 consecutive elements (128-byte rows)
+// and 8 split lanes; lane l sums splits l, l+8, ... with 4 loads in flight, then the 8 lane sums
+// are added in a fixed order (deterministic; split counts here reach several hundred).
+__global__ void __launch_bounds__(256) wgrad_reduce_kernel(const float* __restrict__ slab, float* __restrict__ dw,
+                                                           long n, int splits, float beta) {
+  __shared__ float red[8][33];
+  const int col = threadIdx.x & 31, sl = threadIdx.x >> 5;
+  const long i = (long)blockIdx.x * 32 + col;
+  float acc = 0.f;
+  if (i < n) {
+    int k = sl;
+    float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+    for (; k + 24 < splits; k += 32) {
+      a0 += slab[(long)k * n + i];
+      a1 += slab[(long)(k + 8) * n + i];
+      a2 += slab[(long)(k + 16) * n + i];
+      a3 += slab[(long)(k + 24) * n + i];
+    }
+    for (; k < splits; k += 8) a0 += slab[(long)k * n + i];
+    acc = (a0 + a1) + (a2 + a3);
+  }
+  red[sl][col] = acc;
+  __syncthreads();
+  if (sl == 0 && i < n) {
+    float s = red[0][col];
+#pragma unroll
+    for (int k = 1; k < 8; ++k) s += red[k][col];
     if (beta != 0.f) s += beta * dw[i];
     dw[i] = s;
   }
@@ -308,8 +331,7 @@ extern "C" int cvl_conv_wgrad(const cvl_conv_desc* d, const void* x, const void*
   st = cvl_launch_status();
   if (st || g.direct) return st;
   const long n = (long)g.a.K * g.Cout;
-  int blocks = (int)((n + 255) / 256);
-  blocks = blocks > 4096 ? 4096 : blocks;
+  const int blocks = (int)((n + 31) / 32);
   hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(blocks), dim3(256), 0, s,
                      (const float*)g.out, dw, n, nsplit, beta);
   return cvl_launch_status();

@@ -14,9 +14,9 @@
 // each 256-byte half row (chunk ^= (row & 3) | ((row >> 3) & 1) << 2): the 8 rows one transposed
 // read touches per 32-lane group then fall on 8 distinct bank ranges.  LDS-DMA writes
 // lane-linearly, so the swizzle is applied to each lane's SOURCE address.
-// Row geometry ({dY row, source pixel of tap (0,0), iy0, ix0} per GEMM row) is precomputed in HBM
-// by wgrad_rowtab_kernel and DMA'd NST-2 steps ahead into a small LDS ring, so a lane's DMA
-// addresses cost one LDS read per row and a few integer ops.  The reduction range is split over
+// Row geometry ({dY row, source pixel of tap (0,0), iy0, ix0} per GEMM row) is computed by one wave
+// (in turn) NST-2 steps ahead (one row per lane) into a small LDS ring, so a lane's DMA addresses cost one
+// LDS read per row and a few integer ops.  The reduction range is split over
 // workgroups to fill the GPU; partial tiles go to fp32 slabs reduced in a fixed order
 // (deterministic).
 #include "conv_common.h"
@@ -26,7 +26,7 @@ namespace {
 constexpr int NT = 512;
 constexpr int BKK = 256;
 constexpr int SEGM = 128;          // segment padding granule of the M space (cvl_conv_prepare)
-constexpr int TAB = 64;            // row-table entries per LDS slot (one 1 KiB DMA)
+constexpr int TAB = 64;            // row-table entries per LDS slot (one per wave-0 lane)
 
 struct WgLArgs {
   ConvArgs a;
@@ -35,7 +35,6 @@ struct WgLArgs {
   int ld_dy, dy_coff, Cout, co_tiles, chunk, nsplit;
   float beta;
   int direct;
-  const int4* rowtab;   // [m_total + TAB] row geometry (wgrad_rowtab_kernel)
 };
 
 __device__ __attribute__((aligned(16))) cvl_bf16 g_zero_w[8];
@@ -63,6 +62,26 @@ __device__ __forceinline__ int seg_of(const ConvArgs& a, int m) {
   for (int i = 1; i < kMaxSeg; ++i)
     if (i < a.nseg && m >= a.seg[i].m_start) sg = i;
   return sg;
+}
+
+// {dY row, source pixel of tap (0,0), iy0, ix0} of GEMM row m ({-1, ...} past the rows)
+__device__ __forceinline__ int4 row_entry(const ConvArgs& a, int m) {
+  int4 e = int4{-1, 0, -(1 << 20), -(1 << 20)};
+  if (m < a.m_total) {
+    const ConvSeg& S = a.seg[seg_of(a, m)];
+    const int ml = m - S.m_start;
+    if (ml < S.rows) {
+      const int HW = S.Hr * S.Wr;
+      const int img = ml / HW, q = ml - img * HW;
+      const int y = q / S.Wr, x = q - (q / S.Wr) * S.Wr;
+      const int iy0 = y * a.stride - a.pad_t, ix0 = x * a.stride - a.pad_l;
+      e.x = (int)(S.dst_base + (long)img * S.dst_img) + y * S.Wr + x;
+      e.y = (int)(S.src_base + (long)img * S.src_img) + iy0 * S.Ws + ix0;
+      e.z = iy0;
+      e.w = ix0;
+    }
+  }
+  return e;
 }
 
 template <int BCO>
@@ -125,8 +144,9 @@ __global__ void __launch_bounds__(NT) conv_wgrad_l_kernel(WgLArgs g) {
 
   const int nsteps = (m_hi - m_lo + BR - 1) / BR;
   int4* rowtab = reinterpret_cast<int4*>(lds + NST * STAGE);
-  auto fetch_tab = [&](int t) {     // entries of step t (64 from its first row; the table has slack)
-    if (wave == 0 && t < nsteps) glds16(g.rowtab + (m_lo + t * BR) + lane, rowtab + (t % TS) * TAB);
+  auto fetch_tab = [&](int t) {     // entries of step t (64 from its first row; BR <= 64), written
+    // by the waves in turn (wave t % 8) so the index arithmetic costs each wave 1/8 of the steps
+    if (wave == (t & 7) && t < nsteps) rowtab[(t % TS) * TAB + lane] = row_entry(a, m_lo + t * BR + lane);
   };
   auto issue = [&](int t, int slot) {   // the DMA of step t into ring slot `slot`
     const ConvSeg& S = a.seg[seg_of(a, m_lo + t * BR)];
@@ -167,9 +187,9 @@ __global__ void __launch_bounds__(NT) conv_wgrad_l_kernel(WgLArgs g) {
 
   // Prologue: tables 0..NST-2, then data steps 0..NST-2, then tables NST-1..2NST-4 (the tables the
   // first NST-2 iterations consume), all retired before the loop.
-  // Loop invariant (iteration st, data step tn = st+NST-1 issued): wave 0 fetches the table of
-  // step tn+NST-2 BEFORE issuing D(tn); at the top of the iteration that consumes it, at least
-  // (NST-2)*GPW of wave 0's DMAs were issued after it, so the counted wait below retires it.
+  // Loop invariant (iteration st, data step tn = st+NST-1 issued): wave (tn+NST-2) % 8 writes the
+  // table of step tn+NST-2 (ds_write) BEFORE issuing D(tn); it is consumed NST-2 >= 1 iterations later,
+  // after a barrier whose lgkmcnt(0) retired the write.
   // Table slot reuse: T(t) goes to slot t % TS, whose previous occupant T(t-TS) was consumed by
   // issue(t-TS) one iteration earlier, before this iteration's barrier.
 #pragma unroll
@@ -254,27 +274,6 @@ __global__ void __launch_bounds__(NT) conv_wgrad_l_kernel(WgLArgs g) {
     }
 }
 
-__global__ void wgrad_rowtab_kernel(ConvArgs a, int4* tab) {
-  const int m = blockIdx.x * blockDim.x + threadIdx.x;
-  if (m >= a.m_total + TAB) return;
-  int4 e = int4{-1, 0, -(1 << 20), -(1 << 20)};
-  if (m < a.m_total) {
-    const ConvSeg& S = a.seg[seg_of(a, m)];
-    const int ml = m - S.m_start;
-    if (ml < S.rows) {
-      const int HW = S.Hr * S.Wr;
-      const int img = ml / HW, q = ml - img * HW;
-      const int y = q / S.Wr, x = q - (q / S.Wr) * S.Wr;
-      const int iy0 = y * a.stride - a.pad_t, ix0 = x * a.stride - a.pad_l;
-      e.x = (int)(S.dst_base + (long)img * S.dst_img) + y * S.Wr + x;
-      e.y = (int)(S.src_base + (long)img * S.src_img) + iy0 * S.Ws + ix0;
-      e.z = iy0;
-      e.w = ix0;
-    }
-  }
-  tab[m] = e;
-}
-
 __global__ void wgrad_l_reduce_kernel(const float* slab, float* dw, long n4, int splits, float beta) {
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n4; i += (long)gridDim.x * blockDim.x) {
     f32x4 s = reinterpret_cast<const f32x4*>(slab)[i];
@@ -330,7 +329,7 @@ inline bool wl_plan(const cvl_conv_desc* d, ConvArgs* a, WlPlan* p) {
   p->chunk = ((chunk + SEGM - 1) / SEGM) * SEGM;
   p->nsplit = (a->m_total + p->chunk - 1) / p->chunk;
   p->slab = p->nsplit > 1 ? (size_t)p->nsplit * a->K * d->n_store * sizeof(float) : 0;
-  p->total = p->slab + 256 + (size_t)(a->m_total + TAB) * 16;
+  p->total = p->slab > 0 ? p->slab : 16;
   return true;
 }
 
@@ -362,9 +361,6 @@ int cvl_conv_wgrad_l(const cvl_conv_desc* d, const void* x, const void* dy, floa
   g.nsplit = p.nsplit;
   g.direct = p.nsplit == 1;
   g.out = g.direct ? dw : reinterpret_cast<float*>(workspace);
-  int4* tab = reinterpret_cast<int4*>((reinterpret_cast<uintptr_t>(workspace) + p.slab + 255) & ~(uintptr_t)255);
-  g.rowtab = tab;
-  hipLaunchKernelGGL(wgrad_rowtab_kernel, dim3((g.a.m_total + TAB + 255) / 256), dim3(256), 0, s, g.a, tab);
   if (p.bco == 256) hipLaunchKernelGGL(conv_wgrad_l_kernel<256>, dim3(p.tiles * p.nsplit), dim3(NT), 0, s, g);
   else hipLaunchKernelGGL(conv_wgrad_l_kernel<128>, dim3(p.tiles * p.nsplit), dim3(NT), 0, s, g);
   int st = cvl_launch_status();

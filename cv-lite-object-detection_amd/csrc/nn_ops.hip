@@ -126,42 +126,174 @@ __global__ void im2col_kernel(const float* x, cvl_bf16* out, int B, int H, int W
   }
 }
 
+// the same map, one 16-byte run of 8 k values per thread (Kp % 8 == 0): 32-bit index math, the
+// writes of neighbouring threads are contiguous, the fp32 taps they read overlap in L2
+__global__ void __launch_bounds__(NT) im2col8_kernel(const float* __restrict__ x, cvl_bf16* __restrict__ out,
+                                                     int n8, int H, int W, int C, int KW, int KK, int stride,
+                                                     int pad_t, int pad_l, int Ho, int Wo, int Kp8) {
+  const int i = blockIdx.x * NT + threadIdx.x;
+  if (i >= n8) return;
+  const int row = i / Kp8, j = i - row * Kp8;
+  const int HWo = Ho * Wo;
+  const int b = row / HWo, q = row - b * HWo;
+  const int oy = q / Wo, ox = q - oy * Wo;
+  const float* xb = x + (long)b * H * W * C;
+  const int k0 = j * 8;
+  int tap = k0 / C, c = k0 - tap * C;
+  float v[8];
+#pragma unroll
+  for (int u = 0; u < 8; ++u) {
+    float val = 0.f;
+    if (k0 + u < KK) {
+      const int r = tap / KW, s = tap - r * KW;
+      const int iy = oy * stride - pad_t + r, ix = ox * stride - pad_l + s;
+      if ((unsigned)iy < (unsigned)H && (unsigned)ix < (unsigned)W) val = xb[(iy * W + ix) * C + c];
+    }
+    v[u] = val;
+    if (++c == C) { c = 0; ++tap; }
+  }
+  *reinterpret_cast<s16x8*>(out + (long)i * 8) = pack8(v);
+}
+
+// the stem shape (KH, KW <= 7, stride <= 2, C <= 4): a block owns one segment of <= 64 output
+// pixels of one output row; it stages the KH input rows under them in LDS (coalesced fp32 reads,
+// zero padding materialised) and writes the segment's rows as contiguous 16-byte runs.
+constexpr int I2C_PX = 64;
+constexpr int I2C_MAXF = 7 * ((I2C_PX - 1) * 2 + 7) * 4;
+__global__ void __launch_bounds__(NT) im2col_tile_kernel(const float* __restrict__ x, cvl_bf16* __restrict__ out,
+                                                         int H, int W, int C, int KH, int KW, int stride,
+                                                         int pad_t, int pad_l, int Ho, int Wo, int Kp8) {
+  __shared__ float tile[I2C_MAXF];
+  const int nseg = (Wo + I2C_PX - 1) / I2C_PX;
+  const int sg = blockIdx.x % nseg, t2 = blockIdx.x / nseg;
+  const int oy = t2 % Ho, b = t2 / Ho;
+  const int ox0 = sg * I2C_PX;
+  const int npx = min(I2C_PX, Wo - ox0);
+  const int rowf = ((npx - 1) * stride + KW) * C;      // floats per staged input row
+  const int iy0 = oy * stride - pad_t, ix0 = ox0 * stride - pad_l;
+  const float* xb = x + (long)b * H * W * C;
+  for (int i = threadIdx.x; i < KH * rowf; i += NT) {
+    const int r = i / rowf, f = i - r * rowf;
+    const int iy = iy0 + r, ix = ix0 + f / C;
+    tile[i] = ((unsigned)iy < (unsigned)H && (unsigned)ix < (unsigned)W) ? xb[((long)iy * W + ix0) * C + f] : 0.f;
+  }
+  __syncthreads();
+  const int KK = KH * KW * C;
+  cvl_bf16* ob = out + (((long)b * Ho + oy) * Wo + ox0) * (long)(Kp8 * 8);
+  for (int it = threadIdx.x; it < npx * Kp8; it += NT) {
+    const int px = it / Kp8, j = it - px * Kp8;
+    const int k0 = j * 8;
+    const int tap = k0 / C;
+    int c = k0 - tap * C, r = tap / KW, s = tap - (tap / KW) * KW;
+    float v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      v[u] = k0 + u < KK ? tile[r * rowf + (px * stride + s) * C + c] : 0.f;
+      if (++c == C) {
+        c = 0;
+        if (++s == KW) { s = 0; ++r; }
+      }
+    }
+    *reinterpret_cast<s16x8*>(ob + (long)it * 8) = pack8(v);
+  }
+}
+
 // ---------------------------------------------------------------------------------------------
 // BatchNorm (per-image statistics over H*W, Keras fused-BN semantics)
 // ---------------------------------------------------------------------------------------------
+// per-image moments of one channel from its float64 (sum, sumsq); shared by the finalize kernels
+__device__ __forceinline__ void bn_moments(double s1, double s2, int HW, float eps, float* mean, float* rstd,
+                                           double* var_out) {
+  const double m = s1 / HW;
+  double var = s2 / HW - m * m;
+  var = var > 0.0 ? var : 0.0;
+  *mean = (float)m;
+  *rstd = (float)(1.0 / sqrt(var + (double)eps));
+  *var_out = var;
+}
+
+// running-stat EMA of one channel over the images in order (TF fused BN: unbiased variance)
+__device__ __forceinline__ void bn_running(const double* stats, int B, int C, int c, int HW, float eps,
+                                           float momentum, float* run_mean, float* run_var) {
+  float rm = run_mean[c], rv = run_var[c];
+  for (int b0 = 0; b0 < B; b0 += 8) {       // 8 images' loads in flight, then the in-order EMA
+    double s1[8], s2[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const long i = ((long)min(b0 + u, B - 1) * C + c) * 2;
+      s1[u] = stats[i];
+      s2[u] = stats[i + 1];
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      if (b0 + u >= B) break;
+      float mean, rstd;
+      double var;
+      bn_moments(s1[u], s2[u], HW, eps, &mean, &rstd, &var);
+      const double uvar = HW > 1 ? var * HW / (HW - 1.0) : var;
+      rm = rm * momentum + mean * (1.f - momentum);
+      rv = rv * momentum + (float)uvar * (1.f - momentum);
+    }
+  }
+  run_mean[c] = rm;
+  run_var[c] = rv;
+}
+
 // stats[b][c] = (sum, sumsq) -> mr[b][c] = (mean, rstd); running stats EMA, images in order.
 __global__ void bn_finalize_kernel(const double* stats, float* mr, float* run_mean, float* run_var,
                                    int B, int C, int HW, float eps, float momentum) {
   const int c = blockIdx.x * NT + threadIdx.x;
   if (c >= C) return;
-  float rm = run_mean ? run_mean[c] : 0.f, rv = run_var ? run_var[c] : 0.f;
   for (int b = 0; b < B; ++b) {
-    const double s1 = stats[((long)b * C + c) * 2], s2 = stats[((long)b * C + c) * 2 + 1];
-    const double mean = s1 / HW;
-    double var = s2 / HW - mean * mean;
-    var = var > 0.0 ? var : 0.0;
-    mr[((long)b * C + c) * 2] = (float)mean;
-    mr[((long)b * C + c) * 2 + 1] = (float)(1.0 / sqrt(var + (double)eps));
-    const double uvar = HW > 1 ? var * HW / (HW - 1.0) : var;   // TF fused BN: unbiased for EMA
-    rm = rm * momentum + (float)mean * (1.f - momentum);
-    rv = rv * momentum + (float)uvar * (1.f - momentum);
+    float mean, rstd;
+    double var;
+    bn_moments(stats[((long)b * C + c) * 2], stats[((long)b * C + c) * 2 + 1], HW, eps, &mean, &rstd, &var);
+    mr[((long)b * C + c) * 2] = mean;
+    mr[((long)b * C + c) * 2 + 1] = rstd;
   }
-  if (run_mean) { run_mean[c] = rm; run_var[c] = rv; }
+  if (run_mean) bn_running(stats, B, C, c, HW, eps, momentum, run_mean, run_var);
 }
 
 // y = act(gamma * (z - mean) * rstd + beta [+ residual]).  Grid (row chunk, image); a thread owns
 // 8 channels for the whole chunk (scale/shift loaded once) and streams rows UNR at a time with
 // all 16-byte loads issued before use.
+// FIN: the finalize is fused in -- every block derives (mean, rstd) of its image from the float64
+// stats (same arithmetic as bn_finalize_kernel), chunk-0 blocks store them for the backward and
+// block (0, 0) advances the running statistics.
+struct BnFin {
+  const double* stats;
+  float* mr_out;
+  float* run_mean;
+  float* run_var;
+  float eps, momentum;
+};
+
 constexpr int BNA_UNR = 4;
+constexpr int BN_FIN_MAXC = 2048;
+template <bool FIN>
 __global__ void __launch_bounds__(NT) bn_apply_kernel(const cvl_bf16* __restrict__ z, const float* __restrict__ mr,
                                                       const float* __restrict__ gamma, const float* __restrict__ beta,
                                                       const cvl_bf16* __restrict__ res, cvl_bf16* __restrict__ y,
-                                                      int C, int HW, int relu, int rows_per_blk) {
+                                                      int C, int HW, int relu, int rows_per_blk, BnFin fin) {
   const int b = blockIdx.y;
   const int C8 = C / 8;
   const int tpr = C8 < NT ? C8 : NT;
   const int rpp = NT / tpr;
   const int cg = threadIdx.x % tpr, rsub = threadIdx.x / tpr;
+  __shared__ float2 smr[FIN ? BN_FIN_MAXC : 1];
+  if (FIN) {      // (mean, rstd) of this image, one channel per thread, shared through LDS
+    for (int c = threadIdx.x; c < C; c += NT) {
+      const long bc = (long)b * C + c;
+      float mm, rr;
+      double var;
+      bn_moments(fin.stats[bc * 2], fin.stats[bc * 2 + 1], HW, fin.eps, &mm, &rr, &var);
+      smr[c] = float2{mm, rr};
+      if (blockIdx.x == 0) { fin.mr_out[bc * 2] = mm; fin.mr_out[bc * 2 + 1] = rr; }
+      if (blockIdx.x == 0 && b == 0 && fin.run_mean)
+        bn_running(fin.stats, gridDim.y, C, c, HW, fin.eps, fin.momentum, fin.run_mean, fin.run_var);
+    }
+    __syncthreads();
+  }
   if (rsub >= rpp) return;
   const int r0 = blockIdx.x * rows_per_blk;
   const int r1 = min(r0 + rows_per_blk, HW);
@@ -171,8 +303,13 @@ __global__ void __launch_bounds__(NT) bn_apply_kernel(const cvl_bf16* __restrict
 #pragma unroll
     for (int u = 0; u < 8; ++u) {
       const long bc = (long)b * C + c0 + u;
-      m[u] = mr[bc * 2];
-      rs[u] = mr[bc * 2 + 1];
+      if (FIN) {
+        m[u] = smr[c0 + u].x;
+        rs[u] = smr[c0 + u].y;
+      } else {
+        m[u] = mr[bc * 2];
+        rs[u] = mr[bc * 2 + 1];
+      }
       ga[u] = gamma[c0 + u];
       be[u] = beta[c0 + u];
     }
@@ -223,13 +360,26 @@ inline int bn_rows_per_blk(int B, int HW, int C) {
 // PASS 1: dz = gamma*rstd*(g - mean(g) - xhat*mean(g*xhat)) (+ g_out = g).
 constexpr int BN_UNR = 4;
 
+// parameter gradients folded into pass 1 (block (0, 0), one thread per channel, images in order,
+// float64): dgamma[c] = beta_acc*dgamma + sum_b sum g*xhat ; dbeta[c] = ... + sum_b sum g ;
+// conv_dbias[c] = 0: training-mode BN subtracts the per-image mean of z, so a constant added to z
+// (the preceding conv's bias) cannot change the loss -- sum_rows dz = gamma*rstd*(S_g - S_g -
+// mean(g xhat) * sum xhat) = 0 exactly (TF's fp32 value is rounding noise around this 0)
+struct BnPG {
+  float* dgamma;
+  float* dbeta;
+  float* conv_dbias;
+  float beta_acc;
+  const double* psums;    // per-image sums for the parameter gradients (nullptr: `sums`)
+};
+
 template <int PASS>
 __global__ void __launch_bounds__(NT) bn_bwd_kernel(const cvl_bf16* __restrict__ dy, const cvl_bf16* __restrict__ y,
                                                     const cvl_bf16* __restrict__ z, const float* __restrict__ mr,
                                                     const float* __restrict__ gamma, const double* __restrict__ sums,
                                                     cvl_bf16* __restrict__ dz, cvl_bf16* __restrict__ g_out,
                                                     float* __restrict__ part, int C, int HW, int rows_per_blk,
-                                                    int group, float dz_beta) {
+                                                    int group, float dz_beta, BnPG pg) {
   const int b = blockIdx.y;
   const int C8 = C / 8;
   const int tpr = C8 < NT ? C8 : NT;
@@ -242,6 +392,20 @@ __global__ void __launch_bounds__(NT) bn_bwd_kernel(const cvl_bf16* __restrict__
   const int gsz = min(g0 + group, (int)gridDim.y) - g0;
   const float inv = 1.0f / ((float)HW * (float)gsz);
   __shared__ float red[NT][17];
+  if (PASS == 1 && pg.dgamma && blockIdx.x == 0 && b == 0) {
+    const double* ps = pg.psums ? pg.psums : sums;
+    for (int c = threadIdx.x; c < C; c += NT) {
+      if (pg.conv_dbias) pg.conv_dbias[c] = 0.f;
+      double a1 = 0.0, a2 = 0.0;
+#pragma unroll 8
+      for (int bb = 0; bb < (int)gridDim.y; ++bb) {
+        a1 += ps[((long)bb * C + c) * 2];
+        a2 += ps[((long)bb * C + c) * 2 + 1];
+      }
+      pg.dbeta[c] = (float)a1 + (pg.beta_acc != 0.f ? pg.beta_acc * pg.dbeta[c] : 0.f);
+      pg.dgamma[c] = (float)a2 + (pg.beta_acc != 0.f ? pg.beta_acc * pg.dgamma[c] : 0.f);
+    }
+  }
   for (int cgb = cg; cgb < C8; cgb += tpr) {
     const int c0 = cgb * 8;
     float m[8], rs[8], s1[8], s2[8], k1[8], k2[8], gm[8];
@@ -257,6 +421,7 @@ __global__ void __launch_bounds__(NT) bn_bwd_kernel(const cvl_bf16* __restrict__
         gm[u] = gamma[c0 + u] * rs[u];
       }
     }
+
     if (rsub < rpp) {
       for (int r = r0 + rsub; r < r1; r += rpp * BN_UNR) {
         s16x8 vg[BN_UNR], vz[BN_UNR], vy[BN_UNR];
@@ -365,21 +530,6 @@ __global__ void __launch_bounds__(NT) bn_colsum_kernel(const float* __restrict__
     out[((long)y * C + c) * 2] = t1;
     out[((long)y * C + c) * 2 + 1] = t2;
   }
-}
-
-// dgamma[c] = beta_acc*dgamma + sum_b sum g*xhat ; dbeta[c] = ... + sum_b sum g ;
-// conv_dbias[c] = 0: training-mode BN subtracts the per-image mean of z, so a constant added to z
-// (the preceding conv's bias) cannot change the loss -- sum_rows dz = gamma*rstd*(S_g - S_g -
-// mean(g xhat) * sum xhat) = 0 exactly (TF's fp32 value is rounding noise around this 0)
-__global__ void bn_param_grad_kernel(const double* sums, float* dgamma, float* dbeta, int B, int C,
-                                     float beta_acc, float* conv_dbias) {
-  const int c = blockIdx.x * NT + threadIdx.x;
-  if (c >= C) return;
-  if (conv_dbias) conv_dbias[c] = 0.f;
-  double a1 = 0.0, a2 = 0.0;
-  for (int b = 0; b < B; ++b) { a1 += sums[((long)b * C + c) * 2]; a2 += sums[((long)b * C + c) * 2 + 1]; }
-  dbeta[c] = (float)a1 + (beta_acc != 0.f ? beta_acc * dbeta[c] : 0.f);
-  dgamma[c] = (float)a2 + (beta_acc != 0.f ? beta_acc * dgamma[c] : 0.f);
 }
 
 // row chunking shared by the launcher and the workspace query: 512..2048 blocks over the batch,
@@ -755,6 +905,18 @@ extern "C" int cvl_im2col(const float* x, int B, int H, int W, int C, int KH, in
                           int pad_l, int Ho, int Wo, int Kp, void* out, cvl_stream_t stream) {
   CVL_CHECK_ARG(x && out && B > 0 && Kp >= KH * KW * C);
   const long total = (long)B * Ho * Wo * Kp;
+  if (Kp % 8 == 0 && KH <= 7 && KW <= 7 && stride >= 1 && stride <= 2 && C <= 4 && (long)B * Ho < (1L << 24)) {
+    const int nseg = (Wo + I2C_PX - 1) / I2C_PX;
+    hipLaunchKernelGGL(im2col_tile_kernel, dim3(B * Ho * nseg), dim3(NT), 0, S_, x, (cvl_bf16*)out, H, W, C, KH, KW,
+                       stride, pad_t, pad_l, Ho, Wo, Kp / 8);
+    return cvl_launch_status();
+  }
+  if (Kp % 8 == 0 && total / 8 < (1L << 31) - NT && (long)H * W * C < (1L << 31)) {
+    const int n8 = (int)(total / 8);
+    hipLaunchKernelGGL(im2col8_kernel, dim3((n8 + NT - 1) / NT), dim3(NT), 0, S_, x, (cvl_bf16*)out, n8, H, W, C,
+                       KW, KH * KW * C, stride, pad_t, pad_l, Ho, Wo, Kp / 8);
+    return cvl_launch_status();
+  }
   hipLaunchKernelGGL(im2col_kernel, dim3(grid_for(total)), dim3(NT), 0, S_, x, (cvl_bf16*)out, B, H, W,
                      C, KH, KW, stride, pad_t, pad_l, Ho, Wo, Kp);
   return cvl_launch_status();
@@ -774,8 +936,23 @@ extern "C" int cvl_bn_apply(const void* z, const float* mean_rstd, const float* 
   CVL_CHECK_ARG(z && mean_rstd && gamma && beta && y && C % 8 == 0 && B > 0 && HW > 0);
   CVL_CHECK_ARG(C / 8 <= NT || (C / 8) % NT == 0);
   const int rpb = bn_rows_per_blk(B, HW, C);
-  hipLaunchKernelGGL(bn_apply_kernel, dim3((HW + rpb - 1) / rpb, B), dim3(NT), 0, S_, (const cvl_bf16*)z,
-                     mean_rstd, gamma, beta, (const cvl_bf16*)residual, (cvl_bf16*)y, C, HW, relu, rpb);
+  hipLaunchKernelGGL(bn_apply_kernel<false>, dim3((HW + rpb - 1) / rpb, B), dim3(NT), 0, S_, (const cvl_bf16*)z,
+                     mean_rstd, gamma, beta, (const cvl_bf16*)residual, (cvl_bf16*)y, C, HW, relu, rpb,
+                     BnFin{nullptr, nullptr, nullptr, nullptr, 0.f, 0.f});
+  return cvl_launch_status();
+}
+
+extern "C" int cvl_bn_finalize_apply(const double* stats, float* mean_rstd, float* run_mean, float* run_var,
+                                     const void* z, const float* gamma, const float* beta, const void* residual,
+                                     void* y, int B, int HW, int C, int relu, float eps, float momentum,
+                                     cvl_stream_t stream) {
+  CVL_CHECK_ARG(stats && mean_rstd && z && gamma && beta && y && C % 8 == 0 && B > 0 && HW > 0);
+  CVL_CHECK_ARG(C <= BN_FIN_MAXC && (C / 8 <= NT || (C / 8) % NT == 0));
+  CVL_CHECK_ARG((run_mean == nullptr) == (run_var == nullptr));
+  const int rpb = bn_rows_per_blk(B, HW, C);
+  hipLaunchKernelGGL(bn_apply_kernel<true>, dim3((HW + rpb - 1) / rpb, B), dim3(NT), 0, S_, (const cvl_bf16*)z,
+                     (const float*)nullptr, gamma, beta, (const cvl_bf16*)residual, (cvl_bf16*)y, C, HW, relu, rpb,
+                     BnFin{stats, mean_rstd, run_mean, run_var, eps, momentum});
   return cvl_launch_status();
 }
 
@@ -802,14 +979,12 @@ extern "C" int cvl_bn_backward(const void* dy, const void* y_relu, const void* z
   dim3 g1(nchunk, B);
   hipLaunchKernelGGL(bn_bwd_kernel<0>, g1, dim3(NT), 0, S_, (const cvl_bf16*)dy, (const cvl_bf16*)y_relu,
                      (const cvl_bf16*)z, mean_rstd, gamma, (const double*)nullptr, (cvl_bf16*)nullptr,
-                     (cvl_bf16*)nullptr, part0, C, HW, rpb, 1, 0.f);
+                     (cvl_bf16*)nullptr, part0, C, HW, rpb, 1, 0.f, BnPG{});
   hipLaunchKernelGGL(bn_colsum_kernel, dim3((C + 31) / 32, B), dim3(NT), 0, S_, (const float*)part0, nchunk, C,
                      sums);
   hipLaunchKernelGGL(bn_bwd_kernel<1>, g1, dim3(NT), 0, S_, (const cvl_bf16*)dy, (const cvl_bf16*)y_relu,
                      (const cvl_bf16*)z, mean_rstd, gamma, (const double*)sums, (cvl_bf16*)dz, (cvl_bf16*)g_out,
-                     (float*)nullptr, C, HW, rpb, 1, 0.f);
-  hipLaunchKernelGGL(bn_param_grad_kernel, dim3((C + NT - 1) / NT), dim3(NT), 0, S_, (const double*)sums,
-                     dgamma, dbeta, B, C, beta_acc, conv_dbias);
+                     (float*)nullptr, C, HW, rpb, 1, 0.f, BnPG{dgamma, dbeta, conv_dbias, beta_acc});
   return cvl_launch_status();
 }
 
@@ -943,7 +1118,7 @@ extern "C" int cvl_bn_stats(const void* x, int B, int HW, int C, double* stats, 
   float* part = reinterpret_cast<float*>(workspace);
   hipLaunchKernelGGL(bn_bwd_kernel<2>, dim3(nchunk, B), dim3(NT), 0, S_, (const cvl_bf16*)x,
                      (const cvl_bf16*)nullptr, (const cvl_bf16*)nullptr, (const float*)nullptr, (const float*)nullptr,
-                     (const double*)nullptr, (cvl_bf16*)nullptr, (cvl_bf16*)nullptr, part, C, HW, rpb, 1, 0.f);
+                     (const double*)nullptr, (cvl_bf16*)nullptr, (cvl_bf16*)nullptr, part, C, HW, rpb, 1, 0.f, BnPG{});
   hipLaunchKernelGGL(bn_colsum_kernel, dim3((C + 31) / 32, B), dim3(NT), 0, S_, (const float*)part, nchunk, C,
                      stats);
   return cvl_launch_status();
@@ -981,11 +1156,9 @@ extern "C" int cvl_bn_backward_grouped(const void* dy, const void* y_relu, const
   dim3 g1(nchunk, B);
   hipLaunchKernelGGL(bn_bwd_kernel<0>, g1, dim3(NT), 0, S_, (const cvl_bf16*)dy, (const cvl_bf16*)y_relu,
                      (const cvl_bf16*)z, mean_rstd, gamma, (const double*)nullptr, (cvl_bf16*)nullptr,
-                     (cvl_bf16*)nullptr, part0, C, HW, rpb, group, 0.f);
+                     (cvl_bf16*)nullptr, part0, C, HW, rpb, group, 0.f, BnPG{});
   hipLaunchKernelGGL(bn_colsum_kernel, dim3((C + 31) / 32, B), dim3(NT), 0, S_, (const float*)part0, nchunk, C,
                      sums);
-  hipLaunchKernelGGL(bn_param_grad_kernel, dim3((C + NT - 1) / NT), dim3(NT), 0, S_, (const double*)sums,
-                     dgamma, dbeta, B, C, 0.f, (float*)nullptr);
   const double* use = sums;
   if (group > 1) {
     hipLaunchKernelGGL(bn_group_sum_kernel, dim3((int)(((long)B * C + NT - 1) / NT)), dim3(NT), 0, S_,
@@ -994,6 +1167,6 @@ extern "C" int cvl_bn_backward_grouped(const void* dy, const void* y_relu, const
   }
   hipLaunchKernelGGL(bn_bwd_kernel<1>, g1, dim3(NT), 0, S_, (const cvl_bf16*)dy, (const cvl_bf16*)y_relu,
                      (const cvl_bf16*)z, mean_rstd, gamma, use, (cvl_bf16*)dz, (cvl_bf16*)nullptr,
-                     (float*)nullptr, C, HW, rpb, group, dz_beta);
+                     (float*)nullptr, C, HW, rpb, group, dz_beta, BnPG{dgamma, dbeta, nullptr, 0.f, sums});
   return cvl_launch_status();
 }

@@ -34,6 +34,7 @@ SIGNATURES = {
                            c_int, c_int, P, P]),
     "cvl_bn_finalize": (c_int, [P, P, P, P, c_int, c_int, c_int, c_float, c_float, P]),
     "cvl_bn_apply": (c_int, [P, P, P, P, P, P, c_int, c_int, c_int, c_int, P]),
+    "cvl_bn_finalize_apply": (c_int, [P, P, P, P, P, P, P, P, P, c_int, c_int, c_int, c_int, c_float, c_float, P]),
     "cvl_bn_backward_workspace_size": (c_size_t, [c_int, c_int, c_int]),
     "cvl_bn_backward": (c_int, [P, P, P, P, P, P, c_size_t, P, P, P, P, c_float, P, c_int, c_int, c_int, P]),
     "cvl_maxpool3x3s2": (c_int, [P, P, P, c_int, c_int, c_int, c_int, P]),

@@ -267,10 +267,10 @@ class ConvBN(object):
                                                                          device=x.device)
         z, _, _ = self.conv.fwd(x, B, H, W, stats=stats)
         mr = torch.empty((B, c, 2), dtype=torch.float32, device=x.device)
-        nn.bn_finalize(stats, mr, self.bn.run_mean if train else None, self.bn.run_var if train else None,
-                       B, c, Ho * Wo, self.bn.eps, self.bn.momentum)
         y = torch.empty_like(z)
-        nn.bn_apply(z, mr, self.bn.gamma, self.bn.beta, residual, y, B, Ho * Wo, c, relu)
+        nn.bn_finalize_apply(stats, mr, self.bn.run_mean if train else None, self.bn.run_var if train else None,
+                             z, self.bn.gamma, self.bn.beta, residual, y, B, Ho * Wo, c, relu, self.bn.eps,
+                             self.bn.momentum)
         return y, (x, z, y, mr, B, H, W, Ho, Wo, relu)
 
     def backward(self, dy, saved, dx_out=None, dx_beta=0.0, g_out=None, need_dx=True):

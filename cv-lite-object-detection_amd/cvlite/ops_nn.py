@@ -124,6 +124,12 @@ def bn_apply(z, mean_rstd, gamma, beta, residual, y, B, HW, C, relu):
               B, HW, C, int(bool(relu)), stream())
 
 
+def bn_finalize_apply(stats, mean_rstd, run_mean, run_var, z, gamma, beta, residual, y, B, HW, C, relu, eps,
+                      momentum):
+    _lib.call("cvl_bn_finalize_apply", ptr(stats), ptr(mean_rstd), ptr(run_mean), ptr(run_var), ptr(z), ptr(gamma),
+              ptr(beta), ptr(residual), ptr(y), B, HW, C, int(relu), float(eps), float(momentum), stream())
+
+
 def bn_backward(dy, y_relu, z, mean_rstd, gamma, dz, g_out, dgamma, dbeta, B, HW, C, beta_acc=0.0,
                 conv_dbias=None):
     n = int(_lib.load().cvl_bn_backward_workspace_size(B, HW, C))

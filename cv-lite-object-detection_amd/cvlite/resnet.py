@@ -51,10 +51,10 @@ class Stem(object):
         z = torch.empty((B, Ho, Wo, 64), dtype=BF16, device=x.device)
         nn.conv_igemm(self._desc(B, Ho, Wo), A, z, stats)
         mr = torch.empty((B, 64, 2), dtype=torch.float32, device=x.device)
-        nn.bn_finalize(stats, mr, self.bn.run_mean if train else None, self.bn.run_var if train else None,
-                       B, 64, Ho * Wo, self.bn.eps, self.bn.momentum)
         y = torch.empty_like(z)
-        nn.bn_apply(z, mr, self.bn.gamma, self.bn.beta, None, y, B, Ho * Wo, 64, True)
+        nn.bn_finalize_apply(stats, mr, self.bn.run_mean if train else None, self.bn.run_var if train else None,
+                             z, self.bn.gamma, self.bn.beta, None, y, B, Ho * Wo, 64, True, self.bn.eps,
+                             self.bn.momentum)
         Hp, Wp = (Ho + 2 - 3) // 2 + 1, (Wo + 2 - 3) // 2 + 1
         p = torch.empty((B, Hp, Wp, 64), dtype=BF16, device=x.device)
         arg = torch.empty((B, Hp, Wp, 64), dtype=torch.uint8, device=x.device)

@@ -157,6 +157,12 @@ int cvl_bn_finalize(const double* stats, float* mean_rstd, float* run_mean, floa
                     int C, int HW, float eps, float momentum, cvl_stream_t stream);
 int cvl_bn_apply(const void* z, const float* mean_rstd, const float* gamma, const float* beta,
                  const void* residual, void* y, int B, int HW, int C, int relu, cvl_stream_t stream);
+/* cvl_bn_finalize + cvl_bn_apply in ONE launch (bit-identical results): every block derives the
+ * (mean, rstd) of its image from stats; mean_rstd is still written for the backward and the running
+ * statistics advanced (run_mean/run_var NULL together: inference-style, no EMA). */
+int cvl_bn_finalize_apply(const double* stats, float* mean_rstd, float* run_mean, float* run_var,
+                          const void* z, const float* gamma, const float* beta, const void* residual, void* y,
+                          int B, int HW, int C, int relu, float eps, float momentum, cvl_stream_t stream);
 /* dy: grad of y; y_relu: y when the unit ends in ReLU (mask), else NULL; writes dz (bf16),
  * optionally g_out = masked dy (the residual branch's gradient), dgamma/dbeta (= + beta_acc*old)
  * and, if conv_dbias != NULL, the gradient of the preceding conv's bias, which is exactly 0

@@ -266,6 +266,7 @@ def test_conv_splitk_matches_unsplit(case):
     (4, 32, 32, 256, 256, 3, 2),
     (2, 64, 64, 256, 512, 1, 2),
     (3, 40, 24, 128, 128, 3, 1),      # rows not a multiple of the 128-row granule
+    (16, 128, 128, 64, 256, 1, 1),    # ResNet conv2 1x1, K = 64: hundreds of split-M slabs
 ])
 def test_conv_wgrad_large(case, kern):
     """Weight gradient at sizes that take the 128x256 LDS-DMA kernel (and, with kern == "base",

@@ -54,6 +54,14 @@ def test_bn_forward_backward(B, HW, C, relu, res):
         erv = erv * 0.99 + v[b, 0] * HW / (HW - 1) * 0.01
     torch.testing.assert_close(rm.double().cpu(), erm.detach(), rtol=1e-5, atol=1e-6)
     torch.testing.assert_close(rv.double().cpu(), erv.detach(), rtol=1e-5, atol=1e-6)
+    # the fused finalize+apply launch is bit-identical to the two-launch path
+    mr2 = torch.empty_like(mr)
+    rm2, rv2 = torch.zeros(C, device="cuda"), torch.ones(C, device="cuda")
+    y2 = torch.empty_like(y)
+    nn.bn_finalize_apply(stats, mr2, rm2, rv2, zg, gamma.float().cuda(), beta.float().cuda(),
+                         r.to(BF).cuda() if res else None, y2, B, HW, C, relu, eps, 0.99)
+    assert torch.equal(mr2, mr) and torch.equal(rm2, rm) and torch.equal(rv2, rv)
+    assert torch.equal(y2.view(torch.int16), y.view(torch.int16))
     # backward
     dy = bfr(torch.randn(B, HW, C, generator=g, dtype=torch.float64))
     out.backward(dy)
@@ -179,3 +187,26 @@ def test_pack_multi_matches_single():
         assert torch.equal(e[6], rf)
         if rd is not None:
             assert torch.equal(e[9], rd)
+
+
+@pytest.mark.parametrize("B,H,W,stride,Kp,C,K", [(2, 37, 29, 2, 160, 3, 7), (1, 64, 300, 2, 152, 3, 7),
+                                                 (3, 20, 18, 1, 150, 3, 7), (2, 21, 19, 2, 80, 8, 3)])
+def test_im2col_matches_unfold(B, H, W, stride, Kp, C, K):
+    """ResNet/hourglass stem im2col (7x7, C=3, TF-same pads) vs torch unfold: the LDS-tiled stem
+    kernel (several 64-pixel segments per row at W=300), the 16-byte generic one (C=8) and the
+    scalar one (Kp % 8 != 0).  Exact (bf16 rounding of the same fp32 values)."""
+    from cvlite import ops_nn as nn
+    g = torch.Generator().manual_seed(H * W)
+    x = torch.randn(B, H, W, C, generator=g)
+    Ho, Wo = -(-H // stride), -(-W // stride)
+    ph = max((Ho - 1) * stride + K - H, 0)
+    pw = max((Wo - 1) * stride + K - W, 0)
+    pt, pl = ph // 2, pw // 2
+    out = torch.full((B * Ho * Wo, Kp), 7.0, dtype=BF, device="cuda")
+    nn.im2col(x.cuda(), K, K, stride, pt, pl, Ho, Wo, Kp, out)
+    xp = F.pad(x.permute(0, 3, 1, 2), (pl, pw - pl, pt, ph - pt))
+    cols = F.unfold(xp, K, stride=stride)                    # [B, C*K*K (c, r, s), Ho*Wo]
+    cols = cols.view(B, C, K * K, Ho * Wo).permute(0, 3, 2, 1).reshape(B * Ho * Wo, K * K * C)
+    ref = torch.zeros(B * Ho * Wo, Kp)
+    ref[:, :K * K * C] = cols
+    assert torch.equal(out.cpu().view(torch.int16), ref.to(BF).view(torch.int16))
