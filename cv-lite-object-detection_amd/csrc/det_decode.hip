@@ -1,0 +1,291 @@
+// RetinaNet inference decode on MI355X (RetinaNet/retinanet_module.py:428-529):
+//   cvl_retina_corners   prediction_to_corners (:428-451) for one (level, anchor) map
+//   cvl_retina_decode    image_detections (:483-520) up to the NMS call: corners of every
+//                        (level, anchor, cell), sigmoid class probabilities, per-row max / first
+//                        argmax, `score >= cls_thresh`, rows compacted in the reference's order
+//   cvl_retina_nms       cpu_nms (:453-481): greedy, class-agnostic, score-descending
+//
+// Arithmetic follows the reference's fp32 operation sequence (this file is built with
+// -ffp-contract=off): anchor dims are fp32 (tf.math.sqrt of a python float, :207-209), the grid is
+// a fp32 tf.range, so every corner is fl(fl(g * stride) - fl(t * a)) -+ fl(fl(t' * a') / 2) in
+// fp32.  The sigmoid is evaluated in float64 and rounded to fp32 (TF's own fp32 kernel is an
+// implementation detail outside this image: ulp-level parity unpinned, as for CenterNet).
+//
+// Layout: the model's fused head outputs, row (level offset + cell) of [B][P][ld] with anchor a
+// at box channels 4a..4a+3 (t_y, t_x, t_h, t_w) and class channels aC..aC+C-1.  Output rows are
+// numbered in the reference's concatenation order: level-major, anchor, then cell (row-major).
+#include "cvl_common.h"
+
+namespace {
+
+constexpr int DT = 256;            // decode workgroup
+constexpr int MT = 1024;           // NMS workgroup (one per image)
+
+struct DecodeArgs {
+  const float* reg;
+  const float* cls;
+  const float* adims;              // [5][A][2] (h, w) fp32
+  float* rows;                     // workspace [B][R][6]
+  int32_t* tile_cnt;               // workspace [B][tiles]
+  uint8_t* flag;                   // workspace [B][R]
+  float* dets;                     // [B][R][6]
+  int32_t* count;                  // [B]
+  int ld_reg, ld_cls, A, C, P, R, tiles;
+  int h[5], w[5], stride[5], off[6], roff[6];
+  float thresh;
+};
+
+__device__ __forceinline__ void corners(float ty, float tx, float th, float tw, int y, int x, int stride,
+                                        float ah, float aw, float* o) {
+  const float fs = (float)stride;
+  const float xc = (float)x * fs - tx * aw;             // pred_x_cen (:441)
+  const float yc = (float)y * fs - ty * ah;             // pred_y_cen (:442)
+  const float bw = tw * aw, bh = th * ah;               // (:443-444)
+  const float hh = bh / 2.0f, hw = bw / 2.0f;
+  o[0] = yc - hh;                                       // (:446-449)
+  o[2] = yc + hh;
+  o[1] = xc - hw;
+  o[3] = xc + hw;
+}
+
+__global__ void __launch_bounds__(DT) corners_kernel(const float* xy, int ld, int H, int W, float ah, float aw,
+                                                     int stride, float* out) {
+  const int i = blockIdx.x * DT + threadIdx.x;
+  if (i >= H * W) return;
+  const float* p = xy + (size_t)i * ld;
+  const int y = i / W, x = i - (i / W) * W;
+  float o[4];
+  corners(p[0], p[1], p[2], p[3], y, x, stride, ah, aw, o);
+  float4 v;
+  v.x = o[0]; v.y = o[1]; v.z = o[2]; v.w = o[3];
+  reinterpret_cast<float4*>(out)[i] = v;
+}
+
+// Pass 1: every output row of image blockIdx.y -> its 6 values + keep flag; per-tile counts.
+__global__ void __launch_bounds__(DT) retina_decode_rows(DecodeArgs a) {
+  const int b = blockIdx.y;
+  const int r = blockIdx.x * DT + threadIdx.x;
+  bool keep = false;
+  if (r < a.R) {
+    int l = 0;
+    while (l < 4 && r >= a.roff[l + 1]) ++l;
+    const int hw = a.h[l] * a.w[l];
+    const int rl = r - a.roff[l];
+    const int an = rl / hw, cell = rl - an * hw;
+    const int y = cell / a.w[l], x = cell - (cell / a.w[l]) * a.w[l];
+    const size_t prow = (size_t)b * a.P + a.off[l] + cell;
+    const float* rp = a.reg + prow * a.ld_reg + 4 * an;
+    const float* cp = a.cls + prow * a.ld_cls + (size_t)an * a.C;
+    const float* ad = a.adims + ((size_t)l * a.A + an) * 2;
+    float o[6];
+    corners(rp[0], rp[1], rp[2], rp[3], y, x, a.stride[l], ad[0], ad[1], o);
+    float pmax = 0.f;
+    int lab = 0;
+    for (int c = 0; c < a.C; ++c) {
+      const float pr = (float)(1.0 / (1.0 + exp(-(double)cp[c])));
+      if (c == 0 || pr > pmax) { pmax = pr; lab = c; }      // tf.math.argmax: first maximum
+    }
+    o[4] = pmax;
+    o[5] = (float)lab;
+    keep = pmax >= a.thresh;
+    float* dst = a.rows + ((size_t)b * a.R + r) * 6;
+    for (int k = 0; k < 6; ++k) dst[k] = o[k];
+    a.flag[(size_t)b * a.R + r] = keep ? 1 : 0;
+  }
+  __shared__ int wc[DT / 64];
+  const unsigned long long m = __ballot(keep);
+  if ((threadIdx.x & 63) == 0) wc[threadIdx.x >> 6] = __popcll(m);
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int s = 0;
+    for (int k = 0; k < DT / 64; ++k) s += wc[k];
+    a.tile_cnt[(size_t)b * a.tiles + blockIdx.x] = s;
+  }
+}
+
+// Pass 2: ordered compaction (tile prefix from the per-tile counts + in-tile ballot prefix).
+__global__ void __launch_bounds__(DT) retina_decode_compact(DecodeArgs a) {
+  const int b = blockIdx.y;
+  const int* cnt = a.tile_cnt + (size_t)b * a.tiles;
+  __shared__ int part[DT];
+  __shared__ int wc[DT / 64];
+  int s = 0, tot = 0;
+  for (int t = threadIdx.x; t < a.tiles; t += DT) {
+    const int c = cnt[t];
+    tot += c;
+    if (t < (int)blockIdx.x) s += c;
+  }
+  part[threadIdx.x] = s;
+  __syncthreads();
+  for (int o = DT / 2; o > 0; o >>= 1) {
+    if ((int)threadIdx.x < o) part[threadIdx.x] += part[threadIdx.x + o];
+    __syncthreads();
+  }
+  const int base = part[0];
+  __syncthreads();
+  if (blockIdx.x == 0) {
+    part[threadIdx.x] = tot;
+    __syncthreads();
+    for (int o = DT / 2; o > 0; o >>= 1) {
+      if ((int)threadIdx.x < o) part[threadIdx.x] += part[threadIdx.x + o];
+      __syncthreads();
+    }
+    if (threadIdx.x == 0) a.count[b] = part[0];
+  }
+  const int r = blockIdx.x * DT + threadIdx.x;
+  const bool keep = r < a.R && a.flag[(size_t)b * a.R + r];
+  const unsigned long long m = __ballot(keep);
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  if (lane == 0) wc[wv] = __popcll(m);
+  __syncthreads();
+  if (keep) {
+    int off = base + __popcll(m & ((1ull << lane) - 1ull));
+    for (int k = 0; k < wv; ++k) off += wc[k];
+    const float* src = a.rows + ((size_t)b * a.R + r) * 6;
+    float* dst = a.dets + ((size_t)b * a.R + off) * 6;
+    for (int k = 0; k < 6; ++k) dst[k] = src[k];
+  }
+}
+
+// cpu_nms over image blockIdx.x's first count[b] rows: repeatedly select the highest score among
+// the survivors (lowest row among equal scores: the reference's np.argsort(-scores) is an
+// unstable quicksort, so its tie order is unspecified -- Q1-style, ties are avoided in the
+// goldens), then keep only survivors with ovr <= thr, ovr = inter / (((a_i + a_j) - inter) + 1e-8)
+// in fp32 (:466-478; NaN overlaps are dropped, as `ovr <= thr` is false for them).
+__global__ void __launch_bounds__(MT) retina_nms_kernel(const float* dets, int rows_per_img, const int32_t* count,
+                                                        int n_cap, float thr, int32_t* keep, int32_t* nkeep,
+                                                        uint8_t* alive_ws) {
+  const int b = blockIdx.x;
+  int n = count[b];
+  n = n < n_cap ? n : n_cap;
+  const float* D = dets + (size_t)b * rows_per_img * 6;
+  uint8_t* alive = alive_ws + (size_t)b * n_cap;
+  int32_t* kp = keep + (size_t)b * n_cap;
+  for (int i = threadIdx.x; i < n; i += MT) alive[i] = 1;
+  __shared__ float bs[MT / 64];
+  __shared__ int bi[MT / 64];
+  __shared__ int sel;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  int cnt = 0;
+  __syncthreads();
+  for (;;) {
+    float s = -INFINITY;
+    int si = 0x7fffffff;
+    for (int i = threadIdx.x; i < n; i += MT) {
+      if (!alive[i]) continue;
+      const float sc = D[(size_t)i * 6 + 4];
+      if (sc > s) { s = sc; si = i; }                   // i ascends: first maximum per thread
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+      const float s2 = __shfl_xor(s, o);
+      const int i2 = __shfl_xor(si, o);
+      if (s2 > s || (s2 == s && i2 < si)) { s = s2; si = i2; }
+    }
+    if (lane == 0) { bs[wv] = s; bi[wv] = si; }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      float s0 = bs[0];
+      int i0 = bi[0];
+      for (int k = 1; k < MT / 64; ++k)
+        if (bs[k] > s0 || (bs[k] == s0 && bi[k] < i0)) { s0 = bs[k]; i0 = bi[k]; }
+      sel = (i0 == 0x7fffffff) ? -1 : i0;
+      if (sel >= 0) { kp[cnt] = sel; alive[sel] = 0; }
+    }
+    __syncthreads();
+    const int q = sel;
+    if (q < 0) break;
+    ++cnt;
+    const float* Q = D + (size_t)q * 6;
+    const float qx1 = Q[0], qy1 = Q[1], qx2 = Q[2], qy2 = Q[3];
+    const float qa = (qx2 - qx1) * (qy2 - qy1);
+    for (int i = threadIdx.x; i < n; i += MT) {
+      if (!alive[i]) continue;
+      const float* Rr = D + (size_t)i * 6;
+      const float ra = (Rr[2] - Rr[0]) * (Rr[3] - Rr[1]);
+      const float xx1 = fmaxf(qx1, Rr[0]), yy1 = fmaxf(qy1, Rr[1]);
+      const float xx2 = fminf(qx2, Rr[2]), yy2 = fminf(qy2, Rr[3]);
+      const float w = fmaxf(0.0f, xx2 - xx1), h = fmaxf(0.0f, yy2 - yy1);
+      const float inter = w * h;
+      const float ovr = inter / (((qa + ra) - inter) + 1e-8f);
+      if (!(ovr <= thr)) alive[i] = 0;
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) nkeep[b] = cnt;
+}
+
+bool fill_levels(DecodeArgs& a, const int32_t* level_hw, const int32_t* strides, int A) {
+  a.off[0] = 0;
+  a.roff[0] = 0;
+  for (int l = 0; l < 5; ++l) {
+    if (level_hw[2 * l] <= 0 || level_hw[2 * l + 1] <= 0) return false;
+    if (strides && strides[l] <= 0) return false;
+    a.h[l] = level_hw[2 * l];
+    a.w[l] = level_hw[2 * l + 1];
+    a.stride[l] = strides ? strides[l] : 0;
+    const long hw = (long)a.h[l] * a.w[l];
+    a.off[l + 1] = a.off[l] + (int)hw;
+    if ((long)a.roff[l] + hw * A > 0x7fffffffL / 8) return false;
+    a.roff[l + 1] = a.roff[l] + (int)(hw * A);
+  }
+  a.P = a.off[5];
+  a.R = a.roff[5];
+  a.tiles = (a.R + DT - 1) / DT;
+  return true;
+}
+
+size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
+
+}  // namespace
+
+#define S_ ((hipStream_t)stream)
+
+extern "C" int cvl_retina_corners(const float* xy, int ld, int H, int W, float anchor_h, float anchor_w, int stride,
+                                  float* out, cvl_stream_t stream) {
+  CVL_CHECK_ARG(xy && out && H > 0 && W > 0 && ld >= 4 && stride > 0);
+  hipLaunchKernelGGL(corners_kernel, dim3((H * W + DT - 1) / DT), dim3(DT), 0, S_, xy, ld, H, W, anchor_h,
+                     anchor_w, stride, out);
+  return cvl_launch_status();
+}
+
+extern "C" size_t cvl_retina_decode_workspace_size(int B, const int32_t* level_hw, int n_anchors) {
+  DecodeArgs a;
+  if (B <= 0 || n_anchors <= 0 || !level_hw || !fill_levels(a, level_hw, nullptr, n_anchors)) return 0;
+  return align256((size_t)B * a.R * 6 * sizeof(float)) + align256((size_t)B * a.tiles * sizeof(int32_t)) +
+         align256((size_t)B * a.R);
+}
+
+extern "C" int cvl_retina_decode(const float* reg_pred, int ld_reg, const float* cls_pred, int ld_cls, int B,
+                                 const int32_t* level_hw, const int32_t* strides, const float* anchor_dims,
+                                 int n_anchors, int num_classes, float cls_thresh, float* dets, int32_t* count,
+                                 void* workspace, size_t workspace_bytes, cvl_stream_t stream) {
+  CVL_CHECK_ARG(reg_pred && cls_pred && level_hw && strides && anchor_dims && dets && count && workspace);
+  CVL_CHECK_ARG(B > 0 && n_anchors > 0 && num_classes > 0);
+  CVL_CHECK_ARG(ld_reg >= 4 * n_anchors && ld_cls >= n_anchors * num_classes);
+  DecodeArgs a;
+  CVL_CHECK_ARG(fill_levels(a, level_hw, strides, n_anchors));
+  CVL_CHECK_ARG(workspace_bytes >= cvl_retina_decode_workspace_size(B, level_hw, n_anchors));
+  a.reg = reg_pred; a.cls = cls_pred; a.adims = anchor_dims; a.dets = dets; a.count = count;
+  a.ld_reg = ld_reg; a.ld_cls = ld_cls; a.A = n_anchors; a.C = num_classes; a.thresh = cls_thresh;
+  char* ws = (char*)workspace;
+  a.rows = (float*)ws;
+  ws += align256((size_t)B * a.R * 6 * sizeof(float));
+  a.tile_cnt = (int32_t*)ws;
+  ws += align256((size_t)B * a.tiles * sizeof(int32_t));
+  a.flag = (uint8_t*)ws;
+  hipLaunchKernelGGL(retina_decode_rows, dim3(a.tiles, B), dim3(DT), 0, S_, a);
+  hipLaunchKernelGGL(retina_decode_compact, dim3(a.tiles, B), dim3(DT), 0, S_, a);
+  return cvl_launch_status();
+}
+
+extern "C" size_t cvl_retina_nms_workspace_size(int B, int n_cap) {
+  return B > 0 && n_cap > 0 ? align256((size_t)B * n_cap) : 0;
+}
+
+extern "C" int cvl_retina_nms(const float* dets, int rows_per_img, const int32_t* count, int B, int n_cap,
+                              float iou_thresh, int32_t* keep, int32_t* nkeep, void* workspace, cvl_stream_t stream) {
+  CVL_CHECK_ARG(dets && count && keep && nkeep && workspace && B > 0 && n_cap > 0 && rows_per_img >= n_cap);
+  hipLaunchKernelGGL(retina_nms_kernel, dim3(B), dim3(MT), 0, S_, dets, rows_per_img, count, n_cap, iou_thresh,
+                     keep, nkeep, (uint8_t*)workspace);
+  return cvl_launch_status();
+}

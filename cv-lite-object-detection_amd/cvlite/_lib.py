@@ -78,6 +78,12 @@ SIGNATURES = {
                                      ctypes.c_double, ctypes.c_double, ctypes.c_double, P, P, P]),
     "cvl_nms_workspace_size": (c_size_t, [c_int, c_int]),
     "cvl_nms": (c_int, [P, c_int, P, c_int, ctypes.c_double, P, P, P, P]),
+    "cvl_retina_corners": (c_int, [P, c_int, c_int, c_int, c_float, c_float, c_int, P, P]),
+    "cvl_retina_decode_workspace_size": (c_size_t, [c_int, P, c_int]),
+    "cvl_retina_decode": (c_int, [P, c_int, P, c_int, c_int, P, P, P, c_int, c_int, c_float, P, P, P, c_size_t,
+                                  P]),
+    "cvl_retina_nms_workspace_size": (c_size_t, [c_int, c_int]),
+    "cvl_retina_nms": (c_int, [P, c_int, P, c_int, c_int, c_float, P, P, P, P]),
 }
 
 

@@ -4,9 +4,13 @@
 keeps the reference attributes (`anchor_sizes`, `aspect_ratios`, `anchor_scales`, `strides`,
 `n_anchors`, `box_areas`, `anchor_boxes`) and methods `get_anchors`, `format_data` (device kernel
 cvl_retina_assign: anchor generation + IoU matching per output cell), `focal_loss`,
-`smooth_l1_loss`.  The anchor dimensions are the 45 numbers of retinanet_module.py:205-219,
+`smooth_l1_loss`, and the inference decode `prediction_to_corners`, `cpu_nms`,
+`image_detections` (kernels cvl_retina_corners / cvl_retina_decode / cvl_retina_nms, batched
+form `decode_detections`).  The anchor dimensions are the 45 numbers of retinanet_module.py:205-219,
 computed once on the host with the reference's fp32 operation order.
 """
+import ctypes
+
 import numpy as np
 import torch
 
@@ -137,3 +141,84 @@ class RetinaNet(object):
     def smooth_l1_loss(self, xy_true, xy_pred, mask=1.0, delta=1.0):
         from .fcos import smooth_l1_loss
         return smooth_l1_loss(xy_true, xy_pred, mask, delta)
+
+    # ---- inference decode (retinanet_module.py:428-529) -----------------------------------------
+    def prediction_to_corners(self, xy_pred, anchor_dim, stride):
+        """retinanet_module.py:428-451 -> float64 [S0,S1,4] (y1, x1, y2, x2) (cvl_retina_corners)."""
+        _lib.require_cuda()
+        xy = torch.as_tensor(np.asarray(xy_pred, f32) if not torch.is_tensor(xy_pred) else xy_pred,
+                             dtype=torch.float32).cuda().contiguous()
+        H, W, ld = int(xy.shape[0]), int(xy.shape[1]), int(xy.shape[2])
+        out = torch.empty((H, W, 4), dtype=torch.float32, device="cuda")
+        _lib.call("cvl_retina_corners", _lib.ptr(xy), ld, H, W, float(f32(anchor_dim[0])), float(f32(anchor_dim[1])),
+                  int(stride), _lib.ptr(out), _lib.stream())
+        return out.cpu().numpy().astype(np.float64)
+
+    def cpu_nms(self, dets, base_thr):
+        """retinanet_module.py:453-481 -> int64 indices of the kept rows in selection order
+        (cvl_retina_nms; fp32 arithmetic, the dtype image_detections feeds it)."""
+        _lib.require_cuda()
+        d = torch.as_tensor(np.asarray(dets, f32) if not torch.is_tensor(dets) else dets,
+                            dtype=torch.float32).cuda().contiguous().reshape(-1, int(np.shape(dets)[-1]))
+        n = int(d.shape[0])
+        if n == 0:
+            return np.array([])
+        if d.shape[1] != 6:
+            d6 = torch.zeros((n, 6), dtype=torch.float32, device="cuda")
+            d6[:, :5] = d[:, :5]
+            d = d6
+        cnt = torch.tensor([n], dtype=torch.int32, device="cuda")
+        keep, nk = self._nms(d, n, cnt, 1, n, base_thr)
+        return keep[0, :int(nk[0])].cpu().numpy().astype(np.int64)
+
+    def _nms(self, dets, rows_per_img, count, B, n_cap, thr):
+        keep = torch.empty((B, n_cap), dtype=torch.int32, device="cuda")
+        nk = torch.empty(B, dtype=torch.int32, device="cuda")
+        ws = torch.empty(max(1, _lib.load().cvl_retina_nms_workspace_size(B, n_cap)), dtype=torch.uint8, device="cuda")
+        _lib.call("cvl_retina_nms", _lib.ptr(dets), rows_per_img, _lib.ptr(count), B, n_cap, float(thr),
+                  _lib.ptr(keep), _lib.ptr(nk), _lib.ptr(ws), _lib.stream())
+        return keep, nk
+
+    def decode_detections(self, reg, cls, shapes, iou_thresh=0.5, cls_thresh=0.05, nms_cap=None):
+        """Batched device decode of the fused head outputs (reg [B,P,ld_reg], cls [B,P,ld_cls]
+        fp32, level shapes [(h, w)] x 5): cvl_retina_decode (corners, sigmoid max/argmax,
+        threshold, ordered compaction) then cvl_retina_nms chained on the device counts.
+        Returns a list of B fp32 [k,6] arrays (y1, x1, y2, x2, score, class), as
+        image_detections.  nms_cap bounds the rows NMS considers (default: all)."""
+        _lib.require_cuda(reg, cls)
+        B, ld_reg, ld_cls = int(reg.shape[0]), int(reg.shape[-1]), int(cls.shape[-1])
+        A, C = self.n_anchors, self.n_class
+        hw_arr = (ctypes.c_int32 * 10)(*[int(v) for hwl in shapes for v in hwl])
+        st_arr = (ctypes.c_int32 * 5)(*self.strides)
+        hw, st = ctypes.cast(hw_arr, ctypes.c_void_p), ctypes.cast(st_arr, ctypes.c_void_p)
+        R = A * sum(h * w for h, w in shapes)
+        dets = torch.empty((B, R, 6), dtype=torch.float32, device="cuda")
+        cnt = torch.empty(B, dtype=torch.int32, device="cuda")
+        wsb = _lib.load().cvl_retina_decode_workspace_size(B, hw, A)
+        ws = torch.empty(wsb, dtype=torch.uint8, device="cuda")
+        _lib.call("cvl_retina_decode", _lib.ptr(reg), ld_reg, _lib.ptr(cls), ld_cls, B, hw, st,
+                  _lib.ptr(self.anchor_dims_device()), A, C, float(f32(cls_thresh)), _lib.ptr(dets), _lib.ptr(cnt),
+                  _lib.ptr(ws), wsb, _lib.stream())
+        cap = R if nms_cap is None else min(R, int(nms_cap))
+        keep, nk = self._nms(dets, R, cnt, B, cap, iou_thresh)
+        cnt_h, nk_h, keep_h = cnt.cpu().numpy(), nk.cpu().numpy(), keep.cpu()
+        out = []
+        for b in range(B):
+            n = int(cnt_h[b])
+            if n == 0 or int(nk_h[b]) == 0:
+                out.append(dets[b, :n].cpu().numpy())
+            else:
+                out.append(dets[b][keep_h[b, :int(nk_h[b])].long().cuda()].cpu().numpy())
+        return out
+
+    def image_detections(self, image, iou_thresh=0.5, cls_thresh=0.05):
+        """retinanet_module.py:483-529: inference forward (BN running statistics), decode, NMS ->
+        fp32 [k,6] (y1, x1, y2, x2, score, class) for image [1,H,W,3] (or [H,W,3])."""
+        net = self.model
+        x = torch.as_tensor(image, dtype=torch.float32, device="cuda")
+        if x.dim() == 3:
+            x = x.unsqueeze(0)
+        B, H, W = int(x.shape[0]), int(x.shape[1]), int(x.shape[2])
+        shapes, _, _ = net.layout(B, H, W)
+        reg, cls = net.forward(x.contiguous(), train=False)
+        return self.decode_detections(reg, cls, shapes, iou_thresh, cls_thresh)[0]

@@ -350,6 +350,37 @@ int cvl_adam_clip_update(float* w, const float* g, float* m, float* v, int64_t n
                          int32_t* iterations, float beta1, float beta2, float eps, float inv_bs, float clip,
                          double* sumsq_ws, cvl_stream_t stream);
 
+/* ==========================================================================================
+ * RetinaNet inference decode (RetinaNet/retinanet_module.py:428-529).
+ * ========================================================================================== */
+
+/* prediction_to_corners (:428-451) of one (level, anchor) map: xy [H][W][ld] fp32 (t_y, t_x, t_h,
+ * t_w at 0..3) -> out [H][W][4] = (y1, x1, y2, x2) fp32, centre = (col|row) * stride - t * anchor
+ * (no +0.5, Q21), size = t * anchor; the reference's fp32 operation order. */
+int cvl_retina_corners(const float* xy, int ld, int H, int W, float anchor_h, float anchor_w, int stride,
+                       float* out, cvl_stream_t stream);
+
+/* image_detections (:483-520) up to cpu_nms, for B images of the fused head outputs
+ * (reg [B][P][ld_reg]: anchor a at 4a..4a+3; cls [B][P][ld_cls]: anchor a at aC..aC+C-1; rows
+ * level-major, P = sum h*w).  level_hw [5][2] and strides [5] are HOST arrays; anchor_dims
+ * [5][A][2] fp32 (h, w) on the device.  dets [B][A*P][6] fp32 = (y1, x1, y2, x2, max sigmoid
+ * prob, first-argmax class) for the rows with prob >= cls_thresh, in the reference's
+ * concatenation order (level, anchor, row-major cell); count [B] (device). */
+size_t cvl_retina_decode_workspace_size(int B, const int32_t* level_hw, int n_anchors);
+int cvl_retina_decode(const float* reg_pred, int ld_reg, const float* cls_pred, int ld_cls, int B,
+                      const int32_t* level_hw, const int32_t* strides, const float* anchor_dims, int n_anchors,
+                      int num_classes, float cls_thresh, float* dets, int32_t* count, void* workspace,
+                      size_t workspace_bytes, cvl_stream_t stream);
+
+/* cpu_nms (:453-481) per image over the first min(count[b], n_cap) rows of dets + b*rows_per_img*6
+ * (count on the device: chains after cvl_retina_decode with no host sync): greedy, class-agnostic,
+ * highest score first (lowest row among equal scores), survivors kept iff
+ * inter / (a_i + a_j - inter + 1e-8) <= iou_thresh in fp32.  keep [B][n_cap] = selected rows in
+ * selection order, nkeep [B]. */
+size_t cvl_retina_nms_workspace_size(int B, int n_cap);
+int cvl_retina_nms(const float* dets, int rows_per_img, const int32_t* count, int B, int n_cap, float iou_thresh,
+                   int32_t* keep, int32_t* nkeep, void* workspace, cvl_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -105,3 +105,81 @@ def train_loss_targets(x_pred, x_label):
             cls += fl(t[..., 4:], p[..., 4:])
             reg += sl1(t[..., :4], p[..., :4], m)
     return cls, reg
+
+
+# ----------------------------------------------------------------------------------------------
+# inference decode (retinanet_module.py:428-529)
+# ----------------------------------------------------------------------------------------------
+def prediction_to_corners(xy_pred, anchor_dim, stride):
+    """retinanet_module.py:428-451: fp32 grid (index * stride, no +0.5) - t * anchor; size =
+    t * anchor; corners (y1, x1, y2, x2) = centre -+ size / 2, all in fp32, stored float64."""
+    xy = np.asarray(xy_pred, f32)
+    ah, aw = f32(anchor_dim[0]), f32(anchor_dim[1])
+    gx, gy = np.meshgrid(np.arange(xy.shape[1], dtype=f32), np.arange(xy.shape[0], dtype=f32))
+    xc = gx * f32(stride) - xy[..., 1] * aw
+    yc = gy * f32(stride) - xy[..., 0] * ah
+    bw = xy[..., 3] * aw
+    bh = xy[..., 2] * ah
+    out = np.zeros(xy.shape[:2] + (4,))
+    out[:, :, 0] = yc - bh / f32(2.0)
+    out[:, :, 2] = yc + bh / f32(2.0)
+    out[:, :, 1] = xc - bw / f32(2.0)
+    out[:, :, 3] = xc + bw / f32(2.0)
+    return out
+
+
+def cpu_nms(dets, base_thr):
+    """retinanet_module.py:453-481 in the dets' dtype (fp32 in image_detections).  The reference's
+    np.argsort(-scores) is an unstable quicksort; this restatement uses a stable sort (ties are
+    kept out of the goldens, as for Q1)."""
+    dets = np.asarray(dets)
+    dt = dets.dtype.type
+    x1, y1, x2, y2, scores = dets[:, 0], dets[:, 1], dets[:, 2], dets[:, 3], dets[:, 4]
+    areas = (x2 - x1) * (y2 - y1)
+    order = np.argsort(-scores, kind="stable")
+    keep = []
+    eps = dt(1e-8)
+    while len(order) > 0:
+        i = order[0]
+        keep.append(i)
+        xx1 = np.maximum(x1[i], x1[order[1:]])
+        yy1 = np.maximum(y1[i], y1[order[1:]])
+        xx2 = np.minimum(x2[i], x2[order[1:]])
+        yy2 = np.minimum(y2[i], y2[order[1:]])
+        w = np.maximum(dt(0.0), xx2 - xx1)
+        h = np.maximum(dt(0.0), yy2 - yy1)
+        inter = w * h
+        ovr = inter / (areas[i] + areas[order[1:]] - inter + eps)
+        inds = np.where(ovr <= dt(base_thr))[0]
+        order = order[inds + 1]
+    return np.array(keep, dtype=np.int64)
+
+
+def sigmoid32(x):
+    """fp32 sigmoid evaluated in float64 and rounded (TF's fp32 kernel: ulp-level parity unpinned)."""
+    return (1.0 / (1.0 + np.exp(-np.asarray(x, np.float64)))).astype(f32)
+
+
+def decode_dets(outputs, dims, strides=STRIDES, cls_thresh=0.05):
+    """image_detections (:483-519) before NMS: outputs = nested [5][A] arrays [S0,S1,4+C] (one
+    image) -> fp32 [n,6] rows (y1, x1, y2, x2, max prob, first-argmax class) with prob >=
+    cls_thresh, in (level, anchor, row-major cell) order."""
+    rows = []
+    for l, lev in enumerate(outputs):
+        for a, o in enumerate(lev):
+            o = np.array(o, f32)
+            o[..., :4] = prediction_to_corners(o[..., :4], dims[l][a], strides[l])
+            o[..., 4:] = sigmoid32(o[..., 4:])
+            rows.append(o.reshape(-1, o.shape[-1]))
+    t = np.concatenate(rows, 0)
+    scores = t[:, 4:].max(1)
+    labels = t[:, 4:].argmax(1).astype(f32)
+    dets = np.concatenate([t[:, :4], scores[:, None], labels[:, None]], 1).astype(f32)
+    return dets[dets[:, 4] >= f32(cls_thresh)]
+
+
+def image_detections(outputs, dims, strides=STRIDES, iou_thresh=0.5, cls_thresh=0.05):
+    """image_detections (:483-529) from the model outputs: decode, threshold, cpu_nms."""
+    dets = decode_dets(outputs, dims, strides, cls_thresh)
+    keep = cpu_nms(dets, iou_thresh)
+    return dets[keep] if len(keep) > 0 else dets

@@ -230,7 +230,58 @@ def work_centernet(out_path):
     np.savez_compressed(out_path, **arrays)
 
 
-WORKERS = {"fcos": work_fcos, "retinanet": work_retina, "centernet": work_centernet}
+def work_retina_decode(out_path):
+    """RetinaNet.image_detections / prediction_to_corners / cpu_nms (retinanet_module.py:428-529)
+    with the network replaced by fixed synthetic head outputs.  Every row's winning class logit
+    is a distinct multiple of 1/1024 and the other classes sit >= 0.5 below it, so scores never
+    tie (cpu_nms's quicksort tie order is unspecified) and argmax/threshold decisions sit many
+    ulps from any boundary (the sigmoid is ulp-level unpinned)."""
+    tf = _child_setup("RetinaNet")
+    import retinanet_module as rm
+    rm.build_model = lambda *a, **k: None
+    rng = np.random.default_rng(91)
+    arrays = {}
+    cases = [(128, 80, 0.5, 0.05), (256, 20, 0.3, 0.3), (192, 20, 0.5, 0.05), (128, 20, 0.5, 0.9999)]
+    for i, (D, C, iou_t, cls_t) in enumerate(cases):
+        net = rm.RetinaNet(C, {k: str(k) for k in range(C)}, anchor_sizes=[20.0, 40.0, 80.0, 160.0, 320.0])
+        S = [D // s for s in net.strides]
+        R = 9 * sum(x * x for x in S)
+        win = (rng.permutation(R) - 0.75 * R) / 1024.0
+        outs, o = [], 0
+        for l in range(5):
+            lev = []
+            for a in range(9):
+                n = S[l] * S[l]
+                reg = np.concatenate([rng.normal(0, 0.5, (n, 2)), rng.uniform(0.3, 2.5, (n, 2))], 1)
+                cls = win[o:o + n, None] - rng.uniform(0.5, 6.0, (n, C))
+                cls[np.arange(n), rng.integers(0, C, n)] = win[o:o + n]
+                o += n
+                m = np.concatenate([reg, cls], 1).astype(np.float32).reshape(1, S[l], S[l], 4 + C)
+                lev.append(m)
+            outs.append(lev)
+        net.model = lambda x, training=None, _o=outs: [[tf.constant(m) for m in lev] for lev in _o]
+        dets = net.image_detections(None, iou_thresh=iou_t, cls_thresh=cls_t)
+        arrays["case_%d_cfg" % i] = np.array([D, C, iou_t, cls_t], np.float64)
+        arrays["case_%d_anchor_dims" % i] = np.array(net.anchor_boxes, np.float32)
+        for l in range(5):
+            arrays["case_%d_out_L%d" % (i, l)] = np.concatenate([m for m in outs[l]], 0)
+        arrays["case_%d_dets" % i] = np.asarray(dets, np.float32).reshape(-1, 6)
+        if i == 0:
+            xy = outs[2][4][0][..., :4]
+            arrays["corners_in"] = xy
+            arrays["corners_dims"] = np.asarray(net.anchor_boxes[2][4], np.float32)
+            arrays["corners_out"] = np.asarray(net.prediction_to_corners(xy, net.anchor_boxes[2][4], 32))
+            d = np.concatenate([np.sort(rng.uniform(0, 200, (300, 2)), 1)[:, [0, 1]],
+                                rng.uniform(0, 200, (300, 2))], 1)
+            d = np.stack([d[:, 0], d[:, 2], d[:, 0] + rng.uniform(1, 60, 300), d[:, 2] + rng.uniform(1, 60, 300),
+                          rng.permutation(300) / 300.0 + 0.001, np.zeros(300)], 1).astype(np.float32)
+            arrays["nms_dets"] = d
+            arrays["nms_keep"] = np.asarray(net.cpu_nms(d, 0.45), np.int64)
+    np.savez_compressed(out_path, **arrays)
+
+
+WORKERS = {"fcos": work_fcos, "retinanet": work_retina, "centernet": work_centernet,
+           "retina_decode": work_retina_decode}
 
 
 def main():

@@ -79,3 +79,29 @@ def test_centernet_targets_splat_nms(golden):
     np.testing.assert_array_equal(centernet_ref.center_dist_1d(np.arange(3, 9) + 0.5, 6, 8.0), d["cd1_out"])
     for i in range(8):
         np.testing.assert_array_equal(centernet_ref.nms(d["nms_%d_in" % i], 0.213), d["nms_%d_out" % i])
+
+
+def _retina_decode_case(d, i):
+    D, C, iou_t, cls_t = d["case_%d_cfg" % i]
+    dims = d["case_%d_anchor_dims" % i]
+    outs = [list(d["case_%d_out_L%d" % (i, l)]) for l in range(5)]
+    return int(D), int(C), float(iou_t), float(cls_t), dims, outs
+
+
+def test_retina_decode_nms_oracle(golden):
+    """retinanet_module.py:428-529: corners bit-exact, cpu_nms indices exact, image_detections
+    rows: boxes/labels exact, scores within 4 fp32 ulp (sigmoid evaluation order)."""
+    d = golden("retina_decode")
+    np.testing.assert_array_equal(retina_ref.prediction_to_corners(d["corners_in"], d["corners_dims"], 32),
+                                  d["corners_out"])
+    np.testing.assert_array_equal(retina_ref.cpu_nms(d["nms_dets"], 0.45), d["nms_keep"])
+    i = 0
+    while "case_%d_cfg" % i in d:
+        D, C, iou_t, cls_t, dims, outs = _retina_decode_case(d, i)
+        got = retina_ref.image_detections(outs, dims, iou_thresh=iou_t, cls_thresh=cls_t)
+        ref = d["case_%d_dets" % i]
+        assert got.shape == ref.shape
+        np.testing.assert_array_equal(got[:, [0, 1, 2, 3, 5]], ref[:, [0, 1, 2, 3, 5]])
+        np.testing.assert_allclose(got[:, 4], ref[:, 4], rtol=5e-7, atol=0)
+        i += 1
+    assert i == 4
