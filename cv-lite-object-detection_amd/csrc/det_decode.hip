@@ -4,6 +4,8 @@
 //                        (level, anchor, cell), sigmoid class probabilities, per-row max / first
 //                        argmax, `score >= cls_thresh`, rows compacted in the reference's order
 //   cvl_retina_nms       cpu_nms (:453-481): greedy, class-agnostic, score-descending
+//   cvl_fcos_detect      FCOS/infer_fcos.py:27-62 image_detections: corners, sigmoid scores and
+//                        tf.image.combined_non_max_suppression (restated; TF is absent here)
 //
 // Arithmetic follows the reference's fp32 operation sequence (this file is built with
 // -ffp-contract=off): anchor dims are fp32 (tf.math.sqrt of a python float, :207-209), the grid is
@@ -214,6 +216,170 @@ __global__ void __launch_bounds__(MT) retina_nms_kernel(const float* dets, int r
   if (threadIdx.x == 0) nkeep[b] = cnt;
 }
 
+// ------------------------------------------------------------------------------------------------
+// FCOS inference (FCOS/infer_fcos.py:27-62): boxes = fcos.prediction_to_corners (fp32 grid + 0.5
+// -+ t, times the python-int stride in float64, stored back into the fp32 output array),
+// scores = sigmoid(cls) (or sigmoid(centerness) * sigmoid(cls) with center=True), then
+// tf.image.combined_non_max_suppression (q = 1 shared boxes, clip_boxes=False): per class,
+// candidates with score > score_threshold, greedy by score, a candidate is selected iff no
+// already-selected box of its class has IoU > iou_threshold (TF's IOUGreaterThanThreshold: corners
+// normalised with min/max, a non-positive area never suppresses), at most max_per_class per class;
+// then every class's selections merged by descending score, the first max_total kept, rest zero.
+// TF's priority queue and std::sort leave equal-score order unspecified: here lower box index
+// (per class) and then lower class / earlier selection (merge) win.
+// ------------------------------------------------------------------------------------------------
+constexpr int FT = 1024;
+constexpr int kMaxCells = 16384;           // P held in LDS by the per-class NMS (scores + flags)
+
+struct FcosDetArgs {
+  const float* reg;                        // [B][P][ld_reg] (t, b, l, r, centerness)
+  const float* cls;                        // [B][P][ld_cls]
+  float* boxes;                            // workspace [B][P][4]
+  float* sel_score;                        // workspace [B][C][mpc]
+  int32_t* sel_idx;                        // workspace [B][C][mpc]
+  int32_t* sel_n;                          // workspace [B][C]
+  float* out_boxes;                        // [B][max_total][4]
+  float* out_scores;                       // [B][max_total]
+  float* out_classes;                      // [B][max_total]
+  int32_t* valid;                          // [B]
+  int ld_reg, ld_cls, C, P, center, mpc, max_total;
+  int h[5], w[5], stride[5], off[6];
+  float iou, thr;
+};
+
+__global__ void __launch_bounds__(DT) fcos_boxes_kernel(FcosDetArgs a) {
+  const int b = blockIdx.y;
+  const int i = blockIdx.x * DT + threadIdx.x;
+  if (i >= a.P) return;
+  int l = 0;
+  while (l < 4 && i >= a.off[l + 1]) ++l;
+  const int cell = i - a.off[l];
+  const int y = cell / a.w[l], x = cell - (cell / a.w[l]) * a.w[l];
+  const float* q = a.reg + ((size_t)b * a.P + i) * a.ld_reg;
+  const float gy = (float)y + 0.5f, gx = (float)x + 0.5f;
+  const double st = (double)a.stride[l];
+  float4 v;
+  v.x = (float)(st * (double)(gy - q[0]));
+  v.y = (float)(st * (double)(gx - q[2]));
+  v.z = (float)(st * (double)(gy + q[1]));
+  v.w = (float)(st * (double)(gx + q[3]));
+  reinterpret_cast<float4*>(a.boxes)[(size_t)b * a.P + i] = v;
+}
+
+__device__ __forceinline__ float sigm(float x) { return (float)(1.0 / (1.0 + exp(-(double)x))); }
+
+__device__ __forceinline__ bool iou_gt(float4 bi, float4 bj, float thr) {
+  const float ymin_i = fminf(bi.x, bi.z), xmin_i = fminf(bi.y, bi.w);
+  const float ymax_i = fmaxf(bi.x, bi.z), xmax_i = fmaxf(bi.y, bi.w);
+  const float ymin_j = fminf(bj.x, bj.z), xmin_j = fminf(bj.y, bj.w);
+  const float ymax_j = fmaxf(bj.x, bj.z), xmax_j = fmaxf(bj.y, bj.w);
+  const float area_i = (ymax_i - ymin_i) * (xmax_i - xmin_i);
+  const float area_j = (ymax_j - ymin_j) * (xmax_j - xmin_j);
+  if (area_i <= 0.f || area_j <= 0.f) return false;
+  const float iy = fmaxf(fminf(ymax_i, ymax_j) - fmaxf(ymin_i, ymin_j), 0.0f);
+  const float ix = fmaxf(fminf(xmax_i, xmax_j) - fmaxf(xmin_i, xmin_j), 0.0f);
+  const float inter = iy * ix;
+  return inter / (area_i + area_j - inter) > thr;
+}
+
+// One workgroup per (class, image): scores of the class staged in LDS (-inf = not a candidate).
+__global__ void __launch_bounds__(FT) fcos_class_nms_kernel(FcosDetArgs a) {
+  const int c = blockIdx.x, b = blockIdx.y;
+  __shared__ float sc[kMaxCells];
+  __shared__ float bs[FT / 64];
+  __shared__ int bi[FT / 64];
+  __shared__ int sel;
+  const float4* B4 = reinterpret_cast<const float4*>(a.boxes) + (size_t)b * a.P;
+  for (int i = threadIdx.x; i < a.P; i += FT) {
+    const size_t row = (size_t)b * a.P + i;
+    float s = sigm(a.cls[row * a.ld_cls + c]);
+    if (a.center) s = sigm(a.reg[row * a.ld_reg + 4]) * s;
+    sc[i] = s > a.thr ? s : -INFINITY;
+  }
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const size_t so = ((size_t)b * a.C + c) * a.mpc;
+  int n = 0;
+  __syncthreads();
+  while (n < a.mpc) {
+    float s = -INFINITY;
+    int si = 0x7fffffff;
+    for (int i = threadIdx.x; i < a.P; i += FT)
+      if (sc[i] > s) { s = sc[i]; si = i; }
+    for (int o = 32; o > 0; o >>= 1) {
+      const float s2 = __shfl_xor(s, o);
+      const int i2 = __shfl_xor(si, o);
+      if (s2 > s || (s2 == s && i2 < si)) { s = s2; si = i2; }
+    }
+    if (lane == 0) { bs[wv] = s; bi[wv] = si; }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      float s0 = bs[0];
+      int i0 = bi[0];
+      for (int k = 1; k < FT / 64; ++k)
+        if (bs[k] > s0 || (bs[k] == s0 && bi[k] < i0)) { s0 = bs[k]; i0 = bi[k]; }
+      sel = (s0 == -INFINITY) ? -1 : i0;
+      if (sel >= 0) {
+        a.sel_score[so + n] = s0;
+        a.sel_idx[so + n] = i0;
+        sc[i0] = -INFINITY;
+      }
+    }
+    __syncthreads();
+    const int q = sel;
+    if (q < 0) break;
+    ++n;
+    const float4 bq = B4[q];
+    for (int i = threadIdx.x; i < a.P; i += FT)
+      if (sc[i] != -INFINITY && iou_gt(B4[i], bq, a.iou)) sc[i] = -INFINITY;
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) a.sel_n[(size_t)b * a.C + c] = n;
+}
+
+// Merge per image: each selection's rank under (score desc, class asc, selection order asc);
+// ranks < max_total are written to their slot, the remaining slots are zero.
+__global__ void __launch_bounds__(FT) fcos_merge_kernel(FcosDetArgs a) {
+  const int b = blockIdx.x;
+  const int N = a.C * a.mpc;
+  const float* S = a.sel_score + (size_t)b * N;
+  const int32_t* ns = a.sel_n + (size_t)b * a.C;
+  __shared__ int tot_s;
+  if (threadIdx.x == 0) {
+    int t = 0;
+    for (int c = 0; c < a.C; ++c) t += ns[c];
+    tot_s = t;
+  }
+  for (int k = threadIdx.x; k < a.max_total; k += FT) {
+    float* ob = a.out_boxes + ((size_t)b * a.max_total + k) * 4;
+    ob[0] = ob[1] = ob[2] = ob[3] = 0.f;
+    a.out_scores[(size_t)b * a.max_total + k] = 0.f;
+    a.out_classes[(size_t)b * a.max_total + k] = 0.f;
+  }
+  __syncthreads();
+  for (int e = threadIdx.x; e < N; e += FT) {
+    const int c = e / a.mpc, k = e - c * a.mpc;
+    if (k >= ns[c]) continue;
+    const float s = S[e];
+    int rank = 0;
+    for (int c2 = 0; c2 < a.C && rank < a.max_total; ++c2) {
+      const int n2 = ns[c2];
+      const float* S2 = S + (size_t)c2 * a.mpc;
+      for (int k2 = 0; k2 < n2; ++k2) {
+        const float t = S2[k2];
+        rank += (t > s || (t == s && (c2 < c || (c2 == c && k2 < k)))) ? 1 : 0;
+      }
+    }
+    if (rank < a.max_total) {
+      const float4 bx = reinterpret_cast<const float4*>(a.boxes)[(size_t)b * a.P + a.sel_idx[(size_t)b * N + e]];
+      float* ob = a.out_boxes + ((size_t)b * a.max_total + rank) * 4;
+      ob[0] = bx.x; ob[1] = bx.y; ob[2] = bx.z; ob[3] = bx.w;
+      a.out_scores[(size_t)b * a.max_total + rank] = s;
+      a.out_classes[(size_t)b * a.max_total + rank] = (float)c;
+    }
+  }
+  if (threadIdx.x == 0) a.valid[b] = tot_s < a.max_total ? tot_s : a.max_total;
+}
+
 bool fill_levels(DecodeArgs& a, const int32_t* level_hw, const int32_t* strides, int A) {
   a.off[0] = 0;
   a.roff[0] = 0;
@@ -287,5 +453,52 @@ extern "C" int cvl_retina_nms(const float* dets, int rows_per_img, const int32_t
   CVL_CHECK_ARG(dets && count && keep && nkeep && workspace && B > 0 && n_cap > 0 && rows_per_img >= n_cap);
   hipLaunchKernelGGL(retina_nms_kernel, dim3(B), dim3(MT), 0, S_, dets, rows_per_img, count, n_cap, iou_thresh,
                      keep, nkeep, (uint8_t*)workspace);
+  return cvl_launch_status();
+}
+
+extern "C" size_t cvl_fcos_detect_workspace_size(int B, int P, int num_classes, int max_per_class) {
+  if (B <= 0 || P <= 0 || num_classes <= 0 || max_per_class <= 0) return 0;
+  const size_t sel = (size_t)B * num_classes * max_per_class;
+  return align256((size_t)B * P * 4 * sizeof(float)) + align256(sel * sizeof(float)) +
+         align256(sel * sizeof(int32_t)) + align256((size_t)B * num_classes * sizeof(int32_t));
+}
+
+extern "C" int cvl_fcos_detect(const float* reg_pred, int ld_reg, const float* cls_pred, int ld_cls, int B,
+                               const int32_t* level_hw, const int32_t* strides, int num_classes, int center,
+                               float iou_thresh, float score_thresh, int max_per_class, int max_total,
+                               float* out_boxes, float* out_scores, float* out_classes, int32_t* valid,
+                               void* workspace, size_t workspace_bytes, cvl_stream_t stream) {
+  CVL_CHECK_ARG(reg_pred && cls_pred && level_hw && strides && out_boxes && out_scores && out_classes && valid &&
+                workspace);
+  CVL_CHECK_ARG(B > 0 && num_classes > 0 && ld_reg >= 5 && ld_cls >= num_classes && max_per_class > 0 &&
+                max_total > 0);
+  FcosDetArgs a;
+  a.off[0] = 0;
+  for (int l = 0; l < 5; ++l) {
+    CVL_CHECK_ARG(level_hw[2 * l] > 0 && level_hw[2 * l + 1] > 0 && strides[l] > 0);
+    a.h[l] = level_hw[2 * l];
+    a.w[l] = level_hw[2 * l + 1];
+    a.stride[l] = strides[l];
+    a.off[l + 1] = a.off[l] + a.h[l] * a.w[l];
+  }
+  a.P = a.off[5];
+  CVL_CHECK_ARG(a.P <= kMaxCells);
+  a.mpc = max_per_class < a.P ? max_per_class : a.P;      // TF: min(max_output_size_per_class, boxes)
+  CVL_CHECK_ARG(workspace_bytes >= cvl_fcos_detect_workspace_size(B, a.P, num_classes, a.mpc));
+  a.reg = reg_pred; a.cls = cls_pred; a.ld_reg = ld_reg; a.ld_cls = ld_cls; a.C = num_classes;
+  a.center = center; a.max_total = max_total; a.iou = iou_thresh; a.thr = score_thresh;
+  a.out_boxes = out_boxes; a.out_scores = out_scores; a.out_classes = out_classes; a.valid = valid;
+  const size_t sel = (size_t)B * num_classes * a.mpc;
+  char* ws = (char*)workspace;
+  a.boxes = (float*)ws;
+  ws += align256((size_t)B * a.P * 4 * sizeof(float));
+  a.sel_score = (float*)ws;
+  ws += align256(sel * sizeof(float));
+  a.sel_idx = (int32_t*)ws;
+  ws += align256(sel * sizeof(int32_t));
+  a.sel_n = (int32_t*)ws;
+  hipLaunchKernelGGL(fcos_boxes_kernel, dim3((a.P + DT - 1) / DT, B), dim3(DT), 0, S_, a);
+  hipLaunchKernelGGL(fcos_class_nms_kernel, dim3(num_classes, B), dim3(FT), 0, S_, a);
+  hipLaunchKernelGGL(fcos_merge_kernel, dim3(B), dim3(FT), 0, S_, a);
   return cvl_launch_status();
 }

@@ -381,6 +381,21 @@ size_t cvl_retina_nms_workspace_size(int B, int n_cap);
 int cvl_retina_nms(const float* dets, int rows_per_img, const int32_t* count, int B, int n_cap, float iou_thresh,
                    int32_t* keep, int32_t* nkeep, void* workspace, cvl_stream_t stream);
 
+/* FCOS/infer_fcos.py:27-62 image_detections for B images of the FCOS head outputs (reg [B][P][ld_reg]
+ * = t, b, l, r, centerness; cls [B][P][ld_cls]; rows level-major, P = sum h*w <= 16384; level_hw
+ * [5][2] and strides [5] HOST arrays): boxes = fcos.prediction_to_corners rounded to fp32, scores =
+ * sigmoid(cls) (center != 0: sigmoid(centerness) * sigmoid(cls)), then
+ * tf.image.combined_non_max_suppression(max_output_size_per_class = max_per_class, max_total_size =
+ * max_total, clip_boxes=False): out_boxes [B][max_total][4] (y1, x1, y2, x2), out_scores /
+ * out_classes [B][max_total] (zero padded), valid [B].  TF's op is restated (parity unpinned at
+ * the reference level; equal-score order: lower box index, then lower class). */
+size_t cvl_fcos_detect_workspace_size(int B, int P, int num_classes, int max_per_class);
+int cvl_fcos_detect(const float* reg_pred, int ld_reg, const float* cls_pred, int ld_cls, int B,
+                    const int32_t* level_hw, const int32_t* strides, int num_classes, int center, float iou_thresh,
+                    float score_thresh, int max_per_class, int max_total, float* out_boxes, float* out_scores,
+                    float* out_classes, int32_t* valid, void* workspace, size_t workspace_bytes,
+                    cvl_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

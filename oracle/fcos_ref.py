@@ -195,3 +195,76 @@ def prediction_to_corners(xy_pred, stride):
     out[..., 1] = gx - xy[..., 2]
     out[..., 3] = gx + xy[..., 3]
     return stride * out
+
+
+def sigmoid32(x):
+    """fp32 sigmoid evaluated in float64 and rounded (TF's fp32 kernel: ulp-level parity unpinned)."""
+    return (1.0 / (1.0 + np.exp(-np.asarray(x, np.float64)))).astype(f32)
+
+
+def _iou_gt(bi, bj, thr):
+    """TF non_max_suppression_op.cc IOUGreaterThanThreshold (fp32, min/max-normalised corners; a
+    non-positive area never suppresses) of one box bi against boxes bj [n,4]."""
+    bi = np.asarray(bi, f32)
+    bj = np.asarray(bj, f32)
+    ymin_i, xmin_i = min(bi[0], bi[2]), min(bi[1], bi[3])
+    ymax_i, xmax_i = max(bi[0], bi[2]), max(bi[1], bi[3])
+    ymin_j, xmin_j = np.minimum(bj[:, 0], bj[:, 2]), np.minimum(bj[:, 1], bj[:, 3])
+    ymax_j, xmax_j = np.maximum(bj[:, 0], bj[:, 2]), np.maximum(bj[:, 1], bj[:, 3])
+    area_i = (ymax_i - ymin_i) * (xmax_i - xmin_i)
+    area_j = (ymax_j - ymin_j) * (xmax_j - xmin_j)
+    iy = np.maximum(np.minimum(ymax_i, ymax_j) - np.maximum(ymin_i, ymin_j), f32(0))
+    ix = np.maximum(np.minimum(xmax_i, xmax_j) - np.maximum(xmin_i, xmin_j), f32(0))
+    inter = iy * ix
+    with np.errstate(divide="ignore", invalid="ignore"):
+        iou = inter / (area_i + area_j - inter)
+    return (iou > f32(thr)) & (area_i > 0) & (area_j > 0)
+
+
+def combined_non_max_suppression(boxes, scores, max_output_size_per_class, max_total_size, iou_threshold=0.5,
+                                 score_threshold=0.05):
+    """tf.image.combined_non_max_suppression for one image with q = 1 shared boxes,
+    clip_boxes=False, pad_per_class=False (FCOS/infer_fcos.py:55-58), restated from TF's published
+    kernel (TF is not installed: parity unpinned at the reference level).  boxes [N,4], scores
+    [N,C] fp32 -> (boxes [T,4], scores [T], classes [T], valid) zero padded to T = max_total_size.
+    Equal scores: lower box index first per class, then lower class / earlier selection."""
+    boxes = np.asarray(boxes, f32)
+    scores = np.asarray(scores, f32)
+    N, C = scores.shape
+    per = min(max_output_size_per_class, N)
+    cand = []
+    for c in range(C):
+        s = scores[:, c]
+        idx = np.nonzero(s > f32(score_threshold))[0]
+        order = idx[np.argsort(-s[idx], kind="stable")]
+        sel = []
+        for i in order:
+            if len(sel) >= per:
+                break
+            if sel and _iou_gt(boxes[i], boxes[np.array(sel)], iou_threshold).any():
+                continue
+            sel.append(i)
+        cand += [(s[i], c, k, i) for k, i in enumerate(sel)]
+    cand.sort(key=lambda t: (-float(t[0]), t[1], t[2]))
+    T = max_total_size
+    ob, os_, oc = np.zeros((T, 4), f32), np.zeros(T, f32), np.zeros(T, f32)
+    for r, (s, c, _, i) in enumerate(cand[:T]):
+        ob[r], os_[r], oc[r] = boxes[i], s, c
+    return ob, os_, oc, min(len(cand), T)
+
+
+def image_detections(outputs, num_classes, center=False, iou_thresh=0.5, cls_thresh=0.05, max_detections=100,
+                     max_total_size=100, strides=STRIDES):
+    """FCOS/infer_fcos.py:27-62 from the model outputs (5 arrays [S0,S1,5+C], one image):
+    fp32 boxes from prediction_to_corners (float64, stored back into the fp32 output), sigmoid
+    scores (times the centerness sigmoid with center=True), combined NMS."""
+    rows = []
+    for l, o in enumerate(outputs):
+        o = np.array(o, f32)
+        o[..., :4] = prediction_to_corners(o[..., :4], strides[l])
+        rows.append(o.reshape(-1, num_classes + 5))
+    t = np.concatenate(rows, 0)
+    sc = sigmoid32(t[:, 5:])
+    if center:
+        sc = sigmoid32(t[:, 4])[:, None] * sc
+    return combined_non_max_suppression(t[:, :4], sc, max_detections, max_total_size, iou_thresh, cls_thresh)

@@ -105,3 +105,20 @@ def test_retina_decode_nms_oracle(golden):
         np.testing.assert_allclose(got[:, 4], ref[:, 4], rtol=5e-7, atol=0)
         i += 1
     assert i == 4
+
+
+def test_fcos_combined_nms_known_answer():
+    """Hand-worked case of the tf.image.combined_non_max_suppression restatement (TF is absent:
+    this pins the published semantics, not TF itself): score > threshold (strict), per-class
+    greedy with IoU > thr suppressing, degenerate boxes never suppress, per-class cap, merge by
+    descending score, zero padding, valid count."""
+    boxes = np.array([[0, 0, 10, 10], [1, 1, 11, 11], [20, 20, 30, 30], [5, 5, 5, 9], [0, 0, 10, 10]], np.float32)
+    scores = np.array([[0.9, 0.1], [0.8, 0.7], [0.3, 0.05], [0.6, 0.2], [0.05, 0.95]], np.float32)
+    b, s, c, n = fcos_ref.combined_non_max_suppression(boxes, scores, 2, 6, iou_threshold=0.5, score_threshold=0.05)
+    # class 0: 0 (0.9) keeps; 1 (0.8) IoU 81/119 > 0.5 suppressed; 3 (0.6, zero area) kept -> cap 2 reached
+    # class 1: 4 (0.95); 1 (0.7) IoU with 4 = 81/119 suppressed; 3 (0.2) kept; 2 (0.05) not > 0.05
+    assert n == 4
+    np.testing.assert_array_equal(s, np.array([0.95, 0.9, 0.6, 0.2, 0, 0], np.float32))
+    np.testing.assert_array_equal(c, np.array([1, 0, 0, 1, 0, 0], np.float32))
+    np.testing.assert_array_equal(b[:4], boxes[[4, 0, 3, 3]])
+    assert not b[4:].any()
