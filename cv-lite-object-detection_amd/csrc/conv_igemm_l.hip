@@ -329,9 +329,11 @@ int cvl_conv_igemm_l(const cvl_conv_desc* d, int dst_up, int dst_w, const void* 
   if (cvl_conv_prepare(d, BM, &a)) return -1;
   a.dst_up = dst_up;
   a.dst_w = dst_w;
-  // too few tiles to fill 256 CUs at one 8-wave workgroup each (tests lower the bar); a launch
-  // with too few 256-wide tiles drops to the 128-wide tile first
-  const long min_tiles = cvl_env_int("CVL_CONV_L_MIN_TILES", 384);
+  // below 128 tiles the 128-row kernel with split-K fills the 256 CUs better (tests lower the
+  // bar).  Whole-step sweep (tools/gpu_knob_sweep.sh, FCOS bs=16): 384 -> 773, 256 -> 785,
+  // 192 -> 785, 128 -> 807, 1 -> 789 img/s (conv4_x 3x3 sits at exactly 128 tiles).  A launch
+  // with too few 256-wide tiles drops to the 128-wide tile first.
+  const long min_tiles = cvl_env_int("CVL_CONV_L_MIN_TILES", 128);
   int use_bn = bn;
   if (use_bn == 256 && (long)a.m_tiles * (a.Npad / 256) < cvl_env_int("CVL_CONV_L256_MIN_TILES", 512)) use_bn = 128;
   if ((long)a.m_tiles * (a.Npad / use_bn) < min_tiles) return -1;

@@ -32,7 +32,7 @@ def ref_conv(x, w, b, stride, pad):
 @pytest.fixture(params=["base", "l", "l256"])
 def kern(request, monkeypatch):
     """Run a test through the 128-row register-staged kernel ("base"), the 256-row LDS-DMA kernel
-    ("l", normally taken only by launches with >= 384 tiles; 128/64-wide N tiles) and its
+    ("l", normally taken only by launches with >= 128 tiles; 128/64-wide N tiles) and its
     256x256-tile form ("l256", Npad % 256 == 0 only)."""
     if request.param in ("l", "l256"):
         monkeypatch.setenv("CVL_CONV_L_MIN_TILES", "1")
