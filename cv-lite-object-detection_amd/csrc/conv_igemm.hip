@@ -448,8 +448,10 @@ static inline int pick_ksplit(const ConvArgs& a, int BN_, int BK_) {
   if (a.nseg != 1) return 1;
   const int tiles = a.m_tiles * (a.Npad / BN_);
   const int nk = a.K / BK_;
-  if (tiles >= 192 || nk < 8) return 1;
-  int s = (384 + tiles - 1) / tiles;
+  const int max_tiles = cvl_env_int("CVL_KSPLIT_MAX_TILES", 192);
+  const int target = cvl_env_int("CVL_KSPLIT_TARGET", 384);   // workgroups a split launch aims for
+  if (tiles >= max_tiles || nk < 8) return 1;
+  int s = (target + tiles - 1) / tiles;
   if (s > nk / 4) s = nk / 4;
   return s < 1 ? 1 : s;
 }

@@ -8,13 +8,16 @@ Keras ResNet50 v1 structure (third-party, restated): ZeroPadding2D(3) -> conv1 7
 shortcut of each stack's first block, BN eps 1.001e-5) -> C3 = conv3_block4_out,
 C4 = conv4_block6_out, C5 = conv5_block3_out.
 """
+import os
+
 import torch
 
 from . import ops_nn as nn
 from .layers import BF16, BatchNorm, Conv, ConvBN, StatsArena
 
 STEM_K = 7
-STEM_KP = 160      # im2col K = 7*7*3 = 147 padded to a multiple of 32
+STEM_KP = int(os.environ.get("CVL_STEM_KP", 192))   # im2col K = 7*7*3 = 147 padded: 192 = 3 x 64 lets the
+#                                                      LDS-DMA kernels take the stem (+0.6 % step vs 160)
 
 
 class Stem(object):

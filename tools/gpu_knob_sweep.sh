@@ -9,5 +9,11 @@ run() {  # tag env...
 }
 for r in 1 2; do
   run def X=0
-  for t in ${SWEEP_TILES:-128 192 256 320}; do run lmin$t CVL_CONV_L_MIN_TILES=$t; done
+  if [ -n "$SWEEP_TILES" ]; then
+    for t in $SWEEP_TILES; do run lmin$t CVL_CONV_L_MIN_TILES=$t; done
+  fi
+  for v in ${SWEEP_KSPLIT:-}; do   # entries MAXTILES:TARGET
+    run ks_${v/:/_} CVL_KSPLIT_MAX_TILES=${v%%:*} CVL_KSPLIT_TARGET=${v##*:}
+  done
+  for v in ${SWEEP_ENV:-}; do run ${v%%=*} $v; done
 done
