@@ -291,8 +291,9 @@ inline double wl_time(int tiles, int m_total, int bco, int* best_s) {
   int max_s = m_total / 512;
   if (max_s < 1) max_s = 1;
   if (max_s > 4096 / tiles) max_s = 4096 / tiles > 1 ? 4096 / tiles : 1;
-  const double slab_us = (double)bco * BKK * 4 * 2 / 5.0e6;
-  const double blk_us = bco == 256 ? 4.4 : 2.8;
+  // sweep knobs (tools/gpu_knob_sweep.sh): slab cost in percent, block times in 0.1 us
+  const double slab_us = (double)bco * BKK * 4 * 2 / 5.0e6 * cvl_env_int("CVL_WGL_SLAB_PCT", 100) / 100.0;
+  const double blk_us = bco == 256 ? cvl_env_int("CVL_WGL_BLK256", 44) / 10.0 : cvl_env_int("CVL_WGL_BLK128", 28) / 10.0;
   double best_t = 1e30;
   *best_s = 1;
   for (int s = 1; s <= max_s; ++s) {
