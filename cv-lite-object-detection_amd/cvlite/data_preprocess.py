@@ -1,0 +1,71 @@
+"""Drop-in mirror of FCOS/data_preprocess.py's image path on MI355X.
+
+  random_flip_horizontal(image, boxes, p_flip=0.5)                  data_preprocess.py:24-39
+  resize_and_pad_image(image, jitter, min_side, max_side, stride, equal_dims)   :41-96
+  preprocess_image(image, ..., flip, out)                           fused flip + resize + pad
+
+The resize / normalise / pad (and the flip, when fused) run in one cvl_resize_pad_normalize
+launch per image that can write straight into a slot of the device batch.  JPEG decode
+(`_parse_image`) is outside this module: the input is a decoded [H,W,3] uint8 or fp32 image on
+the GPU (or host; it is copied).  The jitter draw uses numpy's generator instead of
+tf.random.uniform (a different stream by construction).
+"""
+import numpy as np
+import torch
+
+from . import _lib
+
+f32 = np.float32
+
+
+def _plan(H, W, jitter, min_side, max_side, stride, equal_dims, rng):
+    shape = np.array([H, W], f32)
+    if jitter is not None:
+        rng = rng if rng is not None else np.random.default_rng()
+        min_side = f32(rng.uniform(jitter[0], jitter[1]))
+    ratio = f32(min_side) / shape.min()
+    if ratio * shape.max() > f32(max_side):
+        ratio = f32(max_side) / shape.max()
+    new_shape = (ratio * shape).astype(f32)
+    pd = (np.ceil(new_shape / f32(stride)) * f32(stride)).astype(np.int32)
+    if equal_dims:
+        pd = np.array([pd.max(), pd.max()], np.int32)
+    return new_shape, ratio, int(pd[0]), int(pd[1])
+
+
+def preprocess_image(image, jitter=None, min_side=800.0, max_side=1333.0, stride=128.0, equal_dims=True,
+                     flip=False, out=None, rng=None):
+    """Fused flip + resize_and_pad_image: returns (padded [Hp,Wp,C] fp32 on the GPU, new_shape, ratio).
+    out: an optional preallocated [Hp,Wp,C] fp32 slot (e.g. batch[i])."""
+    _lib.require_cuda()
+    img = torch.as_tensor(image).cuda()
+    if img.dtype not in (torch.uint8, torch.float32):
+        img = img.float()
+    img = img.contiguous()
+    H, W, C = int(img.shape[0]), int(img.shape[1]), int(img.shape[2])
+    new_shape, ratio, ph, pw = _plan(H, W, jitter, min_side, max_side, stride, equal_dims, rng)
+    oh, ow = int(new_shape[0]), int(new_shape[1])
+    if out is None:
+        out = torch.empty((ph, pw, C), dtype=torch.float32, device=img.device)
+    assert tuple(out.shape) == (ph, pw, C) and out.dtype == torch.float32 and out.is_contiguous()
+    _lib.call("cvl_resize_pad_normalize", _lib.ptr(img), 1 if img.dtype == torch.uint8 else 0, H, W, C,
+              1 if flip else 0, oh, ow, ph, pw, _lib.ptr(out), _lib.stream())
+    return out, new_shape, ratio
+
+
+def resize_and_pad_image(image, jitter=[640, 1024], min_side=800.0, max_side=1333.0, stride=128.0,
+                         equal_dims=True):
+    """data_preprocess.py:41-96 -> (image_padded, new_shape, ratio)."""
+    return preprocess_image(image, jitter, min_side, max_side, stride, equal_dims)
+
+
+def random_flip_horizontal(image, boxes, p_flip=0.5, rng=None):
+    """data_preprocess.py:24-39: with probability p_flip, flip the image left-right and map the
+    normalised boxes [x1, y1, x2, y2] -> [1 - x2, y1, 1 - x1, y2]."""
+    rng = rng if rng is not None else np.random.default_rng()
+    if rng.uniform() <= p_flip:
+        _lib.require_cuda()
+        img = torch.as_tensor(image).cuda()
+        b = np.asarray(boxes, f32)
+        return torch.flip(img, dims=[1]), np.stack([f32(1.0) - b[:, 2], b[:, 1], f32(1.0) - b[:, 0], b[:, 3]], -1)
+    return image, boxes

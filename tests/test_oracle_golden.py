@@ -122,3 +122,20 @@ def test_fcos_combined_nms_known_answer():
     np.testing.assert_array_equal(c, np.array([1, 0, 0, 1, 0, 0], np.float32))
     np.testing.assert_array_equal(b[:4], boxes[[4, 0, 3, 3]])
     assert not b[4:].any()
+
+
+def test_preprocess_resize_known_answers():
+    """TF2 bilinear resize restatement (data_preprocess.py:41-96; TF absent): equal size is the
+    identity, an exact 2x downscale is the mean of each 2x2 block, edges clamp."""
+    from oracle import preprocess_ref as pr
+    rng = np.random.default_rng(1)
+    a = rng.integers(0, 256, (6, 8, 3)).astype(np.float32)
+    np.testing.assert_array_equal(pr.resize_bilinear(a, 6, 8), a)
+    d = pr.resize_bilinear(a, 3, 4)
+    blocks = a.reshape(3, 2, 4, 2, 3).mean(axis=(1, 3))
+    np.testing.assert_allclose(d, blocks, rtol=0, atol=1e-4)
+    up = pr.resize_bilinear(a[:1, :1], 3, 3)
+    assert (up == a[0, 0]).all()
+    img, ns, r = pr.resize_and_pad_image(a.astype(np.uint8), 12.0, 100.0, 8.0, True)
+    assert img.shape == (16, 16, 3) and tuple(ns) == (12.0, 16.0) and r == np.float32(2.0)
+    assert not img[12:].any()
