@@ -32,6 +32,27 @@ def fcos_assign(boxes, nbox, img_dim, pad_hw, num_classes, strides=FCOS_STRIDES,
     return out, num_targets
 
 
+def fcos_center_assign(boxes, nbox, img_dim, pad_hw, num_classes, strides=FCOS_STRIDES, b_dim=FCOS_BOUNDS,
+                       center_only=False, out=None, num_targets=None):
+    """Batched FCOS-center targets (fcos_center.py:149-317) in cvl_fcos_assign's layout:
+    targets [B, P, 5+C] f32 level-major, num_targets [B,5] i32."""
+    _lib.require_cuda(boxes, nbox, img_dim)
+    assert boxes.dtype == torch.float32 and nbox.dtype == torch.int32 and img_dim.dtype == torch.float32
+    B, nmax = int(boxes.shape[0]), int(boxes.shape[1])
+    P = sum(h * w for h, w in fcos_level_shapes(pad_hw[0], pad_hw[1], strides))
+    if out is None:
+        out = torch.empty((B, P, 5 + num_classes), device=boxes.device, dtype=torch.float32)
+    if num_targets is None:
+        num_targets = torch.empty((B, 5), device=boxes.device, dtype=torch.int32)
+    st = (_lib.ctypes.c_int32 * 5)(*[int(s) for s in strides])
+    bd = (_lib.ctypes.c_float * 4)(*[float(x) for x in b_dim])
+    _lib.call("cvl_fcos_center_assign", ptr(boxes), ptr(nbox), ptr(img_dim), B, nmax, int(pad_hw[0]),
+              int(pad_hw[1]), int(num_classes), _lib.ctypes.cast(st, _lib.c_void_p),
+              _lib.ctypes.cast(bd, _lib.c_void_p), 1 if center_only else 0, ptr(out), ptr(num_targets),
+              _lib.stream())
+    return out, num_targets
+
+
 def fcos_loss(reg_pred, cls_pred, targets, num_classes, reg_type="l1", grad_scale=1.0,
               with_grad=True, grad_dtype=torch.float32, d_reg=None, d_cls=None):
     """Fused focal + smooth-L1/IoU + centerness forward and backward.

@@ -38,7 +38,7 @@ class SGD(object):
 class FCOSTrainer(GraphStepper):
     def __init__(self, net, batch_size, image_hw, n_max=16, init_lr=5e-4, min_lr=1e-5, decay_step=1000,
                  decay_rate=0.9, momentum=0.9, gradient_clip=1.0, reg_type="l1", weight_decay=0.0,
-                 world=1, use_graph=True, st_step=0):
+                 world=1, use_graph=True, st_step=0, targets="fcos", center_only=True):
         if weight_decay != 0.0:
             raise NotImplementedError("weight_decay > 0 (train_fcos.py:118-164) is not supported; the "
                                       "reference FCOS run uses weight_decay=0.0 (train_fcos.py:322)")
@@ -50,6 +50,10 @@ class FCOSTrainer(GraphStepper):
         self.momentum, self.clip = momentum, gradient_clip
         self.sched = (init_lr, min_lr, decay_rate, decay_step)
         self.reg_type = reg_type
+        # targets="center": fcos_center.format_data (train_fcos_center_voc.py:184-187, center_only)
+        if targets not in ("fcos", "center"):
+            raise ValueError("targets must be 'fcos' or 'center'")
+        self.target_kind, self.center_only = targets, center_only
         dev = net.device
         B, H, W = self.B, self.H, self.W
         _, _, self.P = net.layout(B, H, W)
@@ -69,8 +73,12 @@ class FCOSTrainer(GraphStepper):
 
     # ---- the two device phases -------------------------------------------------------------------
     def _fwd_bwd(self, hook=None):
-        tg, _ = ot.fcos_assign(self.boxes, self.nbox, self.img_dim, (self.H, self.W), self.C,
-                               out=self.targets, num_targets=self.ntgt)
+        if self.target_kind == "center":
+            tg, _ = ot.fcos_center_assign(self.boxes, self.nbox, self.img_dim, (self.H, self.W), self.C,
+                                          center_only=self.center_only, out=self.targets, num_targets=self.ntgt)
+        else:
+            tg, _ = ot.fcos_assign(self.boxes, self.nbox, self.img_dim, (self.H, self.W), self.C,
+                                   out=self.targets, num_targets=self.ntgt)
         reg, cls = self.net.forward(self.images)
         losses, _, _ = ot.fcos_loss(reg, cls, tg, self.C, reg_type=self.reg_type, grad_scale=1.0,
                                     d_reg=self.d_reg, d_cls=self.d_cls)

@@ -69,6 +69,16 @@ int cvl_fcos_decode(const float* pred, int ld, int S0, int S1, double stride, do
                     cvl_stream_t stream);
 
 
+/* FCOS/fcos_center.py:149-317 format_data (the variant of train_fcos_center_voc.py): level by
+ * max(h, w) px against b_dim [4] (HOST, reference default {32,64,128,256}); per level, boxes in
+ * ascending area paint the 3x3 cells around int(centre * img_dim / stride + 0.5) (only the centre
+ * cell when center_only): centerness = max(1 / 0.5 / 0.25), ltrb = last box's offsets about the
+ * cell centre (unclamped), class bits OR-ed.  Layout as cvl_fcos_assign: targets [B][P][5+C]
+ * level-major over (pad_h/stride) x (pad_w/stride) maps, num_targets [B][5]; strides [5] HOST. */
+int cvl_fcos_center_assign(const float* boxes, const int32_t* nbox, const float* img_dim, int B, int n_max,
+                           int pad_h, int pad_w, int num_classes, const int32_t* strides, const float* b_dim,
+                           int center_only, float* targets, int32_t* num_targets, cvl_stream_t stream);
+
 /* ------------------------------------------------------------------------------------------
  * Segmented implicit-GEMM convolution (bf16 MFMA, fp32 accumulate).  Replaces every Conv2D of
  * the reference graphs (Keras ResNet50 backbone; FCOS/fcos.py:49-101 FPN, towers and heads;

@@ -268,3 +268,53 @@ def image_detections(outputs, num_classes, center=False, iou_thresh=0.5, cls_thr
     if center:
         sc = sigmoid32(t[:, 4])[:, None] * sc
     return combined_non_max_suppression(t[:, :4], sc, max_detections, max_total_size, iou_thresh, cls_thresh)
+
+
+def center_format_data(gt_labels, img_dim, num_classes, img_pad=None, b_dim=None, strides=None,
+                       center_only=False):
+    """FCOS/fcos_center.py:149-317 (numpy >= 2 scalar promotion: python scalars join fp32 as fp32):
+    per level, boxes by max(h, w) px against b_dim, ascending area (stable: ties avoided, as Q1),
+    3x3 (or centre-only) cells around int(centre * img_dim / stride + 0.5); centerness max of
+    1 / 0.5 / 0.25, ltrb from the last box, class bits OR-ed -> (5 float64 maps, counts)."""
+    strides = list(STRIDES) if strides is None else list(strides)
+    b_dim = [32, 64, 128, 256] if b_dim is None else list(b_dim)
+    dim = np.asarray(img_dim, f32)
+    pad = dim if img_pad is None else np.asarray(img_pad, f32)
+    gt = np.asarray(gt_labels, f32).reshape(-1, 5)
+    gh, gw = gt[:, 2] * dim[0], gt[:, 3] * dim[1]
+    m = np.maximum(gw, gh)
+    outs, counts = [], []
+    for na, stride in enumerate(strides):
+        hr, wr = dim[0] / f32(stride), dim[1] / f32(stride)
+        hmax, wmax = int(pad[0] / f32(stride)), int(pad[1] / f32(stride))
+        out = np.zeros((hmax, wmax, num_classes + 5))
+        if na == 0:
+            idx = np.nonzero(m < b_dim[0])[0]
+        elif na == len(strides) - 1:
+            idx = np.nonzero(m >= b_dim[-1])[0]
+        else:
+            idx = np.nonzero((m >= b_dim[na - 1]) & (m < b_dim[na]))[0]
+        lab = gt[idx]
+        if len(lab) > 1:
+            lab = lab[np.argsort(np.multiply(lab[:, 2] * dim[0], lab[:, 3] * dim[1]), kind="stable")]
+        offs = [0] if center_only else [-1, 0, 1]
+        for t in lab:
+            c0 = (t[0] - f32(0.5) * t[2]) * dim[0] / f32(stride)
+            c1 = (t[1] - f32(0.5) * t[3]) * dim[1] / f32(stride)
+            c2 = (t[0] + f32(0.5) * t[2]) * dim[0] / f32(stride)
+            c3 = (t[1] + f32(0.5) * t[3]) * dim[1] / f32(stride)
+            yc, xc = int(t[0] * hr + f32(0.5)), int(t[1] * wr + f32(0.5))
+            for x in [xc - o for o in offs if xc - o >= 0]:
+                for y in [yc - o for o in offs if yc - o >= 0]:
+                    if y >= hmax or x >= wmax:
+                        continue
+                    yo, xo = yc - y, xc - x
+                    sc = 1.0 if (yo == 0 and xo == 0) else (0.25 if abs(yo) == 1 and abs(xo) == 1 else 0.5)
+                    if sc >= out[y, x, 4]:
+                        out[y, x, 4] = sc
+                    out[y, x, :4] = [f32(y + 0.5) - c0, (c2 - f32(y)) - f32(0.5),
+                                     f32(x + 0.5) - c1, (c3 - f32(x)) - f32(0.5)]
+                    out[y, x, 5 + int(t[4])] = 1.0
+        outs.append(out)
+        counts.append(len(lab))
+    return outs, counts

@@ -280,8 +280,32 @@ def work_retina_decode(out_path):
     np.savez_compressed(out_path, **arrays)
 
 
+def work_fcos_center(out_path):
+    """FCOS/fcos_center.py format_data (train_fcos_center_voc.py: center_only=True; also the 3x3
+    default) on synthetic VOC-shaped boxes with distinct areas."""
+    tf = _child_setup("FCOS")
+    import fcos_center as fc
+    rng = np.random.default_rng(123)
+    arrays = {}
+    C = 20
+    for i in range(24):
+        D = [512, 384, 640][i % 3]
+        boxes = synth_boxes(rng, float(D), float(D), C, lam=2.0 if i < 12 else 30.0, nmax=48, side_lo=4.0,
+                            side_hi=float(D) if i < 12 else 60.0, edge_frac=0.2)
+        img_dim = np.array([D, D], np.float32)
+        co = bool(i % 2)
+        outs, nt = fc.format_data(tf.constant(boxes), img_dim, C, img_pad=[D, D], center_only=co)
+        arrays["case_%d_boxes" % i] = boxes
+        arrays["case_%d_cfg" % i] = np.array([D, int(co)], np.int32)
+        arrays["case_%d_ntgt" % i] = np.array(nt, np.int32)
+        for l in range(5):
+            arrays["case_%d_L%d" % (i, l)] = np.asarray(outs[l]).astype(np.float32)
+    np.savez_compressed(out_path, **arrays)
+
+
 WORKERS = {"fcos": work_fcos, "retinanet": work_retina, "centernet": work_centernet,
-           "retina_decode": work_retina_decode}
+           "retina_decode": work_retina_decode,
+           "fcos_center": work_fcos_center}
 
 
 def main():

@@ -139,3 +139,25 @@ def test_preprocess_resize_known_answers():
     img, ns, r = pr.resize_and_pad_image(a.astype(np.uint8), 12.0, 100.0, 8.0, True)
     assert img.shape == (16, 16, 3) and tuple(ns) == (12.0, 16.0) and r == np.float32(2.0)
     assert not img[12:].any()
+
+
+def _center_cases(d):
+    i = 0
+    while "case_%d_cfg" % i in d:
+        D, co = (int(v) for v in d["case_%d_cfg" % i])
+        yield i, D, bool(co)
+        i += 1
+
+
+def test_fcos_center_format_data_bit_exact(golden):
+    """FCOS/fcos_center.py:149-317 restatement vs the reference's own outputs."""
+    d = golden("fcos_center")
+    overlaps = 0
+    for i, D, co in _center_cases(d):
+        outs, nt = fcos_ref.center_format_data(d["case_%d_boxes" % i], np.array([D, D], np.float32), 20,
+                                               img_pad=[D, D], center_only=co)
+        assert list(nt) == list(d["case_%d_ntgt" % i])
+        for l in range(5):
+            np.testing.assert_array_equal(outs[l].astype(np.float32), d["case_%d_L%d" % (i, l)])
+            overlaps += int((d["case_%d_L%d" % (i, l)][..., 5:].sum(-1) > 1).sum())
+    assert overlaps > 0
