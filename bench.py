@@ -70,21 +70,21 @@ def train_flops_per_image(H, W, C=NUM_CLASSES):
 
 
 def measure_tower_conv(net, B, H, W, iters=20):
-    """Dominant kernel: one shared-tower 3x3 conv over all five FPN levels (conv_igemm fwd),
-    timed with HIP events on the stream it is launched on.  Its input is the training step's own
-    cls-tower layer-1 activation (the last timed step's buffer), so the launch sees the data
-    the step's tower convs see (synthetic N(0, 0.25) only if the step left none)."""
+    """Dominant kernel: one tower layer's 3x3 conv forward, cls + reg towers over all five FPN
+    levels in ONE 10-segment launch (FPNDetector._pair_segs), timed with HIP events on the stream
+    it is launched on.  Its input is the training step's own layer-1 tower activations (the last
+    timed step's buffer), so the launch sees the data the step's tower convs see (synthetic
+    N(0, 0.25) only if the step left none)."""
     shapes, off, P = net.layout(B, H, W)
-    conv = net.cls_tower[1]
     dev = net.device
     saved = getattr(net, "_saved", None)
-    if saved and saved.get("towers") and tuple(saved["towers"][0][1].shape) == (B * P, 256):
-        src = saved["towers"][0][1]
+    if saved and saved.get("tower_bufs") and tuple(saved["tower_bufs"][0].shape) == (2 * B * P, 256):
+        src = saved["tower_bufs"][0]
     else:
         g = torch.Generator(device="cpu").manual_seed(5)
-        src = (torch.randn((B * P, 256), generator=g) * 0.5).to(torch.bfloat16).to(dev)
+        src = (torch.randn((2 * B * P, 256), generator=g) * 0.5).to(torch.bfloat16).to(dev)
     dst = torch.empty_like(src)
-    d = conv.fwd_desc(B, net._tower_segs(conv, B, shapes, off), ld_dst=256)
+    d = net.cls_tower[1].fwd_desc(B, net._pair_segs(1, B, shapes, off, P, fwd=True), ld_dst=256)
     for _ in range(3):
         nn.conv_igemm(d, src, dst)
     s = torch.cuda.current_stream()
@@ -95,12 +95,12 @@ def measure_tower_conv(net, B, H, W, iters=20):
     e1.record(s)
     e1.synchronize()
     ms = e0.elapsed_time(e1) / iters
-    M = B * P
+    M = 2 * B * P
     flops = 2.0 * M * 256 * 9 * 256
     return ms, flops
 
 
-PMC_FILE = "profiles/r01e_pmc_tower_conv.json"
+PMC_FILE = "profiles/r01h_pmc_tower_conv.json"
 
 
 def pmc_traffic():
@@ -113,7 +113,7 @@ def pmc_traffic():
 
 def tower_alg_bytes(B, net, H, W):
     P = net.layout(B, H, W)[2]
-    return 2 * (2 * B * P * 256) + 2 * 256 * 9 * 256
+    return 2 * (2 * (2 * B * P) * 256) + 2 * (2 * 256 * 9 * 256)   # src + dst bf16, 2 towers' weights
 
 
 def cpu_baseline(H, W, n_img=2):
@@ -302,8 +302,8 @@ def main():
                      "traffic_note": "HBM bytes per launch from rocprofv3 --pmc FETCH_SIZE (x2, gfx950) + "
                                      "WRITE_SIZE, separate passes (tools/pmc_tower.sh -> %s); algorithmic "
                                      "bytes per launch %d (src + dst bf16 + weights)" % (PMC_FILE, tower_alg_bytes(B, net, H, W)),
-                     "kernel": "conv_igemm_l_kernel<128, 4, 3, false, true> (fwd), shared FCOS tower 3x3 256->256 over all 5 levels "
-                               "(M=%d, N=256, K=2304), %.3f ms/launch" % (B * net.layout(B, H, W)[2], k_ms)},
+                     "kernel": "conv_igemm_l_kernel<256, 2, 2, false, true> (fwd, 256x256 tile), FCOS cls+reg tower layer 3x3 256->256 over all 5 levels, one 10-segment launch "
+                               "(M=%d, N=256, K=2304), %.3f ms/launch" % (2 * B * net.layout(B, H, W)[2], k_ms)},
         "model_flops_per_image": fl_img,
         "step_mfma_frac": round(img_s / world * fl_img / 1e12 / PEAK_BF16_TFLOPS, 4),
         "last_step_losses_cls_reg_cen": [round(x, 3) for x in losses],

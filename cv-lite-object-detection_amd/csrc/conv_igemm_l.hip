@@ -319,10 +319,12 @@ int cvl_conv_igemm_l(const cvl_conv_desc* d, int dst_up, int dst_w, const void* 
   if (cvl_env_flag("CVL_CONV_NO_L")) return -1;
   if (d->Cin % 64 != 0 || d->relu_in || d->dst_f32 || d->n_store % 8 || d->ld_dst % 8 || d->dst_coff % 8)
     return -1;
-  // 256-wide tiles for forward launches only (measured on the FCOS tower shape: forward +17 % per
-  // tile, data-gradient -35 %, tools/conv_ab.py)
+  // 256-wide tiles (forward and data-gradient) for launches with >= CVL_CONV_L256_MIN_TILES of
+  // them.  A single FCOS tower's dgrad (341 tiles) lost 35 % on them (tools/conv_ab.py); the
+  // paired cls+reg tower dgrad (682 tiles) gains: whole step 813 -> 827 img/s
+  // (tools/gpu_knob_sweep.sh).  CVL_CONV_NO_DGRAD_256=1 restores forward-only.
   const bool w256 = d->Npad % 256 == 0 && !cvl_env_flag("CVL_CONV_NO_256") &&
-                    (d->mode == CVL_CONV_FWD || cvl_env_flag("CVL_CONV_DGRAD_256"));
+                    (d->mode == CVL_CONV_FWD || !cvl_env_flag("CVL_CONV_NO_DGRAD_256"));
   const int bn = w256 ? 256 : (d->Npad % 128 == 0 ? 128 : (d->Npad % 64 == 0 ? 64 : 0));
   if (!bn) return -1;
   ConvArgs a;

@@ -46,6 +46,10 @@ class FCOSNet(FPNDetector):
         """grads = (d_reg, d_cls): bf16 [B, P, 32] (padding channels zero) from the fused loss."""
         d_reg, d_cls = grads
         dAs = []
+        # the two towers' input gradients as the halves of one buffer: the trunk then runs each
+        # tower layer's data gradient as one paired launch (FPNDetector.trunk_backward)
+        a0 = towers[0][0]
+        dA_pair = torch.empty((2,) + tuple(a0.shape), dtype=a0.dtype, device=a0.device)
         for heads, acts, dout in ((self.cls_heads, towers[0], d_cls), (self.reg_heads, towers[1], d_reg)):
             ld = int(dout.shape[-1])
             # heads: weight/bias grads per level, data grad for all levels in one launch
@@ -55,7 +59,7 @@ class FCOSNet(FPNDetector):
                                            dst_base=off[l], dst_img=P)], ld_dst=ld)
                 nn.conv_wgrad(d, acts[-1], dout, hd.dw)
                 nn.bias_grad(dout, ld, 0, hd.cout, off[l], P, h * w, B, hd.db)
-            dA = torch.empty_like(acts[0])
+            dA = dA_pair[len(dAs)]
             segs = [nn.seg(h, w, h, w, heads[l].wd, None, src_base=off[l], src_img=P, dst_base=B * off[l],
                            dst_img=h * w) for l, (h, w) in enumerate(shapes)]
             d = heads[0].dgrad_desc(B, segs, ld_dst=FPN_C)

@@ -11,6 +11,8 @@ MI355X layout decisions:
 * c7_3x3 reads relu(P6) through the conv's relu-on-load flag (fcos.py:70-72).
 * Subclasses add the per-level output heads (`_build_heads`, `_heads_forward`, `_heads_backward`).
 """
+import os
+
 import torch
 
 from . import ops_nn as nn
@@ -20,6 +22,10 @@ from .resnet import ResNet50
 FPN_C = 256
 STRIDES = (8, 16, 32, 64, 128)
 
+
+# CVL_TOWER_PAIR=0 runs the two towers as separate launches (A/B only; the paired 10-segment
+# launches are the default)
+PAIR_TOWERS = os.environ.get("CVL_TOWER_PAIR", "1") != "0"
 
 class FPNDetector(object):
     def _init_common(self, num_classes, backbone_model, device, seed):
@@ -97,6 +103,19 @@ class FPNDetector(object):
         return [nn.seg(h, w, h, w, conv.wf if wf else conv.wd, None, src_base=B * off[l], src_img=h * w,
                        dst_base=B * off[l], dst_img=h * w) for l, (h, w) in enumerate(shapes)]
 
+    def _pair_segs(self, i, B, shapes, off, P, fwd=True):
+        """Segments of tower layer i for BOTH towers (cls rows [0, B*P), reg rows [B*P, 2*B*P) of
+        the source and destination buffers).  Forward layer 0 reads the shared FPN buffer F
+        (both towers at offset 0); dgrad layers read/write the paired gradient buffers."""
+        segs = []
+        for t, tw in enumerate((self.cls_tower, self.reg_tower)):
+            conv = tw[i]
+            s_off = 0 if (fwd and i == 0) else t * B * P
+            segs += [nn.seg(h, w, h, w, conv.wf if fwd else conv.wd, None, src_base=s_off + B * off[l],
+                            src_img=h * w, dst_base=t * B * P + B * off[l], dst_img=h * w)
+                     for l, (h, w) in enumerate(shapes)]
+        return segs
+
     # ---- forward -------------------------------------------------------------------------------------
     def trunk_forward(self, x, train=True):
         """Backbone + FPN + both towers.  Returns the two towers' activation lists (each [F, a1..a4],
@@ -126,17 +145,28 @@ class FPNDetector(object):
                                             self.c7_3x3.bias_arg(), src_base=B * off[3], dst_base=B * off[4])],
                                  ld_dst=FPN_C, relu_in=True)
         nn.conv_igemm(d, F, F)                                      # P7 = conv(relu(P6))
-        towers = []
-        for tw in (self.cls_tower, self.reg_tower):
-            acts = [F]
-            for i, conv in enumerate(tw):
-                out = torch.empty((B * P, FPN_C), dtype=BF16, device=dev)
-                d = conv.fwd_desc(B, self._tower_segs(conv, B, shapes, off), ld_dst=FPN_C, relu_out=(i == 3))
-                nn.conv_igemm(d, acts[-1], out)
-                acts.append(out)
-            towers.append(acts)
+        # fcos.py:76-101: the cls and reg towers share geometry, so each tower layer is ONE launch
+        # of 10 segments (2 towers x 5 levels, each with its own weights) writing a [2*B*P, 256]
+        # buffer whose halves are the two towers' activations
+        towers = [[F], [F]]
+        bufs = []
+        src = F
+        for i in range(4):
+            out = torch.empty((2 * B * P, FPN_C), dtype=BF16, device=dev)
+            if PAIR_TOWERS:
+                d = self.cls_tower[i].fwd_desc(B, self._pair_segs(i, B, shapes, off, P, fwd=True), ld_dst=FPN_C,
+                                               relu_out=(i == 3))
+                nn.conv_igemm(d, src, out)
+            else:                                   # A/B reference: one launch per tower
+                for t, tw in enumerate((self.cls_tower, self.reg_tower)):
+                    d = tw[i].fwd_desc(B, self._tower_segs(tw[i], B, shapes, off), ld_dst=FPN_C, relu_out=(i == 3))
+                    nn.conv_igemm(d, towers[t][-1], out[t * B * P:(t + 1) * B * P])
+            towers[0].append(out[:B * P])
+            towers[1].append(out[B * P:])
+            bufs.append(out)
+            src = out
         self._saved = dict(bsv=bsv, C=(C3, C4, C5), l=(l3, l4, l5), p=(p3r, p4r), F=F, towers=towers,
-                           B=B, H=H, W=W, shapes=shapes, off=off, P=P)
+                           tower_bufs=bufs, B=B, H=H, W=W, shapes=shapes, off=off, P=P)
         return towers
 
     def forward(self, x, train=True):
@@ -178,18 +208,35 @@ class FPNDetector(object):
         dev = s["F"].device
         F, towers = s["F"], s["towers"]
         dF = torch.empty_like(F)
-        for ti, (tw, acts, dA) in enumerate(((self.cls_tower, towers[0], dA_top[0]),
-                                             (self.reg_tower, towers[1], dA_top[1]))):
-            nn.relu_backward(dA, acts[-1], dA)                      # the tower's final ReLU
-            for i in range(3, -1, -1):
+        dAs = list(dA_top)
+        BP = B * P
+        # the two towers' gradients are the halves of one [2*B*P, 256] buffer (the heads' backward
+        # allocates them so): then each tower layer's data gradient is ONE 10-segment launch
+        paired = PAIR_TOWERS and (dAs[1].data_ptr() - dAs[0].data_ptr() == BP * FPN_C * dAs[0].element_size()
+                  and dAs[0].is_contiguous() and dAs[1].is_contiguous())
+        for t in range(2):
+            nn.relu_backward(dAs[t], towers[t][-1], dAs[t])         # the tower's final ReLU
+        for i in range(3, -1, -1):
+            for t, tw in enumerate((self.cls_tower, self.reg_tower)):
                 conv = tw[i]
                 d = conv.fwd_desc(B, self._tower_segs(conv, B, shapes, off), ld_dst=FPN_C)
-                nn.conv_wgrad(d, acts[i], dA, conv.dw)
+                nn.conv_wgrad(d, towers[t][i], dAs[t], conv.dw)
+            if i > 0 and paired:
+                dd = self.cls_tower[i].dgrad_desc(B, self._pair_segs(i, B, shapes, off, P, fwd=False), ld_dst=FPN_C)
+                dst = torch.empty((2 * BP, FPN_C), dtype=BF16, device=dev)
+                src_all = torch.as_strided(dAs[0], (2 * BP, FPN_C), (FPN_C, 1))
+                nn.conv_igemm(dd, src_all, dst)
+                dAs = [dst[:BP], dst[BP:]]
+                continue
+            nxt = []
+            for t, tw in enumerate((self.cls_tower, self.reg_tower)):
+                conv = tw[i]
                 dd = conv.dgrad_desc(B, self._tower_segs(conv, B, shapes, off, wf=False), ld_dst=FPN_C,
-                                     beta=(1.0 if (i == 0 and ti == 1) else 0.0))
+                                     beta=(1.0 if (i == 0 and t == 1) else 0.0))
                 dst = dF if i == 0 else torch.empty_like(F)
-                nn.conv_igemm(dd, dA, dst)
-                dA = dst
+                nn.conv_igemm(dd, dAs[t], dst)
+                nxt.append(dst)
+            dAs = nxt
         hook("heads_towers")
         # ---- FPN backward (fcos.py:49-72) ----
         (C3, C4, C5) = s["C"]

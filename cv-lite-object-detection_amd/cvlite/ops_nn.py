@@ -10,6 +10,7 @@ from ._lib import ptr, stream
 c_int, c_int64, c_float, c_void_p = ctypes.c_int, ctypes.c_int64, ctypes.c_float, ctypes.c_void_p
 BF16 = torch.bfloat16
 FWD, DGRAD = 0, 1
+MAX_SEG = 10        # CVL_CONV_MAX_SEG (include/cvlite.h): cls + reg towers x 5 levels in one launch
 
 
 class ConvSeg(ctypes.Structure):
@@ -23,7 +24,7 @@ class ConvDesc(ctypes.Structure):
                 ("stride", c_int), ("pad_t", c_int), ("pad_l", c_int), ("Npad", c_int),
                 ("n_store", c_int), ("ld_dst", c_int), ("dst_coff", c_int), ("dst_f32", c_int),
                 ("relu_out", c_int), ("relu_in", c_int), ("beta", c_float), ("nseg", c_int),
-                ("seg", ConvSeg * 5)]
+                ("seg", ConvSeg * MAX_SEG)]
 
 
 def seg(Hr, Wr, Hs, Ws, w, bias=None, src_base=0, src_img=None, dst_base=0, dst_img=None):

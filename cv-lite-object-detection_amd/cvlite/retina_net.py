@@ -68,6 +68,10 @@ class RetinaNetNet(FPNDetector):
         """grads = (d_reg [B,P,reg_ld], d_cls [B,P,cls_ld]) bf16, padding channels zero."""
         d_reg, d_cls = grads
         dAs = []
+        # the two towers' input gradients as the halves of one buffer: the trunk then runs each
+        # tower layer's data gradient as one paired launch (FPNDetector.trunk_backward)
+        a0 = towers[0][0]
+        dA_pair = torch.empty((2,) + tuple(a0.shape), dtype=a0.dtype, device=a0.device)
         for heads, acts, dout in ((self.cls_heads, towers[0], d_cls), (self.reg_heads, towers[1], d_reg)):
             ld = int(dout.shape[-1])
             for l, (h, w) in enumerate(shapes):
@@ -76,7 +80,7 @@ class RetinaNetNet(FPNDetector):
                                            dst_base=off[l], dst_img=P)], ld_dst=ld)
                 nn.conv_wgrad(d, acts[-1], dout, hd.dw)
                 nn.bias_grad(dout, ld, 0, hd.cout, off[l], P, h * w, B, hd.db)
-            dA = torch.empty_like(acts[0])
+            dA = dA_pair[len(dAs)]
             segs = [nn.seg(h, w, h, w, heads[l].wd, None, src_base=off[l], src_img=P, dst_base=B * off[l],
                            dst_img=h * w) for l, (h, w) in enumerate(shapes)]
             d = heads[0].dgrad_desc(B, segs, ld_dst=FPN_C)

@@ -94,7 +94,7 @@ int cvl_fcos_center_assign(const float* boxes, const int32_t* nbox, const float*
  * bn_stats (nullable) receives per-(image, out channel) (sum, sumsq) in float64 (atomic adds;
  * zero it first), which requires H*W % 4 == 0.
  * ---------------------------------------------------------------------------------------- */
-#define CVL_CONV_MAX_SEG 5
+#define CVL_CONV_MAX_SEG 10
 enum { CVL_CONV_FWD = 0, CVL_CONV_DGRAD = 1 };
 
 typedef struct {
