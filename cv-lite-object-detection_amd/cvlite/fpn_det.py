@@ -26,6 +26,8 @@ STRIDES = (8, 16, 32, 64, 128)
 # CVL_TOWER_PAIR=0 runs the two towers as separate launches (A/B only; the paired 10-segment
 # launches are the default)
 PAIR_TOWERS = os.environ.get("CVL_TOWER_PAIR", "1") != "0"
+# CVL_FPN_FUSE=0 runs P3..P5's 3x3 output convs as separate launches (A/B only)
+FUSE_FPN = os.environ.get("CVL_FPN_FUSE", "1") != "0"
 
 class FPNDetector(object):
     def _init_common(self, num_classes, backbone_model, device, seed):
@@ -124,18 +126,34 @@ class FPNDetector(object):
         dev = x.device
         (C3, C4, C5), bsv = self.backbone.forward(x, train)
         (c3, H3, W3), (c4, H4, W4), (c5, H5, W5) = C3, C4, C5
+        # the three 3x3 output convs' sources (P3r, P4r, P5 = l5) share one buffer, so the convs run
+        # as ONE 3-segment launch (fcos.py:62-66: same geometry, own weights and biases)
+        n3, n4, n5 = B * H3 * W3, B * H4 * W4, B * H5 * W5
+        PR = torch.empty((n3 + n4 + n5, FPN_C), dtype=BF16, device=dev)
+        p3r = PR[:n3].view(B, H3, W3, FPN_C)
+        p4r = PR[n3:n3 + n4].view(B, H4, W4, FPN_C)
         l3, _, _ = self.c3_1x1.fwd(c3, B, H3, W3)
         l4, _, _ = self.c4_1x1.fwd(c4, B, H4, W4)
-        l5, _, _ = self.c5_1x1.fwd(c5, B, H5, W5)
-        p4r = torch.empty_like(l4)
+        l5, _, _ = self.c5_1x1.fwd(c5, B, H5, W5, out=PR[n3 + n4:].view(B, H5, W5, FPN_C))
         nn.upsample2x_add(l4, l5, p4r, B, H4, W4, FPN_C)          # fcos.py:57-58
-        p3r = torch.empty_like(l3)
         nn.upsample2x_add(l3, l4, p3r, B, H3, W3, FPN_C)          # fcos.py:59-60 (up2 of P4_1x1, Q13)
         shapes, off, P = self.layout(B, H, W)
         F = torch.empty((B * P, FPN_C), dtype=BF16, device=dev)
-        srcs = [(self.c3_3x3, p3r, H3, W3), (self.c4_3x3, p4r, H4, W4), (self.c5_3x3, l5, H5, W5),
-                (self.c6_3x3, c5, H5, W5)]
-        for l, (conv, src, h, w) in enumerate(srcs):
+        pr_base = (0, n3, n3 + n4)
+        if FUSE_FPN:
+            segs = [nn.seg(shapes[l][0], shapes[l][1], h, w, conv.wf, conv.bias_arg(), src_base=pr_base[l],
+                           dst_base=B * off[l])
+                    for l, (conv, h, w) in enumerate(((self.c3_3x3, H3, W3), (self.c4_3x3, H4, W4),
+                                                      (self.c5_3x3, H5, W5)))]
+            nn.conv_igemm(self.c3_3x3.fwd_desc(B, segs, ld_dst=FPN_C), PR, F)
+            srcs = [None, None, None, (self.c6_3x3, c5, H5, W5)]
+        else:
+            srcs = [(self.c3_3x3, p3r, H3, W3), (self.c4_3x3, p4r, H4, W4), (self.c5_3x3, l5, H5, W5),
+                    (self.c6_3x3, c5, H5, W5)]
+        for l, sc in enumerate(srcs):
+            if sc is None:
+                continue
+            conv, src, h, w = sc
             Ho, Wo = shapes[l]
             d = conv.fwd_desc(B, [nn.seg(Ho, Wo, h, w, conv.wf, conv.bias_arg(), dst_base=B * off[l])],
                               ld_dst=FPN_C)
@@ -165,7 +183,7 @@ class FPNDetector(object):
             towers[1].append(out[B * P:])
             bufs.append(out)
             src = out
-        self._saved = dict(bsv=bsv, C=(C3, C4, C5), l=(l3, l4, l5), p=(p3r, p4r), F=F, towers=towers,
+        self._saved = dict(bsv=bsv, C=(C3, C4, C5), l=(l3, l4, l5), p=(p3r, p4r), PR=PR, F=F, towers=towers,
                            tower_bufs=bufs, B=B, H=H, W=W, shapes=shapes, off=off, P=P)
         return towers
 
@@ -259,9 +277,13 @@ class FPNDetector(object):
         nn.relu_backward(dr6, P6, dP6, beta=1.0)
         # c6 (stride 2 on C5), c5_3x3, c4_3x3, c3_3x3: weight/bias grads and data grads
         dC5 = torch.empty_like(c5)
-        dl5 = torch.empty_like(l5)
-        dp4r = torch.empty_like(p4r)
-        dp3r = torch.empty_like(p3r)
+        n3, n4 = p3r.numel() // FPN_C, p4r.numel() // FPN_C
+        dPR = torch.empty_like(s["PR"])
+        dp3r = dPR[:n3].view(p3r.shape)
+        dp4r = dPR[n3:n3 + n4].view(p4r.shape)
+        dl5 = dPR[n3 + n4:].view(l5.shape)
+        pr_base = (0, n3, n3 + n4)
+        trio = []
         for l, (conv, src, h, w, dsrc) in enumerate(((self.c3_3x3, p3r, H3, W3, dp3r),
                                                      (self.c4_3x3, p4r, H4, W4, dp4r),
                                                      (self.c5_3x3, l5, H5, W5, dl5),
@@ -270,9 +292,14 @@ class FPNDetector(object):
             d = conv.fwd_desc(B, [nn.seg(Ho, Wo, h, w, conv.wf, None, dst_base=B * off[l])], ld_dst=FPN_C)
             nn.conv_wgrad(d, src, dF, conv.dw)
             nn.bias_grad(dF, FPN_C, 0, FPN_C, B * off[l], Ho * Wo, Ho * Wo, B, conv.db)
+            if FUSE_FPN and l < 3:            # P3..P5 data gradients: one 3-segment launch below
+                trio.append(nn.seg(h, w, Ho, Wo, conv.wd, None, src_base=B * off[l], dst_base=pr_base[l]))
+                continue
             dd = conv.dgrad_desc(B, [nn.seg(h, w, Ho, Wo, conv.wd, None, src_base=B * off[l])],
                                  ld_dst=conv.cin)
             nn.conv_igemm(dd, dF, dsrc)
+        if trio:
+            nn.conv_igemm(self.c3_3x3.dgrad_desc(B, trio, ld_dst=FPN_C), dF, dPR)
         # top-down adds: p4r = l4 + up(l5); p3r = l3 + up(l4)
         nn.upsample2x_backward(dp4r, dl5, B, H4, W4, FPN_C, beta=1.0)   # dl5 += up^T(dp4r)
         dl4 = dp4r
