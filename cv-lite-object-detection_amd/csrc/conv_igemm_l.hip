@@ -195,6 +195,32 @@ __global__ void __launch_bounds__(NT) conv_igemm_l_kernel(ConvArgs a) {
     const int n = n0 + wn * WN + j * 16 + lr;
     bcol[j] = (S.bias && n < a.n_store) ? S.bias[n] : 0.f;
   }
+  if (a.dst_f32) {
+    // fp32 destination (the head outputs the fused losses read): +bias, ReLU, unrounded 4-byte
+    // stores straight from the accumulators (16 lanes = 64 contiguous bytes per row), as the
+    // 128-row kernel does; no statistics (the host never pairs them with an fp32 output).  All
+    // ring DMA has drained: the last K step waited for vmcnt 0 and issued nothing.
+    float* dstf = reinterpret_cast<float*>(a.dst);
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int ml = mloc0 + wm * WM + i * 16 + lg * 4 + e;
+        if (ml >= S.rows) continue;
+        const int img = ml / HWr, q = ml - img * HWr;
+        const long drow = conv_dst_row(a, S, img, q);
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+          const int n = n0 + wn * WN + j * 16 + lr;
+          if (n >= a.n_store) continue;
+          float v = acc[i][j][e] + bcol[j];
+          if (a.relu_out) v = v > 0.f ? v : 0.f;
+          float* pd = dstf + drow * a.ld_dst + a.dst_coff + n;
+          *pd = a.beta != 0.f ? v + a.beta * *pd : v;
+        }
+      }
+    return;
+  }
 #pragma unroll
   for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -317,7 +343,8 @@ __global__ void __launch_bounds__(NT) conv_igemm_l_kernel(ConvArgs a) {
 int cvl_conv_igemm_l(const cvl_conv_desc* d, int dst_up, int dst_w, const void* src, void* dst, double* bn_stats,
                      hipStream_t s) {
   if (cvl_env_flag("CVL_CONV_NO_L")) return -1;
-  if (d->Cin % 64 != 0 || d->relu_in || d->dst_f32 || d->n_store % 8 || d->ld_dst % 8 || d->dst_coff % 8)
+  if (d->Cin % 64 != 0 || d->relu_in || d->n_store % 8 || (d->dst_f32 && bn_stats) ||
+      (!d->dst_f32 && (d->ld_dst % 8 || d->dst_coff % 8)) || (d->dst_f32 && cvl_env_flag("CVL_CONV_L_NO_F32")))
     return -1;
   // 256-wide tiles (forward and data-gradient) for launches with >= CVL_CONV_L256_MIN_TILES of
   // them.  A single FCOS tower's dgrad (341 tiles) lost 35 % on them (tools/conv_ab.py); the
