@@ -9,6 +9,9 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 constexpr int kMaxSeg = CVL_CONV_MAX_SEG;
 
+// kernel variant of the last cvl_conv_igemm call on this host thread (cvl_conv_igemm_last_kernel)
+extern thread_local int g_cvl_conv_last_kernel;
+
 // Workgroups are dispatched round-robin over the 8 XCDs (hardware id b runs on XCD b % 8).  This
 // bijective remap gives consecutive LOGICAL ids to the workgroups of one XCD, so tiles that read
 // the same rows (the N tiles of an M tile, the (co, k) tiles of one reduction chunk) share that

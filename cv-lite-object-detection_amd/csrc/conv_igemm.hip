@@ -535,6 +535,22 @@ __global__ void zero_gaps_kernel(void* dst, int is_f32, long dst_base, long dst_
   }
 }
 
+thread_local int g_cvl_conv_last_kernel = CVL_CK_NONE;
+
+extern "C" int cvl_conv_igemm_last_kernel(void) { return g_cvl_conv_last_kernel; }
+
+extern "C" const char* cvl_conv_kernel_name(int code) {
+  switch (code) {
+    case CVL_CK_BASE: return "conv_igemm_kernel (128-row)";
+    case CVL_CK_BASE_SPLITK: return "conv_igemm_kernel (128-row, split-K)";
+    case CVL_CK_L64: return "conv_igemm_l_kernel<64> (256x64)";
+    case CVL_CK_L128: return "conv_igemm_l_kernel<128> (256x128)";
+    case CVL_CK_L256: return "conv_igemm_l_kernel<256> (256x256)";
+    case CVL_CK_X256: return "conv_igemm_x_kernel (256x256, 8-phase)";
+    default: return "none";
+  }
+}
+
 extern "C" size_t cvl_conv_igemm_workspace_size(const cvl_conv_desc* d) {
   cvl_conv_desc dd;
   int up = 1, upw = 0;
@@ -548,6 +564,7 @@ extern "C" size_t cvl_conv_igemm_workspace_size(const cvl_conv_desc* d) {
 extern "C" int cvl_conv_igemm(const cvl_conv_desc* d, const void* src, void* dst, double* bn_stats,
                               void* workspace, size_t workspace_bytes, cvl_stream_t stream) {
   hipStream_t s = (hipStream_t)stream;
+  g_cvl_conv_last_kernel = CVL_CK_NONE;
   cvl_conv_desc dd;
   int up = 1, upw = 0;
   if (s2dgrad_transform(d, &dd, &up, &upw)) {
@@ -594,6 +611,7 @@ extern "C" int cvl_conv_igemm(const cvl_conv_desc* d, const void* src, void* dst
     a.slab = reinterpret_cast<float*>(workspace);
   }
   const bool dg = d->mode == CVL_CONV_DGRAD;
+  g_cvl_conv_last_kernel = a.splits > 1 ? CVL_CK_BASE_SPLITK : CVL_CK_BASE;
   if (bn == 128) return launch_bn<128>(a, dg, s);
   if (bn == 64) return launch_bn<64>(a, dg, s);
   return launch_bn<32>(a, dg, s);

@@ -385,6 +385,7 @@ int cvl_conv_igemm_l(const cvl_conv_desc* d, int dst_up, int dst_w, const void* 
       else hipLaunchKernelGGL((conv_igemm_l_kernel<BN_, WGM_, NST_, false, false>), grid, dim3(NT), 0, s, a);      \
     }                                                                                                          \
   } while (0)
+  g_cvl_conv_last_kernel = use_bn == 256 ? CVL_CK_L256 : (use_bn == 128 ? CVL_CK_L128 : CVL_CK_L64);
   if (use_bn == 256) CVL_L_LAUNCH(256, 2, 2);
   else if (use_bn == 128) CVL_L_LAUNCH(128, 4, 3);
   else CVL_L_LAUNCH(64, 4, 3);

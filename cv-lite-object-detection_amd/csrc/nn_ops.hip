@@ -801,6 +801,31 @@ __global__ void sgd_kernel(float* w, const float* g, float* v, long n, const flo
   }
 }
 
+// l2_params_reg = sum_v sqrt(sum(tf.nn.l2_loss(v))) = sum_v sqrt(0.5 * sum(v^2))  (train_fcos.py:118-120):
+// one block per tensor writes its term, then one block sums the terms in tensor order (deterministic)
+__global__ void __launch_bounds__(NT) l2_terms_kernel(const float* __restrict__ flat, const int64_t* __restrict__ off,
+                                                      const int64_t* __restrict__ cnt, float* __restrict__ term) {
+  const int64_t o = off[blockIdx.x], n = cnt[blockIdx.x];
+  double s = 0.0;
+  for (int64_t i = threadIdx.x; i < n; i += NT) { const double v = flat[o + i]; s += v * v; }
+  s = warp_sum_d(s);
+  __shared__ double red[NT / 64];
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double t = 0.0;
+    for (int k = 0; k < NT / 64; ++k) t += red[k];
+    term[blockIdx.x] = sqrtf((float)(0.5 * t));
+  }
+}
+
+__global__ void l2_sum_kernel(const float* __restrict__ term, int n, float* __restrict__ out) {
+  if (threadIdx.x != 0) return;
+  double t = 0.0;
+  for (int i = 0; i < n; ++i) t += term[i];
+  *out = (float)t;
+}
+
 // lr = max(init * rate^floor(step / decay_step), min_lr); step += 1   (train_fcos.py:108-110)
 __global__ void lr_schedule_kernel(int* step, float* lr, double init_lr, double min_lr, double rate,
                                    int decay_step) {
@@ -1076,6 +1101,14 @@ extern "C" int cvl_sgd_clip_update(float* w, const float* g, float* v, int64_t n
   hipLaunchKernelGGL(sumsq_kernel, dim3(grid_for(n, NT * 8, 2048)), dim3(NT), 0, S_, g, (long)n, sumsq_ws);
   hipLaunchKernelGGL(sgd_kernel, dim3(grid_for(n, NT * 4, 4096)), dim3(NT), 0, S_, w, g, v, (long)n, lr_dev,
                      momentum, inv_bs, clip, (const double*)sumsq_ws);
+  return cvl_launch_status();
+}
+
+extern "C" int cvl_l2_params_reg(const float* flat, const int64_t* offsets, const int64_t* sizes, int n_tensors,
+                                 float* terms, float* out, cvl_stream_t stream) {
+  CVL_CHECK_ARG(flat && offsets && sizes && n_tensors > 0 && terms && out);
+  hipLaunchKernelGGL(l2_terms_kernel, dim3(n_tensors), dim3(NT), 0, S_, flat, offsets, sizes, terms);
+  hipLaunchKernelGGL(l2_sum_kernel, dim3(1), dim3(64), 0, S_, (const float*)terms, n_tensors, out);
   return cvl_launch_status();
 }
 

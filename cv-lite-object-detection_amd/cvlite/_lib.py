@@ -26,6 +26,8 @@ SIGNATURES = {
     "cvl_fcos_decode": (c_int, [P, c_int, c_int, c_int, ctypes.c_double, P, P]),
     "cvl_conv_igemm_workspace_size": (c_size_t, [P]),
     "cvl_conv_igemm": (c_int, [P, P, P, P, P, c_size_t, P]),
+    "cvl_conv_igemm_last_kernel": (c_int, []),
+    "cvl_conv_kernel_name": (ctypes.c_char_p, [c_int]),
     "cvl_conv_wgrad_workspace_size": (c_size_t, [P]),
     "cvl_conv_wgrad": (c_int, [P, P, P, P, c_float, P, c_size_t, P]),
     "cvl_pack_conv_weights": (c_int, [P, c_int, c_int, c_int, c_int, c_int, c_int, P, c_int, c_int, P, P]),
@@ -48,6 +50,7 @@ SIGNATURES = {
                               P, c_float, P]),
     "cvl_sgd_clip_update": (c_int, [P, P, P, ctypes.c_int64, P, c_float, c_float, c_float, P, P]),
     "cvl_lr_schedule": (c_int, [P, P, ctypes.c_double, ctypes.c_double, ctypes.c_double, c_int, P]),
+    "cvl_l2_params_reg": (c_int, [P, P, P, c_int, P, P, P]),
     "cvl_select_first_nonzero": (c_int, [P, c_int, c_int, P, P, P]),
     "cvl_gather_rows": (c_int, [P, ctypes.c_int64, P, c_int, P, P]),
     "cvl_retina_assign": (c_int, [P, P, P, c_int, c_int, c_int, c_int, P, c_int, P, c_float, P, P, P]),

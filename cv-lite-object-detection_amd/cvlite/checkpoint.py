@@ -17,9 +17,15 @@ import numpy as np
 import torch
 
 
-def _bns(net):
+def model_bns(net):
+    """Every BatchNorm layer (with moving statistics) of a cvlite network."""
+    if hasattr(net, "bns"):
+        return list(net.bns())
     bb = getattr(net, "backbone", None)
     return list(bb.bns()) if bb is not None and hasattr(bb, "bns") else []
+
+
+_bns = model_bns
 
 
 def _split_map(net):
@@ -102,3 +108,148 @@ def load_keras_weights(net, weights, strict=True):
 def import_keras_weights(net, path, strict=True):
     with np.load(path, allow_pickle=False) as z:
         return load_keras_weights(net, {k: z[k] for k in z.files}, strict=strict)
+
+
+# -------------------------------------------------------------------------------------------------
+# Training-state checkpoints: the tf.train.Checkpoint / tf.train.CheckpointManager pair the
+# reference loops use for resume (FCOS/train_fcos.py:289-310, RetinaNet/train_retinanet_coco.py,
+# CenterNet/train_hourglass_voc.py).  A checkpoint holds the step counter, every parameter, the
+# optimizer slots (SGD momentum lives in the store, Adam m / v / iterations in the optimizer) and
+# the BatchNorm moving statistics; the parameter names are checked against the current layout on
+# restore.  Files are torch archives of plain tensors (read back with weights_only=True).
+# -------------------------------------------------------------------------------------------------
+def _net_of(obj):
+    """The cvlite network behind a model object (FCOSModel.net, RetinaNet.model, or the net)."""
+    for attr in ("net", "model"):
+        inner = getattr(obj, attr, None)
+        if inner is not None and hasattr(inner, "store"):
+            return inner
+    return obj if hasattr(obj, "store") else None
+
+
+def net_state(net):
+    st = net.store
+    return {"params": st.flat.detach().cpu().clone(), "momentum": st.mom.detach().cpu().clone(),
+            "names": [[k, int(o), int(n)] for k, (o, n, _) in st.offsets.items()],
+            "bn": {bn.name: (bn.run_mean.detach().cpu().clone(), bn.run_var.detach().cpu().clone())
+                   for bn in model_bns(net)}}
+
+
+def load_net_state(net, s):
+    st = net.store
+    names = [[k, int(o), int(n)] for k, (o, n, _) in st.offsets.items()]
+    if [list(x) for x in s["names"]] != names:
+        raise ValueError("checkpoint parameter layout does not match this model")
+    st.flat.copy_(s["params"].to(st.flat.device))
+    st.mom.copy_(s["momentum"].to(st.flat.device))
+    for bn in model_bns(net):
+        m, v = s["bn"][bn.name]
+        bn.run_mean.copy_(m)
+        bn.run_var.copy_(v)
+    net.pack()
+
+
+def _opt_state(opt):
+    if getattr(opt, "m", None) is not None:            # train_centernet.Adam once bound
+        return {"m": opt.m.detach().cpu().clone(), "v": opt.v.detach().cpu().clone(),
+                "iterations": opt.iterations.detach().cpu().clone()}
+    return {}
+
+
+def _load_opt_state(opt, s):
+    if s and getattr(opt, "m", None) is not None:
+        opt.m.copy_(s["m"])
+        opt.v.copy_(s["v"])
+        opt.iterations.copy_(s["iterations"])
+
+
+class Variable(object):
+    """tf.Variable stand-in for the integer step counter (`ckpt.step.assign_add(1)`)."""
+
+    def __init__(self, value=0):
+        self.value = int(value)
+
+    def assign_add(self, n):
+        self.value += int(n)
+        return self
+
+    def assign(self, v):
+        self.value = int(v)
+        return self
+
+    def numpy(self):
+        return np.int64(self.value)
+
+
+class Checkpoint(object):
+    """tf.train.Checkpoint(step=tf.Variable(0), <model>=..., <optimizer>=...)."""
+
+    def __init__(self, step=None, **objects):
+        self.step = step if isinstance(step, Variable) else Variable(0 if step is None else step)
+        self.objects = objects
+
+    def state(self):
+        out = {"step": self.step.value, "objects": {}}
+        for name, obj in self.objects.items():
+            net = _net_of(obj)
+            out["objects"][name] = net_state(net) if net is not None else _opt_state(obj)
+        return out
+
+    def write(self, path):
+        torch.save(self.state(), path)
+        return path
+
+    def restore(self, path):
+        if path is None:
+            return self
+        s = torch.load(path, weights_only=True)
+        self.step.assign(int(s["step"]))
+        for name, obj in self.objects.items():
+            if name not in s["objects"]:
+                raise KeyError("checkpoint has no object %r" % name)
+            net = _net_of(obj)
+            if net is not None:
+                load_net_state(net, s["objects"][name])
+            else:
+                _load_opt_state(obj, s["objects"][name])
+        return self
+
+
+class CheckpointManager(object):
+    """tf.train.CheckpointManager(checkpoint, directory, max_to_keep): save() writes
+    `<directory>/ckpt-<n>.pt` and keeps the newest max_to_keep; latest_checkpoint is the newest."""
+
+    def __init__(self, checkpoint, directory, max_to_keep=1):
+        import os
+        self.checkpoint, self.directory, self.max_to_keep = checkpoint, directory, int(max_to_keep)
+        os.makedirs(directory, exist_ok=True)
+        self._counter = max([n for n, _ in self._existing()] or [0])
+
+    def _existing(self):
+        import os
+        import re
+        out = []
+        for f in os.listdir(self.directory):
+            m = re.match(r"ckpt-(\d+)\.pt$", f)
+            if m:
+                out.append((int(m.group(1)), os.path.join(self.directory, f)))
+        return sorted(out)
+
+    @property
+    def checkpoints(self):
+        return [p for _, p in self._existing()]
+
+    @property
+    def latest_checkpoint(self):
+        ex = self._existing()
+        return ex[-1][1] if ex else None
+
+    def save(self):
+        import os
+        self._counter += 1
+        path = os.path.join(self.directory, "ckpt-%d.pt" % self._counter)
+        self.checkpoint.write(path)
+        ex = self._existing()
+        for _, p in ex[:max(0, len(ex) - self.max_to_keep)]:
+            os.remove(p)
+        return path

@@ -242,6 +242,27 @@ class BatchNorm(object):
         self.run_mean = torch.zeros(self.c, dtype=torch.float32, device=device)
         self.run_var = torch.ones(self.c, dtype=torch.float32, device=device)
 
+    def moving_mean_rstd(self, B):
+        """Keras training=False: normalise with the moving statistics (same for every image),
+        as [B][C][2] (mean, rstd) for cvl_bn_apply."""
+        mr = torch.empty((B, self.c, 2), dtype=torch.float32, device=self.run_mean.device)
+        mr[:, :, 0] = self.run_mean
+        mr[:, :, 1] = torch.rsqrt(self.run_var + self.eps)
+        return mr
+
+    def normalize(self, z, stats, B, HW, relu, residual=None, train=True):
+        """y = BN(z) (+ residual) (ReLU): training mode from the conv's fused per-image statistics
+        (and the moving-average update), inference mode from the moving statistics."""
+        y = torch.empty_like(z)
+        if train:
+            mr = torch.empty((B, self.c, 2), dtype=torch.float32, device=z.device)
+            nn.bn_finalize_apply(stats, mr, self.run_mean, self.run_var, z, self.gamma, self.beta, residual, y, B,
+                                 HW, self.c, relu, self.eps, self.momentum)
+        else:
+            mr = self.moving_mean_rstd(B)
+            nn.bn_apply(z, mr, self.gamma, self.beta, residual, y, B, HW, self.c, relu)
+        return y, mr
+
     @property
     def gamma(self):
         return self.store.p(self.gname)
@@ -263,14 +284,12 @@ class ConvBN(object):
     def forward(self, x, B, H, W, relu=True, residual=None, train=True, arena=None):
         c = self.conv.cout
         Ho, Wo, _, _ = self.conv.out_hw(H, W)
-        stats = arena.take(B, c) if arena is not None else torch.zeros((B, c, 2), dtype=torch.float64,
-                                                                         device=x.device)
+        stats = None
+        if train:
+            stats = arena.take(B, c) if arena is not None else torch.zeros((B, c, 2), dtype=torch.float64,
+                                                                             device=x.device)
         z, _, _ = self.conv.fwd(x, B, H, W, stats=stats)
-        mr = torch.empty((B, c, 2), dtype=torch.float32, device=x.device)
-        y = torch.empty_like(z)
-        nn.bn_finalize_apply(stats, mr, self.bn.run_mean if train else None, self.bn.run_var if train else None,
-                             z, self.bn.gamma, self.bn.beta, residual, y, B, Ho * Wo, c, relu, self.bn.eps,
-                             self.bn.momentum)
+        y, mr = self.bn.normalize(z, stats, B, Ho * Wo, relu, residual=residual, train=train)
         return y, (x, z, y, mr, B, H, W, Ho, Wo, relu)
 
     def backward(self, dy, saved, dx_out=None, dx_beta=0.0, g_out=None, need_dx=True):

@@ -185,6 +185,26 @@ def lr_schedule(step_dev, lr_dev, init_lr, min_lr, decay_rate, decay_step):
               float(decay_rate), int(decay_step), stream())
 
 
+class L2Reg(object):
+    """Device l2_params_reg of a ParamStore (train_fcos.py:118-120): sum over the trainable
+    tensors of sqrt(tf.nn.l2_loss(v)); graph-capturable, result in self.out (device float)."""
+
+    def __init__(self, store):
+        dev = store.flat.device
+        offs = [o for (o, n, _) in store.offsets.values()]
+        cnts = [n for (o, n, _) in store.offsets.values()]
+        self.store = store
+        self.offs = torch.tensor(offs, dtype=torch.int64, device=dev)
+        self.cnts = torch.tensor(cnts, dtype=torch.int64, device=dev)
+        self.terms = torch.zeros(len(offs), dtype=torch.float32, device=dev)
+        self.out = torch.zeros(1, dtype=torch.float32, device=dev)
+
+    def run(self):
+        _lib.call("cvl_l2_params_reg", ptr(self.store.flat), ptr(self.offs), ptr(self.cnts), int(self.offs.numel()),
+                  ptr(self.terms), ptr(self.out), stream())
+        return self.out
+
+
 def select_first_nonzero(counts, k, idx, weight):
     _lib.call("cvl_select_first_nonzero", ptr(counts), int(counts.numel()), int(k), ptr(idx), ptr(weight), stream())
 

@@ -49,15 +49,13 @@ class Stem(object):
         Ho, Wo, pt, pl = self.conv.out_hw(H, W)
         A = torch.empty((B * Ho * Wo, STEM_KP), dtype=BF16, device=x.device)
         nn.im2col(x, STEM_K, STEM_K, 2, pt, pl, Ho, Wo, STEM_KP, A)
-        stats = arena.take(B, 64) if arena is not None else torch.zeros((B, 64, 2), dtype=torch.float64,
-                                                                          device=x.device)
+        stats = None
+        if train:
+            stats = arena.take(B, 64) if arena is not None else torch.zeros((B, 64, 2), dtype=torch.float64,
+                                                                              device=x.device)
         z = torch.empty((B, Ho, Wo, 64), dtype=BF16, device=x.device)
         nn.conv_igemm(self._desc(B, Ho, Wo), A, z, stats)
-        mr = torch.empty((B, 64, 2), dtype=torch.float32, device=x.device)
-        y = torch.empty_like(z)
-        nn.bn_finalize_apply(stats, mr, self.bn.run_mean if train else None, self.bn.run_var if train else None,
-                             z, self.bn.gamma, self.bn.beta, None, y, B, Ho * Wo, 64, True, self.bn.eps,
-                             self.bn.momentum)
+        y, mr = self.bn.normalize(z, stats, B, Ho * Wo, True, train=train)
         Hp, Wp = (Ho + 2 - 3) // 2 + 1, (Wo + 2 - 3) // 2 + 1
         p = torch.empty((B, Hp, Wp, 64), dtype=BF16, device=x.device)
         arg = torch.empty((B, Hp, Wp, 64), dtype=torch.uint8, device=x.device)

@@ -31,6 +31,11 @@ class GraphStepper(object):
     def capture(self):
         """Warm the allocator on a side stream, then capture fwd+bwd (in hook-split segments when
         data-parallel, sharing one memory pool) and the update into HIP graphs."""
+        from .checkpoint import model_bns
+        # the warm-up forwards must not move the BatchNorm moving statistics: snapshot / restore
+        # (the captured graph itself applies exactly one EMA update per replayed step)
+        bns = model_bns(self.net)
+        snap = [(bn.run_mean.clone(), bn.run_var.clone()) for bn in bns]
         s = torch.cuda.Stream()
         s.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(s):
@@ -38,6 +43,9 @@ class GraphStepper(object):
                 self._fwd_bwd(None)
         torch.cuda.current_stream().wait_stream(s)
         torch.cuda.synchronize()
+        for bn, (m, v) in zip(bns, snap):
+            bn.run_mean.copy_(m)
+            bn.run_var.copy_(v)
         pool = torch.cuda.graph_pool_handle()
         segs = []
         cap = torch.cuda.Stream()

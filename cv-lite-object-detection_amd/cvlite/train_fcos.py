@@ -39,10 +39,13 @@ class FCOSTrainer(GraphStepper):
     def __init__(self, net, batch_size, image_hw, n_max=16, init_lr=5e-4, min_lr=1e-5, decay_step=1000,
                  decay_rate=0.9, momentum=0.9, gradient_clip=1.0, reg_type="l1", weight_decay=0.0,
                  world=1, use_graph=True, st_step=0, targets="fcos", center_only=True):
-        if weight_decay != 0.0:
-            raise NotImplementedError("weight_decay > 0 (train_fcos.py:118-164) is not supported; the "
-                                      "reference FCOS run uses weight_decay=0.0 (train_fcos.py:322)")
         self.net = net
+        # weight_decay * l2_params_reg (train_fcos.py:118-120, 160-164): the reference computes the
+        # regulariser OUTSIDE the GradientTape, so it is added to each image's reported loss and
+        # contributes nothing to the gradient; it is evaluated on the device at the start of the
+        # step (before the update), as the reference does
+        self.weight_decay = float(weight_decay)
+        self.l2 = nn.L2Reg(net.store) if self.weight_decay > 0.0 else None
         self.B = batch_size
         self.H, self.W = image_hw
         self.C = net.C
@@ -60,7 +63,9 @@ class FCOSTrainer(GraphStepper):
         self.images = torch.zeros((B, H, W, 3), dtype=torch.float32, device=dev)
         self.boxes = torch.zeros((B, n_max, 5), dtype=torch.float32, device=dev)
         self.nbox = torch.zeros((B,), dtype=torch.int32, device=dev)
-        self.img_dim = torch.tensor([[float(H), float(W)]] * B, dtype=torch.float32, device=dev)
+        self.img_dim_pad = torch.tensor([[float(H), float(W)]] * B, dtype=torch.float32, device=dev)
+        self.img_dim = self.img_dim_pad.clone()
+        self._custom_dim = False
         self.targets = torch.zeros((B, self.P, 5 + self.C), dtype=torch.float32, device=dev)
         self.ntgt = torch.zeros((B, 5), dtype=torch.int32, device=dev)
         self.d_reg = torch.zeros((B, self.P, 32), dtype=BF16, device=dev)
@@ -73,6 +78,8 @@ class FCOSTrainer(GraphStepper):
 
     # ---- the two device phases -------------------------------------------------------------------
     def _fwd_bwd(self, hook=None):
+        if self.l2 is not None:
+            self.l2.run()
         if self.target_kind == "center":
             tg, _ = ot.fcos_center_assign(self.boxes, self.nbox, self.img_dim, (self.H, self.W), self.C,
                                           center_only=self.center_only, out=self.targets, num_targets=self.ntgt)
@@ -80,6 +87,7 @@ class FCOSTrainer(GraphStepper):
             tg, _ = ot.fcos_assign(self.boxes, self.nbox, self.img_dim, (self.H, self.W), self.C,
                                    out=self.targets, num_targets=self.ntgt)
         reg, cls = self.net.forward(self.images)
+        self.outputs = (reg, cls)                 # head outputs of the last step (graph memory)
         losses, _, _ = ot.fcos_loss(reg, cls, tg, self.C, reg_type=self.reg_type, grad_scale=1.0,
                                     d_reg=self.d_reg, d_cls=self.d_cls)
         self.losses.copy_(losses)
@@ -93,11 +101,25 @@ class FCOSTrainer(GraphStepper):
                            self.clip, ws=self.sumsq)
         self.net.pack()
 
-    def load_batch(self, images, boxes, nbox):
-        """Device-to-device copy of one batch into the static input buffers."""
+    def load_batch(self, images, boxes, nbox, img_dim=None):
+        """Device-to-device copy of one batch into the static input buffers.  img_dim [B,2]: the
+        unpadded resized [h, w] of each image (data_preprocess.resize_and_pad_image's new_shape,
+        passed to format_data as img_dim while img_pad is the padded batch size,
+        train_fcos.py:131-143); None = the padded size."""
         self.images.copy_(images, non_blocking=True)
         self.boxes.copy_(boxes, non_blocking=True)
         self.nbox.copy_(nbox, non_blocking=True)
+        if img_dim is not None:
+            self.img_dim.copy_(torch.as_tensor(img_dim, dtype=torch.float32).reshape(self.B, 2), non_blocking=True)
+            self._custom_dim = True
+        elif self._custom_dim:
+            self.img_dim.copy_(self.img_dim_pad)
+            self._custom_dim = False
+
+    @property
+    def l2_params_reg(self):
+        """The device l2_params_reg of the last step (None without weight decay)."""
+        return None if self.l2 is None else self.l2.out
 
 
 
@@ -133,89 +155,123 @@ def synthetic_batch(B, H, W, n_classes, n_max=16, seed=1234, device="cuda"):
 # -------------------------------------------------------------------------------------------------
 # reference-shaped training loop (FCOS/train_fcos.py:87-251)
 # -------------------------------------------------------------------------------------------------
+def _batch_from_samples(train_data, idx, n_max):
+    """Host batch from pre-processed samples dict(image=[Hp,Wp,3], bbox=[N,4] (yc,xc,h,w)
+    normalised, label=[N], optional img_dim=[h,w] unpadded resized size)."""
+    bs = len(idx)
+    imgs = np.stack([np.asarray(train_data[i]["image"], np.float32) for i in idx])
+    bx = np.zeros((bs, n_max, 5), np.float32)
+    nb = np.zeros(bs, np.int32)
+    dims = np.zeros((bs, 2), np.float32)
+    for k, i in enumerate(idx):
+        s = train_data[i]
+        n = len(s["label"])
+        bx[k, :n, :4] = s["bbox"]
+        bx[k, :n, 4] = s["label"]
+        nb[k] = n
+        dims[k] = s.get("img_dim", imgs.shape[1:3])
+    return imgs, bx, nb, dims
+
+
 def train(train_data, training_loss, model, batch_size, optimizer, ckpt, ck_manager, st_step, max_steps,
           init_lr=1.0e-3, min_lr=1.0e-5, decay_step=1000, decay_rate=0.99, display_step=50, step_save=100,
           step_cool=1000, weight_decay=1.0e-4, gradient_clip=1.0, save_loss_file="train_losses.csv"):
-    """Same keywords as FCOS/train_fcos.py:87-93.  `model` is a cvlite FCOSNet; `train_data` is a
-    list of pre-processed samples dict(image=[Hp,Wp,3] float in [-1,1], bbox=[N,4] normalised
-    (yc,xc,h,w), label=[N]) of one padded size; `ckpt` is a path prefix for torch checkpoints
-    (ck_manager unused).  The reference's thermal "Cooling GPU" sleep runs only with
-    CVL_COOLING=1.  Returns None like the reference."""
+    """Same keywords and defaults as FCOS/train_fcos.py:87-93.
+    * `model`: what cvlite.fcos.build_model returns (or its FCOSNet).
+    * `train_data`: pre-processed samples dict(image=[Hp,Wp,3] in [-1,1], bbox=[N,4] normalised
+      (yc,xc,h,w), label=[N], optional img_dim=[h,w] = the unpadded resized size that
+      data_preprocess.preprocess_data returns) of one padded size.
+    * `ckpt` / `ck_manager`: cvlite.checkpoint.Checkpoint / CheckpointManager (tf.train.*
+      semantics: ckpt.step += 1 per step, ck_manager.save() every step_save steps), or a path
+      prefix string (torch checkpoint at <prefix>.pt) and None.
+    * weight_decay > 0 adds weight_decay * l2_params_reg to every image's reported loss and not to
+      the gradient, exactly as the reference (the regulariser is computed outside the tape).
+    The reference's thermal "Cooling GPU" sleep runs only with CVL_COOLING=1.  Returns None."""
+    from . import checkpoint as ck
+    net = getattr(model, "net", model)
     n_data = len(train_data)
-    H, W = train_data[0]["image"].shape[:2]
+    H, W = np.asarray(train_data[0]["image"]).shape[:2]
     n_max = max(16, max(len(s["label"]) for s in train_data))
-    trainer = FCOSTrainer(model, batch_size, (H, W), n_max=n_max, init_lr=init_lr, min_lr=min_lr,
+    trainer = FCOSTrainer(net, batch_size, (H, W), n_max=n_max, init_lr=init_lr, min_lr=min_lr,
                           decay_step=decay_step, decay_rate=decay_rate, momentum=optimizer.momentum,
                           gradient_clip=gradient_clip, weight_decay=weight_decay, st_step=st_step)
-    dev = model.device
+    dev = net.device
     start = time.time()
+    elapsed = 0.0
     batch_objs = total_loss = trend_loss = 0.0
     tot = np.zeros(3)
     for step in range(st_step, max_steps):
         idx = np.random.choice(n_data, size=batch_size, replace=False)       # train_fcos.py:112
-        imgs = torch.from_numpy(np.stack([train_data[i]["image"] for i in idx]).astype(np.float32))
-        bx = np.zeros((batch_size, n_max, 5), np.float32)
-        nb = np.zeros(batch_size, np.int32)
-        for k, i in enumerate(idx):
-            s = train_data[i]
-            n = len(s["label"])
-            bx[k, :n, :4] = s["bbox"]
-            bx[k, :n, 4] = s["label"]
-            nb[k] = n
-        trainer.load_batch(imgs.to(dev), torch.from_numpy(bx).to(dev), torch.from_numpy(nb).to(dev))
-        losses = trainer.step().detach().double().sum(0).cpu().numpy()
-        batch_objs += float(trainer.ntgt.sum().item()) / batch_size
-        tot += losses / batch_size
-        total_loss += losses.sum() / batch_size
-        trend_loss += losses.sum() / batch_size
+        imgs, bx, nb, dims = _batch_from_samples(train_data, idx, n_max)
+        trainer.load_batch(torch.from_numpy(imgs).to(dev), torch.from_numpy(bx).to(dev), torch.from_numpy(nb).to(dev),
+                           img_dim=torch.from_numpy(dims).to(dev))
+        per_img = trainer.step().detach().double().cpu().numpy()         # [bs, 3] (cls, reg, cen)
+        ntgt = trainer.ntgt.sum(1).cpu().numpy()
+        for k in np.nonzero(ntgt == 0)[0]:
+            print("No targets at index", str(idx[k]) + ".")
+        wd_term = weight_decay * float(trainer.l2_params_reg.item()) if weight_decay > 0.0 else 0.0
+        acc = per_img.sum() + batch_size * wd_term
+        if isinstance(ckpt, ck.Checkpoint):
+            ckpt.step.assign_add(1)
+        batch_objs += float(ntgt.sum()) / batch_size
+        tot += per_img.sum(0) / batch_size
+        total_loss += acc / batch_size
+        trend_loss += acc / batch_size
         if (step + 1) % display_step == 0:
+            avg_loss = total_loss / display_step
+            avg = tot / display_step
+            avg_objs = batch_objs / display_step
+            batch_objs = total_loss = 0.0
+            tot[:] = 0.0
             elapsed = (time.time() - start) / 60.0
             start = time.time()
-            avg = tot / display_step
             print("Iteration:", str(step + 1))
             print("Learning Rate:", str(float(trainer.lr.item())))
-            print("Average Objs:", str(batch_objs / display_step))
-            print("Average Loss:", str(round(total_loss / display_step, 5)))
+            print("Average Objs:", str(avg_objs))
+            print("Average Loss:", str(round(avg_loss, 5)))
             print("Average Reg Loss:", str(round(avg[1], 5)))
             print("Average Cls Loss:", str(round(avg[0], 5)))
             print("Average Cen Loss:", str(round(avg[2], 5)))
             if (step + 1) % step_save == 0:
-                training_loss.append((step + 1, total_loss / display_step))
+                training_loss.append((step + 1, avg_loss))
                 with open(save_loss_file, "w") as f:
                     f.write("step,train_loss\n")
                     for a, b in training_loss:
                         f.write("%d,%s\n" % (a, b))
-                if ckpt:
-                    save_checkpoint(ckpt, model, trainer, step + 1)
-            batch_objs = total_loss = 0.0
-            tot[:] = 0.0
-            print("Elapsed Time:", str(elapsed), "mins.")
-            print("-" * 50)
+                print("")
+                if ck_manager is not None and hasattr(ck_manager, "save"):
+                    print("Saved model to {}".format(ck_manager.save()))
+                elif isinstance(ckpt, str) and ckpt:
+                    save_checkpoint(ckpt, net, trainer, step + 1)
+                    print("Saved model to {}".format(ckpt + ".pt"))
+            if (step + 1) % step_cool != 0:
+                print("Elapsed Time:", str(elapsed), "mins.")
+                print("-" * 50)
         if (step + 1) % step_cool == 0:
             print("Trend Loss:", str(round(trend_loss / step_cool, 5)))
             trend_loss = 0.0
+            print("Elapsed Time:", str(elapsed), "mins.")
             if os.environ.get("CVL_COOLING") == "1":
                 print("Cooling GPU for 2 minutes.")
                 time.sleep(120)
+            print("-" * 50)
     return None
 
 
 def save_checkpoint(prefix, model, trainer, step):
-    """{step, params, SGD momentum, BN running stats} (tf.train.Checkpoint equivalent)."""
-    bns = {bn.name: (bn.run_mean.cpu(), bn.run_var.cpu()) for bn in model.backbone.bns()}
-    torch.save({"step": int(step), "params": model.store.flat.cpu(), "momentum": model.store.mom.cpu(),
-                "names": list(model.store.offsets.items()), "bn": bns}, prefix + ".pt")
+    """{step, params, SGD momentum, BN running stats, parameter layout} at <prefix>.pt."""
+    from . import checkpoint as ck
+    net = getattr(model, "net", model)
+    st = ck.net_state(net)
+    st["step"] = int(step)
+    torch.save(st, prefix + ".pt")
 
 
 def load_checkpoint(path, model, trainer=None):
-    ck = torch.load(path, weights_only=True)
-    model.store.flat.copy_(ck["params"].to(model.store.flat.device))
-    model.store.mom.copy_(ck["momentum"].to(model.store.flat.device))
-    for bn in model.backbone.bns():
-        m, v = ck["bn"][bn.name]
-        bn.run_mean.copy_(m)
-        bn.run_var.copy_(v)
-    model.pack()
+    from . import checkpoint as ck
+    net = getattr(model, "net", model)
+    s = torch.load(path, weights_only=True)
+    ck.load_net_state(net, s)
     if trainer is not None:
-        trainer.step_dev.fill_(int(ck["step"]))
-    return int(ck["step"])
+        trainer.step_dev.fill_(int(s["step"]))
+    return int(s["step"])

@@ -9,8 +9,9 @@
 * loss = cls + reg summed over the 45 (level, anchor) terms (cvl_retina_loss, fwd+bwd fused);
 * gradients summed over the images, / batch_size (even when fewer were usable), clipped by
   global norm, Keras SGD momentum 0.9 (`tf.optimizers.SGD(momentum=0.9)`, :345);
-* lr = init_lr for step < 60000 and init_lr / 10 after (:164-171; the 80000 branch is
-  unreachable in the reference) = max(init * 0.1^floor(step / 60000), min_lr) up to step 119999.
+* lr = max(init_lr, min_lr) for step < 60000 and max(init_lr / 10, min_lr) for every step after
+  (:164-171; the 80000 branch is unreachable in the reference) = the device schedule
+  max(init * 0.1^floor(step / 60000), max(init / 10, min_lr)).
 BN statistics are per image (the reference forwards one image at a time).
 """
 import numpy as np
@@ -35,7 +36,8 @@ class RetinaTrainer(GraphStepper):
         self.C, self.A = net.C, net.A
         self.world = world
         self.momentum, self.clip = momentum, gradient_clip
-        self.sched = (init_lr, min_lr, 0.1, 60000)
+        # the floor max(init/10, min_lr) stops the decay after the first drop (:164-171)
+        self.sched = (init_lr, max(init_lr / 10.0, min_lr), 0.1, 60000)
         dev = net.device
         B, S = self.B, self.S
         shapes, off, self.P = net.layout(B, S, S)
@@ -67,6 +69,7 @@ class RetinaTrainer(GraphStepper):
         nn.gather_rows(self.cand_images, self.sel, self.images)
         nn.gather_rows(self.cand_targets, self.sel, self.targets)
         reg, cls = self.net.forward(self.images)
+        self.outputs = (reg, cls)
         ot.retina_loss(reg, cls, self.targets, self.level_cells, self.A, self.C, img_weight=self.img_w,
                        d_reg=self.d_reg, d_cls=self.d_cls, losses=self.losses)
         self.net.backward(self.d_reg, self.d_cls, hook=hook)
@@ -124,9 +127,12 @@ def train(train_data, training_loss, model, batch_size, optimizer, ckpt, ck_mana
     `train_data` a list of pre-processed samples dict(image=[S,S,3] in [-1,1], bbox=[N,4] normalised
     (yc,xc,h,w), label=[N]) of one square size S (decode/resize are outside this tier).  Per step
     3*batch_size candidates are drawn without replacement; the device picks the first batch_size
-    with anchor matches.  Prints the reference's progress lines; `ckpt` = torch checkpoint prefix."""
+    with anchor matches.  Prints the reference's progress lines.  `ckpt` / `ck_manager`:
+    cvlite.checkpoint.Checkpoint / CheckpointManager (tf.train semantics), or a path prefix string
+    and None (torch checkpoint with parameters, momentum and BN moving statistics)."""
     import os
     import time
+    from . import checkpoint as ck
     n_data = len(train_data)
     S = int(train_data[0]["image"].shape[0])
     n_max = max(16, max(len(s["label"]) for s in train_data))
@@ -150,6 +156,8 @@ def train(train_data, training_loss, model, batch_size, optimizer, ckpt, ck_mana
             nb[k] = n
         trainer.load_candidates(imgs.to(dev), torch.from_numpy(bx).to(dev), torch.from_numpy(nb).to(dev))
         losses = trainer.step().detach().double().sum(0).cpu().numpy()
+        if isinstance(ckpt, ck.Checkpoint):
+            ckpt.step.assign_add(1)
         sel_w = trainer.img_w.cpu().numpy()
         used = trainer.cand_counts.cpu().numpy()[trainer.sel.cpu().numpy()] * sel_w
         batch_objs += float(used.sum()) / batch_size
@@ -174,9 +182,12 @@ def train(train_data, training_loss, model, batch_size, optimizer, ckpt, ck_mana
                     f.write("step,train_loss,cls_loss,reg_loss\n")
                     for row in training_loss:
                         f.write(",".join(str(v) for v in row) + "\n")
-                if ckpt:
-                    torch.save({"step": step + 1, "params": model.model.store.flat.cpu(),
-                                "momentum": model.model.store.mom.cpu()}, ckpt + ".pt")
+                if ck_manager is not None and hasattr(ck_manager, "save"):
+                    print("Saved model to {}".format(ck_manager.save()))
+                elif isinstance(ckpt, str) and ckpt:
+                    st = ck.net_state(model.model)
+                    st["step"] = step + 1
+                    torch.save(st, ckpt + ".pt")
             if (step + 1) % step_cool != 0:
                 print("Elapsed Time:", str(elapsed), "mins.")
                 print("-" * 50)

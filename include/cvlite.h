@@ -128,6 +128,13 @@ size_t cvl_conv_igemm_workspace_size(const cvl_conv_desc* d);
 int cvl_conv_igemm(const cvl_conv_desc* d, const void* src, void* dst, double* bn_stats,
                    void* workspace, size_t workspace_bytes, cvl_stream_t stream);
 
+/* Test / profiling hook: the kernel variant the last cvl_conv_igemm call on THIS host thread
+ * launched.  CVL_CK_* codes; cvl_conv_kernel_name(code) is a static string. */
+enum { CVL_CK_NONE = 0, CVL_CK_BASE = 1, CVL_CK_BASE_SPLITK = 2, CVL_CK_L64 = 3, CVL_CK_L128 = 4,
+       CVL_CK_L256 = 5, CVL_CK_X256 = 6 };
+int cvl_conv_igemm_last_kernel(void);
+const char* cvl_conv_kernel_name(int code);
+
 /* Weight gradient (replaces Conv2DBackpropFilter + the per-image gradient accumulation of
  * FCOS/train_fcos.py:173-176): dw[KH][KW][Cin][n_store] (HWIO fp32) = beta*dw + sum over all
  * rows of all segments of im2col(x) * dy.  `d` is the FORWARD descriptor (its ld_dst/dst_coff
@@ -214,6 +221,13 @@ int cvl_sgd_clip_update(float* w, const float* g, float* v, int64_t n, const flo
                         float momentum, float inv_bs, float clip, double* sumsq_ws, cvl_stream_t stream);
 int cvl_lr_schedule(int32_t* step, float* lr, double init_lr, double min_lr, double decay_rate,
                     int decay_step, cvl_stream_t stream);
+
+/* l2_params_reg of train_fcos.py:118-120 = sum over tensors v of sqrt(sum(tf.nn.l2_loss(v)))
+ * = sum_v sqrt(0.5 * sum(v^2)), over the tensors at device offsets[i] / sizes[i] of the flat
+ * parameter buffer; terms: n_tensors floats of workspace; *out (device float).  The reference
+ * computes it outside the GradientTape, so it enters the reported loss, not the gradient. */
+int cvl_l2_params_reg(const float* flat, const int64_t* offsets, const int64_t* sizes, int n_tensors,
+                      float* terms, float* out, cvl_stream_t stream);
 
 /* RetinaNet candidate selection (train_retinanet_coco.py:190-209: images without matches are
  * skipped, the first batch_size usable candidates are trained on): idx[k] = the first k indices

@@ -17,6 +17,50 @@ def test_library_exports_header_symbols():
     assert lib.cvl_version() >= 100
 
 
+def _header_decls():
+    """(name -> (return C type, [argument C types])) for every cvl_* function in the header."""
+    hdr = open(os.path.join(ROOT, "include", "cvlite.h")).read()
+    hdr = re.sub(r"/\*.*?\*/", " ", hdr, flags=re.S)
+    hdr = re.sub(r"//[^\n]*", " ", hdr)
+    out = {}
+    for m in re.finditer(r"([A-Za-z_][A-Za-z0-9_ \*]*?)\b(cvl_[a-z0-9_]+)\s*\(([^)]*)\)\s*;", hdr):
+        ret, name, args = m.group(1).strip(), m.group(2), m.group(3).strip()
+        ret = ret.split("\n")[-1].strip()
+        argl = [] if args in ("", "void") else [a.strip() for a in args.split(",")]
+        types = []
+        for a in argl:
+            a = " ".join(a.split())
+            if "*" in a:
+                types.append("ptr")
+            else:
+                types.append(" ".join(a.split(" ")[:-1]).replace("const ", ""))
+        out[name] = ("ptr" if "*" in ret else ret.replace("const ", "").strip(), types)
+    return out
+
+
+def test_ctypes_signatures_match_header_types():
+    """Every argument and return type in _lib.SIGNATURES agrees with the C declaration (an
+    int / int64 / size_t / float / double / pointer drift fails here, not on the GPU)."""
+    import ctypes
+    from cvlite import _lib
+    cmap = {"int": ctypes.c_int, "int32_t": ctypes.c_int, "int64_t": ctypes.c_int64, "long": ctypes.c_long,
+            "size_t": ctypes.c_size_t, "float": ctypes.c_float, "double": ctypes.c_double,
+            "cvl_stream_t": ctypes.c_void_p, "ptr": ctypes.c_void_p}
+    decls = _header_decls()
+    assert set(decls) == set(_lib.SIGNATURES), sorted(set(decls) ^ set(_lib.SIGNATURES))
+    for name, (ret, args) in decls.items():
+        res, argt = _lib.SIGNATURES[name]
+        exp_args = [cmap[a] for a in args]
+        assert len(argt) == len(exp_args), (name, len(argt), len(exp_args))
+        for i, (got, exp) in enumerate(zip(argt, exp_args)):
+            assert ctypes.sizeof(got) == ctypes.sizeof(exp) and (got is exp or (
+                issubclass(got, ctypes._SimpleCData) and got._type_ == exp._type_)), (name, i, got, exp)
+        if ret == "ptr":
+            assert res in (ctypes.c_void_p, ctypes.c_char_p), (name, res)
+        else:
+            assert res is cmap[ret] or res._type_ == cmap[ret]._type_, (name, res, ret)
+
+
 def test_no_cpu_fallback_in_product_path():
     """Without a GPU every cvlite op raises (there is no CPU fallback on the product path)."""
     import numpy as np

@@ -115,6 +115,60 @@ def test_reference_init_deviation_bounded_by_bf16_storage():
         assert e_gpu <= 1.5 * e_emu + 0.02
 
 
+def test_backbone_inference_uses_moving_stats():
+    """Keras training=False (infer_fcos / image_detections): every BN normalises with its moving
+    mean / variance, not the image's own statistics, and the moving statistics are not updated.
+    Non-trivial moving statistics; each block vs the fp32 oracle with moving-statistics BN, fed
+    the oracle's own input."""
+    import torch.nn.functional as F
+    from cvlite.fcos_net import FCOSNet
+    C, B, D = 20, 2, 128
+    net = FCOSNet(C, seed=2)
+    p = net.store.state_dict()
+    g = torch.Generator().manual_seed(4)
+    moving = {}
+    for bn in net.backbone.bns():
+        rm = torch.randn(bn.c, generator=g) * 0.3
+        rv = torch.rand(bn.c, generator=g) * 2.0 + 0.2
+        bn.run_mean.copy_(rm)
+        bn.run_var.copy_(rv)
+        moving[bn.name] = (rm, rv)
+
+    def bn_inf(x, name, eps=1.001e-5):
+        rm, rv = moving[name]
+        gm, bt = p[name + "/gamma"].view(1, -1, 1, 1), p[name + "/beta"].view(1, -1, 1, 1)
+        return (x - rm.view(1, -1, 1, 1)) / torch.sqrt(rv.view(1, -1, 1, 1) + eps) * gm + bt
+
+    rng = np.random.default_rng(5)
+    x = torch.from_numpy(rng.uniform(-1, 1, size=(B, D, D, 3)).astype(np.float32))
+    pool, _ = net.backbone.stem.forward(x.cuda(), train=False)
+    pool_train, _ = net.backbone.stem.forward(x.cuda(), train=True)
+    xn = x.permute(0, 3, 1, 2)
+    hr = F.max_pool2d(F.pad(F.relu(bn_inf(model_ref.conv(xn, p, "conv1_conv", 2, pad=3), "conv1_bn")),
+                            (1, 1, 1, 1)), 3, 2)
+    assert rel(pool.float().cpu().permute(0, 3, 1, 2), hr) < 1e-2
+    assert rel(pool_train.float().cpu().permute(0, 3, 1, 2), hr) > 0.1     # the two modes differ
+    for bn in net.backbone.bns():                                           # restore (train=True moved them)
+        bn.run_mean.copy_(moving[bn.name][0])
+        bn.run_var.copy_(moving[bn.name][1])
+    H = W = hr.shape[2]
+    for si, stage in enumerate(net.backbone.stages):
+        for bi, blk in enumerate(stage):
+            n = "conv%d_block%d" % (si + 2, bi + 1)
+            s = blk.c1.conv.stride
+            hin = hr.permute(0, 2, 3, 1).contiguous().to(torch.bfloat16).cuda()
+            out, H, W, _ = blk.forward(hin, B, H, W, train=False)
+            hb = hin.float().cpu().permute(0, 3, 1, 2)
+            sc = bn_inf(model_ref.conv(hb, p, n + "_0_conv", s), n + "_0_bn") if bi == 0 else hb
+            y = F.relu(bn_inf(model_ref.conv(hb, p, n + "_1_conv", s), n + "_1_bn"))
+            y = F.relu(bn_inf(model_ref.conv(y, p, n + "_2_conv"), n + "_2_bn"))
+            hr = F.relu(bn_inf(model_ref.conv(y, p, n + "_3_conv"), n + "_3_bn") + sc)
+            e = rel(out.float().cpu().permute(0, 3, 1, 2), hr)
+            assert e < 1.5e-2, (n, e)
+    for bn in net.backbone.bns():
+        assert torch.equal(bn.run_mean.cpu(), moving[bn.name][0]) and torch.equal(bn.run_var.cpu(), moving[bn.name][1])
+
+
 def test_backbone_blocks_match_fp32_oracle_with_synced_inputs():
     """Every ResNet-50 block (conv + per-image BN + residual + ReLU, fwd) vs the plain fp32 oracle,
     each fed the oracle's own input: isolates kernel error from the graph's chaotic amplification."""

@@ -1,0 +1,135 @@
+"""Drop-in semantics of the training-loop API (FCOS/train_fcos.py:87-251,
+RetinaNet/train_retinanet_coco.py:145-308) on the GPU path:
+* weight_decay > 0: weight_decay * l2_params_reg (sum_v sqrt(sum(l2_loss(v))), computed before the
+  tape) enters the reported loss only, not the gradient (train_fcos.py:118-120, 160-171);
+* per-image img_dim (the unpadded resized size) reaches format_data with img_pad = the padded
+  size (train_fcos.py:131-143);
+* train() takes what fcos.build_model returns and the Checkpoint / CheckpointManager pair, and a
+  saved checkpoint restores parameters, momentum and BN moving statistics;
+* RetinaNet's LR is init for step < 60000 and init / 10 for every later step (:164-171);
+* capturing the step graph does not move the BN moving statistics."""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def test_weight_decay_reported_not_differentiated():
+    from cvlite.fcos_net import FCOSNet
+    from cvlite.train_fcos import FCOSTrainer, synthetic_batch
+    C, B, S = 20, 2, 128
+    batch = synthetic_batch(B, S, S, C, seed=5)
+    grads, l2s = [], []
+    for wd in (0.0, 1e-4):
+        net = FCOSNet(C, seed=3)
+        p0 = {k: v.double().numpy() for k, v in net.store.state_dict().items()}
+        tr = FCOSTrainer(net, B, (S, S), weight_decay=wd)
+        tr.load_batch(*batch)
+        tr.step()
+        torch.cuda.synchronize()
+        grads.append(net.store.grad.clone())
+        if wd > 0:
+            exp = sum(np.sqrt(0.5 * (v ** 2).sum()) for v in p0.values())
+            np.testing.assert_allclose(float(tr.l2_params_reg.item()), exp, rtol=1e-5)
+    torch.testing.assert_close(grads[1], grads[0], rtol=2e-2, atol=1e-6)
+
+
+def test_img_dim_per_image_reaches_targets():
+    from cvlite.fcos_net import FCOSNet
+    from cvlite.train_fcos import FCOSTrainer
+    from oracle import fcos_ref
+    C, B, S = 20, 2, 384
+    net = FCOSNet(C, seed=1)
+    tr = FCOSTrainer(net, B, (S, S), use_graph=False)
+    rng = np.random.default_rng(3)
+    dims = np.array([[300.0, 384.0], [384.0, 257.0]], np.float32)     # resized, unpadded
+    boxes = np.zeros((B, 16, 5), np.float32)
+    nbox = np.array([5, 7], np.int32)
+    for b in range(B):
+        for i in range(nbox[b]):
+            h, w = np.exp(rng.uniform(np.log(0.05), np.log(0.9), 2))
+            boxes[b, i] = [rng.uniform(h / 2, 1 - h / 2), rng.uniform(w / 2, 1 - w / 2), h, w, rng.integers(0, C)]
+    imgs = torch.rand((B, S, S, 3), device="cuda") * 2 - 1
+    tr.load_batch(imgs, torch.from_numpy(boxes).cuda(), torch.from_numpy(nbox).cuda(), img_dim=torch.from_numpy(dims).cuda())
+    tr.step()
+    tg = tr.targets.cpu().numpy()
+    for b in range(B):
+        outs, _ = fcos_ref.format_data(boxes[b, :nbox[b]], dims[b], C, img_pad=(S, S))
+        np.testing.assert_array_equal(tg[b], fcos_ref.pack_targets(outs))
+    padded, _ = fcos_ref.format_data(boxes[0, :nbox[0]], np.array([S, S], np.float32), C, img_pad=(S, S))
+    assert not np.array_equal(tg[0], fcos_ref.pack_targets(padded))       # the unpadded size matters
+    tr.load_batch(imgs, torch.from_numpy(boxes).cuda(), torch.from_numpy(nbox).cuda())   # back to padded
+    tr.step()
+    np.testing.assert_array_equal(tr.targets[0].cpu().numpy(), fcos_ref.pack_targets(padded))
+
+
+def test_train_loop_with_build_model_and_checkpoint_manager(tmp_path, capsys):
+    from cvlite import checkpoint as ck
+    from cvlite import fcos
+    from cvlite.train_fcos import SGD, train
+    C, S = 20, 128
+    rng = np.random.default_rng(0)
+    data = []
+    for i in range(6):
+        n = int(rng.integers(1, 4))
+        hw = rng.uniform(0.1, 0.8, (n, 2))
+        c = rng.uniform(hw / 2, 1 - hw / 2)
+        data.append(dict(image=rng.uniform(-1, 1, (S, S, 3)).astype(np.float32),
+                         bbox=np.concatenate([c, hw], 1).astype(np.float32),
+                         label=rng.integers(0, C, n), img_dim=np.array([S, S - 8 * (i % 2)], np.float32)))
+    model = fcos.build_model(C)
+    opt = SGD(learning_rate=5e-4, momentum=0.9)
+    ckpt = ck.Checkpoint(step=ck.Variable(0), fcos_model=model, model_optimizer=opt)
+    mgr = ck.CheckpointManager(ckpt, str(tmp_path / "ck"), max_to_keep=1)
+    losses = []
+    train(data, losses, model, 2, opt, ckpt, mgr, 0, 4, init_lr=5e-4, display_step=2, step_save=2, step_cool=4,
+          weight_decay=1e-4, save_loss_file=str(tmp_path / "loss.csv"))
+    out = capsys.readouterr().out
+    assert "Average Loss:" in out and "Trend Loss:" in out and "Saved model to" in out
+    assert int(ckpt.step.numpy()) == 4 and len(losses) == 2 and np.isfinite(losses[-1][1])
+    assert mgr.latest_checkpoint.endswith("ckpt-2.pt") and len(mgr.checkpoints) == 1
+    # restore into a fresh model: parameters, momentum and moving statistics come back
+    net = model.net
+    for bn in net.backbone.bns()[:3]:
+        assert not torch.equal(bn.run_mean, torch.zeros_like(bn.run_mean))
+    model2 = fcos.build_model(C)
+    ck2 = ck.Checkpoint(step=ck.Variable(0), fcos_model=model2, model_optimizer=SGD(5e-4, 0.9))
+    ck2.restore(mgr.latest_checkpoint)
+    assert int(ck2.step.numpy()) == 4
+    assert torch.equal(model2.net.store.flat, net.store.flat) and torch.equal(model2.net.store.mom, net.store.mom)
+    for a, b in zip(model2.net.backbone.bns(), net.backbone.bns()):
+        assert torch.equal(a.run_mean, b.run_mean) and torch.equal(a.run_var, b.run_var)
+
+
+def test_retinanet_lr_schedule_stays_at_init_over_10():
+    from cvlite.retinanet import RetinaNet
+    from cvlite.train_retinanet import RetinaTrainer
+    from cvlite import ops_nn as nn
+    rn = RetinaNet(8, {}, anchor_sizes=[20.0, 40.0, 80.0, 160.0, 320.0])
+    tr = RetinaTrainer(rn.model, rn, 1, 128, n_max=4, init_lr=0.01, min_lr=1e-5, use_graph=False)
+    init, mn, rate, dstep = tr.sched
+    got = []
+    for s in (0, 59999, 60000, 80000, 120000, 500000):
+        tr.step_dev.fill_(s)
+        nn.lr_schedule(tr.step_dev, tr.lr, init, mn, rate, dstep)
+        got.append(float(tr.lr.item()))
+    np.testing.assert_allclose(got, [0.01, 0.01, 0.001, 0.001, 0.001, 0.001], rtol=1e-6)
+
+
+def test_graph_capture_keeps_bn_moving_stats():
+    """After the first (captured) step the moving statistics have received exactly one EMA update
+    per image, as an eager step gives (the warm-up forwards are undone)."""
+    from cvlite.fcos_net import FCOSNet
+    from cvlite.train_fcos import FCOSTrainer, synthetic_batch
+    C, B, S = 20, 2, 128
+    batch = synthetic_batch(B, S, S, C, seed=9)
+    stats = []
+    for graph in (False, True):
+        net = FCOSNet(C, seed=3)
+        tr = FCOSTrainer(net, B, (S, S), use_graph=graph)
+        tr.load_batch(*batch)
+        tr.step()
+        torch.cuda.synchronize()
+        stats.append(torch.cat([torch.cat([bn.run_mean, bn.run_var]) for bn in net.backbone.bns()]))
+    torch.testing.assert_close(stats[1], stats[0], rtol=1e-4, atol=1e-6)

@@ -31,3 +31,51 @@ def test_resize_plan_matches_restatement(H, W, mn, mx, stride, eq):
     img, rns, rratio = preprocess_ref.resize_and_pad_image(np.zeros((H, W, 3), np.uint8), mn, mx, stride, eq)
     np.testing.assert_array_equal(new_shape, rns)
     assert ratio == rratio and (ph, pw) == img.shape[:2]
+
+
+def test_checkpoint_manager_roundtrip_cpu(tmp_path):
+    """tf.train.Checkpoint / CheckpointManager mirror (cvlite.checkpoint): numbered saves,
+    max_to_keep pruning, latest_checkpoint, step counter, parameters + momentum + BN moving
+    statistics restored, layout mismatch rejected.  CPU tensors stand in for the device store."""
+    import torch
+    from cvlite import checkpoint as ck
+    from cvlite.layers import BatchNorm, ParamStore, constant
+
+    class Net(object):
+        def __init__(self, seed, extra=False):
+            self.store = ParamStore()
+            self.store.add("a/kernel", (3, 4), constant(seed))
+            self.bn = BatchNorm(self.store, "a_bn", 4)
+            if extra:
+                self.store.add("b/kernel", (2,), constant(0.0))
+            self.store.finalize("cpu", int(seed))
+            self.bn.init_buffers("cpu")
+            self.packed = 0
+
+        def bns(self):
+            return [self.bn]
+
+        def pack(self):
+            self.packed += 1
+
+    net = Net(1.0)
+    net.store.mom.fill_(0.5)
+    net.bn.run_mean.fill_(0.25)
+    c = ck.Checkpoint(step=ck.Variable(0), model=net)
+    m = ck.CheckpointManager(c, str(tmp_path), max_to_keep=2)
+    assert m.latest_checkpoint is None
+    for i in range(3):
+        c.step.assign_add(1)
+        m.save()
+    assert [p.rsplit("-", 1)[1] for p in m.checkpoints] == ["2.pt", "3.pt"]
+    assert m.latest_checkpoint.endswith("ckpt-3.pt")
+    other = Net(2.0)
+    c2 = ck.Checkpoint(step=ck.Variable(0), model=other)
+    c2.restore(m.latest_checkpoint)
+    assert int(c2.step.numpy()) == 3 and other.packed == 1
+    assert torch.equal(other.store.flat, net.store.flat) and torch.equal(other.store.mom, net.store.mom)
+    assert torch.equal(other.bn.run_mean, net.bn.run_mean)
+    # a manager re-opened on the same directory continues the numbering
+    assert ck.CheckpointManager(c, str(tmp_path), max_to_keep=2).save().endswith("ckpt-4.pt")
+    with pytest.raises(ValueError):
+        ck.Checkpoint(model=Net(3.0, extra=True)).restore(m.latest_checkpoint)
