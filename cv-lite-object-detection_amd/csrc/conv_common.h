@@ -21,6 +21,13 @@ __device__ __forceinline__ int xcd_remap(int b, int nwg) {
   return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + b / 8;
 }
 
+// s_waitcnt with only vmcnt constrained (gfx9 encoding: vmcnt[3:0] + vmcnt[5:4] at [15:14],
+// expcnt [6:4] and lgkmcnt [11:8] left at their maxima)
+template <int N>
+__device__ __forceinline__ void wait_vm() {
+  __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | (7 << 4) | (15 << 8));
+}
+
 struct ConvSeg {
   int Hr, Wr, Hs, Ws;
   long src_base, src_img, dst_base, dst_img;
@@ -42,6 +49,7 @@ struct ConvArgs {
   int m_tiles, m_total;
   float* slab;      // split-K partial sums [splits][m_total][Npad] (fp32) or null
   int splits, ksteps_per_split;
+  int dbg;            // kernel ablation bits for measurement (CVL_X_ABLATE), 0 in production
   int dst_up, dst_w;  // output pixel (y, x) of the GEMM grid lands at (y*dst_up, x*dst_up) of a
                       // dst_w-wide map (1x1 strided data-gradient as a dense GEMM); 1 = identity
 };
@@ -69,6 +77,7 @@ static inline int cvl_conv_prepare(const cvl_conv_desc* d, int bm, ConvArgs* a) 
   a->ksteps_per_split = 0;
   a->dst_up = 1;
   a->dst_w = 0;
+  a->dbg = 0;
   a->nseg = d->nseg;
   a->B = d->B;
   a->Cin = d->Cin; a->KH = d->KH; a->KW = d->KW; a->stride = d->stride;

@@ -13,6 +13,7 @@
 // 0 in steady state) and the barrier a raw s_barrier, so the DMA stays outstanding across it.
 // Padding taps and rows past a segment's end read a 16-byte zero block.
 #include "conv_common.h"
+#include "conv_epilogue.h"
 
 namespace {
 
@@ -27,13 +28,6 @@ __device__ __forceinline__ int swz(int r) { return (r >> 1) & 7; }
 __device__ __forceinline__ void glds16(const void* g, void* l) {
   __builtin_amdgcn_global_load_lds((const void __attribute__((address_space(1)))*)g,
                                    (void __attribute__((address_space(3)))*)l, 16, 0, 0);
-}
-
-// s_waitcnt with only vmcnt constrained (gfx9 encoding: vmcnt[3:0] + vmcnt[5:4] at [15:14],
-// expcnt [6:4] and lgkmcnt [11:8] left at their maxima)
-template <int N>
-__device__ __forceinline__ void wait_vm() {
-  __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | (7 << 4) | (15 << 8));
 }
 
 // BN x WGM x NST: 128/64-wide tiles run 8 waves as 4 (M) x 2 (N) with a 3-deep ring; the
@@ -188,155 +182,12 @@ __global__ void __launch_bounds__(NT) conv_igemm_l_kernel(ConvArgs a) {
     slot = slot == NST - 1 ? 0 : slot + 1;
   }
 
-  // ---- epilogue: +bias, ReLU, bf16 rounding, BN statistics, beta*old, 16-byte stores ----------
-  float bcol[TN];
-#pragma unroll
-  for (int j = 0; j < TN; ++j) {
-    const int n = n0 + wn * WN + j * 16 + lr;
-    bcol[j] = (S.bias && n < a.n_store) ? S.bias[n] : 0.f;
-  }
-  if (a.dst_f32) {
-    // fp32 destination (the head outputs the fused losses read): +bias, ReLU, unrounded 4-byte
-    // stores straight from the accumulators (16 lanes = 64 contiguous bytes per row), as the
-    // 128-row kernel does; no statistics (the host never pairs them with an fp32 output).  All
-    // ring DMA has drained: the last K step waited for vmcnt 0 and issued nothing.
-    float* dstf = reinterpret_cast<float*>(a.dst);
-#pragma unroll
-    for (int i = 0; i < TM; ++i)
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const int ml = mloc0 + wm * WM + i * 16 + lg * 4 + e;
-        if (ml >= S.rows) continue;
-        const int img = ml / HWr, q = ml - img * HWr;
-        const long drow = conv_dst_row(a, S, img, q);
-#pragma unroll
-        for (int j = 0; j < TN; ++j) {
-          const int n = n0 + wn * WN + j * 16 + lr;
-          if (n >= a.n_store) continue;
-          float v = acc[i][j][e] + bcol[j];
-          if (a.relu_out) v = v > 0.f ? v : 0.f;
-          float* pd = dstf + drow * a.ld_dst + a.dst_coff + n;
-          *pd = a.beta != 0.f ? v + a.beta * *pd : v;
-        }
-      }
-    return;
-  }
-#pragma unroll
-  for (int i = 0; i < TM; ++i)
-#pragma unroll
-    for (int j = 0; j < TN; ++j)
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        float v = acc[i][j][e] + bcol[j];
-        if (a.relu_out) v = v > 0.f ? v : 0.f;
-        acc[i][j][e] = bf16_to_f32(f32_to_bf16(v));
-      }
-
-  // one image per tile: each wave reduces its rows (registers + lane shuffles), the WGM waves of a
-  // column are combined through LDS below, then ONE atomic pair per (tile, column)
-  // (the 2-wave-tall 256-wide tile keeps the per-wave atomics: it runs at the register limit)
-  const bool tile_stats = a.stats && HWr % BM == 0;
-  if (WGM == 2 && tile_stats) {
-    const int img = mloc0 / HWr;
-#pragma unroll
-    for (int j = 0; j < TN; ++j) {
-      float s1 = 0.f, s2 = 0.f;
-#pragma unroll
-      for (int i = 0; i < TM; ++i)
-#pragma unroll
-        for (int e = 0; e < 4; ++e) { const float v = acc[i][j][e]; s1 += v; s2 += v * v; }
-      s1 += __shfl_xor(s1, 16, 64); s1 += __shfl_xor(s1, 32, 64);
-      s2 += __shfl_xor(s2, 16, 64); s2 += __shfl_xor(s2, 32, 64);
-      const int n = n0 + wn * WN + j * 16 + lr;
-      if (lg == 0 && n < a.n_store) {
-        double* st = a.stats + ((long)img * a.n_store + n) * 2;
-        atomicAdd(st, (double)s1);
-        atomicAdd(st + 1, (double)s2);
-      }
-    }
-  } else if (a.stats && !tile_stats) {
-    // the 4 rows of an accumulator quad share one image (host: H*W % 4 == 0)
-#pragma unroll
-    for (int i = 0; i < TM; ++i) {
-      const int ml0 = mloc0 + wm * WM + i * 16 + lg * 4;
-      if (ml0 >= S.rows) continue;
-      const int img = ml0 / HWr;
-#pragma unroll
-      for (int j = 0; j < TN; ++j) {
-        const int n = n0 + wn * WN + j * 16 + lr;
-        if (n >= a.n_store) continue;
-        float s1 = 0.f, s2 = 0.f;
-#pragma unroll
-        for (int e = 0; e < 4; ++e) { const float v = acc[i][j][e]; s1 += v; s2 += v * v; }
-        double* st = a.stats + ((long)img * a.n_store + n) * 2;
-        atomicAdd(st, (double)s1);
-        atomicAdd(st + 1, (double)s2);
-      }
-    }
-  }
-
-  wait_vm<0>();
-  __syncthreads();
-  constexpr int CP = BN + 8;
-  cvl_bf16* Cs = lds;
-#pragma unroll
-  for (int i = 0; i < TM; ++i)
-#pragma unroll
-    for (int j = 0; j < TN; ++j)
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const int r = wm * WM + i * 16 + lg * 4 + e;
-        const int c = wn * WN + j * 16 + lr;
-        Cs[r * CP + c] = f32_to_bf16(acc[i][j][e]);
-      }
-  float* sred = reinterpret_cast<float*>(lds + BM * CP);     // [WGM][BN][2]
-  if (WGM > 2 && tile_stats) {
-#pragma unroll
-    for (int j = 0; j < TN; ++j) {
-      float s1 = 0.f, s2 = 0.f;
-#pragma unroll
-      for (int i = 0; i < TM; ++i)
-#pragma unroll
-        for (int e = 0; e < 4; ++e) { const float v = acc[i][j][e]; s1 += v; s2 += v * v; }
-      s1 += __shfl_xor(s1, 16, 64); s1 += __shfl_xor(s1, 32, 64);
-      s2 += __shfl_xor(s2, 16, 64); s2 += __shfl_xor(s2, 32, 64);
-      if (lg == 0) {
-        const int c = wn * WN + j * 16 + lr;
-        sred[(wm * BN + c) * 2] = s1;
-        sred[(wm * BN + c) * 2 + 1] = s2;
-      }
-    }
-  }
-  __syncthreads();
-  if (WGM > 2 && tile_stats && tid < BN && n0 + tid < a.n_store) {
-    float s1 = 0.f, s2 = 0.f;
-#pragma unroll
-    for (int w = 0; w < WGM; ++w) { s1 += sred[(w * BN + tid) * 2]; s2 += sred[(w * BN + tid) * 2 + 1]; }
-    double* st = a.stats + ((long)(mloc0 / HWr) * a.n_store + n0 + tid) * 2;
-    atomicAdd(st, (double)s1);
-    atomicAdd(st + 1, (double)s2);
-  }
-  constexpr int CCH = BN / 8;
-  cvl_bf16* dst = reinterpret_cast<cvl_bf16*>(a.dst);
-  for (int idx = tid; idx < BM * CCH; idx += NT) {
-    const int r = idx / CCH, c8 = (idx - (idx / CCH) * CCH) * 8;
-    const int ml = mloc0 + r;
-    if (ml >= S.rows || n0 + c8 >= a.n_store) continue;
-    const int img = ml / HWr, q = ml - img * HWr;
-    const long drow = conv_dst_row(a, S, img, q);
-    s16x8 v = *reinterpret_cast<const s16x8*>(Cs + r * CP + c8);
-    s16x8* pd = reinterpret_cast<s16x8*>(dst + drow * a.ld_dst + a.dst_coff + n0 + c8);
-    if (a.beta != 0.f) {
-      const s16x8 o = *pd;
-#pragma unroll
-      for (int u = 0; u < 8; ++u)
-        v[u] = (short)f32_to_bf16(bf16_to_f32((cvl_bf16)v[u]) + a.beta * bf16_to_f32((cvl_bf16)o[u]));
-    }
-    *pd = v;
-  }
+  conv_l_epilogue<BN, WGM, TM, TN, NT>(a, S, acc, lds, tid, wm, wn, n0, mloc0, HWr);
 }
 
 }  // namespace
+
+int cvl_conv_igemm_x(const cvl_conv_desc* d, const ConvArgs& a, hipStream_t s);
 
 // Called by cvl_conv_igemm when the launch qualifies (see cvl_conv_igemm_l_ok); returns -1 when
 // it does not, so the caller falls back to the 128-row kernel.
@@ -385,6 +236,10 @@ int cvl_conv_igemm_l(const cvl_conv_desc* d, int dst_up, int dst_w, const void* 
       else hipLaunchKernelGGL((conv_igemm_l_kernel<BN_, WGM_, NST_, false, false>), grid, dim3(NT), 0, s, a);      \
     }                                                                                                          \
   } while (0)
+  if (use_bn == 256) {                    // the 8-phase 256 x 256 kernel when it applies
+    const int xst = cvl_conv_igemm_x(d, a, s);
+    if (xst >= 0) return xst;
+  }
   g_cvl_conv_last_kernel = use_bn == 256 ? CVL_CK_L256 : (use_bn == 128 ? CVL_CK_L128 : CVL_CK_L64);
   if (use_bn == 256) CVL_L_LAUNCH(256, 2, 2);
   else if (use_bn == 128) CVL_L_LAUNCH(128, 4, 3);

@@ -29,18 +29,22 @@ def ref_conv(x, w, b, stride, pad):
     return y.permute(0, 2, 3, 1)
 
 
-@pytest.fixture(params=["base", "l", "l256"])
+@pytest.fixture(params=["base", "l", "l256", "x"])
 def kern(request, monkeypatch):
     """Run a test through the 128-row register-staged kernel ("base"), the 256-row LDS-DMA kernel
-    ("l", normally taken only by launches with >= 128 tiles; 128/64-wide N tiles) and its
-    256x256-tile form ("l256", Npad % 256 == 0 only)."""
-    if request.param in ("l", "l256"):
+    ("l", normally taken only by launches with >= 128 tiles; 128/64-wide N tiles), its
+    256x256-tile form ("l256", Npad % 256 == 0 only) and the 8-phase 256x256 kernel ("x", the
+    default for the launches l256 would take)."""
+    if request.param in ("l", "l256", "x"):
         monkeypatch.setenv("CVL_CONV_L_MIN_TILES", "1")
     if request.param == "l":
         monkeypatch.setenv("CVL_CONV_NO_256", "1")
-    if request.param == "l256":
+    if request.param in ("l256", "x"):
         monkeypatch.setenv("CVL_CONV_L256_MIN_TILES", "1")
-        monkeypatch.setenv("CVL_CONV_DGRAD_256", "1")
+    if request.param == "l256":
+        monkeypatch.setenv("CVL_CONV_NO_X", "1")
+    if request.param in ("l256", "x"):
+        pass
     else:
         monkeypatch.setenv("CVL_CONV_NO_L", "1")
         monkeypatch.setenv("CVL_WGRAD_NO_L", "1")

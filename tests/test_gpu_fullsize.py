@@ -135,6 +135,11 @@ def test_retinanet_step_configs4():
     (fcos_torch.focal(tb[..., 4:], c0) + fcos_torch.smooth_l1(tb[..., :4], r0, mask)).backward()
     gr = d_reg.double().cpu()[0, :, :4 * A].reshape(P, A, 4)
     gc = d_cls.double().cpu()[0, :, :A * C].reshape(P, A, C)
+    bad = ((gc - c0.grad).abs() > 1e-3 + 1e-2 * c0.grad.abs()).nonzero()
+    for (p_, a_, c_) in bad[:8].tolist():
+        print("mismatch cell %d anchor %d class %d: logit %r target %r kernel %r autograd %r" % (
+            p_, a_, c_, float(c0[p_, a_, c_]), float(tb[p_, a_, 4 + c_]), float(gc[p_, a_, c_]),
+            float(c0.grad[p_, a_, c_])))
     torch.testing.assert_close(gr, r0.grad, rtol=1e-2, atol=1e-2)       # bf16 gradient storage
     torch.testing.assert_close(gc, c0.grad, rtol=1e-2, atol=1e-3)
     assert torch.count_nonzero(d_cls[..., A * C:]).item() == 0
