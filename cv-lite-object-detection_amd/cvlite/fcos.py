@@ -35,16 +35,25 @@ def _as_tensor(x, dtype=torch.float32):
 
 class FCOSModel(object):
     """What build_model returns: model(x, training=True) -> list of 5 [B,S,S,5+C] fp32 tensors
-    (channels: t, b, l, r, centerness, C class logits), like the reference's Keras model."""
+    (channels: t, b, l, r, centerness, C class logits), like the reference's Keras model.
+    With autograd enabled and training=True the outputs are differentiable w.r.t.
+    `trainable_variables` (one torch_ops.NetFunction node: the explicit backward of the same
+    kernels the trainer runs), so `torch.autograd.grad(loss, model.trainable_variables)` plays
+    the role of the reference's GradientTape (FCOS/train_fcos.py:152-174)."""
 
     def __init__(self, num_classes, backbone_model="resnet50", seed=0):
         self.net = FCOSNet(num_classes, backbone_model=backbone_model, device=_dev(), seed=seed)
         self.num_classes = num_classes
+        self._vars = None
 
     def __call__(self, x, training=True):
         x = _as_tensor(x)
         B, H, W, _ = x.shape
-        reg, cls = self.net.forward(x, train=training)
+        if training and torch.is_grad_enabled():
+            from .torch_ops import NetFunction
+            reg, cls = NetFunction.apply(self.net, x, *self.trainable_variables)
+        else:
+            reg, cls = self.net.forward(x, train=training)
         shapes, off, P = self.net.layout(B, H, W)
         outs = []
         for l, (h, w) in enumerate(shapes):
@@ -55,8 +64,12 @@ class FCOSModel(object):
 
     @property
     def trainable_variables(self):
-        st = self.net.store
-        return [st.p(k) for k in st.offsets]
+        """Views of the flat fp32 parameter buffer, in Keras creation order (requires_grad leaves,
+        updated in place by the optimizer kernels)."""
+        if self._vars is None:
+            st = self.net.store
+            self._vars = [st.p(k).requires_grad_(True) for k in st.offsets]
+        return self._vars
 
 
 def build_model(num_classes, backbone_model="resnet50"):
@@ -106,17 +119,24 @@ def _packed_loss(targets, reg, cls, C, reg_type):
     return losses[0]
 
 
+def _as_pred(y):
+    """Predictions keep their autograd graph when they already are fp32 device tensors."""
+    if isinstance(y, torch.Tensor) and y.is_cuda and y.dtype == torch.float32:
+        return y
+    return _as_tensor(y)
+
+
 def model_loss(y_true, y_pred, strides, reg_type="l1", cen_type="l1", cls_lambda=2.5, reg_lambda=1.0):
     """fcos.py:464-496.  y_true: 5 maps [S,S,5+C]; y_pred: 5 tensors [1,S,S,5+C] (index [0], Q11).
     Returns (cls_loss, reg_loss, cen_loss) as 0-d fp32 device tensors; strides/lambdas unused
-    exactly as in the reference."""
+    exactly as in the reference.  Differentiable w.r.t. y_pred (torch.ops.cvlite.fcos_loss)."""
+    from . import torch_ops  # noqa: F401  (registers torch.ops.cvlite.*)
     t = torch.cat([_as_tensor(y).reshape(-1, y.shape[-1]) for y in y_true], 0)
-    p = torch.cat([_as_tensor(y)[0].reshape(-1, y.shape[-1]) for y in y_pred], 0)
+    p = torch.cat([_as_pred(y)[0].reshape(-1, y.shape[-1]) for y in y_pred], 0)
     C = t.shape[-1] - 5
-    reg = torch.zeros((1, p.shape[0], 8), dtype=torch.float32, device=p.device)
-    reg[0, :, :5] = p[:, :5]
+    reg = torch.nn.functional.pad(p[:, :5], (0, 3))[None].contiguous()
     cls = p[None, :, 5:].contiguous()
-    l = _packed_loss(t[None].contiguous(), reg, cls, C, "iou" if reg_type == "iou" else "l1")
+    l = torch.ops.cvlite.fcos_loss(reg, cls, t[None].contiguous(), C, 1 if reg_type == "iou" else 0)[0]
     cen = l[2] if cen_type.lower() == "l1" else torch.zeros((), device=p.device)
     return l[0], l[1], cen
 
