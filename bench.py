@@ -116,28 +116,42 @@ def tower_alg_bytes(B, net, H, W):
     return 2 * (2 * (2 * B * P) * 256) + 2 * (2 * 256 * 9 * 256)   # src + dst bf16, 2 towers' weights
 
 
-def cpu_baseline(H, W, n_img=2):
+def cpu_baseline(H, W, cfg1_images=8, bs=16, timed_images=(8, 8, 8)):
     """The torch-CPU restatement of the reference step (oracle/model_ref.py: batch-1 forwards,
-    per-image BN, gradient sum, /bs, clip, Keras SGD) on a bounded sample."""
+    per-image BN, gradient sum, /bs, clip, Keras SGD), SURVEY.md §8d protocol on a bounded sample:
+    BASELINE configs[0] (one step on 8 synthetic 512x512 images) as the warm-up, then three timed
+    steps (each 8 images of the bs=16 workload: per-image fwd+bwd is the whole cost, so images/s
+    does not depend on how a 16-image step is cut), img/s = median over the three.  Threads =
+    every core this process may run on (sched_getaffinity)."""
     from oracle import fcos_ref, model_ref
     import numpy as np
-    threads = torch.get_num_threads()
+    cores = len(os.sched_getaffinity(0))
+    torch.set_num_threads(cores)
     p = FCOSNet.param_dict(NUM_CLASSES, seed=0)
     moms = {k: torch.zeros_like(v) for k, v in p.items()}
-    imgs, boxes, nbox = synthetic_batch(n_img + 1, H, W, NUM_CLASSES, seed=99, device="cpu")
+    n = cfg1_images + sum(timed_images)
+    imgs, boxes, nbox = synthetic_batch(n, H, W, NUM_CLASSES, seed=99, device="cpu")
     tg = []
-    for b in range(n_img + 1):
+    for b in range(n):
         outs, _ = fcos_ref.format_data(boxes[b, :int(nbox[b])].numpy(), np.array([H, W], np.float32),
                                        NUM_CLASSES, img_pad=(H, W))
         tg.append(torch.from_numpy(fcos_ref.pack_targets(outs)))
     tg = torch.stack(tg)
-    model_ref.train_step_reference(p, moms, imgs[:1], tg[:1], NUM_CLASSES, 5e-4)   # warm-up image
     t0 = time.time()
-    model_ref.train_step_reference(p, moms, imgs[1:], tg[1:], NUM_CLASSES, 5e-4)
-    dt = time.time() - t0
-    return {"value": round(n_img / dt, 4), "unit": "images/s", "cores": threads, "kind": "port",
-            "sample": "torch-CPU fp32 restatement of train_fcos.py step (oracle/model_ref.py), one "
-                      "%d-image step at %dx%d (per-image fwd+bwd, clip, SGD), after a 1-image warm-up" % (n_img, H, W)}
+    model_ref.train_step_reference(p, moms, imgs[:cfg1_images], tg[:cfg1_images], NUM_CLASSES, 5e-4)
+    cfg1_s = time.time() - t0
+    rates, o = [], cfg1_images
+    for k in timed_images:
+        t0 = time.time()
+        model_ref.train_step_reference(p, moms, imgs[o:o + k], tg[o:o + k], NUM_CLASSES, 5e-4)
+        rates.append(k / (time.time() - t0))
+        o += k
+    return {"value": round(sorted(rates)[len(rates) // 2], 4), "unit": "images/s", "cores": cores,
+            "kind": "port", "configs0_step_s": round(cfg1_s, 3), "timed_img_s": [round(r, 4) for r in rates],
+            "sample": "torch-CPU fp32 restatement of the train_fcos.py step (oracle/model_ref.py): configs[0] "
+                      "(one step, %d synthetic %dx%d images, %.1f s) as warm-up, then 3 timed steps of 8 images "
+                      "of the bs=%d workload (per-image fwd+bwd, clip, SGD), median img/s, %d threads"
+                      % (cfg1_images, H, W, cfg1_s, bs, cores)}
 
 
 def bench_retinanet(args):

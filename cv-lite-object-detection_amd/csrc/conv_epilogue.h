@@ -55,7 +55,7 @@ __device__ __forceinline__ void conv_l_epilogue(const ConvArgs& a, const ConvSeg
       for (int e = 0; e < 4; ++e) {
         float v = acc[i][j][e] + bcol[j];
         if (a.relu_out) v = v > 0.f ? v : 0.f;
-        acc[i][j][e] = bf16_to_f32(f32_to_bf16(v));
+        acc[i][j][e] = (float)(__bf16)v;      // v_cvt_pk_bf16_f32: round to nearest even, NaN kept
       }
 
   // one image per tile: each wave reduces its rows (registers + lane shuffles), the WGM waves of a
@@ -113,7 +113,7 @@ __device__ __forceinline__ void conv_l_epilogue(const ConvArgs& a, const ConvSeg
       for (int e = 0; e < 4; ++e) {
         const int r = wm * WM + i * 16 + lg * 4 + e;
         const int c = wn * WN + j * 16 + lr;
-        Cs[r * CP + c] = f32_to_bf16(acc[i][j][e]);
+        Cs[r * CP + c] = __builtin_bit_cast(cvl_bf16, (__bf16)acc[i][j][e]);   // exact (already bf16)
       }
   float* sred = reinterpret_cast<float*>(lds + BM * CP);     // [WGM][BN][2]
   if (WGM > 2 && tile_stats) {
@@ -144,12 +144,20 @@ __device__ __forceinline__ void conv_l_epilogue(const ConvArgs& a, const ConvSeg
   }
   constexpr int CCH = BN / 8;
   cvl_bf16* dst = reinterpret_cast<cvl_bf16*>(a.dst);
+  // destination rows are the segment's rows in order (no channel interleave of images, no
+  // stride-2 scatter): the row index is base + ml, no per-row division
+  const bool dense = a.dst_up == 1 && S.dst_img == (long)HWr;
   for (int idx = tid; idx < BM * CCH; idx += NT) {
     const int r = idx / CCH, c8 = (idx - (idx / CCH) * CCH) * 8;
     const int ml = mloc0 + r;
     if (ml >= S.rows || n0 + c8 >= a.n_store) continue;
-    const int img = ml / HWr, q = ml - img * HWr;
-    const long drow = conv_dst_row(a, S, img, q);
+    long drow;
+    if (dense) {
+      drow = S.dst_base + ml;
+    } else {
+      const int img = ml / HWr, q = ml - img * HWr;
+      drow = conv_dst_row(a, S, img, q);
+    }
     s16x8 v = *reinterpret_cast<const s16x8*>(Cs + r * CP + c8);
     s16x8* pd = reinterpret_cast<s16x8*>(dst + drow * a.ld_dst + a.dst_coff + n0 + c8);
     if (a.beta != 0.f) {

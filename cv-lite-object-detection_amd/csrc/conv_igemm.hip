@@ -546,7 +546,8 @@ extern "C" const char* cvl_conv_kernel_name(int code) {
     case CVL_CK_L64: return "conv_igemm_l_kernel<64> (256x64)";
     case CVL_CK_L128: return "conv_igemm_l_kernel<128> (256x128)";
     case CVL_CK_L256: return "conv_igemm_l_kernel<256> (256x256)";
-    case CVL_CK_X256: return "conv_igemm_x_kernel (256x256, 8-phase)";
+    case CVL_CK_X256: return "conv_igemm_x_kernel (256x256, 4 phases per 64-deep K-tile)";
+    case CVL_CK_X32: return "conv_igemm_x32_kernel (256x256, 5-slot ring of 32-deep K-tiles)";
     default: return "none";
   }
 }

@@ -48,12 +48,14 @@ __device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t r, const cvl_bf16* 
                                            0, 0);
 }
 
-template <bool DGRAD>
+template <bool DGRAD, bool DBG>
 __global__ void __launch_bounds__(NT) conv_igemm_x_kernel(ConvArgs a) {
+  // DBG: ablation switches (a.dbg bits) for measurement builds only
+  const int dbg = DBG ? a.dbg : 0;
   __shared__ __attribute__((aligned(16))) cvl_bf16 lds[LDS_EL];
 
   const int tid = threadIdx.x;
-  const int wave = tid >> 6, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;   // wave-uniform
   const int ntn = a.Npad / BN;
   const int L = xcd_remap(blockIdx.x, gridDim.x);
   const int m_tile = L / ntn, n_tile = L % ntn;
@@ -85,15 +87,17 @@ __global__ void __launch_bounds__(NT) conv_igemm_x_kernel(ConvArgs a) {
     const int x0 = DGRAD ? ox + a.pad_l : ox * a.stride - a.pad_l;
     const long pix = S.src_base + (long)img * S.src_img + (long)y0 * Ws + x0;
     aoff[ai] = (unsigned)(pix * Cin * 2) + chs;
-    unsigned m = 0;
-    if (ml < S.rows) {
-      for (int t = 0; t < T; ++t) {
-        const int r = t / KW, s = t - (t / KW) * KW;
-        const int iy = DGRAD ? y0 - r : y0 + r, ix = DGRAD ? x0 - s : x0 + s;
-        if (iy >= 0 && iy < Hs && ix >= 0 && ix < Ws) m |= 1u << t;
-      }
+    // tap validity: bit r*KW + s set when source pixel (y0 +- r, x0 +- s) is inside the map
+    unsigned cm = 0, m = 0;
+    for (int s = 0; s < KW; ++s) {
+      const int ix = DGRAD ? x0 - s : x0 + s;
+      if (ix >= 0 && ix < Ws) cm |= 1u << s;
     }
-    amask[ai] = m;
+    for (int r = 0; r < a.KH; ++r) {
+      const int iy = DGRAD ? y0 - r : y0 + r;
+      if (iy >= 0 && iy < Hs) m |= cm << (r * KW);
+    }
+    amask[ai] = ml < S.rows ? m : 0u;
   }
   // B rows of this thread: n = p*128 + h*32 + (x8 >> 5)*64 + (x8 & 31) (U2: h = 0, U3: h = 1)
   const unsigned boff0 = (unsigned)((n0 + (x8 >> 5) * 64 + (x8 & 31)) * Kdim * 2) + chs;
@@ -101,43 +105,46 @@ __global__ void __launch_bounds__(NT) conv_igemm_x_kernel(ConvArgs a) {
   const __amdgpu_buffer_rsrc_t rsB = __builtin_amdgcn_make_buffer_rsrc((void*)S.w, (short)0, (int)kRecords, 0x00020000);
   const int brow_w = (wave >> 2) * 64 + (wave & 3) * 8;     // first LDS B row of this wave's pieces
 
-  // K-tile kt -> (channel block cb, tap): channel-block-major, tap-minor
-  auto tap_of = [&](int kt, int& tap, unsigned& aoffk, unsigned& boffk) {
-    const int cb = kt / T;
-    tap = kt - cb * T;
-    const int r = tap / KW, s = tap - (tap / KW) * KW;
-    const int d = r * Ws + s;
-    aoffk = (unsigned)((DGRAD ? -d : d) * Cin * 2 + cb * 128);
-    boffk = (unsigned)((tap * Cin + cb * 64) * 2);
+  // K-tiles run channel-block-major, tap-minor.  The issue cursor (K-tile kc, its tap (r, s),
+  // channel block cb and the wave-uniform A / B byte offsets) advances by one K-tile per loop
+  // iteration with a few scalar ops (no divisions in the loop).
+  const int dsgn = DGRAD ? -1 : 1;
+  int kc = 0, ctap = 0, cr = 0, cs = 0, ccb = 0;
+  bool clive = nk > 0;
+  unsigned cak = 0, cbk = 0;          // A / B byte offsets of the cursor's K-tile
+  auto advance = [&]() {
+    ++kc;
+    ++ctap;
+    if (++cs == KW) { cs = 0; ++cr; }
+    if (ctap == T) { ctap = 0; cr = 0; cs = 0; ++ccb; }
+    clive = kc < nk;
+    cak = (unsigned)(dsgn * (cr * Ws + cs) * Cin * 2 + ccb * 128);
+    cbk = (unsigned)((ctap * Cin + ccb * 64) * 2);
   };
   // one unit = 2 LDS-DMA instructions per thread; K-tiles past the end issue out-of-range (zero,
   // no memory traffic) loads so every wait keeps the same count
-  auto issueA = [&](int kt, int h, cvl_bf16* buf) {
-    int tap = 0;
-    unsigned ak = 0, bk = 0;
-    const bool live = kt < nk;
-    if (live) tap_of(kt, tap, ak, bk);
+  auto issueA = [&](int h, cvl_bf16* buf) {
+    if (dbg & 32) return;
 #pragma unroll
     for (int p = 0; p < 2; ++p) {
       const int ai = 2 * p + h;
-      const bool v = live && ((amask[ai] >> tap) & 1u);
-      dma16(rsA, buf + (p * 128 + h * 64 + wave * 8) * BK, (v && !(a.dbg & 1)) ? aoff[ai] + ak : kOOB);
+      const bool v = clive && ((amask[ai] >> ctap) & 1u) && !(dbg & 1);
+      dma16(rsA, buf + (p * 128 + h * 64 + wave * 8) * BK, v ? aoff[ai] + cak : kOOB);
     }
   };
-  auto issueB = [&](int kt, int h, cvl_bf16* buf) {
-    int tap = 0;
-    unsigned ak = 0, bk = 0;
-    const bool live = kt < nk;
-    if (live) tap_of(kt, tap, ak, bk);
+  auto issueB = [&](int h, cvl_bf16* buf) {
+    if (dbg & 32) return;
+    const bool live = clive && !(dbg & 2);
 #pragma unroll
     for (int p = 0; p < 2; ++p)
       dma16(rsB, buf + OPND + (p * 128 + h * 32 + brow_w) * BK,
-            (live && !(a.dbg & 2)) ? boff0 + (unsigned)((p * 128 + h * 32) * Kdim * 2) + bk : kOOB);
+            live ? boff0 + (unsigned)((p * 128 + h * 32) * Kdim * 2) + cbk : kOOB);
   };
 
   const int wm = wave >> 2, wn = wave & 3;
   const int lr = lane & 15, lg = lane >> 4;
   auto readA = [&](s16x8 (&ra)[4][2], int h, const cvl_bf16* buf) {
+    if (dbg & 64) return;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int r = wm * WM + h * 64 + i * 16 + lr;
@@ -147,6 +154,7 @@ __global__ void __launch_bounds__(NT) conv_igemm_x_kernel(ConvArgs a) {
     }
   };
   auto readB = [&](s16x8 (&rb)[2][2], int h, const cvl_bf16* buf) {
+    if (dbg & 64) return;
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
       const int r = wn * WN + h * 32 + j * 16 + lr;
@@ -161,7 +169,7 @@ __global__ void __launch_bounds__(NT) conv_igemm_x_kernel(ConvArgs a) {
 #pragma unroll
     for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
   auto mfma_q = [&](const s16x8 (&ra)[4][2], const s16x8 (&rb)[2][2], int rh, int chh) {
-    if (a.dbg & 4) {
+    if (dbg & 4) {
       asm volatile("" ::"v"(ra[0][0]), "v"(rb[0][0]));
       return;
     }
@@ -179,57 +187,223 @@ __global__ void __launch_bounds__(NT) conv_igemm_x_kernel(ConvArgs a) {
     __builtin_amdgcn_s_setprio(0);
     __builtin_amdgcn_sched_barrier(0);
   };
-  // phase entry: this wave's DMA of the unit read next has landed and its previous LDS reads have
-  // retired (WAR for the unit restaged after the barrier); then every wave's
-  auto sync = [&]() {
-    if (!(a.dbg & 16)) wait_vm<6>();
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    if (!(a.dbg & 8)) __builtin_amdgcn_s_barrier();
+  auto bar = [&]() {
+    if (!(dbg & 8)) __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
+  };
+  auto waitv = [&]() {
+    if (!(dbg & 16)) wait_vm<6>();
+  };
+  // phase = [load segment: wait, issue one unit, LDS reads] barrier [MFMA segment] barrier.  The
+  // two wave groups (waves 0-3, 4-7: one wave of each per SIMD) run one barrier apart, so each
+  // SIMD's MFMA segment of one group overlaps the load segment of the other.  Hence a unit is
+  // waited for (vmcnt, each wave its own part) one phase BEFORE it is read, and an LDS region is
+  // restaged at least two phases after its last read.
+  auto mma = [&](const s16x8 (&ra)[4][2], const s16x8 (&rb)[2][2], int rh, int chh) {
+    bar();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    mfma_q(ra, rb, rh, chh);
+    bar();
   };
 
   cvl_bf16* X = lds;            // buffer of the current K-tile
   cvl_bf16* Y = lds + BUF;      // buffer of the next one
-  s16x8 RA0[4][2], RA1[4][2], RBf[2][2], RBs[2][2];
+  s16x8 RA0[4][2], RA1[4][2], RB0[2][2], RB1[2][2];
 
-  // prologue: K-tile 0 complete (U1..U4) and K-tile 1's U1, U2 in flight, then K-tile 0's A-first
-  issueA(0, 0, X);
-  issueB(0, 0, X);
-  issueB(0, 1, X);
-  issueA(0, 1, X);
-  issueA(1, 0, Y);
-  issueB(1, 0, Y);
+  // prologue: K-tile 0's four units and K-tile 1's U1, U2 (steady state: issued in phases 3, 4
+  // of K-tile -1); then everyone has U1, U2 of K-tile 0
+  issueA(0, X);
+  issueB(0, X);
+  issueB(1, X);
+  issueA(1, X);
+  advance();
+  issueA(0, Y);
+  issueB(0, Y);
   wait_vm<8>();
   __builtin_amdgcn_s_barrier();
   asm volatile("" ::: "memory");
-  readA(RA0, 0, X);
+  if (wm == 1) bar();           // stagger: waves 4-7 run one barrier behind
 
-  // per K-tile: phase 1 (0,0) reads B-first (on demand) and prefetches B-second; phase 2 (0,1)
-  // prefetches A-second; phase 3 (1,1) re-reads B-first; phase 4 (1,0) prefetches the next
-  // K-tile's A-first.  Units of K-tile kt+1 go into Y in phases 1-2 (U3, U4); units U1, U2 of
-  // K-tile kt+2 go into X in phases 3-4, after X's reads for phases <= 2 (U1, U4, U3) and, at the
-  // phase-4 barrier, phase 3's re-read of U2 have retired in every wave.
-  for (int kt = 0; kt < nk; ++kt) {
-    sync();                                   // X.U2, X.U3 landed (X.U2 already for the prologue)
-    issueB(kt + 1, 1, Y);                     // Y.U3
-    readB(RBf, 0, X);
-    readB(RBs, 1, X);
-    mfma_q(RA0, RBf, 0, 0);
-    sync();                                   // X.U4 landed
-    issueA(kt + 1, 1, Y);                     // Y.U4
+  // per K-tile (buffer X), units issued: ph1 U3 -> Y (next K-tile), ph2 U4 -> Y, ph3 U1 -> X and
+  // ph4 U2 -> X (K-tile after next: X's U1 / U2 were last read in ph1, two phases before);
+  // reads: ph1 A-first + B-first, ph2 B-second, ph3 A-second, ph4 none (B-first kept)
+  for (int kt = 0; kt < ((dbg & 256) ? 0 : nk); ++kt) {
+    waitv();                                  // X.U3 of this K-tile (read in ph2)
+    issueB(1, Y);                             // Y.U3
+    readA(RA0, 0, X);
+    readB(RB0, 0, X);
+    mma(RA0, RB0, 0, 0);
+    waitv();                                  // X.U4 (read in ph3)
+    issueA(1, Y);                             // Y.U4
+    readB(RB1, 1, X);
+    mma(RA0, RB1, 0, 1);
+    advance();                                // the cursor moves to K-tile kt+2
+    issueA(0, X);                             // X.U1
     readA(RA1, 1, X);
-    mfma_q(RA0, RBs, 0, 1);
-    issueA(kt + 2, 0, X);                     // X.U1: its reads retired before phase 2's barrier
-    readB(RBf, 0, X);
-    mfma_q(RA1, RBs, 1, 1);
-    sync();                                   // Y.U1, Y.U2 landed; phase 3's X.U2 reads retired
-    issueB(kt + 2, 0, X);                     // X.U2
-    if (kt + 1 < nk) readA(RA0, 0, Y);
-    mfma_q(RA1, RBf, 1, 0);
+    mma(RA1, RB1, 1, 1);
+    waitv();                                  // Y.U1, Y.U2 of K-tile kt+1 (read in its ph1)
+    issueB(0, X);                             // X.U2
+    mma(RA1, RB0, 1, 0);
     cvl_bf16* t = X;
     X = Y;
     Y = t;
   }
+  if (wm == 0) bar();           // equal barrier counts for both groups
+  wait_vm<0>();
+  if (dbg & 128) {
+    if (acc[0][0][0] == 12345.f) a.stats[0] = 1.0;      // keep the accumulators live
+    return;
+  }
+  conv_l_epilogue<BN, WGM, TM, TN, NT>(a, S, acc, lds, tid, wm, wn, n0, mloc0, HWr);
+}
+
+
+// ---------------------------------------------------------------------------------------------
+// X32: the same 256 x 256 tile with 32-deep K-tiles in a 5-slot LDS ring (5 x 32 KiB = the whole
+// 160 KiB LDS) and ONE phase per K-tile: each phase multiplies the wave's whole 128 x 64 block
+// over K = 32 (32 MFMAs, twice the MFMA work per barrier pair of the 4-phase schedule above).
+// Phase t: [wait for K-tile t+1 (own DMA, vmcnt(4)); issue K-tile t+3 into the slot K-tile t-2
+// used; read K-tile t's fragments] barrier [32 MFMAs] barrier.  The two wave groups run one
+// barrier apart (each SIMD alternates one wave's MFMA segment with the other's load segment), so a
+// K-tile is waited for one phase before it is read and a slot is refilled two phases after its
+// last read.  Operand images: 64-B rows, chunk swizzle (r >> 1) & 3 (conflict-free fragment reads).
+// ---------------------------------------------------------------------------------------------
+constexpr int BK32 = 32;
+constexpr int SLOT = 2 * 256 * BK32;      // bf16 elements per ring slot (A + B, 32 KiB)
+constexpr int NSLOT = 5;
+constexpr int LDS32_EL = NSLOT * SLOT > LDS_C ? NSLOT * SLOT : LDS_C;
+
+__device__ __forceinline__ int swz4(int r) { return (r >> 1) & 3; }
+
+template <bool DGRAD>
+__global__ void __launch_bounds__(NT) conv_igemm_x32_kernel(ConvArgs a) {
+  __shared__ __attribute__((aligned(16))) cvl_bf16 lds[LDS32_EL];
+
+  const int tid = threadIdx.x;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
+  const int ntn = a.Npad / BN;
+  const int L = xcd_remap(blockIdx.x, gridDim.x);
+  const int m_tile = L / ntn, n_tile = L % ntn;
+  const int m0 = m_tile * BM, n0 = n_tile * BN;
+  int sg = 0;
+#pragma unroll
+  for (int i = 1; i < kMaxSeg; ++i)
+    if (i < a.nseg && m0 >= a.seg[i].m_start) sg = i;
+  const ConvSeg& S = a.seg[sg];
+  const int HWr = S.Hr * S.Wr;
+  const int mloc0 = m0 - S.m_start;
+  if (mloc0 >= S.rows) return;
+
+  const int Cin = a.Cin, KW = a.KW, T = a.KH * a.KW, Ws = S.Ws, Hs = S.Hs;
+  const int Kdim = a.K;
+  const int nk = Kdim / BK32;
+  // DMA piece of this lane: row x16 of a 128-row block, 16-B chunk ch of the 64-B row
+  const int x16 = wave * 16 + (lane >> 2), ch = lane & 3;
+  const unsigned chs = (unsigned)((ch ^ swz4(x16)) * 16);
+  unsigned aoff[2], amask[2];
+#pragma unroll
+  for (int p = 0; p < 2; ++p) {
+    const int ml = mloc0 + p * 128 + x16;
+    const int img = ml / HWr, q = ml - img * HWr;
+    const int oy = q / S.Wr, ox = q - (q / S.Wr) * S.Wr;
+    const int y0 = DGRAD ? oy + a.pad_t : oy * a.stride - a.pad_t;
+    const int x0 = DGRAD ? ox + a.pad_l : ox * a.stride - a.pad_l;
+    const long pix = S.src_base + (long)img * S.src_img + (long)y0 * Ws + x0;
+    aoff[p] = (unsigned)(pix * Cin * 2) + chs;
+    unsigned cm = 0, m = 0;
+    for (int s = 0; s < KW; ++s) {
+      const int ix = DGRAD ? x0 - s : x0 + s;
+      if (ix >= 0 && ix < Ws) cm |= 1u << s;
+    }
+    for (int r = 0; r < a.KH; ++r) {
+      const int iy = DGRAD ? y0 - r : y0 + r;
+      if (iy >= 0 && iy < Hs) m |= cm << (r * KW);
+    }
+    amask[p] = ml < S.rows ? m : 0u;
+  }
+  const unsigned boff0 = (unsigned)((n0 + x16) * Kdim * 2) + chs;
+  const __amdgpu_buffer_rsrc_t rsA = __builtin_amdgcn_make_buffer_rsrc((void*)a.src, (short)0, (int)kRecords, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rsB = __builtin_amdgcn_make_buffer_rsrc((void*)S.w, (short)0, (int)kRecords, 0x00020000);
+
+  // issue cursor: K-tile kc = (channel block ccb of 32, tap ctap = (cr, cs)), channel-block-major
+  const int dsgn = DGRAD ? -1 : 1;
+  int kc = 0, ctap = 0, cr = 0, cs = 0, ccb = 0, cslot = 0;
+  unsigned cak = 0, cbk = 0;
+  auto issue = [&]() {
+    const bool live = kc < nk;
+    cvl_bf16* Ab = lds + cslot * SLOT;
+    cvl_bf16* Bb = Ab + 256 * BK32;
+#pragma unroll
+    for (int p = 0; p < 2; ++p) {
+      const bool v = live && ((amask[p] >> ctap) & 1u);
+      dma16(rsA, Ab + (p * 128 + wave * 16) * BK32, v ? aoff[p] + cak : kOOB);
+    }
+#pragma unroll
+    for (int p = 0; p < 2; ++p)
+      dma16(rsB, Bb + (p * 128 + wave * 16) * BK32, live ? boff0 + (unsigned)(p * 128 * Kdim * 2) + cbk : kOOB);
+    // advance the cursor
+    ++kc;
+    cslot = cslot == NSLOT - 1 ? 0 : cslot + 1;
+    ++ctap;
+    if (++cs == KW) { cs = 0; ++cr; }
+    if (ctap == T) { ctap = 0; cr = 0; cs = 0; ++ccb; }
+    cak = (unsigned)(dsgn * (cr * Ws + cs) * Cin * 2 + ccb * 64);
+    cbk = (unsigned)((ctap * Cin + ccb * 32) * 2);
+  };
+
+  const int wm = wave >> 2, wn = wave & 3;
+  const int lr = lane & 15, lg = lane >> 4;
+  f32x4 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  auto bar = [&]() {
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+  };
+
+  issue();
+  issue();
+  issue();
+  wait_vm<8>();
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+  if (wm == 1) bar();           // stagger: waves 4-7 run one barrier behind
+
+  int rslot = 0;
+  for (int kt = 0; kt < nk; ++kt) {
+    wait_vm<4>();                                 // K-tile kt+1 (read next phase)
+    issue();                                      // K-tile kt+3
+    const cvl_bf16* Ac = lds + rslot * SLOT;
+    const cvl_bf16* Bc = Ac + 256 * BK32;
+    s16x8 fa[TM], fb[TN];
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      const int r = wm * WM + i * 16 + lr;
+      fa[i] = *reinterpret_cast<const s16x8*>(Ac + r * BK32 + ((lg ^ swz4(r)) * 8));
+    }
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int r = wn * WN + j * 16 + lr;
+      fb[j] = *reinterpret_cast<const s16x8*>(Bc + r * BK32 + ((lg ^ swz4(r)) * 8));
+    }
+    bar();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, fa[i]),
+                                                             __builtin_bit_cast(bf16x8, fb[j]), acc[i][j], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+    __builtin_amdgcn_sched_barrier(0);
+    bar();
+    rslot = rslot == NSLOT - 1 ? 0 : rslot + 1;
+  }
+  if (wm == 0) bar();           // equal barrier counts for both groups
   wait_vm<0>();
   conv_l_epilogue<BN, WGM, TM, TN, NT>(a, S, acc, lds, tid, wm, wn, n0, mloc0, HWr);
 }
@@ -241,7 +415,8 @@ __global__ void __launch_bounds__(NT) conv_igemm_x_kernel(ConvArgs a) {
 int cvl_conv_igemm_x(const cvl_conv_desc* d, const ConvArgs& a, hipStream_t s) {
   if (cvl_env_flag("CVL_CONV_NO_X")) return -1;
   const bool dg = d->mode == CVL_CONV_DGRAD;
-  if (a.Npad % BN || a.Cin % 64 || a.K / BK < 1 || d->KH * d->KW > 32 || a.relu_in ||
+  const bool x32 = !cvl_env_flag("CVL_CONV_NO_X32");
+  if (a.Npad % BN || a.Cin % (x32 ? 32 : 64) || a.K / BK < 1 || d->KH * d->KW > 32 || a.relu_in ||
       (dg && d->stride != 1) || a.dst_up != 1)
     return -1;
   // every source / weight byte offset must stay below the buffer-resource bound
@@ -254,7 +429,16 @@ int cvl_conv_igemm_x(const cvl_conv_desc* d, const ConvArgs& a, hipStream_t s) {
   ConvArgs am = a;
   am.dbg = cvl_env_int("CVL_X_ABLATE", 0);
   g_cvl_conv_last_kernel = CVL_CK_X256;
-  if (dg) hipLaunchKernelGGL((conv_igemm_x_kernel<true>), grid, dim3(NT), 0, s, am);
-  else hipLaunchKernelGGL((conv_igemm_x_kernel<false>), grid, dim3(NT), 0, s, am);
+  if (x32 && !am.dbg) {
+    g_cvl_conv_last_kernel = CVL_CK_X32;
+    if (dg) hipLaunchKernelGGL((conv_igemm_x32_kernel<true>), grid, dim3(NT), 0, s, am);
+    else hipLaunchKernelGGL((conv_igemm_x32_kernel<false>), grid, dim3(NT), 0, s, am);
+  } else if (am.dbg) {
+    if (dg) hipLaunchKernelGGL((conv_igemm_x_kernel<true, true>), grid, dim3(NT), 0, s, am);
+    else hipLaunchKernelGGL((conv_igemm_x_kernel<false, true>), grid, dim3(NT), 0, s, am);
+  } else {
+    if (dg) hipLaunchKernelGGL((conv_igemm_x_kernel<true, false>), grid, dim3(NT), 0, s, am);
+    else hipLaunchKernelGGL((conv_igemm_x_kernel<false, false>), grid, dim3(NT), 0, s, am);
+  }
   return cvl_launch_status();
 }

@@ -17,7 +17,7 @@ import torch
 
 from . import ops_nn as nn
 from .layers import BF16, Conv, ParamStore
-from .resnet import ResNet50
+from .resnet import DEPTHS, ResNet50
 
 FPN_C = 256
 STRIDES = (8, 16, 32, 64, 128)
@@ -31,8 +31,10 @@ FUSE_FPN = os.environ.get("CVL_FPN_FUSE", "1") != "0"
 
 class FPNDetector(object):
     def _init_common(self, num_classes, backbone_model, device, seed):
-        if backbone_model.lower() != "resnet50":
-            raise NotImplementedError("cvlite implements the resnet50 backbone of build_model")
+        if backbone_model.lower() not in DEPTHS:
+            raise NotImplementedError("cvlite implements the %s backbones of build_model, not %r"
+                                      % ("/".join(DEPTHS), backbone_model))
+        self.backbone_model = backbone_model.lower()
         self.C = num_classes
         self.store = st = ParamStore()
         self._build_layers(st, num_classes)
@@ -47,7 +49,7 @@ class FPNDetector(object):
         # creation order follows build_model: towers, backbone, FPN, heads
         self.cls_tower = [Conv(st, "cls_layer_%d" % (i + 1), 3, FPN_C, FPN_C, bias=False) for i in range(4)]
         self.reg_tower = [Conv(st, "reg_layer_%d" % (i + 1), 3, FPN_C, FPN_C, bias=False) for i in range(4)]
-        self.backbone = ResNet50(st)
+        self.backbone = ResNet50(st, getattr(self, "backbone_model", "resnet50"))
         self.c3_1x1 = Conv(st, "c3_1x1", 1, 512, FPN_C)
         self.c4_1x1 = Conv(st, "c4_1x1", 1, 1024, FPN_C)
         self.c5_1x1 = Conv(st, "c5_1x1", 1, 2048, FPN_C)
@@ -59,9 +61,10 @@ class FPNDetector(object):
         self._build_heads(st, num_classes)
 
     @classmethod
-    def param_dict(cls, num_classes, seed=0):
+    def param_dict(cls, num_classes, seed=0, backbone_model="resnet50"):
         """The initial parameters (Keras names -> CPU fp32) without touching a GPU."""
         obj = cls.__new__(cls)
+        obj.backbone_model = backbone_model.lower()
         st = ParamStore()
         obj._build_layers(st, num_classes)
         st.finalize("cpu", seed)

@@ -118,10 +118,21 @@ class Bottleneck(object):
         return dx_out
 
 
+# Keras applications ResNet v1 depths (block counts of conv2_x .. conv5_x); the detectors tap the
+# last block of conv3_x / conv4_x / conv5_x (RetinaNet/retinanet_module.py:32-52:
+# conv3_block4_out / conv4_block23_out for ResNet101, conv3_block8_out / conv4_block36_out for
+# ResNet152; FCOS/fcos.py:30-35 for ResNet50)
+DEPTHS = {"resnet50": (3, 4, 6, 3), "resnet101": (3, 4, 23, 3), "resnet152": (3, 8, 36, 3)}
+
+
 class ResNet50(object):
+    """Keras ResNet50 / ResNet101 / ResNet152 (v1 bottleneck stacks; `depth` picks the block
+    counts, the class name is kept for the default)."""
     STACKS = ((64, 3, 1), (128, 4, 2), (256, 6, 2), (512, 3, 2))
 
-    def __init__(self, store):
+    def __init__(self, store, depth="resnet50"):
+        blocks = DEPTHS[depth.lower()]
+        self.STACKS = tuple((f, nb, st) for (f, _, st), nb in zip(ResNet50.STACKS, blocks))
         self.stem = Stem(store)
         self.stages = []
         cin = 64

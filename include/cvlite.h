@@ -131,7 +131,7 @@ int cvl_conv_igemm(const cvl_conv_desc* d, const void* src, void* dst, double* b
 /* Test / profiling hook: the kernel variant the last cvl_conv_igemm call on THIS host thread
  * launched.  CVL_CK_* codes; cvl_conv_kernel_name(code) is a static string. */
 enum { CVL_CK_NONE = 0, CVL_CK_BASE = 1, CVL_CK_BASE_SPLITK = 2, CVL_CK_L64 = 3, CVL_CK_L128 = 4,
-       CVL_CK_L256 = 5, CVL_CK_X256 = 6 };
+       CVL_CK_L256 = 5, CVL_CK_X256 = 6, CVL_CK_X32 = 7 };
 int cvl_conv_igemm_last_kernel(void);
 const char* cvl_conv_kernel_name(int code);
 

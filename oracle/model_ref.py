@@ -118,12 +118,26 @@ def bn(x, p, name, eps=1.001e-5):
     return (x - m) / torch.sqrt(v + eps) * g + b
 
 
+def _depths(p):
+    """Block counts of conv2_x..conv5_x present in the parameter dict (ResNet50 3/4/6/3,
+    ResNet101 3/4/23/3, ResNet152 3/8/36/3 -- Keras applications v1)."""
+    out = []
+    for st in range(2, 6):
+        n = 0
+        while "conv%d_block%d_1_conv/kernel" % (st, n + 1) in p:
+            n += 1
+        out.append(n)
+    return tuple(out)
+
+
 def resnet50(x, p):
+    """Keras ResNet50 / 101 / 152 v1 (depth read from the parameter names)."""
     h = conv(x, p, "conv1_conv", 2, pad=3)
     h = q(F.relu(bn(h, p, "conv1_bn")))
     h = F.max_pool2d(F.pad(h, (1, 1, 1, 1)), 3, 2)          # ZeroPadding2D(1) + MaxPool (zeros pad)
     taps = []
-    for si, (f, nb, stride) in enumerate(((64, 3, 1), (128, 4, 2), (256, 6, 2), (512, 3, 2))):
+    nbs = _depths(p)
+    for si, (f, nb, stride) in enumerate(((64, nbs[0], 1), (128, nbs[1], 2), (256, nbs[2], 2), (512, nbs[3], 2))):
         for bi in range(nb):
             n = "conv%d_block%d" % (si + 2, bi + 1)
             s = stride if bi == 0 else 1

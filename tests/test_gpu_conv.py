@@ -29,21 +29,23 @@ def ref_conv(x, w, b, stride, pad):
     return y.permute(0, 2, 3, 1)
 
 
-@pytest.fixture(params=["base", "l", "l256", "x"])
+@pytest.fixture(params=["base", "l", "l256", "x", "x32"])
 def kern(request, monkeypatch):
     """Run a test through the 128-row register-staged kernel ("base"), the 256-row LDS-DMA kernel
     ("l", normally taken only by launches with >= 128 tiles; 128/64-wide N tiles), its
     256x256-tile form ("l256", Npad % 256 == 0 only) and the 8-phase 256x256 kernel ("x", the
-    default for the launches l256 would take)."""
-    if request.param in ("l", "l256", "x"):
+    alternative for the launches l256 would take) and its 32-deep-K ring form ("x32", the default)."""
+    if request.param in ("l", "l256", "x", "x32"):
         monkeypatch.setenv("CVL_CONV_L_MIN_TILES", "1")
     if request.param == "l":
         monkeypatch.setenv("CVL_CONV_NO_256", "1")
-    if request.param in ("l256", "x"):
+    if request.param in ("l256", "x", "x32"):
         monkeypatch.setenv("CVL_CONV_L256_MIN_TILES", "1")
     if request.param == "l256":
         monkeypatch.setenv("CVL_CONV_NO_X", "1")
-    if request.param in ("l256", "x"):
+    if request.param == "x":
+        monkeypatch.setenv("CVL_CONV_NO_X32", "1")
+    if request.param in ("l256", "x", "x32"):
         pass
     else:
         monkeypatch.setenv("CVL_CONV_NO_L", "1")

@@ -92,7 +92,7 @@ def test_tower_pair_fwd_dgrad_configs1_layout():
     nn.conv_igemm(d, src, out)
     code, name = last_kernel()
     print("forward kernel:", name)
-    assert code in (5, 6), name          # the 256x256 LDS-DMA tile the bench's roofline names
+    assert code in (5, 6, 7), name          # the 256x256 LDS-DMA tile the bench's roofline names
     srcd = src.to(F64)
     for t in range(2):
         for l, (h, w) in enumerate(shapes):
@@ -112,7 +112,7 @@ def test_tower_pair_fwd_dgrad_configs1_layout():
     nn.conv_igemm(dd, dy, dx)
     code, name = last_kernel()
     print("dgrad kernel:", name)
-    assert code in (5, 6), name
+    assert code in (5, 6, 7), name
     dyd = dy.to(F64)
     for t in range(2):
         for l, (h, w) in enumerate(shapes):
@@ -138,7 +138,7 @@ def test_wide_1x1_with_bn_stats_configs1():
     nn.conv_igemm(d, x, out, stats)
     code, name = last_kernel()
     print("kernel:", name)
-    assert code in (5, 6), name
+    assert code in (5, 6, 7), name
     ref = conv_ref(x.to(F64), w, pt=0, pl=0) + bias.to(F64)
     torch.testing.assert_close(out.to(F64), ref, rtol=1e-2, atol=1e-2)
     o = out.to(F64)
@@ -165,7 +165,7 @@ def test_retina_cls_head_f32_epilogue_configs4():
     nn.conv_igemm(d, act, out)
     code, name = last_kernel()
     print("head kernel:", name)
-    assert code in (4, 5, 6), name      # an LDS-DMA large tile (fp32-destination epilogue)
+    assert code in (4, 5, 6, 7), name      # an LDS-DMA large tile (fp32-destination epilogue)
     a64 = act.to(F64)
     for l, (h, w) in enumerate(shapes):
         x = a64[B * off[l]:B * (off[l] + h * w)].view(B, h, w, C)

@@ -169,13 +169,17 @@ def test_backbone_inference_uses_moving_stats():
         assert torch.equal(bn.run_mean.cpu(), moving[bn.name][0]) and torch.equal(bn.run_var.cpu(), moving[bn.name][1])
 
 
-def test_backbone_blocks_match_fp32_oracle_with_synced_inputs():
-    """Every ResNet-50 block (conv + per-image BN + residual + ReLU, fwd) vs the plain fp32 oracle,
-    each fed the oracle's own input: isolates kernel error from the graph's chaotic amplification."""
+@pytest.mark.parametrize("backbone", ["resnet50", "resnet101"])
+def test_backbone_blocks_match_fp32_oracle_with_synced_inputs(backbone):
+    """Every ResNet-50 / ResNet-101 block (conv + per-image BN + residual + ReLU, fwd) vs the plain
+    fp32 oracle, each fed the oracle's own input: isolates kernel error from the graph's chaotic
+    amplification.  (ResNet-101: retinanet_module.py:39-45, the backbone of
+    train_retinanet_coco.py:347; taps conv4_block23_out.)"""
     import torch.nn.functional as F
     from cvlite.fcos_net import FCOSNet
     C, B, D = 20, 2, 256
-    net = FCOSNet(C, seed=1)
+    net = FCOSNet(C, seed=1, backbone_model=backbone)
+    assert len(net.backbone.stages[2]) == (23 if backbone == "resnet101" else 6)
     p = net.store.state_dict()
     rng = np.random.default_rng(3)
     x = torch.from_numpy(rng.uniform(-1, 1, size=(B, D, D, 3)).astype(np.float32))

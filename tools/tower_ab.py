@@ -13,8 +13,8 @@ import bench  # noqa: E402
 from cvlite import _lib, ops_nn as nn  # noqa: E402
 from cvlite.fcos_net import FCOSNet  # noqa: E402
 
-VARIANTS = {"L256": {"CVL_CONV_NO_X": "1"}, "X": {}}
-KEYS = ("CVL_CONV_NO_X",)
+VARIANTS = {"L256": {"CVL_CONV_NO_X": "1"}, "X": {"CVL_CONV_NO_X32": "1"}, "X32": {}}
+KEYS = ("CVL_CONV_NO_X", "CVL_CONV_NO_X32")
 
 
 def run(fn, iters):
@@ -52,8 +52,10 @@ def main():
             outs[(name, m)] = dst
             print(name, m, "->", lib.cvl_conv_kernel_name(lib.cvl_conv_igemm_last_kernel()).decode(), flush=True)
     for m in ("fwd", "dgrad"):
-        a, b = outs[("L256", m)].float(), outs[("X", m)].float()
-        print("%s max|X-L| %.4g (max|L| %.3g)" % (m, float((a - b).abs().max()), float(a.abs().max())), flush=True)
+        for v in VARIANTS:
+            a, b = outs[("L256", m)].float(), outs[(v, m)].float()
+            print("%s max|%s-L256| %.4g (max|L| %.3g)" % (m, v, float((a - b).abs().max()), float(a.abs().max())),
+                  flush=True)
     res = {k: {"fwd": [], "dgrad": []} for k in VARIANTS}
     dst = torch.empty_like(src)
     for r in range(rounds):

@@ -1,5 +1,6 @@
 """Ablation timings of the X conv kernel on the paired FCOS tower layer (forward): CVL_X_ABLATE
-bits 1 = no A traffic, 2 = no B traffic, 4 = no MFMA, 8 = no barriers, 16 = no vmcnt waits
+bits 1 = no A traffic, 2 = no B traffic, 4 = no MFMA, 8 = no barriers, 16 = no vmcnt waits,
+32 = no LDS-DMA instructions, 64 = no LDS fragment reads
 (results are wrong for every non-zero setting: timing insight only).  Interleaved rounds."""
 import os
 import sys
