@@ -28,6 +28,28 @@ __device__ __forceinline__ void wait_vm() {
   __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | (7 << 4) | (15 << 8));
 }
 
+// ds_read_b64_tr_b16 (gfx950 transposed LDS read, 4 rows x 16 bf16 columns per 16-lane group) as
+// inline asm, address = LDS byte address.  Through the builtin, the compiler's waitcnt pass cannot
+// tell the read from LDS-DMA writes still in flight and drains vmcnt(0) before every read, which
+// empties a DMA ring each step.  The compiler does not track these reads, so a caller orders its
+// DMA itself (counted vmcnt + barriers) and, after the reads, calls lgkm_wait() and then tr_pin() on
+// every result: the pins are volatile asm ordered after the wait and every use (copies included)
+// depends on a pin, so nothing reads a fragment register before the data landed.
+__device__ __forceinline__ s16x4 ds_tr16(unsigned addr) {
+  s16x4 v;
+  asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(v) : "v"(addr));
+  return v;
+}
+__device__ __forceinline__ void lgkm_wait() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+__device__ __forceinline__ void tr_pin(s16x4& v) { asm volatile("" : "+v"(v)); }
+__device__ __forceinline__ s16x8 tr_join(s16x4 l, s16x4 h) {
+  return s16x8{l[0], l[1], l[2], l[3], h[0], h[1], h[2], h[3]};
+}
+
+__device__ __forceinline__ unsigned lds_addr(const void* p) {
+  return (unsigned)(size_t)(const __attribute__((address_space(3))) void*)p;
+}
+
 struct ConvSeg {
   int Hr, Wr, Hs, Ws;
   long src_base, src_img, dst_base, dst_img;

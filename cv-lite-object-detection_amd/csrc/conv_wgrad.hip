@@ -276,7 +276,14 @@ long cvl_conv_wgrad_l_workspace(const cvl_conv_desc* d);
 int cvl_conv_wgrad_l(const cvl_conv_desc* d, const void* x, const void* dy, float* dw, float beta,
                      void* workspace, size_t workspace_bytes, hipStream_t s);
 
-extern "C" size_t cvl_conv_wgrad_workspace_size(const cvl_conv_desc* d) {
+long cvl_conv_wgrad_x_workspace(const cvl_conv_desc* d, int ngroups);
+int cvl_conv_wgrad_x(const cvl_conv_desc* d, int ngroups, const void* x, const void* dy, float* const* dw,
+                     float beta, void* workspace, size_t workspace_bytes, hipStream_t s);
+
+namespace {
+
+// Single-group workspace of the L / 128-tile paths.
+size_t wgrad_single_workspace(const cvl_conv_desc* d) {
   const long wl = cvl_conv_wgrad_l_workspace(d);     // the 128x256 LDS-DMA kernel takes the launch
   if (wl >= 0) return (size_t)wl;
   ConvArgs a;
@@ -287,20 +294,29 @@ extern "C" size_t cvl_conv_wgrad_workspace_size(const cvl_conv_desc* d) {
   return splits > 1 ? (size_t)splits * a.K * a.n_store * sizeof(float) : 16;
 }
 
-extern "C" int cvl_conv_wgrad(const cvl_conv_desc* d, const void* x, const void* dy, float* dw,
-                              float beta, void* workspace, size_t workspace_bytes,
-                              cvl_stream_t stream) {
+// Segments [g*nseg/ngroups, (g+1)*nseg/ngroups) of d as a descriptor of their own.
+cvl_conv_desc group_desc(const cvl_conv_desc* d, int ngroups, int gq) {
+  cvl_conv_desc s = *d;
+  const int spg = d->nseg / ngroups;
+  s.nseg = spg;
+  for (int i = 0; i < spg; ++i) s.seg[i] = d->seg[gq * spg + i];
+  return s;
+}
+
+int wgrad_single(const cvl_conv_desc* d, const void* x, const void* dy, float* dw, float beta, void* workspace,
+                 size_t workspace_bytes, hipStream_t s) {
+  {
+    float* dws[1] = {dw};
+    const int xst = cvl_conv_wgrad_x(d, 1, x, dy, dws, beta, workspace, workspace_bytes, s);
+    if (xst >= 0) return xst;
+  }
+  {
+    const int lst = cvl_conv_wgrad_l(d, x, dy, dw, beta, workspace, workspace_bytes, s);
+    if (lst >= 0) return lst;
+  }
   WgArgs g;
   int st = cvl_conv_prepare(d, BM, &g.a);
   if (st) return st;
-  CVL_CHECK_ARG(d->mode == CVL_CONV_FWD && x && dy && dw);
-  CVL_CHECK_ARG(d->Cin % 8 == 0 && g.a.Npad % 32 == 0);
-  CVL_CHECK_ARG(d->ld_dst % 8 == 0 && d->dst_coff % 8 == 0 && d->ld_dst >= d->dst_coff + g.a.Npad);
-  for (int i = 1; i < d->nseg; ++i) CVL_CHECK_ARG(d->seg[i].w == d->seg[0].w);  // shared weights
-  {
-    const int lst = cvl_conv_wgrad_l(d, x, dy, dw, beta, workspace, workspace_bytes, (hipStream_t)stream);
-    if (lst >= 0) return lst;
-  }
   g.a.src = reinterpret_cast<const cvl_bf16*>(x);
   g.dy = reinterpret_cast<const cvl_bf16*>(dy);
   g.ld_dy = d->ld_dst;
@@ -323,8 +339,8 @@ extern "C" int cvl_conv_wgrad(const cvl_conv_desc* d, const void* x, const void*
   } else {
     g.out = dw;
   }
-  hipStream_t s = (hipStream_t)stream;
   dim3 grid(tiles, nsplit);
+  g_cvl_conv_last_kernel = CVL_CK_WG_S;
   if (bco == 128) hipLaunchKernelGGL(conv_wgrad_kernel<128>, grid, dim3(NT), 0, s, g);
   else if (bco == 64) hipLaunchKernelGGL(conv_wgrad_kernel<64>, grid, dim3(NT), 0, s, g);
   else hipLaunchKernelGGL(conv_wgrad_kernel<32>, grid, dim3(NT), 0, s, g);
@@ -335,4 +351,64 @@ extern "C" int cvl_conv_wgrad(const cvl_conv_desc* d, const void* x, const void*
   hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(blocks), dim3(256), 0, s,
                      (const float*)g.out, dw, n, nsplit, beta);
   return cvl_launch_status();
+}
+
+int check_wgrad_desc(const cvl_conv_desc* d, int ngroups, const void* x, const void* dy, float* const* dw) {
+  ConvArgs a;
+  int st = cvl_conv_prepare(d, BM, &a);
+  if (st) return st;
+  CVL_CHECK_ARG(d->mode == CVL_CONV_FWD && x && dy && dw);
+  CVL_CHECK_ARG(ngroups >= 1 && d->nseg % ngroups == 0);
+  CVL_CHECK_ARG(d->Cin % 8 == 0 && a.Npad % 32 == 0);
+  CVL_CHECK_ARG(d->ld_dst % 8 == 0 && d->dst_coff % 8 == 0 && d->ld_dst >= d->dst_coff + a.Npad);
+  const int spg = d->nseg / ngroups;
+  for (int gq = 0; gq < ngroups; ++gq) {
+    CVL_CHECK_ARG(dw[gq]);
+    for (int i = 1; i < spg; ++i) CVL_CHECK_ARG(d->seg[gq * spg + i].w == d->seg[gq * spg].w);  // shared weights
+  }
+  return CVL_OK;
+}
+
+}  // namespace
+
+extern "C" size_t cvl_conv_wgrad_grouped_workspace_size(const cvl_conv_desc* d, int ngroups) {
+  if (!d || ngroups < 1 || d->nseg % ngroups) return 0;
+  const long wx = cvl_conv_wgrad_x_workspace(d, ngroups);
+  if (wx >= 0) return (size_t)wx;
+  size_t m = 16;
+  for (int gq = 0; gq < ngroups; ++gq) {      // the groups run one after another on one workspace
+    const cvl_conv_desc s = group_desc(d, ngroups, gq);
+    const size_t w = wgrad_single_workspace(&s);
+    m = w > m ? w : m;
+  }
+  return m;
+}
+
+extern "C" size_t cvl_conv_wgrad_workspace_size(const cvl_conv_desc* d) {
+  return cvl_conv_wgrad_grouped_workspace_size(d, 1);
+}
+
+extern "C" int cvl_conv_wgrad_grouped(const cvl_conv_desc* d, int ngroups, const void* x, const void* dy,
+                                      float* const* dw, float beta, void* workspace, size_t workspace_bytes,
+                                      cvl_stream_t stream) {
+  CVL_CHECK_ARG(dw);
+  int st = check_wgrad_desc(d, ngroups, x, dy, dw);
+  if (st) return st;
+  hipStream_t s = (hipStream_t)stream;
+  const int xst = cvl_conv_wgrad_x(d, ngroups, x, dy, dw, beta, workspace, workspace_bytes, s);
+  if (xst >= 0) return xst;
+  if (ngroups == 1) return wgrad_single(d, x, dy, dw[0], beta, workspace, workspace_bytes, s);
+  for (int gq = 0; gq < ngroups; ++gq) {
+    const cvl_conv_desc sd = group_desc(d, ngroups, gq);
+    st = wgrad_single(&sd, x, dy, dw[gq], beta, workspace, workspace_bytes, s);
+    if (st) return st;
+  }
+  return CVL_OK;
+}
+
+extern "C" int cvl_conv_wgrad(const cvl_conv_desc* d, const void* x, const void* dy, float* dw,
+                              float beta, void* workspace, size_t workspace_bytes,
+                              cvl_stream_t stream) {
+  float* dws[1] = {dw};
+  return cvl_conv_wgrad_grouped(d, 1, x, dy, dws, beta, workspace, workspace_bytes, stream);
 }

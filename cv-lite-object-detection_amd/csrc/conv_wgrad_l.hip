@@ -39,8 +39,6 @@ struct WgLArgs {
 
 __device__ __attribute__((aligned(16))) cvl_bf16 g_zero_w[8];
 
-typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
-
 __device__ __forceinline__ void glds16(const void* g, void* l) {
   __builtin_amdgcn_global_load_lds((const void __attribute__((address_space(1)))*)g,
                                    (void __attribute__((address_space(3)))*)l, 16, 0, 0);
@@ -216,29 +214,30 @@ __global__ void __launch_bounds__(NT) conv_wgrad_l_kernel(WgLArgs g) {
     if (tn < nsteps) issue(tn, slot == 0 ? NST - 1 : slot - 1);
     const cvl_bf16* Yc = lds + slot * STAGE;
     const cvl_bf16* Xc = Yc + YSTAGE;
+    const unsigned yc = lds_addr(Yc), xc = lds_addr(Xc);
 #pragma unroll
     for (int ks = 0; ks < BR / 32; ++ks) {
-      s16x8 fa[TM], fb[TN];
+      s16x4 al[TM], ah[TM], bl[TN], bh[TN];
       const int rlo = ks * 32 + 8 * lg + q, rhi = rlo + 4;
       const int slo = rswz(rlo), shi = rswz(rhi);
 #pragma unroll
       for (int i = 0; i < TM; ++i) {
         const int chnk = (wco * (BCO / 2) + i * 16) >> 4;      // 32-B chunk of the co column
-        const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-            (lds_s16x4*)(Yc + rlo * BCO + (sw_chunk(chnk, slo) << 4) + 4 * pp));
-        const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-            (lds_s16x4*)(Yc + rhi * BCO + (sw_chunk(chnk, shi) << 4) + 4 * pp));
-        fa[i] = s16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        al[i] = ds_tr16(yc + 2 * (rlo * BCO + (sw_chunk(chnk, slo) << 4) + 4 * pp));
+        ah[i] = ds_tr16(yc + 2 * (rhi * BCO + (sw_chunk(chnk, shi) << 4) + 4 * pp));
       }
 #pragma unroll
       for (int j = 0; j < TN; ++j) {
         const int chnk = (wk * 64 + j * 16) >> 4;
-        const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-            (lds_s16x4*)(Xc + rlo * BKK + (sw_chunk(chnk, slo) << 4) + 4 * pp));
-        const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-            (lds_s16x4*)(Xc + rhi * BKK + (sw_chunk(chnk, shi) << 4) + 4 * pp));
-        fb[j] = s16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        bl[j] = ds_tr16(xc + 2 * (rlo * BKK + (sw_chunk(chnk, slo) << 4) + 4 * pp));
+        bh[j] = ds_tr16(xc + 2 * (rhi * BKK + (sw_chunk(chnk, shi) << 4) + 4 * pp));
       }
+      lgkm_wait();
+      s16x8 fa[TM], fb[TN];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) { tr_pin(al[i]); tr_pin(ah[i]); fa[i] = tr_join(al[i], ah[i]); }
+#pragma unroll
+      for (int j = 0; j < TN; ++j) { tr_pin(bl[j]); tr_pin(bh[j]); fb[j] = tr_join(bl[j], bh[j]); }
 #pragma unroll
       for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -362,6 +361,7 @@ int cvl_conv_wgrad_l(const cvl_conv_desc* d, const void* x, const void* dy, floa
   g.nsplit = p.nsplit;
   g.direct = p.nsplit == 1;
   g.out = g.direct ? dw : reinterpret_cast<float*>(workspace);
+  g_cvl_conv_last_kernel = p.bco == 256 ? CVL_CK_WG_L256 : CVL_CK_WG_L128;
   if (p.bco == 256) hipLaunchKernelGGL(conv_wgrad_l_kernel<256>, dim3(p.tiles * p.nsplit), dim3(NT), 0, s, g);
   else hipLaunchKernelGGL(conv_wgrad_l_kernel<128>, dim3(p.tiles * p.nsplit), dim3(NT), 0, s, g);
   int st = cvl_launch_status();

@@ -1,0 +1,359 @@
+// 256 x 256 convolution weight gradient with the X32 schedule (gfx950).
+//
+// Same math and contract as conv_wgrad.hip / conv_wgrad_l.hip (the TF2 Conv2DBackpropFilter and
+// per-image gradient sum of FCOS/train_fcos.py:173-176):
+//   dW_g[(r, s, c), co] = sum over the rows m of group g of  A[m, (r, s, c)] * dY[m, co]
+// and it adds GROUPS: the segments of one descriptor split into `ngroups` consecutive equal groups,
+// each summed into its own dW.  The FCOS cls and reg towers (fcos.py:16-27, 76-101) share geometry,
+// so one tower layer's weight gradient for BOTH towers is one launch (2 groups x 5 levels).
+//
+// * Tile 256 (co) x 256 (k) per workgroup, 8 waves as 2 (co) x 4 (k), each a 128 x 64 block of
+//   v_mfma_f32_16x16x32_bf16 accumulators; the reduction runs over 32-row steps.
+// * Both operands move global -> LDS by buffer_load ... lds (LDS-DMA) into a 5-slot ring of 32 KiB
+//   slots (dY rows [32][256] + im2col rows [32][256], 512-B rows): the whole 160 KiB LDS.  One
+//   step per phase: [wait for step t+1 (own DMA, vmcnt(4)); issue step t+3 into the slot step t-2
+//   used; read step t's fragments (ds_read_b64_tr_b16 transposes)] barrier [32 MFMAs] barrier.
+//   The two wave groups (co halves) run one barrier apart, so each SIMD alternates one wave's MFMA
+//   segment with the other's load segment (the X32 forward kernel's stagger, conv_igemm_x.hip).
+// * No row table: each lane owns two rows of every step (one per DMA instruction pair) and walks
+//   them with a division-free cursor (image, y, x) advanced by 32 rows per step; a step never
+//   straddles segments (segments and split chunks are 128-row aligned), so the segment is uniform
+//   and a new one is entered by one uniform seek.  Padding taps and rows get an out-of-range buffer
+//   offset and the DMA writes zeros.
+// * The LDS image of a row is XOR-swizzled in 32-byte chunks within each 256-byte half (applied to
+//   the lane's SOURCE offset, LDS-DMA writes lane-linearly): the transposed reads are conflict-free.
+// * The reduction range of a group is split over workgroups to fill the GPU; partial tiles go to
+//   fp32 slabs summed in a fixed order by wgrad_x_reduce_kernel (deterministic), or straight to dW
+//   (with beta) when one split covers the range.
+#include "conv_common.h"
+
+namespace {
+
+constexpr int NT = 512, BCO = 256, BKK = 256, BR = 32, NSLOT = 5;
+constexpr int YST = BR * BCO;             // bf16 elements of the dY image of a slot (16 KiB)
+constexpr int SLOT = YST + BR * BKK;      // + the im2col image (16 KiB)
+constexpr int SEGM = 128;                 // segment / chunk alignment of the M space
+constexpr int TM = 8, TN = 4;
+constexpr int kMaxGroups = 2;
+constexpr unsigned kRecords = 0x7fffffffu;
+constexpr unsigned kOOB = 0x80000000u;
+
+struct WxArgs {
+  ConvArgs a;
+  const cvl_bf16* dy;
+  float* out[kMaxGroups];                 // per group: fp32 slab [nsplit][K][Cout], or dW (direct)
+  int g_m0[kMaxGroups], g_m1[kMaxGroups]; // M range of each group
+  int ld_dy, dy_coff, Cout, co_tiles, tiles, nsplit, chunk, direct;
+  float beta;
+};
+
+__device__ __forceinline__ int rswz(int r) { return (r & 3) | (((r >> 3) & 1) << 2); }
+__device__ __forceinline__ int sw_chunk(int c, int s) { return (c & ~7) | ((c & 7) ^ s); }
+
+__device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t r, const cvl_bf16* lds_dst, unsigned voff) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)lds_dst, 16, (int)voff, 0,
+                                           0, 0);
+}
+
+__global__ void __launch_bounds__(NT) conv_wgrad_x_kernel(WxArgs g) {
+  __shared__ __attribute__((aligned(16))) cvl_bf16 lds[NSLOT * SLOT];
+  const ConvArgs& a = g.a;
+  const int tid = threadIdx.x;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
+  // logical id: the (co, k) tiles of one (group, split) are consecutive, i.e. on one XCD's L2
+  const int L = xcd_remap(blockIdx.x, gridDim.x);
+  const int tile = L % g.tiles, rest = L / g.tiles;
+  const int split = rest % g.nsplit, grp = rest / g.nsplit;
+  const int co0 = (tile % g.co_tiles) * BCO, k0 = (tile / g.co_tiles) * BKK;
+  const int m_lo = g.g_m0[grp] + split * g.chunk;
+  const int m_hi = min(m_lo + g.chunk, g.g_m1[grp]);
+  const int nsteps = m_hi > m_lo ? (m_hi - m_lo) / BR : 0;
+
+  // ---- per-lane DMA constants: rows rr and rr + 16 of each step, 16-B piece pc of the row -------
+  const int rr = 2 * wave + (lane >> 5), pc = lane & 31;
+  const int lp = pc ^ (rswz(rr) << 1);                    // logical piece (rswz(rr + 16) == rswz(rr))
+  const unsigned ycol = (unsigned)((g.dy_coff + co0 + lp * 8) * 2);
+  const int kx = k0 + lp * 8;
+  const bool kok = kx < a.K;
+  const int tap = kok ? kx / a.Cin : 0;
+  const int ci = kx - tap * a.Cin;
+  const int tr_ = tap / a.KW, ts_ = tap - (tap / a.KW) * a.KW;
+  const int ry = tr_ - a.pad_t, rx = ts_ - a.pad_l;       // iy = oy * stride + ry
+  const unsigned xcol = (unsigned)(ci * 2);
+  const int rowb = g.ld_dy * 2, pixb = a.Cin * 2;
+  const __amdgpu_buffer_rsrc_t rsY = __builtin_amdgcn_make_buffer_rsrc((void*)g.dy, (short)0, (int)kRecords, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rsX = __builtin_amdgcn_make_buffer_rsrc((void*)a.src, (short)0, (int)kRecords, 0x00020000);
+
+  // ---- issue cursor ----------------------------------------------------------------------------
+  int ist = 0, im = m_lo, cslot = 0;
+  int seg_end = -1;                                       // forces a seek at the first live step
+  int Wr = 1, Hr = 1, Ws = 1, Hs = 1, rows = 0, sbase = 0, simg = 0, dbase = 0, dimg = 0;
+  int d_img = 0, d_oy = 0, d_ox = 0;
+  int cml[2], cimg[2], coy[2], cox[2];
+  auto seek = [&](int m) {
+    int sg = 0;
+#pragma unroll
+    for (int i = 1; i < kMaxSeg; ++i)
+      if (i < a.nseg && m >= a.seg[i].m_start) sg = i;
+    const ConvSeg& S = a.seg[sg];
+    Wr = S.Wr; Hr = S.Hr; Ws = S.Ws; Hs = S.Hs; rows = S.rows;
+    sbase = (int)S.src_base; simg = (int)S.src_img; dbase = (int)S.dst_base; dimg = (int)S.dst_img;
+    seg_end = sg + 1 < a.nseg ? a.seg[sg + 1].m_start : 0x7fffffff;
+    const int HW = Hr * Wr;
+    d_img = BR / HW;
+    const int rem = BR - d_img * HW;
+    d_oy = rem / Wr;
+    d_ox = rem - d_oy * Wr;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int ml = m - S.m_start + 16 * j + rr;
+      cml[j] = ml;
+      cimg[j] = ml / HW;
+      const int q = ml - cimg[j] * HW;
+      coy[j] = q / Wr;
+      cox[j] = q - coy[j] * Wr;
+    }
+  };
+  auto issue = [&]() {
+    const bool live = ist < nsteps;
+    if (live && im >= seg_end) seek(im);
+    cvl_bf16* Yb = lds + cslot * SLOT;
+    cvl_bf16* Xb = Yb + YST;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const bool rv = live && cml[j] < rows;
+      const int drow = dbase + cimg[j] * dimg + coy[j] * Wr + cox[j];
+      dma16(rsY, Yb + (16 * j + 2 * wave) * BCO, rv ? (unsigned)(drow * rowb) + ycol : kOOB);
+      const int iy = coy[j] * a.stride + ry, ix = cox[j] * a.stride + rx;
+      const bool xv = rv && kok && (unsigned)iy < (unsigned)Hs && (unsigned)ix < (unsigned)Ws;
+      const int pix = sbase + cimg[j] * simg + iy * Ws + ix;
+      dma16(rsX, Xb + (16 * j + 2 * wave) * BKK, xv ? (unsigned)(pix * pixb) + xcol : kOOB);
+      // advance the row by BR: (img, y, x) with one carry per level (d_ox < Wr, d_oy < Hr)
+      cml[j] += BR;
+      cox[j] += d_ox;
+      const int cy = cox[j] >= Wr;
+      cox[j] -= cy ? Wr : 0;
+      coy[j] += d_oy + cy;
+      const int cq = coy[j] >= Hr;
+      coy[j] -= cq ? Hr : 0;
+      cimg[j] += d_img + cq;
+    }
+    im += BR;
+    ++ist;
+    cslot = cslot == NSLOT - 1 ? 0 : cslot + 1;
+  };
+
+  const int wco = wave >> 2, wk = wave & 3;
+  const int lr = lane & 15, lg = lane >> 4;
+  const int q4 = lr >> 2, pp = lr & 3;
+  f32x4 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  auto bar = [&]() {
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+  };
+  // fragment read byte offsets inside a slot: rows 8*lg + q4 (+4), this lane's column
+  const int rlo = 8 * lg + q4, rhi = rlo + 4;
+  const int slo = rswz(rlo), shi = rswz(rhi);
+  const unsigned lds0 = lds_addr(lds);
+  unsigned ya[TM], yb[TM], xa[TN], xb[TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+    const int ch = wco * 8 + i;
+    ya[i] = 2 * (rlo * BCO + (sw_chunk(ch, slo) << 4) + 4 * pp);
+    yb[i] = 2 * (rhi * BCO + (sw_chunk(ch, shi) << 4) + 4 * pp);
+  }
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    const int ch = wk * 4 + j;
+    xa[j] = 2 * (YST + rlo * BKK + (sw_chunk(ch, slo) << 4) + 4 * pp);
+    xb[j] = 2 * (YST + rhi * BKK + (sw_chunk(ch, shi) << 4) + 4 * pp);
+  }
+
+  issue();
+  issue();
+  issue();
+  wait_vm<8>();
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+  if (wco == 1) bar();                          // stagger: waves 4-7 run one barrier behind
+
+  int rslot = 0;
+  for (int st = 0; st < nsteps; ++st) {
+    wait_vm<4>();                               // step st+1 (read next phase)
+    issue();                                    // step st+3
+    const unsigned base = lds0 + rslot * (SLOT * 2);
+    s16x4 al[TM], ah[TM], bl[TN], bh[TN];
+#pragma unroll
+    for (int i = 0; i < TM; ++i) { al[i] = ds_tr16(base + ya[i]); ah[i] = ds_tr16(base + yb[i]); }
+#pragma unroll
+    for (int j = 0; j < TN; ++j) { bl[j] = ds_tr16(base + xa[j]); bh[j] = ds_tr16(base + xb[j]); }
+    bar();
+    lgkm_wait();
+#pragma unroll
+    for (int i = 0; i < TM; ++i) { tr_pin(al[i]); tr_pin(ah[i]); }
+#pragma unroll
+    for (int j = 0; j < TN; ++j) { tr_pin(bl[j]); tr_pin(bh[j]); }
+    s16x8 fa[TM], fb[TN];
+#pragma unroll
+    for (int i = 0; i < TM; ++i) fa[i] = tr_join(al[i], ah[i]);
+#pragma unroll
+    for (int j = 0; j < TN; ++j) fb[j] = tr_join(bl[j], bh[j]);
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, fa[i]),
+                                                             __builtin_bit_cast(bf16x8, fb[j]), acc[i][j], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+    __builtin_amdgcn_sched_barrier(0);
+    bar();
+    rslot = rslot == NSLOT - 1 ? 0 : rslot + 1;
+  }
+  if (wco == 0) bar();                          // equal barrier counts for both groups
+  wait_vm<0>();
+
+  // ---- epilogue: C[co][k] -> out[k][co] (HWIO), 4 consecutive co per lane -------------------------
+  float* out = g.out[grp] + (g.direct ? 0 : (size_t)split * a.K * g.Cout);
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int k = k0 + wk * 64 + j * 16 + lr;
+      const int co = co0 + wco * 128 + i * 16 + 4 * lg;
+      if (k >= a.K || co >= g.Cout) continue;
+      f32x4 v = acc[i][j];
+      if (co + 3 < g.Cout && (g.Cout & 3) == 0) {
+        f32x4* po = reinterpret_cast<f32x4*>(out + (size_t)k * g.Cout + co);
+        if (g.direct && g.beta != 0.f) v += g.beta * *po;
+        *po = v;
+      } else {
+        for (int e = 0; e < 4 && co + e < g.Cout; ++e) {
+          float* po = out + (size_t)k * g.Cout + co + e;
+          *po = (g.direct && g.beta != 0.f) ? v[e] + g.beta * *po : v[e];
+        }
+      }
+    }
+}
+
+// dW_g = beta * dW_g + sum over splits s (in order) of slab_g[s]; slabs of group g at g * splits * n4
+__global__ void wgrad_x_reduce_kernel(const float* slab, float* dw0, float* dw1, long n4, int splits, int groups,
+                                      float beta) {
+  const long total = n4 * groups;
+  for (long t = blockIdx.x * (long)blockDim.x + threadIdx.x; t < total; t += (long)gridDim.x * blockDim.x) {
+    const int gq = (int)(t / n4);
+    const long i = t - gq * n4;
+    const f32x4* sl = reinterpret_cast<const f32x4*>(slab) + (long)gq * splits * n4;
+    f32x4 s = sl[i];
+    for (int k = 1; k < splits; ++k) s += sl[(long)k * n4 + i];
+    f32x4* d = reinterpret_cast<f32x4*>(gq == 0 ? dw0 : dw1) + i;
+    if (beta != 0.f) s += beta * *d;
+    *d = s;
+  }
+}
+
+struct WxPlan {
+  int ngroups, spg, tiles, co_tiles, nsplit, chunk;
+  int g_m0[kMaxGroups], g_m1[kMaxGroups];
+  size_t slab;
+};
+
+// Modelled time of s splits: rounds of 256 workgroups (one per CU) x 32-row steps per chunk
+// (CVL_WGX_STEP, 0.01 us; ~0.8 us measured on the tower shape) + the fp32 slab round trip.
+inline bool wx_plan(const cvl_conv_desc* d, int ngroups, ConvArgs* a, WxPlan* p) {
+  if (cvl_env_flag("CVL_WGRAD_NO_X")) return false;
+  if (cvl_conv_prepare(d, SEGM, a)) return false;
+  if (ngroups < 1 || ngroups > kMaxGroups || d->nseg % ngroups || d->relu_in || a->Npad % BCO ||
+      d->Cin % 8 || d->n_store % 4 || a->K < BKK / 2 || a->m_total < 1024)
+    return false;
+  // every dY / source byte offset must stay below the buffer-resource bound (32-bit cursors)
+  for (int i = 0; i < a->nseg; ++i) {
+    const ConvSeg& q = a->seg[i];
+    const long dy_end = (q.dst_base + (long)a->B * q.dst_img) * d->ld_dst * 2;
+    const long src_end = (q.src_base + (long)a->B * q.src_img) * a->Cin * 2;
+    if (dy_end >= (long)kRecords - 65536 || src_end >= (long)kRecords - 65536) return false;
+  }
+  p->ngroups = ngroups;
+  p->spg = d->nseg / ngroups;
+  int mg = 0;
+  for (int gq = 0; gq < ngroups; ++gq) {
+    p->g_m0[gq] = a->seg[gq * p->spg].m_start;
+    p->g_m1[gq] = (gq + 1) * p->spg < a->nseg ? a->seg[(gq + 1) * p->spg].m_start : a->m_total;
+    mg = p->g_m1[gq] - p->g_m0[gq] > mg ? p->g_m1[gq] - p->g_m0[gq] : mg;
+  }
+  for (int gq = ngroups; gq < kMaxGroups; ++gq) p->g_m0[gq] = p->g_m1[gq] = 0;
+  p->co_tiles = a->Npad / BCO;
+  p->tiles = p->co_tiles * ((a->K + BKK - 1) / BKK);
+  const int tg = p->tiles * ngroups;
+  const double step_us = cvl_env_int("CVL_WGX_STEP", 80) / 100.0;
+  const double slab_us = (double)BCO * BKK * 4 * 2 / 5.0e6 * cvl_env_int("CVL_WGX_SLAB_PCT", 100) / 100.0;
+  int max_s = mg / 512;
+  if (max_s < 1) max_s = 1;
+  if (max_s > 2048 / tg) max_s = 2048 / tg > 1 ? 2048 / tg : 1;
+  double best_t = 1e30;
+  int best_s = 1;
+  for (int s = 1; s <= max_s; ++s) {
+    const int rounds = (tg * s + 255) / 256;
+    const int chunk = ((mg + s - 1) / s + SEGM - 1) / SEGM * SEGM;
+    const double t = rounds * (chunk / BR) * step_us + (s > 1 ? tg * s * slab_us : 0.0);
+    if (t < best_t) { best_t = t; best_s = s; }
+  }
+  const int forced = cvl_env_int("CVL_WGX_SPLITS", 0);
+  if (forced > 0) best_s = forced;
+  p->chunk = ((mg + best_s - 1) / best_s + SEGM - 1) / SEGM * SEGM;
+  p->nsplit = (mg + p->chunk - 1) / p->chunk;
+  p->slab = p->nsplit > 1 ? (size_t)ngroups * p->nsplit * a->K * d->n_store * sizeof(float) : 0;
+  return true;
+}
+
+}  // namespace
+
+// Workspace the X path needs (>= 16), or -1 when the launch does not qualify.
+long cvl_conv_wgrad_x_workspace(const cvl_conv_desc* d, int ngroups) {
+  ConvArgs a;
+  WxPlan p;
+  if (!wx_plan(d, ngroups, &a, &p)) return -1;
+  return (long)(p.slab > 16 ? p.slab : 16);
+}
+
+// Returns -1 when the launch does not qualify (the caller takes another kernel), else a status.
+int cvl_conv_wgrad_x(const cvl_conv_desc* d, int ngroups, const void* x, const void* dy, float* const* dw,
+                     float beta, void* workspace, size_t workspace_bytes, hipStream_t s) {
+  WxArgs g;
+  WxPlan p;
+  if (!wx_plan(d, ngroups, &g.a, &p)) return -1;
+  if (!workspace || workspace_bytes < (p.slab > 16 ? p.slab : 16)) return CVL_EINVAL;
+  g.a.src = reinterpret_cast<const cvl_bf16*>(x);
+  g.dy = reinterpret_cast<const cvl_bf16*>(dy);
+  g.ld_dy = d->ld_dst;
+  g.dy_coff = d->dst_coff;
+  g.Cout = d->n_store;
+  g.beta = beta;
+  g.co_tiles = p.co_tiles;
+  g.tiles = p.tiles;
+  g.nsplit = p.nsplit;
+  g.chunk = p.chunk;
+  g.direct = p.nsplit == 1;
+  const size_t per_group = (size_t)p.nsplit * g.a.K * g.Cout;
+  for (int gq = 0; gq < kMaxGroups; ++gq) {
+    g.g_m0[gq] = p.g_m0[gq];
+    g.g_m1[gq] = p.g_m1[gq];
+    const int gs = gq < ngroups ? gq : 0;
+    g.out[gq] = g.direct ? dw[gs] : reinterpret_cast<float*>(workspace) + gs * per_group;
+  }
+  g_cvl_conv_last_kernel = CVL_CK_WG_X;
+  hipLaunchKernelGGL(conv_wgrad_x_kernel, dim3(p.tiles * p.nsplit * ngroups), dim3(NT), 0, s, g);
+  int st = cvl_launch_status();
+  if (st || g.direct) return st;
+  const long n4 = (long)g.a.K * g.Cout / 4;
+  long blocks = (n4 * ngroups + 255) / 256;
+  blocks = blocks > 4096 ? 4096 : blocks;
+  hipLaunchKernelGGL(wgrad_x_reduce_kernel, dim3((int)blocks), dim3(256), 0, s, (const float*)workspace, dw[0],
+                     ngroups > 1 ? dw[1] : dw[0], n4, p.nsplit, ngroups, beta);
+  return cvl_launch_status();
+}

@@ -238,10 +238,16 @@ class FPNDetector(object):
         for t in range(2):
             nn.relu_backward(dAs[t], towers[t][-1], dAs[t])         # the tower's final ReLU
         for i in range(3, -1, -1):
-            for t, tw in enumerate((self.cls_tower, self.reg_tower)):
-                conv = tw[i]
-                d = conv.fwd_desc(B, self._tower_segs(conv, B, shapes, off), ld_dst=FPN_C)
-                nn.conv_wgrad(d, towers[t][i], dAs[t], conv.dw)
+            if paired:      # both towers' weight gradients: ONE launch, 2 groups x 5 levels
+                d = self.cls_tower[i].fwd_desc(B, self._pair_segs(i, B, shapes, off, P, fwd=True), ld_dst=FPN_C)
+                x_all = F if i == 0 else s["tower_bufs"][i - 1]
+                dy_all = torch.as_strided(dAs[0], (2 * BP, FPN_C), (FPN_C, 1))
+                nn.conv_wgrad_grouped(d, x_all, dy_all, [self.cls_tower[i].dw, self.reg_tower[i].dw])
+            else:
+                for t, tw in enumerate((self.cls_tower, self.reg_tower)):
+                    conv = tw[i]
+                    d = conv.fwd_desc(B, self._tower_segs(conv, B, shapes, off), ld_dst=FPN_C)
+                    nn.conv_wgrad(d, towers[t][i], dAs[t], conv.dw)
             if i > 0 and paired:
                 dd = self.cls_tower[i].dgrad_desc(B, self._pair_segs(i, B, shapes, off, P, fwd=False), ld_dst=FPN_C)
                 dst = torch.empty((2 * BP, FPN_C), dtype=BF16, device=dev)

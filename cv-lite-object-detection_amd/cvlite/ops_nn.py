@@ -68,6 +68,17 @@ def conv_wgrad(desc, x, dy, dw, beta=0.0):
               ws.numel(), stream())
 
 
+def conv_wgrad_grouped(desc, x, dy, dws, beta=0.0):
+    """Weight gradients of `len(dws)` segment groups in one launch (cvl_conv_wgrad_grouped): the
+    descriptor's segments split into equal consecutive groups, group g summed into dws[g]."""
+    lib = _lib.load()
+    n = int(lib.cvl_conv_wgrad_grouped_workspace_size(ctypes.byref(desc), len(dws)))
+    ws = torch.empty(max(n, 16), dtype=torch.uint8, device=x.device)
+    arr = (c_void_p * len(dws))(*[t.data_ptr() for t in dws])
+    _lib.call("cvl_conv_wgrad_grouped", ctypes.byref(desc), len(dws), ptr(x), ptr(dy), arr, float(beta), ptr(ws),
+              ws.numel(), stream())
+
+
 def pack_conv_weights(w_hwio, KH, KW, Cin, Cout, Cin_k, Npad, w_fwd, Cin_pad=0, Cout_pad=0, w_dgrad=None):
     _lib.call("cvl_pack_conv_weights", ptr(w_hwio), KH, KW, Cin, Cout, Cin_k, Npad, ptr(w_fwd),
               Cin_pad, Cout_pad, ptr(w_dgrad), stream())

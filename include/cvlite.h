@@ -128,10 +128,11 @@ size_t cvl_conv_igemm_workspace_size(const cvl_conv_desc* d);
 int cvl_conv_igemm(const cvl_conv_desc* d, const void* src, void* dst, double* bn_stats,
                    void* workspace, size_t workspace_bytes, cvl_stream_t stream);
 
-/* Test / profiling hook: the kernel variant the last cvl_conv_igemm call on THIS host thread
- * launched.  CVL_CK_* codes; cvl_conv_kernel_name(code) is a static string. */
+/* Test / profiling hook: the kernel variant the last cvl_conv_igemm / cvl_conv_wgrad* call on THIS
+ * host thread launched.  CVL_CK_* codes; cvl_conv_kernel_name(code) is a static string. */
 enum { CVL_CK_NONE = 0, CVL_CK_BASE = 1, CVL_CK_BASE_SPLITK = 2, CVL_CK_L64 = 3, CVL_CK_L128 = 4,
-       CVL_CK_L256 = 5, CVL_CK_X256 = 6, CVL_CK_X32 = 7 };
+       CVL_CK_L256 = 5, CVL_CK_X256 = 6, CVL_CK_X32 = 7,
+       CVL_CK_WG_S = 8, CVL_CK_WG_L128 = 9, CVL_CK_WG_L256 = 10, CVL_CK_WG_X = 11 };
 int cvl_conv_igemm_last_kernel(void);
 const char* cvl_conv_kernel_name(int code);
 
@@ -142,6 +143,14 @@ const char* cvl_conv_kernel_name(int code);
 size_t cvl_conv_wgrad_workspace_size(const cvl_conv_desc* d);
 int cvl_conv_wgrad(const cvl_conv_desc* d, const void* x, const void* dy, float* dw, float beta,
                    void* workspace, size_t workspace_bytes, cvl_stream_t stream);
+
+/* Grouped weight gradient: the segments of `d` split into `ngroups` consecutive equal groups (each
+ * sharing one weight pointer), group g summed into dw[g] (a HOST array of device pointers).  The
+ * FCOS cls and reg tower layers (FCOS/fcos.py:16-27, 76-101: same geometry, own weights) are one
+ * call with 10 segments and 2 groups.  workspace >= cvl_conv_wgrad_grouped_workspace_size(d, ngroups). */
+size_t cvl_conv_wgrad_grouped_workspace_size(const cvl_conv_desc* d, int ngroups);
+int cvl_conv_wgrad_grouped(const cvl_conv_desc* d, int ngroups, const void* x, const void* dy, float* const* dw,
+                           float beta, void* workspace, size_t workspace_bytes, cvl_stream_t stream);
 
 /* fp32 HWIO [KH][KW][Cin][Cout] master weights -> bf16 forward pack [Npad][KH*KW*Cin_k]
  * (zero rows >= Cout and channels >= Cin) and/or dgrad pack [Cin_pad][KH*KW*Cout_pad]. */

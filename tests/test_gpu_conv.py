@@ -34,7 +34,9 @@ def kern(request, monkeypatch):
     """Run a test through the 128-row register-staged kernel ("base"), the 256-row LDS-DMA kernel
     ("l", normally taken only by launches with >= 128 tiles; 128/64-wide N tiles), its
     256x256-tile form ("l256", Npad % 256 == 0 only) and the 8-phase 256x256 kernel ("x", the
-    alternative for the launches l256 would take) and its 32-deep-K ring form ("x32", the default)."""
+    alternative for the launches l256 would take) and its 32-deep-K ring form ("x32", the default).
+    Weight gradients: "base" runs the 128-wide k-tile kernel, "l"/"l256"/"x" the row-table LDS-DMA
+    kernel (conv_wgrad_l.hip), "x32" the default dispatch (conv_wgrad_x.hip where Npad % 256 == 0)."""
     if request.param in ("l", "l256", "x", "x32"):
         monkeypatch.setenv("CVL_CONV_L_MIN_TILES", "1")
     if request.param == "l":
@@ -45,9 +47,9 @@ def kern(request, monkeypatch):
         monkeypatch.setenv("CVL_CONV_NO_X", "1")
     if request.param == "x":
         monkeypatch.setenv("CVL_CONV_NO_X32", "1")
-    if request.param in ("l256", "x", "x32"):
-        pass
-    else:
+    if request.param != "x32":
+        monkeypatch.setenv("CVL_WGRAD_NO_X", "1")
+    if request.param not in ("l256", "x", "x32"):
         monkeypatch.setenv("CVL_CONV_NO_L", "1")
         monkeypatch.setenv("CVL_WGRAD_NO_L", "1")
     return request.param
@@ -327,3 +329,94 @@ def test_conv_wgrad_large_segments(kern):
         y.backward(dy[B * off[l]:B * off[l] + B * h * ww].reshape(B, h, ww, C).double().cpu())
         ref += wl.grad
     torch.testing.assert_close(dw.double().cpu(), ref, rtol=1e-4, atol=1e-4)
+
+
+def _tower_pair_case(B, C, shapes, seed):
+    off, o = [], 0
+    for h, w in shapes:
+        off.append(o)
+        o += h * w
+    P = o
+    g = torch.Generator().manual_seed(seed)
+    xs = rnd(2 * B * P, C, gen=g)
+    dys = rnd(2 * B * P, C, gen=g)
+    return off, P, xs, dys
+
+
+@pytest.mark.parametrize("shared_x", [False, True])
+@pytest.mark.parametrize("variant", ["wx", "fallback"])
+def test_conv_wgrad_grouped_tower_pair(shared_x, variant, monkeypatch):
+    """cvl_conv_wgrad_grouped in the paired-tower form (fcos.py:16-27, 76-101): 10 segments = 2 towers
+    x 5 levels, group g -> dW_g, dY rows of tower t at t*B*P; the source is either the paired
+    activation buffer (layers 1-3) or one map both towers read (layer 0, shared_x).  "fallback"
+    runs one single-group launch per group.  Reference: per level and tower, torch fp64 autograd."""
+    from cvlite import _lib, ops_nn as nn
+    if variant == "fallback":
+        monkeypatch.setenv("CVL_WGRAD_NO_X", "1")
+    B, C = 4, 256
+    shapes = [(24, 20), (12, 10), (6, 5), (3, 3), (2, 2)]
+    off, P, xs, dys = _tower_pair_case(B, C, shapes, 21)
+    BP = B * P
+    w0 = torch.zeros((3, 3, C, C))
+    wf = torch.empty((C, 9 * C), dtype=BF, device="cuda")
+    wf2 = torch.empty_like(wf)
+    segs = []
+    for t in range(2):
+        src0 = 0 if shared_x else t * BP
+        segs += [nn.seg(h, w, h, w, (wf, wf2)[t], None, src_base=src0 + B * off[l], src_img=h * w,
+                        dst_base=t * BP + B * off[l], dst_img=h * w) for l, (h, w) in enumerate(shapes)]
+    d = nn.make_desc(nn.FWD, B, C, 3, 3, 1, 1, 1, C, C, C, segs)
+    dws = [torch.full((3, 3, C, C), 0.25, device="cuda") for _ in range(2)]
+    xg, dyg = xs.to(BF).cuda(), dys.to(BF).cuda()
+    nn.conv_wgrad_grouped(d, xg, dyg, dws, beta=2.0)
+    code = _lib.load().cvl_conv_igemm_last_kernel()
+    name = _lib.load().cvl_conv_kernel_name(code).decode()
+    print("wgrad kernel:", name)
+    if variant == "wx":
+        assert code == 11, name
+    for t in range(2):
+        ref = torch.zeros(3, 3, C, C, dtype=torch.float64)
+        for l, (h, w) in enumerate(shapes):
+            src0 = 0 if shared_x else t * BP
+            xm = xs[src0 + B * off[l]:src0 + B * (off[l] + h * w)].reshape(B, h, w, C)
+            wl = w0.double().clone().requires_grad_(True)
+            y = ref_conv(xm, wl, None, 1, "same")
+            y.backward(dys[t * BP + B * off[l]:t * BP + B * (off[l] + h * w)].reshape(B, h, w, C))
+            ref += wl.grad
+        exp = ref + 0.5
+        scale = ref.abs().max().item()
+        torch.testing.assert_close(dws[t].double().cpu(), exp, rtol=1e-4, atol=1e-5 * scale,
+                                   msg=lambda m: "tower %d: %s" % (t, m))
+
+
+def test_conv_wgrad_x_deterministic():
+    """The split-M reduction of the 256x256 wgrad kernel sums its fp32 slabs in a fixed order: two
+    runs give bit-identical dW (tower-layer shape at bs 16 / 512 for one tower)."""
+    from cvlite import _lib, ops_nn as nn
+    B, C = 16, 256
+    shapes = [(64, 64), (32, 32), (16, 16), (8, 8), (4, 4)]
+    off, o = [], 0
+    for h, w in shapes:
+        off.append(o)
+        o += h * w
+    P = o
+    gen = torch.Generator(device="cuda").manual_seed(3)
+    x = torch.randn((B * P, C), generator=gen, device="cuda").to(BF)
+    dy = torch.randn((B * P, C), generator=gen, device="cuda").to(BF)
+    wf = torch.empty((C, 9 * C), dtype=BF, device="cuda")
+    segs = [nn.seg(h, w, h, w, wf, None, src_base=B * off[l], dst_base=B * off[l]) for l, (h, w) in enumerate(shapes)]
+    d = nn.make_desc(nn.FWD, B, C, 3, 3, 1, 1, 1, C, C, C, segs)
+    outs = []
+    for _ in range(2):
+        dw = torch.empty((3, 3, C, C), device="cuda")
+        nn.conv_wgrad(d, x, dy, dw)
+        assert _lib.load().cvl_conv_igemm_last_kernel() == 11
+        outs.append(dw)
+    assert torch.equal(outs[0], outs[1])
+    # level 0 alone vs torch (fp32 accumulate of the bf16 operands on the GPU)
+    xm = x[:B * 4096].float().view(B, 64, 64, C).permute(0, 3, 1, 2)
+    dym = dy[:B * 4096].float().view(B, 64, 64, C).permute(0, 3, 1, 2)
+    ref = torch.nn.grad.conv2d_weight(xm.double(), (C, C, 3, 3), dym.double(), padding=1)
+    dw0 = torch.empty((3, 3, C, C), device="cuda")
+    nn.conv_wgrad(nn.make_desc(nn.FWD, B, C, 3, 3, 1, 1, 1, C, C, C, segs[:1]), x, dy, dw0)
+    torch.testing.assert_close(dw0.double(), ref.permute(2, 3, 1, 0), rtol=1e-4, atol=2e-3)

@@ -1,0 +1,125 @@
+"""Per-shape table of every conv launch of one FCOS training step (configs[1]: 512x512, bs 16):
+the launches are recorded during one eager step (ops_nn.conv_igemm / conv_wgrad /
+conv_wgrad_grouped), then each distinct launch is replayed alone with HIP events on its stream.
+Prints a markdown table (kernel chosen, us per launch, TFLOP/s, fraction of the 2.5 PF bf16 dense
+peak, ms per step) sorted by time per step.
+usage: conv_table.py [--bs 16] [--size 512] [--iters 10] [--out file.md]"""
+import argparse
+import collections
+import ctypes
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "cv-lite-object-detection_amd")]
+import torch  # noqa: E402
+
+from cvlite import _lib, ops_nn as nn  # noqa: E402
+from cvlite.fcos_net import FCOSNet  # noqa: E402
+from cvlite.train_fcos import FCOSTrainer, synthetic_batch  # noqa: E402
+
+PEAK = 2500.0
+
+
+def desc_key(kind, d):
+    segs = tuple((d.seg[i].Hr, d.seg[i].Wr, d.seg[i].Hs, d.seg[i].Ws) for i in range(d.nseg))
+    return (kind, d.mode, d.B, d.Cin, d.KH, d.KW, d.stride, d.Npad, d.n_store, d.dst_f32, d.relu_in, segs)
+
+
+def describe(kind, d, ngroups=1):
+    s0 = d.seg[0]
+    mode = {0: "fwd", 1: "dgrad"}[d.mode] if kind == "igemm" else "wgrad"
+    geo = "%dx%d" % (d.KH, d.KW) + (" s%d" % d.stride if d.stride > 1 else "")
+    if kind == "igemm" and d.mode == 1:
+        chans = "%d->%d" % (d.Cin, d.n_store)
+    else:
+        chans = "%d->%d" % (d.Cin, d.n_store)
+    lv = "%dx%d" % (s0.Hr, s0.Wr) + (" +%d seg" % (d.nseg - 1) if d.nseg > 1 else "")
+    g = " (%d groups)" % ngroups if ngroups > 1 else ""
+    return "%s %s %s @ %s%s" % (mode, geo, chans, lv, g)
+
+
+def flops(kind, d):
+    rows = sum(d.B * d.seg[i].Hr * d.seg[i].Wr for i in range(d.nseg))
+    K = d.KH * d.KW * d.Cin
+    return 2.0 * rows * K * d.n_store
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--bs", type=int, default=16)
+    ap.add_argument("--size", type=int, default=512)
+    ap.add_argument("--iters", type=int, default=10)
+    ap.add_argument("--out", default=None)
+    args = ap.parse_args()
+    B, H = args.bs, args.size
+    net = FCOSNet(20, device=torch.device("cuda"), seed=0)
+    tr = FCOSTrainer(net, B, (H, H), use_graph=False)
+    tr.load_batch(*synthetic_batch(B, H, H, 20, seed=1234, device="cuda"))
+    tr.step()                      # warm-up (allocations, first-touch)
+    torch.cuda.synchronize()
+    calls = collections.OrderedDict()
+    counts = collections.Counter()
+    orig = (nn.conv_igemm, nn.conv_wgrad, nn.conv_wgrad_grouped)
+
+    def rec(key, replay, d, kind, ng=1):
+        counts[key] += 1
+        if key not in calls:
+            calls[key] = (replay, d, kind, ng)
+
+    def igemm(desc, src, dst, stats=None):
+        rec(desc_key("igemm", desc), lambda: orig[0](desc, src, dst, stats), desc, "igemm")
+        return orig[0](desc, src, dst, stats)
+
+    def wgrad(desc, x, dy, dw, beta=0.0):
+        rec(desc_key("wgrad", desc), lambda: orig[1](desc, x, dy, dw, beta), desc, "wgrad")
+        return orig[1](desc, x, dy, dw, beta)
+
+    def wgrad_g(desc, x, dy, dws, beta=0.0):
+        rec(desc_key("wgrad_g", desc), lambda: orig[2](desc, x, dy, dws, beta), desc, "wgrad", len(dws))
+        return orig[2](desc, x, dy, dws, beta)
+
+    nn.conv_igemm, nn.conv_wgrad, nn.conv_wgrad_grouped = igemm, wgrad, wgrad_g
+    tr.load_batch(*synthetic_batch(B, H, H, 20, seed=77, device="cuda"))
+    tr.step()
+    torch.cuda.synchronize()
+    nn.conv_igemm, nn.conv_wgrad, nn.conv_wgrad_grouped = orig
+    lib = _lib.load()
+    rows = []
+    s = torch.cuda.current_stream()
+    for key, (replay, d, kind, ng) in calls.items():
+        replay()
+        code = lib.cvl_conv_igemm_last_kernel()
+        kname = lib.cvl_conv_kernel_name(code).decode().split(" (")[0]
+        replay()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(s)
+        for _ in range(args.iters):
+            replay()
+        e1.record(s)
+        e1.synchronize()
+        us = e0.elapsed_time(e1) / args.iters * 1e3
+        fl = flops(kind, d)
+        n = counts[key]
+        rows.append((us * n / 1e3, describe(kind, d, ng), kname, n, us, fl / us / 1e6))
+    rows.sort(key=lambda r: -r[0])
+    tot = sum(r[0] for r in rows)
+    by_mode = collections.defaultdict(float)
+    for r in rows:
+        by_mode[r[1].split()[0]] += r[0]
+    lines = ["# Conv launches of one FCOS step (bs %d, %dx%d), replayed alone" % (B, H, H), "",
+             "Total %.3f ms per step over %d launches (%s)." % (
+                 tot, sum(counts.values()), ", ".join("%s %.3f ms" % kv for kv in sorted(by_mode.items()))), "",
+             "| ms/step | launch | kernel | per step | us/launch | TFLOP/s | frac of 2.5 PF |",
+             "|---|---|---|---|---|---|---|"]
+    for ms, desc, kname, n, us, tf in rows:
+        lines.append("| %.3f | %s | %s | %d | %.1f | %.0f | %.3f |" % (ms, desc, kname, n, us, tf, tf / PEAK))
+    text = "\n".join(lines) + "\n"
+    print(text, flush=True)
+    if args.out:
+        with open(args.out, "w") as f:
+            f.write(text)
+
+
+if __name__ == "__main__":
+    main()
