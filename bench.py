@@ -97,18 +97,25 @@ def measure_tower_conv(net, B, H, W, iters=20):
     ms = e0.elapsed_time(e1) / iters
     M = 2 * B * P
     flops = 2.0 * M * 256 * 9 * 256
-    return ms, flops
+    from cvlite import _lib
+    L = _lib.load()
+    kname = L.cvl_conv_kernel_name(L.cvl_conv_igemm_last_kernel()).decode()
+    return ms, flops, kname
 
 
-PMC_FILE = "profiles/r01h_pmc_tower_conv.json"
+PMC_FILE = "profiles/r02k_pmc_tower_conv.json"
 
 
-def pmc_traffic():
-    """Per-launch HBM bytes of the dominant kernel, measured by tools/pmc_tower.sh (committed)."""
+def pmc_traffic(kname):
+    """Per-launch HBM bytes of the dominant kernel, measured by tools/pmc_tower.sh (committed); null
+    when the committed measurement is of a different kernel than the one this run launched."""
     p = os.path.join(ROOT, PMC_FILE)
     if not os.path.exists(p):
         return None
-    return int(json.load(open(p))["hbm_bytes"])
+    d = json.load(open(p))
+    if d["kernel"].split("<")[0] not in kname:
+        return None
+    return int(d["hbm_bytes"])
 
 
 def tower_alg_bytes(B, net, H, W):
@@ -291,7 +298,7 @@ def main():
     if rank != 0:
         dist.barrier()
         return
-    k_ms, k_flops = measure_tower_conv(net, B, H, W)
+    k_ms, k_flops, k_name = measure_tower_conv(net, B, H, W)
     achieved = k_flops / (k_ms * 1e-3) / 1e12
     out = {
         "metric": METRIC,
@@ -312,12 +319,13 @@ def main():
                    "model": "FCOS-ResNet50-FPN", "global_batch": B * world, "image_size": H,
                    "parallelism": "dp%d" % world},
         "roofline": {"bound": "mfma", "achieved": round(achieved, 2), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
-                     "frac": round(achieved / PEAK_BF16_TFLOPS, 4), "traffic": pmc_traffic(),
+                     "frac": round(achieved / PEAK_BF16_TFLOPS, 4), "traffic": pmc_traffic(k_name),
                      "traffic_note": "HBM bytes per launch from rocprofv3 --pmc FETCH_SIZE (x2, gfx950) + "
                                      "WRITE_SIZE, separate passes (tools/pmc_tower.sh -> %s); algorithmic "
                                      "bytes per launch %d (src + dst bf16 + weights)" % (PMC_FILE, tower_alg_bytes(B, net, H, W)),
-                     "kernel": "conv_igemm_l_kernel<256, 2, 2, false, true> (fwd, 256x256 tile), FCOS cls+reg tower layer 3x3 256->256 over all 5 levels, one 10-segment launch "
-                               "(M=%d, N=256, K=2304), %.3f ms/launch" % (2 * B * net.layout(B, H, W)[2], k_ms)},
+                     "kernel": "%s, fwd: FCOS cls+reg tower layer 3x3 256->256 over all 5 levels, one "
+                               "10-segment launch (M=%d, N=256, K=2304), %.3f ms/launch"
+                               % (k_name, 2 * B * net.layout(B, H, W)[2], k_ms)},
         "model_flops_per_image": fl_img,
         "step_mfma_frac": round(img_s / world * fl_img / 1e12 / PEAK_BF16_TFLOPS, 4),
         "last_step_losses_cls_reg_cen": [round(x, 3) for x in losses],

@@ -269,6 +269,12 @@ struct BnFin {
 };
 
 constexpr int BNA_UNR = 4;
+
+// the BN + affine output before the residual / ReLU, one explicit fma: the backward recomputes it
+// from z to rebuild the ReLU mask of non-residual units (bit-identical to the forward's value)
+__device__ __forceinline__ float bn_affine(float z, float m, float rs, float ga, float be) {
+  return __builtin_fmaf(ga, (z - m) * rs, be);
+}
 constexpr int BN_FIN_MAXC = 2048;
 template <bool FIN>
 __global__ void __launch_bounds__(NT) bn_apply_kernel(const cvl_bf16* __restrict__ z, const float* __restrict__ mr,
@@ -331,7 +337,7 @@ __global__ void __launch_bounds__(NT) bn_apply_kernel(const cvl_bf16* __restrict
         if (res) unpack8(vr[q], rr);
 #pragma unroll
         for (int u = 0; u < 8; ++u) {
-          float o = ga[u] * ((v[u] - m[u]) * rs[u]) + be[u];
+          float o = bn_affine(v[u], m[u], rs[u], ga[u], be[u]);
           if (res) o += rr[u];
           if (relu) o = o > 0.f ? o : 0.f;
           v[u] = o;
@@ -380,7 +386,8 @@ __global__ void __launch_bounds__(NT) bn_bwd_kernel(const cvl_bf16* __restrict__
                                                     const float* __restrict__ gamma, const double* __restrict__ sums,
                                                     cvl_bf16* __restrict__ dz, cvl_bf16* __restrict__ g_out,
                                                     float* __restrict__ part, int C, int HW, int rows_per_blk,
-                                                    int group, float dz_beta, BnPG pg) {
+                                                    int group, float dz_beta, BnPG pg,
+                                                    const float* __restrict__ bnb) {
   const int b = blockIdx.y;
   const int C8 = C / 8;
   const int tpr = C8 < NT ? C8 : NT;
@@ -409,12 +416,17 @@ __global__ void __launch_bounds__(NT) bn_bwd_kernel(const cvl_bf16* __restrict__
   }
   for (int cgb = cg; cgb < C8; cgb += tpr) {
     const int c0 = cgb * 8;
-    float m[8], rs[8], s1[8], s2[8], k1[8], k2[8], gm[8];
+    float m[8], rs[8], s1[8], s2[8], k1[8], k2[8], gm[8], ga[8], be[8];
+    // mask source: y (relu output, residual units) or, when y is null and bnb is given, the
+    // ReLU of bn_affine(z) recomputed (non-residual units: one tensor fewer to read)
+    const bool zmask = PASS != 2 && !y && bnb;
 #pragma unroll
     for (int u = 0; u < 8; ++u) {
       const long bc = (long)b * C + c0 + u;
       m[u] = PASS == 2 ? 0.f : mr[bc * 2];
       rs[u] = PASS == 2 ? 1.f : mr[bc * 2 + 1];
+      ga[u] = zmask ? gamma[c0 + u] : 0.f;
+      be[u] = zmask ? bnb[c0 + u] : 0.f;
       s1[u] = 0.f; s2[u] = 0.f;
       if (PASS == 1) {
         k1[u] = (float)sums[bc * 2] * inv;          // mean(g)
@@ -453,6 +465,9 @@ __global__ void __launch_bounds__(NT) bn_bwd_kernel(const cvl_bf16* __restrict__
             unpack8(vy[q], yy);
 #pragma unroll
             for (int u = 0; u < 8; ++u) g[u] = yy[u] > 0.f ? g[u] : 0.f;
+          } else if (zmask) {
+#pragma unroll
+            for (int u = 0; u < 8; ++u) g[u] = bn_affine(zz[u], m[u], rs[u], ga[u], be[u]) > 0.f ? g[u] : 0.f;
           }
           if (PASS == 0) {
             if (ok) {
@@ -770,6 +785,110 @@ inline void colsum8_geometry(int ncol, long nrows, int* ncol8, int* rows_per_blk
   *nblk = (int)((nrows + rpb - 1) / rpb);
 }
 
+// Batched bias gradients (cvl_bias_grad_multi): block -> (item, image, row chunk) through the
+// per-item block prefix; rows of a block lie in one image (no per-row division).  Pass 1 writes
+// per-block column partials, pass 2 (one block per item) sums them in block order in float64.
+struct BiasMulti {
+  cvl_bias_item it[CVL_BIAS_MAX_ITEMS];
+  int blk0[CVL_BIAS_MAX_ITEMS + 1];   // first block of each item (prefix), blk0[n] = grid
+  int chunks[CVL_BIAS_MAX_ITEMS];     // row chunks per image
+  int rpb[CVL_BIAS_MAX_ITEMS];        // rows per chunk (multiple of the item's rows per pass)
+  long poff[CVL_BIAS_MAX_ITEMS];      // float offset of the item's partials in the workspace
+  int n;
+  float* part;
+};
+
+__global__ void __launch_bounds__(NT) colsum_multi_kernel(BiasMulti m) {
+  int i = 0;
+  for (int k = 1; k < m.n; ++k)
+    if ((int)blockIdx.x >= m.blk0[k]) i = k;
+  const cvl_bias_item& it = m.it[i];
+  const int local = blockIdx.x - m.blk0[i];
+  const int b = local / m.chunks[i], chunk = local - b * m.chunks[i];
+  const int ncol8 = (it.ncol + 7) / 8, tpr = ncol8, rpp = NT / tpr;
+  const int cg = threadIdx.x % tpr, rsub = threadIdx.x / tpr;
+  const int r0 = chunk * m.rpb[i];
+  const int r1 = min(r0 + m.rpb[i], it.HW);
+  const cvl_bf16* dy = reinterpret_cast<const cvl_bf16*>(it.dy) + (it.base + (long)b * it.img_stride) * it.ld +
+                       it.coff + cg * 8;
+  float s[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  if (rsub < rpp) {
+    for (int r = r0 + rsub; r < r1; r += rpp * CS_UNR) {
+      s16x8 v[CS_UNR];
+#pragma unroll
+      for (int q = 0; q < CS_UNR; ++q) {
+        const int rq = min(r + q * rpp, r1 - 1);        // clamped: loads stay unconditional
+        v[q] = *reinterpret_cast<const s16x8*>(dy + (long)rq * it.ld);
+      }
+#pragma unroll
+      for (int q = 0; q < CS_UNR; ++q) {
+        if (r + q * rpp >= r1) break;
+        float f[8];
+        unpack8(v[q], f);
+#pragma unroll
+        for (int u = 0; u < 8; ++u) s[u] += f[u];
+      }
+    }
+  }
+  __shared__ float red[NT][9];
+#pragma unroll
+  for (int u = 0; u < 8; ++u) red[threadIdx.x][u] = s[u];
+  __syncthreads();
+  if (rsub == 0) {
+    float* pp = m.part + m.poff[i] + (long)local * ncol8 * 8 + cg * 8;
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      float a = 0.f;
+      for (int k = 0; k < rpp; ++k) a += red[k * tpr + cg][u];
+      pp[u] = a;
+    }
+  }
+}
+
+__global__ void __launch_bounds__(256) colsum_multi_finish_kernel(BiasMulti m) {
+  const int i = blockIdx.x;
+  const cvl_bias_item& it = m.it[i];
+  const int nblk = m.blk0[i + 1] - m.blk0[i], ld = (it.ncol + 7) / 8 * 8;
+  for (int c = threadIdx.x; c < it.ncol; c += 256) {
+    double a = 0.0;
+    const float* p = m.part + m.poff[i] + c;
+    for (int k = 0; k < nblk; ++k) a += p[(long)k * ld];
+    it.db[c] = (float)a + (it.beta != 0.f ? it.beta * it.db[c] : 0.f);
+  }
+}
+
+// per-item geometry: ~16+ passes of rows per block, chunks per image so the launch has work for
+// every CU without tiny blocks
+inline bool bias_multi_plan(const cvl_bias_item* items, int n, BiasMulti* m, long* total_floats) {
+  if (n <= 0 || n > CVL_BIAS_MAX_ITEMS) return false;
+  int blk = 0;
+  long off = 0;
+  for (int i = 0; i < n; ++i) {
+    const cvl_bias_item& it = items[i];
+    if (!it.dy || !it.db || it.ncol <= 0 || it.ncol > 8 * NT || it.HW <= 0 || it.B <= 0 || it.ld % 8 ||
+        it.coff % 8 || it.coff + (it.ncol + 7) / 8 * 8 > it.ld)
+      return false;
+    const int ncol8 = (it.ncol + 7) / 8, rpp = NT / ncol8;
+    int rpb = rpp * CS_UNR * 4;
+    const long want = (long)it.B * it.HW / 96 + 1;      // ~96 blocks of rows per item at most
+    if (want > rpb) rpb = (int)((want + rpp - 1) / rpp * rpp);
+    if (rpb > it.HW) rpb = (it.HW + rpp - 1) / rpp * rpp;
+    m->it[i] = it;
+    m->rpb[i] = rpb;
+    m->chunks[i] = (it.HW + rpb - 1) / rpb;
+    m->blk0[i] = blk;
+    m->poff[i] = off;
+    const int nb = it.B * m->chunks[i];
+    blk += nb;
+    off += (long)nb * ncol8 * 8;
+  }
+  m->blk0[n] = blk;
+  m->n = n;
+  m->part = nullptr;
+  *total_floats = off;
+  return true;
+}
+
 // ---------------------------------------------------------------------------------------------
 // optimizer: clip_by_global_norm(g * inv_bs, clip) + Keras SGD momentum, flat fp32 buffers
 // ---------------------------------------------------------------------------------------------
@@ -990,10 +1109,10 @@ extern "C" size_t cvl_bn_backward_workspace_size(int B, int HW, int C) {
   return sizeof(double) * 2 * ((size_t)B * C + C) + sizeof(float) * 2 * 2 * (size_t)B * nchunk * C;
 }
 
-extern "C" int cvl_bn_backward(const void* dy, const void* y_relu, const void* z, const float* mean_rstd,
-                               const float* gamma, void* workspace, size_t workspace_bytes, void* dz, void* g_out,
-                               float* dgamma, float* dbeta, float beta_acc, float* conv_dbias, int B, int HW,
-                               int C, cvl_stream_t stream) {
+static int bn_backward_impl(const void* dy, const void* y_relu, const float* bn_beta, const void* z,
+                            const float* mean_rstd, const float* gamma, void* workspace, size_t workspace_bytes,
+                            void* dz, void* g_out, float* dgamma, float* dbeta, float beta_acc, float* conv_dbias,
+                            int B, int HW, int C, cvl_stream_t stream) {
   CVL_CHECK_ARG(dy && z && mean_rstd && gamma && workspace && dz && dgamma && dbeta && C % 8 == 0);
   CVL_CHECK_ARG(B > 0 && HW > 0 && (C / 8 <= NT || (C / 8) % NT == 0));
   CVL_CHECK_ARG(workspace_bytes >= cvl_bn_backward_workspace_size(B, HW, C));
@@ -1006,13 +1125,30 @@ extern "C" int cvl_bn_backward(const void* dy, const void* y_relu, const void* z
   dim3 g1(nchunk, B);
   hipLaunchKernelGGL(bn_bwd_kernel<0>, g1, dim3(NT), 0, S_, (const cvl_bf16*)dy, (const cvl_bf16*)y_relu,
                      (const cvl_bf16*)z, mean_rstd, gamma, (const double*)nullptr, (cvl_bf16*)nullptr,
-                     (cvl_bf16*)nullptr, part0, C, HW, rpb, 1, 0.f, BnPG{});
+                     (cvl_bf16*)nullptr, part0, C, HW, rpb, 1, 0.f, BnPG{}, bn_beta);
   hipLaunchKernelGGL(bn_colsum_kernel, dim3((C + 31) / 32, B), dim3(NT), 0, S_, (const float*)part0, nchunk, C,
                      sums);
   hipLaunchKernelGGL(bn_bwd_kernel<1>, g1, dim3(NT), 0, S_, (const cvl_bf16*)dy, (const cvl_bf16*)y_relu,
                      (const cvl_bf16*)z, mean_rstd, gamma, (const double*)sums, (cvl_bf16*)dz, (cvl_bf16*)g_out,
-                     (float*)nullptr, C, HW, rpb, 1, 0.f, BnPG{dgamma, dbeta, conv_dbias, beta_acc});
+                     (float*)nullptr, C, HW, rpb, 1, 0.f, BnPG{dgamma, dbeta, conv_dbias, beta_acc}, bn_beta);
   return cvl_launch_status();
+}
+
+extern "C" int cvl_bn_backward(const void* dy, const void* y_relu, const void* z, const float* mean_rstd,
+                               const float* gamma, void* workspace, size_t workspace_bytes, void* dz, void* g_out,
+                               float* dgamma, float* dbeta, float beta_acc, float* conv_dbias, int B, int HW,
+                               int C, cvl_stream_t stream) {
+  return bn_backward_impl(dy, y_relu, nullptr, z, mean_rstd, gamma, workspace, workspace_bytes, dz, g_out, dgamma,
+                          dbeta, beta_acc, conv_dbias, B, HW, C, stream);
+}
+
+extern "C" int cvl_bn_backward_relu(const void* dy, const void* z, const float* mean_rstd, const float* gamma,
+                                    const float* beta, void* workspace, size_t workspace_bytes, void* dz,
+                                    float* dgamma, float* dbeta, float beta_acc, float* conv_dbias, int B, int HW,
+                                    int C, cvl_stream_t stream) {
+  CVL_CHECK_ARG(beta);
+  return bn_backward_impl(dy, nullptr, beta, z, mean_rstd, gamma, workspace, workspace_bytes, dz, nullptr, dgamma,
+                          dbeta, beta_acc, conv_dbias, B, HW, C, stream);
 }
 
 extern "C" int cvl_maxpool3x3s2(const void* x, void* y, uint8_t* argmax, int B, int H, int W, int C,
@@ -1092,6 +1228,25 @@ extern "C" int cvl_bias_grad(const void* dy, int ld, int coff, int ncol, int64_t
   return cvl_launch_status();
 }
 
+extern "C" size_t cvl_bias_grad_multi_workspace_size(const cvl_bias_item* items, int n) {
+  BiasMulti m;
+  long tot = 0;
+  if (!items || !bias_multi_plan(items, n, &m, &tot)) return 0;
+  return sizeof(float) * (size_t)tot;
+}
+
+extern "C" int cvl_bias_grad_multi(const cvl_bias_item* items, int n, void* workspace, size_t workspace_bytes,
+                                   cvl_stream_t stream) {
+  BiasMulti m;
+  long tot = 0;
+  CVL_CHECK_ARG(items && workspace && bias_multi_plan(items, n, &m, &tot));
+  CVL_CHECK_ARG(workspace_bytes >= sizeof(float) * (size_t)tot);
+  m.part = reinterpret_cast<float*>(workspace);
+  hipLaunchKernelGGL(colsum_multi_kernel, dim3(m.blk0[n]), dim3(NT), 0, S_, m);
+  hipLaunchKernelGGL(colsum_multi_finish_kernel, dim3(n), dim3(256), 0, S_, m);
+  return cvl_launch_status();
+}
+
 extern "C" int cvl_sgd_clip_update(float* w, const float* g, float* v, int64_t n, const float* lr_dev,
                                    float momentum, float inv_bs, float clip, double* sumsq_ws,
                                    cvl_stream_t stream) {
@@ -1153,7 +1308,8 @@ extern "C" int cvl_bn_stats(const void* x, int B, int HW, int C, double* stats, 
   float* part = reinterpret_cast<float*>(workspace);
   hipLaunchKernelGGL(bn_bwd_kernel<2>, dim3(nchunk, B), dim3(NT), 0, S_, (const cvl_bf16*)x,
                      (const cvl_bf16*)nullptr, (const cvl_bf16*)nullptr, (const float*)nullptr, (const float*)nullptr,
-                     (const double*)nullptr, (cvl_bf16*)nullptr, (cvl_bf16*)nullptr, part, C, HW, rpb, 1, 0.f, BnPG{});
+                     (const double*)nullptr, (cvl_bf16*)nullptr, (cvl_bf16*)nullptr, part, C, HW, rpb, 1, 0.f, BnPG{},
+                     (const float*)nullptr);
   hipLaunchKernelGGL(bn_colsum_kernel, dim3((C + 31) / 32, B), dim3(NT), 0, S_, (const float*)part, nchunk, C,
                      stats);
   return cvl_launch_status();
@@ -1191,7 +1347,7 @@ extern "C" int cvl_bn_backward_grouped(const void* dy, const void* y_relu, const
   dim3 g1(nchunk, B);
   hipLaunchKernelGGL(bn_bwd_kernel<0>, g1, dim3(NT), 0, S_, (const cvl_bf16*)dy, (const cvl_bf16*)y_relu,
                      (const cvl_bf16*)z, mean_rstd, gamma, (const double*)nullptr, (cvl_bf16*)nullptr,
-                     (cvl_bf16*)nullptr, part0, C, HW, rpb, group, 0.f, BnPG{});
+                     (cvl_bf16*)nullptr, part0, C, HW, rpb, group, 0.f, BnPG{}, (const float*)nullptr);
   hipLaunchKernelGGL(bn_colsum_kernel, dim3((C + 31) / 32, B), dim3(NT), 0, S_, (const float*)part0, nchunk, C,
                      sums);
   const double* use = sums;
@@ -1202,6 +1358,7 @@ extern "C" int cvl_bn_backward_grouped(const void* dy, const void* y_relu, const
   }
   hipLaunchKernelGGL(bn_bwd_kernel<1>, g1, dim3(NT), 0, S_, (const cvl_bf16*)dy, (const cvl_bf16*)y_relu,
                      (const cvl_bf16*)z, mean_rstd, gamma, use, (cvl_bf16*)dz, (cvl_bf16*)nullptr,
-                     (float*)nullptr, C, HW, rpb, group, dz_beta, BnPG{dgamma, dbeta, nullptr, 0.f, sums});
+                     (float*)nullptr, C, HW, rpb, group, dz_beta, BnPG{dgamma, dbeta, nullptr, 0.f, sums},
+                     (const float*)nullptr);
   return cvl_launch_status();
 }

@@ -41,6 +41,7 @@ SIGNATURES = {
     "cvl_bn_finalize_apply": (c_int, [P, P, P, P, P, P, P, P, P, c_int, c_int, c_int, c_int, c_float, c_float, P]),
     "cvl_bn_backward_workspace_size": (c_size_t, [c_int, c_int, c_int]),
     "cvl_bn_backward": (c_int, [P, P, P, P, P, P, c_size_t, P, P, P, P, c_float, P, c_int, c_int, c_int, P]),
+    "cvl_bn_backward_relu": (c_int, [P, P, P, P, P, P, c_size_t, P, P, P, c_float, P, c_int, c_int, c_int, P]),
     "cvl_maxpool3x3s2": (c_int, [P, P, P, c_int, c_int, c_int, c_int, P]),
     "cvl_maxpool3x3s2_backward": (c_int, [P, P, P, c_int, c_int, c_int, c_int, P]),
     "cvl_upsample2x_add": (c_int, [P, P, P, c_int, c_int, c_int, c_int, P]),
@@ -48,6 +49,8 @@ SIGNATURES = {
     "cvl_relu_backward": (c_int, [P, P, P, ctypes.c_long, c_float, P]),
     "cvl_add": (c_int, [P, P, P, ctypes.c_long, P]),
     "cvl_bias_grad_workspace_size": (c_size_t, [c_int, c_int, c_int]),
+    "cvl_bias_grad_multi_workspace_size": (c_size_t, [P, c_int]),
+    "cvl_bias_grad_multi": (c_int, [P, c_int, P, c_size_t, P]),
     "cvl_bias_grad": (c_int, [P, c_int, c_int, c_int, ctypes.c_int64, ctypes.c_int64, c_int, c_int, P, c_size_t,
                               P, c_float, P]),
     "cvl_sgd_clip_update": (c_int, [P, P, P, ctypes.c_int64, P, c_float, c_float, c_float, P, P]),

@@ -50,15 +50,18 @@ class FCOSNet(FPNDetector):
         # tower layer's data gradient as one paired launch (FPNDetector.trunk_backward)
         a0 = towers[0][0]
         dA_pair = torch.empty((2,) + tuple(a0.shape), dtype=a0.dtype, device=a0.device)
+        # the ten per-level head bias gradients (column sums of the loss gradients): one launch pair
+        nn.bias_grad_multi([(dout, int(dout.shape[-1]), 0, heads[l].cout, off[l], P, h * w, B, heads[l].db, 0.0)
+                            for heads, dout in ((self.cls_heads, d_cls), (self.reg_heads, d_reg))
+                            for l, (h, w) in enumerate(shapes)])
         for heads, acts, dout in ((self.cls_heads, towers[0], d_cls), (self.reg_heads, towers[1], d_reg)):
             ld = int(dout.shape[-1])
-            # heads: weight/bias grads per level, data grad for all levels in one launch
+            # heads: weight grads per level, data grad for all levels in one launch
             for l, (h, w) in enumerate(shapes):
                 hd = heads[l]
                 d = hd.fwd_desc(B, [nn.seg(h, w, h, w, hd.wf, None, src_base=B * off[l], src_img=h * w,
                                            dst_base=off[l], dst_img=P)], ld_dst=ld)
                 nn.conv_wgrad(d, acts[-1], dout, hd.dw)
-                nn.bias_grad(dout, ld, 0, hd.cout, off[l], P, h * w, B, hd.db)
             dA = dA_pair[len(dAs)]
             segs = [nn.seg(h, w, h, w, heads[l].wd, None, src_base=off[l], src_img=P, dst_base=B * off[l],
                            dst_img=h * w) for l, (h, w) in enumerate(shapes)]

@@ -276,7 +276,8 @@ class FPNDetector(object):
         d = self.c7_3x3.fwd_desc(B, [nn.seg(h7, w7, h6, w6, self.c7_3x3.wf, None, src_base=B * off[3],
                                             dst_base=B * off[4])], ld_dst=FPN_C, relu_in=True)
         nn.conv_wgrad(d, F, dF, self.c7_3x3.dw)
-        nn.bias_grad(dF, FPN_C, 0, FPN_C, B * off[4], h7 * w7, h7 * w7, B, self.c7_3x3.db)
+        # bias gradients of the eight FPN convs: collected, then one batched launch pair
+        bias_items = [(dF, FPN_C, 0, FPN_C, B * off[4], h7 * w7, h7 * w7, B, self.c7_3x3.db, 0.0)]
         dr6 = torch.empty((B, h6, w6, FPN_C), dtype=BF16, device=dev)
         dd = self.c7_3x3.dgrad_desc(B, [nn.seg(h6, w6, h7, w7, self.c7_3x3.wd, None, src_base=B * off[4])],
                                     ld_dst=FPN_C)
@@ -300,7 +301,7 @@ class FPNDetector(object):
             Ho, Wo = shapes[l]
             d = conv.fwd_desc(B, [nn.seg(Ho, Wo, h, w, conv.wf, None, dst_base=B * off[l])], ld_dst=FPN_C)
             nn.conv_wgrad(d, src, dF, conv.dw)
-            nn.bias_grad(dF, FPN_C, 0, FPN_C, B * off[l], Ho * Wo, Ho * Wo, B, conv.db)
+            bias_items.append((dF, FPN_C, 0, FPN_C, B * off[l], Ho * Wo, Ho * Wo, B, conv.db, 0.0))
             if FUSE_FPN and l < 3:            # P3..P5 data gradients: one 3-segment launch below
                 trio.append(nn.seg(h, w, Ho, Wo, conv.wd, None, src_base=B * off[l], dst_base=pr_base[l]))
                 continue
@@ -319,8 +320,10 @@ class FPNDetector(object):
         for conv, src, h, w, dl, dC, beta in ((self.c3_1x1, c3, H3, W3, dl3, dC3, 0.0),
                                               (self.c4_1x1, c4, H4, W4, dl4, dC4, 0.0),
                                               (self.c5_1x1, c5, H5, W5, dl5, dC5, 1.0)):
-            conv.wgrad(src, dl, B, h, w)
+            conv.wgrad(src, dl, B, h, w, bias=False)
+            bias_items.append((dl, FPN_C, 0, FPN_C, 0, h * w, h * w, B, conv.db, 0.0))
             conv.dgrad(dl, B, h, w, out=dC, beta=beta)
+        nn.bias_grad_multi(bias_items)
         hook("fpn")
         self.backbone.backward([dC3, dC4, dC5], s["bsv"], hook=hook)
         self._saved = None

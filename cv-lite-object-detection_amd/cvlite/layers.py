@@ -290,15 +290,19 @@ class ConvBN(object):
                                                                              device=x.device)
         z, _, _ = self.conv.fwd(x, B, H, W, stats=stats)
         y, mr = self.bn.normalize(z, stats, B, Ho * Wo, relu, residual=residual, train=train)
-        return y, (x, z, y, mr, B, H, W, Ho, Wo, relu)
+        return y, (x, z, y, mr, B, H, W, Ho, Wo, relu, residual is not None)
 
     def backward(self, dy, saved, dx_out=None, dx_beta=0.0, g_out=None, need_dx=True):
-        x, z, y, mr, B, H, W, Ho, Wo, relu = saved
+        x, z, y, mr, B, H, W, Ho, Wo, relu, has_res = saved
         c = self.conv.cout
         dz = torch.empty_like(z)
-        nn.bn_backward(dy, y if relu else None, z, mr, self.bn.gamma, dz, g_out,
-                       self.bn.store.g(self.bn.gname), self.bn.store.g(self.bn.bname), B, Ho * Wo, c,
-                       conv_dbias=self.conv.db)
+        st = self.bn.store
+        if relu and not has_res and g_out is None:      # ReLU mask rebuilt from z: y is not read
+            nn.bn_backward_relu(dy, z, mr, self.bn.gamma, self.bn.beta, dz, st.g(self.bn.gname),
+                                st.g(self.bn.bname), B, Ho * Wo, c, conv_dbias=self.conv.db)
+        else:
+            nn.bn_backward(dy, y if relu else None, z, mr, self.bn.gamma, dz, g_out, st.g(self.bn.gname),
+                           st.g(self.bn.bname), B, Ho * Wo, c, conv_dbias=self.conv.db)
         self.conv.wgrad(x, dz, B, H, W, bias=False)
         if not need_dx:
             return None

@@ -151,6 +151,14 @@ def bn_backward(dy, y_relu, z, mean_rstd, gamma, dz, g_out, dgamma, dbeta, B, HW
               stream())
 
 
+def bn_backward_relu(dy, z, mean_rstd, gamma, beta, dz, dgamma, dbeta, B, HW, C, beta_acc=0.0, conv_dbias=None):
+    """bn_backward of a BN -> ReLU unit without a residual add: the mask is rebuilt from z."""
+    n = int(_lib.load().cvl_bn_backward_workspace_size(B, HW, C))
+    ws = torch.empty(n, dtype=torch.uint8, device=dy.device)
+    _lib.call("cvl_bn_backward_relu", ptr(dy), ptr(z), ptr(mean_rstd), ptr(gamma), ptr(beta), ptr(ws), n, ptr(dz),
+              ptr(dgamma), ptr(dbeta), float(beta_acc), ptr(conv_dbias), B, HW, C, stream())
+
+
 def maxpool3x3s2(x, y, argmax):
     B, H, W, C = x.shape
     _lib.call("cvl_maxpool3x3s2", ptr(x), ptr(y), ptr(argmax), B, H, W, C, stream())
@@ -182,6 +190,32 @@ def bias_grad(dy, ld, coff, ncol, base, img_stride, HW, B, db, beta=0.0):
     ws = torch.empty(max(n, 16), dtype=torch.uint8, device=dy.device)
     _lib.call("cvl_bias_grad", ptr(dy), ld, coff, ncol, int(base), int(img_stride), HW, B, ptr(ws), ws.numel(),
               ptr(db), float(beta), stream())
+
+
+class BiasItem(ctypes.Structure):
+    _fields_ = [("dy", c_void_p), ("db", c_void_p), ("base", ctypes.c_int64), ("img_stride", ctypes.c_int64),
+                ("ld", c_int), ("coff", c_int), ("ncol", c_int), ("HW", c_int), ("B", c_int), ("beta", ctypes.c_float)]
+
+
+BIAS_MAX_ITEMS = 16
+
+
+def bias_grad_multi(items):
+    """Several bias gradients in one launch pair (cvl_bias_grad_multi).  items: list of
+    (dy, ld, coff, ncol, base, img_stride, HW, B, db, beta) -- bias_grad's arguments."""
+    for k in range(0, len(items), BIAS_MAX_ITEMS):
+        chunk = items[k:k + BIAS_MAX_ITEMS]
+        arr = (BiasItem * len(chunk))()
+        dev = chunk[0][0].device
+        for i, (dy, ld, coff, ncol, base, img_stride, HW, B, db, beta) in enumerate(chunk):
+            _lib.require_cuda(dy, db)
+            arr[i] = BiasItem(dy.data_ptr(), db.data_ptr(), int(base), int(img_stride), int(ld), int(coff), int(ncol),
+                              int(HW), int(B), float(beta))
+        n = int(_lib.load().cvl_bias_grad_multi_workspace_size(arr, len(chunk)))
+        if n == 0:
+            raise _lib.CvlError("cvl_bias_grad_multi: invalid items")
+        ws = torch.empty(n, dtype=torch.uint8, device=dev)
+        _lib.call("cvl_bias_grad_multi", arr, len(chunk), ptr(ws), ws.numel(), stream())
 
 
 def sgd_clip_update(w, g, v, lr_dev, momentum, inv_bs, clip, ws=None):

@@ -68,8 +68,8 @@ class Stem(object):
         nn.maxpool3x3s2_backward(dp, arg, dy)
         dz = torch.empty_like(z)
         st = self.bn.store
-        nn.bn_backward(dy, y, z, mr, self.bn.gamma, dz, None, st.g(self.bn.gname), st.g(self.bn.bname),
-                       B, Ho * Wo, 64, conv_dbias=self.conv.db)
+        nn.bn_backward_relu(dy, z, mr, self.bn.gamma, self.bn.beta, dz, st.g(self.bn.gname), st.g(self.bn.bname),
+                            B, Ho * Wo, 64, conv_dbias=self.conv.db)
         dw = torch.empty((STEM_KP, 64), dtype=torch.float32, device=dp.device)
         nn.conv_wgrad(self._desc(B, Ho, Wo), A, dz, dw)
         self.conv.dw.view(147, 64).copy_(dw[:147])

@@ -199,6 +199,14 @@ int cvl_bn_backward(const void* dy, const void* y_relu, const void* z, const flo
                     const float* gamma, void* workspace, size_t workspace_bytes, void* dz, void* g_out,
                     float* dgamma, float* dbeta, float beta_acc, float* conv_dbias, int B, int HW, int C,
                     cvl_stream_t stream);
+/* cvl_bn_backward for a unit that ends in ReLU WITHOUT a residual add (the conv1/conv2 units of a
+ * Keras ResNet bottleneck, the stem): the ReLU mask is recomputed from z as
+ * fma(gamma, (z - mean) * rstd, beta) > 0 -- the forward's own arithmetic (cvl_bn_apply) -- so y
+ * is not read (two passes read 2 tensors instead of 3).  beta = the BN's beta parameter. */
+int cvl_bn_backward_relu(const void* dy, const void* z, const float* mean_rstd, const float* gamma,
+                         const float* beta, void* workspace, size_t workspace_bytes, void* dz, float* dgamma,
+                         float* dbeta, float beta_acc, float* conv_dbias, int B, int HW, int C,
+                         cvl_stream_t stream);
 
 /* ResNet50 pool1: ZeroPadding2D(1) + MaxPooling2D(3, 2); argmax [B][Ho][Wo][C] uint8 (0..8). */
 int cvl_maxpool3x3s2(const void* x, void* y, uint8_t* argmax, int B, int H, int W, int C,
@@ -219,6 +227,22 @@ int cvl_add(const void* a, const void* b, void* out, long n, cvl_stream_t stream
 size_t cvl_bias_grad_workspace_size(int ncol, int HW, int B);
 int cvl_bias_grad(const void* dy, int ld, int coff, int ncol, int64_t base, int64_t img_stride, int HW,
                   int B, void* workspace, size_t workspace_bytes, float* db, float beta, cvl_stream_t stream);
+/* Batched form of cvl_bias_grad: up to CVL_BIAS_MAX_ITEMS bias gradients (e.g. the per-level
+ * heads `logits_output_l` / `reg_output_l` of FCOS/fcos.py:85-101, the FPN convs of fcos.py:49-74)
+ * in ONE partial-sum launch + ONE fixed-order finish launch.  items: HOST array (passed by value to
+ * the kernels, so the call is graph-capturable); same per-item contract as cvl_bias_grad with
+ * ncol <= 2048; workspace >= cvl_bias_grad_multi_workspace_size(items, n) bytes. */
+#define CVL_BIAS_MAX_ITEMS 16
+typedef struct {
+  const void* dy;      /* bf16 rows [*][ld] */
+  float* db;           /* fp32 [ncol] */
+  int64_t base, img_stride;
+  int ld, coff, ncol, HW, B;
+  float beta;
+} cvl_bias_item;
+size_t cvl_bias_grad_multi_workspace_size(const cvl_bias_item* items, int n);
+int cvl_bias_grad_multi(const cvl_bias_item* items, int n, void* workspace, size_t workspace_bytes,
+                        cvl_stream_t stream);
 
 /* ------------------------------------------------------------------------------------------
  * Optimizer (train_fcos.py:179-185): g <- (g * inv_bs) clipped by global norm `clip`

@@ -81,6 +81,14 @@ def test_bn_forward_backward(B, HW, C, relu, res):
         torch.testing.assert_close(gout.double().cpu(), dy * (y.double().cpu() > 0))
     torch.testing.assert_close(dgam.double().cpu(), gg.grad, rtol=2e-2, atol=2e-2 * gg.grad.abs().max().item())
     torch.testing.assert_close(dbet.double().cpu(), bb.grad, rtol=2e-2, atol=2e-2 * bb.grad.abs().max().item())
+    if relu and not res:
+        # the non-residual form rebuilds the ReLU mask from z: bit-identical to reading y
+        dz2, dgam2, dbet2 = torch.empty_like(zg), torch.zeros(C, device="cuda"), torch.zeros(C, device="cuda")
+        cdb2 = torch.full((C,), 7.0, device="cuda")
+        nn.bn_backward_relu(dy.to(BF).cuda(), zg, mr, gamma.float().cuda(), beta.float().cuda(), dz2, dgam2, dbet2,
+                            B, HW, C, conv_dbias=cdb2)
+        assert torch.equal(dz2.view(torch.int16), dz.view(torch.int16))
+        assert torch.equal(dgam2, dgam) and torch.equal(dbet2, dbet) and torch.count_nonzero(cdb2).item() == 0
 
 
 def test_maxpool_and_upsample():
@@ -136,6 +144,35 @@ def test_relu_bwd_bias_grad_sgd_lr():
         nn.bias_grad(t.to(BF).cuda(), ld, coff, ncol, base, P, HW, B, db)
         exp = t[:, base:base + HW, coff:coff + ncol].sum((0, 1))
         torch.testing.assert_close(db.double().cpu(), exp, rtol=1e-5, atol=1e-3)
+    # batched form: FCOS heads (5 levels x 2 heads at 512 / bs 16), a RetinaNet 720-column head,
+    # an FPN-style level of a packed [rows, 256] buffer, a beta-accumulating item; one launch pair
+    B, P = 16, 5456
+    d_cls = bfr(torch.randn(B, P, 32, generator=g, dtype=torch.float64))
+    d_ret = bfr(torch.randn(2, 300, 736, generator=g, dtype=torch.float64))
+    fpn = bfr(torch.randn(B * 100 + 37, 256, generator=g, dtype=torch.float64))
+    dc, dr, df = d_cls.to(BF).cuda(), d_ret.to(BF).cuda(), fpn.to(BF).cuda()
+    items, exps = [], []
+    off = 0
+    for s in (64, 32, 16, 8, 4):
+        for ncol in (20, 5):
+            db = torch.zeros(ncol, device="cuda")
+            items.append((dc, 32, 0, ncol, off, P, s * s, B, db, 0.0))
+            exps.append((db, d_cls[:, off:off + s * s, :ncol].sum((0, 1))))
+        off += s * s
+    db = torch.zeros(720, device="cuda")
+    items.append((dr, 736, 0, 720, 17, 300, 250, 2, db, 0.0))
+    exps.append((db, d_ret[:, 17:267, :720].sum((0, 1))))
+    db = torch.full((256,), 2.0, device="cuda")
+    items.append((df, 256, 0, 256, 37, 100, 100, B, db, 0.5))
+    exps.append((db, 1.0 + fpn[37:].reshape(B, 100, 256).sum((0, 1))))
+    nn.bias_grad_multi(items)
+    for db, exp in exps:
+        torch.testing.assert_close(db.double().cpu(), exp, rtol=1e-5, atol=2e-3)
+    # deterministic: a second launch gives the same bits
+    first = [db.clone() for db, _ in exps[:-1]]
+    nn.bias_grad_multi(items[:-1])
+    for a, (db, _) in zip(first, exps[:-1]):
+        assert torch.equal(a, db)
     # clip + SGD (Keras form), lr from device memory
     n = 100003
     w = torch.randn(n, generator=g)
