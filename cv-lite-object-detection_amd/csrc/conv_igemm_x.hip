@@ -408,6 +408,272 @@ __global__ void __launch_bounds__(NT) conv_igemm_x32_kernel(ConvArgs a) {
   conv_l_epilogue<BN, WGM, TM, TN, NT>(a, S, acc, lds, tid, wm, wn, n0, mloc0, HWr);
 }
 
+// ---------------------------------------------------------------------------------------------
+// X32H: the X32 schedule for 3x3 / stride 1 / pad 1 convolutions (fwd and dgrad) with the A
+// operand held as an LDS HALO instead of nine shifted im2col tiles.  The nine taps of a channel
+// block re-read the same input pixels; here the input pixels of a tile are staged ONCE per
+// 32-channel block and every tap reads its A fragments at a pixel offset dy * pitch + dx.
+// * Halo image of a tile: single-image tiles (H*W >= 256: R = 256 / W whole rows) hold rows
+//   y0-1 .. y0+R of width W+2 (zero columns at both sides); tiles of whole small images
+//   (H*W < 256: 256 / HW images) hold a mosaic of mx x my images separated by shared one-pixel zero
+//   borders.  Rows are padded to a pitch that is a multiple of 8 pixels (64-B pixels), so a dy
+//   shift never changes the XOR swizzle of a pixel ((p >> 1) & 3 on its 16-B chunk): each lane
+//   precomputes, per A fragment, the swizzled LDS address for dx = -1, 0, +1, and a tap adds the
+//   wave-uniform dy * pitch * 64 (one VALU add per fragment per K-tile).  Zero padding (image
+//   borders, mosaic seams, absent images) is written by out-of-range DMA.
+// * LDS: two halo buffers (<= 512 px = 32 KiB each; block cb in buffer cb & 1, block cb + 1's 32
+//   DMA pieces issued in taps 1-4 of block cb, one per wave per phase) + a 6-slot weight ring
+//   (16 KiB per 32-deep K-tile) = 160 KiB.  Phase t: [wait for weight tile t+1 (vmcnt = DMAs issued
+//   after it in phases t-2, t-1: two weight tiles + their halo pieces); issue a halo piece (taps
+//   1-4); issue weight tile t+4; read A from the halo, B from the ring] barrier [32 MFMAs] barrier, the
+//   two wave groups staggered as in X32.  Halo buffers and ring slots are refilled two phases
+//   after their last read.  Per K-tile the L2 -> LDS stream is the 16 KiB weight tile plus ~1/9 of
+//   a halo (<= 4.4 KiB) instead of 32 KiB.
+// * Fragment reads: 16 consecutive pixels at any shift are bank-conflict free under the swizzle
+//   (mosaic fragments that cross image rows: at most 2-way).
+// ---------------------------------------------------------------------------------------------
+constexpr int HPX_MAX = 512;                  // halo pixels per buffer (32 DMA pieces of 16)
+constexpr int HPIECE = HPX_MAX / 16 / 8;      // halo DMA pieces per wave (issued in taps 1..HPIECE)
+constexpr int HBUF = HPX_MAX * BK32;          // bf16 elements per halo buffer (32 KiB)
+constexpr int BSLOT = 256 * BK32;             // bf16 elements of one weight ring slot (16 KiB)
+constexpr int NBSLOT = 6;                     // weight tiles t+1 .. t+4 in flight at phase t
+constexpr int LDSH_EL = 2 * HBUF + NBSLOT * BSLOT > LDS_C ? 2 * HBUF + NBSLOT * BSLOT : LDS_C;
+
+// halo geometry of a segment (host and device agree): mosaic columns/rows, image rows per halo
+// image, pitch (pixels, multiple of 8) and halo rows
+struct HaloGeo {
+  int whole, mx, my, th, pitch, rows;
+};
+__host__ __device__ inline HaloGeo halo_geo(int H, int W) {
+  HaloGeo g;
+  const int HW = H * W;
+  g.whole = HW < 256;
+  if (g.whole) {
+    const int n = 256 / HW;
+    int lg = 0;
+    while ((1 << (lg + 1)) <= n) ++lg;
+    g.mx = 1 << ((lg + 1) / 2);
+    g.my = n / g.mx;
+    g.th = H;
+  } else {
+    g.mx = g.my = 1;
+    g.th = 256 / W;
+  }
+  g.pitch = (g.mx * (W + 1) + 1 + 7) & ~7;
+  g.rows = g.my * (g.th + 1) + 1;
+  return g;
+}
+
+template <bool DGRAD, bool DBG>
+__global__ void __launch_bounds__(NT) conv_igemm_x32h_kernel(ConvArgs a) {
+  // DBG: ablation switches (a.dbg bits, CVL_X_ABLATE) for measurement builds only: 1 no halo
+  // traffic, 2 no weight traffic, 4 no MFMA, 8 no barriers, 16 no vmcnt waits, 32 no DMA
+  // instructions, 64 no LDS reads
+  const int dbg = DBG ? a.dbg : 0;
+  __shared__ __attribute__((aligned(16))) cvl_bf16 lds[LDSH_EL];
+
+  const int tid = threadIdx.x;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane0 = tid & 63;
+  const int ntn = a.Npad / BN;
+  const int lane = lane0;
+  const int L = xcd_remap(blockIdx.x, gridDim.x);
+  const int m_tile = L / ntn, n_tile = L % ntn;
+  const int m0 = m_tile * BM, n0 = n_tile * BN;
+  int sg = 0;
+#pragma unroll
+  for (int i = 1; i < kMaxSeg; ++i)
+    if (i < a.nseg && m0 >= a.seg[i].m_start) sg = i;
+  const ConvSeg& S = a.seg[sg];
+  const int HWr = S.Hr * S.Wr;
+  const int mloc0 = m0 - S.m_start;
+  if (mloc0 >= S.rows) return;
+
+  const int Cin = a.Cin, W = S.Wr, H = S.Hr;
+  const int Kdim = a.K;
+  const int ncb = Cin / BK32;
+  const HaloGeo G = halo_geo(H, W);
+  const int img0 = mloc0 / HWr;
+  const int y0 = G.whole ? 0 : (mloc0 - img0 * HWr) / W;
+  const int hpx = G.rows * G.pitch;
+
+  // this lane's halo DMA pieces: piece k = wave + 8 j covers halo pixels 16 k .. 16 k + 15
+  const int hch = lane & 3;
+  unsigned hoff[HPIECE], hmask = 0;
+#pragma unroll
+  for (int j = 0; j < HPIECE; ++j) {
+    const int hp = 16 * (wave + 8 * j) + (lane >> 2);
+    const int hy = hp / G.pitch, hx = hp - hy * G.pitch;
+    int img, gy, gx;
+    bool ok;
+    if (!G.whole) {
+      img = img0;
+      gy = y0 + hy - 1;
+      gx = hx - 1;
+      ok = gy >= 0 && gy < H && gx >= 0 && gx < W;
+    } else {
+      const int ix = (hx - 1) / (W + 1), iy = (hy - 1) / (H + 1);
+      gx = hx - 1 - ix * (W + 1);
+      gy = hy - 1 - iy * (H + 1);
+      img = img0 + iy * G.mx + ix;
+      ok = hx >= 1 && hy >= 1 && gx < W && gy < H && ix < G.mx && iy < G.my;
+    }
+    ok = ok && hp < hpx && img < a.B;
+    const long pix = S.src_base + (long)img * S.src_img + (long)gy * W + gx;
+    hoff[j] = ok ? (unsigned)(pix * Cin * 2) + (unsigned)((hch ^ swz4(hp)) * 16) : 0u;
+    hmask |= ok ? 1u << j : 0u;
+  }
+  // weight DMA piece of this lane (as X32): row x16 of a 128-row block, chunk ch
+  const int x16 = wave * 16 + (lane >> 2);
+  const unsigned boff0 = (unsigned)((n0 + x16) * Kdim * 2) + (unsigned)((hch ^ swz4(x16)) * 16);
+  const __amdgpu_buffer_rsrc_t rsA = __builtin_amdgcn_make_buffer_rsrc((void*)a.src, (short)0, (int)kRecords, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rsB = __builtin_amdgcn_make_buffer_rsrc((void*)S.w, (short)0, (int)kRecords, 0x00020000);
+
+  cvl_bf16* const hb0 = lds;
+  cvl_bf16* const ring = lds + 2 * HBUF;
+  auto issue_halo = [&](int j, int cb) {
+    if (dbg & 32) return;
+    cvl_bf16* dst = hb0 + (cb & 1) * HBUF + (wave + 8 * j) * 16 * BK32;
+    const bool v = cb < ncb && ((hmask >> j) & 1u) && !(dbg & 1);
+    dma16(rsA, dst, v ? hoff[j] + (unsigned)(cb * BK32 * 2) : kOOB);
+  };
+  // weight cursor: K-tile kb = (channel block bcb, tap btap), ring slot bslot
+  int kb = 0, btap = 0, bcb = 0, bslot = 0;
+  const int nk = 9 * ncb;
+  auto issue_b = [&]() {
+    if (dbg & 32) return;
+    const bool live = kb < nk && !(dbg & 2);
+    const unsigned cbk = (unsigned)((btap * Cin + bcb * BK32) * 2);
+    cvl_bf16* Bb = ring + bslot * BSLOT;
+#pragma unroll
+    for (int p = 0; p < 2; ++p)
+      dma16(rsB, Bb + (p * 128 + wave * 16) * BK32, live ? boff0 + (unsigned)(p * 128 * Kdim * 2) + cbk : kOOB);
+    ++kb;
+    bslot = bslot == NBSLOT - 1 ? 0 : bslot + 1;
+    if (++btap == 9) { btap = 0; ++bcb; }
+  };
+
+  const int wm = wave >> 2, wn = wave & 3;
+  const int lr = lane & 15, lg = lane >> 4;
+  // swizzled LDS byte offset (within a halo buffer) of each A fragment row of this lane, for
+  // dx = -1, 0, +1 (the dy shift is added per tap)
+  unsigned afr[TM][3];
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+    const int r = wm * WM + i * 16 + lr;
+    const int ii = r / HWr, q = r - ii * HWr;          // whole-image tiles: image ii of the mosaic
+    const int yy = q / W, xx = q - yy * W;
+    const int hy = 1 + (G.whole ? (ii / G.mx) * (H + 1) : 0) + yy;
+    const int hx = 1 + (G.whole ? (ii % G.mx) * (W + 1) : 0) + xx;
+    const int pc = hy * G.pitch + hx;
+#pragma unroll
+    for (int d = 0; d < 3; ++d) {
+      const int p = pc + d - 1;
+      afr[i][d] = (unsigned)(p * BK32 * 2 + ((lg ^ swz4(p)) * 16));
+    }
+  }
+  f32x4 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  auto bar = [&]() {
+    if (!(dbg & 8)) __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+  };
+
+  // prologue: the halo of channel block 0, weight tiles 0..3; wait for the halo and tile 0
+#pragma unroll
+  for (int j = 0; j < HPIECE; ++j) issue_halo(j, 0);
+  issue_b();
+  issue_b();
+  issue_b();
+  issue_b();
+  wait_vm<6>();
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+  if (wm == 1) bar();           // stagger: waves 4-7 run one barrier behind
+
+  const int prow = G.pitch * BK32 * 2;            // bytes per halo row
+  int rslot = 0;
+  for (int cb = 0; cb < ((dbg & 256) ? 0 : ncb); ++cb) {
+    const char* Hc = reinterpret_cast<const char*>(hb0 + (cb & 1) * HBUF);
+#pragma unroll 1
+    for (int r = 0; r < 3; ++r) {
+      const int dyoff = (DGRAD ? 1 - r : r - 1) * prow;
+#pragma unroll
+      for (int s = 0; s < 3; ++s) {
+        const int d = DGRAD ? 2 - s : s;
+        const int tap = 3 * r + s;
+        // weight tile t+1 landed: after it were issued, in phases t-2 and t-1, weight tiles t+2,
+        // t+3 (2 DMAs each) and a halo piece in each of those phases that is a tap 1..4
+        if (dbg & 16) {
+        } else if (tap >= 3 && tap <= 5) wait_vm<6>();
+        else if (tap == 2 || tap == 6) wait_vm<5>();
+        else wait_vm<4>();
+        if (tap >= 1 && tap <= HPIECE) issue_halo(tap - 1, cb + 1);
+        issue_b();
+        const cvl_bf16* Bc = ring + rslot * BSLOT;
+        s16x8 fa[TM], fb[TN];
+        if (!(dbg & 64)) {
+#pragma unroll
+          for (int i = 0; i < TM; ++i) fa[i] = *reinterpret_cast<const s16x8*>(Hc + afr[i][d] + dyoff);
+#pragma unroll
+          for (int j = 0; j < TN; ++j) {
+            const int rr = wn * WN + j * 16 + lr;
+            fb[j] = *reinterpret_cast<const s16x8*>(Bc + rr * BK32 + ((lg ^ swz4(rr)) * 8));
+          }
+        } else {
+#pragma unroll
+          for (int i = 0; i < TM; ++i) fa[i] = s16x8{(short)lr, 0, 0, 0, 0, 0, 0, (short)s};
+#pragma unroll
+          for (int j = 0; j < TN; ++j) fb[j] = s16x8{(short)j, 0, 0, 0, 0, 0, 0, (short)lg};
+        }
+        bar();
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_sched_barrier(0);
+        __builtin_amdgcn_s_setprio(1);
+        if (!(dbg & 4)) {
+#pragma unroll
+          for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int j = 0; j < TN; ++j)
+              acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, fa[i]),
+                                                                   __builtin_bit_cast(bf16x8, fb[j]), acc[i][j], 0, 0, 0);
+        } else {
+          asm volatile("" ::"v"(fa[0]), "v"(fb[0]), "v"(fa[7]), "v"(fb[3]));
+        }
+        __builtin_amdgcn_s_setprio(0);
+        __builtin_amdgcn_sched_barrier(0);
+        bar();
+        rslot = rslot == NBSLOT - 1 ? 0 : rslot + 1;
+      }
+    }
+  }
+  if (wm == 0) bar();           // equal barrier counts for both groups
+  wait_vm<0>();
+  if (dbg & 128) {
+    if (acc[0][0][0] == 12345.f) a.stats[0] = 1.0;      // keep the accumulators live
+    return;
+  }
+  conv_l_epilogue<BN, WGM, TM, TN, NT>(a, S, acc, lds, tid, wm, wn, n0, mloc0, HWr);
+}
+
+// Geometry the halo kernel covers: 3x3, stride 1, pad 1, source map = output map, and every
+// segment's 256-row tiles are whole rows of one image (W | 256, HW % 256 == 0) or whole images
+// (HW | 256), with the halo image within HPX_MAX pixels.
+static bool x32h_fits(const cvl_conv_desc* d, const ConvArgs& a) {
+  if (d->KH != 3 || d->KW != 3 || d->stride != 1 || d->pad_t != 1 || d->pad_l != 1 || a.Cin % BK32) return false;
+  for (int i = 0; i < a.nseg; ++i) {
+    const ConvSeg& q = a.seg[i];
+    if (q.Hr != q.Hs || q.Wr != q.Ws) return false;
+    const int W = q.Wr, HW = q.Hr * q.Wr;
+    if (HW >= BM ? (BM % W || HW % BM) : (BM % HW)) return false;
+    const HaloGeo g = halo_geo(q.Hr, W);
+    if (g.mx * g.my * (g.whole ? HW : BM) != BM || g.rows * g.pitch > HPX_MAX) return false;
+  }
+  return true;
+}
+
 }  // namespace
 
 // Called by cvl_conv_igemm_l for launches it would run on the 256 x 256 L tile; returns -1 when
@@ -429,7 +695,16 @@ int cvl_conv_igemm_x(const cvl_conv_desc* d, const ConvArgs& a, hipStream_t s) {
   ConvArgs am = a;
   am.dbg = cvl_env_int("CVL_X_ABLATE", 0);
   g_cvl_conv_last_kernel = CVL_CK_X256;
-  if (x32 && !am.dbg) {
+  // the halo variant is opt-in (CVL_CONV_HALO=1): on the FCOS towers it measures at parity with
+  // X32 (both ~0.2 ms; the L2 -> LDS stream it removes is not what bounds X32), see DESIGN.md
+  if (x32 && cvl_env_flag("CVL_CONV_HALO") && x32h_fits(d, a)) {
+    g_cvl_conv_last_kernel = CVL_CK_X32H;
+    if (am.dbg) {
+      if (dg) hipLaunchKernelGGL((conv_igemm_x32h_kernel<true, true>), grid, dim3(NT), 0, s, am);
+      else hipLaunchKernelGGL((conv_igemm_x32h_kernel<false, true>), grid, dim3(NT), 0, s, am);
+    } else if (dg) hipLaunchKernelGGL((conv_igemm_x32h_kernel<true, false>), grid, dim3(NT), 0, s, am);
+    else hipLaunchKernelGGL((conv_igemm_x32h_kernel<false, false>), grid, dim3(NT), 0, s, am);
+  } else if (x32 && !am.dbg) {
     g_cvl_conv_last_kernel = CVL_CK_X32;
     if (dg) hipLaunchKernelGGL((conv_igemm_x32_kernel<true>), grid, dim3(NT), 0, s, am);
     else hipLaunchKernelGGL((conv_igemm_x32_kernel<false>), grid, dim3(NT), 0, s, am);

@@ -92,7 +92,7 @@ def test_tower_pair_fwd_dgrad_configs1_layout():
     nn.conv_igemm(d, src, out)
     code, name = last_kernel()
     print("forward kernel:", name)
-    assert code in (5, 6, 7), name          # the 256x256 LDS-DMA tile the bench's roofline names
+    assert code == 7, name                  # X32: the 256x256 LDS-DMA tile the bench's roofline names
     srcd = src.to(F64)
     for t in range(2):
         for l, (h, w) in enumerate(shapes):
@@ -112,7 +112,7 @@ def test_tower_pair_fwd_dgrad_configs1_layout():
     nn.conv_igemm(dd, dy, dx)
     code, name = last_kernel()
     print("dgrad kernel:", name)
-    assert code in (5, 6, 7), name
+    assert code == 7, name
     dyd = dy.to(F64)
     for t in range(2):
         for l, (h, w) in enumerate(shapes):
@@ -187,3 +187,46 @@ def test_retina_cls_head_f32_epilogue_configs4():
         ref = dgrad_ref(d64[:, off[l]:off[l] + h * w, :N].reshape(B, h, w, N), ws[l])
         got = dx[B * off[l]:B * (off[l] + h * w)].view(B, h, w, C).to(F64)
         torch.testing.assert_close(got, ref, rtol=1e-2, atol=2e-2, msg=lambda m: "dgrad level %d: %s" % (l, m))
+
+
+@pytest.mark.parametrize("mode,B,H,W,C,N", [("fwd", 2, 64, 64, 256, 256), ("dgrad", 3, 32, 32, 512, 256),
+                                           ("fwd", 3, 8, 8, 256, 256), ("dgrad", 5, 4, 4, 256, 512),
+                                           ("fwd", 2, 16, 16, 256, 256), ("fwd", 1, 64, 64, 64, 256)])
+def test_halo_tile_geometries(monkeypatch, mode, B, H, W, C, N):
+    """The opt-in 3x3 halo kernel (X32H, CVL_CONV_HALO=1) on every tile shape it accepts: R image rows of one image
+    (W = 64 / 32 / 16), whole images per tile (8x8: 4, 4x4: 16 per tile, batches that leave
+    the last tile's images partly absent), Cin 64 / 256 / 512, fwd with bias + ReLU + BN statistics
+    and dgrad.  Against fp64 and bit-identical to the X32 kernel (same K order, same MFMA chain)."""
+    from cvlite import ops_nn as nn
+    monkeypatch.setenv("CVL_CONV_L_MIN_TILES", "1")
+    monkeypatch.setenv("CVL_CONV_L256_MIN_TILES", "1")
+    g = torch.Generator(device="cuda").manual_seed(B * 1000 + H + C)
+    x = rnd((B, H, W, C), 1.0, g)
+    if mode == "fwd":
+        w = rnd((3, 3, C, N), (9 * C) ** -0.5, g).to(F64)
+        wf, _ = packs(w)
+        bias = torch.randn(N, generator=g, device="cuda")
+        d = nn.make_desc(nn.FWD, B, C, 3, 3, 1, 1, 1, N, N, N, [nn.seg(H, W, H, W, wf, bias)], relu_out=True)
+        ref = torch.relu(conv_ref(x.to(F64), w) + bias.to(F64))
+        shape_out = (B, H, W, N)
+    else:
+        w = rnd((3, 3, N, C), (9 * C) ** -0.5, g).to(F64)      # forward conv N -> C; dgrad C -> N
+        _, wd = packs(w)
+        d = nn.make_desc(nn.DGRAD, B, C, 3, 3, 1, 1, 1, N, N, N, [nn.seg(H, W, H, W, wd, None)])
+        ref = dgrad_ref(x.to(F64), w)
+        shape_out = (B, H, W, N)
+    outs = {}
+    for halo in (True, False):
+        monkeypatch.setenv("CVL_CONV_HALO", "1" if halo else "0")
+        out = torch.empty(shape_out, dtype=BF, device="cuda")
+        stats = torch.zeros((B, N, 2), dtype=F64, device="cuda") if mode == "fwd" else None
+        nn.conv_igemm(d, x, out, stats)
+        code, name = last_kernel()
+        assert code == (12 if halo else 7), name
+        outs[halo] = (out, stats)
+    out, stats = outs[True]
+    torch.testing.assert_close(out.to(F64), ref, rtol=1e-2, atol=2e-2)
+    assert torch.equal(out.view(torch.int16), outs[False][0].view(torch.int16)), "X32H != X32 bits"
+    if stats is not None:
+        o = out.to(F64)
+        torch.testing.assert_close(stats, torch.stack([o.sum((1, 2)), (o * o).sum((1, 2))], -1), rtol=1e-5, atol=1e-3)

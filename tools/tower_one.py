@@ -23,10 +23,20 @@ def main():
     d = net.cls_tower[1].fwd_desc(B, net._pair_segs(1, B, shapes, off, P, fwd=True), ld_dst=256) if mode == "fwd" \
         else net.cls_tower[1].dgrad_desc(B, net._pair_segs(1, B, shapes, off, P, fwd=False), ld_dst=256)
     dst = torch.empty_like(src)
+    nn.conv_igemm(d, src, dst)
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
     for _ in range(iters):
         nn.conv_igemm(d, src, dst)
-    torch.cuda.synchronize()
-    print("done", iters, mode)
+    e1.record()
+    e1.synchronize()
+    us = e0.elapsed_time(e1) / iters * 1e3
+    from cvlite import _lib
+    L = _lib.load()
+    M = 2 * B * P
+    print("done", iters, mode, L.cvl_conv_kernel_name(L.cvl_conv_igemm_last_kernel()).decode(),
+          "%.1f us  %.0f TFLOP/s" % (us, 2.0 * M * 256 * 2304 / us / 1e6))
 
 
 if __name__ == "__main__":
