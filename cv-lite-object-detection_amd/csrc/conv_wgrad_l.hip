@@ -304,9 +304,12 @@ inline double wl_time(int tiles, int m_total, int bco, int* best_s) {
   return best_t;
 }
 
+// Npad 128 (one 128-wide co tile) runs faster on the register-staged 128 x 128 kernel
+// (tools/wgrad_sweep.py at bs 16: 3x3 128->128 @ 64x64 85 -> 72 us, 1x1 512->128 65 -> 46 us)
 inline bool wl_eligible(const cvl_conv_desc* d, const ConvArgs& a) {
   return !cvl_env_flag("CVL_WGRAD_NO_L") && !d->relu_in && a.K >= BKK && d->Cin % 8 == 0 &&
-         d->n_store % 4 == 0 && a.m_total >= 1024 && a.Npad % 128 == 0;
+         d->n_store % 4 == 0 && a.m_total >= 1024 && a.Npad % 128 == 0 &&
+         a.Npad >= cvl_env_int("CVL_WGL_MIN_NPAD", 256);
 }
 
 struct WlPlan {

@@ -265,11 +265,13 @@ struct WxPlan {
 
 // Modelled time of s splits: rounds of 256 workgroups (one per CU) x 32-row steps per chunk
 // (CVL_WGX_STEP, 0.01 us; ~0.8 us measured on the tower shape) + the fp32 slab round trip.
+// K below one 256-deep tile (1x1 convs with Cin 128) leaves half of every tile idle: those go to
+// the 128-wide kernels (tools/wgrad_sweep.py: 1x1 128->512 @ 64x64, 59 -> 47 us).
 inline bool wx_plan(const cvl_conv_desc* d, int ngroups, ConvArgs* a, WxPlan* p) {
   if (cvl_env_flag("CVL_WGRAD_NO_X")) return false;
   if (cvl_conv_prepare(d, SEGM, a)) return false;
   if (ngroups < 1 || ngroups > kMaxGroups || d->nseg % ngroups || d->relu_in || a->Npad % BCO ||
-      d->Cin % 8 || d->n_store % 4 || a->K < BKK / 2 || a->m_total < 1024)
+      d->Cin % 8 || d->n_store % 4 || a->K < cvl_env_int("CVL_WGX_MIN_K", BKK) || a->m_total < 1024)
     return false;
   // every dY / source byte offset must stay below the buffer-resource bound (32-bit cursors)
   for (int i = 0; i < a->nseg; ++i) {

@@ -582,13 +582,28 @@ __global__ void __launch_bounds__(NT) retina_loss_kernel(RetinaLossArgs a) {
   }
 }
 
-__global__ void det_loss_finalize(const double* partial, float* losses, int tiles) {
-  const int b = blockIdx.x, k = threadIdx.x;
-  if (k < 2) {
-    double s = 0.0;
-    for (int i = 0; i < tiles; ++i) s += partial[((size_t)b * tiles + i) * 2 + k];
-    losses[b * 2 + k] = (float)s;
+// losses[b][k] = sum_i partial[b][i][k]: one 256-thread block per image; thread t sums tiles
+// t, t + 256, ... (both terms), then a fixed-shape LDS tree (deterministic, no atomics)
+constexpr int FIN_T = 256;
+__global__ void __launch_bounds__(FIN_T) det_loss_finalize(const double* partial, float* losses, int tiles) {
+  const int b = blockIdx.x, t = threadIdx.x;
+  double s0 = 0.0, s1 = 0.0;
+  for (int i = t; i < tiles; i += FIN_T) {
+    s0 += partial[((size_t)b * tiles + i) * 2];
+    s1 += partial[((size_t)b * tiles + i) * 2 + 1];
   }
+  __shared__ double red[2][FIN_T];
+  red[0][t] = s0;
+  red[1][t] = s1;
+  __syncthreads();
+  for (int w = FIN_T / 2; w > 0; w >>= 1) {
+    if (t < w) {
+      red[0][t] += red[0][t + w];
+      red[1][t] += red[1][t + w];
+    }
+    __syncthreads();
+  }
+  if (t < 2) losses[b * 2 + t] = (float)red[t][0];
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -653,6 +668,100 @@ __global__ void nms_kernel(const double* boxes /*[n][6] x1 y1 x2 y2 score cls*/,
   if (threadIdx.x == 0) nkeep[ci] = count;
 }
 
+// Soft-NMS (tf_centernet_hourglass.py:44-85, method 'soft-nms', float64): per class, repeatedly
+// emit the first maximum of the current (decayed) scores among the survivors with that score,
+// then multiply every other survivor's score by exp(-(1.0 * iou^2 / sigma)) (bboxes_iou with the
+// fp32-eps floor) and drop those whose score is no longer > 0.  One workgroup per class; the
+// running scores live in the workspace.
+__global__ void soft_nms_kernel(const double* boxes, int n, const double* classes, int ncls, double sigma,
+                                int32_t* keep, double* keep_score, int32_t* nkeep, double* score_ws,
+                                uint8_t* alive_ws) {
+  const int ci = blockIdx.x;
+  if (ci >= ncls) return;
+  const double cval = classes[ci];
+  uint8_t* alive = alive_ws + (size_t)ci * n;
+  double* sc = score_ws + (size_t)ci * n;
+  for (int i = threadIdx.x; i < n; i += blockDim.x) {
+    sc[i] = boxes[i * 6 + 4];
+    alive[i] = boxes[i * 6 + 5] == cval ? 1 : 0;
+  }
+  __shared__ double best_s[NT];
+  __shared__ int best_i[NT];
+  __shared__ int sel;
+  int count = 0;
+  __syncthreads();
+  for (;;) {
+    double bsc = -INFINITY;
+    int bi = 0x7fffffff;
+    for (int i = threadIdx.x; i < n; i += blockDim.x) {
+      if (!alive[i]) continue;
+      if (sc[i] > bsc || (sc[i] == bsc && i < bi)) { bsc = sc[i]; bi = i; }
+    }
+    best_s[threadIdx.x] = bsc;
+    best_i[threadIdx.x] = bi;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      double s0 = -INFINITY;
+      int i0 = 0x7fffffff;
+      for (int k = 0; k < (int)blockDim.x; ++k)
+        if (best_s[k] > s0 || (best_s[k] == s0 && best_i[k] < i0)) { s0 = best_s[k]; i0 = best_i[k]; }
+      sel = (i0 == 0x7fffffff) ? -1 : i0;
+      if (sel >= 0) {
+        keep[(size_t)ci * n + count] = sel;
+        keep_score[(size_t)ci * n + count] = sc[sel];
+        alive[sel] = 0;
+      }
+    }
+    __syncthreads();
+    const int s = sel;
+    if (s < 0) break;
+    ++count;
+    const double* q = boxes + s * 6;
+    const double qa = (q[2] - q[0]) * (q[3] - q[1]);
+    for (int i = threadIdx.x; i < n; i += blockDim.x) {
+      if (!alive[i]) continue;
+      const double* r = boxes + i * 6;
+      const double ra = (r[2] - r[0]) * (r[3] - r[1]);
+      const double l0 = q[0] > r[0] ? q[0] : r[0], l1 = q[1] > r[1] ? q[1] : r[1];
+      const double h0 = q[2] < r[2] ? q[2] : r[2], h1 = q[3] < r[3] ? q[3] : r[3];
+      const double w0 = h0 - l0 > 0.0 ? h0 - l0 : 0.0, w1 = h1 - l1 > 0.0 ? h1 - l1 : 0.0;
+      const double inter = w0 * w1;
+      double iou = 1.0 * inter / (qa + ra - inter);
+      const double eps = 1.1920928955078125e-07;        // np.finfo(np.float32).eps
+      iou = iou > eps ? iou : eps;
+      const double wgt = exp(-(1.0 * (iou * iou) / sigma));
+      sc[i] = sc[i] * wgt;
+      if (!(sc[i] > 0.0)) alive[i] = 0;
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) nkeep[ci] = count;
+}
+
+// tf_centernet.py:6-19 center_dist_1d / _2d on a grid of n points (float64): g = 1 / (x - mu_x)^p
+// [* 1 / (y - mu_y)^p], divided by its maximum (tf.reduce_max).  One workgroup: pass 1 the values
+// and a block max (NaN-propagating like reduce_max over inf/nan is not modelled: the reference grids
+// never hit a pole), pass 2 the division.
+__global__ void center_dist_kernel(const double* gx, const double* gy, int n, double mu_x, double mu_y,
+                                   double spread, double* out) {
+  __shared__ double red[NT];
+  double m = -INFINITY;
+  for (int i = threadIdx.x; i < n; i += NT) {
+    double g = 1.0 / pow(gx[i] - mu_x, spread);
+    if (gy) g = g * (1.0 / pow(gy[i] - mu_y, spread));
+    out[i] = g;
+    m = g > m ? g : m;
+  }
+  red[threadIdx.x] = m;
+  __syncthreads();
+  for (int w = NT / 2; w > 0; w >>= 1) {
+    if (threadIdx.x < w) red[threadIdx.x] = red[threadIdx.x + w] > red[threadIdx.x] ? red[threadIdx.x + w] : red[threadIdx.x];
+    __syncthreads();
+  }
+  const double z = red[0];
+  for (int i = threadIdx.x; i < n; i += NT) out[i] = out[i] / z;
+}
+
 }  // namespace
 
 #define S_ ((hipStream_t)stream)
@@ -703,6 +812,13 @@ extern "C" int cvl_centernet_assign(const float* boxes, const int32_t* nbox, con
   return cvl_launch_status();
 }
 
+extern "C" int cvl_center_dist(const double* grid_x, const double* grid_y, int n, double mu_x, double mu_y,
+                               double spread, double* out, cvl_stream_t stream) {
+  CVL_CHECK_ARG(grid_x && out && n > 0);
+  hipLaunchKernelGGL(center_dist_kernel, dim3(1), dim3(NT), 0, S_, grid_x, grid_y, n, mu_x, mu_y, spread, out);
+  return cvl_launch_status();
+}
+
 extern "C" int cvl_centernet_splat(const float* boxes, const int32_t* nbox, const float* img_dim, int B,
                                    int n_max, int pad_h, int pad_w, int num_classes, int stride, float sigma,
                                    float* targets, cvl_stream_t stream) {
@@ -734,7 +850,7 @@ extern "C" int cvl_det_loss(const float* reg_pred, int ld_reg, const float* cls_
   a.tiles = (P + NT - 1) / NT;
   a.grad_scale_cls = grad_scale_cls; a.grad_scale_reg = grad_scale_reg;
   hipLaunchKernelGGL(det_loss_kernel, dim3(a.tiles, B), dim3(NT), 0, S_, a);
-  hipLaunchKernelGGL(det_loss_finalize, dim3(B), dim3(64), 0, S_, (const double*)workspace, losses, a.tiles);
+  hipLaunchKernelGGL(det_loss_finalize, dim3(B), dim3(FIN_T), 0, S_, (const double*)workspace, losses, a.tiles);
   return cvl_launch_status();
 }
 
@@ -768,7 +884,7 @@ extern "C" int cvl_retina_loss(const float* reg_pred, int ld_reg, const float* c
   CVL_CHECK_ARG(4 + num_classes <= RL_MAXW);
   a.tiles = (int)(((long)a.P * a.A + RL_ROWS - 1) / RL_ROWS);
   hipLaunchKernelGGL(retina_loss_kernel, dim3(a.tiles, B), dim3(NT), 0, S_, a);
-  hipLaunchKernelGGL(det_loss_finalize, dim3(B), dim3(64), 0, S_, (const double*)workspace, losses, a.tiles);
+  hipLaunchKernelGGL(det_loss_finalize, dim3(B), dim3(FIN_T), 0, S_, (const double*)workspace, losses, a.tiles);
   return cvl_launch_status();
 }
 
@@ -782,6 +898,21 @@ extern "C" int cvl_nms(const double* boxes, int n, const double* classes, int nc
   return cvl_launch_status();
 }
 
+extern "C" size_t cvl_soft_nms_workspace_size(int n, int ncls) {
+  return (size_t)n * ncls * (sizeof(double) + 1) + 16;
+}
+
+extern "C" int cvl_soft_nms(const double* boxes, int n, const double* classes, int ncls, double sigma,
+                            int32_t* keep, double* keep_score, int32_t* nkeep, void* workspace,
+                            cvl_stream_t stream) {
+  CVL_CHECK_ARG(boxes && classes && keep && keep_score && nkeep && workspace && n > 0 && ncls > 0 && sigma > 0.0);
+  double* scw = reinterpret_cast<double*>(workspace);
+  uint8_t* alive = reinterpret_cast<uint8_t*>(scw + (size_t)n * ncls);
+  hipLaunchKernelGGL(soft_nms_kernel, dim3(ncls), dim3(NT), 0, S_, boxes, n, classes, ncls, sigma, keep, keep_score,
+                     nkeep, scw, alive);
+  return cvl_launch_status();
+}
+
 extern "C" int cvl_centernet_loss(const float* pred, int ld_pred, const float* targets, int B, int P, int num_classes,
                                   float cls_scale, float reg_scale, float* losses, void* d_pred, int ld_d,
                                   void* workspace, cvl_stream_t stream) {
@@ -792,7 +923,7 @@ extern "C" int cvl_centernet_loss(const float* pred, int ld_pred, const float* t
   a.ld_pred = ld_pred; a.ld_d = ld_d; a.P = P; a.C = num_classes; a.tiles = (P + NT - 1) / NT;
   a.cls_scale = cls_scale; a.reg_scale = reg_scale;
   hipLaunchKernelGGL(centernet_loss_kernel, dim3(a.tiles, B), dim3(NT), 0, S_, a);
-  hipLaunchKernelGGL(det_loss_finalize, dim3(B), dim3(64), 0, S_, (const double*)workspace, losses, a.tiles);
+  hipLaunchKernelGGL(det_loss_finalize, dim3(B), dim3(FIN_T), 0, S_, (const double*)workspace, losses, a.tiles);
   return cvl_launch_status();
 }
 

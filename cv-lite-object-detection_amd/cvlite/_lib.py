@@ -60,6 +60,7 @@ SIGNATURES = {
     "cvl_gather_rows": (c_int, [P, ctypes.c_int64, P, c_int, P, P]),
     "cvl_retina_assign": (c_int, [P, P, P, c_int, c_int, c_int, c_int, P, c_int, P, c_float, P, P, P]),
     "cvl_centernet_assign": (c_int, [P, P, P, c_int, c_int, c_int, c_int, c_int, c_int, P, P]),
+    "cvl_center_dist": (c_int, [P, P, c_int, ctypes.c_double, ctypes.c_double, ctypes.c_double, P, P]),
     "cvl_centernet_splat": (c_int, [P, P, P, c_int, c_int, c_int, c_int, c_int, c_int, c_float, P, P]),
     "cvl_det_loss_workspace_size": (c_size_t, [c_int, c_int]),
     "cvl_det_loss": (c_int, [P, c_int, P, c_int, P, c_int, c_int, c_int, c_float, c_float, P, P, P, P, P]),
@@ -86,6 +87,8 @@ SIGNATURES = {
                                      ctypes.c_double, ctypes.c_double, ctypes.c_double, P, P, P]),
     "cvl_nms_workspace_size": (c_size_t, [c_int, c_int]),
     "cvl_nms": (c_int, [P, c_int, P, c_int, ctypes.c_double, P, P, P, P]),
+    "cvl_soft_nms_workspace_size": (c_size_t, [c_int, c_int]),
+    "cvl_soft_nms": (c_int, [P, c_int, P, c_int, ctypes.c_double, P, P, P, P, P]),
     "cvl_retina_corners": (c_int, [P, c_int, c_int, c_int, c_float, c_float, c_int, P, P]),
     "cvl_retina_decode_workspace_size": (c_size_t, [c_int, P, c_int]),
     "cvl_retina_decode": (c_int, [P, c_int, P, c_int, c_int, P, P, P, c_int, c_int, c_float, P, P, P, c_size_t,

@@ -40,17 +40,20 @@ def model_loss(y_true, y_pred):
 
 
 def nms(bboxes, iou_threshold, sigma=0.3, method="nms"):
-    """tf_centernet_hourglass.py:44-85 with method 'nms': rows (xmin, ymin, w, h, score, cls) ->
-    list of kept rows (x1, y1, x2, y2, score, cls), classes in python-set order."""
+    """tf_centernet_hourglass.py:44-85: rows (xmin, ymin, w, h, score, cls) -> list of emitted rows
+    (x1, y1, x2, y2, score, cls), classes in python-set order.  method 'nms' (cvl_nms: greedy, IoU >
+    iou_threshold suppressed) or 'soft-nms' (cvl_soft_nms: Gaussian decay exp(-iou^2 / sigma); the
+    emitted rows carry their decayed scores)."""
     assert method in ["nms", "soft-nms"]
-    if method != "nms":
-        raise NotImplementedError("soft-nms is outside the measured path")
     b = np.array(bboxes, dtype=np.float64)
     classes = list(set(b[:, 5]))
     b[:, 2] = b[:, 0] + b[:, 2]
     b[:, 3] = b[:, 1] + b[:, 3]
     _lib.require_cuda()
-    kept = ot.nms(torch.tensor(b, device="cuda"), classes, iou_threshold)
+    if method == "soft-nms":
+        kept = ot.soft_nms(torch.tensor(b, device="cuda"), classes, sigma)
+    else:
+        kept = ot.nms(torch.tensor(b, device="cuda"), classes, iou_threshold)
     return [row for row in kept.cpu().numpy()]
 
 

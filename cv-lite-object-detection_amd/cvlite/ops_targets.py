@@ -181,6 +181,27 @@ def nms(boxes_xyxy, classes, iou_threshold):
     return boxes_xyxy[idx.long()]
 
 
+def soft_nms(boxes_xyxy, classes, sigma=0.3):
+    """Soft-NMS (cvl_soft_nms): boxes [n, 6] float64 (x1, y1, x2, y2, score, cls) device, classes in
+    processing order.  Returns the emitted rows (reference order) with their decayed scores."""
+    _lib.require_cuda(boxes_xyxy)
+    n = int(boxes_xyxy.shape[0])
+    dev = boxes_xyxy.device
+    cls = torch.tensor(list(classes), dtype=torch.float64, device=dev)
+    ncls = int(cls.numel())
+    keep = torch.empty((ncls, n), dtype=torch.int32, device=dev)
+    ksc = torch.empty((ncls, n), dtype=torch.float64, device=dev)
+    nkeep = torch.empty((ncls,), dtype=torch.int32, device=dev)
+    ws = torch.empty(int(_lib.load().cvl_soft_nms_workspace_size(n, ncls)), dtype=torch.uint8, device=dev)
+    _lib.call("cvl_soft_nms", ptr(boxes_xyxy), n, ptr(cls), ncls, float(sigma), ptr(keep), ptr(ksc), ptr(nkeep),
+              ptr(ws), _lib.stream())
+    nk = nkeep.cpu().tolist()
+    idx = torch.cat([keep[c, :nk[c]] for c in range(ncls)]).long()
+    rows = boxes_xyxy[idx].clone()
+    rows[:, 4] = torch.cat([ksc[c, :nk[c]] for c in range(ncls)])
+    return rows
+
+
 def centernet_loss(pred, targets, num_classes, cls_scale=2.5, reg_scale=1.0, d_pred=None, losses=None):
     """CenterNet model_loss fwd+bwd (tf_centernet_hourglass.py:492-505 in train_step :537-549) off
     the output conv.  pred [B,P,ld] f32 (reg 0..3, cls 4..), targets [B,P,4+C] f32.

@@ -293,6 +293,10 @@ int cvl_centernet_assign(const float* boxes, const int32_t* nbox, const float* i
 int cvl_centernet_splat(const float* boxes, const int32_t* nbox, const float* img_dim, int B, int n_max,
                         int pad_h, int pad_w, int num_classes, int stride, float sigma, float* targets,
                         cvl_stream_t stream);
+/* CenterNet/tf_centernet.py:6-19 center_dist_1d (grid_y NULL) / center_dist_2d: out[i] =
+ * g[i] / max(g), g = 1 / (grid_x - mu_x)^spread [* 1 / (grid_y - mu_y)^spread], float64, n points. */
+int cvl_center_dist(const double* grid_x, const double* grid_y, int n, double mu_x, double mu_y, double spread,
+                    double* out, cvl_stream_t stream);
 
 /* Focal (alpha .25, gamma 2) on C class logits + smooth-L1 on 4 box channels masked by
  * max(class target) > 0: CenterNet model_loss (tf_centernet_hourglass.py:492-505) and one
@@ -322,6 +326,13 @@ int cvl_retina_loss(const float* reg_pred, int ld_reg, const float* cls_pred, in
 size_t cvl_nms_workspace_size(int n, int ncls);
 int cvl_nms(const double* boxes, int n, const double* classes, int ncls, double iou_threshold,
             int32_t* keep, int32_t* nkeep, void* workspace, cvl_stream_t stream);
+/* Soft-NMS (tf_centernet_hourglass.py:44-85, method 'soft-nms'; Bodla et al. 2017, Gaussian
+ * decay): per class, emit the first maximum of the running scores, then scale every survivor's
+ * score by exp(-(iou^2 / sigma)) (float64) and drop scores that are no longer > 0.  Same layout as
+ * cvl_nms plus keep_score [ncls][n] = the emitted (decayed) score of each kept row. */
+size_t cvl_soft_nms_workspace_size(int n, int ncls);
+int cvl_soft_nms(const double* boxes, int n, const double* classes, int ncls, double sigma, int32_t* keep,
+                 double* keep_score, int32_t* nkeep, void* workspace, cvl_stream_t stream);
 
 /* ==========================================================================================
  * CenterNet hourglass training path (CenterNet/tf_centernet_hourglass.py:87-353 build_model,

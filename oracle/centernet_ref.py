@@ -175,6 +175,26 @@ def nms(bboxes, iou_threshold):
     return np.array(best, np.float64).reshape(-1, 6)
 
 
+def soft_nms(bboxes, sigma=0.3):
+    """tf_centernet_hourglass.py:44-85, method='soft-nms' (Gaussian decay, float64).  Input rows
+    (x, y, w, h, score, cls); output rows (x1, y1, x2, y2, decayed score, cls) in emission order."""
+    bb = np.array(bboxes, np.float64)
+    bb[:, 2] = bb[:, 0] + bb[:, 2]
+    bb[:, 3] = bb[:, 1] + bb[:, 3]
+    best = []
+    for c in list(set(bb[:, 5])):
+        cb = bb[bb[:, 5] == c]
+        while len(cb) > 0:
+            i = int(np.argmax(cb[:, 4]))
+            b = cb[i]
+            best.append(b.copy())
+            cb = np.concatenate([cb[:i], cb[i + 1:]])
+            iou = bboxes_iou(b[np.newaxis, :4], cb[:, :4])
+            cb[:, 4] = cb[:, 4] * np.exp(-(1.0 * iou ** 2 / sigma))
+            cb = cb[cb[:, 4] > 0.0]
+    return np.array(best, np.float64).reshape(-1, 6)
+
+
 def prediction_to_corners(xy_pred, stride):
     """tf_centernet_hourglass.py:355-377: fp32 grid (cell + 0.5) -+ ltrb, stored float64, * stride."""
     xy = np.asarray(xy_pred, np.float32)

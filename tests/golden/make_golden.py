@@ -303,7 +303,31 @@ def work_fcos_center(out_path):
     np.savez_compressed(out_path, **arrays)
 
 
+def work_centernet_softnms(out_path):
+    """tf_centernet_hourglass.nms(method='soft-nms') (:44-85): the Gaussian-decay branch, on random
+    (x, y, w, h, score, cls) rows with distinct scores (ties would be broken by argmax order in
+    both; distinct keeps the first-maximum rule out of the float64 exp's last ulp)."""
+    tf = _child_setup("CenterNet")
+    import tf_centernet_hourglass as hg
+    rng = np.random.default_rng(777)
+    arrays = {}
+    for i in range(8):
+        n = [12, 40, 64, 5, 30, 48, 20, 33][i]
+        xy = rng.uniform(0, 200, size=(n, 2))
+        wh = rng.uniform(10, 120, size=(n, 2))
+        sc = (rng.permutation(n) + 1.0).reshape(n, 1) / n * 0.9
+        cl = rng.integers(0, 1 + i % 3, size=(n, 1)).astype(np.float64)
+        bb = np.concatenate([xy, wh, sc, cl], axis=1)
+        sigma = [0.3, 0.5, 0.1, 0.3, 1.0, 0.3, 0.05, 0.3][i]
+        arrays["soft_%d_in" % i] = bb.copy()
+        arrays["soft_%d_sigma" % i] = np.float64(sigma)
+        res = hg.nms(bb.copy(), 0.5, sigma=sigma, method="soft-nms")
+        arrays["soft_%d_out" % i] = np.array(res, dtype=np.float64).reshape(-1, 6)
+    np.savez_compressed(out_path, **arrays)
+
+
 WORKERS = {"fcos": work_fcos, "retinanet": work_retina, "centernet": work_centernet,
+           "centernet_softnms": work_centernet_softnms,
            "retina_decode": work_retina_decode,
            "fcos_center": work_fcos_center}
 
@@ -315,7 +339,10 @@ def main():
     if not os.path.isdir(REF):
         print("reference not present at %s: nothing to do" % REF)
         return
+    only = sys.argv[1:]                   # optional: regenerate only these families
     for fam in WORKERS:
+        if only and fam not in only:
+            continue
         out = os.path.join(HERE, "golden_%s.npz" % fam)
         subprocess.check_call([sys.executable, os.path.abspath(__file__), fam, out])
         print("wrote", out, os.path.getsize(out), "bytes")

@@ -116,6 +116,25 @@ def test_nms_matches_reference(golden):
         np.testing.assert_array_equal(got, d["nms_%d_out" % i])
 
 
+def test_soft_nms_and_center_dist_match_reference(golden):
+    """cvl_soft_nms vs tf_centernet_hourglass.nms(method='soft-nms') goldens: emission order, boxes
+    and classes exact; decayed scores within 4 ulp (the device float64 exp vs numpy's); and
+    cvl_center_dist vs tf_centernet.center_dist_1d/2d goldens (float64 pow: 1e-15 relative)."""
+    from cvlite import centernet_hourglass as hg
+    from cvlite import centernet_splat as cs
+    d = golden("centernet_softnms")
+    for i in range(8):
+        got = np.array(hg.nms(d["soft_%d_in" % i], 0.5, sigma=float(d["soft_%d_sigma" % i]), method="soft-nms"),
+                       np.float64).reshape(-1, 6)
+        exp = d["soft_%d_out" % i]
+        assert got.shape == exp.shape
+        np.testing.assert_array_equal(got[:, [0, 1, 2, 3, 5]], exp[:, [0, 1, 2, 3, 5]])
+        np.testing.assert_allclose(got[:, 4], exp[:, 4], rtol=1e-15, atol=0)
+    c = golden("centernet")
+    np.testing.assert_allclose(cs.center_dist_2d(c["cd2_gx"], c["cd2_gy"], 5, 12, 8.0), c["cd2_out"], rtol=1e-15)
+    np.testing.assert_allclose(cs.center_dist_1d(np.arange(3, 9) + 0.5, 6, 8.0), c["cd1_out"], rtol=1e-15)
+
+
 def test_centernet_decode_matches_restatement():
     """cvl_centernet_decode + cvl_nms vs the numpy restatement of obj_detect_results' decode
     (oracle/centernet_ref.py) on random heads: bit-exact rows, including boxes clamped at the image

@@ -161,3 +161,12 @@ def test_fcos_center_format_data_bit_exact(golden):
             np.testing.assert_array_equal(outs[l].astype(np.float32), d["case_%d_L%d" % (i, l)])
             overlaps += int((d["case_%d_L%d" % (i, l)][..., 5:].sum(-1) > 1).sum())
     assert overlaps > 0
+
+
+def test_centernet_soft_nms_oracle(golden):
+    """tf_centernet_hourglass.nms(method='soft-nms') goldens (make_golden.py centernet_softnms):
+    emission order and boxes exact, decayed scores bit-exact (same float64 numpy sequence)."""
+    d = golden("centernet_softnms")
+    for i in range(8):
+        got = centernet_ref.soft_nms(d["soft_%d_in" % i], float(d["soft_%d_sigma" % i]))
+        np.testing.assert_array_equal(got, d["soft_%d_out" % i])
