@@ -4,6 +4,13 @@
 //   cen = sum smoothL1(targets[4], sigmoid(reg[4]))     over ALL cells (fcos.py:483-486, Q10)
 //   reg = sum mask * smoothL1(targets[:4], reg[:4])     (l1)  or  -log IoU (iou, fcos.py:393-441)
 //   mask = max(targets[5:]) >= 1                        (fcos.py:475-477)
+// Variant flags (bits of reg_type above the reg kind in bits 0-1):
+//   4  FOCAL_CEN  centerness as focal(targets[4], logit) (fcos_center.py:386-389, cen_type="focal";
+//                 fcos_center_v1.py:305-307)
+//   8  SIG_REG    smooth-L1 on sigmoid(reg[:4]) (fcos_center_v1.py:115 applies the sigmoid in the model)
+//   16 CEN_IN_CLS the centerness logit (and its gradient) is column cc = round_up(C, 8) of the class
+//                 rows (the centre variants' cen_output_l head sits on the cls tower,
+//                 fcos_center.py:85-101; the 8-aligned column lets its weight gradient read it)
 // "smooth L1" is the reference's discontinuous 0.5 d^2 (|d|<1) / |d| (Q8).  One pass reads the
 // predictions and targets once and writes the gradients once (HBM-bound); per-image sums are
 // reduced deterministically (per-tile partials in float64, then a fixed-order second pass).
@@ -39,54 +46,76 @@ __device__ __forceinline__ float sl1(float d, float* g) {
   return ad;
 }
 
+// focal loss term (alpha .25, gamma 2, the reference's stable form) and d/dx
+__device__ __forceinline__ float focal_term(float y, float x, float* g) {
+  const float alpha = 0.25f;
+  const float e = expf(-fabsf(x));
+  const float L = log1pf(e);                       // log(1 + exp(-|x|))
+  const float p1 = x >= 0.f ? 1.0f / (1.0f + e) : e / (1.0f + e);   // sigmoid(x)
+  const float q1 = x >= 0.f ? e / (1.0f + e) : 1.0f / (1.0f + e);   // 1 - sigmoid(x)
+  const float nlp = L - fminf(x, 0.f);             // -log p
+  const float nlq = L + fmaxf(x, 0.f);             // -log(1-p)
+  const float wpos = y * alpha * q1 * q1;
+  const float wneg = (1.0f - y) * (1.0f - alpha) * p1 * p1;
+  *g = -y * alpha * q1 * q1 * (2.0f * p1 * nlp + q1) + (1.0f - y) * (1.0f - alpha) * p1 * p1 * (2.0f * q1 * nlq + p1);
+  return wpos * nlp + wneg * nlq;
+}
+
 __global__ void __launch_bounds__(kThreads) fcos_loss_kernel(LossArgs a) {
   const int b = blockIdx.y;
   const int p = blockIdx.x * kThreads + threadIdx.x;
   float s_cls = 0.f, s_reg = 0.f, s_cen = 0.f;
+  const int kind = a.reg_type & 3;
+  const bool focal_cen = a.reg_type & 4, sig_reg = a.reg_type & 8, cen_in_cls = a.reg_type & 16;
+  const int cc = (a.C + 7) / 8 * 8;                // centerness column of the class rows (CEN_IN_CLS)
   if (p < a.P) {
     const size_t cell = (size_t)b * a.P + p;
     const float* t = a.tgt + cell * (5 + a.C);
     const float* xr = a.reg + cell * a.ld_reg;
     const float* xc = a.cls + cell * a.ld_cls;
-    const float alpha = 0.25f;
     float tmax = 0.f;
     for (int c = 0; c < a.C; ++c) {
       const float y = t[5 + c];
       tmax = fmaxf(tmax, y);
-      const float x = xc[c];
-      const float e = expf(-fabsf(x));
-      const float L = log1pf(e);                       // log(1 + exp(-|x|))
-      const float p1 = x >= 0.f ? 1.0f / (1.0f + e) : e / (1.0f + e);   // sigmoid(x)
-      const float q1 = x >= 0.f ? e / (1.0f + e) : 1.0f / (1.0f + e);   // 1 - sigmoid(x)
-      const float nlp = L - fminf(x, 0.f);             // -log p
-      const float nlq = L + fmaxf(x, 0.f);             // -log(1-p)
-      const float wpos = y * alpha * q1 * q1;
-      const float wneg = (1.0f - y) * (1.0f - alpha) * p1 * p1;
-      s_cls += wpos * nlp + wneg * nlq;
-      if (a.dcls) {
-        const float g = -y * alpha * q1 * q1 * (2.0f * p1 * nlp + q1) +
-                        (1.0f - y) * (1.0f - alpha) * p1 * p1 * (2.0f * q1 * nlq + p1);
-        store_g(a.dcls, cell * a.ld_dcls + c, g * a.grad_scale, a.dcls_bf16);
-      }
+      float g;
+      s_cls += focal_term(y, xc[c], &g);
+      if (a.dcls) store_g(a.dcls, cell * a.ld_dcls + c, g * a.grad_scale, a.dcls_bf16);
     }
     if (a.dcls)
       for (int c = a.C; c < a.ld_dcls; ++c) store_g(a.dcls, cell * a.ld_dcls + c, 0.f, a.dcls_bf16);
     const float mask = tmax >= 1.0f ? 1.0f : 0.0f;
     float g[5] = {0.f, 0.f, 0.f, 0.f, 0.f};
-    // centerness: smooth-L1 on sigmoid(logit), all cells
+    // centerness: smooth-L1 on sigmoid(logit) (fcos.py:483-486) or focal (centre variants), all cells
     {
-      const float x = xr[4];
-      const float sg = 1.0f / (1.0f + expf(-x));
-      float gd;
-      s_cen += sl1(t[4] - sg, &gd);
-      g[4] = gd * sg * (1.0f - sg);
+      const float x = cen_in_cls ? xc[cc] : xr[4];
+      float gc;
+      if (focal_cen) {
+        s_cen += focal_term(t[4], x, &gc);
+      } else {
+        const float sg = 1.0f / (1.0f + expf(-x));
+        float gd;
+        s_cen += sl1(t[4] - sg, &gd);
+        gc = gd * sg * (1.0f - sg);
+      }
+      if (cen_in_cls) {
+        if (a.dcls) store_g(a.dcls, cell * a.ld_dcls + cc, gc * a.grad_scale, a.dcls_bf16);
+      } else {
+        g[4] = gc;
+      }
     }
-    if (a.reg_type == 0) {
+    if (kind == 0) {
       for (int j = 0; j < 4; ++j) {
         float gd;
-        const float l = sl1(t[j] - xr[j], &gd);
-        s_reg += mask * l;
-        g[j] = mask * gd;
+        if (sig_reg) {                             // fcos_center_v1.py:115: reg = sigmoid(conv)
+          const float sg = 1.0f / (1.0f + expf(-xr[j]));
+          const float l = sl1(t[j] - sg, &gd);
+          s_reg += mask * l;
+          g[j] = mask * gd * sg * (1.0f - sg);
+        } else {
+          const float l = sl1(t[j] - xr[j], &gd);
+          s_reg += mask * l;
+          g[j] = mask * gd;
+        }
       }
     } else if (mask != 0.f) {
       // IoU of ltrb boxes about the same grid point (grid offsets cancel)
@@ -151,10 +180,13 @@ extern "C" int cvl_fcos_loss(const float* reg_pred, int ld_reg, const float* cls
                              int dreg_dtype, void* d_cls, int ld_dcls, int dcls_dtype,
                              void* workspace, cvl_stream_t stream) {
   CVL_CHECK_ARG(reg_pred && cls_pred && targets && losses && workspace);
-  CVL_CHECK_ARG(B > 0 && P > 0 && num_classes > 0 && ld_reg >= 5 && ld_cls >= num_classes);
-  CVL_CHECK_ARG(reg_type == 0 || reg_type == 1);
+  CVL_CHECK_ARG(B > 0 && P > 0 && num_classes > 0);
+  const int kind = reg_type & 3, cen_in_cls = (reg_type & 16) ? 1 : 0;
+  CVL_CHECK_ARG((kind == 0 || kind == 1) && (reg_type & ~31) == 0 && !(kind == 1 && (reg_type & 8)));
+  const int ncls_cols = cen_in_cls ? (num_classes + 7) / 8 * 8 + 1 : num_classes;
+  CVL_CHECK_ARG(ld_reg >= (cen_in_cls ? 4 : 5) && ld_cls >= ncls_cols);
   CVL_CHECK_ARG(!d_reg || ld_dreg >= 5);
-  CVL_CHECK_ARG(!d_cls || ld_dcls >= num_classes);
+  CVL_CHECK_ARG(!d_cls || ld_dcls >= ncls_cols);
   CVL_CHECK_ARG((dreg_dtype == 0 || dreg_dtype == 1) && (dcls_dtype == 0 || dcls_dtype == 1));
   LossArgs a;
   a.reg = reg_pred; a.cls = cls_pred; a.tgt = targets; a.losses = losses;
@@ -186,6 +218,22 @@ __global__ void fcos_decode_kernel(const float* p, int ld, int S0, int S1, doubl
   out[i * 4 + 2] = stride * (double)(gy + q[1]);
   out[i * 4 + 3] = stride * (double)(gx + q[3]);
 }
+
+// fcos_center_v1.py:124-147 prediction_to_corners(xy_pred, box_sc, stride): fp32 centre
+// (grid + offset) * stride (grid WITHOUT +0.5), size * box_sc, fp32 corners stored as float64
+__global__ void fcos_v1_decode_kernel(const float* p, int ld, int S0, int S1, float box_sc, float stride,
+                                      double* out) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= S0 * S1) return;
+  const int y = i / S1, x = i - (i / S1) * S1;
+  const float* q = p + (size_t)i * ld;
+  const float yc = ((float)y + q[0]) * stride, xc = ((float)x + q[1]) * stride;
+  const float bh = q[2] * box_sc, bw = q[3] * box_sc;
+  out[i * 4 + 0] = (double)(yc - bh / 2.0f);            // TF fp32 ops, stored into float64
+  out[i * 4 + 2] = (double)(yc + bh / 2.0f);
+  out[i * 4 + 1] = (double)(xc - bw / 2.0f);
+  out[i * 4 + 3] = (double)(xc + bw / 2.0f);
+}
 }  // namespace
 
 extern "C" int cvl_fcos_decode(const float* pred, int ld, int S0, int S1, double stride, double* out,
@@ -193,5 +241,13 @@ extern "C" int cvl_fcos_decode(const float* pred, int ld, int S0, int S1, double
   CVL_CHECK_ARG(pred && out && ld >= 4 && S0 > 0 && S1 > 0);
   hipLaunchKernelGGL(fcos_decode_kernel, dim3((S0 * S1 + 255) / 256), dim3(256), 0, (hipStream_t)stream, pred,
                      ld, S0, S1, stride, out);
+  return cvl_launch_status();
+}
+
+extern "C" int cvl_fcos_v1_decode(const float* pred, int ld, int S0, int S1, float box_sc, float stride, double* out,
+                                  cvl_stream_t stream) {
+  CVL_CHECK_ARG(pred && out && ld >= 4 && S0 > 0 && S1 > 0);
+  hipLaunchKernelGGL(fcos_v1_decode_kernel, dim3((S0 * S1 + 255) / 256), dim3(256), 0, (hipStream_t)stream, pred,
+                     ld, S0, S1, box_sc, stride, out);
   return cvl_launch_status();
 }

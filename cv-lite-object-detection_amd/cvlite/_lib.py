@@ -24,6 +24,7 @@ SIGNATURES = {
     "cvl_fcos_loss": (c_int, [P, c_int, P, c_int, P, c_int, c_int, c_int, c_int, c_float, P,
                               P, c_int, c_int, P, c_int, c_int, P, P]),
     "cvl_fcos_decode": (c_int, [P, c_int, c_int, c_int, ctypes.c_double, P, P]),
+    "cvl_fcos_v1_decode": (c_int, [P, c_int, c_int, c_int, c_float, c_float, P, P]),
     "cvl_conv_igemm_workspace_size": (c_size_t, [P]),
     "cvl_conv_igemm": (c_int, [P, P, P, P, P, c_size_t, P]),
     "cvl_conv_igemm_last_kernel": (c_int, []),
@@ -96,6 +97,7 @@ SIGNATURES = {
     "cvl_retina_nms_workspace_size": (c_size_t, [c_int, c_int]),
     "cvl_retina_nms": (c_int, [P, c_int, P, c_int, c_int, c_float, P, P, P, P]),
     "cvl_fcos_center_assign": (c_int, [P, P, P, c_int, c_int, c_int, c_int, c_int, P, P, c_int, P, P, P]),
+    "cvl_fcos_center_v1_assign": (c_int, [P, P, P, c_int, c_int, c_int, c_int, c_int, P, P, P, P, P]),
     "cvl_resize_pad_normalize": (c_int, [P, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, P, P]),
     "cvl_fcos_detect_workspace_size": (c_size_t, [c_int, c_int, c_int, c_int]),
     "cvl_fcos_detect": (c_int, [P, c_int, P, c_int, c_int, P, P, c_int, c_int, c_float, c_float, c_int, c_int, P, P,

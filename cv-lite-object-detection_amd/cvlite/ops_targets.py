@@ -53,15 +53,37 @@ def fcos_center_assign(boxes, nbox, img_dim, pad_hw, num_classes, strides=FCOS_S
     return out, num_targets
 
 
+def fcos_center_v1_assign(boxes, nbox, img_dim, pad_hw, num_classes, strides=FCOS_STRIDES, b_dim=FCOS_BOUNDS,
+                          out=None, num_targets=None):
+    """fcos_center_v1.format_data batched (cvl_fcos_center_v1_assign): centroid cells only,
+    (y_off, x_off, h / box_sc, w / box_sc, 1, class bits).  Same layout as fcos_center_assign."""
+    B, nmax = _boxes_args(boxes, nbox, img_dim)
+    P = sum(h * w for h, w in fcos_level_shapes(pad_hw[0], pad_hw[1], strides))
+    if out is None:
+        out = torch.empty((B, P, 5 + num_classes), device=boxes.device, dtype=torch.float32)
+    if num_targets is None:
+        num_targets = torch.empty((B, 5), device=boxes.device, dtype=torch.int32)
+    st = (_lib.ctypes.c_int32 * 5)(*[int(s) for s in strides])
+    bd = (_lib.ctypes.c_float * 4)(*[float(x) for x in b_dim])
+    _lib.call("cvl_fcos_center_v1_assign", ptr(boxes), ptr(nbox), ptr(img_dim), B, nmax, int(pad_hw[0]),
+              int(pad_hw[1]), int(num_classes), _lib.ctypes.cast(st, _lib.c_void_p),
+              _lib.ctypes.cast(bd, _lib.c_void_p), ptr(out), ptr(num_targets), _lib.stream())
+    return out, num_targets
+
+
 def fcos_loss(reg_pred, cls_pred, targets, num_classes, reg_type="l1", grad_scale=1.0,
-              with_grad=True, grad_dtype=torch.float32, d_reg=None, d_cls=None):
+              with_grad=True, grad_dtype=torch.float32, d_reg=None, d_cls=None, cen_type="l1",
+              reg_sigmoid=False, cen_in_cls=False):
     """Fused focal + smooth-L1/IoU + centerness forward and backward.
     reg_pred [B,P,ld_reg>=5] f32, cls_pred [B,P,ld_cls>=C] f32, targets [B,P,5+C] f32.
+    Centre variants (fcos_center / fcos_center_v1): cen_type "focal", reg_sigmoid (v1's sigmoid
+    reg head), cen_in_cls (centerness logit in class column round_up(C, 8)).
     Returns (losses [B,3] f32 = (cls, reg, cen) per image, d_reg, d_cls)."""
     _lib.require_cuda(reg_pred, cls_pred, targets)
     B, P = int(targets.shape[0]), int(targets.shape[1])
     assert reg_pred.shape[:2] == (B, P) and cls_pred.shape[:2] == (B, P)
-    rt = {"l1": 0, "iou": 1}[reg_type]
+    rt = reg_type if isinstance(reg_type, int) else {"l1": 0, "iou": 1}[reg_type]    # int: raw kernel flags
+    rt |= (4 if cen_type.lower() == "focal" else 0) | (8 if reg_sigmoid else 0) | (16 if cen_in_cls else 0)
     dev = targets.device
     losses = torch.empty((B, 3), device=dev, dtype=torch.float32)
     ws = torch.empty(int(_lib.load().cvl_fcos_loss_workspace_size(B, P)), device=dev, dtype=torch.uint8)

@@ -164,9 +164,10 @@ def _(boxes, nbox, img_dim, pad_h, pad_w, num_classes, stride, sigma):
 def fcos_loss(reg: torch.Tensor, cls: torch.Tensor, targets: torch.Tensor, num_classes: int,
               reg_type: int) -> torch.Tensor:
     """fcos.model_loss per image: reg [B,P,>=5] fp32, cls [B,P,>=C] fp32, targets [B,P,5+C]
-    -> [B,3] = (cls, reg, cen) (reg_type 0 = smooth-L1, 1 = IoU)."""
+    -> [B,3] = (cls, reg, cen) (reg_type: cvl_fcos_loss flags, 0 = smooth-L1, 1 = IoU, +4 focal
+    centerness, +8 sigmoid reg)."""
     losses, _, _ = ot.fcos_loss(reg.contiguous(), cls.contiguous(), targets.contiguous(), num_classes,
-                                reg_type=("l1", "iou")[reg_type], with_grad=False)
+                                reg_type=int(reg_type), with_grad=False)
     return losses
 
 
@@ -184,7 +185,7 @@ def _loss_setup(ctx, inputs, output):
 def _loss_backward(ctx, g):
     reg, cls, targets = ctx.saved_tensors
     _, d_reg, d_cls = ot.fcos_loss(reg.contiguous(), cls.contiguous(), targets.contiguous(), ctx.C,
-                                   reg_type=("l1", "iou")[ctx.reg_type], grad_scale=1.0)
+                                   reg_type=int(ctx.reg_type), grad_scale=1.0)
     g = g.to(torch.float32)
     # cls term -> class logits; reg term -> ltrb channels 0..3; centerness term -> channel 4;
     # padding channels get exactly zero

@@ -53,10 +53,16 @@ class FCOSTrainer(GraphStepper):
         self.momentum, self.clip = momentum, gradient_clip
         self.sched = (init_lr, min_lr, decay_rate, decay_step)
         self.reg_type = reg_type
-        # targets="center": fcos_center.format_data (train_fcos_center_voc.py:184-187, center_only)
-        if targets not in ("fcos", "center"):
-            raise ValueError("targets must be 'fcos' or 'center'")
+        # targets="center": fcos_center.format_data (train_fcos_center_voc.py:184-187, center_only);
+        # "center_v1": fcos_center_v1.format_data (train_fcos_center_v1_voc.py)
+        if targets not in ("fcos", "center", "center_v1"):
+            raise ValueError("targets must be 'fcos', 'center' or 'center_v1'")
         self.target_kind, self.center_only = targets, center_only
+        # the centre networks (cvlite.fcos_center_net): focal centerness from the cls-tower head in
+        # class column cen_col (train_fcos_center_voc.py:194-195), v1's sigmoid regression head
+        centre = hasattr(net, "cen_heads")
+        self.loss_flags = dict(cen_type="focal" if centre else "l1", cen_in_cls=centre,
+                               reg_sigmoid=bool(getattr(net, "v1", False)))
         dev = net.device
         B, H, W = self.B, self.H, self.W
         _, _, self.P = net.layout(B, H, W)
@@ -83,13 +89,16 @@ class FCOSTrainer(GraphStepper):
         if self.target_kind == "center":
             tg, _ = ot.fcos_center_assign(self.boxes, self.nbox, self.img_dim, (self.H, self.W), self.C,
                                           center_only=self.center_only, out=self.targets, num_targets=self.ntgt)
+        elif self.target_kind == "center_v1":
+            tg, _ = ot.fcos_center_v1_assign(self.boxes, self.nbox, self.img_dim, (self.H, self.W), self.C,
+                                             out=self.targets, num_targets=self.ntgt)
         else:
             tg, _ = ot.fcos_assign(self.boxes, self.nbox, self.img_dim, (self.H, self.W), self.C,
                                    out=self.targets, num_targets=self.ntgt)
         reg, cls = self.net.forward(self.images)
         self.outputs = (reg, cls)                 # head outputs of the last step (graph memory)
         losses, _, _ = ot.fcos_loss(reg, cls, tg, self.C, reg_type=self.reg_type, grad_scale=1.0,
-                                    d_reg=self.d_reg, d_cls=self.d_cls)
+                                    d_reg=self.d_reg, d_cls=self.d_cls, **self.loss_flags)
         self.losses.copy_(losses)
         self.net.backward(self.d_reg, self.d_cls, hook=hook)
 

@@ -55,7 +55,11 @@ int cvl_fcos_assign(const float* boxes, const int32_t* nbox, const float* img_di
  * losses[b*3 + {0,1,2}] = (cls, reg, cen) float32 sums for image b (model_loss's tuple).
  * If d_reg / d_cls are non-null, writes grad_scale * d(cls+reg+cen)/d(pred) with the same
  * strides (padding channels zeroed); *_dtype 0 = float32, 1 = bf16.
- * reg_type 0 = "l1" (smooth-L1), 1 = "iou".  `workspace` >= cvl_fcos_loss_workspace_size(B, P).
+ * reg_type bits 0-1: 0 = "l1" (smooth-L1), 1 = "iou"; flags for the centre variants: +4 focal
+ * centerness (fcos_center.py:386-389 cen_type="focal", fcos_center_v1.py:305-307), +8 smooth-L1 on
+ * sigmoid(reg[:4]) (fcos_center_v1.py:115, l1 only), +16 the centerness logit / gradient is column
+ * round_up(C, 8) of the class rows (cen_output_l lives on the cls tower).
+ * `workspace` >= cvl_fcos_loss_workspace_size(B, P).
  * ---------------------------------------------------------------------------------------- */
 size_t cvl_fcos_loss_workspace_size(int B, int P);
 int cvl_fcos_loss(const float* reg_pred, int ld_reg, const float* cls_pred, int ld_cls,
@@ -67,6 +71,11 @@ int cvl_fcos_loss(const float* reg_pred, int ld_reg, const float* cls_pred, int 
  * out [S0][S1][4] float64 = stride * (y_lo, x_lo, y_hi, x_hi) around cell centres (fp32 math). */
 int cvl_fcos_decode(const float* pred, int ld, int S0, int S1, double stride, double* out,
                     cvl_stream_t stream);
+/* FCOS/fcos_center_v1.py:124-147 prediction_to_corners(xy_pred, box_sc, stride): pred [S0][S1][ld>=4]
+ * (y_off, x_off, h, w) fp32 -> out [S0][S1][4] float64 corners of the box centred at
+ * ((cell + off) * stride) with size (h, w) * box_sc (fp32 arithmetic, stored as float64). */
+int cvl_fcos_v1_decode(const float* pred, int ld, int S0, int S1, float box_sc, float stride, double* out,
+                       cvl_stream_t stream);
 
 
 /* FCOS/fcos_center.py:149-317 format_data (the variant of train_fcos_center_voc.py): level by
@@ -78,6 +87,13 @@ int cvl_fcos_decode(const float* pred, int ld, int S0, int S1, double stride, do
 int cvl_fcos_center_assign(const float* boxes, const int32_t* nbox, const float* img_dim, int B, int n_max,
                            int pad_h, int pad_w, int num_classes, const int32_t* strides, const float* b_dim,
                            int center_only, float* targets, int32_t* num_targets, cvl_stream_t stream);
+/* FCOS/fcos_center_v1.py:149-281 format_data (train_fcos_center_v1_voc.py): same level selection and
+ * ascending-area order as cvl_fcos_center_assign; each box writes ONLY its centroid cell
+ * (int(centre * img_dim / stride)): (y_off, x_off, h / box_sc, w / box_sc) of the last box there,
+ * centre score 1, class bits OR-ed; box_sc = b_dim[l] (l < 4) or max(img_dim) (l = 4). */
+int cvl_fcos_center_v1_assign(const float* boxes, const int32_t* nbox, const float* img_dim, int B, int n_max,
+                              int pad_h, int pad_w, int num_classes, const int32_t* strides, const float* b_dim,
+                              float* targets, int32_t* num_targets, cvl_stream_t stream);
 
 /* ------------------------------------------------------------------------------------------
  * Segmented implicit-GEMM convolution (bf16 MFMA, fp32 accumulate).  Replaces every Conv2D of

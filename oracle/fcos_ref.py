@@ -318,3 +318,78 @@ def center_format_data(gt_labels, img_dim, num_classes, img_pad=None, b_dim=None
         outs.append(out)
         counts.append(len(lab))
     return outs, counts
+
+
+def center_v1_prediction_to_corners(xy_pred, box_sc, stride):
+    """FCOS/fcos_center_v1.py:124-147: fp32 tensor math (grid + offset) * stride, size * box_sc,
+    centre -+ size / 2, stored into a float64 array."""
+    p = np.asarray(xy_pred, np.float32)
+    gy, gx = np.meshgrid(np.arange(p.shape[0], dtype=np.float32), np.arange(p.shape[1], dtype=np.float32),
+                         indexing="ij")
+    f32 = np.float32
+    yc = (gy + p[..., 0]) * f32(stride)
+    xc = (gx + p[..., 1]) * f32(stride)
+    bh = p[..., 2] * f32(box_sc)
+    bw = p[..., 3] * f32(box_sc)
+    out = np.zeros(p.shape[:2] + (4,))
+    out[..., 0], out[..., 2] = yc - bh / f32(2.0), yc + bh / f32(2.0)
+    out[..., 1], out[..., 3] = xc - bw / f32(2.0), xc + bw / f32(2.0)
+    return out
+
+
+def center_v1_format_data(gt_labels, img_dim, num_classes, img_pad=None, b_dim=None, strides=None):
+    """FCOS/fcos_center_v1.py:149-281 (numpy >= 2 promotion): level by max(h, w) px against b_dim,
+    ascending area; each box writes its centroid cell int(centre * img_dim / stride):
+    (y_off, x_off, h / box_sc, w / box_sc), centre 1, class bit; box_sc = b_dim[l] or max(img_dim)."""
+    strides = list(STRIDES) if strides is None else list(strides)
+    b_dim = [32, 64, 128, 256] if b_dim is None else list(b_dim)
+    dim = np.asarray(img_dim, f32)
+    pad = dim if img_pad is None else np.asarray(img_pad, f32)
+    gt = np.asarray(gt_labels, f32).reshape(-1, 5)
+    gh, gw = gt[:, 2] * dim[0], gt[:, 3] * dim[1]
+    m = np.maximum(gw, gh)
+    outs, counts = [], []
+    for na, stride in enumerate(strides):
+        hmax, wmax = int(pad[0] / f32(stride)), int(pad[1] / f32(stride))
+        out = np.zeros((hmax, wmax, num_classes + 5))
+        if na == 0:
+            sc, idx = f32(b_dim[0]), np.nonzero(m < b_dim[0])[0]
+        elif na == len(strides) - 1:
+            sc, idx = max(dim[0], dim[1]), np.nonzero(m >= b_dim[-1])[0]
+        else:
+            sc, idx = f32(b_dim[na]), np.nonzero((m >= b_dim[na - 1]) & (m < b_dim[na]))[0]
+        lab = gt[idx]
+        if len(lab) > 1:
+            lab = lab[np.argsort(np.multiply(lab[:, 2] * dim[0], lab[:, 3] * dim[1]), kind="stable")]
+        for t in lab:
+            ry, rx = t[0] * dim[0], t[1] * dim[1]
+            yc, xc = int(ry / f32(stride)), int(rx / f32(stride))
+            out[yc, xc, :4] = [(ry - f32(yc * stride)) / f32(stride), (rx - f32(xc * stride)) / f32(stride),
+                               (t[2] * dim[0]) / sc, (t[3] * dim[1]) / sc]
+            out[yc, xc, 4] = 1.0
+            out[yc, xc, 5 + int(t[4])] = 1.0
+        outs.append(out)
+        counts.append(len(lab))
+    return outs, counts
+
+
+def center_model_loss(y_true, y_pred, reg_type="l1", cen_type="l1", reg_sigmoid=False):
+    """FCOS/fcos_center.py:365-399 (cen_type "l1" | "focal") and, with reg_sigmoid=True and
+    cen_type="focal", FCOS/fcos_center_v1.py:283-317 fed the raw head logits (the v1 model applies
+    the sigmoid to the reg head, fcos_center_v1.py:115).  y_pred: list of [1,S,S,5+C] raw outputs."""
+    cls = reg = cen = 0.0
+    for yt, yp in zip(y_true, y_pred):
+        yt = np.asarray(yt)
+        yp = np.asarray(yp, np.float32)[0].astype(np.float64)
+        mask = (yt[..., 5:].max(-1) >= 1).astype(np.float64)
+        cls += focal_loss(yt[..., 5:], yp[..., 5:])
+        if cen_type.lower() == "l1":
+            cen += smooth_l1_loss(yt[..., 4], _sig(yp[..., 4]), mask=1.0)
+        else:
+            cen += focal_loss(yt[..., 4], yp[..., 4])
+        r = _sig(yp[..., :4]) if reg_sigmoid else yp[..., :4]
+        if reg_type == "iou":
+            reg += iou_loss(yt[..., :4], r, mask)
+        else:
+            reg += smooth_l1_loss(yt[..., :4], r, mask=mask)
+    return cls, reg, cen

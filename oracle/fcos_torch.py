@@ -40,3 +40,18 @@ def packed_loss(reg, cls, tgt, C, reg_type="l1"):
     else:
         lr = smooth_l1(tgt[:, :4], reg[:, :4], mask)
     return lc, lr, le
+
+
+def centre_packed_loss(reg, cen, cls, tgt, C, reg_type="l1", cen_type="focal", reg_sigmoid=False):
+    """FCOS/fcos_center.py:365-399 / fcos_center_v1.py:283-317 (oracle/fcos_ref.center_model_loss):
+    reg [N,>=4] raw head (sigmoid'd first when reg_sigmoid), cen [N] logit, cls [N,>=C]."""
+    mask = (tgt[:, 5:5 + C].max(-1).values >= 1).to(tgt.dtype)
+    lc = focal(tgt[:, 5:5 + C], cls[:, :C])
+    if cen_type == "focal":
+        le = focal(tgt[:, 4], cen)
+    else:
+        d = tgt[:, 4] - torch.sigmoid(cen)
+        le = torch.where(d.abs() < 1, 0.5 * d * d, d.abs()).sum()
+    r = torch.sigmoid(reg[:, :4]) if reg_sigmoid else reg[:, :4]
+    lr = iou(tgt[:, :4], r, mask) if reg_type == "iou" else smooth_l1(tgt[:, :4], r, mask)
+    return lc, lr, le

@@ -326,7 +326,51 @@ def work_centernet_softnms(out_path):
     np.savez_compressed(out_path, **arrays)
 
 
+def work_fcos_center_v1(out_path):
+    """FCOS/fcos_center_v1.py format_data (centroid-cell targets) and model_loss (focal cls + focal
+    centerness + smooth-L1 on the sigmoid reg head), plus fcos_center.py's model_loss with
+    cen_type="focal" (what train_fcos_center_voc.py trains) on the same random heads."""
+    tf = _child_setup("FCOS")
+    import fcos_center as fc
+    import fcos_center_v1 as f1
+    rng = np.random.default_rng(321)
+    arrays = {}
+    C = 20
+    for i in range(16):
+        D = [512, 384, 640, 448][i % 4]
+        boxes = synth_boxes(rng, float(D), float(D), C, lam=2.0 if i < 8 else 20.0, nmax=40, side_lo=4.0,
+                            side_hi=float(D) if i < 8 else 80.0, edge_frac=0.2)
+        img_dim = np.array([D, D], np.float32)
+        outs, nt = f1.format_data(tf.constant(boxes), img_dim, C, img_pad=[D, D])
+        arrays["case_%d_boxes" % i] = boxes
+        arrays["case_%d_D" % i] = np.int32(D)
+        arrays["case_%d_ntgt" % i] = np.array(nt, np.int32)
+        for l in range(5):
+            arrays["case_%d_L%d" % (i, l)] = np.asarray(outs[l]).astype(np.float32)
+        if i in (1, 5, 9):                  # D = 384: small heads keep the fixture small
+            raw = [rng.normal(0, 1.5, size=(1,) + np.asarray(o).shape).astype(np.float32) for o in outs]
+            for l in range(5):
+                raw[l][..., 4:] -= 2.0
+            sig = []
+            for r in raw:
+                q = r.copy()
+                q[..., :4] = np.asarray(tf.nn.sigmoid(tf.constant(r[..., :4])))
+                sig.append(tf.constant(q))
+            yt = [np.asarray(o, np.float32) for o in outs]
+            arrays["loss_%d_out" % i] = np.array([float(v) for v in f1.model_loss(yt, sig)], np.float64)
+            arrays["loss_%d_center_focal" % i] = np.array(
+                [float(v) for v in fc.model_loss(yt, [tf.constant(r) for r in raw], cen_type="focal")], np.float64)
+            for l in range(5):
+                arrays["loss_%d_raw_L%d" % (i, l)] = raw[l]
+    # prediction_to_corners (:124-147): sigmoid-range offsets/sizes, non-square map
+    p = rng.uniform(0.0, 1.0, (12, 9, 5 + C)).astype(np.float32)
+    arrays["p2c_in"] = p
+    arrays["p2c_out"] = np.asarray(f1.prediction_to_corners(tf.constant(p), 320.0, 16), np.float64)
+    np.savez_compressed(out_path, **arrays)
+
+
 WORKERS = {"fcos": work_fcos, "retinanet": work_retina, "centernet": work_centernet,
+           "fcos_center_v1": work_fcos_center_v1,
            "centernet_softnms": work_centernet_softnms,
            "retina_decode": work_retina_decode,
            "fcos_center": work_fcos_center}

@@ -170,3 +170,28 @@ def test_centernet_soft_nms_oracle(golden):
     for i in range(8):
         got = centernet_ref.soft_nms(d["soft_%d_in" % i], float(d["soft_%d_sigma" % i]))
         np.testing.assert_array_equal(got, d["soft_%d_out" % i])
+
+
+def test_fcos_center_v1_format_data_and_losses(golden):
+    """FCOS/fcos_center_v1.py format_data (bit-exact maps and counts) and model_loss (the v1 model's
+    sigmoid reg head), and fcos_center.py model_loss with cen_type="focal", vs the reference's own
+    outputs (make_golden.py fcos_center_v1)."""
+    d = golden("fcos_center_v1")
+    n_loss = 0
+    for i in range(16):
+        D = int(d["case_%d_D" % i])
+        outs, nt = fcos_ref.center_v1_format_data(d["case_%d_boxes" % i], np.array([D, D], np.float32), 20,
+                                                  img_pad=[D, D])
+        assert list(nt) == list(d["case_%d_ntgt" % i])
+        for l in range(5):
+            np.testing.assert_array_equal(outs[l].astype(np.float32), d["case_%d_L%d" % (i, l)])
+        if "loss_%d_out" % i in d.files:
+            n_loss += 1
+            yt = [d["case_%d_L%d" % (i, l)] for l in range(5)]
+            raw = [d["loss_%d_raw_L%d" % (i, l)] for l in range(5)]
+            np.testing.assert_allclose(fcos_ref.center_model_loss(yt, raw, cen_type="focal", reg_sigmoid=True),
+                                       d["loss_%d_out" % i], rtol=1e-5)
+            np.testing.assert_allclose(fcos_ref.center_model_loss(yt, raw, cen_type="focal"),
+                                       d["loss_%d_center_focal" % i], rtol=1e-5)
+    assert n_loss == 3
+    np.testing.assert_array_equal(fcos_ref.center_v1_prediction_to_corners(d["p2c_in"], 320.0, 16), d["p2c_out"])
