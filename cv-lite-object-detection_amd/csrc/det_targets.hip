@@ -6,6 +6,7 @@
 //   cvl_centernet_splat  CenterNet/tf_centernet.py:6-19, 152-342
 //   cvl_det_loss         tf_centernet_hourglass.py:458-505 / retinanet_module.py:367-426
 //   cvl_nms              tf_centernet_hourglass.py:22-85 (method 'nms')
+//   cvl_hourglass_v2_*   CenterNet/train_hourglass_voc.py:96-160, tf_hourglass_net.py:398-447
 // Index/target kernels follow the reference's fp32 operation sequences exactly (this file is
 // compiled with -ffp-contract=off) and keep float64 where the reference computes in float64.
 #include "cvl_common.h"
@@ -418,6 +419,160 @@ __global__ void __launch_bounds__(NT) centernet_loss_kernel(CnLossArgs a) {
       d[j] = f32_to_bf16(mask * g * a.reg_scale);
     }
     for (int c = 4 + a.C; c < a.ld_d; ++c) d[c] = 0;
+  }
+  __shared__ double red[2][NT / 64];
+  double v0 = warp_sum_d((double)s_cls), v1 = warp_sum_d((double)s_reg);
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  if (lane == 0) { red[0][w] = v0; red[1][w] = v1; }
+  __syncthreads();
+  if (threadIdx.x < 2) {
+    double s = 0.0;
+    for (int k = 0; k < NT / 64; ++k) s += red[threadIdx.x][k];
+    a.partial[((size_t)b * a.tiles + blockIdx.x) * 2 + threadIdx.x] = s;
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// CenterNet v2 (CenterNet/tf_hourglass_net.py) targets: the inline builder of
+// CenterNet/train_hourglass_voc.py train() :96-160 for one batch.  boxes [B][n_max][5] are the
+// dataset's corner rows (b0, b1, b2, b3, label), converted by utils.convert_to_xywh (:16-27) to
+// (x_cen, y_cen, w, h); one (raw_dims, img_dims) per batch (the step's jitter scale), pad_dims =
+// int((img_dims - raw_dims) / 2).  Output [B][S][S][4][5+C], S = img_dims / 8.  Boxes go in
+// ascending w*h*100 order (stable on ties); each writes (y_off, x_off, h_reg, w_reg, 1) of its
+// (cell, scale) -- the last writer wins -- and ORs its class bit.  fp32 sequences as the
+// reference's numpy float32 scalars (NEP 50); negative cell indices wrap as numpy indexing does,
+// cells past the map (an IndexError there) and labels outside [0, C) are skipped.
+// ------------------------------------------------------------------------------------------------
+struct Hg2Args {
+  const float* boxes;
+  const int32_t* nbox;
+  float* out;
+  int n_max, C, S, raw, img;
+};
+
+__global__ void __launch_bounds__(NT) hg2_assign_kernel(Hg2Args a) {
+  const int b = blockIdx.y;
+  const int tid = threadIdx.x;
+  __shared__ int order[kMaxBox];
+  __shared__ float area[kMaxBox];
+  __shared__ int key[kMaxBox];                 // (row * S + col) * 4 + scale, -1 = no write
+  __shared__ int cls[kMaxBox];
+  __shared__ float val[kMaxBox][4];
+  int n = a.nbox[b];
+  n = n < 0 ? 0 : (n > a.n_max ? a.n_max : n);
+  const float* bx = a.boxes + (size_t)b * a.n_max * 5;
+  for (int i = tid; i < n; i += NT) {
+    const float* r = bx + i * 5;
+    area[i] = ((r[2] - r[0]) * (r[3] - r[1])) * 100.0f;           // tmp_box_areas (:113-114)
+  }
+  __syncthreads();
+  for (int i = tid; i < n; i += NT) {
+    int rk = 0;
+    for (int j = 0; j < n; ++j) rk += (area[j] < area[i]) || (area[j] == area[i] && j < i);
+    order[rk] = i;
+  }
+  __syncthreads();
+  const float rawf = (float)a.raw;
+  const float padf = (float)((a.img - a.raw) / 2);
+  float sc[4];                                                      // img_scale (:108-109)
+#pragma unroll
+  for (int k = 0; k < 4; ++k) sc[k] = (float)((double)a.img / (double)(1 << (3 - k)));
+  for (int k = tid; k < n; k += NT) {
+    const float* r = bx + order[k] * 5;
+    const float x0 = (r[0] + r[2]) / 2.0f, y0 = (r[1] + r[3]) / 2.0f;
+    const float bw = r[2] - r[0], bh = r[3] - r[1];
+    const float xcen = padf + x0 * rawf, ycen = padf + y0 * rawf;  // :123-126
+    const float width = bw * rawf, height = bh * rawf;
+    int kk = -1;
+    if (!(width < 0.f || height < 0.f)) {
+      int id = 3;
+      if (width < sc[0] && height < sc[0]) id = 0;
+      else if (width < sc[1] && height < sc[1]) id = 1;
+      else if (width < sc[2] && height < sc[2]) id = 2;
+      const float bs = sc[id];
+      const float wreg = width / bs, hreg = height / bs;              // :144-151
+      int wc = (int)(xcen / 8.0f), hc = (int)(ycen / 8.0f);
+      const float woff = (xcen - (float)(wc * 8)) / 8.0f;
+      const float hoff = (ycen - (float)(hc * 8)) / 8.0f;
+      if (wc < 0) wc += a.S;
+      if (hc < 0) hc += a.S;
+      if (wc >= 0 && wc < a.S && hc >= 0 && hc < a.S) {
+        kk = (hc * a.S + wc) * 4 + id;
+        val[k][0] = hoff; val[k][1] = woff; val[k][2] = hreg; val[k][3] = wreg;
+      }
+    }
+    key[k] = kk;
+    cls[k] = (int)r[4];
+  }
+  __syncthreads();
+  const int R = 5 + a.C;
+  const int rows = a.S * a.S * 4;
+  for (int row = blockIdx.x * NT + tid; row < rows; row += gridDim.x * NT) {
+    float v[5] = {0.f, 0.f, 0.f, 0.f, 0.f};
+    uint32_t bits[kWords];
+#pragma unroll
+    for (int k = 0; k < kWords; ++k) bits[k] = 0u;
+    for (int k = 0; k < n; ++k) {
+      if (key[k] != row) continue;
+      v[0] = val[k][0]; v[1] = val[k][1]; v[2] = val[k][2]; v[3] = val[k][3]; v[4] = 1.0f;
+      if (cls[k] >= 0 && cls[k] < a.C) bits[cls[k] >> 5] |= 1u << (cls[k] & 31);
+    }
+    float* o = a.out + ((size_t)b * rows + row) * R;
+#pragma unroll
+    for (int k = 0; k < 5; ++k) o[k] = v[k];
+    for (int c = 0; c < a.C; ++c) o[5 + c] = ((bits[c >> 5] >> (c & 31)) & 1u) ? 1.0f : 0.0f;
+  }
+}
+
+// CenterNet v2 model_loss (tf_hourglass_net.py:398-413) inside train_step (:415-447) straight off
+// the head conv: pred [B*P][ld_pred] fp32 = the Conv2D(4*(5+C)) logits with b_focal folded into
+// the class channels' bias (channel sc*(5+C) + j of cell p = row (p, sc) of the [S,S,4,5+C]
+// reshape); targets [B*P][4][5+C].  reg = sum |t - sigmoid(x)| * mask (mask = t[4]); cls = focal
+// (loss_type "focal") or sigmoid cross-entropy over channels 4..4+C (labels cast to int).  Writes
+// the bf16 gradient of cls_scale*cls + reg_scale*reg [B*P][ld_d] (channels >= 4*(5+C) zeroed).
+struct Hg2LossArgs {
+  const float* pred;
+  const float* tgt;
+  double* partial;
+  cvl_bf16* d;
+  int ld_pred, ld_d, P, C, tiles, sce;
+  float cls_scale, reg_scale;
+};
+
+__global__ void __launch_bounds__(NT) hg2_loss_kernel(Hg2LossArgs a) {
+  const int b = blockIdx.y;
+  const int row = blockIdx.x * NT + threadIdx.x;            // (pixel, scale)
+  const int R = 5 + a.C;
+  float s_cls = 0.f, s_reg = 0.f;
+  if (row < a.P * 4) {
+    const int p = row >> 2, sc = row & 3;
+    const float* t = a.tgt + ((size_t)b * a.P * 4 + row) * R;
+    const float* x = a.pred + ((size_t)b * a.P + p) * a.ld_pred + sc * R;
+    cvl_bf16* d = a.d + ((size_t)b * a.P + p) * a.ld_d + sc * R;
+    const float m = t[4];
+    const bool prob = (a.sce & 2) != 0;                     // box channels already sigmoid'd
+    for (int j = 0; j < 4; ++j) {
+      const float s = prob ? x[j] : 1.0f / (1.0f + expf(-x[j]));
+      const float df = t[j] - s;
+      s_reg += fabsf(df) * m;
+      const float sg = df > 0.f ? -1.0f : (df < 0.f ? 1.0f : 0.0f);
+      d[j] = f32_to_bf16(m * sg * (prob ? 1.0f : s * (1.0f - s)) * a.reg_scale);
+    }
+    for (int j = 4; j < R; ++j) {
+      const float y = (float)(int)t[j];
+      const float xv = x[j];
+      float g;
+      if (a.sce & 1) {
+        const float e = expf(-fabsf(xv));
+        s_cls += (fmaxf(xv, 0.f) - xv * y) + log1pf(e);
+        g = (xv >= 0.f ? 1.0f / (1.0f + e) : e / (1.0f + e)) - y;
+      } else {
+        s_cls += focal_elem(y, xv, &g);
+      }
+      d[j] = f32_to_bf16(g * a.cls_scale);
+    }
+    if (sc == 3)
+      for (int c = 4 * R; c < a.ld_d; ++c) a.d[((size_t)b * a.P + p) * a.ld_d + c] = 0;
   }
   __shared__ double red[2][NT / 64];
   double v0 = warp_sum_d((double)s_cls), v1 = warp_sum_d((double)s_reg);
@@ -933,5 +1088,38 @@ extern "C" int cvl_centernet_decode(const float* pred, int ld, int H, int W, int
   CVL_CHECK_ARG(pred && rows && count && H > 0 && W > 0 && num_classes > 0 && ld >= 4 + num_classes);
   hipLaunchKernelGGL(centernet_decode_kernel, dim3(1), dim3(1024), 0, S_, pred, ld, H, W, num_classes, stride, thresh,
                      w_ratio, h_ratio, img_width, img_height, rows, count);
+  return cvl_launch_status();
+}
+
+extern "C" int cvl_hourglass_v2_assign(const float* boxes, const int32_t* nbox, int B, int n_max, int raw_dims,
+                                       int img_dims, int num_classes, float* targets, cvl_stream_t stream) {
+  CVL_CHECK_ARG(boxes && nbox && targets && B > 0 && n_max > 0 && n_max <= kMaxBox);
+  CVL_CHECK_ARG(num_classes > 0 && num_classes <= 32 * kWords && raw_dims > 0 && img_dims >= raw_dims);
+  CVL_CHECK_ARG(img_dims % 8 == 0);
+  Hg2Args a;
+  a.boxes = boxes; a.nbox = nbox; a.out = targets; a.n_max = n_max; a.C = num_classes;
+  a.S = img_dims / 8; a.raw = raw_dims; a.img = img_dims;
+  const int rows = a.S * a.S * 4;
+  int gx = (rows + NT - 1) / NT;
+  gx = gx > 64 ? 64 : gx;
+  hipLaunchKernelGGL(hg2_assign_kernel, dim3(gx, B), dim3(NT), 0, S_, a);
+  return cvl_launch_status();
+}
+
+extern "C" size_t cvl_hourglass_v2_loss_workspace_size(int B, int P) {
+  return (size_t)B * ((4 * (size_t)P + NT - 1) / NT) * 2 * sizeof(double);
+}
+
+extern "C" int cvl_hourglass_v2_loss(const float* pred, int ld_pred, const float* targets, int B, int P,
+                                     int num_classes, int loss_type, float cls_scale, float reg_scale, float* losses,
+                                     void* d_pred, int ld_d, void* workspace, cvl_stream_t stream) {
+  CVL_CHECK_ARG(pred && targets && losses && d_pred && workspace && B > 0 && P > 0 && num_classes > 0);
+  CVL_CHECK_ARG(ld_pred >= 4 * (5 + num_classes) && ld_d >= 4 * (5 + num_classes) && loss_type >= 0 && loss_type <= 3);
+  Hg2LossArgs a;
+  a.pred = pred; a.tgt = targets; a.partial = (double*)workspace; a.d = (cvl_bf16*)d_pred;
+  a.ld_pred = ld_pred; a.ld_d = ld_d; a.P = P; a.C = num_classes; a.tiles = (4 * P + NT - 1) / NT;
+  a.sce = loss_type; a.cls_scale = cls_scale; a.reg_scale = reg_scale;
+  hipLaunchKernelGGL(hg2_loss_kernel, dim3(a.tiles, B), dim3(NT), 0, S_, a);
+  hipLaunchKernelGGL(det_loss_finalize, dim3(B), dim3(FIN_T), 0, S_, (const double*)workspace, losses, a.tiles);
   return cvl_launch_status();
 }

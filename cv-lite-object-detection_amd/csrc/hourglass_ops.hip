@@ -191,10 +191,11 @@ __global__ void __launch_bounds__(NT) sep_fold_kernel(const cvl_sep_item* __rest
   const int2 r = rows[blockIdx.x];
   const cvl_sep_item it = items[r.x];
   const int ci = r.y;
+  const int cl = it.cin_ld ? it.cin_ld : it.cin, ol = it.cout_ld ? it.cout_ld : it.cout;
   for (int co = threadIdx.x; co < it.cout; co += NT) {
     const float p = it.pw[(long)ci * it.cout + co];
     for (int t = 0; t < it.taps; ++t)
-      it.weff[((long)t * it.cin + ci) * it.cout + co] = it.dw[(long)t * it.cin + ci] * p;
+      it.weff[((long)t * cl + ci) * ol + co] = it.dw[(long)t * it.cin + ci] * p;
   }
 }
 
@@ -205,10 +206,11 @@ __global__ void __launch_bounds__(NT) sep_unfold_kernel(const cvl_sep_item* __re
   const cvl_sep_item it = items[r.x];
   const int ci = r.y;
   __shared__ float red[NT / 64][64];
+  const int cl = it.cin_ld ? it.cin_ld : it.cin, ol = it.cout_ld ? it.cout_ld : it.cout;
   for (int co = threadIdx.x; co < it.cout; co += NT) {
     float a = 0.f;
     for (int t = 0; t < it.taps; ++t)
-      a += it.gweff[((long)t * it.cin + ci) * it.cout + co] * it.dw[(long)t * it.cin + ci];
+      a += it.gweff[((long)t * cl + ci) * ol + co] * it.dw[(long)t * it.cin + ci];
     it.gpw[(long)ci * it.cout + co] = a;
   }
   const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -218,7 +220,7 @@ __global__ void __launch_bounds__(NT) sep_unfold_kernel(const cvl_sep_item* __re
       const int t = t0 + k;
       float a = 0.f;
       for (int co = threadIdx.x; co < it.cout; co += NT)
-        a += it.gweff[((long)t * it.cin + ci) * it.cout + co] * it.pw[(long)ci * it.cout + co];
+        a += it.gweff[((long)t * cl + ci) * ol + co] * it.pw[(long)ci * it.cout + co];
       a = warp_sum(a);
       if (lane == 0) red[wv][k] = a;
     }
@@ -291,6 +293,148 @@ __global__ void adam_kernel(float* w, const float* g, float* m, float* v, long n
 }
 
 __global__ void incr_kernel(int32_t* c) { *c = *c + 1; }
+
+// ---------------------------------------------------------------------------------------------
+// CenterNet v2 (tf_hourglass_net.py:115-449) memory-bound pieces:
+//   * bilinear x2 up-sampling of a residual sum, UpSampling2D(a + b) (:252-305), in one pass: the
+//     taps of a + b are formed in fp32 (no bf16 rounding of the sum);
+//   * the "pass through" reshape-concat (:307-344, Q36): every feature map [B][h][w][C] is
+//     tf.reshape'd to [B][S][S][C*h*w/(S*S)] -- a reinterpretation of the row-major NHWC bytes,
+//     not a space-to-depth -- and the 12 maps are concatenated on channels.  Maps live with a
+//     padded channel pitch (c_ld >= C, pads zero): destination element (b, q, off_k + j) is source
+//     element f = q*W_k + j of map k (W_k = C_k*h_k*w_k/(S*S)), pixel f / C_k, channel f % C_k.
+//     C_k % 4 == 0 and W_k % 4 == 0, so 4 channels (8 bytes) move together.  The backward is the
+//     inverse permutation (d_src = beta*d_src + d_dst gathered), pads of d_src written zero.
+// ---------------------------------------------------------------------------------------------
+__global__ void up2_sum_kernel(const cvl_bf16* __restrict__ pa, const cvl_bf16* __restrict__ pb,
+                               cvl_bf16* __restrict__ out, int h, int w, int C, long total) {
+  const int C8 = C / 8;
+  const int H = 2 * h, W = 2 * w;
+  for (long i = blockIdx.x * (long)NT + threadIdx.x; i < total; i += (long)gridDim.x * NT) {
+    const long pix = i / C8;
+    const int c0 = (int)(i - pix * C8) * 8;
+    const long hw = (long)H * W;
+    const int b = (int)(pix / hw);
+    const int q = (int)(pix - (long)b * hw);
+    const int oy = q / W, ox = q - (q / W) * W;
+    int y0, y1, x0, x1;
+    float ly, lx;
+    bilin_taps(oy, h, &y0, &y1, &ly);
+    bilin_taps(ox, w, &x0, &x1, &lx);
+    const long ib = (long)b * h * w * C + c0;
+    const long o4[4] = {((long)y0 * w + x0) * C, ((long)y0 * w + x1) * C, ((long)y1 * w + x0) * C,
+                        ((long)y1 * w + x1) * C};
+    float t[4][8];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      unpack8(*reinterpret_cast<const s16x8*>(pa + ib + o4[k]), t[k]);
+      if (pb) {
+        float u[8];
+        unpack8(*reinterpret_cast<const s16x8*>(pb + ib + o4[k]), u);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) t[k][e] += u[e];
+      }
+    }
+    float o[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const float top = t[0][u] + (t[1][u] - t[0][u]) * lx;
+      const float bot = t[2][u] + (t[3][u] - t[2][u]) * lx;
+      o[u] = top + (bot - top) * ly;
+    }
+    *reinterpret_cast<s16x8*>(out + pix * C + c0) = pack8(o);
+  }
+}
+
+struct RcPlan {
+  cvl_rc_item it[CVL_RC_MAX_ITEMS];
+  long off[CVL_RC_MAX_ITEMS + 1];     // destination column offsets (prefix of W_k)
+  int n, S2, ld_dst;
+};
+
+__global__ void reshape_concat_kernel(RcPlan p, cvl_bf16* __restrict__ dst, long total4) {
+  const int ld4 = p.ld_dst / 4;
+  for (long i = blockIdx.x * (long)NT + threadIdx.x; i < total4; i += (long)gridDim.x * NT) {
+    const long bq = i / ld4;
+    const int j = (int)(i - bq * ld4) * 4;
+    const int b = (int)(bq / p.S2);
+    const long q = bq - (long)b * p.S2;
+    uint2 v = make_uint2(0u, 0u);
+    int k = 0;
+    while (k < p.n && j >= p.off[k + 1]) ++k;
+    if (k < p.n) {
+      const cvl_rc_item& s = p.it[k];
+      const long wk = p.off[k + 1] - p.off[k];
+      const long f = q * wk + (j - p.off[k]);
+      const long px = f / s.c, c = f - (f / s.c) * s.c;
+      v = *reinterpret_cast<const uint2*>(static_cast<const cvl_bf16*>(s.src) +
+                                          ((long)b * s.hw + px) * s.c_ld + c);
+    }
+    *reinterpret_cast<uint2*>(dst + bq * p.ld_dst + j) = v;
+  }
+}
+
+// grid.y = item: walks the item's source elements (4 channels per thread, pads included)
+__global__ void reshape_concat_bwd_kernel(RcPlan p, const cvl_bf16* __restrict__ ddst, int B) {
+  const cvl_rc_item s = p.it[blockIdx.y];
+  const long wk = p.off[blockIdx.y + 1] - p.off[blockIdx.y];
+  const int l4 = s.c_ld / 4;
+  const long total4 = (long)B * s.hw * l4;
+  cvl_bf16* dsrc = static_cast<cvl_bf16*>(s.dsrc);
+  for (long i = blockIdx.x * (long)NT + threadIdx.x; i < total4; i += (long)gridDim.x * NT) {
+    const long bp = i / l4;
+    const int c = (int)(i - bp * l4) * 4;
+    const int b = (int)(bp / s.hw);
+    const long px = bp - (long)b * s.hw;
+    cvl_bf16* o = dsrc + bp * s.c_ld + c;
+    if (c >= s.c) {
+      if (s.beta == 0.f) *reinterpret_cast<uint2*>(o) = make_uint2(0u, 0u);
+      continue;
+    }
+    const long f = px * s.c + c;
+    const long q = f / wk, j = f - (f / wk) * wk;
+    const uint2 g = *reinterpret_cast<const uint2*>(ddst + ((long)b * p.S2 + q) * p.ld_dst + p.off[blockIdx.y] + j);
+    if (s.beta == 0.f) {
+      *reinterpret_cast<uint2*>(o) = g;
+    } else {
+      const uint2 old = *reinterpret_cast<const uint2*>(o);
+      const uint32_t gw[2] = {g.x, g.y}, ow[2] = {old.x, old.y};
+      uint32_t rw[2];
+#pragma unroll
+      for (int e = 0; e < 2; ++e) {
+        const float g0 = bf16_to_f32((cvl_bf16)(gw[e] & 0xffffu)), g1 = bf16_to_f32((cvl_bf16)(gw[e] >> 16));
+        const float o0 = bf16_to_f32((cvl_bf16)(ow[e] & 0xffffu)), o1 = bf16_to_f32((cvl_bf16)(ow[e] >> 16));
+        rw[e] = (uint32_t)f32_to_bf16(g0 + s.beta * o0) | ((uint32_t)f32_to_bf16(g1 + s.beta * o1) << 16);
+      }
+      *reinterpret_cast<uint2*>(o) = make_uint2(rw[0], rw[1]);
+    }
+  }
+}
+
+// b_eff[c] = bias[c] + ((c % period) >= c0 ? *scalar : 0)   (the v2 head: b_focal on every scale's
+// class channels, tf_hourglass_net.py:380-385)
+__global__ void bias_scalar_fold_p_kernel(const float* bias, const float* scalar, float* b_eff, int n, int period,
+                                          int c0) {
+  const int c = blockIdx.x * NT + threadIdx.x;
+  if (c < n) b_eff[c] = bias[c] + ((c % period) >= c0 ? *scalar : 0.f);
+}
+
+__global__ void bias_scalar_unfold_p_kernel(const float* g_eff, float* g_bias, float* g_scalar, int n, int period,
+                                            int c0) {
+  __shared__ float red[NT];
+  float s = 0.f;
+  for (int c = threadIdx.x; c < n; c += NT) {
+    g_bias[c] = g_eff[c];
+    if ((c % period) >= c0) s += g_eff[c];
+  }
+  red[threadIdx.x] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float t = 0.f;
+    for (int k = 0; k < NT; ++k) t += red[k];
+    *g_scalar = t;
+  }
+}
 
 }  // namespace
 
@@ -372,5 +516,74 @@ extern "C" int cvl_adam_clip_update(float* w, const float* g, float* m, float* v
   hipLaunchKernelGGL(adam_kernel, dim3(grid_for(n, NT * 4, 4096)), dim3(NT), 0, S_, w, g, m, v, (long)n, lr_dev,
                      (const int32_t*)iterations, beta1, beta2, eps, inv_bs, clip, (const double*)sumsq_ws);
   hipLaunchKernelGGL(incr_kernel, dim3(1), dim3(1), 0, S_, iterations);
+  return cvl_launch_status();
+}
+
+extern "C" int cvl_upsample_bilinear2x_sum(const void* a, const void* b, void* out, int B, int h, int w, int C,
+                                           cvl_stream_t stream) {
+  CVL_CHECK_ARG(a && out && B > 0 && h > 0 && w > 0 && C % 8 == 0);
+  const long total = (long)B * 4 * h * w * (C / 8);
+  hipLaunchKernelGGL(up2_sum_kernel, dim3(grid_for(total)), dim3(NT), 0, S_, (const cvl_bf16*)a, (const cvl_bf16*)b,
+                     (cvl_bf16*)out, h, w, C, total);
+  return cvl_launch_status();
+}
+
+static int rc_plan(const cvl_rc_item* items, int n, int S2, int ld_dst, RcPlan* p) {
+  CVL_CHECK_ARG(items && n > 0 && n <= CVL_RC_MAX_ITEMS && S2 > 0 && ld_dst % 4 == 0);
+  p->n = n; p->S2 = S2; p->ld_dst = ld_dst;
+  p->off[0] = 0;
+  for (int k = 0; k < n; ++k) {
+    const cvl_rc_item& s = items[k];
+    CVL_CHECK_ARG(s.c > 0 && s.c % 4 == 0 && s.c_ld >= s.c && s.c_ld % 4 == 0 && s.hw > 0);
+    const long elems = (long)s.c * s.hw;
+    CVL_CHECK_ARG(elems % S2 == 0 && (elems / S2) % 4 == 0);
+    p->it[k] = s;
+    p->off[k + 1] = p->off[k] + elems / S2;
+  }
+  CVL_CHECK_ARG(p->off[n] <= ld_dst);
+  return CVL_OK;
+}
+
+extern "C" int cvl_reshape_concat(const cvl_rc_item* items, int n_items, int B, int S2, void* dst, int ld_dst,
+                                  cvl_stream_t stream) {
+  RcPlan p;
+  int st = rc_plan(items, n_items, S2, ld_dst, &p);
+  if (st != CVL_OK) return st;
+  CVL_CHECK_ARG(dst && B > 0);
+  for (int k = 0; k < n_items; ++k) CVL_CHECK_ARG(items[k].src);
+  const long total4 = (long)B * S2 * (ld_dst / 4);
+  hipLaunchKernelGGL(reshape_concat_kernel, dim3(grid_for(total4)), dim3(NT), 0, S_, p, (cvl_bf16*)dst, total4);
+  return cvl_launch_status();
+}
+
+extern "C" int cvl_reshape_concat_backward(const cvl_rc_item* items, int n_items, int B, int S2, const void* d_dst,
+                                           int ld_dst, cvl_stream_t stream) {
+  RcPlan p;
+  int st = rc_plan(items, n_items, S2, ld_dst, &p);
+  if (st != CVL_OK) return st;
+  CVL_CHECK_ARG(d_dst && B > 0);
+  long mx = 0;
+  for (int k = 0; k < n_items; ++k) {
+    CVL_CHECK_ARG(items[k].dsrc);
+    const long t = (long)B * items[k].hw * (items[k].c_ld / 4);
+    mx = t > mx ? t : mx;
+  }
+  hipLaunchKernelGGL(reshape_concat_bwd_kernel, dim3(grid_for(mx, NT, 2048), n_items), dim3(NT), 0, S_, p,
+                     (const cvl_bf16*)d_dst, B);
+  return cvl_launch_status();
+}
+
+extern "C" int cvl_bias_scalar_fold_periodic(const float* bias, const float* scalar, float* b_eff, int n, int period,
+                                             int c0, cvl_stream_t stream) {
+  CVL_CHECK_ARG(bias && scalar && b_eff && n > 0 && period > 0 && c0 >= 0);
+  hipLaunchKernelGGL(bias_scalar_fold_p_kernel, dim3((n + NT - 1) / NT), dim3(NT), 0, S_, bias, scalar, b_eff, n,
+                     period, c0);
+  return cvl_launch_status();
+}
+
+extern "C" int cvl_bias_scalar_unfold_periodic(const float* g_eff, float* g_bias, float* g_scalar, int n, int period,
+                                               int c0, cvl_stream_t stream) {
+  CVL_CHECK_ARG(g_eff && g_bias && g_scalar && n > 0 && period > 0 && c0 >= 0);
+  hipLaunchKernelGGL(bias_scalar_unfold_p_kernel, dim3(1), dim3(NT), 0, S_, g_eff, g_bias, g_scalar, n, period, c0);
   return cvl_launch_status();
 }

@@ -414,8 +414,13 @@ __global__ void __launch_bounds__(NT) bn_bwd_kernel(const cvl_bf16* __restrict__
       pg.dgamma[c] = (float)a2 + (pg.beta_acc != 0.f ? pg.beta_acc * pg.dgamma[c] : 0.f);
     }
   }
-  for (int cgb = cg; cgb < C8; cgb += tpr) {
-    const int c0 = cgb * 8;
+  // uniform trip count over the channel groups (the reduction below synchronises the block):
+  // threads past the last group clamp their parameter loads and neither stream rows nor store
+  const int n_iter = (C8 + tpr - 1) / tpr;
+  for (int itr = 0; itr < n_iter; ++itr) {
+    const int cgb = itr * tpr + cg;
+    const bool act = cgb < C8;
+    const int c0 = (act ? cgb : C8 - 1) * 8;
     float m[8], rs[8], s1[8], s2[8], k1[8], k2[8], gm[8], ga[8], be[8];
     // mask source: y (relu output, residual units) or, when y is null and bnb is given, the
     // ReLU of bn_affine(z) recomputed (non-residual units: one tensor fewer to read)
@@ -435,7 +440,7 @@ __global__ void __launch_bounds__(NT) bn_bwd_kernel(const cvl_bf16* __restrict__
       }
     }
 
-    if (rsub < rpp) {
+    if (rsub < rpp && act) {
       for (int r = r0 + rsub; r < r1; r += rpp * BN_UNR) {
         s16x8 vg[BN_UNR], vz[BN_UNR], vy[BN_UNR];
         long off[BN_UNR];
@@ -501,7 +506,7 @@ __global__ void __launch_bounds__(NT) bn_bwd_kernel(const cvl_bf16* __restrict__
 #pragma unroll
     for (int u = 0; u < 8; ++u) { red[threadIdx.x][u] = s1[u]; red[threadIdx.x][8 + u] = s2[u]; }
     __syncthreads();
-    if (rsub == 0) {
+    if (rsub == 0 && act) {
       float* pp = part + (((long)b * gridDim.x + blockIdx.x) * C + c0) * 2;
       for (int u = 0; u < 8; ++u) {
         float a1 = 0.f, a2 = 0.f;
@@ -1080,7 +1085,6 @@ extern "C" int cvl_bn_apply(const void* z, const float* mean_rstd, const float* 
                             const void* residual, void* y, int B, int HW, int C, int relu,
                             cvl_stream_t stream) {
   CVL_CHECK_ARG(z && mean_rstd && gamma && beta && y && C % 8 == 0 && B > 0 && HW > 0);
-  CVL_CHECK_ARG(C / 8 <= NT || (C / 8) % NT == 0);
   const int rpb = bn_rows_per_blk(B, HW, C);
   hipLaunchKernelGGL(bn_apply_kernel<false>, dim3((HW + rpb - 1) / rpb, B), dim3(NT), 0, S_, (const cvl_bf16*)z,
                      mean_rstd, gamma, beta, (const cvl_bf16*)residual, (cvl_bf16*)y, C, HW, relu, rpb,
@@ -1093,7 +1097,7 @@ extern "C" int cvl_bn_finalize_apply(const double* stats, float* mean_rstd, floa
                                      void* y, int B, int HW, int C, int relu, float eps, float momentum,
                                      cvl_stream_t stream) {
   CVL_CHECK_ARG(stats && mean_rstd && z && gamma && beta && y && C % 8 == 0 && B > 0 && HW > 0);
-  CVL_CHECK_ARG(C <= BN_FIN_MAXC && (C / 8 <= NT || (C / 8) % NT == 0));
+  CVL_CHECK_ARG(C <= BN_FIN_MAXC);
   CVL_CHECK_ARG((run_mean == nullptr) == (run_var == nullptr));
   const int rpb = bn_rows_per_blk(B, HW, C);
   hipLaunchKernelGGL(bn_apply_kernel<true>, dim3((HW + rpb - 1) / rpb, B), dim3(NT), 0, S_, (const cvl_bf16*)z,
@@ -1114,7 +1118,7 @@ static int bn_backward_impl(const void* dy, const void* y_relu, const float* bn_
                             void* dz, void* g_out, float* dgamma, float* dbeta, float beta_acc, float* conv_dbias,
                             int B, int HW, int C, cvl_stream_t stream) {
   CVL_CHECK_ARG(dy && z && mean_rstd && gamma && workspace && dz && dgamma && dbeta && C % 8 == 0);
-  CVL_CHECK_ARG(B > 0 && HW > 0 && (C / 8 <= NT || (C / 8) % NT == 0));
+  CVL_CHECK_ARG(B > 0 && HW > 0);
   CVL_CHECK_ARG(workspace_bytes >= cvl_bn_backward_workspace_size(B, HW, C));
   const int rpb = bn_bwd_rows_per_blk(B, HW, C);
   const int nchunk = (HW + rpb - 1) / rpb;
@@ -1301,7 +1305,6 @@ extern "C" size_t cvl_bn_stats_workspace_size(int B, int HW, int C) {
 extern "C" int cvl_bn_stats(const void* x, int B, int HW, int C, double* stats, void* workspace,
                             size_t workspace_bytes, cvl_stream_t stream) {
   CVL_CHECK_ARG(x && stats && workspace && C % 8 == 0 && B > 0 && HW > 0);
-  CVL_CHECK_ARG(C / 8 <= NT || (C / 8) % NT == 0);
   CVL_CHECK_ARG(workspace_bytes >= cvl_bn_stats_workspace_size(B, HW, C));
   const int rpb = bn_bwd_rows_per_blk(B, HW, C);
   const int nchunk = (HW + rpb - 1) / rpb;
@@ -1334,7 +1337,7 @@ extern "C" int cvl_bn_backward_grouped(const void* dy, const void* y_relu, const
                                        float dz_beta, float* dgamma, float* dbeta, int B, int HW, int C, int group,
                                        cvl_stream_t stream) {
   CVL_CHECK_ARG(dy && z && mean_rstd && gamma && workspace && dz && dgamma && dbeta && C % 8 == 0 && group > 0);
-  CVL_CHECK_ARG(B > 0 && HW > 0 && (C / 8 <= NT || (C / 8) % NT == 0));
+  CVL_CHECK_ARG(B > 0 && HW > 0);
   CVL_CHECK_ARG(workspace_bytes >= cvl_bn_backward_grouped_workspace_size(B, HW, C));
   const int rpb = bn_bwd_rows_per_blk(B, HW, C);
   const int nchunk = (HW + rpb - 1) / rpb;

@@ -77,6 +77,14 @@ SIGNATURES = {
     "cvl_maxpool2x2_backward": (c_int, [P, P, P, c_int, c_int, c_int, c_int, P]),
     "cvl_upsample_bilinear2x_add": (c_int, [P, P, P, c_int, c_int, c_int, c_int, P]),
     "cvl_upsample_bilinear2x_backward": (c_int, [P, P, c_int, c_int, c_int, c_int, c_float, P]),
+    "cvl_upsample_bilinear2x_sum": (c_int, [P, P, P, c_int, c_int, c_int, c_int, P]),
+    "cvl_reshape_concat": (c_int, [P, c_int, c_int, c_int, P, c_int, P]),
+    "cvl_reshape_concat_backward": (c_int, [P, c_int, c_int, c_int, P, c_int, P]),
+    "cvl_bias_scalar_fold_periodic": (c_int, [P, P, P, c_int, c_int, c_int, P]),
+    "cvl_bias_scalar_unfold_periodic": (c_int, [P, P, P, c_int, c_int, c_int, P]),
+    "cvl_hourglass_v2_assign": (c_int, [P, P, c_int, c_int, c_int, c_int, c_int, P, P]),
+    "cvl_hourglass_v2_loss_workspace_size": (c_size_t, [c_int, c_int]),
+    "cvl_hourglass_v2_loss": (c_int, [P, c_int, P, c_int, c_int, c_int, c_int, c_float, c_float, P, P, c_int, P, P]),
     "cvl_sep_fold_multi": (c_int, [P, P, c_int, P]),
     "cvl_sep_unfold_multi": (c_int, [P, P, c_int, P]),
     "cvl_bias_scalar_fold": (c_int, [P, P, P, c_int, c_int, P]),

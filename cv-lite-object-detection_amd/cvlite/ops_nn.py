@@ -304,13 +304,15 @@ def upsample_bilinear2x_backward(dout, dprev, beta=0.0):
 
 class SepItem(ctypes.Structure):
     _fields_ = [("dw", c_void_p), ("pw", c_void_p), ("weff", c_void_p), ("gweff", c_void_p), ("gdw", c_void_p),
-                ("gpw", c_void_p), ("taps", c_int), ("cin", c_int), ("cout", c_int), ("pad_", c_int)]
+                ("gpw", c_void_p), ("taps", c_int), ("cin", c_int), ("cout", c_int),
+                ("cin_ld", c_int), ("cout_ld", c_int), ("pad_", c_int)]
 
 
 class SepPlan(object):
     """Device tables of cvl_sep_fold_multi / cvl_sep_unfold_multi: every SeparableConv2D's dense
     fold (forward) and gradient unfold (backward) in one launch each.
-    entries: (dw [kh,kw,Cin,1], pw [1,1,Cin,Cout], weff, gweff, gdw, gpw) fp32 device tensors."""
+    entries: (dw [kh,kw,Cin,1], pw [1,1,Cin,Cout], weff, gweff, gdw, gpw) fp32 device tensors;
+    weff / gweff may be channel-padded [kh,kw,Cin_p,Cout_p] (pads stay as they are, i.e. zero)."""
 
     def __init__(self, entries, device):
         items = (SepItem * len(entries))()
@@ -319,8 +321,10 @@ class SepPlan(object):
         for i, (dw, pw, weff, gweff, gdw, gpw) in enumerate(entries):
             kh, kw, cin, _ = dw.shape
             cout = pw.shape[3]
-            assert tuple(weff.shape) == (kh, kw, cin, cout) and gweff.shape == weff.shape
+            assert tuple(weff.shape[:2]) == (kh, kw) and weff.shape[2] >= cin and weff.shape[3] >= cout
+            assert gweff.shape == weff.shape
             it = items[i]
+            it.cin_ld, it.cout_ld = int(weff.shape[2]), int(weff.shape[3])
             it.dw, it.pw, it.weff = dw.data_ptr(), pw.data_ptr(), weff.data_ptr()
             it.gweff, it.gdw, it.gpw = gweff.data_ptr(), gdw.data_ptr(), gpw.data_ptr()
             it.taps, it.cin, it.cout = kh * kw, cin, cout
@@ -343,6 +347,53 @@ def bias_scalar_fold(bias, scalar, b_eff, c0):
 
 def bias_scalar_unfold(g_eff, g_bias, g_scalar, c0):
     _lib.call("cvl_bias_scalar_unfold", ptr(g_eff), ptr(g_bias), ptr(g_scalar), int(g_eff.numel()), int(c0), stream())
+
+
+def bias_scalar_fold_periodic(bias, scalar, b_eff, period, c0):
+    _lib.call("cvl_bias_scalar_fold_periodic", ptr(bias), ptr(scalar), ptr(b_eff), int(bias.numel()), int(period),
+              int(c0), stream())
+
+
+def bias_scalar_unfold_periodic(g_eff, g_bias, g_scalar, period, c0):
+    _lib.call("cvl_bias_scalar_unfold_periodic", ptr(g_eff), ptr(g_bias), ptr(g_scalar), int(g_eff.numel()),
+              int(period), int(c0), stream())
+
+
+def upsample_bilinear2x_sum(a, b, out):
+    """out = UpSampling2D(bilinear)(a + b) (b may be None): one pass, taps summed in fp32."""
+    B, h, w, C = a.shape
+    assert tuple(out.shape) == (B, 2 * h, 2 * w, C) and (b is None or b.shape == a.shape)
+    _lib.call("cvl_upsample_bilinear2x_sum", ptr(a), ptr(b), ptr(out), B, h, w, C, stream())
+
+
+class RcItem(ctypes.Structure):
+    _fields_ = [("src", c_void_p), ("dsrc", c_void_p), ("c", c_int), ("c_ld", c_int), ("hw", c_int),
+                ("beta", ctypes.c_float)]
+
+
+def _rc_items(maps):
+    items = (RcItem * len(maps))()
+    for k, (src, dsrc, c, beta) in enumerate(maps):
+        t = src if src is not None else dsrc
+        it = items[k]
+        it.src = src.data_ptr() if src is not None else None
+        it.dsrc = dsrc.data_ptr() if dsrc is not None else None
+        it.c, it.c_ld, it.hw, it.beta = int(c), int(t.shape[-1]), int(t.shape[1] * t.shape[2]), float(beta)
+    return items
+
+
+def reshape_concat(maps, dst):
+    """maps: [(src [B,h,w,c_ld] bf16, c_real)]; dst [B,S,S,ld] bf16 (tf_hourglass_net.py:307-344)."""
+    B, S0, S1, ld = dst.shape
+    items = _rc_items([(m, None, c, 0.0) for m, c in maps])
+    _lib.call("cvl_reshape_concat", ctypes.cast(items, c_void_p), len(maps), B, S0 * S1, ptr(dst), ld, stream())
+
+
+def reshape_concat_backward(maps, d_dst):
+    """maps: [(dsrc [B,h,w,c_ld] bf16, c_real, beta)]: dsrc = beta*dsrc + gather(d_dst)."""
+    B, S0, S1, ld = d_dst.shape
+    items = _rc_items([(None, d, c, beta) for d, c, beta in maps])
+    _lib.call("cvl_reshape_concat_backward", ctypes.cast(items, c_void_p), len(maps), B, S0 * S1, ptr(d_dst), ld, stream())
 
 
 def adam_clip_update(w, g, m, v, lr_dev, iterations, beta1, beta2, eps, inv_bs, clip, ws=None):

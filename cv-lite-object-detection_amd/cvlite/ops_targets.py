@@ -240,3 +240,40 @@ def centernet_loss(pred, targets, num_classes, cls_scale=2.5, reg_scale=1.0, d_p
               float(cls_scale), float(reg_scale), ptr(losses), ptr(d_pred), int(d_pred.shape[-1]), ptr(ws),
               _lib.stream())
     return losses, d_pred
+
+
+def hourglass_v2_assign(boxes, nbox, raw_dims, img_dims, num_classes, out=None):
+    """CenterNet v2 targets of one batch (train_hourglass_voc.py train() :96-160): boxes [B,n_max,5]
+    f32 = dataset corner rows + label, nbox [B] i32; returns [B, S, S, 4, 5+C] f32, S = img_dims/8."""
+    _lib.require_cuda(boxes, nbox)
+    assert boxes.dtype == torch.float32 and nbox.dtype == torch.int32
+    B, nmax = int(boxes.shape[0]), int(boxes.shape[1])
+    S = int(img_dims) // 8
+    if out is None:
+        out = torch.empty((B, S, S, 4, 5 + num_classes), device=boxes.device, dtype=torch.float32)
+    assert tuple(out.shape) == (B, S, S, 4, 5 + num_classes) and out.is_contiguous()
+    _lib.call("cvl_hourglass_v2_assign", ptr(boxes), ptr(nbox), B, nmax, int(raw_dims), int(img_dims),
+              int(num_classes), ptr(out), _lib.stream())
+    return out
+
+
+def hourglass_v2_loss(pred, targets, num_classes, loss_type="focal", cls_scale=2.5, reg_scale=1.0, d_pred=None,
+                      losses=None, reg_is_prob=False):
+    """CenterNet v2 model_loss fwd+bwd (tf_hourglass_net.py:398-413 in train_step :415-447) off the
+    head conv.  pred [B,P,ld] f32 (channel sc*(5+C)+j, b_focal folded), targets [B,P,4,5+C] f32.
+    reg_is_prob: pred's box channels are the model's sigmoid outputs (model_loss's `outputs`).
+    Returns (losses [B,2] = (cls, reg), d_pred bf16 [B,P,ld_d] of cls_scale*cls + reg_scale*reg)."""
+    _lib.require_cuda(pred, targets)
+    B, P = int(targets.shape[0]), int(targets.shape[1])
+    assert tuple(targets.shape[2:]) == (4, 5 + num_classes) and pred.shape[:2] == (B, P)
+    dev = targets.device
+    if losses is None:
+        losses = torch.empty((B, 2), device=dev, dtype=torch.float32)
+    if d_pred is None:
+        d_pred = torch.empty((B, P, (4 * (5 + num_classes) + 31) // 32 * 32), device=dev, dtype=torch.bfloat16)
+    ws = torch.empty(int(_lib.load().cvl_hourglass_v2_loss_workspace_size(B, P)), device=dev, dtype=torch.uint8)
+    lt = (1 if loss_type == "sigmoid" else 0) | (2 if reg_is_prob else 0)
+    _lib.call("cvl_hourglass_v2_loss", ptr(pred), int(pred.shape[-1]), ptr(targets), B, P, int(num_classes), lt,
+              float(cls_scale), float(reg_scale), ptr(losses), ptr(d_pred), int(d_pred.shape[-1]), ptr(ws),
+              _lib.stream())
+    return losses, d_pred

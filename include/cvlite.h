@@ -385,11 +385,56 @@ int cvl_upsample_bilinear2x_add(const void* prev, const void* other, void* out, 
 int cvl_upsample_bilinear2x_backward(const void* dout, void* dprev, int B, int h, int w, int C, float beta,
                                      cvl_stream_t stream);
 
+/* CenterNet v2 (CenterNet/tf_hourglass_net.py:115-449, n_filters 12 in train_hourglass_voc.py:298-331)
+ * --------------------------------------------------------------------------------------------
+ * out = UpSampling2D(bilinear)(a + b) (:252-305; b nullable): taps of a + b in fp32, one pass. */
+int cvl_upsample_bilinear2x_sum(const void* a, const void* b, void* out, int B, int h, int w, int C,
+                                cvl_stream_t stream);
+/* The "pass through" reshape-concat (:307-344): map k [B][hw][c_ld] bf16 (c real channels, pads
+ * zero) is tf.reshape'd to [B][S2][c*hw/S2] (row-major reinterpretation, Q36) and the maps are
+ * concatenated on channels into dst [B][S2][ld_dst] (columns past the sum zeroed).  c % 4 == 0,
+ * (c*hw/S2) % 4 == 0.  Backward: dsrc = beta*dsrc + the inverse gather of d_dst (pads of dsrc
+ * written zero when beta == 0).  items: HOST array. */
+#define CVL_RC_MAX_ITEMS 16
+typedef struct {
+  const void* src;     /* forward source map */
+  void* dsrc;          /* backward destination (gradient of the map) */
+  int c, c_ld, hw;     /* real channels, channel pitch, pixels per image */
+  float beta;          /* backward accumulate factor */
+} cvl_rc_item;
+int cvl_reshape_concat(const cvl_rc_item* items, int n_items, int B, int S2, void* dst, int ld_dst,
+                       cvl_stream_t stream);
+int cvl_reshape_concat_backward(const cvl_rc_item* items, int n_items, int B, int S2, const void* d_dst,
+                                int ld_dst, cvl_stream_t stream);
+/* b_focal on every scale's class channels (:380-385): b_eff[c] = bias[c] + ((c % period) >= c0 ?
+ * *scalar : 0); unfold: g_bias = g_eff, *g_scalar = sum over those channels (fixed order). */
+int cvl_bias_scalar_fold_periodic(const float* bias, const float* scalar, float* b_eff, int n, int period, int c0,
+                                  cvl_stream_t stream);
+int cvl_bias_scalar_unfold_periodic(const float* g_eff, float* g_bias, float* g_scalar, int n, int period, int c0,
+                                    cvl_stream_t stream);
+/* Targets of train_hourglass_voc.py train() :96-160 for one batch: boxes [B][n_max][5] = the
+ * dataset's corner rows + label (utils.convert_to_xywh :16-27 applied inside), one (raw_dims,
+ * img_dims) per batch (pad_dims = (img - raw) / 2); targets [B][S][S][4][5+C] fp32, S = img/8:
+ * ascending w*h*100, last writer per (cell, scale) sets (y_off, x_off, h_reg, w_reg, 1), class
+ * bits OR'd.  Bit-exact to the reference's float32 arithmetic. */
+int cvl_hourglass_v2_assign(const float* boxes, const int32_t* nbox, int B, int n_max, int raw_dims, int img_dims,
+                            int num_classes, float* targets, cvl_stream_t stream);
+/* model_loss (:398-413) fwd + bwd off the head conv: pred [B*P][ld_pred] fp32 (channel sc*(5+C)+j,
+ * b_focal folded), targets [B*P][4][5+C]; loss_type bit 0: sigmoid cross-entropy (else focal) on
+ * channels 4..4+C; L1 on sigmoid(pred[0..3]) masked by t[4] (bit 1: pred[0..3] are already the
+ * model's sigmoid outputs, as model_loss receives them).  losses [B][2] = (cls, reg); d_pred bf16
+ * [B*P][ld_d] = d(cls_scale*cls + reg_scale*reg)/d(pred).  workspace >= *_workspace_size(B, P). */
+size_t cvl_hourglass_v2_loss_workspace_size(int B, int P);
+int cvl_hourglass_v2_loss(const float* pred, int ld_pred, const float* targets, int B, int P, int num_classes,
+                          int loss_type, float cls_scale, float reg_scale, float* losses, void* d_pred, int ld_d,
+                          void* workspace, cvl_stream_t stream);
+
 /* SeparableConv2D (:110-123, :178-181; depth_multiplier 1) runs as ONE dense conv on the MFMA
  * conv kernels with the folded kernel W[t][ci][co] = D[t][ci] * P[ci][co] (t = kh*kw taps; D =
  * Keras depthwise_kernel [kh][kw][Cin][1], P = pointwise_kernel [1][1][Cin][Cout]).
  * cvl_sep_fold_multi writes weff (fp32 HWIO) for every item; cvl_sep_unfold_multi turns the dense
- * kernel gradient gweff into gdw / gpw.  rows: DEVICE int32 [nrows][2] = (item, ci), one row per
+ * kernel gradient gweff into gdw / gpw (weff / gweff [t][cin_ld][cout_ld] when the pitches are set,
+ * pads untouched).  rows: DEVICE int32 [nrows][2] = (item, ci), one row per
  * input channel of every item.  items: DEVICE array. */
 typedef struct {
   const float* dw;
@@ -398,7 +443,9 @@ typedef struct {
   const float* gweff;
   float* gdw;
   float* gpw;
-  int taps, cin, cout, pad_;
+  int taps, cin, cout;
+  int cin_ld, cout_ld;  /* weff / gweff channel pitches (0 = cin / cout): padded dense kernels */
+  int pad_;
 } cvl_sep_item;
 int cvl_sep_fold_multi(const cvl_sep_item* items, const int32_t* rows, int nrows, cvl_stream_t stream);
 int cvl_sep_unfold_multi(const cvl_sep_item* items, const int32_t* rows, int nrows, cvl_stream_t stream);

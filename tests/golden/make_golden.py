@@ -369,8 +369,89 @@ def work_fcos_center_v1(out_path):
     np.savez_compressed(out_path, **arrays)
 
 
+def work_hourglass_v2(out_path):
+    """CenterNet v2: the target maps the REFERENCE's own train_hourglass_voc.train() builds
+    (:96-160) -- its function definitions are executed (module-level script code is not) with the
+    image reader, the augmentation and tf_hourglass_net.train_step replaced by capturing stubs --
+    and tf_hourglass_net.model_loss (focal and sigmoid) on random heads."""
+    import ast
+    import types
+    tf = _child_setup("CenterNet")
+    import tf_hourglass_net as hg
+    path = os.path.join(REF, "CenterNet", "train_hourglass_voc.py")
+    tree = ast.parse(open(path).read())
+    tree.body = [n for n in tree.body if isinstance(n, (ast.FunctionDef, ast.Import, ast.ImportFrom))]
+    ns = {"__name__": "train_hourglass_voc_defs"}
+    exec(compile(tree, path, "exec"), ns)
+    captured = []
+
+    def train_step(model, sub_batch_sz, images, bboxes, masks, optimizer, learning_rate=None):
+        captured.append((np.asarray(bboxes.numpy(), np.float32), float(learning_rate)))
+        return (0.0, 0.0)
+    ns["_parse_image"] = lambda f, img_rows, img_cols: np.zeros((img_rows, img_cols, 3), np.float32)
+    ns["image_augment"] = lambda img, bbox, p=0.5: (img, bbox)
+    ns["tf_obj_detector"] = types.SimpleNamespace(train_step=train_step)
+    tf.image = types.SimpleNamespace(pad_to_bounding_box=lambda x, a, b, h, w: np.zeros((h, w, 3), np.float32))
+    rng = np.random.default_rng(777)
+    C, n_data, batch, steps = 20, 40, 4, 6
+    data = []
+    for i in range(n_data):
+        n = int(rng.integers(1, 25 if i % 3 else 60))
+        cen = rng.uniform(0.02, 0.98, (n, 2))
+        if i % 5 == 0:                       # clustered centres: shared cells / scales
+            cen = 0.5 + rng.normal(0, 0.02, (n, 2))
+        side = np.exp(rng.uniform(np.log(0.01), np.log(1.0), (n, 2)))
+        lo, hi = cen - side / 2, cen + side / 2
+        bbox = np.concatenate([lo, hi], 1).astype(np.float32)
+        if i % 7 == 3:
+            bbox[0, [0, 2]] = bbox[0, [2, 0]]   # negative width: skipped by the builder
+        data.append({"image": "img_%d.jpg" % i, "objects": {"bbox": bbox,
+                                                            "label": rng.integers(0, C, n).astype(np.int64)}})
+    ckpt = types.SimpleNamespace(step=types.SimpleNamespace(assign_add=lambda v: None))
+    np.random.seed(4321)
+    ns["train"](None, C, 2, batch, data, [], 0, steps, None, ckpt, None, {}, init_lr=1e-3, min_lr=1e-5,
+                decay=0.99, display_step=10 ** 9, step_cool=10 ** 9)
+    np.random.seed(4321)
+    arrays = {"C": np.int32(C)}
+    for st in range(steps):
+        sample = np.random.choice(n_data, size=batch, replace=False)
+        rnd = np.random.uniform(low=0.6, high=1.3)
+        bbox, lr = captured[st]
+        raw = int(rnd * 320)
+        img = bbox.shape[1] * 8
+        arrays["step_%d_raw_img" % st] = np.array([raw, img], np.int32)
+        arrays["step_%d_lr" % st] = np.float64(lr)
+        nmax = max(len(data[k]["objects"]["label"]) for k in sample)
+        boxes = np.zeros((batch, nmax, 5), np.float32)
+        nbox = np.zeros(batch, np.int32)
+        for j, k in enumerate(sample):
+            o = data[k]["objects"]
+            boxes[j, :len(o["label"]), :4] = o["bbox"]
+            boxes[j, :len(o["label"]), 4] = o["label"]
+            nbox[j] = len(o["label"])
+        arrays["step_%d_boxes" % st] = boxes
+        arrays["step_%d_nbox" % st] = nbox
+        arrays["step_%d_targets" % st] = bbox
+    # model_loss on random heads of two captured batches
+    for st in (0, 3):                       # 2 images, a 16x16 window around the map centre
+        S = arrays["step_%d_targets" % st].shape[1]
+        bbox = np.ascontiguousarray(arrays["step_%d_targets" % st][:2, S // 2 - 8:S // 2 + 8, S // 2 - 8:S // 2 + 8])
+        arrays["loss_%d_targets" % st] = bbox
+        raw = rng.normal(0.0, 1.5, bbox.shape).astype(np.float32)
+        bfocal = np.float32(np.log((1.0 - 0.99) / 0.99))
+        outs = np.concatenate([np.asarray(tf.nn.sigmoid(tf.constant(raw[..., :4])).numpy(), np.float32),
+                               raw[..., 4:] + bfocal], -1)
+        arrays["loss_%d_raw" % st] = raw
+        arrays["loss_%d_bfocal" % st] = np.float32(bfocal)
+        for lt in ("focal", "sigmoid"):
+            cls_l, reg_l = hg.model_loss(tf.constant(bbox), tf.constant(bbox[..., 4]), tf.constant(outs),
+                                         loss_type=lt)
+            arrays["loss_%d_%s" % (st, lt)] = np.array([float(cls_l), float(reg_l)], np.float64)
+    np.savez_compressed(out_path, **arrays)
+
+
 WORKERS = {"fcos": work_fcos, "retinanet": work_retina, "centernet": work_centernet,
-           "fcos_center_v1": work_fcos_center_v1,
+           "fcos_center_v1": work_fcos_center_v1, "hourglass_v2": work_hourglass_v2,
            "centernet_softnms": work_centernet_softnms,
            "retina_decode": work_retina_decode,
            "fcos_center": work_fcos_center}

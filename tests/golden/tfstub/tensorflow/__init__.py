@@ -191,6 +191,7 @@ def reduce_sum(x, axis=None):
     if isinstance(x, (list, tuple)):
         x = stack(x)
     a = _arr(_t(x))
+    axis = tuple(axis) if isinstance(axis, list) else axis
     return Tensor(_np.sum(a, axis=axis).astype(a.dtype))
 
 
@@ -326,6 +327,13 @@ class _NN(object):
     def relu(x):
         a = _arr(_t(x))
         return Tensor(_np.maximum(a, 0).astype(a.dtype))
+
+    @staticmethod
+    def sigmoid_cross_entropy_with_logits(labels=None, logits=None):
+        # TF's stable form: max(x, 0) - x * z + log(1 + exp(-|x|)), in the logits' dtype
+        x = _arr(_t(logits))
+        z = _arr(_t(labels)).astype(x.dtype)
+        return Tensor((_np.maximum(x, 0) - x * z + _np.log1p(_np.exp(-_np.abs(x)))).astype(x.dtype))
 
 
 nn = _NN()

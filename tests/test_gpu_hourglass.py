@@ -93,11 +93,13 @@ def test_sep_fold_unfold():
         assert rel(gdw, a) < 1e-5 and rel(gpw, b) < 1e-5
 
 
-@pytest.mark.parametrize("group", [1, 2, 3])
-def test_bn_grouped_stats_and_backward(group):
+@pytest.mark.parametrize("group,C", [(1, 64), (2, 64), (3, 64), (2, 2272)])
+def test_bn_grouped_stats_and_backward(group, C):
+    """C = 2272: more than 256 8-channel groups and not a multiple of them (the CenterNet v2
+    concat, tf_hourglass_net.py:337-344) -- the uniform channel-group loop."""
     from cvlite import ops_nn as nn
     g = torch.Generator().manual_seed(3)
-    B, H, W, C = 5, 12, 10, 64
+    B, H, W = 5, 12, 10
     x = bf(torch.randn(B, H, W, C, generator=g) * 2 + 0.5).cuda()
     gamma = (torch.rand(C, generator=g) + 0.5).cuda()
     beta = torch.randn(C, generator=g).cuda()

@@ -1,0 +1,269 @@
+"""CenterNet v2 (CenterNet/tf_hourglass_net.py + train_hourglass_voc.py) on the GPU.
+
+  * targets: cvl_hourglass_v2_assign bit-exact vs the maps the reference's own train() built
+    (tests/golden/golden_hourglass_v2.npz), plus a larger batch vs the oracle restatement;
+  * loss: cvl_hourglass_v2_loss vs the reference's model_loss outputs (rtol 2e-5, fp32 kernel vs
+    fp32 TF ops), in the training layout (logits, b_focal folded) and the model_loss layout
+    (sigmoid'd outputs); gradient vs float64 autograd (rtol 1e-2 / bf16 output rounding);
+  * reshape-concat (a permutation: exact) and its adjoint, up-sampling of a sum (1 bf16 ulp of the
+    fp32 reference on the same operands);
+  * whole graph (64x64, B = 4, BN sub-batches of 2) vs the torch restatement storing bf16 where the
+    GPU path does (oracle/hourglass_v2_ref.py), rel-L2 bounds as test_gpu_hourglass.py;
+  * train steps through the captured graph: targets, losses vs the oracle, Adam update direction.
+"""
+import math
+
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+from oracle import hourglass_v2_ref as hv
+
+pytestmark = pytest.mark.gpu
+
+
+def rel(a, b):
+    a, b = a.double().cpu(), b.double().cpu()
+    return float((a - b).norm() / max(float(b.norm()), 1e-30))
+
+
+def test_hourglass_v2_assign_vs_reference(golden):
+    from cvlite import ops_targets as ot
+    d = golden("hourglass_v2")
+    C = int(d["C"])
+    for st in range(6):
+        raw, img = (int(v) for v in d["step_%d_raw_img" % st])
+        tg = ot.hourglass_v2_assign(torch.from_numpy(d["step_%d_boxes" % st]).cuda(),
+                                    torch.from_numpy(d["step_%d_nbox" % st]).cuda(), raw, img, C)
+        np.testing.assert_array_equal(tg.cpu().numpy(), d["step_%d_targets" % st])
+
+
+def test_hourglass_v2_assign_batched_vs_oracle():
+    from cvlite import ops_targets as ot
+    rng = np.random.default_rng(5)
+    B, C, nmax = 8, 20, 120
+    for raw, img in ((416, 448), (192, 192), (300, 320)):
+        boxes = np.zeros((B, nmax, 5), np.float32)
+        nbox = rng.integers(0, nmax + 1, B).astype(np.int32)
+        nbox[1] = 0
+        for b in range(B):
+            n = nbox[b]
+            cen = rng.uniform(-0.05, 1.05, (n, 2))
+            side = np.exp(rng.uniform(np.log(0.005), np.log(1.2), (n, 2)))
+            boxes[b, :n, :2] = cen - side / 2
+            boxes[b, :n, 2:4] = cen + side / 2
+            boxes[b, :n, 4] = rng.integers(0, C, n)
+            if n > 2:
+                boxes[b, 0, [0, 2]] = boxes[b, 0, [2, 0]]          # negative width: skipped
+        tg = ot.hourglass_v2_assign(torch.from_numpy(boxes).cuda(), torch.from_numpy(nbox).cuda(), raw, img, C)
+        np.testing.assert_array_equal(tg.cpu().numpy(), hv.format_data(boxes, nbox, raw, img, C))
+
+
+@pytest.mark.parametrize("loss_type", ["focal", "sigmoid"])
+def test_hourglass_v2_loss_vs_reference_and_grad(golden, loss_type):
+    from cvlite import ops_targets as ot
+    from cvlite import tf_hourglass_net as thn
+    d = golden("hourglass_v2")
+    C = int(d["C"])
+    R = 5 + C
+    for st in (0, 3):
+        t = d["loss_%d_targets" % st]
+        raw = d["loss_%d_raw" % st]
+        bf = float(d["loss_%d_bfocal" % st])
+        B, S = t.shape[0], t.shape[1]
+        P = S * S
+        ld = (4 * R + 31) // 32 * 32
+        pred = np.zeros((B, P, ld), np.float32)
+        x = raw.copy()
+        x[..., 4:] += np.float32(bf)                                # b_focal folded into the head bias
+        pred[..., :4 * R] = x.reshape(B, P, 4 * R)
+        losses, dp = ot.hourglass_v2_loss(torch.from_numpy(pred).cuda(), torch.from_numpy(t).cuda().view(B, P, 4, R),
+                                          C, loss_type, cls_scale=2.5, reg_scale=1.0)
+        got = losses.double().sum(0).cpu().numpy()
+        np.testing.assert_allclose(got, d["loss_%d_%s" % (st, loss_type)], rtol=2e-5)
+        # model_loss mirror on the model's outputs (sigmoid'd box channels)
+        outs = np.concatenate([1.0 / (1.0 + np.exp(-raw[..., :4].astype(np.float64))), x[..., 4:]], -1)
+        got2 = thn.model_loss(t.astype(np.float32), t[..., 4], outs.astype(np.float32), loss_type=loss_type)
+        np.testing.assert_allclose(got2, d["loss_%d_%s" % (st, loss_type)], rtol=2e-5)
+        # gradient vs float64 autograd
+        xt = torch.from_numpy(raw).double().requires_grad_()
+        lc, lr = hv.model_loss_torch(torch.from_numpy(t).double(), xt, torch.tensor(bf, dtype=torch.float64),
+                                     loss_type)
+        (2.5 * lc + 1.0 * lr).backward()
+        g = dp.float().cpu()[..., :4 * R].reshape(B, S, S, 4, R).double()
+        ref = xt.grad
+        assert torch.allclose(g, ref, rtol=1e-2, atol=1e-6), float((g - ref).abs().max())
+        assert not dp[..., 4 * R:].any()
+
+
+def test_reshape_concat_and_up_sum():
+    from cvlite import ops_nn as nn
+    g = torch.Generator().manual_seed(3)
+    B, S = 2, 4
+    # (h, w, c_real, c_ld): the v2 layout at a 32x32 input with nf = 4 (pads zero)
+    specs = [(16, 16, 8, 32), (8, 8, 16, 32), (4, 4, 32, 32), (2, 2, 64, 64), (1, 1, 128, 128), (32, 32, 4, 32)]
+    maps, real = [], []
+    for h, w, c, cl in specs:
+        t = torch.zeros(B, h, w, cl, dtype=torch.bfloat16)
+        t[..., :c] = torch.randn(B, h, w, c, generator=g).to(torch.bfloat16)
+        maps.append(t.cuda())
+        real.append(t[..., :c])
+    ctot = sum(c * h * w // (S * S) for h, w, c, _ in specs)
+    ld = (ctot + 31) // 32 * 32
+    dst = torch.full((B, S, S, ld), 7.0, dtype=torch.bfloat16, device="cuda")
+    nn.reshape_concat([(m, c) for m, (_, _, c, _) in zip(maps, specs)], dst)
+    ref = torch.cat([r.reshape(B, S, S, -1) for r in real], -1)
+    assert torch.equal(dst[..., :ctot].cpu(), ref) and not dst[..., ctot:].any()
+    # adjoint: exact inverse permutation, beta accumulate, pads zero
+    dd = torch.randn(B, S, S, ld, generator=g).to(torch.bfloat16).cuda()
+    grads = [torch.full_like(m, 3.0) for m in maps]
+    betas = [0.0, 1.0, 0.0, 1.0, 0.0, 0.0]
+    nn.reshape_concat_backward([(gr, c, bt) for gr, (_, _, c, _), bt in zip(grads, specs, betas)], dd)
+    o = 0
+    for gr, (h, w, c, cl), bt in zip(grads, specs, betas):
+        wk = c * h * w // (S * S)
+        exp = dd[..., o:o + wk].cpu().reshape(B, h, w, c).float() + (3.0 if bt else 0.0)
+        assert torch.equal(gr[..., :c].cpu().float(), exp.to(torch.bfloat16).float())
+        if bt == 0.0:
+            assert not gr[..., c:].any()
+        o += wk
+    # up-sampling of a sum
+    for (h, w, C) in [(4, 4, 64), (1, 1, 32), (3, 5, 16)]:
+        a = torch.randn(B, h, w, C, generator=g).to(torch.bfloat16).cuda()
+        b = torch.randn(B, h, w, C, generator=g).to(torch.bfloat16).cuda()
+        out = torch.empty((B, 2 * h, 2 * w, C), dtype=torch.bfloat16, device="cuda")
+        nn.upsample_bilinear2x_sum(a, b, out)
+        s = (a.double() + b.double()).permute(0, 3, 1, 2)
+        up = F.interpolate(s, scale_factor=2, mode="bilinear", align_corners=False).permute(0, 2, 3, 1)
+        err = (out.double() - up).abs() / up.abs().clamp(min=1e-3)
+        assert float(err.max()) <= 2 ** -7, float(err.max())
+        nn.upsample_bilinear2x_sum(a, None, out)
+        up = F.interpolate(a.double().permute(0, 3, 1, 2), scale_factor=2, mode="bilinear",
+                           align_corners=False).permute(0, 2, 3, 1)
+        err = (out.double() - up).abs() / up.abs().clamp(min=1e-3)
+        assert float(err.max()) <= 2 ** -7, float(err.max())
+
+
+def _targets(rng, B, S, C, n=6):
+    t = np.zeros((B, S, S, 4, 5 + C), np.float32)
+    for b in range(B):
+        for _ in range(n):
+            i, j, s = rng.integers(0, S, 2).tolist() + [int(rng.integers(0, 4))]
+            t[b, i, j, s, :4] = rng.uniform(0, 1, 4)
+            t[b, i, j, s, 4] = 1.0
+            t[b, i, j, s, 5 + int(rng.integers(0, C))] = 1.0
+    return torch.from_numpy(t)
+
+
+def _small_net(C, seed):
+    from cvlite.hourglass_v2_net import HourglassV2Net
+    return HourglassV2Net(C, n_filters=12, n_features=64, seed=seed)
+
+
+def test_hourglass_v2_forward_loss_backward_vs_oracle():
+    """Whole graph, B = 4 images of 64x64 (S = 8; the six stride-2 stages reach 1x1) in BN
+    sub-batches of 2, vs the oracle storing activations / weights / gradients in bf16 at the GPU
+    path's points; every channel-padded map's pads stay zero."""
+    from cvlite import ops_targets as ot
+    from oracle.model_ref import emulate_bf16
+    C, B, D, G = 20, 4, 64, 2
+    net = _small_net(C, seed=1)
+    params = net.real_params()
+    gx = torch.Generator().manual_seed(7)
+    x = torch.rand(B, D, D, 3, generator=gx) * 2 - 1
+    S = D // 8
+    tg = _targets(np.random.default_rng(2), B, S, C)
+    out = net.forward(x.cuda(), group=G)
+    v = net._saved[0]
+    for k in ("blk0", "cnn1", "blk1", "in2", "blk2", "dec5", "dec6", "feats"):
+        rc = {"blk0": 12, "cnn1": 12, "blk1": 24, "in2": 24, "blk2": 48, "dec5": 24, "dec6": 12,
+              "feats": net.feat_c}[k]
+        assert not v[k][..., rc:].any(), k
+    d_out = torch.zeros((B, S, S, net.cout_ld), dtype=torch.bfloat16, device="cuda")
+    R = 5 + C
+    losses, _ = ot.hourglass_v2_loss(out.view(B, S * S, -1), tg.cuda().view(B, S * S, 4, R), C, "focal",
+                                     d_pred=d_out.view(B, S * S, -1))
+    net.backward(d_out)
+    torch.cuda.synchronize()
+    with emulate_bf16():
+        c16, r16, g16, o16 = hv.loss_and_grads(params, x, tg, C, G)
+    c32, r32, g32, o32 = hv.loss_and_grads(params, x, tg, C, G)
+    logits = out[..., :4 * R].reshape(B, S, S, 4, R).cpu().clone()
+    logits[..., 4:] -= float(params["b_focal"])
+    e_out, e_own = rel(logits, o16), rel(o16, o32)
+    print("logits vs bf16-oracle %.4f | bf16-oracle vs fp32 %.4f" % (e_out, e_own))
+    # ~45 conv+BN layers: bf16 storage alone moves the oracle by e_own; summation-order differences
+    # (one bf16 rounding each) are amplified the same way, so bound by a fraction of it
+    assert e_out < max(3e-2, 0.6 * e_own)
+    lc, lr = float(losses[:, 0].sum()), float(losses[:, 1].sum())
+    assert abs(lc - c16) / abs(c16) < 3e-2 and abs(lr - r16) / abs(r16) < 5e-2
+
+    def overall(ga, gb):
+        n = d = 0.0
+        for k in gb:
+            n += float((ga[k].double() - gb[k].double()).norm() ** 2)
+            d += float(gb[k].double().norm() ** 2)
+        return math.sqrt(n / d)
+    gpu = net.real_params(grads=True)
+    e16, e32, own = overall(gpu, g16), overall(gpu, g32), overall(g16, g32)
+    print("grad rel-L2: gpu vs bf16-oracle %.4f, gpu vs fp32 %.4f, bf16-oracle vs fp32 %.4f" % (e16, e32, own))
+    assert e32 < 1.5 * own + 0.03 and e16 < 1.5 * own + 0.03
+    tot = math.sqrt(sum(float(g.double().norm() ** 2) for g in g32.values()))
+    bad = []
+    for k, gref in g32.items():
+        if float(gref.norm()) < 1e-3 * tot:
+            continue
+        eg, eo = rel(gpu[k], gref), rel(g16[k], gref)
+        if eg > 2.0 * eo + 0.1:
+            bad.append((k, round(eg, 3), round(eo, 3)))
+    assert not bad, bad
+    # pads of the padded parameters receive exactly zero gradient
+    full = net.store
+    for blk in net.blocks():
+        units = [(r.bn, r.sep) for r in blk.reps] if hasattr(blk, "reps") else [(blk.bn, blk.sep)]
+        for bn, sep in units:
+            assert not full.g(bn.gname)[sep.cin:].any() and not full.g(sep.bname)[sep.cout:].any()
+
+
+def test_hourglass_v2_train_steps_vs_oracle():
+    """Two device train steps through the captured graph (targets from boxes on the GPU, BN
+    sub-batches of 2, Adam, fold + re-pack) vs the oracle's train_step on the same targets."""
+    from cvlite.train_hourglass_v2 import HourglassV2Trainer
+    from oracle.model_ref import emulate_bf16
+    C, B, D, G = 20, 4, 64, 2
+    net = _small_net(C, seed=2)
+    p0 = net.real_params()
+    tr = HourglassV2Trainer(net, B, D, sub_batch_sz=G, n_max=8, use_graph=True)
+    rng = np.random.default_rng(9)
+    boxes = np.zeros((B, 8, 5), np.float32)
+    nbox = np.full(B, 6, np.int32)
+    for b in range(B):
+        cen = rng.uniform(0.1, 0.9, (6, 2))
+        side = np.exp(rng.uniform(np.log(0.05), np.log(0.9), (6, 2)))
+        boxes[b, :6, :2], boxes[b, :6, 2:4] = cen - side / 2, cen + side / 2
+        boxes[b, :6, 4] = rng.integers(0, C, 6)
+    imgs = torch.rand(B, D, D, 3, generator=torch.Generator().manual_seed(4)) * 2 - 1
+    P = {k: v.clone() for k, v in p0.items()}
+    M = {k: torch.zeros_like(v) for k, v in P.items()}
+    V = {k: torch.zeros_like(v) for k, v in P.items()}
+    for it in range(2):
+        tr.load_batch(imgs.cuda(), torch.from_numpy(boxes).cuda(), torch.from_numpy(nbox).cuda(), 56)
+        tg = torch.from_numpy(hv.format_data(boxes, nbox, 56, D, C))
+        assert torch.equal(tr.targets.cpu(), tg)
+        losses = tr.step().double().sum(0).cpu()
+        with emulate_bf16():
+            c, r = hv.train_step_reference(P, M, V, it, imgs, tg, C, G)
+        print("step %d: gpu cls %.4f reg %.4f | oracle %.4f %.4f" % (it, losses[0] / B, losses[1] / B, c, r))
+        assert abs(float(losses[0]) / B - c) / abs(c) < 3e-2
+        assert abs(float(losses[1]) / B - r) / max(abs(r), 1e-6) < 5e-2
+    agree = tot = 0
+    now = net.real_params()
+    for k in P:
+        dg = now[k].double() - p0[k].double()
+        dr = P[k].double() - p0[k].double()
+        agree += int(((dg > 0) == (dr > 0)).sum())
+        tot += dg.numel()
+    print("update sign agreement %.4f" % (agree / tot))
+    assert agree / tot > 0.8
+    assert torch.isfinite(net.store.flat).all()

@@ -195,3 +195,24 @@ def test_fcos_center_v1_format_data_and_losses(golden):
                                        d["loss_%d_center_focal" % i], rtol=1e-5)
     assert n_loss == 3
     np.testing.assert_array_equal(fcos_ref.center_v1_prediction_to_corners(d["p2c_in"], 320.0, 16), d["p2c_out"])
+
+
+def test_hourglass_v2_targets_and_loss(golden):
+    """CenterNet v2: the restated target builder vs the maps the reference's own
+    train_hourglass_voc.train() built (bit-exact), and model_loss (focal / sigmoid) vs the
+    reference's tf_hourglass_net.model_loss (rtol 1e-5: fp32 TF ops vs the float64 restatement)."""
+    from oracle import hourglass_v2_ref as hv
+    d = golden("hourglass_v2")
+    C = int(d["C"])
+    n_rows = 0
+    for st in range(6):
+        raw, img = (int(v) for v in d["step_%d_raw_img" % st])
+        got = hv.format_data(d["step_%d_boxes" % st], d["step_%d_nbox" % st], raw, img, C)
+        np.testing.assert_array_equal(got, d["step_%d_targets" % st])
+        n_rows += int((got[..., 4] > 0).sum())
+    assert n_rows > 200
+    for st in (0, 3):
+        t = d["loss_%d_targets" % st]
+        for lt in ("focal", "sigmoid"):
+            np.testing.assert_allclose(hv.model_loss(t, d["loss_%d_raw" % st], d["loss_%d_bfocal" % st], lt),
+                                       d["loss_%d_%s" % (st, lt)], rtol=1e-5)
