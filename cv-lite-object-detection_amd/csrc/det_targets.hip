@@ -7,6 +7,7 @@
 //   cvl_det_loss         tf_centernet_hourglass.py:458-505 / retinanet_module.py:367-426
 //   cvl_nms              tf_centernet_hourglass.py:22-85 (method 'nms')
 //   cvl_hourglass_v2_*   CenterNet/train_hourglass_voc.py:96-160, tf_hourglass_net.py:398-447
+//   cvl_centernet_s8_*   CenterNet/tf_centernet_resnet_s8.py:243-385
 // Index/target kernels follow the reference's fp32 operation sequences exactly (this file is
 // compiled with -ffp-contract=off) and keep float64 where the reference computes in float64.
 #include "cvl_common.h"
@@ -587,6 +588,158 @@ __global__ void __launch_bounds__(NT) hg2_loss_kernel(Hg2LossArgs a) {
 }
 
 // ------------------------------------------------------------------------------------------------
+// CenterNet ResNet stride-8 multi-scale targets: CenterNet/tf_centernet_resnet_s8.py format_data
+// (:243-330) as train_centernet_crowdhuman.py (:64-104) calls it: gt_labels rows (y, x, h, w, cls)
+// normalised, concatenated with the int64 class column, hence float64 arithmetic throughout
+// (inputs are the float32 box values); img_dim [B][2] = the resized (raw) size, img_pad the padded
+// size.  Output [B][pad_w/stride][pad_h/stride][n_scales][4+C] (h_max from img_pad[1], w_max from
+// img_pad[0], kept): ascending area, each box writes (y_off, x_off, h/scale, w/scale) at its
+// centre cell and first scale with max(h, w) < box_scales[sc], ORs its class bit.  Boxes with no
+// such scale (a ValueError there) or a centre off the map are skipped.
+// ------------------------------------------------------------------------------------------------
+constexpr int kMaxScales = 8;
+
+struct S8Args {
+  const float* boxes;
+  const int32_t* nbox;
+  const float* img_dim;
+  float* out;
+  int n_max, C, hm, wm, ns, stride;
+  double pad_h, pad_w;
+  double scales[kMaxScales];
+};
+
+__global__ void __launch_bounds__(NT) s8_assign_kernel(S8Args a) {
+  const int b = blockIdx.y;
+  const int tid = threadIdx.x;
+  __shared__ int order[kMaxBox];
+  __shared__ double dar[kMaxBox];
+  __shared__ int key[kMaxBox];
+  __shared__ int cls[kMaxBox];
+  __shared__ float val[kMaxBox][4];
+  int n = a.nbox[b];
+  n = n < 0 ? 0 : (n > a.n_max ? a.n_max : n);
+  const double D0 = (double)a.img_dim[2 * b], D1 = (double)a.img_dim[2 * b + 1];
+  const float* bx = a.boxes + (size_t)b * a.n_max * 5;
+  for (int i = tid; i < n; i += NT) dar[i] = ((double)bx[i * 5 + 2] * D0) * ((double)bx[i * 5 + 3] * D1);
+  __syncthreads();
+  for (int i = tid; i < n; i += NT) {
+    int rk = 0;
+    if (n > 1)
+      for (int j = 0; j < n; ++j) rk += (dar[j] < dar[i]) || (dar[j] == dar[i] && j < i);
+    else
+      rk = i;
+    order[rk] = i;
+  }
+  __syncthreads();
+  const double st = (double)a.stride;
+  const double py = (double)(int)((a.pad_w - D1) / 2.0), px = (double)(int)((a.pad_h - D0) / 2.0);
+  for (int k = tid; k < n; k += NT) {
+    const float* r = bx + order[k] * 5;
+    const double y = r[0], x = r[1], h = r[2], w = r[3];
+    const double c0 = (y - 0.5 * h) * D0, c1 = (x - 0.5 * w) * D1;
+    const double c2 = (y + 0.5 * h) * D0, c3 = (x + 0.5 * w) * D1;
+    const double bh = c2 - c0, bw = c3 - c1;
+    const double bd = bh > bw ? bh : bw;                               // max(box_h, box_w)
+    int id = -1;
+    for (int s = 0; s < a.ns; ++s)
+      if (bd < a.scales[s]) { id = s; break; }
+    int kk = -1;
+    if (id >= 0) {
+      const double ryc = (c0 + c2) / 2.0, rxc = (c1 + c3) / 2.0;
+      int yc = (int)((py + ryc) / st), xc = (int)((px + rxc) / st);
+      const double yo = (py + ryc - (double)yc * st), xo = (px + rxc - (double)xc * st);
+      val[k][0] = (float)(yo / st); val[k][1] = (float)(xo / st);
+      val[k][2] = (float)(bh / a.scales[id]); val[k][3] = (float)(bw / a.scales[id]);
+      if (yc < 0) yc += a.hm;
+      if (xc < 0) xc += a.wm;
+      if (yc >= 0 && yc < a.hm && xc >= 0 && xc < a.wm) kk = (yc * a.wm + xc) * a.ns + id;
+    }
+    key[k] = kk;
+    cls[k] = (int)r[4];
+  }
+  __syncthreads();
+  const int R = 4 + a.C;
+  const int rows = a.hm * a.wm * a.ns;
+  for (int row = blockIdx.x * NT + tid; row < rows; row += gridDim.x * NT) {
+    float v[4] = {0.f, 0.f, 0.f, 0.f};
+    uint32_t bits[kWords];
+#pragma unroll
+    for (int k = 0; k < kWords; ++k) bits[k] = 0u;
+    for (int k = 0; k < n; ++k) {
+      if (key[k] != row) continue;
+      v[0] = val[k][0]; v[1] = val[k][1]; v[2] = val[k][2]; v[3] = val[k][3];
+      if (cls[k] >= 0 && cls[k] < a.C) bits[cls[k] >> 5] |= 1u << (cls[k] & 31);
+    }
+    float* o = a.out + ((size_t)b * rows + row) * R;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) o[k] = v[k];
+    for (int c = 0; c < a.C; ++c) o[4 + c] = ((bits[c >> 5] >> (c & 31)) & 1u) ? 1.0f : 0.0f;
+  }
+}
+
+// tf_centernet_resnet_s8.model_loss (:368-385) in train_step (:387-444) off the two head convs:
+// reg [B*P][ld_reg] fp32 holds the n_scales x 4 raw box logits of a cell (scale-major), cls
+// [B*P][ld_cls] the n_scales x C class logits; targets [B*P][n_scales][4+C].  Per (cell, scale):
+// focal on the classes, smooth-L1 (Q8) of sigmoid(box) masked by max(class target) > 0.
+// Writes bf16 gradients of cls_scale*cls + reg_scale*reg into d_reg / d_cls (pads zeroed).
+struct S8LossArgs {
+  const float* reg;
+  const float* cls;
+  const float* tgt;
+  double* partial;
+  cvl_bf16* dreg;
+  cvl_bf16* dcls;
+  int ld_reg, ld_cls, ld_dreg, ld_dcls, P, C, ns, tiles;
+  float cls_scale, reg_scale;
+};
+
+__global__ void __launch_bounds__(NT) s8_loss_kernel(S8LossArgs a) {
+  const int b = blockIdx.y;
+  const int row = blockIdx.x * NT + threadIdx.x;              // (cell, scale)
+  const int R = 4 + a.C;
+  float s_cls = 0.f, s_reg = 0.f;
+  if (row < a.P * a.ns) {
+    const int p = row / a.ns, sc = row - (row / a.ns) * a.ns;
+    const size_t cell = (size_t)b * a.P + p;
+    const float* t = a.tgt + ((size_t)b * a.P * a.ns + row) * R;
+    const float* xr = a.reg + cell * a.ld_reg + sc * 4;
+    const float* xc = a.cls + cell * a.ld_cls + sc * a.C;
+    cvl_bf16* dr = a.dreg + cell * a.ld_dreg + sc * 4;
+    cvl_bf16* dc = a.dcls + cell * a.ld_dcls + sc * a.C;
+    float tmax = 0.f;
+    for (int c = 0; c < a.C; ++c) {
+      const float y = t[4 + c];
+      tmax = fmaxf(tmax, y);
+      float g;
+      s_cls += focal_elem(y, xc[c], &g);
+      dc[c] = f32_to_bf16(g * a.cls_scale);
+    }
+    const float mask = tmax > 0.f ? 1.0f : 0.0f;
+    for (int j = 0; j < 4; ++j) {
+      const float sg = 1.0f / (1.0f + expf(-xr[j]));
+      float g;
+      s_reg += mask * sl1_elem(t[j], sg, &g);
+      dr[j] = f32_to_bf16(mask * g * (sg * (1.0f - sg)) * a.reg_scale);
+    }
+    if (sc == a.ns - 1) {
+      for (int c = a.ns * 4; c < a.ld_dreg; ++c) a.dreg[cell * a.ld_dreg + c] = 0;
+      for (int c = a.ns * a.C; c < a.ld_dcls; ++c) a.dcls[cell * a.ld_dcls + c] = 0;
+    }
+  }
+  __shared__ double red[2][NT / 64];
+  double v0 = warp_sum_d((double)s_cls), v1 = warp_sum_d((double)s_reg);
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  if (lane == 0) { red[0][w] = v0; red[1][w] = v1; }
+  __syncthreads();
+  if (threadIdx.x < 2) {
+    double s = 0.0;
+    for (int k = 0; k < NT / 64; ++k) s += red[threadIdx.x][k];
+    a.partial[((size_t)b * a.tiles + blockIdx.x) * 2 + threadIdx.x] = s;
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
 // CenterNet detection decode (tf_centernet_hourglass.py:576-650, the part before `nms`): corners
 // from prediction_to_corners (:355-377: fp32 grid +- ltrb, then stride * in float64), sigmoid class
 // probabilities (fp32; evaluated in float64 and rounded), per-cell max / first argmax, threshold,
@@ -1120,6 +1273,46 @@ extern "C" int cvl_hourglass_v2_loss(const float* pred, int ld_pred, const float
   a.ld_pred = ld_pred; a.ld_d = ld_d; a.P = P; a.C = num_classes; a.tiles = (4 * P + NT - 1) / NT;
   a.sce = loss_type; a.cls_scale = cls_scale; a.reg_scale = reg_scale;
   hipLaunchKernelGGL(hg2_loss_kernel, dim3(a.tiles, B), dim3(NT), 0, S_, a);
+  hipLaunchKernelGGL(det_loss_finalize, dim3(B), dim3(FIN_T), 0, S_, (const double*)workspace, losses, a.tiles);
+  return cvl_launch_status();
+}
+
+extern "C" int cvl_centernet_s8_assign(const float* boxes, const int32_t* nbox, const float* img_dim, int B,
+                                       int n_max, int pad_h, int pad_w, int num_classes, const float* box_scales,
+                                       int n_scales, int stride, float* targets, cvl_stream_t stream) {
+  CVL_CHECK_ARG(boxes && nbox && img_dim && targets && box_scales && B > 0 && n_max > 0 && n_max <= kMaxBox);
+  CVL_CHECK_ARG(num_classes > 0 && num_classes <= 32 * kWords && stride > 0 && n_scales > 0 &&
+                n_scales <= kMaxScales);
+  S8Args a;
+  a.boxes = boxes; a.nbox = nbox; a.img_dim = img_dim; a.out = targets; a.n_max = n_max; a.C = num_classes;
+  a.hm = (int)((double)pad_w / stride); a.wm = (int)((double)pad_h / stride);   // h_max from img_pad[1]
+  a.ns = n_scales; a.stride = stride; a.pad_h = pad_h; a.pad_w = pad_w;
+  for (int s = 0; s < kMaxScales; ++s) a.scales[s] = s < n_scales ? (double)box_scales[s] : 0.0;
+  const int rows = a.hm * a.wm * a.ns;
+  int gx = (rows + NT - 1) / NT;
+  gx = gx > 64 ? 64 : gx;
+  hipLaunchKernelGGL(s8_assign_kernel, dim3(gx, B), dim3(NT), 0, S_, a);
+  return cvl_launch_status();
+}
+
+extern "C" size_t cvl_centernet_s8_loss_workspace_size(int B, int P, int n_scales) {
+  return (size_t)B * (((size_t)P * n_scales + NT - 1) / NT) * 2 * sizeof(double);
+}
+
+extern "C" int cvl_centernet_s8_loss(const float* reg_pred, int ld_reg, const float* cls_pred, int ld_cls,
+                                     const float* targets, int B, int P, int n_scales, int num_classes,
+                                     float cls_scale, float reg_scale, float* losses, void* d_reg, int ld_dreg,
+                                     void* d_cls, int ld_dcls, void* workspace, cvl_stream_t stream) {
+  CVL_CHECK_ARG(reg_pred && cls_pred && targets && losses && d_reg && d_cls && workspace && B > 0 && P > 0);
+  CVL_CHECK_ARG(n_scales > 0 && num_classes > 0 && ld_reg >= 4 * n_scales && ld_cls >= num_classes * n_scales);
+  CVL_CHECK_ARG(ld_dreg >= 4 * n_scales && ld_dcls >= num_classes * n_scales);
+  S8LossArgs a;
+  a.reg = reg_pred; a.cls = cls_pred; a.tgt = targets; a.partial = (double*)workspace;
+  a.dreg = (cvl_bf16*)d_reg; a.dcls = (cvl_bf16*)d_cls;
+  a.ld_reg = ld_reg; a.ld_cls = ld_cls; a.ld_dreg = ld_dreg; a.ld_dcls = ld_dcls;
+  a.P = P; a.C = num_classes; a.ns = n_scales; a.tiles = (P * n_scales + NT - 1) / NT;
+  a.cls_scale = cls_scale; a.reg_scale = reg_scale;
+  hipLaunchKernelGGL(s8_loss_kernel, dim3(a.tiles, B), dim3(NT), 0, S_, a);
   hipLaunchKernelGGL(det_loss_finalize, dim3(B), dim3(FIN_T), 0, S_, (const double*)workspace, losses, a.tiles);
   return cvl_launch_status();
 }

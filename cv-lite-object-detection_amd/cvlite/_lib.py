@@ -83,6 +83,10 @@ SIGNATURES = {
     "cvl_bias_scalar_fold_periodic": (c_int, [P, P, P, c_int, c_int, c_int, P]),
     "cvl_bias_scalar_unfold_periodic": (c_int, [P, P, P, c_int, c_int, c_int, P]),
     "cvl_hourglass_v2_assign": (c_int, [P, P, c_int, c_int, c_int, c_int, c_int, P, P]),
+    "cvl_centernet_s8_assign": (c_int, [P, P, P, c_int, c_int, c_int, c_int, c_int, P, c_int, c_int, P, P]),
+    "cvl_centernet_s8_loss_workspace_size": (c_size_t, [c_int, c_int, c_int]),
+    "cvl_centernet_s8_loss": (c_int, [P, c_int, P, c_int, P, c_int, c_int, c_int, c_int, c_float, c_float, P, P, c_int,
+                                      P, c_int, P, P]),
     "cvl_hourglass_v2_loss_workspace_size": (c_size_t, [c_int, c_int]),
     "cvl_hourglass_v2_loss": (c_int, [P, c_int, P, c_int, c_int, c_int, c_int, c_float, c_float, P, P, c_int, P, P]),
     "cvl_sep_fold_multi": (c_int, [P, P, c_int, P]),

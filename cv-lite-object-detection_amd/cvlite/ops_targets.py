@@ -277,3 +277,42 @@ def hourglass_v2_loss(pred, targets, num_classes, loss_type="focal", cls_scale=2
               float(cls_scale), float(reg_scale), ptr(losses), ptr(d_pred), int(d_pred.shape[-1]), ptr(ws),
               _lib.stream())
     return losses, d_pred
+
+
+def centernet_s8_assign(boxes, nbox, img_dim, pad_hw, num_classes, box_scales, stride=8, out=None):
+    """tf_centernet_resnet_s8.format_data batched (cvl_centernet_s8_assign): boxes [B,n_max,5]
+    normalised (y, x, h, w, cls), img_dim [B,2] the resized size, pad_hw the padded size.
+    Returns [B, pad_w/stride, pad_h/stride, n_scales, 4+C] f32."""
+    B, nmax = _boxes_args(boxes, nbox, img_dim)
+    ns = len(box_scales)
+    hm, wm = int(pad_hw[1] / stride), int(pad_hw[0] / stride)
+    if out is None:
+        out = torch.empty((B, hm, wm, ns, 4 + num_classes), device=boxes.device, dtype=torch.float32)
+    assert tuple(out.shape) == (B, hm, wm, ns, 4 + num_classes) and out.is_contiguous()
+    sc = (_lib.ctypes.c_float * ns)(*[float(v) for v in box_scales])
+    _lib.call("cvl_centernet_s8_assign", ptr(boxes), ptr(nbox), ptr(img_dim), B, nmax, int(pad_hw[0]), int(pad_hw[1]),
+              int(num_classes), _lib.ctypes.cast(sc, _lib.c_void_p), ns, int(stride), ptr(out), _lib.stream())
+    return out
+
+
+def centernet_s8_loss(reg, cls, targets, num_classes, n_scales, cls_scale=1.0, reg_scale=1.0, d_reg=None,
+                      d_cls=None, losses=None):
+    """tf_centernet_resnet_s8.model_loss fwd+bwd off the two head convs: reg [B,P,>=ns*4], cls
+    [B,P,>=ns*C] f32 raw logits, targets [B,P,ns,4+C].  Returns (losses [B,2], d_reg, d_cls) with
+    bf16 gradients of cls_scale*cls + reg_scale*reg."""
+    _lib.require_cuda(reg, cls, targets)
+    B, P = int(targets.shape[0]), int(targets.shape[1])
+    assert tuple(targets.shape[2:]) == (n_scales, 4 + num_classes)
+    dev = targets.device
+    if losses is None:
+        losses = torch.empty((B, 2), device=dev, dtype=torch.float32)
+    if d_reg is None:
+        d_reg = torch.empty((B, P, (4 * n_scales + 31) // 32 * 32), device=dev, dtype=torch.bfloat16)
+    if d_cls is None:
+        d_cls = torch.empty((B, P, (num_classes * n_scales + 31) // 32 * 32), device=dev, dtype=torch.bfloat16)
+    ws = torch.empty(int(_lib.load().cvl_centernet_s8_loss_workspace_size(B, P, n_scales)), device=dev,
+                     dtype=torch.uint8)
+    _lib.call("cvl_centernet_s8_loss", ptr(reg), int(reg.shape[-1]), ptr(cls), int(cls.shape[-1]), ptr(targets), B, P,
+              int(n_scales), int(num_classes), float(cls_scale), float(reg_scale), ptr(losses), ptr(d_reg),
+              int(d_reg.shape[-1]), ptr(d_cls), int(d_cls.shape[-1]), ptr(ws), _lib.stream())
+    return losses, d_reg, d_cls

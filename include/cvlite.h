@@ -424,6 +424,22 @@ int cvl_hourglass_v2_assign(const float* boxes, const int32_t* nbox, int B, int 
  * channels 4..4+C; L1 on sigmoid(pred[0..3]) masked by t[4] (bit 1: pred[0..3] are already the
  * model's sigmoid outputs, as model_loss receives them).  losses [B][2] = (cls, reg); d_pred bf16
  * [B*P][ld_d] = d(cls_scale*cls + reg_scale*reg)/d(pred).  workspace >= *_workspace_size(B, P). */
+/* CenterNet ResNet stride-8 multi-scale (CenterNet/tf_centernet_resnet_s8.py) targets, format_data
+ * (:243-330) batched: boxes [B][n_max][5] normalised (y, x, h, w, cls) fp32, img_dim [B][2] the
+ * resized size, (pad_h, pad_w) the padded size, box_scales HOST [n_scales] (<= 8), stride 8 in the
+ * reference.  targets [B][pad_w/stride][pad_h/stride][n_scales][4+C] fp32; float64 arithmetic
+ * (the reference's gt_labels are float64), bit-exact. */
+int cvl_centernet_s8_assign(const float* boxes, const int32_t* nbox, const float* img_dim, int B, int n_max,
+                            int pad_h, int pad_w, int num_classes, const float* box_scales, int n_scales, int stride,
+                            float* targets, cvl_stream_t stream);
+/* model_loss (:368-385) fwd + bwd off the two head convs: reg_pred [B*P][ld_reg] (n_scales x 4 raw
+ * box logits per cell, sigmoid applied here), cls_pred [B*P][ld_cls] (n_scales x C logits),
+ * targets [B*P][n_scales][4+C]; focal + smooth-L1 of sigmoid(box) masked by max(class) > 0.
+ * losses [B][2] = (cls, reg); d_reg / d_cls bf16 (pitches ld_dreg / ld_dcls, pads zeroed). */
+size_t cvl_centernet_s8_loss_workspace_size(int B, int P, int n_scales);
+int cvl_centernet_s8_loss(const float* reg_pred, int ld_reg, const float* cls_pred, int ld_cls, const float* targets,
+                          int B, int P, int n_scales, int num_classes, float cls_scale, float reg_scale, float* losses,
+                          void* d_reg, int ld_dreg, void* d_cls, int ld_dcls, void* workspace, cvl_stream_t stream);
 size_t cvl_hourglass_v2_loss_workspace_size(int B, int P);
 int cvl_hourglass_v2_loss(const float* pred, int ld_pred, const float* targets, int B, int P, int num_classes,
                           int loss_type, float cls_scale, float reg_scale, float* losses, void* d_pred, int ld_d,

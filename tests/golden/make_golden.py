@@ -450,8 +450,48 @@ def work_hourglass_v2(out_path):
     np.savez_compressed(out_path, **arrays)
 
 
+def work_centernet_s8(out_path):
+    """CenterNet/tf_centernet_resnet_s8.py format_data (fed as train_centernet_crowdhuman.py does: a
+    float32 box array concatenated with the int64 class column -> float64 rows, img_dim the resized
+    [raw, raw], img_pad [img, img]) and model_loss on random heads."""
+    tf = _child_setup("CenterNet")
+    import tf_centernet_resnet_s8 as s8
+    rng = np.random.default_rng(808)
+    arrays = {}
+    scales = [32.0, 64.0, 128.0, 256.0, 512.0]
+    C = 3
+    for i in range(12):
+        img = [512, 384, 256][i % 3]
+        raw = img - int(rng.integers(0, 96)) if i % 4 else img
+        n = int(rng.integers(1, 40))
+        y = rng.uniform(0.02, 0.98, n)
+        x = rng.uniform(0.02, 0.98, n)
+        h = np.exp(rng.uniform(np.log(0.01), np.log(0.99), n))
+        w = np.exp(rng.uniform(np.log(0.01), np.log(0.99), n))
+        if i % 5 == 1:                           # crowded: shared cells / scales
+            y = 0.5 + rng.normal(0, 0.01, n)
+            x = 0.5 + rng.normal(0, 0.01, n)
+        box = np.stack([y, x, h, w], 1).astype(np.float32)
+        cls = rng.integers(0, C, n).astype(np.int64)[:, None]
+        rows = np.concatenate((box, cls), axis=1)          # float64, as the trainer's gt_labels
+        out, nt = s8.format_data(tf.constant(rows), scales, [raw, raw], C, img_pad=[img, img], stride=8)
+        arrays["case_%d_rows" % i] = np.concatenate([box, cls.astype(np.float32)], 1)
+        arrays["case_%d_dims" % i] = np.array([raw, img], np.int32)
+        arrays["case_%d_out" % i] = np.asarray(out).astype(np.float32)
+        arrays["case_%d_n" % i] = np.int32(nt)
+    # model_loss on a 2-image batch (targets of cases 2 and 5: 256 / 384 -> crop both to 32x32)
+    yt = np.stack([arrays["case_2_out"][:32, :32], arrays["case_5_out"][:32, :32]])
+    rl = rng.normal(0, 1.5, yt.shape[:-1] + (4,)).astype(np.float32)
+    cl = rng.normal(-1.0, 2.0, yt.shape[:-1] + (C,)).astype(np.float32)
+    pred = np.concatenate([np.asarray(tf.nn.sigmoid(tf.constant(rl)).numpy(), np.float32), cl], -1)
+    lc, lr = s8.model_loss(tf.constant(yt), tf.constant(pred))
+    arrays["loss_y"], arrays["loss_reg_logits"], arrays["loss_cls_logits"] = yt, rl, cl
+    arrays["loss_out"] = np.array([float(lc), float(lr)], np.float64)
+    np.savez_compressed(out_path, **arrays)
+
+
 WORKERS = {"fcos": work_fcos, "retinanet": work_retina, "centernet": work_centernet,
-           "fcos_center_v1": work_fcos_center_v1, "hourglass_v2": work_hourglass_v2,
+           "fcos_center_v1": work_fcos_center_v1, "hourglass_v2": work_hourglass_v2, "centernet_s8": work_centernet_s8,
            "centernet_softnms": work_centernet_softnms,
            "retina_decode": work_retina_decode,
            "fcos_center": work_fcos_center}

@@ -216,3 +216,21 @@ def test_hourglass_v2_targets_and_loss(golden):
         for lt in ("focal", "sigmoid"):
             np.testing.assert_allclose(hv.model_loss(t, d["loss_%d_raw" % st], d["loss_%d_bfocal" % st], lt),
                                        d["loss_%d_%s" % (st, lt)], rtol=1e-5)
+
+
+def test_centernet_s8_targets_and_loss(golden):
+    """tf_centernet_resnet_s8.format_data (float64 rows as the crowdhuman trainer feeds it) and
+    model_loss vs the reference's own outputs."""
+    from oracle import centernet_s8_ref as s8
+    d = golden("centernet_s8")
+    scales = [32.0, 64.0, 128.0, 256.0, 512.0]
+    hits = 0
+    for i in range(12):
+        raw, img = (int(v) for v in d["case_%d_dims" % i])
+        out, n = s8.format_data(d["case_%d_rows" % i], scales, [raw, raw], 3, img_pad=[img, img])
+        np.testing.assert_array_equal(out, d["case_%d_out" % i])
+        assert n == int(d["case_%d_n" % i])
+        hits += int((out[..., 4:].sum(-1) > 0).sum())
+    assert hits > 100
+    pred = np.concatenate([1.0 / (1.0 + np.exp(-d["loss_reg_logits"].astype(np.float64))), d["loss_cls_logits"]], -1)
+    np.testing.assert_allclose(s8.model_loss(d["loss_y"], pred), d["loss_out"], rtol=1e-5)
