@@ -340,6 +340,7 @@ __global__ void __launch_bounds__(NT) bn_apply_kernel(const cvl_bf16* __restrict
           float o = bn_affine(v[u], m[u], rs[u], ga[u], be[u]);
           if (res) o += rr[u];
           if (relu) o = o > 0.f ? o : 0.f;
+          if (relu == 2) o = fminf(o, 6.0f);                     // ReLU6 (MobileNetV2)
           v[u] = o;
         }
         *reinterpret_cast<s16x8*>(y + off[q]) = pack8(v);
@@ -387,7 +388,7 @@ __global__ void __launch_bounds__(NT) bn_bwd_kernel(const cvl_bf16* __restrict__
                                                     cvl_bf16* __restrict__ dz, cvl_bf16* __restrict__ g_out,
                                                     float* __restrict__ part, int C, int HW, int rows_per_blk,
                                                     int group, float dz_beta, BnPG pg,
-                                                    const float* __restrict__ bnb) {
+                                                    const float* __restrict__ bnb, float act_hi) {
   const int b = blockIdx.y;
   const int C8 = C / 8;
   const int tpr = C8 < NT ? C8 : NT;
@@ -469,10 +470,13 @@ __global__ void __launch_bounds__(NT) bn_bwd_kernel(const cvl_bf16* __restrict__
             float yy[8];
             unpack8(vy[q], yy);
 #pragma unroll
-            for (int u = 0; u < 8; ++u) g[u] = yy[u] > 0.f ? g[u] : 0.f;
+            for (int u = 0; u < 8; ++u) g[u] = (yy[u] > 0.f && yy[u] < act_hi) ? g[u] : 0.f;   // ReLU / ReLU6
           } else if (zmask) {
 #pragma unroll
-            for (int u = 0; u < 8; ++u) g[u] = bn_affine(zz[u], m[u], rs[u], ga[u], be[u]) > 0.f ? g[u] : 0.f;
+            for (int u = 0; u < 8; ++u) {
+              const float a = bn_affine(zz[u], m[u], rs[u], ga[u], be[u]);
+              g[u] = (a > 0.f && a < act_hi) ? g[u] : 0.f;
+            }
           }
           if (PASS == 0) {
             if (ok) {
@@ -1116,7 +1120,7 @@ extern "C" size_t cvl_bn_backward_workspace_size(int B, int HW, int C) {
 static int bn_backward_impl(const void* dy, const void* y_relu, const float* bn_beta, const void* z,
                             const float* mean_rstd, const float* gamma, void* workspace, size_t workspace_bytes,
                             void* dz, void* g_out, float* dgamma, float* dbeta, float beta_acc, float* conv_dbias,
-                            int B, int HW, int C, cvl_stream_t stream) {
+                            int B, int HW, int C, cvl_stream_t stream, float act_hi = INFINITY) {
   CVL_CHECK_ARG(dy && z && mean_rstd && gamma && workspace && dz && dgamma && dbeta && C % 8 == 0);
   CVL_CHECK_ARG(B > 0 && HW > 0);
   CVL_CHECK_ARG(workspace_bytes >= cvl_bn_backward_workspace_size(B, HW, C));
@@ -1129,12 +1133,13 @@ static int bn_backward_impl(const void* dy, const void* y_relu, const float* bn_
   dim3 g1(nchunk, B);
   hipLaunchKernelGGL(bn_bwd_kernel<0>, g1, dim3(NT), 0, S_, (const cvl_bf16*)dy, (const cvl_bf16*)y_relu,
                      (const cvl_bf16*)z, mean_rstd, gamma, (const double*)nullptr, (cvl_bf16*)nullptr,
-                     (cvl_bf16*)nullptr, part0, C, HW, rpb, 1, 0.f, BnPG{}, bn_beta);
+                     (cvl_bf16*)nullptr, part0, C, HW, rpb, 1, 0.f, BnPG{}, bn_beta, act_hi);
   hipLaunchKernelGGL(bn_colsum_kernel, dim3((C + 31) / 32, B), dim3(NT), 0, S_, (const float*)part0, nchunk, C,
                      sums);
   hipLaunchKernelGGL(bn_bwd_kernel<1>, g1, dim3(NT), 0, S_, (const cvl_bf16*)dy, (const cvl_bf16*)y_relu,
                      (const cvl_bf16*)z, mean_rstd, gamma, (const double*)sums, (cvl_bf16*)dz, (cvl_bf16*)g_out,
-                     (float*)nullptr, C, HW, rpb, 1, 0.f, BnPG{dgamma, dbeta, conv_dbias, beta_acc}, bn_beta);
+                     (float*)nullptr, C, HW, rpb, 1, 0.f, BnPG{dgamma, dbeta, conv_dbias, beta_acc}, bn_beta,
+                     act_hi);
   return cvl_launch_status();
 }
 
@@ -1153,6 +1158,15 @@ extern "C" int cvl_bn_backward_relu(const void* dy, const void* z, const float* 
   CVL_CHECK_ARG(beta);
   return bn_backward_impl(dy, nullptr, beta, z, mean_rstd, gamma, workspace, workspace_bytes, dz, nullptr, dgamma,
                           dbeta, beta_acc, conv_dbias, B, HW, C, stream);
+}
+
+extern "C" int cvl_bn_backward_relu6(const void* dy, const void* z, const float* mean_rstd, const float* gamma,
+                                     const float* beta, void* workspace, size_t workspace_bytes, void* dz,
+                                     float* dgamma, float* dbeta, float beta_acc, float* conv_dbias, int B, int HW,
+                                     int C, cvl_stream_t stream) {
+  CVL_CHECK_ARG(beta);
+  return bn_backward_impl(dy, nullptr, beta, z, mean_rstd, gamma, workspace, workspace_bytes, dz, nullptr, dgamma,
+                          dbeta, beta_acc, conv_dbias, B, HW, C, stream, 6.0f);
 }
 
 extern "C" int cvl_maxpool3x3s2(const void* x, void* y, uint8_t* argmax, int B, int H, int W, int C,
@@ -1312,7 +1326,7 @@ extern "C" int cvl_bn_stats(const void* x, int B, int HW, int C, double* stats, 
   hipLaunchKernelGGL(bn_bwd_kernel<2>, dim3(nchunk, B), dim3(NT), 0, S_, (const cvl_bf16*)x,
                      (const cvl_bf16*)nullptr, (const cvl_bf16*)nullptr, (const float*)nullptr, (const float*)nullptr,
                      (const double*)nullptr, (cvl_bf16*)nullptr, (cvl_bf16*)nullptr, part, C, HW, rpb, 1, 0.f, BnPG{},
-                     (const float*)nullptr);
+                     (const float*)nullptr, INFINITY);
   hipLaunchKernelGGL(bn_colsum_kernel, dim3((C + 31) / 32, B), dim3(NT), 0, S_, (const float*)part, nchunk, C,
                      stats);
   return cvl_launch_status();
@@ -1350,7 +1364,7 @@ extern "C" int cvl_bn_backward_grouped(const void* dy, const void* y_relu, const
   dim3 g1(nchunk, B);
   hipLaunchKernelGGL(bn_bwd_kernel<0>, g1, dim3(NT), 0, S_, (const cvl_bf16*)dy, (const cvl_bf16*)y_relu,
                      (const cvl_bf16*)z, mean_rstd, gamma, (const double*)nullptr, (cvl_bf16*)nullptr,
-                     (cvl_bf16*)nullptr, part0, C, HW, rpb, group, 0.f, BnPG{}, (const float*)nullptr);
+                     (cvl_bf16*)nullptr, part0, C, HW, rpb, group, 0.f, BnPG{}, (const float*)nullptr, INFINITY);
   hipLaunchKernelGGL(bn_colsum_kernel, dim3((C + 31) / 32, B), dim3(NT), 0, S_, (const float*)part0, nchunk, C,
                      sums);
   const double* use = sums;
@@ -1362,6 +1376,6 @@ extern "C" int cvl_bn_backward_grouped(const void* dy, const void* y_relu, const
   hipLaunchKernelGGL(bn_bwd_kernel<1>, g1, dim3(NT), 0, S_, (const cvl_bf16*)dy, (const cvl_bf16*)y_relu,
                      (const cvl_bf16*)z, mean_rstd, gamma, use, (cvl_bf16*)dz, (cvl_bf16*)nullptr,
                      (float*)nullptr, C, HW, rpb, group, dz_beta, BnPG{dgamma, dbeta, nullptr, 0.f, sums},
-                     (const float*)nullptr);
+                     (const float*)nullptr, INFINITY);
   return cvl_launch_status();
 }

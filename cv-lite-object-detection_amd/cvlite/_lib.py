@@ -78,6 +78,13 @@ SIGNATURES = {
     "cvl_upsample_bilinear2x_add": (c_int, [P, P, P, c_int, c_int, c_int, c_int, P]),
     "cvl_upsample_bilinear2x_backward": (c_int, [P, P, c_int, c_int, c_int, c_int, c_float, P]),
     "cvl_upsample_bilinear2x_sum": (c_int, [P, P, P, c_int, c_int, c_int, c_int, P]),
+    "cvl_bn_backward_relu6": (c_int, [P, P, P, P, P, P, c_size_t, P, P, P, c_float, P, c_int, c_int, c_int, P]),
+    "cvl_depthwise_fwd": (c_int, [P, P, P, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, P]),
+    "cvl_depthwise_dgrad": (c_int, [P, P, P, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int,
+                                    c_float, P]),
+    "cvl_depthwise_wgrad_workspace_size": (c_size_t, [c_int, c_int, c_int, c_int, c_int]),
+    "cvl_depthwise_wgrad": (c_int, [P, P, P, c_float, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int,
+                                    c_int, P, c_size_t, P]),
     "cvl_reshape_concat": (c_int, [P, c_int, c_int, c_int, P, c_int, P]),
     "cvl_reshape_concat_backward": (c_int, [P, c_int, c_int, c_int, P, c_int, P]),
     "cvl_bias_scalar_fold_periodic": (c_int, [P, P, P, c_int, c_int, c_int, P]),

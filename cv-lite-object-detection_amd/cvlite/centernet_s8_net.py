@@ -16,7 +16,7 @@ fp32 weights before each re-pack; their weight / bias gradients are scattered ba
 The towers' weight gradient therefore sums over the scales exactly as the reference's repeated
 layer calls do.  Reference quirk kept visible: build_model's `if resnet50 / if resnet101 / else
 MobileNetV2` sends backbone_model="resnet50" to the MobileNetV2 branch (Q-s8); only "resnet101"
-builds a ResNet.
+builds a ResNet (cvlite.mobilenet_v2 serves the other names).
 """
 import math
 
@@ -24,6 +24,7 @@ import torch
 
 from . import ops_nn as nn
 from .layers import BF16, Conv, ParamStore, constant
+from .mobilenet_v2 import MobileNetV2
 from .resnet import ResNet50
 
 FPN_C = 256
@@ -31,12 +32,9 @@ FPN_C = 256
 
 class CenterNetS8Net(object):
     def __init__(self, num_classes, n_scales=5, backbone_model="resnet101", device="cuda", seed=0):
-        bm = backbone_model.lower()
-        if bm != "resnet101":
-            raise NotImplementedError(
-                "tf_centernet_resnet_s8.build_model builds ResNet101 only for backbone_model='resnet101'; "
-                "every other value (including 'resnet50', :117-131) takes its MobileNetV2 branch, which cvlite "
-                "does not implement")
+        # :117-131: `if resnet50: ...` is followed by `if resnet101: ... else: MobileNetV2`, so only
+        # "resnet101" keeps a ResNet; every other name (including "resnet50") ends on MobileNetV2
+        self.backbone_model = "resnet101" if backbone_model.lower() == "resnet101" else "mobilenetv2"
         self.C, self.ns = num_classes, n_scales
         self.device = torch.device(device)
         st, eff = ParamStore(), ParamStore()
@@ -55,10 +53,12 @@ class CenterNetS8Net(object):
         # creation order follows build_model: towers, backbone, FPN, feature map, heads
         self.cls_tower = [Conv(st, "cls_layer_%d" % (i + 1), 3, FPN_C, FPN_C, bias=False) for i in range(4)]
         self.reg_tower = [Conv(st, "reg_layer_%d" % (i + 1), 3, FPN_C, FPN_C, bias=False) for i in range(4)]
-        self.backbone = ResNet50(st, "resnet101")
-        self.c3_1x1 = Conv(st, "c3_1x1", 1, 512, FPN_C)
-        self.c4_1x1 = Conv(st, "c4_1x1", 1, 1024, FPN_C)
-        self.c5_1x1 = Conv(st, "c5_1x1", 1, 2048, FPN_C)
+        kind = getattr(self, "backbone_model", "resnet101")
+        self.backbone = ResNet50(st, "resnet101") if kind == "resnet101" else MobileNetV2(st)
+        t3, t4, t5 = self.backbone.tap_channels
+        self.c3_1x1 = Conv(st, "c3_1x1", 1, t3, FPN_C)
+        self.c4_1x1 = Conv(st, "c4_1x1", 1, t4, FPN_C)
+        self.c5_1x1 = Conv(st, "c5_1x1", 1, t5, FPN_C)
         self.c6_3x3 = Conv(st, "c6_3x3", 3, FPN_C, FPN_C, stride=2)
         self.c7_3x3 = Conv(st, "c7_3x3", 3, FPN_C, FPN_C, stride=2)
         self.feat = Conv(st, "cnn_feature_map", 3, FPN_C, FPN_C)
@@ -207,9 +207,10 @@ class CenterNetS8Net(object):
         return torch.cat([r, cls.view(B, S0, S1, self.ns, self.C)], -1)
 
     @staticmethod
-    def param_dict(num_classes, n_scales=5, seed=0):
+    def param_dict(num_classes, n_scales=5, seed=0, backbone_model="resnet101"):
         """Initial parameters (Keras names -> CPU fp32) without a GPU (oracle / checkpoints)."""
         obj = CenterNetS8Net.__new__(CenterNetS8Net)
+        obj.backbone_model = "resnet101" if backbone_model.lower() == "resnet101" else "mobilenetv2"
         st, eff = ParamStore(), ParamStore()
         obj._build(st, eff, num_classes, n_scales)
         st.finalize("cpu", seed)

@@ -17,7 +17,8 @@ import torch
 
 from . import ops_nn as nn
 from .layers import BF16, Conv, ParamStore
-from .resnet import DEPTHS, ResNet50
+from .mobilenet_v2 import MobileNetV2
+from .resnet import ResNet50
 
 FPN_C = 256
 STRIDES = (8, 16, 32, 64, 128)
@@ -30,11 +31,14 @@ PAIR_TOWERS = os.environ.get("CVL_TOWER_PAIR", "1") != "0"
 FUSE_FPN = os.environ.get("CVL_FPN_FUSE", "1") != "0"
 
 class FPNDetector(object):
+    @staticmethod
+    def backbone_kind(name):
+        """FCOS/fcos.py:29-41 (and fcos_center*.py): "resnet50" builds ResNet50, EVERY other name
+        builds MobileNetV2."""
+        return "resnet50" if name.lower() == "resnet50" else "mobilenetv2"
+
     def _init_common(self, num_classes, backbone_model, device, seed):
-        if backbone_model.lower() not in DEPTHS:
-            raise NotImplementedError("cvlite implements the %s backbones of build_model, not %r"
-                                      % ("/".join(DEPTHS), backbone_model))
-        self.backbone_model = backbone_model.lower()
+        self.backbone_model = self.backbone_kind(backbone_model)
         self.C = num_classes
         self.store = st = ParamStore()
         self._build_layers(st, num_classes)
@@ -49,14 +53,16 @@ class FPNDetector(object):
         # creation order follows build_model: towers, backbone, FPN, heads
         self.cls_tower = [Conv(st, "cls_layer_%d" % (i + 1), 3, FPN_C, FPN_C, bias=False) for i in range(4)]
         self.reg_tower = [Conv(st, "reg_layer_%d" % (i + 1), 3, FPN_C, FPN_C, bias=False) for i in range(4)]
-        self.backbone = ResNet50(st, getattr(self, "backbone_model", "resnet50"))
-        self.c3_1x1 = Conv(st, "c3_1x1", 1, 512, FPN_C)
-        self.c4_1x1 = Conv(st, "c4_1x1", 1, 1024, FPN_C)
-        self.c5_1x1 = Conv(st, "c5_1x1", 1, 2048, FPN_C)
+        kind = getattr(self, "backbone_model", "resnet50")
+        self.backbone = MobileNetV2(st) if kind == "mobilenetv2" else ResNet50(st, kind)
+        t3, t4, t5 = self.backbone.tap_channels
+        self.c3_1x1 = Conv(st, "c3_1x1", 1, t3, FPN_C)
+        self.c4_1x1 = Conv(st, "c4_1x1", 1, t4, FPN_C)
+        self.c5_1x1 = Conv(st, "c5_1x1", 1, t5, FPN_C)
         self.c3_3x3 = Conv(st, "c3_3x3", 3, FPN_C, FPN_C)
         self.c4_3x3 = Conv(st, "c4_3x3", 3, FPN_C, FPN_C)
         self.c5_3x3 = Conv(st, "c5_3x3", 3, FPN_C, FPN_C)
-        self.c6_3x3 = Conv(st, "c6_3x3", 3, 2048, FPN_C, stride=2)
+        self.c6_3x3 = Conv(st, "c6_3x3", 3, t5, FPN_C, stride=2)
         self.c7_3x3 = Conv(st, "c7_3x3", 3, FPN_C, FPN_C, stride=2)
         self._build_heads(st, num_classes)
 
@@ -64,7 +70,7 @@ class FPNDetector(object):
     def param_dict(cls, num_classes, seed=0, backbone_model="resnet50"):
         """The initial parameters (Keras names -> CPU fp32) without touching a GPU."""
         obj = cls.__new__(cls)
-        obj.backbone_model = backbone_model.lower()
+        obj.backbone_model = cls.backbone_kind(backbone_model)
         st = ParamStore()
         obj._build_layers(st, num_classes)
         st.finalize("cpu", seed)
@@ -208,6 +214,8 @@ class FPNDetector(object):
         g = [("heads_towers", names(self.head_convs() + self.cls_tower + self.reg_tower)),
              ("fpn", names([self.c3_1x1, self.c4_1x1, self.c5_1x1, self.c3_3x3, self.c4_3x3, self.c5_3x3,
                             self.c6_3x3, self.c7_3x3]))]
+        if isinstance(bb, MobileNetV2):
+            return g + [("backbone", bb.param_names())]
         for si in (3, 2, 1):
             g.append(("conv%d" % (si + 2), units([u for b in bb.stages[si] for u in b.units()])))
         stem = [bb.stem.conv.wname, bb.stem.conv.bname, bb.stem.bn.gname, bb.stem.bn.bname]

@@ -133,7 +133,7 @@ def bn_finalize(stats, mean_rstd, run_mean, run_var, B, C, HW, eps, momentum):
 
 def bn_apply(z, mean_rstd, gamma, beta, residual, y, B, HW, C, relu):
     _lib.call("cvl_bn_apply", ptr(z), ptr(mean_rstd), ptr(gamma), ptr(beta), ptr(residual), ptr(y),
-              B, HW, C, int(bool(relu)), stream())
+              B, HW, C, int(relu), stream())          # relu: 0 none, 1 ReLU, 2 ReLU6
 
 
 def bn_finalize_apply(stats, mean_rstd, run_mean, run_var, z, gamma, beta, residual, y, B, HW, C, relu, eps,
@@ -149,6 +149,43 @@ def bn_backward(dy, y_relu, z, mean_rstd, gamma, dz, g_out, dgamma, dbeta, B, HW
     _lib.call("cvl_bn_backward", ptr(dy), ptr(y_relu), ptr(z), ptr(mean_rstd), ptr(gamma), ptr(ws), n,
               ptr(dz), ptr(g_out), ptr(dgamma), ptr(dbeta), float(beta_acc), ptr(conv_dbias), B, HW, C,
               stream())
+
+
+def bn_backward_relu6(dy, z, mean_rstd, gamma, beta, dz, dgamma, dbeta, B, HW, C, beta_acc=0.0, conv_dbias=None):
+    """bn_backward of a BN -> ReLU6 unit without a residual (mask 0 < bn(z) < 6 rebuilt from z)."""
+    n = int(_lib.load().cvl_bn_backward_workspace_size(B, HW, C))
+    ws = torch.empty(n, dtype=torch.uint8, device=dy.device)
+    _lib.call("cvl_bn_backward_relu6", ptr(dy), ptr(z), ptr(mean_rstd), ptr(gamma), ptr(beta), ptr(ws), n, ptr(dz),
+              ptr(dgamma), ptr(dbeta), float(beta_acc), ptr(conv_dbias), B, HW, C, stream())
+
+
+def _dw_shapes(x, Ho, Wo):
+    B, H, W, C = x.shape
+    return B, H, W, C, Ho, Wo
+
+
+def depthwise_fwd(x, w, y, k, stride, pad_t, pad_l):
+    """Keras DepthwiseConv2D: x [B,H,W,C] bf16, w [k,k,C(,1)] fp32 -> y [B,Ho,Wo,C] bf16."""
+    B, H, W, C = x.shape
+    Ho, Wo = y.shape[1], y.shape[2]
+    _lib.call("cvl_depthwise_fwd", ptr(x), ptr(w), ptr(y), B, H, W, C, int(k), int(stride), int(pad_t), int(pad_l),
+              Ho, Wo, stream())
+
+
+def depthwise_dgrad(dy, w, dx, k, stride, pad_t, pad_l, beta=0.0):
+    B, H, W, C = dx.shape
+    Ho, Wo = dy.shape[1], dy.shape[2]
+    _lib.call("cvl_depthwise_dgrad", ptr(dy), ptr(w), ptr(dx), B, H, W, C, int(k), int(stride), int(pad_t),
+              int(pad_l), Ho, Wo, float(beta), stream())
+
+
+def depthwise_wgrad(x, dy, dw, k, stride, pad_t, pad_l, beta=0.0):
+    B, H, W, C = x.shape
+    Ho, Wo = dy.shape[1], dy.shape[2]
+    n = int(_lib.load().cvl_depthwise_wgrad_workspace_size(B, Ho, Wo, C, int(k)))
+    ws = torch.empty(max(n, 16), dtype=torch.uint8, device=x.device)
+    _lib.call("cvl_depthwise_wgrad", ptr(x), ptr(dy), ptr(dw), float(beta), B, H, W, C, int(k), int(stride),
+              int(pad_t), int(pad_l), Ho, Wo, ptr(ws), ws.numel(), stream())
 
 
 def bn_backward_relu(dy, z, mean_rstd, gamma, beta, dz, dgamma, dbeta, B, HW, C, beta_acc=0.0, conv_dbias=None):

@@ -129,6 +129,7 @@ class ResNet50(object):
     """Keras ResNet50 / ResNet101 / ResNet152 (v1 bottleneck stacks; `depth` picks the block
     counts, the class name is kept for the default)."""
     STACKS = ((64, 3, 1), (128, 4, 2), (256, 6, 2), (512, 3, 2))
+    tap_channels = (512, 1024, 2048)
 
     def __init__(self, store, depth="resnet50"):
         blocks = DEPTHS[depth.lower()]

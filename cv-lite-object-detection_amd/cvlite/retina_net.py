@@ -21,6 +21,18 @@ from .layers import Conv
 
 
 class RetinaNetNet(FPNDetector):
+    @staticmethod
+    def backbone_kind(name):
+        """RetinaNet/retinanet_module.py:30-71: ResNet50 / 101 / 152, ResNeXt50 / 101 (third-party
+        classification_models, not built), every other name MobileNetV2."""
+        n = name.lower()
+        if n in ("resnet50", "resnet101", "resnet152"):
+            return n
+        if n in ("resnext50", "resnext101"):
+            raise NotImplementedError("the ResNeXt backbones come from the third-party classification_models "
+                                      "package; cvlite builds the ResNet and MobileNetV2 branches")
+        return "mobilenetv2"
+
     A = 9
     def __init__(self, num_classes, n_anchors=9, backbone_model="resnet50", device="cuda", seed=0):
         self.A = n_anchors

@@ -1,8 +1,9 @@
 """Drop-in mirror of CenterNet/tf_centernet_resnet_s8.py (the CenterNet of
 train_centernet_crowdhuman.py) on MI355X.
 
-  build_model(num_classes, n_scales, backbone_model)         :87-208 -> S8Model (ResNet101 only:
-      the reference's if/if/else sends every other backbone_model to MobileNetV2)
+  build_model(num_classes, n_scales, backbone_model)         :87-208 -> S8Model (ResNet101 for
+      "resnet101"; the reference's if/if/else sends every other name, "resnet50" included, to
+      MobileNetV2, cvlite.mobilenet_v2)
   prediction_to_corners(xy_pred, box_scales, stride)          :210-241 -> cvl_fcos_v1_decode per scale
   format_data(gt_labels, box_scales, img_dim, num_classes, img_pad, stride)  :243-330
       -> cvl_centernet_s8_assign (bit-exact, float64 as the reference)

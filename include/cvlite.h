@@ -223,6 +223,12 @@ int cvl_bn_backward_relu(const void* dy, const void* z, const float* mean_rstd, 
                          const float* beta, void* workspace, size_t workspace_bytes, void* dz, float* dgamma,
                          float* dbeta, float beta_acc, float* conv_dbias, int B, int HW, int C,
                          cvl_stream_t stream);
+/* BN -> ReLU6 unit without a residual (MobileNetV2: Keras ReLU(6.)): as cvl_bn_backward_relu with
+ * the TF Relu6Grad mask 0 < bn(z) < 6 rebuilt from z in fp32 (the forward's exact pre-clamp value);
+ * cvl_bn_apply / cvl_bn_finalize_apply take relu = 2 for ReLU6. */
+int cvl_bn_backward_relu6(const void* dy, const void* z, const float* mean_rstd, const float* gamma,
+                          const float* beta, void* workspace, size_t workspace_bytes, void* dz, float* dgamma,
+                          float* dbeta, float beta_acc, float* conv_dbias, int B, int HW, int C, cvl_stream_t stream);
 
 /* ResNet50 pool1: ZeroPadding2D(1) + MaxPooling2D(3, 2); argmax [B][Ho][Wo][C] uint8 (0..8). */
 int cvl_maxpool3x3s2(const void* x, void* y, uint8_t* argmax, int B, int H, int W, int C,
@@ -384,6 +390,20 @@ int cvl_upsample_bilinear2x_add(const void* prev, const void* other, void* out, 
                                 cvl_stream_t stream);
 int cvl_upsample_bilinear2x_backward(const void* dout, void* dprev, int B, int h, int w, int C, float beta,
                                      cvl_stream_t stream);
+
+/* Depthwise convolution (Keras DepthwiseConv2D, depth_multiplier 1, no bias; the MobileNetV2
+ * backbone of FCOS/fcos.py:36-41 and its siblings): x [B][H][W][C] bf16, w [k][k][C] fp32 (Keras
+ * depthwise_kernel [k][k][C][1]), y [B][Ho][Wo][C] bf16, explicit top/left padding (TF "same" or
+ * ZeroPadding2D(correct_pad) + "valid"), C % 8 == 0.  dgrad: dx = beta*dx + conv^T(dy).  wgrad
+ * (k = 3): dw = beta*dw + sum over all output pixels, deterministic; workspace >= *_size. */
+int cvl_depthwise_fwd(const void* x, const float* w, void* y, int B, int H, int W, int C, int k, int stride,
+                      int pad_t, int pad_l, int Ho, int Wo, cvl_stream_t stream);
+int cvl_depthwise_dgrad(const void* dy, const float* w, void* dx, int B, int H, int W, int C, int k, int stride,
+                        int pad_t, int pad_l, int Ho, int Wo, float beta, cvl_stream_t stream);
+size_t cvl_depthwise_wgrad_workspace_size(int B, int Ho, int Wo, int C, int k);
+int cvl_depthwise_wgrad(const void* x, const void* dy, float* dw, float beta, int B, int H, int W, int C, int k,
+                        int stride, int pad_t, int pad_l, int Ho, int Wo, void* workspace, size_t workspace_bytes,
+                        cvl_stream_t stream);
 
 /* CenterNet v2 (CenterNet/tf_hourglass_net.py:115-449, n_filters 12 in train_hourglass_voc.py:298-331)
  * --------------------------------------------------------------------------------------------

@@ -153,9 +153,49 @@ def resnet50(x, p):
     return taps[1:]
 
 
+# Keras MobileNetV2 (alpha 1) blocks 0..16: (expansion, channels, stride)
+MBV2_CFG = ((1, 16, 1), (6, 24, 2), (6, 24, 1), (6, 32, 2), (6, 32, 1), (6, 32, 1), (6, 64, 2), (6, 64, 1),
+            (6, 64, 1), (6, 64, 1), (6, 96, 1), (6, 96, 1), (6, 96, 1), (6, 160, 2), (6, 160, 1), (6, 160, 1),
+            (6, 320, 1))
+
+
+def mobilenet_v2(x, p):
+    """tf.keras.applications.MobileNetV2 (include_top=False) taps block_6_expand, block_13_expand,
+    Conv_1 (raw conv outputs; fcos.py:36-41).  BN eps 1e-3 per image, ReLU6, depthwise 3x3 with
+    ZeroPadding2D((0,1),(0,1)) + valid at stride 2.  The parameters may carry zero channel pads (the
+    cvlite store's layout): zero channels stay zero through every layer, so the result is the
+    Keras graph's.  Depthwise kernels are fp32 on the GPU path (no bf16 weight rounding here)."""
+    relu6 = lambda t: torch.clamp(t, 0.0, 6.0)  # noqa: E731
+    h = q(relu6(bn(conv(x, p, "Conv1", 2, bias=False), p, "bn_Conv1", 1e-3)))
+    taps = []
+    cin = 32
+    for bid, (t, c, s) in enumerate(MBV2_CFG):
+        pre = "expanded_conv_" if bid == 0 else "block_%d_" % bid
+        res = s == 1 and cin == c
+        cin = c
+        inp = h
+        if t != 1:
+            z = conv(h, p, pre + "expand", bias=False)
+            if bid in (6, 13):
+                taps.append(z)
+            h = q(relu6(bn(z, p, pre + "expand_BN", 1e-3)))
+        w = p[pre + "depthwise/depthwise_kernel"]
+        hp = F.pad(h, (1, 1, 1, 1)) if s == 1 else F.pad(h, (0, 1, 0, 1))
+        z = q(F.conv2d(hp, w.permute(2, 3, 0, 1), None, s, groups=w.shape[2]))
+        h = q(relu6(bn(z, p, pre + "depthwise_BN", 1e-3)))
+        y = bn(conv(h, p, pre + "project", bias=False), p, pre + "project_BN", 1e-3)
+        h = q(y + inp) if res else q(y)
+    taps.append(conv(h, p, "Conv_1", bias=False))
+    return taps
+
+
+def backbone_taps(x, p):
+    return mobilenet_v2(x, p) if "Conv1/kernel" in p else resnet50(x, p)
+
+
 def fpn_levels(x, p):
     """Backbone + FPN (fcos.py:49-72 == retinanet_module.py:74-105): [P3..P7] NCHW."""
-    c3, c4, c5 = resnet50(x, p)
+    c3, c4, c5 = backbone_taps(x, p)
     l3 = conv(c3, p, "c3_1x1")
     l4 = conv(c4, p, "c4_1x1")
     l5 = conv(c5, p, "c5_1x1")

@@ -176,9 +176,9 @@ def test_backbone_blocks_match_fp32_oracle_with_synced_inputs(backbone):
     amplification.  (ResNet-101: retinanet_module.py:39-45, the backbone of
     train_retinanet_coco.py:347; taps conv4_block23_out.)"""
     import torch.nn.functional as F
-    from cvlite.fcos_net import FCOSNet
+    from cvlite.retina_net import RetinaNetNet
     C, B, D = 20, 2, 256
-    net = FCOSNet(C, seed=1, backbone_model=backbone)
+    net = RetinaNetNet(C, seed=1, backbone_model=backbone)       # retinanet_module.py:30-45
     assert len(net.backbone.stages[2]) == (23 if backbone == "resnet101" else 6)
     p = net.store.state_dict()
     rng = np.random.default_rng(3)
