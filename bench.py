@@ -132,8 +132,14 @@ def cpu_baseline(H, W, cfg1_images=8, bs=16, timed_images=(8, 8, 8)):
     every core this process may run on (sched_getaffinity)."""
     from oracle import fcos_ref, model_ref
     import numpy as np
+    # the host cores this process may use: the affinity mask, capped by OMP_NUM_THREADS (the GPU box
+    # exports its CPU share there; the affinity mask / nproc show the whole machine)
     cores = len(os.sched_getaffinity(0))
+    omp = os.environ.get("OMP_NUM_THREADS")
+    if omp and omp.isdigit() and int(omp) > 0:
+        cores = min(cores, int(omp))
     torch.set_num_threads(cores)
+    print("[bench] cpu_baseline: %d threads" % cores, file=sys.stderr, flush=True)
     p = FCOSNet.param_dict(NUM_CLASSES, seed=0)
     moms = {k: torch.zeros_like(v) for k, v in p.items()}
     n = cfg1_images + sum(timed_images)
@@ -148,11 +154,13 @@ def cpu_baseline(H, W, cfg1_images=8, bs=16, timed_images=(8, 8, 8)):
     model_ref.train_step_reference(p, moms, imgs[:cfg1_images], tg[:cfg1_images], NUM_CLASSES, 5e-4)
     cfg1_s = time.time() - t0
     rates, o = [], cfg1_images
+    print("[bench] cpu_baseline configs[0] step: %.1f s" % cfg1_s, file=sys.stderr, flush=True)
     for k in timed_images:
         t0 = time.time()
         model_ref.train_step_reference(p, moms, imgs[o:o + k], tg[o:o + k], NUM_CLASSES, 5e-4)
         rates.append(k / (time.time() - t0))
         o += k
+        print("[bench] cpu_baseline timed step: %.3f img/s" % rates[-1], file=sys.stderr, flush=True)
     return {"value": round(sorted(rates)[len(rates) // 2], 4), "unit": "images/s", "cores": cores,
             "kind": "port", "configs0_step_s": round(cfg1_s, 3), "timed_img_s": [round(r, 4) for r in rates],
             "sample": "torch-CPU fp32 restatement of the train_fcos.py step (oracle/model_ref.py): configs[0] "
