@@ -17,12 +17,19 @@ import torch.distributed as tdist
 BUCKET_BYTES = 64 << 20
 
 
+def force_sync():
+    """CVL_DP_FORCE_SYNC=1: run the gradient all-reduce path even at world size 1 (a one-rank RCCL
+    group exercises ProcessGroupNCCL's stream ordering against the HIP-graph segments on a 1-GPU
+    box; the SUM over one rank is the identity, so the step must be bit-identical)."""
+    return os.environ.get("CVL_DP_FORCE_SYNC", "0") == "1"
+
+
 def init_from_env(backend=None):
     """torchrun-style env (RANK, WORLD_SIZE, LOCAL_RANK, MASTER_ADDR/PORT).  Returns (rank, world, local)."""
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1 and not tdist.is_initialized():
+    if (world > 1 or (force_sync() and "MASTER_ADDR" in os.environ)) and not tdist.is_initialized():
         if backend is None:
             backend = "nccl" if torch.cuda.is_available() else "gloo"
         if backend == "nccl":
@@ -87,7 +94,7 @@ class GradSync(object):
         assert len(names) == len(set(names)) == len(store.offsets), \
             "gradient groups must cover every parameter exactly once"
         self.works = []
-        self.active = tdist.is_initialized() and tdist.get_world_size(group) > 1
+        self.active = tdist.is_initialized() and (tdist.get_world_size(group) > 1 or force_sync())
 
     def ready(self, name):
         if not self.active:

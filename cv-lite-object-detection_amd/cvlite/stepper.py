@@ -20,7 +20,8 @@ class GraphStepper(object):
     def _init_stepper(self, net, world, use_graph):
         self.world = world
         self.use_graph = use_graph
-        self.sync = dist.GradSync(net.store, net.grad_groups()) if world > 1 else None
+        self.sync = (dist.GradSync(net.store, net.grad_groups())
+                     if world > 1 or (dist.force_sync() and torch.distributed.is_initialized()) else None)
         self.segs = None
         self.g_up = None
 

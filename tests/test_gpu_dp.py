@@ -90,3 +90,53 @@ def test_dp_overlapped_allreduce_matches_single_process():
     e = float((got["delta"] - ref).norm() / ref.norm())
     print("DP (2 ranks x 2 images, overlapped all-reduce) vs serial shards: weight-update rel-L2 %.2e" % e)
     assert e < 1e-5
+
+
+def _nccl_worker(rank, port, out):
+    """One rank on an RCCL ("nccl") process group with the gradient all-reduce forced on: the
+    trainer captures its backward in hook-split graph segments and GradSync queues async RCCL
+    all-reduces on ProcessGroupNCCL's stream between the segment replays (the N>1 bench path)."""
+    sys.path[:0] = [ROOT, PKG]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK="0", WORLD_SIZE="1",
+                      CVL_DP_FORCE_SYNC="1")
+    import torch.distributed as tdist
+    from cvlite import dist
+    from cvlite.fcos_net import FCOSNet
+    from cvlite.train_fcos import FCOSTrainer, synthetic_batch
+    torch.cuda.set_device(0)
+    dist.init_from_env(backend="nccl")
+    assert tdist.get_backend() == "nccl"
+    net = FCOSNet(C, device=torch.device("cuda", 0), seed=0)
+    w0 = net.store.flat.clone()
+    tr = FCOSTrainer(net, BS, (D, D), world=1, use_graph=True)
+    assert tr.sync is not None and tr.sync.active
+    for i in range(2):
+        tr.load_batch(*synthetic_batch(BS, D, D, C, seed=11 + i, device="cuda"))
+        tr.step()
+    torch.cuda.synchronize()
+    torch.save({"delta": (net.store.flat - w0).cpu(), "nseg": len(tr.segs)}, out)
+    tdist.barrier()
+    tdist.destroy_process_group()
+
+
+def test_rccl_segmented_allreduce_matches_plain_step():
+    """The RCCL branch of dist.init_from_env + GradSync against HIP-graph segment replay (one GPU per
+    box, so one rank: the SUM all-reduce is the identity and the two steps must be bit-identical to
+    the same trainer without the collective path)."""
+    with tempfile.TemporaryDirectory() as td:
+        out = os.path.join(td, "nccl.pt")
+        mp.start_processes(_nccl_worker, args=(_port(), out), nprocs=1, join=True, start_method="spawn")
+        got = torch.load(out, weights_only=True)
+    from cvlite.fcos_net import FCOSNet
+    from cvlite.train_fcos import FCOSTrainer, synthetic_batch
+    net = FCOSNet(C, device=torch.device("cuda", 0), seed=0)
+    w0 = net.store.flat.clone()
+    tr = FCOSTrainer(net, BS, (D, D), world=1, use_graph=True)
+    assert tr.sync is None
+    for i in range(2):
+        tr.load_batch(*synthetic_batch(BS, D, D, C, seed=11 + i, device="cuda"))
+        tr.step()
+    torch.cuda.synchronize()
+    assert got["nseg"] == 6
+    ref = (net.store.flat - w0).cpu()
+    assert torch.equal(got["delta"], ref), float((got["delta"] - ref).abs().max())
