@@ -29,6 +29,9 @@ SIGNATURES = {
     "cvl_conv_igemm": (c_int, [P, P, P, P, P, c_size_t, P]),
     "cvl_conv_igemm_last_kernel": (c_int, []),
     "cvl_conv_kernel_name": (ctypes.c_char_p, [c_int]),
+    "cvl_probe_begin": (c_int, [P, P]),
+    "cvl_probe_end": (c_int, [P, P]),
+    "cvl_probe_clock_hz": (ctypes.c_double, []),
     "cvl_conv_wgrad_workspace_size": (c_size_t, [P]),
     "cvl_conv_wgrad": (c_int, [P, P, P, P, c_float, P, c_size_t, P]),
     "cvl_conv_wgrad_grouped_workspace_size": (c_size_t, [P, c_int]),

@@ -60,6 +60,22 @@ def conv_igemm(desc, src, dst, stats=None):
               n if ws is not None else 0, stream())
 
 
+def probe_begin(slot):
+    """Start stamp of an in-graph launch probe (slot: uint64 [3] device tensor, cvl_probe_begin)."""
+    _lib.call("cvl_probe_begin", ptr(slot), stream())
+
+
+def probe_end(slot):
+    _lib.call("cvl_probe_end", ptr(slot), stream())
+
+
+def probe_seconds(slot):
+    """Mean seconds per probed launch over every probed launch since the slot was zeroed, and the count."""
+    hz = _lib.load().cvl_probe_clock_hz()
+    ticks, n = (int(v) for v in slot[1:3].cpu().tolist())
+    return (ticks / n / hz if n and hz > 0 else None), n
+
+
 def conv_wgrad(desc, x, dy, dw, beta=0.0):
     lib = _lib.load()
     n = int(lib.cvl_conv_wgrad_workspace_size(ctypes.byref(desc)))

@@ -152,6 +152,14 @@ enum { CVL_CK_NONE = 0, CVL_CK_BASE = 1, CVL_CK_BASE_SPLITK = 2, CVL_CK_L64 = 3,
 int cvl_conv_igemm_last_kernel(void);
 const char* cvl_conv_kernel_name(int code);
 
+/* Measurement hook (no reference counterpart: bench.py's in-step roofline timing).  Launch
+ * cvl_probe_begin / cvl_probe_end around a kernel on the same stream (graph-capturable): slot[0]
+ * = start stamp, slot[1] += elapsed ticks, slot[2] += 1 (uint64 x3 device buffer, zero it first).
+ * cvl_probe_clock_hz = ticks per second of the GPU wall clock. */
+int cvl_probe_begin(uint64_t* slot, cvl_stream_t stream);
+int cvl_probe_end(uint64_t* slot, cvl_stream_t stream);
+double cvl_probe_clock_hz(void);
+
 /* Weight gradient (replaces Conv2DBackpropFilter + the per-image gradient accumulation of
  * FCOS/train_fcos.py:173-176): dw[KH][KW][Cin][n_store] (HWIO fp32) = beta*dw + sum over all
  * rows of all segments of im2col(x) * dy.  `d` is the FORWARD descriptor (its ld_dst/dst_coff
