@@ -549,6 +549,7 @@ extern "C" const char* cvl_conv_kernel_name(int code) {
     case CVL_CK_X256: return "conv_igemm_x_kernel (256x256, 4 phases per 64-deep K-tile)";
     case CVL_CK_X32: return "conv_igemm_x32_kernel (256x256, 5-slot ring of 32-deep K-tiles)";
     case CVL_CK_X32H: return "conv_igemm_x32h_kernel (256x256, 3x3 halo tile in LDS, 6-slot weight ring)";
+    case CVL_CK_WG_SN: return "conv_wgrad_sn_kernel (Npad 32, taps on the dY side, chunk slabs)";
     case CVL_CK_WG_S: return "conv_wgrad_kernel (128-wide k tile)";
     case CVL_CK_WG_L128: return "conv_wgrad_l_kernel<128> (128x256)";
     case CVL_CK_WG_L256: return "conv_wgrad_l_kernel<256> (256x256)";

@@ -276,6 +276,10 @@ long cvl_conv_wgrad_l_workspace(const cvl_conv_desc* d);
 int cvl_conv_wgrad_l(const cvl_conv_desc* d, const void* x, const void* dy, float* dw, float beta,
                      void* workspace, size_t workspace_bytes, hipStream_t s);
 
+long cvl_conv_wgrad_sn_workspace(const cvl_conv_desc* d, int ngroups);
+int cvl_conv_wgrad_sn(const cvl_conv_desc* d, int ngroups, const void* x, const void* dy, float* const* dw,
+                      float beta, void* workspace, size_t workspace_bytes, hipStream_t s);
+
 long cvl_conv_wgrad_x_workspace(const cvl_conv_desc* d, int ngroups);
 int cvl_conv_wgrad_x(const cvl_conv_desc* d, int ngroups, const void* x, const void* dy, float* const* dw,
                      float beta, void* workspace, size_t workspace_bytes, hipStream_t s);
@@ -373,6 +377,8 @@ int check_wgrad_desc(const cvl_conv_desc* d, int ngroups, const void* x, const v
 
 extern "C" size_t cvl_conv_wgrad_grouped_workspace_size(const cvl_conv_desc* d, int ngroups) {
   if (!d || ngroups < 1 || d->nseg % ngroups) return 0;
+  const long wsn = cvl_conv_wgrad_sn_workspace(d, ngroups);
+  if (wsn >= 0) return (size_t)(wsn > 16 ? wsn : 16);
   const long wx = cvl_conv_wgrad_x_workspace(d, ngroups);
   if (wx >= 0) return (size_t)wx;
   size_t m = 16;
@@ -395,6 +401,8 @@ extern "C" int cvl_conv_wgrad_grouped(const cvl_conv_desc* d, int ngroups, const
   int st = check_wgrad_desc(d, ngroups, x, dy, dw);
   if (st) return st;
   hipStream_t s = (hipStream_t)stream;
+  const int snst = cvl_conv_wgrad_sn(d, ngroups, x, dy, dw, beta, workspace, workspace_bytes, s);
+  if (snst >= 0) return snst;
   const int xst = cvl_conv_wgrad_x(d, ngroups, x, dy, dw, beta, workspace, workspace_bytes, s);
   if (xst >= 0) return xst;
   if (ngroups == 1) return wgrad_single(d, x, dy, dw[0], beta, workspace, workspace_bytes, s);

@@ -502,3 +502,122 @@ extern "C" int cvl_fcos_detect(const float* reg_pred, int ld_reg, const float* c
   hipLaunchKernelGGL(fcos_merge_kernel, dim3(B), dim3(FT), 0, S_, a);
   return cvl_launch_status();
 }
+
+// ---------------------------------------------------------------------------------------------
+// CenterNet 3x3 max-pool peak decode (BASELINE north_star's "3x3 max-pool peak decode"; the
+// reference itself thresholds every cell's max class probability and runs NMS,
+// tf_centernet_hourglass.py:566-656 = cvl_centernet_decode).  Standard CenterNet form on the same
+// model output [B][H][W][ld] (ltrb 0..3, class logits 4..4+C): a (cell, class) is a peak when its
+// sigmoid probability equals the 3x3 max-pool of that class map (-inf padding: ties keep every
+// equal cell), and it is kept when the probability >= thresh.  The K highest (probability, then
+// lower flat index cell*C + class) peaks of each image become rows (y_lo, x_lo, y_hi, x_hi, prob,
+// class) with the corners of prediction_to_corners (:355-377) in fp32 times `stride`.
+// Pass 1 (one thread per (cell, class)) appends 64-bit keys (ordered probability bits << 32 |
+// ~flat index) to a per-image list; pass 2 (one workgroup per image) takes the K largest keys in
+// K rounds of a block max below the previous key -- keys are unique, so the result is independent
+// of the append order (deterministic).  No parity anchor exists in the reference: pinned to the
+// numpy restatement (oracle/centernet_peak_ref.py), parity unpinned at the reference level.
+// ---------------------------------------------------------------------------------------------
+namespace {
+
+constexpr int PK = 1024;
+
+__device__ __forceinline__ float cn_sigmoid(float v) { return (float)(1.0 / (1.0 + exp(-(double)v))); }
+
+__global__ void __launch_bounds__(DT) peak_candidates_kernel(const float* __restrict__ pred, int ld, int H, int W,
+                                                             int C, float thresh, unsigned long long* keys,
+                                                             int32_t* n_keys) {
+  const long per = (long)H * W * C;
+  const long i = (long)blockIdx.x * DT + threadIdx.x;
+  const int b = blockIdx.y;
+  if (i >= per) return;
+  const int c = (int)(i % C);
+  const int cell = (int)(i / C);
+  const int y = cell / W, x = cell % W;
+  const float* img = pred + (long)b * H * W * ld;
+  const float p = cn_sigmoid(img[(long)cell * ld + 4 + c]);
+  if (!(p >= thresh)) return;
+  for (int dy = -1; dy <= 1; ++dy)
+    for (int dx = -1; dx <= 1; ++dx) {
+      const int yy = y + dy, xx = x + dx;
+      if ((dy == 0 && dx == 0) || yy < 0 || yy >= H || xx < 0 || xx >= W) continue;
+      if (cn_sigmoid(img[((long)yy * W + xx) * ld + 4 + c]) > p) return;
+    }
+  const int slot = atomicAdd(n_keys + b, 1);
+  // probabilities are in [0, 1]: their fp32 bit patterns order as unsigned integers
+  keys[(long)b * per + slot] = ((unsigned long long)__float_as_uint(p) << 32) | (unsigned)(~(unsigned)i);
+}
+
+__global__ void __launch_bounds__(PK) peak_select_kernel(const float* __restrict__ pred, int ld, int H, int W, int C,
+                                                         float stride, int K, const unsigned long long* keys,
+                                                         const int32_t* n_keys, double* dets, int32_t* count) {
+  const int b = blockIdx.x;
+  const long per = (long)H * W * C;
+  const int n = n_keys[b];
+  const unsigned long long* kb = keys + (long)b * per;
+  __shared__ unsigned long long red[PK / 64];
+  __shared__ unsigned long long sel;
+  unsigned long long prev = ~0ull;
+  const int kk = n < K ? n : K;
+  for (int r = 0; r < kk; ++r) {
+    unsigned long long m = 0;
+    for (int j = threadIdx.x; j < n; j += PK) {
+      const unsigned long long v = kb[j];
+      if (v < prev && v > m) m = v;
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+      const unsigned long long v = __shfl_xor(m, o);
+      m = v > m ? v : m;
+    }
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      unsigned long long t = red[0];
+      for (int w = 1; w < PK / 64; ++w) t = red[w] > t ? red[w] : t;
+      sel = t;
+      const unsigned idx = ~(unsigned)(t & 0xffffffffull);
+      const int c = (int)(idx % (unsigned)C), cell = (int)(idx / (unsigned)C);
+      const int y = cell / W, x = cell % W;
+      const float* q = pred + ((long)b * H * W + cell) * ld;
+      const float gy = (float)y + 0.5f, gx = (float)x + 0.5f;
+      double* o = dets + ((long)b * K + r) * 6;
+      o[0] = (double)(stride * (gy - q[0]));
+      o[1] = (double)(stride * (gx - q[2]));
+      o[2] = (double)(stride * (gy + q[1]));
+      o[3] = (double)(stride * (gx + q[3]));
+      o[4] = (double)__uint_as_float((unsigned)(t >> 32));
+      o[5] = (double)c;
+    }
+    __syncthreads();
+    prev = sel;
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) count[b] = kk;
+}
+
+}  // namespace
+
+extern "C" size_t cvl_centernet_peak_decode_workspace_size(int B, int H, int W, int num_classes) {
+  return (size_t)B * H * W * num_classes * sizeof(unsigned long long) + (size_t)B * sizeof(int32_t) + 256;
+}
+
+extern "C" int cvl_centernet_peak_decode(const float* pred, int ld, int B, int H, int W, int num_classes,
+                                         float stride, float thresh, int K, double* dets, int32_t* count,
+                                         void* workspace, size_t workspace_bytes, cvl_stream_t stream) {
+  CVL_CHECK_ARG(pred && dets && count && workspace && B > 0 && H > 0 && W > 0 && num_classes > 0 && K > 0);
+  CVL_CHECK_ARG(ld >= 4 + num_classes);
+  CVL_CHECK_ARG(workspace_bytes >= cvl_centernet_peak_decode_workspace_size(B, H, W, num_classes));
+  CVL_CHECK_ARG((long)H * W * num_classes < 0x7fffffffL);
+  hipStream_t s = (hipStream_t)stream;
+  unsigned long long* keys = reinterpret_cast<unsigned long long*>(workspace);
+  int32_t* nk = reinterpret_cast<int32_t*>(keys + (size_t)B * H * W * num_classes);
+  if (hipMemsetAsync(nk, 0, sizeof(int32_t) * B, s) != hipSuccess) return cvl_launch_status();
+  const long per = (long)H * W * num_classes;
+  hipLaunchKernelGGL(peak_candidates_kernel, dim3((unsigned)((per + DT - 1) / DT), B), dim3(DT), 0, s, pred, ld, H,
+                     W, num_classes, thresh, keys, nk);
+  int st = cvl_launch_status();
+  if (st) return st;
+  hipLaunchKernelGGL(peak_select_kernel, dim3(B), dim3(PK), 0, s, pred, ld, H, W, num_classes, stride, K, keys, nk,
+                     dets, count);
+  return cvl_launch_status();
+}

@@ -29,6 +29,9 @@ SIGNATURES = {
     "cvl_conv_igemm": (c_int, [P, P, P, P, P, c_size_t, P]),
     "cvl_conv_igemm_last_kernel": (c_int, []),
     "cvl_conv_kernel_name": (ctypes.c_char_p, [c_int]),
+    "cvl_centernet_peak_decode_workspace_size": (ctypes.c_size_t, [c_int, c_int, c_int, c_int]),
+    "cvl_centernet_peak_decode": (c_int, [P, c_int, c_int, c_int, c_int, c_int, c_float, c_float, c_int, P, P, P,
+                                          ctypes.c_size_t, P]),
     "cvl_probe_begin": (c_int, [P, P]),
     "cvl_probe_end": (c_int, [P, P]),
     "cvl_probe_clock_hz": (ctypes.c_double, []),

@@ -114,3 +114,28 @@ def decode_detections(pred, thresh=0.50, downsample=8, iou_thresh=0.213, img_row
     if n == 0:
         return raw, np.zeros((0, 6))
     return raw, np.array(nms(raw.copy(), iou_thresh), np.float64).reshape(-1, 6)
+
+
+def peak_detections(pred, thresh=0.3, K=100, downsample=8, num_classes=None):
+    """CenterNet 3x3 max-pool peak decode (cvl_centernet_peak_decode): pred [B, H, W, 4+C] or
+    [H, W, 4+C] model output (device or host) -> one float64 array [n <= K, 6] per image of
+    (y_lo, x_lo, y_hi, x_hi, prob, class), probability-descending; corners as
+    prediction_to_corners (tf_centernet_hourglass.py:355-377) x downsample.  The standard
+    CenterNet decode the BASELINE north_star names; the reference's own obj_detect_results decode
+    (threshold + NMS) is decode_detections."""
+    _lib.require_cuda()
+    p = torch.as_tensor(pred, dtype=torch.float32).cuda().contiguous()
+    single = p.dim() == 3
+    if single:
+        p = p.unsqueeze(0)
+    B, H, W, ld = (int(v) for v in p.shape)
+    C = ld - 4 if num_classes is None else int(num_classes)
+    ws = torch.empty(int(_lib.load().cvl_centernet_peak_decode_workspace_size(B, H, W, C)), dtype=torch.uint8,
+                     device="cuda")
+    dets = torch.zeros((B, K, 6), dtype=torch.float64, device="cuda")
+    cnt = torch.zeros(B, dtype=torch.int32, device="cuda")
+    _lib.call("cvl_centernet_peak_decode", _lib.ptr(p), ld, B, H, W, C, float(downsample), float(thresh), int(K),
+              _lib.ptr(dets), _lib.ptr(cnt), _lib.ptr(ws), ws.numel(), _lib.stream())
+    d, n = dets.cpu().numpy(), cnt.cpu().tolist()
+    out = [d[b, :n[b]] for b in range(B)]
+    return out[0] if single else out

@@ -103,11 +103,10 @@ class FCOSCenterNet(FCOSNet):
                                         (self.cen_heads, towers[0], d_cls, self.cen_col),
                                         (self.reg_heads, towers[1], d_reg, 0)):
             ld = int(dout.shape[-1])
-            for l, (h, w) in enumerate(shapes):
-                hd = heads[l]
-                d = hd.fwd_desc(B, [nn.seg(h, w, h, w, hd.wf, None, src_base=B * off[l], src_img=h * w,
-                                           dst_base=off[l], dst_img=P)], ld_dst=ld, dst_coff=coff)
-                nn.conv_wgrad(d, acts[-1], dout, hd.dw)
+            d = heads[0].fwd_desc(B, [nn.seg(h, w, h, w, heads[l].wf, None, src_base=B * off[l], src_img=h * w,
+                                             dst_base=off[l], dst_img=P) for l, (h, w) in enumerate(shapes)],
+                                  ld_dst=ld, dst_coff=coff)
+            nn.conv_wgrad_grouped(d, acts[-1], dout, [heads[l].dw for l in range(len(shapes))])
         # data gradients: cls tower from the combined class + centerness kernels over all d_cls
         # columns (pitch ld = the combined kernel's K channels); reg tower from the reg head
         ld = self._comb_ld

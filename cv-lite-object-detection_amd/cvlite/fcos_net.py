@@ -56,12 +56,12 @@ class FCOSNet(FPNDetector):
                             for l, (h, w) in enumerate(shapes)])
         for heads, acts, dout in ((self.cls_heads, towers[0], d_cls), (self.reg_heads, towers[1], d_reg)):
             ld = int(dout.shape[-1])
-            # heads: weight grads per level, data grad for all levels in one launch
-            for l, (h, w) in enumerate(shapes):
-                hd = heads[l]
-                d = hd.fwd_desc(B, [nn.seg(h, w, h, w, hd.wf, None, src_base=B * off[l], src_img=h * w,
-                                           dst_base=off[l], dst_img=P)], ld_dst=ld)
-                nn.conv_wgrad(d, acts[-1], dout, hd.dw)
+            # heads: the five levels' weight gradients as one grouped launch (one group per level,
+            # each with its own dw; small-N kernel conv_wgrad_sn), data grad for all levels in one launch
+            d = heads[0].fwd_desc(B, [nn.seg(h, w, h, w, heads[l].wf, None, src_base=B * off[l], src_img=h * w,
+                                             dst_base=off[l], dst_img=P) for l, (h, w) in enumerate(shapes)],
+                                  ld_dst=ld)
+            nn.conv_wgrad_grouped(d, acts[-1], dout, [heads[l].dw for l in range(len(shapes))])
             dA = dA_pair[len(dAs)]
             segs = [nn.seg(h, w, h, w, heads[l].wd, None, src_base=off[l], src_img=P, dst_base=B * off[l],
                            dst_img=h * w) for l, (h, w) in enumerate(shapes)]

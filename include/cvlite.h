@@ -148,7 +148,7 @@ int cvl_conv_igemm(const cvl_conv_desc* d, const void* src, void* dst, double* b
  * host thread launched.  CVL_CK_* codes; cvl_conv_kernel_name(code) is a static string. */
 enum { CVL_CK_NONE = 0, CVL_CK_BASE = 1, CVL_CK_BASE_SPLITK = 2, CVL_CK_L64 = 3, CVL_CK_L128 = 4,
        CVL_CK_L256 = 5, CVL_CK_X256 = 6, CVL_CK_X32 = 7,
-       CVL_CK_WG_S = 8, CVL_CK_WG_L128 = 9, CVL_CK_WG_L256 = 10, CVL_CK_WG_X = 11, CVL_CK_X32H = 12 };
+       CVL_CK_WG_S = 8, CVL_CK_WG_L128 = 9, CVL_CK_WG_L256 = 10, CVL_CK_WG_X = 11, CVL_CK_X32H = 12, CVL_CK_WG_SN = 13 };
 int cvl_conv_igemm_last_kernel(void);
 const char* cvl_conv_kernel_name(int code);
 
@@ -516,6 +516,19 @@ int cvl_centernet_loss(const float* pred, int ld_pred, const float* targets, int
 int cvl_centernet_decode(const float* pred, int ld, int H, int W, int num_classes, double stride, float thresh,
                          double w_ratio, double h_ratio, double img_width, double img_height, double* rows,
                          int32_t* count, cvl_stream_t stream);
+
+/* CenterNet 3x3 max-pool peak decode (the north_star's peak decode; the reference's own decode is
+ * cvl_centernet_decode above): pred [B][H][W][ld] fp32 (ltrb 0..3, class logits 4..4+C).  A
+ * (cell, class) is a peak when sigmoid(logit) equals the 3x3 max-pool of its class map (-inf
+ * padding, ties kept) and >= thresh; per image the K highest (probability desc, flat index
+ * cell*C+class asc) peaks -> dets [B][K][6] float64 = (y_lo, x_lo, y_hi, x_hi, prob, class), the
+ * corners as prediction_to_corners (tf_centernet_hourglass.py:355-377) x stride in fp32;
+ * count [B] = rows written (<= K).  Sigmoid in float64 rounded to fp32.  Deterministic.
+ * workspace >= cvl_centernet_peak_decode_workspace_size(B, H, W, C). */
+size_t cvl_centernet_peak_decode_workspace_size(int B, int H, int W, int num_classes);
+int cvl_centernet_peak_decode(const float* pred, int ld, int B, int H, int W, int num_classes, float stride,
+                              float thresh, int K, double* dets, int32_t* count, void* workspace,
+                              size_t workspace_bytes, cvl_stream_t stream);
 
 /* train_step update (:555-563) with tf.keras.optimizers.Adam (train_hourglass_voc.py:330):
  * g <- clip_by_global_norm(g * inv_bs, clip); t = *iterations + 1;

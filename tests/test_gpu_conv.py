@@ -420,3 +420,52 @@ def test_conv_wgrad_x_deterministic():
     dw0 = torch.empty((3, 3, C, C), device="cuda")
     nn.conv_wgrad(nn.make_desc(nn.FWD, B, C, 3, 3, 1, 1, 1, C, C, C, segs[:1]), x, dy, dw0)
     torch.testing.assert_close(dw0.double(), ref.permute(2, 3, 1, 0), rtol=1e-4, atol=2e-3)
+
+
+@pytest.mark.parametrize("n_store,coff,ld,B,shapes", [
+    (20, 0, 32, 3, [(24, 20), (12, 10), (6, 5), (3, 3), (2, 1)]),      # cls head, ragged levels
+    (5, 0, 32, 2, [(16, 16), (8, 8), (4, 4), (2, 2), (1, 1)]),          # reg head (t, b, l, r, cen)
+    (1, 24, 64, 2, [(9, 7), (5, 4), (3, 2), (2, 1), (1, 1)]),           # centerness column of the cls rows
+    (20, 0, 32, 16, [(64, 64), (32, 32), (16, 16), (8, 8), (4, 4)]),    # bench geometry (bs 16, 512)
+])
+def test_conv_wgrad_small_n_heads_grouped(n_store, coff, ld, B, shapes):
+    """The five per-level FCOS head weight gradients (fcos.py:92-110: 3x3 'same', 256 -> n_store, own
+    weights per level) as ONE grouped call (group = level): the small-N kernel conv_wgrad_sn
+    (taps on the dY side, deterministic chunk-slab reduction) vs torch fp64 per level, with
+    beta accumulation; a second run is bit-identical."""
+    from cvlite import _lib, ops_nn as nn
+    C = 256
+    off, o = [], 0
+    for h, w in shapes:
+        off.append(o)
+        o += h * w
+    P = o
+    g = torch.Generator().manual_seed(7 + n_store)
+    x = rnd(B * P, C, gen=g)                                   # packed level-major [sum_l B*h*w, C]
+    dy = rnd(B * P, ld, gen=g)                                 # image-major [B, P, ld] loss gradient
+    dy[:, coff + n_store:] = 0.0                               # (padding columns are zero in the model)
+    wf = [torch.empty((32, 9 * C), dtype=BF, device="cuda") for _ in shapes]
+    segs = [nn.seg(h, w, h, w, wf[l], None, src_base=B * off[l], src_img=h * w, dst_base=off[l], dst_img=P)
+            for l, (h, w) in enumerate(shapes)]
+    d = nn.make_desc(nn.FWD, B, C, 3, 3, 1, 1, 1, 32, n_store, ld, segs, dst_coff=coff)
+    xg, dyg = x.to(BF).cuda(), dy.to(BF).cuda()
+    outs = []
+    for _ in range(2):
+        dws = [torch.full((3, 3, C, n_store), 0.5, device="cuda") for _ in shapes]
+        nn.conv_wgrad_grouped(d, xg, dyg, dws, beta=1.0)
+        code = _lib.load().cvl_conv_igemm_last_kernel()
+        assert code == 13, _lib.load().cvl_conv_kernel_name(code).decode()
+        outs.append(torch.stack([t.flatten() for t in dws]))
+    assert torch.equal(outs[0], outs[1])
+    dyi = dy.view(B, P, ld)
+    for l, (h, w) in enumerate(shapes):
+        xm = x[B * off[l]:B * (off[l] + h * w)].reshape(B, h, w, C)
+        ns = max(n_store, 2)                                   # (torch's fp64 CPU conv wants >= 2 outputs)
+        dm = torch.zeros(B, h * w, ns, dtype=torch.float64)
+        dm[..., :n_store] = dyi[:, off[l]:off[l] + h * w, coff:coff + n_store]
+        wl = torch.zeros(3, 3, C, ns, dtype=torch.float64, requires_grad=True)
+        ref_conv(xm, wl, None, 1, "same").backward(dm.view(B, h, w, ns))
+        exp = wl.grad[..., :n_store] + 0.5
+        got = outs[0][l].view(3, 3, C, n_store).double().cpu()
+        scale = (exp - 0.5).abs().max().item()
+        torch.testing.assert_close(got, exp, rtol=1e-4, atol=1e-5 * scale, msg=lambda m: "level %d: %s" % (l, m))

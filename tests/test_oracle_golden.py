@@ -234,3 +234,33 @@ def test_centernet_s8_targets_and_loss(golden):
     assert hits > 100
     pred = np.concatenate([1.0 / (1.0 + np.exp(-d["loss_reg_logits"].astype(np.float64))), d["loss_cls_logits"]], -1)
     np.testing.assert_allclose(s8.model_loss(d["loss_y"], pred), d["loss_out"], rtol=1e-5)
+
+
+def test_centernet_peak_decode_restatement_known_answer():
+    """oracle/centernet_peak_ref.py on a hand-made 5x5, 2-class map: local maxima only (3x3, ties on a
+    plateau all kept), threshold, probability-descending order with flat-index tie break, K cut,
+    prediction_to_corners boxes (tf_centernet_hourglass.py:355-377).  No reference implementation
+    exists (the reference decodes by threshold + NMS): parity unpinned at the reference level."""
+    import numpy as np
+    from oracle.centernet_peak_ref import peak_decode
+    H, W, C = 5, 5, 2
+    pred = np.zeros((H, W, 4 + C), np.float32)
+    pred[..., :4] = [1.0, 2.0, 3.0, 4.0]                    # (top, bottom, left, right) in cells
+    cls0 = np.full((H, W), -6.0, np.float32)
+    cls0[1, 1] = 2.0                                         # isolated peak
+    cls0[1, 2] = 1.0                                         # its neighbour: suppressed
+    cls0[3, 3] = cls0[3, 4] = 0.5                            # plateau: both kept
+    cls0[4, 0] = -3.0                                        # a local max below thresh
+    cls1 = np.full((H, W), -6.0, np.float32)
+    cls1[1, 1] = 2.0                                         # same prob as class 0 at (1,1)
+    pred[..., 4], pred[..., 5] = cls0, cls1
+    rows = peak_decode(pred, C, stride=8, thresh=0.3, K=10)
+    # order: (1,1) c0 [idx 12], (1,1) c1 [idx 13], then the plateau (3,3) [36], (3,4) [38]
+    assert rows.shape == (4, 6)
+    np.testing.assert_array_equal(rows[:, 5], [0, 1, 0, 0])
+    np.testing.assert_allclose(rows[0, :4], [8 * (1.5 - 1), 8 * (1.5 - 3), 8 * (1.5 + 2), 8 * (1.5 + 4)])
+    np.testing.assert_allclose(rows[2, :4], [8 * (3.5 - 1), 8 * (3.5 - 3), 8 * (3.5 + 2), 8 * (3.5 + 4)])
+    np.testing.assert_allclose(rows[3, :4], [8 * (3.5 - 1), 8 * (4.5 - 3), 8 * (3.5 + 2), 8 * (4.5 + 4)])
+    np.testing.assert_allclose(rows[:, 4], 1 / (1 + np.exp(-np.array([2.0, 2.0, 0.5, 0.5]))), rtol=1e-6)
+    assert len(peak_decode(pred, C, 8, 0.3, K=1)) == 1
+    assert len(peak_decode(pred, C, 8, 0.99, K=10)) == 0
