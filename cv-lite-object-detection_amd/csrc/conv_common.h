@@ -74,6 +74,25 @@ struct ConvArgs {
   int dbg;            // kernel ablation bits for measurement (CVL_X_ABLATE), 0 in production
   int dst_up, dst_w;  // output pixel (y, x) of the GEMM grid lands at (y*dst_up, x*dst_up) of a
                       // dst_w-wide map (1x1 strided data-gradient as a dense GEMM); 1 = identity
+  // BN-backward first pass fused into a data-gradient epilogue (cvl_conv_igemm_dgrad_bnsum): the
+  // result is dy of a BN -> ReLU unit whose pre-BN z / (mean, rstd) / gamma / beta are given;
+  // bsum[img][c] += (sum g, sum g * xhat), g = dy * (0 < bn(z) < bhi).  bsum null = off.
+  const cvl_bf16* bz;
+  const float* bmr;
+  const float* bga;
+  const float* bbe;
+  double* bsum;
+  float bhi;
+};
+
+// host-side bundle of the fused BN-backward sums arguments (cvl_conv_igemm_dgrad_bnsum)
+struct BnSumArgs {
+  const cvl_bf16* z;
+  const float* mr;
+  const float* gamma;
+  const float* beta;
+  double* sums;
+  float hi;
 };
 
 // destination row of GEMM row q (within image img) of segment S
@@ -100,6 +119,7 @@ static inline int cvl_conv_prepare(const cvl_conv_desc* d, int bm, ConvArgs* a) 
   a->dst_up = 1;
   a->dst_w = 0;
   a->dbg = 0;
+  a->bz = nullptr; a->bmr = nullptr; a->bga = nullptr; a->bbe = nullptr; a->bsum = nullptr; a->bhi = 0.f;
   a->nseg = d->nseg;
   a->B = d->B;
   a->Cin = d->Cin; a->KH = d->KH; a->KW = d->KW; a->stride = d->stride;

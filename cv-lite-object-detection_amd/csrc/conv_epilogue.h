@@ -6,10 +6,52 @@
 #pragma once
 #include "conv_common.h"
 
-template <int BN, int WGM, int TM, int TN, int NT>
+// z chunks of the fused BN-backward sums (a.bsum; 64/128-wide tiles): thread tid's fixed 8-channel
+// chunk of the rows it stores in the epilogue.  The kernel fetches them at its start, so their
+// latency hides behind the main loop (the counted ring waits only ever wait for them early).
+template <int BN, int NT>
+struct BnSumPre {
+  static constexpr int N = BN <= 128 ? 256 * (BN / 8) / NT : 1;
+};
+
+// per-channel (mean, rstd, gamma, beta) of the thread's 8 channels, also fetched at kernel start
+struct BnSumPar {
+  float m[8], rs[8], ga[8], be[8];
+};
+
+template <int BN, int NT>
+__device__ __forceinline__ void bnsum_prefetch(const ConvArgs& a, const ConvSeg& S, int tid, int n0, int mloc0,
+                                               s16x8 (&zpre)[BnSumPre<BN, NT>::N], BnSumPar& par) {
+  if constexpr (BN <= 128) {
+    if (a.bsum) {
+      constexpr int CCH = BN / 8;
+      const int cb = n0 + (tid % CCH) * 8;
+      const int bimg = mloc0 / (S.Hr * S.Wr);
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int c = cb + u < a.n_store ? cb + u : a.n_store - 1;
+        const long bc = (long)bimg * a.n_store + c;
+        par.m[u] = a.bmr[bc * 2];
+        par.rs[u] = a.bmr[bc * 2 + 1];
+        par.ga[u] = a.bga[c];
+        par.be[u] = a.bbe[c];
+      }
+#pragma unroll
+      for (int k = 0; k < BnSumPre<BN, NT>::N; ++k) {
+        const int ml = mloc0 + tid / CCH + k * (NT / CCH);
+        zpre[k] = s16x8{0, 0, 0, 0, 0, 0, 0, 0};
+        if (ml < S.rows && cb < a.n_store)
+          zpre[k] = *reinterpret_cast<const s16x8*>(a.bz + (S.dst_base + ml) * a.ld_dst + a.dst_coff + cb);
+      }
+    }
+  }
+}
+
+template <int BN, int WGM, int TM, int TN, int NT, bool BS = false>
 __device__ __forceinline__ void conv_l_epilogue(const ConvArgs& a, const ConvSeg& S, f32x4 (&acc)[TM][TN],
                                                 cvl_bf16* lds, int tid, int wm, int wn, int n0, int mloc0,
-                                                int HWr) {
+                                                int HWr, const s16x8 (&zpre)[BnSumPre<BN, NT>::N],
+                                                const BnSumPar& par) {
   constexpr int BM = 256;
   constexpr int WGN = 8 / WGM;
   constexpr int WM = BM / WGM, WN = BN / WGN;
@@ -103,6 +145,20 @@ __device__ __forceinline__ void conv_l_epilogue(const ConvArgs& a, const ConvSeg
 
   wait_vm<0>();
   __syncthreads();
+  // fused BN-backward sums (a.bsum, 64/128-wide tiles only): a thread's 8-channel chunk is fixed
+  // over the store loop (NT % CCH == 0) and the tile is one image (host: H*W % 256 == 0, dense
+  // rows), so its per-channel parameters load once; its z chunks arrive prefetched (zpre)
+  constexpr int CCH = BN / 8;
+  constexpr int ITER = BM * CCH / NT;
+  static_assert(NT % CCH == 0 && (BM * CCH) % NT == 0, "fixed channel chunk per thread");
+  constexpr bool kBs = BS && BN <= 128;           // a separate kernel instantiation (BSUM)
+  const bool bsum = kBs && a.bsum != nullptr;
+  static_assert(!kBs || ITER == BnSumPre<BN, NT>::N, "prefetch layout");
+  float bs1[8], bs2[8];
+  const int bimg = mloc0 / HWr;
+#pragma unroll
+  for (int u = 0; u < 8; ++u) { bs1[u] = 0.f; bs2[u] = 0.f; }
+
   constexpr int CP = BN + 8;
   cvl_bf16* Cs = lds;
 #pragma unroll
@@ -142,12 +198,13 @@ __device__ __forceinline__ void conv_l_epilogue(const ConvArgs& a, const ConvSeg
     atomicAdd(st, (double)s1);
     atomicAdd(st + 1, (double)s2);
   }
-  constexpr int CCH = BN / 8;
   cvl_bf16* dst = reinterpret_cast<cvl_bf16*>(a.dst);
   // destination rows are the segment's rows in order (no channel interleave of images, no
   // stride-2 scatter): the row index is base + ml, no per-row division
   const bool dense = a.dst_up == 1 && S.dst_img == (long)HWr;
-  for (int idx = tid; idx < BM * CCH; idx += NT) {
+#pragma unroll
+  for (int k = 0; k < ITER; ++k) {
+    const int idx = tid + k * NT;
     const int r = idx / CCH, c8 = (idx - (idx / CCH) * CCH) * 8;
     const int ml = mloc0 + r;
     if (ml >= S.rows || n0 + c8 >= a.n_store) continue;
@@ -160,6 +217,18 @@ __device__ __forceinline__ void conv_l_epilogue(const ConvArgs& a, const ConvSeg
     }
     s16x8 v = *reinterpret_cast<const s16x8*>(Cs + r * CP + c8);
     s16x8* pd = reinterpret_cast<s16x8*>(dst + drow * a.ld_dst + a.dst_coff + n0 + c8);
+    if (bsum) {        // g = dy * ReLU mask rebuilt from z (exactly the forward's bn_affine value)
+      const s16x8 zv = zpre[kBs ? k : 0];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const float zf = bf16_to_f32((cvl_bf16)zv[u]);
+        const float xh = (zf - par.m[u]) * par.rs[u];
+        const float af = __builtin_fmaf(par.ga[u], xh, par.be[u]);
+        const float g = (af > 0.f && af < a.bhi) ? bf16_to_f32((cvl_bf16)v[u]) : 0.f;
+        bs1[u] += g;
+        bs2[u] += g * xh;
+      }
+    }
     if (a.beta != 0.f) {
       const s16x8 o = *pd;
 #pragma unroll
@@ -167,5 +236,38 @@ __device__ __forceinline__ void conv_l_epilogue(const ConvArgs& a, const ConvSeg
         v[u] = (short)f32_to_bf16(bf16_to_f32((cvl_bf16)v[u]) + a.beta * bf16_to_f32((cvl_bf16)o[u]));
     }
     *pd = v;
+  }
+  if (bsum) {          // the NT / CCH threads of a channel chunk, summed in a fixed order:
+    // lanes l, l + CCH, ... of a wave by xor shuffles, then the NT / 64 waves through LDS
+#pragma unroll
+    for (int o = CCH; o < 64; o <<= 1)
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        bs1[u] += __shfl_xor(bs1[u], o, 64);
+        bs2[u] += __shfl_xor(bs2[u], o, 64);
+      }
+    __syncthreads();
+    float* red = reinterpret_cast<float*>(lds);                // [NT / 64][CCH][16]
+    const int wv = tid >> 6, ln = tid & 63;
+    if (ln < CCH) {
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        red[(wv * CCH + ln) * 16 + u] = bs1[u];
+        red[(wv * CCH + ln) * 16 + 8 + u] = bs2[u];
+      }
+    }
+    __syncthreads();
+    if (tid < BN && n0 + tid < a.n_store) {
+      const int c8 = tid / 8, u = tid % 8;
+      float t1 = 0.f, t2 = 0.f;
+#pragma unroll
+      for (int w = 0; w < NT / 64; ++w) {
+        t1 += red[(w * CCH + c8) * 16 + u];
+        t2 += red[(w * CCH + c8) * 16 + 8 + u];
+      }
+      double* st = a.bsum + ((long)bimg * a.n_store + n0 + tid) * 2;
+      atomicAdd(st, (double)t1);
+      atomicAdd(st + 1, (double)t2);
+    }
   }
 }

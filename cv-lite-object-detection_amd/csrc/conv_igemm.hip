@@ -496,7 +496,7 @@ static inline int pick_bn(int npad) { return npad % 128 == 0 ? 128 : (npad % 64 
 }  // namespace
 
 int cvl_conv_igemm_l(const cvl_conv_desc* d, int dst_up, int dst_w, const void* src, void* dst, double* bn_stats,
-                     hipStream_t s);
+                     hipStream_t s, const BnSumArgs* bsum = nullptr);
 
 // 1x1 strided data-gradient: only every stride-th dX pixel receives a gradient, so instead of a
 // DGRAD gather that finds no valid tap for (s^2-1)/s^2 of the rows, run a dense 1x1 GEMM over the
@@ -622,4 +622,35 @@ extern "C" int cvl_conv_igemm(const cvl_conv_desc* d, const void* src, void* dst
   if (bn == 128) return launch_bn<128>(a, dg, s);
   if (bn == 64) return launch_bn<64>(a, dg, s);
   return launch_bn<32>(a, dg, s);
+}
+
+// Data gradient whose epilogue also forms the first pass of the NEXT BN's backward (the dgrad
+// result is dy of a BN -> ReLU unit without a residual): sums[img][c] += (sum g, sum g*xhat).
+// Taken when the 256-row LDS-DMA kernel runs the launch with one image per tile; otherwise the
+// plain data gradient runs and *fused = 0 (the caller then runs the two-pass BN backward).
+extern "C" int cvl_conv_igemm_dgrad_bnsum(const cvl_conv_desc* d, const void* src, void* dst, const void* z,
+                                          const float* mean_rstd, const float* gamma, const float* beta, float act_hi,
+                                          double* sums, int32_t* fused, void* workspace, size_t workspace_bytes,
+                                          cvl_stream_t stream) {
+  CVL_CHECK_ARG(d && fused && z && mean_rstd && gamma && beta && sums);
+  *fused = 0;
+  if (!cvl_env_flag("CVL_NO_BNSUM_FUSE") && d->mode == CVL_CONV_DGRAD && !d->dst_f32 && d->beta == 0.f &&
+      d->Cin % 32 == 0 && d->Npad % 32 == 0 && d->ld_dst % 8 == 0 && d->dst_coff % 8 == 0 && d->n_store % 8 == 0 &&
+      src && dst) {
+    cvl_conv_desc dd;
+    int up = 1, upw = 0;
+    if (!s2dgrad_transform(d, &dd, &up, &upw)) {
+      ConvArgs chk;
+      if (cvl_conv_prepare(d, BM, &chk) == CVL_OK) {
+        const BnSumArgs b{reinterpret_cast<const cvl_bf16*>(z), mean_rstd, gamma, beta, sums, act_hi};
+        g_cvl_conv_last_kernel = CVL_CK_NONE;
+        const int lst = cvl_conv_igemm_l(d, 1, 0, src, dst, nullptr, (hipStream_t)stream, &b);
+        if (lst >= 0) {
+          *fused = lst == CVL_OK ? 1 : 0;
+          return lst;
+        }
+      }
+    }
+  }
+  return cvl_conv_igemm(d, src, dst, nullptr, workspace, workspace_bytes, stream);
 }

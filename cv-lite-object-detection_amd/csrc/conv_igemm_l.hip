@@ -33,7 +33,7 @@ __device__ __forceinline__ void glds16(const void* g, void* l) {
 // BN x WGM x NST: 128/64-wide tiles run 8 waves as 4 (M) x 2 (N) with a 3-deep ring; the
 // 256-wide tile runs them as 2 x 4 (each wave 128 x 64: a quarter fewer LDS bytes per MFMA and
 // half the DMA issues per FLOP) with a 2-deep ring (2 x 64 KiB).
-template <int BN, int WGM, int NST, bool DGRAD, bool PRIO>
+template <int BN, int WGM, int NST, bool DGRAD, bool PRIO, bool BSUM = false>
 __global__ void __launch_bounds__(NT) conv_igemm_l_kernel(ConvArgs a) {
   constexpr int WGN = 8 / WGM;
   constexpr int WM = BM / WGM, WN = BN / WGN;
@@ -62,6 +62,10 @@ __global__ void __launch_bounds__(NT) conv_igemm_l_kernel(ConvArgs a) {
   const int HWr = S.Hr * S.Wr;
   const int mloc0 = m0 - S.m_start;
   if (mloc0 >= S.rows) return;
+  // z chunks of the fused BN-backward sums, fetched now so the main loop hides their latency
+  s16x8 zpre[BnSumPre<BN, NT>::N];
+  BnSumPar bpar;
+  if constexpr (BSUM) bnsum_prefetch<BN, NT>(a, S, tid, n0, mloc0, zpre, bpar);
 
   // piece p of this thread: row p*64 + wave*8 + lane/8, chunk lane%8 (lane-linear 1 KiB image)
   const int prow = wave * 8 + (lane >> 3), ch = lane & 7;
@@ -182,7 +186,7 @@ __global__ void __launch_bounds__(NT) conv_igemm_l_kernel(ConvArgs a) {
     slot = slot == NST - 1 ? 0 : slot + 1;
   }
 
-  conv_l_epilogue<BN, WGM, TM, TN, NT>(a, S, acc, lds, tid, wm, wn, n0, mloc0, HWr);
+  conv_l_epilogue<BN, WGM, TM, TN, NT, BSUM>(a, S, acc, lds, tid, wm, wn, n0, mloc0, HWr, zpre, bpar);
 }
 
 }  // namespace
@@ -192,8 +196,9 @@ int cvl_conv_igemm_x(const cvl_conv_desc* d, const ConvArgs& a, hipStream_t s);
 // Called by cvl_conv_igemm when the launch qualifies (see cvl_conv_igemm_l_ok); returns -1 when
 // it does not, so the caller falls back to the 128-row kernel.
 int cvl_conv_igemm_l(const cvl_conv_desc* d, int dst_up, int dst_w, const void* src, void* dst, double* bn_stats,
-                     hipStream_t s) {
+                     hipStream_t s, const BnSumArgs* bsum) {
   if (cvl_env_flag("CVL_CONV_NO_L")) return -1;
+  if (bsum && (d->mode != CVL_CONV_DGRAD || d->dst_f32 || d->beta != 0.f || dst_up != 1 || bn_stats)) return -1;
   if (d->Cin % 64 != 0 || d->relu_in || d->n_store % 8 || (d->dst_f32 && bn_stats) ||
       (!d->dst_f32 && (d->ld_dst % 8 || d->dst_coff % 8)) || (d->dst_f32 && cvl_env_flag("CVL_CONV_L_NO_F32")))
     return -1;
@@ -220,6 +225,13 @@ int cvl_conv_igemm_l(const cvl_conv_desc* d, int dst_up, int dst_w, const void* 
   if (bn_stats)
     for (int i = 0; i < a.nseg; ++i)
       if ((a.seg[i].Hr * a.seg[i].Wr) % 4) return -1;
+  if (bsum) {          // one image per 256-row tile; the 256-wide tiles keep their own epilogue budget
+    if (use_bn == 256) return -1;
+    for (int i = 0; i < a.nseg; ++i)
+      if ((a.seg[i].Hr * a.seg[i].Wr) % BM || a.seg[i].dst_img != (long)a.seg[i].Hr * a.seg[i].Wr) return -1;
+    a.bz = bsum->z; a.bmr = bsum->mr; a.bga = bsum->gamma; a.bbe = bsum->beta; a.bsum = bsum->sums;
+    a.bhi = bsum->hi;
+  }
   a.src = reinterpret_cast<const cvl_bf16*>(src);
   a.dst = dst;
   a.stats = bn_stats;
@@ -228,7 +240,9 @@ int cvl_conv_igemm_l(const cvl_conv_desc* d, int dst_up, int dst_w, const void* 
   const bool prio = !cvl_env_flag("CVL_CONV_NO_PRIO");
 #define CVL_L_LAUNCH(BN_, WGM_, NST_)                                                                          \
   do {                                                                                                         \
-    if (dg) {                                                                                                  \
+    if (dg && a.bsum) {                                                                                        \
+      hipLaunchKernelGGL((conv_igemm_l_kernel<BN_, WGM_, NST_, true, true, true>), grid, dim3(NT), 0, s, a);     \
+    } else if (dg) {                                                                                           \
       if (prio) hipLaunchKernelGGL((conv_igemm_l_kernel<BN_, WGM_, NST_, true, true>), grid, dim3(NT), 0, s, a);   \
       else hipLaunchKernelGGL((conv_igemm_l_kernel<BN_, WGM_, NST_, true, false>), grid, dim3(NT), 0, s, a);       \
     } else {                                                                                                   \

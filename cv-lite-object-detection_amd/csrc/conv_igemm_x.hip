@@ -254,7 +254,8 @@ __global__ void __launch_bounds__(NT) conv_igemm_x_kernel(ConvArgs a) {
     if (acc[0][0][0] == 12345.f) a.stats[0] = 1.0;      // keep the accumulators live
     return;
   }
-  conv_l_epilogue<BN, WGM, TM, TN, NT>(a, S, acc, lds, tid, wm, wn, n0, mloc0, HWr);
+  const s16x8 znone[1] = {s16x8{0, 0, 0, 0, 0, 0, 0, 0}};     // (256-wide tiles: no fused BN sums)
+  conv_l_epilogue<BN, WGM, TM, TN, NT>(a, S, acc, lds, tid, wm, wn, n0, mloc0, HWr, znone, BnSumPar{});
 }
 
 
@@ -405,7 +406,8 @@ __global__ void __launch_bounds__(NT) conv_igemm_x32_kernel(ConvArgs a) {
   }
   if (wm == 0) bar();           // equal barrier counts for both groups
   wait_vm<0>();
-  conv_l_epilogue<BN, WGM, TM, TN, NT>(a, S, acc, lds, tid, wm, wn, n0, mloc0, HWr);
+  const s16x8 znone[1] = {s16x8{0, 0, 0, 0, 0, 0, 0, 0}};     // (256-wide tiles: no fused BN sums)
+  conv_l_epilogue<BN, WGM, TM, TN, NT>(a, S, acc, lds, tid, wm, wn, n0, mloc0, HWr, znone, BnSumPar{});
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -655,7 +657,8 @@ __global__ void __launch_bounds__(NT) conv_igemm_x32h_kernel(ConvArgs a) {
     if (acc[0][0][0] == 12345.f) a.stats[0] = 1.0;      // keep the accumulators live
     return;
   }
-  conv_l_epilogue<BN, WGM, TM, TN, NT>(a, S, acc, lds, tid, wm, wn, n0, mloc0, HWr);
+  const s16x8 znone[1] = {s16x8{0, 0, 0, 0, 0, 0, 0, 0}};     // (256-wide tiles: no fused BN sums)
+  conv_l_epilogue<BN, WGM, TM, TN, NT>(a, S, acc, lds, tid, wm, wn, n0, mloc0, HWr, znone, BnSumPar{});
 }
 
 // Geometry the halo kernel covers: 3x3, stride 1, pad 1, source map = output map, and every

@@ -1169,6 +1169,23 @@ extern "C" int cvl_bn_backward_relu6(const void* dy, const void* z, const float*
                           dbeta, beta_acc, conv_dbias, B, HW, C, stream, 6.0f);
 }
 
+// Second pass only, from (sum g, sum g*xhat) per (image, channel) that the producing data-gradient
+// epilogue formed (cvl_conv_igemm_dgrad_bnsum): BN -> ReLU (act_hi = INF) or ReLU6 (act_hi = 6)
+// unit without a residual, mask rebuilt from z.
+extern "C" int cvl_bn_backward_relu_sums(const void* dy, const void* z, const float* mean_rstd, const float* gamma,
+                                         const float* beta, const double* sums, void* dz, float* dgamma,
+                                         float* dbeta, float beta_acc, float* conv_dbias, float act_hi, int B,
+                                         int HW, int C, cvl_stream_t stream) {
+  CVL_CHECK_ARG(dy && z && mean_rstd && gamma && beta && sums && dz && dgamma && dbeta && C % 8 == 0);
+  CVL_CHECK_ARG(B > 0 && HW > 0);
+  const int rpb = bn_bwd_rows_per_blk(B, HW, C);
+  const int nchunk = (HW + rpb - 1) / rpb;
+  hipLaunchKernelGGL(bn_bwd_kernel<1>, dim3(nchunk, B), dim3(NT), 0, S_, (const cvl_bf16*)dy, (const cvl_bf16*)nullptr,
+                     (const cvl_bf16*)z, mean_rstd, gamma, sums, (cvl_bf16*)dz, (cvl_bf16*)nullptr, (float*)nullptr,
+                     C, HW, rpb, 1, 0.f, BnPG{dgamma, dbeta, conv_dbias, beta_acc}, beta, act_hi);
+  return cvl_launch_status();
+}
+
 extern "C" int cvl_maxpool3x3s2(const void* x, void* y, uint8_t* argmax, int B, int H, int W, int C,
                                 cvl_stream_t stream) {
   CVL_CHECK_ARG(x && y && argmax && C % 8 == 0);

@@ -3,6 +3,8 @@
   random_flip_horizontal(image, boxes, p_flip=0.5)                  data_preprocess.py:24-39
   resize_and_pad_image(image, jitter, min_side, max_side, stride, equal_dims)   :41-96
   preprocess_image(image, ..., flip, out)                           fused flip + resize + pad
+  preprocess_data(sample)                                           :98-133 (one training sample)
+  box_targets(bbox, flip)                                           flip + swap_xy + convert_to_xywh
 
 The resize / normalise / pad (and the flip, when fused) run in one cvl_resize_pad_normalize
 launch per image that can write straight into a slot of the device batch.  JPEG decode
@@ -69,3 +71,40 @@ def random_flip_horizontal(image, boxes, p_flip=0.5, rng=None):
         b = np.asarray(boxes, f32)
         return torch.flip(img, dims=[1]), np.stack([f32(1.0) - b[:, 2], b[:, 1], f32(1.0) - b[:, 0], b[:, 3]], -1)
     return image, boxes
+
+
+def box_targets(bbox, flip):
+    """The box half of preprocess_data (data_preprocess.py:120-131) in the reference's fp32 order:
+    random_flip_horizontal's box map [b0, b1, b2, b3] -> [1-b2, b1, 1-b0, b3] when flipped
+    (:36-39), utils.swap_xy (:5-13), utils.convert_to_xywh (:15-27)."""
+    b = np.asarray(bbox, f32).reshape(-1, 4)
+    if flip:
+        b = np.stack([f32(1.0) - b[:, 2], b[:, 1], f32(1.0) - b[:, 0], b[:, 3]], -1)
+    s = np.stack([b[:, 1], b[:, 0], b[:, 3], b[:, 2]], -1)
+    return np.concatenate([(s[:, :2] + s[:, 2:]) / f32(2.0), s[:, 2:] - s[:, :2]], -1).astype(f32)
+
+
+def preprocess_data(sample, rng=None, out=None):
+    """data_preprocess.py:98-133 preprocess_data (pad_flag=True) for one sample dict with the
+    reference's keys: image (a DECODED [H,W,3] image, uint8 or fp32, host or device -- the JPEG
+    decode of `_parse_image` is outside this tier), objects = {bbox [N,4] normalised, label [N]},
+    l_jitter / u_jitter, min_side, max_side.  Returns (image_padded [Hp,Wp,3] fp32 on the GPU,
+    bbox [N,4] (the reference's xywh of the swapped corners), class_id [N] int32, img_shp [2] fp32 =
+    the unpadded resized shape).  The flip draw (p = 0.5) and the jitter draw use `rng` (numpy) in
+    the reference's order: flip first, then the jitter size."""
+    rng = rng if rng is not None else np.random.default_rng()
+    jitter = [sample["l_jitter"], sample["u_jitter"]]
+    flip = bool(rng.uniform() <= 0.5)
+    img, new_shape, _ = preprocess_image(sample["image"], jitter=jitter, min_side=sample["min_side"],
+                                         max_side=sample["max_side"], flip=flip, out=out, rng=rng)
+    bbox = box_targets(sample["objects"]["bbox"], flip)
+    cls = np.asarray(sample["objects"]["label"], np.int32).reshape(-1)
+    return img, bbox, cls, np.asarray(new_shape, f32)
+
+
+def padded_size(sample_hw, jitter, min_side, max_side, rng, stride=128.0):
+    """Host-only size plan of preprocess_data (the padded square side and new_shape) for the same
+    rng draw order (flip, then jitter): used to bucket a batch before any image moves."""
+    flip = bool(rng.uniform() <= 0.5)
+    new_shape, _, ph, pw = _plan(sample_hw[0], sample_hw[1], jitter, min_side, max_side, stride, True, rng)
+    return flip, new_shape, ph

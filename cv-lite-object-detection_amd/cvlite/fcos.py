@@ -73,7 +73,8 @@ class FCOSModel(object):
 
 
 def build_model(num_classes, backbone_model="resnet50"):
-    """fcos.py:6-110 (ResNet-50 backbone; MobileNetV2 is outside this tier)."""
+    """fcos.py:6-110 (backbone_model "resnet50" -> ResNet-50, anything else -> MobileNetV2 as the
+    reference)."""
     return FCOSModel(num_classes, backbone_model=backbone_model)
 
 

@@ -9,6 +9,8 @@ names of the reference graph (e.g. `conv2_block1_1_conv/kernel`, `cls_layer_1/ke
 """
 import math
 
+import os
+
 import torch
 
 from . import ops_nn as nn
@@ -203,13 +205,28 @@ class Conv(object):
     def cout_pad_ld(self, dy):
         return int(dy.shape[-1])
 
-    def dgrad(self, dy, B, H, W, out=None, beta=0.0):
+    def dgrad(self, dy, B, H, W, out=None, beta=0.0, bn_next=None):
+        """dX (= out, beta accumulate).  bn_next = (z, mean_rstd, gamma, beta, zeroed sums or None) of the BN -> ReLU unit
+        whose dy this is: returns (dX, sums) with that BN backward's first pass fused into the
+        epilogue (sums None when the launch could not fuse)."""
         Ho, Wo, _, _ = self.out_hw(H, W)
         if out is None:
             out = torch.empty((B, H, W, self.cin), dtype=BF16, device=dy.device)
         d = self.dgrad_desc(B, [nn.seg(H, W, Ho, Wo, self.wd)], ld_dst=self.cin, beta=beta)
-        nn.conv_igemm(d, dy, out)
-        return out
+        if bn_next is None:
+            nn.conv_igemm(d, dy, out)
+            return out
+        z, mr, ga, be, sums = bn_next
+        zero = sums is None
+        if zero:
+            sums = torch.empty((B, self.cin, 2), dtype=torch.float64, device=dy.device)
+        fused = nn.conv_igemm_dgrad_bnsum(d, dy, out, z, mr, ga, be, sums, zero=zero)
+        return out, (sums if fused else None)
+
+
+# the BN backward's first pass fused into the producing data gradient (CVL_NO_BNSUM_FUSE=1: off,
+# for A/B measurement)
+FUSE_BNSUM = os.environ.get("CVL_NO_BNSUM_FUSE", "0") != "1"
 
 
 class StatsArena(object):
@@ -292,12 +309,29 @@ class ConvBN(object):
         y, mr = self.bn.normalize(z, stats, B, Ho * Wo, relu, residual=residual, train=train)
         return y, (x, z, y, mr, B, H, W, Ho, Wo, relu, residual is not None)
 
-    def backward(self, dy, saved, dx_out=None, dx_beta=0.0, g_out=None, need_dx=True):
+    def bn_next_ctx(self, saved, arena=None):
+        """What a producer of this unit's dy needs to fuse the BN backward's first pass into its
+        data-gradient epilogue (conv_igemm_dgrad_bnsum); None unless BN -> ReLU without residual.
+        The sums buffer comes zeroed from the step's StatsArena when one is given."""
+        x, z, y, mr, B, H, W, Ho, Wo, relu, has_res = saved
+        if not relu or has_res or not FUSE_BNSUM:
+            return None
+        return (z, mr, self.bn.gamma, self.bn.beta, arena.take(B, self.bn.c) if arena is not None else None)
+
+    def backward(self, dy, saved, dx_out=None, dx_beta=0.0, g_out=None, need_dx=True, sums=None, bn_next=None):
+        """dz = BN backward of dy, the conv's weight gradient, and (need_dx) its data gradient.
+        sums: this unit's BN-backward first pass, already formed by the producer of dy (skip it).
+        bn_next: the NEXT unit's bn_next_ctx -- the data gradient then also forms that unit's first
+        pass, and the return value is (dx, sums or None) instead of dx."""
         x, z, y, mr, B, H, W, Ho, Wo, relu, has_res = saved
         c = self.conv.cout
         dz = torch.empty_like(z)
         st = self.bn.store
-        if relu and not has_res and g_out is None:      # ReLU mask rebuilt from z: y is not read
+        if sums is not None:                             # first pass fused upstream
+            assert relu and not has_res and g_out is None
+            nn.bn_backward_relu_sums(dy, z, mr, self.bn.gamma, self.bn.beta, sums, dz, st.g(self.bn.gname),
+                                     st.g(self.bn.bname), B, Ho * Wo, c, conv_dbias=self.conv.db)
+        elif relu and not has_res and g_out is None:    # ReLU mask rebuilt from z: y is not read
             nn.bn_backward_relu(dy, z, mr, self.bn.gamma, self.bn.beta, dz, st.g(self.bn.gname),
                                 st.g(self.bn.bname), B, Ho * Wo, c, conv_dbias=self.conv.db)
         else:
@@ -306,4 +340,8 @@ class ConvBN(object):
         self.conv.wgrad(x, dz, B, H, W, bias=False)
         if not need_dx:
             return None
-        return self.conv.dgrad(dz, B, H, W, out=dx_out, beta=dx_beta)
+        if bn_next is None:
+            return self.conv.dgrad(dz, B, H, W, out=dx_out, beta=dx_beta)
+        assert dx_beta == 0.0
+        dx = self.conv.dgrad(dz, B, H, W, out=dx_out, bn_next=bn_next)
+        return dx

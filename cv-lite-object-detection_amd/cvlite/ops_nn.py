@@ -204,6 +204,29 @@ def depthwise_wgrad(x, dy, dw, k, stride, pad_t, pad_l, beta=0.0):
               int(pad_t), int(pad_l), Ho, Wo, ptr(ws), ws.numel(), stream())
 
 
+def conv_igemm_dgrad_bnsum(desc, src, dst, z, mean_rstd, gamma, beta, sums, act_hi=float("inf"), zero=True):
+    """DGRAD conv whose epilogue also forms the next BN's backward first pass into `sums`
+    [B][C][2] float64 (zeroed here first unless zero=False: the caller's buffer is already zero).
+    Returns True when fused; False = the plain data gradient ran and `sums` is untouched (run the
+    two-pass BN backward)."""
+    n = int(_lib.load().cvl_conv_igemm_workspace_size(ctypes.byref(desc)))
+    ws = torch.empty(n, dtype=torch.uint8, device=src.device) if n > 16 else None
+    if zero:
+        sums.zero_()
+    flag = ctypes.c_int32(0)
+    _lib.call("cvl_conv_igemm_dgrad_bnsum", ctypes.byref(desc), ptr(src), ptr(dst), ptr(z), ptr(mean_rstd), ptr(gamma),
+              ptr(beta), float(act_hi), ptr(sums), ctypes.addressof(flag), ptr(ws), n if ws is not None else 0,
+              stream())
+    return bool(flag.value)
+
+
+def bn_backward_relu_sums(dy, z, mean_rstd, gamma, beta, sums, dz, dgamma, dbeta, B, HW, C, beta_acc=0.0,
+                          conv_dbias=None, act_hi=float("inf")):
+    """Second pass of bn_backward_relu from the fused first-pass sums (conv_igemm_dgrad_bnsum)."""
+    _lib.call("cvl_bn_backward_relu_sums", ptr(dy), ptr(z), ptr(mean_rstd), ptr(gamma), ptr(beta), ptr(sums), ptr(dz),
+              ptr(dgamma), ptr(dbeta), float(beta_acc), ptr(conv_dbias), float(act_hi), B, HW, C, stream())
+
+
 def bn_backward_relu(dy, z, mean_rstd, gamma, beta, dz, dgamma, dbeta, B, HW, C, beta_acc=0.0, conv_dbias=None):
     """bn_backward of a BN -> ReLU unit without a residual add: the mask is rebuilt from z."""
     n = int(_lib.load().cvl_bn_backward_workspace_size(B, HW, C))

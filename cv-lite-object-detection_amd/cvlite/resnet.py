@@ -100,7 +100,7 @@ class Bottleneck(object):
         y3, sv3 = self.c3.forward(y2, B, H1, W1, relu=True, residual=s, train=train, arena=arena)
         return y3, H1, W1, (sv_s, sv1, sv2, sv3)
 
-    def backward(self, dy, saved, dx_out=None, dx_beta=0.0):
+    def backward(self, dy, saved, dx_out=None, dx_beta=0.0, arena=None):
         sv_s, sv1, sv2, sv3 = saved
         x = sv1[0]
         if dx_out is None:
@@ -110,11 +110,21 @@ class Bottleneck(object):
             g = dx_out                     # residual gradient lands directly in dx
         else:
             g = torch.empty_like(dy)
-        dy2 = self.c3.backward(dy, sv3, g_out=g)
-        dy1 = self.c2.backward(dy2, sv2)
+        # conv1 / conv2 units (BN -> ReLU, one producer of their dy): the producing data gradient
+        # also forms their BN backward's first pass (sums), so that pass is skipped
+        ctx2, ctx1 = self.c2.bn_next_ctx(sv2, arena), self.c1.bn_next_ctx(sv1, arena)
+        s2 = s1 = None
+        if ctx2 is not None:
+            dy2, s2 = self.c3.backward(dy, sv3, g_out=g, bn_next=ctx2)
+        else:
+            dy2 = self.c3.backward(dy, sv3, g_out=g)
+        if ctx1 is not None:
+            dy1, s1 = self.c2.backward(dy2, sv2, sums=s2, bn_next=ctx1)
+        else:
+            dy1 = self.c2.backward(dy2, sv2, sums=s2)
         if self.sc is not None:
             self.sc.backward(g, sv_s, dx_out=dx_out, dx_beta=dx_beta)
-        self.c1.backward(dy1, sv1, dx_out=dx_out, dx_beta=1.0)
+        self.c1.backward(dy1, sv1, dx_out=dx_out, dx_beta=1.0, sums=s1)
         return dx_out
 
 
@@ -176,7 +186,8 @@ class ResNet50(object):
     def forward(self, x, train=True):
         """x: fp32 NHWC [B,H,W,3] in [-1,1].  Returns [C3, C4, C5] bf16 NHWC and saved state."""
         B = x.shape[0]
-        arena = StatsArena(2 * B * sum(bn.c for bn in self.bns()), x.device)
+        # forward BN statistics + (second half) the backward's fused first-pass sums: one memset
+        arena = StatsArena(4 * B * sum(bn.c for bn in self.bns()), x.device)
         h, sv_stem = self.stem.forward(x, train, arena)
         H, W = h.shape[1], h.shape[2]
         saved, taps = [], []
@@ -187,14 +198,15 @@ class ResNet50(object):
                 ssv.append(sv)
             saved.append(ssv)
             taps.append((h, H, W))
-        return taps[1:], (sv_stem, saved)
+        return taps[1:], (sv_stem, saved, arena)
 
     def backward(self, d_taps, saved, hook=None):
         """d_taps: gradients of [C3, C4, C5]; they are used in place as stage-output buffers.
         hook(name) fires when a stage's parameter gradients are final ("conv5" .. "conv3", then
         "conv2_stem")."""
         hook = hook or (lambda name: None)
-        sv_stem, ssv = saved
+        sv_stem, ssv = saved[0], saved[1]
+        arena = saved[2] if len(saved) > 2 else None
         dC = {1: d_taps[0], 2: d_taps[1], 3: d_taps[2]}
         dh = dC[3]
         for si in range(3, -1, -1):
@@ -203,9 +215,9 @@ class ResNet50(object):
                 if bi == 0 and (si - 1) in dC:
                     # this block's input is the previous stage's tap (C3 / C4), whose buffer
                     # already holds the FPN lateral's gradient: accumulate into it
-                    dh = st[bi].backward(dh, ssv[si][bi], dx_out=dC[si - 1], dx_beta=1.0)
+                    dh = st[bi].backward(dh, ssv[si][bi], dx_out=dC[si - 1], dx_beta=1.0, arena=arena)
                 else:
-                    dh = st[bi].backward(dh, ssv[si][bi])
+                    dh = st[bi].backward(dh, ssv[si][bi], arena=arena)
             if si > 0:
                 hook("conv%d" % (si + 2))
         self.stem.backward(dh, sv_stem)

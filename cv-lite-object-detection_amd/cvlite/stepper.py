@@ -73,6 +73,20 @@ class GraphStepper(object):
             self._update()
         torch.cuda.synchronize()
 
+    def run_fwd_bwd(self):
+        """Forward + backward only (targets, loss and the parameter gradients), replayed from the
+        captured segments: the shape-bucketed step (train_fcos.JitterFCOSTrainer) sums several
+        buckets' gradients before one update.  No data-parallel hooks on this path."""
+        assert self.sync is None, "bucketed gradient accumulation runs without the all-reduce hooks"
+        if self.use_graph:
+            if self.segs is None:
+                self.capture()
+            for g, _ in self.segs:
+                g.replay()
+        else:
+            self._fwd_bwd(None)
+        return self.losses
+
     def invalidate(self):
         self.segs = None
         self.g_up = None

@@ -132,6 +132,104 @@ class FCOSTrainer(GraphStepper):
 
 
 
+class JitterFCOSTrainer(object):
+    """The FCOS step over a batch whose images have different padded sizes (FCOS/train_fcos.py:
+    128-176 preprocesses every image with its own jittered size and runs it as a batch-1 forward).
+    Per-image BatchNorm makes a group of equal-size images one batch with the same math, so the
+    batch is split into shape BUCKETS: one FCOSTrainer (its own HIP graphs) per (padded size,
+    image count), created on first use and kept in an LRU of `max_buckets`; each bucket's
+    forward + backward runs from its graphs, the parameter gradients are summed across buckets,
+    then ONE clip + SGD update with 1 / batch_size (train_fcos.py:179-185)."""
+
+    def __init__(self, net, batch_size, n_max=16, init_lr=5e-4, min_lr=1e-5, decay_step=1000, decay_rate=0.9,
+                 momentum=0.9, gradient_clip=1.0, reg_type="l1", weight_decay=0.0, st_step=0, use_graph=True,
+                 max_buckets=12):
+        self.net, self.B, self.n_max = net, batch_size, n_max
+        self.momentum, self.clip = momentum, gradient_clip
+        self.sched = (init_lr, min_lr, decay_rate, decay_step)
+        self.reg_type, self.use_graph, self.max_buckets = reg_type, use_graph, max_buckets
+        self.weight_decay = float(weight_decay)
+        self.l2 = nn.L2Reg(net.store) if self.weight_decay > 0.0 else None
+        dev = net.device
+        self.buckets = {}
+        self.acc = torch.zeros_like(net.store.grad)
+        self.lr = torch.tensor([init_lr], dtype=torch.float32, device=dev)
+        self.step_dev = torch.tensor([st_step], dtype=torch.int32, device=dev)
+        self.sumsq = torch.zeros(1, dtype=torch.float64, device=dev)
+        self.losses = torch.zeros((batch_size, 3), dtype=torch.float32, device=dev)
+        self.ntgt = torch.zeros((batch_size, 5), dtype=torch.int32, device=dev)
+
+    def bucket(self, size, count):
+        key = (int(size), int(count))
+        tr = self.buckets.pop(key, None)
+        if tr is None:
+            if len(self.buckets) >= self.max_buckets:          # evict the least recently used
+                self.buckets.pop(next(iter(self.buckets)))
+            tr = FCOSTrainer(self.net, count, (size, size), n_max=self.n_max, reg_type=self.reg_type,
+                             use_graph=self.use_graph)
+        self.buckets[key] = tr
+        return tr
+
+    def step(self, images, boxes, nbox, img_dim):
+        """images: list of bs device [S_i, S_i, 3] fp32 (preprocess_data outputs); boxes [bs, n_max, 5]
+        (yc, xc, h, w, cls) normalised to img_dim; nbox [bs]; img_dim [bs, 2] = unpadded sizes.
+        Returns the per-image (cls, reg, cen) losses [bs, 3] in the input order."""
+        bs = len(images)
+        assert bs == self.B
+        dev = self.net.device
+        boxes = torch.as_tensor(boxes, dtype=torch.float32, device=dev)
+        nbox = torch.as_tensor(nbox, dtype=torch.int32, device=dev)
+        img_dim = torch.as_tensor(img_dim, dtype=torch.float32, device=dev)
+        if self.l2 is not None:
+            self.l2.run()
+        sizes = [int(t.shape[0]) for t in images]
+        first = True
+        for S in sorted(set(sizes)):
+            idx = [i for i in range(bs) if sizes[i] == S]
+            tr = self.bucket(S, len(idx))
+            it = torch.tensor(idx, device=dev)
+            tr.load_batch(torch.stack([images[i] for i in idx]), boxes.index_select(0, it)[:, :tr.boxes.shape[1]],
+                          nbox.index_select(0, it), img_dim=img_dim.index_select(0, it))
+            tr.run_fwd_bwd()
+            if first:
+                self.acc.copy_(self.net.store.grad)
+                first = False
+            else:
+                self.acc.add_(self.net.store.grad)
+            self.losses.index_copy_(0, it, tr.losses)
+            self.ntgt.index_copy_(0, it, tr.ntgt)
+        st = self.net.store
+        st.grad.copy_(self.acc)
+        init_lr, min_lr, rate, dstep = self.sched
+        nn.lr_schedule(self.step_dev, self.lr, init_lr, min_lr, rate, dstep)
+        nn.sgd_clip_update(st.flat, st.grad, st.mom, self.lr, self.momentum, 1.0 / bs, self.clip, ws=self.sumsq)
+        self.net.pack()
+        return self.losses
+
+    @property
+    def l2_params_reg(self):
+        return None if self.l2 is None else self.l2.out
+
+
+def _raw_batch(train_data, idx, rng):
+    """preprocess_data (data_preprocess.py:98-133) of each chosen raw sample: device images of their
+    own padded sizes + boxes / counts / unpadded sizes for the bucketed step."""
+    from .data_preprocess import preprocess_data
+    imgs, boxes, dims = [], [], []
+    for i in idx:
+        img, bbox, cls, shp = preprocess_data(train_data[i], rng=rng)
+        imgs.append(img)
+        boxes.append(np.concatenate([bbox, cls.astype(np.float32)[:, None]], 1))
+        dims.append(shp)
+    n_max = max(16, max(len(b) for b in boxes))
+    bx = np.zeros((len(idx), n_max, 5), np.float32)
+    nb = np.zeros(len(idx), np.int32)
+    for k, b in enumerate(boxes):
+        bx[k, :len(b)] = b
+        nb[k] = len(b)
+    return imgs, bx, nb, np.stack(dims)
+
+
 # -------------------------------------------------------------------------------------------------
 # synthetic VOC-shaped batches (SURVEY.md §8d)
 # -------------------------------------------------------------------------------------------------
@@ -187,9 +285,12 @@ def train(train_data, training_loss, model, batch_size, optimizer, ckpt, ck_mana
           step_cool=1000, weight_decay=1.0e-4, gradient_clip=1.0, save_loss_file="train_losses.csv"):
     """Same keywords and defaults as FCOS/train_fcos.py:87-93.
     * `model`: what cvlite.fcos.build_model returns (or its FCOSNet).
-    * `train_data`: pre-processed samples dict(image=[Hp,Wp,3] in [-1,1], bbox=[N,4] normalised
-      (yc,xc,h,w), label=[N], optional img_dim=[h,w] = the unpadded resized size that
-      data_preprocess.preprocess_data returns) of one padded size.
+    * `train_data`: either the reference's raw samples dict(image = a DECODED [H,W,3] image,
+      objects = {bbox, label}, l_jitter, u_jitter, min_side, max_side) -- each chosen image then
+      runs data_preprocess.preprocess_data (flip + jittered resize + pad) on the GPU and the
+      batch trains as shape buckets (JitterFCOSTrainer) -- or pre-processed samples
+      dict(image=[Hp,Wp,3] in [-1,1], bbox=[N,4] normalised (yc,xc,h,w), label=[N], optional
+      img_dim=[h,w]) of one padded size.
     * `ckpt` / `ck_manager`: cvlite.checkpoint.Checkpoint / CheckpointManager (tf.train.*
       semantics: ckpt.step += 1 per step, ck_manager.save() every step_save steps), or a path
       prefix string (torch checkpoint at <prefix>.pt) and None.
@@ -199,11 +300,19 @@ def train(train_data, training_loss, model, batch_size, optimizer, ckpt, ck_mana
     from . import checkpoint as ck
     net = getattr(model, "net", model)
     n_data = len(train_data)
-    H, W = np.asarray(train_data[0]["image"]).shape[:2]
-    n_max = max(16, max(len(s["label"]) for s in train_data))
-    trainer = FCOSTrainer(net, batch_size, (H, W), n_max=n_max, init_lr=init_lr, min_lr=min_lr,
-                          decay_step=decay_step, decay_rate=decay_rate, momentum=optimizer.momentum,
-                          gradient_clip=gradient_clip, weight_decay=weight_decay, st_step=st_step)
+    raw = "objects" in train_data[0]
+    if raw:          # reference-format samples: per-image jittered sizes, shape-bucketed step
+        n_max = max(16, max(len(s["objects"]["label"]) for s in train_data))
+        trainer = JitterFCOSTrainer(net, batch_size, n_max=n_max, init_lr=init_lr, min_lr=min_lr,
+                                    decay_step=decay_step, decay_rate=decay_rate, momentum=optimizer.momentum,
+                                    gradient_clip=gradient_clip, weight_decay=weight_decay, st_step=st_step)
+        rng = np.random.default_rng()
+    else:
+        H, W = np.asarray(train_data[0]["image"]).shape[:2]
+        n_max = max(16, max(len(s["label"]) for s in train_data))
+        trainer = FCOSTrainer(net, batch_size, (H, W), n_max=n_max, init_lr=init_lr, min_lr=min_lr,
+                              decay_step=decay_step, decay_rate=decay_rate, momentum=optimizer.momentum,
+                              gradient_clip=gradient_clip, weight_decay=weight_decay, st_step=st_step)
     dev = net.device
     start = time.time()
     elapsed = 0.0
@@ -211,10 +320,14 @@ def train(train_data, training_loss, model, batch_size, optimizer, ckpt, ck_mana
     tot = np.zeros(3)
     for step in range(st_step, max_steps):
         idx = np.random.choice(n_data, size=batch_size, replace=False)       # train_fcos.py:112
-        imgs, bx, nb, dims = _batch_from_samples(train_data, idx, n_max)
-        trainer.load_batch(torch.from_numpy(imgs).to(dev), torch.from_numpy(bx).to(dev), torch.from_numpy(nb).to(dev),
-                           img_dim=torch.from_numpy(dims).to(dev))
-        per_img = trainer.step().detach().double().cpu().numpy()         # [bs, 3] (cls, reg, cen)
+        if raw:
+            imgs, bx, nb, dims = _raw_batch(train_data, idx, rng)
+            per_img = trainer.step(imgs, bx, nb, dims).detach().double().cpu().numpy()
+        else:
+            imgs, bx, nb, dims = _batch_from_samples(train_data, idx, n_max)
+            trainer.load_batch(torch.from_numpy(imgs).to(dev), torch.from_numpy(bx).to(dev),
+                               torch.from_numpy(nb).to(dev), img_dim=torch.from_numpy(dims).to(dev))
+            per_img = trainer.step().detach().double().cpu().numpy()     # [bs, 3] (cls, reg, cen)
         ntgt = trainer.ntgt.sum(1).cpu().numpy()
         for k in np.nonzero(ntgt == 0)[0]:
             print("No targets at index", str(idx[k]) + ".")

@@ -231,6 +231,24 @@ int cvl_bn_backward_relu(const void* dy, const void* z, const float* mean_rstd, 
                          const float* beta, void* workspace, size_t workspace_bytes, void* dz, float* dgamma,
                          float* dbeta, float beta_acc, float* conv_dbias, int B, int HW, int C,
                          cvl_stream_t stream);
+/* Fused BN-backward first pass.  cvl_conv_igemm_dgrad_bnsum runs a DGRAD conv (beta 0) whose
+ * result is dy of a BN -> ReLU (act_hi = INFINITY) / ReLU6 (act_hi = 6) unit without a residual
+ * (the bottleneck's conv1 / conv2 units: their dy has one producer) and, when the 256-row
+ * LDS-DMA kernel takes the launch with one image per tile, adds per (image, channel)
+ * (sum g, sum g*xhat), g = dy * mask(bn(z)), into sums [B][C][2] float64 (zero it first) and sets
+ * *fused (HOST) = 1; otherwise it runs the plain data gradient and sets *fused = 0.  z / mean_rstd
+ * / gamma / beta are the unit's pre-BN conv output (same layout as dst), (mean, rstd) [B][C][2]
+ * and BN parameters.  cvl_bn_backward_relu_sums is cvl_bn_backward_relu's second pass from those
+ * sums (the first pass and its reduction are skipped). */
+int cvl_conv_igemm_dgrad_bnsum(const cvl_conv_desc* d, const void* src, void* dst, const void* z,
+                               const float* mean_rstd, const float* gamma, const float* beta, float act_hi,
+                               double* sums, int32_t* fused, void* workspace, size_t workspace_bytes,
+                               cvl_stream_t stream);
+int cvl_bn_backward_relu_sums(const void* dy, const void* z, const float* mean_rstd, const float* gamma,
+                              const float* beta, const double* sums, void* dz, float* dgamma, float* dbeta,
+                              float beta_acc, float* conv_dbias, float act_hi, int B, int HW, int C,
+                              cvl_stream_t stream);
+
 /* BN -> ReLU6 unit without a residual (MobileNetV2: Keras ReLU(6.)): as cvl_bn_backward_relu with
  * the TF Relu6Grad mask 0 < bn(z) < 6 rebuilt from z in fp32 (the forward's exact pre-clamp value);
  * cvl_bn_apply / cvl_bn_finalize_apply take relu = 2 for ReLU6. */

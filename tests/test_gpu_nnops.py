@@ -247,3 +247,61 @@ def test_im2col_matches_unfold(B, H, W, stride, Kp, C, K):
     ref = torch.zeros(B * Ho * Wo, Kp)
     ref[:, :K * K * C] = cols
     assert torch.equal(out.cpu().view(torch.int16), ref.to(BF).view(torch.int16))
+
+
+@pytest.mark.parametrize("B,H,Cin,Cout,k,expect_fused", [
+    (2, 128, 64, 64, 3, True),       # conv2_x 3x3 data gradient -> conv2_x conv1 BN (L64 kernel)
+    (8, 64, 512, 128, 1, True),      # conv3_x conv3 1x1 data gradient -> conv2 BN (L128 kernel)
+    (2, 16, 2048, 512, 1, False),    # conv5_x: too few tiles for the 256-row kernel -> plain path
+])
+def test_dgrad_fused_bn_backward_first_pass(B, H, Cin, Cout, k, expect_fused):
+    """cvl_conv_igemm_dgrad_bnsum + cvl_bn_backward_relu_sums (the first BN-backward pass formed in
+    the data-gradient epilogue) against the plain data gradient + two-pass cvl_bn_backward_relu on
+    the same operands: dX bit-identical, first-pass sums within fp32 summation order, dz / dgamma /
+    dbeta within one bf16 rounding; the unfusable launch reports fused=False and leaves sums 0."""
+    from cvlite import ops_nn as nn
+    from cvlite.layers import Conv, ParamStore
+    W = H
+    C = Cout                     # dgrad output channels = the conv's input channels = the BN's channels
+    dev = torch.device("cuda")
+    st = ParamStore()
+    conv = Conv(st, "c", k, C, Cin, 1, "same", bias=False)     # forward C -> Cin; its dgrad yields dC
+    st.finalize(dev, seed=3)
+    conv.pack()
+    g = torch.Generator(device="cpu").manual_seed(B + H + Cin)
+    dy_next = (torch.randn(B, H, W, Cin, generator=g) * 0.5).to(BF).to(dev)
+    z = (torch.randn(B, H, W, C, generator=g) * 1.5 + 0.2).to(BF).to(dev)
+    mr = torch.empty((B, C, 2), dtype=torch.float32, device=dev)
+    zf = z.double().view(B, H * W, C)
+    mr[..., 0] = zf.mean(1).float()
+    mr[..., 1] = torch.rsqrt(zf.var(1, unbiased=False) + 1e-3).float()
+    gamma = (torch.rand(C, generator=g) + 0.5).to(dev)
+    beta = torch.randn(C, generator=g).to(dev) * 0.3
+    d = conv.dgrad_desc(B, [nn.seg(H, W, H, W, conv.wd)], ld_dst=C)
+    # fused
+    dx_f = torch.empty((B, H, W, C), dtype=BF, device=dev)
+    sums = torch.empty((B, C, 2), dtype=torch.float64, device=dev)
+    fused = nn.conv_igemm_dgrad_bnsum(d, dy_next, dx_f, z, mr, gamma, beta, sums)
+    assert fused == expect_fused
+    # plain
+    dx_p = torch.empty_like(dx_f)
+    nn.conv_igemm(d, dy_next, dx_p)
+    assert torch.equal(dx_f, dx_p)
+    if not expect_fused:
+        assert float(sums.abs().max()) == 0.0
+        return
+    # reference first-pass sums (fp64 on the same bf16 values)
+    xh = (z.float() - mr[..., 0].view(B, 1, 1, C)) * mr[..., 1].view(B, 1, 1, C)
+    a = gamma * xh + beta
+    gm = torch.where(a > 0, dx_p.float(), torch.zeros_like(a)).double()
+    ref = torch.stack([gm.sum((1, 2)), (gm * xh.double()).sum((1, 2))], -1)
+    torch.testing.assert_close(sums, ref, rtol=1e-5, atol=1e-6 * float(ref.abs().max()))
+    HW = H * W
+    dz_f, dz_p = torch.empty_like(z), torch.empty_like(z)
+    dg_f, db_f = torch.zeros(C, device=dev), torch.zeros(C, device=dev)
+    dg_p, db_p = torch.zeros(C, device=dev), torch.zeros(C, device=dev)
+    nn.bn_backward_relu_sums(dx_f, z, mr, gamma, beta, sums, dz_f, dg_f, db_f, B, HW, C)
+    nn.bn_backward_relu(dx_p, z, mr, gamma, beta, dz_p, dg_p, db_p, B, HW, C)
+    torch.testing.assert_close(dz_f.float(), dz_p.float(), rtol=1e-2, atol=1e-2 * float(dz_p.float().abs().max()))
+    torch.testing.assert_close(dg_f, dg_p, rtol=1e-5, atol=1e-5 * float(dg_p.abs().max()))
+    torch.testing.assert_close(db_f, db_p, rtol=1e-5, atol=1e-5 * float(db_p.abs().max()))

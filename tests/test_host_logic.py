@@ -79,3 +79,24 @@ def test_checkpoint_manager_roundtrip_cpu(tmp_path):
     assert ck.CheckpointManager(c, str(tmp_path), max_to_keep=2).save().endswith("ckpt-4.pt")
     with pytest.raises(ValueError):
         ck.Checkpoint(model=Net(3.0, extra=True)).restore(m.latest_checkpoint)
+
+
+def test_preprocess_box_path_and_size_plan():
+    """preprocess_data's box path (FCOS/data_preprocess.py:120-131: random_flip_horizontal's box map,
+    utils.swap_xy, utils.convert_to_xywh) and the host size plan used to bucket jittered batches:
+    square padded sizes, multiples of 128, new_shape = ratio * shape in fp32."""
+    import numpy as np
+    from cvlite.data_preprocess import box_targets, padded_size
+    b = np.array([[0.1, 0.2, 0.5, 0.9], [0.0, 0.3, 1.0, 0.4]], np.float32)
+    for flip in (False, True):
+        t = b.copy()
+        if flip:
+            t = np.stack([1 - b[:, 2], b[:, 1], 1 - b[:, 0], b[:, 3]], -1).astype(np.float32)
+        s = t[:, [1, 0, 3, 2]]
+        exp = np.concatenate([(s[:, :2] + s[:, 2:]) / np.float32(2), s[:, 2:] - s[:, :2]], -1)
+        np.testing.assert_array_equal(box_targets(b, flip), exp)
+    rng = np.random.default_rng(0)
+    for _ in range(20):
+        flip, shp, S = padded_size((375, 500), [640, 1024], 800.0, 1333.0, rng)
+        assert S % 128 == 0 and S >= shp.max() and shp.dtype == np.float32
+        assert 640 - 1e-3 <= shp.min() <= 1024 + 1e-3 or shp.max() <= 1333.0 + 1e-3
