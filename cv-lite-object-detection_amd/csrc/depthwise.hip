@@ -181,12 +181,33 @@ __global__ void __launch_bounds__(NT) dw_wgrad_kernel(const cvl_bf16* __restrict
   }
 }
 
-// dw[i] = beta*dw[i] + sum_b part[b][i] (blocks in order)
-__global__ void dw_wgrad_reduce_kernel(const float* __restrict__ part, float* __restrict__ dw, long n, int nblk,
-                                       float beta) {
-  for (long i = blockIdx.x * (long)NT + threadIdx.x; i < n; i += (long)gridDim.x * NT) {
-    float s = 0.f;
-    for (int b = 0; b < nblk; ++b) s += part[(long)b * n + i];
+// dw[i] = beta*dw[i] + sum_b part[b][i]: a block owns 32 consecutive outputs and 8 block lanes;
+// lane l sums partials l, l+8, ... with 4 loads in flight, then the 8 lane sums are added in a
+// fixed order (deterministic; hundreds of partials per output at large maps)
+__global__ void __launch_bounds__(256) dw_wgrad_reduce_kernel(const float* __restrict__ part, float* __restrict__ dw,
+                                                              long n, int nblk, float beta) {
+  __shared__ float red[8][33];
+  const int col = threadIdx.x & 31, sl = threadIdx.x >> 5;
+  const long i = (long)blockIdx.x * 32 + col;
+  float acc = 0.f;
+  if (i < n) {
+    float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+    int b = sl;
+    for (; b + 24 < nblk; b += 32) {
+      a0 += part[(long)b * n + i];
+      a1 += part[(long)(b + 8) * n + i];
+      a2 += part[(long)(b + 16) * n + i];
+      a3 += part[(long)(b + 24) * n + i];
+    }
+    for (; b < nblk; b += 8) a0 += part[(long)b * n + i];
+    acc = (a0 + a1) + (a2 + a3);
+  }
+  red[sl][col] = acc;
+  __syncthreads();
+  if (sl == 0 && i < n) {
+    float s = red[0][col];
+#pragma unroll
+    for (int k = 1; k < 8; ++k) s += red[k][col];
     dw[i] = (beta != 0.f ? beta * dw[i] : 0.f) + s;
   }
 }
@@ -194,7 +215,7 @@ __global__ void dw_wgrad_reduce_kernel(const float* __restrict__ part, float* __
 inline int wgrad_pix_per_blk(long npix, int C) {
   const int C8 = C / 8;
   const int rpp = NT / (C8 < NT ? C8 : NT);
-  long want = npix / 512;                              // ~512 blocks
+  long want = npix / 1024;                             // ~1024 blocks
   if (want < rpp * 8) want = rpp * 8;                  // >= 8 pixels per lane
   return (int)((want + rpp - 1) / rpp * rpp);
 }
@@ -256,6 +277,7 @@ extern "C" int cvl_depthwise_wgrad(const void* x, const void* dy, float* dw, flo
   hipLaunchKernelGGL(dw_wgrad_kernel<3>, dim3(nblk), dim3(NT), 0, S_, (const cvl_bf16*)x, (const cvl_bf16*)dy, part,
                      g, npix, ppb);
   const long n = (long)k * k * C;
-  hipLaunchKernelGGL(dw_wgrad_reduce_kernel, dim3(grid_for(n)), dim3(NT), 0, S_, (const float*)part, dw, n, nblk, beta);
+  hipLaunchKernelGGL(dw_wgrad_reduce_kernel, dim3((unsigned)((n + 31) / 32)), dim3(256), 0, S_, (const float*)part, dw,
+                     n, nblk, beta);
   return cvl_launch_status();
 }

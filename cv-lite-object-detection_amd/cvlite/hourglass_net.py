@@ -19,6 +19,7 @@ Reference quirk kept (cnn_block :103-155): from the second repeat on the residua
 OUTPUT (`tmp_input` is rebound to the normalised tensor before the convs).
 """
 import math
+import os
 
 import torch
 
@@ -46,10 +47,37 @@ def block_graph(n_stacks=1):
     return out
 
 
+# 3x3 separable convs on maps of at least this many pixels run SPLIT: depthwise kernel
+# (cvl_depthwise_*, HBM-bound) + pointwise 1x1 GEMM, instead of the dense fold whose 3x3 GEMM does
+# 9x the pointwise FLOPs; below it the fold's single launch wins (CVL_SEP_SPLIT_MIN_HW, 0 = never)
+SPLIT_MIN_HW = int(os.environ.get("CVL_SEP_SPLIT_MIN_HW", str(128 * 128)))
+
+
+class _PointwiseOf(Conv):
+    """The pointwise half of a split SeparableConv2D as a 1x1 Conv whose weight IS the layer's
+    trainable pointwise_kernel [1,1,Cin,Cout] (HWIO of a 1x1 conv): packing reads it and the
+    weight gradient lands in its gradient slot, with no fold / unfold."""
+
+    def __init__(self, store, pwname, cin, cout):
+        self.name, self.k, self.cin, self.cout, self.stride, self.pad = pwname, 1, cin, cout, 1, "same"
+        self.cin_k = cin
+        self.npad = max(32, (cout + 31) // 32 * 32)
+        self.cout_pad = self.npad
+        self.cin_pad = (cin + 31) // 32 * 32
+        self.has_bias = False
+        self.need_dgrad = True
+        self.wname, self.bname = pwname, None
+        self.store = store
+        self.wf = self.wd = None
+
+
 class SepConv(object):
     """Keras SeparableConv2D(cout, k, stride, "same") = dense conv with the folded kernel D x P.
     The trainable D / P / bias live in the model store; the folded kernel and its gradient in
-    the `eff` store (not optimised)."""
+    the `eff` store (not optimised).  3x3 / stride 1 convs on large maps run split instead
+    (depthwise kernel on D + 1x1 GEMM on P, gradients written straight to D / P): `split` is
+    decided on the first forward at a map size and fixes which of the two forms the model's
+    fold / pack plans carry."""
 
     def __init__(self, store, eff, name, k, cin, cout, stride=1, cin_k=None, dgrad=True):
         self.name, self.k, self.cin, self.cout = name, k, cin, cout
@@ -58,6 +86,14 @@ class SepConv(object):
         self.bname = store.add(name + "/bias", (cout,), constant(0.0))
         self.store = store
         self.conv = Conv(eff, name, k, cin, cout, stride, "same", bias=False, cin_k=cin_k, dgrad=dgrad)
+        self.can_split = k == 3 and stride == 1 and cin % 8 == 0
+        self.split = False
+        self.pw = _PointwiseOf(store, self.pwname, cin, cout) if self.can_split else None
+        self.on_mode_change = None         # the owning net's plan invalidation
+        self._t = self._dt = None
+
+    def want_split(self, H, W):
+        return self.can_split and 0 < SPLIT_MIN_HW <= H * W
 
     @property
     def b(self):
@@ -72,7 +108,25 @@ class SepConv(object):
         return (st.p(self.dwname), st.p(self.pwname), self.conv.w, self.conv.dw, st.g(self.dwname),
                 st.g(self.pwname))
 
+    def _set_split(self, on):
+        if on != self.split:
+            self.split = on
+            if on:
+                self.pw.pack()                  # eager: the plans pick the pointwise up from now on
+            if self.on_mode_change is not None:
+                self.on_mode_change()
+
     def fwd(self, x, B, H, W, relu_out=False):
+        self._set_split(self.want_split(H, W))
+        if self.split:
+            # depthwise (TF "same" 3x3: pad 1) then the pointwise GEMM with the layer's bias
+            t = torch.empty((B, H, W, self.cin), dtype=BF16, device=x.device)
+            nn.depthwise_fwd(x, self.store.p(self.dwname), t, 3, 1, 1, 1)
+            self._t = t
+            out = torch.empty((B, H, W, self.cout), dtype=BF16, device=x.device)
+            d = self.pw.fwd_desc(B, [nn.seg(H, W, H, W, self.pw.wf, self.b)], ld_dst=self.cout, relu_out=relu_out)
+            nn.conv_igemm(d, t, out)
+            return out
         c = self.conv
         Ho, Wo, _, _ = c.out_hw(H, W)
         out = torch.empty((B, Ho, Wo, self.cout), dtype=BF16, device=x.device)
@@ -81,11 +135,23 @@ class SepConv(object):
         return out
 
     def wgrad(self, x, dy, B, H, W):
-        self.conv.wgrad(x, dy, B, H, W, bias=False)
         HW = H * W
+        if self.split:
+            # dP = t^T dy; dt = dy P^T (kept for dgrad); dD = depthwise weight gradient of (x, dt)
+            self.pw.wgrad(self._t, dy, B, H, W, bias=False)
+            self._dt = self.pw.dgrad(dy, B, H, W)
+            nn.depthwise_wgrad(x, self._dt, self.store.g(self.dwname), 3, 1, 1, 1)
+        else:
+            self.conv.wgrad(x, dy, B, H, W, bias=False)
         nn.bias_grad(dy, int(dy.shape[-1]), 0, self.cout, 0, HW, HW, B, self.db)
 
     def dgrad(self, dy, B, H, W, out=None, beta=0.0):
+        if self.split:
+            assert self._dt is not None, "split SepConv: wgrad (which forms dt) runs before dgrad"
+            if out is None:
+                out = torch.empty((B, H, W, self.cin), dtype=BF16, device=dy.device)
+            nn.depthwise_dgrad(self._dt, self.store.p(self.dwname), out, 3, 1, 1, 1, beta=beta)
+            return out
         return self.conv.dgrad(dy, B, H, W, out=out, beta=beta)
 
 
@@ -233,6 +299,8 @@ class HourglassNet(object):
         self.store, self.eff = store, eff
         for bn in self.bns():
             bn.init_buffers(self.device)
+        for s in self.seps():
+            s.on_mode_change = self._mode_changed
         self.cout_ld = (4 + n_classes + 31) // 32 * 32
         self.b_eff = torch.zeros(4 + n_classes, dtype=torch.float32, device=self.device)
         self.g_beff = torch.zeros(4 + n_classes, dtype=torch.float32, device=self.device)
@@ -258,10 +326,14 @@ class HourglassNet(object):
         return [bn for b in self.blocks.values() for bn in b.bns()]
 
     def _make_plan(self):
-        entries = [self.stem.pack_entry()] + [s.conv.pack_entry() for s in self.seps()[1:]]
+        seps = self.seps()
+        entries = [self.stem.pack_entry()] + [(s.pw if s.split else s.conv).pack_entry() for s in seps[1:]]
         entries.append(self.cnn_out.pack_entry())
-        self._plan = (nn.SepPlan([s.sep_entry() for s in self.seps()], self.device),
+        self._plan = (nn.SepPlan([s.sep_entry() for s in seps if not s.split], self.device),
                       nn.PackPlan(entries, self.device))
+
+    def _mode_changed(self):
+        self._plan = None
 
     def pack(self):
         """fold every separable conv, fold b_focal, re-pack all bf16 conv weights (3 launches)."""
@@ -350,6 +422,8 @@ class HourglassNet(object):
         d = c.fwd_desc(B, [nn.seg(Ho, Wo, Ho, Wo, c.wf, self.b_eff)], ld_dst=4 + self.C, dst_f32=True)
         nn.conv_igemm(d, v["o4"], out)
         self._saved = (sv_stem, saved, v, hw, B, group)
+        if self._plan is None:        # a separable conv switched form at this map size: re-plan now
+            self._make_plan()
         return out
 
     def backward(self, d_out, hook=None):

@@ -207,11 +207,15 @@ def _targets(B, Hs, C, seed):
     return tg
 
 
-def test_hourglass_forward_loss_backward_vs_oracle():
+@pytest.mark.parametrize("split", [False, True])
+def test_hourglass_forward_loss_backward_vs_oracle(split, monkeypatch):
     """Whole graph, B=4 images of 128x128 in 2 BN sub-batches of 2, vs the oracle storing
-    activations / weights / gradients in bf16 at the GPU path's points."""
-    from cvlite import ops_targets as ot
+    activations / weights / gradients in bf16 at the GPU path's points.  split=True lowers the
+    split threshold so every 3x3 separable conv on a >= 16x16 map runs as depthwise kernel +
+    pointwise GEMM (the form the bench's 256x256 / 128x128 maps take)."""
+    from cvlite import hourglass_net, ops_targets as ot
     from oracle import centernet_model_ref as cm
+    monkeypatch.setattr(hourglass_net, "SPLIT_MIN_HW", 256 if split else 10 ** 9)
     C, B, D, G = 20, 4, 128, 2
     net = _small_net(C, seed=1)
     params = net.store.state_dict()
@@ -225,6 +229,8 @@ def test_hourglass_forward_loss_backward_vs_oracle():
                                   d_pred=d_out.view(B, Hs * Hs, -1))
     net.backward(d_out)
     torch.cuda.synchronize()
+    n_split = sum(1 for sc in net.seps() if sc.split)
+    assert (n_split > 0) == split, n_split
     with cm.emulate_bf16():
         c16, r16, g16, o16 = cm.loss_and_grads(params, x, tg, C, G)
     c32, r32, g32, o32 = cm.loss_and_grads(params, x, tg, C, G)
@@ -258,13 +264,16 @@ def test_hourglass_forward_loss_backward_vs_oracle():
     assert not bad, bad
 
 
-def test_hourglass_train_steps_vs_oracle():
+@pytest.mark.parametrize("split", [False, True])
+def test_hourglass_train_steps_vs_oracle(split, monkeypatch):
     """Two full device train steps (targets from boxes on the GPU, BN sub-batches of 2, Adam,
     re-pack) vs the oracle's train_step on the same targets: loss within bf16 tolerance and the
-    parameter updates (Adam: ~lr per element) in rel-L2."""
-    from cvlite import ops_targets as ot
+    parameter updates (Adam: ~lr per element) in rel-L2; split=True as above (the mode switch on
+    the first forward re-plans the fold / pack tables before the graphs are captured)."""
+    from cvlite import hourglass_net, ops_targets as ot
     from cvlite.train_centernet import CenterNetTrainer, synthetic_batch
     from oracle import centernet_model_ref as cm
+    monkeypatch.setattr(hourglass_net, "SPLIT_MIN_HW", 256 if split else 10 ** 9)
     C, B, D, G = 20, 4, 128, 2
     net = _small_net(C, seed=2)
     p0 = net.store.state_dict()
