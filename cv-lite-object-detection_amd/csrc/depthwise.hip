@@ -181,6 +181,101 @@ __global__ void __launch_bounds__(NT) dw_wgrad_kernel(const cvl_bf16* __restrict
   }
 }
 
+// 3x3 / stride 1 weight gradient with a sliding tap window: a pixel lane walks a run of `seg`
+// consecutive output pixels of one row, keeping the 3x3 window of x (3 rows x 3 columns x 8
+// channels) in registers, so each step loads one new x column (3 rows) and one dy vector instead
+// of 9 + 1 (the CenterNet hourglass's split separable convs at 256x256 / 128x128).  Same
+// partial layout and fixed-order reductions as dw_wgrad_kernel.
+__global__ void __launch_bounds__(NT) dw_wgrad_rows_kernel(const cvl_bf16* __restrict__ x,
+                                                           const cvl_bf16* __restrict__ dy, float* __restrict__ part,
+                                                           DwGeo g, int seg, int spr, long nseg) {
+  const int C8 = g.C / 8;
+  const int tpr = C8;                          // host: C8 <= NT
+  const int rpp = NT / tpr;
+  const int cg = threadIdx.x % tpr, lane = threadIdx.x / tpr;
+  const int c0 = cg * 8;
+  __shared__ float red[NT][9];
+  float acc[9][8];
+#pragma unroll
+  for (int t = 0; t < 9; ++t)
+#pragma unroll
+    for (int u = 0; u < 8; ++u) acc[t][u] = 0.f;
+  const long sgi = (long)blockIdx.x * rpp + lane;
+  if (lane < rpp && sgi < nseg) {
+    const long row = sgi / spr;                          // b * Ho + oy
+    const int x0 = (int)(sgi - row * spr) * seg;
+    const int x1 = x0 + seg < g.Wo ? x0 + seg : g.Wo;
+    const int b = (int)(row / g.Ho), oy = (int)(row - (long)b * g.Ho);
+    const cvl_bf16* xb = x + (long)b * g.H * g.W * g.C + c0;
+    bool rok[3];
+    long roff[3];
+#pragma unroll
+    for (int ky = 0; ky < 3; ++ky) {
+      const int iy = oy - g.pt + ky;
+      rok[ky] = iy >= 0 && iy < g.H;
+      roff[ky] = (long)(rok[ky] ? iy : 0) * g.W;
+    }
+    auto ld = [&](int ky, int ix, float* v) {
+      if (rok[ky] && ix >= 0 && ix < g.W) {
+        unpack8(*reinterpret_cast<const s16x8*>(xb + (roff[ky] + ix) * g.C), v);
+      } else {
+#pragma unroll
+        for (int u = 0; u < 8; ++u) v[u] = 0.f;
+      }
+    };
+    float win[3][3][8];
+#pragma unroll
+    for (int ky = 0; ky < 3; ++ky) {
+      ld(ky, x0 - g.pl, win[ky][0]);
+      ld(ky, x0 - g.pl + 1, win[ky][1]);
+    }
+    const cvl_bf16* dyr = dy + row * g.Wo * g.C + c0;
+    for (int ox = x0; ox < x1; ++ox) {
+      float gd[8];
+      unpack8(*reinterpret_cast<const s16x8*>(dyr + (long)ox * g.C), gd);
+#pragma unroll
+      for (int ky = 0; ky < 3; ++ky) ld(ky, ox - g.pl + 2, win[ky][2]);
+#pragma unroll
+      for (int ky = 0; ky < 3; ++ky)
+#pragma unroll
+        for (int kx = 0; kx < 3; ++kx)
+#pragma unroll
+          for (int u = 0; u < 8; ++u) acc[ky * 3 + kx][u] += win[ky][kx][u] * gd[u];
+#pragma unroll
+      for (int ky = 0; ky < 3; ++ky)
+#pragma unroll
+        for (int u = 0; u < 8; ++u) { win[ky][0][u] = win[ky][1][u]; win[ky][1][u] = win[ky][2][u]; }
+    }
+  }
+  // reduce the rpp pixel lanes of each channel group, one tap at a time (fixed order)
+#pragma unroll
+  for (int t = 0; t < 9; ++t) {
+    __syncthreads();
+#pragma unroll
+    for (int u = 0; u < 8; ++u) red[threadIdx.x][u] = acc[t][u];
+    __syncthreads();
+    if (lane == 0) {
+      float sm[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+      for (int r = 0; r < rpp; ++r)
+#pragma unroll
+        for (int u = 0; u < 8; ++u) sm[u] += red[r * tpr + cg][u];
+      float* o = part + ((long)blockIdx.x * 9 + t) * g.C + c0;
+      *reinterpret_cast<float4*>(o) = make_float4(sm[0], sm[1], sm[2], sm[3]);
+      *reinterpret_cast<float4*>(o + 4) = make_float4(sm[4], sm[5], sm[6], sm[7]);
+    }
+  }
+}
+
+// row-walk plan of dw_wgrad_rows_kernel: segment length, segments per row, blocks (0 = not taken)
+inline int rows_plan(int B, int Ho, int Wo, int C, int k, int s, int* seg, int* spr) {
+  if (k != 3 || s != 1 || C / 8 > NT || cvl_env_flag("CVL_DW_NO_ROWS")) return 0;
+  *seg = Wo >= 128 ? 32 : (Wo >= 32 ? 16 : 8);
+  *spr = (Wo + *seg - 1) / *seg;
+  const int rpp = NT / (C / 8);
+  const long nseg = (long)B * Ho * *spr;
+  return (int)((nseg + rpp - 1) / rpp);
+}
+
 // dw[i] = beta*dw[i] + sum_b part[b][i]: a block owns 32 consecutive outputs and 8 block lanes;
 // lane l sums partials l, l+8, ... with 4 loads in flight, then the 8 lane sums are added in a
 // fixed order (deterministic; hundreds of partials per output at large maps)
@@ -258,9 +353,12 @@ extern "C" int cvl_depthwise_dgrad(const void* dy, const float* w, void* dx, int
 }
 
 extern "C" size_t cvl_depthwise_wgrad_workspace_size(int B, int Ho, int Wo, int C, int k) {
+  int seg, spr;
+  const int rb = rows_plan(B, Ho, Wo, C, k, 1, &seg, &spr);   // (stride unknown here: size for both)
   const long npix = (long)B * Ho * Wo;
   const long nblk = (npix + wgrad_pix_per_blk(npix, C) - 1) / wgrad_pix_per_blk(npix, C);
-  return (size_t)nblk * k * k * C * sizeof(float);
+  const long nb = rb > nblk ? rb : nblk;
+  return (size_t)nb * k * k * C * sizeof(float);
 }
 
 extern "C" int cvl_depthwise_wgrad(const void* x, const void* dy, float* dw, float beta, int B, int H, int W, int C,
@@ -271,11 +369,18 @@ extern "C" int cvl_depthwise_wgrad(const void* x, const void* dy, float* dw, flo
   CVL_CHECK_ARG(workspace_bytes >= cvl_depthwise_wgrad_workspace_size(B, Ho, Wo, C, k));
   DwGeo g{H, W, C, Ho, Wo, k, stride, pad_t, pad_l};
   const long npix = (long)B * Ho * Wo;
-  const int ppb = wgrad_pix_per_blk(npix, C);
-  const int nblk = (int)((npix + ppb - 1) / ppb);
   float* part = reinterpret_cast<float*>(workspace);
-  hipLaunchKernelGGL(dw_wgrad_kernel<3>, dim3(nblk), dim3(NT), 0, S_, (const cvl_bf16*)x, (const cvl_bf16*)dy, part,
-                     g, npix, ppb);
+  int seg = 0, spr = 0;
+  int nblk = rows_plan(B, Ho, Wo, C, k, stride, &seg, &spr);
+  if (nblk > 0) {                              // stride 1: the sliding-window row walk
+    hipLaunchKernelGGL(dw_wgrad_rows_kernel, dim3(nblk), dim3(NT), 0, S_, (const cvl_bf16*)x, (const cvl_bf16*)dy,
+                       part, g, seg, spr, (long)B * Ho * spr);
+  } else {
+    const int ppb = wgrad_pix_per_blk(npix, C);
+    nblk = (int)((npix + ppb - 1) / ppb);
+    hipLaunchKernelGGL(dw_wgrad_kernel<3>, dim3(nblk), dim3(NT), 0, S_, (const cvl_bf16*)x, (const cvl_bf16*)dy, part,
+                       g, npix, ppb);
+  }
   const long n = (long)k * k * C;
   hipLaunchKernelGGL(dw_wgrad_reduce_kernel, dim3((unsigned)((n + 31) / 32)), dim3(256), 0, S_, (const float*)part, dw,
                      n, nblk, beta);

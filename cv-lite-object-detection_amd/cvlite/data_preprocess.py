@@ -8,8 +8,8 @@
 
 The resize / normalise / pad (and the flip, when fused) run in one cvl_resize_pad_normalize
 launch per image that can write straight into a slot of the device batch.  JPEG decode
-(`_parse_image`) is outside this module: the input is a decoded [H,W,3] uint8 or fp32 image on
-the GPU (or host; it is copied).  The jitter draw uses numpy's generator instead of
+(`_parse_image`) is a host step (PIL; no GPU JPEG decoder in this image), as the reference's
+tf.image.decode_jpeg is; everything after it runs on the GPU.  The jitter draw uses numpy's generator instead of
 tf.random.uniform (a different stream by construction).
 """
 import numpy as np
@@ -73,6 +73,16 @@ def random_flip_horizontal(image, boxes, p_flip=0.5, rng=None):
     return image, boxes
 
 
+def _parse_image(filename):
+    """data_preprocess.py:5-9 `_parse_image`: read + decode a JPEG/PNG file to an [H,W,3] uint8
+    array (host; PIL's libjpeg decode with its default islow IDCT, where the reference uses
+    tf.image.decode_jpeg -- parity unpinned at the pixel level, TF absent).  The decoded image
+    then goes to the GPU resize / pad kernel."""
+    from PIL import Image
+    with Image.open(filename) as im:
+        return np.asarray(im.convert("RGB"), dtype=np.uint8)
+
+
 def box_targets(bbox, flip):
     """The box half of preprocess_data (data_preprocess.py:120-131) in the reference's fp32 order:
     random_flip_horizontal's box map [b0, b1, b2, b3] -> [1-b2, b1, 1-b0, b3] when flipped
@@ -86,16 +96,19 @@ def box_targets(bbox, flip):
 
 def preprocess_data(sample, rng=None, out=None):
     """data_preprocess.py:98-133 preprocess_data (pad_flag=True) for one sample dict with the
-    reference's keys: image (a DECODED [H,W,3] image, uint8 or fp32, host or device -- the JPEG
-    decode of `_parse_image` is outside this tier), objects = {bbox [N,4] normalised, label [N]},
+    reference's keys: image (a file name, decoded on the host by _parse_image, or an already
+    decoded [H,W,3] image, uint8 or fp32, host or device), objects = {bbox [N,4] normalised, label [N]},
     l_jitter / u_jitter, min_side, max_side.  Returns (image_padded [Hp,Wp,3] fp32 on the GPU,
     bbox [N,4] (the reference's xywh of the swapped corners), class_id [N] int32, img_shp [2] fp32 =
     the unpadded resized shape).  The flip draw (p = 0.5) and the jitter draw use `rng` (numpy) in
     the reference's order: flip first, then the jitter size."""
     rng = rng if rng is not None else np.random.default_rng()
     jitter = [sample["l_jitter"], sample["u_jitter"]]
+    image = sample["image"]
+    if isinstance(image, str):                   # a file name, as the reference's samples hold
+        image = _parse_image(image)
     flip = bool(rng.uniform() <= 0.5)
-    img, new_shape, _ = preprocess_image(sample["image"], jitter=jitter, min_side=sample["min_side"],
+    img, new_shape, _ = preprocess_image(image, jitter=jitter, min_side=sample["min_side"],
                                          max_side=sample["max_side"], flip=flip, out=out, rng=rng)
     bbox = box_targets(sample["objects"]["bbox"], flip)
     cls = np.asarray(sample["objects"]["label"], np.int32).reshape(-1)

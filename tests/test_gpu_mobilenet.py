@@ -32,6 +32,7 @@ def _pads(s):
 
 
 @pytest.mark.parametrize("B,H,W,C,s", [(2, 16, 16, 32, 1), (2, 16, 16, 160, 2), (1, 9, 12, 64, 1), (2, 8, 8, 960, 1),
+                                       (2, 64, 160, 128, 1),       # hourglass split-conv form (row walk)
                                        (3, 14, 10, 96, 2)])
 def test_depthwise_fwd_dgrad_wgrad(B, H, W, C, s):
     from cvlite import ops_nn as nn

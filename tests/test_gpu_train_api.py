@@ -205,13 +205,17 @@ def test_jitter_buckets_sum_gradients_and_update_once():
     assert float((d_jit - d_ref).norm() / d_ref.norm()) < 1e-4
 
 
-def test_train_loop_raw_samples_jittered():
+def test_train_loop_raw_samples_jittered(tmp_path):
     """train() on reference-format raw samples: per-image preprocess_data + shape buckets, finite
     losses, weights move."""
     from cvlite import fcos
     from cvlite.train_fcos import SGD, train
     C = 20
     samples = _raw_samples(C, 9) * 2
+    from PIL import Image                               # one sample by file name (host decode)
+    path = str(tmp_path / "s0.png")
+    Image.fromarray(samples[0]["image"]).save(path)
+    samples[0] = dict(samples[0], image=path)
     model = fcos.build_model(C)
     net = model.net
     w0 = net.store.flat.clone()

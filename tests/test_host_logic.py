@@ -100,3 +100,20 @@ def test_preprocess_box_path_and_size_plan():
         flip, shp, S = padded_size((375, 500), [640, 1024], 800.0, 1333.0, rng)
         assert S % 128 == 0 and S >= shp.max() and shp.dtype == np.float32
         assert 640 - 1e-3 <= shp.min() <= 1024 + 1e-3 or shp.max() <= 1333.0 + 1e-3
+
+
+def test_parse_image_decodes_files(tmp_path):
+    """_parse_image (FCOS/data_preprocess.py:5-9) reads a JPEG / PNG file into [H,W,3] uint8 (PNG:
+    lossless, so the decode must return the written pixels exactly)."""
+    import numpy as np
+    from PIL import Image
+    from cvlite.data_preprocess import _parse_image
+    rng = np.random.default_rng(0)
+    a = rng.integers(0, 256, (37, 53, 3)).astype(np.uint8)
+    Image.fromarray(a).save(tmp_path / "x.png")
+    np.testing.assert_array_equal(_parse_image(str(tmp_path / "x.png")), a)
+    yy, xx = np.mgrid[0:37, 0:53]
+    sm = np.stack([yy * 6, xx * 4, (yy + xx) * 2], -1).astype(np.uint8)     # smooth: JPEG-friendly
+    Image.fromarray(sm).save(tmp_path / "x.jpg", quality=95)
+    j = _parse_image(str(tmp_path / "x.jpg"))
+    assert j.shape == (37, 53, 3) and j.dtype == np.uint8 and np.abs(j.astype(int) - sm).mean() < 3
