@@ -70,8 +70,9 @@ __device__ __forceinline__ void cursor_advance(const ConvSeg& S, RowCursor& c, i
   }
 }
 
-template <int BCO>
+template <int BCO, int BRT>
 __global__ void __launch_bounds__(NT) conv_wgrad_kernel(WgArgs g) {
+  constexpr int BR = BRT;      // reduction rows per step (64: two MFMA K-steps; 128: four)
   constexpr int PITCH_Y = BCO + 16;
   constexpr int PITCH_A = BKK + 16;
   constexpr int WCO = BCO / 2, WK = BKK / 2;
@@ -345,9 +346,19 @@ int wgrad_single(const cvl_conv_desc* d, const void* x, const void* dy, float* d
   }
   dim3 grid(tiles, nsplit);
   g_cvl_conv_last_kernel = CVL_CK_WG_S;
-  if (bco == 128) hipLaunchKernelGGL(conv_wgrad_kernel<128>, grid, dim3(NT), 0, s, g);
-  else if (bco == 64) hipLaunchKernelGGL(conv_wgrad_kernel<64>, grid, dim3(NT), 0, s, g);
-  else hipLaunchKernelGGL(conv_wgrad_kernel<32>, grid, dim3(NT), 0, s, g);
+  // 128-row steps (twice the MFMA work per barrier pair and loads in flight); the chunks are
+  // multiples of BM = 128, so a step never straddles a segment either way
+  const bool r128 = cvl_env_flag("CVL_WG_BR128");
+  if (bco == 128) {
+    if (r128) hipLaunchKernelGGL((conv_wgrad_kernel<128, 128>), grid, dim3(NT), 0, s, g);
+    else hipLaunchKernelGGL((conv_wgrad_kernel<128, 64>), grid, dim3(NT), 0, s, g);
+  } else if (bco == 64) {
+    if (r128) hipLaunchKernelGGL((conv_wgrad_kernel<64, 128>), grid, dim3(NT), 0, s, g);
+    else hipLaunchKernelGGL((conv_wgrad_kernel<64, 64>), grid, dim3(NT), 0, s, g);
+  } else {
+    if (r128) hipLaunchKernelGGL((conv_wgrad_kernel<32, 128>), grid, dim3(NT), 0, s, g);
+    else hipLaunchKernelGGL((conv_wgrad_kernel<32, 64>), grid, dim3(NT), 0, s, g);
+  }
   st = cvl_launch_status();
   if (st || g.direct) return st;
   const long n = (long)g.a.K * g.Cout;
