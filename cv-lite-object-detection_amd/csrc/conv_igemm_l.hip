@@ -221,7 +221,15 @@ int cvl_conv_igemm_l(const cvl_conv_desc* d, int dst_up, int dst_w, const void* 
   const long min_tiles = cvl_env_int("CVL_CONV_L_MIN_TILES", 128);
   int use_bn = bn;
   if (use_bn == 256 && (long)a.m_tiles * (a.Npad / 256) < cvl_env_int("CVL_CONV_L256_MIN_TILES", 512)) use_bn = 128;
+  // a launch that would leave CUs idle with 128-wide tiles takes 64-wide ones (twice the tiles),
+  // also when that lifts it over min_tiles (from the split-K 128-row kernel): FCOS A/B 970 -> 983
+  // img/s at 256 for the 128-tile conv4_x launches, -> 988 with the conv5_x ones (512: 966, 1024: 941)
+  static const int fill = cvl_env_int("CVL_CONV_L64_FILL", 256);
+  static const bool fill_pre = !cvl_env_flag("CVL_CONV_L64_NO_FILL_PRE");
+  const bool to64 = fill && use_bn == 128 && (long)a.m_tiles * (a.Npad / 128) < fill && a.Npad % 64 == 0;
+  if (fill_pre && to64) use_bn = 64;
   if ((long)a.m_tiles * (a.Npad / use_bn) < min_tiles) return -1;
+  if (to64) use_bn = 64;
   if (bn_stats)
     for (int i = 0; i < a.nseg; ++i)
       if ((a.seg[i].Hr * a.seg[i].Wr) % 4) return -1;
