@@ -199,7 +199,9 @@ int cvl_conv_igemm_l(const cvl_conv_desc* d, int dst_up, int dst_w, const void* 
                      hipStream_t s, const BnSumArgs* bsum) {
   if (cvl_env_flag("CVL_CONV_NO_L")) return -1;
   if (bsum && (d->mode != CVL_CONV_DGRAD || d->dst_f32 || d->beta != 0.f || dst_up != 1 || bn_stats)) return -1;
-  if (d->Cin % 64 != 0 || d->relu_in || d->n_store % 8 || (d->dst_f32 && bn_stats) ||
+  // fp32 destinations store element-wise: any n_store (the RetinaNet box heads: 9 anchors x 4 = 36)
+  const bool n_ok = d->dst_f32 ? (d->n_store % 4 == 0 && !cvl_env_flag("CVL_CONV_L_F32_N8")) : d->n_store % 8 == 0;
+  if (d->Cin % 64 != 0 || d->relu_in || !n_ok || (d->dst_f32 && bn_stats) ||
       (!d->dst_f32 && (d->ld_dst % 8 || d->dst_coff % 8)) || (d->dst_f32 && cvl_env_flag("CVL_CONV_L_NO_F32")))
     return -1;
   // 256-wide tiles (forward and data-gradient) for launches with >= CVL_CONV_L256_MIN_TILES of
