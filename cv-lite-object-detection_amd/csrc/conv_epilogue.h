@@ -122,6 +122,44 @@ __device__ __forceinline__ void conv_l_epilogue(const ConvArgs& a, const ConvSeg
         atomicAdd(st + 1, (double)s2);
       }
     }
+  } else if (a.stats && !tile_stats && HWr >= WM) {
+    // maps of H*W % 256 != 0 (RetinaNet's 40x40 / 20x20 at 640): a wave's WM rows span at most two
+    // images, so each column's sums split at the image boundary, reduce over the wave by lane
+    // shuffles, and one atomic pair per (wave, image, column) replaces one per accumulator quad
+    const int r0 = mloc0 + wm * WM;
+    const int imgA = r0 / HWr;
+    const int rb = (imgA + 1) * HWr;            // first row of the next image
+    const int rend = r0 + WM < S.rows ? r0 + WM : S.rows;
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      float a1 = 0.f, a2 = 0.f, b1 = 0.f, b2 = 0.f;
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int ml = r0 + i * 16 + lg * 4 + e;
+          const float v = acc[i][j][e];
+          if (ml < rend) {
+            if (ml < rb) { a1 += v; a2 += v * v; }
+            else { b1 += v; b2 += v * v; }
+          }
+        }
+      a1 += __shfl_xor(a1, 16, 64); a1 += __shfl_xor(a1, 32, 64);
+      a2 += __shfl_xor(a2, 16, 64); a2 += __shfl_xor(a2, 32, 64);
+      b1 += __shfl_xor(b1, 16, 64); b1 += __shfl_xor(b1, 32, 64);
+      b2 += __shfl_xor(b2, 16, 64); b2 += __shfl_xor(b2, 32, 64);
+      const int n = n0 + wn * WN + j * 16 + lr;
+      if (lg == 0 && n < a.n_store && r0 < rend) {
+        double* st = a.stats + ((long)imgA * a.n_store + n) * 2;
+        atomicAdd(st, (double)a1);
+        atomicAdd(st + 1, (double)a2);
+        if (rb < rend) {
+          double* sb = a.stats + ((long)(imgA + 1) * a.n_store + n) * 2;
+          atomicAdd(sb, (double)b1);
+          atomicAdd(sb + 1, (double)b2);
+        }
+      }
+    }
   } else if (a.stats && !tile_stats) {
     // the 4 rows of an accumulator quad share one image (host: H*W % 4 == 0)
 #pragma unroll

@@ -469,3 +469,25 @@ def test_conv_wgrad_small_n_heads_grouped(n_store, coff, ld, B, shapes):
         got = outs[0][l].view(3, 3, C, n_store).double().cpu()
         scale = (exp - 0.5).abs().max().item()
         torch.testing.assert_close(got, exp, rtol=1e-4, atol=1e-5 * scale, msg=lambda m: "level %d: %s" % (l, m))
+
+
+@pytest.mark.parametrize("B,H,Cin,Cout,k", [(3, 40, 256, 1024, 1), (4, 20, 256, 256, 3), (5, 10, 128, 128, 3),
+                                            (2, 40, 256, 256, 3)])
+def test_conv_bn_stats_maps_not_tile_aligned(B, H, Cin, Cout, k, kern):
+    """Fused BN statistics when H*W % 256 != 0 (RetinaNet 640: 40x40, 20x20 maps; 10x10): a tile's
+    waves straddle image boundaries, the per-(wave, image, column) split reduction must equal the
+    per-image column sums of the bf16 output."""
+    from cvlite import ops_nn as nn
+    g = torch.Generator().manual_seed(B * H + Cout)
+    x = rnd(B, H, H, Cin, gen=g)
+    w = rnd(k, k, Cin, Cout, scale=(k * k * Cin) ** -0.5, gen=g)
+    wf, _, npad, _, _ = packs(w)
+    bias = (torch.randn(npad, generator=g) * 0.1).float().cuda()
+    out = torch.zeros((B, H, H, Cout), dtype=BF, device="cuda")
+    stats = torch.zeros((B, Cout, 2), dtype=torch.float64, device="cuda")
+    pad = (k - 1) // 2
+    d = nn.make_desc(nn.FWD, B, Cin, k, k, 1, pad, pad, npad, Cout, Cout, [nn.seg(H, H, H, H, wf, bias)])
+    nn.conv_igemm(d, x.to(BF).cuda(), out, stats)
+    o = out.double().cpu()
+    st = torch.stack([o.sum((1, 2)), (o * o).sum((1, 2))], -1)
+    torch.testing.assert_close(stats.cpu(), st, rtol=1e-5, atol=1e-3)

@@ -51,11 +51,26 @@ def main():
     ap.add_argument("--size", type=int, default=512)
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--out", default=None)
+    ap.add_argument("--model", default="fcos", choices=["fcos", "retinanet", "centernet"])
     args = ap.parse_args()
     B, H = args.bs, args.size
-    net = FCOSNet(20, device=torch.device("cuda"), seed=0)
-    tr = FCOSTrainer(net, B, (H, H), use_graph=False)
-    tr.load_batch(*synthetic_batch(B, H, H, 20, seed=1234, device="cuda"))
+    dev = torch.device("cuda")
+    if args.model == "retinanet":              # configs[4]: 640, bs 8, C = 80
+        from cvlite.retinanet import RetinaNet
+        from cvlite.train_retinanet import RetinaTrainer, synthetic_coco_batch
+        rn = RetinaNet(80, {}, anchor_sizes=[20.0, 40.0, 80.0, 160.0, 320.0])
+        tr = RetinaTrainer(rn.model, rn, B, H, n_max=50, use_graph=False)
+        tr.load_candidates(*synthetic_coco_batch(3 * B, H, 80, n_max=50, seed=4321, device=dev))
+    elif args.model == "centernet":            # configs[3]: 512, bs 8, BN sub-batch 2
+        from cvlite.hourglass_net import HourglassNet
+        from cvlite.train_centernet import CenterNetTrainer, synthetic_batch as cn_batch
+        net = HourglassNet(20, device=dev, seed=0)
+        tr = CenterNetTrainer(net, B, (H, H), sub_batch_sz=2, n_max=16, use_graph=False)
+        tr.load_batch(*cn_batch(B, H, H, 20, n_max=16, seed=777, device=dev))
+    else:
+        net = FCOSNet(20, device=dev, seed=0)
+        tr = FCOSTrainer(net, B, (H, H), use_graph=False)
+        tr.load_batch(*synthetic_batch(B, H, H, 20, seed=1234, device="cuda"))
     tr.step()                      # warm-up (allocations, first-touch)
     torch.cuda.synchronize()
     calls = collections.OrderedDict()
@@ -80,7 +95,8 @@ def main():
         return orig[2](desc, x, dy, dws, beta)
 
     nn.conv_igemm, nn.conv_wgrad, nn.conv_wgrad_grouped = igemm, wgrad, wgrad_g
-    tr.load_batch(*synthetic_batch(B, H, H, 20, seed=77, device="cuda"))
+    if args.model == "fcos":
+        tr.load_batch(*synthetic_batch(B, H, H, 20, seed=77, device="cuda"))
     tr.step()
     torch.cuda.synchronize()
     nn.conv_igemm, nn.conv_wgrad, nn.conv_wgrad_grouped = orig
@@ -107,7 +123,7 @@ def main():
     by_mode = collections.defaultdict(float)
     for r in rows:
         by_mode[r[1].split()[0]] += r[0]
-    lines = ["# Conv launches of one FCOS step (bs %d, %dx%d), replayed alone" % (B, H, H), "",
+    lines = ["# Conv launches of one %s step (bs %d, %dx%d), replayed alone" % (args.model, B, H, H), "",
              "Total %.3f ms per step over %d launches (%s)." % (
                  tot, sum(counts.values()), ", ".join("%s %.3f ms" % kv for kv in sorted(by_mode.items()))), "",
              "| ms/step | launch | kernel | per step | us/launch | TFLOP/s | frac of 2.5 PF |",
