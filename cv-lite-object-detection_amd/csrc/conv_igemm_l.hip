@@ -219,15 +219,20 @@ int cvl_conv_igemm_l(const cvl_conv_desc* d, int dst_up, int dst_w, const void* 
   // below 128 tiles the 128-row kernel with split-K fills the 256 CUs better (tests lower the
   // bar).  Whole-step sweep (tools/gpu_knob_sweep.sh, FCOS bs=16): 384 -> 773, 256 -> 785,
   // 192 -> 785, 128 -> 807, 1 -> 789 img/s (conv4_x 3x3 sits at exactly 128 tiles).  A launch
-  // with too few 256-wide tiles drops to the 128-wide tile first.
+  // with too few 256-wide tiles drops to the 128-wide tile first (since the X32 kernel: 256 tiles,
+  // e.g. one tower's 341-tile data gradient into F, FCOS 989 -> 995 img/s; 128: within noise).
   const long min_tiles = cvl_env_int("CVL_CONV_L_MIN_TILES", 128);
   int use_bn = bn;
-  if (use_bn == 256 && (long)a.m_tiles * (a.Npad / 256) < cvl_env_int("CVL_CONV_L256_MIN_TILES", 512)) use_bn = 128;
+  if (use_bn == 256 && (long)a.m_tiles * (a.Npad / 256) < cvl_env_int("CVL_CONV_L256_MIN_TILES", 256)) use_bn = 128;
+  // short-K launches are HBM-bound: 128-wide tiles (more of them) beat the 256-wide ones (FCOS +0.6 %,
+  // CenterNet +0.4 % at K < 512)
+  const int w256_min_k = cvl_env_int("CVL_CONV_W256_MIN_K", 512);
+  if (use_bn == 256 && a.K < w256_min_k) use_bn = 128;
   // a launch that would leave CUs idle with 128-wide tiles takes 64-wide ones (twice the tiles),
   // also when that lifts it over min_tiles (from the split-K 128-row kernel): FCOS A/B 970 -> 983
   // img/s at 256 for the 128-tile conv4_x launches, -> 988 with the conv5_x ones (512: 966, 1024: 941)
-  static const int fill = cvl_env_int("CVL_CONV_L64_FILL", 256);
-  static const bool fill_pre = !cvl_env_flag("CVL_CONV_L64_NO_FILL_PRE");
+  const int fill = cvl_env_int("CVL_CONV_L64_FILL", 256);
+  const bool fill_pre = !cvl_env_flag("CVL_CONV_L64_NO_FILL_PRE");
   const bool to64 = fill && use_bn == 128 && (long)a.m_tiles * (a.Npad / 128) < fill && a.Npad % 64 == 0;
   if (fill_pre && to64) use_bn = 64;
   if ((long)a.m_tiles * (a.Npad / use_bn) < min_tiles) return -1;

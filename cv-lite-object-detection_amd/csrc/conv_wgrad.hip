@@ -258,7 +258,7 @@ int pick_splits(int tiles, int m_total, int bco) {
   // per workgroup (~0.8 us per 64-row step) + the fp32 slab round trip; the cheapest split wins
   // rows per split at least: 128 (one BM granule) lets small-M launches (CenterNet 16x16 maps at
   // bs 8: 2048 rows) spread over more workgroups: CenterNet 488 -> 510 img/s vs 512
-  static const int min_chunk = cvl_env_int("CVL_WG_MIN_CHUNK", 128);
+  const int min_chunk = cvl_env_int("CVL_WG_MIN_CHUNK", 128);
   int max_s = m_total / min_chunk;
   if (max_s < 1) max_s = 1;
   if (max_s > 8192 / tiles) max_s = 8192 / tiles > 1 ? 8192 / tiles : 1;
