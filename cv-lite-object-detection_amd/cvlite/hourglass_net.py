@@ -90,6 +90,7 @@ class SepConv(object):
         self.split = False
         self.pw = _PointwiseOf(store, self.pwname, cin, cout) if self.can_split else None
         self.on_mode_change = None         # the owning net's plan invalidation
+        self.bias_sink = None              # the owning net's deferred bias-gradient list
         self._t = self._dt = None
 
     def want_split(self, H, W):
@@ -143,7 +144,11 @@ class SepConv(object):
             nn.depthwise_wgrad(x, self._dt, self.store.g(self.dwname), 3, 1, 1, 1)
         else:
             self.conv.wgrad(x, dy, B, H, W, bias=False)
-        nn.bias_grad(dy, int(dy.shape[-1]), 0, self.cout, 0, HW, HW, B, self.db)
+        item = (dy, int(dy.shape[-1]), 0, self.cout, 0, HW, HW, B, self.db, 0.0)
+        if self.bias_sink is not None:      # batched at the end of the net's backward
+            self.bias_sink.append(item)
+        else:
+            nn.bias_grad(*item[:9])
 
     def dgrad(self, dy, B, H, W, out=None, beta=0.0):
         if self.split:
@@ -435,9 +440,13 @@ class HourglassNet(object):
         c = self.cnn_out
         Ho, Wo = hw["o4"]
         HW = Ho * Wo
+        # the separable convs' bias gradients (column sums of their output gradients) are collected
+        # and run as batched cvl_bias_grad_multi launches (16 per launch pair) at the end, instead
+        # of two launches per conv (91 convs)
+        sink = [(d_out, int(d_out.shape[-1]), 0, 4 + self.C, 0, HW, HW, B, self.g_beff, 0.0)]
+        for sc in self.seps()[1:]:
+            sc.bias_sink = sink
         c.wgrad(v["o4"], d_out, B, Ho, Wo, bias=False)
-        nn.bias_grad(d_out, int(d_out.shape[-1]), 0, 4 + self.C, 0, HW, HW, B, self.g_beff)
-        nn.bias_scalar_unfold(self.g_beff, c.db, self.store.g(self.bfocal), 4)
         g = {}
         g["o4"] = c.dgrad(d_out, B, Ho, Wo)
 
@@ -495,6 +504,10 @@ class HourglassNet(object):
         unpool("stack_in", "cnn1")
         blk("cnn_block_1", g["cnn1"], "blk0", 0.0)
         self.stem.backward(g["blk0"], sv_stem)
+        for sc in self.seps()[1:]:
+            sc.bias_sink = None
+        nn.bias_grad_multi(sink)
+        nn.bias_scalar_unfold(self.g_beff, c.db, self.store.g(self.bfocal), 4)
         self.unfold_grads()
         self._saved = None
         if hook is not None:
