@@ -13,7 +13,7 @@ import os
 import torch
 
 from . import ops_nn as nn
-from .layers import BF16, BatchNorm, Conv, ConvBN, StatsArena
+from .layers import join_side, BF16, BatchNorm, Conv, ConvBN, StatsArena
 
 STEM_K = 7
 STEM_KP = int(os.environ.get("CVL_STEM_KP", 192))   # im2col K = 7*7*3 = 147 padded: 192 = 3 x 64 lets the
@@ -219,6 +219,8 @@ class ResNet50(object):
                 else:
                     dh = st[bi].backward(dh, ssv[si][bi], arena=arena)
             if si > 0:
+                join_side(dh.device)          # this stage's weight gradients are final
                 hook("conv%d" % (si + 2))
         self.stem.backward(dh, sv_stem)
+        join_side(dh.device)
         hook("conv2_stem")
