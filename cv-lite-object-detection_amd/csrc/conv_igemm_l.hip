@@ -212,6 +212,7 @@ int cvl_conv_igemm_l(const cvl_conv_desc* d, int dst_up, int dst_w, const void* 
                     (d->mode == CVL_CONV_FWD || !cvl_env_flag("CVL_CONV_NO_DGRAD_256"));
   const int bn = w256 ? 256 : (d->Npad % 128 == 0 ? 128 : (d->Npad % 64 == 0 ? 64 : 0));
   if (!bn) return -1;
+  if (d->KH * d->KW * d->Cin < cvl_env_int("CVL_CONV_L_MIN_K", 0) && !bsum) return -1;   // A/B knob
   ConvArgs a;
   if (cvl_conv_prepare(d, BM, &a)) return -1;
   a.dst_up = dst_up;
