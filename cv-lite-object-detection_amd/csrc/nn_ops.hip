@@ -159,7 +159,8 @@ __global__ void __launch_bounds__(NT) im2col8_kernel(const float* __restrict__ x
 // pixels of one output row; it stages the KH input rows under them in LDS (coalesced fp32 reads,
 // zero padding materialised) and writes the segment's rows as contiguous 16-byte runs.
 constexpr int I2C_PX = 64;
-constexpr int I2C_MAXF = 7 * ((I2C_PX - 1) * 2 + 7) * 4;
+constexpr int I2C_OY = 2;                                // output rows per block (share staged rows)
+constexpr int I2C_MAXF = (7 + (I2C_OY - 1) * 2) * ((I2C_PX - 1) * 2 + 7) * 4;
 constexpr int I2C_MAXK = 256;                            // padded im2col width the table covers
 __global__ void __launch_bounds__(NT) im2col_tile_kernel(const float* __restrict__ x, cvl_bf16* __restrict__ out,
                                                          int H, int W, int C, int KH, int KW, int stride,
@@ -167,35 +168,40 @@ __global__ void __launch_bounds__(NT) im2col_tile_kernel(const float* __restrict
   __shared__ float tile[I2C_MAXF];
   __shared__ int koff[I2C_MAXK];                        // tile offset of im2col column k (-1: pad)
   const int nseg = (Wo + I2C_PX - 1) / I2C_PX;
+  const int nrb = (Ho + I2C_OY - 1) / I2C_OY;
   const int sg = blockIdx.x % nseg, t2 = blockIdx.x / nseg;
-  const int oy = t2 % Ho, b = t2 / Ho;
+  const int oy0 = (t2 % nrb) * I2C_OY, b = t2 / nrb;
+  const int noy = min(I2C_OY, Ho - oy0);
   const int ox0 = sg * I2C_PX;
   const int npx = min(I2C_PX, Wo - ox0);
   const int rowf = ((npx - 1) * stride + KW) * C;      // floats per staged input row
+  const int nrows = KH + (noy - 1) * stride;            // staged input rows (shared by the output rows)
   const int KK = KH * KW * C;
   for (int k = threadIdx.x; k < Kp8 * 8; k += NT) {     // the (row, tap, channel) decode, once
     const int tap = k / C, c = k - (k / C) * C;
     koff[k] = k < KK ? (tap / KW) * rowf + (tap - (tap / KW) * KW) * C + c : -1;
   }
-  const int iy0 = oy * stride - pad_t, ix0 = ox0 * stride - pad_l;
+  const int iy0 = oy0 * stride - pad_t, ix0 = ox0 * stride - pad_l;
   const float* xb = x + (long)b * H * W * C;
-  for (int i = threadIdx.x; i < KH * rowf; i += NT) {
+  for (int i = threadIdx.x; i < nrows * rowf; i += NT) {
     const int r = i / rowf, f = i - r * rowf;
     const int iy = iy0 + r, ix = ix0 + f / C;
     tile[i] = ((unsigned)iy < (unsigned)H && (unsigned)ix < (unsigned)W) ? xb[((long)iy * W + ix0) * C + f] : 0.f;
   }
   __syncthreads();
-  cvl_bf16* ob = out + (((long)b * Ho + oy) * Wo + ox0) * (long)(Kp8 * 8);
-  for (int it = threadIdx.x; it < npx * Kp8; it += NT) {
-    const int px = it / Kp8, j = it - px * Kp8;
-    const int base = px * stride * C;
+  const int per_row = npx * Kp8;
+  for (int it = threadIdx.x; it < noy * per_row; it += NT) {
+    const int q = it / per_row, rem = it - q * per_row;
+    const int px = rem / Kp8, j = rem - px * Kp8;
+    const int base = q * stride * rowf + px * stride * C;
     float v[8];
 #pragma unroll
     for (int u = 0; u < 8; ++u) {
       const int o = koff[j * 8 + u];
       v[u] = o >= 0 ? tile[o + base] : 0.f;
     }
-    *reinterpret_cast<s16x8*>(ob + (long)it * 8) = pack8(v);
+    cvl_bf16* ob = out + (((long)b * Ho + oy0 + q) * Wo + ox0) * (long)(Kp8 * 8);
+    *reinterpret_cast<s16x8*>(ob + (long)rem * 8) = pack8(v);
   }
 }
 
@@ -1064,7 +1070,8 @@ extern "C" int cvl_im2col(const float* x, int B, int H, int W, int C, int KH, in
   if (Kp % 8 == 0 && Kp <= I2C_MAXK && KH <= 7 && KW <= 7 && stride >= 1 && stride <= 2 && C <= 4 &&
       (long)B * Ho < (1L << 24)) {
     const int nseg = (Wo + I2C_PX - 1) / I2C_PX;
-    hipLaunchKernelGGL(im2col_tile_kernel, dim3(B * Ho * nseg), dim3(NT), 0, S_, x, (cvl_bf16*)out, H, W, C, KH, KW,
+    const int nrb = (Ho + I2C_OY - 1) / I2C_OY;
+    hipLaunchKernelGGL(im2col_tile_kernel, dim3(B * nrb * nseg), dim3(NT), 0, S_, x, (cvl_bf16*)out, H, W, C, KH, KW,
                        stride, pad_t, pad_l, Ho, Wo, Kp / 8);
     return cvl_launch_status();
   }
