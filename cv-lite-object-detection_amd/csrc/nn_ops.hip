@@ -529,6 +529,118 @@ __global__ void __launch_bounds__(NT) bn_bwd_kernel(const cvl_bf16* __restrict__
   }
 }
 
+// BN backward for small maps (H*W <= CVL_BN_SMALL_MAX_HW): the statistics are per image, so one
+// workgroup owning (image b, 16 channels) over ALL its rows can form (sum g, sum g*xhat), reduce
+// them in LDS (fixed order) and run the second pass right away -- one launch instead of pass 0 +
+// column reduction + pass 1 (the 32x32 / 16x16 stages are launch-bound on those three); its
+// second read of dy / z / y hits L2.  Per-image sums go to `sums` for the parameter gradients.
+constexpr int BNS_CB = 16;                    // channels per workgroup (2 x 8-channel thread columns)
+__global__ void __launch_bounds__(NT) bn_bwd_small_kernel(const cvl_bf16* __restrict__ dy,
+                                                          const cvl_bf16* __restrict__ y,
+                                                          const cvl_bf16* __restrict__ z, const float* __restrict__ mr,
+                                                          const float* __restrict__ gamma,
+                                                          const float* __restrict__ bnb, cvl_bf16* __restrict__ dz,
+                                                          cvl_bf16* __restrict__ g_out, double* __restrict__ sums,
+                                                          int C, int HW, float dz_beta, float act_hi) {
+  constexpr int TPR = BNS_CB / 8, RPP = NT / TPR;
+  const int b = blockIdx.y;
+  const int cg = threadIdx.x % TPR, rsub = threadIdx.x / TPR;
+  const int c0 = blockIdx.x * BNS_CB + cg * 8;
+  const bool zmask = !y && bnb;
+  float m[8], rs[8], ga[8], be[8], s1[8], s2[8];
+#pragma unroll
+  for (int u = 0; u < 8; ++u) {
+    const long bc = (long)b * C + c0 + u;
+    m[u] = mr[bc * 2];
+    rs[u] = mr[bc * 2 + 1];
+    ga[u] = gamma[c0 + u];
+    be[u] = zmask ? bnb[c0 + u] : 0.f;
+    s1[u] = 0.f;
+    s2[u] = 0.f;
+  }
+  auto grad = [&](long off, float* g, float* xh) {
+    float zz[8];
+    unpack8(*reinterpret_cast<const s16x8*>(dy + off), g);
+    unpack8(*reinterpret_cast<const s16x8*>(z + off), zz);
+    if (y) {
+      float yy[8];
+      unpack8(*reinterpret_cast<const s16x8*>(y + off), yy);
+#pragma unroll
+      for (int u = 0; u < 8; ++u) g[u] = (yy[u] > 0.f && yy[u] < act_hi) ? g[u] : 0.f;
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      xh[u] = (zz[u] - m[u]) * rs[u];
+      if (zmask) {
+        const float a = bn_affine(zz[u], m[u], rs[u], ga[u], be[u]);
+        g[u] = (a > 0.f && a < act_hi) ? g[u] : 0.f;
+      }
+    }
+  };
+  const long base = (long)b * HW;
+  for (int r = rsub; r < HW; r += RPP) {
+    float g[8], xh[8];
+    grad((base + r) * C + c0, g, xh);
+#pragma unroll
+    for (int u = 0; u < 8; ++u) { s1[u] += g[u]; s2[u] += g[u] * xh[u]; }
+  }
+  __shared__ float red[NT][17];
+  __shared__ float tot[BNS_CB][2];
+#pragma unroll
+  for (int u = 0; u < 8; ++u) { red[threadIdx.x][u] = s1[u]; red[threadIdx.x][8 + u] = s2[u]; }
+  __syncthreads();
+  if (threadIdx.x < BNS_CB) {                 // channel cc: its column's RPP partials in order
+    const int cc = threadIdx.x, col = cc / 8, u = cc % 8;
+    float a1 = 0.f, a2 = 0.f;
+    for (int k = 0; k < RPP; ++k) { a1 += red[k * TPR + col][u]; a2 += red[k * TPR + col][8 + u]; }
+    tot[cc][0] = a1;
+    tot[cc][1] = a2;
+    double* o = sums + ((long)b * C + blockIdx.x * BNS_CB + cc) * 2;
+    o[0] = (double)a1;
+    o[1] = (double)a2;
+  }
+  __syncthreads();
+  const float inv = 1.0f / (float)HW;
+  float k1[8], k2[8], gm[8];
+#pragma unroll
+  for (int u = 0; u < 8; ++u) {
+    k1[u] = (float)(double)tot[cg * 8 + u][0] * inv;
+    k2[u] = (float)(double)tot[cg * 8 + u][1] * inv;
+    gm[u] = ga[u] * rs[u];
+  }
+  for (int r = rsub; r < HW; r += RPP) {
+    const long off = (base + r) * C + c0;
+    float g[8], xh[8], o[8];
+    grad(off, g, xh);
+    if (g_out) *reinterpret_cast<s16x8*>(g_out + off) = pack8(g);
+#pragma unroll
+    for (int u = 0; u < 8; ++u) o[u] = gm[u] * (g[u] - k1[u] - xh[u] * k2[u]);
+    if (dz_beta != 0.f) {
+      float old[8];
+      unpack8(*reinterpret_cast<const s16x8*>(dz + off), old);
+#pragma unroll
+      for (int u = 0; u < 8; ++u) o[u] += dz_beta * old[u];
+    }
+    *reinterpret_cast<s16x8*>(dz + off) = pack8(o);
+  }
+}
+
+// parameter gradients from the per-image sums, images in order (float64):
+// dbeta[c] = sum_b S_g(b, c) (+ beta_acc * old), dgamma[c] = sum_b S_gx(b, c) (+ ...), conv bias 0
+__global__ void bn_param_grads_kernel(const double* __restrict__ sums, int B, int C, float* dgamma, float* dbeta,
+                                      float* conv_dbias, float beta_acc) {
+  const int c = blockIdx.x * NT + threadIdx.x;
+  if (c >= C) return;
+  double a1 = 0.0, a2 = 0.0;
+  for (int bb = 0; bb < B; ++bb) {
+    a1 += sums[((long)bb * C + c) * 2];
+    a2 += sums[((long)bb * C + c) * 2 + 1];
+  }
+  if (conv_dbias) conv_dbias[c] = 0.f;
+  dbeta[c] = (float)a1 + (beta_acc != 0.f ? beta_acc * dbeta[c] : 0.f);
+  dgamma[c] = (float)a2 + (beta_acc != 0.f ? beta_acc * dgamma[c] : 0.f);
+}
+
 // out[y][c][0..1] = sum_r part[y][r][c][0..1]: a block owns 32 channels (256 contiguous bytes per
 // row) and 8 row groups; the row groups are combined in a fixed order (deterministic, float64)
 __global__ void __launch_bounds__(NT) bn_colsum_kernel(const float* __restrict__ part, int R, int C,
@@ -1139,6 +1251,16 @@ static int bn_backward_impl(const void* dy, const void* y_relu, const float* bn_
   double* sums = reinterpret_cast<double*>(workspace);
   double* dbsum = sums + 2 * (size_t)B * C;
   float* part0 = reinterpret_cast<float*>(dbsum + 2 * (size_t)C);
+  // one-launch form: opt-in (CVL_BN_SMALL_MAX_HW=<max H*W>); measured slower than the three
+  // launches on the bench (FCOS 1004 -> 996 at 256, -> 958 at 1024: too few, too long workgroups)
+  if (HW <= cvl_env_int("CVL_BN_SMALL_MAX_HW", 0) && C % BNS_CB == 0) {
+    hipLaunchKernelGGL(bn_bwd_small_kernel, dim3(C / BNS_CB, B), dim3(NT), 0, S_, (const cvl_bf16*)dy,
+                       (const cvl_bf16*)y_relu, (const cvl_bf16*)z, mean_rstd, gamma, bn_beta, (cvl_bf16*)dz,
+                       (cvl_bf16*)g_out, sums, C, HW, 0.f, act_hi);
+    hipLaunchKernelGGL(bn_param_grads_kernel, dim3((C + NT - 1) / NT), dim3(NT), 0, S_, (const double*)sums, B, C,
+                       dgamma, dbeta, conv_dbias, beta_acc);
+    return cvl_launch_status();
+  }
   dim3 g1(nchunk, B);
   hipLaunchKernelGGL(bn_bwd_kernel<0>, g1, dim3(NT), 0, S_, (const cvl_bf16*)dy, (const cvl_bf16*)y_relu,
                      (const cvl_bf16*)z, mean_rstd, gamma, (const double*)nullptr, (cvl_bf16*)nullptr,

@@ -138,7 +138,9 @@ def test_fcos_mobilenetv2_graph_vs_oracle():
         if float(gr.norm()) < 1e-3 * big or k.endswith("_conv/bias"):
             continue
         e_gpu, e_emu = rel(net.store.g(k).cpu(), gr), rel(g16[k], gr)
-        excess.append((e_gpu - (1.5 * e_emu + 0.05), e_gpu, e_emu, k))
+        # per tensor within 2x the bf16-storage oracle's own divergence + 0.1, the bound the FCOS
+        # whole-graph test uses (chaotic random-init tensors reach rel-L2 ~0.7 in the oracle itself)
+        excess.append((e_gpu - (2.0 * e_emu + 0.1), e_gpu, e_emu, k))
     excess.sort(reverse=True)
     print("worst (excess, gpu, bf16-oracle, tensor):", excess[:4])
     assert excess[0][0] <= 0, excess[:4]

@@ -19,8 +19,12 @@ def bfr(t):
 @pytest.mark.parametrize("B,HW,C,relu,res", [(2, 64, 64, True, False), (3, 16, 256, False, True),
                                              (1, 256, 32, True, True), (2, 1000, 64, True, False),
                                              (1, 300, 2048, True, True), (2, 4096, 256, True, False)])
-def test_bn_forward_backward(B, HW, C, relu, res):
+@pytest.mark.parametrize("small", [False, True])
+def test_bn_forward_backward(B, HW, C, relu, res, small, monkeypatch):
+    """small=True: the opt-in one-launch backward for small maps (CVL_BN_SMALL_MAX_HW)."""
     from cvlite import ops_nn as nn
+    if small:
+        monkeypatch.setenv("CVL_BN_SMALL_MAX_HW", "4096")
     g = torch.Generator().manual_seed(B * 100 + C)
     z = bfr(torch.randn(B, HW, C, generator=g, dtype=torch.float64) * 2 + 0.5)
     gamma = torch.rand(C, generator=g, dtype=torch.float64) + 0.5
