@@ -234,7 +234,8 @@ int cvl_conv_igemm_l(const cvl_conv_desc* d, int dst_up, int dst_w, const void* 
   // img/s at 256 for the 128-tile conv4_x launches, -> 988 with the conv5_x ones (512: 966, 1024: 941)
   const int fill = cvl_env_int("CVL_CONV_L64_FILL", 256);
   const bool fill_pre = !cvl_env_flag("CVL_CONV_L64_NO_FILL_PRE");
-  const bool to64 = fill && use_bn == 128 && (long)a.m_tiles * (a.Npad / 128) < fill && a.Npad % 64 == 0;
+  const bool to64 = fill && use_bn == 128 && (long)a.m_tiles * (a.Npad / 128) < fill && a.Npad % 64 == 0 &&
+                    !(bsum && cvl_env_flag("CVL_BSUM_NO_FILL"));
   if (fill_pre && to64) use_bn = 64;
   if ((long)a.m_tiles * (a.Npad / use_bn) < min_tiles) return -1;
   if (to64) use_bn = 64;
