@@ -27,6 +27,9 @@ STRIDES = (8, 16, 32, 64, 128)
 # CVL_TOWER_PAIR=0 runs the two towers as separate launches (A/B only; the paired 10-segment
 # launches are the default)
 PAIR_TOWERS = os.environ.get("CVL_TOWER_PAIR", "1") != "0"
+# tower layer 0 reads the shared F: its two data gradients as ONE paired launch into a temporary
+# + one add (CVL_TOWER0_PAIR=0: two launches, the second accumulating into dF)
+PAIR_TOWER0_DGRAD = os.environ.get("CVL_TOWER0_PAIR", "1") != "0"
 # CVL_FPN_FUSE=0 runs P3..P5's 3x3 output convs as separate launches (A/B only)
 FUSE_FPN = os.environ.get("CVL_FPN_FUSE", "1") != "0"
 
@@ -261,12 +264,16 @@ class FPNDetector(object):
                     conv = tw[i]
                     d = conv.fwd_desc(B, self._tower_segs(conv, B, shapes, off), ld_dst=FPN_C)
                     nn.conv_wgrad(d, towers[t][i], dAs[t], conv.dw)
-            if i > 0 and paired:
+            if paired and (i > 0 or PAIR_TOWER0_DGRAD):
                 dd = self.cls_tower[i].dgrad_desc(B, self._pair_segs(i, B, shapes, off, P, fwd=False), ld_dst=FPN_C)
                 dst = torch.empty((2 * BP, FPN_C), dtype=BF16, device=dev)
                 src_all = torch.as_strided(dAs[0], (2 * BP, FPN_C), (FPN_C, 1))
                 nn.conv_igemm(dd, src_all, dst)
-                dAs = [dst[:BP], dst[BP:]]
+                if i == 0:          # both towers read F: dF = the two halves' sum (one 682-tile launch)
+                    nn.add(dst[:BP], dst[BP:], dF)
+                    dAs = [dF, dF]
+                else:
+                    dAs = [dst[:BP], dst[BP:]]
                 continue
             nxt = []
             for t, tw in enumerate((self.cls_tower, self.reg_tower)):
