@@ -5,6 +5,12 @@
     python bench.py [--gpus N] [--steps K] [--warmup W]
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 ... bench.py --gpus N
 
+`--gpus N` (N > 1) without a torchrun environment (no WORLD_SIZE) starts the N ranks itself: it
+runs `python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1` on this same
+command line as a CHILD process (before anything touches the GPU; no exec) and exits with its
+status, so `bench.py --gpus 8` measures 8 ranks, one per GPU, over RCCL.  `--dry-run` forms the
+process group (RCCL on GPUs, gloo without) and prints the world it saw, without any GPU work.
+
 A step = synthetic batch copy into the static input buffers (device-to-device) + target
 assignment + forward + fused loss + backward + (RCCL all-reduce) + clip/SGD + weight re-pack,
 i.e. the whole reference train_fcos.py step for 16 images.  Rank 0 prints ONE JSON line.
@@ -12,6 +18,8 @@ i.e. the whole reference train_fcos.py step for 16 images.  Rank 0 prints ONE JS
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -259,6 +267,43 @@ def bench_centernet(args):
         dist.barrier()
 
 
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def launch_ranks(n, argv):
+    """`bench.py --gpus N` outside torchrun: N ranks (one process per GPU) under
+    torch.distributed.run, started as a child process; returns its exit status."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(n),
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.abspath(__file__)] + list(argv)
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")     # dmabuf IPC (RCCL peer buffers)
+    print("[bench] launching %d ranks: %s" % (n, " ".join(cmd)), file=sys.stderr, flush=True)
+    return subprocess.call(cmd, env=env)
+
+
+def dist_info(world):
+    import torch.distributed as tdist
+    if tdist.is_available() and tdist.is_initialized():
+        return {"backend": tdist.get_backend(), "world_size": tdist.get_world_size()}
+    return {"backend": None, "world_size": world}
+
+
+def dry_run(args):
+    """Form the process group exactly as a bench run does, report the world, touch no GPU."""
+    rank, world, _ = dist.init_from_env()
+    info = dist_info(world)
+    dist.barrier()
+    if rank == 0:
+        print(json.dumps({"dry_run": True, "n_gpus": world, "requested_gpus": args.gpus, "dist": info,
+                          "global_batch": args.bs * world}), flush=True)
+    dist.barrier()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -271,13 +316,18 @@ def main():
     ap.add_argument("--model", default="fcos", choices=["fcos", "retinanet", "centernet"],
                     help="fcos = the headline metric (configs[1]/[2]); retinanet = configs[4] "
                          "(R50-FPN 640x640 COCO-80 bs=8/GPU), a side line")
+    ap.add_argument("--dry-run", action="store_true", help="form the rank group, print the world, no GPU work")
     args = ap.parse_args()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
+    if args.dry_run:
+        return dry_run(args)
     if args.model == "retinanet":
         return bench_retinanet(args)
     if args.model == "centernet":
         return bench_centernet(args)
     rank, world, local = dist.init_from_env()
-    if world > 1 and args.gpus != world:
+    if args.gpus != world:
         print("warning: --gpus %d but WORLD_SIZE %d" % (args.gpus, world), file=sys.stderr)
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
@@ -347,6 +397,7 @@ def main():
                      "burst_ms_per_launch": round(k_ms, 4),
                      "burst_frac": round(k_flops / (k_ms * 1e-3) / 1e12 / PEAK_BF16_TFLOPS, 4),
                      "burst_note": "the same launch repeated back to back on its own (20x, HIP events)"},
+        "dist": dist_info(world),
         "model_flops_per_image": fl_img,
         "step_mfma_frac": round(img_s / world * fl_img / 1e12 / PEAK_BF16_TFLOPS, 4),
         "last_step_losses_cls_reg_cen": [round(x, 3) for x in losses],

@@ -1076,9 +1076,11 @@ __global__ void l2_sum_kernel(const float* __restrict__ term, int n, float* __re
 
 // lr = max(init * rate^floor(step / decay_step), min_lr); step += 1   (train_fcos.py:108-110)
 __global__ void lr_schedule_kernel(int* step, float* lr, double init_lr, double min_lr, double rate,
-                                   int decay_step) {
+                                   int decay_step, int max_decays) {
   const int s = *step;
-  const double l = init_lr * pow(rate, (double)(s / decay_step));
+  int e = s / decay_step;
+  if (max_decays >= 0 && e > max_decays) e = max_decays;
+  const double l = init_lr * pow(rate, (double)e);
   *lr = (float)(l > min_lr ? l : min_lr);
   *step = s + 1;
 }
@@ -1438,7 +1440,15 @@ extern "C" int cvl_lr_schedule(int32_t* step, float* lr, double init_lr, double 
                                int decay_step, cvl_stream_t stream) {
   CVL_CHECK_ARG(step && lr && decay_step > 0);
   hipLaunchKernelGGL(lr_schedule_kernel, dim3(1), dim3(1), 0, S_, step, lr, init_lr, min_lr, decay_rate,
-                     decay_step);
+                     decay_step, -1);
+  return cvl_launch_status();
+}
+
+extern "C" int cvl_lr_schedule_capped(int32_t* step, float* lr, double init_lr, double min_lr, double decay_rate,
+                                      int decay_step, int max_decays, cvl_stream_t stream) {
+  CVL_CHECK_ARG(step && lr && decay_step > 0 && max_decays >= 0);
+  hipLaunchKernelGGL(lr_schedule_kernel, dim3(1), dim3(1), 0, S_, step, lr, init_lr, min_lr, decay_rate,
+                     decay_step, max_decays);
   return cvl_launch_status();
 }
 

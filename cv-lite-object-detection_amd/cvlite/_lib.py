@@ -64,6 +64,7 @@ SIGNATURES = {
                               P, c_float, P]),
     "cvl_sgd_clip_update": (c_int, [P, P, P, ctypes.c_int64, P, c_float, c_float, c_float, P, P]),
     "cvl_lr_schedule": (c_int, [P, P, ctypes.c_double, ctypes.c_double, ctypes.c_double, c_int, P]),
+    "cvl_lr_schedule_capped": (c_int, [P, P, ctypes.c_double, ctypes.c_double, ctypes.c_double, c_int, c_int, P]),
     "cvl_l2_params_reg": (c_int, [P, P, P, c_int, P, P, P]),
     "cvl_select_first_nonzero": (c_int, [P, c_int, c_int, P, P, P]),
     "cvl_gather_rows": (c_int, [P, ctypes.c_int64, P, c_int, P, P]),

@@ -157,10 +157,16 @@ def _opt_state(opt):
 
 
 def _load_opt_state(opt, s):
-    if s and getattr(opt, "m", None) is not None:
-        opt.m.copy_(s["m"])
-        opt.v.copy_(s["v"])
-        opt.iterations.copy_(s["iterations"])
+    """Adam slots into a bound optimizer, or kept on it until bind() (a restore before the trainer
+    exists must not silently restart Adam at m = v = iterations = 0)."""
+    if not s:
+        return
+    if getattr(opt, "m", None) is not None:
+        opt.load_state(s)
+    elif hasattr(opt, "pending_state"):
+        opt.pending_state = s
+    else:
+        raise ValueError("checkpoint holds optimizer slots this optimizer object cannot take")
 
 
 class Variable(object):

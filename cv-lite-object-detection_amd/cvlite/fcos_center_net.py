@@ -28,6 +28,14 @@ from .layers import Conv
 
 
 class FCOSCenterNet(FCOSNet):
+    @staticmethod
+    def backbone_kind(name):
+        """FCOS/fcos_center.py:30-48 (and fcos_center_v1.py:30-48): "resnet50" -> ResNet50,
+        "resnet101" -> ResNet101 (taps conv3_block4_out / conv4_block23_out / conv5_block3_out),
+        every other name -> MobileNetV2.  (Plain fcos.py:29-41 has no ResNet101 branch.)"""
+        n = name.lower()
+        return n if n in ("resnet50", "resnet101") else "mobilenetv2"
+
     def __init__(self, num_classes, backbone_model="resnet50", device="cuda", seed=0, v1=False):
         self.v1 = v1
         self._init_common(num_classes, backbone_model, device, seed)

@@ -27,17 +27,22 @@ STRIDES = (8, 16, 32, 64, 128)
 # CVL_TOWER_PAIR=0 runs the two towers as separate launches (A/B only; the paired 10-segment
 # launches are the default)
 PAIR_TOWERS = os.environ.get("CVL_TOWER_PAIR", "1") != "0"
-# tower layer 0 reads the shared F: its two data gradients as ONE paired launch into a temporary
-# + one add (CVL_TOWER0_PAIR=0: two launches, the second accumulating into dF)
-PAIR_TOWER0_DGRAD = os.environ.get("CVL_TOWER0_PAIR", "1") != "0"
+
+
+def pair_tower0_dgrad():
+    """Tower layer 0 reads the shared F: its two data gradients as ONE paired launch into a
+    temporary + one add (default), or (CVL_TOWER0_PAIR=0) two launches, the second accumulating
+    into dF.  Read per backward, so both forms are testable in one process."""
+    return os.environ.get("CVL_TOWER0_PAIR", "1") != "0"
+
 # CVL_FPN_FUSE=0 runs P3..P5's 3x3 output convs as separate launches (A/B only)
 FUSE_FPN = os.environ.get("CVL_FPN_FUSE", "1") != "0"
 
 class FPNDetector(object):
     @staticmethod
     def backbone_kind(name):
-        """FCOS/fcos.py:29-41 (and fcos_center*.py): "resnet50" builds ResNet50, EVERY other name
-        builds MobileNetV2."""
+        """FCOS/fcos.py:29-41: "resnet50" builds ResNet50, EVERY other name builds MobileNetV2
+        (fcos_center*.py add a ResNet101 branch: FCOSCenterNet.backbone_kind)."""
         return "resnet50" if name.lower() == "resnet50" else "mobilenetv2"
 
     def _init_common(self, num_classes, backbone_model, device, seed):
@@ -251,6 +256,7 @@ class FPNDetector(object):
         # allocates them so): then each tower layer's data gradient is ONE 10-segment launch
         paired = PAIR_TOWERS and (dAs[1].data_ptr() - dAs[0].data_ptr() == BP * FPN_C * dAs[0].element_size()
                   and dAs[0].is_contiguous() and dAs[1].is_contiguous())
+        pair0 = pair_tower0_dgrad()
         for t in range(2):
             nn.relu_backward(dAs[t], towers[t][-1], dAs[t])         # the tower's final ReLU
         for i in range(3, -1, -1):
@@ -264,7 +270,7 @@ class FPNDetector(object):
                     conv = tw[i]
                     d = conv.fwd_desc(B, self._tower_segs(conv, B, shapes, off), ld_dst=FPN_C)
                     nn.conv_wgrad(d, towers[t][i], dAs[t], conv.dw)
-            if paired and (i > 0 or PAIR_TOWER0_DGRAD):
+            if paired and (i > 0 or pair0):
                 dd = self.cls_tower[i].dgrad_desc(B, self._pair_segs(i, B, shapes, off, P, fwd=False), ld_dst=FPN_C)
                 dst = torch.empty((2 * BP, FPN_C), dtype=BF16, device=dev)
                 src_all = torch.as_strided(dAs[0], (2 * BP, FPN_C), (FPN_C, 1))

@@ -301,9 +301,13 @@ def sgd_clip_update(w, g, v, lr_dev, momentum, inv_bs, clip, ws=None):
               float(inv_bs), float(clip), ptr(ws), stream())
 
 
-def lr_schedule(step_dev, lr_dev, init_lr, min_lr, decay_rate, decay_step):
-    _lib.call("cvl_lr_schedule", ptr(step_dev), ptr(lr_dev), float(init_lr), float(min_lr),
-              float(decay_rate), int(decay_step), stream())
+def lr_schedule(step_dev, lr_dev, init_lr, min_lr, decay_rate, decay_step, max_decays=None):
+    if max_decays is None:
+        _lib.call("cvl_lr_schedule", ptr(step_dev), ptr(lr_dev), float(init_lr), float(min_lr),
+                  float(decay_rate), int(decay_step), stream())
+    else:
+        _lib.call("cvl_lr_schedule_capped", ptr(step_dev), ptr(lr_dev), float(init_lr), float(min_lr),
+                  float(decay_rate), int(decay_step), int(max_decays), stream())
 
 
 class L2Reg(object):

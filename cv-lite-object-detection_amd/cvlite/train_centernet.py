@@ -27,6 +27,10 @@ class Adam(object):
         self.lr = float(learning_rate)
         self.beta_1, self.beta_2, self.epsilon = float(beta_1), float(beta_2), float(epsilon)
         self.m = self.v = self.iterations = self.lr_dev = self.ws = None
+        # slots restored from a checkpoint before the optimizer met its parameters (the reference
+        # restores tf.train.Checkpoint before training starts, train_hourglass_voc.py:332-344):
+        # applied by bind()
+        self.pending_state = None
 
     def bind(self, store):
         if self.m is None:
@@ -36,7 +40,17 @@ class Adam(object):
             self.iterations = torch.zeros(1, dtype=torch.int32, device=dev)
             self.lr_dev = torch.tensor([self.lr], dtype=torch.float32, device=dev)
             self.ws = torch.zeros(1, dtype=torch.float64, device=dev)
+        if self.pending_state is not None:
+            s, self.pending_state = self.pending_state, None
+            if s["m"].numel() != self.m.numel():
+                raise ValueError("restored Adam slots do not match the parameter layout")
+            self.load_state(s)
         return self
+
+    def load_state(self, s):
+        self.m.copy_(s["m"])
+        self.v.copy_(s["v"])
+        self.iterations.copy_(s["iterations"])
 
     def apply(self, store, inv_bs, clip):
         nn.adam_clip_update(store.flat, store.grad, self.m, self.v, self.lr_dev, self.iterations, self.beta_1,

@@ -38,8 +38,19 @@ class SGD(object):
 class FCOSTrainer(GraphStepper):
     def __init__(self, net, batch_size, image_hw, n_max=16, init_lr=5e-4, min_lr=1e-5, decay_step=1000,
                  decay_rate=0.9, momentum=0.9, gradient_clip=1.0, reg_type="l1", weight_decay=0.0,
-                 world=1, use_graph=True, st_step=0, targets="fcos", center_only=True):
+                 world=1, use_graph=True, st_step=0, targets="fcos", center_only=True, optimizer=None,
+                 max_decays=None):
         self.net = net
+        # optimizer: None or SGD -> Keras SGD with `momentum` (train_fcos.py:284-285); an Adam
+        # (cvlite.train_centernet.Adam, the tf.optimizers.Adam() stand-in) -> Keras Adam, what the
+        # centre variant trains with (train_fcos_center_voc.py:327).  The scheduled learning rate
+        # is written into the optimizer's device lr either way.  max_decays caps the decay
+        # exponent (the centre loops' step schedule, train_fcos_center_voc.py:150-157: init_lr,
+        # then init_lr / 10 from step 8000 on = decay_rate 0.1, decay_step 8000, max_decays 1).
+        self.adam = optimizer.bind(net.store) if hasattr(optimizer, "bind") else None
+        if optimizer is not None and self.adam is None:
+            momentum = float(getattr(optimizer, "momentum", momentum))
+        self.max_decays = max_decays
         # weight_decay * l2_params_reg (train_fcos.py:118-120, 160-164): the reference computes the
         # regulariser OUTSIDE the GradientTape, so it is added to each image's reported loss and
         # contributes nothing to the gradient; it is evaluated on the device at the start of the
@@ -77,7 +88,11 @@ class FCOSTrainer(GraphStepper):
         self.d_reg = torch.zeros((B, self.P, 32), dtype=BF16, device=dev)
         self.d_cls = torch.zeros((B, self.P, net.cls_ld), dtype=BF16, device=dev)
         self.losses = torch.zeros((B, 3), dtype=torch.float32, device=dev)
-        self.lr = torch.tensor([init_lr], dtype=torch.float32, device=dev)
+        if self.adam is not None:
+            self.lr = self.adam.lr_dev
+            self.lr.fill_(init_lr)
+        else:
+            self.lr = torch.tensor([init_lr], dtype=torch.float32, device=dev)
         self.step_dev = torch.tensor([st_step], dtype=torch.int32, device=dev)
         self.sumsq = torch.zeros(1, dtype=torch.float64, device=dev)
         self._init_stepper(net, world, use_graph)
@@ -104,10 +119,13 @@ class FCOSTrainer(GraphStepper):
 
     def _update(self):
         init_lr, min_lr, rate, dstep = self.sched
-        nn.lr_schedule(self.step_dev, self.lr, init_lr, min_lr, rate, dstep)
+        nn.lr_schedule(self.step_dev, self.lr, init_lr, min_lr, rate, dstep, max_decays=self.max_decays)
         st = self.net.store
-        nn.sgd_clip_update(st.flat, st.grad, st.mom, self.lr, self.momentum, 1.0 / (self.B * self.world),
-                           self.clip, ws=self.sumsq)
+        if self.adam is not None:
+            self.adam.apply(st, 1.0 / (self.B * self.world), self.clip)
+        else:
+            nn.sgd_clip_update(st.flat, st.grad, st.mom, self.lr, self.momentum, 1.0 / (self.B * self.world),
+                               self.clip, ws=self.sumsq)
         self.net.pack()
 
     def load_batch(self, images, boxes, nbox, img_dim=None):
@@ -143,8 +161,11 @@ class JitterFCOSTrainer(object):
 
     def __init__(self, net, batch_size, n_max=16, init_lr=5e-4, min_lr=1e-5, decay_step=1000, decay_rate=0.9,
                  momentum=0.9, gradient_clip=1.0, reg_type="l1", weight_decay=0.0, st_step=0, use_graph=True,
-                 max_buckets=12):
-        self.net, self.B, self.n_max = net, batch_size, n_max
+                 max_buckets=12, world=1):
+        # world > 1: data-parallel (dist.py) -- each rank runs its own bs images through its buckets,
+        # the summed gradient is all-reduced (one bucketed SUM over RCCL) before the shared update
+        # with 1 / (world * bs); the buckets differ per rank, so there is no overlap with the backward
+        self.net, self.B, self.n_max, self.world = net, batch_size, n_max, int(world)
         self.momentum, self.clip = momentum, gradient_clip
         self.sched = (init_lr, min_lr, decay_rate, decay_step)
         self.reg_type, self.use_graph, self.max_buckets = reg_type, use_graph, max_buckets
@@ -188,8 +209,16 @@ class JitterFCOSTrainer(object):
             idx = [i for i in range(bs) if sizes[i] == S]
             tr = self.bucket(S, len(idx))
             it = torch.tensor(idx, device=dev)
-            tr.load_batch(torch.stack([images[i] for i in idx]), boxes.index_select(0, it)[:, :tr.boxes.shape[1]],
-                          nbox.index_select(0, it), img_dim=img_dim.index_select(0, it))
+            bsel = boxes.index_select(0, it)
+            nmax = tr.boxes.shape[1]
+            if bsel.shape[1] < nmax:       # the batch's box arrays may be narrower than the trainer's
+                bsel = torch.cat([bsel, bsel.new_zeros((bsel.shape[0], nmax - bsel.shape[1], 5))], 1)
+            elif bsel.shape[1] > nmax:
+                if int(nbox.max()) > nmax:
+                    raise ValueError("an image has %d boxes, the trainer holds %d" % (int(nbox.max()), nmax))
+                bsel = bsel[:, :nmax]
+            tr.load_batch(torch.stack([images[i] for i in idx]), bsel.contiguous(), nbox.index_select(0, it),
+                          img_dim=img_dim.index_select(0, it))
             tr.run_fwd_bwd()
             if first:
                 self.acc.copy_(self.net.store.grad)
@@ -200,9 +229,12 @@ class JitterFCOSTrainer(object):
             self.ntgt.index_copy_(0, it, tr.ntgt)
         st = self.net.store
         st.grad.copy_(self.acc)
+        if self.world > 1:
+            dist.allreduce_grads(st.grad)
         init_lr, min_lr, rate, dstep = self.sched
         nn.lr_schedule(self.step_dev, self.lr, init_lr, min_lr, rate, dstep)
-        nn.sgd_clip_update(st.flat, st.grad, st.mom, self.lr, self.momentum, 1.0 / bs, self.clip, ws=self.sumsq)
+        nn.sgd_clip_update(st.flat, st.grad, st.mom, self.lr, self.momentum, 1.0 / (bs * self.world), self.clip,
+                           ws=self.sumsq)
         self.net.pack()
         return self.losses
 
@@ -282,7 +314,7 @@ def _batch_from_samples(train_data, idx, n_max):
 
 def train(train_data, training_loss, model, batch_size, optimizer, ckpt, ck_manager, st_step, max_steps,
           init_lr=1.0e-3, min_lr=1.0e-5, decay_step=1000, decay_rate=0.99, display_step=50, step_save=100,
-          step_cool=1000, weight_decay=1.0e-4, gradient_clip=1.0, save_loss_file="train_losses.csv"):
+          step_cool=1000, weight_decay=1.0e-4, gradient_clip=1.0, save_loss_file="train_losses.csv", world=None):
     """Same keywords and defaults as FCOS/train_fcos.py:87-93.
     * `model`: what cvlite.fcos.build_model returns (or its FCOSNet).
     * `train_data`: either the reference's raw samples dict(image = a DECODED [H,W,3] image,
@@ -296,41 +328,69 @@ def train(train_data, training_loss, model, batch_size, optimizer, ckpt, ck_mana
       prefix string (torch checkpoint at <prefix>.pt) and None.
     * weight_decay > 0 adds weight_decay * l2_params_reg to every image's reported loss and not to
       the gradient, exactly as the reference (the regulariser is computed outside the tape).
+    * world (cvlite extension; the reference is single-device): data-parallel over the initialised
+      torch.distributed group (None = its world size, 1 without one).  Every rank draws the same
+      global sample of world * batch_size indices from np.random (seed it identically on every
+      rank for a partition) and trains its own batch_size shard; gradients are all-reduced, the
+      reported losses are averaged over all world * batch_size images, and only rank 0 prints and
+      saves.
     The reference's thermal "Cooling GPU" sleep runs only with CVL_COOLING=1.  Returns None."""
     from . import checkpoint as ck
+    import torch.distributed as tdist
     net = getattr(model, "net", model)
     n_data = len(train_data)
     raw = "objects" in train_data[0]
+    dist_on = tdist.is_available() and tdist.is_initialized()
+    if world is None:
+        world = tdist.get_world_size() if dist_on else 1
+    world = int(world)
+    rank = tdist.get_rank() if (dist_on and world > 1) else 0
+    if world > 1 and not (dist_on and tdist.get_world_size() == world):
+        raise ValueError("train(world=%d) needs an initialised process group of that size" % world)
+    if n_data < world * batch_size:
+        raise ValueError("train_data holds %d samples, fewer than world * batch_size" % n_data)
+    say = print if rank == 0 else (lambda *a, **k: None)
     if raw:          # reference-format samples: per-image jittered sizes, shape-bucketed step
         n_max = max(16, max(len(s["objects"]["label"]) for s in train_data))
         trainer = JitterFCOSTrainer(net, batch_size, n_max=n_max, init_lr=init_lr, min_lr=min_lr,
                                     decay_step=decay_step, decay_rate=decay_rate, momentum=optimizer.momentum,
-                                    gradient_clip=gradient_clip, weight_decay=weight_decay, st_step=st_step)
+                                    gradient_clip=gradient_clip, weight_decay=weight_decay, st_step=st_step,
+                                    world=world)
         rng = np.random.default_rng()
     else:
         H, W = np.asarray(train_data[0]["image"]).shape[:2]
         n_max = max(16, max(len(s["label"]) for s in train_data))
         trainer = FCOSTrainer(net, batch_size, (H, W), n_max=n_max, init_lr=init_lr, min_lr=min_lr,
                               decay_step=decay_step, decay_rate=decay_rate, momentum=optimizer.momentum,
-                              gradient_clip=gradient_clip, weight_decay=weight_decay, st_step=st_step)
+                              gradient_clip=gradient_clip, weight_decay=weight_decay, st_step=st_step,
+                              world=world)
     dev = net.device
     start = time.time()
     elapsed = 0.0
     batch_objs = total_loss = trend_loss = 0.0
     tot = np.zeros(3)
     for step in range(st_step, max_steps):
-        idx = np.random.choice(n_data, size=batch_size, replace=False)       # train_fcos.py:112
+        idx = np.random.choice(n_data, size=world * batch_size, replace=False)   # train_fcos.py:112
+        idx = idx[rank * batch_size:(rank + 1) * batch_size]
         if raw:
             imgs, bx, nb, dims = _raw_batch(train_data, idx, rng)
-            per_img = trainer.step(imgs, bx, nb, dims).detach().double().cpu().numpy()
+            per_img = trainer.step(imgs, bx, nb, dims).detach().double()
         else:
             imgs, bx, nb, dims = _batch_from_samples(train_data, idx, n_max)
             trainer.load_batch(torch.from_numpy(imgs).to(dev), torch.from_numpy(bx).to(dev),
                                torch.from_numpy(nb).to(dev), img_dim=torch.from_numpy(dims).to(dev))
-            per_img = trainer.step().detach().double().cpu().numpy()     # [bs, 3] (cls, reg, cen)
-        ntgt = trainer.ntgt.sum(1).cpu().numpy()
-        for k in np.nonzero(ntgt == 0)[0]:
+            per_img = trainer.step().detach().double()     # [bs, 3] (cls, reg, cen)
+        ntgt = trainer.ntgt.sum(1)
+        for k in np.nonzero(ntgt.cpu().numpy() == 0)[0]:
             print("No targets at index", str(idx[k]) + ".")
+        if world > 1:        # report over the global batch: sums of every rank's images
+            red = torch.cat([per_img.sum(0), ntgt.sum().double().view(1)])
+            tdist.all_reduce(red)
+            per_img = (red[:3] / world).view(1, 3).cpu().numpy()
+            ntgt = np.array([float(red[3]) / world])
+        else:
+            per_img = per_img.cpu().numpy()
+            ntgt = ntgt.cpu().numpy()
         wd_term = weight_decay * float(trainer.l2_params_reg.item()) if weight_decay > 0.0 else 0.0
         acc = per_img.sum() + batch_size * wd_term
         if isinstance(ckpt, ck.Checkpoint):
@@ -347,36 +407,39 @@ def train(train_data, training_loss, model, batch_size, optimizer, ckpt, ck_mana
             tot[:] = 0.0
             elapsed = (time.time() - start) / 60.0
             start = time.time()
-            print("Iteration:", str(step + 1))
-            print("Learning Rate:", str(float(trainer.lr.item())))
-            print("Average Objs:", str(avg_objs))
-            print("Average Loss:", str(round(avg_loss, 5)))
-            print("Average Reg Loss:", str(round(avg[1], 5)))
-            print("Average Cls Loss:", str(round(avg[0], 5)))
-            print("Average Cen Loss:", str(round(avg[2], 5)))
+            say("Iteration:", str(step + 1))
+            say("Learning Rate:", str(float(trainer.lr.item())))
+            say("Average Objs:", str(avg_objs))
+            say("Average Loss:", str(round(avg_loss, 5)))
+            say("Average Reg Loss:", str(round(avg[1], 5)))
+            say("Average Cls Loss:", str(round(avg[0], 5)))
+            say("Average Cen Loss:", str(round(avg[2], 5)))
             if (step + 1) % step_save == 0:
                 training_loss.append((step + 1, avg_loss))
-                with open(save_loss_file, "w") as f:
-                    f.write("step,train_loss\n")
-                    for a, b in training_loss:
-                        f.write("%d,%s\n" % (a, b))
-                print("")
-                if ck_manager is not None and hasattr(ck_manager, "save"):
-                    print("Saved model to {}".format(ck_manager.save()))
+                if rank == 0:
+                    with open(save_loss_file, "w") as f:
+                        f.write("step,train_loss\n")
+                        for a, b in training_loss:
+                            f.write("%d,%s\n" % (a, b))
+                say("")
+                if rank != 0:
+                    pass
+                elif ck_manager is not None and hasattr(ck_manager, "save"):
+                    say("Saved model to {}".format(ck_manager.save()))
                 elif isinstance(ckpt, str) and ckpt:
                     save_checkpoint(ckpt, net, trainer, step + 1)
-                    print("Saved model to {}".format(ckpt + ".pt"))
+                    say("Saved model to {}".format(ckpt + ".pt"))
             if (step + 1) % step_cool != 0:
-                print("Elapsed Time:", str(elapsed), "mins.")
-                print("-" * 50)
+                say("Elapsed Time:", str(elapsed), "mins.")
+                say("-" * 50)
         if (step + 1) % step_cool == 0:
-            print("Trend Loss:", str(round(trend_loss / step_cool, 5)))
+            say("Trend Loss:", str(round(trend_loss / step_cool, 5)))
             trend_loss = 0.0
-            print("Elapsed Time:", str(elapsed), "mins.")
+            say("Elapsed Time:", str(elapsed), "mins.")
             if os.environ.get("CVL_COOLING") == "1":
-                print("Cooling GPU for 2 minutes.")
+                say("Cooling GPU for 2 minutes.")
                 time.sleep(120)
-            print("-" * 50)
+            say("-" * 50)
     return None
 
 

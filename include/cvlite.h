@@ -297,11 +297,16 @@ int cvl_bias_grad_multi(const cvl_bias_item* items, int n, void* workspace, size
  * (tf.clip_by_global_norm), then Keras SGD momentum v = m*v - lr*g; w += v.  Flat fp32 buffers;
  * lr read from device memory (graph-capturable); sumsq_ws: one float64.
  * cvl_lr_schedule: lr = max(init*rate^floor(step/decay_step), min_lr); step += 1 (device ints).
+ * cvl_lr_schedule_capped: the same with the exponent capped at max_decays (>= 0): the centre
+ * variants' step schedule (FCOS/train_fcos_center_voc.py:150-157: init_lr below step 8000, init/10
+ * from then on -- its init/100 branch is unreachable) is rate 0.1, decay_step 8000, max_decays 1.
  * ---------------------------------------------------------------------------------------- */
 int cvl_sgd_clip_update(float* w, const float* g, float* v, int64_t n, const float* lr_dev,
                         float momentum, float inv_bs, float clip, double* sumsq_ws, cvl_stream_t stream);
 int cvl_lr_schedule(int32_t* step, float* lr, double init_lr, double min_lr, double decay_rate,
                     int decay_step, cvl_stream_t stream);
+int cvl_lr_schedule_capped(int32_t* step, float* lr, double init_lr, double min_lr, double decay_rate,
+                           int decay_step, int max_decays, cvl_stream_t stream);
 
 /* l2_params_reg of train_fcos.py:118-120 = sum over tensors v of sqrt(sum(tf.nn.l2_loss(v)))
  * = sum_v sqrt(0.5 * sum(v^2)), over the tensors at device offsets[i] / sizes[i] of the flat

@@ -140,3 +140,46 @@ def test_rccl_segmented_allreduce_matches_plain_step():
     assert got["nseg"] == 6
     ref = (net.store.flat - w0).cpu()
     assert torch.equal(got["delta"], ref), float((got["delta"] - ref).abs().max())
+
+
+def _train_api_worker(rank, world, port, out):
+    """cvlite.train_fcos.train (the reference's loop API, FCOS/train_fcos.py:87-251) with world=2:
+    each rank trains its shard of the same global sample; the ranks must end bit-identical."""
+    sys.path[:0] = [ROOT, PKG]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    import numpy as np
+    import torch.distributed as tdist
+    from cvlite import dist
+    from cvlite.fcos_net import FCOSNet
+    from cvlite.train_fcos import SGD, synthetic_batch, train
+    torch.cuda.set_device(0)
+    dist.init_from_env(backend="gloo")
+    D2 = 128
+    imgs, boxes, nbox = synthetic_batch(8, D2, D2, C, seed=3, device="cpu")
+    data = [dict(image=imgs[i].numpy(), bbox=boxes[i, :int(nbox[i]), :4].numpy(),
+                 label=boxes[i, :int(nbox[i]), 4].numpy()) for i in range(8)]
+    net = FCOSNet(C, device=torch.device("cuda", 0), seed=0)
+    w0 = net.store.flat.clone()
+    np.random.seed(123)                      # the same global sample on every rank
+    with tempfile.TemporaryDirectory() as td:
+        train(data, [], net, 2, SGD(5e-4, 0.9), None, None, 0, 3, display_step=1, step_save=100,
+              step_cool=1000, weight_decay=0.0, save_loss_file=os.path.join(td, "l.csv"), world=world)
+    torch.cuda.synchronize()
+    w = net.store.flat.cpu()
+    other = w.clone()
+    tdist.broadcast(other, src=0)
+    if rank == 1:
+        torch.save({"equal": bool(torch.equal(w, other)), "moved": float((w - w0.cpu()).norm()),
+                    "finite": bool(torch.isfinite(w).all())}, out)
+    tdist.barrier()
+    tdist.destroy_process_group()
+
+
+def test_train_api_data_parallel_world2():
+    world = 2
+    with tempfile.TemporaryDirectory() as td:
+        out = os.path.join(td, "train.pt")
+        mp.start_processes(_train_api_worker, args=(world, _port(), out), nprocs=world, join=True,
+                           start_method="spawn")
+        got = torch.load(out, weights_only=True)
+    assert got["equal"] and got["finite"] and got["moved"] > 0

@@ -117,3 +117,16 @@ def test_parse_image_decodes_files(tmp_path):
     Image.fromarray(sm).save(tmp_path / "x.jpg", quality=95)
     j = _parse_image(str(tmp_path / "x.jpg"))
     assert j.shape == (37, 53, 3) and j.dtype == np.uint8 and np.abs(j.astype(int) - sm).mean() < 3
+
+
+def test_fcos_center_resnet101_branch():
+    """fcos_center.py:37-43 / fcos_center_v1.py:37-43 build ResNet-101 for "resnet101"; fcos.py:
+    29-41 has no such branch (every non-resnet50 name is MobileNetV2)."""
+    from cvlite.fcos_center_net import FCOSCenterNet
+    from cvlite.fcos_net import FCOSNet
+    p = FCOSCenterNet.param_dict(20, backbone_model="resnet101")
+    assert "conv4_block23_3_conv/kernel" in p and "conv4_block24_1_conv/kernel" not in p
+    assert "cen_output_1/kernel" in p
+    assert "Conv1/kernel" in FCOSNet.param_dict(20, backbone_model="resnet101")
+    assert "conv4_block6_3_conv/kernel" in FCOSCenterNet.param_dict(20, backbone_model="resnet50")
+    assert "Conv1/kernel" in FCOSCenterNet.param_dict(20, backbone_model="mobilenetv2")
