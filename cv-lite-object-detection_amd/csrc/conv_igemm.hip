@@ -562,7 +562,10 @@ extern "C" const char* cvl_conv_kernel_name(int code) {
   }
 }
 
+int cvl_conv_f32(const cvl_conv_desc* d, const void* src, void* dst, double* bn_stats, hipStream_t s);
+
 extern "C" size_t cvl_conv_igemm_workspace_size(const cvl_conv_desc* d) {
+  if (d && d->prec == CVL_PREC_F32) return 16;
   cvl_conv_desc dd;
   int up = 1, upw = 0;
   if (s2dgrad_transform(d, &dd, &up, &upw)) d = &dd;
@@ -576,6 +579,9 @@ extern "C" int cvl_conv_igemm(const cvl_conv_desc* d, const void* src, void* dst
                               void* workspace, size_t workspace_bytes, cvl_stream_t stream) {
   hipStream_t s = (hipStream_t)stream;
   g_cvl_conv_last_kernel = CVL_CK_NONE;
+  CVL_CHECK_ARG(d);
+  if (d->prec == CVL_PREC_F32) return cvl_conv_f32(d, src, dst, bn_stats, s);    // parity mode
+  CVL_CHECK_ARG(d->prec == CVL_PREC_BF16);
   cvl_conv_desc dd;
   int up = 1, upw = 0;
   if (s2dgrad_transform(d, &dd, &up, &upw)) {
@@ -638,7 +644,8 @@ extern "C" int cvl_conv_igemm_dgrad_bnsum(const cvl_conv_desc* d, const void* sr
                                           cvl_stream_t stream) {
   CVL_CHECK_ARG(d && fused && z && mean_rstd && gamma && beta && sums);
   *fused = 0;
-  if (!cvl_env_flag("CVL_NO_BNSUM_FUSE") && d->mode == CVL_CONV_DGRAD && !d->dst_f32 && d->beta == 0.f &&
+  if (!cvl_env_flag("CVL_NO_BNSUM_FUSE") && d->prec == CVL_PREC_BF16 && d->mode == CVL_CONV_DGRAD &&
+      !d->dst_f32 && d->beta == 0.f &&
       d->Cin % 32 == 0 && d->Npad % 32 == 0 && d->ld_dst % 8 == 0 && d->dst_coff % 8 == 0 && d->n_store % 8 == 0 &&
       src && dst) {
     cvl_conv_desc dd;

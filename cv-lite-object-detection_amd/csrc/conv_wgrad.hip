@@ -389,8 +389,13 @@ int check_wgrad_desc(const cvl_conv_desc* d, int ngroups, const void* x, const v
 
 }  // namespace
 
+size_t cvl_conv_wgrad_f32_workspace(const cvl_conv_desc* d, int ngroups);
+int cvl_conv_wgrad_f32(const cvl_conv_desc* d, int ngroups, const void* x, const void* dy, float* const* dw,
+                       float beta, void* workspace, size_t workspace_bytes, hipStream_t s);
+
 extern "C" size_t cvl_conv_wgrad_grouped_workspace_size(const cvl_conv_desc* d, int ngroups) {
   if (!d || ngroups < 1 || d->nseg % ngroups) return 0;
+  if (d->prec == CVL_PREC_F32) return cvl_conv_wgrad_f32_workspace(d, ngroups);
   const long wsn = cvl_conv_wgrad_sn_workspace(d, ngroups);
   if (wsn >= 0) return (size_t)(wsn > 16 ? wsn : 16);
   const long wx = cvl_conv_wgrad_x_workspace(d, ngroups);
@@ -411,7 +416,10 @@ extern "C" size_t cvl_conv_wgrad_workspace_size(const cvl_conv_desc* d) {
 extern "C" int cvl_conv_wgrad_grouped(const cvl_conv_desc* d, int ngroups, const void* x, const void* dy,
                                       float* const* dw, float beta, void* workspace, size_t workspace_bytes,
                                       cvl_stream_t stream) {
-  CVL_CHECK_ARG(dw);
+  CVL_CHECK_ARG(dw && d);
+  if (d->prec == CVL_PREC_F32)                       // parity mode (parity_f32.hip)
+    return cvl_conv_wgrad_f32(d, ngroups, x, dy, dw, beta, workspace, workspace_bytes, (hipStream_t)stream);
+  CVL_CHECK_ARG(d->prec == CVL_PREC_BF16);
   int st = check_wgrad_desc(d, ngroups, x, dy, dw);
   if (st) return st;
   hipStream_t s = (hipStream_t)stream;

@@ -818,6 +818,7 @@ struct RetinaLossArgs {
   int ld_reg, ld_cls, ld_dreg, ld_dcls, P, A, C, tiles;
   int off[6];          // per-image cell offsets of the 5 levels (+ P)
   float grad_scale;
+  int grad_f32;        // 1: d_reg / d_cls are fp32 (the parity mode), 0: bf16
 };
 
 // A workgroup owns RL_ROWS consecutive target rows of one image (a contiguous [rows][4+C] slab):
@@ -871,11 +872,19 @@ __global__ void __launch_bounds__(NT) retina_loss_kernel(RetinaLossArgs a) {
     if (ch < 4) {
       const float m = mask_s[row];
       s_reg += m * sl1_elem(y, a.reg[prow * a.ld_reg + an * 4 + ch], &g);
-      if (a.dreg) a.dreg[prow * a.ld_dreg + an * 4 + ch] = f32_to_bf16(m * g * gs);
+      if (a.dreg) {
+        const long o = prow * a.ld_dreg + an * 4 + ch;
+        if (a.grad_f32) reinterpret_cast<float*>(a.dreg)[o] = m * g * gs;
+        else a.dreg[o] = f32_to_bf16(m * g * gs);
+      }
     } else {
       const int c = ch - 4;
       s_cls += focal_elem(y, a.cls[prow * a.ld_cls + (long)an * a.C + c], &g);
-      if (a.dcls) a.dcls[prow * a.ld_dcls + (long)an * a.C + c] = f32_to_bf16(g * gs);
+      if (a.dcls) {
+        const long o = prow * a.ld_dcls + (long)an * a.C + c;
+        if (a.grad_f32) reinterpret_cast<float*>(a.dcls)[o] = g * gs;
+        else a.dcls[o] = f32_to_bf16(g * gs);
+      }
     }
   }
   __shared__ double red[2][NT / 64];
@@ -1166,11 +1175,11 @@ extern "C" size_t cvl_retina_loss_workspace_size(int B, int P, int n_anchors) {
   return (size_t)B * (((size_t)P * n_anchors + RL_ROWS - 1) / RL_ROWS) * 2 * sizeof(double);
 }
 
-extern "C" int cvl_retina_loss(const float* reg_pred, int ld_reg, const float* cls_pred, int ld_cls,
-                               const float* targets, int B, const int32_t* level_cells, int n_anchors,
-                               int num_classes, const float* img_weight, float grad_scale, float* losses,
-                               void* d_reg, int ld_dreg, void* d_cls, int ld_dcls, void* workspace,
-                               cvl_stream_t stream) {
+static int retina_loss_impl(const float* reg_pred, int ld_reg, const float* cls_pred, int ld_cls,
+                            const float* targets, int B, const int32_t* level_cells, int n_anchors,
+                            int num_classes, const float* img_weight, float grad_scale, float* losses,
+                            void* d_reg, int ld_dreg, void* d_cls, int ld_dcls, void* workspace,
+                            cvl_stream_t stream, int grad_f32) {
   CVL_CHECK_ARG(reg_pred && cls_pred && targets && losses && workspace && level_cells && B > 0);
   CVL_CHECK_ARG(n_anchors > 0 && num_classes > 0 && ld_reg >= 4 * n_anchors && ld_cls >= n_anchors * num_classes);
   CVL_CHECK_ARG(!d_reg || ld_dreg >= 4 * n_anchors);
@@ -1181,6 +1190,7 @@ extern "C" int cvl_retina_loss(const float* reg_pred, int ld_reg, const float* c
   a.dreg = (cvl_bf16*)d_reg; a.dcls = (cvl_bf16*)d_cls;
   a.ld_reg = ld_reg; a.ld_cls = ld_cls; a.ld_dreg = ld_dreg; a.ld_dcls = ld_dcls;
   a.A = n_anchors; a.C = num_classes; a.grad_scale = grad_scale;
+  a.grad_f32 = grad_f32;
   int o = 0;
   for (int l = 0; l < 5; ++l) {
     CVL_CHECK_ARG(level_cells[l] > 0);
@@ -1194,6 +1204,24 @@ extern "C" int cvl_retina_loss(const float* reg_pred, int ld_reg, const float* c
   hipLaunchKernelGGL(retina_loss_kernel, dim3(a.tiles, B), dim3(NT), 0, S_, a);
   hipLaunchKernelGGL(det_loss_finalize, dim3(B), dim3(FIN_T), 0, S_, (const double*)workspace, losses, a.tiles);
   return cvl_launch_status();
+}
+
+extern "C" int cvl_retina_loss(const float* reg_pred, int ld_reg, const float* cls_pred, int ld_cls,
+                               const float* targets, int B, const int32_t* level_cells, int n_anchors,
+                               int num_classes, const float* img_weight, float grad_scale, float* losses,
+                               void* d_reg, int ld_dreg, void* d_cls, int ld_dcls, void* workspace,
+                               cvl_stream_t stream) {
+  return retina_loss_impl(reg_pred, ld_reg, cls_pred, ld_cls, targets, B, level_cells, n_anchors, num_classes,
+                          img_weight, grad_scale, losses, d_reg, ld_dreg, d_cls, ld_dcls, workspace, stream, 0);
+}
+
+extern "C" int cvl_retina_loss_f32(const float* reg_pred, int ld_reg, const float* cls_pred, int ld_cls,
+                                   const float* targets, int B, const int32_t* level_cells, int n_anchors,
+                                   int num_classes, const float* img_weight, float grad_scale, float* losses,
+                                   float* d_reg, int ld_dreg, float* d_cls, int ld_dcls, void* workspace,
+                                   cvl_stream_t stream) {
+  return retina_loss_impl(reg_pred, ld_reg, cls_pred, ld_cls, targets, B, level_cells, n_anchors, num_classes,
+                          img_weight, grad_scale, losses, d_reg, ld_dreg, d_cls, ld_dcls, workspace, stream, 1);
 }
 
 extern "C" size_t cvl_nms_workspace_size(int n, int ncls) { return (size_t)n * ncls + 16; }

@@ -76,6 +76,23 @@ __global__ void __launch_bounds__(NT) pack_multi_kernel(const cvl_pack_item* __r
     tile[r][col] = (ci < it.Cin && co < it.Cout) ? src[(long)ci * it.Cout + co] : 0.f;
   }
   __syncthreads();
+  if (it.f32_out) {        // fp32 parity-mode images, element by element (any Cin_k / Cout_pad)
+    for (int idx = threadIdx.x; idx < 64 * 64; idx += NT) {
+      const int r = idx >> 6, c = idx & 63;
+      if (it.w_fwd) {       // [co0 + r][tap * Cin_k + ci0 + c]
+        const int co = co0 + r, ci = ci0 + c;
+        if (co < it.Npad && ci < it.Cin_k)
+          reinterpret_cast<float*>(it.w_fwd)[(long)co * it.KHW * it.Cin_k + (long)tap * it.Cin_k + ci] = tile[c][r];
+      }
+      if (it.w_dgrad) {     // [ci0 + r][tap * Cout_pad + co0 + c]
+        const int ci = ci0 + r, co = co0 + c;
+        if (ci < it.Cin_pad && co < it.Cout_pad)
+          reinterpret_cast<float*>(it.w_dgrad)[(long)ci * it.KHW * it.Cout_pad + (long)tap * it.Cout_pad + co] =
+              tile[r][c];
+      }
+    }
+    return;
+  }
 #pragma unroll
   for (int j = 0; j < 2; ++j) {
     const int idx = threadIdx.x + j * NT;

@@ -130,6 +130,22 @@ SIGNATURES = {
     "cvl_fcos_detect_workspace_size": (c_size_t, [c_int, c_int, c_int, c_int]),
     "cvl_fcos_detect": (c_int, [P, c_int, P, c_int, c_int, P, P, c_int, c_int, c_float, c_float, c_int, c_int, P, P,
                                 P, P, P, c_size_t, P]),
+    # fp32 parity mode (include/cvlite.h "fp32 parity mode")
+    "cvl_bn_apply_f32": (c_int, [P, P, P, P, P, P, c_int, c_int, c_int, c_int, P]),
+    "cvl_bn_finalize_apply_f32": (c_int, [P, P, P, P, P, P, P, P, P, c_int, c_int, c_int, c_int, c_float, c_float,
+                                          P]),
+    "cvl_bn_backward_f32_workspace_size": (c_size_t, [c_int, c_int]),
+    "cvl_bn_backward_f32": (c_int, [P, P, P, P, P, P, P, c_size_t, P, P, P, P, c_float, P, c_float, c_int, c_int,
+                                    c_int, P]),
+    "cvl_maxpool3x3s2_f32": (c_int, [P, P, P, c_int, c_int, c_int, c_int, P]),
+    "cvl_maxpool3x3s2_backward_f32": (c_int, [P, P, P, c_int, c_int, c_int, c_int, P]),
+    "cvl_upsample2x_add_f32": (c_int, [P, P, P, c_int, c_int, c_int, c_int, P]),
+    "cvl_upsample2x_backward_f32": (c_int, [P, P, c_int, c_int, c_int, c_int, c_float, P]),
+    "cvl_relu_backward_f32": (c_int, [P, P, P, ctypes.c_long, c_float, P]),
+    "cvl_add_f32": (c_int, [P, P, P, ctypes.c_long, P]),
+    "cvl_bias_grad_multi_f32": (c_int, [P, c_int, P]),
+    "cvl_retina_loss_f32": (c_int, [P, c_int, P, c_int, P, c_int, P, c_int, c_int, P, c_float, P, P, c_int, P, c_int,
+                                    P, P]),
 }
 
 

@@ -38,7 +38,8 @@ class FCOSCenterNet(FCOSNet):
 
     def __init__(self, num_classes, backbone_model="resnet50", device="cuda", seed=0, v1=False):
         self.v1 = v1
-        self._init_common(num_classes, backbone_model, device, seed)
+        # the combined class + centerness data-gradient kernels are packed bf16: production precision
+        self._init_common(num_classes, backbone_model, device, seed, precision="bf16")
         self.cen_col, self.cls_ld = self._comb_cc, self._comb_ld
         self.reg_ld = 8
 

@@ -15,8 +15,9 @@ from .layers import Conv
 
 
 class FCOSNet(FPNDetector):
-    def __init__(self, num_classes, backbone_model="resnet50", device="cuda", seed=0):
-        self._init_common(num_classes, backbone_model, device, seed)
+    def __init__(self, num_classes, backbone_model="resnet50", device="cuda", seed=0, precision=None):
+        """precision: "bf16" (production) / "fp32" (parity mode); None = CVL_PRECISION or bf16."""
+        self._init_common(num_classes, backbone_model, device, seed, precision)
         self.cls_ld = self.cls_heads[0].npad          # >= C, multiple of 32
         self.reg_ld = 8
 

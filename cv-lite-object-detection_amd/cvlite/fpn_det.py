@@ -16,7 +16,7 @@ import os
 import torch
 
 from . import ops_nn as nn
-from .layers import BF16, Conv, ParamStore
+from .layers import BF16, Conv, ParamStore, act_dtype
 from .mobilenet_v2 import MobileNetV2
 from .resnet import ResNet50
 
@@ -45,10 +45,13 @@ class FPNDetector(object):
         (fcos_center*.py add a ResNet101 branch: FCOSCenterNet.backbone_kind)."""
         return "resnet50" if name.lower() == "resnet50" else "mobilenetv2"
 
-    def _init_common(self, num_classes, backbone_model, device, seed):
+    def _init_common(self, num_classes, backbone_model, device, seed, precision=None):
         self.backbone_model = self.backbone_kind(backbone_model)
         self.C = num_classes
         self.store = st = ParamStore()
+        st.act = act_dtype(precision)      # bf16 (production) or fp32 (parity mode)
+        if st.act != BF16 and self.backbone_model != "resnet50" and self.backbone_model != "resnet101":
+            raise NotImplementedError("the fp32 parity mode covers the ResNet backbones")
         self._build_layers(st, num_classes)
         st.finalize(device, seed)
         for bn in self.backbone.bns():
@@ -146,7 +149,7 @@ class FPNDetector(object):
         # the three 3x3 output convs' sources (P3r, P4r, P5 = l5) share one buffer, so the convs run
         # as ONE 3-segment launch (fcos.py:62-66: same geometry, own weights and biases)
         n3, n4, n5 = B * H3 * W3, B * H4 * W4, B * H5 * W5
-        PR = torch.empty((n3 + n4 + n5, FPN_C), dtype=BF16, device=dev)
+        PR = torch.empty((n3 + n4 + n5, FPN_C), dtype=self.store.act, device=dev)
         p3r = PR[:n3].view(B, H3, W3, FPN_C)
         p4r = PR[n3:n3 + n4].view(B, H4, W4, FPN_C)
         l3, _, _ = self.c3_1x1.fwd(c3, B, H3, W3)
@@ -155,7 +158,7 @@ class FPNDetector(object):
         nn.upsample2x_add(l4, l5, p4r, B, H4, W4, FPN_C)          # fcos.py:57-58
         nn.upsample2x_add(l3, l4, p3r, B, H3, W3, FPN_C)          # fcos.py:59-60 (up2 of P4_1x1, Q13)
         shapes, off, P = self.layout(B, H, W)
-        F = torch.empty((B * P, FPN_C), dtype=BF16, device=dev)
+        F = torch.empty((B * P, FPN_C), dtype=self.store.act, device=dev)
         pr_base = (0, n3, n3 + n4)
         if FUSE_FPN:
             segs = [nn.seg(shapes[l][0], shapes[l][1], h, w, conv.wf, conv.bias_arg(), src_base=pr_base[l],
@@ -187,7 +190,7 @@ class FPNDetector(object):
         bufs = []
         src = F
         for i in range(4):
-            out = torch.empty((2 * B * P, FPN_C), dtype=BF16, device=dev)
+            out = torch.empty((2 * B * P, FPN_C), dtype=self.store.act, device=dev)
             if PAIR_TOWERS:
                 d = self.cls_tower[i].fwd_desc(B, self._pair_segs(i, B, shapes, off, P, fwd=True), ld_dst=FPN_C,
                                                relu_out=(i == 3))
@@ -272,7 +275,7 @@ class FPNDetector(object):
                     nn.conv_wgrad(d, towers[t][i], dAs[t], conv.dw)
             if paired and (i > 0 or pair0):
                 dd = self.cls_tower[i].dgrad_desc(B, self._pair_segs(i, B, shapes, off, P, fwd=False), ld_dst=FPN_C)
-                dst = torch.empty((2 * BP, FPN_C), dtype=BF16, device=dev)
+                dst = torch.empty((2 * BP, FPN_C), dtype=self.store.act, device=dev)
                 src_all = torch.as_strided(dAs[0], (2 * BP, FPN_C), (FPN_C, 1))
                 nn.conv_igemm(dd, src_all, dst)
                 if i == 0:          # both towers read F: dF = the two halves' sum (one 682-tile launch)
@@ -304,7 +307,7 @@ class FPNDetector(object):
         nn.conv_wgrad(d, F, dF, self.c7_3x3.dw)
         # bias gradients of the eight FPN convs: collected, then one batched launch pair
         bias_items = [(dF, FPN_C, 0, FPN_C, B * off[4], h7 * w7, h7 * w7, B, self.c7_3x3.db, 0.0)]
-        dr6 = torch.empty((B, h6, w6, FPN_C), dtype=BF16, device=dev)
+        dr6 = torch.empty((B, h6, w6, FPN_C), dtype=self.store.act, device=dev)
         dd = self.c7_3x3.dgrad_desc(B, [nn.seg(h6, w6, h7, w7, self.c7_3x3.wd, None, src_base=B * off[4])],
                                     ld_dst=FPN_C)
         nn.conv_igemm(dd, dF, dr6)

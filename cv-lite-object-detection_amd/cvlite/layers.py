@@ -16,6 +16,18 @@ import torch
 from . import ops_nn as nn
 
 BF16 = torch.bfloat16
+F32 = torch.float32
+
+
+def act_dtype(precision=None):
+    """Activation / activation-gradient storage type of a network: "bf16" (production: bf16
+    storage, bf16 MFMA convs, fp32 accumulation and master weights) or "fp32" (the parity mode of
+    SURVEY.md §8b: fp32 everywhere, for whole-graph parity with the reference's fp32 Keras graph).
+    None reads CVL_PRECISION (default bf16)."""
+    p = (precision or os.environ.get("CVL_PRECISION", "bf16")).lower()
+    if p not in ("bf16", "fp32"):
+        raise ValueError("precision must be 'bf16' or 'fp32'")
+    return F32 if p == "fp32" else BF16
 
 
 def glorot_uniform(fan_in, fan_out):
@@ -46,6 +58,7 @@ class ParamStore(object):
         self.specs = []      # (name, shape, init)
         self.index = {}
         self.finalized = False
+        self.act = BF16      # activation storage type of the network (act_dtype)
 
     def add(self, name, shape, init):
         assert not self.finalized and name not in self.index
@@ -149,10 +162,10 @@ class Conv(object):
     def alloc_packed(self):
         dev = self.store.flat.device
         K = self.k * self.k * self.cin_k
-        if self.wf is None:
-            self.wf = torch.empty((self.npad, K), dtype=BF16, device=dev)
+        if self.wf is None:      # packed operand copies in the activation type (fp32 in parity mode)
+            self.wf = torch.empty((self.npad, K), dtype=self.store.act, device=dev)
             if self.need_dgrad:
-                self.wd = torch.empty((self.cin_pad, self.k * self.k * self.cout_pad), dtype=BF16, device=dev)
+                self.wd = torch.empty((self.cin_pad, self.k * self.k * self.cout_pad), dtype=self.store.act, device=dev)
 
     def pack_entry(self):
         """Row of an ops_nn.PackPlan (the batched re-pack of every conv)."""
@@ -188,7 +201,7 @@ class Conv(object):
     def fwd(self, x, B, H, W, out=None, stats=None, relu_out=False, relu_in=False):
         Ho, Wo, _, _ = self.out_hw(H, W)
         if out is None:
-            out = torch.empty((B, Ho, Wo, self.cout), dtype=BF16, device=x.device)
+            out = torch.empty((B, Ho, Wo, self.cout), dtype=x.dtype, device=x.device)
         d = self.fwd_desc(B, [nn.seg(Ho, Wo, H, W, self.wf, self.bias_arg())], ld_dst=self.cout,
                           relu_out=relu_out, relu_in=relu_in)
         nn.conv_igemm(d, x, out, stats)
@@ -211,7 +224,7 @@ class Conv(object):
         epilogue (sums None when the launch could not fuse)."""
         Ho, Wo, _, _ = self.out_hw(H, W)
         if out is None:
-            out = torch.empty((B, H, W, self.cin), dtype=BF16, device=dy.device)
+            out = torch.empty((B, H, W, self.cin), dtype=dy.dtype, device=dy.device)
         d = self.dgrad_desc(B, [nn.seg(H, W, Ho, Wo, self.wd)], ld_dst=self.cin, beta=beta)
         if bn_next is None:
             nn.conv_igemm(d, dy, out)
@@ -337,7 +350,7 @@ class ConvBN(object):
         data-gradient epilogue (conv_igemm_dgrad_bnsum); None unless BN -> ReLU without residual.
         The sums buffer comes zeroed from the step's StatsArena when one is given."""
         x, z, y, mr, B, H, W, Ho, Wo, relu, has_res = saved
-        if not relu or has_res or not FUSE_BNSUM:
+        if not relu or has_res or not FUSE_BNSUM or z.dtype != BF16:      # (fp32 parity mode: two passes)
             return None
         return (z, mr, self.bn.gamma, self.bn.beta, arena.take(B, self.bn.c) if arena is not None else None)
 

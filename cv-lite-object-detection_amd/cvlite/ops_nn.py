@@ -1,5 +1,9 @@
 """Device ops of the conv/BN/FPN training graph: thin torch-tensor wrappers over the C ABI
-(include/cvlite.h).  Tensors are raw storage (bf16 activations NHWC, fp32 params); no autograd."""
+(include/cvlite.h).  Tensors are raw storage (bf16 activations NHWC, fp32 params); no autograd.
+
+fp32 parity mode (CVL_PRECISION=fp32, layers.act_dtype): the same wrappers take fp32 activations
+and dispatch on the tensor dtype -- convolutions through cvl_conv_desc.prec = CVL_PREC_F32, the
+memory-bound ops through their *_f32 entry points."""
 import ctypes
 
 import torch
@@ -24,7 +28,20 @@ class ConvDesc(ctypes.Structure):
                 ("stride", c_int), ("pad_t", c_int), ("pad_l", c_int), ("Npad", c_int),
                 ("n_store", c_int), ("ld_dst", c_int), ("dst_coff", c_int), ("dst_f32", c_int),
                 ("relu_out", c_int), ("relu_in", c_int), ("beta", c_float), ("nseg", c_int),
-                ("seg", ConvSeg * MAX_SEG)]
+                ("seg", ConvSeg * MAX_SEG), ("prec", c_int)]
+
+
+PREC_BF16, PREC_F32 = 0, 1      # cvl_conv_desc.prec
+
+
+def _is_f32(t):
+    return t is not None and t.dtype == torch.float32
+
+
+def _prec(desc, src):
+    """The descriptor's operand precision follows its source tensor (bf16: production MFMA path;
+    fp32: the parity mode, whose weights are packed fp32)."""
+    desc.prec = PREC_F32 if _is_f32(src) else PREC_BF16
 
 
 def seg(Hr, Wr, Hs, Ws, w, bias=None, src_base=0, src_img=None, dst_base=0, dst_img=None):
@@ -54,6 +71,7 @@ def make_desc(mode, B, Cin, KH, KW, stride, pad_t, pad_l, Npad, n_store, ld_dst,
 
 
 def conv_igemm(desc, src, dst, stats=None):
+    _prec(desc, src)
     n = int(_lib.load().cvl_conv_igemm_workspace_size(ctypes.byref(desc)))
     ws = torch.empty(n, dtype=torch.uint8, device=src.device) if n > 16 else None
     _lib.call("cvl_conv_igemm", ctypes.byref(desc), ptr(src), ptr(dst), ptr(stats), ptr(ws),
@@ -77,6 +95,7 @@ def probe_seconds(slot):
 
 
 def conv_wgrad(desc, x, dy, dw, beta=0.0):
+    _prec(desc, x)
     lib = _lib.load()
     n = int(lib.cvl_conv_wgrad_workspace_size(ctypes.byref(desc)))
     ws = torch.empty(max(n, 16), dtype=torch.uint8, device=x.device)
@@ -87,6 +106,7 @@ def conv_wgrad(desc, x, dy, dw, beta=0.0):
 def conv_wgrad_grouped(desc, x, dy, dws, beta=0.0):
     """Weight gradients of `len(dws)` segment groups in one launch (cvl_conv_wgrad_grouped): the
     descriptor's segments split into equal consecutive groups, group g summed into dws[g]."""
+    _prec(desc, x)
     lib = _lib.load()
     n = int(lib.cvl_conv_wgrad_grouped_workspace_size(ctypes.byref(desc), len(dws)))
     ws = torch.empty(max(n, 16), dtype=torch.uint8, device=x.device)
@@ -103,7 +123,7 @@ def pack_conv_weights(w_hwio, KH, KW, Cin, Cout, Cin_k, Npad, w_fwd, Cin_pad=0, 
 class PackItem(ctypes.Structure):
     _fields_ = [("w", c_void_p), ("w_fwd", c_void_p), ("w_dgrad", c_void_p), ("KHW", c_int), ("Cin", c_int),
                 ("Cout", c_int), ("Cin_k", c_int), ("Npad", c_int), ("Cin_pad", c_int), ("Cout_pad", c_int),
-                ("pad_", c_int)]
+                ("f32_out", c_int)]
 
 
 class PackPlan(object):
@@ -121,6 +141,7 @@ class PackPlan(object):
             it.w_dgrad = wd.data_ptr() if wd is not None else None
             it.KHW, it.Cin, it.Cout, it.Cin_k, it.Npad = khw, cin, cout, cin_k, npad
             it.Cin_pad, it.Cout_pad = (cin_pad, cout_pad) if wd is not None else (0, 0)
+            it.f32_out = int(_is_f32(wf if wf is not None else wd))       # parity-mode fp32 packs
             self._keep.append((w, wf, wd))
             ci_hi = max(cin_k, it.Cin_pad)
             co_hi = max(npad, it.Cout_pad)
@@ -148,22 +169,35 @@ def bn_finalize(stats, mean_rstd, run_mean, run_var, B, C, HW, eps, momentum):
 
 
 def bn_apply(z, mean_rstd, gamma, beta, residual, y, B, HW, C, relu):
-    _lib.call("cvl_bn_apply", ptr(z), ptr(mean_rstd), ptr(gamma), ptr(beta), ptr(residual), ptr(y),
+    _lib.call("cvl_bn_apply_f32" if _is_f32(z) else "cvl_bn_apply", ptr(z), ptr(mean_rstd), ptr(gamma), ptr(beta), ptr(residual), ptr(y),
               B, HW, C, int(relu), stream())          # relu: 0 none, 1 ReLU, 2 ReLU6
 
 
 def bn_finalize_apply(stats, mean_rstd, run_mean, run_var, z, gamma, beta, residual, y, B, HW, C, relu, eps,
                       momentum):
-    _lib.call("cvl_bn_finalize_apply", ptr(stats), ptr(mean_rstd), ptr(run_mean), ptr(run_var), ptr(z), ptr(gamma),
+    _lib.call("cvl_bn_finalize_apply_f32" if _is_f32(z) else "cvl_bn_finalize_apply", ptr(stats), ptr(mean_rstd), ptr(run_mean), ptr(run_var), ptr(z), ptr(gamma),
               ptr(beta), ptr(residual), ptr(y), B, HW, C, int(relu), float(eps), float(momentum), stream())
 
 
 def bn_backward(dy, y_relu, z, mean_rstd, gamma, dz, g_out, dgamma, dbeta, B, HW, C, beta_acc=0.0,
                 conv_dbias=None):
+    if _is_f32(dy):
+        return bn_backward_f32(dy, y_relu, z, mean_rstd, gamma, None, dz, g_out, dgamma, dbeta, B, HW, C, beta_acc,
+                               conv_dbias)
     n = int(_lib.load().cvl_bn_backward_workspace_size(B, HW, C))
     ws = torch.empty(n, dtype=torch.uint8, device=dy.device)
     _lib.call("cvl_bn_backward", ptr(dy), ptr(y_relu), ptr(z), ptr(mean_rstd), ptr(gamma), ptr(ws), n,
               ptr(dz), ptr(g_out), ptr(dgamma), ptr(dbeta), float(beta_acc), ptr(conv_dbias), B, HW, C,
+              stream())
+
+
+def bn_backward_f32(dy, y_relu, z, mean_rstd, gamma, bn_beta, dz, g_out, dgamma, dbeta, B, HW, C, beta_acc=0.0,
+                    conv_dbias=None, act_hi=float("inf")):
+    """fp32 parity form of bn_backward (y_relu given) / bn_backward_relu (bn_beta given)."""
+    n = int(_lib.load().cvl_bn_backward_f32_workspace_size(B, C))
+    ws = torch.empty(n, dtype=torch.uint8, device=dy.device)
+    _lib.call("cvl_bn_backward_f32", ptr(dy), ptr(y_relu), ptr(z), ptr(mean_rstd), ptr(gamma), ptr(bn_beta), ptr(ws), n,
+              ptr(dz), ptr(g_out), ptr(dgamma), ptr(dbeta), float(beta_acc), ptr(conv_dbias), float(act_hi), B, HW, C,
               stream())
 
 
@@ -209,6 +243,7 @@ def conv_igemm_dgrad_bnsum(desc, src, dst, z, mean_rstd, gamma, beta, sums, act_
     [B][C][2] float64 (zeroed here first unless zero=False: the caller's buffer is already zero).
     Returns True when fused; False = the plain data gradient ran and `sums` is untouched (run the
     two-pass BN backward)."""
+    _prec(desc, src)
     n = int(_lib.load().cvl_conv_igemm_workspace_size(ctypes.byref(desc)))
     ws = torch.empty(n, dtype=torch.uint8, device=src.device) if n > 16 else None
     if zero:
@@ -229,6 +264,9 @@ def bn_backward_relu_sums(dy, z, mean_rstd, gamma, beta, sums, dz, dgamma, dbeta
 
 def bn_backward_relu(dy, z, mean_rstd, gamma, beta, dz, dgamma, dbeta, B, HW, C, beta_acc=0.0, conv_dbias=None):
     """bn_backward of a BN -> ReLU unit without a residual add: the mask is rebuilt from z."""
+    if _is_f32(dy):
+        return bn_backward_f32(dy, None, z, mean_rstd, gamma, beta, dz, None, dgamma, dbeta, B, HW, C, beta_acc,
+                               conv_dbias)
     n = int(_lib.load().cvl_bn_backward_workspace_size(B, HW, C))
     ws = torch.empty(n, dtype=torch.uint8, device=dy.device)
     _lib.call("cvl_bn_backward_relu", ptr(dy), ptr(z), ptr(mean_rstd), ptr(gamma), ptr(beta), ptr(ws), n, ptr(dz),
@@ -237,31 +275,33 @@ def bn_backward_relu(dy, z, mean_rstd, gamma, beta, dz, dgamma, dbeta, B, HW, C,
 
 def maxpool3x3s2(x, y, argmax):
     B, H, W, C = x.shape
-    _lib.call("cvl_maxpool3x3s2", ptr(x), ptr(y), ptr(argmax), B, H, W, C, stream())
+    _lib.call("cvl_maxpool3x3s2_f32" if _is_f32(x) else "cvl_maxpool3x3s2", ptr(x), ptr(y), ptr(argmax), B, H, W, C, stream())
 
 
 def maxpool3x3s2_backward(dy, argmax, dx):
     B, H, W, C = dx.shape
-    _lib.call("cvl_maxpool3x3s2_backward", ptr(dy), ptr(argmax), ptr(dx), B, H, W, C, stream())
+    _lib.call("cvl_maxpool3x3s2_backward_f32" if _is_f32(dy) else "cvl_maxpool3x3s2_backward", ptr(dy), ptr(argmax), ptr(dx), B, H, W, C, stream())
 
 
 def upsample2x_add(a, b, out, B, H, W, C):
-    _lib.call("cvl_upsample2x_add", ptr(a), ptr(b), ptr(out), B, H, W, C, stream())
+    _lib.call("cvl_upsample2x_add_f32" if _is_f32(a) else "cvl_upsample2x_add", ptr(a), ptr(b), ptr(out), B, H, W, C, stream())
 
 
 def upsample2x_backward(dout, db, B, H, W, C, beta=0.0):
-    _lib.call("cvl_upsample2x_backward", ptr(dout), ptr(db), B, H, W, C, float(beta), stream())
+    _lib.call("cvl_upsample2x_backward_f32" if _is_f32(dout) else "cvl_upsample2x_backward", ptr(dout), ptr(db), B, H, W, C, float(beta), stream())
 
 
 def relu_backward(dy, y, dx, beta=0.0):
-    _lib.call("cvl_relu_backward", ptr(dy), ptr(y), ptr(dx), dy.numel(), float(beta), stream())
+    _lib.call("cvl_relu_backward_f32" if _is_f32(dy) else "cvl_relu_backward", ptr(dy), ptr(y), ptr(dx), dy.numel(), float(beta), stream())
 
 
 def add(a, b, out):
-    _lib.call("cvl_add", ptr(a), ptr(b), ptr(out), a.numel(), stream())
+    _lib.call("cvl_add_f32" if _is_f32(a) else "cvl_add", ptr(a), ptr(b), ptr(out), a.numel(), stream())
 
 
 def bias_grad(dy, ld, coff, ncol, base, img_stride, HW, B, db, beta=0.0):
+    if _is_f32(dy):
+        return bias_grad_multi([(dy, ld, coff, ncol, base, img_stride, HW, B, db, beta)])
     n = int(_lib.load().cvl_bias_grad_workspace_size(ncol, HW, B))
     ws = torch.empty(max(n, 16), dtype=torch.uint8, device=dy.device)
     _lib.call("cvl_bias_grad", ptr(dy), ld, coff, ncol, int(base), int(img_stride), HW, B, ptr(ws), ws.numel(),
@@ -287,6 +327,10 @@ def bias_grad_multi(items):
             _lib.require_cuda(dy, db)
             arr[i] = BiasItem(dy.data_ptr(), db.data_ptr(), int(base), int(img_stride), int(ld), int(coff), int(ncol),
                               int(HW), int(B), float(beta))
+        if _is_f32(chunk[0][0]):
+            assert all(_is_f32(it[0]) for it in chunk)
+            _lib.call("cvl_bias_grad_multi_f32", arr, len(chunk), stream())
+            continue
         n = int(_lib.load().cvl_bias_grad_multi_workspace_size(arr, len(chunk)))
         if n == 0:
             raise _lib.CvlError("cvl_bias_grad_multi: invalid items")

@@ -168,7 +168,8 @@ def retina_loss(reg_pred, cls_pred, targets, level_cells, n_anchors, num_classes
                 grad_scale=1.0, d_reg=None, d_cls=None, losses=None):
     """RetinaNet.train_loss fwd+bwd (cvl_retina_loss).  reg_pred [B,P,ld>=4A] / cls_pred [B,P,ld>=AC] f32
     from the grouped heads, targets [B, A*P, 4+C] (cvl_retina_assign order).  d_reg / d_cls: bf16
-    buffers written at the prediction positions (None = no gradient).  Returns losses [B,2]."""
+    (fp32 in the parity mode) buffers written at the prediction positions (None = no gradient).
+    Returns losses [B,2]."""
     _lib.require_cuda(reg_pred, cls_pred, targets)
     B, P = int(reg_pred.shape[0]), int(reg_pred.shape[1])
     assert sum(level_cells) == P and int(targets.shape[1]) == n_anchors * P
@@ -177,9 +178,10 @@ def retina_loss(reg_pred, cls_pred, targets, level_cells, n_anchors, num_classes
         losses = torch.empty((B, 2), device=dev, dtype=torch.float32)
     ws = torch.empty(int(_lib.load().cvl_retina_loss_workspace_size(B, P, n_anchors)), device=dev, dtype=torch.uint8)
     lc = (_lib.ctypes.c_int32 * 5)(*[int(c) for c in level_cells])
+    f32 = any(t is not None and t.dtype == torch.float32 for t in (d_reg, d_cls))    # fp32 parity mode
     for t in (d_reg, d_cls):
-        assert t is None or t.dtype == torch.bfloat16
-    _lib.call("cvl_retina_loss", ptr(reg_pred), int(reg_pred.shape[-1]), ptr(cls_pred), int(cls_pred.shape[-1]),
+        assert t is None or t.dtype == (torch.float32 if f32 else torch.bfloat16)
+    _lib.call("cvl_retina_loss_f32" if f32 else "cvl_retina_loss", ptr(reg_pred), int(reg_pred.shape[-1]), ptr(cls_pred), int(cls_pred.shape[-1]),
               ptr(targets), B, _lib.ctypes.cast(lc, _lib.c_void_p), int(n_anchors), int(num_classes), ptr(img_weight),
               float(grad_scale), ptr(losses), ptr(d_reg), int(d_reg.shape[-1]) if d_reg is not None else 0,
               ptr(d_cls), int(d_cls.shape[-1]) if d_cls is not None else 0, ptr(ws), _lib.stream())

@@ -29,11 +29,21 @@ class Stem(object):
         self.bn = BatchNorm(store, "conv1_bn", 64)
 
     def pack_entry(self):
-        # HWIO [7][7][3][64] == [1][1][147][64]: pack as a 1x1 conv with 147 -> 160 channels
+        # HWIO [7][7][3][64] == [1][1][147][64]: pack as a 1x1 conv with 147 -> 192 channels (the
+        # im2col GEMM); fp32 parity mode: a direct 7x7/2 conv over the 3 image channels
         c = self.conv
+        if c.store.act != BF16:
+            if c.wf is None:
+                c.wf = torch.empty((64, 147), dtype=c.store.act, device=c.store.flat.device)
+            return (c.w, 49, 3, 64, 3, 64, c.wf, 0, 0, None)
         if c.wf is None:
             c.wf = torch.empty((64, STEM_KP), dtype=BF16, device=c.store.flat.device)
         return (c.w, 1, 147, 64, STEM_KP, 64, c.wf, 0, 0, None)
+
+    def _desc7(self, B, H, W, Ho, Wo):
+        """fp32 parity mode: conv1 as a direct 7x7/2 conv (ZeroPadding2D(3) = explicit pad 3)."""
+        return nn.make_desc(nn.FWD, B, 3, STEM_K, STEM_K, 2, 3, 3, 64, 64, 64,
+                            [nn.seg(Ho, Wo, H, W, self.conv.wf, self.conv.b)])
 
     def pack(self):
         c = self.conv
@@ -47,17 +57,22 @@ class Stem(object):
     def forward(self, x, train=True, arena=None):
         B, H, W, _ = x.shape
         Ho, Wo, pt, pl = self.conv.out_hw(H, W)
-        A = torch.empty((B * Ho * Wo, STEM_KP), dtype=BF16, device=x.device)
-        nn.im2col(x, STEM_K, STEM_K, 2, pt, pl, Ho, Wo, STEM_KP, A)
+        act = self.conv.store.act
         stats = None
         if train:
             stats = arena.take(B, 64) if arena is not None else torch.zeros((B, 64, 2), dtype=torch.float64,
                                                                               device=x.device)
-        z = torch.empty((B, Ho, Wo, 64), dtype=BF16, device=x.device)
-        nn.conv_igemm(self._desc(B, Ho, Wo), A, z, stats)
+        z = torch.empty((B, Ho, Wo, 64), dtype=act, device=x.device)
+        if act == BF16:
+            A = torch.empty((B * Ho * Wo, STEM_KP), dtype=BF16, device=x.device)
+            nn.im2col(x, STEM_K, STEM_K, 2, pt, pl, Ho, Wo, STEM_KP, A)
+            nn.conv_igemm(self._desc(B, Ho, Wo), A, z, stats)
+        else:
+            A = x                                   # the fp32 image itself (direct conv)
+            nn.conv_igemm(self._desc7(B, H, W, Ho, Wo), x, z, stats)
         y, mr = self.bn.normalize(z, stats, B, Ho * Wo, True, train=train)
         Hp, Wp = (Ho + 2 - 3) // 2 + 1, (Wo + 2 - 3) // 2 + 1
-        p = torch.empty((B, Hp, Wp, 64), dtype=BF16, device=x.device)
+        p = torch.empty((B, Hp, Wp, 64), dtype=act, device=x.device)
         arg = torch.empty((B, Hp, Wp, 64), dtype=torch.uint8, device=x.device)
         nn.maxpool3x3s2(y, p, arg)
         return p, (A, z, y, mr, arg, B, Ho, Wo)
@@ -70,6 +85,9 @@ class Stem(object):
         st = self.bn.store
         nn.bn_backward_relu(dy, z, mr, self.bn.gamma, self.bn.beta, dz, st.g(self.bn.gname), st.g(self.bn.bname),
                             B, Ho * Wo, 64, conv_dbias=self.conv.db)
+        if A.dtype != BF16:                         # fp32 parity mode: 7x7 weight gradient in place
+            nn.conv_wgrad(self._desc7(B, A.shape[1], A.shape[2], Ho, Wo), A, dz, self.conv.dw)
+            return
         dw = torch.empty((STEM_KP, 64), dtype=torch.float32, device=dp.device)
         nn.conv_wgrad(self._desc(B, Ho, Wo), A, dz, dw)
         self.conv.dw.view(147, 64).copy_(dw[:147])

@@ -34,9 +34,10 @@ class RetinaNetNet(FPNDetector):
         return "mobilenetv2"
 
     A = 9
-    def __init__(self, num_classes, n_anchors=9, backbone_model="resnet50", device="cuda", seed=0):
+    def __init__(self, num_classes, n_anchors=9, backbone_model="resnet50", device="cuda", seed=0, precision=None):
+        """precision: "bf16" (production) / "fp32" (parity mode); None = CVL_PRECISION or bf16."""
         self.A = n_anchors
-        self._init_common(num_classes, backbone_model, device, seed)
+        self._init_common(num_classes, backbone_model, device, seed, precision)
         self.cls_ld = self.cls_heads[0].npad
         self.reg_ld = self.reg_heads[0].npad
 

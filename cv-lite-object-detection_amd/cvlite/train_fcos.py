@@ -85,8 +85,9 @@ class FCOSTrainer(GraphStepper):
         self._custom_dim = False
         self.targets = torch.zeros((B, self.P, 5 + self.C), dtype=torch.float32, device=dev)
         self.ntgt = torch.zeros((B, 5), dtype=torch.int32, device=dev)
-        self.d_reg = torch.zeros((B, self.P, 32), dtype=BF16, device=dev)
-        self.d_cls = torch.zeros((B, self.P, net.cls_ld), dtype=BF16, device=dev)
+        act = net.store.act                   # bf16, or fp32 in the parity mode
+        self.d_reg = torch.zeros((B, self.P, 32), dtype=act, device=dev)
+        self.d_cls = torch.zeros((B, self.P, net.cls_ld), dtype=act, device=dev)
         self.losses = torch.zeros((B, 3), dtype=torch.float32, device=dev)
         if self.adam is not None:
             self.lr = self.adam.lr_dev

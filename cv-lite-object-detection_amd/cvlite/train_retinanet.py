@@ -54,8 +54,8 @@ class RetinaTrainer(GraphStepper):
         self.images = torch.zeros((B, S, S, 3), dtype=torch.float32, device=dev)
         self.targets = torch.zeros((B, T, 4 + self.C), dtype=torch.float32, device=dev)
         # padding channels of the head gradients must stay zero: written once, never touched
-        self.d_reg = torch.zeros((B, self.P, net.reg_ld), dtype=BF16, device=dev)
-        self.d_cls = torch.zeros((B, self.P, net.cls_ld), dtype=BF16, device=dev)
+        self.d_reg = torch.zeros((B, self.P, net.reg_ld), dtype=net.store.act, device=dev)   # bf16 | fp32 parity
+        self.d_cls = torch.zeros((B, self.P, net.cls_ld), dtype=net.store.act, device=dev)
         self.losses = torch.zeros((B, 2), dtype=torch.float32, device=dev)
         self.lr = torch.tensor([init_lr], dtype=torch.float32, device=dev)
         self.step_dev = torch.tensor([st_step], dtype=torch.int32, device=dev)

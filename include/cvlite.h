@@ -136,7 +136,13 @@ typedef struct {
   float beta;          /* dst = result + beta * dst */
   int nseg;
   cvl_conv_seg seg[CVL_CONV_MAX_SEG];
+  int prec;            /* CVL_PREC_BF16 (0): bf16 source / weights / destination (dst_f32 aside),
+                          bf16 MFMA.  CVL_PREC_F32 (1): the fp32 parity mode -- fp32 source, fp32
+                          packed weights (cvl_pack_item.f32_out), fp32 destination, fp32 FMA,
+                          deterministic; bn_stats then needs nseg == 1 (cvl_conv_wgrad* take the
+                          same field for x / dy). */
 } cvl_conv_desc;
+enum { CVL_PREC_BF16 = 0, CVL_PREC_F32 = 1 };
 
 /* workspace (optional, >= cvl_conv_igemm_workspace_size(d) bytes) enables split-K for grids too
  * small to fill the GPU (fp32 partial slabs + a finishing pass); NULL = no split. */
@@ -189,7 +195,8 @@ typedef struct {
   const float* w;      /* HWIO fp32 master [KH*KW][Cin][Cout] */
   void* w_fwd;         /* bf16 [Npad][KHW*Cin_k] or NULL */
   void* w_dgrad;       /* bf16 [Cin_pad][KHW*Cout_pad] or NULL */
-  int KHW, Cin, Cout, Cin_k, Npad, Cin_pad, Cout_pad, pad_;
+  int KHW, Cin, Cout, Cin_k, Npad, Cin_pad, Cout_pad;
+  int f32_out;         /* 1: w_fwd / w_dgrad are fp32 (the CVL_PREC_F32 parity mode; any Cin_k) */
 } cvl_pack_item;
 int cvl_pack_conv_weights_multi(const cvl_pack_item* items, const int32_t* tiles, int ntiles,
                                 cvl_stream_t stream);
@@ -291,6 +298,45 @@ typedef struct {
 size_t cvl_bias_grad_multi_workspace_size(const cvl_bias_item* items, int n);
 int cvl_bias_grad_multi(const cvl_bias_item* items, int n, void* workspace, size_t workspace_bytes,
                         cvl_stream_t stream);
+
+/* ------------------------------------------------------------------------------------------
+ * fp32 parity mode (SURVEY.md §8b "Parity modes", CVL_PRECISION=fp32): the same training graph
+ * with fp32 activations and activation gradients, for whole-graph parity with the reference's
+ * fp32 Keras graph (FCOS/fcos.py:6-110, RetinaNet/retinanet_module.py:8-159).  Convolutions take
+ * cvl_conv_desc.prec = CVL_PREC_F32; the memory-bound ops below are the fp32 forms of the
+ * entry points of the same names (same arguments, float tensors; every reduction fixed-order).
+ * cvl_bn_backward_f32 covers cvl_bn_backward (y_relu = the ReLU output, bn_beta NULL) and
+ * cvl_bn_backward_relu (y_relu NULL, bn_beta = the BN's beta: mask rebuilt from z), act_hi =
+ * INFINITY (ReLU) or 6 (ReLU6); workspace >= cvl_bn_backward_f32_workspace_size(B, C).
+ * cvl_bias_grad_multi_f32 takes cvl_bias_item rows of fp32 dy (no workspace).
+ * ---------------------------------------------------------------------------------------- */
+int cvl_bn_apply_f32(const float* z, const float* mean_rstd, const float* gamma, const float* beta,
+                     const float* residual, float* y, int B, int HW, int C, int relu, cvl_stream_t stream);
+int cvl_bn_finalize_apply_f32(const double* stats, float* mean_rstd, float* run_mean, float* run_var,
+                              const float* z, const float* gamma, const float* beta, const float* residual,
+                              float* y, int B, int HW, int C, int relu, float eps, float momentum,
+                              cvl_stream_t stream);
+size_t cvl_bn_backward_f32_workspace_size(int B, int C);
+int cvl_bn_backward_f32(const float* dy, const float* y_relu, const float* z, const float* mean_rstd,
+                        const float* gamma, const float* bn_beta, void* workspace, size_t workspace_bytes,
+                        float* dz, float* g_out, float* dgamma, float* dbeta, float beta_acc,
+                        float* conv_dbias, float act_hi, int B, int HW, int C, cvl_stream_t stream);
+int cvl_maxpool3x3s2_f32(const float* x, float* y, uint8_t* argmax, int B, int H, int W, int C,
+                         cvl_stream_t stream);
+int cvl_maxpool3x3s2_backward_f32(const float* dy, const uint8_t* argmax, float* dx, int B, int H, int W,
+                                  int C, cvl_stream_t stream);
+int cvl_upsample2x_add_f32(const float* a, const float* b, float* out, int B, int H, int W, int C,
+                           cvl_stream_t stream);
+int cvl_upsample2x_backward_f32(const float* dout, float* db, int B, int H, int W, int C, float beta,
+                                cvl_stream_t stream);
+int cvl_relu_backward_f32(const float* dy, const float* y, float* dx, long n, float beta, cvl_stream_t stream);
+int cvl_add_f32(const float* a, const float* b, float* out, long n, cvl_stream_t stream);
+int cvl_bias_grad_multi_f32(const cvl_bias_item* items, int n, cvl_stream_t stream);
+/* cvl_retina_loss with fp32 gradient outputs (the parity mode's RetinaNet heads). */
+int cvl_retina_loss_f32(const float* reg_pred, int ld_reg, const float* cls_pred, int ld_cls, const float* targets,
+                        int B, const int32_t* level_cells, int n_anchors, int num_classes, const float* img_weight,
+                        float grad_scale, float* losses, float* d_reg, int ld_dreg, float* d_cls, int ld_dcls,
+                        void* workspace, cvl_stream_t stream);
 
 /* ------------------------------------------------------------------------------------------
  * Optimizer (train_fcos.py:179-185): g <- (g * inv_bs) clipped by global norm `clip`

@@ -78,3 +78,33 @@ def test_no_cpu_fallback_in_product_path():
         net.prediction_to_corners(np.zeros((4, 4, 4), np.float32), net.anchor_boxes[0][0], 8)
     with pytest.raises(_lib.CvlError):
         fcos.prediction_to_corners(np.zeros((4, 4, 4), np.float32), 8)
+
+
+def test_struct_layouts_match_header(tmp_path):
+    """The ctypes mirrors of the header's structs (cvl_conv_desc incl. the parity-mode `prec`
+    field, cvl_conv_seg, cvl_pack_item, cvl_bias_item) have the C layout: sizes and the offsets
+    of every field, as gcc lays out include/cvlite.h."""
+    import ctypes
+    import shutil
+    import subprocess
+    from cvlite import ops_nn as nn
+    if shutil.which("gcc") is None:
+        import pytest
+        pytest.skip("no gcc")
+    checks = [("cvl_conv_desc", nn.ConvDesc), ("cvl_conv_seg", nn.ConvSeg), ("cvl_pack_item", nn.PackItem),
+              ("cvl_bias_item", nn.BiasItem)]
+    lines = []
+    for cname, cls in checks:
+        lines.append('printf("%s size %%zu\\n", sizeof(%s));' % (cname, cname))
+        for f in cls._fields_:
+            lines.append('printf("%s.%s %%zu\\n", offsetof(%s, %s));' % (cname, f[0], cname, f[0]))
+    src = tmp_path / "layout.c"
+    src.write_text('#include <stdio.h>\n#include <stddef.h>\n#include "%s"\nint main(void){%s return 0;}\n'
+                   % (os.path.join(ROOT, "include", "cvlite.h"), "\n".join(lines)))
+    exe = tmp_path / "layout"
+    subprocess.check_call(["gcc", "-I/opt/rocm/include", str(src), "-o", str(exe)])
+    got = dict(ln.rsplit(" ", 1) for ln in subprocess.check_output([str(exe)], text=True).splitlines())
+    for cname, cls in checks:
+        assert int(got["%s size" % cname]) == ctypes.sizeof(cls), cname
+        for f in cls._fields_:
+            assert int(got["%s.%s" % (cname, f[0])]) == getattr(cls, f[0]).offset, (cname, f[0])

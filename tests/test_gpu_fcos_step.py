@@ -78,7 +78,7 @@ def test_fcos_trainer_two_steps_match_reference_step():
         assert e_m <= 1.5 * own_m + 0.02 and e_m16 <= 1.5 * own_m + 0.02
         assert e_w <= 1.5 * own_w + 0.02 and e_w16 <= 1.5 * own_w + 0.02
     assert int(tr.step_dev.item()) == 2
-    assert abs(float(tr.lr.item()) - lr) < 1e-12            # max(5e-4 * 0.9^floor(1/1000), 1e-5)
+    assert float(tr.lr.item()) == float(np.float32(lr))       # max(5e-4 * 0.9^floor(1/1000), 1e-5)
 
 
 def test_fcos_center_trains_with_keras_adam_and_step_schedule():
