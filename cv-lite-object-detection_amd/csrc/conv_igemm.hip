@@ -500,7 +500,21 @@ static inline int pick_bn(int npad) { return npad % 128 == 0 ? 128 : (npad % 64 
 }  // namespace
 
 int cvl_conv_igemm_l(const cvl_conv_desc* d, int dst_up, int dst_w, const void* src, void* dst, double* bn_stats,
-                     hipStream_t s, const BnSumArgs* bsum = nullptr);
+                     hipStream_t s, const BnSumArgs* bsum = nullptr, void* workspace = nullptr,
+                     size_t workspace_bytes = 0);
+size_t cvl_conv_h_workspace(const cvl_conv_desc* d, const ConvArgs& a);
+
+// the split-K finishing pass of a single-segment launch whose partial slabs a.slab holds (used by
+// the halo kernel conv_igemm_h.hip as well)
+int cvl_conv_splitk_finish(const ConvArgs& a, hipStream_t s) {
+  const ConvSeg& S = a.seg[0];
+  const int HW = S.Hr * S.Wr;
+  int chunks = (512 + a.B - 1) / a.B;
+  int rpb = (HW + chunks - 1) / chunks;
+  rpb = rpb < 4 ? 4 : rpb;
+  hipLaunchKernelGGL(conv_splitk_finish, dim3((HW + rpb - 1) / rpb, a.B), dim3(NT), 0, s, a, rpb);
+  return cvl_launch_status();
+}
 
 // 1x1 strided data-gradient: only every stride-th dX pixel receives a gradient, so instead of a
 // DGRAD gather that finds no valid tap for (s^2-1)/s^2 of the rows, run a dense 1x1 GEMM over the
@@ -558,6 +572,7 @@ extern "C" const char* cvl_conv_kernel_name(int code) {
     case CVL_CK_WG_L128: return "conv_wgrad_l_kernel<128> (128x256)";
     case CVL_CK_WG_L256: return "conv_wgrad_l_kernel<256> (256x256)";
     case CVL_CK_WG_X: return "conv_wgrad_x_kernel (256x256, 5-slot ring of 32-row steps, grouped)";
+    case CVL_CK_H64: return "conv_igemm_h_kernel (256x64, 3x3 halo + 9-tap weight stage per channel block)";
     default: return "none";
   }
 }
@@ -572,7 +587,13 @@ extern "C" size_t cvl_conv_igemm_workspace_size(const cvl_conv_desc* d) {
   ConvArgs a;
   if (cvl_conv_prepare(d, BM, &a)) return 0;
   const int sp = pick_ksplit(a, pick_bn(a.Npad), a.Cin % 64 == 0 ? 64 : 32);
-  return sp > 1 ? (size_t)sp * a.m_total * a.Npad * sizeof(float) : 16;
+  size_t n = sp > 1 ? (size_t)sp * a.m_total * a.Npad * sizeof(float) : 16;
+  ConvArgs a256;                                   // the halo kernel's split-K slabs (256-row tiles)
+  if (cvl_conv_prepare(d, 256, &a256) == CVL_OK) {
+    const size_t h = cvl_conv_h_workspace(d, a256);
+    n = h > n ? h : n;
+  }
+  return n;
 }
 
 extern "C" int cvl_conv_igemm(const cvl_conv_desc* d, const void* src, void* dst, double* bn_stats,
@@ -614,7 +635,7 @@ extern "C" int cvl_conv_igemm(const cvl_conv_desc* d, const void* src, void* dst
     }
   }
   {
-    const int lst = cvl_conv_igemm_l(d, up, upw, src, dst, bn_stats, s);
+    const int lst = cvl_conv_igemm_l(d, up, upw, src, dst, bn_stats, s, nullptr, workspace, workspace_bytes);
     if (lst >= 0) return lst;          // the 256-row LDS-DMA kernel took the launch
   }
   a.src = reinterpret_cast<const cvl_bf16*>(src);
@@ -655,7 +676,8 @@ extern "C" int cvl_conv_igemm_dgrad_bnsum(const cvl_conv_desc* d, const void* sr
       if (cvl_conv_prepare(d, BM, &chk) == CVL_OK) {
         const BnSumArgs b{reinterpret_cast<const cvl_bf16*>(z), mean_rstd, gamma, beta, sums, act_hi};
         g_cvl_conv_last_kernel = CVL_CK_NONE;
-        const int lst = cvl_conv_igemm_l(d, 1, 0, src, dst, nullptr, (hipStream_t)stream, &b);
+        const int lst = cvl_conv_igemm_l(d, 1, 0, src, dst, nullptr, (hipStream_t)stream, &b, workspace,
+                                         workspace_bytes);
         if (lst >= 0) {
           *fused = lst == CVL_OK ? 1 : 0;
           return lst;

@@ -1,0 +1,350 @@
+// H64: 3x3 / stride 1 / pad 1 segmented implicit-GEMM convolution (forward and data gradient)
+// for the NARROW launches -- 256 x 64 tiles -- with the A operand staged once per channel block as
+// an LDS halo (gfx950, bf16 MFMA).
+//
+// Customers: the ResNet-50 3x3 units conv2_x..conv5_x (64->64 @ 128^2, 128->128 @ 64^2,
+// 256->256 @ 32^2, 512->512 @ 16^2 at 512 / bs 16; Keras ResNet50 behind FCOS/fcos.py:30-46 and
+// RetinaNet/retinanet_module.py:32-38), the FPN's 3x3 output convs (fcos.py:62-66) and any 3x3
+// launch whose 256-wide tiles would under-fill the chip.  These went through the L kernel's
+// 256 x 64 / 256 x 128 tiles, whose per-K-step im2col A tile (256 rows x 32 channels) costs
+// 16 LDS-DMA pieces for 64 MFMAs (A bytes per MFMA = 16 KiB / N): DMA issue, not the matrix pipe,
+// bounded them (0.11-0.25 of the bf16 peak).
+//
+// * Tile 256 (M) x 64 (N), 8 waves as 4 (M) x 2 (N); wave = 64 x 32 of C = 4 x 2
+//   v_mfma_f32_16x16x32_bf16 accumulators.
+// * Per 32-channel block cb one STAGE = the halo of the tile's 256 output pixels (rows of W + 2
+//   pixels incl. zero columns; whole small images as a mosaic with shared zero borders; <= 608
+//   pixels x 64 B) + the 9 taps' weights (9 x 64 rows x 64 B) = 74 KiB, double-buffered (2 stages
+//   = the 148 KiB of LDS).  A stage is 74 LDS-DMA pieces (1 KiB each): ~10 per wave per channel
+//   block, i.e. 0.12 pieces per MFMA for any N (the L kernel: 0.31 at N = 64).
+// * Three PHASES per channel block (kernel row r): a phase reads the fragments of the 3 taps
+//   (r, 0..2) -- A at the halo pixel offset (dy, dx), B from the tap's weight image -- and runs 24
+//   MFMAs.  The two wave groups (waves 0-3 / 4-7, one of each per SIMD) run one barrier apart, so
+//   each SIMD alternates one group's MFMA segment with the other's load segment (as X32).
+//   Stage cb + 1 is issued in phases 0 and 1 of block cb into the buffer block cb - 1 used, and
+//   each wave waits for its own pieces (vmcnt 0) at the start of phase 2: both groups' pieces
+//   have landed before the barrier that precedes the first read of block cb + 1.
+// * Operands arrive by buffer_load ... lds through buffer resources: out-of-map halo pixels,
+//   mosaic seams and absent images get an out-of-range offset and the hardware writes zeros.
+//   Halo pixels are 64-B rows with the XOR swizzle (p >> 1) & 3 on the 16-B chunk, applied to the
+//   per-lane SOURCE offset; the row pitch is a multiple of 8 pixels, so a dy shift keeps the
+//   swizzle (fragment reads conflict-free), and each lane precomputes its fragment addresses for
+//   dx = -1, 0, +1.
+// * Small grids split the channel blocks over blockIdx.z (fp32 slabs + conv_igemm.hip's finish).
+// * Epilogue (bias, ReLU, BN statistics, the fused BN-backward first pass, fp32 / bf16, beta):
+//   conv_epilogue.h, the L kernel's 256 x 64 form.
+#include "conv_common.h"
+#include "conv_epilogue.h"
+
+namespace {
+
+constexpr int BM = 256, BN = 64, NT = 512, BK = 32;
+constexpr int WGM = 4, WM = 64, WN = 32, TM = 4, TN = 2;
+constexpr int HPX = 608;                            // halo pixels per stage
+constexpr int HPC = HPX / 16;                       // halo DMA pieces (16 pixels each): 38
+constexpr int WPC = 9 * BN * BK * 2 / 1024;         // weight DMA pieces per stage: 36
+constexpr int NPC = HPC + WPC;                      // 74
+constexpr int PPW = (NPC + 7) / 8;                  // piece slots per wave: 10
+constexpr int HALO_EL = HPX * BK;                   // bf16 elements of a halo image (38,912 B)
+constexpr int WT_EL = 9 * BN * BK;                  // bf16 elements of a stage's weights (36,864 B)
+constexpr int STAGE_EL = HALO_EL + WT_EL;
+constexpr int LDS_C = BM * (BN + 8) + WGM * BN * 2 * 2;
+constexpr int LDS_EL = 2 * STAGE_EL > LDS_C ? 2 * STAGE_EL : LDS_C;
+constexpr unsigned kRecords = 0x7fffffffu;
+constexpr unsigned kOOB = 0x80000000u;
+
+__device__ __forceinline__ int swz4(int r) { return (r >> 1) & 3; }
+
+__device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t r, const cvl_bf16* lds_dst, unsigned voff) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)lds_dst, 16, (int)voff, 0,
+                                           0, 0);
+}
+
+// halo geometry of a segment (host and device agree): mosaic columns / rows of whole small
+// images, image rows per tile, pitch (pixels, multiple of 8) and halo rows
+struct HGeo {
+  int whole, mx, my, th, pitch, rows;
+};
+__host__ __device__ inline HGeo h_geo(int H, int W) {
+  HGeo g;
+  const int HW = H * W;
+  g.whole = HW < BM;
+  if (g.whole) {
+    const int n = BM / HW;
+    int lg = 0;
+    while ((1 << (lg + 1)) <= n) ++lg;
+    g.mx = 1 << ((lg + 1) / 2);
+    g.my = n / g.mx;
+    g.th = H;
+  } else {
+    g.mx = g.my = 1;
+    g.th = BM / W;
+  }
+  g.pitch = (g.mx * (W + 1) + 1 + 7) & ~7;
+  g.rows = g.my * (g.th + 1) + 1;
+  return g;
+}
+
+template <bool DGRAD, bool BSUM>
+__global__ void __launch_bounds__(NT) conv_igemm_h_kernel(ConvArgs a) {
+  __shared__ __attribute__((aligned(16))) cvl_bf16 lds[LDS_EL];
+
+  const int tid = threadIdx.x;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
+  const int ntn = a.Npad / BN;
+  const int nmn = gridDim.x;                        // m tiles x n tiles (the z dimension splits K)
+  const int L = xcd_remap(blockIdx.x, nmn);
+  const int m_tile = L / ntn, n_tile = L % ntn;
+  const int m0 = m_tile * BM, n0 = n_tile * BN;
+  int sg = 0;
+#pragma unroll
+  for (int i = 1; i < kMaxSeg; ++i)
+    if (i < a.nseg && m0 >= a.seg[i].m_start) sg = i;
+  const ConvSeg& S = a.seg[sg];
+  const int HWr = S.Hr * S.Wr;
+  const int mloc0 = m0 - S.m_start;
+  if (mloc0 >= S.rows) return;
+  s16x8 zpre[BnSumPre<BN, NT>::N];
+  BnSumPar bpar;
+  if constexpr (BSUM) bnsum_prefetch<BN, NT>(a, S, tid, n0, mloc0, zpre, bpar);
+
+  const int Cin = a.Cin, W = S.Wr, H = S.Hr;
+  const int Kdim = a.K;
+  const int ncb_all = Cin / BK;
+  int cb0 = 0, cb1 = ncb_all;
+  if (a.splits > 1) {
+    cb0 = blockIdx.z * a.ksteps_per_split;
+    cb1 = min(ncb_all, cb0 + a.ksteps_per_split);
+  }
+  const HGeo G = h_geo(H, W);
+  const int img0 = mloc0 / HWr;
+  const int y0 = G.whole ? 0 : (mloc0 - img0 * HWr) / W;
+  const int hpx = G.rows * G.pitch;
+
+  // this lane's DMA pieces: piece k = wave + 8 j; k < HPC: halo pixels 16k .. 16k+15 (lane: pixel
+  // lane / 4, chunk lane % 4); HPC <= k < NPC: weight rows 16 (k - HPC) % 64 .. of tap (k - HPC) / 4
+  const int hch = lane & 3;
+  unsigned poff[PPW];
+  unsigned pvalid = 0;
+#pragma unroll
+  for (int j = 0; j < PPW; ++j) {
+    const int k = wave + 8 * j;
+    poff[j] = 0u;
+    if (k < HPC) {
+      const int hp = 16 * k + (lane >> 2);
+      const int hy = hp / G.pitch, hx = hp - hy * G.pitch;
+      int img, gy, gx;
+      bool ok;
+      if (!G.whole) {
+        img = img0;
+        gy = y0 + hy - 1;
+        gx = hx - 1;
+        ok = gy >= 0 && gy < H && gx >= 0 && gx < W;
+      } else {
+        const int ix = (hx - 1) / (W + 1), iy = (hy - 1) / (H + 1);
+        gx = hx - 1 - ix * (W + 1);
+        gy = hy - 1 - iy * (H + 1);
+        img = img0 + iy * G.mx + ix;
+        ok = hx >= 1 && hy >= 1 && gx < W && gy < H && ix < G.mx && iy < G.my;
+      }
+      ok = ok && hp < hpx && img < a.B;
+      const long pix = S.src_base + (long)img * S.src_img + (long)gy * W + gx;
+      if (ok) {
+        poff[j] = (unsigned)(pix * Cin * 2) + (unsigned)((hch ^ swz4(hp)) * 16);
+        pvalid |= 1u << j;
+      }
+    } else if (k < NPC) {
+      const int w = k - HPC, tap = w >> 2;
+      const int row = (w & 3) * 16 + (lane >> 2);
+      poff[j] = (unsigned)(((n0 + row) * Kdim + tap * Cin) * 2) + (unsigned)((hch ^ swz4(row)) * 16);
+      pvalid |= 1u << j;
+    }
+  }
+  const __amdgpu_buffer_rsrc_t rsA = __builtin_amdgcn_make_buffer_rsrc((void*)a.src, (short)0, (int)kRecords, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rsB = __builtin_amdgcn_make_buffer_rsrc((void*)S.w, (short)0, (int)kRecords, 0x00020000);
+
+  // piece slots [j0, j1) of channel block cb into stage buffer sb (cb >= cb1: nothing)
+  auto issue = [&](int j0, int j1, int cb) {
+    if (cb >= cb1) return;
+    cvl_bf16* st = lds + (cb & 1) * STAGE_EL;
+    const unsigned cbo = (unsigned)(cb * BK * 2);
+#pragma unroll
+    for (int j = 0; j < PPW; ++j) {
+      if (j < j0 || j >= j1) continue;
+      const int k = wave + 8 * j;
+      if (k < HPC) dma16(rsA, st + k * 16 * BK, ((pvalid >> j) & 1u) ? poff[j] + cbo : kOOB);
+      else if (k < NPC) dma16(rsB, st + HALO_EL + (k - HPC) * 16 * BK, poff[j] + cbo);
+    }
+  };
+
+  const int wm = wave >> 1, wn = wave & 1;          // conv_l_epilogue's 4 x 2 wave grid
+  const int grp = wave >> 2;                        // stagger group (wm 0-1 / 2-3)
+  const int lr = lane & 15, lg = lane >> 4;
+  // swizzled LDS byte offset (within a halo image) of each A fragment row of this lane for
+  // dx = -1, 0, +1 (the dy shift is added per phase)
+  unsigned afr[TM][3];
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+    const int r = wm * WM + i * 16 + lr;
+    const int ii = r / HWr, q = r - ii * HWr;
+    const int yy = q / W, xx = q - yy * W;
+    const int hy = 1 + (G.whole ? (ii / G.mx) * (H + 1) : 0) + yy;
+    const int hx = 1 + (G.whole ? (ii % G.mx) * (W + 1) : 0) + xx;
+    const int pc = hy * G.pitch + hx;
+#pragma unroll
+    for (int d = 0; d < 3; ++d) {
+      const int p = pc + d - 1;
+      afr[i][d] = (unsigned)(p * BK * 2 + ((lg ^ swz4(p)) * 16));
+    }
+  }
+  // B fragment byte offsets within a tap's weight image
+  unsigned bfr[TN];
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    const int rr = wn * WN + j * 16 + lr;
+    bfr[j] = (unsigned)(rr * BK * 2 + ((lg ^ swz4(rr)) * 16));
+  }
+  f32x4 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  auto bar = [&]() {
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+  };
+
+  // prologue: stage cb0 complete everywhere
+  issue(0, PPW, cb0);
+  wait_vm<0>();
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+  if (grp == 1) bar();            // stagger: waves 4-7 run one barrier behind
+
+  const int prow = G.pitch * BK * 2;                // bytes per halo row
+  for (int cb = cb0; cb < cb1; ++cb) {
+    const char* Hc = reinterpret_cast<const char*>(lds + (cb & 1) * STAGE_EL);
+    const char* Wc = Hc + HALO_EL * 2;
+#pragma unroll 1
+    for (int r = 0; r < 3; ++r) {
+      if (r == 0) issue(0, PPW / 2, cb + 1);
+      else if (r == 1) issue(PPW / 2, PPW, cb + 1);
+      else wait_vm<0>();                            // this wave's pieces of stage cb + 1 landed
+      const int dyoff = (DGRAD ? 1 - r : r - 1) * prow;
+      s16x8 fa[3][TM], fb[3][TN];
+#pragma unroll
+      for (int s = 0; s < 3; ++s) {
+        const int d = DGRAD ? 2 - s : s;
+        const char* Wt = Wc + (3 * r + s) * BN * BK * 2;
+#pragma unroll
+        for (int i = 0; i < TM; ++i) fa[s][i] = *reinterpret_cast<const s16x8*>(Hc + afr[i][d] + dyoff);
+#pragma unroll
+        for (int j = 0; j < TN; ++j) fb[s][j] = *reinterpret_cast<const s16x8*>(Wt + bfr[j]);
+      }
+      bar();
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int s = 0; s < 3; ++s)
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, fa[s][i]),
+                                                                 __builtin_bit_cast(bf16x8, fb[s][j]), acc[i][j], 0, 0,
+                                                                 0);
+      __builtin_amdgcn_s_setprio(0);
+      __builtin_amdgcn_sched_barrier(0);
+      bar();
+    }
+  }
+  if (grp == 0) bar();            // equal barrier counts for both groups
+  wait_vm<0>();
+  if (a.splits > 1) {             // raw fp32 partials; conv_igemm.hip's finish applies the epilogue
+    float* slab = a.slab + (size_t)blockIdx.z * a.m_total * a.Npad;
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int rr = m0 + wm * WM + i * 16 + lg * 4 + e;
+          const int c = n0 + wn * WN + j * 16 + lr;
+          slab[(size_t)rr * a.Npad + c] = acc[i][j][e];
+        }
+    return;
+  }
+  conv_l_epilogue<BN, WGM, TM, TN, NT, BSUM>(a, S, acc, lds, tid, wm, wn, n0, mloc0, HWr, zpre, bpar);
+}
+
+}  // namespace
+
+int cvl_conv_splitk_finish(const ConvArgs& a, hipStream_t s);
+
+// Geometry H64 covers: 3x3, stride 1, pad 1, source map = output map, every segment's 256-row tiles
+// whole image rows (W | 256, H*W % 256 == 0) or whole images (H*W | 256), halo within HPX pixels.
+bool cvl_conv_h_fits(const cvl_conv_desc* d, const ConvArgs& a) {
+  if (d->KH != 3 || d->KW != 3 || d->stride != 1 || d->pad_t != 1 || d->pad_l != 1 || a.Cin % BK ||
+      a.Npad % BN || a.relu_in || a.dst_up != 1)
+    return false;
+  for (int i = 0; i < a.nseg; ++i) {
+    const ConvSeg& q = a.seg[i];
+    if (q.Hr != q.Hs || q.Wr != q.Ws) return false;
+    const int W = q.Wr, HW = q.Hr * q.Wr;
+    if (HW >= BM ? (BM % W || HW % BM) : (BM % HW)) return false;
+    const HGeo g = h_geo(q.Hr, W);
+    if (g.mx * g.my * (g.whole ? HW : BM) != BM || g.rows * g.pitch > HPX) return false;
+    const long src_bytes = (q.src_base + (long)a.B * q.src_img) * a.Cin * 2;
+    if (src_bytes >= (long)kRecords - 65536) return false;
+  }
+  return (long)a.Npad * a.K * 2 < (long)kRecords;
+}
+
+// Runs the launch on H64 (called by cvl_conv_igemm_l for 3x3 launches it would give 64/128-wide
+// tiles); -1 when it does not apply.  `slab` / `slab_bytes`: the caller's split-K workspace (may be
+// null: no split).
+int cvl_conv_igemm_h(const cvl_conv_desc* d, const ConvArgs& a0, hipStream_t s, void* slab, size_t slab_bytes) {
+  if (cvl_env_flag("CVL_CONV_NO_H") || !cvl_conv_h_fits(d, a0)) return -1;
+  ConvArgs a = a0;
+  const bool dg = d->mode == CVL_CONV_DGRAD;
+  const int tiles = a.m_tiles * (a.Npad / BN);
+  const int ncb = a.Cin / BK;
+  // split the channel blocks of grids that leave CUs idle (fp32 slabs, single segment, no fused
+  // BN-backward sums: the finish kernel forms BN statistics but not those)
+  int splits = 1;
+  const int target = cvl_env_int("CVL_CONV_H_SPLIT_TARGET", 256);
+  if (tiles < target && a.nseg == 1 && !a.bsum && slab && d->n_store % 8 == 0 && d->dst_coff % 8 == 0 &&
+      (d->dst_f32 || d->ld_dst % 8 == 0) && d->n_store / 8 <= 256) {
+    splits = (target + tiles - 1) / tiles;
+    if (splits > ncb / 2) splits = ncb / 2;
+    if (splits < 1) splits = 1;
+    if ((size_t)splits * a.m_total * a.Npad * sizeof(float) > slab_bytes) splits = 1;
+  }
+  if (splits > 1) {
+    a.ksteps_per_split = (ncb + splits - 1) / splits;
+    a.splits = (ncb + a.ksteps_per_split - 1) / a.ksteps_per_split;
+    a.slab = reinterpret_cast<float*>(slab);
+  } else {
+    a.splits = 1;
+  }
+  dim3 grid(tiles, 1, a.splits);
+  g_cvl_conv_last_kernel = CVL_CK_H64;
+  if (dg && a.bsum) hipLaunchKernelGGL((conv_igemm_h_kernel<true, true>), grid, dim3(NT), 0, s, a);
+  else if (dg) hipLaunchKernelGGL((conv_igemm_h_kernel<true, false>), grid, dim3(NT), 0, s, a);
+  else hipLaunchKernelGGL((conv_igemm_h_kernel<false, false>), grid, dim3(NT), 0, s, a);
+  int st = cvl_launch_status();
+  if (st || a.splits <= 1) return st;
+  return cvl_conv_splitk_finish(a, s);
+}
+
+// split-K workspace H64 would use for this descriptor (0: none)
+size_t cvl_conv_h_workspace(const cvl_conv_desc* d, const ConvArgs& a) {
+  if (!cvl_conv_h_fits(d, a) || a.nseg != 1) return 0;
+  const int tiles = a.m_tiles * (a.Npad / BN);
+  const int target = cvl_env_int("CVL_CONV_H_SPLIT_TARGET", 256);
+  if (tiles >= target) return 0;
+  int splits = (target + tiles - 1) / tiles;
+  if (splits > (a.Cin / BK) / 2) splits = (a.Cin / BK) / 2;
+  return splits > 1 ? (size_t)splits * a.m_total * a.Npad * sizeof(float) : 0;
+}

@@ -192,18 +192,20 @@ __global__ void __launch_bounds__(NT) conv_igemm_l_kernel(ConvArgs a) {
 }  // namespace
 
 int cvl_conv_igemm_x(const cvl_conv_desc* d, const ConvArgs& a, hipStream_t s);
+int cvl_conv_igemm_h(const cvl_conv_desc* d, const ConvArgs& a, hipStream_t s, void* slab, size_t slab_bytes);
 
 // Called by cvl_conv_igemm when the launch qualifies (see cvl_conv_igemm_l_ok); returns -1 when
 // it does not, so the caller falls back to the 128-row kernel.
 int cvl_conv_igemm_l(const cvl_conv_desc* d, int dst_up, int dst_w, const void* src, void* dst, double* bn_stats,
-                     hipStream_t s, const BnSumArgs* bsum) {
+                     hipStream_t s, const BnSumArgs* bsum, void* workspace, size_t workspace_bytes) {
   if (cvl_env_flag("CVL_CONV_NO_L")) return -1;
   if (bsum && (d->mode != CVL_CONV_DGRAD || d->dst_f32 || d->beta != 0.f || dst_up != 1 || bn_stats)) return -1;
   // fp32 destinations store element-wise: any n_store (the RetinaNet box heads: 9 anchors x 4 = 36)
   const bool n_ok = d->dst_f32 ? (d->n_store % 4 == 0 && !cvl_env_flag("CVL_CONV_L_F32_N8")) : d->n_store % 8 == 0;
-  if (d->Cin % 64 != 0 || d->relu_in || !n_ok || (d->dst_f32 && bn_stats) ||
+  if (d->Cin % 32 != 0 || d->relu_in || !n_ok || (d->dst_f32 && bn_stats) ||
       (!d->dst_f32 && (d->ld_dst % 8 || d->dst_coff % 8)) || (d->dst_f32 && cvl_env_flag("CVL_CONV_L_NO_F32")))
     return -1;
+  const bool l_cin = d->Cin % 64 == 0;          // the L / X kernels: 64-channel K steps
   // 256-wide tiles (forward and data-gradient) for launches with >= CVL_CONV_L256_MIN_TILES of
   // them.  A single FCOS tower's dgrad (341 tiles) lost 35 % on them (tools/conv_ab.py); the
   // paired cls+reg tower dgrad (682 tiles) gains: whole step 813 -> 827 img/s
@@ -212,7 +214,7 @@ int cvl_conv_igemm_l(const cvl_conv_desc* d, int dst_up, int dst_w, const void* 
                     (d->mode == CVL_CONV_FWD || !cvl_env_flag("CVL_CONV_NO_DGRAD_256"));
   const int bn = w256 ? 256 : (d->Npad % 128 == 0 ? 128 : (d->Npad % 64 == 0 ? 64 : 0));
   if (!bn) return -1;
-  if (d->KH * d->KW * d->Cin < cvl_env_int("CVL_CONV_L_MIN_K", 0) && !bsum) return -1;   // A/B knob
+  if (l_cin && d->KH * d->KW * d->Cin < cvl_env_int("CVL_CONV_L_MIN_K", 0) && !bsum) return -1;   // A/B knob
   ConvArgs a;
   if (cvl_conv_prepare(d, BM, &a)) return -1;
   a.dst_up = dst_up;
@@ -229,6 +231,28 @@ int cvl_conv_igemm_l(const cvl_conv_desc* d, int dst_up, int dst_w, const void* 
   // CenterNet +0.4 % at K < 512)
   const int w256_min_k = cvl_env_int("CVL_CONV_W256_MIN_K", 512);
   if (use_bn == 256 && a.K < w256_min_k) use_bn = 128;
+  // 3x3 / stride 1 launches that do not take the 256 x 256 tiles: the halo-staged 256 x 64 kernel
+  // (conv_igemm_h.hip), whose A traffic is one halo per channel block instead of nine im2col tiles
+  if (use_bn != 256 && (!bsum || ((a.seg[0].Hr * a.seg[0].Wr) % BM == 0 && !bn_stats))) {
+    ConvArgs ah = a;
+    ah.dst_up = dst_up;
+    ah.dst_w = dst_w;
+    ah.src = reinterpret_cast<const cvl_bf16*>(src);
+    ah.dst = dst;
+    ah.stats = bn_stats;
+    bool bs_ok = true;
+    if (bsum) {
+      for (int i = 0; i < ah.nseg; ++i)
+        if ((ah.seg[i].Hr * ah.seg[i].Wr) % BM || ah.seg[i].dst_img != (long)ah.seg[i].Hr * ah.seg[i].Wr) bs_ok = false;
+      ah.bz = bsum->z; ah.bmr = bsum->mr; ah.bga = bsum->gamma; ah.bbe = bsum->beta; ah.bsum = bsum->sums;
+      ah.bhi = bsum->hi;
+    }
+    if (bs_ok) {
+      const int hst = cvl_conv_igemm_h(d, ah, s, workspace, workspace_bytes);
+      if (hst >= 0) return hst;
+    }
+  }
+  if (!l_cin) return -1;
   // a launch that would leave CUs idle with 128-wide tiles takes 64-wide ones (twice the tiles),
   // also when that lifts it over min_tiles (from the split-K 128-row kernel): FCOS A/B 970 -> 983
   // img/s at 256 for the 128-tile conv4_x launches, -> 988 with the conv5_x ones (512: 966, 1024: 941)
