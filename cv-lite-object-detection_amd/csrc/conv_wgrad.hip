@@ -389,6 +389,9 @@ int check_wgrad_desc(const cvl_conv_desc* d, int ngroups, const void* x, const v
 
 }  // namespace
 
+long cvl_conv_wgrad_h_workspace(const cvl_conv_desc* d, int ngroups);
+int cvl_conv_wgrad_h(const cvl_conv_desc* d, int ngroups, const void* x, const void* dy, float* const* dw, float beta,
+                     void* workspace, size_t workspace_bytes, hipStream_t s);
 size_t cvl_conv_wgrad_f32_workspace(const cvl_conv_desc* d, int ngroups);
 int cvl_conv_wgrad_f32(const cvl_conv_desc* d, int ngroups, const void* x, const void* dy, float* const* dw,
                        float beta, void* workspace, size_t workspace_bytes, hipStream_t s);
@@ -398,6 +401,8 @@ extern "C" size_t cvl_conv_wgrad_grouped_workspace_size(const cvl_conv_desc* d, 
   if (d->prec == CVL_PREC_F32) return cvl_conv_wgrad_f32_workspace(d, ngroups);
   const long wsn = cvl_conv_wgrad_sn_workspace(d, ngroups);
   if (wsn >= 0) return (size_t)(wsn > 16 ? wsn : 16);
+  const long wh = cvl_conv_wgrad_h_workspace(d, ngroups);
+  if (wh >= 0) return (size_t)wh;
   const long wx = cvl_conv_wgrad_x_workspace(d, ngroups);
   if (wx >= 0) return (size_t)wx;
   size_t m = 16;
@@ -425,6 +430,8 @@ extern "C" int cvl_conv_wgrad_grouped(const cvl_conv_desc* d, int ngroups, const
   hipStream_t s = (hipStream_t)stream;
   const int snst = cvl_conv_wgrad_sn(d, ngroups, x, dy, dw, beta, workspace, workspace_bytes, s);
   if (snst >= 0) return snst;
+  const int hst = cvl_conv_wgrad_h(d, ngroups, x, dy, dw, beta, workspace, workspace_bytes, s);
+  if (hst >= 0) return hst;
   const int xst = cvl_conv_wgrad_x(d, ngroups, x, dy, dw, beta, workspace, workspace_bytes, s);
   if (xst >= 0) return xst;
   if (ngroups == 1) return wgrad_single(d, x, dy, dw[0], beta, workspace, workspace_bytes, s);

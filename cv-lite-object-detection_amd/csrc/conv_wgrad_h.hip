@@ -1,0 +1,309 @@
+// WH: 3x3 / stride 1 / pad 1 convolution WEIGHT gradient with the source staged as an LDS halo
+// (gfx950, bf16 MFMA, fp32 accumulation) -- the Conv2DBackpropFilter + per-image gradient sum of
+// FCOS/train_fcos.py:173-176 for the ResNet-50 3x3 units (Keras ResNet50 behind fcos.py:30-46) and
+// the FPN 3x3 convs on maps of width 16..128:
+//   dW[(r, s, c), co] = sum over the rows m (output pixels) of  X[m shifted by (r-1, s-1), c] * dY[m, co]
+// The generic kernels stage nine shifted im2col tiles per 32-row step; here a 128-row step (whole
+// image rows) stages its source pixels ONCE as a halo (rows y0-1 .. y0+R, W+2 pixels wide) and the
+// nine taps read it at pixel offsets: 67 LDS-DMA pieces per 1,152 MFMAs (0.06 per MFMA).
+// * Workgroup = (64 input channels) x (64 output channels) x all 9 taps = a 64 x 576 C tile, over a
+//   chunk of 128-row steps; 8 waves as 2 (co halves) x 4 (16-channel quarters), each wave
+//   2 x 9 v_mfma_f32_16x16x32_bf16 accumulators (co tile x tap).
+// * Stage = halo [<= 408 px][64 ch] + dY [128 rows][64 co], 128-B rows, double-buffered (134 KiB).
+//   Two phases per step (2 x 32-row sub-steps, 36 MFMAs per wave each); the wave groups (channel
+//   quarters 0-1 / 2-3) run one barrier apart; step s+1 is issued in phase 0 of step s into the
+//   buffer step s-1 used and waited for (vmcnt 0) at the start of phase 1.
+// * Fragments by ds_read_b64_tr_b16 (the reduction index is the LDS row index): dY^T (co) is the
+//   MFMA A operand, the shifted X^T (channels) the B operand.  16-B chunks are XOR-swizzled by
+//   bits 1 and 3 of the pixel / row index (applied to the per-lane DMA SOURCE offset), which keeps
+//   every 32-lane transposed read conflict-free under any tap shift.
+// * Chunks of steps are spread over workgroups to fill the GPU; partial tiles go to fp32 slabs
+//   summed in a fixed order (deterministic), or straight into dW (with beta) for one chunk.
+#include "conv_common.h"
+
+namespace {
+
+constexpr int NT = 512, BCI = 64, BCO = 64, RS = 128;
+constexpr int HPX = 408;                             // halo pixels per stage (W = 128: 3 x 136)
+constexpr int HALO_B = HPX * 128;                    // bytes
+constexpr int DY_B = RS * 128;
+constexpr int STAGE_B = HALO_B + DY_B;               // 68,608 B
+constexpr int NPS = HPX / 8 + RS / 8;                // DMA pieces per stage (max): 51 + 16
+constexpr int PPW = (NPS + 7) / 8;                   // piece slots per wave: 9
+constexpr unsigned kRecords = 0x7fffffffu;
+constexpr unsigned kOOB = 0x80000000u;
+
+__device__ __forceinline__ int swz8(int p) { return ((((p >> 1) & 1) | (((p >> 3) & 1) << 1)) << 1); }
+
+__device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t r, const void* lds_dst, unsigned voff) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)lds_dst, 16, (int)voff, 0,
+                                           0, 0);
+}
+
+
+struct WhArgs {
+  const cvl_bf16* x;
+  const cvl_bf16* dy;
+  float* out;                 // slab [nsplit][K][Cout] or dW (direct)
+  long src_base, src_img, dst_base, dst_img;
+  int B, H, W, Cin, Cout, ld_dy, dy_coff;
+  int ci_tiles, co_tiles, steps, chunk, nsplit, direct;
+  float beta;
+};
+
+__global__ void __launch_bounds__(NT) conv_wgrad_h_kernel(WhArgs g) {
+  __shared__ __attribute__((aligned(16))) char lds[2 * STAGE_B];
+  const int tid = threadIdx.x;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
+  const int tiles = g.ci_tiles * g.co_tiles;
+  const int L = xcd_remap(blockIdx.x, gridDim.x);
+  const int tile = L % tiles, split = L / tiles;      // the tiles of one chunk share an XCD's L2
+  const int ci0 = (tile % g.ci_tiles) * BCI, co0 = (tile / g.ci_tiles) * BCO;
+  const int s0 = split * g.chunk, s1 = min(s0 + g.chunk, g.steps);
+  const int W = g.W, H = g.H, HW = H * W;
+  const int R = RS / W;                                // image rows per step
+  const int P = (W + 2 + 7) & ~7;                      // halo pitch (pixels)
+  const int hpx = (R + 2) * P;
+  const int nh = (hpx + 7) / 8;                        // halo pieces; dY pieces follow
+  const int ch = lane & 7;
+
+  // piece slots of this lane: k = wave + 8 j
+  int pk_hy[PPW], pk_hx[PPW];
+  unsigned pk_chs[PPW];
+#pragma unroll
+  for (int j = 0; j < PPW; ++j) {
+    const int k = wave + 8 * j;
+    if (k < nh) {
+      const int hp = 8 * k + (lane >> 3);
+      pk_hy[j] = hp < hpx ? hp / P : -1000;
+      pk_hx[j] = hp - (hp / P) * P;
+      pk_chs[j] = (unsigned)((ch ^ swz8(hp)) * 16);
+    } else {
+      const int m = 8 * (k - nh) + (lane >> 3);
+      pk_hy[j] = m;                                  // dY row of the step
+      pk_hx[j] = 0;
+      pk_chs[j] = (unsigned)((ch ^ swz8(m)) * 16);
+    }
+  }
+  const __amdgpu_buffer_rsrc_t rsX = __builtin_amdgcn_make_buffer_rsrc((void*)g.x, (short)0, (int)kRecords, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rsY = __builtin_amdgcn_make_buffer_rsrc((void*)g.dy, (short)0, (int)kRecords, 0x00020000);
+
+  auto issue = [&](int s) {
+    if (s >= s1) return;
+    char* st = lds + (s & 1) * STAGE_B;
+    const int m0 = s * RS;
+    const int img = m0 / HW;
+    const int y0 = (m0 - img * HW) / W;
+#pragma unroll
+    for (int j = 0; j < PPW; ++j) {
+      const int k = wave + 8 * j;
+      if (k < nh) {
+        const int gy = y0 + pk_hy[j] - 1, gx = pk_hx[j] - 1;
+        const bool ok = gy >= 0 && gy < H && gx >= 0 && gx < W;
+        const long pix = g.src_base + (long)img * g.src_img + (long)gy * W + gx;
+        dma16(rsX, st + k * 1024, ok ? (unsigned)((pix * g.Cin + ci0) * 2) + pk_chs[j] : kOOB);
+      } else if (k < nh + RS / 8) {
+        const long drow = g.dst_base + (long)img * g.dst_img + (long)y0 * W + pk_hy[j];
+        dma16(rsY, st + HALO_B + (k - nh) * 1024,
+              (unsigned)((drow * g.ld_dy + g.dy_coff + co0) * 2) + pk_chs[j]);
+      }
+    }
+  };
+
+  const int wco = wave & 1, wk = wave >> 1, grp = wave >> 2;
+  const int lr = lane & 15, lg = lane >> 4;
+  const int q = lr >> 2, p = lr & 3;
+  // per-lane transposed-read byte offsets (within a stage) for the rows of sub-step u (0..3):
+  // lo = row 32u + 8lg + q, hi = lo + 4.  dY: co tile i; X: halo pixel of the row at dx = s
+  // (the dy = r shift adds r * P * 128 bytes, which keeps the swizzle: P % 8 == 0)
+  unsigned yof[4][2][2], xof[4][2][3];
+#pragma unroll
+  for (int u = 0; u < 4; ++u)
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int m = 32 * u + 8 * lg + q + 4 * h;
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int c16 = (wco * 32 + i * 16) / 8 + (p >> 1);     // 16-B chunk of the co column
+        yof[u][h][i] = (unsigned)(HALO_B + m * 128 + ((c16 ^ swz8(m)) * 16) + (p & 1) * 8);
+      }
+      const int oy = m / W, ox = m - (m / W) * W;
+      const int c16 = (wk * 16) / 8 + (p >> 1);
+#pragma unroll
+      for (int s = 0; s < 3; ++s) {
+        const int hp = oy * P + ox + s;
+        xof[u][h][s] = (unsigned)(hp * 128 + ((c16 ^ swz8(hp)) * 16) + (p & 1) * 8);
+      }
+    }
+  const unsigned rowb = (unsigned)(P * 128);
+
+  f32x4 acc[2][9];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int t = 0; t < 9; ++t) acc[i][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+  auto bar = [&]() {
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+  };
+  const unsigned lds0 = lds_addr(lds);
+
+  issue(s0);
+  wait_vm<0>();
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+  if (grp == 1) bar();            // stagger: waves 4-7 run one barrier behind
+
+  for (int s = s0; s < s1; ++s) {
+    const unsigned sb = lds0 + (unsigned)((s & 1) * STAGE_B);
+#pragma unroll 1
+    for (int ph = 0; ph < 2; ++ph) {
+      if (ph == 0) issue(s + 1);
+      else wait_vm<0>();                       // this wave's pieces of step s + 1 landed
+      // transposed reads as inline asm (conv_common.h ds_tr16: the builtin would make the compiler
+      // drain the in-flight DMA of step s + 1 before every read); pinned after the lgkmcnt wait
+      s16x4 ylo[2][2], yhi[2][2], xlo[2][9], xhi[2][9];
+#pragma unroll
+      for (int uu = 0; uu < 2; ++uu) {
+        const int u = 2 * ph + uu;
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+          ylo[uu][i] = ds_tr16(sb + yof[u][0][i]);
+          yhi[uu][i] = ds_tr16(sb + yof[u][1][i]);
+        }
+#pragma unroll
+        for (int t = 0; t < 9; ++t) {
+          const int r = t / 3, c = t - 3 * (t / 3);
+          xlo[uu][t] = ds_tr16(sb + xof[u][0][c] + r * rowb);
+          xhi[uu][t] = ds_tr16(sb + xof[u][1][c] + r * rowb);
+        }
+      }
+      bar();
+      lgkm_wait();
+#pragma unroll
+      for (int uu = 0; uu < 2; ++uu) {
+#pragma unroll
+        for (int i = 0; i < 2; ++i) { tr_pin(ylo[uu][i]); tr_pin(yhi[uu][i]); }
+#pragma unroll
+        for (int t = 0; t < 9; ++t) { tr_pin(xlo[uu][t]); tr_pin(xhi[uu][t]); }
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int uu = 0; uu < 2; ++uu)
+#pragma unroll
+        for (int t = 0; t < 9; ++t)
+#pragma unroll
+          for (int i = 0; i < 2; ++i)
+            acc[i][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+                __builtin_bit_cast(bf16x8, tr_join(ylo[uu][i], yhi[uu][i])),
+                __builtin_bit_cast(bf16x8, tr_join(xlo[uu][t], xhi[uu][t])), acc[i][t], 0, 0, 0);
+      __builtin_amdgcn_s_setprio(0);
+      __builtin_amdgcn_sched_barrier(0);
+      bar();
+    }
+  }
+  if (grp == 0) bar();            // equal barrier counts for both groups
+  wait_vm<0>();
+  // C[co][k] -> out[k][co] (HWIO), 4 consecutive co per lane
+  const long K = 9L * g.Cin;
+  float* out = g.direct ? g.out : g.out + (size_t)split * K * g.Cout;
+#pragma unroll
+  for (int t = 0; t < 9; ++t)
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const long k = (long)t * g.Cin + ci0 + wk * 16 + lr;
+      const int co = co0 + wco * 32 + i * 16 + 4 * lg;
+      f32x4 v = acc[i][t];
+      f32x4* po = reinterpret_cast<f32x4*>(out + k * g.Cout + co);
+      if (g.direct && g.beta != 0.f) v += g.beta * *po;
+      *po = v;
+    }
+}
+
+// dw[i] = beta*dw[i] + sum over splits of slab[split][i], splits in order (deterministic)
+__global__ void __launch_bounds__(256) wgrad_h_reduce(const float* __restrict__ slab, float* __restrict__ dw, long n4,
+                                                      int nsplit, float beta) {
+  for (long i = blockIdx.x * 256L + threadIdx.x; i < n4; i += (long)gridDim.x * 256) {
+    f32x4 s = f32x4{0.f, 0.f, 0.f, 0.f};
+    const f32x4* p = reinterpret_cast<const f32x4*>(slab) + i;
+    int k = 0;
+    for (; k + 4 <= nsplit; k += 4) {
+      const f32x4 a0 = p[(long)k * n4], a1 = p[(long)(k + 1) * n4];
+      const f32x4 a2 = p[(long)(k + 2) * n4], a3 = p[(long)(k + 3) * n4];
+      s += (a0 + a1) + (a2 + a3);
+    }
+    for (; k < nsplit; ++k) s += p[(long)k * n4];
+    f32x4* d = reinterpret_cast<f32x4*>(dw) + i;
+    if (beta != 0.f) s += beta * *d;
+    *d = s;
+  }
+}
+
+struct WhPlan {
+  int steps, nsplit, chunk;
+  size_t slab;
+};
+
+inline bool wh_plan(const cvl_conv_desc* d, int ngroups, WhPlan* pl) {
+  if (cvl_env_flag("CVL_WGRAD_NO_H") || ngroups != 1 || d->nseg != 1 || d->mode != CVL_CONV_FWD) return false;
+  if (d->prec != CVL_PREC_BF16 || d->KH != 3 || d->KW != 3 || d->stride != 1 || d->pad_t != 1 || d->pad_l != 1 ||
+      d->relu_in || d->Cin % BCI || d->n_store % BCO || d->ld_dst % 8 || d->dst_coff % 8)
+    return false;
+  const cvl_conv_seg& q = d->seg[0];
+  const int W = q.Wr, HW = q.Hr * q.Wr;
+  if (q.Hr != q.Hs || q.Wr != q.Ws || W < 16 || RS % W || HW % RS || q.src_img != HW || q.dst_img < HW) return false;
+  if ((RS / W + 2) * ((W + 2 + 7) & ~7) > HPX) return false;
+  const long src_end = (q.src_base + (long)d->B * q.src_img) * d->Cin * 2;
+  const long dy_end = (q.dst_base + (long)d->B * q.dst_img) * d->ld_dst * 2;
+  if (src_end >= (long)kRecords - 65536 || dy_end >= (long)kRecords - 65536) return false;
+  const int tiles = (d->Cin / BCI) * (d->n_store / BCO);
+  pl->steps = d->B * HW / RS;
+  // one workgroup per CU (134 KiB of LDS): ~256 workgroups, >= 4 steps each
+  const int target = cvl_env_int("CVL_WGH_WGS", 256);
+  int ns = (target + tiles - 1) / tiles;
+  if (ns > pl->steps / 4) ns = pl->steps / 4;
+  if (ns < 1) ns = 1;
+  pl->chunk = (pl->steps + ns - 1) / ns;
+  pl->nsplit = (pl->steps + pl->chunk - 1) / pl->chunk;
+  pl->slab = pl->nsplit > 1 ? (size_t)pl->nsplit * 9 * d->Cin * d->n_store * sizeof(float) : 0;
+  return true;
+}
+
+}  // namespace
+
+// workspace the halo weight gradient needs (>= 16), or -1 when the launch does not qualify
+long cvl_conv_wgrad_h_workspace(const cvl_conv_desc* d, int ngroups) {
+  WhPlan pl;
+  if (!d || !wh_plan(d, ngroups, &pl)) return -1;
+  return (long)(pl.slab > 16 ? pl.slab : 16);
+}
+
+int cvl_conv_wgrad_h(const cvl_conv_desc* d, int ngroups, const void* x, const void* dy, float* const* dw, float beta,
+                     void* workspace, size_t workspace_bytes, hipStream_t s) {
+  WhPlan pl;
+  if (!wh_plan(d, ngroups, &pl)) return -1;
+  if (!workspace || workspace_bytes < (pl.slab > 16 ? pl.slab : 16)) return CVL_EINVAL;
+  const cvl_conv_seg& q = d->seg[0];
+  WhArgs g;
+  g.x = reinterpret_cast<const cvl_bf16*>(x);
+  g.dy = reinterpret_cast<const cvl_bf16*>(dy);
+  g.src_base = q.src_base; g.src_img = q.src_img; g.dst_base = q.dst_base; g.dst_img = q.dst_img;
+  g.B = d->B; g.H = q.Hr; g.W = q.Wr; g.Cin = d->Cin; g.Cout = d->n_store;
+  g.ld_dy = d->ld_dst; g.dy_coff = d->dst_coff;
+  g.ci_tiles = d->Cin / BCI; g.co_tiles = d->n_store / BCO;
+  g.steps = pl.steps; g.chunk = pl.chunk; g.nsplit = pl.nsplit;
+  g.direct = pl.nsplit == 1;
+  g.beta = beta;
+  g.out = g.direct ? dw[0] : reinterpret_cast<float*>(workspace);
+  g_cvl_conv_last_kernel = CVL_CK_WG_H;
+  hipLaunchKernelGGL(conv_wgrad_h_kernel, dim3(g.ci_tiles * g.co_tiles * pl.nsplit), dim3(NT), 0, s, g);
+  int st = cvl_launch_status();
+  if (st || g.direct) return st;
+  const long n4 = 9L * d->Cin * d->n_store / 4;
+  long blocks = (n4 + 255) / 256;
+  blocks = blocks > 4096 ? 4096 : blocks;
+  hipLaunchKernelGGL(wgrad_h_reduce, dim3((int)blocks), dim3(256), 0, s, (const float*)workspace, dw[0], n4, pl.nsplit,
+                     beta);
+  return cvl_launch_status();
+}

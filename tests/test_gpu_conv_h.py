@@ -200,3 +200,41 @@ def test_h_dgrad_fused_bn_backward_sums():
     gm = torch.where(a > 0, dx_p.float(), torch.zeros_like(a)).double()
     ref = torch.stack([gm.sum((1, 2)), (gm * xh.double()).sum((1, 2))], -1)
     torch.testing.assert_close(sums, ref, rtol=1e-5, atol=1e-6 * float(ref.abs().max()))
+
+
+WG_CASES = [  # (B, H, W, Cin, Cout): the 3x3 units' weight gradients (conv2_x..conv5_x), FPN c4/c5
+    (2, 128, 128, 64, 64),
+    (2, 64, 64, 128, 128),
+    (4, 32, 32, 256, 256),
+    (16, 16, 16, 512, 512),
+    (1, 16, 16, 64, 128),
+]
+
+
+@pytest.mark.parametrize("case", WG_CASES)
+def test_h_wgrad(case):
+    """conv_wgrad_h_kernel (halo-staged 3x3 weight gradient, split over row chunks with a
+    fixed-order slab reduction, or direct with beta) vs float64 on the same bf16 operands."""
+    from cvlite import ops_nn as nn
+    B, H, W, Cin, Cout = case
+    g = torch.Generator().manual_seed(H * Cin + Cout + B)
+    x = rnd(B, H, W, Cin, gen=g)
+    w = rnd(3, 3, Cin, Cout, scale=(9 * Cin) ** -0.5, gen=g).requires_grad_(True)
+    y = conv3(x, w)
+    dy = rnd(*y.shape, gen=g)
+    y.backward(dy)
+    wf, _, npad, _ = packs(w.detach())
+    ld = Cout + 8                                     # dY rows wider than Cout, at a channel offset
+    dyg = torch.zeros((B, H, W, ld), dtype=BF, device="cuda")
+    dyg[..., 8:8 + Cout] = dy.to(BF).cuda()
+    d = nn.make_desc(nn.FWD, B, Cin, 3, 3, 1, 1, 1, npad, Cout, ld, [nn.seg(H, W, H, W, wf)], dst_coff=8)
+    old = torch.randn((3, 3, Cin, Cout), generator=g).cuda()
+    dw = old.clone()
+    nn.conv_wgrad(d, x.to(BF).cuda(), dyg, dw, beta=1.0)
+    assert "conv_wgrad_h_kernel" in last_kernel(), last_kernel()
+    ref = w.grad + old.double().cpu()
+    scale = float(w.grad.abs().max())
+    torch.testing.assert_close(dw.double().cpu(), ref, rtol=1e-4, atol=2e-5 * scale)
+    dw0 = torch.zeros((3, 3, Cin, Cout), device="cuda")
+    nn.conv_wgrad(d, x.to(BF).cuda(), dyg, dw0)
+    torch.testing.assert_close(dw0.double().cpu(), w.grad, rtol=1e-4, atol=2e-5 * scale)
