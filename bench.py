@@ -111,6 +111,70 @@ def measure_tower_conv(net, B, H, W, iters=20):
     return ms, flops, kname
 
 
+def measure_backbone_3x3(net, B, H, W, iters=20):
+    """roofline.backbone_3x3: the 16 ResNet-50 3x3 convs (conv2_x..conv5_x units' `_2_conv`, the
+    shapes north_star names) -- forward (with the BN statistics the step forms), data gradient
+    (with the conv1 unit's fused BN-backward first pass, as the step runs it) and weight gradient,
+    each distinct launch replayed alone with HIP events on its stream on random N(0, 1) operands
+    (the step's own launch descriptors and packed weights); returns the FLOP-weighted fraction
+    of the bf16 dense peak over all 48 launches and the per-shape rows."""
+    from cvlite import _lib
+    L = _lib.load()
+    dev = net.device
+    bb = net.backbone
+    rows, tot_f, tot_t = [], 0.0, 0.0
+    h, w = -(-H // 4), -(-W // 4)                 # after the stem's stride 2 and the max-pool
+    g = torch.Generator(device="cpu").manual_seed(3)
+    s = torch.cuda.current_stream()
+
+    def timed(fn):
+        for _ in range(3):
+            fn()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(s)
+        for _ in range(iters):
+            fn()
+        e1.record(s)
+        e1.synchronize()
+        return e0.elapsed_time(e1) / iters * 1e-3, L.cvl_conv_kernel_name(L.cvl_conv_igemm_last_kernel()).decode()
+    for si, stage in enumerate(bb.stages):
+        if si > 0:
+            h, w = -(-h // 2), -(-w // 2)
+        conv = stage[-1].c2.conv                  # every block of a stage has the same 3x3 shape
+        bn = stage[-1].c1.bn
+        C = conv.cin
+        x = torch.randn((B, h, w, C), generator=g).to(torch.bfloat16).to(dev)
+        dy = torch.randn((B, h, w, conv.cout_pad), generator=g).to(torch.bfloat16).to(dev)
+        dy[..., conv.cout:] = 0
+        y = torch.empty((B, h, w, conv.cout), dtype=torch.bfloat16, device=dev)
+        st = torch.zeros((B, conv.cout, 2), dtype=torch.float64, device=dev)
+        dx = torch.empty((B, h, w, C), dtype=torch.bfloat16, device=dev)
+        mr = torch.empty((B, C, 2), dtype=torch.float32, device=dev)
+        mr[..., 0] = 0.0
+        mr[..., 1] = 1.0
+        sums = torch.zeros((B, C, 2), dtype=torch.float64, device=dev)
+        dwb = torch.zeros_like(conv.dw)
+        fd = conv.fwd_desc(B, [nn.seg(h, w, h, w, conv.wf, conv.bias_arg())], ld_dst=conv.cout)
+        dd = conv.dgrad_desc(B, [nn.seg(h, w, h, w, conv.wd)], ld_dst=C)
+        wd = conv.fwd_desc(B, [nn.seg(h, w, h, w, conv.wf, None)], ld_dst=conv.cout_pad)
+        flops = 2.0 * B * h * w * 9 * C * conv.cout
+        for kind, fn in (("fwd", lambda: nn.conv_igemm(fd, x, y, st)),
+                         ("dgrad", lambda: nn.conv_igemm_dgrad_bnsum(dd, dy, dx, x, mr, bn.gamma, bn.beta, sums)),
+                         ("wgrad", lambda: nn.conv_wgrad(wd, x, dy, dwb))):
+            t, kname = timed(fn)
+            n = len(stage)
+            rows.append({"shape": "%s 3x3 %d->%d @ %dx%d" % (kind, C, conv.cout, h, w), "count": n,
+                         "us": round(t * 1e6, 2), "frac": round(flops / t / 1e12 / PEAK_BF16_TFLOPS, 4),
+                         "kernel": kname.split(" (")[0]})
+            tot_f += n * flops
+            tot_t += n * t
+    return {"frac": round(tot_f / tot_t / 1e12 / PEAK_BF16_TFLOPS, 4), "achieved": round(tot_f / tot_t / 1e12, 2),
+            "unit": "TFLOP/s", "peak": PEAK_BF16_TFLOPS, "launches": 48, "ms_per_step": round(tot_t * 1e3, 4),
+            "gflop_per_step": round(tot_f / 1e9, 2),
+            "timing": "each distinct launch replayed alone (20x, HIP events on its stream) after the timed steps; "
+                      "counts from the ResNet-50 stage depths (3/4/6/3)", "per_shape": rows}
+
+
 PMC_FILE = "profiles/r02k_pmc_tower_conv.json"
 
 
@@ -363,6 +427,7 @@ def main():
     in_s, in_n = nn.probe_seconds(net.tower_probe)
     net.tower_probe = None
     k_ms, k_flops, k_name = measure_tower_conv(net, B, H, W)
+    bb3 = measure_backbone_3x3(net, B, H, W)
     in_ms = in_s * 1e3 if in_s else k_ms
     achieved = k_flops / (in_ms * 1e-3) / 1e12
     out = {
@@ -396,7 +461,8 @@ def main():
                                "inter-kernel gaps)" % in_n,
                      "burst_ms_per_launch": round(k_ms, 4),
                      "burst_frac": round(k_flops / (k_ms * 1e-3) / 1e12 / PEAK_BF16_TFLOPS, 4),
-                     "burst_note": "the same launch repeated back to back on its own (20x, HIP events)"},
+                     "burst_note": "the same launch repeated back to back on its own (20x, HIP events)",
+                     "backbone_3x3": bb3},
         "dist": dist_info(world),
         "model_flops_per_image": fl_img,
         "step_mfma_frac": round(img_s / world * fl_img / 1e12 / PEAK_BF16_TFLOPS, 4),
