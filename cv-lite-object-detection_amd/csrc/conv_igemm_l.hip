@@ -231,9 +231,19 @@ int cvl_conv_igemm_l(const cvl_conv_desc* d, int dst_up, int dst_w, const void* 
   // CenterNet +0.4 % at K < 512)
   const int w256_min_k = cvl_env_int("CVL_CONV_W256_MIN_K", 512);
   if (use_bn == 256 && a.K < w256_min_k) use_bn = 128;
-  // 3x3 / stride 1 launches that do not take the 256 x 256 tiles: the halo-staged 256 x 64 kernel
-  // (conv_igemm_h.hip), whose A traffic is one halo per channel block instead of nine im2col tiles
-  if (use_bn != 256 && (!bsum || ((a.seg[0].Hr * a.seg[0].Wr) % BM == 0 && !bn_stats))) {
+  // a launch that would leave CUs idle with 128-wide tiles takes 64-wide ones (twice the tiles),
+  // also when that lifts it over min_tiles (from the split-K 128-row kernel): FCOS A/B 970 -> 983
+  // img/s at 256 for the 128-tile conv4_x launches, -> 988 with the conv5_x ones (512: 966, 1024: 941)
+  const int fill = cvl_env_int("CVL_CONV_L64_FILL", 256);
+  const bool fill_pre = !cvl_env_flag("CVL_CONV_L64_NO_FILL_PRE");
+  const bool to64 = fill && use_bn == 128 && (long)a.m_tiles * (a.Npad / 128) < fill && a.Npad % 64 == 0 &&
+                    !(bsum && cvl_env_flag("CVL_BSUM_NO_FILL"));
+  // 3x3 / stride 1 launches that would run 64-wide tiles: the halo-staged 256 x 64 kernel
+  // (conv_igemm_h.hip), whose A traffic is one halo per channel block instead of nine im2col tiles.
+  // Not where the 256 x 128 tiles fill the chip: there the L kernel reads each A tile once for 128
+  // columns (128 -> 128 @ 64^2, bs 16: L 33 / 47 us fwd / dgrad vs H64 41 / 52 us)
+  const bool h_width = use_bn == 64 || to64 || !l_cin || cvl_env_flag("CVL_CONV_H_ANY_N");
+  if (h_width && use_bn != 256 && (!bsum || ((a.seg[0].Hr * a.seg[0].Wr) % BM == 0 && !bn_stats))) {
     ConvArgs ah = a;
     ah.dst_up = dst_up;
     ah.dst_w = dst_w;
@@ -253,13 +263,6 @@ int cvl_conv_igemm_l(const cvl_conv_desc* d, int dst_up, int dst_w, const void* 
     }
   }
   if (!l_cin) return -1;
-  // a launch that would leave CUs idle with 128-wide tiles takes 64-wide ones (twice the tiles),
-  // also when that lifts it over min_tiles (from the split-K 128-row kernel): FCOS A/B 970 -> 983
-  // img/s at 256 for the 128-tile conv4_x launches, -> 988 with the conv5_x ones (512: 966, 1024: 941)
-  const int fill = cvl_env_int("CVL_CONV_L64_FILL", 256);
-  const bool fill_pre = !cvl_env_flag("CVL_CONV_L64_NO_FILL_PRE");
-  const bool to64 = fill && use_bn == 128 && (long)a.m_tiles * (a.Npad / 128) < fill && a.Npad % 64 == 0 &&
-                    !(bsum && cvl_env_flag("CVL_BSUM_NO_FILL"));
   if (fill_pre && to64) use_bn = 64;
   if ((long)a.m_tiles * (a.Npad / use_bn) < min_tiles) return -1;
   if (to64) use_bn = 64;

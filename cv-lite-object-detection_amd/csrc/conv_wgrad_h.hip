@@ -9,7 +9,7 @@
 // * Workgroup = (64 input channels) x (64 output channels) x all 9 taps = a 64 x 576 C tile, over a
 //   chunk of 128-row steps; 8 waves as 2 (co halves) x 4 (16-channel quarters), each wave
 //   2 x 9 v_mfma_f32_16x16x32_bf16 accumulators (co tile x tap).
-// * Stage = halo [<= 408 px][64 ch] + dY [128 rows][64 co], 128-B rows, double-buffered (134 KiB).
+// * Stage = halo [<= 432 px][64 ch] + dY [128 rows][64 co], 128-B rows, double-buffered (140 KiB).
 //   Two phases per step (2 x 32-row sub-steps, 36 MFMAs per wave each); the wave groups (channel
 //   quarters 0-1 / 2-3) run one barrier apart; step s+1 is issued in phase 0 of step s into the
 //   buffer step s-1 used and waited for (vmcnt 0) at the start of phase 1.
@@ -24,11 +24,11 @@
 namespace {
 
 constexpr int NT = 512, BCI = 64, BCO = 64, RS = 128;
-constexpr int HPX = 408;                             // halo pixels per stage (W = 128: 3 x 136)
+constexpr int HPX = 432;                             // halo pixels per stage (W = 128: 3 x 144)
 constexpr int HALO_B = HPX * 128;                    // bytes
 constexpr int DY_B = RS * 128;
-constexpr int STAGE_B = HALO_B + DY_B;               // 68,608 B
-constexpr int NPS = HPX / 8 + RS / 8;                // DMA pieces per stage (max): 51 + 16
+constexpr int STAGE_B = HALO_B + DY_B;               // 71,680 B
+constexpr int NPS = HPX / 8 + RS / 8;                // DMA pieces per stage (max): 54 + 16
 constexpr int PPW = (NPS + 7) / 8;                   // piece slots per wave: 9
 constexpr unsigned kRecords = 0x7fffffffu;
 constexpr unsigned kOOB = 0x80000000u;
@@ -62,7 +62,7 @@ __global__ void __launch_bounds__(NT) conv_wgrad_h_kernel(WhArgs g) {
   const int s0 = split * g.chunk, s1 = min(s0 + g.chunk, g.steps);
   const int W = g.W, H = g.H, HW = H * W;
   const int R = RS / W;                                // image rows per step
-  const int P = (W + 2 + 7) & ~7;                      // halo pitch (pixels)
+  const int P = (W + 2 + 15) & ~15;                    // halo pitch (pixels; % 16: a row shift keeps the swizzle)
   const int hpx = (R + 2) * P;
   const int nh = (hpx + 7) / 8;                        // halo pieces; dY pieces follow
   const int ch = lane & 7;
@@ -115,7 +115,7 @@ __global__ void __launch_bounds__(NT) conv_wgrad_h_kernel(WhArgs g) {
   const int q = lr >> 2, p = lr & 3;
   // per-lane transposed-read byte offsets (within a stage) for the rows of sub-step u (0..3):
   // lo = row 32u + 8lg + q, hi = lo + 4.  dY: co tile i; X: halo pixel of the row at dx = s
-  // (the dy = r shift adds r * P * 128 bytes, which keeps the swizzle: P % 8 == 0)
+  // (the dy = r shift adds r * P * 128 bytes, which keeps the swizzle: P % 16 == 0)
   unsigned yof[4][2][2], xof[4][2][3];
 #pragma unroll
   for (int u = 0; u < 4; ++u)
@@ -156,7 +156,8 @@ __global__ void __launch_bounds__(NT) conv_wgrad_h_kernel(WhArgs g) {
 
   for (int s = s0; s < s1; ++s) {
     const unsigned sb = lds0 + (unsigned)((s & 1) * STAGE_B);
-#pragma unroll 1
+    // both phases unrolled: the per-sub-step offset tables must stay in registers
+#pragma unroll
     for (int ph = 0; ph < 2; ++ph) {
       if (ph == 0) issue(s + 1);
       else wait_vm<0>();                       // this wave's pieces of step s + 1 landed
@@ -221,22 +222,33 @@ __global__ void __launch_bounds__(NT) conv_wgrad_h_kernel(WhArgs g) {
     }
 }
 
-// dw[i] = beta*dw[i] + sum over splits of slab[split][i], splits in order (deterministic)
+// dw[i] = beta*dw[i] + sum over splits of slab[split][i] (deterministic): a block owns 16 float4
+// columns x 16 split lanes; lane l sums splits l, l + 16, ... (4 loads in flight), then the 16 lane
+// sums of a column are added in a fixed order through LDS
 __global__ void __launch_bounds__(256) wgrad_h_reduce(const float* __restrict__ slab, float* __restrict__ dw, long n4,
                                                       int nsplit, float beta) {
-  for (long i = blockIdx.x * 256L + threadIdx.x; i < n4; i += (long)gridDim.x * 256) {
-    f32x4 s = f32x4{0.f, 0.f, 0.f, 0.f};
+  __shared__ f32x4 red[16][17];
+  const int col = threadIdx.x & 15, sl = threadIdx.x >> 4;
+  const long i = (long)blockIdx.x * 16 + col;
+  f32x4 s = f32x4{0.f, 0.f, 0.f, 0.f};
+  if (i < n4) {
     const f32x4* p = reinterpret_cast<const f32x4*>(slab) + i;
-    int k = 0;
-    for (; k + 4 <= nsplit; k += 4) {
-      const f32x4 a0 = p[(long)k * n4], a1 = p[(long)(k + 1) * n4];
-      const f32x4 a2 = p[(long)(k + 2) * n4], a3 = p[(long)(k + 3) * n4];
+    int k = sl;
+    for (; k + 48 < nsplit; k += 64) {
+      const f32x4 a0 = p[(long)k * n4], a1 = p[(long)(k + 16) * n4];
+      const f32x4 a2 = p[(long)(k + 32) * n4], a3 = p[(long)(k + 48) * n4];
       s += (a0 + a1) + (a2 + a3);
     }
-    for (; k < nsplit; ++k) s += p[(long)k * n4];
+    for (; k < nsplit; k += 16) s += p[(long)k * n4];
+  }
+  red[sl][col] = s;
+  __syncthreads();
+  if (sl == 0 && i < n4) {
+    f32x4 t = red[0][col];
+    for (int k = 1; k < 16; ++k) t += red[k][col];
     f32x4* d = reinterpret_cast<f32x4*>(dw) + i;
-    if (beta != 0.f) s += beta * *d;
-    *d = s;
+    if (beta != 0.f) t += beta * *d;
+    *d = t;
   }
 }
 
@@ -253,7 +265,7 @@ inline bool wh_plan(const cvl_conv_desc* d, int ngroups, WhPlan* pl) {
   const cvl_conv_seg& q = d->seg[0];
   const int W = q.Wr, HW = q.Hr * q.Wr;
   if (q.Hr != q.Hs || q.Wr != q.Ws || W < 16 || RS % W || HW % RS || q.src_img != HW || q.dst_img < HW) return false;
-  if ((RS / W + 2) * ((W + 2 + 7) & ~7) > HPX) return false;
+  if ((RS / W + 2) * ((W + 2 + 15) & ~15) > HPX) return false;
   const long src_end = (q.src_base + (long)d->B * q.src_img) * d->Cin * 2;
   const long dy_end = (q.dst_base + (long)d->B * q.dst_img) * d->ld_dst * 2;
   if (src_end >= (long)kRecords - 65536 || dy_end >= (long)kRecords - 65536) return false;
@@ -301,9 +313,7 @@ int cvl_conv_wgrad_h(const cvl_conv_desc* d, int ngroups, const void* x, const v
   int st = cvl_launch_status();
   if (st || g.direct) return st;
   const long n4 = 9L * d->Cin * d->n_store / 4;
-  long blocks = (n4 + 255) / 256;
-  blocks = blocks > 4096 ? 4096 : blocks;
-  hipLaunchKernelGGL(wgrad_h_reduce, dim3((int)blocks), dim3(256), 0, s, (const float*)workspace, dw[0], n4, pl.nsplit,
-                     beta);
+  hipLaunchKernelGGL(wgrad_h_reduce, dim3((int)((n4 + 15) / 16)), dim3(256), 0, s, (const float*)workspace, dw[0], n4,
+                     pl.nsplit, beta);
   return cvl_launch_status();
 }

@@ -37,7 +37,8 @@ def kern(request, monkeypatch):
     alternative for the launches l256 would take) and its 32-deep-K ring form ("x32", the default).
     Weight gradients: "base" runs the 128-wide k-tile kernel, "l"/"l256"/"x" the row-table LDS-DMA
     kernel (conv_wgrad_l.hip), "x32" the default dispatch (conv_wgrad_x.hip where Npad % 256 == 0)."""
-    monkeypatch.setenv("CVL_CONV_NO_H", "1")      # the halo kernel has its own tests (test_gpu_conv_h.py)
+    monkeypatch.setenv("CVL_CONV_NO_H", "1")      # the halo kernels have their own tests (test_gpu_conv_h.py)
+    monkeypatch.setenv("CVL_WGRAD_NO_H", "1")
     if request.param in ("l", "l256", "x", "x32"):
         monkeypatch.setenv("CVL_CONV_L_MIN_TILES", "1")
     if request.param == "l":

@@ -161,10 +161,11 @@ def test_h_split_k_small_grid():
         outs.append(out.double().cpu())
         sts.append(st.cpu())
     ref = conv3(x, w, b).clamp(min=0)
-    for o in outs:
+    for o, st in zip(outs, sts):
         torch.testing.assert_close(o, ref, rtol=1e-2, atol=1e-2)
+        # each path's statistics are those of its own output (to the bf16 rounding of the stored values)
+        torch.testing.assert_close(st, torch.stack([o.sum((1, 2)), (o * o).sum((1, 2))], -1), rtol=1e-3, atol=1e-2)
     torch.testing.assert_close(outs[0], outs[1], rtol=1e-2, atol=1e-2)
-    torch.testing.assert_close(sts[0], sts[1], rtol=1e-5, atol=1e-2)
 
 
 def test_h_dgrad_fused_bn_backward_sums():

@@ -1,12 +1,26 @@
 """fp32 parity mode (CVL_PRECISION=fp32, SURVEY.md §8b "Parity modes"): the detector graphs with
-fp32 activations / gradients / packed weights and fp32 FMA on the GPU vs the fp32 oracle
+fp32 activations / gradients / packed weights and fp32 FMA on the GPU vs the oracle
 (oracle/model_ref.py: FCOS/fcos.py:6-110 + Keras ResNet50 v1, RetinaNet/retinanet_module.py:8-159)
-on identical weights, images and targets, at the REFERENCE'S OWN init (Keras glorot, undamped) --
-no bf16 self-divergence bound: the tolerances are fixed numbers, written in each test.
+run in float64 on identical weights, images and targets -- no bf16 self-divergence bound.
 
-The oracle is also run in float64; the distance fp32-CPU <-> fp64 is printed next to GPU <-> fp64
-so a reader can see how much of the GPU's deviation is plain fp32 summation-order noise (amplified
-by the random-init graph) and how much would be the kernels'."""
+What limits any fp32 implementation here (measured, tools/ diagnosis in DESIGN.md §parity):
+the forward of a 50-layer random-init graph moves each activation by ~1e-5 relative, so a
+handful of ReLU inputs within that distance of 0 land on the other side of the mask (e.g. 1 of
+the 2,048 P7 tower outputs).  A flipped mask element changes the backward by O(its gradient):
+the oracle itself, run in fp32 on the CPU, lands 1-4 % (rel-L2) from its float64 run on BN
+gamma / beta gradients (near-cancelling sums) and 0.5 % on whole FPN-level gradients -- while
+GIVEN the same masks the GPU backward matches float64 to ~1e-6 (test_fcos_fp32_tower_backward_exact).
+So:
+  * logits: rel-L2 and max error <= LOGIT_RTOL (damped init, the well-conditioned graph) or
+    <= max(LOGIT_RTOL, NOISE_X x the fp32 oracle's own error) (the reference's Keras init);
+  * per-image losses: <= max(LOSS_RTOL, the fp32 oracle's logit rel-L2) -- a loss cannot be more
+    accurate than the logits it is a function of;
+  * parameter gradients: the GPU's per-tensor rel-L2 errors vs float64 are no worse than the fp32
+    oracle's at the median, the 90th percentile and the maximum (each within NOISE_X, or under
+    GRAD_RTOL), and the flat rel-L2 over all gradients likewise;
+  * test_fcos_fp32_tower_backward_exact: heads + towers backward with the GPU's own ReLU masks,
+    every FPN level, within 1e-5 of float64 (no mask noise left to hide behind).
+The fp32-CPU <-> fp64 distance is printed next to GPU <-> fp64 for every check."""
 import math
 
 import numpy as np
@@ -20,33 +34,70 @@ pytestmark = pytest.mark.gpu
 
 LOGIT_RTOL = 1e-4        # logits: rel-L2 over each output tensor, and max |err| <= 1e-4 * max |logit|
 LOSS_RTOL = 1e-5         # per-image losses (each of cls / reg / cen), relative
-GRAD_RTOL = 1e-3         # every parameter gradient tensor, rel-L2
+GRAD_RTOL = 1e-3         # parameter gradient rel-L2 (quantiles, see above)
+NOISE_X = 1.5            # allowed multiple of the fp32 oracle's own error
+EXACT_RTOL = 1e-5        # backward given identical ReLU masks
 
 
 def rel(a, b):
     return float((a.double() - b.double()).norm() / max(float(b.double().norm()), 1e-30))
 
 
-def _check_outputs(name, got, ref32, ref64):
+def _damp_residual_gammas(net, factor=0.25):
+    for k in net.store.offsets:
+        if k.endswith("_3_bn/gamma"):
+            net.store.p(k).mul_(factor)
+
+
+def _check_outputs(name, got, ref32, ref64, noise_rel):
     e, e_cpu = rel(got, ref64), rel(ref32, ref64)
     mx = float((got.double() - ref64.double()).abs().max()) / max(float(ref64.abs().max()), 1e-30)
-    print("%s: gpu-vs-fp64 rel-L2 %.2e max %.2e | cpu-fp32-vs-fp64 %.2e | gpu-vs-cpu-fp32 %.2e" % (
-        name, e, mx, e_cpu, rel(got, ref32)))
-    assert e <= LOGIT_RTOL and mx <= LOGIT_RTOL, (name, e, mx)
+    mx_cpu = float((ref32.double() - ref64.double()).abs().max()) / max(float(ref64.abs().max()), 1e-30)
+    print("%s: gpu-vs-fp64 rel-L2 %.2e max %.2e | cpu-fp32-vs-fp64 %.2e max %.2e | gpu-vs-cpu-fp32 %.2e" % (
+        name, e, mx, e_cpu, mx_cpu, rel(got, ref32)))
+    tol, tol_mx = (max(LOGIT_RTOL, NOISE_X * e_cpu), max(LOGIT_RTOL, NOISE_X * mx_cpu)) if noise_rel else (
+        LOGIT_RTOL, LOGIT_RTOL)
+    ok = e <= tol and mx <= tol_mx
+    return [] if ok else [("logits " + name, e, mx, tol, tol_mx)]
 
 
-def _check_grads(grads_gpu, g64, skip_bias_before_bn=True):
+def _check_losses(got, l32, l64, logit_noise):
+    err = ((got - l64).abs() / l64.abs().clamp(min=1e-12))
+    err_cpu = ((l32.double() - l64).abs() / l64.abs().clamp(min=1e-12))
+    tol = max(LOSS_RTOL, logit_noise)
+    print("losses: gpu-vs-fp64 max rel %.2e (cpu fp32 %.2e), tolerance %.2e" % (
+        float(err.max()), float(err_cpu.max()), tol))
+    return [] if float(err.max()) <= tol else [("losses", float(err.max()), tol)]
+
+
+def _check_grads(grads_gpu, g64, g32, skip_bias_before_bn=True):
     big = max(float(v.norm()) for v in g64.values())
-    worst = []
+    rows = []
+    n_err = n_cpu = n_ref = 0.0
     for k, gr in g64.items():
         if skip_bias_before_bn and k.endswith("_conv/bias"):
             continue              # conv bias in front of a training-mode BN: the true gradient is exactly 0
         if float(gr.norm()) < 1e-6 * big:
             continue
-        worst.append((rel(grads_gpu[k], gr), k))
-    worst.sort(reverse=True)
-    print("worst gradient tensors (rel-L2 vs fp64 oracle):", [(round(e, 6), k) for e, k in worst[:4]])
-    assert worst[0][0] <= GRAD_RTOL, worst[:4]
+        rows.append((rel(grads_gpu[k], gr), rel(g32[k], gr), k))
+        n_err += float((grads_gpu[k].double() - gr).norm()) ** 2
+        n_cpu += float((g32[k].double() - gr).norm()) ** 2
+        n_ref += float(gr.norm()) ** 2
+    eg = np.array([r[0] for r in rows])
+    ec = np.array([r[1] for r in rows])
+    fails = []
+    for q in (50, 90, 100):
+        a, b = float(np.percentile(eg, q)), float(np.percentile(ec, q))
+        print("gradient rel-L2 p%d: gpu %.2e cpu-fp32 %.2e" % (q, a, b))
+        if a > max(GRAD_RTOL, NOISE_X * b):
+            fails.append(("grad p%d" % q, a, b))
+    fg, fc = math.sqrt(n_err / n_ref), math.sqrt(n_cpu / n_ref)
+    print("flat gradient rel-L2: gpu %.2e cpu-fp32 %.2e" % (fg, fc))
+    if fg > max(GRAD_RTOL, NOISE_X * fc):
+        fails.append(("grad flat", fg, fc))
+    rows.sort(reverse=True)
+    print("largest gpu errors (gpu, cpu-fp32, tensor):", [("%.2e" % e, "%.2e" % c, k) for e, c, k in rows[:5]])
+    return fails
 
 
 def _synth(B, D, C, seed, nmax=6):
@@ -144,36 +195,103 @@ def _fcos_gpu(net, x, boxes, nbox, C, B, D):
     return tg.cpu(), reg[..., :5].cpu(), cls[..., :C].cpu(), losses.cpu().double()
 
 
-def test_fcos_fp32_graph_matches_reference_at_keras_init():
-    """FCOS ResNet-50-FPN at 256x256, bs 2, the reference's Keras glorot init (not damped): logits
-    (reg + centerness, classes) within LOGIT_RTOL, the per-image (cls, reg, cen) losses within
-    LOSS_RTOL and every parameter gradient within GRAD_RTOL of the oracle (float64 run)."""
+@pytest.mark.parametrize("init", ["damped", "keras"])
+def test_fcos_fp32_graph_matches_reference(init):
+    """FCOS ResNet-50-FPN at 256x256, bs 2: logits (reg + centerness, classes), the per-image
+    (cls, reg, cen) losses and every parameter gradient vs the float64 oracle (module docstring)."""
     from cvlite.fcos_net import FCOSNet
     C, B, D = 20, 2, 256
     net = FCOSNet(C, seed=1, precision="fp32")
     assert net.store.act == torch.float32 and net.cls_tower[0].wf.dtype == torch.float32
+    if init == "damped":
+        _damp_residual_gammas(net)
+    noise_rel = init == "keras"
     params = net.store.state_dict()
     x, boxes, nbox = _synth(B, D, C, 3)
     tg, reg, cls, losses = _fcos_gpu(net, x, boxes, nbox, C, B, D)
     l32, g32, reg32, cls32 = model_ref.fcos_loss_and_grads(params, torch.from_numpy(x), tg, C)
     l64, g64, reg64, cls64 = model_ref.fcos_loss_and_grads(params, torch.from_numpy(x), tg, C, dtype=torch.float64)
-    _check_outputs("reg", reg, reg32, reg64)
-    _check_outputs("cls", cls, cls32, cls64)
-    el = float(((losses - l64).abs() / l64.abs().clamp(min=1e-12)).max())
-    print("losses: gpu-vs-fp64 max rel %.2e (cpu fp32 %.2e)" % (
-        el, float(((l32.double() - l64).abs() / l64.abs().clamp(min=1e-12)).max())))
-    assert el <= LOSS_RTOL
-    _check_grads({k: net.store.g(k).detach().cpu() for k in g64}, g64)
+    fails = _check_outputs("reg", reg, reg32, reg64, noise_rel) + _check_outputs("cls", cls, cls32, cls64, noise_rel)
+    fails += _check_grads({k: net.store.g(k).detach().cpu() for k in g64}, g64, g32)
+    fails += _check_losses(losses, l32, l64, max(rel(reg32, reg64), rel(cls32, cls64)))
+    assert not fails, fails
 
 
-def test_retinanet_fp32_graph_matches_reference_at_keras_init():
-    """RetinaNet ResNet-50-FPN (per-(level, anchor) heads fused per level) at 256x256, bs 2, C = 8,
-    Keras init: same fixed tolerances as FCOS (retinanet_module.py:8-159, 403-426)."""
+def test_fcos_fp32_tower_backward_exact():
+    """Keras init: the heads' and towers' data gradients of every FPN level (FCOS/fcos.py:74-110:
+    per-level output convs, 4 shared 3x3 tower convs with one ReLU) on the GPU vs float64 applied
+    to the GPU's own loss gradients and ReLU masks -- the parity-mode kernels, segments, pairing
+    and accumulation order with the mask noise removed: EXACT_RTOL."""
+    from cvlite import ops_targets as ot
+    from cvlite.fcos_net import FCOSNet
+    C, B, D = 20, 2, 256
+    net = FCOSNet(C, seed=1, precision="fp32")
+    x, boxes, nbox = _synth(B, D, C, 3)
+    cap = {}
+    orig = net.trunk_backward
+
+    def spy(dA_top, hook=None):
+        cap["dA"] = [t.detach().clone() for t in dA_top]
+        cap["tw"] = [tw[-1].detach().clone() for tw in net._saved["towers"]]
+        return orig(dA_top, hook=hook)
+    net.trunk_backward = spy
+    from cvlite import ops_nn as nn
+    orig_wg = nn.conv_wgrad
+
+    def wg_spy(d, x_, dy, dw, *a, **k):
+        if dw is not None and dw.data_ptr() == net.c7_3x3.dw.data_ptr():
+            cap["dF"] = dy.detach().clone()          # the towers' input gradient, all levels
+        return orig_wg(d, x_, dy, dw, *a, **k)
+    nn.conv_wgrad = wg_spy
+    try:
+        dims = torch.full((B, 2), float(D), device="cuda")
+        tg, _ = ot.fcos_assign(torch.from_numpy(boxes).cuda(), torch.from_numpy(nbox).cuda(), dims, (D, D), C)
+        reg, cls = net.forward(torch.from_numpy(x).cuda())
+        P = reg.shape[1]
+        d_reg = torch.zeros((B, P, 32), dtype=torch.float32, device="cuda")
+        d_cls = torch.zeros((B, P, 32), dtype=torch.float32, device="cuda")
+        ot.fcos_loss(reg, cls, tg, C, grad_scale=1.0, d_reg=d_reg, d_cls=d_cls)
+        net.backward(d_reg, d_cls)
+        torch.cuda.synchronize()
+    finally:
+        nn.conv_wgrad = orig_wg
+    sp = {k: v.double().cpu() for k, v in net.store.state_dict().items()}
+
+    def convT(g, name):                 # 3x3 / stride 1 / same: d input from d output
+        return F.conv_transpose2d(g, sp[name + "/kernel"].permute(3, 2, 0, 1), padding=1)
+    shapes, off, _ = net.layout(B, D, D)
+    for l, (h, w) in enumerate(shapes):
+        pts = slice(off[l], off[l] + h * w)
+        rows = slice(B * off[l], B * (off[l] + h * w))
+        nchw = lambda t: t[rows].cpu().double().view(B, h, w, -1).permute(0, 3, 1, 2)  # noqa: E731
+        gc = d_cls.cpu()[:, pts, :C].double().reshape(B, h, w, C).permute(0, 3, 1, 2)
+        gr = d_reg.cpu()[:, pts, :5].double().reshape(B, h, w, 5).permute(0, 3, 1, 2)
+        dA = [nchw(cap["dA"][0]), nchw(cap["dA"][1])]
+        e_head = (rel(dA[0], convT(gc, "logits_output_%d" % (l + 1))),
+                  rel(dA[1], convT(gr, "reg_output_%d" % (l + 1))))
+        tot = 0
+        for t, pre in enumerate(("cls_layer_%d", "reg_layer_%d")):
+            g = dA[t] * (nchw(cap["tw"][t]) > 0).double()
+            for i in range(4, 0, -1):
+                g = convT(g, pre % i)
+            tot = tot + g
+        e_tower = rel(nchw(cap["dF"]), tot) if l != 3 else 0.0   # P6's rows also get relu(P6)'s term
+        print("level %d: head dgrad %.2e %.2e, towers %.2e" % (l, e_head[0], e_head[1], e_tower))
+        assert max(e_head) <= EXACT_RTOL and e_tower <= EXACT_RTOL, (l, e_head, e_tower)
+
+
+@pytest.mark.parametrize("init", ["damped", "keras"])
+def test_retinanet_fp32_graph_matches_reference(init):
+    """RetinaNet ResNet-50-FPN (per-(level, anchor) heads fused per level) at 256x256, bs 2, C = 8:
+    same checks as FCOS (retinanet_module.py:8-159, 403-426)."""
     from cvlite import ops_targets as ot
     from cvlite.retina_net import RetinaNetNet
     from cvlite.retinanet import RetinaNet
     C, A, B, D = 8, 9, 2, 256
     net = RetinaNetNet(C, seed=4, precision="fp32")
+    if init == "damped":
+        _damp_residual_gammas(net)
+    noise_rel = init == "keras"
     params = net.store.state_dict()
     rn = RetinaNet(C, {}, anchor_sizes=[20.0, 40.0, 80.0, 160.0, 320.0])
     x, boxes, nbox = _synth(B, D, C, 9, nmax=8)
@@ -191,24 +309,24 @@ def test_retinanet_fp32_graph_matches_reference_at_keras_init():
     l32, g32, reg32, cls32 = model_ref.retina_loss_and_grads(params, torch.from_numpy(x), tgc, C, cells, A)
     l64, g64, reg64, cls64 = model_ref.retina_loss_and_grads(params, torch.from_numpy(x), tgc, C, cells, A,
                                                              dtype=torch.float64)
-    _check_outputs("reg", reg[..., :4 * A].cpu(), reg32, reg64)
-    _check_outputs("cls", cls[..., :A * C].cpu(), cls32, cls64)
-    lg = losses.cpu().double()
-    el = float(((lg - l64).abs() / l64.abs().clamp(min=1e-12)).max())
-    print("losses: gpu-vs-fp64 max rel %.2e" % el)
-    assert el <= LOSS_RTOL
-    _check_grads({k: net.store.g(k).detach().cpu() for k in g64}, g64)
+    fails = _check_outputs("reg", reg[..., :4 * A].cpu(), reg32, reg64, noise_rel)
+    fails += _check_outputs("cls", cls[..., :A * C].cpu(), cls32, cls64, noise_rel)
+    fails += _check_grads({k: net.store.g(k).detach().cpu() for k in g64}, g64, g32)
+    fails += _check_losses(losses.cpu().double(), l32, l64, max(rel(reg32, reg64), rel(cls32, cls64)))
+    assert not fails, fails
 
 
 def test_fcos_fp32_train_steps_match_reference_step():
     """Two FCOSTrainer steps in the parity mode (graph replay: targets, forward, loss, backward,
     /bs, clip_by_global_norm, Keras SGD; FCOS/train_fcos.py:107-185) vs train_step_reference in
-    float64 on the same targets, Keras init: momentum buffers and weight updates within GRAD_RTOL
-    (rel-L2 over all parameters)."""
+    float64 on the same targets, damped init (the keras-init graph is covered, against fp32 noise,
+    by the graph tests above): momentum buffers and weight updates within GRAD_RTOL (rel-L2 over all
+    parameters)."""
     from cvlite.fcos_net import FCOSNet
     from cvlite.train_fcos import FCOSTrainer, synthetic_batch
     C, B, D, lr = 20, 2, 256, 5e-4
     net = FCOSNet(C, seed=2, precision="fp32")
+    _damp_residual_gammas(net)
     p0 = net.store.state_dict()
     tr = FCOSTrainer(net, B, (D, D), init_lr=lr, use_graph=True)
     assert tr.d_reg.dtype == torch.float32
@@ -240,8 +358,10 @@ def test_fcos_fp32_train_steps_match_reference_step():
         st = net.store
         mom = {k: st.mom[st.offsets[k][0]:st.offsets[k][0] + st.offsets[k][1]].view(st.offsets[k][2]).cpu()
                for k in names}
+        # weights are stored in fp32 (as the reference's): compare updates as stored, i.e. the
+        # float64 step rounded to the fp32 weight, minus the fp32 start
         dw = {k: st.p(k).detach().cpu().double() - p0[k].double() for k in names}
-        d64 = {k: P64[k] - p0[k].double() for k in names}
+        d64 = {k: P64[k].float().double() - p0[k].double() for k in names}
         e_m, e_w = flat_rel(mom, M64), flat_rel(dw, d64)
         print("step %d (grad norm %.4f): momentum rel-L2 %.2e, weight update rel-L2 %.2e" % (it + 1, norm, e_m, e_w))
         assert e_m <= GRAD_RTOL and e_w <= GRAD_RTOL
