@@ -249,8 +249,17 @@ __global__ void wgrad_x_reduce_kernel(const float* slab, float* dw0, float* dw1,
     const int gq = (int)(t / n4);
     const long i = t - gq * n4;
     const f32x4* sl = reinterpret_cast<const f32x4*>(slab) + (long)gq * splits * n4;
+    // splits added in order (deterministic); loads 8 at a time so they are in flight together
     f32x4 s = sl[i];
-    for (int k = 1; k < splits; ++k) s += sl[(long)k * n4 + i];
+    int k = 1;
+    for (; k + 8 <= splits; k += 8) {
+      f32x4 v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = sl[(long)(k + u) * n4 + i];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) s += v[u];
+    }
+    for (; k < splits; ++k) s += sl[(long)k * n4 + i];
     f32x4* d = reinterpret_cast<f32x4*>(gq == 0 ? dw0 : dw1) + i;
     if (beta != 0.f) s += beta * *d;
     *d = s;

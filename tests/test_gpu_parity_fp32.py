@@ -70,33 +70,44 @@ def _check_losses(got, l32, l64, logit_noise):
     return [] if float(err.max()) <= tol else [("losses", float(err.max()), tol)]
 
 
-def _check_grads(grads_gpu, g64, g32, skip_bias_before_bn=True):
+def _perturbed(x, seed):
+    """x with every element moved by +-1 ulp (fp32): another realisation of fp32 forward noise."""
+    g = torch.Generator().manual_seed(seed)
+    u = torch.randint(0, 2, x.shape, generator=g).double() * 2 - 1
+    return (x.double() * (1 + u * 2.0 ** -23)).float()
+
+
+def _check_grads(grads_gpu, g64, g32s, skip_bias_before_bn=True):
+    """g32s: the fp32 oracle's gradients for several realisations of fp32 noise (the images and
+    their +-1-ulp perturbations): which tensors a ReLU-mask flip hits varies from one realisation
+    to the next (measured: p90 1.3e-3 .. 2.8e-3 over five realisations of one RetinaNet graph),
+    so the yardstick is the largest of the realisations at each quantile."""
     big = max(float(v.norm()) for v in g64.values())
-    rows = []
-    n_err = n_cpu = n_ref = 0.0
-    for k, gr in g64.items():
-        if skip_bias_before_bn and k.endswith("_conv/bias"):
-            continue              # conv bias in front of a training-mode BN: the true gradient is exactly 0
-        if float(gr.norm()) < 1e-6 * big:
-            continue
-        rows.append((rel(grads_gpu[k], gr), rel(g32[k], gr), k))
-        n_err += float((grads_gpu[k].double() - gr).norm()) ** 2
-        n_cpu += float((g32[k].double() - gr).norm()) ** 2
-        n_ref += float(gr.norm()) ** 2
-    eg = np.array([r[0] for r in rows])
-    ec = np.array([r[1] for r in rows])
+    keys = [k for k, gr in g64.items()
+            if not (skip_bias_before_bn and k.endswith("_conv/bias")) and float(gr.norm()) >= 1e-6 * big]
+    # (conv bias in front of a training-mode BN: the true gradient is exactly 0)
+
+    def errs(gg):
+        e = np.array([rel(gg[k], g64[k]) for k in keys])
+        n_err = sum(float((gg[k].double() - g64[k]).norm()) ** 2 for k in keys)
+        n_ref = sum(float(g64[k].norm()) ** 2 for k in keys)
+        return e, math.sqrt(n_err / n_ref)
+    eg, fg = errs(grads_gpu)
+    cpu = [errs(g) for g in g32s]
     fails = []
     for q in (50, 90, 100):
-        a, b = float(np.percentile(eg, q)), float(np.percentile(ec, q))
-        print("gradient rel-L2 p%d: gpu %.2e cpu-fp32 %.2e" % (q, a, b))
-        if a > max(GRAD_RTOL, NOISE_X * b):
-            fails.append(("grad p%d" % q, a, b))
-    fg, fc = math.sqrt(n_err / n_ref), math.sqrt(n_cpu / n_ref)
-    print("flat gradient rel-L2: gpu %.2e cpu-fp32 %.2e" % (fg, fc))
-    if fg > max(GRAD_RTOL, NOISE_X * fc):
-        fails.append(("grad flat", fg, fc))
-    rows.sort(reverse=True)
-    print("largest gpu errors (gpu, cpu-fp32, tensor):", [("%.2e" % e, "%.2e" % c, k) for e, c, k in rows[:5]])
+        a = float(np.percentile(eg, q))
+        bs = [float(np.percentile(e, q)) for e, _ in cpu]
+        print("gradient rel-L2 p%d: gpu %.2e | cpu-fp32 realisations %s" % (q, a, " ".join("%.2e" % b for b in bs)))
+        if a > max(GRAD_RTOL, NOISE_X * max(bs)):
+            fails.append(("grad p%d" % q, a, max(bs)))
+    fcs = [f for _, f in cpu]
+    print("flat gradient rel-L2: gpu %.2e | cpu-fp32 realisations %s" % (fg, " ".join("%.2e" % f for f in fcs)))
+    if fg > max(GRAD_RTOL, NOISE_X * max(fcs)):
+        fails.append(("grad flat", fg, max(fcs)))
+    order = np.argsort(-eg)[:5]
+    print("largest gpu errors (gpu, cpu-fp32 base, tensor):",
+          [("%.2e" % eg[i], "%.2e" % cpu[0][0][i], keys[i]) for i in order])
     return fails
 
 
@@ -209,10 +220,12 @@ def test_fcos_fp32_graph_matches_reference(init):
     params = net.store.state_dict()
     x, boxes, nbox = _synth(B, D, C, 3)
     tg, reg, cls, losses = _fcos_gpu(net, x, boxes, nbox, C, B, D)
-    l32, g32, reg32, cls32 = model_ref.fcos_loss_and_grads(params, torch.from_numpy(x), tg, C)
-    l64, g64, reg64, cls64 = model_ref.fcos_loss_and_grads(params, torch.from_numpy(x), tg, C, dtype=torch.float64)
+    xt = torch.from_numpy(x)
+    l32, g32, reg32, cls32 = model_ref.fcos_loss_and_grads(params, xt, tg, C)
+    l64, g64, reg64, cls64 = model_ref.fcos_loss_and_grads(params, xt, tg, C, dtype=torch.float64)
+    g32s = [g32] + [model_ref.fcos_loss_and_grads(params, _perturbed(xt, s), tg, C)[1] for s in (1, 2)]
     fails = _check_outputs("reg", reg, reg32, reg64, noise_rel) + _check_outputs("cls", cls, cls32, cls64, noise_rel)
-    fails += _check_grads({k: net.store.g(k).detach().cpu() for k in g64}, g64, g32)
+    fails += _check_grads({k: net.store.g(k).detach().cpu() for k in g64}, g64, g32s)
     fails += _check_losses(losses, l32, l64, max(rel(reg32, reg64), rel(cls32, cls64)))
     assert not fails, fails
 
@@ -306,12 +319,13 @@ def test_retinanet_fp32_graph_matches_reference(init):
     net.backward(d_reg, d_cls)
     torch.cuda.synchronize()
     tgc = tg.cpu()
-    l32, g32, reg32, cls32 = model_ref.retina_loss_and_grads(params, torch.from_numpy(x), tgc, C, cells, A)
-    l64, g64, reg64, cls64 = model_ref.retina_loss_and_grads(params, torch.from_numpy(x), tgc, C, cells, A,
-                                                             dtype=torch.float64)
+    xt = torch.from_numpy(x)
+    l32, g32, reg32, cls32 = model_ref.retina_loss_and_grads(params, xt, tgc, C, cells, A)
+    l64, g64, reg64, cls64 = model_ref.retina_loss_and_grads(params, xt, tgc, C, cells, A, dtype=torch.float64)
+    g32s = [g32] + [model_ref.retina_loss_and_grads(params, _perturbed(xt, s), tgc, C, cells, A)[1] for s in (1, 2)]
     fails = _check_outputs("reg", reg[..., :4 * A].cpu(), reg32, reg64, noise_rel)
     fails += _check_outputs("cls", cls[..., :A * C].cpu(), cls32, cls64, noise_rel)
-    fails += _check_grads({k: net.store.g(k).detach().cpu() for k in g64}, g64, g32)
+    fails += _check_grads({k: net.store.g(k).detach().cpu() for k in g64}, g64, g32s)
     fails += _check_losses(losses.cpu().double(), l32, l64, max(rel(reg32, reg64), rel(cls32, cls64)))
     assert not fails, fails
 
@@ -320,8 +334,11 @@ def test_fcos_fp32_train_steps_match_reference_step():
     """Two FCOSTrainer steps in the parity mode (graph replay: targets, forward, loss, backward,
     /bs, clip_by_global_norm, Keras SGD; FCOS/train_fcos.py:107-185) vs train_step_reference in
     float64 on the same targets, damped init (the keras-init graph is covered, against fp32 noise,
-    by the graph tests above): momentum buffers and weight updates within GRAD_RTOL (rel-L2 over all
-    parameters)."""
+    by the graph tests above): the momentum buffers (= the clipped, scaled gradient history) within
+    GRAD_RTOL (rel-L2 over all parameters) of float64, and the weights exactly the Keras fp32
+    update of the GPU's own momentum, w = fl32(w_prev + v) (the weight-update rel-L2 vs float64 is
+    printed: on top of the momentum error it carries fp32 weight-storage rounding, updates of
+    ~1e-7 relative on O(0.05) weights)."""
     from cvlite.fcos_net import FCOSNet
     from cvlite.train_fcos import FCOSTrainer, synthetic_batch
     C, B, D, lr = 20, 2, 256, 5e-4
@@ -338,7 +355,9 @@ def test_fcos_fp32_train_steps_match_reference_step():
     def flat_rel(a, b):
         n = sum(float((a[k].double() - b[k]).norm() ** 2) for k in names)
         return math.sqrt(n / sum(float(b[k].norm() ** 2) for k in names))
+    st = net.store
     for it in range(2):
+        p_prev = {k: st.p(k).detach().cpu().clone() for k in names}
         tr.load_batch(imgs, boxes, nbox)
         tr.step()
         torch.cuda.synchronize()
@@ -364,4 +383,6 @@ def test_fcos_fp32_train_steps_match_reference_step():
         d64 = {k: P64[k].float().double() - p0[k].double() for k in names}
         e_m, e_w = flat_rel(mom, M64), flat_rel(dw, d64)
         print("step %d (grad norm %.4f): momentum rel-L2 %.2e, weight update rel-L2 %.2e" % (it + 1, norm, e_m, e_w))
-        assert e_m <= GRAD_RTOL and e_w <= GRAD_RTOL
+        assert e_m <= GRAD_RTOL
+        for k in names:
+            torch.testing.assert_close(st.p(k).detach().cpu(), p_prev[k] + mom[k], rtol=0, atol=0)
