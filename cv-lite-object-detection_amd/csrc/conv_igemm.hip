@@ -366,81 +366,95 @@ __global__ void __launch_bounds__(NT) conv_igemm_kernel(ConvArgs a) {
   }
 }
 
-// Split-K epilogue for single-segment convs: sum the partial slabs, + bias, ReLU, beta*old,
-// BN statistics (per image: a workgroup owns rows of one image), bf16/fp32 store.
+// Split-K epilogue for single-segment convs: sum the partial slabs (fixed split order), + bias,
+// ReLU, beta*old, BN statistics, bf16/fp32 store.  Workgroup = (64-channel chunk, image, row part):
+// 8 lanes of 8 channels x 32 row lanes, every load of a row issued before the row's sums; the BN
+// sums of a chunk reduce over the row lanes in a fixed order through LDS, then ONE atomic pair per
+// (image, channel, row part) -- a plain single contribution when the image is one row part.
+constexpr int FIN_RL = NT / 8;                       // row lanes per workgroup
 __global__ void __launch_bounds__(NT) conv_splitk_finish(ConvArgs a, int rows_per_blk) {
   const ConvSeg& S = a.seg[0];
   const int HW = S.Hr * S.Wr;
   const int img = blockIdx.y;
-  const int C8 = a.n_store / 8;
-  const int tpr = C8 < NT ? C8 : NT;
-  const int rpp = NT / tpr;
-  const int cg = threadIdx.x % tpr, rsub = threadIdx.x / tpr;
+  const int cgi = threadIdx.x & 7, rl = threadIdx.x >> 3;
+  const int c0 = blockIdx.z * 64 + cgi * 8;
+  const bool cok = c0 < a.n_store;
   const int q0 = blockIdx.x * rows_per_blk;
   const int q1 = min(q0 + rows_per_blk, HW);
-  __shared__ float red[NT][17];
-  for (int cgb = cg; cgb < C8; cgb += tpr) {
-    const int c0 = cgb * 8;
-    float s1[8], s2[8], bb[8];
+  __shared__ float red[FIN_RL][8][17];
+  float s1[8], s2[8], bb[8];
 #pragma unroll
-    for (int u = 0; u < 8; ++u) { s1[u] = 0.f; s2[u] = 0.f; bb[u] = S.bias ? S.bias[c0 + u] : 0.f; }
-    if (rsub < rpp) {
-      for (int q = q0 + rsub; q < q1; q += rpp) {
-        const long ml = (long)img * HW + q;
-        float v[8];
+  for (int u = 0; u < 8; ++u) { s1[u] = 0.f; s2[u] = 0.f; bb[u] = (S.bias && cok) ? S.bias[c0 + u] : 0.f; }
+  if (cok) {
+    for (int q = q0 + rl; q < q1; q += FIN_RL) {
+      const long ml = (long)img * HW + q;
+      float v[8];
 #pragma unroll
-        for (int u = 0; u < 8; ++u) v[u] = bb[u];
-        for (int z = 0; z < a.splits; ++z) {
-          const f32x4* p = reinterpret_cast<const f32x4*>(a.slab + ((size_t)z * a.m_total + ml) * a.Npad + c0);
-          const f32x4 x0 = p[0], x1 = p[1];
-          v[0] += x0[0]; v[1] += x0[1]; v[2] += x0[2]; v[3] += x0[3];
-          v[4] += x1[0]; v[5] += x1[1]; v[6] += x1[2]; v[7] += x1[3];
-        }
-        const long drow = conv_dst_row(a, S, img, q);
-        if (a.dst_f32) {
-          float* pd = reinterpret_cast<float*>(a.dst) + drow * a.ld_dst + a.dst_coff + c0;
-#pragma unroll
-          for (int u = 0; u < 8; ++u) {
-            float o = v[u];
-            if (a.relu_out) o = o > 0.f ? o : 0.f;
-            s1[u] += o; s2[u] += o * o;
-            if (a.beta != 0.f) o += a.beta * pd[u];
-            pd[u] = o;
-          }
-        } else {
-          s16x8* pd = reinterpret_cast<s16x8*>(reinterpret_cast<cvl_bf16*>(a.dst) + drow * a.ld_dst + a.dst_coff + c0);
-          s16x8 old;
-          if (a.beta != 0.f) old = *pd;
-          s16x8 o;
-#pragma unroll
-          for (int u = 0; u < 8; ++u) {
-            float x = v[u];
-            if (a.relu_out) x = x > 0.f ? x : 0.f;
-            x = bf16_to_f32(f32_to_bf16(x));
-            s1[u] += x; s2[u] += x * x;
-            if (a.beta != 0.f) x += a.beta * bf16_to_f32((cvl_bf16)old[u]);
-            o[u] = (short)f32_to_bf16(x);
-          }
-          *pd = o;
-        }
+      for (int u = 0; u < 8; ++u) v[u] = bb[u];
+      for (int z = 0; z < a.splits; ++z) {
+        const f32x4* p = reinterpret_cast<const f32x4*>(a.slab + ((size_t)z * a.m_total + ml) * a.Npad + c0);
+        const f32x4 x0 = p[0], x1 = p[1];
+        v[0] += x0[0]; v[1] += x0[1]; v[2] += x0[2]; v[3] += x0[3];
+        v[4] += x1[0]; v[5] += x1[1]; v[6] += x1[2]; v[7] += x1[3];
       }
-    }
-    if (a.stats) {
-      __syncthreads();
+      const long drow = conv_dst_row(a, S, img, q);
+      if (a.dst_f32) {
+        float* pd = reinterpret_cast<float*>(a.dst) + drow * a.ld_dst + a.dst_coff + c0;
 #pragma unroll
-      for (int u = 0; u < 8; ++u) { red[threadIdx.x][u] = s1[u]; red[threadIdx.x][8 + u] = s2[u]; }
-      __syncthreads();
-      if (rsub == 0) {
         for (int u = 0; u < 8; ++u) {
-          double t1 = 0.0, t2 = 0.0;
-          for (int k = 0; k < rpp; ++k) { t1 += red[k * tpr + cg][u]; t2 += red[k * tpr + cg][8 + u]; }
-          double* st = a.stats + ((long)img * a.n_store + c0 + u) * 2;
-          atomicAdd(st, t1);
-          atomicAdd(st + 1, t2);
+          float o = v[u];
+          if (a.relu_out) o = o > 0.f ? o : 0.f;
+          s1[u] += o; s2[u] += o * o;
+          if (a.beta != 0.f) o += a.beta * pd[u];
+          pd[u] = o;
         }
+      } else {
+        s16x8* pd = reinterpret_cast<s16x8*>(reinterpret_cast<cvl_bf16*>(a.dst) + drow * a.ld_dst + a.dst_coff + c0);
+        s16x8 old;
+        if (a.beta != 0.f) old = *pd;
+        s16x8 o;
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          float x = v[u];
+          if (a.relu_out) x = x > 0.f ? x : 0.f;
+          x = bf16_to_f32(f32_to_bf16(x));
+          s1[u] += x; s2[u] += x * x;
+          if (a.beta != 0.f) x += a.beta * bf16_to_f32((cvl_bf16)old[u]);
+          o[u] = (short)f32_to_bf16(x);
+        }
+        *pd = o;
       }
     }
   }
+  if (a.stats) {
+#pragma unroll
+    for (int u = 0; u < 8; ++u) { red[rl][cgi][u] = s1[u]; red[rl][cgi][8 + u] = s2[u]; }
+    __syncthreads();
+    if (threadIdx.x < 64) {
+      const int cg2 = threadIdx.x >> 3, u = threadIdx.x & 7;
+      const int c = blockIdx.z * 64 + cg2 * 8 + u;
+      if (c < a.n_store) {
+        double t1 = 0.0, t2 = 0.0;
+        for (int k = 0; k < FIN_RL; ++k) { t1 += red[k][cg2][u]; t2 += red[k][cg2][8 + u]; }
+        double* st = a.stats + ((long)img * a.n_store + c) * 2;
+        atomicAdd(st, t1);
+        atomicAdd(st + 1, t2);
+      }
+    }
+  }
+}
+
+// launch geometry of the finish: (row parts, images, 64-channel chunks), ~512 workgroups, >= 64 rows each
+static int splitk_finish_launch(const ConvArgs& a, hipStream_t s) {
+  const ConvSeg& S = a.seg[0];
+  const int HW = S.Hr * S.Wr;
+  const int nch = (a.n_store + 63) / 64;
+  int parts = 512 / (a.B * nch);
+  if (parts > HW / 64) parts = HW / 64;
+  if (parts < 1) parts = 1;
+  const int rpb = (HW + parts - 1) / parts;
+  hipLaunchKernelGGL(conv_splitk_finish, dim3((HW + rpb - 1) / rpb, a.B, nch), dim3(NT), 0, s, a, rpb);
+  return cvl_launch_status();
 }
 
 // split-K factor: only for grids that cannot fill the chip (small M, e.g. conv5 / c6 at 16x16)
@@ -480,13 +494,7 @@ int launch_bn_bk(const ConvArgs& a0, bool dgrad, hipStream_t s) {
   }
   int st = cvl_launch_status();
   if (st || a.splits <= 1) return st;
-  const ConvSeg& S = a.seg[0];
-  const int HW = S.Hr * S.Wr;
-  int chunks = (512 + a.B - 1) / a.B;
-  int rpb = (HW + chunks - 1) / chunks;
-  rpb = rpb < 4 ? 4 : rpb;
-  hipLaunchKernelGGL(conv_splitk_finish, dim3((HW + rpb - 1) / rpb, a.B), dim3(NT), 0, s, a, rpb);
-  return cvl_launch_status();
+  return splitk_finish_launch(a, s);
 }
 
 template <int BN>
@@ -506,15 +514,7 @@ size_t cvl_conv_h_workspace(const cvl_conv_desc* d, const ConvArgs& a);
 
 // the split-K finishing pass of a single-segment launch whose partial slabs a.slab holds (used by
 // the halo kernel conv_igemm_h.hip as well)
-int cvl_conv_splitk_finish(const ConvArgs& a, hipStream_t s) {
-  const ConvSeg& S = a.seg[0];
-  const int HW = S.Hr * S.Wr;
-  int chunks = (512 + a.B - 1) / a.B;
-  int rpb = (HW + chunks - 1) / chunks;
-  rpb = rpb < 4 ? 4 : rpb;
-  hipLaunchKernelGGL(conv_splitk_finish, dim3((HW + rpb - 1) / rpb, a.B), dim3(NT), 0, s, a, rpb);
-  return cvl_launch_status();
-}
+int cvl_conv_splitk_finish(const ConvArgs& a, hipStream_t s) { return splitk_finish_launch(a, s); }
 
 // 1x1 strided data-gradient: only every stride-th dX pixel receives a gradient, so instead of a
 // DGRAD gather that finds no valid tap for (s^2-1)/s^2 of the rows, run a dense 1x1 GEMM over the

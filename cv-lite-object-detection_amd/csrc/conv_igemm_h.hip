@@ -40,12 +40,10 @@ namespace {
 
 constexpr int BM = 256, BN = 64, NT = 512, BK = 32;
 constexpr int WGM = 4, WM = 64, WN = 32, TM = 4, TN = 2;
-constexpr int HPX = 608;                            // halo pixels per stage
-constexpr int HPC = HPX / 16;                       // halo DMA pieces (16 pixels each): 38
-constexpr int WPC = 9 * BN * BK * 2 / 1024;         // weight DMA pieces per stage: 36
-constexpr int NPC = HPC + WPC;                      // 74
-constexpr int PPW = (NPC + 7) / 8;                  // piece slots per wave: 10
-constexpr int HALO_EL = HPX * BK;                   // bf16 elements of a halo image (38,912 B)
+constexpr int HPX = 640;                            // halo pixels per stage
+constexpr int HPW = HPX / 16 / 8;                   // halo DMA pieces (16 pixels each) per wave: 5
+constexpr int WPC = 9 * BN * BK * 2 / 1024;         // weight DMA pieces per stage: 36 (4 or 5 per wave)
+constexpr int HALO_EL = HPX * BK;                   // bf16 elements of a halo image (40,960 B)
 constexpr int WT_EL = 9 * BN * BK;                  // bf16 elements of a stage's weights (36,864 B)
 constexpr int STAGE_EL = HALO_EL + WT_EL;
 constexpr int LDS_C = BM * (BN + 8) + WGM * BN * 2 * 2;
@@ -85,9 +83,21 @@ __host__ __device__ inline HGeo h_geo(int H, int W) {
   return g;
 }
 
-template <bool DGRAD, bool BSUM>
+template <bool DGRAD, bool BSUM, bool DBG = false>
 __global__ void __launch_bounds__(NT) conv_igemm_h_kernel(ConvArgs a) {
+  // DBG: ablation switches (a.dbg bits, CVL_X_ABLATE) for measurement builds only: 1 no halo
+  // traffic, 2 no weight traffic, 4 no MFMA, 8 no epilogue, 16 no vmcnt waits, 64 no LDS reads
+  const int dbg = DBG ? a.dbg : 0;
   __shared__ __attribute__((aligned(16))) cvl_bf16 lds[LDS_EL];
+  // 256: wall-clock stamps of thread 0 of every workgroup into dst (u64 [grid][8]: entry, set-up
+  // done, prologue landed, main loop done, exit, HW_ID, XCC_ID)
+  unsigned long long* stamp = (DBG && (dbg & 256) && threadIdx.x == 0)
+                                  ? reinterpret_cast<unsigned long long*>(a.dst) + (size_t)blockIdx.x * 8 : nullptr;
+  if (stamp) {
+    stamp[0] = wall_clock64();
+    stamp[5] = __builtin_amdgcn_s_getreg((31 << 11) | 4);
+    stamp[6] = __builtin_amdgcn_s_getreg((31 << 11) | 20);
+  }
 
   const int tid = threadIdx.x;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
@@ -121,64 +131,62 @@ __global__ void __launch_bounds__(NT) conv_igemm_h_kernel(ConvArgs a) {
   const int y0 = G.whole ? 0 : (mloc0 - img0 * HWr) / W;
   const int hpx = G.rows * G.pitch;
 
-  // this lane's DMA pieces: piece k = wave + 8 j; k < HPC: halo pixels 16k .. 16k+15 (lane: pixel
-  // lane / 4, chunk lane % 4); HPC <= k < NPC: weight rows 16 (k - HPC) % 64 .. of tap (k - HPC) / 4
+  // DMA pieces of this lane, straight-line per stage: halo pieces k = wave + 8 j (j < HPW; pixels
+  // 16 k .. 16 k + 15, lane: pixel lane / 4, chunk lane % 4), weight pieces k = wave + 8 j (j < 4,
+  // and j = 4 on waves 0-3; rows 16 (k % 4) .. of tap k / 4).  Invalid halo pixels (outside the
+  // map, mosaic seams, absent images, past the halo) carry the out-of-range offset, which stays
+  // out of range when the channel block's byte offset is added.
   const int hch = lane & 3;
-  unsigned poff[PPW];
-  unsigned pvalid = 0;
+  unsigned hoff[HPW], woff[5];
 #pragma unroll
-  for (int j = 0; j < PPW; ++j) {
-    const int k = wave + 8 * j;
-    poff[j] = 0u;
-    if (k < HPC) {
-      const int hp = 16 * k + (lane >> 2);
-      const int hy = hp / G.pitch, hx = hp - hy * G.pitch;
-      int img, gy, gx;
-      bool ok;
-      if (!G.whole) {
-        img = img0;
-        gy = y0 + hy - 1;
-        gx = hx - 1;
-        ok = gy >= 0 && gy < H && gx >= 0 && gx < W;
-      } else {
-        const int ix = (hx - 1) / (W + 1), iy = (hy - 1) / (H + 1);
-        gx = hx - 1 - ix * (W + 1);
-        gy = hy - 1 - iy * (H + 1);
-        img = img0 + iy * G.mx + ix;
-        ok = hx >= 1 && hy >= 1 && gx < W && gy < H && ix < G.mx && iy < G.my;
-      }
-      ok = ok && hp < hpx && img < a.B;
-      const long pix = S.src_base + (long)img * S.src_img + (long)gy * W + gx;
-      if (ok) {
-        poff[j] = (unsigned)(pix * Cin * 2) + (unsigned)((hch ^ swz4(hp)) * 16);
-        pvalid |= 1u << j;
-      }
-    } else if (k < NPC) {
-      const int w = k - HPC, tap = w >> 2;
-      const int row = (w & 3) * 16 + (lane >> 2);
-      poff[j] = (unsigned)(((n0 + row) * Kdim + tap * Cin) * 2) + (unsigned)((hch ^ swz4(row)) * 16);
-      pvalid |= 1u << j;
+  for (int j = 0; j < HPW; ++j) {
+    const int hp = 16 * (wave + 8 * j) + (lane >> 2);
+    const int hy = hp / G.pitch, hx = hp - hy * G.pitch;
+    int img, gy, gx;
+    bool ok;
+    if (!G.whole) {
+      img = img0;
+      gy = y0 + hy - 1;
+      gx = hx - 1;
+      ok = gy >= 0 && gy < H && gx >= 0 && gx < W;
+    } else {
+      const int ix = (hx - 1) / (W + 1), iy = (hy - 1) / (H + 1);
+      gx = hx - 1 - ix * (W + 1);
+      gy = hy - 1 - iy * (H + 1);
+      img = img0 + iy * G.mx + ix;
+      ok = hx >= 1 && hy >= 1 && gx < W && gy < H && ix < G.mx && iy < G.my;
     }
+    ok = ok && hp < hpx && img < a.B;
+    const long pix = S.src_base + (long)img * S.src_img + (long)gy * W + gx;
+    hoff[j] = ok ? (unsigned)(pix * Cin * 2) + (unsigned)((hch ^ swz4(hp)) * 16) : kOOB;
+  }
+#pragma unroll
+  for (int j = 0; j < 5; ++j) {
+    const int w = (wave + 8 * j) % WPC, tap = w >> 2;
+    const int row = (w & 3) * 16 + (lane >> 2);
+    woff[j] = (unsigned)(((n0 + row) * Kdim + tap * Cin) * 2) + (unsigned)((hch ^ swz4(row)) * 16);
   }
   const __amdgpu_buffer_rsrc_t rsA = __builtin_amdgcn_make_buffer_rsrc((void*)a.src, (short)0, (int)kRecords, 0x00020000);
   const __amdgpu_buffer_rsrc_t rsB = __builtin_amdgcn_make_buffer_rsrc((void*)S.w, (short)0, (int)kRecords, 0x00020000);
 
-  // piece slots [j0, j1) of channel block cb into stage buffer sb (cb >= cb1: nothing)
-  auto issue = [&](int j0, int j1, int cb) {
-    if (cb >= cb1) return;
+  // the halo / the weights of channel block cb into stage buffer cb & 1
+  auto issue_halo = [&](int cb) {
+    if (dbg & 1) return;
     cvl_bf16* st = lds + (cb & 1) * STAGE_EL;
     const unsigned cbo = (unsigned)(cb * BK * 2);
 #pragma unroll
-    for (int j = 0; j < PPW; ++j) {
-      if (j < j0 || j >= j1) continue;
-      const int k = wave + 8 * j;
-      if (k < HPC) dma16(rsA, st + k * 16 * BK, ((pvalid >> j) & 1u) ? poff[j] + cbo : kOOB);
-      else if (k < NPC) dma16(rsB, st + HALO_EL + (k - HPC) * 16 * BK, poff[j] + cbo);
-    }
+    for (int j = 0; j < HPW; ++j) dma16(rsA, st + (wave + 8 * j) * 16 * BK, hoff[j] + cbo);
+  };
+  auto issue_w = [&](int cb) {
+    if (dbg & 2) return;
+    cvl_bf16* st = lds + (cb & 1) * STAGE_EL + HALO_EL;
+    const unsigned cbo = (unsigned)(cb * BK * 2);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) dma16(rsB, st + (wave + 8 * j) * 16 * BK, woff[j] + cbo);
+    if (wave < WPC - 32) dma16(rsB, st + (wave + 32) * 16 * BK, woff[4] + cbo);
   };
 
   const int wm = wave >> 1, wn = wave & 1;          // conv_l_epilogue's 4 x 2 wave grid
-  const int grp = wave >> 2;                        // stagger group (wm 0-1 / 2-3)
   const int lr = lane & 15, lg = lane >> 4;
   // swizzled LDS byte offset (within a halo image) of each A fragment row of this lane for
   // dx = -1, 0, +1 (the dy shift is added per phase)
@@ -193,8 +201,8 @@ __global__ void __launch_bounds__(NT) conv_igemm_h_kernel(ConvArgs a) {
     const int pc = hy * G.pitch + hx;
 #pragma unroll
     for (int d = 0; d < 3; ++d) {
-      const int p = pc + d - 1;
-      afr[i][d] = (unsigned)(p * BK * 2 + ((lg ^ swz4(p)) * 16));
+      const int pp = pc + d - 1;
+      afr[i][d] = (unsigned)(pp * BK * 2 + ((lg ^ swz4(pp)) * 16));
     }
   }
   // B fragment byte offsets within a tap's weight image
@@ -210,57 +218,84 @@ __global__ void __launch_bounds__(NT) conv_igemm_h_kernel(ConvArgs a) {
 #pragma unroll
     for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
   auto bar = [&]() {
-    __builtin_amdgcn_s_barrier();
+    if (!(dbg & 512)) __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
   };
 
   // prologue: stage cb0 complete everywhere
-  issue(0, PPW, cb0);
+  if (stamp) stamp[1] = wall_clock64();
+  issue_halo(cb0);
+  issue_w(cb0);
   wait_vm<0>();
   __builtin_amdgcn_s_barrier();
   asm volatile("" ::: "memory");
-  if (grp == 1) bar();            // stagger: waves 4-7 run one barrier behind
+  if (stamp) stamp[2] = wall_clock64();
 
   const int prow = G.pitch * BK * 2;                // bytes per halo row
-  for (int cb = cb0; cb < cb1; ++cb) {
-    const char* Hc = reinterpret_cast<const char*>(lds + (cb & 1) * STAGE_EL);
-    const char* Wc = Hc + HALO_EL * 2;
-#pragma unroll 1
-    for (int r = 0; r < 3; ++r) {
-      if (r == 0) issue(0, PPW / 2, cb + 1);
-      else if (r == 1) issue(PPW / 2, PPW, cb + 1);
-      else wait_vm<0>();                            // this wave's pieces of stage cb + 1 landed
-      const int dyoff = (DGRAD ? 1 - r : r - 1) * prow;
-      s16x8 fa[3][TM], fb[3][TN];
+  // One channel block = nine taps, software-pipelined inside each wave: the fragments of tap t + 1
+  // are read from LDS while the 8 MFMAs of tap t issue, and the DMA pieces of block cb + 1 (into
+  // the other stage buffer, free since the barrier that opened block cb) are spread over the taps.
+  // Both waves of a SIMD run this same stream; whichever is not stalled on an issue feeds the
+  // matrix pipe.  One barrier per block: every wave's pieces of block cb + 1 have landed (vmcnt 0)
+  // and every wave is done reading block cb.
+  s16x8 fa[2][TM], fb[2][TN];
+  auto read_tap = [&](int buf, const char* Hc, int t) {
+    const int r = t / 3, sx = t - 3 * (t / 3);
+    const int d = DGRAD ? 2 - sx : sx;
+    const char* Hr = Hc + (DGRAD ? 1 - r : r - 1) * prow;
+    const char* Wt = Hc + HALO_EL * 2 + t * BN * BK * 2;
+    if (dbg & 64) {
 #pragma unroll
-      for (int s = 0; s < 3; ++s) {
-        const int d = DGRAD ? 2 - s : s;
-        const char* Wt = Wc + (3 * r + s) * BN * BK * 2;
+      for (int i = 0; i < TM; ++i) fa[buf][i] = s16x8{(short)lane, 0, 0, 0, 0, 0, 0, (short)t};
 #pragma unroll
-        for (int i = 0; i < TM; ++i) fa[s][i] = *reinterpret_cast<const s16x8*>(Hc + afr[i][d] + dyoff);
-#pragma unroll
-        for (int j = 0; j < TN; ++j) fb[s][j] = *reinterpret_cast<const s16x8*>(Wt + bfr[j]);
-      }
-      bar();
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      __builtin_amdgcn_sched_barrier(0);
-      __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-      for (int s = 0; s < 3; ++s)
-#pragma unroll
-        for (int i = 0; i < TM; ++i)
-#pragma unroll
-          for (int j = 0; j < TN; ++j)
-            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, fa[s][i]),
-                                                                 __builtin_bit_cast(bf16x8, fb[s][j]), acc[i][j], 0, 0,
-                                                                 0);
-      __builtin_amdgcn_s_setprio(0);
-      __builtin_amdgcn_sched_barrier(0);
-      bar();
+      for (int j = 0; j < TN; ++j) fb[buf][j] = s16x8{(short)j, 0, 0, 0, 0, 0, 0, (short)t};
+      return;
     }
+#pragma unroll
+    for (int i = 0; i < TM; ++i) fa[buf][i] = *reinterpret_cast<const s16x8*>(Hr + afr[i][d]);
+#pragma unroll
+    for (int j = 0; j < TN; ++j) fb[buf][j] = *reinterpret_cast<const s16x8*>(Wt + bfr[j]);
+  };
+  auto mma_tap = [&](int buf) {
+    if (dbg & 4) {
+      asm volatile("" ::"v"(fa[buf][0]), "v"(fb[buf][0]), "v"(fa[buf][TM - 1]), "v"(fb[buf][TN - 1]));
+      return;
+    }
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, fa[buf][i]),
+                                                             __builtin_bit_cast(bf16x8, fb[buf][j]), acc[i][j], 0, 0, 0);
+  };
+  const cvl_bf16* hw0 = lds;
+  for (int cb = cb0; cb < cb1; ++cb) {
+    const char* Hc = reinterpret_cast<const char*>(hw0 + (cb & 1) * STAGE_EL);
+    const bool more = cb + 1 < cb1;
+    cvl_bf16* nh = lds + ((cb + 1) & 1) * STAGE_EL;
+    const unsigned cbo = (unsigned)((cb + 1) * BK * 2);
+    read_tap(0, Hc, 0);
+#pragma unroll
+    for (int t = 0; t < 9; ++t) {
+      // DMA pieces of block cb + 1: halo piece t (t < HPW), weight piece t - HPW
+      if (more && !(dbg & 1) && t < HPW) dma16(rsA, nh + (wave + 8 * t) * 16 * BK, hoff[t] + cbo);
+      if (more && !(dbg & 2) && t >= HPW && t < HPW + 4)
+        dma16(rsB, nh + HALO_EL + (wave + 8 * (t - HPW)) * 16 * BK, woff[t - HPW] + cbo);
+      if (t == 8 && more && !(dbg & 2) && wave < WPC - 32)
+        dma16(rsB, nh + HALO_EL + (wave + 32) * 16 * BK, woff[4] + cbo);
+      if (t < 8) read_tap((t + 1) & 1, Hc, t + 1);
+      mma_tap(t & 1);
+    }
+    if (!(dbg & 16)) wait_vm<0>();                  // this wave's pieces of block cb + 1 landed
+    bar();                                          // ... and everyone's; block cb fully read
   }
-  if (grp == 0) bar();            // equal barrier counts for both groups
   wait_vm<0>();
+  if (stamp) stamp[3] = wall_clock64();
+  if (dbg & 8) {
+    if (stamp) stamp[4] = wall_clock64();
+    if (acc[0][0][0] == 12345.f) reinterpret_cast<float*>(a.dst)[0] = 1.f;      // keep the accumulators live
+    return;
+  }
   if (a.splits > 1) {             // raw fp32 partials; conv_igemm.hip's finish applies the epilogue
     float* slab = a.slab + (size_t)blockIdx.z * a.m_total * a.Npad;
 #pragma unroll
@@ -273,6 +308,13 @@ __global__ void __launch_bounds__(NT) conv_igemm_h_kernel(ConvArgs a) {
           const int c = n0 + wn * WN + j * 16 + lr;
           slab[(size_t)rr * a.Npad + c] = acc[i][j][e];
         }
+    return;
+  }
+  if (DBG && (dbg & 256)) {       // (the stamps live in dst: the epilogue stores to a scratch copy)
+    ConvArgs b = a;
+    b.dst = a.slab;
+    conv_l_epilogue<BN, WGM, TM, TN, NT, BSUM>(b, S, acc, lds, tid, wm, wn, n0, mloc0, HWr, zpre, bpar);
+    if (stamp) stamp[4] = wall_clock64();
     return;
   }
   conv_l_epilogue<BN, WGM, TM, TN, NT, BSUM>(a, S, acc, lds, tid, wm, wn, n0, mloc0, HWr, zpre, bpar);
@@ -330,7 +372,23 @@ int cvl_conv_igemm_h(const cvl_conv_desc* d, const ConvArgs& a0, hipStream_t s, 
   }
   dim3 grid(tiles, 1, a.splits);
   g_cvl_conv_last_kernel = CVL_CK_H64;
-  if (dg && a.bsum) hipLaunchKernelGGL((conv_igemm_h_kernel<true, true>), grid, dim3(NT), 0, s, a);
+  a.dbg = cvl_env_int("CVL_X_ABLATE", 0);
+  if ((a.dbg & 256) && a.splits <= 1) {   // stamps: the epilogue writes a scratch image instead of dst
+    static void* scratch = nullptr;
+    static size_t scratch_bytes = 0;
+    const size_t need = (size_t)a.m_total * a.ld_dst * (a.dst_f32 ? 4 : 2) + 4096;
+    if (scratch_bytes < need) {
+      if (scratch) (void)hipFree(scratch);
+      if (hipMalloc(&scratch, need) != hipSuccess) return CVL_EHIP;
+      scratch_bytes = need;
+    }
+    a.slab = reinterpret_cast<float*>(scratch);
+  }
+  if (a.dbg) {
+    if (dg && a.bsum) hipLaunchKernelGGL((conv_igemm_h_kernel<true, true, true>), grid, dim3(NT), 0, s, a);
+    else if (dg) hipLaunchKernelGGL((conv_igemm_h_kernel<true, false, true>), grid, dim3(NT), 0, s, a);
+    else hipLaunchKernelGGL((conv_igemm_h_kernel<false, false, true>), grid, dim3(NT), 0, s, a);
+  } else if (dg && a.bsum) hipLaunchKernelGGL((conv_igemm_h_kernel<true, true>), grid, dim3(NT), 0, s, a);
   else if (dg) hipLaunchKernelGGL((conv_igemm_h_kernel<true, false>), grid, dim3(NT), 0, s, a);
   else hipLaunchKernelGGL((conv_igemm_h_kernel<false, false>), grid, dim3(NT), 0, s, a);
   int st = cvl_launch_status();

@@ -1,0 +1,35 @@
+"""A/B probe of the backbone 3x3 launches (bench.measure_backbone_3x3) under environment settings
+given on the command line, e.g. `bb3_probe.py "" CVL_X_ABLATE=4 "CVL_X_ABLATE=1 CVL_FOO=2"`: one
+column of us-per-launch per setting (knobs are read per launch)."""
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "cv-lite-object-detection_amd")]
+import torch  # noqa: E402
+
+import bench  # noqa: E402
+from cvlite.fcos_net import FCOSNet  # noqa: E402
+
+
+def main():
+    settings = sys.argv[1:] or [""]
+    net = FCOSNet(bench.NUM_CLASSES, device=torch.device("cuda", 0), seed=0)
+    cols = []
+    for st in settings:
+        kv = [x.split("=", 1) for x in st.split()]
+        for k, v in kv:
+            os.environ[k] = v
+        r = bench.measure_backbone_3x3(net, 16, 512, 512, iters=10)
+        for k, _ in kv:
+            del os.environ[k]
+        cols.append(r)
+        print("setting %-40r frac %.4f ms/step %.4f" % (st, r["frac"], r["ms_per_step"]), flush=True)
+    print("| shape | kernel | " + " | ".join(repr(s) for s in settings) + " |")
+    print("|---|---|" + "---|" * len(settings))
+    for i, row in enumerate(cols[0]["per_shape"]):
+        print("| %s | %s | " % (row["shape"], row["kernel"]) + " | ".join("%.1f" % c["per_shape"][i]["us"] for c in cols) + " |")
+
+
+if __name__ == "__main__":
+    main()

@@ -16,7 +16,7 @@ def main():
     iters = int(sys.argv[1]) if len(sys.argv) > 1 else 20
     net = FCOSNet(bench.NUM_CLASSES, device="cuda", seed=0)
     net.forward(torch.zeros((16, 512, 512, 3), device="cuda"))   # leaves the real tower buffers
-    ms, fl = bench.measure_tower_conv(net, 16, 512, 512, iters=iters)
+    ms, fl, _ = bench.measure_tower_conv(net, 16, 512, 512, iters=iters)
     torch.cuda.synchronize()
     print("tower conv %.4f ms/launch, %.1f TFLOP/s" % (ms, fl / ms / 1e9))
 
