@@ -574,6 +574,7 @@ extern "C" const char* cvl_conv_kernel_name(int code) {
     case CVL_CK_WG_X: return "conv_wgrad_x_kernel (256x256, 5-slot ring of 32-row steps, grouped)";
     case CVL_CK_WG_H: return "conv_wgrad_h_kernel (64 ci x 64 co x 9 taps, 128-row halo steps)";
     case CVL_CK_H64: return "conv_igemm_h_kernel (256x64, 3x3 halo + 9-tap weight stage per channel block)";
+    case CVL_CK_P: return "conv_igemm_p_kernel (persistent 1x1, K-tile stream across tiles)";
     default: return "none";
   }
 }

@@ -193,6 +193,7 @@ __global__ void __launch_bounds__(NT) conv_igemm_l_kernel(ConvArgs a) {
 
 int cvl_conv_igemm_x(const cvl_conv_desc* d, const ConvArgs& a, hipStream_t s);
 int cvl_conv_igemm_h(const cvl_conv_desc* d, const ConvArgs& a, hipStream_t s, void* slab, size_t slab_bytes);
+int cvl_conv_igemm_p(const cvl_conv_desc* d, const ConvArgs& a, hipStream_t s);
 
 // Called by cvl_conv_igemm when the launch qualifies (see cvl_conv_igemm_l_ok); returns -1 when
 // it does not, so the caller falls back to the 128-row kernel.
@@ -224,6 +225,15 @@ int cvl_conv_igemm_l(const cvl_conv_desc* d, int dst_up, int dst_w, const void* 
   // 192 -> 785, 128 -> 807, 1 -> 789 img/s (conv4_x 3x3 sits at exactly 128 tiles).  A launch
   // with too few 256-wide tiles drops to the 128-wide tile first (since the X32 kernel: 256 tiles,
   // e.g. one tower's 341-tile data gradient into F, FCOS 989 -> 995 img/s; 128: within noise).
+  // 1x1 launches (no fused BN-backward sums): the persistent streaming kernel (conv_igemm_p.hip)
+  if (d->KH == 1 && d->KW == 1 && !bsum) {
+    ConvArgs ap = a;
+    ap.src = reinterpret_cast<const cvl_bf16*>(src);
+    ap.dst = dst;
+    ap.stats = bn_stats;
+    const int pst = cvl_conv_igemm_p(d, ap, s);
+    if (pst >= 0) return pst;
+  }
   const long min_tiles = cvl_env_int("CVL_CONV_L_MIN_TILES", 128);
   int use_bn = bn;
   if (use_bn == 256 && (long)a.m_tiles * (a.Npad / 256) < cvl_env_int("CVL_CONV_L256_MIN_TILES", 256)) use_bn = 128;

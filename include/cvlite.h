@@ -155,7 +155,7 @@ int cvl_conv_igemm(const cvl_conv_desc* d, const void* src, void* dst, double* b
 enum { CVL_CK_NONE = 0, CVL_CK_BASE = 1, CVL_CK_BASE_SPLITK = 2, CVL_CK_L64 = 3, CVL_CK_L128 = 4,
        CVL_CK_L256 = 5, CVL_CK_X256 = 6, CVL_CK_X32 = 7,
        CVL_CK_WG_S = 8, CVL_CK_WG_L128 = 9, CVL_CK_WG_L256 = 10, CVL_CK_WG_X = 11, CVL_CK_X32H = 12, CVL_CK_WG_SN = 13,
-       CVL_CK_H64 = 14, CVL_CK_WG_H = 15 };
+       CVL_CK_H64 = 14, CVL_CK_WG_H = 15, CVL_CK_P = 16 };
 int cvl_conv_igemm_last_kernel(void);
 const char* cvl_conv_kernel_name(int code);
 

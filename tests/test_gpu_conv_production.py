@@ -122,12 +122,18 @@ def test_tower_pair_fwd_dgrad_configs1_layout():
             torch.testing.assert_close(got, ref, rtol=1e-2, atol=2e-2, msg=lambda m: "dgrad tower %d level %d: %s" % (t, l, m))
 
 
-@pytest.mark.parametrize("wide", [False, True])
-def test_wide_1x1_with_bn_stats_configs1(wide, monkeypatch):
+@pytest.mark.parametrize("variant", ["p", "p64", "p256", "l128", "wide"])
+def test_wide_1x1_with_bn_stats_configs1(variant, monkeypatch):
     """conv2_block1_3 (1x1 64 -> 256 at 128x128, bs 16: 1,024 M tiles) with the fused per-image BN
-    statistics epilogue, as ConvBN.forward runs it (short K: the 256x128 tile), and forced onto the
-    256-wide tiles (CVL_CONV_W256_MIN_K=0)."""
+    statistics epilogue, as ConvBN.forward runs it: on the persistent 1x1 kernel (default; also
+    forced to its 64- and 256-wide tiles), and with it off on the one-tile-per-workgroup L kernel's
+    256x128 tile and forced onto the 256-wide tiles (CVL_CONV_W256_MIN_K=0)."""
     from cvlite import ops_nn as nn
+    wide = variant == "wide"
+    if variant in ("l128", "wide"):
+        monkeypatch.setenv("CVL_CONV_NO_P", "1")
+    if variant in ("p64", "p256"):
+        monkeypatch.setenv("CVL_CONV_P_BN", variant[1:])
     if wide:
         monkeypatch.setenv("CVL_CONV_W256_MIN_K", "0")
     B, H, Cin, Cout = 16, 128, 64, 256
@@ -142,7 +148,7 @@ def test_wide_1x1_with_bn_stats_configs1(wide, monkeypatch):
     nn.conv_igemm(d, x, out, stats)
     code, name = last_kernel()
     print("kernel:", name)
-    assert code in ((5, 6, 7) if wide else (4,)), name
+    assert code in ((5, 6, 7) if wide else ((4,) if variant == "l128" else (16,))), name
     ref = conv_ref(x.to(F64), w, pt=0, pl=0) + bias.to(F64)
     torch.testing.assert_close(out.to(F64), ref, rtol=1e-2, atol=1e-2)
     o = out.to(F64)
