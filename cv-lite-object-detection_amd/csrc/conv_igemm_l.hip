@@ -225,12 +225,16 @@ int cvl_conv_igemm_l(const cvl_conv_desc* d, int dst_up, int dst_w, const void* 
   // 192 -> 785, 128 -> 807, 1 -> 789 img/s (conv4_x 3x3 sits at exactly 128 tiles).  A launch
   // with too few 256-wide tiles drops to the 128-wide tile first (since the X32 kernel: 256 tiles,
   // e.g. one tower's 341-tile data gradient into F, FCOS 989 -> 995 img/s; 128: within noise).
-  // 1x1 launches (no fused BN-backward sums): the persistent streaming kernel (conv_igemm_p.hip)
-  if (d->KH == 1 && d->KW == 1 && !bsum) {
+  // 1x1 launches: the persistent streaming kernel (conv_igemm_p.hip)
+  if (d->KH == 1 && d->KW == 1) {
     ConvArgs ap = a;
     ap.src = reinterpret_cast<const cvl_bf16*>(src);
     ap.dst = dst;
     ap.stats = bn_stats;
+    if (bsum) {
+      ap.bz = bsum->z; ap.bmr = bsum->mr; ap.bga = bsum->gamma; ap.bbe = bsum->beta; ap.bsum = bsum->sums;
+      ap.bhi = bsum->hi;
+    }
     const int pst = cvl_conv_igemm_p(d, ap, s);
     if (pst >= 0) return pst;
   }

@@ -57,7 +57,38 @@ struct PCfg {
   static_assert(D >= 2, "ring too short");
 };
 
-template <int BN>
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+
+// s_waitcnt vmcnt(n') with n' the largest bucket <= n (a wait for at least the ops older than the n
+// youngest); n is known only at run time
+__device__ __forceinline__ void wait_vm_atleast(int n) {
+  if (n >= 63) wait_vm<63>();
+  else if (n >= 48) wait_vm<48>();
+  else if (n >= 36) wait_vm<36>();
+  else if (n >= 30) wait_vm<30>();
+  else if (n >= 24) wait_vm<24>();
+  else if (n >= 21) wait_vm<21>();
+  else if (n >= 18) wait_vm<18>();
+  else if (n >= 15) wait_vm<15>();
+  else if (n >= 12) wait_vm<12>();
+  else if (n >= 9) wait_vm<9>();
+  else if (n >= 6) wait_vm<6>();
+  else if (n >= 3) wait_vm<3>();
+  else wait_vm<0>();
+}
+
+// a 16-B global load the compiler does not track (its consumer waits with wait_vm_atleast and then
+// pins the value, as conv_common.h's ds_tr16 / tr_pin)
+__device__ __forceinline__ s16x8 gload16_untracked(const void* p) {
+  s16x8 v;
+  asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(v) : "v"(p) : "memory");
+  return v;
+}
+__device__ __forceinline__ void pin16(s16x8& v) { asm volatile("" : "+v"(v)); }
+
+template <int BN, bool RELU, bool F32, bool BS = false>
 __global__ void __launch_bounds__(NT) conv_igemm_p_kernel(ConvArgs a, int ntiles) {
   using C = PCfg<BN>;
   constexpr int TM = C::TM, TN = C::TN, NS = C::NS, D = C::D;
@@ -101,7 +132,7 @@ __global__ void __launch_bounds__(NT) conv_igemm_p_kernel(ConvArgs a, int ntiles
     const int m0 = (mt0 + k) * BM;
 #pragma unroll
     for (int p = 0; p < 2; ++p) {
-      const int ml = m0 + p * 128 + prow;
+      const int ml = ((a.dbg & 16) ? 0 : m0) + p * 128 + prow;
       long pix;
       if (dense_src) {
         pix = S.src_base + ml;
@@ -172,7 +203,26 @@ __global__ void __launch_bounds__(NT) conv_igemm_p_kernel(ConvArgs a, int ntiles
       const int n = n0 + wn * C::WN + j * 16 + 4 * lg + e;
       bcol[j][e] = (S.bias && n < a.n_store) ? S.bias[n] : 0.f;
     }
+  // fused BN-backward sums (BS, data gradient): the lane's 8 channels per column-block pair after
+  // the store regrouping; gamma / beta now, (mean, rstd) per image in the epilogue
+  constexpr int NJP = BS ? TN / 2 : 1;
+  const int lgo = ((lg & 1) ? 16 : 0) + ((lg & 2) ? 8 : 0);
+  float bga[NJP][8], bbe[NJP][8], bm[NJP][8], brs[NJP][8], bs1[NJP][8], bs2[NJP][8];
+  int bimg = -1;
+  if (BS) {
+#pragma unroll
+    for (int jp = 0; jp < NJP; ++jp)
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int c = n0 + wn * C::WN + jp * 32 + lgo + u;
+        bga[jp][u] = a.bga[c];
+        bbe[jp][u] = a.bbe[c];
+        bs1[jp][u] = 0.f;
+        bs2[jp][u] = 0.f;
+      }
+  }
   wait_vm<0>();
+  s16x8 zv[BS ? TM : 1][NJP];
 
   // BN statistics: per-lane sums over this workgroup's rows of the current image, reduced over
   // the 16 rows of a lane quad by DPP (xor 1, xor 2, half-row mirror, row mirror: every lane ends
@@ -215,35 +265,58 @@ __global__ void __launch_bounds__(NT) conv_igemm_p_kernel(ConvArgs a, int ntiles
     }
   };
 
-  // epilogue of my k-th tile (rows m0.., columns n0..)
+  auto flush_bsum = [&](int img) {
+#pragma unroll
+    for (int jp = 0; jp < NJP; ++jp)
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const float t1 = row16_sum(bs1[jp][u]), t2 = row16_sum(bs2[jp][u]);
+        bs1[jp][u] = 0.f;
+        bs2[jp][u] = 0.f;
+        if (lr == 0) {
+          const int c = wn * C::WN + jp * 32 + lgo + u;
+          red[(wm * BN + c) * 2] = t1;
+          red[(wm * BN + c) * 2 + 1] = t2;
+        }
+      }
+    __syncthreads();
+    if (tid < BN && n0 + tid < a.n_store) {
+      float t1 = 0.f, t2 = 0.f;
+#pragma unroll
+      for (int w = 0; w < C::WGM; ++w) { t1 += red[(w * BN + tid) * 2]; t2 += red[(w * BN + tid) * 2 + 1]; }
+      double* st = a.bsum + ((long)img * a.n_store + n0 + tid) * 2;
+      atomicAdd(st, (double)t1);
+      atomicAdd(st + 1, (double)t2);
+    }
+  };
+
+  // epilogue of my k-th tile (rows m0.., columns n0..).  RELU / F32 are template flags: the
+  // per-element code is add, max, one packed conversion per pair (and the statistics FMAs).
   auto epilogue = [&](int k) {
     const int m0 = (mt0 + k) * BM;
-#pragma unroll
-    for (int i = 0; i < TM; ++i)
-#pragma unroll
-      for (int j = 0; j < TN; ++j)
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          float v = acc[i][j][e] + bcol[j][e];
-          if (a.relu_out) v = v > 0.f ? v : 0.f;
-          if (!a.dst_f32) v = (float)(__bf16)v;       // v_cvt_pk_bf16_f32: round to nearest even
-          acc[i][j][e] = v;
-        }
-    if (a.stats && !(a.dbg & 1)) {                     // a tile lies inside one image
-#pragma unroll
-      for (int j = 0; j < TN; ++j)
-#pragma unroll
-        for (int e = 0; e < 4; ++e)
-#pragma unroll
-          for (int i = 0; i < TM; ++i) {
-            const float v = acc[i][j][e];
-            ss1[j][e] += v;
-            ss2[j][e] += v * v;
-          }
-      const int img = m0 / HWr;
-      if (k == my_tiles - 1 || (m0 + BM) / HWr != img) flush_stats(img);
-    }
     const bool dense_dst = a.dst_up == 1 && S.dst_img == (long)HWr;
+    const bool do_stats = a.stats && !(a.dbg & 1);
+    if (BS) {
+      // the tile's z chunks (issued with its first K-tile) have landed: younger than them are the
+      // DMA pieces of its other nk - 1 K-tiles
+      wait_vm_atleast(C::PW * (nk - 1));
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int jp = 0; jp < NJP; ++jp) pin16(zv[i][jp]);
+      const int img = m0 / HWr;
+      if (img != bimg) {
+        bimg = img;
+#pragma unroll
+        for (int jp = 0; jp < NJP; ++jp)
+#pragma unroll
+          for (int u = 0; u < 8; ++u) {
+            const long bc = (long)img * a.n_store + n0 + wn * C::WN + jp * 32 + lgo + u;
+            bm[jp][u] = a.bmr[bc * 2];
+            brs[jp][u] = a.bmr[bc * 2 + 1];
+          }
+      }
+    }
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
       const int ml = m0 + wm * C::WM + i * 16 + lr;
@@ -255,39 +328,70 @@ __global__ void __launch_bounds__(NT) conv_igemm_p_kernel(ConvArgs a, int ntiles
         const int img = ml / HWr, q = ml - img * HWr;
         drow = conv_dst_row(a, S, img, q);
       }
-      if (a.dst_f32) {              // 4 consecutive fp32 channels per lane: 16-B stores
+      if (F32) {                    // 4 consecutive fp32 channels per lane: 16-B stores
 #pragma unroll
         for (int j = 0; j < TN; ++j) {
+          f32x4 v;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            v[e] = acc[i][j][e] + bcol[j][e];
+            if (RELU) v[e] = fmaxf(v[e], 0.f);
+          }
           const int n = n0 + wn * C::WN + j * 16 + 4 * lg;
           if (!row_ok || n >= a.n_store) continue;
           f32x4* pd = reinterpret_cast<f32x4*>(reinterpret_cast<float*>(a.dst) + drow * a.ld_dst + a.dst_coff + n);
-          f32x4 v = acc[i][j];
           if (a.beta != 0.f) v += a.beta * *pd;
           *pd = v;
         }
         continue;
       }
-      // bf16: the quads of column blocks j and j + 1 are regrouped by one v_permlane16_swap per
-      // packed register pair so that every lane holds 8 CONSECUTIVE channels (16-B stores, 64
-      // contiguous bytes per pixel row and instruction): lane quarter lg ends with channels
-      // j*16 + {0, 16, 8, 24}[lg] .. + 8
+      // bf16: pairs packed by one v_cvt_pk_bf16_f32 (round to nearest even); the BN statistics
+      // take the rounded values; then the quads of column blocks j and j + 1 are regrouped by one
+      // v_permlane16_swap per packed register so that every lane holds 8 CONSECUTIVE channels
+      // (16-B stores, 64 contiguous bytes per pixel row and instruction): lane quarter lg ends
+      // with channels j*16 + {0, 16, 8, 24}[lg] .. + 8
 #pragma unroll
       for (int j = 0; j < TN; j += 2) {
-        unsigned p0[2], p1[2];
+        unsigned pk[2][2];
+#pragma unroll
+        for (int jj = 0; jj < 2; ++jj)
+#pragma unroll
+          for (int h = 0; h < 2; ++h) {
+            float v0 = acc[i][j + jj][2 * h] + bcol[j + jj][2 * h];
+            float v1 = acc[i][j + jj][2 * h + 1] + bcol[j + jj][2 * h + 1];
+            if (RELU) { v0 = fmaxf(v0, 0.f); v1 = fmaxf(v1, 0.f); }
+            const unsigned u = __builtin_bit_cast(unsigned, __builtin_convertvector((f32x2){v0, v1}, bf16x2));
+            pk[jj][h] = u;
+            if (do_stats) {
+              const float r0 = __uint_as_float(u << 16), r1 = __uint_as_float(u & 0xffff0000u);
+              ss1[j + jj][2 * h] += r0;
+              ss2[j + jj][2 * h] = __builtin_fmaf(r0, r0, ss2[j + jj][2 * h]);
+              ss1[j + jj][2 * h + 1] += r1;
+              ss2[j + jj][2 * h + 1] = __builtin_fmaf(r1, r1, ss2[j + jj][2 * h + 1]);
+            }
+          }
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
-          p0[h] = (unsigned)__builtin_bit_cast(unsigned short, (__bf16)acc[i][j][2 * h]) |
-                  ((unsigned)__builtin_bit_cast(unsigned short, (__bf16)acc[i][j][2 * h + 1]) << 16);
-          p1[h] = (unsigned)__builtin_bit_cast(unsigned short, (__bf16)acc[i][j + 1][2 * h]) |
-                  ((unsigned)__builtin_bit_cast(unsigned short, (__bf16)acc[i][j + 1][2 * h + 1]) << 16);
-          const auto sw = __builtin_amdgcn_permlane16_swap(p0[h], p1[h], false, false);
-          p0[h] = sw[0];
-          p1[h] = sw[1];
+          const auto sw = __builtin_amdgcn_permlane16_swap(pk[0][h], pk[1][h], false, false);
+          pk[0][h] = sw[0];
+          pk[1][h] = sw[1];
         }
         const int n = n0 + wn * C::WN + j * 16 + ((lg & 1) ? 16 : 0) + ((lg & 2) ? 8 : 0);
         if (!row_ok || n >= a.n_store) continue;
         s16x8* pd = reinterpret_cast<s16x8*>(reinterpret_cast<cvl_bf16*>(a.dst) + drow * a.ld_dst + a.dst_coff + n);
-        s16x8 o = __builtin_bit_cast(s16x8, (unsigned __attribute__((ext_vector_type(4)))){p0[0], p0[1], p1[0], p1[1]});
+        s16x8 o = __builtin_bit_cast(s16x8, (u32x4){pk[0][0], pk[0][1], pk[1][0], pk[1][1]});
+        if (BS) {                   // g = dy * ReLU mask rebuilt from z (the forward's bn_affine value)
+          const s16x8 zz = zv[i][j / 2];
+#pragma unroll
+          for (int u = 0; u < 8; ++u) {
+            const float zf = bf16_to_f32((cvl_bf16)zz[u]);
+            const float xh = (zf - bm[j / 2][u]) * brs[j / 2][u];
+            const float af = __builtin_fmaf(bga[j / 2][u], xh, bbe[j / 2][u]);
+            const float gv = (af > 0.f && af < a.bhi) ? bf16_to_f32((cvl_bf16)o[u]) : 0.f;
+            bs1[j / 2][u] += gv;
+            bs2[j / 2][u] = __builtin_fmaf(gv, xh, bs2[j / 2][u]);
+          }
+        }
         if (a.beta != 0.f) {
           const s16x8 old = *pd;
 #pragma unroll
@@ -296,6 +400,14 @@ __global__ void __launch_bounds__(NT) conv_igemm_p_kernel(ConvArgs a, int ntiles
         }
         *pd = o;
       }
+    }
+    if (do_stats) {                                    // a tile lies inside one image
+      const int img = m0 / HWr;
+      if (k == my_tiles - 1 || (m0 + BM) / HWr != img) flush_stats(img);
+    }
+    if (BS) {
+      const int img = m0 / HWr;
+      if (k == my_tiles - 1 || (m0 + BM) / HWr != img) flush_bsum(img);
     }
 #pragma unroll
     for (int i = 0; i < TM; ++i)
@@ -314,6 +426,16 @@ __global__ void __launch_bounds__(NT) conv_igemm_p_kernel(ConvArgs a, int ntiles
     __builtin_amdgcn_s_barrier();                  // ... everyone's; slot of K-tile g - 2 free
     asm volatile("" ::: "memory");
     issue();                                       // K-tile g + D
+    if (BS && ck == 0) {                           // z chunks of tile ct for the epilogue
+      const int m0 = (mt0 + ct) * BM;
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int jp = 0; jp < NJP; ++jp) {
+          const long row = S.dst_base + m0 + wm * C::WM + i * 16 + lr;
+          zv[i][jp] = gload16_untracked(a.bz + row * a.ld_dst + a.dst_coff + n0 + wn * C::WN + jp * 32 + lgo);
+        }
+    }
     const char* sl = lds + rslot * C::SLOT_B;
     s16x8 fa[TM], fb[TN];
 #pragma unroll
@@ -342,7 +464,10 @@ __global__ void __launch_bounds__(NT) conv_igemm_p_kernel(ConvArgs a, int ntiles
 // Runs a 1x1 launch on the persistent kernel; -1 when it does not apply.
 int cvl_conv_igemm_p(const cvl_conv_desc* d, const ConvArgs& a0, hipStream_t s) {
   if (cvl_env_flag("CVL_CONV_NO_P")) return -1;
-  if (d->KH != 1 || d->KW != 1 || d->pad_t || d->pad_l || a0.relu_in || a0.nseg != 1 || a0.K % BK || a0.bsum)
+  if (d->KH != 1 || d->KW != 1 || d->pad_t || d->pad_l || a0.relu_in || a0.nseg != 1 || a0.K % BK) return -1;
+  if (a0.bsum && (d->mode != CVL_CONV_DGRAD || a0.dst_f32 || a0.beta != 0.f || a0.dst_up != 1 || a0.stats ||
+                  (a0.seg[0].Hr * a0.seg[0].Wr) % BM || a0.seg[0].dst_img != (long)a0.seg[0].Hr * a0.seg[0].Wr ||
+                  a0.Npad % 64 || cvl_env_flag("CVL_CONV_P_NO_BSUM")))
     return -1;
   if (d->mode == CVL_CONV_DGRAD && d->stride != 1) return -1;
   const ConvSeg& q = a0.seg[0];
@@ -353,10 +478,12 @@ int cvl_conv_igemm_p(const cvl_conv_desc* d, const ConvArgs& a0, hipStream_t s) 
   if (a0.stats && (a0.dst_f32 || (q.Hr * q.Wr) % BM)) return -1;
   const long src_bytes = (q.src_base + (long)a0.B * q.src_img) * a0.Cin * 2;
   if (src_bytes >= (long)kRecords - 65536 || (long)a0.Npad * a0.K * 2 >= (long)kRecords) return -1;
-  // 64-wide N tiles measured fastest on every backbone 1x1 shape (the 256-wide tile spills)
-  const int bn = a0.Npad % 64 == 0 ? 64 : 0;
+  // N tile: 128 for short K (<= 256: fwd 1x1 64->256 @ 128^2 44 -> 36 us, 128->512 @ 64^2 31 -> 26,
+  // 256->1024 @ 32^2 25 -> 21), 64 for long K (1024->256 @ 32^2 20.5 vs 23, 2048->512 @ 16^2 29.5
+  // vs 35; tools/p_probe.py)
+  const int bn = a0.K <= 256 && a0.Npad % 128 == 0 ? 128 : (a0.Npad % 64 == 0 ? 64 : 0);
   const int fbn = cvl_env_int("CVL_CONV_P_BN", 0);
-  const int use = fbn && a0.Npad % fbn == 0 ? fbn : bn;
+  const int use = a0.bsum ? 64 : (fbn && a0.Npad % fbn == 0 ? fbn : bn);
   if (!use) return -1;
   const int ntiles = a0.m_tiles * (a0.Npad / use);
   const int ntn = a0.Npad / use;
@@ -367,8 +494,21 @@ int cvl_conv_igemm_p(const cvl_conv_desc* d, const ConvArgs& a0, hipStream_t s) 
   ConvArgs a = a0;
   a.dbg = cvl_env_int("CVL_P_ABLATE", 0);
   g_cvl_conv_last_kernel = CVL_CK_P;
-  if (use == 256) hipLaunchKernelGGL(conv_igemm_p_kernel<256>, dim3(grid), dim3(NT), 0, s, a, ntiles);
-  else if (use == 128) hipLaunchKernelGGL(conv_igemm_p_kernel<128>, dim3(grid), dim3(NT), 0, s, a, ntiles);
-  else hipLaunchKernelGGL(conv_igemm_p_kernel<64>, dim3(grid), dim3(NT), 0, s, a, ntiles);
+#define CVL_P_LAUNCH(BN_)                                                                                   \
+  do {                                                                                                      \
+    if (a.dst_f32) {                                                                                        \
+      if (a.relu_out) hipLaunchKernelGGL((conv_igemm_p_kernel<BN_, true, true>), dim3(grid), dim3(NT), 0, s, a, ntiles);   \
+      else hipLaunchKernelGGL((conv_igemm_p_kernel<BN_, false, true>), dim3(grid), dim3(NT), 0, s, a, ntiles);            \
+    } else if (a.relu_out) {                                                                                \
+      hipLaunchKernelGGL((conv_igemm_p_kernel<BN_, true, false>), dim3(grid), dim3(NT), 0, s, a, ntiles);                 \
+    } else {                                                                                                \
+      hipLaunchKernelGGL((conv_igemm_p_kernel<BN_, false, false>), dim3(grid), dim3(NT), 0, s, a, ntiles);                \
+    }                                                                                                       \
+  } while (0)
+  if (a.bsum) hipLaunchKernelGGL((conv_igemm_p_kernel<64, false, false, true>), dim3(grid), dim3(NT), 0, s, a, ntiles);
+  else if (use == 256) CVL_P_LAUNCH(256);
+  else if (use == 128) CVL_P_LAUNCH(128);
+  else CVL_P_LAUNCH(64);
+#undef CVL_P_LAUNCH
   return cvl_launch_status();
 }

@@ -255,8 +255,10 @@ def test_im2col_matches_unfold(B, H, W, stride, Kp, C, K):
 
 @pytest.mark.parametrize("B,H,Cin,Cout,k,expect_fused", [
     (2, 128, 64, 64, 3, True),       # conv2_x 3x3 data gradient -> conv2_x conv1 BN (L64 kernel)
-    (8, 64, 512, 128, 1, True),      # conv3_x conv3 1x1 data gradient -> conv2 BN (L128 kernel)
-    (2, 16, 2048, 512, 1, False),    # conv5_x: too few tiles for the 256-row kernel -> plain path
+    (8, 64, 512, 128, 1, True),      # conv3_x conv3 1x1 data gradient -> conv2 BN (persistent 1x1 kernel)
+    (16, 128, 256, 64, 1, True),     # conv2_x conv3 1x1 data gradient at bs 16 (persistent, 4 tiles per workgroup)
+    (2, 16, 2048, 512, 1, True),     # conv5_x: one tile per image (persistent 1x1 kernel)
+    (2, 12, 256, 64, 1, False),      # H*W % 256 != 0: no per-image tiles -> plain path
 ])
 def test_dgrad_fused_bn_backward_first_pass(B, H, Cin, Cout, k, expect_fused):
     """cvl_conv_igemm_dgrad_bnsum + cvl_bn_backward_relu_sums (the first BN-backward pass formed in
