@@ -276,9 +276,18 @@ constexpr int LDS32_EL = NSLOT * SLOT > LDS_C ? NSLOT * SLOT : LDS_C;
 
 __device__ __forceinline__ int swz4(int r) { return (r >> 1) & 3; }
 
-template <bool DGRAD>
+template <bool DGRAD, bool DBG = false, bool MIX = false>
 __global__ void __launch_bounds__(NT) conv_igemm_x32_kernel(ConvArgs a) {
+  // DBG: ablation switches (a.dbg bits, CVL_X_ABLATE) for measurement builds only: 1 no A traffic,
+  // 2 no B traffic, 4 no MFMA, 8 no epilogue, 16 no vmcnt waits, 32 no DMA instructions, 64 no LDS
+  // reads, 512 no barriers
+  const int dbg = DBG ? a.dbg : 0;
   __shared__ __attribute__((aligned(16))) cvl_bf16 lds[LDS32_EL];
+  // 256 (with 8): wall-clock stamps of thread 0 of every workgroup into dst (u64 [grid][4]: entry,
+  // prologue landed, main loop done, K-tiles)
+  unsigned long long* stamp = (DBG && (dbg & 256) && threadIdx.x == 0)
+                                  ? reinterpret_cast<unsigned long long*>(a.dst) + (size_t)blockIdx.x * 4 : nullptr;
+  if (stamp) stamp[0] = wall_clock64();
 
   const int tid = threadIdx.x;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
@@ -330,19 +339,22 @@ __global__ void __launch_bounds__(NT) conv_igemm_x32_kernel(ConvArgs a) {
   const int dsgn = DGRAD ? -1 : 1;
   int kc = 0, ctap = 0, cr = 0, cs = 0, ccb = 0, cslot = 0;
   unsigned cak = 0, cbk = 0;
-  auto issue = [&]() {
+  // piece q of the cursor's K-tile: A rows q * 128 + .. (q < 2), B rows (q - 2) * 128 + .. (q >= 2)
+  auto issue_piece = [&](int q) {
+    if (dbg & 32) return;
     const bool live = kc < nk;
     cvl_bf16* Ab = lds + cslot * SLOT;
     cvl_bf16* Bb = Ab + 256 * BK32;
-#pragma unroll
-    for (int p = 0; p < 2; ++p) {
-      const bool v = live && ((amask[p] >> ctap) & 1u);
-      dma16(rsA, Ab + (p * 128 + wave * 16) * BK32, v ? aoff[p] + cak : kOOB);
+    if (q < 2) {
+      const bool v = live && ((amask[q] >> ctap) & 1u) && !(dbg & 1);
+      dma16(rsA, Ab + (q * 128 + wave * 16) * BK32, v ? aoff[q] + cak : kOOB);
+    } else {
+      const int p = q - 2;
+      dma16(rsB, Bb + (p * 128 + wave * 16) * BK32,
+            live && !(dbg & 2) ? boff0 + (unsigned)(p * 128 * Kdim * 2) + cbk : kOOB);
     }
-#pragma unroll
-    for (int p = 0; p < 2; ++p)
-      dma16(rsB, Bb + (p * 128 + wave * 16) * BK32, live ? boff0 + (unsigned)(p * 128 * Kdim * 2) + cbk : kOOB);
-    // advance the cursor
+  };
+  auto advance = [&]() {
     ++kc;
     cslot = cslot == NSLOT - 1 ? 0 : cslot + 1;
     ++ctap;
@@ -350,6 +362,11 @@ __global__ void __launch_bounds__(NT) conv_igemm_x32_kernel(ConvArgs a) {
     if (ctap == T) { ctap = 0; cr = 0; cs = 0; ++ccb; }
     cak = (unsigned)(dsgn * (cr * Ws + cs) * Cin * 2 + ccb * 64);
     cbk = (unsigned)((ctap * Cin + ccb * 32) * 2);
+  };
+  auto issue = [&]() {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) issue_piece(q);
+    advance();
   };
 
   const int wm = wave >> 2, wn = wave & 3;
@@ -360,7 +377,7 @@ __global__ void __launch_bounds__(NT) conv_igemm_x32_kernel(ConvArgs a) {
 #pragma unroll
     for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
   auto bar = [&]() {
-    __builtin_amdgcn_s_barrier();
+    if (!(dbg & 512)) __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
   };
 
@@ -371,34 +388,56 @@ __global__ void __launch_bounds__(NT) conv_igemm_x32_kernel(ConvArgs a) {
   __builtin_amdgcn_s_barrier();
   asm volatile("" ::: "memory");
   if (wm == 1) bar();           // stagger: waves 4-7 run one barrier behind
+  if (stamp) stamp[1] = wall_clock64();
 
   int rslot = 0;
   for (int kt = 0; kt < nk; ++kt) {
-    wait_vm<4>();                                 // K-tile kt+1 (read next phase)
-    issue();                                      // K-tile kt+3
+    if (!(dbg & 16)) wait_vm<4>();                // K-tile kt+1 (read next phase)
+    if (!MIX) issue();                            // K-tile kt+3
     const cvl_bf16* Ac = lds + rslot * SLOT;
     const cvl_bf16* Bc = Ac + 256 * BK32;
     s16x8 fa[TM], fb[TN];
+    if (dbg & 64) {
 #pragma unroll
-    for (int i = 0; i < TM; ++i) {
-      const int r = wm * WM + i * 16 + lr;
-      fa[i] = *reinterpret_cast<const s16x8*>(Ac + r * BK32 + ((lg ^ swz4(r)) * 8));
-    }
+      for (int i = 0; i < TM; ++i) fa[i] = s16x8{(short)lr, 0, 0, 0, 0, 0, 0, (short)kt};
 #pragma unroll
-    for (int j = 0; j < TN; ++j) {
-      const int r = wn * WN + j * 16 + lr;
-      fb[j] = *reinterpret_cast<const s16x8*>(Bc + r * BK32 + ((lg ^ swz4(r)) * 8));
+      for (int j = 0; j < TN; ++j) fb[j] = s16x8{(short)j, 0, 0, 0, 0, 0, 0, (short)lg};
+    } else {
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const int r = wm * WM + i * 16 + lr;
+        fa[i] = *reinterpret_cast<const s16x8*>(Ac + r * BK32 + ((lg ^ swz4(r)) * 8));
+      }
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int r = wn * WN + j * 16 + lr;
+        fb[j] = *reinterpret_cast<const s16x8*>(Bc + r * BK32 + ((lg ^ swz4(r)) * 8));
+      }
     }
     bar();
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_sched_barrier(0);
     __builtin_amdgcn_s_setprio(1);
+    if (dbg & 4) {
+      asm volatile("" ::"v"(fa[0]), "v"(fb[0]), "v"(fa[TM - 1]), "v"(fb[TN - 1]));
+      if (MIX) issue();
+    } else {
 #pragma unroll
-    for (int i = 0; i < TM; ++i)
+      for (int i = 0; i < TM; ++i) {
 #pragma unroll
-      for (int j = 0; j < TN; ++j)
-        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, fa[i]),
-                                                             __builtin_bit_cast(bf16x8, fb[j]), acc[i][j], 0, 0, 0);
+        for (int j = 0; j < TN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, fa[i]),
+                                                               __builtin_bit_cast(bf16x8, fb[j]), acc[i][j], 0, 0, 0);
+        // MIX: K-tile kt+3's four DMA pieces go out between the MFMAs (one per 8), where a piece's
+        // issue overlaps the matrix pipe instead of lengthening the load segment
+        if (MIX && (i & 1)) {
+          __builtin_amdgcn_sched_barrier(0);
+          issue_piece(i >> 1);
+          __builtin_amdgcn_sched_barrier(0);
+        }
+      }
+      if (MIX) advance();
+    }
     __builtin_amdgcn_s_setprio(0);
     __builtin_amdgcn_sched_barrier(0);
     bar();
@@ -406,6 +445,11 @@ __global__ void __launch_bounds__(NT) conv_igemm_x32_kernel(ConvArgs a) {
   }
   if (wm == 0) bar();           // equal barrier counts for both groups
   wait_vm<0>();
+  if (stamp) { stamp[2] = wall_clock64(); stamp[3] = nk; }
+  if (dbg & 8) {
+    if (acc[0][0][0] == 12345.f) reinterpret_cast<float*>(a.dst)[1] = 1.f;     // keep the accumulators live
+    return;
+  }
   const s16x8 znone[1] = {s16x8{0, 0, 0, 0, 0, 0, 0, 0}};     // (256-wide tiles: no fused BN sums)
   conv_l_epilogue<BN, WGM, TM, TN, NT>(a, S, acc, lds, tid, wm, wn, n0, mloc0, HWr, znone, BnSumPar{});
 }
@@ -709,8 +753,18 @@ int cvl_conv_igemm_x(const cvl_conv_desc* d, const ConvArgs& a, hipStream_t s) {
     else hipLaunchKernelGGL((conv_igemm_x32h_kernel<false, false>), grid, dim3(NT), 0, s, am);
   } else if (x32 && !am.dbg) {
     g_cvl_conv_last_kernel = CVL_CK_X32;
-    if (dg) hipLaunchKernelGGL((conv_igemm_x32_kernel<true>), grid, dim3(NT), 0, s, am);
-    else hipLaunchKernelGGL((conv_igemm_x32_kernel<false>), grid, dim3(NT), 0, s, am);
+    if (cvl_env_flag("CVL_X32_MIX")) {
+      if (dg) hipLaunchKernelGGL((conv_igemm_x32_kernel<true, false, true>), grid, dim3(NT), 0, s, am);
+      else hipLaunchKernelGGL((conv_igemm_x32_kernel<false, false, true>), grid, dim3(NT), 0, s, am);
+    } else if (dg) {
+      hipLaunchKernelGGL((conv_igemm_x32_kernel<true>), grid, dim3(NT), 0, s, am);
+    } else {
+      hipLaunchKernelGGL((conv_igemm_x32_kernel<false>), grid, dim3(NT), 0, s, am);
+    }
+  } else if (x32 && am.dbg && !cvl_env_flag("CVL_X_ABLATE_X64")) {
+    g_cvl_conv_last_kernel = CVL_CK_X32;
+    if (dg) hipLaunchKernelGGL((conv_igemm_x32_kernel<true, true>), grid, dim3(NT), 0, s, am);
+    else hipLaunchKernelGGL((conv_igemm_x32_kernel<false, true>), grid, dim3(NT), 0, s, am);
   } else if (am.dbg) {
     if (dg) hipLaunchKernelGGL((conv_igemm_x_kernel<true, true>), grid, dim3(NT), 0, s, am);
     else hipLaunchKernelGGL((conv_igemm_x_kernel<false, true>), grid, dim3(NT), 0, s, am);

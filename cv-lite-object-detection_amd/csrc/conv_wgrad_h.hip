@@ -24,12 +24,11 @@
 namespace {
 
 constexpr int NT = 512, BCI = 64, BCO = 64, RS = 128;
-constexpr int HPX = 432;                             // halo pixels per stage (W = 128: 3 x 144)
+constexpr int HPX = 448;                             // halo pixels per stage (W = 128: 3 x 144 used)
+constexpr int HPW = HPX / 8 / 8;                     // halo DMA pieces (8 pixels each) per wave: 7
 constexpr int HALO_B = HPX * 128;                    // bytes
 constexpr int DY_B = RS * 128;
-constexpr int STAGE_B = HALO_B + DY_B;               // 71,680 B
-constexpr int NPS = HPX / 8 + RS / 8;                // DMA pieces per stage (max): 54 + 16
-constexpr int PPW = (NPS + 7) / 8;                   // piece slots per wave: 9
+constexpr int STAGE_B = HALO_B + DY_B;               // 73,728 B
 constexpr unsigned kRecords = 0x7fffffffu;
 constexpr unsigned kOOB = 0x80000000u;
 
@@ -64,26 +63,29 @@ __global__ void __launch_bounds__(NT) conv_wgrad_h_kernel(WhArgs g) {
   const int R = RS / W;                                // image rows per step
   const int P = (W + 2 + 15) & ~15;                    // halo pitch (pixels; % 16: a row shift keeps the swizzle)
   const int hpx = (R + 2) * P;
-  const int nh = (hpx + 7) / 8;                        // halo pieces; dY pieces follow
   const int ch = lane & 7;
+  const int Cin2 = g.Cin * 2;
 
-  // piece slots of this lane: k = wave + 8 j
-  int pk_hy[PPW], pk_hx[PPW];
-  unsigned pk_chs[PPW];
+  // DMA pieces of this lane, straight-line per step: halo pieces k = wave + 8 j (j < HPW: halo
+  // pixels 8k + lane / 8, chunk lane % 8; those past the halo write zeros into its tail), dY pieces
+  // k = wave + 8 j (j < 2: rows 8k + lane / 8 of the step).  Per lane the halo pixel's row hy and
+  // its offset relative to the step's first pixel are fixed; a step only adds its base and
+  // checks its top / bottom image rows.
+  int hy[HPW];
+  bool hok[HPW];
+  unsigned hlo[HPW], ylo[2];
 #pragma unroll
-  for (int j = 0; j < PPW; ++j) {
-    const int k = wave + 8 * j;
-    if (k < nh) {
-      const int hp = 8 * k + (lane >> 3);
-      pk_hy[j] = hp < hpx ? hp / P : -1000;
-      pk_hx[j] = hp - (hp / P) * P;
-      pk_chs[j] = (unsigned)((ch ^ swz8(hp)) * 16);
-    } else {
-      const int m = 8 * (k - nh) + (lane >> 3);
-      pk_hy[j] = m;                                  // dY row of the step
-      pk_hx[j] = 0;
-      pk_chs[j] = (unsigned)((ch ^ swz8(m)) * 16);
-    }
+  for (int j = 0; j < HPW; ++j) {
+    const int hp = 8 * (wave + 8 * j) + (lane >> 3);
+    const int y = hp / P, x = hp - y * P;
+    hy[j] = y;
+    hok[j] = hp < hpx && x >= 1 && x <= W;
+    hlo[j] = (unsigned)(((y - 1) * W + (x - 1)) * Cin2 + ci0 * 2) + (unsigned)((ch ^ swz8(hp)) * 16);
+  }
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int m = 8 * (wave + 8 * j) + (lane >> 3);
+    ylo[j] = (unsigned)((m * g.ld_dy + g.dy_coff + co0) * 2) + (unsigned)((ch ^ swz8(m)) * 16);
   }
   const __amdgpu_buffer_rsrc_t rsX = __builtin_amdgcn_make_buffer_rsrc((void*)g.x, (short)0, (int)kRecords, 0x00020000);
   const __amdgpu_buffer_rsrc_t rsY = __builtin_amdgcn_make_buffer_rsrc((void*)g.dy, (short)0, (int)kRecords, 0x00020000);
@@ -94,20 +96,16 @@ __global__ void __launch_bounds__(NT) conv_wgrad_h_kernel(WhArgs g) {
     const int m0 = s * RS;
     const int img = m0 / HW;
     const int y0 = (m0 - img * HW) / W;
+    const unsigned xb = (unsigned)((g.src_base + (long)img * g.src_img + (long)y0 * W) * Cin2);
+    const unsigned yb = (unsigned)((g.dst_base + (long)img * g.dst_img + (long)y0 * W) * g.ld_dy * 2);
+    const bool top = y0 == 0, bot = y0 + R == H;
 #pragma unroll
-    for (int j = 0; j < PPW; ++j) {
-      const int k = wave + 8 * j;
-      if (k < nh) {
-        const int gy = y0 + pk_hy[j] - 1, gx = pk_hx[j] - 1;
-        const bool ok = gy >= 0 && gy < H && gx >= 0 && gx < W;
-        const long pix = g.src_base + (long)img * g.src_img + (long)gy * W + gx;
-        dma16(rsX, st + k * 1024, ok ? (unsigned)((pix * g.Cin + ci0) * 2) + pk_chs[j] : kOOB);
-      } else if (k < nh + RS / 8) {
-        const long drow = g.dst_base + (long)img * g.dst_img + (long)y0 * W + pk_hy[j];
-        dma16(rsY, st + HALO_B + (k - nh) * 1024,
-              (unsigned)((drow * g.ld_dy + g.dy_coff + co0) * 2) + pk_chs[j]);
-      }
+    for (int j = 0; j < HPW; ++j) {
+      const bool ok = hok[j] && !(top && hy[j] == 0) && !(bot && hy[j] == R + 1);
+      dma16(rsX, st + (wave + 8 * j) * 1024, ok ? xb + hlo[j] : kOOB);
     }
+#pragma unroll
+    for (int j = 0; j < 2; ++j) dma16(rsY, st + HALO_B + (wave + 8 * j) * 1024, yb + ylo[j]);
   };
 
   const int wco = wave & 1, wk = wave >> 1, grp = wave >> 2;

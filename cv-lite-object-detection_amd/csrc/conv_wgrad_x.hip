@@ -29,11 +29,19 @@
 
 namespace {
 
-constexpr int NT = 512, BCO = 256, BKK = 256, BR = 32, NSLOT = 5;
-constexpr int YST = BR * BCO;             // bf16 elements of the dY image of a slot (16 KiB)
-constexpr int SLOT = YST + BR * BKK;      // + the im2col image (16 KiB)
+constexpr int NT = 512, BR = 32, NSLOT = 5;
 constexpr int SEGM = 128;                 // segment / chunk alignment of the M space
-constexpr int TM = 8, TN = 4;
+// tile T (co) x T (k), T = 256 (the tower) or 128 (small outputs: 4x fewer fp32 slab bytes per split)
+template <int T>
+struct WxCfg {
+  static constexpr int BCO = T, BKK = T;
+  static constexpr int YST = BR * BCO;    // bf16 elements of the dY image of a slot
+  static constexpr int SLOT = YST + BR * BKK;
+  static constexpr int TM = T / 32, TN = T / 64;   // 8 waves as 2 (co) x 4 (k)
+  static constexpr int LPR = T / 8;       // DMA lanes per row (16-B pieces)
+  static constexpr int RPI = 64 / LPR;    // rows per DMA instruction
+  static constexpr int J = BR / (8 * RPI);  // DMA instructions per wave per operand and step
+};
 constexpr int kMaxGroups = 2;
 constexpr unsigned kRecords = 0x7fffffffu;
 constexpr unsigned kOOB = 0x80000000u;
@@ -55,7 +63,11 @@ __device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t r, const cvl_bf16* 
                                            0, 0);
 }
 
+template <int T>
 __global__ void __launch_bounds__(NT) conv_wgrad_x_kernel(WxArgs g) {
+  using C = WxCfg<T>;
+  constexpr int BCO = C::BCO, BKK = C::BKK, YST = C::YST, SLOT = C::SLOT, TM = C::TM, TN = C::TN;
+  constexpr int J = C::J;
   __shared__ __attribute__((aligned(16))) cvl_bf16 lds[NSLOT * SLOT];
   const ConvArgs& a = g.a;
   const int tid = threadIdx.x;
@@ -69,8 +81,8 @@ __global__ void __launch_bounds__(NT) conv_wgrad_x_kernel(WxArgs g) {
   const int m_hi = min(m_lo + g.chunk, g.g_m1[grp]);
   const int nsteps = m_hi > m_lo ? (m_hi - m_lo) / BR : 0;
 
-  // ---- per-lane DMA constants: rows rr and rr + 16 of each step, 16-B piece pc of the row -------
-  const int rr = 2 * wave + (lane >> 5), pc = lane & 31;
+  // ---- per-lane DMA constants: rows rr + 8 RPI j of each step, 16-B piece pc of the row ---------
+  const int rr = C::RPI * wave + lane / C::LPR, pc = lane % C::LPR;
   const int lp = pc ^ (rswz(rr) << 1);                    // logical piece (rswz(rr + 16) == rswz(rr))
   const unsigned ycol = (unsigned)((g.dy_coff + co0 + lp * 8) * 2);
   const int kx = k0 + lp * 8;
@@ -89,7 +101,7 @@ __global__ void __launch_bounds__(NT) conv_wgrad_x_kernel(WxArgs g) {
   int seg_end = -1;                                       // forces a seek at the first live step
   int Wr = 1, Hr = 1, Ws = 1, Hs = 1, rows = 0, sbase = 0, simg = 0, dbase = 0, dimg = 0;
   int d_img = 0, d_oy = 0, d_ox = 0;
-  int cml[2], cimg[2], coy[2], cox[2];
+  int cml[J], cimg[J], coy[J], cox[J];
   auto seek = [&](int m) {
     int sg = 0;
 #pragma unroll
@@ -105,8 +117,8 @@ __global__ void __launch_bounds__(NT) conv_wgrad_x_kernel(WxArgs g) {
     d_oy = rem / Wr;
     d_ox = rem - d_oy * Wr;
 #pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const int ml = m - S.m_start + 16 * j + rr;
+    for (int j = 0; j < J; ++j) {
+      const int ml = m - S.m_start + 8 * C::RPI * j + rr;
       cml[j] = ml;
       cimg[j] = ml / HW;
       const int q = ml - cimg[j] * HW;
@@ -120,14 +132,14 @@ __global__ void __launch_bounds__(NT) conv_wgrad_x_kernel(WxArgs g) {
     cvl_bf16* Yb = lds + cslot * SLOT;
     cvl_bf16* Xb = Yb + YST;
 #pragma unroll
-    for (int j = 0; j < 2; ++j) {
+    for (int j = 0; j < J; ++j) {
       const bool rv = live && cml[j] < rows;
       const int drow = dbase + cimg[j] * dimg + coy[j] * Wr + cox[j];
-      dma16(rsY, Yb + (16 * j + 2 * wave) * BCO, rv ? (unsigned)(drow * rowb) + ycol : kOOB);
+      dma16(rsY, Yb + (8 * C::RPI * j + C::RPI * wave) * BCO, rv ? (unsigned)(drow * rowb) + ycol : kOOB);
       const int iy = coy[j] * a.stride + ry, ix = cox[j] * a.stride + rx;
       const bool xv = rv && kok && (unsigned)iy < (unsigned)Hs && (unsigned)ix < (unsigned)Ws;
       const int pix = sbase + cimg[j] * simg + iy * Ws + ix;
-      dma16(rsX, Xb + (16 * j + 2 * wave) * BKK, xv ? (unsigned)(pix * pixb) + xcol : kOOB);
+      dma16(rsX, Xb + (8 * C::RPI * j + C::RPI * wave) * BKK, xv ? (unsigned)(pix * pixb) + xcol : kOOB);
       // advance the row by BR: (img, y, x) with one carry per level (d_ox < Wr, d_oy < Hr)
       cml[j] += BR;
       cox[j] += d_ox;
@@ -162,28 +174,29 @@ __global__ void __launch_bounds__(NT) conv_wgrad_x_kernel(WxArgs g) {
   unsigned ya[TM], yb[TM], xa[TN], xb[TN];
 #pragma unroll
   for (int i = 0; i < TM; ++i) {
-    const int ch = wco * 8 + i;
+    const int ch = wco * TM + i;
     ya[i] = 2 * (rlo * BCO + (sw_chunk(ch, slo) << 4) + 4 * pp);
     yb[i] = 2 * (rhi * BCO + (sw_chunk(ch, shi) << 4) + 4 * pp);
   }
 #pragma unroll
   for (int j = 0; j < TN; ++j) {
-    const int ch = wk * 4 + j;
+    const int ch = wk * TN + j;
     xa[j] = 2 * (YST + rlo * BKK + (sw_chunk(ch, slo) << 4) + 4 * pp);
     xb[j] = 2 * (YST + rhi * BKK + (sw_chunk(ch, shi) << 4) + 4 * pp);
   }
 
+  constexpr int PW = 2 * J;                     // DMA pieces per wave per step
   issue();
   issue();
   issue();
-  wait_vm<8>();
+  wait_vm<2 * PW>();
   __builtin_amdgcn_s_barrier();
   asm volatile("" ::: "memory");
   if (wco == 1) bar();                          // stagger: waves 4-7 run one barrier behind
 
   int rslot = 0;
   for (int st = 0; st < nsteps; ++st) {
-    wait_vm<4>();                               // step st+1 (read next phase)
+    wait_vm<PW>();                              // step st+1 (read next phase)
     issue();                                    // step st+3
     const unsigned base = lds0 + rslot * (SLOT * 2);
     s16x4 al[TM], ah[TM], bl[TN], bh[TN];
@@ -224,8 +237,8 @@ __global__ void __launch_bounds__(NT) conv_wgrad_x_kernel(WxArgs g) {
   for (int i = 0; i < TM; ++i)
 #pragma unroll
     for (int j = 0; j < TN; ++j) {
-      const int k = k0 + wk * 64 + j * 16 + lr;
-      const int co = co0 + wco * 128 + i * 16 + 4 * lg;
+      const int k = k0 + wk * (BKK / 4) + j * 16 + lr;
+      const int co = co0 + wco * (BCO / 2) + i * 16 + 4 * lg;
       if (k >= a.K || co >= g.Cout) continue;
       f32x4 v = acc[i][j];
       if (co + 3 < g.Cout && (g.Cout & 3) == 0) {
@@ -267,20 +280,22 @@ __global__ void wgrad_x_reduce_kernel(const float* slab, float* dw0, float* dw1,
 }
 
 struct WxPlan {
-  int ngroups, spg, tiles, co_tiles, nsplit, chunk;
+  int T, ngroups, spg, tiles, co_tiles, nsplit, chunk;
   int g_m0[kMaxGroups], g_m1[kMaxGroups];
   size_t slab;
 };
 
-// Modelled time of s splits: rounds of 256 workgroups (one per CU) x 32-row steps per chunk
-// (CVL_WGX_STEP, 0.01 us; ~0.8 us measured on the tower shape) + the fp32 slab round trip.
-// K below one 256-deep tile (1x1 convs with Cin 128) leaves half of every tile idle: those go to
-// the 128-wide kernels (tools/wgrad_sweep.py: 1x1 128->512 @ 64x64, 59 -> 47 us).
+// Modelled time of s splits at tile width T: rounds of 256 workgroups (one per CU; 512 for T = 128) x 32-row steps
+// per chunk (CVL_WGX_STEP, 0.01 us; ~0.8 us measured on the tower shape; CVL_WGX_STEP128 for the
+// 128-wide tile, a quarter of the MFMA work per step) + the fp32 slab round trip.  The 128-wide tile
+// serves the 1x1 / small-output launches (e.g. 1x1 256->1024 @ 32x32: 4 tiles of 256 -> 64 splits,
+// 64 MiB of slabs; 16 tiles of 128 -> 16 splits, 16 MiB).
+// K below one 256-deep tile (1x1 convs with Cin 128) leaves half of every 256 tile idle.
 inline bool wx_plan(const cvl_conv_desc* d, int ngroups, ConvArgs* a, WxPlan* p) {
   if (cvl_env_flag("CVL_WGRAD_NO_X")) return false;
   if (cvl_conv_prepare(d, SEGM, a)) return false;
-  if (ngroups < 1 || ngroups > kMaxGroups || d->nseg % ngroups || d->relu_in || a->Npad % BCO ||
-      d->Cin % 8 || d->n_store % 4 || a->K < cvl_env_int("CVL_WGX_MIN_K", BKK) || a->m_total < 1024)
+  if (ngroups < 1 || ngroups > kMaxGroups || d->nseg % ngroups || d->relu_in || a->Npad % 128 || d->Cin % 8 ||
+      d->n_store % 4 || a->m_total < 1024)
     return false;
   // every dY / source byte offset must stay below the buffer-resource bound (32-bit cursors)
   for (int i = 0; i < a->nseg; ++i) {
@@ -298,22 +313,32 @@ inline bool wx_plan(const cvl_conv_desc* d, int ngroups, ConvArgs* a, WxPlan* p)
     mg = p->g_m1[gq] - p->g_m0[gq] > mg ? p->g_m1[gq] - p->g_m0[gq] : mg;
   }
   for (int gq = ngroups; gq < kMaxGroups; ++gq) p->g_m0[gq] = p->g_m1[gq] = 0;
-  p->co_tiles = a->Npad / BCO;
-  p->tiles = p->co_tiles * ((a->K + BKK - 1) / BKK);
-  const int tg = p->tiles * ngroups;
-  const double step_us = cvl_env_int("CVL_WGX_STEP", 80) / 100.0;
-  const double slab_us = (double)BCO * BKK * 4 * 2 / 5.0e6 * cvl_env_int("CVL_WGX_SLAB_PCT", 100) / 100.0;
-  int max_s = mg / 512;
-  if (max_s < 1) max_s = 1;
-  if (max_s > 2048 / tg) max_s = 2048 / tg > 1 ? 2048 / tg : 1;
+  const int forced_t = cvl_env_int("CVL_WGX_T", 0);
   double best_t = 1e30;
-  int best_s = 1;
-  for (int s = 1; s <= max_s; ++s) {
-    const int rounds = (tg * s + 255) / 256;
-    const int chunk = ((mg + s - 1) / s + SEGM - 1) / SEGM * SEGM;
-    const double t = rounds * (chunk / BR) * step_us + (s > 1 ? tg * s * slab_us : 0.0);
-    if (t < best_t) { best_t = t; best_s = s; }
+  int best_s = 0, best_T = 0;
+  for (int T = 256; T >= 128; T /= 2) {
+    if (forced_t && forced_t != T) continue;
+    if (a->Npad % T || a->K < cvl_env_int(T == 256 ? "CVL_WGX_MIN_K" : "CVL_WGX_MIN_K128", T == 256 ? 256 : 64))
+      continue;
+    const int tg = (a->Npad / T) * ((a->K + T - 1) / T) * ngroups;
+    const double step_us =
+        T == 256 ? cvl_env_int("CVL_WGX_STEP", 80) / 100.0 : cvl_env_int("CVL_WGX_STEP128", 30) / 100.0;
+    const double slab_us = (double)T * T * 4 * 2 / 5.0e6 * cvl_env_int("CVL_WGX_SLAB_PCT", 100) / 100.0;
+    int max_s = mg / 512;
+    if (max_s < 1) max_s = 1;
+    if (max_s > 2048 / tg) max_s = 2048 / tg > 1 ? 2048 / tg : 1;
+    const int per_round = T == 256 ? 256 : 512;   // the 128-wide tile (80 KiB of LDS) runs 2 per CU
+    for (int s = 1; s <= max_s; ++s) {
+      const int rounds = (tg * s + per_round - 1) / per_round;
+      const int chunk = ((mg + s - 1) / s + SEGM - 1) / SEGM * SEGM;
+      const double t = rounds * (chunk / BR) * step_us + (s > 1 ? tg * s * slab_us : 0.0);
+      if (t < best_t) { best_t = t; best_s = s; best_T = T; }
+    }
   }
+  if (!best_T) return false;
+  p->T = best_T;
+  p->co_tiles = a->Npad / best_T;
+  p->tiles = p->co_tiles * ((a->K + best_T - 1) / best_T);
   const int forced = cvl_env_int("CVL_WGX_SPLITS", 0);
   if (forced > 0) best_s = forced;
   p->chunk = ((mg + best_s - 1) / best_s + SEGM - 1) / SEGM * SEGM;
@@ -358,7 +383,8 @@ int cvl_conv_wgrad_x(const cvl_conv_desc* d, int ngroups, const void* x, const v
     g.out[gq] = g.direct ? dw[gs] : reinterpret_cast<float*>(workspace) + gs * per_group;
   }
   g_cvl_conv_last_kernel = CVL_CK_WG_X;
-  hipLaunchKernelGGL(conv_wgrad_x_kernel, dim3(p.tiles * p.nsplit * ngroups), dim3(NT), 0, s, g);
+  if (p.T == 256) hipLaunchKernelGGL(conv_wgrad_x_kernel<256>, dim3(p.tiles * p.nsplit * ngroups), dim3(NT), 0, s, g);
+  else hipLaunchKernelGGL(conv_wgrad_x_kernel<128>, dim3(p.tiles * p.nsplit * ngroups), dim3(NT), 0, s, g);
   int st = cvl_launch_status();
   if (st || g.direct) return st;
   const long n4 = (long)g.a.K * g.Cout / 4;
