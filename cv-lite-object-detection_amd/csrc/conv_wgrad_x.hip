@@ -287,7 +287,9 @@ struct WxPlan {
 
 // Modelled time of s splits at tile width T: rounds of 256 workgroups (one per CU; 512 for T = 128) x 32-row steps
 // per chunk (CVL_WGX_STEP, 0.01 us; ~0.8 us measured on the tower shape; CVL_WGX_STEP128 for the
-// 128-wide tile, a quarter of the MFMA work per step) + the fp32 slab round trip.  The 128-wide tile
+// 128-wide tile: also ~0.8 us measured -- two per CU, the step is bound by its DMA / barrier
+// overheads, not its MFMA work: the tower at 0.3 us picked 128 and took 323 us vs 232) + the fp32
+// slab round trip.  The 128-wide tile
 // serves the 1x1 / small-output launches (e.g. 1x1 256->1024 @ 32x32: 4 tiles of 256 -> 64 splits,
 // 64 MiB of slabs; 16 tiles of 128 -> 16 splits, 16 MiB).
 // K below one 256-deep tile (1x1 convs with Cin 128) leaves half of every 256 tile idle.
@@ -322,7 +324,7 @@ inline bool wx_plan(const cvl_conv_desc* d, int ngroups, ConvArgs* a, WxPlan* p)
       continue;
     const int tg = (a->Npad / T) * ((a->K + T - 1) / T) * ngroups;
     const double step_us =
-        T == 256 ? cvl_env_int("CVL_WGX_STEP", 80) / 100.0 : cvl_env_int("CVL_WGX_STEP128", 30) / 100.0;
+        T == 256 ? cvl_env_int("CVL_WGX_STEP", 80) / 100.0 : cvl_env_int("CVL_WGX_STEP128", 80) / 100.0;
     const double slab_us = (double)T * T * 4 * 2 / 5.0e6 * cvl_env_int("CVL_WGX_SLAB_PCT", 100) / 100.0;
     int max_s = mg / 512;
     if (max_s < 1) max_s = 1;
