@@ -111,7 +111,7 @@ def measure_tower_conv(net, B, H, W, iters=20):
     return ms, flops, kname
 
 
-def measure_backbone_3x3(net, B, H, W, iters=20):
+def measure_backbone_3x3(net, B, H, W, iters=20, eager=False):
     """roofline.backbone_3x3: the 16 ResNet-50 3x3 convs (conv2_x..conv5_x units' `_2_conv`, the
     shapes north_star names) -- forward (with the BN statistics the step forms), data gradient
     (with the conv1 unit's fused BN-backward first pass, as the step runs it) and weight gradient,
@@ -134,6 +134,11 @@ def measure_backbone_3x3(net, B, H, W, iters=20):
         for _ in range(3):
             fn()
         kname = L.cvl_conv_kernel_name(L.cvl_conv_igemm_last_kernel()).decode()
+        if eager:                                  # (counter collection: plain launches)
+            for _ in range(iters):
+                fn()
+            torch.cuda.synchronize()
+            return float("nan"), kname
         g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g):
             for _ in range(iters):
@@ -185,7 +190,7 @@ def measure_backbone_3x3(net, B, H, W, iters=20):
                       "counts from the ResNet-50 stage depths (3/4/6/3)", "per_shape": rows}
 
 
-PMC_FILE = "profiles/r02k_pmc_tower_conv.json"
+PMC_FILE = "profiles/r03c_pmc_tower_conv.json"
 
 
 def pmc_traffic(kname):
@@ -461,7 +466,7 @@ def main():
         "roofline": {"bound": "mfma", "achieved": round(achieved, 2), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
                      "frac": round(achieved / PEAK_BF16_TFLOPS, 4), "traffic": pmc_traffic(k_name),
                      "traffic_note": "HBM bytes per launch from rocprofv3 --pmc FETCH_SIZE (x2, gfx950) + "
-                                     "WRITE_SIZE, separate passes (tools/pmc_tower.sh -> %s); algorithmic "
+                                     "WRITE_SIZE, separate passes (tools/pmc3.sh -> %s); algorithmic "
                                      "bytes per launch %d (src + dst bf16 + weights)" % (PMC_FILE, tower_alg_bytes(B, net, H, W)),
                      "kernel": "%s, fwd: FCOS cls+reg tower layer 3x3 256->256 over all 5 levels, one "
                                "10-segment launch (M=%d, N=256, K=2304)" % (k_name, 2 * B * net.layout(B, H, W)[2]),

@@ -16,7 +16,7 @@ from cvlite.fcos_net import FCOSNet  # noqa: E402
 def main():
     iters = int(sys.argv[1]) if len(sys.argv) > 1 else 8
     net = FCOSNet(bench.NUM_CLASSES, device=torch.device("cuda", 0), seed=0)
-    r = bench.measure_backbone_3x3(net, 16, 512, 512, iters=iters)
+    r = bench.measure_backbone_3x3(net, 16, 512, 512, iters=iters, eager=True)
     for row in r["per_shape"]:
         print(row)
     print("backbone_3x3 frac", r["frac"], "ms/step", r["ms_per_step"])
