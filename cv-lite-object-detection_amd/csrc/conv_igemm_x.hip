@@ -643,7 +643,8 @@ __global__ void __launch_bounds__(NT) conv_igemm_x32h_kernel(ConvArgs a) {
   int rslot = 0;
   for (int cb = 0; cb < ((dbg & 256) ? 0 : ncb); ++cb) {
     const char* Hc = reinterpret_cast<const char*>(hb0 + (cb & 1) * HBUF);
-#pragma unroll 1
+    // the nine taps unrolled: every wait count / halo piece / read offset is a compile-time choice
+#pragma unroll
     for (int r = 0; r < 3; ++r) {
       const int dyoff = (DGRAD ? 1 - r : r - 1) * prow;
 #pragma unroll
