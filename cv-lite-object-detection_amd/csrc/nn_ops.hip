@@ -319,9 +319,12 @@ __global__ void __launch_bounds__(NT) bn_apply_kernel(const cvl_bf16* __restrict
       bn_moments(fin.stats[bc * 2], fin.stats[bc * 2 + 1], HW, fin.eps, &mm, &rr, &var);
       smr[c] = float2{mm, rr};
       if (blockIdx.x == 0) { fin.mr_out[bc * 2] = mm; fin.mr_out[bc * 2 + 1] = rr; }
-      if (blockIdx.x == 0 && b == 0 && fin.run_mean)
-        bn_running(fin.stats, gridDim.y, C, c, HW, fin.eps, fin.momentum, fin.run_mean, fin.run_var);
     }
+    // running statistics: one channel per thread over the image-0 blocks (a serial float64 chain
+    // over the images -- in one block it was the critical path of the small launches)
+    if (b == 0 && fin.run_mean)
+      for (int c = blockIdx.x * NT + threadIdx.x; c < C; c += gridDim.x * NT)
+        bn_running(fin.stats, gridDim.y, C, c, HW, fin.eps, fin.momentum, fin.run_mean, fin.run_var);
     __syncthreads();
   }
   if (rsub >= rpp) return;
@@ -390,7 +393,10 @@ inline int bn_rows_per_blk(int B, int HW, int C) {
 // part[b][chunk][C][2]; small follow-up kernels reduce them in a fixed order (deterministic).
 // PASS 0: (sum g, sum g*xhat), g = dy * (y > 0 if relu).
 // PASS 1: dz = gamma*rstd*(g - mean(g) - xhat*mean(g*xhat)) (+ g_out = g).
-constexpr int BN_UNR = 4;
+#ifndef BN_UNR_V
+#define BN_UNR_V 4
+#endif
+constexpr int BN_UNR = BN_UNR_V;
 
 // parameter gradients folded into pass 1 (block (0, 0), one thread per channel, images in order,
 // float64): dgamma[c] = beta_acc*dgamma + sum_b sum g*xhat ; dbeta[c] = ... + sum_b sum g ;
@@ -405,7 +411,10 @@ struct BnPG {
   const double* psums;    // per-image sums for the parameter gradients (nullptr: `sums`)
 };
 
-template <int PASS>
+// MASK selects the ReLU-mask source at compile time (1: y, 2: bn_affine(z) recomputed; 0: decided at
+// run time from y / bnb) -- the run-time form holds the registers of both paths (pass 0: 215 VGPRs,
+// 2 waves/SIMD; pass 1: 141, 3 waves), the specialised ones fit 4-5 waves
+template <int PASS, int MASK = 0>
 __global__ void __launch_bounds__(NT) bn_bwd_kernel(const cvl_bf16* __restrict__ dy, const cvl_bf16* __restrict__ y,
                                                     const cvl_bf16* __restrict__ z, const float* __restrict__ mr,
                                                     const float* __restrict__ gamma, const double* __restrict__ sums,
@@ -425,9 +434,9 @@ __global__ void __launch_bounds__(NT) bn_bwd_kernel(const cvl_bf16* __restrict__
   const int gsz = min(g0 + group, (int)gridDim.y) - g0;
   const float inv = 1.0f / ((float)HW * (float)gsz);
   __shared__ float red[NT][17];
-  if (PASS == 1 && pg.dgamma && blockIdx.x == 0 && b == 0) {
+  if (PASS == 1 && pg.dgamma && b == 0) {          // spread over the image-0 blocks, a channel per thread
     const double* ps = pg.psums ? pg.psums : sums;
-    for (int c = threadIdx.x; c < C; c += NT) {
+    for (int c = blockIdx.x * NT + threadIdx.x; c < C; c += gridDim.x * NT) {
       if (pg.conv_dbias) pg.conv_dbias[c] = 0.f;
       double a1 = 0.0, a2 = 0.0;
 #pragma unroll 8
@@ -449,7 +458,8 @@ __global__ void __launch_bounds__(NT) bn_bwd_kernel(const cvl_bf16* __restrict__
     float m[8], rs[8], s1[8], s2[8], k1[8], k2[8], gm[8], ga[8], be[8];
     // mask source: y (relu output, residual units) or, when y is null and bnb is given, the
     // ReLU of bn_affine(z) recomputed (non-residual units: one tensor fewer to read)
-    const bool zmask = PASS != 2 && !y && bnb;
+    const bool use_y = PASS != 2 && (MASK == 0 ? y != nullptr : MASK == 1);
+    const bool zmask = PASS != 2 && (MASK == 0 ? (!y && bnb) : MASK == 2);
 #pragma unroll
     for (int u = 0; u < 8; ++u) {
       const long bc = (long)b * C + c0 + u;
@@ -475,7 +485,7 @@ __global__ void __launch_bounds__(NT) bn_bwd_kernel(const cvl_bf16* __restrict__
           off[q] = ((long)b * HW + rq) * C + c0;
           vg[q] = *reinterpret_cast<const s16x8*>(dy + off[q]);
           if (PASS != 2) vz[q] = *reinterpret_cast<const s16x8*>(z + off[q]);
-          if (y) vy[q] = *reinterpret_cast<const s16x8*>(y + off[q]);
+          if (use_y) vy[q] = *reinterpret_cast<const s16x8*>(y + off[q]);
         }
 #pragma unroll
         for (int q = 0; q < BN_UNR; ++q) {
@@ -490,7 +500,7 @@ __global__ void __launch_bounds__(NT) bn_bwd_kernel(const cvl_bf16* __restrict__
             continue;
           }
           unpack8(vz[q], zz);
-          if (y) {
+          if (use_y) {
             float yy[8];
             unpack8(vy[q], yy);
 #pragma unroll
@@ -1282,14 +1292,19 @@ static int bn_backward_impl(const void* dy, const void* y_relu, const float* bn_
     return cvl_launch_status();
   }
   dim3 g1(nchunk, B);
-  hipLaunchKernelGGL(bn_bwd_kernel<0>, g1, dim3(NT), 0, S_, (const cvl_bf16*)dy, (const cvl_bf16*)y_relu,
+  const bool ym = y_relu != nullptr, zm = !ym && bn_beta != nullptr;
+  auto k0 = ym ? bn_bwd_kernel<0, 1> : zm ? bn_bwd_kernel<0, 2> : bn_bwd_kernel<0, 0>;
+  auto k1 = ym ? bn_bwd_kernel<1, 1> : zm ? bn_bwd_kernel<1, 2> : bn_bwd_kernel<1, 0>;
+  hipLaunchKernelGGL(k0, g1, dim3(NT), 0, S_, (const cvl_bf16*)dy, (const cvl_bf16*)y_relu,
                      (const cvl_bf16*)z, mean_rstd, gamma, (const double*)nullptr, (cvl_bf16*)nullptr,
                      (cvl_bf16*)nullptr, part0, C, HW, rpb, 1, 0.f, BnPG{}, bn_beta, act_hi);
   hipLaunchKernelGGL(bn_colsum_kernel, dim3((C + 31) / 32, B), dim3(NT), 0, S_, (const float*)part0, nchunk, C,
                      sums);
-  hipLaunchKernelGGL(bn_bwd_kernel<1>, g1, dim3(NT), 0, S_, (const cvl_bf16*)dy, (const cvl_bf16*)y_relu,
+  // pass 1 is elementwise (no partials): the apply kernels' finer chunking (~2048 workgroups)
+  const int rpb1 = bn_rows_per_blk(B, HW, C);
+  hipLaunchKernelGGL(k1, dim3((HW + rpb1 - 1) / rpb1, B), dim3(NT), 0, S_, (const cvl_bf16*)dy, (const cvl_bf16*)y_relu,
                      (const cvl_bf16*)z, mean_rstd, gamma, (const double*)sums, (cvl_bf16*)dz, (cvl_bf16*)g_out,
-                     (float*)nullptr, C, HW, rpb, 1, 0.f, BnPG{dgamma, dbeta, conv_dbias, beta_acc}, bn_beta,
+                     (float*)nullptr, C, HW, rpb1, 1, 0.f, BnPG{dgamma, dbeta, conv_dbias, beta_acc}, bn_beta,
                      act_hi);
   return cvl_launch_status();
 }
@@ -1329,9 +1344,9 @@ extern "C" int cvl_bn_backward_relu_sums(const void* dy, const void* z, const fl
                                          int HW, int C, cvl_stream_t stream) {
   CVL_CHECK_ARG(dy && z && mean_rstd && gamma && beta && sums && dz && dgamma && dbeta && C % 8 == 0);
   CVL_CHECK_ARG(B > 0 && HW > 0);
-  const int rpb = bn_bwd_rows_per_blk(B, HW, C);
+  const int rpb = bn_rows_per_blk(B, HW, C);
   const int nchunk = (HW + rpb - 1) / rpb;
-  hipLaunchKernelGGL(bn_bwd_kernel<1>, dim3(nchunk, B), dim3(NT), 0, S_, (const cvl_bf16*)dy, (const cvl_bf16*)nullptr,
+  hipLaunchKernelGGL((bn_bwd_kernel<1, 2>), dim3(nchunk, B), dim3(NT), 0, S_, (const cvl_bf16*)dy, (const cvl_bf16*)nullptr,
                      (const cvl_bf16*)z, mean_rstd, gamma, sums, (cvl_bf16*)dz, (cvl_bf16*)nullptr, (float*)nullptr,
                      C, HW, rpb, 1, 0.f, BnPG{dgamma, dbeta, conv_dbias, beta_acc}, beta, act_hi);
   return cvl_launch_status();
