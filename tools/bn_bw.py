@@ -26,6 +26,8 @@ def timeit(fn, reps=20):
 
 shapes = [(16, 16384, 256), (16, 16384, 64), (16, 4096, 512), (16, 4096, 128), (16, 1024, 1024), (16, 65536, 64),
           (16, 256, 2048)]
+if os.environ.get("BNBW_SHAPES"):
+    shapes = [tuple(int(v) for v in t.split("x")) for t in os.environ["BNBW_SHAPES"].split(",")]
 for B, HW, C in shapes:
     n = B * HW * C
     z = torch.randn(n, device=dev).to(BF)
