@@ -254,28 +254,40 @@ __global__ void __launch_bounds__(NT) conv_wgrad_x_kernel(WxArgs g) {
     }
 }
 
-// dW_g = beta * dW_g + sum over splits s (in order) of slab_g[s]; slabs of group g at g * splits * n4
+// dW_g = beta * dW_g + sum over splits s of slab_g[s]; slabs of group g at g * splits * n4.
+// P consecutive lanes share one float4 element: lane j sums the splits j, j + P, ... in order and
+// the P partials are combined by a fixed xor tree (deterministic); P > 1 for the small outputs whose
+// many splits made one thread's serial chain the whole kernel (16 blocks, 14.8 us)
+template <int P>
 __global__ void wgrad_x_reduce_kernel(const float* slab, float* dw0, float* dw1, long n4, int splits, int groups,
                                       float beta) {
-  const long total = n4 * groups;
+  const long total = n4 * groups * P;
   for (long t = blockIdx.x * (long)blockDim.x + threadIdx.x; t < total; t += (long)gridDim.x * blockDim.x) {
-    const int gq = (int)(t / n4);
-    const long i = t - gq * n4;
+    const long e = t / P;
+    const int j = (int)(t % P);
+    const int gq = (int)(e / n4);
+    const long i = e - gq * n4;
     const f32x4* sl = reinterpret_cast<const f32x4*>(slab) + (long)gq * splits * n4;
-    // splits added in order (deterministic); loads 8 at a time so they are in flight together
-    f32x4 s = sl[i];
-    int k = 1;
-    for (; k + 8 <= splits; k += 8) {
+    f32x4 s = f32x4{0.f, 0.f, 0.f, 0.f};
+    int k = j;
+    for (; k + 7 * P < splits; k += 8 * P) {        // 8 loads in flight
       f32x4 v[8];
 #pragma unroll
-      for (int u = 0; u < 8; ++u) v[u] = sl[(long)(k + u) * n4 + i];
+      for (int u = 0; u < 8; ++u) v[u] = sl[(long)(k + u * P) * n4 + i];
 #pragma unroll
       for (int u = 0; u < 8; ++u) s += v[u];
     }
-    for (; k < splits; ++k) s += sl[(long)k * n4 + i];
-    f32x4* d = reinterpret_cast<f32x4*>(gq == 0 ? dw0 : dw1) + i;
-    if (beta != 0.f) s += beta * *d;
-    *d = s;
+    for (; k < splits; k += P) s += sl[(long)k * n4 + i];
+#pragma unroll
+    for (int m = 1; m < P; m <<= 1) {
+#pragma unroll
+      for (int c = 0; c < 4; ++c) s[c] += __shfl_xor(s[c], m);
+    }
+    if (j == 0) {
+      f32x4* d = reinterpret_cast<f32x4*>(gq == 0 ? dw0 : dw1) + i;
+      if (beta != 0.f) s += beta * *d;
+      *d = s;
+    }
   }
 }
 
@@ -318,6 +330,9 @@ inline bool wx_plan(const cvl_conv_desc* d, int ngroups, ConvArgs* a, WxPlan* p)
   const int forced_t = cvl_env_int("CVL_WGX_T", 0);
   double best_t = 1e30;
   int best_s = 0, best_T = 0;
+  int s256 = 0, tg256 = 0;
+  double t128 = 1e30;
+  int s128 = 0;
   for (int T = 256; T >= 128; T /= 2) {
     if (forced_t && forced_t != T) continue;
     if (a->Npad % T || a->K < cvl_env_int(T == 256 ? "CVL_WGX_MIN_K" : "CVL_WGX_MIN_K128", T == 256 ? 256 : 64))
@@ -335,7 +350,17 @@ inline bool wx_plan(const cvl_conv_desc* d, int ngroups, ConvArgs* a, WxPlan* p)
       const int chunk = ((mg + s - 1) / s + SEGM - 1) / SEGM * SEGM;
       const double t = rounds * (chunk / BR) * step_us + (s > 1 ? tg * s * slab_us : 0.0);
       if (t < best_t) { best_t = t; best_s = s; best_T = T; }
+      if (T == 256 && best_T == 256) { s256 = best_s; tg256 = tg; }
+      if (T == 128 && t < t128) { t128 = t; s128 = s; }
     }
+  }
+  // a 256-wide plan that cannot occupy every CU (tiles x splits < 256: the 1x1 / small-output
+  // launches, capped by the 512-row minimum chunk) loses to the 128-wide one in the per-shape
+  // sweep (1x1 256->1024 @ 32x32: 38 -> 31 us; 3x3 s2 2048->256 @ 8x8: 45 -> 34 us); the tower
+  // (18 tiles x 14 splits) keeps 256 (230 vs 322 us)
+  if (best_T == 256 && s128 && tg256 * s256 < 240 && !cvl_env_flag("CVL_WGX_KEEP256")) {
+    best_T = 128;
+    best_s = s128;
   }
   if (!best_T) return false;
   p->T = best_T;
@@ -390,9 +415,14 @@ int cvl_conv_wgrad_x(const cvl_conv_desc* d, int ngroups, const void* x, const v
   int st = cvl_launch_status();
   if (st || g.direct) return st;
   const long n4 = (long)g.a.K * g.Cout / 4;
-  long blocks = (n4 * ngroups + 255) / 256;
+  // lanes per element: grow while the grid stays under ~64K threads and each lane keeps >= 4 splits
+  int P = 1;
+  while (P < 16 && n4 * ngroups * P * 2 <= 65536 && p.nsplit >= 8 * P) P *= 2;
+  long blocks = (n4 * ngroups * P + 255) / 256;
   blocks = blocks > 4096 ? 4096 : blocks;
-  hipLaunchKernelGGL(wgrad_x_reduce_kernel, dim3((int)blocks), dim3(256), 0, s, (const float*)workspace, dw[0],
+  auto rk = P == 1 ? wgrad_x_reduce_kernel<1> : P == 2 ? wgrad_x_reduce_kernel<2> : P == 4 ? wgrad_x_reduce_kernel<4>
+          : P == 8 ? wgrad_x_reduce_kernel<8> : wgrad_x_reduce_kernel<16>;
+  hipLaunchKernelGGL(rk, dim3((int)blocks), dim3(256), 0, s, (const float*)workspace, dw[0],
                      ngroups > 1 ? dw[1] : dw[0], n4, p.nsplit, ngroups, beta);
   return cvl_launch_status();
 }
