@@ -721,6 +721,8 @@ inline int bn_bwd_rows_per_blk(int B, int HW, int C) {
 // max-pool 3x3 / 2 after ZeroPadding2D(1) (Keras ResNet50 pool1): zero padding is a real input
 // value; the gradient goes to the first maximum in row-major window order (TF MaxPoolGrad).
 // ---------------------------------------------------------------------------------------------
+// a thread owns 8 channels of one output pixel: the 9 window loads are issued together (padding
+// taps load a clamped in-range pixel and select 0), the 8 argmax bytes leave as one 8-byte store
 __global__ void maxpool_fwd_kernel(const cvl_bf16* x, cvl_bf16* y, uint8_t* arg, int B, int H, int W,
                                    int C, int Ho, int Wo) {
   const int C8 = C / 8;
@@ -731,29 +733,39 @@ __global__ void maxpool_fwd_kernel(const cvl_bf16* x, cvl_bf16* y, uint8_t* arg,
     const int b = (int)(pix / ((long)Ho * Wo));
     const int q = (int)(pix - (long)b * Ho * Wo);
     const int oy = q / Wo, ox = q - (q / Wo) * Wo;
-    float best[8];
-    uint8_t bi[8];
+    s16x8 raw[9];
+    bool ok[9];
 #pragma unroll
-    for (int u = 0; u < 8; ++u) { best[u] = -INFINITY; bi[u] = 0; }
     for (int t = 0; t < 9; ++t) {
       const int iy = oy * 2 - 1 + t / 3, ix = ox * 2 - 1 + t % 3;
+      ok[t] = iy >= 0 && ix >= 0 && iy < H && ix < W;
+      const int cy = min(max(iy, 0), H - 1), cx = min(max(ix, 0), W - 1);
+      raw[t] = *reinterpret_cast<const s16x8*>(x + (((long)b * H + cy) * W + cx) * C + c0);
+    }
+    float best[8];
+    unsigned long long bi = 0;
+#pragma unroll
+    for (int u = 0; u < 8; ++u) best[u] = -INFINITY;
+#pragma unroll
+    for (int t = 0; t < 9; ++t) {
       float v[8];
-      if (iy >= 0 && ix >= 0 && iy < H && ix < W) {
-        unpack8(*reinterpret_cast<const s16x8*>(x + (((long)b * H + iy) * W + ix) * C + c0), v);
-      } else {
+      unpack8(raw[t], v);
 #pragma unroll
-        for (int u = 0; u < 8; ++u) v[u] = 0.f;
+      for (int u = 0; u < 8; ++u) {
+        const float vv = ok[t] ? v[u] : 0.f;
+        if (vv > best[u]) {
+          best[u] = vv;
+          bi = (bi & ~(0xffull << (8 * u))) | ((unsigned long long)t << (8 * u));
+        }
       }
-#pragma unroll
-      for (int u = 0; u < 8; ++u)
-        if (v[u] > best[u]) { best[u] = v[u]; bi[u] = (uint8_t)t; }
     }
     *reinterpret_cast<s16x8*>(y + pix * C + c0) = pack8(best);
-#pragma unroll
-    for (int u = 0; u < 8; ++u) arg[pix * C + c0 + u] = bi[u];
+    *reinterpret_cast<unsigned long long*>(arg + pix * C + c0) = bi;
   }
 }
 
+// a thread owns 8 channels of one input pixel: the (at most 2 x 2) windows holding it are visited
+// with their dy and argmax bytes (one 8-byte load) loaded together
 __global__ void maxpool_bwd_kernel(const cvl_bf16* dy, const uint8_t* arg, cvl_bf16* dx, int B, int H,
                                    int W, int C, int Ho, int Wo) {
   const int C8 = C / 8;
@@ -764,18 +776,29 @@ __global__ void maxpool_bwd_kernel(const cvl_bf16* dy, const uint8_t* arg, cvl_b
     const int b = (int)(pix / ((long)H * W));
     const int q = (int)(pix - (long)b * H * W);
     const int iy = q / W, ix = q - (q / W) * W;
-    float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
     // outputs whose window [2o-1, 2o+1] contains (iy, ix): o in [i>>1, (i+1)>>1]
-    for (int oy = iy >> 1; oy <= ((iy + 1) >> 1) && oy < Ho; ++oy) {
-      for (int ox = ix >> 1; ox <= ((ix + 1) >> 1) && ox < Wo; ++ox) {
-        const int t = (iy - (oy * 2 - 1)) * 3 + (ix - (ox * 2 - 1));
-        const long o = (((long)b * Ho + oy) * Wo + ox) * C + c0;
-        float g[8];
-        unpack8(*reinterpret_cast<const s16x8*>(dy + o), g);
+    const int oy0 = iy >> 1, ox0 = ix >> 1;
+    s16x8 g[4];
+    unsigned long long am[4];
+    bool ok[4];
 #pragma unroll
-        for (int u = 0; u < 8; ++u)
-          if (arg[o + u] == t) acc[u] += g[u];
-      }
+    for (int k = 0; k < 4; ++k) {
+      const int oy = oy0 + (k >> 1), ox = ox0 + (k & 1);
+      ok[k] = oy <= ((iy + 1) >> 1) && oy < Ho && ox <= ((ix + 1) >> 1) && ox < Wo;
+      const long o = (((long)b * Ho + min(oy, Ho - 1)) * Wo + min(ox, Wo - 1)) * C + c0;
+      g[k] = *reinterpret_cast<const s16x8*>(dy + o);
+      am[k] = *reinterpret_cast<const unsigned long long*>(arg + o);
+    }
+    float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {       // window order (oy, ox) row-major, as before
+      const int oy = oy0 + (k >> 1), ox = ox0 + (k & 1);
+      const unsigned t = (unsigned)((iy - (oy * 2 - 1)) * 3 + (ix - (ox * 2 - 1)));
+      float gv[8];
+      unpack8(g[k], gv);
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+        if (ok[k] && ((am[k] >> (8 * u)) & 0xff) == t) acc[u] += gv[u];
     }
     *reinterpret_cast<s16x8*>(dx + pix * C + c0) = pack8(acc);
   }
@@ -1048,9 +1071,27 @@ inline bool bias_multi_plan(const cvl_bias_item* items, int n, BiasMulti* m, lon
 // ---------------------------------------------------------------------------------------------
 // optimizer: clip_by_global_norm(g * inv_bs, clip) + Keras SGD momentum, flat fp32 buffers
 // ---------------------------------------------------------------------------------------------
-__global__ void sumsq_kernel(const float* g, long n, double* out) {
+// global gradient norm, deterministic: every block writes its float64 partial to ws[1 + block]
+// (16-B loads, 4 in flight per thread), sumsq_final_kernel adds them in block order into ws[0]
+// (the former single fp64 atomic per block made the sum order -- and its last bits -- vary)
+constexpr int SQ_BLOCKS = CVL_SUMSQ_WS - 1;
+__global__ void __launch_bounds__(NT) sumsq_kernel(const float* __restrict__ g, long n, double* __restrict__ ws) {
   float s = 0.f;
-  for (long i = blockIdx.x * (long)NT + threadIdx.x; i < n; i += (long)gridDim.x * NT) s += g[i] * g[i];
+  const long n4 = n / 4, stride = (long)gridDim.x * NT;
+  const f32x4* g4 = reinterpret_cast<const f32x4*>(g);
+  long i = blockIdx.x * (long)NT + threadIdx.x;
+  for (; i + 3 * stride < n4; i += 4 * stride) {
+    f32x4 v[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) v[u] = g4[i + u * stride];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) s += v[u][0] * v[u][0] + v[u][1] * v[u][1] + v[u][2] * v[u][2] + v[u][3] * v[u][3];
+  }
+  for (; i < n4; i += stride) {
+    const f32x4 v = g4[i];
+    s += v[0] * v[0] + v[1] * v[1] + v[2] * v[2] + v[3] * v[3];
+  }
+  if (blockIdx.x == 0 && threadIdx.x < (int)(n - n4 * 4)) s += g[n4 * 4 + threadIdx.x] * g[n4 * 4 + threadIdx.x];
   double d = warp_sum_d((double)s);
   __shared__ double red[NT / 64];
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = d;
@@ -1058,17 +1099,45 @@ __global__ void sumsq_kernel(const float* g, long n, double* out) {
   if (threadIdx.x == 0) {
     double t = 0.0;
     for (int k = 0; k < NT / 64; ++k) t += red[k];
-    atomicAdd(out, t);
+    ws[1 + blockIdx.x] = t;
   }
 }
 
-__global__ void sgd_kernel(float* w, const float* g, float* v, long n, const float* lr_dev,
-                           float momentum, float inv_bs, float clip, const double* gsumsq) {
+__global__ void __launch_bounds__(64) sumsq_final_kernel(double* ws, int nblk) {
+  double t = 0.0;
+  for (int k = threadIdx.x; k < nblk; k += 64) t += ws[1 + k];
+  t = warp_sum_d(t);
+  if (threadIdx.x == 0) ws[0] = t;
+}
+
+// 16-B lanes; sgd_tail_kernel covers the n % 4 last elements
+__global__ void __launch_bounds__(NT) sgd_kernel(float* __restrict__ w, const float* __restrict__ g,
+                                                 float* __restrict__ v, long n4, const float* lr_dev,
+                                                 float momentum, float inv_bs, float clip, const double* gsumsq) {
   // gsumsq holds sum((g)^2) of the UNscaled grads: norm of (g * inv_bs) = sqrt(gsumsq) * inv_bs
   const double norm = sqrt(*gsumsq) * (double)inv_bs;
   const float scale = inv_bs * (float)(clip > 0.f ? (double)clip / (norm > clip ? norm : (double)clip) : 1.0);
   const float lr = *lr_dev;
-  for (long i = blockIdx.x * (long)NT + threadIdx.x; i < n; i += (long)gridDim.x * NT) {
+  f32x4* w4 = reinterpret_cast<f32x4*>(w);
+  f32x4* v4 = reinterpret_cast<f32x4*>(v);
+  const f32x4* g4 = reinterpret_cast<const f32x4*>(g);
+  for (long i = blockIdx.x * (long)NT + threadIdx.x; i < n4; i += (long)gridDim.x * NT) {
+    const f32x4 gg = g4[i] * scale, vo = v4[i], wo = w4[i];
+    f32x4 vv;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) vv[e] = momentum * vo[e] - lr * gg[e];
+    v4[i] = vv;
+    w4[i] = wo + vv;
+  }
+}
+
+__global__ void sgd_tail_kernel(float* w, const float* g, float* v, long n0, long n, const float* lr_dev,
+                                float momentum, float inv_bs, float clip, const double* gsumsq) {
+  const double norm = sqrt(*gsumsq) * (double)inv_bs;
+  const float scale = inv_bs * (float)(clip > 0.f ? (double)clip / (norm > clip ? norm : (double)clip) : 1.0);
+  const float lr = *lr_dev;
+  const long i = n0 + threadIdx.x;
+  if (i < n) {
     const float gg = g[i] * scale;
     const float vv = momentum * v[i] - lr * gg;
     v[i] = vv;
@@ -1452,11 +1521,17 @@ extern "C" int cvl_sgd_clip_update(float* w, const float* g, float* v, int64_t n
                                    float momentum, float inv_bs, float clip, double* sumsq_ws,
                                    cvl_stream_t stream) {
   CVL_CHECK_ARG(w && g && v && n > 0 && lr_dev && sumsq_ws);
-  hipError_t e = hipMemsetAsync(sumsq_ws, 0, sizeof(double), S_);
-  if (e != hipSuccess) return CVL_EHIP + (int)e;
-  hipLaunchKernelGGL(sumsq_kernel, dim3(grid_for(n, NT * 8, 2048)), dim3(NT), 0, S_, g, (long)n, sumsq_ws);
-  hipLaunchKernelGGL(sgd_kernel, dim3(grid_for(n, NT * 4, 4096)), dim3(NT), 0, S_, w, g, v, (long)n, lr_dev,
-                     momentum, inv_bs, clip, (const double*)sumsq_ws);
+  CVL_CHECK_ARG(((uintptr_t)w | (uintptr_t)g | (uintptr_t)v) % 16 == 0);
+  const int nb = grid_for(n / 4 > 0 ? n / 4 : 1, NT * 4, SQ_BLOCKS);
+  hipLaunchKernelGGL(sumsq_kernel, dim3(nb), dim3(NT), 0, S_, g, (long)n, sumsq_ws);
+  hipLaunchKernelGGL(sumsq_final_kernel, dim3(1), dim3(64), 0, S_, sumsq_ws, nb);
+  const long n4 = n / 4;
+  if (n4 > 0)
+    hipLaunchKernelGGL(sgd_kernel, dim3(grid_for(n4, NT * 4, 4096)), dim3(NT), 0, S_, w, g, v, n4, lr_dev,
+                       momentum, inv_bs, clip, (const double*)sumsq_ws);
+  if (n % 4)
+    hipLaunchKernelGGL(sgd_tail_kernel, dim3(1), dim3(64), 0, S_, w, g, v, n4 * 4, (long)n, lr_dev, momentum,
+                       inv_bs, clip, (const double*)sumsq_ws);
   return cvl_launch_status();
 }
 

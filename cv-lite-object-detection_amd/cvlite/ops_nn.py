@@ -338,9 +338,13 @@ def bias_grad_multi(items):
         _lib.call("cvl_bias_grad_multi", arr, len(chunk), ptr(ws), ws.numel(), stream())
 
 
+SUMSQ_WS = 1025     # include/cvlite.h CVL_SUMSQ_WS: norm total + per-block partials (float64)
+
+
 def sgd_clip_update(w, g, v, lr_dev, momentum, inv_bs, clip, ws=None):
     if ws is None:
-        ws = torch.empty(1, dtype=torch.float64, device=w.device)
+        ws = torch.empty(SUMSQ_WS, dtype=torch.float64, device=w.device)
+    assert ws.numel() >= SUMSQ_WS
     _lib.call("cvl_sgd_clip_update", ptr(w), ptr(g), ptr(v), w.numel(), ptr(lr_dev), float(momentum),
               float(inv_bs), float(clip), ptr(ws), stream())
 

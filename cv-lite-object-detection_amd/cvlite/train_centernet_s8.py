@@ -51,7 +51,7 @@ class S8Trainer(GraphStepper):
         self.d_cls = torch.zeros((B, self.P, net.cls_ld), dtype=torch.bfloat16, device=dev)
         self.losses = torch.zeros((B, 2), dtype=torch.float32, device=dev)
         self.lr = torch.tensor([init_lr], dtype=torch.float32, device=dev)
-        self.sumsq = torch.zeros(1, dtype=torch.float64, device=dev)
+        self.sumsq = torch.zeros(nn.SUMSQ_WS, dtype=torch.float64, device=dev)
         self._init_stepper(net, world, use_graph)
 
     skip_assign = False         # True: targets are loaded pre-formatted (train_step's `bboxes`)

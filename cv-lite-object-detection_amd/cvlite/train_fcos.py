@@ -95,7 +95,7 @@ class FCOSTrainer(GraphStepper):
         else:
             self.lr = torch.tensor([init_lr], dtype=torch.float32, device=dev)
         self.step_dev = torch.tensor([st_step], dtype=torch.int32, device=dev)
-        self.sumsq = torch.zeros(1, dtype=torch.float64, device=dev)
+        self.sumsq = torch.zeros(nn.SUMSQ_WS, dtype=torch.float64, device=dev)
         self._init_stepper(net, world, use_graph)
 
     # ---- the two device phases -------------------------------------------------------------------
@@ -177,7 +177,7 @@ class JitterFCOSTrainer(object):
         self.acc = torch.zeros_like(net.store.grad)
         self.lr = torch.tensor([init_lr], dtype=torch.float32, device=dev)
         self.step_dev = torch.tensor([st_step], dtype=torch.int32, device=dev)
-        self.sumsq = torch.zeros(1, dtype=torch.float64, device=dev)
+        self.sumsq = torch.zeros(nn.SUMSQ_WS, dtype=torch.float64, device=dev)
         self.losses = torch.zeros((batch_size, 3), dtype=torch.float32, device=dev)
         self.ntgt = torch.zeros((batch_size, 5), dtype=torch.int32, device=dev)
 

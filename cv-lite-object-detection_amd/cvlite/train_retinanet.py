@@ -59,7 +59,7 @@ class RetinaTrainer(GraphStepper):
         self.losses = torch.zeros((B, 2), dtype=torch.float32, device=dev)
         self.lr = torch.tensor([init_lr], dtype=torch.float32, device=dev)
         self.step_dev = torch.tensor([st_step], dtype=torch.int32, device=dev)
-        self.sumsq = torch.zeros(1, dtype=torch.float64, device=dev)
+        self.sumsq = torch.zeros(nn.SUMSQ_WS, dtype=torch.float64, device=dev)
         self._init_stepper(net, world, use_graph)
 
     def _fwd_bwd(self, hook=None):

@@ -342,12 +342,14 @@ int cvl_retina_loss_f32(const float* reg_pred, int ld_reg, const float* cls_pred
 /* ------------------------------------------------------------------------------------------
  * Optimizer (train_fcos.py:179-185): g <- (g * inv_bs) clipped by global norm `clip`
  * (tf.clip_by_global_norm), then Keras SGD momentum v = m*v - lr*g; w += v.  Flat fp32 buffers;
- * lr read from device memory (graph-capturable); sumsq_ws: one float64.
+ * lr read from device memory (graph-capturable); sumsq_ws: CVL_SUMSQ_WS float64 (total + the
+ * per-block partials of the deterministic norm reduction); w / g / v 16-byte aligned.
  * cvl_lr_schedule: lr = max(init*rate^floor(step/decay_step), min_lr); step += 1 (device ints).
  * cvl_lr_schedule_capped: the same with the exponent capped at max_decays (>= 0): the centre
  * variants' step schedule (FCOS/train_fcos_center_voc.py:150-157: init_lr below step 8000, init/10
  * from then on -- its init/100 branch is unreachable) is rate 0.1, decay_step 8000, max_decays 1.
  * ---------------------------------------------------------------------------------------- */
+#define CVL_SUMSQ_WS 1025
 int cvl_sgd_clip_update(float* w, const float* g, float* v, int64_t n, const float* lr_dev,
                         float momentum, float inv_bs, float clip, double* sumsq_ws, cvl_stream_t stream);
 int cvl_lr_schedule(int32_t* step, float* lr, double init_lr, double min_lr, double decay_rate,

@@ -199,7 +199,7 @@ def test_jitter_buckets_sum_gradients_and_update_once():
     ref.store.grad.copy_(acc)
     lr = torch.tensor([1e-3], device="cuda")
     nn.sgd_clip_update(ref.store.flat, ref.store.grad, ref.store.mom, lr, 0.9, 1.0 / 3, 1.0,
-                       ws=torch.zeros(1, dtype=torch.float64, device="cuda"))
+                       ws=torch.zeros(nn.SUMSQ_WS, dtype=torch.float64, device="cuda"))
     d_ref, d_jit = ref.store.flat - w0, w_jit - w0
     assert float(d_jit.abs().max()) > 0
     assert float((d_jit - d_ref).norm() / d_ref.norm()) < 1e-4
