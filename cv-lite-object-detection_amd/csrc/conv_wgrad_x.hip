@@ -85,6 +85,7 @@ __global__ void __launch_bounds__(NT) conv_wgrad_x_kernel(WxArgs g) {
   const int rr = C::RPI * wave + lane / C::LPR, pc = lane % C::LPR;
   const int lp = pc ^ (rswz(rr) << 1);                    // logical piece (rswz(rr + 16) == rswz(rr))
   const unsigned ycol = (unsigned)((g.dy_coff + co0 + lp * 8) * 2);
+  const bool yok = co0 + lp * 8 < g.Cout;                 // a 128-wide tile over a 64-channel output
   const int kx = k0 + lp * 8;
   const bool kok = kx < a.K;
   const int tap = kok ? kx / a.Cin : 0;
@@ -135,7 +136,7 @@ __global__ void __launch_bounds__(NT) conv_wgrad_x_kernel(WxArgs g) {
     for (int j = 0; j < J; ++j) {
       const bool rv = live && cml[j] < rows;
       const int drow = dbase + cimg[j] * dimg + coy[j] * Wr + cox[j];
-      dma16(rsY, Yb + (8 * C::RPI * j + C::RPI * wave) * BCO, rv ? (unsigned)(drow * rowb) + ycol : kOOB);
+      dma16(rsY, Yb + (8 * C::RPI * j + C::RPI * wave) * BCO, rv && yok ? (unsigned)(drow * rowb) + ycol : kOOB);
       const int iy = coy[j] * a.stride + ry, ix = cox[j] * a.stride + rx;
       const bool xv = rv && kok && (unsigned)iy < (unsigned)Hs && (unsigned)ix < (unsigned)Ws;
       const int pix = sbase + cimg[j] * simg + iy * Ws + ix;
@@ -308,7 +309,7 @@ struct WxPlan {
 inline bool wx_plan(const cvl_conv_desc* d, int ngroups, ConvArgs* a, WxPlan* p) {
   if (cvl_env_flag("CVL_WGRAD_NO_X")) return false;
   if (cvl_conv_prepare(d, SEGM, a)) return false;
-  if (ngroups < 1 || ngroups > kMaxGroups || d->nseg % ngroups || d->relu_in || a->Npad % 128 || d->Cin % 8 ||
+  if (ngroups < 1 || ngroups > kMaxGroups || d->nseg % ngroups || d->relu_in || a->Npad % 64 || d->Cin % 8 ||
       d->n_store % 4 || a->m_total < 1024)
     return false;
   // every dY / source byte offset must stay below the buffer-resource bound (32-bit cursors)
@@ -335,9 +336,11 @@ inline bool wx_plan(const cvl_conv_desc* d, int ngroups, ConvArgs* a, WxPlan* p)
   int s128 = 0;
   for (int T = 256; T >= 128; T /= 2) {
     if (forced_t && forced_t != T) continue;
-    if (a->Npad % T || a->K < cvl_env_int(T == 256 ? "CVL_WGX_MIN_K" : "CVL_WGX_MIN_K128", T == 256 ? 256 : 64))
+    // T = 128 also takes 64-channel outputs (half of each tile idle: the stem's and the 1x1 ->64
+    // weight gradients, on the generic kernel at 149 / 44 / 37 us before)
+    if ((T == 256 && a->Npad % T) || a->K < cvl_env_int(T == 256 ? "CVL_WGX_MIN_K" : "CVL_WGX_MIN_K128", T == 256 ? 256 : 64))
       continue;
-    const int tg = (a->Npad / T) * ((a->K + T - 1) / T) * ngroups;
+    const int tg = ((a->Npad + T - 1) / T) * ((a->K + T - 1) / T) * ngroups;
     const double step_us =
         T == 256 ? cvl_env_int("CVL_WGX_STEP", 80) / 100.0 : cvl_env_int("CVL_WGX_STEP128", 80) / 100.0;
     const double slab_us = (double)T * T * 4 * 2 / 5.0e6 * cvl_env_int("CVL_WGX_SLAB_PCT", 100) / 100.0;
@@ -364,7 +367,7 @@ inline bool wx_plan(const cvl_conv_desc* d, int ngroups, ConvArgs* a, WxPlan* p)
   }
   if (!best_T) return false;
   p->T = best_T;
-  p->co_tiles = a->Npad / best_T;
+  p->co_tiles = (a->Npad + best_T - 1) / best_T;
   p->tiles = p->co_tiles * ((a->K + best_T - 1) / best_T);
   const int forced = cvl_env_int("CVL_WGX_SPLITS", 0);
   if (forced > 0) best_s = forced;

@@ -411,8 +411,8 @@ struct BnPG {
   const double* psums;    // per-image sums for the parameter gradients (nullptr: `sums`)
 };
 
-// MASK selects the ReLU-mask source at compile time (1: y, 2: bn_affine(z) recomputed; 0: decided at
-// run time from y / bnb) -- the run-time form holds the registers of both paths (pass 0: 215 VGPRs,
+// MASK selects the ReLU-mask source at compile time (1: y, 2: bn_affine(z) recomputed, 3: no mask --
+// BN without ReLU; 0: decided at run time from y / bnb) -- the run-time form holds the registers of both paths (pass 0: 215 VGPRs,
 // 2 waves/SIMD; pass 1: 141, 3 waves), the specialised ones fit 4-5 waves
 template <int PASS, int MASK = 0>
 __global__ void __launch_bounds__(NT) bn_bwd_kernel(const cvl_bf16* __restrict__ dy, const cvl_bf16* __restrict__ y,
@@ -1362,8 +1362,8 @@ static int bn_backward_impl(const void* dy, const void* y_relu, const float* bn_
   }
   dim3 g1(nchunk, B);
   const bool ym = y_relu != nullptr, zm = !ym && bn_beta != nullptr;
-  auto k0 = ym ? bn_bwd_kernel<0, 1> : zm ? bn_bwd_kernel<0, 2> : bn_bwd_kernel<0, 0>;
-  auto k1 = ym ? bn_bwd_kernel<1, 1> : zm ? bn_bwd_kernel<1, 2> : bn_bwd_kernel<1, 0>;
+  auto k0 = ym ? bn_bwd_kernel<0, 1> : zm ? bn_bwd_kernel<0, 2> : bn_bwd_kernel<0, 3>;
+  auto k1 = ym ? bn_bwd_kernel<1, 1> : zm ? bn_bwd_kernel<1, 2> : bn_bwd_kernel<1, 3>;
   hipLaunchKernelGGL(k0, g1, dim3(NT), 0, S_, (const cvl_bf16*)dy, (const cvl_bf16*)y_relu,
                      (const cvl_bf16*)z, mean_rstd, gamma, (const double*)nullptr, (cvl_bf16*)nullptr,
                      (cvl_bf16*)nullptr, part0, C, HW, rpb, 1, 0.f, BnPG{}, bn_beta, act_hi);

@@ -277,6 +277,9 @@ def test_conv_splitk_matches_unsplit(case):
     (2, 64, 64, 256, 512, 1, 2),
     (3, 40, 24, 128, 128, 3, 1),      # rows not a multiple of the 128-row granule
     (16, 128, 128, 64, 256, 1, 1),    # ResNet conv2 1x1, K = 64: hundreds of split-M slabs
+    (8, 64, 64, 256, 64, 1, 1),       # 64-channel outputs: half of each 128-wide tile idle
+    (4, 64, 64, 64, 64, 1, 1),
+    (2, 128, 128, 192, 64, 1, 1),     # the stem's im2col GEMM shape (K = 192 = 128 + 64)
 ])
 def test_conv_wgrad_large(case, kern):
     """Weight gradient at sizes that take the 128x256 LDS-DMA kernel (and, with kern == "base",
