@@ -85,6 +85,12 @@ struct ConvArgs {
   float bhi;
 };
 
+// split-M weight-gradient reductions (conv_wgrad_defer.hip): queued while cvl_wgrad_defer(1) is on
+int cvl_wgrad_reduce(const float* slab, float* dst0, float* dst1, long n4, int splits, int groups, float beta,
+                     hipStream_t s);
+int cvl_wgrad_defer_guard(const float* dst, hipStream_t s);
+int cvl_wgrad_reduce_lanes(long elems4, int splits);
+
 // host-side bundle of the fused BN-backward sums arguments (cvl_conv_igemm_dgrad_bnsum)
 struct BnSumArgs {
   const cvl_bf16* z;

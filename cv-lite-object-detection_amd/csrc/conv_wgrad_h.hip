@@ -220,35 +220,6 @@ __global__ void __launch_bounds__(NT) conv_wgrad_h_kernel(WhArgs g) {
     }
 }
 
-// dw[i] = beta*dw[i] + sum over splits of slab[split][i] (deterministic): a block owns 16 float4
-// columns x 16 split lanes; lane l sums splits l, l + 16, ... (4 loads in flight), then the 16 lane
-// sums of a column are added in a fixed order through LDS
-__global__ void __launch_bounds__(256) wgrad_h_reduce(const float* __restrict__ slab, float* __restrict__ dw, long n4,
-                                                      int nsplit, float beta) {
-  __shared__ f32x4 red[16][17];
-  const int col = threadIdx.x & 15, sl = threadIdx.x >> 4;
-  const long i = (long)blockIdx.x * 16 + col;
-  f32x4 s = f32x4{0.f, 0.f, 0.f, 0.f};
-  if (i < n4) {
-    const f32x4* p = reinterpret_cast<const f32x4*>(slab) + i;
-    int k = sl;
-    for (; k + 48 < nsplit; k += 64) {
-      const f32x4 a0 = p[(long)k * n4], a1 = p[(long)(k + 16) * n4];
-      const f32x4 a2 = p[(long)(k + 32) * n4], a3 = p[(long)(k + 48) * n4];
-      s += (a0 + a1) + (a2 + a3);
-    }
-    for (; k < nsplit; k += 16) s += p[(long)k * n4];
-  }
-  red[sl][col] = s;
-  __syncthreads();
-  if (sl == 0 && i < n4) {
-    f32x4 t = red[0][col];
-    for (int k = 1; k < 16; ++k) t += red[k][col];
-    f32x4* d = reinterpret_cast<f32x4*>(dw) + i;
-    if (beta != 0.f) t += beta * *d;
-    *d = t;
-  }
-}
 
 struct WhPlan {
   int steps, nsplit, chunk;
@@ -307,11 +278,12 @@ int cvl_conv_wgrad_h(const cvl_conv_desc* d, int ngroups, const void* x, const v
   g.beta = beta;
   g.out = g.direct ? dw[0] : reinterpret_cast<float*>(workspace);
   g_cvl_conv_last_kernel = CVL_CK_WG_H;
+  if (g.direct) {                               // writes dW now: a queued reduction into it first
+    const int gs = cvl_wgrad_defer_guard(dw[0], s);
+    if (gs) return gs;
+  }
   hipLaunchKernelGGL(conv_wgrad_h_kernel, dim3(g.ci_tiles * g.co_tiles * pl.nsplit), dim3(NT), 0, s, g);
   int st = cvl_launch_status();
   if (st || g.direct) return st;
-  const long n4 = 9L * d->Cin * d->n_store / 4;
-  hipLaunchKernelGGL(wgrad_h_reduce, dim3((int)((n4 + 15) / 16)), dim3(256), 0, s, (const float*)workspace, dw[0], n4,
-                     pl.nsplit, beta);
-  return cvl_launch_status();
+  return cvl_wgrad_reduce((const float*)workspace, dw[0], dw[0], 9L * d->Cin * d->n_store / 4, pl.nsplit, 1, beta, s);
 }

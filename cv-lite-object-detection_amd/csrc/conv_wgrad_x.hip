@@ -23,7 +23,7 @@
 // * The LDS image of a row is XOR-swizzled in 32-byte chunks within each 256-byte half (applied to
 //   the lane's SOURCE offset, LDS-DMA writes lane-linearly): the transposed reads are conflict-free.
 // * The reduction range of a group is split over workgroups to fill the GPU; partial tiles go to
-//   fp32 slabs summed in a fixed order by wgrad_x_reduce_kernel (deterministic), or straight to dW
+//   fp32 slabs summed in a fixed order by cvl_wgrad_reduce (conv_wgrad_defer.hip; deterministic), or straight to dW
 //   (with beta) when one split covers the range.
 #include "conv_common.h"
 
@@ -255,43 +255,6 @@ __global__ void __launch_bounds__(NT) conv_wgrad_x_kernel(WxArgs g) {
     }
 }
 
-// dW_g = beta * dW_g + sum over splits s of slab_g[s]; slabs of group g at g * splits * n4.
-// P consecutive lanes share one float4 element: lane j sums the splits j, j + P, ... in order and
-// the P partials are combined by a fixed xor tree (deterministic); P > 1 for the small outputs whose
-// many splits made one thread's serial chain the whole kernel (16 blocks, 14.8 us)
-template <int P>
-__global__ void wgrad_x_reduce_kernel(const float* slab, float* dw0, float* dw1, long n4, int splits, int groups,
-                                      float beta) {
-  const long total = n4 * groups * P;
-  for (long t = blockIdx.x * (long)blockDim.x + threadIdx.x; t < total; t += (long)gridDim.x * blockDim.x) {
-    const long e = t / P;
-    const int j = (int)(t % P);
-    const int gq = (int)(e / n4);
-    const long i = e - gq * n4;
-    const f32x4* sl = reinterpret_cast<const f32x4*>(slab) + (long)gq * splits * n4;
-    f32x4 s = f32x4{0.f, 0.f, 0.f, 0.f};
-    int k = j;
-    for (; k + 7 * P < splits; k += 8 * P) {        // 8 loads in flight
-      f32x4 v[8];
-#pragma unroll
-      for (int u = 0; u < 8; ++u) v[u] = sl[(long)(k + u * P) * n4 + i];
-#pragma unroll
-      for (int u = 0; u < 8; ++u) s += v[u];
-    }
-    for (; k < splits; k += P) s += sl[(long)k * n4 + i];
-#pragma unroll
-    for (int m = 1; m < P; m <<= 1) {
-#pragma unroll
-      for (int c = 0; c < 4; ++c) s[c] += __shfl_xor(s[c], m);
-    }
-    if (j == 0) {
-      f32x4* d = reinterpret_cast<f32x4*>(gq == 0 ? dw0 : dw1) + i;
-      if (beta != 0.f) s += beta * *d;
-      *d = s;
-    }
-  }
-}
-
 struct WxPlan {
   int T, ngroups, spg, tiles, co_tiles, nsplit, chunk;
   int g_m0[kMaxGroups], g_m1[kMaxGroups];
@@ -413,19 +376,15 @@ int cvl_conv_wgrad_x(const cvl_conv_desc* d, int ngroups, const void* x, const v
     g.out[gq] = g.direct ? dw[gs] : reinterpret_cast<float*>(workspace) + gs * per_group;
   }
   g_cvl_conv_last_kernel = CVL_CK_WG_X;
+  if (g.direct) {                               // writes dW now: a queued reduction into it first
+    int gs = cvl_wgrad_defer_guard(dw[0], s);
+    if (!gs && ngroups > 1) gs = cvl_wgrad_defer_guard(dw[1], s);
+    if (gs) return gs;
+  }
   if (p.T == 256) hipLaunchKernelGGL(conv_wgrad_x_kernel<256>, dim3(p.tiles * p.nsplit * ngroups), dim3(NT), 0, s, g);
   else hipLaunchKernelGGL(conv_wgrad_x_kernel<128>, dim3(p.tiles * p.nsplit * ngroups), dim3(NT), 0, s, g);
   int st = cvl_launch_status();
   if (st || g.direct) return st;
-  const long n4 = (long)g.a.K * g.Cout / 4;
-  // lanes per element: grow while the grid stays under ~64K threads and each lane keeps >= 4 splits
-  int P = 1;
-  while (P < 16 && n4 * ngroups * P * 2 <= 65536 && p.nsplit >= 8 * P) P *= 2;
-  long blocks = (n4 * ngroups * P + 255) / 256;
-  blocks = blocks > 4096 ? 4096 : blocks;
-  auto rk = P == 1 ? wgrad_x_reduce_kernel<1> : P == 2 ? wgrad_x_reduce_kernel<2> : P == 4 ? wgrad_x_reduce_kernel<4>
-          : P == 8 ? wgrad_x_reduce_kernel<8> : wgrad_x_reduce_kernel<16>;
-  hipLaunchKernelGGL(rk, dim3((int)blocks), dim3(256), 0, s, (const float*)workspace, dw[0],
-                     ngroups > 1 ? dw[1] : dw[0], n4, p.nsplit, ngroups, beta);
-  return cvl_launch_status();
+  return cvl_wgrad_reduce((const float*)workspace, dw[0], ngroups > 1 ? dw[1] : dw[0], (long)g.a.K * g.Cout / 4,
+                          p.nsplit, ngroups, beta, s);
 }

@@ -62,6 +62,8 @@ SIGNATURES = {
     "cvl_bias_grad_multi": (c_int, [P, c_int, P, c_size_t, P]),
     "cvl_bias_grad": (c_int, [P, c_int, c_int, c_int, ctypes.c_int64, ctypes.c_int64, c_int, c_int, P, c_size_t,
                               P, c_float, P]),
+    "cvl_wgrad_defer": (c_int, [c_int, P]),
+    "cvl_wgrad_flush": (c_int, [P]),
     "cvl_sgd_clip_update": (c_int, [P, P, P, ctypes.c_int64, P, c_float, c_float, c_float, P, P]),
     "cvl_lr_schedule": (c_int, [P, P, ctypes.c_double, ctypes.c_double, ctypes.c_double, c_int, P]),
     "cvl_lr_schedule_capped": (c_int, [P, P, ctypes.c_double, ctypes.c_double, ctypes.c_double, c_int, c_int, P]),

@@ -37,6 +37,8 @@ def pair_tower0_dgrad():
 
 # CVL_FPN_FUSE=0 runs P3..P5's 3x3 output convs as separate launches (A/B only)
 FUSE_FPN = os.environ.get("CVL_FPN_FUSE", "1") != "0"
+# weight-gradient split reductions batched per gradient group (ops_nn.deferred_wgrad)
+DEFER_WGRAD = os.environ.get("CVL_NO_WGRAD_DEFER", "0") != "1"
 
 class FPNDetector(object):
     @staticmethod
@@ -240,9 +242,21 @@ class FPNDetector(object):
 
     # ---- backward ------------------------------------------------------------------------------------
     def backward(self, *head_grads, hook=None):
+        """The split weight-gradient reductions run deferred: one batched launch before each gradient
+        group is reported final (hook) and one at the end (DEFER_WGRAD; CVL_NO_WGRAD_DEFER=1: off)."""
         s = self._saved
-        dA = self._heads_backward(head_grads, s["towers"], s["B"], s["shapes"], s["off"], s["P"])
-        self.trunk_backward(dA, hook=hook)
+        if not DEFER_WGRAD:
+            dA = self._heads_backward(head_grads, s["towers"], s["B"], s["shapes"], s["off"], s["P"])
+            self.trunk_backward(dA, hook=hook)
+            return
+
+        def flush_then(name):
+            nn.wgrad_flush()
+            if hook is not None:
+                hook(name)
+        with nn.deferred_wgrad():
+            dA = self._heads_backward(head_grads, s["towers"], s["B"], s["shapes"], s["off"], s["P"])
+            self.trunk_backward(dA, hook=flush_then)
 
     def trunk_backward(self, dA_top, hook=None):
         """dA_top: per tower, the gradient w.r.t. its ReLU output (buffer reused in place).

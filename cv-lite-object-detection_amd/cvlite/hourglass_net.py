@@ -191,6 +191,7 @@ class Stem(object):
         A, B, Ho, Wo = saved
         dw = torch.empty((STEM_KP, self.nf), dtype=torch.float32, device=dz.device)
         nn.conv_wgrad(self._desc(B, Ho, Wo), A, dz, dw)
+        nn.wgrad_flush()                             # dw is read right away (deferred reductions)
         self.sep.conv.dw.view(147, self.nf).copy_(dw[:147])
         HW = Ho * Wo
         nn.bias_grad(dz, self.nf, 0, self.nf, 0, HW, HW, B, self.sep.db)

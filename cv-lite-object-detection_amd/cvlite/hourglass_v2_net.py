@@ -134,6 +134,7 @@ class StemV2(object):
         A, B, H, W = saved
         dw = torch.empty((STEM_KP, self.cpo), dtype=torch.float32, device=dz.device)
         nn.conv_wgrad(self._desc(B, H, W), A, dz, dw)
+        nn.wgrad_flush()                             # dw is read right away (deferred reductions)
         self.conv.dw.view(27, self.nf).copy_(dw[:27, :self.nf])
         nn.bias_grad(dz, self.cpo, 0, self.cpo, 0, H * W, H * W, B, self.store.g(self.bname))
 

@@ -265,6 +265,7 @@ class MobileNetV2(object):
                              st.g(self.stem_bn.bname), B, Ho * Wo, 32)
         dw = torch.empty((STEM_KP, 32), dtype=torch.float32, device=dz.device)
         nn.conv_wgrad(self._stem_desc(B, Ho, Wo), A, dz, dw)
+        nn.wgrad_flush()                             # dw is read right away (deferred reductions)
         st.g(self.stem_wname).view(27, 32).copy_(dw[:27])
         if hook is not None:
             hook("backbone")

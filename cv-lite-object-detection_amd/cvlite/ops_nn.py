@@ -94,6 +94,38 @@ def probe_seconds(slot):
     return (ticks / n / hz if n and hz > 0 else None), n
 
 
+# workspaces of the weight gradients whose split reductions are pending (cvl_wgrad_defer); None =
+# deferral off.  Kept alive until the flush has been enqueued.
+_wgrad_pending = None
+
+
+class deferred_wgrad(object):
+    """with deferred_wgrad(): the split-M weight-gradient reductions of the block are batched into
+    one launch per wgrad_flush() (and one at exit); dW is final only after the flush."""
+
+    def __enter__(self):
+        global _wgrad_pending
+        self.outer = _wgrad_pending is not None
+        if not self.outer:
+            _wgrad_pending = []
+            _lib.call("cvl_wgrad_defer", 1, stream())
+        return self
+
+    def __exit__(self, *exc):
+        global _wgrad_pending
+        if not self.outer:
+            _lib.call("cvl_wgrad_defer", 0, stream())
+            _wgrad_pending = None
+        return False
+
+
+def wgrad_flush():
+    """Reduce every pending weight gradient (no-op when none / deferral off)."""
+    if _wgrad_pending is not None:
+        _lib.call("cvl_wgrad_flush", stream())
+        del _wgrad_pending[:]
+
+
 def conv_wgrad(desc, x, dy, dw, beta=0.0):
     _prec(desc, x)
     lib = _lib.load()
@@ -101,6 +133,8 @@ def conv_wgrad(desc, x, dy, dw, beta=0.0):
     ws = torch.empty(max(n, 16), dtype=torch.uint8, device=x.device)
     _lib.call("cvl_conv_wgrad", ctypes.byref(desc), ptr(x), ptr(dy), ptr(dw), float(beta), ptr(ws),
               ws.numel(), stream())
+    if _wgrad_pending is not None:
+        _wgrad_pending.append(ws)
 
 
 def conv_wgrad_grouped(desc, x, dy, dws, beta=0.0):
@@ -113,6 +147,8 @@ def conv_wgrad_grouped(desc, x, dy, dws, beta=0.0):
     arr = (c_void_p * len(dws))(*[t.data_ptr() for t in dws])
     _lib.call("cvl_conv_wgrad_grouped", ctypes.byref(desc), len(dws), ptr(x), ptr(dy), arr, float(beta), ptr(ws),
               ws.numel(), stream())
+    if _wgrad_pending is not None:
+        _wgrad_pending.append(ws)
 
 
 def pack_conv_weights(w_hwio, KH, KW, Cin, Cout, Cin_k, Npad, w_fwd, Cin_pad=0, Cout_pad=0, w_dgrad=None):

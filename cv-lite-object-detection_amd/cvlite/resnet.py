@@ -90,6 +90,7 @@ class Stem(object):
             return
         dw = torch.empty((STEM_KP, 64), dtype=torch.float32, device=dp.device)
         nn.conv_wgrad(self._desc(B, Ho, Wo), A, dz, dw)
+        nn.wgrad_flush()                             # dw is read right away (deferred reductions)
         self.conv.dw.view(147, 64).copy_(dw[:147])
 
 

@@ -179,6 +179,14 @@ int cvl_conv_wgrad(const cvl_conv_desc* d, const void* x, const void* dy, float*
  * sharing one weight pointer), group g summed into dw[g] (a HOST array of device pointers).  The
  * FCOS cls and reg tower layers (FCOS/fcos.py:16-27, 76-101: same geometry, own weights) are one
  * call with 10 segments and 2 groups.  workspace >= cvl_conv_wgrad_grouped_workspace_size(d, ngroups). */
+/* Deferred split reductions of the weight gradients.  cvl_wgrad_defer(1): the split-M weight
+ * gradients (cvl_conv_wgrad / _grouped) leave their fp32 slabs pending instead of reducing them into
+ * dW at once; cvl_wgrad_flush reduces everything pending in ONE batched launch (deterministic, the
+ * same arithmetic as the immediate form).  The caller keeps every pending call's workspace alive and
+ * dW unread until the flush; cvl_wgrad_defer(0) flushes and turns deferral off.  A reduction or
+ * unsplit write into a dW that is already pending flushes first. */
+int cvl_wgrad_defer(int on, cvl_stream_t stream);
+int cvl_wgrad_flush(cvl_stream_t stream);
 size_t cvl_conv_wgrad_grouped_workspace_size(const cvl_conv_desc* d, int ngroups);
 int cvl_conv_wgrad_grouped(const cvl_conv_desc* d, int ngroups, const void* x, const void* dy, float* const* dw,
                            float beta, void* workspace, size_t workspace_bytes, cvl_stream_t stream);

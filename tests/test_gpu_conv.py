@@ -496,3 +496,45 @@ def test_conv_bn_stats_maps_not_tile_aligned(B, H, Cin, Cout, k, kern):
     o = out.double().cpu()
     st = torch.stack([o.sum((1, 2)), (o * o).sum((1, 2))], -1)
     torch.testing.assert_close(stats.cpu(), st, rtol=1e-5, atol=1e-3)
+
+
+@pytest.mark.gpu
+def test_conv_wgrad_deferred_reduction():
+    """Deferred split reductions (ops_nn.deferred_wgrad, cvl_wgrad_defer / _flush) give dW
+    bit-identical to the immediate form: a 1x1 (wgrad_x, 128-wide tiles), a 3x3 (halo kernel) and a
+    beta-accumulating second gradient into the SAME dW while the first is still pending (the queue
+    flushes before the second record)."""
+    from cvlite import ops_nn as nn
+    g = torch.Generator(device="cuda").manual_seed(11)
+    cases = [(16, 32, 32, 256, 1024, 1), (16, 32, 32, 256, 256, 3)]
+    data = []
+    for B, H, W, Cin, Cout, k in cases:
+        x = torch.randn((B, H, W, Cin), generator=g, device="cuda").to(BF)
+        dy = torch.randn((B, H, W, Cout), generator=g, device="cuda").to(BF)
+        wf = torch.empty((Cout, k * k * Cin), dtype=BF, device="cuda")
+        d = nn.make_desc(nn.FWD, B, Cin, k, k, 1, k // 2, k // 2, Cout, Cout, Cout, [nn.seg(H, W, H, W, wf)])
+        data.append((d, x, dy, (k, k, Cin, Cout)))
+
+    def run(deferred):
+        outs = [torch.zeros(s, device="cuda") for (_, _, _, s) in data]
+        acc = torch.ones(data[0][3], device="cuda")
+
+        def body():
+            for (d, x, dy, _), o in zip(data, outs):
+                nn.conv_wgrad(d, x, dy, o)
+            nn.conv_wgrad(data[0][0], data[0][1], data[0][2], acc, beta=0.5)
+            nn.conv_wgrad(data[0][0], data[0][1], data[0][2], acc, beta=1.0)   # same dW, first still pending
+        if deferred:
+            with nn.deferred_wgrad():
+                body()
+                nn.wgrad_flush()
+        else:
+            body()
+        torch.cuda.synchronize()
+        return outs + [acc]
+
+    imm, dfr = run(False), run(True)
+    for a, b in zip(imm, dfr):
+        assert torch.equal(a, b)
+    # and the accumulated one is 0.5 + 2 * dW (fp32 tolerance)
+    torch.testing.assert_close(imm[2], 0.5 + 2 * imm[0], rtol=1e-5, atol=1e-3)
