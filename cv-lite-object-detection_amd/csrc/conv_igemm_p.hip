@@ -88,7 +88,7 @@ __device__ __forceinline__ s16x8 gload16_untracked(const void* p) {
 }
 __device__ __forceinline__ void pin16(s16x8& v) { asm volatile("" : "+v"(v)); }
 
-template <int BN, bool RELU, bool F32, bool BS = false>
+template <int BN, bool RELU, bool F32, bool BS = false, bool ACC = false>
 __global__ void __launch_bounds__(NT) conv_igemm_p_kernel(ConvArgs a, int ntiles) {
   using C = PCfg<BN>;
   constexpr int TM = C::TM, TN = C::TN, NS = C::NS, D = C::D;
@@ -223,6 +223,9 @@ __global__ void __launch_bounds__(NT) conv_igemm_p_kernel(ConvArgs a, int ntiles
   }
   wait_vm<0>();
   s16x8 zv[BS ? TM : 1][NJP];
+  // ACC (bf16 dst, beta != 0): the tile's old dst chunks, prefetched with its first K-tile like z (a
+  // plain load in the epilogue made the compiler drain the DMA ring at every tile)
+  s16x8 ov[ACC ? TM : 1][ACC ? TN / 2 : 1];
 
   // BN statistics: per-lane sums over this workgroup's rows of the current image, reduced over
   // the 16 rows of a lane quad by DPP (xor 1, xor 2, half-row mirror, row mirror: every lane ends
@@ -296,6 +299,13 @@ __global__ void __launch_bounds__(NT) conv_igemm_p_kernel(ConvArgs a, int ntiles
     const int m0 = (mt0 + k) * BM;
     const bool dense_dst = a.dst_up == 1 && S.dst_img == (long)HWr;
     const bool do_stats = a.stats && !(a.dbg & 1);
+    if (ACC) {
+      wait_vm_atleast(C::PW * (nk - 1));           // the old chunks (issued with K-tile 0) landed
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int jp = 0; jp < TN / 2; ++jp) pin16(ov[i][jp]);
+    }
     if (BS) {
       // the tile's z chunks (issued with its first K-tile) have landed: younger than them are the
       // DMA pieces of its other nk - 1 K-tiles
@@ -392,7 +402,12 @@ __global__ void __launch_bounds__(NT) conv_igemm_p_kernel(ConvArgs a, int ntiles
             bs2[j / 2][u] = __builtin_fmaf(gv, xh, bs2[j / 2][u]);
           }
         }
-        if (a.beta != 0.f) {
+        if (ACC) {
+          const s16x8 old = ov[i][j / 2];
+#pragma unroll
+          for (int u = 0; u < 8; ++u)
+            o[u] = (short)f32_to_bf16(bf16_to_f32((cvl_bf16)o[u]) + a.beta * bf16_to_f32((cvl_bf16)old[u]));
+        } else if (a.beta != 0.f) {
           const s16x8 old = *pd;
 #pragma unroll
           for (int u = 0; u < 8; ++u)
@@ -426,6 +441,29 @@ __global__ void __launch_bounds__(NT) conv_igemm_p_kernel(ConvArgs a, int ntiles
     __builtin_amdgcn_s_barrier();                  // ... everyone's; slot of K-tile g - 2 free
     asm volatile("" ::: "memory");
     issue();                                       // K-tile g + D
+    if (ACC && ck == 0) {                          // old dst chunks of tile ct for the epilogue
+      const int m0 = (mt0 + ct) * BM;
+      const bool dense_dst = a.dst_up == 1 && S.dst_img == (long)HWr;
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const int ml = m0 + wm * C::WM + i * 16 + lr;
+        long drow = S.dst_base;                    // rows past the segment: a harmless in-range row
+        if (ml < S.rows) {
+          if (dense_dst) {
+            drow = S.dst_base + ml;
+          } else {
+            const int img = ml / HWr, q = ml - img * HWr;
+            drow = conv_dst_row(a, S, img, q);
+          }
+        }
+#pragma unroll
+        for (int jp = 0; jp < TN / 2; ++jp) {
+          int n = n0 + wn * C::WN + jp * 32 + lgo;
+          if (n >= a.n_store) n = 0;
+          ov[i][jp] = gload16_untracked(reinterpret_cast<const cvl_bf16*>(a.dst) + drow * a.ld_dst + a.dst_coff + n);
+        }
+      }
+    }
     if (BS && ck == 0) {                           // z chunks of tile ct for the epilogue
       const int m0 = (mt0 + ct) * BM;
 #pragma unroll
@@ -494,21 +532,23 @@ int cvl_conv_igemm_p(const cvl_conv_desc* d, const ConvArgs& a0, hipStream_t s) 
   ConvArgs a = a0;
   a.dbg = cvl_env_int("CVL_P_ABLATE", 0);
   g_cvl_conv_last_kernel = CVL_CK_P;
-#define CVL_P_LAUNCH(BN_)                                                                                   \
+#define CVL_P_LAUNCH(BN_, ACC_)                                                                                 \
   do {                                                                                                      \
     if (a.dst_f32) {                                                                                        \
       if (a.relu_out) hipLaunchKernelGGL((conv_igemm_p_kernel<BN_, true, true>), dim3(grid), dim3(NT), 0, s, a, ntiles);   \
       else hipLaunchKernelGGL((conv_igemm_p_kernel<BN_, false, true>), dim3(grid), dim3(NT), 0, s, a, ntiles);            \
     } else if (a.relu_out) {                                                                                \
       hipLaunchKernelGGL((conv_igemm_p_kernel<BN_, true, false>), dim3(grid), dim3(NT), 0, s, a, ntiles);                 \
+    } else if (a.beta != 0.f && !cvl_env_flag("CVL_P_NO_ACC")) {                                            \
+      hipLaunchKernelGGL((conv_igemm_p_kernel<BN_, false, false, false, ACC_>), dim3(grid), dim3(NT), 0, s, a, ntiles);   \
     } else {                                                                                                \
       hipLaunchKernelGGL((conv_igemm_p_kernel<BN_, false, false>), dim3(grid), dim3(NT), 0, s, a, ntiles);                \
     }                                                                                                       \
   } while (0)
   if (a.bsum) hipLaunchKernelGGL((conv_igemm_p_kernel<64, false, false, true>), dim3(grid), dim3(NT), 0, s, a, ntiles);
-  else if (use == 256) CVL_P_LAUNCH(256);
-  else if (use == 128) CVL_P_LAUNCH(128);
-  else CVL_P_LAUNCH(64);
+  else if (use == 256) CVL_P_LAUNCH(256, false);      // (the 256-wide ACC form spills)
+  else if (use == 128) CVL_P_LAUNCH(128, true);
+  else CVL_P_LAUNCH(64, true);
 #undef CVL_P_LAUNCH
   return cvl_launch_status();
 }
