@@ -83,6 +83,7 @@ struct ConvArgs {
   const float* bbe;
   double* bsum;
   float bhi;
+  const cvl_bf16* by;     // non-null: the ReLU mask comes from y > 0 (a residual unit's output), not bn(z)
 };
 
 // split-M weight-gradient reductions (conv_wgrad_defer.hip): queued while cvl_wgrad_defer(1) is on
@@ -99,6 +100,7 @@ struct BnSumArgs {
   const float* beta;
   double* sums;
   float hi;
+  const cvl_bf16* y;      // residual unit: mask y > 0 (null: rebuilt from z)
 };
 
 // destination row of GEMM row q (within image img) of segment S
@@ -126,6 +128,7 @@ static inline int cvl_conv_prepare(const cvl_conv_desc* d, int bm, ConvArgs* a) 
   a->dst_w = 0;
   a->dbg = 0;
   a->bz = nullptr; a->bmr = nullptr; a->bga = nullptr; a->bbe = nullptr; a->bsum = nullptr; a->bhi = 0.f;
+  a->by = nullptr;
   a->nseg = d->nseg;
   a->B = d->B;
   a->Cin = d->Cin; a->KH = d->KH; a->KW = d->KW; a->stride = d->stride;

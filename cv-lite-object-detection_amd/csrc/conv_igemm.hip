@@ -689,3 +689,33 @@ extern "C" int cvl_conv_igemm_dgrad_bnsum(const cvl_conv_desc* d, const void* sr
   }
   return cvl_conv_igemm(d, src, dst, nullptr, workspace, workspace_bytes, stream);
 }
+
+// The residual-unit form: the dgrad result, accumulated into dst with d->beta (the block-input
+// gradient a bottleneck's first 1x1 data gradient completes), is dy of a BN whose output passes
+// through (+ shortcut) -> ReLU; the mask is y > 0 from that unit's output y.  1x1 launches on the
+// persistent kernel only; otherwise the plain data gradient runs and *fused = 0.
+extern "C" int cvl_conv_igemm_dgrad_bnsum_res(const cvl_conv_desc* d, const void* src, void* dst, const void* y,
+                                              const void* z, const float* mean_rstd, const float* gamma,
+                                              const float* beta, double* sums, int32_t* fused, void* workspace,
+                                              size_t workspace_bytes, cvl_stream_t stream) {
+  CVL_CHECK_ARG(d && fused && y && z && mean_rstd && gamma && beta && sums);
+  *fused = 0;
+  if (!cvl_env_flag("CVL_NO_BNSUM_FUSE") && !cvl_env_flag("CVL_NO_BNSUM_RES") && d->prec == CVL_PREC_BF16 &&
+      d->mode == CVL_CONV_DGRAD && !d->dst_f32 && d->beta != 0.f && d->KH == 1 && d->KW == 1 && d->stride == 1 &&
+      d->Cin % 32 == 0 && d->Npad % 32 == 0 && d->ld_dst % 8 == 0 && d->dst_coff % 8 == 0 && d->n_store % 8 == 0 &&
+      src && dst) {
+    ConvArgs chk;
+    if (cvl_conv_prepare(d, BM, &chk) == CVL_OK) {
+      BnSumArgs b{reinterpret_cast<const cvl_bf16*>(z), mean_rstd, gamma, beta, sums, INFINITY};
+      b.y = reinterpret_cast<const cvl_bf16*>(y);
+      g_cvl_conv_last_kernel = CVL_CK_NONE;
+      const int lst = cvl_conv_igemm_l(d, 1, 0, src, dst, nullptr, (hipStream_t)stream, &b, workspace,
+                                       workspace_bytes);
+      if (lst >= 0) {
+        *fused = lst == CVL_OK ? 1 : 0;
+        return lst;
+      }
+    }
+  }
+  return cvl_conv_igemm(d, src, dst, nullptr, workspace, workspace_bytes, stream);
+}

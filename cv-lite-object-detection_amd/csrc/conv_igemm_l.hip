@@ -200,7 +200,10 @@ int cvl_conv_igemm_p(const cvl_conv_desc* d, const ConvArgs& a, hipStream_t s);
 int cvl_conv_igemm_l(const cvl_conv_desc* d, int dst_up, int dst_w, const void* src, void* dst, double* bn_stats,
                      hipStream_t s, const BnSumArgs* bsum, void* workspace, size_t workspace_bytes) {
   if (cvl_env_flag("CVL_CONV_NO_L")) return -1;
-  if (bsum && (d->mode != CVL_CONV_DGRAD || d->dst_f32 || d->beta != 0.f || dst_up != 1 || bn_stats)) return -1;
+  if (bsum && (d->mode != CVL_CONV_DGRAD || d->dst_f32 || (d->beta != 0.f && !bsum->y) || dst_up != 1 || bn_stats))
+    return -1;
+  // the residual (y-mask) form exists on the 1x1 persistent kernel only
+  if (bsum && bsum->y && (d->KH != 1 || d->KW != 1)) return -1;
   // fp32 destinations store element-wise: any n_store (the RetinaNet box heads: 9 anchors x 4 = 36)
   const bool n_ok = d->dst_f32 ? (d->n_store % 4 == 0 && !cvl_env_flag("CVL_CONV_L_F32_N8")) : d->n_store % 8 == 0;
   if (d->Cin % 32 != 0 || d->relu_in || !n_ok || (d->dst_f32 && bn_stats) ||
@@ -234,9 +237,11 @@ int cvl_conv_igemm_l(const cvl_conv_desc* d, int dst_up, int dst_w, const void* 
     if (bsum) {
       ap.bz = bsum->z; ap.bmr = bsum->mr; ap.bga = bsum->gamma; ap.bbe = bsum->beta; ap.bsum = bsum->sums;
       ap.bhi = bsum->hi;
+      ap.by = bsum->y;
     }
     const int pst = cvl_conv_igemm_p(d, ap, s);
     if (pst >= 0) return pst;
+    if (bsum && bsum->y) return -1;
   }
   const long min_tiles = cvl_env_int("CVL_CONV_L_MIN_TILES", 128);
   int use_bn = bn;

@@ -88,7 +88,7 @@ __device__ __forceinline__ s16x8 gload16_untracked(const void* p) {
 }
 __device__ __forceinline__ void pin16(s16x8& v) { asm volatile("" : "+v"(v)); }
 
-template <int BN, bool RELU, bool F32, bool BS = false, bool ACC = false>
+template <int BN, bool RELU, bool F32, int BS = 0, bool ACC = false>
 __global__ void __launch_bounds__(NT) conv_igemm_p_kernel(ConvArgs a, int ntiles) {
   using C = PCfg<BN>;
   constexpr int TM = C::TM, TN = C::TN, NS = C::NS, D = C::D;
@@ -203,7 +203,9 @@ __global__ void __launch_bounds__(NT) conv_igemm_p_kernel(ConvArgs a, int ntiles
       const int n = n0 + wn * C::WN + j * 16 + 4 * lg + e;
       bcol[j][e] = (S.bias && n < a.n_store) ? S.bias[n] : 0.f;
     }
-  // fused BN-backward sums (BS, data gradient): the lane's 8 channels per column-block pair after
+  // fused BN-backward sums (BS, data gradient; 1: ReLU mask rebuilt from z, 2: residual unit, mask
+  // y > 0 from its output y, sums over the FINAL value after the beta accumulate): the lane's 8
+  // channels per column-block pair after
   // the store regrouping; gamma / beta now, (mean, rstd) per image in the epilogue
   constexpr int NJP = BS ? TN / 2 : 1;
   const int lgo = ((lg & 1) ? 16 : 0) + ((lg & 2) ? 8 : 0);
@@ -223,6 +225,7 @@ __global__ void __launch_bounds__(NT) conv_igemm_p_kernel(ConvArgs a, int ntiles
   }
   wait_vm<0>();
   s16x8 zv[BS ? TM : 1][NJP];
+  s16x8 yv[BS == 2 ? TM : 1][BS == 2 ? NJP : 1];
   // ACC (bf16 dst, beta != 0): the tile's old dst chunks, prefetched with its first K-tile like z (a
   // plain load in the epilogue made the compiler drain the DMA ring at every tile)
   s16x8 ov[ACC ? TM : 1][ACC ? TN / 2 : 1];
@@ -313,7 +316,10 @@ __global__ void __launch_bounds__(NT) conv_igemm_p_kernel(ConvArgs a, int ntiles
 #pragma unroll
       for (int i = 0; i < TM; ++i)
 #pragma unroll
-        for (int jp = 0; jp < NJP; ++jp) pin16(zv[i][jp]);
+        for (int jp = 0; jp < NJP; ++jp) {
+          pin16(zv[i][jp]);
+          if (BS == 2) pin16(yv[i][jp]);
+        }
       const int img = m0 / HWr;
       if (img != bimg) {
         bimg = img;
@@ -390,18 +396,6 @@ __global__ void __launch_bounds__(NT) conv_igemm_p_kernel(ConvArgs a, int ntiles
         if (!row_ok || n >= a.n_store) continue;
         s16x8* pd = reinterpret_cast<s16x8*>(reinterpret_cast<cvl_bf16*>(a.dst) + drow * a.ld_dst + a.dst_coff + n);
         s16x8 o = __builtin_bit_cast(s16x8, (u32x4){pk[0][0], pk[0][1], pk[1][0], pk[1][1]});
-        if (BS) {                   // g = dy * ReLU mask rebuilt from z (the forward's bn_affine value)
-          const s16x8 zz = zv[i][j / 2];
-#pragma unroll
-          for (int u = 0; u < 8; ++u) {
-            const float zf = bf16_to_f32((cvl_bf16)zz[u]);
-            const float xh = (zf - bm[j / 2][u]) * brs[j / 2][u];
-            const float af = __builtin_fmaf(bga[j / 2][u], xh, bbe[j / 2][u]);
-            const float gv = (af > 0.f && af < a.bhi) ? bf16_to_f32((cvl_bf16)o[u]) : 0.f;
-            bs1[j / 2][u] += gv;
-            bs2[j / 2][u] = __builtin_fmaf(gv, xh, bs2[j / 2][u]);
-          }
-        }
         if (ACC) {
           const s16x8 old = ov[i][j / 2];
 #pragma unroll
@@ -412,6 +406,24 @@ __global__ void __launch_bounds__(NT) conv_igemm_p_kernel(ConvArgs a, int ntiles
 #pragma unroll
           for (int u = 0; u < 8; ++u)
             o[u] = (short)f32_to_bf16(bf16_to_f32((cvl_bf16)o[u]) + a.beta * bf16_to_f32((cvl_bf16)old[u]));
+        }
+        if (BS) {                   // g = dy * ReLU mask (bn_affine(z) as the forward formed it, or y > 0)
+          const s16x8 zz = zv[i][j / 2];
+#pragma unroll
+          for (int u = 0; u < 8; ++u) {
+            const float zf = bf16_to_f32((cvl_bf16)zz[u]);
+            const float xh = (zf - bm[j / 2][u]) * brs[j / 2][u];
+            bool on;
+            if (BS == 2) {
+              on = bf16_to_f32((cvl_bf16)yv[i][j / 2][u]) > 0.f;
+            } else {
+              const float af = __builtin_fmaf(bga[j / 2][u], xh, bbe[j / 2][u]);
+              on = af > 0.f && af < a.bhi;
+            }
+            const float gv = on ? bf16_to_f32((cvl_bf16)o[u]) : 0.f;
+            bs1[j / 2][u] += gv;
+            bs2[j / 2][u] = __builtin_fmaf(gv, xh, bs2[j / 2][u]);
+          }
         }
         *pd = o;
       }
@@ -472,6 +484,8 @@ __global__ void __launch_bounds__(NT) conv_igemm_p_kernel(ConvArgs a, int ntiles
         for (int jp = 0; jp < NJP; ++jp) {
           const long row = S.dst_base + m0 + wm * C::WM + i * 16 + lr;
           zv[i][jp] = gload16_untracked(a.bz + row * a.ld_dst + a.dst_coff + n0 + wn * C::WN + jp * 32 + lgo);
+          if (BS == 2)
+            yv[i][jp] = gload16_untracked(a.by + row * a.ld_dst + a.dst_coff + n0 + wn * C::WN + jp * 32 + lgo);
         }
     }
     const char* sl = lds + rslot * C::SLOT_B;
@@ -503,7 +517,9 @@ __global__ void __launch_bounds__(NT) conv_igemm_p_kernel(ConvArgs a, int ntiles
 int cvl_conv_igemm_p(const cvl_conv_desc* d, const ConvArgs& a0, hipStream_t s) {
   if (cvl_env_flag("CVL_CONV_NO_P")) return -1;
   if (d->KH != 1 || d->KW != 1 || d->pad_t || d->pad_l || a0.relu_in || a0.nseg != 1 || a0.K % BK) return -1;
-  if (a0.bsum && (d->mode != CVL_CONV_DGRAD || a0.dst_f32 || a0.beta != 0.f || a0.dst_up != 1 || a0.stats ||
+  // bsum forms: z-mask without beta; y-mask (residual unit) with the beta accumulate
+  if (a0.bsum && (d->mode != CVL_CONV_DGRAD || a0.dst_f32 || (a0.beta != 0.f) != (a0.by != nullptr) ||
+                  a0.dst_up != 1 || a0.stats ||
                   (a0.seg[0].Hr * a0.seg[0].Wr) % BM || a0.seg[0].dst_img != (long)a0.seg[0].Hr * a0.seg[0].Wr ||
                   a0.Npad % 64 || cvl_env_flag("CVL_CONV_P_NO_BSUM")))
     return -1;
@@ -545,7 +561,8 @@ int cvl_conv_igemm_p(const cvl_conv_desc* d, const ConvArgs& a0, hipStream_t s) 
       hipLaunchKernelGGL((conv_igemm_p_kernel<BN_, false, false>), dim3(grid), dim3(NT), 0, s, a, ntiles);                \
     }                                                                                                       \
   } while (0)
-  if (a.bsum) hipLaunchKernelGGL((conv_igemm_p_kernel<64, false, false, true>), dim3(grid), dim3(NT), 0, s, a, ntiles);
+  if (a.bsum && a.by) hipLaunchKernelGGL((conv_igemm_p_kernel<64, false, false, 2, true>), dim3(grid), dim3(NT), 0, s, a, ntiles);
+  else if (a.bsum) hipLaunchKernelGGL((conv_igemm_p_kernel<64, false, false, 1>), dim3(grid), dim3(NT), 0, s, a, ntiles);
   else if (use == 256) CVL_P_LAUNCH(256, false);      // (the 256-wide ACC form spills)
   else if (use == 128) CVL_P_LAUNCH(128, true);
   else CVL_P_LAUNCH(64, true);

@@ -1421,6 +1421,22 @@ extern "C" int cvl_bn_backward_relu_sums(const void* dy, const void* z, const fl
   return cvl_launch_status();
 }
 
+// Second pass only for a residual unit (mask y > 0, g_out = the masked gradient for the shortcut),
+// from the (sum g, sum g*xhat) the producing data gradient formed (cvl_conv_igemm_dgrad_bnsum_res).
+extern "C" int cvl_bn_backward_res_sums(const void* dy, const void* y, const void* z, const float* mean_rstd,
+                                        const float* gamma, const double* sums, void* dz, void* g_out,
+                                        float* dgamma, float* dbeta, float beta_acc, float* conv_dbias, int B,
+                                        int HW, int C, cvl_stream_t stream) {
+  CVL_CHECK_ARG(dy && y && z && mean_rstd && gamma && sums && dz && dgamma && dbeta && C % 8 == 0);
+  CVL_CHECK_ARG(B > 0 && HW > 0);
+  const int rpb = bn_rows_per_blk(B, HW, C);
+  const int nchunk = (HW + rpb - 1) / rpb;
+  hipLaunchKernelGGL((bn_bwd_kernel<1, 1>), dim3(nchunk, B), dim3(NT), 0, S_, (const cvl_bf16*)dy, (const cvl_bf16*)y,
+                     (const cvl_bf16*)z, mean_rstd, gamma, sums, (cvl_bf16*)dz, (cvl_bf16*)g_out, (float*)nullptr,
+                     C, HW, rpb, 1, 0.f, BnPG{dgamma, dbeta, conv_dbias, beta_acc}, (const float*)nullptr, INFINITY);
+  return cvl_launch_status();
+}
+
 extern "C" int cvl_maxpool3x3s2(const void* x, void* y, uint8_t* argmax, int B, int H, int W, int C,
                                 cvl_stream_t stream) {
   CVL_CHECK_ARG(x && y && argmax && C % 8 == 0);

@@ -229,17 +229,23 @@ class Conv(object):
         if bn_next is None:
             nn.conv_igemm(d, dy, out)
             return out
-        z, mr, ga, be, sums = bn_next
+        z, mr, ga, be, sums = bn_next[:5]
+        y = bn_next[5] if len(bn_next) > 5 else None       # residual unit: mask y > 0 (bn_res_ctx)
         zero = sums is None
         if zero:
             sums = torch.empty((B, self.cin, 2), dtype=torch.float64, device=dy.device)
-        fused = nn.conv_igemm_dgrad_bnsum(d, dy, out, z, mr, ga, be, sums, zero=zero)
+        if y is not None:
+            fused = nn.conv_igemm_dgrad_bnsum_res(d, dy, out, y, z, mr, ga, be, sums, zero=zero)
+        else:
+            fused = nn.conv_igemm_dgrad_bnsum(d, dy, out, z, mr, ga, be, sums, zero=zero)
         return out, (sums if fused else None)
 
 
 # the BN backward's first pass fused into the producing data gradient (CVL_NO_BNSUM_FUSE=1: off,
 # for A/B measurement)
 FUSE_BNSUM = os.environ.get("CVL_NO_BNSUM_FUSE", "0") != "1"
+# ... and a residual unit's (BN3) first pass into the next block's conv1 data gradient (CVL_NO_BNSUM_RES=1: off)
+FUSE_BNSUM_RES = FUSE_BNSUM and os.environ.get("CVL_NO_BNSUM_RES", "0") != "1"
 
 # weight gradients of the backbone units on a side stream, concurrent with the data-gradient chain
 # (the two are independent; the small-map launches leave most CUs idle on their own).  The owner
@@ -354,6 +360,15 @@ class ConvBN(object):
             return None
         return (z, mr, self.bn.gamma, self.bn.beta, arena.take(B, self.bn.c) if arena is not None else None)
 
+    def bn_res_ctx(self, saved, arena=None):
+        """As bn_next_ctx for a residual unit (BN -> + shortcut -> ReLU, the bottleneck's conv3): its dy
+        is completed by the next block's first 1x1 data gradient accumulating into the block-output
+        gradient, whose epilogue then forms this BN backward's first pass with the mask y > 0."""
+        x, z, y, mr, B, H, W, Ho, Wo, relu, has_res = saved
+        if not relu or not has_res or not FUSE_BNSUM_RES or z.dtype != BF16:
+            return None
+        return (z, mr, self.bn.gamma, self.bn.beta, arena.take(B, self.bn.c) if arena is not None else None, y)
+
     def backward(self, dy, saved, dx_out=None, dx_beta=0.0, g_out=None, need_dx=True, sums=None, bn_next=None):
         """dz = BN backward of dy, the conv's weight gradient, and (need_dx) its data gradient.
         sums: this unit's BN-backward first pass, already formed by the producer of dy (skip it).
@@ -363,7 +378,11 @@ class ConvBN(object):
         c = self.conv.cout
         dz = torch.empty_like(z)
         st = self.bn.store
-        if sums is not None:                             # first pass fused upstream
+        if sums is not None and has_res:                 # residual unit, first pass fused upstream
+            assert relu
+            nn.bn_backward_res_sums(dy, y, z, mr, self.bn.gamma, sums, dz, g_out, st.g(self.bn.gname),
+                                    st.g(self.bn.bname), B, Ho * Wo, c, conv_dbias=self.conv.db)
+        elif sums is not None:                           # first pass fused upstream
             assert relu and not has_res and g_out is None
             nn.bn_backward_relu_sums(dy, z, mr, self.bn.gamma, self.bn.beta, sums, dz, st.g(self.bn.gname),
                                      st.g(self.bn.bname), B, Ho * Wo, c, conv_dbias=self.conv.db)
@@ -386,6 +405,7 @@ class ConvBN(object):
             return None
         if bn_next is None:
             return self.conv.dgrad(dz, B, H, W, out=dx_out, beta=dx_beta)
-        assert dx_beta == 0.0
-        dx = self.conv.dgrad(dz, B, H, W, out=dx_out, bn_next=bn_next)
+        # beta-accumulating producers take the residual (y-mask) form only (bn_res_ctx)
+        assert dx_beta == 0.0 or len(bn_next) > 5
+        dx = self.conv.dgrad(dz, B, H, W, out=dx_out, beta=dx_beta, bn_next=bn_next)
         return dx

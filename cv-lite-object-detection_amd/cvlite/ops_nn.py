@@ -291,6 +291,29 @@ def conv_igemm_dgrad_bnsum(desc, src, dst, z, mean_rstd, gamma, beta, sums, act_
     return bool(flag.value)
 
 
+def conv_igemm_dgrad_bnsum_res(desc, src, dst, y, z, mean_rstd, gamma, beta, sums, zero=True):
+    """Residual-unit form of conv_igemm_dgrad_bnsum: a beta-accumulating 1x1 DGRAD that completes dy of
+    a BN -> (+ shortcut) -> ReLU unit with output y; its epilogue forms that BN backward's first pass
+    (mask y > 0) into `sums`.  True when fused, else the plain data gradient ran."""
+    _prec(desc, src)
+    n = int(_lib.load().cvl_conv_igemm_workspace_size(ctypes.byref(desc)))
+    ws = torch.empty(n, dtype=torch.uint8, device=src.device) if n > 16 else None
+    if zero:
+        sums.zero_()
+    flag = ctypes.c_int32(0)
+    _lib.call("cvl_conv_igemm_dgrad_bnsum_res", ctypes.byref(desc), ptr(src), ptr(dst), ptr(y), ptr(z),
+              ptr(mean_rstd), ptr(gamma), ptr(beta), ptr(sums), ctypes.addressof(flag), ptr(ws),
+              n if ws is not None else 0, stream())
+    return bool(flag.value)
+
+
+def bn_backward_res_sums(dy, y, z, mean_rstd, gamma, sums, dz, g_out, dgamma, dbeta, B, HW, C, beta_acc=0.0,
+                         conv_dbias=None):
+    """Second pass of a residual unit's BN backward (mask y > 0, g_out = masked dy) from the fused sums."""
+    _lib.call("cvl_bn_backward_res_sums", ptr(dy), ptr(y), ptr(z), ptr(mean_rstd), ptr(gamma), ptr(sums), ptr(dz),
+              ptr(g_out), ptr(dgamma), ptr(dbeta), float(beta_acc), ptr(conv_dbias), B, HW, C, stream())
+
+
 def bn_backward_relu_sums(dy, z, mean_rstd, gamma, beta, sums, dz, dgamma, dbeta, B, HW, C, beta_acc=0.0,
                           conv_dbias=None, act_hi=float("inf")):
     """Second pass of bn_backward_relu from the fused first-pass sums (conv_igemm_dgrad_bnsum)."""

@@ -119,7 +119,11 @@ class Bottleneck(object):
         y3, sv3 = self.c3.forward(y2, B, H1, W1, relu=True, residual=s, train=train, arena=arena)
         return y3, H1, W1, (sv_s, sv1, sv2, sv3)
 
-    def backward(self, dy, saved, dx_out=None, dx_beta=0.0, arena=None):
+    def backward(self, dy, saved, dx_out=None, dx_beta=0.0, arena=None, sums3=None, prev_ctx=None):
+        """Returns (dx, sums of the previous block's conv3 BN or None).  sums3: this block's conv3 BN
+        first pass, formed by the next block's conv1 data gradient (skipped here); prev_ctx: the
+        previous block's conv3 bn_res_ctx -- this block's conv1 data gradient completes that unit's
+        dy (the block-input gradient) and forms its first pass."""
         sv_s, sv1, sv2, sv3 = saved
         x = sv1[0]
         if dx_out is None:
@@ -134,17 +138,20 @@ class Bottleneck(object):
         ctx2, ctx1 = self.c2.bn_next_ctx(sv2, arena), self.c1.bn_next_ctx(sv1, arena)
         s2 = s1 = None
         if ctx2 is not None:
-            dy2, s2 = self.c3.backward(dy, sv3, g_out=g, bn_next=ctx2)
+            dy2, s2 = self.c3.backward(dy, sv3, g_out=g, bn_next=ctx2, sums=sums3)
         else:
-            dy2 = self.c3.backward(dy, sv3, g_out=g)
+            dy2 = self.c3.backward(dy, sv3, g_out=g, sums=sums3)
         if ctx1 is not None:
             dy1, s1 = self.c2.backward(dy2, sv2, sums=s2, bn_next=ctx1)
         else:
             dy1 = self.c2.backward(dy2, sv2, sums=s2)
         if self.sc is not None:
             self.sc.backward(g, sv_s, dx_out=dx_out, dx_beta=dx_beta)
+        if prev_ctx is not None and self.c1.conv.stride == 1:
+            _, s_prev = self.c1.backward(dy1, sv1, dx_out=dx_out, dx_beta=1.0, sums=s1, bn_next=prev_ctx)
+            return dx_out, s_prev
         self.c1.backward(dy1, sv1, dx_out=dx_out, dx_beta=1.0, sums=s1)
-        return dx_out
+        return dx_out, None
 
 
 # Keras applications ResNet v1 depths (block counts of conv2_x .. conv5_x); the detectors tap the
@@ -230,13 +237,17 @@ class ResNet50(object):
         dh = dC[3]
         for si in range(3, -1, -1):
             st = self.stages[si]
+            pending = None          # the next-processed block's conv3 BN first pass, fused upstream
             for bi in range(len(st) - 1, -1, -1):
+                # an identity predecessor's conv3 BN first pass rides on this block's conv1 dgrad
+                prev = st[bi - 1].c3.bn_res_ctx(ssv[si][bi - 1][3], arena) if bi >= 1 else None
                 if bi == 0 and (si - 1) in dC:
                     # this block's input is the previous stage's tap (C3 / C4), whose buffer
                     # already holds the FPN lateral's gradient: accumulate into it
-                    dh = st[bi].backward(dh, ssv[si][bi], dx_out=dC[si - 1], dx_beta=1.0, arena=arena)
+                    dh, pending = st[bi].backward(dh, ssv[si][bi], dx_out=dC[si - 1], dx_beta=1.0, arena=arena,
+                                                  sums3=pending, prev_ctx=prev)
                 else:
-                    dh = st[bi].backward(dh, ssv[si][bi], arena=arena)
+                    dh, pending = st[bi].backward(dh, ssv[si][bi], arena=arena, sums3=pending, prev_ctx=prev)
             if si > 0:
                 join_side(dh.device)          # this stage's weight gradients are final
                 hook("conv%d" % (si + 2))

@@ -264,6 +264,19 @@ int cvl_bn_backward_relu_sums(const void* dy, const void* z, const float* mean_r
                               const float* beta, const double* sums, void* dz, float* dgamma, float* dbeta,
                               float beta_acc, float* conv_dbias, float act_hi, int B, int HW, int C,
                               cvl_stream_t stream);
+/* The residual-unit form (a bottleneck's BN3: BN -> + shortcut -> ReLU, the block output y).  The
+ * block-input gradient of the NEXT block is completed by its first 1x1 data gradient accumulating
+ * into dst (d->beta != 0); cvl_conv_igemm_dgrad_bnsum_res runs that launch and, on the persistent
+ * 1x1 kernel, adds (sum g, sum g*xhat), g = final dst * (y > 0), into sums (zeroed) and sets
+ * *fused = 1 (else the plain data gradient, *fused = 0).  cvl_bn_backward_res_sums is then that BN
+ * backward's second pass from the sums: dz, g_out (= g, the shortcut's gradient) and dgamma/dbeta
+ * (replaces cvl_bn_backward with y_relu given). */
+int cvl_conv_igemm_dgrad_bnsum_res(const cvl_conv_desc* d, const void* src, void* dst, const void* y, const void* z,
+                                   const float* mean_rstd, const float* gamma, const float* beta, double* sums,
+                                   int32_t* fused, void* workspace, size_t workspace_bytes, cvl_stream_t stream);
+int cvl_bn_backward_res_sums(const void* dy, const void* y, const void* z, const float* mean_rstd, const float* gamma,
+                             const double* sums, void* dz, void* g_out, float* dgamma, float* dbeta, float beta_acc,
+                             float* conv_dbias, int B, int HW, int C, cvl_stream_t stream);
 
 /* BN -> ReLU6 unit without a residual (MobileNetV2: Keras ReLU(6.)): as cvl_bn_backward_relu with
  * the TF Relu6Grad mask 0 < bn(z) < 6 rebuilt from z in fp32 (the forward's exact pre-clamp value);

@@ -311,3 +311,57 @@ def test_dgrad_fused_bn_backward_first_pass(B, H, Cin, Cout, k, expect_fused):
     torch.testing.assert_close(dz_f.float(), dz_p.float(), rtol=1e-2, atol=1e-2 * float(dz_p.float().abs().max()))
     torch.testing.assert_close(dg_f, dg_p, rtol=1e-5, atol=1e-5 * float(dg_p.abs().max()))
     torch.testing.assert_close(db_f, db_p, rtol=1e-5, atol=1e-5 * float(db_p.abs().max()))
+
+
+@pytest.mark.parametrize("B,H,Cin,Cout", [
+    (16, 128, 64, 256),      # conv2_x: the next block's conv1 (256 -> 64) data gradient, 4 tiles per workgroup
+    (8, 32, 256, 1024),      # conv4_x
+    (4, 16, 512, 2048),      # conv5_x: one tile per image
+])
+def test_dgrad_fused_bn_backward_residual(B, H, Cin, Cout):
+    """cvl_conv_igemm_dgrad_bnsum_res + cvl_bn_backward_res_sums (a bottleneck's conv3 BN, whose dy the
+    next block's conv1 data gradient completes by accumulating onto the shortcut gradient) against the
+    plain accumulating data gradient + two-pass cvl_bn_backward with the y mask: dX bit-identical,
+    first-pass sums within fp32 summation order, dz / g_out / dgamma / dbeta as the two-pass form."""
+    from cvlite import ops_nn as nn
+    from cvlite.layers import Conv, ParamStore
+    W = H
+    C = Cout                     # block width: the BN3 channels = the next conv1's input channels
+    dev = torch.device("cuda")
+    st = ParamStore()
+    conv = Conv(st, "c1", 1, C, Cin, 1, "same", bias=False)     # next block's conv1: C -> Cin
+    st.finalize(dev, seed=5)
+    conv.pack()
+    g = torch.Generator(device="cpu").manual_seed(B + H + Cin)
+    dy_next = (torch.randn(B, H, W, Cin, generator=g) * 0.5).to(BF).to(dev)
+    old = (torch.randn(B, H, W, C, generator=g) * 0.5).to(BF).to(dev)      # the shortcut's gradient
+    z = (torch.randn(B, H, W, C, generator=g) * 1.5 + 0.2).to(BF).to(dev)
+    y = torch.relu(torch.randn(B, H, W, C, generator=g)).to(BF).to(dev)   # block output (zeros = masked)
+    mr = torch.empty((B, C, 2), dtype=torch.float32, device=dev)
+    zf = z.double().view(B, H * W, C)
+    mr[..., 0] = zf.mean(1).float()
+    mr[..., 1] = torch.rsqrt(zf.var(1, unbiased=False) + 1e-3).float()
+    gamma = (torch.rand(C, generator=g) + 0.5).to(dev)
+    beta = torch.randn(C, generator=g).to(dev) * 0.3
+    d = conv.dgrad_desc(B, [nn.seg(H, W, H, W, conv.wd)], ld_dst=C, beta=1.0)
+    dx_f = old.clone()
+    sums = torch.empty((B, C, 2), dtype=torch.float64, device=dev)
+    assert nn.conv_igemm_dgrad_bnsum_res(d, dy_next, dx_f, y, z, mr, gamma, beta, sums)
+    dx_p = old.clone()
+    nn.conv_igemm(d, dy_next, dx_p)
+    assert torch.equal(dx_f, dx_p)
+    xh = (z.float() - mr[..., 0].view(B, 1, 1, C)) * mr[..., 1].view(B, 1, 1, C)
+    gm = torch.where(y.float() > 0, dx_p.float(), torch.zeros_like(xh)).double()
+    ref = torch.stack([gm.sum((1, 2)), (gm * xh.double()).sum((1, 2))], -1)
+    torch.testing.assert_close(sums, ref, rtol=1e-5, atol=1e-6 * float(ref.abs().max()))
+    HW = H * W
+    dz_f, dz_p = torch.empty_like(z), torch.empty_like(z)
+    go_f, go_p = torch.empty_like(z), torch.empty_like(z)
+    dg_f, db_f = torch.zeros(C, device=dev), torch.zeros(C, device=dev)
+    dg_p, db_p = torch.zeros(C, device=dev), torch.zeros(C, device=dev)
+    nn.bn_backward_res_sums(dx_f, y, z, mr, gamma, sums, dz_f, go_f, dg_f, db_f, B, HW, C)
+    nn.bn_backward(dx_p, y, z, mr, gamma, dz_p, go_p, dg_p, db_p, B, HW, C)
+    assert torch.equal(go_f, go_p)
+    torch.testing.assert_close(dz_f.float(), dz_p.float(), rtol=1e-2, atol=1e-2 * float(dz_p.float().abs().max()))
+    torch.testing.assert_close(dg_f, dg_p, rtol=1e-5, atol=1e-5 * float(dg_p.abs().max()))
+    torch.testing.assert_close(db_f, db_p, rtol=1e-5, atol=1e-5 * float(db_p.abs().max()))
