@@ -68,12 +68,28 @@ __global__ void __launch_bounds__(NT) pack_multi_kernel(const cvl_pack_item* __r
   const cvl_pack_item it = items[t.x];
   const int tap = t.y, ci0 = t.z, co0 = t.w;
   __shared__ float tile[64][65];
-  const int col = threadIdx.x & 63, r0 = threadIdx.x >> 6;
   const float* src = it.w + (long)tap * it.Cin * it.Cout;
+  // 16-B loads when the rows allow (Cout % 4: every ResNet / FPN / tower conv), all 4 in flight
+  if ((it.Cout & 3) == 0 && ((uintptr_t)src & 15) == 0) {
+    const int c4 = (threadIdx.x & 15) * 4, r0 = threadIdx.x >> 4;
+    f32x4 v[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int r = r0 + 16 * j, ci = ci0 + r, co = co0 + c4;
+      v[j] = (ci < it.Cin && co < it.Cout) ? *reinterpret_cast<const f32x4*>(src + (long)ci * it.Cout + co)
+                                           : f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) tile[r0 + 16 * j][c4 + e] = v[j][e];
+  } else {
+    const int col = threadIdx.x & 63, r0 = threadIdx.x >> 6;
 #pragma unroll 4
-  for (int j = 0; j < 16; ++j) {
-    const int r = r0 + 4 * j, ci = ci0 + r, co = co0 + col;
-    tile[r][col] = (ci < it.Cin && co < it.Cout) ? src[(long)ci * it.Cout + co] : 0.f;
+    for (int j = 0; j < 16; ++j) {
+      const int r = r0 + 4 * j, ci = ci0 + r, co = co0 + col;
+      tile[r][col] = (ci < it.Cin && co < it.Cout) ? src[(long)ci * it.Cout + co] : 0.f;
+    }
   }
   __syncthreads();
   if (it.f32_out) {        // fp32 parity-mode images, element by element (any Cin_k / Cout_pad)
