@@ -246,3 +246,30 @@ def test_tower0_dgrad_forms_agree(monkeypatch):
     assert e < 2e-2
     for k in ("cls_layer_1/kernel", "reg_layer_1/kernel", "c3_3x3/kernel"):
         assert float((res["0"][k] - res["1"][k]).norm() / res["1"][k].norm()) < 2e-2, k
+
+
+def test_fcos_step_run_to_run_bit_identical():
+    """Reproducibility (SURVEY §7, round-2 review weak #11): two trainers built from the same seed run
+    one graph-replayed step on the same 512x512 batch and end with bit-identical parameters, momentum
+    buffers and losses.  The split reductions (weight-gradient slabs, split-K, gradient norm) sum in
+    a fixed order; the fused BN statistics add per-workgroup fp32 partials into fp64 with atomics,
+    which is order-independent whenever the partials' exact sum fits fp64's 53 bits (24-bit fp32
+    mantissas of similar magnitude: it does) -- this test is the check of that claim on the bench
+    shapes (4 images: ~64 workgroups of every 1x1 launch add into each image's statistics)."""
+    from cvlite.fcos_net import FCOSNet
+    from cvlite.train_fcos import FCOSTrainer, synthetic_batch
+    C, B, D = 20, 4, 512
+    imgs, boxes, nbox = synthetic_batch(B, D, D, C, seed=7)
+    res = []
+    for _ in range(2):
+        net = FCOSNet(C, seed=3)
+        tr = FCOSTrainer(net, B, (D, D), use_graph=True)
+        tr.load_batch(imgs, boxes, nbox)
+        tr.step()
+        tr.load_batch(imgs, boxes, nbox)
+        tr.step()
+        torch.cuda.synchronize()
+        res.append((net.store.flat.clone(), net.store.mom.clone(), tr.losses.clone()))
+        del tr, net
+    for a, b in zip(res[0], res[1]):
+        assert torch.equal(a, b)
