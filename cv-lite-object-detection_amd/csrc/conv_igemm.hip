@@ -702,6 +702,9 @@ extern "C" int cvl_conv_igemm_dgrad_bnsum_res(const cvl_conv_desc* d, const void
   *fused = 0;
   if (!cvl_env_flag("CVL_NO_BNSUM_FUSE") && !cvl_env_flag("CVL_NO_BNSUM_RES") && d->prec == CVL_PREC_BF16 &&
       d->mode == CVL_CONV_DGRAD && !d->dst_f32 && d->beta != 0.f && d->KH == 1 && d->KW == 1 && d->stride == 1 &&
+      // small maps: the fused launch (64-wide N tiles, three prefetched operands) loses to the
+      // plain one + the separate pass (A/B per stage; CVL_BNSUM_RES_MIN_HW)
+      (long)d->seg[0].Hr * d->seg[0].Wr >= cvl_env_int("CVL_BNSUM_RES_MIN_HW", 4096) &&
       d->Cin % 32 == 0 && d->Npad % 32 == 0 && d->ld_dst % 8 == 0 && d->dst_coff % 8 == 0 && d->n_store % 8 == 0 &&
       src && dst) {
     ConvArgs chk;
