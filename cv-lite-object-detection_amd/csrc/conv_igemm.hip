@@ -668,7 +668,9 @@ extern "C" int cvl_conv_igemm_dgrad_bnsum(const cvl_conv_desc* d, const void* sr
   CVL_CHECK_ARG(d && fused && z && mean_rstd && gamma && beta && sums);
   *fused = 0;
   if (!cvl_env_flag("CVL_NO_BNSUM_FUSE") && d->prec == CVL_PREC_BF16 && d->mode == CVL_CONV_DGRAD &&
-      !d->dst_f32 && d->beta == 0.f &&
+      // (CVL_BNSUM_MIN_HW: A/B knob; unlike the residual form this one pays on every stage -- a 64x64
+      // floor cost 0.6 %, 32x32 was neutral)
+      !d->dst_f32 && d->beta == 0.f && (long)d->seg[0].Hr * d->seg[0].Wr >= cvl_env_int("CVL_BNSUM_MIN_HW", 0) &&
       d->Cin % 32 == 0 && d->Npad % 32 == 0 && d->ld_dst % 8 == 0 && d->dst_coff % 8 == 0 && d->n_store % 8 == 0 &&
       src && dst) {
     cvl_conv_desc dd;
