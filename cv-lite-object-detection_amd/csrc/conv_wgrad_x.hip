@@ -32,15 +32,18 @@ namespace {
 constexpr int NT = 512, BR = 32, NSLOT = 5;
 constexpr int SEGM = 128;                 // segment / chunk alignment of the M space
 // tile T (co) x T (k), T = 256 (the tower) or 128 (small outputs: 4x fewer fp32 slab bytes per split)
-template <int T>
+// SR: reduction rows per step (one barrier pair): 32, or 64 for the 128-wide tile (the whole 160 KiB
+// of LDS, one workgroup per CU, half the barriers and DMA hand-offs per MFMA)
+template <int T, int SR = BR>
 struct WxCfg {
   static constexpr int BCO = T, BKK = T;
-  static constexpr int YST = BR * BCO;    // bf16 elements of the dY image of a slot
-  static constexpr int SLOT = YST + BR * BKK;
+  static constexpr int YST = SR * BCO;    // bf16 elements of the dY image of a slot
+  static constexpr int SLOT = YST + SR * BKK;
   static constexpr int TM = T / 32, TN = T / 64;   // 8 waves as 2 (co) x 4 (k)
   static constexpr int LPR = T / 8;       // DMA lanes per row (16-B pieces)
   static constexpr int RPI = 64 / LPR;    // rows per DMA instruction
-  static constexpr int J = BR / (8 * RPI);  // DMA instructions per wave per operand and step
+  static constexpr int J = SR / (8 * RPI);  // DMA instructions per wave per operand and step
+  static constexpr int KS = SR / BR;      // 32-deep MFMA sub-steps per step
 };
 constexpr int kMaxGroups = 2;
 constexpr unsigned kRecords = 0x7fffffffu;
@@ -63,9 +66,9 @@ __device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t r, const cvl_bf16* 
                                            0, 0);
 }
 
-template <int T>
+template <int T, int SR = BR>
 __global__ void __launch_bounds__(NT) conv_wgrad_x_kernel(WxArgs g) {
-  using C = WxCfg<T>;
+  using C = WxCfg<T, SR>;
   constexpr int BCO = C::BCO, BKK = C::BKK, YST = C::YST, SLOT = C::SLOT, TM = C::TM, TN = C::TN;
   constexpr int J = C::J;
   __shared__ __attribute__((aligned(16))) cvl_bf16 lds[NSLOT * SLOT];
@@ -79,7 +82,7 @@ __global__ void __launch_bounds__(NT) conv_wgrad_x_kernel(WxArgs g) {
   const int co0 = (tile % g.co_tiles) * BCO, k0 = (tile / g.co_tiles) * BKK;
   const int m_lo = g.g_m0[grp] + split * g.chunk;
   const int m_hi = min(m_lo + g.chunk, g.g_m1[grp]);
-  const int nsteps = m_hi > m_lo ? (m_hi - m_lo) / BR : 0;
+  const int nsteps = m_hi > m_lo ? (m_hi - m_lo) / SR : 0;
 
   // ---- per-lane DMA constants: rows rr + 8 RPI j of each step, 16-B piece pc of the row ---------
   const int rr = C::RPI * wave + lane / C::LPR, pc = lane % C::LPR;
@@ -113,8 +116,8 @@ __global__ void __launch_bounds__(NT) conv_wgrad_x_kernel(WxArgs g) {
     sbase = (int)S.src_base; simg = (int)S.src_img; dbase = (int)S.dst_base; dimg = (int)S.dst_img;
     seg_end = sg + 1 < a.nseg ? a.seg[sg + 1].m_start : 0x7fffffff;
     const int HW = Hr * Wr;
-    d_img = BR / HW;
-    const int rem = BR - d_img * HW;
+    d_img = SR / HW;
+    const int rem = SR - d_img * HW;
     d_oy = rem / Wr;
     d_ox = rem - d_oy * Wr;
 #pragma unroll
@@ -141,8 +144,8 @@ __global__ void __launch_bounds__(NT) conv_wgrad_x_kernel(WxArgs g) {
       const bool xv = rv && kok && (unsigned)iy < (unsigned)Hs && (unsigned)ix < (unsigned)Ws;
       const int pix = sbase + cimg[j] * simg + iy * Ws + ix;
       dma16(rsX, Xb + (8 * C::RPI * j + C::RPI * wave) * BKK, xv ? (unsigned)(pix * pixb) + xcol : kOOB);
-      // advance the row by BR: (img, y, x) with one carry per level (d_ox < Wr, d_oy < Hr)
-      cml[j] += BR;
+      // advance the row by SR: (img, y, x) with one carry per level (d_ox < Wr, d_oy < Hr)
+      cml[j] += SR;
       cox[j] += d_ox;
       const int cy = cox[j] >= Wr;
       cox[j] -= cy ? Wr : 0;
@@ -151,7 +154,7 @@ __global__ void __launch_bounds__(NT) conv_wgrad_x_kernel(WxArgs g) {
       coy[j] -= cq ? Hr : 0;
       cimg[j] += d_img + cq;
     }
-    im += BR;
+    im += SR;
     ++ist;
     cslot = cslot == NSLOT - 1 ? 0 : cslot + 1;
   };
@@ -200,30 +203,41 @@ __global__ void __launch_bounds__(NT) conv_wgrad_x_kernel(WxArgs g) {
     wait_vm<PW>();                              // step st+1 (read next phase)
     issue();                                    // step st+3
     const unsigned base = lds0 + rslot * (SLOT * 2);
-    s16x4 al[TM], ah[TM], bl[TN], bh[TN];
+    constexpr int KS = C::KS;
+    s16x4 al[KS][TM], ah[KS][TM], bl[KS][TN], bh[KS][TN];
 #pragma unroll
-    for (int i = 0; i < TM; ++i) { al[i] = ds_tr16(base + ya[i]); ah[i] = ds_tr16(base + yb[i]); }
+    for (int h = 0; h < KS; ++h) {               // sub-step h: rows h*32 .. h*32+31 of the slot images
+      const unsigned yo = base + h * BR * BCO * 2, xo = base + h * BR * BKK * 2;
 #pragma unroll
-    for (int j = 0; j < TN; ++j) { bl[j] = ds_tr16(base + xa[j]); bh[j] = ds_tr16(base + xb[j]); }
+      for (int i = 0; i < TM; ++i) { al[h][i] = ds_tr16(yo + ya[i]); ah[h][i] = ds_tr16(yo + yb[i]); }
+#pragma unroll
+      for (int j = 0; j < TN; ++j) { bl[h][j] = ds_tr16(xo + xa[j]); bh[h][j] = ds_tr16(xo + xb[j]); }
+    }
     bar();
     lgkm_wait();
 #pragma unroll
-    for (int i = 0; i < TM; ++i) { tr_pin(al[i]); tr_pin(ah[i]); }
+    for (int h = 0; h < KS; ++h) {
 #pragma unroll
-    for (int j = 0; j < TN; ++j) { tr_pin(bl[j]); tr_pin(bh[j]); }
-    s16x8 fa[TM], fb[TN];
+      for (int i = 0; i < TM; ++i) { tr_pin(al[h][i]); tr_pin(ah[h][i]); }
 #pragma unroll
-    for (int i = 0; i < TM; ++i) fa[i] = tr_join(al[i], ah[i]);
-#pragma unroll
-    for (int j = 0; j < TN; ++j) fb[j] = tr_join(bl[j], bh[j]);
+      for (int j = 0; j < TN; ++j) { tr_pin(bl[h][j]); tr_pin(bh[h][j]); }
+    }
     __builtin_amdgcn_sched_barrier(0);
     __builtin_amdgcn_s_setprio(1);
 #pragma unroll
-    for (int i = 0; i < TM; ++i)
+    for (int h = 0; h < KS; ++h) {
+      s16x8 fa[TM], fb[TN];
 #pragma unroll
-      for (int j = 0; j < TN; ++j)
-        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, fa[i]),
-                                                             __builtin_bit_cast(bf16x8, fb[j]), acc[i][j], 0, 0, 0);
+      for (int i = 0; i < TM; ++i) fa[i] = tr_join(al[h][i], ah[h][i]);
+#pragma unroll
+      for (int j = 0; j < TN; ++j) fb[j] = tr_join(bl[h][j], bh[h][j]);
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, fa[i]),
+                                                               __builtin_bit_cast(bf16x8, fb[j]), acc[i][j], 0, 0, 0);
+    }
     __builtin_amdgcn_s_setprio(0);
     __builtin_amdgcn_sched_barrier(0);
     bar();
@@ -256,7 +270,7 @@ __global__ void __launch_bounds__(NT) conv_wgrad_x_kernel(WxArgs g) {
 }
 
 struct WxPlan {
-  int T, ngroups, spg, tiles, co_tiles, nsplit, chunk;
+  int T, SR, ngroups, spg, tiles, co_tiles, nsplit, chunk;
   int g_m0[kMaxGroups], g_m1[kMaxGroups];
   size_t slab;
 };
@@ -304,13 +318,15 @@ inline bool wx_plan(const cvl_conv_desc* d, int ngroups, ConvArgs* a, WxPlan* p)
     if ((T == 256 && a->Npad % T) || a->K < cvl_env_int(T == 256 ? "CVL_WGX_MIN_K" : "CVL_WGX_MIN_K128", T == 256 ? 256 : 64))
       continue;
     const int tg = ((a->Npad + T - 1) / T) * ((a->K + T - 1) / T) * ngroups;
+    const bool sr64 = T == 128 && cvl_env_int("CVL_WGX_SR", 64) == 64;
     const double step_us =
-        T == 256 ? cvl_env_int("CVL_WGX_STEP", 80) / 100.0 : cvl_env_int("CVL_WGX_STEP128", 80) / 100.0;
+        T == 256 ? cvl_env_int("CVL_WGX_STEP", 80) / 100.0
+                 : (sr64 ? cvl_env_int("CVL_WGX_STEP64", 120) / 200.0 : cvl_env_int("CVL_WGX_STEP128", 80) / 100.0);
     const double slab_us = (double)T * T * 4 * 2 / 5.0e6 * cvl_env_int("CVL_WGX_SLAB_PCT", 100) / 100.0;
     int max_s = mg / 512;
     if (max_s < 1) max_s = 1;
     if (max_s > 2048 / tg) max_s = 2048 / tg > 1 ? 2048 / tg : 1;
-    const int per_round = T == 256 ? 256 : 512;   // the 128-wide tile (80 KiB of LDS) runs 2 per CU
+    const int per_round = T == 256 || sr64 ? 256 : 512;   // the 32-row 128-wide tile (80 KiB of LDS): 2 per CU
     for (int s = 1; s <= max_s; ++s) {
       const int rounds = (tg * s + per_round - 1) / per_round;
       const int chunk = ((mg + s - 1) / s + SEGM - 1) / SEGM * SEGM;
@@ -330,6 +346,10 @@ inline bool wx_plan(const cvl_conv_desc* d, int ngroups, ConvArgs* a, WxPlan* p)
   }
   if (!best_T) return false;
   p->T = best_T;
+  // 64-row steps on the 128-wide tile (CVL_WGX_SR=32 reverts): one workgroup per CU, half the
+  // splits of the 32-row form at the same workgroup count per CU-round -- half the slab bytes (in-step
+  // trace: the reductions 90 -> 63 / 133 -> 100 us per batch, the kernels +1-3 us; FCOS +0.6 %)
+  p->SR = best_T == 128 && cvl_env_int("CVL_WGX_SR", 64) == 64 ? 64 : 32;
   p->co_tiles = (a->Npad + best_T - 1) / best_T;
   p->tiles = p->co_tiles * ((a->K + best_T - 1) / best_T);
   const int forced = cvl_env_int("CVL_WGX_SPLITS", 0);
@@ -382,6 +402,7 @@ int cvl_conv_wgrad_x(const cvl_conv_desc* d, int ngroups, const void* x, const v
     if (gs) return gs;
   }
   if (p.T == 256) hipLaunchKernelGGL(conv_wgrad_x_kernel<256>, dim3(p.tiles * p.nsplit * ngroups), dim3(NT), 0, s, g);
+  else if (p.SR == 64) hipLaunchKernelGGL((conv_wgrad_x_kernel<128, 64>), dim3(p.tiles * p.nsplit * ngroups), dim3(NT), 0, s, g);
   else hipLaunchKernelGGL(conv_wgrad_x_kernel<128>, dim3(p.tiles * p.nsplit * ngroups), dim3(NT), 0, s, g);
   int st = cvl_launch_status();
   if (st || g.direct) return st;
