@@ -194,7 +194,7 @@ PMC_FILE = "profiles/r03c_pmc_tower_conv.json"
 
 
 def pmc_traffic(kname):
-    """Per-launch HBM bytes of the dominant kernel, measured by tools/pmc_tower.sh (committed); null
+    """Per-launch HBM bytes of the dominant kernel, measured by tools/pmc3.sh (committed); null
     when the committed measurement is of a different kernel than the one this run launched."""
     p = os.path.join(ROOT, PMC_FILE)
     if not os.path.exists(p):
