@@ -780,6 +780,68 @@ __global__ void maxpool_fwd_kernel(const cvl_bf16* x, cvl_bf16* y, uint8_t* arg,
   }
 }
 
+// The stem's BN -> ReLU -> ZeroPadding2D(1) -> MaxPool 3x3/2 in one pass (Keras ResNet50 conv1_bn,
+// conv1_relu, pool1_pad, pool1_pool): each window tap is normalised from z with the per-image
+// (mean, rstd) (bn_affine, ReLU, bf16 rounding -- the value bn_apply would have stored) and pooled as
+// maxpool_fwd_kernel does (padding taps 0, first maximum in window order).  The full-size BN output
+// is never written: the stem's backward rebuilds the ReLU mask from z and routes through argmax.
+__global__ void bn_relu_maxpool_kernel(const cvl_bf16* z, const float* __restrict__ mr, const float* __restrict__ gamma,
+                                       const float* __restrict__ beta, cvl_bf16* y, uint8_t* arg, int B, int H,
+                                       int W, int C, int Ho, int Wo) {
+  const int C8 = C / 8;
+  const long total = (long)B * Ho * Wo * C8;
+  for (long i = blockIdx.x * (long)NT + threadIdx.x; i < total; i += (long)gridDim.x * NT) {
+    const long pix = i / C8;
+    const int c0 = (int)(i - pix * C8) * 8;
+    const int b = (int)(pix / ((long)Ho * Wo));
+    const int q = (int)(pix - (long)b * Ho * Wo);
+    const int oy = q / Wo, ox = q - (q / Wo) * Wo;
+    s16x8 raw[9];
+    bool ok[9];
+#pragma unroll
+    for (int t = 0; t < 9; ++t) {
+      const int iy = oy * 2 - 1 + t / 3, ix = ox * 2 - 1 + t % 3;
+      ok[t] = iy >= 0 && ix >= 0 && iy < H && ix < W;
+      const int cy = min(max(iy, 0), H - 1), cx = min(max(ix, 0), W - 1);
+      raw[t] = *reinterpret_cast<const s16x8*>(z + (((long)b * H + cy) * W + cx) * C + c0);
+    }
+    float m[8], rs[8], ga[8], be[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const long bc = (long)b * C + c0 + u;
+      m[u] = mr[bc * 2];
+      rs[u] = mr[bc * 2 + 1];
+      ga[u] = gamma[c0 + u];
+      be[u] = beta[c0 + u];
+    }
+    float best[8];
+    unsigned long long bi = 0;
+#pragma unroll
+    for (int u = 0; u < 8; ++u) best[u] = -INFINITY;
+#pragma unroll
+    for (int t = 0; t < 9; ++t) {
+      float v[8];
+      unpack8(raw[t], v);
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const float a = bn_affine(v[u], m[u], rs[u], ga[u], be[u]);
+        v[u] = a > 0.f ? a : 0.f;
+      }
+      unpack8(pack8(v), v);                         // the bf16 value the BN output would hold
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const float vv = ok[t] ? v[u] : 0.f;
+        if (vv > best[u]) {
+          best[u] = vv;
+          bi = (bi & ~(0xffull << (8 * u))) | ((unsigned long long)t << (8 * u));
+        }
+      }
+    }
+    *reinterpret_cast<s16x8*>(y + pix * C + c0) = pack8(best);
+    *reinterpret_cast<unsigned long long*>(arg + pix * C + c0) = bi;
+  }
+}
+
 // a thread owns 8 channels of one input pixel: the (at most 2 x 2) windows holding it are visited
 // with their dy and argmax bytes (one 8-byte load) loaded together
 __global__ void maxpool_bwd_kernel(const cvl_bf16* dy, const uint8_t* arg, cvl_bf16* dx, int B, int H,
@@ -1450,6 +1512,16 @@ extern "C" int cvl_bn_backward_res_sums(const void* dy, const void* y, const voi
   hipLaunchKernelGGL((bn_bwd_kernel<1, 1>), dim3(nchunk, B), dim3(NT), 0, S_, (const cvl_bf16*)dy, (const cvl_bf16*)y,
                      (const cvl_bf16*)z, mean_rstd, gamma, sums, (cvl_bf16*)dz, (cvl_bf16*)g_out, (float*)nullptr,
                      C, HW, rpb, 1, 0.f, BnPG{dgamma, dbeta, conv_dbias, beta_acc}, (const float*)nullptr, INFINITY);
+  return cvl_launch_status();
+}
+
+extern "C" int cvl_bn_relu_maxpool3x3s2(const void* z, const float* mean_rstd, const float* gamma, const float* beta,
+                                        void* y, uint8_t* argmax, int B, int H, int W, int C, cvl_stream_t stream) {
+  CVL_CHECK_ARG(z && mean_rstd && gamma && beta && y && argmax && C % 8 == 0 && B > 0);
+  const int Ho = (H + 2 - 3) / 2 + 1, Wo = (W + 2 - 3) / 2 + 1;
+  const long total = (long)B * Ho * Wo * (C / 8);
+  hipLaunchKernelGGL(bn_relu_maxpool_kernel, dim3(grid_for(total)), dim3(NT), 0, S_, (const cvl_bf16*)z, mean_rstd,
+                     gamma, beta, (cvl_bf16*)y, argmax, B, H, W, C, Ho, Wo);
   return cvl_launch_status();
 }
 

@@ -332,6 +332,13 @@ def bn_backward_relu(dy, z, mean_rstd, gamma, beta, dz, dgamma, dbeta, B, HW, C,
               ptr(dgamma), ptr(dbeta), float(beta_acc), ptr(conv_dbias), B, HW, C, stream())
 
 
+def bn_relu_maxpool3x3s2(z, mean_rstd, gamma, beta, y, argmax):
+    """The stem's BN -> ReLU -> pad 1 -> max-pool 3x3/2 from the pre-BN z (bf16), no full-size BN output."""
+    B, H, W, C = z.shape
+    _lib.call("cvl_bn_relu_maxpool3x3s2", ptr(z), ptr(mean_rstd), ptr(gamma), ptr(beta), ptr(y), ptr(argmax), B, H,
+              W, C, stream())
+
+
 def maxpool3x3s2(x, y, argmax):
     B, H, W, C = x.shape
     _lib.call("cvl_maxpool3x3s2_f32" if _is_f32(x) else "cvl_maxpool3x3s2", ptr(x), ptr(y), ptr(argmax), B, H, W, C, stream())

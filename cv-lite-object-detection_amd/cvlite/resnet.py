@@ -16,6 +16,8 @@ from . import ops_nn as nn
 from .layers import join_side, BF16, BatchNorm, Conv, ConvBN, StatsArena
 
 STEM_K = 7
+# the stem's BN -> ReLU -> max-pool as one pass from z (CVL_STEM_NO_FUSE_POOL=1: BN apply + pool)
+FUSE_POOL = os.environ.get("CVL_STEM_NO_FUSE_POOL", "0") != "1"
 STEM_KP = int(os.environ.get("CVL_STEM_KP", 192))   # im2col K = 7*7*3 = 147 padded: 192 = 3 x 64 lets the
 #                                                      LDS-DMA kernels take the stem (+0.6 % step vs 160)
 
@@ -70,16 +72,27 @@ class Stem(object):
         else:
             A = x                                   # the fp32 image itself (direct conv)
             nn.conv_igemm(self._desc7(B, H, W, Ho, Wo), x, z, stats)
-        y, mr = self.bn.normalize(z, stats, B, Ho * Wo, True, train=train)
         Hp, Wp = (Ho + 2 - 3) // 2 + 1, (Wo + 2 - 3) // 2 + 1
         p = torch.empty((B, Hp, Wp, 64), dtype=act, device=x.device)
         arg = torch.empty((B, Hp, Wp, 64), dtype=torch.uint8, device=x.device)
+        if act == BF16 and FUSE_POOL:
+            # conv1_bn -> relu -> pool1 in one pass from z: the 256x256x64 BN output is never stored
+            # (the backward rebuilds the ReLU mask from z and routes through argmax)
+            if train:
+                mr = torch.empty((B, 64, 2), dtype=torch.float32, device=x.device)
+                nn.bn_finalize(stats, mr, self.bn.run_mean, self.bn.run_var, B, 64, Ho * Wo, self.bn.eps,
+                               self.bn.momentum)
+            else:
+                mr = self.bn.moving_mean_rstd(B)
+            nn.bn_relu_maxpool3x3s2(z, mr, self.bn.gamma, self.bn.beta, p, arg)
+            return p, (A, z, None, mr, arg, B, Ho, Wo)
+        y, mr = self.bn.normalize(z, stats, B, Ho * Wo, True, train=train)
         nn.maxpool3x3s2(y, p, arg)
         return p, (A, z, y, mr, arg, B, Ho, Wo)
 
     def backward(self, dp, saved):
         A, z, y, mr, arg, B, Ho, Wo = saved
-        dy = torch.empty_like(y)
+        dy = torch.empty_like(z)
         nn.maxpool3x3s2_backward(dp, arg, dy)
         dz = torch.empty_like(z)
         st = self.bn.store

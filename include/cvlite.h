@@ -286,6 +286,11 @@ int cvl_bn_backward_relu6(const void* dy, const void* z, const float* mean_rstd,
                           float* dbeta, float beta_acc, float* conv_dbias, int B, int HW, int C, cvl_stream_t stream);
 
 /* ResNet50 pool1: ZeroPadding2D(1) + MaxPooling2D(3, 2); argmax [B][Ho][Wo][C] uint8 (0..8). */
+/* Stem BN -> ReLU -> ZeroPadding2D(1) -> MaxPool 3x3/2 fused (Keras ResNet50 conv1_bn .. pool1_pool):
+ * from the pre-BN z [B,H,W,C] bf16 and (mean, rstd) [B][C][2]; writes the pooled y and argmax as
+ * cvl_maxpool3x3s2 would from the stored BN output (bit-identical), without that full-size output. */
+int cvl_bn_relu_maxpool3x3s2(const void* z, const float* mean_rstd, const float* gamma, const float* beta, void* y,
+                             uint8_t* argmax, int B, int H, int W, int C, cvl_stream_t stream);
 int cvl_maxpool3x3s2(const void* x, void* y, uint8_t* argmax, int B, int H, int W, int C,
                      cvl_stream_t stream);
 int cvl_maxpool3x3s2_backward(const void* dy, const uint8_t* argmax, void* dx, int B, int H, int W,

@@ -372,3 +372,29 @@ def test_dgrad_fused_bn_backward_residual(B, H, Cin, Cout, monkeypatch):
         dx_2 = old.clone()
         assert not nn.conv_igemm_dgrad_bnsum_res(d, dy_next, dx_2, y, z, mr, gamma, beta, sums2)
         assert torch.equal(dx_2, dx_p) and float(sums2.abs().max()) == 0.0
+
+
+@pytest.mark.parametrize("B,H,W", [(2, 256, 256), (3, 17, 23)])
+def test_bn_relu_maxpool_matches_apply_then_pool(B, H, W):
+    """cvl_bn_relu_maxpool3x3s2 (the stem's BN -> ReLU -> pad 1 -> max-pool 3x3/2 from z) equals
+    cvl_bn_apply (ReLU) + cvl_maxpool3x3s2 on the same operands, pooled values and argmax bit-exact
+    (zero padding ties and all-masked windows included)."""
+    from cvlite import ops_nn as nn
+    C = 64
+    dev = torch.device("cuda")
+    g = torch.Generator(device="cpu").manual_seed(B * H + W)
+    z = (torch.randn(B, H, W, C, generator=g) * 2.0).to(BF).to(dev)
+    mr = torch.stack([torch.randn(B, C, generator=g) * 0.3, torch.rand(B, C, generator=g) + 0.5], -1).float().to(dev)
+    gamma = (torch.rand(C, generator=g) + 0.5).to(dev)
+    beta = (torch.randn(C, generator=g) * 0.5).to(dev)
+    Ho, Wo = (H + 2 - 3) // 2 + 1, (W + 2 - 3) // 2 + 1
+    y = torch.empty_like(z)
+    nn.bn_apply(z, mr, gamma, beta, None, y, B, H * W, C, 1)
+    p_ref = torch.empty((B, Ho, Wo, C), dtype=BF, device=dev)
+    a_ref = torch.empty((B, Ho, Wo, C), dtype=torch.uint8, device=dev)
+    nn.maxpool3x3s2(y, p_ref, a_ref)
+    p = torch.empty_like(p_ref)
+    a = torch.empty_like(a_ref)
+    nn.bn_relu_maxpool3x3s2(z, mr, gamma, beta, p, a)
+    assert torch.equal(p.view(torch.int16), p_ref.view(torch.int16))
+    assert torch.equal(a, a_ref)
