@@ -54,6 +54,7 @@ SIGNATURES = {
     "cvl_bn_backward": (c_int, [P, P, P, P, P, P, c_size_t, P, P, P, P, c_float, P, c_int, c_int, c_int, P]),
     "cvl_bn_backward_relu": (c_int, [P, P, P, P, P, P, c_size_t, P, P, P, c_float, P, c_int, c_int, c_int, P]),
     "cvl_maxpool3x3s2": (c_int, [P, P, P, c_int, c_int, c_int, c_int, P]),
+    "cvl_maxpool_bn_backward_relu": (c_int, [P, P, P, P, P, P, P, ctypes.c_size_t, P, P, P, c_float, P, c_int, c_int, c_int, c_int, P]),
     "cvl_bn_relu_maxpool3x3s2": (c_int, [P, P, P, P, P, P, c_int, c_int, c_int, c_int, P]),
     "cvl_maxpool3x3s2_backward": (c_int, [P, P, P, c_int, c_int, c_int, c_int, P]),
     "cvl_upsample2x_add": (c_int, [P, P, P, c_int, c_int, c_int, c_int, P]),

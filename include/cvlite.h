@@ -291,6 +291,14 @@ int cvl_bn_backward_relu6(const void* dy, const void* z, const float* mean_rstd,
  * cvl_maxpool3x3s2 would from the stored BN output (bit-identical), without that full-size output. */
 int cvl_bn_relu_maxpool3x3s2(const void* z, const float* mean_rstd, const float* gamma, const float* beta, void* y,
                              uint8_t* argmax, int B, int H, int W, int C, cvl_stream_t stream);
+/* Its backward fused into conv1_bn's: cvl_bn_backward_relu of the pool-input gradient, which both BN
+ * passes form on the fly from the pooled gradient dp [B][Ho][Wo][C] and argmax (as
+ * cvl_maxpool3x3s2_backward would, bit-exact); H, W: the BN map.  workspace >=
+ * cvl_bn_backward_workspace_size(B, H*W, C). */
+int cvl_maxpool_bn_backward_relu(const void* dp, const uint8_t* argmax, const void* z, const float* mean_rstd,
+                                 const float* gamma, const float* beta, void* workspace, size_t workspace_bytes,
+                                 void* dz, float* dgamma, float* dbeta, float beta_acc, float* conv_dbias, int B,
+                                 int H, int W, int C, cvl_stream_t stream);
 int cvl_maxpool3x3s2(const void* x, void* y, uint8_t* argmax, int B, int H, int W, int C,
                      cvl_stream_t stream);
 int cvl_maxpool3x3s2_backward(const void* dy, const uint8_t* argmax, void* dx, int B, int H, int W,

@@ -398,3 +398,32 @@ def test_bn_relu_maxpool_matches_apply_then_pool(B, H, W):
     nn.bn_relu_maxpool3x3s2(z, mr, gamma, beta, p, a)
     assert torch.equal(p.view(torch.int16), p_ref.view(torch.int16))
     assert torch.equal(a, a_ref)
+
+
+@pytest.mark.parametrize("B,H,W", [(2, 256, 256), (3, 17, 23)])
+def test_maxpool_bn_backward_matches_two_step(B, H, W):
+    """cvl_maxpool_bn_backward_relu (the stem's pool backward inside conv1_bn's backward passes) equals
+    cvl_maxpool3x3s2_backward + cvl_bn_backward_relu: the routed gradient is the same bf16 value in
+    the same row order, so dz, dgamma and dbeta are bit-identical."""
+    from cvlite import ops_nn as nn
+    C = 64
+    dev = torch.device("cuda")
+    g = torch.Generator(device="cpu").manual_seed(B * H + W + 1)
+    z = (torch.randn(B, H, W, C, generator=g) * 2.0).to(BF).to(dev)
+    mr = torch.stack([torch.randn(B, C, generator=g) * 0.3, torch.rand(B, C, generator=g) + 0.5], -1).float().to(dev)
+    gamma = (torch.rand(C, generator=g) + 0.5).to(dev)
+    beta = (torch.randn(C, generator=g) * 0.5).to(dev)
+    Ho, Wo = (H + 2 - 3) // 2 + 1, (W + 2 - 3) // 2 + 1
+    p = torch.empty((B, Ho, Wo, C), dtype=BF, device=dev)
+    arg = torch.empty((B, Ho, Wo, C), dtype=torch.uint8, device=dev)
+    nn.bn_relu_maxpool3x3s2(z, mr, gamma, beta, p, arg)
+    dp = torch.randn(B, Ho, Wo, C, generator=g).to(BF).to(dev)
+    dy = torch.empty_like(z)
+    nn.maxpool3x3s2_backward(dp, arg, dy)
+    dz_r, dz_f = torch.empty_like(z), torch.empty_like(z)
+    dg_r, db_r = torch.zeros(C, device=dev), torch.zeros(C, device=dev)
+    dg_f, db_f = torch.zeros(C, device=dev), torch.zeros(C, device=dev)
+    nn.bn_backward_relu(dy, z, mr, gamma, beta, dz_r, dg_r, db_r, B, H * W, C)
+    nn.maxpool_bn_backward_relu(dp, arg, z, mr, gamma, beta, dz_f, dg_f, db_f)
+    assert torch.equal(dz_f.view(torch.int16), dz_r.view(torch.int16))
+    assert torch.equal(dg_f, dg_r) and torch.equal(db_f, db_r)
