@@ -421,7 +421,14 @@ extern "C" size_t cvl_conv_wgrad_workspace_size(const cvl_conv_desc* d) {
 extern "C" int cvl_conv_wgrad_grouped(const cvl_conv_desc* d, int ngroups, const void* x, const void* dy,
                                       float* const* dw, float beta, void* workspace, size_t workspace_bytes,
                                       cvl_stream_t stream) {
-  CVL_CHECK_ARG(dw && d);
+  CVL_CHECK_ARG(dw && d && ngroups >= 1);
+  // every writer of a dW with a pending deferred reduction (the split kernels below, but also the
+  // unsplit small-N / generic / fp32 paths that write dW directly) must see that reduction land
+  // first: flush here, before any path is chosen
+  for (int gq = 0; gq < ngroups; ++gq) {
+    const int gs = cvl_wgrad_defer_guard(dw[gq], (hipStream_t)stream);
+    if (gs) return gs;
+  }
   if (d->prec == CVL_PREC_F32)                       // parity mode (parity_f32.hip)
     return cvl_conv_wgrad_f32(d, ngroups, x, dy, dw, beta, workspace, workspace_bytes, (hipStream_t)stream);
   CVL_CHECK_ARG(d->prec == CVL_PREC_BF16);

@@ -186,6 +186,7 @@ class PackPlan(object):
                     for co0 in range(0, co_hi, 64):
                         tiles.append((i, tap, ci0, co0))
         raw = bytes(items)
+        self.host_items = items          # geometry of every entry (host copy of the device table)
         self.items = torch.frombuffer(bytearray(raw), dtype=torch.uint8).to(device)
         self.tiles = torch.tensor(tiles, dtype=torch.int32, device=device)
         self.ntiles = len(tiles)

@@ -538,3 +538,47 @@ def test_conv_wgrad_deferred_reduction():
         assert torch.equal(a, b)
     # and the accumulated one is 0.5 + 2 * dW (fp32 tolerance)
     torch.testing.assert_close(imm[2], 0.5 + 2 * imm[0], rtol=1e-5, atol=1e-3)
+
+
+@pytest.mark.gpu
+def test_conv_wgrad_deferred_then_direct_writer():
+    """a dW whose split reduction is still pending (deferral on, beta 0) is then
+    accumulated (beta 1) by a launch on a DIRECT-writing path (the small-N head kernel, no slabs):
+    cvl_conv_wgrad_grouped flushes the pending record before any path writes, so the result is
+    bit-identical to the immediate form (without the guard the late reduction overwrote the
+    direct write)."""
+    from cvlite import _lib, ops_nn as nn
+    g = torch.Generator(device="cuda").manual_seed(5)
+    B, H, W, Cin, Cout = 16, 32, 32, 256, 1024
+    x1 = torch.randn((B, H, W, Cin), generator=g, device="cuda").to(BF)
+    dy1 = torch.randn((B, H, W, Cout), generator=g, device="cuda").to(BF)
+    wf1 = torch.empty((Cout, Cin), dtype=BF, device="cuda")
+    d1 = nn.make_desc(nn.FWD, B, Cin, 1, 1, 1, 0, 0, Cout, Cout, Cout, [nn.seg(H, W, H, W, wf1)])
+    B2, H2, n2 = 2, 16, 20
+    x2 = torch.randn((B2, H2, H2, Cin), generator=g, device="cuda").to(BF)
+    dy2 = torch.randn((B2, H2, H2, 32), generator=g, device="cuda").to(BF)
+    wf2 = torch.empty((32, 9 * Cin), dtype=BF, device="cuda")
+    d2 = nn.make_desc(nn.FWD, B2, Cin, 3, 3, 1, 1, 1, 32, n2, 32, [nn.seg(H2, H2, H2, H2, wf2)])
+    kinds = []
+
+    def run(deferred):
+        dw = torch.zeros((Cin, Cout), device="cuda")
+        head = dw.view(-1)[:9 * Cin * n2].view(3, 3, Cin, n2)        # same base pointer as dw
+
+        def body():
+            nn.conv_wgrad(d1, x1, dy1, dw)
+            kinds.append(int(_lib.load().cvl_conv_igemm_last_kernel()))
+            nn.conv_wgrad(d2, x2, dy2, head, beta=1.0)
+            kinds.append(int(_lib.load().cvl_conv_igemm_last_kernel()))
+        if deferred:
+            with nn.deferred_wgrad():
+                body()
+                nn.wgrad_flush()
+        else:
+            body()
+        torch.cuda.synchronize()
+        return dw
+
+    imm, dfr = run(False), run(True)
+    assert kinds[0] == 11 and kinds[1] != 11, kinds        # split wgrad_x first, a non-split writer second
+    assert torch.equal(imm, dfr)
