@@ -11,6 +11,10 @@
 //   16 CEN_IN_CLS the centerness logit (and its gradient) is column cc = round_up(C, 8) of the class
 //                 rows (the centre variants' cen_output_l head sits on the cls tower,
 //                 fcos_center.py:85-101; the 8-aligned column lets its weight gradient read it)
+//   32 MASK_T5    the regression mask is the float value targets[5] itself (the drop-in
+//                 smooth_l1_loss / iou_loss(mask=<float map>) of fcos.py:380-441; C = 1)
+// cvl_fcos_loss_ex takes the focal alpha / gamma and the smooth-L1 delta (fcos.py:380, 443-444
+// keywords); cvl_fcos_loss is it with the reference defaults 0.25 / 2 / 1.
 // "smooth L1" is the reference's discontinuous 0.5 d^2 (|d|<1) / |d| (Q8).  One pass reads the
 // predictions and targets once and writes the gradients once (HBM-bound); per-image sums are
 // reduced deterministically (per-tile partials in float64, then a fixed-order second pass).
@@ -31,6 +35,7 @@ struct LossArgs {
   int ld_reg, ld_cls, ld_dreg, ld_dcls, dreg_bf16, dcls_bf16;
   int P, C, reg_type, tiles;
   float grad_scale;
+  float alpha, gamma, delta;
 };
 
 __device__ __forceinline__ void store_g(void* base, size_t idx, float v, int is_bf16) {
@@ -38,26 +43,31 @@ __device__ __forceinline__ void store_g(void* base, size_t idx, float v, int is_
   else reinterpret_cast<float*>(base)[idx] = v;
 }
 
-__device__ __forceinline__ float sl1(float d, float* g) {
+__device__ __forceinline__ float sl1(float d, float delta, float* g) {
   // loss of d = t - x and its derivative w.r.t. x (TF gradient of the tf.where form)
   const float ad = fabsf(d);
-  if (ad < 1.0f) { *g = -d; return 0.5f * d * d; }
+  if (ad < delta) { *g = -d; return 0.5f * d * d; }
   *g = d > 0.f ? -1.0f : (d < 0.f ? 1.0f : 0.0f);
   return ad;
 }
 
-// focal loss term (alpha .25, gamma 2, the reference's stable form) and d/dx
-__device__ __forceinline__ float focal_term(float y, float x, float* g) {
-  const float alpha = 0.25f;
+// q^gamma: the reference default gamma = 2 as a product (the values every training path uses)
+__device__ __forceinline__ float powg(float q, float gamma) { return gamma == 2.0f ? q * q : powf(q, gamma); }
+
+// focal loss term (the reference's stable form, fcos.py:443-462) and d/dx:
+//   y a q^g (L - min(x,0)) + (1-y)(1-a) p^g (L + max(x,0)),  p = sigmoid(x), q = 1 - p, L = log(1+e^-|x|)
+//   d/dx = -y a q^g (g p nlp + q) + (1-y)(1-a) p^g (g q nlq + p)
+__device__ __forceinline__ float focal_term(float y, float x, float alpha, float gamma, float* g) {
   const float e = expf(-fabsf(x));
   const float L = log1pf(e);                       // log(1 + exp(-|x|))
   const float p1 = x >= 0.f ? 1.0f / (1.0f + e) : e / (1.0f + e);   // sigmoid(x)
   const float q1 = x >= 0.f ? e / (1.0f + e) : 1.0f / (1.0f + e);   // 1 - sigmoid(x)
   const float nlp = L - fminf(x, 0.f);             // -log p
   const float nlq = L + fmaxf(x, 0.f);             // -log(1-p)
-  const float wpos = y * alpha * q1 * q1;
-  const float wneg = (1.0f - y) * (1.0f - alpha) * p1 * p1;
-  *g = -y * alpha * q1 * q1 * (2.0f * p1 * nlp + q1) + (1.0f - y) * (1.0f - alpha) * p1 * p1 * (2.0f * q1 * nlq + p1);
+  const float qg = powg(q1, gamma), pg = powg(p1, gamma);
+  const float wpos = y * alpha * qg;
+  const float wneg = (1.0f - y) * (1.0f - alpha) * pg;
+  *g = -wpos * (gamma * p1 * nlp + q1) + wneg * (gamma * q1 * nlq + p1);
   return wpos * nlp + wneg * nlq;
 }
 
@@ -78,23 +88,23 @@ __global__ void __launch_bounds__(kThreads) fcos_loss_kernel(LossArgs a) {
       const float y = t[5 + c];
       tmax = fmaxf(tmax, y);
       float g;
-      s_cls += focal_term(y, xc[c], &g);
+      s_cls += focal_term(y, xc[c], a.alpha, a.gamma, &g);
       if (a.dcls) store_g(a.dcls, cell * a.ld_dcls + c, g * a.grad_scale, a.dcls_bf16);
     }
     if (a.dcls)
       for (int c = a.C; c < a.ld_dcls; ++c) store_g(a.dcls, cell * a.ld_dcls + c, 0.f, a.dcls_bf16);
-    const float mask = tmax >= 1.0f ? 1.0f : 0.0f;
+    const float mask = (a.reg_type & 32) ? t[5] : (tmax >= 1.0f ? 1.0f : 0.0f);
     float g[5] = {0.f, 0.f, 0.f, 0.f, 0.f};
     // centerness: smooth-L1 on sigmoid(logit) (fcos.py:483-486) or focal (centre variants), all cells
     {
       const float x = cen_in_cls ? xc[cc] : xr[4];
       float gc;
       if (focal_cen) {
-        s_cen += focal_term(t[4], x, &gc);
+        s_cen += focal_term(t[4], x, a.alpha, a.gamma, &gc);
       } else {
         const float sg = 1.0f / (1.0f + expf(-x));
         float gd;
-        s_cen += sl1(t[4] - sg, &gd);
+        s_cen += sl1(t[4] - sg, a.delta, &gd);
         gc = gd * sg * (1.0f - sg);
       }
       if (cen_in_cls) {
@@ -108,11 +118,11 @@ __global__ void __launch_bounds__(kThreads) fcos_loss_kernel(LossArgs a) {
         float gd;
         if (sig_reg) {                             // fcos_center_v1.py:115: reg = sigmoid(conv)
           const float sg = 1.0f / (1.0f + expf(-xr[j]));
-          const float l = sl1(t[j] - sg, &gd);
+          const float l = sl1(t[j] - sg, a.delta, &gd);
           s_reg += mask * l;
           g[j] = mask * gd * sg * (1.0f - sg);
         } else {
-          const float l = sl1(t[j] - xr[j], &gd);
+          const float l = sl1(t[j] - xr[j], a.delta, &gd);
           s_reg += mask * l;
           g[j] = mask * gd;
         }
@@ -128,8 +138,8 @@ __global__ void __launch_bounds__(kThreads) fcos_loss_kernel(LossArgs a) {
       const float I = ih * iw;
       const float Ue = th * tw + ph * pw - I + 1.0e-12f;
       const float iou = I / Ue;
-      s_reg += -logf(iou + 1.0e-12f);
-      const float dL = -1.0f / (iou + 1.0e-12f);
+      s_reg += -logf(iou + 1.0e-12f) * mask;
+      const float dL = -mask / (iou + 1.0e-12f);
       const float dI = (Ue + I) / (Ue * Ue);            // d iou / d I (U depends on -I)
       const float dph = -I * pw / (Ue * Ue), dpw = -I * ph / (Ue * Ue);
       const float gih = ihr > 0.f ? dI * iw : 0.f;
@@ -174,15 +184,17 @@ extern "C" size_t cvl_fcos_loss_workspace_size(int B, int P) {
   return (size_t)B * tiles * 3 * sizeof(double);
 }
 
-extern "C" int cvl_fcos_loss(const float* reg_pred, int ld_reg, const float* cls_pred, int ld_cls,
-                             const float* targets, int B, int P, int num_classes, int reg_type,
-                             float grad_scale, float* losses, void* d_reg, int ld_dreg,
-                             int dreg_dtype, void* d_cls, int ld_dcls, int dcls_dtype,
-                             void* workspace, cvl_stream_t stream) {
+extern "C" int cvl_fcos_loss_ex(const float* reg_pred, int ld_reg, const float* cls_pred, int ld_cls,
+                                const float* targets, int B, int P, int num_classes, int reg_type,
+                                float grad_scale, float alpha, float gamma, float delta, float* losses,
+                                void* d_reg, int ld_dreg, int dreg_dtype, void* d_cls, int ld_dcls, int dcls_dtype,
+                                void* workspace, cvl_stream_t stream) {
   CVL_CHECK_ARG(reg_pred && cls_pred && targets && losses && workspace);
   CVL_CHECK_ARG(B > 0 && P > 0 && num_classes > 0);
   const int kind = reg_type & 3, cen_in_cls = (reg_type & 16) ? 1 : 0;
-  CVL_CHECK_ARG((kind == 0 || kind == 1) && (reg_type & ~31) == 0 && !(kind == 1 && (reg_type & 8)));
+  CVL_CHECK_ARG((kind == 0 || kind == 1) && (reg_type & ~63) == 0 && !(kind == 1 && (reg_type & 8)));
+  CVL_CHECK_ARG(!(reg_type & 32) || num_classes == 1);
+  CVL_CHECK_ARG(gamma >= 0.f && delta > 0.f);
   const int ncls_cols = cen_in_cls ? (num_classes + 7) / 8 * 8 + 1 : num_classes;
   CVL_CHECK_ARG(ld_reg >= (cen_in_cls ? 4 : 5) && ld_cls >= ncls_cols);
   CVL_CHECK_ARG(!d_reg || ld_dreg >= 5);
@@ -194,6 +206,7 @@ extern "C" int cvl_fcos_loss(const float* reg_pred, int ld_reg, const float* cls
   a.ld_reg = ld_reg; a.ld_cls = ld_cls; a.ld_dreg = ld_dreg; a.ld_dcls = ld_dcls;
   a.dreg_bf16 = dreg_dtype; a.dcls_bf16 = dcls_dtype;
   a.P = P; a.C = num_classes; a.reg_type = reg_type; a.grad_scale = grad_scale;
+  a.alpha = alpha; a.gamma = gamma; a.delta = delta;
   a.tiles = (P + kThreads - 1) / kThreads;
   hipLaunchKernelGGL(fcos_loss_kernel, dim3(a.tiles, B), dim3(kThreads), 0, (hipStream_t)stream, a);
   int st = cvl_launch_status();
@@ -201,6 +214,17 @@ extern "C" int cvl_fcos_loss(const float* reg_pred, int ld_reg, const float* cls
   hipLaunchKernelGGL(fcos_loss_finalize, dim3(B), dim3(64), 0, (hipStream_t)stream,
                      (const double*)workspace, losses, a.tiles);
   return cvl_launch_status();
+}
+
+extern "C" int cvl_fcos_loss(const float* reg_pred, int ld_reg, const float* cls_pred, int ld_cls,
+                             const float* targets, int B, int P, int num_classes, int reg_type,
+                             float grad_scale, float* losses, void* d_reg, int ld_dreg,
+                             int dreg_dtype, void* d_cls, int ld_dcls, int dcls_dtype,
+                             void* workspace, cvl_stream_t stream) {
+  CVL_CHECK_ARG((reg_type & 32) == 0);
+  return cvl_fcos_loss_ex(reg_pred, ld_reg, cls_pred, ld_cls, targets, B, P, num_classes, reg_type, grad_scale,
+                          0.25f, 2.0f, 1.0f, losses, d_reg, ld_dreg, dreg_dtype, d_cls, ld_dcls, dcls_dtype,
+                          workspace, stream);
 }
 
 // ---------------------------------------------------------------------------------------------

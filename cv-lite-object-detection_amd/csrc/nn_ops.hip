@@ -430,56 +430,20 @@ struct BnPG {
 // MASK selects the ReLU-mask source at compile time (1: y, 2: bn_affine(z) recomputed, 3: no mask --
 // BN without ReLU; 0: decided at run time from y / bnb) -- the run-time form holds the registers of both paths (pass 0: 215 VGPRs,
 // 2 waves/SIMD; pass 1: 141, 3 waves), the specialised ones fit 4-5 waves
-// POOL: dy is the gradient of the stem's pad-1 / 3x3/2 max-pool OUTPUT (dp [B][Ho][Wo][C] + argmax),
-// routed back to each BN-output pixel on the fly exactly as maxpool_bwd_kernel does (same window
-// order, bf16-rounded): the full-size pool-input gradient is never stored
-struct BnPool {
-  const uint8_t* arg;
-  int W, Ho, Wo;
-};
-
-template <int PASS, int MASK = 0, bool POOL = false>
+template <int PASS, int MASK = 0>
 __global__ void __launch_bounds__(NT) bn_bwd_kernel(const cvl_bf16* __restrict__ dy, const cvl_bf16* __restrict__ y,
                                                     const cvl_bf16* __restrict__ z, const float* __restrict__ mr,
                                                     const float* __restrict__ gamma, const double* __restrict__ sums,
                                                     cvl_bf16* __restrict__ dz, cvl_bf16* __restrict__ g_out,
                                                     float* __restrict__ part, int C, int HW, int rows_per_blk,
                                                     int group, float dz_beta, BnPG pg,
-                                                    const float* __restrict__ bnb, float act_hi, BnPool pool) {
+                                                    const float* __restrict__ bnb, float act_hi) {
   const int b = blockIdx.y;
   const int C8 = C / 8;
   const int tpr = C8 < NT ? C8 : NT;
   const int rpp = NT / tpr;
   const int cg = threadIdx.x % tpr, rsub = threadIdx.x / tpr;
   const int r0 = blockIdx.x * rows_per_blk;
-  // POOL: dy of BN-output pixel rq (channels c0..c0+7) from the pooled gradient
-  auto pooled = [&](int rq, int c0) -> s16x8 {
-    const int iy = rq / pool.W, ix = rq - (rq / pool.W) * pool.W;
-    const int oy0 = iy >> 1, ox0 = ix >> 1;
-    s16x8 gk[4];
-    unsigned long long am[4];
-    bool okk[4];
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const int oy = oy0 + (k >> 1), ox = ox0 + (k & 1);
-      okk[k] = oy <= ((iy + 1) >> 1) && oy < pool.Ho && ox <= ((ix + 1) >> 1) && ox < pool.Wo;
-      const long o = (((long)b * pool.Ho + min(oy, pool.Ho - 1)) * pool.Wo + min(ox, pool.Wo - 1)) * C + c0;
-      gk[k] = *reinterpret_cast<const s16x8*>(dy + o);
-      am[k] = *reinterpret_cast<const unsigned long long*>(pool.arg + o);
-    }
-    float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const int oy = oy0 + (k >> 1), ox = ox0 + (k & 1);
-      const unsigned t = (unsigned)((iy - (oy * 2 - 1)) * 3 + (ix - (ox * 2 - 1)));
-      float gv[8];
-      unpack8(gk[k], gv);
-#pragma unroll
-      for (int u = 0; u < 8; ++u)
-        if (okk[k] && ((am[k] >> (8 * u)) & 0xff) == t) acc[u] += gv[u];
-    }
-    return pack8(acc);
-  };
   const int r1 = min(r0 + rows_per_blk, HW);
   // BN over a sub-batch of `group` images (the last group may be short): sums hold group totals
   const int g0 = (b / group) * group;
@@ -535,7 +499,7 @@ __global__ void __launch_bounds__(NT) bn_bwd_kernel(const cvl_bf16* __restrict__
         for (int q = 0; q < BN_UNR; ++q) {
           const int rq = min(r + q * rpp, r1 - 1);       // clamped: loads stay unconditional
           off[q] = ((long)b * HW + rq) * C + c0;
-          vg[q] = POOL ? pooled(rq, c0) : *reinterpret_cast<const s16x8*>(dy + off[q]);
+          vg[q] = *reinterpret_cast<const s16x8*>(dy + off[q]);
           if (PASS != 2) vz[q] = *reinterpret_cast<const s16x8*>(z + off[q]);
           if (use_y) vy[q] = *reinterpret_cast<const s16x8*>(y + off[q]);
         }
@@ -608,117 +572,6 @@ __global__ void __launch_bounds__(NT) bn_bwd_kernel(const cvl_bf16* __restrict__
   }
 }
 
-// BN backward for small maps (H*W <= CVL_BN_SMALL_MAX_HW): the statistics are per image, so one
-// workgroup owning (image b, 16 channels) over ALL its rows can form (sum g, sum g*xhat), reduce
-// them in LDS (fixed order) and run the second pass right away -- one launch instead of pass 0 +
-// column reduction + pass 1 (the 32x32 / 16x16 stages are launch-bound on those three); its
-// second read of dy / z / y hits L2.  Per-image sums go to `sums` for the parameter gradients.
-constexpr int BNS_CB = 16;                    // channels per workgroup (2 x 8-channel thread columns)
-__global__ void __launch_bounds__(NT) bn_bwd_small_kernel(const cvl_bf16* __restrict__ dy,
-                                                          const cvl_bf16* __restrict__ y,
-                                                          const cvl_bf16* __restrict__ z, const float* __restrict__ mr,
-                                                          const float* __restrict__ gamma,
-                                                          const float* __restrict__ bnb, cvl_bf16* __restrict__ dz,
-                                                          cvl_bf16* __restrict__ g_out, double* __restrict__ sums,
-                                                          int C, int HW, float dz_beta, float act_hi) {
-  constexpr int TPR = BNS_CB / 8, RPP = NT / TPR;
-  const int b = blockIdx.y;
-  const int cg = threadIdx.x % TPR, rsub = threadIdx.x / TPR;
-  const int c0 = blockIdx.x * BNS_CB + cg * 8;
-  const bool zmask = !y && bnb;
-  float m[8], rs[8], ga[8], be[8], s1[8], s2[8];
-#pragma unroll
-  for (int u = 0; u < 8; ++u) {
-    const long bc = (long)b * C + c0 + u;
-    m[u] = mr[bc * 2];
-    rs[u] = mr[bc * 2 + 1];
-    ga[u] = gamma[c0 + u];
-    be[u] = zmask ? bnb[c0 + u] : 0.f;
-    s1[u] = 0.f;
-    s2[u] = 0.f;
-  }
-  auto grad = [&](long off, float* g, float* xh) {
-    float zz[8];
-    unpack8(*reinterpret_cast<const s16x8*>(dy + off), g);
-    unpack8(*reinterpret_cast<const s16x8*>(z + off), zz);
-    if (y) {
-      float yy[8];
-      unpack8(*reinterpret_cast<const s16x8*>(y + off), yy);
-#pragma unroll
-      for (int u = 0; u < 8; ++u) g[u] = (yy[u] > 0.f && yy[u] < act_hi) ? g[u] : 0.f;
-    }
-#pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      xh[u] = (zz[u] - m[u]) * rs[u];
-      if (zmask) {
-        const float a = bn_affine(zz[u], m[u], rs[u], ga[u], be[u]);
-        g[u] = (a > 0.f && a < act_hi) ? g[u] : 0.f;
-      }
-    }
-  };
-  const long base = (long)b * HW;
-  for (int r = rsub; r < HW; r += RPP) {
-    float g[8], xh[8];
-    grad((base + r) * C + c0, g, xh);
-#pragma unroll
-    for (int u = 0; u < 8; ++u) { s1[u] += g[u]; s2[u] += g[u] * xh[u]; }
-  }
-  __shared__ float red[NT][17];
-  __shared__ float tot[BNS_CB][2];
-#pragma unroll
-  for (int u = 0; u < 8; ++u) { red[threadIdx.x][u] = s1[u]; red[threadIdx.x][8 + u] = s2[u]; }
-  __syncthreads();
-  if (threadIdx.x < BNS_CB) {                 // channel cc: its column's RPP partials in order
-    const int cc = threadIdx.x, col = cc / 8, u = cc % 8;
-    float a1 = 0.f, a2 = 0.f;
-    for (int k = 0; k < RPP; ++k) { a1 += red[k * TPR + col][u]; a2 += red[k * TPR + col][8 + u]; }
-    tot[cc][0] = a1;
-    tot[cc][1] = a2;
-    double* o = sums + ((long)b * C + blockIdx.x * BNS_CB + cc) * 2;
-    o[0] = (double)a1;
-    o[1] = (double)a2;
-  }
-  __syncthreads();
-  const float inv = 1.0f / (float)HW;
-  float k1[8], k2[8], gm[8];
-#pragma unroll
-  for (int u = 0; u < 8; ++u) {
-    k1[u] = (float)(double)tot[cg * 8 + u][0] * inv;
-    k2[u] = (float)(double)tot[cg * 8 + u][1] * inv;
-    gm[u] = ga[u] * rs[u];
-  }
-  for (int r = rsub; r < HW; r += RPP) {
-    const long off = (base + r) * C + c0;
-    float g[8], xh[8], o[8];
-    grad(off, g, xh);
-    if (g_out) *reinterpret_cast<s16x8*>(g_out + off) = pack8(g);
-#pragma unroll
-    for (int u = 0; u < 8; ++u) o[u] = gm[u] * (g[u] - k1[u] - xh[u] * k2[u]);
-    if (dz_beta != 0.f) {
-      float old[8];
-      unpack8(*reinterpret_cast<const s16x8*>(dz + off), old);
-#pragma unroll
-      for (int u = 0; u < 8; ++u) o[u] += dz_beta * old[u];
-    }
-    *reinterpret_cast<s16x8*>(dz + off) = pack8(o);
-  }
-}
-
-// parameter gradients from the per-image sums, images in order (float64):
-// dbeta[c] = sum_b S_g(b, c) (+ beta_acc * old), dgamma[c] = sum_b S_gx(b, c) (+ ...), conv bias 0
-__global__ void bn_param_grads_kernel(const double* __restrict__ sums, int B, int C, float* dgamma, float* dbeta,
-                                      float* conv_dbias, float beta_acc) {
-  const int c = blockIdx.x * NT + threadIdx.x;
-  if (c >= C) return;
-  double a1 = 0.0, a2 = 0.0;
-  for (int bb = 0; bb < B; ++bb) {
-    a1 += sums[((long)bb * C + c) * 2];
-    a2 += sums[((long)bb * C + c) * 2 + 1];
-  }
-  if (conv_dbias) conv_dbias[c] = 0.f;
-  dbeta[c] = (float)a1 + (beta_acc != 0.f ? beta_acc * dbeta[c] : 0.f);
-  dgamma[c] = (float)a2 + (beta_acc != 0.f ? beta_acc * dgamma[c] : 0.f);
-}
 
 // out[y][c][0..1] = sum_r part[y][r][c][0..1]: a block owns 32 channels (256 contiguous bytes per
 // row) and 8 row groups; the row groups are combined in a fixed order (deterministic, float64)
@@ -1464,23 +1317,13 @@ static int bn_backward_impl(const void* dy, const void* y_relu, const float* bn_
   double* sums = reinterpret_cast<double*>(workspace);
   double* dbsum = sums + 2 * (size_t)B * C;
   float* part0 = reinterpret_cast<float*>(dbsum + 2 * (size_t)C);
-  // one-launch form: opt-in (CVL_BN_SMALL_MAX_HW=<max H*W>); measured slower than the three
-  // launches on the bench (FCOS 1004 -> 996 at 256, -> 958 at 1024: too few, too long workgroups)
-  if (HW <= cvl_env_int("CVL_BN_SMALL_MAX_HW", 0) && C % BNS_CB == 0) {
-    hipLaunchKernelGGL(bn_bwd_small_kernel, dim3(C / BNS_CB, B), dim3(NT), 0, S_, (const cvl_bf16*)dy,
-                       (const cvl_bf16*)y_relu, (const cvl_bf16*)z, mean_rstd, gamma, bn_beta, (cvl_bf16*)dz,
-                       (cvl_bf16*)g_out, sums, C, HW, 0.f, act_hi);
-    hipLaunchKernelGGL(bn_param_grads_kernel, dim3((C + NT - 1) / NT), dim3(NT), 0, S_, (const double*)sums, B, C,
-                       dgamma, dbeta, conv_dbias, beta_acc);
-    return cvl_launch_status();
-  }
   dim3 g1(nchunk, B);
   const bool ym = y_relu != nullptr, zm = !ym && bn_beta != nullptr;
   auto k0 = ym ? bn_bwd_kernel<0, 1> : zm ? bn_bwd_kernel<0, 2> : bn_bwd_kernel<0, 3>;
   auto k1 = ym ? bn_bwd_kernel<1, 1> : zm ? bn_bwd_kernel<1, 2> : bn_bwd_kernel<1, 3>;
   hipLaunchKernelGGL(k0, g1, dim3(NT), 0, S_, (const cvl_bf16*)dy, (const cvl_bf16*)y_relu,
                      (const cvl_bf16*)z, mean_rstd, gamma, (const double*)nullptr, (cvl_bf16*)nullptr,
-                     (cvl_bf16*)nullptr, part0, C, HW, rpb, 1, 0.f, BnPG{}, bn_beta, act_hi, BnPool{});
+                     (cvl_bf16*)nullptr, part0, C, HW, rpb, 1, 0.f, BnPG{}, bn_beta, act_hi);
   hipLaunchKernelGGL(bn_colsum_kernel, dim3((C + 31) / 32, B), dim3(NT), 0, S_, (const float*)part0, nchunk, C,
                      sums);
   // pass 1 is elementwise (no partials): the apply kernels' finer chunking (~2048 workgroups)
@@ -1488,7 +1331,7 @@ static int bn_backward_impl(const void* dy, const void* y_relu, const float* bn_
   hipLaunchKernelGGL(k1, dim3((HW + rpb1 - 1) / rpb1, B), dim3(NT), 0, S_, (const cvl_bf16*)dy, (const cvl_bf16*)y_relu,
                      (const cvl_bf16*)z, mean_rstd, gamma, (const double*)sums, (cvl_bf16*)dz, (cvl_bf16*)g_out,
                      (float*)nullptr, C, HW, rpb1, 1, 0.f, BnPG{dgamma, dbeta, conv_dbias, beta_acc}, bn_beta,
-                     act_hi, BnPool{});
+                     act_hi);
   return cvl_launch_status();
 }
 
@@ -1507,38 +1350,6 @@ extern "C" int cvl_bn_backward_relu(const void* dy, const void* z, const float* 
   CVL_CHECK_ARG(beta);
   return bn_backward_impl(dy, nullptr, beta, z, mean_rstd, gamma, workspace, workspace_bytes, dz, nullptr, dgamma,
                           dbeta, beta_acc, conv_dbias, B, HW, C, stream);
-}
-
-// The stem's pool1 backward fused into conv1_bn's backward (BN -> ReLU unit, mask rebuilt from z):
-// dp [B][Ho][Wo][C] + argmax are the 3x3/2 pad-1 max-pool's output gradient and argmax; both BN
-// passes route dp back on the fly (cvl_maxpool3x3s2_backward's arithmetic), so the full-size
-// pool-input gradient is never stored.  Workspace: cvl_bn_backward_workspace_size(B, H*W, C).
-extern "C" int cvl_maxpool_bn_backward_relu(const void* dp, const uint8_t* argmax, const void* z,
-                                            const float* mean_rstd, const float* gamma, const float* beta,
-                                            void* workspace, size_t workspace_bytes, void* dz, float* dgamma,
-                                            float* dbeta, float beta_acc, float* conv_dbias, int B, int H, int W,
-                                            int C, cvl_stream_t stream) {
-  CVL_CHECK_ARG(dp && argmax && z && mean_rstd && gamma && beta && workspace && dz && dgamma && dbeta && C % 8 == 0);
-  CVL_CHECK_ARG(B > 0 && H > 0 && W > 0);
-  const int HW = H * W;
-  CVL_CHECK_ARG(workspace_bytes >= cvl_bn_backward_workspace_size(B, HW, C));
-  const BnPool pool{argmax, W, (H + 2 - 3) / 2 + 1, (W + 2 - 3) / 2 + 1};
-  const int rpb = bn_bwd_rows_per_blk(B, HW, C);
-  const int nchunk = (HW + rpb - 1) / rpb;
-  double* sums = reinterpret_cast<double*>(workspace);
-  double* dbsum = sums + 2 * (size_t)B * C;
-  float* part0 = reinterpret_cast<float*>(dbsum + 2 * (size_t)C);
-  hipLaunchKernelGGL((bn_bwd_kernel<0, 2, true>), dim3(nchunk, B), dim3(NT), 0, S_, (const cvl_bf16*)dp,
-                     (const cvl_bf16*)nullptr, (const cvl_bf16*)z, mean_rstd, gamma, (const double*)nullptr,
-                     (cvl_bf16*)nullptr, (cvl_bf16*)nullptr, part0, C, HW, rpb, 1, 0.f, BnPG{}, beta, INFINITY, pool);
-  hipLaunchKernelGGL(bn_colsum_kernel, dim3((C + 31) / 32, B), dim3(NT), 0, S_, (const float*)part0, nchunk, C,
-                     sums);
-  const int rpb1 = bn_rows_per_blk(B, HW, C);
-  hipLaunchKernelGGL((bn_bwd_kernel<1, 2, true>), dim3((HW + rpb1 - 1) / rpb1, B), dim3(NT), 0, S_,
-                     (const cvl_bf16*)dp, (const cvl_bf16*)nullptr, (const cvl_bf16*)z, mean_rstd, gamma,
-                     (const double*)sums, (cvl_bf16*)dz, (cvl_bf16*)nullptr, (float*)nullptr, C, HW, rpb1, 1, 0.f,
-                     BnPG{dgamma, dbeta, conv_dbias, beta_acc}, beta, INFINITY, pool);
-  return cvl_launch_status();
 }
 
 extern "C" int cvl_bn_backward_relu6(const void* dy, const void* z, const float* mean_rstd, const float* gamma,
@@ -1563,7 +1374,7 @@ extern "C" int cvl_bn_backward_relu_sums(const void* dy, const void* z, const fl
   const int nchunk = (HW + rpb - 1) / rpb;
   hipLaunchKernelGGL((bn_bwd_kernel<1, 2>), dim3(nchunk, B), dim3(NT), 0, S_, (const cvl_bf16*)dy, (const cvl_bf16*)nullptr,
                      (const cvl_bf16*)z, mean_rstd, gamma, sums, (cvl_bf16*)dz, (cvl_bf16*)nullptr, (float*)nullptr,
-                     C, HW, rpb, 1, 0.f, BnPG{dgamma, dbeta, conv_dbias, beta_acc}, beta, act_hi, BnPool{});
+                     C, HW, rpb, 1, 0.f, BnPG{dgamma, dbeta, conv_dbias, beta_acc}, beta, act_hi);
   return cvl_launch_status();
 }
 
@@ -1579,7 +1390,7 @@ extern "C" int cvl_bn_backward_res_sums(const void* dy, const void* y, const voi
   const int nchunk = (HW + rpb - 1) / rpb;
   hipLaunchKernelGGL((bn_bwd_kernel<1, 1>), dim3(nchunk, B), dim3(NT), 0, S_, (const cvl_bf16*)dy, (const cvl_bf16*)y,
                      (const cvl_bf16*)z, mean_rstd, gamma, sums, (cvl_bf16*)dz, (cvl_bf16*)g_out, (float*)nullptr,
-                     C, HW, rpb, 1, 0.f, BnPG{dgamma, dbeta, conv_dbias, beta_acc}, (const float*)nullptr, INFINITY, BnPool{});
+                     C, HW, rpb, 1, 0.f, BnPG{dgamma, dbeta, conv_dbias, beta_acc}, (const float*)nullptr, INFINITY);
   return cvl_launch_status();
 }
 
@@ -1764,7 +1575,7 @@ extern "C" int cvl_bn_stats(const void* x, int B, int HW, int C, double* stats, 
   hipLaunchKernelGGL(bn_bwd_kernel<2>, dim3(nchunk, B), dim3(NT), 0, S_, (const cvl_bf16*)x,
                      (const cvl_bf16*)nullptr, (const cvl_bf16*)nullptr, (const float*)nullptr, (const float*)nullptr,
                      (const double*)nullptr, (cvl_bf16*)nullptr, (cvl_bf16*)nullptr, part, C, HW, rpb, 1, 0.f, BnPG{},
-                     (const float*)nullptr, INFINITY, BnPool{});
+                     (const float*)nullptr, INFINITY);
   hipLaunchKernelGGL(bn_colsum_kernel, dim3((C + 31) / 32, B), dim3(NT), 0, S_, (const float*)part, nchunk, C,
                      stats);
   return cvl_launch_status();
@@ -1802,7 +1613,7 @@ extern "C" int cvl_bn_backward_grouped(const void* dy, const void* y_relu, const
   dim3 g1(nchunk, B);
   hipLaunchKernelGGL(bn_bwd_kernel<0>, g1, dim3(NT), 0, S_, (const cvl_bf16*)dy, (const cvl_bf16*)y_relu,
                      (const cvl_bf16*)z, mean_rstd, gamma, (const double*)nullptr, (cvl_bf16*)nullptr,
-                     (cvl_bf16*)nullptr, part0, C, HW, rpb, group, 0.f, BnPG{}, (const float*)nullptr, INFINITY, BnPool{});
+                     (cvl_bf16*)nullptr, part0, C, HW, rpb, group, 0.f, BnPG{}, (const float*)nullptr, INFINITY);
   hipLaunchKernelGGL(bn_colsum_kernel, dim3((C + 31) / 32, B), dim3(NT), 0, S_, (const float*)part0, nchunk, C,
                      sums);
   const double* use = sums;
@@ -1814,6 +1625,6 @@ extern "C" int cvl_bn_backward_grouped(const void* dy, const void* y_relu, const
   hipLaunchKernelGGL(bn_bwd_kernel<1>, g1, dim3(NT), 0, S_, (const cvl_bf16*)dy, (const cvl_bf16*)y_relu,
                      (const cvl_bf16*)z, mean_rstd, gamma, use, (cvl_bf16*)dz, (cvl_bf16*)nullptr,
                      (float*)nullptr, C, HW, rpb, group, dz_beta, BnPG{dgamma, dbeta, nullptr, 0.f, sums},
-                     (const float*)nullptr, INFINITY, BnPool{});
+                     (const float*)nullptr, INFINITY);
   return cvl_launch_status();
 }

@@ -11,7 +11,7 @@ import os
 import torch  # noqa: F401  (must precede the CDLL load, see module docstring)
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.environ.get("CVL_LIB") or os.path.join(_HERE, "libcvlite_hip.so")   # CVL_LIB: A/B builds
+LIB_PATH = os.path.join(_HERE, "libcvlite_hip.so")
 
 c_int, c_float, c_size_t, c_void_p = ctypes.c_int, ctypes.c_float, ctypes.c_size_t, ctypes.c_void_p
 P = c_void_p
@@ -23,6 +23,8 @@ SIGNATURES = {
     "cvl_fcos_loss_workspace_size": (c_size_t, [c_int, c_int]),
     "cvl_fcos_loss": (c_int, [P, c_int, P, c_int, P, c_int, c_int, c_int, c_int, c_float, P,
                               P, c_int, c_int, P, c_int, c_int, P, P]),
+    "cvl_fcos_loss_ex": (c_int, [P, c_int, P, c_int, P, c_int, c_int, c_int, c_int, c_float, c_float, c_float,
+                                 c_float, P, P, c_int, c_int, P, c_int, c_int, P, P]),
     "cvl_fcos_decode": (c_int, [P, c_int, c_int, c_int, ctypes.c_double, P, P]),
     "cvl_fcos_v1_decode": (c_int, [P, c_int, c_int, c_int, c_float, c_float, P, P]),
     "cvl_conv_igemm_workspace_size": (c_size_t, [P]),
@@ -54,7 +56,6 @@ SIGNATURES = {
     "cvl_bn_backward": (c_int, [P, P, P, P, P, P, c_size_t, P, P, P, P, c_float, P, c_int, c_int, c_int, P]),
     "cvl_bn_backward_relu": (c_int, [P, P, P, P, P, P, c_size_t, P, P, P, c_float, P, c_int, c_int, c_int, P]),
     "cvl_maxpool3x3s2": (c_int, [P, P, P, c_int, c_int, c_int, c_int, P]),
-    "cvl_maxpool_bn_backward_relu": (c_int, [P, P, P, P, P, P, P, ctypes.c_size_t, P, P, P, c_float, P, c_int, c_int, c_int, c_int, P]),
     "cvl_bn_relu_maxpool3x3s2": (c_int, [P, P, P, P, P, P, c_int, c_int, c_int, c_int, P]),
     "cvl_maxpool3x3s2_backward": (c_int, [P, P, P, c_int, c_int, c_int, c_int, P]),
     "cvl_upsample2x_add": (c_int, [P, P, P, c_int, c_int, c_int, c_int, P]),

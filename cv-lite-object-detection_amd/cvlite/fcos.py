@@ -115,8 +115,8 @@ def format_data(gt_labels, img_dim, num_classes, img_pad=None, areas=None, strid
     return outs, [int(v) for v in nt[0].cpu().numpy()]
 
 
-def _packed_loss(targets, reg, cls, C, reg_type):
-    losses, _, _ = ot.fcos_loss(reg, cls, targets, C, reg_type=reg_type, with_grad=False)
+def _packed_loss(targets, reg, cls, C, reg_type, **kw):
+    losses, _, _ = ot.fcos_loss(reg, cls, targets, C, reg_type=reg_type, with_grad=False, **kw)
     return losses[0]
 
 
@@ -143,9 +143,8 @@ def model_loss(y_true, y_pred, strides, reg_type="l1", cen_type="l1", cls_lambda
 
 
 def focal_loss(labels, logits, alpha=0.25, gamma=2.0):
-    """fcos.py:443-462 (sum over all elements) through the fused kernel's class path."""
-    if alpha != 0.25 or gamma != 2.0:
-        raise NotImplementedError("the fused kernel implements the reference's alpha=0.25, gamma=2")
+    """fcos.py:443-462 (sum over all elements, any alpha / gamma >= 0, soft labels) through the
+    fused kernel's class path."""
     x = _as_tensor(logits)
     y = _as_tensor(labels)
     C = int(x.shape[-1])
@@ -153,15 +152,18 @@ def focal_loss(labels, logits, alpha=0.25, gamma=2.0):
     tg = torch.zeros((1, N, 5 + C), dtype=torch.float32, device=x.device)
     tg[0, :, 5:] = y.reshape(N, C)
     reg = torch.zeros((1, N, 8), dtype=torch.float32, device=x.device)
-    return _packed_loss(tg, reg, x.reshape(1, N, C).contiguous(), C, "l1")[0]
+    return _packed_loss(tg, reg, x.reshape(1, N, C).contiguous(), C, "l1", alpha=float(alpha),
+                        gamma=float(gamma))[0]
 
 
-def _masked_reg_loss(xy_true, xy_pred, mask, reg_type):
+def _masked_reg_loss(xy_true, xy_pred, mask, reg_type, delta=1.0):
+    """sum over cells of mask * (per-cell loss summed over the last axis) (fcos.py:380-441): the
+    fused kernel's regression path with the float mask in targets[..., 5] (cvl_fcos_loss_ex flag
+    32); smooth-L1 rows of k > 4 values run as ceil(k / 4) 4-wide rows of the same cell mask."""
     t = _as_tensor(xy_true)
     p = _as_tensor(xy_pred)
     k = int(t.shape[-1])
     N = t.numel() // k
-    m = _as_tensor(mask).reshape(-1) if not np.isscalar(mask) else None
     if reg_type == "iou":
         assert k == 4
         groups = 1
@@ -176,19 +178,20 @@ def _masked_reg_loss(xy_true, xy_pred, mask, reg_type):
     tg[0, :, :4] = tt.reshape(N * groups, 4)
     reg[0, :, :4] = pp.reshape(N * groups, 4)
     tg[0, :, 4] = 0.5                                   # centerness path: sigmoid(0) == 0.5, no loss
-    mk = torch.ones(N, device=t.device) if m is None else (m >= 1).float() * (m > 0).float()
-    if m is not None and not torch.all((m == 0) | (m == 1)):
-        raise NotImplementedError("the fused kernel supports binary masks (as the reference uses)")
+    if np.isscalar(mask) or (isinstance(mask, np.ndarray) and mask.ndim == 0):
+        mk = torch.full((N,), float(mask), dtype=torch.float32, device=t.device)
+    else:
+        mk = _as_tensor(mask).reshape(-1)
+        assert mk.numel() == N, "mask must have the shape of xy_true without its last axis"
     tg[0, :, 5] = mk.repeat_interleave(groups)
     cls = torch.full((1, N * groups, 1), -100.0, dtype=torch.float32, device=t.device)
-    return _packed_loss(tg, reg, cls, 1, reg_type)[1]
+    return _packed_loss(tg, reg, cls, 1, reg_type, delta=float(delta), float_mask=True)[1]
 
 
 def smooth_l1_loss(xy_true, xy_pred, mask=1.0, delta=1.0):
-    """fcos.py:380-391 (discontinuous 'smooth L1', Q8) summed over all elements."""
-    if delta != 1.0:
-        raise NotImplementedError("delta must be 1.0 (reference default)")
-    return _masked_reg_loss(xy_true, xy_pred, mask, "l1")
+    """fcos.py:380-391 (discontinuous 'smooth L1', Q8: 0.5 d^2 if |d| < delta else |d|) times the
+    (float) cell mask, summed over all elements."""
+    return _masked_reg_loss(xy_true, xy_pred, mask, "l1", delta)
 
 
 def iou_loss(xy_true, xy_pred, mask):

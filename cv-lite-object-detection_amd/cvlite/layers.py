@@ -247,30 +247,6 @@ FUSE_BNSUM = os.environ.get("CVL_NO_BNSUM_FUSE", "0") != "1"
 # ... and a residual unit's (BN3) first pass into the next block's conv1 data gradient (CVL_NO_BNSUM_RES=1: off)
 FUSE_BNSUM_RES = FUSE_BNSUM and os.environ.get("CVL_NO_BNSUM_RES", "0") != "1"
 
-# weight gradients of the backbone units on a side stream, concurrent with the data-gradient chain
-# (the two are independent; the small-map launches leave most CUs idle on their own).  The owner
-# joins the side stream before any gradient group is reported final.  Off by default: measured
-# -1 % (FCOS) and -2 % (RetinaNet) against the serial order (CVL_BWD_SIDE_STREAM=1 to try).
-SIDE_WGRAD = os.environ.get("CVL_BWD_SIDE_STREAM", "0") == "1"
-_side = {}
-
-
-def side_stream(device):
-    """The per-device side stream of the backward's weight gradients (created on first use)."""
-    key = torch.device(device).index
-    if key not in _side:
-        _side[key] = torch.cuda.Stream(device=device)
-    return _side[key]
-
-
-def join_side(device):
-    """Make the current stream wait for every weight gradient queued on the side stream."""
-    if SIDE_WGRAD and torch.device(device).type == "cuda":
-        key = torch.device(device).index
-        if key in _side:
-            torch.cuda.current_stream(device).wait_stream(_side[key])
-
-
 class StatsArena(object):
     """One zeroed float64 buffer holding the (sum, sumsq) BN statistics of every conv of a forward
     pass (one memset per step instead of one per BN)."""
@@ -392,15 +368,7 @@ class ConvBN(object):
         else:
             nn.bn_backward(dy, y if relu else None, z, mr, self.bn.gamma, dz, g_out, st.g(self.bn.gname),
                            st.g(self.bn.bname), B, Ho * Wo, c, conv_dbias=self.conv.db)
-        if SIDE_WGRAD and dz.is_cuda:
-            side = side_stream(dz.device)
-            side.wait_stream(torch.cuda.current_stream(dz.device))
-            with torch.cuda.stream(side):
-                self.conv.wgrad(x, dz, B, H, W, bias=False)
-            x.record_stream(side)            # read on the side stream: not reused until it is done
-            dz.record_stream(side)
-        else:
-            self.conv.wgrad(x, dz, B, H, W, bias=False)
+        self.conv.wgrad(x, dz, B, H, W, bias=False)
         if not need_dx:
             return None
         if bn_next is None:

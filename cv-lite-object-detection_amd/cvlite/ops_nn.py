@@ -340,16 +340,6 @@ def bn_relu_maxpool3x3s2(z, mean_rstd, gamma, beta, y, argmax):
               W, C, stream())
 
 
-def maxpool_bn_backward_relu(dp, argmax, z, mean_rstd, gamma, beta, dz, dgamma, dbeta, beta_acc=0.0, conv_dbias=None):
-    """bn_backward_relu of the stem BN whose output fed the 3x3/2 max-pool: dp is the POOL's output
-    gradient; the pool backward runs inside both BN passes (no full-size pool-input gradient)."""
-    B, H, W, C = z.shape
-    n = int(_lib.load().cvl_bn_backward_workspace_size(B, H * W, C))
-    ws = torch.empty(n, dtype=torch.uint8, device=z.device)
-    _lib.call("cvl_maxpool_bn_backward_relu", ptr(dp), ptr(argmax), ptr(z), ptr(mean_rstd), ptr(gamma), ptr(beta),
-              ptr(ws), n, ptr(dz), ptr(dgamma), ptr(dbeta), float(beta_acc), ptr(conv_dbias), B, H, W, C, stream())
-
-
 def maxpool3x3s2(x, y, argmax):
     B, H, W, C = x.shape
     _lib.call("cvl_maxpool3x3s2_f32" if _is_f32(x) else "cvl_maxpool3x3s2", ptr(x), ptr(y), ptr(argmax), B, H, W, C, stream())

@@ -73,17 +73,20 @@ def fcos_center_v1_assign(boxes, nbox, img_dim, pad_hw, num_classes, strides=FCO
 
 def fcos_loss(reg_pred, cls_pred, targets, num_classes, reg_type="l1", grad_scale=1.0,
               with_grad=True, grad_dtype=torch.float32, d_reg=None, d_cls=None, cen_type="l1",
-              reg_sigmoid=False, cen_in_cls=False):
+              reg_sigmoid=False, cen_in_cls=False, alpha=0.25, gamma=2.0, delta=1.0, float_mask=False):
     """Fused focal + smooth-L1/IoU + centerness forward and backward.
     reg_pred [B,P,ld_reg>=5] f32, cls_pred [B,P,ld_cls>=C] f32, targets [B,P,5+C] f32.
     Centre variants (fcos_center / fcos_center_v1): cen_type "focal", reg_sigmoid (v1's sigmoid
     reg head), cen_in_cls (centerness logit in class column round_up(C, 8)).
+    alpha / gamma / delta: the focal_loss / smooth_l1_loss keywords (fcos.py:380, 443-444);
+    float_mask: the regression mask is targets[..., 5] itself (C = 1).
     Returns (losses [B,3] f32 = (cls, reg, cen) per image, d_reg, d_cls)."""
     _lib.require_cuda(reg_pred, cls_pred, targets)
     B, P = int(targets.shape[0]), int(targets.shape[1])
     assert reg_pred.shape[:2] == (B, P) and cls_pred.shape[:2] == (B, P)
     rt = reg_type if isinstance(reg_type, int) else {"l1": 0, "iou": 1}[reg_type]    # int: raw kernel flags
     rt |= (4 if cen_type.lower() == "focal" else 0) | (8 if reg_sigmoid else 0) | (16 if cen_in_cls else 0)
+    rt |= 32 if float_mask else 0
     dev = targets.device
     losses = torch.empty((B, 3), device=dev, dtype=torch.float32)
     ws = torch.empty(int(_lib.load().cvl_fcos_loss_workspace_size(B, P)), device=dev, dtype=torch.uint8)
@@ -93,11 +96,15 @@ def fcos_loss(reg_pred, cls_pred, targets, num_classes, reg_type="l1", grad_scal
         if d_cls is None:
             d_cls = torch.empty((B, P, cls_pred.shape[2]), device=dev, dtype=grad_dtype)
     dt = lambda t: 0 if t is None or t.dtype == torch.float32 else 1  # noqa: E731
-    _lib.call("cvl_fcos_loss", ptr(reg_pred), int(reg_pred.shape[2]), ptr(cls_pred), int(cls_pred.shape[2]),
-              ptr(targets), B, P, int(num_classes), rt, float(grad_scale), ptr(losses),
-              ptr(d_reg), int(d_reg.shape[2]) if d_reg is not None else 0, dt(d_reg),
-              ptr(d_cls), int(d_cls.shape[2]) if d_cls is not None else 0, dt(d_cls),
-              ptr(ws), _lib.stream())
+    dflt = alpha == 0.25 and gamma == 2.0 and delta == 1.0 and not float_mask
+    tail = (ptr(d_reg), int(d_reg.shape[2]) if d_reg is not None else 0, dt(d_reg),
+            ptr(d_cls), int(d_cls.shape[2]) if d_cls is not None else 0, dt(d_cls), ptr(ws), _lib.stream())
+    head = (ptr(reg_pred), int(reg_pred.shape[2]), ptr(cls_pred), int(cls_pred.shape[2]), ptr(targets), B, P,
+            int(num_classes), rt, float(grad_scale))
+    if dflt:
+        _lib.call("cvl_fcos_loss", *head, ptr(losses), *tail)
+    else:
+        _lib.call("cvl_fcos_loss_ex", *head, float(alpha), float(gamma), float(delta), ptr(losses), *tail)
     return losses, d_reg, d_cls
 
 

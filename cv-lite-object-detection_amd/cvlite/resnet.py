@@ -13,15 +13,11 @@ import os
 import torch
 
 from . import ops_nn as nn
-from .layers import join_side, BF16, BatchNorm, Conv, ConvBN, StatsArena
+from .layers import BF16, BatchNorm, Conv, ConvBN, StatsArena
 
 STEM_K = 7
 # the stem's BN -> ReLU -> max-pool as one pass from z (CVL_STEM_NO_FUSE_POOL=1: BN apply + pool)
 FUSE_POOL = os.environ.get("CVL_STEM_NO_FUSE_POOL", "0") != "1"
-# ... and pool1's backward inside conv1_bn's backward passes (CVL_STEM_POOL_BWD_FUSE=1): bit-exact but
-# measured 0.8 % slower -- the per-row gather over up to four windows (218 VGPRs, 2 waves / SIMD) costs
-# more than the 134 MB pool-input gradient it avoids storing and re-reading
-FUSE_POOL_BWD = os.environ.get("CVL_STEM_POOL_BWD_FUSE", "0") == "1"
 STEM_KP = int(os.environ.get("CVL_STEM_KP", 192))   # im2col K = 7*7*3 = 147 padded: 192 = 3 x 64 lets the
 #                                                      LDS-DMA kernels take the stem (+0.6 % step vs 160)
 
@@ -98,14 +94,10 @@ class Stem(object):
         A, z, y, mr, arg, B, Ho, Wo = saved
         dz = torch.empty_like(z)
         st = self.bn.store
-        if z.dtype == BF16 and FUSE_POOL_BWD:     # pool1 backward inside conv1_bn's two backward passes
-            nn.maxpool_bn_backward_relu(dp, arg, z, mr, self.bn.gamma, self.bn.beta, dz, st.g(self.bn.gname),
-                                        st.g(self.bn.bname), conv_dbias=self.conv.db)
-        else:
-            dy = torch.empty_like(z)
-            nn.maxpool3x3s2_backward(dp, arg, dy)
-            nn.bn_backward_relu(dy, z, mr, self.bn.gamma, self.bn.beta, dz, st.g(self.bn.gname),
-                                st.g(self.bn.bname), B, Ho * Wo, 64, conv_dbias=self.conv.db)
+        dy = torch.empty_like(z)
+        nn.maxpool3x3s2_backward(dp, arg, dy)
+        nn.bn_backward_relu(dy, z, mr, self.bn.gamma, self.bn.beta, dz, st.g(self.bn.gname),
+                            st.g(self.bn.bname), B, Ho * Wo, 64, conv_dbias=self.conv.db)
         if A.dtype != BF16:                         # fp32 parity mode: 7x7 weight gradient in place
             nn.conv_wgrad(self._desc7(B, A.shape[1], A.shape[2], Ho, Wo), A, dz, self.conv.dw)
             return
@@ -270,8 +262,6 @@ class ResNet50(object):
                 else:
                     dh, pending = st[bi].backward(dh, ssv[si][bi], arena=arena, sums3=pending, prev_ctx=prev)
             if si > 0:
-                join_side(dh.device)          # this stage's weight gradients are final
-                hook("conv%d" % (si + 2))
+                hook("conv%d" % (si + 2))     # this stage's weight gradients are final
         self.stem.backward(dh, sv_stem)
-        join_side(dh.device)
         hook("conv2_stem")

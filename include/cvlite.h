@@ -66,6 +66,16 @@ int cvl_fcos_loss(const float* reg_pred, int ld_reg, const float* cls_pred, int 
                   const float* targets, int B, int P, int num_classes, int reg_type,
                   float grad_scale, float* losses, void* d_reg, int ld_dreg, int dreg_dtype,
                   void* d_cls, int ld_dcls, int dcls_dtype, void* workspace, cvl_stream_t stream);
+/* cvl_fcos_loss with the loss keywords of FCOS/fcos.py:380 smooth_l1_loss(delta) and :443-444
+ * focal_loss(alpha, gamma) (RetinaNet/retinanet_module.py:367-401 has the same two), and one more
+ * reg_type flag: +32 the regression mask is the float value targets[5] itself instead of
+ * (max class target >= 1) -- the drop-in smooth_l1_loss / iou_loss(mask=<float map>) (C = 1).
+ * cvl_fcos_loss(...) == cvl_fcos_loss_ex(..., 0.25f, 2.0f, 1.0f, ...).  gamma >= 0, delta > 0. */
+int cvl_fcos_loss_ex(const float* reg_pred, int ld_reg, const float* cls_pred, int ld_cls,
+                     const float* targets, int B, int P, int num_classes, int reg_type,
+                     float grad_scale, float alpha, float gamma, float delta, float* losses, void* d_reg,
+                     int ld_dreg, int dreg_dtype, void* d_cls, int ld_dcls, int dcls_dtype, void* workspace,
+                     cvl_stream_t stream);
 
 /* FCOS/fcos.py:112-134 prediction_to_corners: pred [S0][S1][ld>=4] (t, b, l, r) fp32 ->
  * out [S0][S1][4] float64 = stride * (y_lo, x_lo, y_hi, x_hi) around cell centres (fp32 math). */
@@ -151,7 +161,8 @@ int cvl_conv_igemm(const cvl_conv_desc* d, const void* src, void* dst, double* b
                    void* workspace, size_t workspace_bytes, cvl_stream_t stream);
 
 /* Test / profiling hook: the kernel variant the last cvl_conv_igemm / cvl_conv_wgrad* call on THIS
- * host thread launched.  CVL_CK_* codes; cvl_conv_kernel_name(code) is a static string. */
+ * host thread launched.  CVL_CK_* codes; cvl_conv_kernel_name(code) is a static string.  Codes 6
+ * (X256) and 12 (X32H) belong to retired kernels and are no longer returned. */
 enum { CVL_CK_NONE = 0, CVL_CK_BASE = 1, CVL_CK_BASE_SPLITK = 2, CVL_CK_L64 = 3, CVL_CK_L128 = 4,
        CVL_CK_L256 = 5, CVL_CK_X256 = 6, CVL_CK_X32 = 7,
        CVL_CK_WG_S = 8, CVL_CK_WG_L128 = 9, CVL_CK_WG_L256 = 10, CVL_CK_WG_X = 11, CVL_CK_X32H = 12, CVL_CK_WG_SN = 13,
@@ -291,14 +302,6 @@ int cvl_bn_backward_relu6(const void* dy, const void* z, const float* mean_rstd,
  * cvl_maxpool3x3s2 would from the stored BN output (bit-identical), without that full-size output. */
 int cvl_bn_relu_maxpool3x3s2(const void* z, const float* mean_rstd, const float* gamma, const float* beta, void* y,
                              uint8_t* argmax, int B, int H, int W, int C, cvl_stream_t stream);
-/* Its backward fused into conv1_bn's: cvl_bn_backward_relu of the pool-input gradient, which both BN
- * passes form on the fly from the pooled gradient dp [B][Ho][Wo][C] and argmax (as
- * cvl_maxpool3x3s2_backward would, bit-exact); H, W: the BN map.  workspace >=
- * cvl_bn_backward_workspace_size(B, H*W, C). */
-int cvl_maxpool_bn_backward_relu(const void* dp, const uint8_t* argmax, const void* z, const float* mean_rstd,
-                                 const float* gamma, const float* beta, void* workspace, size_t workspace_bytes,
-                                 void* dz, float* dgamma, float* dbeta, float beta_acc, float* conv_dbias, int B,
-                                 int H, int W, int C, cvl_stream_t stream);
 int cvl_maxpool3x3s2(const void* x, void* y, uint8_t* argmax, int B, int H, int W, int C,
                      cvl_stream_t stream);
 int cvl_maxpool3x3s2_backward(const void* dy, const uint8_t* argmax, void* dx, int B, int H, int W,

@@ -497,6 +497,44 @@ WORKERS = {"fcos": work_fcos, "retinanet": work_retina, "centernet": work_center
            "fcos_center": work_fcos_center}
 
 
+def work_loss_kwargs(out_path):
+    """FCOS/fcos.py focal_loss / smooth_l1_loss and RetinaNet/retinanet_module.py's methods of the same
+    names at NON-default keyword values (alpha, gamma, delta) and with soft (non-binary) float
+    masks / labels: the keyword surface of the drop-in loss functions."""
+    tf = _child_setup("FCOS")
+    import fcos as ref
+    rng = np.random.default_rng(4242)
+    arrays, meta = {}, {"focal": [], "sl1": []}
+    for k, (alpha, gamma, soft) in enumerate([(0.25, 2.0, False), (0.5, 1.0, False), (0.1, 3.0, True),
+                                              (0.75, 0.0, True), (0.25, 1.5, True), (0.9, 2.5, False)]):
+        x = rng.normal(0, 3, size=(9, 7, 13)).astype(np.float32)
+        y = rng.uniform(size=(9, 7, 13)) if soft else (rng.uniform(size=(9, 7, 13)) < 0.2).astype(np.float64)
+        arrays["focal_%d_x" % k] = x
+        arrays["focal_%d_y" % k] = y.astype(np.float32)
+        arrays["focal_%d_out" % k] = np.float64(float(ref.focal_loss(y.astype(np.float32), tf.constant(x),
+                                                                     alpha=alpha, gamma=gamma)))
+        meta["focal"].append([alpha, gamma])
+    for k, (delta, mask_kind) in enumerate([(1.0, "soft"), (0.5, "binary"), (2.0, "soft"), (0.25, "none"),
+                                            (3.0, "binary")]):
+        a = rng.normal(0, 1.5, size=(8, 6, 4)).astype(np.float32)
+        b = rng.normal(0, 1.5, size=(8, 6, 4)).astype(np.float32)
+        arrays["sl1_%d_pred" % k] = a
+        arrays["sl1_%d_true" % k] = b
+        if mask_kind == "none":
+            out = ref.smooth_l1_loss(b, tf.constant(a), delta=delta)
+        else:
+            m = (rng.uniform(size=(8, 6)) if mask_kind == "soft"
+                 else (rng.uniform(size=(8, 6)) < 0.5)).astype(np.float32)
+            arrays["sl1_%d_mask" % k] = m
+            out = ref.smooth_l1_loss(b, tf.constant(a), mask=tf.constant(m), delta=delta)
+        arrays["sl1_%d_out" % k] = np.float64(float(out))
+        meta["sl1"].append([delta, mask_kind])
+    np.savez_compressed(out_path, meta=json.dumps(meta), **arrays)
+
+
+WORKERS["loss_kwargs"] = work_loss_kwargs
+
+
 def main():
     if len(sys.argv) == 3 and sys.argv[1] in WORKERS:
         WORKERS[sys.argv[1]](sys.argv[2])

@@ -789,17 +789,6 @@ def check_maxpool3x3s2_backward(lp, name, launch, dy, argmax, dx):
     lp.cmp(name, "3x3/2 bwd %dx%dx%d B%d" % (H, W, C, B), "dx", dx, _pool3_bwd_ref(dy, argmax, H, W))
 
 
-def check_maxpool_bn_backward_relu(lp, name, launch, dp, argmax, z, mean_rstd, gamma, beta, dz, dgamma, dbeta,
-                                   beta_acc=0.0, conv_dbias=None):
-    dg0, db0 = _clone(dgamma, dbeta)
-    launch(dp, argmax, z, mean_rstd, gamma, beta, dz, dgamma, dbeta, beta_acc=beta_acc, conv_dbias=conv_dbias)
-    B, H, W, C = z.shape
-    dy = _pool3_bwd_ref(dp, argmax, H, W).to(torch.bfloat16)            # the pool-input gradient, rounded
-    mask = _mask_relu_z(z, mean_rstd, gamma, beta, B, H * W, C)
-    _check_bn_bwd(lp, name, "stem pool+bn bwd %dx%dx%d B%d" % (H, W, C, B), dy, z, mean_rstd, gamma, dz, None, 0.0,
-                  None, dgamma, dbeta, dg0, db0, beta_acc, conv_dbias, B, H * W, C, mask)
-
-
 def _up2(b):
     return b.repeat_interleave(2, 1).repeat_interleave(2, 2)
 
@@ -1116,7 +1105,6 @@ CHECKS = {
     "bn_backward_relu_sums": check_bn_backward_relu_sums,
     "bn_backward_res_sums": check_bn_backward_res_sums,
     "bn_relu_maxpool3x3s2": check_bn_relu_maxpool,
-    "maxpool_bn_backward_relu": check_maxpool_bn_backward_relu,
     "maxpool3x3s2": check_maxpool3x3s2,
     "maxpool3x3s2_backward": check_maxpool3x3s2_backward,
     "upsample2x_add": check_upsample2x_add,

@@ -29,26 +29,24 @@ def ref_conv(x, w, b, stride, pad):
     return y.permute(0, 2, 3, 1)
 
 
-@pytest.fixture(params=["base", "l", "l256", "x", "x32"])
+@pytest.fixture(params=["base", "l", "l256", "x32"])
 def kern(request, monkeypatch):
     """Run a test through the 128-row register-staged kernel ("base"), the 256-row LDS-DMA kernel
     ("l", normally taken only by launches with >= 128 tiles; 128/64-wide N tiles), its
-    256x256-tile form ("l256", Npad % 256 == 0 only) and the 8-phase 256x256 kernel ("x", the
-    alternative for the launches l256 would take) and its 32-deep-K ring form ("x32", the default).
-    Weight gradients: "base" runs the 128-wide k-tile kernel, "l"/"l256"/"x" the row-table LDS-DMA
-    kernel (conv_wgrad_l.hip), "x32" the default dispatch (conv_wgrad_x.hip where Npad % 256 == 0)."""
+    256x256-tile form ("l256", Npad % 256 == 0 only) and the 256x256 32-deep-K ring kernel ("x32",
+    the default for those launches).  Weight gradients: "base" runs the 128-wide k-tile kernel,
+    "l"/"l256" the row-table LDS-DMA kernel (conv_wgrad_l.hip), "x32" the default dispatch
+    (conv_wgrad_x.hip where Npad % 256 == 0)."""
     monkeypatch.setenv("CVL_CONV_NO_H", "1")      # the halo kernels have their own tests (test_gpu_conv_h.py)
     monkeypatch.setenv("CVL_WGRAD_NO_H", "1")
-    if request.param in ("l", "l256", "x", "x32"):
+    if request.param in ("l", "l256", "x32"):
         monkeypatch.setenv("CVL_CONV_L_MIN_TILES", "1")
     if request.param == "l":
         monkeypatch.setenv("CVL_CONV_NO_256", "1")
-    if request.param in ("l256", "x", "x32"):
+    if request.param in ("l256", "x32"):
         monkeypatch.setenv("CVL_CONV_L256_MIN_TILES", "1")
     if request.param == "l256":
         monkeypatch.setenv("CVL_CONV_NO_X", "1")
-    if request.param == "x":
-        monkeypatch.setenv("CVL_CONV_NO_X32", "1")
     if request.param != "x32":
         monkeypatch.setenv("CVL_WGRAD_NO_X", "1")
     if request.param not in ("l256", "x", "x32"):

@@ -204,14 +204,15 @@ def test_retina_cls_head_f32_epilogue_configs4(N, NP):
 @pytest.mark.parametrize("mode,B,H,W,C,N", [("fwd", 2, 64, 64, 256, 256), ("dgrad", 3, 32, 32, 512, 256),
                                            ("fwd", 3, 8, 8, 256, 256), ("dgrad", 5, 4, 4, 256, 512),
                                            ("fwd", 2, 16, 16, 256, 256), ("fwd", 1, 64, 64, 64, 256)])
-def test_halo_tile_geometries(monkeypatch, mode, B, H, W, C, N):
-    """The opt-in 3x3 halo kernel (X32H, CVL_CONV_HALO=1) on every tile shape it accepts: R image rows of one image
-    (W = 64 / 32 / 16), whole images per tile (8x8: 4, 4x4: 16 per tile, batches that leave
-    the last tile's images partly absent), Cin 64 / 256 / 512, fwd with bias + ReLU + BN statistics
-    and dgrad.  Against fp64 and bit-identical to the X32 kernel (same K order, same MFMA chain)."""
+def test_x32_tile_geometries(monkeypatch, mode, B, H, W, C, N):
+    """The 256x256 ring kernel (X32) on 3x3 tile geometries: R image rows of one image (W = 64 / 32 /
+    16), several whole images per tile (8x8: 4, 4x4: 16 per tile, batches that leave the last
+    tile's images partly absent), Cin 64 / 256 / 512, fwd with bias + ReLU + BN statistics and
+    dgrad, against fp64."""
     from cvlite import ops_nn as nn
     monkeypatch.setenv("CVL_CONV_L_MIN_TILES", "1")
     monkeypatch.setenv("CVL_CONV_L256_MIN_TILES", "1")
+    monkeypatch.setenv("CVL_CONV_NO_H", "1")
     g = torch.Generator(device="cuda").manual_seed(B * 1000 + H + C)
     x = rnd((B, H, W, C), 1.0, g)
     if mode == "fwd":
@@ -220,25 +221,17 @@ def test_halo_tile_geometries(monkeypatch, mode, B, H, W, C, N):
         bias = torch.randn(N, generator=g, device="cuda")
         d = nn.make_desc(nn.FWD, B, C, 3, 3, 1, 1, 1, N, N, N, [nn.seg(H, W, H, W, wf, bias)], relu_out=True)
         ref = torch.relu(conv_ref(x.to(F64), w) + bias.to(F64))
-        shape_out = (B, H, W, N)
     else:
         w = rnd((3, 3, N, C), (9 * C) ** -0.5, g).to(F64)      # forward conv N -> C; dgrad C -> N
         _, wd = packs(w)
         d = nn.make_desc(nn.DGRAD, B, C, 3, 3, 1, 1, 1, N, N, N, [nn.seg(H, W, H, W, wd, None)])
         ref = dgrad_ref(x.to(F64), w)
-        shape_out = (B, H, W, N)
-    outs = {}
-    for halo in (True, False):
-        monkeypatch.setenv("CVL_CONV_HALO", "1" if halo else "0")
-        out = torch.empty(shape_out, dtype=BF, device="cuda")
-        stats = torch.zeros((B, N, 2), dtype=F64, device="cuda") if mode == "fwd" else None
-        nn.conv_igemm(d, x, out, stats)
-        code, name = last_kernel()
-        assert code == (12 if halo else 7), name
-        outs[halo] = (out, stats)
-    out, stats = outs[True]
+    out = torch.empty((B, H, W, N), dtype=BF, device="cuda")
+    stats = torch.zeros((B, N, 2), dtype=F64, device="cuda") if mode == "fwd" else None
+    nn.conv_igemm(d, x, out, stats)
+    code, name = last_kernel()
+    assert code == 7, name
     torch.testing.assert_close(out.to(F64), ref, rtol=1e-2, atol=2e-2)
-    assert torch.equal(out.view(torch.int16), outs[False][0].view(torch.int16)), "X32H != X32 bits"
     if stats is not None:
         o = out.to(F64)
         torch.testing.assert_close(stats, torch.stack([o.sum((1, 2)), (o * o).sum((1, 2))], -1), rtol=1e-5, atol=1e-3)

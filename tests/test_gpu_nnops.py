@@ -19,12 +19,8 @@ def bfr(t):
 @pytest.mark.parametrize("B,HW,C,relu,res", [(2, 64, 64, True, False), (3, 16, 256, False, True),
                                              (1, 256, 32, True, True), (2, 1000, 64, True, False),
                                              (1, 300, 2048, True, True), (2, 4096, 256, True, False)])
-@pytest.mark.parametrize("small", [False, True])
-def test_bn_forward_backward(B, HW, C, relu, res, small, monkeypatch):
-    """small=True: the opt-in one-launch backward for small maps (CVL_BN_SMALL_MAX_HW)."""
+def test_bn_forward_backward(B, HW, C, relu, res):
     from cvlite import ops_nn as nn
-    if small:
-        monkeypatch.setenv("CVL_BN_SMALL_MAX_HW", "4096")
     g = torch.Generator().manual_seed(B * 100 + C)
     z = bfr(torch.randn(B, HW, C, generator=g, dtype=torch.float64) * 2 + 0.5)
     gamma = torch.rand(C, generator=g, dtype=torch.float64) + 0.5
@@ -398,32 +394,3 @@ def test_bn_relu_maxpool_matches_apply_then_pool(B, H, W):
     nn.bn_relu_maxpool3x3s2(z, mr, gamma, beta, p, a)
     assert torch.equal(p.view(torch.int16), p_ref.view(torch.int16))
     assert torch.equal(a, a_ref)
-
-
-@pytest.mark.parametrize("B,H,W", [(2, 256, 256), (3, 17, 23)])
-def test_maxpool_bn_backward_matches_two_step(B, H, W):
-    """cvl_maxpool_bn_backward_relu (the stem's pool backward inside conv1_bn's backward passes) equals
-    cvl_maxpool3x3s2_backward + cvl_bn_backward_relu: the routed gradient is the same bf16 value in
-    the same row order, so dz, dgamma and dbeta are bit-identical."""
-    from cvlite import ops_nn as nn
-    C = 64
-    dev = torch.device("cuda")
-    g = torch.Generator(device="cpu").manual_seed(B * H + W + 1)
-    z = (torch.randn(B, H, W, C, generator=g) * 2.0).to(BF).to(dev)
-    mr = torch.stack([torch.randn(B, C, generator=g) * 0.3, torch.rand(B, C, generator=g) + 0.5], -1).float().to(dev)
-    gamma = (torch.rand(C, generator=g) + 0.5).to(dev)
-    beta = (torch.randn(C, generator=g) * 0.5).to(dev)
-    Ho, Wo = (H + 2 - 3) // 2 + 1, (W + 2 - 3) // 2 + 1
-    p = torch.empty((B, Ho, Wo, C), dtype=BF, device=dev)
-    arg = torch.empty((B, Ho, Wo, C), dtype=torch.uint8, device=dev)
-    nn.bn_relu_maxpool3x3s2(z, mr, gamma, beta, p, arg)
-    dp = torch.randn(B, Ho, Wo, C, generator=g).to(BF).to(dev)
-    dy = torch.empty_like(z)
-    nn.maxpool3x3s2_backward(dp, arg, dy)
-    dz_r, dz_f = torch.empty_like(z), torch.empty_like(z)
-    dg_r, db_r = torch.zeros(C, device=dev), torch.zeros(C, device=dev)
-    dg_f, db_f = torch.zeros(C, device=dev), torch.zeros(C, device=dev)
-    nn.bn_backward_relu(dy, z, mr, gamma, beta, dz_r, dg_r, db_r, B, H * W, C)
-    nn.maxpool_bn_backward_relu(dp, arg, z, mr, gamma, beta, dz_f, dg_f, db_f)
-    assert torch.equal(dz_f.view(torch.int16), dz_r.view(torch.int16))
-    assert torch.equal(dg_f, dg_r) and torch.equal(db_f, db_r)

