@@ -210,6 +210,43 @@ def tower_alg_bytes(B, net, H, W):
     return 2 * (2 * (2 * B * P) * 256) + 2 * (2 * 256 * 9 * 256)   # src + dst bf16, 2 towers' weights
 
 
+def timed_runs(step, load, pool, args, dev):
+    """W untimed warm-up steps, then `runs` timed runs of EXACTLY K steps each, every run bracketed
+    by a barrier + device synchronize on both sides and maxed over ranks (100 timed
+    steps, median of 3 runs).  Returns the per-run seconds; the reported line uses the median run."""
+    for i in range(args.warmup):
+        load(pool[i % len(pool)])
+        step()
+    times = []
+    for r in range(args.runs):
+        torch.cuda.synchronize()
+        dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for i in range(args.steps):
+            load(pool[i % len(pool)])
+            step()
+        torch.cuda.synchronize()
+        dist.barrier()
+        torch.cuda.synchronize()
+        times.append(dist.max_over_ranks(time.perf_counter() - t0, dev))
+    return times
+
+
+def _median_run(times):
+    return sorted(times)[len(times) // 2]
+
+
+def _cores():
+    """Host cores this process may use: the affinity mask capped by OMP_NUM_THREADS (the GPU box
+    exports its CPU share there; the affinity mask / nproc show the whole machine)."""
+    cores = len(os.sched_getaffinity(0))
+    omp = os.environ.get("OMP_NUM_THREADS")
+    if omp and omp.isdigit() and int(omp) > 0:
+        cores = min(cores, int(omp))
+    return cores
+
+
 def cpu_baseline(H, W, cfg1_images=8, bs=16, timed_images=(8, 8, 8)):
     """The torch-CPU restatement of the reference step (oracle/model_ref.py: batch-1 forwards,
     per-image BN, gradient sum, /bs, clip, Keras SGD), SURVEY.md §8d protocol on a bounded sample:
@@ -219,12 +256,7 @@ def cpu_baseline(H, W, cfg1_images=8, bs=16, timed_images=(8, 8, 8)):
     every core this process may run on (sched_getaffinity)."""
     from oracle import fcos_ref, model_ref
     import numpy as np
-    # the host cores this process may use: the affinity mask, capped by OMP_NUM_THREADS (the GPU box
-    # exports its CPU share there; the affinity mask / nproc show the whole machine)
-    cores = len(os.sched_getaffinity(0))
-    omp = os.environ.get("OMP_NUM_THREADS")
-    if omp and omp.isdigit() and int(omp) > 0:
-        cores = min(cores, int(omp))
+    cores = _cores()
     torch.set_num_threads(cores)
     print("[bench] cpu_baseline: %d threads" % cores, file=sys.stderr, flush=True)
     p = FCOSNet.param_dict(NUM_CLASSES, seed=0)
@@ -256,6 +288,209 @@ def cpu_baseline(H, W, cfg1_images=8, bs=16, timed_images=(8, 8, 8)):
                       % (cfg1_images, H, W, cfg1_s, bs, cores)}
 
 
+def cpu_baseline_retina(S, C, timed_images=2):
+    """configs[4]'s CPU reference: the torch-CPU fp32 restatement of RetinaNet.train_loss + its
+    backward + clip / Keras SGD (oracle/model_ref.retina_loss_and_grads, targets from the oracle's
+    format_data restatement), one warm-up image then `timed_images` images timed one at a time
+    (a batch-1 step each, as train_retinanet_coco.py runs them); img/s = median."""
+    import numpy as np
+    from oracle import model_ref, retina_ref
+    from cvlite.retina_net import RetinaNetNet
+    from cvlite.train_retinanet import synthetic_coco_batch
+    cores = _cores()
+    torch.set_num_threads(cores)
+    sizes = [20.0, 40.0, 80.0, 160.0, 320.0]
+    p = RetinaNetNet.param_dict(C, seed=0)
+    imgs, boxes, nbox = synthetic_coco_batch(1 + timed_images, S, C, n_max=50, seed=4321, device="cpu")
+    ad = retina_ref.anchor_dims(sizes)
+    cells = [(-(-S // s)) ** 2 for s in (8, 16, 32, 64, 128)]
+    rates = []
+    for i in range(1 + timed_images):
+        outs, _ = retina_ref.format_data(boxes[i, :int(nbox[i])].numpy(), np.array([S, S], np.float32), ad, C,
+                                         img_pad=[S, S])
+        tg = torch.from_numpy(np.concatenate([np.stack(outs[l]).reshape(-1, 4 + C) for l in range(5)], 0))
+        t0 = time.time()
+        _, grads, _, _ = model_ref.retina_loss_and_grads(p, imgs[i:i + 1], tg[None].float(), C, cells, 9)
+        with torch.no_grad():
+            norm = float(torch.sqrt(sum((g.double() ** 2).sum() for g in grads.values())))
+            sc = 1.0 / max(norm, 1.0)
+            for k, g in grads.items():
+                p[k] -= 0.01 * sc * g
+        if i > 0:
+            rates.append(1.0 / (time.time() - t0))
+        print("[bench] cpu_baseline retinanet image %d: %.1f s" % (i, time.time() - t0), file=sys.stderr, flush=True)
+    return {"value": round(sorted(rates)[len(rates) // 2], 4), "unit": "images/s", "cores": cores, "kind": "port",
+            "sample": "torch-CPU fp32 restatement of RetinaNet.train_loss fwd+bwd + clip/SGD (oracle/model_ref.py), "
+                      "%dx%d C=%d, 1 warm-up + %d timed single-image steps, median, %d threads" % (S, S, C, timed_images,
+                                                                                           cores)}
+
+
+def cpu_baseline_centernet(S, C, timed_batches=2, sub_batch=2):
+    """configs[3]'s CPU reference: tf_centernet_hourglass.train_step restated in torch-CPU fp32
+    (oracle/centernet_model_ref.train_step_reference: sub-batch BN, 2.5 cls + 1.0 reg, clip, Keras
+    Adam), one warm-up sub-batch step then `timed_batches` timed steps of one sub-batch each; median."""
+    import numpy as np
+    from oracle import centernet_model_ref as cm, centernet_ref
+    from cvlite.hourglass_net import HourglassNet
+    from cvlite.train_centernet import synthetic_batch as cn_batch
+    cores = _cores()
+    torch.set_num_threads(cores)
+    p = HourglassNet.param_dict(C, seed=0)
+    m = {k: torch.zeros_like(v) for k, v in p.items()}
+    v = {k: torch.zeros_like(t) for k, t in p.items()}
+    n = sub_batch * (1 + timed_batches)
+    imgs, boxes, nbox = cn_batch(n, S, S, C, n_max=16, seed=77, device="cpu")
+    tg = torch.stack([torch.from_numpy(centernet_ref.hourglass_format_data(
+        boxes[b, :int(nbox[b])].numpy(), np.array([S, S], np.float32), C, img_pad=[S, S], stride=4)[0]).float()
+        for b in range(n)])
+    rates = []
+    for i in range(1 + timed_batches):
+        sl = slice(i * sub_batch, (i + 1) * sub_batch)
+        t0 = time.time()
+        cm.train_step_reference(p, m, v, i, imgs[sl], tg[sl], C, sub_batch)
+        if i > 0:
+            rates.append(sub_batch / (time.time() - t0))
+        print("[bench] cpu_baseline centernet step %d: %.1f s" % (i, time.time() - t0), file=sys.stderr, flush=True)
+    return {"value": round(sorted(rates)[len(rates) // 2], 4), "unit": "images/s", "cores": cores, "kind": "port",
+            "sample": "torch-CPU fp32 restatement of tf_centernet_hourglass.train_step (oracle/centernet_model_ref.py),"
+                      " %dx%d C=%d, sub-batch %d: 1 warm-up + %d timed steps of %d images, median, %d threads"
+                      % (S, S, C, sub_batch, timed_batches, sub_batch, cores)}
+
+
+PEAK_HBM_GBS = 8000.0          # MI355X HBM3E (MI355X_MICROARCH.md)
+
+
+def dominant_conv_roofline(run_step, iters=10):
+    """`roofline` of a model's dominant conv launch: every conv launch of one eager forward+backward
+    (ops_nn.conv_igemm / conv_wgrad / conv_wgrad_grouped) is recorded, each distinct launch is
+    captured `iters`x into a HIP graph and replayed alone (HIP events on its stream), and the launch
+    with the most time per step is reported against its bound: MFMA when its algorithmic FLOP/byte
+    is above the ridge (2.5 PF / 8 TB/s = 312), else HBM with its algorithmic bytes (operands +
+    result once)."""
+    from cvlite import _lib
+    L = _lib.load()
+    calls, counts = {}, {}
+    orig = (nn.conv_igemm, nn.conv_wgrad, nn.conv_wgrad_grouped)
+
+    def key(kind, d, extra=()):
+        segs = tuple((d.seg[i].Hr, d.seg[i].Wr, d.seg[i].Hs, d.seg[i].Ws) for i in range(d.nseg))
+        return (kind, d.mode, d.B, d.Cin, d.KH, d.KW, d.stride, d.Npad, d.n_store, d.dst_f32, segs) + extra
+
+    def work(kind, d, ng=1):
+        rows = sum(d.B * d.seg[i].Hr * d.seg[i].Wr for i in range(d.nseg))
+        srows = sum(d.B * d.seg[i].Hs * d.seg[i].Ws for i in range(d.nseg))
+        K = d.KH * d.KW * d.Cin
+        fl = 2.0 * rows * K * d.n_store
+        if kind == "igemm":
+            by = srows * d.Cin * 2 + rows * d.n_store * (4 if d.dst_f32 else 2) + d.nseg * d.Npad * K * 2
+        else:
+            by = srows * d.Cin * 2 + rows * d.n_store * 2 + ng * K * d.n_store * 4
+        return fl, by
+
+    def rec(kind, fn, d, args, ng=1):
+        k = key(kind, d, (ng,))
+        counts[k] = counts.get(k, 0) + 1
+        if k not in calls:
+            calls[k] = (fn, d, args, work(kind, d, ng), kind)
+
+    def p_igemm(d, src, dst, stats=None):
+        orig[0](d, src, dst, stats)
+        rec("igemm", orig[0], d, (src, dst, stats))
+
+    def p_wgrad(d, x, dy, dw, beta=0.0):
+        orig[1](d, x, dy, dw, beta)
+        rec("wgrad", orig[1], d, (x, dy, dw, beta))
+
+    def p_wgrad_g(d, x, dy, dws, beta=0.0):
+        orig[2](d, x, dy, dws, beta)
+        rec("wgrad", orig[2], d, (x, dy, dws, beta), len(dws))
+    nn.conv_igemm, nn.conv_wgrad, nn.conv_wgrad_grouped = p_igemm, p_wgrad, p_wgrad_g
+    try:
+        run_step()
+        torch.cuda.synchronize()
+    finally:
+        nn.conv_igemm, nn.conv_wgrad, nn.conv_wgrad_grouped = orig
+    best = None
+    for k, (fn, d, a, (fl, by), kind) in calls.items():
+        with nn.deferred_wgrad():                 # split reductions inside the timed launch
+            fn(d, *a)
+            nn.wgrad_flush()
+        kname = L.cvl_conv_kernel_name(L.cvl_conv_igemm_last_kernel()).decode().split(" (")[0]
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            for _ in range(iters):
+                fn(d, *a)
+        g.replay()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        gs = torch.cuda.current_stream()
+        e0.record(gs)
+        g.replay()
+        e1.record(gs)
+        e1.synchronize()
+        t = e0.elapsed_time(e1) / iters * 1e-3
+        if best is None or t * counts[k] > best[0]:
+            best = (t * counts[k], t, k, fl, by, kind, kname, d)
+        del g
+    tot, t, k, fl, by, kind, kname, d = best
+    mfma = fl / by > PEAK_BF16_TFLOPS * 1e12 / (PEAK_HBM_GBS * 1e9)
+    s0 = d.seg[0]
+    what = "%s %dx%d/%d %d->%d @ %dx%d%s B%d" % ({0: "fwd", 1: "dgrad"}[d.mode] if kind == "igemm" else "wgrad",
+                                              d.KH, d.KW, d.stride, d.Cin, d.n_store, s0.Hr, s0.Wr,
+                                              " +%d seg" % (d.nseg - 1) if d.nseg > 1 else "", d.B)
+    if mfma:
+        ach = fl / t / 1e12
+        r = {"bound": "mfma", "achieved": round(ach, 2), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
+             "frac": round(ach / PEAK_BF16_TFLOPS, 4)}
+    else:
+        ach = by / t / 1e9
+        r = {"bound": "hbm", "achieved": round(ach, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
+             "frac": round(ach / PEAK_HBM_GBS, 4)}
+    r.update({"traffic": None, "kernel": "%s: %s, x%d per step (%.3f ms/step of %d conv launches)"
+              % (kname, what, counts[k], tot * 1e3, sum(counts.values())),
+              "ms_per_launch": round(t * 1e3, 4), "algorithmic": {"flop": fl, "bytes": by},
+              "timing": "the step's own launch (descriptor, packed weights, activations of one eager step) captured "
+                        "%dx into a HIP graph and replayed alone, HIP events on its stream" % iters})
+    return r
+
+
+def centernet_roofline(net, tr, B, S):
+    return dominant_conv_roofline(lambda: tr._fwd_bwd(None))
+
+
+def tower_roofline(net, B, H, W, probe_s=None, probe_n=0, pmc=True):
+    """`roofline` of the FPN detectors' dominant launch (one tower layer of both towers over all five
+    levels, conv_igemm_x32_kernel): in-step probe timing when given, else the burst timing."""
+    k_ms, k_flops, k_name = measure_tower_conv(net, B, H, W)
+    in_ms = probe_s * 1e3 if probe_s else k_ms
+    achieved = k_flops / (in_ms * 1e-3) / 1e12
+    M = 2 * B * net.layout(B, H, W)[2]
+    return {"bound": "mfma", "achieved": round(achieved, 2), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
+            "frac": round(achieved / PEAK_BF16_TFLOPS, 4), "traffic": pmc_traffic(k_name) if pmc else None,
+            "traffic_note": ("HBM bytes per launch from rocprofv3 --pmc FETCH_SIZE (x2, gfx950) + "
+                             "WRITE_SIZE, separate passes (tools/pmc3.sh -> %s; FCOS 512 bs16 geometry)" % PMC_FILE
+                             if pmc else "no PMC pass of this geometry") +
+                            "; algorithmic bytes per launch %d (src + dst bf16 + weights)" % tower_alg_bytes(B, net, H, W),
+            "kernel": "%s, fwd: tower layer 3x3 256->256 of both towers over all 5 levels, one 10-segment launch "
+                      "(M=%d, N=256, K=2304)" % (k_name, M),
+            "ms_per_launch": round(in_ms, 4),
+            "timing": ("mean over the %d tower launches of the timed steps (GPU wall-clock stamps launched "
+                       "before/after each, inside the step graph; includes the two inter-kernel gaps)" % probe_n)
+            if probe_s else "the launch repeated back to back on its own (20x, HIP events on its stream)",
+            "burst_ms_per_launch": round(k_ms, 4),
+            "burst_frac": round(k_flops / (k_ms * 1e-3) / 1e12 / PEAK_BF16_TFLOPS, 4)}
+
+
+def _line(metric, world, B, args, times, extra):
+    el = _median_run(times)
+    out = {"metric": metric, "value": round(world * B * args.steps / el, 3), "unit": "images/s", "n_gpus": world,
+           "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(1000.0 * el / args.steps, 3),
+           "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "bf16",
+           "runs": {"n": len(times), "img_s": [round(world * B * args.steps / t, 3) for t in times],
+                    "reported": "median run (SURVEY.md 8d: median of 3 runs of the timed steps)"}}
+    out.update(extra)
+    return out
+
+
 def bench_retinanet(args):
     """configs[4]: RetinaNet ResNet-50-FPN 640x640 COCO-80, bs=8/GPU (3*bs candidates per step,
     anchor sizes 20..320 as train_retinanet_coco.py:343)."""
@@ -268,34 +503,29 @@ def bench_retinanet(args):
     S = args.size if args.size != 512 else 640
     rn = RetinaNet(80, {}, anchor_sizes=[20.0, 40.0, 80.0, 160.0, 320.0])
     net = rn.model
+    net.tower_probe = torch.zeros(3, dtype=torch.int64, device=dev)
     tr = RetinaTrainer(net, rn, B, S, n_max=50, world=world, use_graph=not args.no_graph)
     pool = [synthetic_coco_batch(3 * B, S, 80, n_max=50, seed=4321 + 97 * rank + i, device=dev) for i in range(2)]
-    for i in range(args.warmup):
+    for i in range(2):                           # capture + one replay before the probe counts
         tr.load_candidates(*pool[i % 2])
         tr.step()
     torch.cuda.synchronize()
-    dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for i in range(args.steps):
-        tr.load_candidates(*pool[i % 2])
-        tr.step()
-    torch.cuda.synchronize()
-    dist.barrier()
-    torch.cuda.synchronize()
-    elapsed = dist.max_over_ranks(time.perf_counter() - t0, dev)
+    net.tower_probe.zero_()
+    times = timed_runs(tr.step, lambda b: tr.load_candidates(*b), pool, args, dev)
     if rank != 0:
         dist.barrier()
         return
-    out = {"metric": "training images/sec (whole node), RetinaNet-R50-FPN COCO 640x640 bs=8/GPU",
-           "value": round(world * B * args.steps / elapsed, 3), "unit": "images/s", "n_gpus": world,
-           "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(1000.0 * elapsed / args.steps, 3),
-           "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "bf16",
-           "data": "synthetic COCO-shaped: 3*bs candidates/step, 1+Poisson(6.3) boxes, C=80; random init",
-           "config": {"workload": "RetinaNet R50-FPN train step (assign 3bs candidates + select + fwd + loss + "
-                                  "bwd + clip/SGD)", "model": "RetinaNet-ResNet50-FPN", "global_batch": B * world,
-                      "image_size": S, "parallelism": "dp%d" % world},
-           "last_step_losses_cls_reg": [round(x, 3) for x in tr.losses.double().sum(0).cpu().tolist()]}
+    in_s, in_n = nn.probe_seconds(net.tower_probe)
+    net.tower_probe = None
+    out = _line("training images/sec (whole node), RetinaNet-R50-FPN COCO 640x640 bs=8/GPU", world, B, args, times, {
+        "data": "synthetic COCO-shaped: 3*bs candidates/step, 1+Poisson(6.3) boxes, C=80; random init",
+        "config": {"workload": "RetinaNet R50-FPN train step (assign 3bs candidates + select + fwd + loss + "
+                               "bwd + clip/SGD)", "model": "RetinaNet-ResNet50-FPN", "global_batch": B * world,
+                   "image_size": S, "parallelism": "dp%d" % world},
+        "roofline": tower_roofline(net, B, S, S, in_s, in_n, pmc=False),
+        "last_step_losses_cls_reg": [round(x, 3) for x in tr.losses.double().sum(0).cpu().tolist()]})
+    if world == 1 and not args.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline_retina(S, 80)
     print(json.dumps(out), flush=True)
     if world > 1:
         dist.barrier()
@@ -315,32 +545,19 @@ def bench_centernet(args):
     net = HourglassNet(NUM_CLASSES, device=dev, seed=0)
     tr = CenterNetTrainer(net, B, (S, S), sub_batch_sz=2, n_max=16, world=world, use_graph=not args.no_graph)
     pool = [cn_batch(B, S, S, NUM_CLASSES, n_max=16, seed=777 + 97 * rank + i, device=dev) for i in range(2)]
-    for i in range(args.warmup):
-        tr.load_batch(*pool[i % 2])
-        tr.step()
-    torch.cuda.synchronize()
-    dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for i in range(args.steps):
-        tr.load_batch(*pool[i % 2])
-        tr.step()
-    torch.cuda.synchronize()
-    dist.barrier()
-    torch.cuda.synchronize()
-    elapsed = dist.max_over_ranks(time.perf_counter() - t0, dev)
+    times = timed_runs(tr.step, lambda b: tr.load_batch(*b), pool, args, dev)
     if rank != 0:
         dist.barrier()
         return
-    out = {"metric": "training images/sec (whole node), CenterNet-hourglass VOC 512x512 bs=8/GPU",
-           "value": round(world * B * args.steps / elapsed, 3), "unit": "images/s", "n_gpus": world,
-           "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(1000.0 * elapsed / args.steps, 3),
-           "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "bf16",
-           "data": "synthetic VOC-shaped: U[-1,1) images, 1+Poisson(1.4) boxes, C=20; random init",
-           "config": {"workload": "CenterNet hourglass train step (centroid targets + fwd + loss + bwd + clip/Adam), "
-                                  "BN sub-batch 2", "model": "CenterNet-separable-hourglass-nf128",
-                      "global_batch": B * world, "image_size": S, "parallelism": "dp%d" % world},
-           "last_step_losses_cls_reg": [round(x, 3) for x in tr.losses.double().sum(0).cpu().tolist()]}
+    out = _line("training images/sec (whole node), CenterNet-hourglass VOC 512x512 bs=8/GPU", world, B, args, times, {
+        "data": "synthetic VOC-shaped: U[-1,1) images, 1+Poisson(1.4) boxes, C=20; random init",
+        "config": {"workload": "CenterNet hourglass train step (centroid targets + fwd + loss + bwd + clip/Adam), "
+                               "BN sub-batch 2", "model": "CenterNet-separable-hourglass-nf128",
+                   "global_batch": B * world, "image_size": S, "parallelism": "dp%d" % world},
+        "roofline": centernet_roofline(net, tr, B, S),
+        "last_step_losses_cls_reg": [round(x, 3) for x in tr.losses.double().sum(0).cpu().tolist()]})
+    if world == 1 and not args.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline_centernet(S, NUM_CLASSES)
     print(json.dumps(out), flush=True)
     if world > 1:
         dist.barrier()
@@ -386,8 +603,9 @@ def dry_run(args):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--steps", type=int, default=100)
+    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--runs", type=int, default=3, help="timed runs of --steps steps each; the line reports the median")
     ap.add_argument("--bs", type=int, default=16)
     ap.add_argument("--size", type=int, default=512)
     ap.add_argument("--no-graph", action="store_true")
@@ -417,72 +635,34 @@ def main():
     net.tower_probe = torch.zeros(3, dtype=torch.int64, device=dev)
     tr = FCOSTrainer(net, B, (H, W), world=world, use_graph=not args.no_graph)
     pool = [synthetic_batch(B, H, W, NUM_CLASSES, seed=1234 + 97 * rank + i, device=dev) for i in range(4)]
-    for i in range(args.warmup):
+    for i in range(2):                           # capture + one replay before the probe counts
         tr.load_batch(*pool[i % 4])
         tr.step()
     torch.cuda.synchronize()
     net.tower_probe.zero_()                      # count only the timed steps' tower launches
-    dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for i in range(args.steps):
-        tr.load_batch(*pool[i % 4])
-        tr.step()
-    torch.cuda.synchronize()
-    dist.barrier()
-    torch.cuda.synchronize()
-    elapsed = dist.max_over_ranks(time.perf_counter() - t0, dev)
+    times = timed_runs(tr.step, lambda b: tr.load_batch(*b), pool, args, dev)
     losses = tr.losses.detach().double().sum(0).cpu().tolist()
-    ms_step = 1000.0 * elapsed / args.steps
-    img_s = world * B * args.steps / elapsed
+    img_s = world * B * args.steps / _median_run(times)
     fl_img = train_flops_per_image(H, W)
     if rank != 0:
         dist.barrier()
         return
     in_s, in_n = nn.probe_seconds(net.tower_probe)
     net.tower_probe = None
-    k_ms, k_flops, k_name = measure_tower_conv(net, B, H, W)
-    bb3 = measure_backbone_3x3(net, B, H, W)
-    in_ms = in_s * 1e3 if in_s else k_ms
-    achieved = k_flops / (in_ms * 1e-3) / 1e12
-    out = {
-        "metric": METRIC,
-        "value": round(img_s, 3),
-        "unit": "images/s",
-        "n_gpus": world,
-        "steps": args.steps,
-        "warmup": args.warmup,
-        "ms_per_step": round(ms_step, 3),
-        "higher_is_better": True,
-        "scaling": "weak",
-        "vs_baseline": None,
-        "dtype": "bf16",
+    roof = tower_roofline(net, B, H, W, in_s, in_n, pmc=(B, H, W) == (16, 512, 512))
+    roof["backbone_3x3"] = measure_backbone_3x3(net, B, H, W)
+    out = _line(METRIC, world, B, args, times, {
         "data": "synthetic VOC-shaped: U[-1,1) 512x512 images, 1+Poisson(1.4) boxes, log-uniform 12-480 px, "
                 "C=20; random-init (Keras glorot) weights",
         "config": {"workload": "FCOS ResNet-50-FPN train step (targets + fwd + loss + bwd + clip/SGD), "
                                "512x512, bs=16 per GPU",
                    "model": "FCOS-ResNet50-FPN", "global_batch": B * world, "image_size": H,
                    "parallelism": "dp%d" % world},
-        "roofline": {"bound": "mfma", "achieved": round(achieved, 2), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
-                     "frac": round(achieved / PEAK_BF16_TFLOPS, 4), "traffic": pmc_traffic(k_name),
-                     "traffic_note": "HBM bytes per launch from rocprofv3 --pmc FETCH_SIZE (x2, gfx950) + "
-                                     "WRITE_SIZE, separate passes (tools/pmc3.sh -> %s); algorithmic "
-                                     "bytes per launch %d (src + dst bf16 + weights)" % (PMC_FILE, tower_alg_bytes(B, net, H, W)),
-                     "kernel": "%s, fwd: FCOS cls+reg tower layer 3x3 256->256 over all 5 levels, one "
-                               "10-segment launch (M=%d, N=256, K=2304)" % (k_name, 2 * B * net.layout(B, H, W)[2]),
-                     "ms_per_launch": round(in_ms, 4),
-                     "timing": "mean over the %d tower launches of the timed steps (GPU wall-clock stamps "
-                               "launched before/after each, inside the step graph; includes the two "
-                               "inter-kernel gaps)" % in_n,
-                     "burst_ms_per_launch": round(k_ms, 4),
-                     "burst_frac": round(k_flops / (k_ms * 1e-3) / 1e12 / PEAK_BF16_TFLOPS, 4),
-                     "burst_note": "the same launch repeated back to back on its own (20x, HIP events)",
-                     "backbone_3x3": bb3},
+        "roofline": roof,
         "dist": dist_info(world),
         "model_flops_per_image": fl_img,
         "step_mfma_frac": round(img_s / world * fl_img / 1e12 / PEAK_BF16_TFLOPS, 4),
-        "last_step_losses_cls_reg_cen": [round(x, 3) for x in losses],
-    }
+        "last_step_losses_cls_reg_cen": [round(x, 3) for x in losses]})
     if world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(H, W)
     print(json.dumps(out), flush=True)
