@@ -83,241 +83,270 @@ __host__ __device__ inline HGeo h_geo(int H, int W) {
   return g;
 }
 
-template <bool DGRAD, bool BSUM, bool DBG = false>
-__global__ void __launch_bounds__(NT) conv_igemm_h_kernel(ConvArgs a) {
-  // DBG: ablation switches (a.dbg bits, CVL_X_ABLATE) for measurement builds only: 1 no halo
-  // traffic, 2 no weight traffic, 4 no MFMA, 8 no epilogue, 16 no vmcnt waits, 64 no LDS reads
-  const int dbg = DBG ? a.dbg : 0;
-  __shared__ __attribute__((aligned(16))) cvl_bf16 lds[LDS_EL];
-  // 256: wall-clock stamps of thread 0 of every workgroup into dst (u64 [grid][8]: entry, set-up
-  // done, prologue landed, main loop done, exit, HW_ID, XCC_ID)
-  unsigned long long* stamp = (DBG && (dbg & 256) && threadIdx.x == 0)
-                                  ? reinterpret_cast<unsigned long long*>(a.dst) + (size_t)blockIdx.x * 8 : nullptr;
-  if (stamp) {
-    stamp[0] = wall_clock64();
-    stamp[5] = __builtin_amdgcn_s_getreg((31 << 11) | 4);
-    stamp[6] = __builtin_amdgcn_s_getreg((31 << 11) | 20);
-  }
+// Per-segment constants of the halo DMA: for each of this lane's HPW halo pieces, its pixel
+// relative to the tile (row mode: (hy - 1) * W + hx - 1 and the row hy - 1 for the vertical
+// bound; mosaic: the image index within the tile + (gy, gx)), or invalid (past the halo, a zero
+// column / seam).  The per-tile offsets then cost an add and a compare per piece.
+struct HaloPieces {
+  int rel[HPW];       // row mode: pixel offset from the tile's first row; mosaic: gy * W + gx
+  int yrow[HPW];      // row mode: halo row - 1; mosaic: image index within the tile
+  unsigned valid;     // bit j: the piece is inside the halo image and not a zero column / seam
+};
 
+__device__ __forceinline__ HaloPieces halo_pieces(const HGeo& G, int H, int W, int wave, int lane) {
+  HaloPieces P;
+  P.valid = 0;
+  const int hpx = G.rows * G.pitch;
+#pragma unroll
+  for (int j = 0; j < HPW; ++j) {
+    const int hp = 16 * (wave + 8 * j) + (lane >> 2);
+    const int hy = hp / G.pitch, hx = hp - hy * G.pitch;
+    bool ok;
+    if (!G.whole) {
+      const int gx = hx - 1;
+      ok = gx >= 0 && gx < W;
+      P.rel[j] = (hy - 1) * W + gx;
+      P.yrow[j] = hy - 1;
+    } else {
+      const int ix = (hx - 1) / (W + 1), iy = (hy - 1) / (H + 1);
+      const int gx = hx - 1 - ix * (W + 1), gy = hy - 1 - iy * (H + 1);
+      ok = hx >= 1 && hy >= 1 && gx < W && gy < H && ix < G.mx && iy < G.my;
+      P.rel[j] = gy * W + gx;
+      P.yrow[j] = iy * G.mx + ix;
+    }
+    if (ok && hp < hpx) P.valid |= 1u << j;
+  }
+  return P;
+}
+
+// H64, persistent: a workgroup runs a contiguous chunk of the launch's 256 x 64 tiles (all of
+// them when the launch is split over K: then one tile per workgroup).  The DMA stream runs across
+// tile boundaries: during the last channel block of a tile the first stage of the next tile is
+// issued, so that tile's halo and weights land while the current tile's epilogue runs (the
+// epilogue stages its C image in the stage buffer just consumed), and the per-tile set-up is a
+// few adds (halo_pieces is per segment).  One workgroup per CU (148 KiB of LDS).
+template <bool DGRAD, bool BSUM>
+__global__ void __launch_bounds__(NT) conv_igemm_h_kernel(ConvArgs a) {
+  __shared__ __attribute__((aligned(16))) cvl_bf16 lds[LDS_EL];
   const int tid = threadIdx.x;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
   const int ntn = a.Npad / BN;
-  const int nmn = gridDim.x;                        // m tiles x n tiles (the z dimension splits K)
-  const int L = xcd_remap(blockIdx.x, nmn);
-  const int m_tile = L / ntn, n_tile = L % ntn;
-  const int m0 = m_tile * BM, n0 = n_tile * BN;
-  int sg = 0;
-#pragma unroll
-  for (int i = 1; i < kMaxSeg; ++i)
-    if (i < a.nseg && m0 >= a.seg[i].m_start) sg = i;
-  const ConvSeg& S = a.seg[sg];
-  const int HWr = S.Hr * S.Wr;
-  const int mloc0 = m0 - S.m_start;
-  if (mloc0 >= S.rows) return;
-  s16x8 zpre[BnSumPre<BN, NT>::N];
-  BnSumPar bpar;
-  if constexpr (BSUM) bnsum_prefetch<BN, NT>(a, S, tid, n0, mloc0, zpre, bpar);
+  const int ntiles = a.m_tiles * ntn;
+  const int G_ = gridDim.x;
+  const int wl = xcd_remap(blockIdx.x, G_);
+  const int t_lo = (int)((long)wl * ntiles / G_), t_hi = (int)((long)(wl + 1) * ntiles / G_);
 
-  const int Cin = a.Cin, W = S.Wr, H = S.Hr;
-  const int Kdim = a.K;
+  const int Cin = a.Cin, Kdim = a.K;
   const int ncb_all = Cin / BK;
   int cb0 = 0, cb1 = ncb_all;
   if (a.splits > 1) {
     cb0 = blockIdx.z * a.ksteps_per_split;
     cb1 = min(ncb_all, cb0 + a.ksteps_per_split);
   }
-  const HGeo G = h_geo(H, W);
-  const int img0 = mloc0 / HWr;
-  const int y0 = G.whole ? 0 : (mloc0 - img0 * HWr) / W;
-  const int hpx = G.rows * G.pitch;
-
-  // DMA pieces of this lane, straight-line per stage: halo pieces k = wave + 8 j (j < HPW; pixels
-  // 16 k .. 16 k + 15, lane: pixel lane / 4, chunk lane % 4), weight pieces k = wave + 8 j (j < 4,
-  // and j = 4 on waves 0-3; rows 16 (k % 4) .. of tap k / 4).  Invalid halo pixels (outside the
-  // map, mosaic seams, absent images, past the halo) carry the out-of-range offset, which stays
-  // out of range when the channel block's byte offset is added.
-  const int hch = lane & 3;
-  unsigned hoff[HPW], woff[5];
+  // a tile's segment / local row; -1 segment = padding tile (no rows)
+  auto tile_seg = [&](int L, int* sg, int* mloc0, int* n0) {
+    const int m0 = (L / ntn) * BM;
+    *n0 = (L % ntn) * BN;
+    int q = 0;
 #pragma unroll
-  for (int j = 0; j < HPW; ++j) {
-    const int hp = 16 * (wave + 8 * j) + (lane >> 2);
-    const int hy = hp / G.pitch, hx = hp - hy * G.pitch;
-    int img, gy, gx;
-    bool ok;
-    if (!G.whole) {
-      img = img0;
-      gy = y0 + hy - 1;
-      gx = hx - 1;
-      ok = gy >= 0 && gy < H && gx >= 0 && gx < W;
-    } else {
-      const int ix = (hx - 1) / (W + 1), iy = (hy - 1) / (H + 1);
-      gx = hx - 1 - ix * (W + 1);
-      gy = hy - 1 - iy * (H + 1);
-      img = img0 + iy * G.mx + ix;
-      ok = hx >= 1 && hy >= 1 && gx < W && gy < H && ix < G.mx && iy < G.my;
-    }
-    ok = ok && hp < hpx && img < a.B;
-    const long pix = S.src_base + (long)img * S.src_img + (long)gy * W + gx;
-    hoff[j] = ok ? (unsigned)(pix * Cin * 2) + (unsigned)((hch ^ swz4(hp)) * 16) : kOOB;
-  }
-#pragma unroll
-  for (int j = 0; j < 5; ++j) {
-    const int w = (wave + 8 * j) % WPC, tap = w >> 2;
-    const int row = (w & 3) * 16 + (lane >> 2);
-    woff[j] = (unsigned)(((n0 + row) * Kdim + tap * Cin) * 2) + (unsigned)((hch ^ swz4(row)) * 16);
-  }
-  const __amdgpu_buffer_rsrc_t rsA = __builtin_amdgcn_make_buffer_rsrc((void*)a.src, (short)0, (int)kRecords, 0x00020000);
-  const __amdgpu_buffer_rsrc_t rsB = __builtin_amdgcn_make_buffer_rsrc((void*)S.w, (short)0, (int)kRecords, 0x00020000);
-
-  // the halo / the weights of channel block cb into stage buffer cb & 1
-  auto issue_halo = [&](int cb) {
-    if (dbg & 1) return;
-    cvl_bf16* st = lds + (cb & 1) * STAGE_EL;
-    const unsigned cbo = (unsigned)(cb * BK * 2);
-#pragma unroll
-    for (int j = 0; j < HPW; ++j) dma16(rsA, st + (wave + 8 * j) * 16 * BK, hoff[j] + cbo);
+    for (int i = 1; i < kMaxSeg; ++i)
+      if (i < a.nseg && m0 >= a.seg[i].m_start) q = i;
+    *sg = q;
+    *mloc0 = m0 - a.seg[q].m_start;
+    return *mloc0 < a.seg[q].rows;
   };
-  auto issue_w = [&](int cb) {
-    if (dbg & 2) return;
-    cvl_bf16* st = lds + (cb & 1) * STAGE_EL + HALO_EL;
-    const unsigned cbo = (unsigned)(cb * BK * 2);
+  auto next_tile = [&](int L) {            // first tile >= L of this chunk with rows, or t_hi
+    int sg, ml, n0;
+    while (L < t_hi && !tile_seg(L, &sg, &ml, &n0)) ++L;
+    return L;
+  };
+
+  // ---- issue cursor: the channel block whose stage the next issue slots load ------------------
+  const int hch = lane & 3;
+  int i_L = next_tile(t_lo), i_cb = cb0, i_sg = -1;
+  unsigned hoff[HPW], woff[5];
+  HaloPieces HP;
+  HP.valid = 0;
+  auto cursor_tile = [&]() {               // hoff / woff of the cursor's tile
+    int sg, mloc0, n0;
+    tile_seg(i_L, &sg, &mloc0, &n0);
+    const ConvSeg& S = a.seg[sg];
+    const int W = S.Wr, H = S.Hr, HWr = H * W;
+    const HGeo G = h_geo(H, W);
+    if (sg != i_sg) {
+      HP = halo_pieces(G, H, W, wave, lane);
+      i_sg = sg;
+    }
+    const int img0 = mloc0 / HWr;
+    const int y0 = G.whole ? 0 : (mloc0 - img0 * HWr) / W;
+    const long base = S.src_base + (long)img0 * S.src_img + (long)y0 * W;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) dma16(rsB, st + (wave + 8 * j) * 16 * BK, woff[j] + cbo);
-    if (wave < WPC - 32) dma16(rsB, st + (wave + 32) * 16 * BK, woff[4] + cbo);
+    for (int j = 0; j < HPW; ++j) {
+      const int hp = 16 * (wave + 8 * j) + (lane >> 2);
+      bool ok = (HP.valid >> j) & 1u;
+      long pix;
+      if (!G.whole) {
+        ok = ok && (unsigned)(y0 + HP.yrow[j]) < (unsigned)H && img0 < a.B;
+        pix = base + HP.rel[j];
+      } else {
+        const int img = img0 + HP.yrow[j];
+        ok = ok && img < a.B;
+        pix = S.src_base + (long)img * S.src_img + HP.rel[j];
+      }
+      hoff[j] = ok ? (unsigned)(pix * Cin * 2) + (unsigned)((hch ^ swz4(hp)) * 16) : kOOB;
+    }
+#pragma unroll
+    for (int j = 0; j < 5; ++j) {
+      const int w = (wave + 8 * j) % WPC, tap = w >> 2;
+      const int row = (w & 3) * 16 + (lane >> 2);
+      woff[j] = (unsigned)(((n0 + row) * Kdim + tap * Cin) * 2) + (unsigned)((hch ^ swz4(row)) * 16);
+    }
+  };
+  if (i_L >= t_hi) return;
+  cursor_tile();
+  const __amdgpu_buffer_rsrc_t rsA = __builtin_amdgcn_make_buffer_rsrc((void*)a.src, (short)0, (int)kRecords, 0x00020000);
+  // the weight resource of the cursor's segment (segments may own different weights)
+  __amdgpu_buffer_rsrc_t rsB = __builtin_amdgcn_make_buffer_rsrc((void*)a.seg[i_sg].w, (short)0, (int)kRecords, 0x00020000);
+  auto advance = [&]() {                   // the cursor moves one channel block (and maybe a tile)
+    if (++i_cb < cb1) return;
+    i_cb = cb0;
+    i_L = next_tile(i_L + 1);
+    if (i_L < t_hi) {
+      cursor_tile();
+      rsB = __builtin_amdgcn_make_buffer_rsrc((void*)a.seg[i_sg].w, (short)0, (int)kRecords, 0x00020000);
+    }
   };
 
   const int wm = wave >> 1, wn = wave & 1;          // conv_l_epilogue's 4 x 2 wave grid
   const int lr = lane & 15, lg = lane >> 4;
-  // swizzled LDS byte offset (within a halo image) of each A fragment row of this lane for
-  // dx = -1, 0, +1 (the dy shift is added per phase)
-  unsigned afr[TM][3];
-#pragma unroll
-  for (int i = 0; i < TM; ++i) {
-    const int r = wm * WM + i * 16 + lr;
-    const int ii = r / HWr, q = r - ii * HWr;
-    const int yy = q / W, xx = q - yy * W;
-    const int hy = 1 + (G.whole ? (ii / G.mx) * (H + 1) : 0) + yy;
-    const int hx = 1 + (G.whole ? (ii % G.mx) * (W + 1) : 0) + xx;
-    const int pc = hy * G.pitch + hx;
-#pragma unroll
-    for (int d = 0; d < 3; ++d) {
-      const int pp = pc + d - 1;
-      afr[i][d] = (unsigned)(pp * BK * 2 + ((lg ^ swz4(pp)) * 16));
-    }
-  }
-  // B fragment byte offsets within a tap's weight image
+  // B fragment byte offsets within a tap's weight image (tile-invariant)
   unsigned bfr[TN];
 #pragma unroll
   for (int j = 0; j < TN; ++j) {
     const int rr = wn * WN + j * 16 + lr;
     bfr[j] = (unsigned)(rr * BK * 2 + ((lg ^ swz4(rr)) * 16));
   }
-  f32x4 acc[TM][TN];
-#pragma unroll
-  for (int i = 0; i < TM; ++i)
-#pragma unroll
-    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  auto bar = [&]() {
-    if (!(dbg & 512)) __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");
-  };
 
-  // prologue: stage cb0 complete everywhere
-  if (stamp) stamp[1] = wall_clock64();
-  issue_halo(cb0);
-  issue_w(cb0);
+  // prologue: the first channel block's stage complete everywhere
+  {
+    cvl_bf16* st = lds;
+    const unsigned cbo = (unsigned)(i_cb * BK * 2);
+#pragma unroll
+    for (int j = 0; j < HPW; ++j) dma16(rsA, st + (wave + 8 * j) * 16 * BK, hoff[j] + cbo);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) dma16(rsB, st + HALO_EL + (wave + 8 * j) * 16 * BK, woff[j] + cbo);
+    if (wave < WPC - 32) dma16(rsB, st + HALO_EL + (wave + 32) * 16 * BK, woff[4] + cbo);
+    advance();
+  }
   wait_vm<0>();
   __builtin_amdgcn_s_barrier();
   asm volatile("" ::: "memory");
-  if (stamp) stamp[2] = wall_clock64();
 
-  const int prow = G.pitch * BK * 2;                // bytes per halo row
-  // One channel block = nine taps, software-pipelined inside each wave: the fragments of tap t + 1
-  // are read from LDS while the 8 MFMAs of tap t issue, and the DMA pieces of block cb + 1 (into
-  // the other stage buffer, free since the barrier that opened block cb) are spread over the taps.
-  // Both waves of a SIMD run this same stream; whichever is not stalled on an issue feeds the
-  // matrix pipe.  One barrier per block: every wave's pieces of block cb + 1 have landed (vmcnt 0)
-  // and every wave is done reading block cb.
-  s16x8 fa[2][TM], fb[2][TN];
-  auto read_tap = [&](int buf, const char* Hc, int t) {
-    const int r = t / 3, sx = t - 3 * (t / 3);
-    const int d = DGRAD ? 2 - sx : sx;
-    const char* Hr = Hc + (DGRAD ? 1 - r : r - 1) * prow;
-    const char* Wt = Hc + HALO_EL * 2 + t * BN * BK * 2;
-    if (dbg & 64) {
+  int gb = 0;                                       // global channel-block counter (stage parity)
+  int c_sg = -1;
+  unsigned afr[TM][3];
+  int HWr = 1, prow = 0;
+  for (int L = next_tile(t_lo); L < t_hi; L = next_tile(L + 1)) {
+    int sg, mloc0, n0;
+    tile_seg(L, &sg, &mloc0, &n0);
+    const ConvSeg& S = a.seg[sg];
+    if (sg != c_sg) {                               // compute-side constants of the segment
+      c_sg = sg;
+      const int W = S.Wr, H = S.Hr;
+      HWr = H * W;
+      const HGeo G = h_geo(H, W);
+      prow = G.pitch * BK * 2;
 #pragma unroll
-      for (int i = 0; i < TM; ++i) fa[buf][i] = s16x8{(short)lane, 0, 0, 0, 0, 0, 0, (short)t};
+      for (int i = 0; i < TM; ++i) {
+        const int r = wm * WM + i * 16 + lr;
+        const int ii = r / HWr, q = r - ii * HWr;
+        const int yy = q / W, xx = q - yy * W;
+        const int hy = 1 + (G.whole ? (ii / G.mx) * (H + 1) : 0) + yy;
+        const int hx = 1 + (G.whole ? (ii % G.mx) * (W + 1) : 0) + xx;
+        const int pc = hy * G.pitch + hx;
 #pragma unroll
-      for (int j = 0; j < TN; ++j) fb[buf][j] = s16x8{(short)j, 0, 0, 0, 0, 0, 0, (short)t};
-      return;
+        for (int d = 0; d < 3; ++d) {
+          const int pp = pc + d - 1;
+          afr[i][d] = (unsigned)(pp * BK * 2 + ((lg ^ swz4(pp)) * 16));
+        }
+      }
     }
-#pragma unroll
-    for (int i = 0; i < TM; ++i) fa[buf][i] = *reinterpret_cast<const s16x8*>(Hr + afr[i][d]);
-#pragma unroll
-    for (int j = 0; j < TN; ++j) fb[buf][j] = *reinterpret_cast<const s16x8*>(Wt + bfr[j]);
-  };
-  auto mma_tap = [&](int buf) {
-    if (dbg & 4) {
-      asm volatile("" ::"v"(fa[buf][0]), "v"(fb[buf][0]), "v"(fa[buf][TM - 1]), "v"(fb[buf][TN - 1]));
-      return;
-    }
+    s16x8 zpre[BnSumPre<BN, NT>::N];
+    BnSumPar bpar;
+    if constexpr (BSUM) bnsum_prefetch<BN, NT>(a, S, tid, n0, mloc0, zpre, bpar);
+    f32x4 acc[TM][TN];
 #pragma unroll
     for (int i = 0; i < TM; ++i)
 #pragma unroll
-      for (int j = 0; j < TN; ++j)
-        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, fa[buf][i]),
-                                                             __builtin_bit_cast(bf16x8, fb[buf][j]), acc[i][j], 0, 0, 0);
-  };
-  const cvl_bf16* hw0 = lds;
-  for (int cb = cb0; cb < cb1; ++cb) {
-    const char* Hc = reinterpret_cast<const char*>(hw0 + (cb & 1) * STAGE_EL);
-    const bool more = cb + 1 < cb1;
-    cvl_bf16* nh = lds + ((cb + 1) & 1) * STAGE_EL;
-    const unsigned cbo = (unsigned)((cb + 1) * BK * 2);
-    read_tap(0, Hc, 0);
+      for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    // One channel block = nine taps, software-pipelined inside each wave: the fragments of tap
+    // t + 1 are read from LDS while the 8 MFMAs of tap t issue, and the DMA pieces of the cursor's
+    // block (the next block of this tile, or the first of the next tile) go into the other stage
+    // buffer, spread over the taps.  One barrier per block: every wave's pieces of the next block
+    // have landed (vmcnt 0) and every wave is done reading this one.
+    s16x8 fa[2][TM], fb[2][TN];
+    auto read_tap = [&](int buf, const char* Hc, int t) {
+      const int r = t / 3, sx = t - 3 * (t / 3);
+      const int d = DGRAD ? 2 - sx : sx;
+      const char* Hr = Hc + (DGRAD ? 1 - r : r - 1) * prow;
+      const char* Wt = Hc + HALO_EL * 2 + t * BN * BK * 2;
 #pragma unroll
-    for (int t = 0; t < 9; ++t) {
-      // DMA pieces of block cb + 1: halo piece t (t < HPW), weight piece t - HPW
-      if (more && !(dbg & 1) && t < HPW) dma16(rsA, nh + (wave + 8 * t) * 16 * BK, hoff[t] + cbo);
-      if (more && !(dbg & 2) && t >= HPW && t < HPW + 4)
-        dma16(rsB, nh + HALO_EL + (wave + 8 * (t - HPW)) * 16 * BK, woff[t - HPW] + cbo);
-      if (t == 8 && more && !(dbg & 2) && wave < WPC - 32)
-        dma16(rsB, nh + HALO_EL + (wave + 32) * 16 * BK, woff[4] + cbo);
-      if (t < 8) read_tap((t + 1) & 1, Hc, t + 1);
-      mma_tap(t & 1);
+      for (int i = 0; i < TM; ++i) fa[buf][i] = *reinterpret_cast<const s16x8*>(Hr + afr[i][d]);
+#pragma unroll
+      for (int j = 0; j < TN; ++j) fb[buf][j] = *reinterpret_cast<const s16x8*>(Wt + bfr[j]);
+    };
+    auto mma_tap = [&](int buf) {
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, fa[buf][i]),
+                                                               __builtin_bit_cast(bf16x8, fb[buf][j]), acc[i][j], 0, 0, 0);
+    };
+    for (int cb = cb0; cb < cb1; ++cb) {
+      const char* Hc = reinterpret_cast<const char*>(lds + (gb & 1) * STAGE_EL);
+      const bool more = i_L < t_hi;
+      cvl_bf16* nh = lds + ((gb + 1) & 1) * STAGE_EL;
+      const unsigned cbo = (unsigned)(i_cb * BK * 2);
+      read_tap(0, Hc, 0);
+#pragma unroll
+      for (int t = 0; t < 9; ++t) {
+        if (more && t < HPW) dma16(rsA, nh + (wave + 8 * t) * 16 * BK, hoff[t] + cbo);
+        if (more && t >= HPW && t < HPW + 4) dma16(rsB, nh + HALO_EL + (wave + 8 * (t - HPW)) * 16 * BK, woff[t - HPW] + cbo);
+        if (t == 8 && more && wave < WPC - 32) dma16(rsB, nh + HALO_EL + (wave + 32) * 16 * BK, woff[4] + cbo);
+        if (t < 8) read_tap((t + 1) & 1, Hc, t + 1);
+        mma_tap(t & 1);
+      }
+      if (more) advance();
+      wait_vm<0>();                                 // this wave's pieces of the next block landed
+      __builtin_amdgcn_s_barrier();                 // ... and everyone's; this block fully read
+      asm volatile("" ::: "memory");
+      ++gb;
     }
-    if (!(dbg & 16)) wait_vm<0>();                  // this wave's pieces of block cb + 1 landed
-    bar();                                          // ... and everyone's; block cb fully read
+    if (a.splits > 1) {           // raw fp32 partials; conv_igemm.hip's finish applies the epilogue
+      const int m0 = mloc0 + S.m_start;
+      float* slab = a.slab + (size_t)blockIdx.z * a.m_total * a.Npad;
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const int rr = m0 + wm * WM + i * 16 + lg * 4 + e;
+            const int c = n0 + wn * WN + j * 16 + lr;
+            slab[(size_t)rr * a.Npad + c] = acc[i][j][e];
+          }
+      continue;
+    }
+    // the epilogue's C image goes into the stage buffer just consumed (the other one holds the
+    // next tile's first stage, in flight); the barrier after it frees that buffer for the DMA
+    conv_l_epilogue<BN, WGM, TM, TN, NT, BSUM>(a, S, acc, lds + ((gb - 1) & 1) * STAGE_EL, tid, wm, wn, n0, mloc0,
+                                                HWr, zpre, bpar);
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
   }
   wait_vm<0>();
-  if (stamp) stamp[3] = wall_clock64();
-  if (dbg & 8) {
-    if (stamp) stamp[4] = wall_clock64();
-    if (acc[0][0][0] == 12345.f) reinterpret_cast<float*>(a.dst)[0] = 1.f;      // keep the accumulators live
-    return;
-  }
-  if (a.splits > 1) {             // raw fp32 partials; conv_igemm.hip's finish applies the epilogue
-    float* slab = a.slab + (size_t)blockIdx.z * a.m_total * a.Npad;
-#pragma unroll
-    for (int i = 0; i < TM; ++i)
-#pragma unroll
-      for (int j = 0; j < TN; ++j)
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const int rr = m0 + wm * WM + i * 16 + lg * 4 + e;
-          const int c = n0 + wn * WN + j * 16 + lr;
-          slab[(size_t)rr * a.Npad + c] = acc[i][j][e];
-        }
-    return;
-  }
-  if (DBG && (dbg & 256)) {       // (the stamps live in dst: the epilogue stores to a scratch copy)
-    ConvArgs b = a;
-    b.dst = a.slab;
-    conv_l_epilogue<BN, WGM, TM, TN, NT, BSUM>(b, S, acc, lds, tid, wm, wn, n0, mloc0, HWr, zpre, bpar);
-    if (stamp) stamp[4] = wall_clock64();
-    return;
-  }
-  conv_l_epilogue<BN, WGM, TM, TN, NT, BSUM>(a, S, acc, lds, tid, wm, wn, n0, mloc0, HWr, zpre, bpar);
 }
 
 }  // namespace
@@ -370,25 +399,14 @@ int cvl_conv_igemm_h(const cvl_conv_desc* d, const ConvArgs& a0, hipStream_t s, 
   } else {
     a.splits = 1;
   }
-  dim3 grid(tiles, 1, a.splits);
+  // persistent: one workgroup per CU walks a contiguous chunk of tiles (split launches: one tile
+  // per workgroup, the K splits on blockIdx.z)
+  static const int ncu = cvl_device_cus();
+  const int per_cu = cvl_env_int("CVL_CONV_H_WG_PER_CU", 1);
+  const int wgs = a.splits > 1 ? tiles : (tiles < ncu * per_cu ? tiles : ncu * per_cu);
+  dim3 grid(wgs, 1, a.splits);
   g_cvl_conv_last_kernel = CVL_CK_H64;
-  a.dbg = cvl_env_int("CVL_X_ABLATE", 0);
-  if ((a.dbg & 256) && a.splits <= 1) {   // stamps: the epilogue writes a scratch image instead of dst
-    static void* scratch = nullptr;
-    static size_t scratch_bytes = 0;
-    const size_t need = (size_t)a.m_total * a.ld_dst * (a.dst_f32 ? 4 : 2) + 4096;
-    if (scratch_bytes < need) {
-      if (scratch) (void)hipFree(scratch);
-      if (hipMalloc(&scratch, need) != hipSuccess) return CVL_EHIP;
-      scratch_bytes = need;
-    }
-    a.slab = reinterpret_cast<float*>(scratch);
-  }
-  if (a.dbg) {
-    if (dg && a.bsum) hipLaunchKernelGGL((conv_igemm_h_kernel<true, true, true>), grid, dim3(NT), 0, s, a);
-    else if (dg) hipLaunchKernelGGL((conv_igemm_h_kernel<true, false, true>), grid, dim3(NT), 0, s, a);
-    else hipLaunchKernelGGL((conv_igemm_h_kernel<false, false, true>), grid, dim3(NT), 0, s, a);
-  } else if (dg && a.bsum) hipLaunchKernelGGL((conv_igemm_h_kernel<true, true>), grid, dim3(NT), 0, s, a);
+  if (dg && a.bsum) hipLaunchKernelGGL((conv_igemm_h_kernel<true, true>), grid, dim3(NT), 0, s, a);
   else if (dg) hipLaunchKernelGGL((conv_igemm_h_kernel<true, false>), grid, dim3(NT), 0, s, a);
   else hipLaunchKernelGGL((conv_igemm_h_kernel<false, false>), grid, dim3(NT), 0, s, a);
   int st = cvl_launch_status();

@@ -28,6 +28,16 @@ static inline int cvl_env_int(const char* name, int dflt) {
   return (v && v[0]) ? atoi(v) : dflt;
 }
 
+// compute units of the current device (persistent kernels size their grids by it; one process
+// drives one GPU, so the first query is cached)
+static inline int cvl_device_cus() {
+  int dev = 0, n = 0;
+  if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+      n <= 0)
+    return 256;
+  return n;
+}
+
 // ---- bf16 helpers (bit-level; round-to-nearest-even, NaN-preserving) ------------------------
 typedef uint16_t cvl_bf16;
 

@@ -59,15 +59,15 @@ def nms(bboxes, iou_threshold, sigma=0.3, method="nms"):
 
 def build_model(n_classes, tmp_pi=0.99, n_filters=128, n_stacks=1, n_repeats=2, seperable=True, batch_norm=True,
                 norm_order="norm_first"):
-    """tf_centernet_hourglass.py:163-353 -> cvlite HourglassNet (callable: model(x) -> [B,H/4,W/4,4+C])."""
+    """tf_centernet_hourglass.py:163-353 -> cvlite HourglassNet (callable: model(x) -> [B,H/4,W/4,4+C]),
+    every build option of the reference: stacked hourglasses, Conv2D instead of SeparableConv2D,
+    no BatchNormalization, norm_last."""
     from .hourglass_net import HourglassNet
-    if not (seperable and batch_norm and norm_order == "norm_first"):
-        raise NotImplementedError("the MI355X path builds the reference default (seperable=True, batch_norm=True, "
-                                  "norm_order='norm_first')")
-    if n_stacks != 1:
-        raise NotImplementedError("n_stacks > 1 backward wiring is not built (reference default is 1)")
+    if norm_order not in ("norm_first", "norm_last"):
+        raise ValueError("norm_order must be 'norm_first' or 'norm_last'")
     _lib.require_cuda()
-    return HourglassNet(n_classes, tmp_pi=tmp_pi, n_filters=n_filters, n_stacks=n_stacks, n_repeats=n_repeats)
+    return HourglassNet(n_classes, tmp_pi=tmp_pi, n_filters=n_filters, n_stacks=n_stacks, n_repeats=n_repeats,
+                        seperable=seperable, batch_norm=batch_norm, norm_order=norm_order)
 
 
 def train_step(voc_model, sub_batch_sz, images, bboxes, optimizer, cls_lambda=2.5, reg_lambda=1.0,

@@ -1,6 +1,10 @@
-"""CenterNet hourglass (CenterNet/tf_centernet_hourglass.py:87-353, defaults n_filters=128,
-n_stacks=1, n_repeats=2, seperable=True, batch_norm=True, norm_order="norm_first") as an explicit
-forward/backward graph on the cvlite MFMA conv and HIP memory-bound kernels.
+"""CenterNet hourglass (CenterNet/tf_centernet_hourglass.py:87-353: build_model(n_classes, tmp_pi,
+n_filters, n_stacks, n_repeats, seperable, batch_norm, norm_order); the reference defaults are
+n_filters=128, n_stacks=1, n_repeats=2, seperable=True, batch_norm=True, norm_order="norm_first")
+as an explicit forward/backward graph on the cvlite MFMA conv and HIP memory-bound kernels.
+Every build option is supported: stacked hourglasses (the output of stack s is the input of
+stack s + 1), Conv2D instead of SeparableConv2D (seperable=False), no BatchNormalization, and
+norm_last (BN on each repeat's 2nf-channel output, before its ReLU).
 
 MI355X mapping:
   * every SeparableConv2D (depthwise D, no bias; pointwise P + bias) runs as ONE dense conv on the
@@ -32,18 +36,25 @@ BN_EPS = 1e-3          # Keras BatchNormalization default (the hourglass passes 
 BN_MOMENTUM = 0.99
 
 
+def skey(s, name):
+    """Key of a per-stack tensor (stack s, 1-based) in the forward / backward value maps."""
+    return "%d:%s" % (s, name)
+
+
 def block_graph(n_stacks=1):
-    """(name, input, output) of every cnn_block in graph order (tf_centernet_hourglass.py:189-333)."""
+    """(name, input, output) of every cnn_block in graph order (tf_centernet_hourglass.py:189-333);
+    the tensors of stack s are keyed skey(s, ...)."""
     out = [("cnn_block_1", "blk0", "cnn1")]
-    for s in range(n_stacks):
-        st = "stack_%d_" % (s + 1)
-        out += [(st + "enc_block_1", "stack_in", "enc1"), (st + "enc_block_2", "e1", "enc2"),
-                (st + "enc_block_3", "e2", "enc3"), (st + "enc_block_4a", "e3", "enc4a"),
-                (st + "enc_block_4b", "enc4a", "enc4b"), (st + "enc_block_4", "enc4b", "enc4"),
-                (st + "dec_block_1", "e3", "dec1"), (st + "dec_out_1", "d1res", "o1"),
-                (st + "dec_block_2", "e2", "dec2"), (st + "dec_out_2", "d2res", "o2"),
-                (st + "dec_block_3", "e1", "dec3"), (st + "dec_out_3", "d3res", "o3"),
-                (st + "dec_block_4", "stack_in", "dec4"), (st + "dec_out_4", "d4res", "o4")]
+    for s in range(1, n_stacks + 1):
+        st = "stack_%d_" % s
+        k = lambda n: skey(s, n)   # noqa: E731
+        out += [(st + "enc_block_1", k("stack_in"), k("enc1")), (st + "enc_block_2", k("e1"), k("enc2")),
+                (st + "enc_block_3", k("e2"), k("enc3")), (st + "enc_block_4a", k("e3"), k("enc4a")),
+                (st + "enc_block_4b", k("enc4a"), k("enc4b")), (st + "enc_block_4", k("enc4b"), k("enc4")),
+                (st + "dec_block_1", k("e3"), k("dec1")), (st + "dec_out_1", k("d1res"), k("o1")),
+                (st + "dec_block_2", k("e2"), k("dec2")), (st + "dec_out_2", k("d2res"), k("o2")),
+                (st + "dec_block_3", k("e1"), k("dec3")), (st + "dec_out_3", k("d3res"), k("o3")),
+                (st + "dec_block_4", k("stack_in"), k("dec4")), (st + "dec_out_4", k("d4res"), k("o4"))]
     return out
 
 
@@ -160,12 +171,61 @@ class SepConv(object):
         return self.conv.dgrad(dy, B, H, W, out=out, beta=beta)
 
 
-class Stem(object):
-    """cnn_block_0: SeparableConv2D(n_filters, 7x7, stride 2, "same") on the 3-channel image as
-    im2col (TF-same pads) + one K=160 GEMM with the folded kernel [7][7][3][nf]."""
+class DenseConv(object):
+    """Keras Conv2D(cout, k, stride, "same") with bias (build_model(seperable=False), :124-136,
+    :174-182) behind SepConv's interface: the trainable HWIO kernel is packed directly."""
+    split = False
+    can_split = False
 
-    def __init__(self, store, eff, nf):
-        self.sep = SepConv(store, eff, "cnn_block_0", STEM_K, 3, nf, stride=2, cin_k=STEM_KP, dgrad=False)
+    def __init__(self, store, name, k, cin, cout, stride=1, cin_k=None, dgrad=True):
+        self.name, self.k, self.cin, self.cout = name, k, cin, cout
+        self.conv = Conv(store, name, k, cin, cout, stride, "same", bias=True, cin_k=cin_k, dgrad=dgrad)
+        self.store = store
+        self.on_mode_change = None
+        self.bias_sink = None
+
+    @property
+    def b(self):
+        return self.conv.b
+
+    @property
+    def db(self):
+        return self.conv.db
+
+    def fwd(self, x, B, H, W, relu_out=False):
+        c = self.conv
+        Ho, Wo, _, _ = c.out_hw(H, W)
+        out = torch.empty((B, Ho, Wo, self.cout), dtype=BF16, device=x.device)
+        d = c.fwd_desc(B, [nn.seg(Ho, Wo, H, W, c.wf, self.b)], ld_dst=self.cout, relu_out=relu_out)
+        nn.conv_igemm(d, x, out)
+        return out
+
+    def wgrad(self, x, dy, B, H, W):
+        self.conv.wgrad(x, dy, B, H, W, bias=False)
+        HW = H * W
+        item = (dy, int(dy.shape[-1]), 0, self.cout, 0, HW, HW, B, self.db, 0.0)
+        if self.bias_sink is not None:
+            self.bias_sink.append(item)
+        else:
+            nn.bias_grad(*item[:9])
+
+    def dgrad(self, dy, B, H, W, out=None, beta=0.0):
+        return self.conv.dgrad(dy, B, H, W, out=out, beta=beta)
+
+
+def make_conv(seperable, store, eff, name, k, cin, cout, stride=1, cin_k=None, dgrad=True):
+    if seperable:
+        return SepConv(store, eff, name, k, cin, cout, stride=stride, cin_k=cin_k, dgrad=dgrad)
+    return DenseConv(store, name, k, cin, cout, stride=stride, cin_k=cin_k, dgrad=dgrad)
+
+
+class Stem(object):
+    """cnn_block_0: SeparableConv2D (or Conv2D) (n_filters, 7x7, stride 2, "same") on the 3-channel
+    image as im2col (TF-same pads) + one K=160 GEMM with the (folded) kernel [7][7][3][nf]."""
+
+    def __init__(self, store, eff, nf, seperable=True):
+        self.sep = make_conv(seperable, store, eff, "cnn_block_0", STEM_K, 3, nf, stride=2, cin_k=STEM_KP,
+                             dgrad=False)
         self.nf = nf
 
     def pack_entry(self):
@@ -198,71 +258,104 @@ class Stem(object):
 
 
 class Repeat(object):
-    """One cnn_block repeat: BN -> sep 1x1 (nf) -> sep 3x3 (nf) -> sep 1x1 (2nf) -> ReLU (+ BN out)."""
+    """One cnn_block repeat (tf_centernet_hourglass.py:96-155): norm_first: BN -> conv 1x1 (nf) ->
+    conv 3x3 (nf) -> conv 1x1 (2nf) -> ReLU, residual (r >= 1) adds the BN OUTPUT (the input is
+    rebound to it); norm_last: conv 1x1 -> 3x3 -> 1x1 -> BN -> ReLU, residual adds the input;
+    batch_norm=False drops the BN; the convs are SeparableConv2D or Conv2D (seperable)."""
 
-    def __init__(self, store, eff, blk, r, cin, nf):
+    def __init__(self, store, eff, blk, r, cin, nf, seperable=True, batch_norm=True, norm_order="norm_first"):
+        if norm_order not in ("norm_first", "norm_last"):
+            raise ValueError("norm_order must be 'norm_first' or 'norm_last'")
         self.r = r
-        self.bn = BatchNorm(store, "%s_bn_%d" % (blk, r), cin, eps=BN_EPS, momentum=BN_MOMENTUM)
-        self.bot = SepConv(store, eff, "%s_bot_%d" % (blk, r), 1, cin, nf)
-        self.cnn = SepConv(store, eff, "%s_cnn_%d" % (blk, r), 3, nf, nf)
-        self.out = SepConv(store, eff, "%s_out_%d" % (blk, r), 1, nf, 2 * nf)
+        self.norm_first = norm_order == "norm_first"
+        self.bn = (BatchNorm(store, "%s_bn_%d" % (blk, r), cin if self.norm_first else 2 * nf, eps=BN_EPS,
+                             momentum=BN_MOMENTUM) if batch_norm else None)
+        self.bot = make_conv(seperable, store, eff, "%s_bot_%d" % (blk, r), 1, cin, nf)
+        self.cnn = make_conv(seperable, store, eff, "%s_cnn_%d" % (blk, r), 3, nf, nf)
+        self.out = make_conv(seperable, store, eff, "%s_out_%d" % (blk, r), 1, nf, 2 * nf)
         self.cin, self.cout = cin, 2 * nf
 
     def seps(self):
         return [self.bot, self.cnn, self.out]
 
-    def forward(self, t, B, H, W, group, train=True):
-        c, HW = self.cin, H * W
-        dev = t.device
-        bn = self.bn
-        mr = torch.empty((B, c, 2), dtype=torch.float32, device=dev)
+    def _bn(self, t, B, HW, group, train, relu):
+        c, bn = self.bn.c, self.bn
+        mr = torch.empty((B, c, 2), dtype=torch.float32, device=t.device)
         if train:
-            stats = torch.empty((B, c, 2), dtype=torch.float64, device=dev)
+            stats = torch.empty((B, c, 2), dtype=torch.float64, device=t.device)
             nn.bn_stats(t, B, HW, c, stats)
             nn.bn_finalize_grouped(stats, mr, bn.run_mean, bn.run_var, B, c, HW, group, bn.eps, bn.momentum)
         else:                                     # Keras inference: moving statistics
             mr[:, :, 0] = bn.run_mean
             mr[:, :, 1] = torch.rsqrt(bn.run_var + bn.eps)
         a = torch.empty_like(t)
-        nn.bn_apply(t, mr, bn.gamma, bn.beta, None, a, B, HW, c, False)
+        nn.bn_apply(t, mr, bn.gamma, bn.beta, None, a, B, HW, c, relu)
+        return a, mr
+
+    def forward(self, t, B, H, W, group, train=True):
+        HW = H * W
+        mr = z = None
+        a = t
+        if self.bn is not None and self.norm_first:
+            a, mr = self._bn(t, B, HW, group, train, False)
         u = self.bot.fwd(a, B, H, W)
         v = self.cnn.fwd(u, B, H, W)
-        y = self.out.fwd(v, B, H, W, relu_out=True)
+        if self.bn is not None and not self.norm_first:
+            z = self.out.fwd(v, B, H, W)
+            y, mr = self._bn(z, B, HW, group, train, True)
+        else:
+            y = self.out.fwd(v, B, H, W, relu_out=True)
         if self.r == 0:
             o = y
         else:
             o = torch.empty_like(y)
             nn.add(y, a, o)
-        return o, (t, mr, a, u, v, y, B, H, W, group)
+        return o, (t, mr, a, u, v, z, y, B, H, W, group)
 
     def backward(self, dout, saved, dx_out, dx_beta=0.0):
-        """dout: grad of this repeat's output (clobbered when r >= 1: it becomes the BN-output
-        gradient); writes / accumulates (dx_beta) the grad of its input into dx_out."""
-        t, mr, a, u, v, y, B, H, W, group = saved
-        st = self.bn.store
+        """dout: grad of this repeat's output (clobbered when r >= 1: it becomes the residual
+        addend's gradient); writes / accumulates (dx_beta) the grad of its input into dx_out."""
+        t, mr, a, u, v, z, y, B, H, W, group = saved
+        st = self.store_of()
         dz3 = torch.empty_like(y)
-        nn.relu_backward(dout, y, dz3)
+        if z is not None:                          # norm_last: ReLU -> BN backward onto the conv output
+            nn.bn_backward_grouped(dout, z, mr, self.bn.gamma, dz3, st.g(self.bn.gname), st.g(self.bn.bname),
+                                   B, H * W, self.cout, group, y_relu=y)
+        else:
+            nn.relu_backward(dout, y, dz3)
         self.out.wgrad(v, dz3, B, H, W)
         dv = self.out.dgrad(dz3, B, H, W)
         self.cnn.wgrad(u, dv, B, H, W)
         du = self.cnn.dgrad(dv, B, H, W)
         self.bot.wgrad(a, du, B, H, W)
-        if self.r == 0:
-            da = self.bot.dgrad(du, B, H, W)
-        else:
-            da = self.bot.dgrad(du, B, H, W, out=dout, beta=1.0)     # + residual branch (BN output)
-        nn.bn_backward_grouped(da, t, mr, self.bn.gamma, dx_out, st.g(self.bn.gname), st.g(self.bn.bname),
-                               B, H * W, self.cin, group, dz_beta=dx_beta)
+        if self.bn is not None and self.norm_first:
+            if self.r == 0:
+                da = self.bot.dgrad(du, B, H, W)
+            else:
+                da = self.bot.dgrad(du, B, H, W, out=dout, beta=1.0)     # + residual branch (BN output)
+            nn.bn_backward_grouped(da, t, mr, self.bn.gamma, dx_out, st.g(self.bn.gname), st.g(self.bn.bname),
+                                   B, H * W, self.cin, group, dz_beta=dx_beta)
+        elif self.r == 0:
+            self.bot.dgrad(du, B, H, W, out=dx_out, beta=dx_beta)
+        else:                                     # residual adds the input itself
+            da = self.bot.dgrad(du, B, H, W, out=dout, beta=1.0)
+            if dx_beta:
+                nn.add(dx_out, da, dx_out)
+            else:
+                dx_out.copy_(da)
         return dx_out
+
+    def store_of(self):
+        return self.bot.store
 
 
 class CnnBlock(object):
-    def __init__(self, store, eff, name, cin, nf, n_repeats):
+    def __init__(self, store, eff, name, cin, nf, n_repeats, **opts):
         self.name = name
         self.reps = []
         c = cin
         for r in range(n_repeats):
-            self.reps.append(Repeat(store, eff, name, r, c, nf))
+            self.reps.append(Repeat(store, eff, name, r, c, nf, **opts))
             c = 2 * nf
         self.cout = c
 
@@ -270,7 +363,7 @@ class CnnBlock(object):
         return [s for r in self.reps for s in r.seps()]
 
     def bns(self):
-        return [r.bn for r in self.reps]
+        return [r.bn for r in self.reps if r.bn is not None]
 
     def forward(self, x, B, H, W, group, train=True):
         h, saved = x, []
@@ -293,13 +386,15 @@ class HourglassNet(object):
     """tf_centernet_hourglass.build_model(n_classes, tmp_pi, n_filters, n_stacks, n_repeats) on
     MI355X.  forward(x [B,H,W,3] fp32) -> [B,H/4,W/4,4+C] fp32; backward(d_out bf16)."""
 
-    def __init__(self, n_classes, tmp_pi=0.99, n_filters=128, n_stacks=1, n_repeats=2, device="cuda", seed=0):
+    def __init__(self, n_classes, tmp_pi=0.99, n_filters=128, n_stacks=1, n_repeats=2, device="cuda", seed=0,
+                 seperable=True, batch_norm=True, norm_order="norm_first"):
         self.C = n_classes
         self.nf = n_filters
         self.n_stacks = n_stacks
         self.device = torch.device(device)
         store, eff = ParamStore(), ParamStore()
-        self._build(store, eff, n_classes, tmp_pi, n_filters, n_stacks, n_repeats)
+        self._build(store, eff, n_classes, tmp_pi, n_filters, n_stacks, n_repeats,
+                    dict(seperable=seperable, batch_norm=batch_norm, norm_order=norm_order))
         store.finalize(self.device, seed)
         eff.finalize(self.device, seed + 1)
         self.store, self.eff = store, eff
@@ -313,11 +408,12 @@ class HourglassNet(object):
         self._plan = None
         self.pack()
 
-    def _build(self, store, eff, C, tmp_pi, nf, n_stacks, n_repeats):
-        self.stem = Stem(store, eff, nf)
+    def _build(self, store, eff, C, tmp_pi, nf, n_stacks, n_repeats, opts=None):
+        opts = opts or {}
+        self.stem = Stem(store, eff, nf, opts.get("seperable", True))
         self.blocks = {}
         for name, i, o in block_graph(n_stacks):       # only cnn_block_1 sees the stem's nf channels
-            self.blocks[name] = CnnBlock(store, eff, name, nf if i == "blk0" else 2 * nf, nf, n_repeats)
+            self.blocks[name] = CnnBlock(store, eff, name, nf if i == "blk0" else 2 * nf, nf, n_repeats, **opts)
         self.cnn_out = Conv(store, "cnn_out", 3, 2 * nf, 4 + C, bias=True)
         self.bfocal = store.add("b_focal", (1,), constant(math.log((1.0 - tmp_pi) / tmp_pi)))
 
@@ -335,8 +431,8 @@ class HourglassNet(object):
         seps = self.seps()
         entries = [self.stem.pack_entry()] + [(s.pw if s.split else s.conv).pack_entry() for s in seps[1:]]
         entries.append(self.cnn_out.pack_entry())
-        self._plan = (nn.SepPlan([s.sep_entry() for s in seps if not s.split], self.device),
-                      nn.PackPlan(entries, self.device))
+        folds = [s.sep_entry() for s in seps if isinstance(s, SepConv) and not s.split]
+        self._plan = (nn.SepPlan(folds, self.device) if folds else None, nn.PackPlan(entries, self.device))
 
     def _mode_changed(self):
         self._plan = None
@@ -346,12 +442,14 @@ class HourglassNet(object):
         if self._plan is None:
             self._make_plan()
         sep, pk = self._plan
-        sep.fold()
+        if sep is not None:
+            sep.fold()
         pk.run()
         nn.bias_scalar_fold(self.cnn_out.b, self.store.p(self.bfocal), self.b_eff, 4)
 
     def unfold_grads(self):
-        self._plan[0].unfold()
+        if self._plan[0] is not None:
+            self._plan[0].unfold()
 
     def grad_groups(self):
         """One group: the separable-conv unfold finalises every gradient at the end of backward
@@ -408,20 +506,22 @@ class HourglassNet(object):
 
         self._graph = dict((b[0], b) for b in block_graph(self.n_stacks))
         run("cnn_block_1")
-        pool("cnn1", "stack_in")
-        for s in range(self.n_stacks):
-            st = "stack_%d_" % (s + 1)
-            run(st + "enc_block_1"); res_add("stack_in", "enc1", "e1res"); pool("e1res", "e1")   # noqa: E702
-            run(st + "enc_block_2"); res_add("e1", "enc2", "e2res"); pool("e2res", "e2")         # noqa: E702
-            run(st + "enc_block_3"); res_add("e2", "enc3", "e3res"); pool("e3res", "e3")         # noqa: E702
-            run(st + "enc_block_4a"); run(st + "enc_block_4b"); run(st + "enc_block_4")          # noqa: E702
-            res_add("e3", "enc4", "e4res"); pool("e4res", "e4")                                   # noqa: E702
-            run(st + "dec_block_1"); up_add("e4", "dec1", "d1res"); run(st + "dec_out_1")         # noqa: E702
-            run(st + "dec_block_2"); up_add("o1", "dec2", "d2res"); run(st + "dec_out_2")         # noqa: E702
-            run(st + "dec_block_3"); up_add("o2", "dec3", "d3res"); run(st + "dec_out_3")         # noqa: E702
-            run(st + "dec_block_4"); up_add("o3", "dec4", "d4res"); run(st + "dec_out_4")         # noqa: E702
-            if s + 1 < self.n_stacks:
-                v["stack_in"], hw["stack_in"] = v["o4"], hw["o4"]
+        pool("cnn1", skey(1, "stack_in"))
+        for s in range(1, self.n_stacks + 1):
+            st = "stack_%d_" % s
+            k = lambda n: skey(s, n)   # noqa: E731
+            run(st + "enc_block_1"); res_add(k("stack_in"), k("enc1"), k("e1res")); pool(k("e1res"), k("e1"))  # noqa: E702
+            run(st + "enc_block_2"); res_add(k("e1"), k("enc2"), k("e2res")); pool(k("e2res"), k("e2"))        # noqa: E702
+            run(st + "enc_block_3"); res_add(k("e2"), k("enc3"), k("e3res")); pool(k("e3res"), k("e3"))        # noqa: E702
+            run(st + "enc_block_4a"); run(st + "enc_block_4b"); run(st + "enc_block_4")                         # noqa: E702
+            res_add(k("e3"), k("enc4"), k("e4res")); pool(k("e4res"), k("e4"))                                  # noqa: E702
+            run(st + "dec_block_1"); up_add(k("e4"), k("dec1"), k("d1res")); run(st + "dec_out_1")             # noqa: E702
+            run(st + "dec_block_2"); up_add(k("o1"), k("dec2"), k("d2res")); run(st + "dec_out_2")             # noqa: E702
+            run(st + "dec_block_3"); up_add(k("o2"), k("dec3"), k("d3res")); run(st + "dec_out_3")             # noqa: E702
+            run(st + "dec_block_4"); up_add(k("o3"), k("dec4"), k("d4res")); run(st + "dec_out_4")             # noqa: E702
+            if s < self.n_stacks:         # the stack's output is the next stack's input
+                v[skey(s + 1, "stack_in")], hw[skey(s + 1, "stack_in")] = v[k("o4")], hw[k("o4")]
+        v["o4"], hw["o4"] = v[skey(self.n_stacks, "o4")], hw[skey(self.n_stacks, "o4")]
         Ho, Wo = hw["o4"]
         c = self.cnn_out
         out = torch.empty((B, Ho, Wo, 4 + self.C), dtype=torch.float32, device=dev)
@@ -435,21 +535,19 @@ class HourglassNet(object):
     def backward(self, d_out, hook=None):
         """d_out: bf16 [B,Ho,Wo,cout_ld] gradient of the output (cvl_centernet_loss).  Writes every
         parameter gradient of the store (overwrite semantics)."""
-        assert self.n_stacks == 1, "backward wiring is written for one stack (the reference default)"
         sv_stem, saved, v, hw, B, group = self._saved
-        st = "stack_1_"
         c = self.cnn_out
         Ho, Wo = hw["o4"]
         HW = Ho * Wo
-        # the separable convs' bias gradients (column sums of their output gradients) are collected
-        # and run as batched cvl_bias_grad_multi launches (16 per launch pair) at the end, instead
-        # of two launches per conv (91 convs)
+        # the convs' bias gradients (column sums of their output gradients) are collected and run as
+        # batched cvl_bias_grad_multi launches (16 per launch pair) at the end, instead of two
+        # launches per conv (91 convs per stack)
         sink = [(d_out, int(d_out.shape[-1]), 0, 4 + self.C, 0, HW, HW, B, self.g_beff, 0.0)]
         for sc in self.seps()[1:]:
             sc.bias_sink = sink
         c.wgrad(v["o4"], d_out, B, Ho, Wo, bias=False)
         g = {}
-        g["o4"] = c.dgrad(d_out, B, Ho, Wo)
+        g[skey(self.n_stacks, "o4")] = c.dgrad(d_out, B, Ho, Wo)
 
         def blk(name, dy, dx_key, beta):
             _, i, _ = self._graph[name]
@@ -474,35 +572,40 @@ class HourglassNet(object):
             else:
                 g[dst] = g[src].clone()
 
-        # decoder, last merge first: dX_res feeds both the dec block and the up-sampled input
-        blk(st + "dec_out_4", g["o4"], "d4res", 0.0)
-        upb("d4res", "o3")
-        blk(st + "dec_block_4", g["d4res"], "stack_in", 0.0)
-        blk(st + "dec_out_3", g["o3"], "d3res", 0.0)
-        upb("d3res", "o2")
-        blk(st + "dec_block_3", g["d3res"], "e1", 0.0)
-        blk(st + "dec_out_2", g["o2"], "d2res", 0.0)
-        upb("d2res", "o1")
-        blk(st + "dec_block_2", g["d2res"], "e2", 0.0)
-        blk(st + "dec_out_1", g["o1"], "d1res", 0.0)
-        upb("d1res", "e4")
-        blk(st + "dec_block_1", g["d1res"], "e3", 0.0)
-        # encoder: x_res = x + cnn(x) -> pool
-        unpool("e4", "e4res")
-        acc("e3", "e4res")
-        blk(st + "enc_block_4", g["e4res"], "enc4b", 0.0)
-        blk(st + "enc_block_4b", g["enc4b"], "enc4a", 0.0)
-        blk(st + "enc_block_4a", g["enc4a"], "e3", 1.0)
-        unpool("e3", "e3res")
-        acc("e2", "e3res")
-        blk(st + "enc_block_3", g["e3res"], "e2", 1.0)
-        unpool("e2", "e2res")
-        acc("e1", "e2res")
-        blk(st + "enc_block_2", g["e2res"], "e1", 1.0)
-        unpool("e1", "e1res")
-        acc("stack_in", "e1res")
-        blk(st + "enc_block_1", g["e1res"], "stack_in", 1.0)
-        unpool("stack_in", "cnn1")
+        for s in range(self.n_stacks, 0, -1):
+            st = "stack_%d_" % s
+            k = lambda n: skey(s, n)   # noqa: E731
+            # decoder, last merge first: dX_res feeds both the dec block and the up-sampled input
+            blk(st + "dec_out_4", g[k("o4")], k("d4res"), 0.0)
+            upb(k("d4res"), k("o3"))
+            blk(st + "dec_block_4", g[k("d4res")], k("stack_in"), 0.0)
+            blk(st + "dec_out_3", g[k("o3")], k("d3res"), 0.0)
+            upb(k("d3res"), k("o2"))
+            blk(st + "dec_block_3", g[k("d3res")], k("e1"), 0.0)
+            blk(st + "dec_out_2", g[k("o2")], k("d2res"), 0.0)
+            upb(k("d2res"), k("o1"))
+            blk(st + "dec_block_2", g[k("d2res")], k("e2"), 0.0)
+            blk(st + "dec_out_1", g[k("o1")], k("d1res"), 0.0)
+            upb(k("d1res"), k("e4"))
+            blk(st + "dec_block_1", g[k("d1res")], k("e3"), 0.0)
+            # encoder: x_res = x + cnn(x) -> pool
+            unpool(k("e4"), k("e4res"))
+            acc(k("e3"), k("e4res"))
+            blk(st + "enc_block_4", g[k("e4res")], k("enc4b"), 0.0)
+            blk(st + "enc_block_4b", g[k("enc4b")], k("enc4a"), 0.0)
+            blk(st + "enc_block_4a", g[k("enc4a")], k("e3"), 1.0)
+            unpool(k("e3"), k("e3res"))
+            acc(k("e2"), k("e3res"))
+            blk(st + "enc_block_3", g[k("e3res")], k("e2"), 1.0)
+            unpool(k("e2"), k("e2res"))
+            acc(k("e1"), k("e2res"))
+            blk(st + "enc_block_2", g[k("e2res")], k("e1"), 1.0)
+            unpool(k("e1"), k("e1res"))
+            acc(k("stack_in"), k("e1res"))
+            blk(st + "enc_block_1", g[k("e1res")], k("stack_in"), 1.0)
+            if s > 1:                         # this stack's input is the previous stack's output
+                g[skey(s - 1, "o4")] = g[k("stack_in")]
+        unpool(skey(1, "stack_in"), "cnn1")
         blk("cnn_block_1", g["cnn1"], "blk0", 0.0)
         self.stem.backward(g["blk0"], sv_stem)
         for sc in self.seps()[1:]:
@@ -521,6 +624,8 @@ class HourglassNet(object):
         net.C = n_classes
         store, eff = ParamStore(), ParamStore()
         net._build(store, eff, n_classes, kw.get("tmp_pi", 0.99), kw.get("n_filters", 128),
-                   kw.get("n_stacks", 1), kw.get("n_repeats", 2))
+                   kw.get("n_stacks", 1), kw.get("n_repeats", 2),
+                   dict(seperable=kw.get("seperable", True), batch_norm=kw.get("batch_norm", True),
+                        norm_order=kw.get("norm_order", "norm_first")))
         store.finalize("cpu", seed)
         return {k: store.p(k).clone() for k in store.offsets}

@@ -1,6 +1,8 @@
 """CenterNet v2 — the network CenterNet/train_hourglass_voc.py trains (tf_hourglass_net.build_model,
 :115-394, with the script's n_filters=12, n_features=64, n_repeats=2, separable, norm_first BN) —
-as an explicit forward / backward graph on the cvlite kernels.
+as an explicit forward / backward graph on the cvlite kernels.  The other build options are
+supported too: Conv2D instead of SeparableConv2D (seperable=False), no BatchNormalization, and
+norm_last (BN on each conv's output, before its ReLU: cnn_block :47-77, downsample_block :79-113).
 
 Graph (nf = n_filters): a 3x3 separable conv on the image (no BN / ReLU), cnn_block_1 (nf), six
 [downsample (BN -> separable 3x3/2 -> ReLU) + cnn_block + residual] encoder stages to 64 nf at
@@ -94,18 +96,56 @@ class SepConvP(object):
         return self.conv.dgrad(dy, B, H, W, out=out, beta=beta)
 
 
+def padded_glorot(k, cin, cout, cpi, cpo):
+    """Glorot-uniform over the real [k,k,cin,cout] block of a channel-padded kernel, zero pads."""
+    lim = math.sqrt(6.0 / (k * k * cin + k * k * cout))
+
+    def init(gen, shape):
+        w = torch.zeros(shape, dtype=torch.float32)
+        w[:, :, :cin, :cout] = (torch.rand((k, k, cin, cout), generator=gen, dtype=torch.float64) * 2 - 1).mul_(lim).float()
+        return w
+    return init
+
+
+class DenseConvP(SepConvP):
+    """Keras Conv2D(cout, k, stride, "same") with bias (seperable=False) on channel-padded maps: the
+    trainable kernel is kept at its padded shape [k][k][cp(cin)][cp(cout)] (zero pads, which get
+    zero gradients), the bias padded to cp(cout) like every v2 per-channel parameter."""
+
+    def __init__(self, store, name, k, cin, cout, stride=1):
+        self.name, self.k, self.cin, self.cout, self.stride = name, k, cin, cout, stride
+        self.cpi, self.cpo = cp(cin), cp(cout)
+        self.conv = Conv(store, name, k, self.cpi, self.cpo, stride, "same", bias=False,
+                         w_init=padded_glorot(k, cin, cout, self.cpi, self.cpo))
+        self.bname = store.add(name + "/bias", (self.cpo,), constant(0.0))
+        self.store = store
+
+    def sep_entry(self):
+        raise TypeError("a Conv2D has no separable fold")
+
+
+def conv_p(seperable, store, eff, name, k, cin, cout, stride=1):
+    if seperable:
+        return SepConvP(store, eff, name, k, cin, cout, stride=stride)
+    return DenseConvP(store, name, k, cin, cout, stride=stride)
+
+
 class StemV2(object):
     """cnn_block_0 (:131-140): SeparableConv2D(nf, 3x3, "same") on the 3-channel image as im2col
     (K = 27 -> 32) + one GEMM with the folded kernel [3][3][3][nf]; output pitch cp(nf)."""
 
-    def __init__(self, store, eff, nf):
+    def __init__(self, store, eff, nf, seperable=True):
         self.nf, self.cpo = nf, cp(nf)
+        self.seperable = seperable
         name = "cnn_block_0"
-        self.dwname = store.add(name + "/depthwise_kernel", (3, 3, 3, 1), glorot_uniform(27, 9))
-        self.pwname = store.add(name + "/pointwise_kernel", (1, 1, 3, nf), glorot_uniform(3, nf))
+        if seperable:
+            self.dwname = store.add(name + "/depthwise_kernel", (3, 3, 3, 1), glorot_uniform(27, 9))
+            self.pwname = store.add(name + "/pointwise_kernel", (1, 1, 3, nf), glorot_uniform(3, nf))
         self.bname = store.add(name + "/bias", (self.cpo,), constant(0.0))
         self.store = store
-        self.conv = Conv(eff, name, 3, 3, nf, 1, "same", bias=False, cin_k=STEM_KP, npad=self.cpo, dgrad=False)
+        # separable: the folded kernel in the eff store; Conv2D: the trainable kernel itself
+        self.conv = Conv(eff if seperable else store, name, 3, 3, nf, 1, "same", bias=False, cin_k=STEM_KP,
+                         npad=self.cpo, dgrad=False)
 
     def sep_entry(self):
         st = self.store
@@ -139,7 +179,7 @@ class StemV2(object):
         nn.bias_grad(dz, self.cpo, 0, self.cpo, 0, H * W, H * W, B, self.store.g(self.bname))
 
 
-def _bn_forward(bn, t, B, HW, group, train):
+def _bn_forward(bn, t, B, HW, group, train, relu=False):
     c = bn.c
     mr = torch.empty((B, c, 2), dtype=torch.float32, device=t.device)
     if train:
@@ -150,55 +190,108 @@ def _bn_forward(bn, t, B, HW, group, train):
         mr[:, :, 0] = bn.run_mean
         mr[:, :, 1] = torch.rsqrt(bn.run_var + bn.eps)
     a = torch.empty_like(t)
-    nn.bn_apply(t, mr, bn.gamma, bn.beta, None, a, B, HW, c, False)
+    nn.bn_apply(t, mr, bn.gamma, bn.beta, None, a, B, HW, c, relu)
     return a, mr
 
 
-class RepeatV2(object):
-    """One cnn_block repeat (:35-77, separable, norm_first): a = BN(t); y = ReLU(sep3x3(a));
-    out = y (r = 0) or y + a (the residual adds the BN OUTPUT: tmp_input is rebound to it)."""
+class _UnitV2(object):
+    """A conv unit of tf_hourglass_net (:35-113): [BN (norm_first)] -> conv -> [BN (norm_last)] -> ReLU
+    (batch_norm=False: no BN).  The norm_first BN is over the unit's input, the norm_last one over
+    its output; both keep channel-padded parameters and the real channel count in bn_c."""
 
-    def __init__(self, store, eff, blk, r, cin, nf):
+    def _init_unit(self, store, eff, bn_name, conv_name, cin, cout, stride, seperable, batch_norm, norm_order):
+        if norm_order not in ("norm_first", "norm_last"):
+            raise ValueError("norm_order must be 'norm_first' or 'norm_last'")
+        self.norm_first = norm_order == "norm_first"
+        self.bn_c = cin if self.norm_first else cout
+        self.bn = BatchNorm(store, bn_name, cp(self.bn_c), eps=BN_EPS, momentum=BN_MOMENTUM) if batch_norm else None
+        self.sep = conv_p(seperable, store, eff, conv_name, 3, cin, cout, stride)
+        self.store = store
+
+    def _unit_fwd(self, t, B, H, W, group, train):
+        a, mr, z = t, None, None
+        if self.bn is not None and self.norm_first:
+            a, mr = _bn_forward(self.bn, t, B, H * W, group, train)
+        if self.bn is not None and not self.norm_first:
+            z = self.sep.fwd(a, B, H, W)
+            Ho, Wo = self.sep.out_hw(H, W)
+            y, mr = _bn_forward(self.bn, z, B, Ho * Wo, group, train, relu=True)
+        else:
+            y = self.sep.fwd(a, B, H, W, relu_out=True)
+        return a, mr, z, y
+
+    def _unit_bwd_to_a(self, dout, a, mr, z, y, B, H, W, group):
+        """gradient of the conv's output (through ReLU [and the norm_last BN]) -> wgrad, returns du."""
+        st = self.store
+        du = torch.empty_like(y)
+        if z is not None:
+            Ho, Wo = self.sep.out_hw(H, W)
+            nn.bn_backward_grouped(dout, z, mr, self.bn.gamma, du, st.g(self.bn.gname), st.g(self.bn.bname),
+                                   B, Ho * Wo, self.bn.c, group, y_relu=y)
+        else:
+            nn.relu_backward(dout, y, du)
+        self.sep.wgrad(a, du, B, H, W)
+        return du
+
+    def _input_grad(self, da, t, mr, B, H, W, group, dx_out, dx_beta):
+        st = self.store
+        if self.bn is not None and self.norm_first:
+            nn.bn_backward_grouped(da, t, mr, self.bn.gamma, dx_out, st.g(self.bn.gname), st.g(self.bn.bname),
+                                   B, H * W, self.bn.c, group, dz_beta=dx_beta)
+        elif da is not dx_out:
+            if dx_beta:
+                nn.add(dx_out, da, dx_out)
+            else:
+                dx_out.copy_(da)
+
+
+class RepeatV2(_UnitV2):
+    """One cnn_block repeat (:35-77): norm_first: a = BN(t); y = ReLU(conv3x3(a)); out = y (r = 0) or
+    y + a (the residual adds the BN OUTPUT: tmp_input is rebound to it); norm_last: y =
+    ReLU(BN(conv3x3(t))), out = y or y + t."""
+
+    def __init__(self, store, eff, blk, r, cin, nf, seperable=True, batch_norm=True, norm_order="norm_first"):
         self.r, self.cin, self.cout = r, cin, nf
-        self.bn = BatchNorm(store, "%s_bn_%d" % (blk, r), cp(cin), eps=BN_EPS, momentum=BN_MOMENTUM)
-        self.sep = SepConvP(store, eff, "%s_cnn_%d" % (blk, r), 3, cin, nf)
+        self._init_unit(store, eff, "%s_bn_%d" % (blk, r), "%s_cnn_%d" % (blk, r), cin, nf, 1, seperable, batch_norm,
+                        norm_order)
 
     def forward(self, t, B, H, W, group, train=True):
-        a, mr = _bn_forward(self.bn, t, B, H * W, group, train)
-        y = self.sep.fwd(a, B, H, W, relu_out=True)
+        a, mr, z, y = self._unit_fwd(t, B, H, W, group, train)
         if self.r == 0:
             o = y
         else:
             o = torch.empty_like(y)
             nn.add(y, a, o)
-        return o, (t, mr, a, y, B, H, W, group)
+        return o, (t, mr, a, z, y, B, H, W, group)
 
     def backward(self, dout, saved, dx_out, dx_beta=0.0):
-        """dout is clobbered when r >= 1 (it becomes the BN-output gradient)."""
-        t, mr, a, y, B, H, W, group = saved
-        st = self.bn.store
-        du = torch.empty_like(y)
-        nn.relu_backward(dout, y, du)
-        self.sep.wgrad(a, du, B, H, W)
-        if self.r == 0:
+        """dout is clobbered when r >= 1 (it becomes the residual addend's gradient)."""
+        t, mr, a, z, y, B, H, W, group = saved
+        du = self._unit_bwd_to_a(dout, a, mr, z, y, B, H, W, group)
+        direct = self.r == 0 and not (self.bn is not None and self.norm_first)
+        if direct:
+            da = self.sep.dgrad(du, B, H, W, out=dx_out, beta=dx_beta)
+        elif self.r == 0:
             da = self.sep.dgrad(du, B, H, W)
         else:
             da = self.sep.dgrad(du, B, H, W, out=dout, beta=1.0)       # + the residual branch
-        nn.bn_backward_grouped(da, t, mr, self.bn.gamma, dx_out, st.g(self.bn.gname), st.g(self.bn.bname),
-                               B, H * W, self.bn.c, group, dz_beta=dx_beta)
+        self._input_grad(da, t, mr, B, H, W, group, dx_out, dx_beta)
 
 
 class CnnBlockV2(object):
-    def __init__(self, store, eff, name, cin, nf, n_repeats):
+    def __init__(self, store, eff, name, cin, nf, n_repeats, **opts):
         self.name = name
-        self.reps = [RepeatV2(store, eff, name, r, cin if r == 0 else nf, nf) for r in range(n_repeats)]
+        self.reps = [RepeatV2(store, eff, name, r, cin if r == 0 else nf, nf, **opts) for r in range(n_repeats)]
         self.cout = nf
 
     def seps(self):
         return [r.sep for r in self.reps]
 
     def bns(self):
-        return [r.bn for r in self.reps]
+        return [r.bn for r in self.reps if r.bn is not None]
+
+    def units(self):
+        return list(self.reps)
 
     def forward(self, x, B, H, W, group, train=True):
         h, saved = x, []
@@ -217,34 +310,34 @@ class CnnBlockV2(object):
         return dx_out
 
 
-class DownV2(object):
-    """downsample_block (:79-113): BN -> SeparableConv2D 3x3 / 2 "same" -> ReLU."""
+class DownV2(_UnitV2):
+    """downsample_block (:79-113): [BN] -> conv 3x3 / 2 "same" -> [BN] -> ReLU."""
 
-    def __init__(self, store, eff, name, cin, cout):
-        self.bn = BatchNorm(store, name + "_bnorm", cp(cin), eps=BN_EPS, momentum=BN_MOMENTUM)
-        self.sep = SepConvP(store, eff, name, 3, cin, cout, stride=2)
+    def __init__(self, store, eff, name, cin, cout, seperable=True, batch_norm=True, norm_order="norm_first"):
+        self._init_unit(store, eff, name + "_bnorm", name, cin, cout, 2, seperable, batch_norm, norm_order)
         self.cout = cout
 
     def seps(self):
         return [self.sep]
 
     def bns(self):
-        return [self.bn]
+        return [self.bn] if self.bn is not None else []
+
+    def units(self):
+        return [self]
 
     def forward(self, t, B, H, W, group, train=True):
-        a, mr = _bn_forward(self.bn, t, B, H * W, group, train)
-        y = self.sep.fwd(a, B, H, W, relu_out=True)
-        return y, (t, mr, a, y, B, H, W, group)
+        a, mr, z, y = self._unit_fwd(t, B, H, W, group, train)
+        return y, (t, mr, a, z, y, B, H, W, group)
 
     def backward(self, dout, saved, dx_out, dx_beta=0.0):
-        t, mr, a, y, B, H, W, group = saved
-        st = self.bn.store
-        du = torch.empty_like(y)
-        nn.relu_backward(dout, y, du)
-        self.sep.wgrad(a, du, B, H, W)
-        da = self.sep.dgrad(du, B, H, W)
-        nn.bn_backward_grouped(da, t, mr, self.bn.gamma, dx_out, st.g(self.bn.gname), st.g(self.bn.bname),
-                               B, H * W, self.bn.c, group, dz_beta=dx_beta)
+        t, mr, a, z, y, B, H, W, group = saved
+        du = self._unit_bwd_to_a(dout, a, mr, z, y, B, H, W, group)
+        if self.bn is not None and self.norm_first:
+            da = self.sep.dgrad(du, B, H, W)
+        else:
+            da = self.sep.dgrad(du, B, H, W, out=dx_out, beta=dx_beta)
+        self._input_grad(da, t, mr, B, H, W, group, dx_out, dx_beta)
 
 
 CONCAT_ORDER = ("blk1", "blk2", "blk3", "blk4", "blk5", "blk6", "dec1", "dec2", "dec3", "dec4", "dec5", "dec6")
@@ -256,13 +349,15 @@ class HourglassV2Net(object):
     (channel sc*(5+C) + j; b_focal folded into the class channels' bias, no sigmoid);
     backward(d_out bf16 [B, H/8, W/8, ld])."""
 
-    def __init__(self, n_classes, n_filters=12, tmp_pi=0.99, n_repeats=2, n_features=64, device="cuda", seed=0):
+    def __init__(self, n_classes, n_filters=12, tmp_pi=0.99, n_repeats=2, n_features=64, device="cuda", seed=0,
+                 seperable=True, batch_norm=True, norm_order="norm_first"):
         assert n_filters % 4 == 0 and n_features % 32 == 0, "n_filters % 4, n_features % 32 (reshape / conv pitch)"
         self.C, self.nf, self.nfeat = n_classes, n_filters, n_features
         self.R = 5 + n_classes
         self.device = torch.device(device)
         store, eff = ParamStore(), ParamStore()
-        self._build(store, eff, n_classes, tmp_pi, n_filters, n_repeats, n_features)
+        self.opts = dict(seperable=seperable, batch_norm=batch_norm, norm_order=norm_order)
+        self._build(store, eff, n_classes, tmp_pi, n_filters, n_repeats, n_features, self.opts)
         store.finalize(self.device, seed)
         eff.finalize(self.device, seed + 1)
         eff.flat.zero_()                     # folded kernels: zero outside the real (cin, cout) block
@@ -277,18 +372,19 @@ class HourglassV2Net(object):
         self._saved = None
         self.pack()
 
-    def _build(self, store, eff, C, tmp_pi, nf, n_repeats, n_features):
-        self.stem = StemV2(store, eff, nf)
-        self.enc = [CnnBlockV2(store, eff, "cnn_block_1", nf, nf, n_repeats)]
-        self.down = [DownV2(store, eff, "down_block_1", nf, 2 * nf)]
+    def _build(self, store, eff, C, tmp_pi, nf, n_repeats, n_features, opts=None):
+        o = opts or {}
+        self.stem = StemV2(store, eff, nf, o.get("seperable", True))
+        self.enc = [CnnBlockV2(store, eff, "cnn_block_1", nf, nf, n_repeats, **o)]
+        self.down = [DownV2(store, eff, "down_block_1", nf, 2 * nf, **o)]
         for k in range(2, 7):
             c = (2 ** (k - 1)) * nf
-            self.enc.append(CnnBlockV2(store, eff, "cnn_block_%d" % k, c, c, n_repeats))
-            self.down.append(DownV2(store, eff, "down_block_%d" % k, c, 2 * c))
-        self.dec = [CnnBlockV2(store, eff, "dec_block_%d" % k, (2 ** (7 - k)) * nf, (2 ** (6 - k)) * nf, n_repeats)
-                    for k in range(1, 7)]
+            self.enc.append(CnnBlockV2(store, eff, "cnn_block_%d" % k, c, c, n_repeats, **o))
+            self.down.append(DownV2(store, eff, "down_block_%d" % k, c, 2 * c, **o))
+        self.dec = [CnnBlockV2(store, eff, "dec_block_%d" % k, (2 ** (7 - k)) * nf, (2 ** (6 - k)) * nf, n_repeats,
+                               **o) for k in range(1, 7)]
         self.feat_c = 189 * nf                           # 63 nf encoder + 126 nf decoder channels
-        self.final = CnnBlockV2(store, eff, "final_out", self.feat_c, n_features, n_repeats)
+        self.final = CnnBlockV2(store, eff, "final_out", self.feat_c, n_features, n_repeats, **o)
         self.head = Conv(store, "head_out", 3, n_features, 4 * (5 + C), bias=True)
         self.bfocal = store.add("b_focal", (1,), constant(math.log((1.0 - tmp_pi) / tmp_pi)))
 
@@ -305,15 +401,17 @@ class HourglassV2Net(object):
     def _make_plan(self):
         seps = self.seps()
         entries = [self.stem.pack_entry()] + [s.conv.pack_entry() for s in seps] + [self.head.pack_entry()]
-        self._plan = (nn.SepPlan([self.stem.sep_entry()] + [s.sep_entry() for s in seps], self.device),
-                      nn.PackPlan(entries, self.device))
+        folds = ([self.stem.sep_entry()] if self.stem.seperable else []) + \
+            [s.sep_entry() for s in seps if not isinstance(s, DenseConvP)]
+        self._plan = (nn.SepPlan(folds, self.device) if folds else None, nn.PackPlan(entries, self.device))
 
     def pack(self):
         """Fold every separable conv, fold b_focal, re-pack every bf16 conv kernel (3 launches)."""
         if self._plan is None:
             self._make_plan()
         sep, pk = self._plan
-        sep.fold()
+        if sep is not None:
+            sep.fold()
         pk.run()
         nn.bias_scalar_fold_periodic(self.head.b, self.store.p(self.bfocal), self.b_eff, self.R, 4)
 
@@ -331,9 +429,13 @@ class HourglassV2Net(object):
         out = {k: get(k).detach().cpu().clone() for k in self.store.offsets}
         cut = [(self.stem.bname, self.nf)]
         for blk in self.blocks():
-            units = [(r.bn, r.sep) for r in blk.reps] if hasattr(blk, "reps") else [(blk.bn, blk.sep)]
-            for bn, sep in units:
-                cut += [(bn.gname, sep.cin), (bn.bname, sep.cin), (sep.bname, sep.cout)]
+            for u in blk.units():
+                if u.bn is not None:
+                    cut += [(u.bn.gname, u.bn_c), (u.bn.bname, u.bn_c)]
+                cut.append((u.sep.bname, u.sep.cout))
+                if isinstance(u.sep, DenseConvP):          # Conv2D kernel kept channel-padded
+                    k = u.sep.conv.wname
+                    out[k] = out[k][:, :, :u.sep.cin, :u.sep.cout].clone()
         for k, c in cut:
             out[k] = out[k][:c].clone()
         return out
@@ -434,7 +536,8 @@ class HourglassV2Net(object):
         g["blk0"] = torch.empty_like(v["blk0"])
         self.enc[0].backward(g["cnn1"], sv["cnn1"], g["blk0"], 0.0)
         self.stem.backward(g["blk0"], sv["stem"])
-        self._plan[0].unfold()
+        if self._plan[0] is not None:
+            self._plan[0].unfold()
         self._saved = None
         if hook is not None:
             hook("all")

@@ -112,7 +112,7 @@ class Conv(object):
     pad: 'same' (TF padding), 'valid', or an explicit leading pad int (ZeroPadding2D + valid)."""
 
     def __init__(self, store, name, k, cin, cout, stride=1, pad="same", bias=True, bias_init=0.0,
-                 cin_k=None, npad=None, cout_pad=None, dgrad=True, init_fan_out=None):
+                 cin_k=None, npad=None, cout_pad=None, dgrad=True, init_fan_out=None, w_init=None):
         self.name, self.k, self.cin, self.cout, self.stride, self.pad = name, k, cin, cout, stride, pad
         self.cin_k = cin if cin_k is None else cin_k       # channels per tap in the forward pack
         self.npad = npad if npad is not None else max(32, (cout + 31) // 32 * 32)
@@ -121,7 +121,8 @@ class Conv(object):
         self.has_bias = bias
         self.need_dgrad = dgrad
         fan_out = k * k * cout if init_fan_out is None else init_fan_out
-        self.wname = store.add(name + "/kernel", (k, k, cin, cout), glorot_uniform(k * k * cin, fan_out))
+        self.wname = store.add(name + "/kernel", (k, k, cin, cout),
+                               w_init if w_init is not None else glorot_uniform(k * k * cin, fan_out))
         self.bname = store.add(name + "/bias", (cout,), constant(bias_init)) if bias else None
         self.store = store
         self.wf = self.wd = None

@@ -43,11 +43,13 @@ class HourglassV2Model(object):
 
 def build_model(n_filters, n_classes, tmp_pi=0.99, n_repeats=2, n_features=256, seperable=True, batch_norm=True,
                 norm_order="norm_first", seed=0):
-    if not (seperable and batch_norm and norm_order == "norm_first"):
-        raise NotImplementedError("cvlite builds the configuration train_hourglass_voc.py trains "
-                                  "(seperable=True, batch_norm=True, norm_order='norm_first')")
+    """tf_hourglass_net.py:115-394, every build option (Conv2D for seperable=False, no BN,
+    norm_last)."""
+    if norm_order not in ("norm_first", "norm_last"):
+        raise ValueError("norm_order must be 'norm_first' or 'norm_last'")
     return HourglassV2Model(HourglassV2Net(n_classes, n_filters=n_filters, tmp_pi=tmp_pi, n_repeats=n_repeats,
-                                           n_features=n_features, device=_dev(), seed=seed))
+                                           n_features=n_features, device=_dev(), seed=seed, seperable=seperable,
+                                           batch_norm=batch_norm, norm_order=norm_order))
 
 
 def model_loss(bboxes, masks, outputs, img_size=448, reg_lambda=0.10, loss_type="sigmoid", eps=1.0e-6):

@@ -61,6 +61,20 @@ def sepconv(x, p, name, stride=1):
     return F.conv2d(y, pw.permute(3, 2, 0, 1), b)
 
 
+def dense_conv(x, p, name, stride=1):
+    """Keras Conv2D(..., padding="same") with bias (build_model(seperable=False), :124-136)."""
+    w, b = p[name + "/kernel"], p[name + "/bias"]
+    k = w.shape[0]
+    pt, pb = _same_pads(x.shape[2], k, stride)
+    pl, pr = _same_pads(x.shape[3], k, stride)
+    xp = F.pad(x, (pl, pr, pt, pb)) if (pt or pb or pl or pr) else x
+    return q(F.conv2d(q(xp), qw(w).permute(3, 2, 0, 1), b, stride))
+
+
+def conv(x, p, name, seperable, stride=1):
+    return sepconv(x, p, name, stride) if seperable else dense_conv(x, p, name, stride)
+
+
 def bn_group(x, p, name, group, stats=None):
     """Training-mode BN over sub-batches of `group` images (one Keras forward per sub-batch)."""
     g, bta = p[name + "/gamma"].view(1, -1, 1, 1), p[name + "/beta"].view(1, -1, 1, 1)
@@ -76,14 +90,22 @@ def bn_group(x, p, name, group, stats=None):
     return q(torch.cat(outs, 0))
 
 
-def cnn_block(x, p, blk, group, n_repeats=2, stats=None):
+def cnn_block(x, p, blk, group, n_repeats=2, stats=None, seperable=True, batch_norm=True, norm_order="norm_first"):
+    """tf_centernet_hourglass.py:87-156 with its options: norm_first (BN on the repeat input, which
+    is then the residual's addend) or norm_last (BN on the 2nf-channel output before the ReLU);
+    batch_norm=False drops the BN; seperable=False uses Conv2D."""
     t = x
     res = None
     for r in range(n_repeats):
-        t = bn_group(t, p, "%s_bn_%d" % (blk, r), group, stats)
-        y = sepconv(t, p, "%s_bot_%d" % (blk, r))
-        y = sepconv(y, p, "%s_cnn_%d" % (blk, r))
-        y = torch.relu(sepconv(y, p, "%s_out_%d" % (blk, r)))
+        bn = "%s_bn_%d" % (blk, r)
+        if norm_order == "norm_first" and batch_norm:
+            t = bn_group(t, p, bn, group, stats)
+        y = conv(t, p, "%s_bot_%d" % (blk, r), seperable)
+        y = conv(y, p, "%s_cnn_%d" % (blk, r), seperable)
+        y = conv(y, p, "%s_out_%d" % (blk, r), seperable)
+        if norm_order == "norm_last" and batch_norm:
+            y = bn_group(y, p, bn, group, stats)
+        y = torch.relu(y)
         res = y if r == 0 else q(y + t)
         t = res
     return res
@@ -97,15 +119,17 @@ def up(x):
     return F.interpolate(x, scale_factor=2, mode="bilinear", align_corners=False)
 
 
-def forward(x_nhwc, p, num_classes, group, n_stacks=1, stats=None):
+def forward(x_nhwc, p, num_classes, group, n_stacks=1, stats=None, seperable=True, batch_norm=True,
+            norm_order="norm_first"):
     """x [B,H,W,3] fp32 -> [B,H/4,W/4,4+C] (reg | cls + b_focal)."""
     x = x_nhwc.permute(0, 3, 1, 2)
-    v = {"blk0": sepconv(x, p, "cnn_block_0", stride=2)}
+    v = {"blk0": conv(x, p, "cnn_block_0", seperable, stride=2)}
     blk = dict((b[0], b) for b in blocks(n_stacks))
 
     def run(name):
         _, i, o = blk[name]
-        v[o] = cnn_block(v[i], p, name, group, stats=stats)
+        v[o] = cnn_block(v[i], p, name, group, stats=stats, seperable=seperable, batch_norm=batch_norm,
+                         norm_order=norm_order)
         return v[o]
     run("cnn_block_1")
     v["stack_in"] = pool(v["cnn1"])
@@ -143,11 +167,12 @@ def model_loss(y_true, y_pred):
     return cls, reg
 
 
-def loss_and_grads(params, x, targets, num_classes, sub_batch, cls_lambda=2.5, reg_lambda=1.0):
-    """Per sub-batch forward + loss; returns (cls_sum, reg_sum, summed grads dict, output)."""
+def loss_and_grads(params, x, targets, num_classes, sub_batch, cls_lambda=2.5, reg_lambda=1.0, **build):
+    """Per sub-batch forward + loss; returns (cls_sum, reg_sum, summed grads dict, output).
+    build: forward()'s build_model options (n_stacks, seperable, batch_norm, norm_order)."""
     p = {k: v.detach().clone().requires_grad_(True) for k, v in params.items()}
     B = x.shape[0]
-    out = forward(x, p, num_classes, sub_batch)
+    out = forward(x, p, num_classes, sub_batch, **build)
     total_cls = total_reg = 0.0
     tot = 0.0
     for s in range(0, B, sub_batch):
@@ -175,10 +200,10 @@ def adam_step(params, grads, m, v, it, lr, B, clip=1.0, b1=0.9, b2=0.999, eps=1e
     return norm
 
 
-def train_step_reference(params, m, v, it, images, targets, num_classes, sub_batch, lr=1e-3, clip=1.0):
+def train_step_reference(params, m, v, it, images, targets, num_classes, sub_batch, lr=1e-3, clip=1.0, **build):
     """One reference train_step on CPU (in place).  Returns (avg_cls, avg_reg)."""
     B = images.shape[0]
-    c, r, g, _ = loss_and_grads(params, images, targets, num_classes, sub_batch)
+    c, r, g, _ = loss_and_grads(params, images, targets, num_classes, sub_batch, **build)
     with torch.no_grad():
         adam_step(params, g, m, v, it, lr, B, clip)
     return c / B, r / B

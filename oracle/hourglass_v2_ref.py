@@ -106,56 +106,73 @@ def model_loss_torch(bboxes, logits, b_focal, loss_type="focal"):
 
 
 # ---- network ---------------------------------------------------------------------------------
-def cnn_block(x, p, blk, group, n_repeats=2):
-    """tf_hourglass_net.cnn_block (:35-77), separable, norm_first: the residual of repeats >= 1
-    adds the BN OUTPUT (tmp_input is rebound to it)."""
+def _conv(x, p, name, seperable, stride=1):
+    from .centernet_model_ref import dense_conv
+    return sepconv(x, p, name, stride=stride) if seperable else dense_conv(x, p, name, stride)
+
+
+def cnn_block(x, p, blk, group, n_repeats=2, seperable=True, batch_norm=True, norm_order="norm_first"):
+    """tf_hourglass_net.cnn_block (:35-77): norm_first (the residual of repeats >= 1 adds the BN
+    OUTPUT: tmp_input is rebound to it) or norm_last (BN on the conv output), with / without BN,
+    SeparableConv2D or Conv2D."""
     t, res = x, None
     for r in range(n_repeats):
-        t = bn_group(t, p, "%s_bn_%d" % (blk, r), group)
-        y = torch.relu(sepconv(t, p, "%s_cnn_%d" % (blk, r)))
+        bn = "%s_bn_%d" % (blk, r)
+        if batch_norm and norm_order == "norm_first":
+            t = bn_group(t, p, bn, group)
+        y = _conv(t, p, "%s_cnn_%d" % (blk, r), seperable)
+        if batch_norm and norm_order == "norm_last":
+            y = bn_group(y, p, bn, group)
+        y = torch.relu(y)
         res = y if r == 0 else q(y + t)
         t = res
     return res
 
 
-def downsample_block(x, p, name, group):
-    """:79-113: BN -> SeparableConv 3x3 / 2 ("same") -> ReLU."""
-    t = bn_group(x, p, name + "_bnorm", group)
-    return torch.relu(sepconv(t, p, name, stride=2))
+def downsample_block(x, p, name, group, seperable=True, batch_norm=True, norm_order="norm_first"):
+    """:79-113: [BN] -> conv 3x3 / 2 ("same") -> [BN] -> ReLU."""
+    t = bn_group(x, p, name + "_bnorm", group) if batch_norm and norm_order == "norm_first" else x
+    y = _conv(t, p, name, seperable, stride=2)
+    if batch_norm and norm_order == "norm_last":
+        y = bn_group(y, p, name + "_bnorm", group)
+    return torch.relu(y)
 
 
 def _nhwc(t):
     return t.permute(0, 2, 3, 1)
 
 
-def forward(x_nhwc, p, num_classes, group, n_repeats=2):
+def forward(x_nhwc, p, num_classes, group, n_repeats=2, seperable=True, batch_norm=True, norm_order="norm_first"):
     """x [B,H,W,3] -> head logits [B,S,S,4,5+C] (before the sigmoid / b_focal), S = H/8."""
+    o = dict(seperable=seperable, batch_norm=batch_norm, norm_order=norm_order)
     x = x_nhwc.permute(0, 3, 1, 2)
     B, _, H, W = x.shape
-    v = {"blk0": sepconv(x, p, "cnn_block_0")}
-    v["cnn1"] = cnn_block(v["blk0"], p, "cnn_block_1", group, n_repeats)
-    v["blk1"] = downsample_block(v["cnn1"], p, "down_block_1", group)
+    v = {"blk0": _conv(x, p, "cnn_block_0", seperable)}
+    v["cnn1"] = cnn_block(v["blk0"], p, "cnn_block_1", group, n_repeats, **o)
+    v["blk1"] = downsample_block(v["cnn1"], p, "down_block_1", group, **o)
     for k in range(2, 7):
-        c = cnn_block(v["blk%d" % (k - 1)], p, "cnn_block_%d" % k, group, n_repeats)
+        c = cnn_block(v["blk%d" % (k - 1)], p, "cnn_block_%d" % k, group, n_repeats, **o)
         v["in%d" % k] = q(v["blk%d" % (k - 1)] + c)
-        v["blk%d" % k] = downsample_block(v["in%d" % k], p, "down_block_%d" % k, group)
-    v["dec1"] = cnn_block(q(up(v["blk6"])), p, "dec_block_1", group, n_repeats)
+        v["blk%d" % k] = downsample_block(v["in%d" % k], p, "down_block_%d" % k, group, **o)
+    v["dec1"] = cnn_block(q(up(v["blk6"])), p, "dec_block_1", group, n_repeats, **o)
     for k in range(2, 7):
         u = q(up(v["in%d" % (8 - k)] + v["dec%d" % (k - 1)]))
-        v["dec%d" % k] = cnn_block(u, p, "dec_block_%d" % k, group, n_repeats)
+        v["dec%d" % k] = cnn_block(u, p, "dec_block_%d" % k, group, n_repeats, **o)
     S0, S1 = H // 8, W // 8
     order = ["blk1", "blk2", "blk3", "blk4", "blk5", "blk6", "dec1", "dec2", "dec3", "dec4", "dec5", "dec6"]
     feats = torch.cat([_nhwc(v[k]).reshape(B, S0, S1, -1) for k in order], -1).permute(0, 3, 1, 2)
-    h = cnn_block(feats, p, "final_out", group, n_repeats)
+    h = cnn_block(feats, p, "final_out", group, n_repeats, **o)
     w = p["head_out/kernel"]
-    o = F.conv2d(F.pad(q(h), (1, 1, 1, 1)), qw(w).permute(3, 2, 0, 1), p["head_out/bias"])
-    return qg(_nhwc(o).reshape(B, S0, S1, 4, 5 + num_classes))
+    out = F.conv2d(F.pad(q(h), (1, 1, 1, 1)), qw(w).permute(3, 2, 0, 1), p["head_out/bias"])
+    return qg(_nhwc(out).reshape(B, S0, S1, 4, 5 + num_classes))
 
 
-def loss_and_grads(params, x, targets, num_classes, sub_batch, loss_type="focal", cls_lambda=2.5, reg_lambda=1.0):
-    """train_step's loss over all sub-batches (sums are additive) -> (cls, reg, grads, logits)."""
+def loss_and_grads(params, x, targets, num_classes, sub_batch, loss_type="focal", cls_lambda=2.5, reg_lambda=1.0,
+                   **build):
+    """train_step's loss over all sub-batches (sums are additive) -> (cls, reg, grads, logits).
+    build: forward()'s build options (n_repeats, seperable, batch_norm, norm_order)."""
     p = {k: v.detach().clone().requires_grad_(True) for k, v in params.items()}
-    logits = forward(x, p, num_classes, sub_batch)
+    logits = forward(x, p, num_classes, sub_batch, **build)
     lc, lr = model_loss_torch(targets.to(logits.dtype), logits, p["b_focal"], loss_type)
     tot = cls_lambda * lc + reg_lambda * lr
     grads = torch.autograd.grad(tot, list(p.values()), allow_unused=True)

@@ -191,9 +191,9 @@ def test_centernet_loss_kernel():
         assert torch.all(d[b].view(Hs, Hs, -1)[..., 4 + C:] == 0)
 
 
-def _small_net(C=20, seed=0):
+def _small_net(C=20, seed=0, **opts):
     from cvlite.hourglass_net import HourglassNet
-    return HourglassNet(C, seed=seed)
+    return HourglassNet(C, seed=seed, **opts)
 
 
 def _targets(B, Hs, C, seed):
@@ -316,3 +316,53 @@ def _moment_rel(tr, net, M):
         num += float((mg - M[k].double()).norm() ** 2)
         den += float(M[k].double().norm() ** 2)
     return math.sqrt(num / den)
+
+
+BUILD_OPTIONS = [dict(n_stacks=2), dict(seperable=False), dict(batch_norm=False), dict(norm_order="norm_last"),
+                 dict(n_stacks=2, seperable=False, batch_norm=True, norm_order="norm_last")]
+
+
+@pytest.mark.parametrize("opts", BUILD_OPTIONS, ids=lambda o: "-".join("%s=%s" % kv for kv in sorted(o.items())))
+def test_hourglass_build_options_vs_oracle(opts):
+    """tf_centernet_hourglass.build_model's non-default options (VERDICT r03 missing #3): stacked
+    hourglasses, Conv2D (seperable=False), no BatchNormalization, norm_last -- forward output,
+    losses and parameter gradients vs the oracle with bf16 storage emulated at the GPU path's
+    points (same bounds as the default build's test above)."""
+    from cvlite import ops_targets as ot
+    from cvlite.centernet_hourglass import build_model
+    from oracle import centernet_model_ref as cm
+    C, B, D, G = 20, 4, 128, 2
+    net = build_model(C, n_filters=64, **opts)
+    params = net.store.state_dict()
+    gx = torch.Generator().manual_seed(17)
+    x = torch.rand(B, D, D, 3, generator=gx) * 2 - 1
+    Hs = D // 4
+    tg = _targets(B, Hs, C, 18)
+    out = net.forward(x.cuda(), group=G)
+    d_out = torch.zeros((B, Hs, Hs, net.cout_ld), dtype=torch.bfloat16, device="cuda")
+    losses, _ = ot.centernet_loss(out.view(B, -1, 4 + C), tg.cuda().view(B, -1, 4 + C), C, 2.5, 1.0,
+                                  d_pred=d_out.view(B, Hs * Hs, -1))
+    net.backward(d_out)
+    torch.cuda.synchronize()
+    build = dict(n_stacks=opts.get("n_stacks", 1), seperable=opts.get("seperable", True),
+                 batch_norm=opts.get("batch_norm", True), norm_order=opts.get("norm_order", "norm_first"))
+    with cm.emulate_bf16():
+        c16, r16, g16, o16 = cm.loss_and_grads(params, x, tg, C, G, **build)
+    c32, r32, g32, o32 = cm.loss_and_grads(params, x, tg, C, G, **build)
+    e_out = rel(out.cpu(), o16)
+    print("%r: out vs bf16-oracle %.4f | bf16-oracle vs fp32 %.4f" % (opts, e_out, rel(o16, o32)))
+    assert e_out < 3e-2
+    lc, lr = float(losses[:, 0].sum()), float(losses[:, 1].sum())
+    assert abs(lc - c16) / abs(c16) < 3e-2 and abs(lr - r16) / abs(r16) < 3e-2
+
+    def overall(ga, gb):
+        n = d = 0.0
+        for k in gb:
+            n += float((ga[k].double() - gb[k].double()).norm() ** 2)
+            d += float(gb[k].double().norm() ** 2)
+        return math.sqrt(n / d)
+    gpu = {k: net.store.g(k).detach().cpu() for k in g32}
+    assert set(gpu) == set(params)
+    e16, e32, own = overall(gpu, g16), overall(gpu, g32), overall(g16, g32)
+    print("grad rel-L2: gpu vs bf16-oracle %.4f, gpu vs fp32 %.4f, bf16-oracle vs fp32 %.4f" % (e16, e32, own))
+    assert e32 < 1.5 * own + 0.02 and e16 < 1.5 * own + 0.02

@@ -110,3 +110,19 @@ def test_launch_parity_catches_a_wrong_kernel(monkeypatch):
         conv.fwd(x, 2, 32, 32)
     torch.cuda.synchronize()
     assert lp.failures() and lp.records[0].op == "conv_igemm"
+
+
+@pytest.mark.parametrize("opts", [dict(n_stacks=2), dict(seperable=False, norm_order="norm_last"),
+                                  dict(batch_norm=False)], ids=["stacks2", "dense-normlast", "nobn"])
+def test_centernet_build_options_launch_parity(opts):
+    """The non-default tf_centernet_hourglass.build_model options, every launch of one training step
+    (256x256, bs 4, sub-batch 2) teacher-forced against float64."""
+    from cvlite.hourglass_net import HourglassNet
+    from cvlite.train_centernet import CenterNetTrainer, synthetic_batch
+    C, S, B = 20, 256, 4
+    net = HourglassNet(C, seed=0, n_filters=64, **opts)
+    tr = CenterNetTrainer(net, B, (S, S), sub_batch_sz=2, n_max=16, use_graph=False)
+    tr.load_batch(*synthetic_batch(B, S, S, C, n_max=16, seed=78))
+    with LaunchParity(imgs=_imgs()) as lp:
+        tr.step()
+    _report(lp, "centernet_opts_%s" % "_".join("%s%s" % kv for kv in sorted(opts.items())))
