@@ -8,8 +8,9 @@
 
 The resize / normalise / pad (and the flip, when fused) run in one cvl_resize_pad_normalize
 launch per image that can write straight into a slot of the device batch.  JPEG decode
-(`_parse_image`) is a host step (PIL; no GPU JPEG decoder in this image), as the reference's
-tf.image.decode_jpeg is; everything after it runs on the GPU.  The jitter draw uses numpy's generator instead of
+(`_parse_image`, data_preprocess.py:5-9) is a host step (PIL's libjpeg; this ROCm image ships no
+rocJPEG / GPU JPEG decoder), as the reference's tf.image.decode_jpeg runs on the host CPU too;
+everything after it runs on the GPU.  The jitter draw uses numpy's generator instead of
 tf.random.uniform (a different stream by construction).
 """
 import numpy as np
@@ -94,25 +95,49 @@ def box_targets(bbox, flip):
     return np.concatenate([(s[:, :2] + s[:, 2:]) / f32(2.0), s[:, 2:] - s[:, :2]], -1).astype(f32)
 
 
-def preprocess_data(sample, rng=None, out=None):
-    """data_preprocess.py:98-133 preprocess_data (pad_flag=True) for one sample dict with the
-    reference's keys: image (a file name, decoded on the host by _parse_image, or an already
-    decoded [H,W,3] image, uint8 or fp32, host or device), objects = {bbox [N,4] normalised, label [N]},
-    l_jitter / u_jitter, min_side, max_side.  Returns (image_padded [Hp,Wp,3] fp32 on the GPU,
-    bbox [N,4] (the reference's xywh of the swapped corners), class_id [N] int32, img_shp [2] fp32 =
-    the unpadded resized shape).  The flip draw (p = 0.5) and the jitter draw use `rng` (numpy) in
-    the reference's order: flip first, then the jitter size."""
+def preprocess_data(sample, img_dims=384, pad_flag=True, rng=None, out=None):
+    """data_preprocess.py:98-133 preprocess_data(sample, img_dims, pad_flag) for one sample dict with
+    the reference's keys: image (a file name, decoded on the host by _parse_image, or an already
+    decoded [H,W,3] image, uint8 or fp32, host or device), objects = {bbox [N,4] normalised, label
+    [N]}, l_jitter / u_jitter, min_side, max_side.  Returns (image [Hp,Wp,3] fp32 on the GPU, bbox
+    [N,4] (the reference's xywh of the swapped corners), class_id [N] int32, img_shp [2] fp32).
+    pad_flag=True: flip + jittered resize_and_pad_image (img_shp = the unpadded resized shape);
+    pad_flag=False: resize to [img_dims, img_dims] (:111-113), flip, /127.5 - 1 (:124-125),
+    img_shp = [img_dims, img_dims] -- one fused launch either way (a bilinear half-pixel resize
+    commutes with the left-right flip).  The flip draw (p = 0.5) and the jitter draw use `rng`
+    (numpy) in the reference's order: flip first, then the jitter size."""
     rng = rng if rng is not None else np.random.default_rng()
     jitter = [sample["l_jitter"], sample["u_jitter"]]
     image = sample["image"]
     if isinstance(image, str):                   # a file name, as the reference's samples hold
         image = _parse_image(image)
     flip = bool(rng.uniform() <= 0.5)
-    img, new_shape, _ = preprocess_image(image, jitter=jitter, min_side=sample["min_side"],
-                                         max_side=sample["max_side"], flip=flip, out=out, rng=rng)
+    if pad_flag:
+        img, new_shape, _ = preprocess_image(image, jitter=jitter, min_side=sample["min_side"],
+                                             max_side=sample["max_side"], flip=flip, out=out, rng=rng)
+    else:
+        img = resize_normalize(image, int(img_dims), int(img_dims), flip=flip, out=out)
+        new_shape = np.array([img_dims, img_dims], f32)
     bbox = box_targets(sample["objects"]["bbox"], flip)
     cls = np.asarray(sample["objects"]["label"], np.int32).reshape(-1)
     return img, bbox, cls, np.asarray(new_shape, f32)
+
+
+def resize_normalize(image, oh, ow, flip=False, out=None):
+    """tf.image.resize(image, [oh, ow]) (bilinear, half-pixel) [+ flip_left_right], / 127.5 - 1,
+    no padding: one cvl_resize_pad_normalize launch (output size = padded size)."""
+    _lib.require_cuda()
+    img = torch.as_tensor(image).cuda()
+    if img.dtype not in (torch.uint8, torch.float32):
+        img = img.float()
+    img = img.contiguous()
+    H, W, C = int(img.shape[0]), int(img.shape[1]), int(img.shape[2])
+    if out is None:
+        out = torch.empty((oh, ow, C), dtype=torch.float32, device=img.device)
+    assert tuple(out.shape) == (oh, ow, C) and out.dtype == torch.float32 and out.is_contiguous()
+    _lib.call("cvl_resize_pad_normalize", _lib.ptr(img), 1 if img.dtype == torch.uint8 else 0, H, W, C,
+              1 if flip else 0, oh, ow, oh, ow, _lib.ptr(out), _lib.stream())
+    return out
 
 
 def padded_size(sample_hw, jitter, min_side, max_side, rng, stride=128.0):

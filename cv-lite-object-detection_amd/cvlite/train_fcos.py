@@ -318,9 +318,10 @@ def train(train_data, training_loss, model, batch_size, optimizer, ckpt, ck_mana
           step_cool=1000, weight_decay=1.0e-4, gradient_clip=1.0, save_loss_file="train_losses.csv", world=None):
     """Same keywords and defaults as FCOS/train_fcos.py:87-93.
     * `model`: what cvlite.fcos.build_model returns (or its FCOSNet).
-    * `train_data`: either the reference's raw samples dict(image = a DECODED [H,W,3] image,
-      objects = {bbox, label}, l_jitter, u_jitter, min_side, max_side) -- each chosen image then
-      runs data_preprocess.preprocess_data (flip + jittered resize + pad) on the GPU and the
+    * `train_data`: either the reference's raw samples dict(image = a JPEG / PNG file name (decoded
+      on the host, data_preprocess._parse_image) or a decoded [H,W,3] image, objects = {bbox,
+      label}, l_jitter, u_jitter, min_side, max_side) -- each chosen image then runs
+      data_preprocess.preprocess_data (flip + jittered resize + pad) on the GPU and the
       batch trains as shape buckets (JitterFCOSTrainer) -- or pre-processed samples
       dict(image=[Hp,Wp,3] in [-1,1], bbox=[N,4] normalised (yc,xc,h,w), label=[N], optional
       img_dim=[h,w]) of one padded size.

@@ -44,3 +44,42 @@ def test_batch_slot_and_flip_boxes():
     im2, b2 = random_flip_horizontal(torch.tensor(imgs[0]).cuda(), boxes, p_flip=1.0)
     np.testing.assert_array_equal(im2.cpu().numpy(), imgs[0][:, ::-1])
     np.testing.assert_array_equal(b2, preprocess_ref.flip_boxes(boxes))
+
+
+def test_preprocess_data_from_jpeg_file(tmp_path):
+    """data_preprocess.preprocess_data on a sample whose image is a JPEG FILE NAME (the reference's
+    VOC sample schema, data_preprocess.py:5-9 _parse_image -> :98-133): host decode (PIL) then the
+    fused GPU flip + resize + pad -- identical to the restatement on the same decoded pixels and
+    the same flip / jitter draws; and the pad_flag=False form (resize to img_dims, flip, /127.5-1)."""
+    from PIL import Image
+    from cvlite.data_preprocess import preprocess_data, _parse_image
+    rng = np.random.default_rng(5)
+    img = rng.integers(0, 256, (333, 500, 3), dtype=np.uint8)
+    path = str(tmp_path / "sample.jpg")
+    Image.fromarray(img).save(path, quality=90)
+    dec = _parse_image(path)
+    assert dec.shape == (333, 500, 3) and dec.dtype == np.uint8
+    sample = {"image": path, "objects": {"bbox": np.array([[0.1, 0.2, 0.6, 0.9]], np.float32),
+                                         "label": np.array([3], np.int32)},
+              "l_jitter": 480, "u_jitter": 544, "min_side": 512.0, "max_side": 512.0}
+    for seed in (0, 1, 2, 3):
+        out, bbox, cls, shp = preprocess_data(sample, rng=np.random.default_rng(seed))
+        r = np.random.default_rng(seed)
+        flip = bool(r.uniform() <= 0.5)
+        side = np.float32(r.uniform(480, 544))
+        ref, rns, _ = preprocess_ref.resize_and_pad_image(dec, side, 512.0, 128.0, True, flip=flip)
+        np.testing.assert_array_equal(out.cpu().numpy(), ref)
+        np.testing.assert_array_equal(shp, rns)
+        assert cls.tolist() == [3]
+        b = preprocess_ref.flip_boxes(sample["objects"]["bbox"]) if flip else sample["objects"]["bbox"]
+        np.testing.assert_allclose(bbox, [[(b[0, 1] + b[0, 3]) / 2, (b[0, 0] + b[0, 2]) / 2,
+                                           b[0, 3] - b[0, 1], b[0, 2] - b[0, 0]]], rtol=1e-6)
+        # pad_flag=False: tf.image.resize to img_dims, then the flip, then /127.5 - 1
+        out2, _, _, shp2 = preprocess_data(sample, img_dims=384, pad_flag=False, rng=np.random.default_rng(seed))
+        a = dec[:, ::-1] if flip else dec
+        ref2 = preprocess_ref.resize_bilinear(a, 384, 384) / np.float32(127.5) - np.float32(1.0)
+        np.testing.assert_array_equal(out2.cpu().numpy(), ref2)
+        rf = preprocess_ref.resize_bilinear(dec, 384, 384)                 # the reference's order
+        rf = (rf[:, ::-1] if flip else rf) / np.float32(127.5) - np.float32(1.0)
+        np.testing.assert_allclose(out2.cpu().numpy(), rf, atol=1e-5)      # bilinear resize commutes with the flip
+        np.testing.assert_array_equal(shp2, [384.0, 384.0])

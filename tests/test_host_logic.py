@@ -130,3 +130,24 @@ def test_fcos_center_resnet101_branch():
     assert "Conv1/kernel" in FCOSNet.param_dict(20, backbone_model="resnet101")
     assert "conv4_block6_3_conv/kernel" in FCOSCenterNet.param_dict(20, backbone_model="resnet50")
     assert "Conv1/kernel" in FCOSCenterNet.param_dict(20, backbone_model="mobilenetv2")
+
+
+def test_parse_image_decodes_jpeg_and_png(tmp_path):
+    """data_preprocess._parse_image (FCOS/data_preprocess.py:5-9): a JPEG / PNG file -> [H,W,3] uint8
+    (host PIL decode, RGB; grayscale and RGBA inputs are converted like decode_jpeg(channels=3))."""
+    import numpy as np
+    from PIL import Image
+    from cvlite.data_preprocess import _parse_image
+    rng = np.random.default_rng(0)
+    img = rng.integers(0, 256, (37, 53, 3), dtype=np.uint8)
+    p = str(tmp_path / "a.png")
+    Image.fromarray(img).save(p)
+    np.testing.assert_array_equal(_parse_image(p), img)                 # lossless
+    q = str(tmp_path / "a.jpg")
+    Image.fromarray(img).save(q, quality=95)
+    with Image.open(q) as im:
+        ref = np.asarray(im.convert("RGB"))
+    np.testing.assert_array_equal(_parse_image(q), ref)
+    g = str(tmp_path / "g.jpg")
+    Image.fromarray(img[..., 0]).save(g)
+    assert _parse_image(g).shape == (37, 53, 3)
