@@ -487,6 +487,8 @@ def _line(metric, world, B, args, times, extra):
            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "bf16",
            "runs": {"n": len(times), "img_s": [round(world * B * args.steps / t, 3) for t in times],
                     "reported": "median run (SURVEY.md 8d: median of 3 runs of the timed steps)"}}
+    if torch.cuda.is_available():     # peak HBM the step's tensors held (allocator high-water mark)
+        out["peak_hbm_gib"] = round(torch.cuda.max_memory_allocated() / 2.0 ** 30, 3)
     out.update(extra)
     return out
 

@@ -162,12 +162,14 @@ class JitterFCOSTrainer(object):
 
     def __init__(self, net, batch_size, n_max=16, init_lr=5e-4, min_lr=1e-5, decay_step=1000, decay_rate=0.9,
                  momentum=0.9, gradient_clip=1.0, reg_type="l1", weight_decay=0.0, st_step=0, use_graph=True,
-                 max_buckets=12, world=1):
+                 max_buckets=12, world=1, optimizer=None, max_decays=None):
         # world > 1: data-parallel (dist.py) -- each rank runs its own bs images through its buckets,
         # the summed gradient is all-reduced (one bucketed SUM over RCCL) before the shared update
         # with 1 / (world * bs); the buckets differ per rank, so there is no overlap with the backward
         self.net, self.B, self.n_max, self.world = net, batch_size, n_max, int(world)
         self.momentum, self.clip = momentum, gradient_clip
+        self.adam = optimizer.bind(net.store) if hasattr(optimizer, "bind") else None    # Keras Adam
+        self.max_decays = max_decays
         self.sched = (init_lr, min_lr, decay_rate, decay_step)
         self.reg_type, self.use_graph, self.max_buckets = reg_type, use_graph, max_buckets
         self.weight_decay = float(weight_decay)
@@ -175,7 +177,11 @@ class JitterFCOSTrainer(object):
         dev = net.device
         self.buckets = {}
         self.acc = torch.zeros_like(net.store.grad)
-        self.lr = torch.tensor([init_lr], dtype=torch.float32, device=dev)
+        if self.adam is not None:
+            self.lr = self.adam.lr_dev
+            self.lr.fill_(init_lr)
+        else:
+            self.lr = torch.tensor([init_lr], dtype=torch.float32, device=dev)
         self.step_dev = torch.tensor([st_step], dtype=torch.int32, device=dev)
         self.sumsq = torch.zeros(nn.SUMSQ_WS, dtype=torch.float64, device=dev)
         self.losses = torch.zeros((batch_size, 3), dtype=torch.float32, device=dev)
@@ -233,9 +239,12 @@ class JitterFCOSTrainer(object):
         if self.world > 1:
             dist.allreduce_grads(st.grad)
         init_lr, min_lr, rate, dstep = self.sched
-        nn.lr_schedule(self.step_dev, self.lr, init_lr, min_lr, rate, dstep)
-        nn.sgd_clip_update(st.flat, st.grad, st.mom, self.lr, self.momentum, 1.0 / (bs * self.world), self.clip,
-                           ws=self.sumsq)
+        nn.lr_schedule(self.step_dev, self.lr, init_lr, min_lr, rate, dstep, max_decays=self.max_decays)
+        if self.adam is not None:
+            self.adam.apply(st, 1.0 / (bs * self.world), self.clip)
+        else:
+            nn.sgd_clip_update(st.flat, st.grad, st.mom, self.lr, self.momentum, 1.0 / (bs * self.world), self.clip,
+                               ws=self.sumsq)
         self.net.pack()
         return self.losses
 
@@ -315,7 +324,8 @@ def _batch_from_samples(train_data, idx, n_max):
 
 def train(train_data, training_loss, model, batch_size, optimizer, ckpt, ck_manager, st_step, max_steps,
           init_lr=1.0e-3, min_lr=1.0e-5, decay_step=1000, decay_rate=0.99, display_step=50, step_save=100,
-          step_cool=1000, weight_decay=1.0e-4, gradient_clip=1.0, save_loss_file="train_losses.csv", world=None):
+          step_cool=1000, weight_decay=1.0e-4, gradient_clip=1.0, save_loss_file="train_losses.csv", world=None,
+          max_decays=None):
     """Same keywords and defaults as FCOS/train_fcos.py:87-93.
     * `model`: what cvlite.fcos.build_model returns (or its FCOSNet).
     * `train_data`: either the reference's raw samples dict(image = a JPEG / PNG file name (decoded
@@ -331,11 +341,15 @@ def train(train_data, training_loss, model, batch_size, optimizer, ckpt, ck_mana
     * weight_decay > 0 adds weight_decay * l2_params_reg to every image's reported loss and not to
       the gradient, exactly as the reference (the regulariser is computed outside the tape).
     * world (cvlite extension; the reference is single-device): data-parallel over the initialised
-      torch.distributed group (None = its world size, 1 without one).  Every rank draws the same
-      global sample of world * batch_size indices from np.random (seed it identically on every
-      rank for a partition) and trains its own batch_size shard; gradients are all-reduced, the
+      torch.distributed group (None = its world size, 1 without one).  Rank 0 draws the global
+      sample of world * batch_size indices from np.random and broadcasts it, so the shards
+      partition it whatever the ranks' seeds; each rank trains its own batch_size shard; gradients are all-reduced, the
       reported losses are averaged over all world * batch_size images, and only rank 0 prints and
       saves.
+    * `optimizer`: the SGD stand-in (momentum read from it, train_fcos.py:284-285) or
+      cvlite.train_centernet.Adam (Keras Adam, what train_fcos_center_voc.py:327 trains with);
+      max_decays caps the decay exponent (the centre loops' step schedule, :150-157).  A string
+      ckpt prefix saves the optimizer's slots too (SGD momentum or Adam m / v / iterations).
     The reference's thermal "Cooling GPU" sleep runs only with CVL_COOLING=1.  Returns None."""
     from . import checkpoint as ck
     import torch.distributed as tdist
@@ -352,20 +366,21 @@ def train(train_data, training_loss, model, batch_size, optimizer, ckpt, ck_mana
     if n_data < world * batch_size:
         raise ValueError("train_data holds %d samples, fewer than world * batch_size" % n_data)
     say = print if rank == 0 else (lambda *a, **k: None)
+    momentum = float(getattr(optimizer, "momentum", 0.9))
     if raw:          # reference-format samples: per-image jittered sizes, shape-bucketed step
         n_max = max(16, max(len(s["objects"]["label"]) for s in train_data))
         trainer = JitterFCOSTrainer(net, batch_size, n_max=n_max, init_lr=init_lr, min_lr=min_lr,
-                                    decay_step=decay_step, decay_rate=decay_rate, momentum=optimizer.momentum,
+                                    decay_step=decay_step, decay_rate=decay_rate, momentum=momentum,
                                     gradient_clip=gradient_clip, weight_decay=weight_decay, st_step=st_step,
-                                    world=world)
+                                    world=world, optimizer=optimizer, max_decays=max_decays)
         rng = np.random.default_rng()
     else:
         H, W = np.asarray(train_data[0]["image"]).shape[:2]
         n_max = max(16, max(len(s["label"]) for s in train_data))
         trainer = FCOSTrainer(net, batch_size, (H, W), n_max=n_max, init_lr=init_lr, min_lr=min_lr,
-                              decay_step=decay_step, decay_rate=decay_rate, momentum=optimizer.momentum,
+                              decay_step=decay_step, decay_rate=decay_rate, momentum=momentum,
                               gradient_clip=gradient_clip, weight_decay=weight_decay, st_step=st_step,
-                              world=world)
+                              world=world, optimizer=optimizer, max_decays=max_decays)
     dev = net.device
     start = time.time()
     elapsed = 0.0
@@ -373,6 +388,11 @@ def train(train_data, training_loss, model, batch_size, optimizer, ckpt, ck_mana
     tot = np.zeros(3)
     for step in range(st_step, max_steps):
         idx = np.random.choice(n_data, size=world * batch_size, replace=False)   # train_fcos.py:112
+        if world > 1:        # rank 0's draw for every rank: the shards partition one global sample
+            t = torch.from_numpy(idx.astype(np.int64))
+            t = t.to(dev) if tdist.get_backend() == "nccl" else t
+            tdist.broadcast(t, 0)
+            idx = t.cpu().numpy()
         idx = idx[rank * batch_size:(rank + 1) * batch_size]
         if raw:
             imgs, bx, nb, dims = _raw_batch(train_data, idx, rng)
@@ -384,7 +404,7 @@ def train(train_data, training_loss, model, batch_size, optimizer, ckpt, ck_mana
             per_img = trainer.step().detach().double()     # [bs, 3] (cls, reg, cen)
         ntgt = trainer.ntgt.sum(1)
         for k in np.nonzero(ntgt.cpu().numpy() == 0)[0]:
-            print("No targets at index", str(idx[k]) + ".")
+            say("No targets at index", str(idx[k]) + ".")
         if world > 1:        # report over the global batch: sums of every rank's images
             red = torch.cat([per_img.sum(0), ntgt.sum().double().view(1)])
             tdist.all_reduce(red)
@@ -446,11 +466,16 @@ def train(train_data, training_loss, model, batch_size, optimizer, ckpt, ck_mana
 
 
 def save_checkpoint(prefix, model, trainer, step):
-    """{step, params, SGD momentum, BN running stats, parameter layout} at <prefix>.pt."""
+    """{step, params, SGD momentum, BN running stats, parameter layout[, Adam m / v / iterations]}
+    at <prefix>.pt."""
     from . import checkpoint as ck
     net = getattr(model, "net", model)
     st = ck.net_state(net)
     st["step"] = int(step)
+    adam = getattr(trainer, "adam", None)
+    if adam is not None:
+        st["adam"] = {"m": adam.m.detach().cpu().clone(), "v": adam.v.detach().cpu().clone(),
+                      "iterations": adam.iterations.detach().cpu().clone()}
     torch.save(st, prefix + ".pt")
 
 
@@ -461,4 +486,7 @@ def load_checkpoint(path, model, trainer=None):
     ck.load_net_state(net, s)
     if trainer is not None:
         trainer.step_dev.fill_(int(s["step"]))
+        adam = getattr(trainer, "adam", None)
+        if adam is not None and "adam" in s:
+            adam.load_state({k: v.to(adam.m.device) for k, v in s["adam"].items()})
     return int(s["step"])

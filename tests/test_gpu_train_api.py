@@ -224,3 +224,33 @@ def test_train_loop_raw_samples_jittered(tmp_path):
           weight_decay=0.0)
     torch.cuda.synchronize()
     assert torch.isfinite(net.store.flat).all() and not torch.equal(w0, net.store.flat)
+
+
+def test_train_loop_adam_jittered_checkpoint_roundtrip(tmp_path):
+    """train() forwards an Adam optimizer and max_decays into the jitter trainer (Keras Adam is
+    what train_fcos_center_voc.py:327 uses); a string ckpt prefix saves the Adam slots and
+    load_checkpoint restores them into a fresh trainer."""
+    from cvlite import fcos
+    from cvlite.fcos_net import FCOSNet
+    from cvlite.train_centernet import Adam
+    from cvlite.train_fcos import JitterFCOSTrainer, load_checkpoint, train
+    C = 20
+    samples = _raw_samples(C, 9) * 2
+    model = fcos.build_model(C)
+    net = model.net
+    w0 = net.store.flat.clone()
+    opt = Adam(1e-3)
+    prefix = str(tmp_path / "adam")
+    train(samples, [], model, 3, opt, prefix, None, 0, 2, display_step=1, step_save=2, weight_decay=0.0,
+          max_decays=1)
+    torch.cuda.synchronize()
+    assert int(opt.iterations.item()) == 2
+    assert torch.isfinite(net.store.flat).all() and not torch.equal(w0, net.store.flat)
+    assert float(opt.v.abs().max()) > 0
+    net2 = FCOSNet(C, seed=5)
+    opt2 = Adam(1e-3)
+    jt = JitterFCOSTrainer(net2, 3, use_graph=False, optimizer=opt2)
+    assert load_checkpoint(prefix + ".pt", net2, jt) == 2
+    assert torch.equal(net2.store.flat, net.store.flat)
+    assert torch.equal(opt2.m, opt.m) and torch.equal(opt2.v, opt.v)
+    assert int(opt2.iterations.item()) == 2
