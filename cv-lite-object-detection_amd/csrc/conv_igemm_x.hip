@@ -55,7 +55,7 @@ __global__ void __launch_bounds__(NT) conv_igemm_x32_kernel(ConvArgs a) {
   const int dbg = DBG ? a.dbg : 0;
   __shared__ __attribute__((aligned(16))) cvl_bf16 lds[LDS32_EL];
   // 256 (with 8): wall-clock stamps of thread 0 of every workgroup into dst (u64 [grid][4]: entry,
-  // prologue landed, main loop done, K-tiles)
+  // prologue landed, main loop done, shader-clock ticks of the loop)
   unsigned long long* stamp = (DBG && (dbg & 256) && threadIdx.x == 0)
                                   ? reinterpret_cast<unsigned long long*>(a.dst) + (size_t)blockIdx.x * 4 : nullptr;
   if (stamp) stamp[0] = wall_clock64();
@@ -159,7 +159,8 @@ __global__ void __launch_bounds__(NT) conv_igemm_x32_kernel(ConvArgs a) {
   __builtin_amdgcn_s_barrier();
   asm volatile("" ::: "memory");
   if (wm == 1) bar();           // stagger: waves 4-7 run one barrier behind
-  if (stamp) stamp[1] = wall_clock64();
+  unsigned long long clk0 = 0;
+  if (stamp) { stamp[1] = wall_clock64(); clk0 = __builtin_amdgcn_s_memtime(); }
 
   int rslot = 0;
   for (int kt = 0; kt < nk; ++kt) {
@@ -207,7 +208,8 @@ __global__ void __launch_bounds__(NT) conv_igemm_x32_kernel(ConvArgs a) {
   }
   if (wm == 0) bar();           // equal barrier counts for both groups
   wait_vm<0>();
-  if (stamp) { stamp[2] = wall_clock64(); stamp[3] = nk; }
+  // stamp[3]: shader clock ticks over the loop (in-kernel clock = ticks / wall ticks x 100 MHz)
+  if (stamp) { stamp[2] = wall_clock64(); stamp[3] = __builtin_amdgcn_s_memtime() - clk0; }
   if (dbg & 8) {
     if (acc[0][0][0] == 12345.f) reinterpret_cast<float*>(a.dst)[1] = 1.f;     // keep the accumulators live
     return;
