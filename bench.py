@@ -161,12 +161,12 @@ def measure_backbone_3x3(net, B, H, W, iters=20, eager=False):
         dy = torch.randn((B, h, w, conv.cout_pad), generator=g).to(torch.bfloat16).to(dev)
         dy[..., conv.cout:] = 0
         y = torch.empty((B, h, w, conv.cout), dtype=torch.bfloat16, device=dev)
-        st = torch.zeros((B, conv.cout, 2), dtype=torch.float64, device=dev)
+        st = nn.bn_acc(B, conv.cout, dev)
         dx = torch.empty((B, h, w, C), dtype=torch.bfloat16, device=dev)
         mr = torch.empty((B, C, 2), dtype=torch.float32, device=dev)
         mr[..., 0] = 0.0
         mr[..., 1] = 1.0
-        sums = torch.zeros((B, C, 2), dtype=torch.float64, device=dev)
+        sums = nn.bn_acc(B, C, dev)
         dwb = torch.zeros_like(conv.dw)
         fd = conv.fwd_desc(B, [nn.seg(h, w, h, w, conv.wf, conv.bias_arg())], ld_dst=conv.cout)
         dd = conv.dgrad_desc(B, [nn.seg(h, w, h, w, conv.wd)], ld_dst=C)

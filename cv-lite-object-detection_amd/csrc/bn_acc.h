@@ -1,0 +1,103 @@
+// Internal: exact, order-independent accumulators for the BatchNorm statistics (sum, sumsq) and
+// the BN-backward sums (sum g, sum g * xhat) that many workgroups add into one (image, channel).
+//
+// Floating-point atomics make a sum depend on the order the adds arrive in.  Here each fp32
+// partial p = m * 2^(e - 150) (24-bit significand m, biased exponent e) is added EXACTLY, as an
+// integer, into one of 7 int64 bins chosen by its exponent: bin k holds multiples of
+// 2^(E0 + 22k - 150), p lands in bin (e - E0) / 22 as m << ((e - E0) % 22) (< 2^45, so 2^18
+// partials fit a bin with no overflow).  Integer adds commute, so the bins -- and the value decoded
+// from them in a fixed order -- are bit-identical whatever the order of the atomics.  Slot 7 counts
+// non-finite partials (and partials >= 2^54): the decoded value is then NaN, as a float sum would be.
+// Partials below 2^-100 in magnitude (subnormals included) are dropped: far below the statistics'
+// resolution, and the drop itself is deterministic.
+//
+// Layout: one statistic = 8 consecutive uint64 ("slots"); a (B, C) statistics buffer is
+// [B][C][2][8] (the public header's cvl_bn_acc layout).  Zero it before the producer.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+constexpr int kAccSlots = 8;            // uint64 per statistic
+constexpr int kAccBins = 7;
+constexpr int kAccW = 22;               // exponents per bin
+constexpr int kAccE0 = 27;              // biased exponent of bin 0's floor (2^-100)
+
+typedef unsigned long long acc_u64;
+
+// (bin, signed integer) of an fp32 partial; bin -1 = nothing to add, kAccBins = the non-finite slot
+__device__ __forceinline__ int acc_split(float p, long long* v) {
+  const unsigned u = __float_as_uint(p);
+  const int e = (int)((u >> 23) & 0xffu);
+  if (e == 255) { *v = 1; return kAccBins; }
+  const int r = e - kAccE0;
+  if (e == 0 || r < 0) { *v = 0; return -1; }
+  const int k = r / kAccW;
+  if (k >= kAccBins) { *v = 1; return kAccBins; }
+  const long long m = (long long)((u & 0x7fffffu) | 0x800000u) << (r - k * kAccW);
+  *v = (u >> 31) ? -m : m;
+  return k;
+}
+
+// atomic add of one fp32 partial into the statistic at s (8 slots)
+__device__ __forceinline__ void acc_add(acc_u64* s, float p) {
+  long long v;
+  const int k = acc_split(p, &v);
+  if (k >= 0) atomicAdd(s + k, (acc_u64)v);
+}
+
+// atomic add of a float64 partial, exactly: split into three fp32 pieces hi + mid + lo (72
+// significand bits >= 53, each remainder exact in float64)
+__device__ __forceinline__ void acc_add_f64(acc_u64* s, double p) {
+  const float hi = (float)p;
+  const double r = p - (double)hi;
+  const float mid = (float)r;
+  const float lo = (float)(r - (double)mid);
+  acc_add(s, hi);
+  if (mid != 0.f) acc_add(s, mid);
+  if (lo != 0.f) acc_add(s, lo);
+}
+
+// register-resident accumulator (a single writer: store with acc_store, no atomics); the bin is
+// selected arithmetically so the array stays in registers
+struct AccLocal {
+  long long b[kAccSlots];
+  __device__ __forceinline__ void zero() {
+#pragma unroll
+    for (int k = 0; k < kAccSlots; ++k) b[k] = 0;
+  }
+  __device__ __forceinline__ void add(float p) {
+    long long v;
+    const int k = acc_split(p, &v);
+#pragma unroll
+    for (int j = 0; j < kAccSlots; ++j) b[j] += (j == k) ? v : 0;
+  }
+  __device__ __forceinline__ void add_f64(double p) {
+    const float hi = (float)p;
+    const double r = p - (double)hi;
+    const float mid = (float)r;
+    add(hi);
+    add(mid);
+    add((float)(r - (double)mid));
+  }
+  __device__ __forceinline__ void add(const acc_u64* s) {      // another accumulator's slots
+#pragma unroll
+    for (int j = 0; j < kAccSlots; ++j) b[j] += (long long)s[j];
+  }
+  __device__ __forceinline__ void store(acc_u64* s) const {
+#pragma unroll
+    for (int j = 0; j < kAccSlots; ++j) s[j] = (acc_u64)b[j];
+  }
+};
+
+// the statistic's value: bins decoded in a fixed order (smallest first), each exact integer
+// rounded once to float64 and scaled by a power of two
+__device__ __forceinline__ double acc_value(const acc_u64* s) {
+  if (s[kAccBins] != 0) return __builtin_nan("");
+  double t = 0.0;
+#pragma unroll
+  for (int k = 0; k < kAccBins; ++k) t += (double)(long long)s[k] * __builtin_ldexp(1.0, kAccE0 + kAccW * k - 150);
+  return t;
+}
+
+// statistic s (0 or 1) of (image b, channel c) in a [B][C][2][8] buffer
+__device__ __forceinline__ long acc_idx(long bc, int s) { return (bc * 2 + s) * kAccSlots; }

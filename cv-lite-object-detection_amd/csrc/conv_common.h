@@ -1,6 +1,7 @@
 // Internal: segmented-conv argument block shared by the fwd/dgrad and wgrad kernels.
 #pragma once
 #include "cvl_common.h"
+#include "bn_acc.h"
 
 typedef short s16x8 __attribute__((ext_vector_type(8)));
 typedef short s16x4 __attribute__((ext_vector_type(4)));
@@ -62,7 +63,7 @@ struct ConvSeg {
 struct ConvArgs {
   const cvl_bf16* src;
   void* dst;
-  double* stats;
+  acc_u64* stats;     // BN statistics accumulators [B][n_store][2][8] (bn_acc.h) or null
   int nseg, B;
   ConvSeg seg[kMaxSeg];
   int Cin, KH, KW, stride, pad_t, pad_l;
@@ -81,7 +82,7 @@ struct ConvArgs {
   const float* bmr;
   const float* bga;
   const float* bbe;
-  double* bsum;
+  acc_u64* bsum;
   float bhi;
   const cvl_bf16* by;     // non-null: the ReLU mask comes from y > 0 (a residual unit's output), not bn(z)
 };
@@ -98,7 +99,7 @@ struct BnSumArgs {
   const float* mr;
   const float* gamma;
   const float* beta;
-  double* sums;
+  acc_u64* sums;
   float hi;
   const cvl_bf16* y;      // residual unit: mask y > 0 (null: rebuilt from z)
 };

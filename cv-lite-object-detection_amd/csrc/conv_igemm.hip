@@ -281,9 +281,9 @@ __global__ void __launch_bounds__(NT) conv_igemm_kernel(ConvArgs a) {
         float s1 = 0.f, s2 = 0.f;
 #pragma unroll
         for (int e = 0; e < 4; ++e) { const float v = acc[i][j][e]; s1 += v; s2 += v * v; }
-        double* st = a.stats + ((long)img * a.n_store + n) * 2;
-        atomicAdd(st, (double)s1);
-        atomicAdd(st + 1, (double)s2);
+        acc_u64* st = a.stats + acc_idx((long)img * a.n_store + n, 0);
+        acc_add(st, s1);
+        acc_add(st + kAccSlots, s2);
       }
     }
   } else if (a.stats) {   // one image per tile (H*W % BM == 0): reduce the tile's rows first
@@ -303,9 +303,9 @@ __global__ void __launch_bounds__(NT) conv_igemm_kernel(ConvArgs a) {
       s2 += __shfl_xor(s2, 16, 64); s2 += __shfl_xor(s2, 32, 64);
       const int n = n0 + wn * WN + j * 16 + lr;
       if (lg == 0 && n < a.n_store) {
-        double* st = a.stats + ((long)img * a.n_store + n) * 2;
-        atomicAdd(st, (double)s1);
-        atomicAdd(st + 1, (double)s2);
+        acc_u64* st = a.stats + acc_idx((long)img * a.n_store + n, 0);
+        acc_add(st, s1);
+        acc_add(st + kAccSlots, s2);
       }
     }
   }
@@ -436,9 +436,9 @@ __global__ void __launch_bounds__(NT) conv_splitk_finish(ConvArgs a, int rows_pe
       if (c < a.n_store) {
         double t1 = 0.0, t2 = 0.0;
         for (int k = 0; k < FIN_RL; ++k) { t1 += red[k][cg2][u]; t2 += red[k][cg2][8 + u]; }
-        double* st = a.stats + ((long)img * a.n_store + c) * 2;
-        atomicAdd(st, t1);
-        atomicAdd(st + 1, t2);
+        acc_u64* st = a.stats + acc_idx((long)img * a.n_store + c, 0);
+        acc_add_f64(st, t1);
+        acc_add_f64(st + kAccSlots, t2);
       }
     }
   }
@@ -507,7 +507,7 @@ static inline int pick_bn(int npad) { return npad % 128 == 0 ? 128 : (npad % 64 
 
 }  // namespace
 
-int cvl_conv_igemm_l(const cvl_conv_desc* d, int dst_up, int dst_w, const void* src, void* dst, double* bn_stats,
+int cvl_conv_igemm_l(const cvl_conv_desc* d, int dst_up, int dst_w, const void* src, void* dst, acc_u64* bn_stats,
                      hipStream_t s, const BnSumArgs* bsum = nullptr, void* workspace = nullptr,
                      size_t workspace_bytes = 0);
 size_t cvl_conv_h_workspace(const cvl_conv_desc* d, const ConvArgs& a);
@@ -579,7 +579,7 @@ extern "C" const char* cvl_conv_kernel_name(int code) {
   }
 }
 
-int cvl_conv_f32(const cvl_conv_desc* d, const void* src, void* dst, double* bn_stats, hipStream_t s);
+int cvl_conv_f32(const cvl_conv_desc* d, const void* src, void* dst, acc_u64* bn_stats, hipStream_t s);
 
 extern "C" size_t cvl_conv_igemm_workspace_size(const cvl_conv_desc* d) {
   if (d && d->prec == CVL_PREC_F32) return 16;
@@ -598,8 +598,9 @@ extern "C" size_t cvl_conv_igemm_workspace_size(const cvl_conv_desc* d) {
   return n;
 }
 
-extern "C" int cvl_conv_igemm(const cvl_conv_desc* d, const void* src, void* dst, double* bn_stats,
+extern "C" int cvl_conv_igemm(const cvl_conv_desc* d, const void* src, void* dst, uint64_t* bn_stats_acc,
                               void* workspace, size_t workspace_bytes, cvl_stream_t stream) {
+  acc_u64* bn_stats = reinterpret_cast<acc_u64*>(bn_stats_acc);
   hipStream_t s = (hipStream_t)stream;
   g_cvl_conv_last_kernel = CVL_CK_NONE;
   CVL_CHECK_ARG(d);
@@ -663,7 +664,7 @@ extern "C" int cvl_conv_igemm(const cvl_conv_desc* d, const void* src, void* dst
 // plain data gradient runs and *fused = 0 (the caller then runs the two-pass BN backward).
 extern "C" int cvl_conv_igemm_dgrad_bnsum(const cvl_conv_desc* d, const void* src, void* dst, const void* z,
                                           const float* mean_rstd, const float* gamma, const float* beta, float act_hi,
-                                          double* sums, int32_t* fused, void* workspace, size_t workspace_bytes,
+                                          uint64_t* sums, int32_t* fused, void* workspace, size_t workspace_bytes,
                                           cvl_stream_t stream) {
   CVL_CHECK_ARG(d && fused && z && mean_rstd && gamma && beta && sums);
   *fused = 0;
@@ -678,7 +679,8 @@ extern "C" int cvl_conv_igemm_dgrad_bnsum(const cvl_conv_desc* d, const void* sr
     if (!s2dgrad_transform(d, &dd, &up, &upw)) {
       ConvArgs chk;
       if (cvl_conv_prepare(d, BM, &chk) == CVL_OK) {
-        const BnSumArgs b{reinterpret_cast<const cvl_bf16*>(z), mean_rstd, gamma, beta, sums, act_hi};
+        const BnSumArgs b{reinterpret_cast<const cvl_bf16*>(z), mean_rstd, gamma, beta,
+                          reinterpret_cast<acc_u64*>(sums), act_hi};
         g_cvl_conv_last_kernel = CVL_CK_NONE;
         const int lst = cvl_conv_igemm_l(d, 1, 0, src, dst, nullptr, (hipStream_t)stream, &b, workspace,
                                          workspace_bytes);
@@ -698,7 +700,7 @@ extern "C" int cvl_conv_igemm_dgrad_bnsum(const cvl_conv_desc* d, const void* sr
 // persistent kernel only; otherwise the plain data gradient runs and *fused = 0.
 extern "C" int cvl_conv_igemm_dgrad_bnsum_res(const cvl_conv_desc* d, const void* src, void* dst, const void* y,
                                               const void* z, const float* mean_rstd, const float* gamma,
-                                              const float* beta, double* sums, int32_t* fused, void* workspace,
+                                              const float* beta, uint64_t* sums, int32_t* fused, void* workspace,
                                               size_t workspace_bytes, cvl_stream_t stream) {
   CVL_CHECK_ARG(d && fused && y && z && mean_rstd && gamma && beta && sums);
   *fused = 0;
@@ -711,7 +713,8 @@ extern "C" int cvl_conv_igemm_dgrad_bnsum_res(const cvl_conv_desc* d, const void
       src && dst) {
     ConvArgs chk;
     if (cvl_conv_prepare(d, BM, &chk) == CVL_OK) {
-      BnSumArgs b{reinterpret_cast<const cvl_bf16*>(z), mean_rstd, gamma, beta, sums, INFINITY};
+      BnSumArgs b{reinterpret_cast<const cvl_bf16*>(z), mean_rstd, gamma, beta, reinterpret_cast<acc_u64*>(sums),
+                  INFINITY};
       b.y = reinterpret_cast<const cvl_bf16*>(y);
       g_cvl_conv_last_kernel = CVL_CK_NONE;
       const int lst = cvl_conv_igemm_l(d, 1, 0, src, dst, nullptr, (hipStream_t)stream, &b, workspace,

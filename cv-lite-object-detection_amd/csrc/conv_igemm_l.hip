@@ -197,7 +197,7 @@ int cvl_conv_igemm_p(const cvl_conv_desc* d, const ConvArgs& a, hipStream_t s);
 
 // Called by cvl_conv_igemm when the launch qualifies (see cvl_conv_igemm_l_ok); returns -1 when
 // it does not, so the caller falls back to the 128-row kernel.
-int cvl_conv_igemm_l(const cvl_conv_desc* d, int dst_up, int dst_w, const void* src, void* dst, double* bn_stats,
+int cvl_conv_igemm_l(const cvl_conv_desc* d, int dst_up, int dst_w, const void* src, void* dst, acc_u64* bn_stats,
                      hipStream_t s, const BnSumArgs* bsum, void* workspace, size_t workspace_bytes) {
   if (cvl_env_flag("CVL_CONV_NO_L")) return -1;
   if (bsum && (d->mode != CVL_CONV_DGRAD || d->dst_f32 || (d->beta != 0.f && !bsum->y) || dst_up != 1 || bn_stats))

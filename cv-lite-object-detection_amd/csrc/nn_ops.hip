@@ -253,16 +253,16 @@ __device__ __forceinline__ void bn_moments(double s1, double s2, int HW, float e
 }
 
 // running-stat EMA of one channel over the images in order (TF fused BN: unbiased variance)
-__device__ __forceinline__ void bn_running(const double* stats, int B, int C, int c, int HW, float eps,
+__device__ __forceinline__ void bn_running(const acc_u64* stats, int B, int C, int c, int HW, float eps,
                                            float momentum, float* run_mean, float* run_var) {
   float rm = run_mean[c], rv = run_var[c];
   for (int b0 = 0; b0 < B; b0 += 8) {       // 8 images' loads in flight, then the in-order EMA
     double s1[8], s2[8];
 #pragma unroll
     for (int u = 0; u < 8; ++u) {
-      const long i = ((long)min(b0 + u, B - 1) * C + c) * 2;
-      s1[u] = stats[i];
-      s2[u] = stats[i + 1];
+      const long bc = (long)min(b0 + u, B - 1) * C + c;
+      s1[u] = acc_value(stats + acc_idx(bc, 0));
+      s2[u] = acc_value(stats + acc_idx(bc, 1));
     }
 #pragma unroll
     for (int u = 0; u < 8; ++u) {
@@ -279,15 +279,16 @@ __device__ __forceinline__ void bn_running(const double* stats, int B, int C, in
   run_var[c] = rv;
 }
 
-// stats[b][c] = (sum, sumsq) -> mr[b][c] = (mean, rstd); running stats EMA, images in order.
-__global__ void bn_finalize_kernel(const double* stats, float* mr, float* run_mean, float* run_var,
+// stats[b][c] = (sum, sumsq) accumulators -> mr[b][c] = (mean, rstd); running stats EMA, images in order.
+__global__ void bn_finalize_kernel(const acc_u64* stats, float* mr, float* run_mean, float* run_var,
                                    int B, int C, int HW, float eps, float momentum) {
   const int c = blockIdx.x * NT + threadIdx.x;
   if (c >= C) return;
   for (int b = 0; b < B; ++b) {
     float mean, rstd;
     double var;
-    bn_moments(stats[((long)b * C + c) * 2], stats[((long)b * C + c) * 2 + 1], HW, eps, &mean, &rstd, &var);
+    const long bc = (long)b * C + c;
+    bn_moments(acc_value(stats + acc_idx(bc, 0)), acc_value(stats + acc_idx(bc, 1)), HW, eps, &mean, &rstd, &var);
     mr[((long)b * C + c) * 2] = mean;
     mr[((long)b * C + c) * 2 + 1] = rstd;
   }
@@ -301,7 +302,7 @@ __global__ void bn_finalize_kernel(const double* stats, float* mr, float* run_me
 // stats (same arithmetic as bn_finalize_kernel), chunk-0 blocks store them for the backward and
 // block (0, 0) advances the running statistics.
 struct BnFin {
-  const double* stats;
+  const acc_u64* stats;
   float* mr_out;
   float* run_mean;
   float* run_var;
@@ -332,7 +333,8 @@ __global__ void __launch_bounds__(NT) bn_apply_kernel(const cvl_bf16* __restrict
       const long bc = (long)b * C + c;
       float mm, rr;
       double var;
-      bn_moments(fin.stats[bc * 2], fin.stats[bc * 2 + 1], HW, fin.eps, &mm, &rr, &var);
+      bn_moments(acc_value(fin.stats + acc_idx(bc, 0)), acc_value(fin.stats + acc_idx(bc, 1)), HW, fin.eps, &mm, &rr,
+                 &var);
       smr[c] = float2{mm, rr};
       if (blockIdx.x == 0) { fin.mr_out[bc * 2] = mm; fin.mr_out[bc * 2 + 1] = rr; }
     }
@@ -424,7 +426,7 @@ struct BnPG {
   float* dbeta;
   float* conv_dbias;
   float beta_acc;
-  const double* psums;    // per-image sums for the parameter gradients (nullptr: `sums`)
+  const acc_u64* psums;   // per-image sums for the parameter gradients (nullptr: `sums`)
 };
 
 // MASK selects the ReLU-mask source at compile time (1: y, 2: bn_affine(z) recomputed, 3: no mask --
@@ -433,7 +435,7 @@ struct BnPG {
 template <int PASS, int MASK = 0>
 __global__ void __launch_bounds__(NT) bn_bwd_kernel(const cvl_bf16* __restrict__ dy, const cvl_bf16* __restrict__ y,
                                                     const cvl_bf16* __restrict__ z, const float* __restrict__ mr,
-                                                    const float* __restrict__ gamma, const double* __restrict__ sums,
+                                                    const float* __restrict__ gamma, const acc_u64* __restrict__ sums,
                                                     cvl_bf16* __restrict__ dz, cvl_bf16* __restrict__ g_out,
                                                     float* __restrict__ part, int C, int HW, int rows_per_blk,
                                                     int group, float dz_beta, BnPG pg,
@@ -451,14 +453,14 @@ __global__ void __launch_bounds__(NT) bn_bwd_kernel(const cvl_bf16* __restrict__
   const float inv = 1.0f / ((float)HW * (float)gsz);
   __shared__ float red[NT][17];
   if (PASS == 1 && pg.dgamma && b == 0) {          // spread over the image-0 blocks, a channel per thread
-    const double* ps = pg.psums ? pg.psums : sums;
+    const acc_u64* ps = pg.psums ? pg.psums : sums;
     for (int c = blockIdx.x * NT + threadIdx.x; c < C; c += gridDim.x * NT) {
       if (pg.conv_dbias) pg.conv_dbias[c] = 0.f;
       double a1 = 0.0, a2 = 0.0;
 #pragma unroll 8
       for (int bb = 0; bb < (int)gridDim.y; ++bb) {
-        a1 += ps[((long)bb * C + c) * 2];
-        a2 += ps[((long)bb * C + c) * 2 + 1];
+        a1 += acc_value(ps + acc_idx((long)bb * C + c, 0));
+        a2 += acc_value(ps + acc_idx((long)bb * C + c, 1));
       }
       pg.dbeta[c] = (float)a1 + (pg.beta_acc != 0.f ? pg.beta_acc * pg.dbeta[c] : 0.f);
       pg.dgamma[c] = (float)a2 + (pg.beta_acc != 0.f ? pg.beta_acc * pg.dgamma[c] : 0.f);
@@ -485,8 +487,8 @@ __global__ void __launch_bounds__(NT) bn_bwd_kernel(const cvl_bf16* __restrict__
       be[u] = zmask ? bnb[c0 + u] : 0.f;
       s1[u] = 0.f; s2[u] = 0.f;
       if (PASS == 1) {
-        k1[u] = (float)sums[bc * 2] * inv;          // mean(g)
-        k2[u] = (float)sums[bc * 2 + 1] * inv;      // mean(g * xhat)
+        k1[u] = (float)acc_value(sums + acc_idx(bc, 0)) * inv;     // mean(g)
+        k2[u] = (float)acc_value(sums + acc_idx(bc, 1)) * inv;     // mean(g * xhat)
         gm[u] = gamma[c0 + u] * rs[u];
       }
     }
@@ -574,9 +576,10 @@ __global__ void __launch_bounds__(NT) bn_bwd_kernel(const cvl_bf16* __restrict__
 
 
 // out[y][c][0..1] = sum_r part[y][r][c][0..1]: a block owns 32 channels (256 contiguous bytes per
-// row) and 8 row groups; the row groups are combined in a fixed order (deterministic, float64)
+// row) and 8 row groups; the row groups are combined in a fixed order (deterministic, float64) and
+// the total is stored exactly as an accumulator (bn_acc.h; the format the fused producers write)
 __global__ void __launch_bounds__(NT) bn_colsum_kernel(const float* __restrict__ part, int R, int C,
-                                                       double* __restrict__ out) {
+                                                       acc_u64* __restrict__ out) {
   const int y = blockIdx.y;
   const int cl = threadIdx.x & 31, rg = threadIdx.x >> 5;
   const int c = blockIdx.x * 32 + cl;
@@ -603,8 +606,9 @@ __global__ void __launch_bounds__(NT) bn_colsum_kernel(const float* __restrict__
   if (rg == 0 && c < C) {
     double t1 = 0.0, t2 = 0.0;
     for (int k = 0; k < 8; ++k) { t1 += red[k][cl][0]; t2 += red[k][cl][1]; }
-    out[((long)y * C + c) * 2] = t1;
-    out[((long)y * C + c) * 2 + 1] = t2;
+    AccLocal l;
+    l.zero(); l.add_f64(t1); l.store(out + acc_idx((long)y * C + c, 0));
+    l.zero(); l.add_f64(t2); l.store(out + acc_idx((long)y * C + c, 1));
   }
 }
 
@@ -1173,15 +1177,19 @@ __global__ void gather_rows_kernel(const int4* src, long row16, const int32_t* i
 // [g*G, min((g+1)*G, B)), the last may be short).  Running stats are updated once per group, in
 // group order, as the reference's sequential sub-batch forwards do.
 // ---------------------------------------------------------------------------------------------
-__global__ void bn_finalize_grouped_kernel(const double* stats, float* mr, float* run_mean, float* run_var,
+__global__ void bn_finalize_grouped_kernel(const acc_u64* stats, float* mr, float* run_mean, float* run_var,
                                            int B, int C, int HW, int group, float eps, float momentum) {
   const int c = blockIdx.x * NT + threadIdx.x;
   if (c >= C) return;
   float rm = run_mean ? run_mean[c] : 0.f, rv = run_var ? run_var[c] : 0.f;
   for (int g0 = 0; g0 < B; g0 += group) {
     const int g1 = min(g0 + group, B);
-    double s1 = 0.0, s2 = 0.0;
-    for (int b = g0; b < g1; ++b) { s1 += stats[((long)b * C + c) * 2]; s2 += stats[((long)b * C + c) * 2 + 1]; }
+    AccLocal l1, l2;                // the group's images summed exactly (integer bins), then decoded
+    l1.zero(); l2.zero();
+    for (int b = g0; b < g1; ++b) { l1.add(stats + acc_idx((long)b * C + c, 0)); l2.add(stats + acc_idx((long)b * C + c, 1)); }
+    acc_u64 t1[kAccSlots], t2[kAccSlots];
+    l1.store(t1); l2.store(t2);
+    const double s1 = acc_value(t1), s2 = acc_value(t2);
     const double n = (double)(g1 - g0) * HW;
     const double mean = s1 / n;
     double var = s2 / n - mean * mean;
@@ -1195,16 +1203,21 @@ __global__ void bn_finalize_grouped_kernel(const double* stats, float* mr, float
   if (run_mean) { run_mean[c] = rm; run_var[c] = rv; }
 }
 
-// gs[b][c] = sum over b's group of s[b'][c] (fixed order: deterministic)
-__global__ void bn_group_sum_kernel(const double* s, double* gs, int B, int C, int group) {
+__global__ void bn_acc_decode_kernel(const acc_u64* acc, double* out, long n) {
+  for (long i = blockIdx.x * (long)NT + threadIdx.x; i < n; i += (long)gridDim.x * NT) out[i] = acc_value(acc + i * kAccSlots);
+}
+
+// gs[b][c] = sum over b's group of s[b'][c] (integer bin sums: exact)
+__global__ void bn_group_sum_kernel(const acc_u64* s, acc_u64* gs, int B, int C, int group) {
   const long i = blockIdx.x * (long)NT + threadIdx.x;
   if (i >= (long)B * C) return;
   const int b = (int)(i / C), c = (int)(i - (long)b * C);
   const int g0 = (b / group) * group, g1 = min(g0 + group, B);
-  double a1 = 0.0, a2 = 0.0;
-  for (int k = g0; k < g1; ++k) { a1 += s[((long)k * C + c) * 2]; a2 += s[((long)k * C + c) * 2 + 1]; }
-  gs[i * 2] = a1;
-  gs[i * 2 + 1] = a2;
+  AccLocal a1, a2;
+  a1.zero(); a2.zero();
+  for (int k = g0; k < g1; ++k) { a1.add(s + acc_idx((long)k * C + c, 0)); a2.add(s + acc_idx((long)k * C + c, 1)); }
+  a1.store(gs + acc_idx(i, 0));
+  a2.store(gs + acc_idx(i, 1));
 }
 
 }  // namespace
@@ -1264,10 +1277,17 @@ extern "C" int cvl_im2col(const float* x, int B, int H, int W, int C, int KH, in
   return cvl_launch_status();
 }
 
-extern "C" int cvl_bn_finalize(const double* stats, float* mean_rstd, float* run_mean, float* run_var,
+extern "C" int cvl_bn_acc_decode(const uint64_t* acc, double* out, int64_t n, cvl_stream_t stream) {
+  CVL_CHECK_ARG(acc && out && n >= 0);
+  if (n == 0) return CVL_OK;
+  hipLaunchKernelGGL(bn_acc_decode_kernel, dim3(grid_for(n)), dim3(NT), 0, S_, (const acc_u64*)acc, out, (long)n);
+  return cvl_launch_status();
+}
+
+extern "C" int cvl_bn_finalize(const uint64_t* stats, float* mean_rstd, float* run_mean, float* run_var,
                                int B, int C, int HW, float eps, float momentum, cvl_stream_t stream) {
   CVL_CHECK_ARG(stats && mean_rstd && B > 0 && C > 0 && HW > 0);
-  hipLaunchKernelGGL(bn_finalize_kernel, dim3((C + NT - 1) / NT), dim3(NT), 0, S_, stats, mean_rstd,
+  hipLaunchKernelGGL(bn_finalize_kernel, dim3((C + NT - 1) / NT), dim3(NT), 0, S_, (const acc_u64*)stats, mean_rstd,
                      run_mean, run_var, B, C, HW, eps, momentum);
   return cvl_launch_status();
 }
@@ -1283,7 +1303,7 @@ extern "C" int cvl_bn_apply(const void* z, const float* mean_rstd, const float* 
   return cvl_launch_status();
 }
 
-extern "C" int cvl_bn_finalize_apply(const double* stats, float* mean_rstd, float* run_mean, float* run_var,
+extern "C" int cvl_bn_finalize_apply(const uint64_t* stats, float* mean_rstd, float* run_mean, float* run_var,
                                      const void* z, const float* gamma, const float* beta, const void* residual,
                                      void* y, int B, int HW, int C, int relu, float eps, float momentum,
                                      cvl_stream_t stream) {
@@ -1293,7 +1313,7 @@ extern "C" int cvl_bn_finalize_apply(const double* stats, float* mean_rstd, floa
   const int rpb = bn_rows_per_blk(B, HW, C);
   hipLaunchKernelGGL(bn_apply_kernel<true>, dim3((HW + rpb - 1) / rpb, B), dim3(NT), 0, S_, (const cvl_bf16*)z,
                      (const float*)nullptr, gamma, beta, (const cvl_bf16*)residual, (cvl_bf16*)y, C, HW, relu, rpb,
-                     BnFin{stats, mean_rstd, run_mean, run_var, eps, momentum});
+                     BnFin{(const acc_u64*)stats, mean_rstd, run_mean, run_var, eps, momentum});
   return cvl_launch_status();
 }
 
@@ -1301,7 +1321,8 @@ extern "C" size_t cvl_bn_backward_workspace_size(int B, int HW, int C) {
   if (B <= 0 || HW <= 0 || C <= 0) return 0;
   const int rpb = bn_bwd_rows_per_blk(B, HW, C);
   const int nchunk = (HW + rpb - 1) / rpb;
-  return sizeof(double) * 2 * ((size_t)B * C + C) + sizeof(float) * 2 * 2 * (size_t)B * nchunk * C;
+  return sizeof(acc_u64) * 2 * kAccSlots * (size_t)B * C + sizeof(double) * 2 * (size_t)C +
+         sizeof(float) * 2 * 2 * (size_t)B * nchunk * C;
 }
 
 static int bn_backward_impl(const void* dy, const void* y_relu, const float* bn_beta, const void* z,
@@ -1313,23 +1334,23 @@ static int bn_backward_impl(const void* dy, const void* y_relu, const float* bn_
   CVL_CHECK_ARG(workspace_bytes >= cvl_bn_backward_workspace_size(B, HW, C));
   const int rpb = bn_bwd_rows_per_blk(B, HW, C);
   const int nchunk = (HW + rpb - 1) / rpb;
-  // workspace: sums [B][C][2] f64 | (unused [C][2] f64) | pass-0 partials [B][nchunk][C][2] f32
-  double* sums = reinterpret_cast<double*>(workspace);
-  double* dbsum = sums + 2 * (size_t)B * C;
+  // workspace: sums [B][C][2][8] accumulators | (unused [C][2] f64) | pass-0 partials [B][nchunk][C][2] f32
+  acc_u64* sums = reinterpret_cast<acc_u64*>(workspace);
+  double* dbsum = reinterpret_cast<double*>(sums + 2 * kAccSlots * (size_t)B * C);
   float* part0 = reinterpret_cast<float*>(dbsum + 2 * (size_t)C);
   dim3 g1(nchunk, B);
   const bool ym = y_relu != nullptr, zm = !ym && bn_beta != nullptr;
   auto k0 = ym ? bn_bwd_kernel<0, 1> : zm ? bn_bwd_kernel<0, 2> : bn_bwd_kernel<0, 3>;
   auto k1 = ym ? bn_bwd_kernel<1, 1> : zm ? bn_bwd_kernel<1, 2> : bn_bwd_kernel<1, 3>;
   hipLaunchKernelGGL(k0, g1, dim3(NT), 0, S_, (const cvl_bf16*)dy, (const cvl_bf16*)y_relu,
-                     (const cvl_bf16*)z, mean_rstd, gamma, (const double*)nullptr, (cvl_bf16*)nullptr,
+                     (const cvl_bf16*)z, mean_rstd, gamma, (const acc_u64*)nullptr, (cvl_bf16*)nullptr,
                      (cvl_bf16*)nullptr, part0, C, HW, rpb, 1, 0.f, BnPG{}, bn_beta, act_hi);
   hipLaunchKernelGGL(bn_colsum_kernel, dim3((C + 31) / 32, B), dim3(NT), 0, S_, (const float*)part0, nchunk, C,
                      sums);
   // pass 1 is elementwise (no partials): the apply kernels' finer chunking (~2048 workgroups)
   const int rpb1 = bn_rows_per_blk(B, HW, C);
   hipLaunchKernelGGL(k1, dim3((HW + rpb1 - 1) / rpb1, B), dim3(NT), 0, S_, (const cvl_bf16*)dy, (const cvl_bf16*)y_relu,
-                     (const cvl_bf16*)z, mean_rstd, gamma, (const double*)sums, (cvl_bf16*)dz, (cvl_bf16*)g_out,
+                     (const cvl_bf16*)z, mean_rstd, gamma, (const acc_u64*)sums, (cvl_bf16*)dz, (cvl_bf16*)g_out,
                      (float*)nullptr, C, HW, rpb1, 1, 0.f, BnPG{dgamma, dbeta, conv_dbias, beta_acc}, bn_beta,
                      act_hi);
   return cvl_launch_status();
@@ -1365,7 +1386,7 @@ extern "C" int cvl_bn_backward_relu6(const void* dy, const void* z, const float*
 // epilogue formed (cvl_conv_igemm_dgrad_bnsum): BN -> ReLU (act_hi = INF) or ReLU6 (act_hi = 6)
 // unit without a residual, mask rebuilt from z.
 extern "C" int cvl_bn_backward_relu_sums(const void* dy, const void* z, const float* mean_rstd, const float* gamma,
-                                         const float* beta, const double* sums, void* dz, float* dgamma,
+                                         const float* beta, const uint64_t* sums, void* dz, float* dgamma,
                                          float* dbeta, float beta_acc, float* conv_dbias, float act_hi, int B,
                                          int HW, int C, cvl_stream_t stream) {
   CVL_CHECK_ARG(dy && z && mean_rstd && gamma && beta && sums && dz && dgamma && dbeta && C % 8 == 0);
@@ -1373,7 +1394,7 @@ extern "C" int cvl_bn_backward_relu_sums(const void* dy, const void* z, const fl
   const int rpb = bn_rows_per_blk(B, HW, C);
   const int nchunk = (HW + rpb - 1) / rpb;
   hipLaunchKernelGGL((bn_bwd_kernel<1, 2>), dim3(nchunk, B), dim3(NT), 0, S_, (const cvl_bf16*)dy, (const cvl_bf16*)nullptr,
-                     (const cvl_bf16*)z, mean_rstd, gamma, sums, (cvl_bf16*)dz, (cvl_bf16*)nullptr, (float*)nullptr,
+                     (const cvl_bf16*)z, mean_rstd, gamma, (const acc_u64*)sums, (cvl_bf16*)dz, (cvl_bf16*)nullptr, (float*)nullptr,
                      C, HW, rpb, 1, 0.f, BnPG{dgamma, dbeta, conv_dbias, beta_acc}, beta, act_hi);
   return cvl_launch_status();
 }
@@ -1381,7 +1402,7 @@ extern "C" int cvl_bn_backward_relu_sums(const void* dy, const void* z, const fl
 // Second pass only for a residual unit (mask y > 0, g_out = the masked gradient for the shortcut),
 // from the (sum g, sum g*xhat) the producing data gradient formed (cvl_conv_igemm_dgrad_bnsum_res).
 extern "C" int cvl_bn_backward_res_sums(const void* dy, const void* y, const void* z, const float* mean_rstd,
-                                        const float* gamma, const double* sums, void* dz, void* g_out,
+                                        const float* gamma, const uint64_t* sums, void* dz, void* g_out,
                                         float* dgamma, float* dbeta, float beta_acc, float* conv_dbias, int B,
                                         int HW, int C, cvl_stream_t stream) {
   CVL_CHECK_ARG(dy && y && z && mean_rstd && gamma && sums && dz && dgamma && dbeta && C % 8 == 0);
@@ -1389,7 +1410,7 @@ extern "C" int cvl_bn_backward_res_sums(const void* dy, const void* y, const voi
   const int rpb = bn_rows_per_blk(B, HW, C);
   const int nchunk = (HW + rpb - 1) / rpb;
   hipLaunchKernelGGL((bn_bwd_kernel<1, 1>), dim3(nchunk, B), dim3(NT), 0, S_, (const cvl_bf16*)dy, (const cvl_bf16*)y,
-                     (const cvl_bf16*)z, mean_rstd, gamma, sums, (cvl_bf16*)dz, (cvl_bf16*)g_out, (float*)nullptr,
+                     (const cvl_bf16*)z, mean_rstd, gamma, (const acc_u64*)sums, (cvl_bf16*)dz, (cvl_bf16*)g_out, (float*)nullptr,
                      C, HW, rpb, 1, 0.f, BnPG{dgamma, dbeta, conv_dbias, beta_acc}, (const float*)nullptr, INFINITY);
   return cvl_launch_status();
 }
@@ -1565,7 +1586,7 @@ extern "C" size_t cvl_bn_stats_workspace_size(int B, int HW, int C) {
   return sizeof(float) * 2 * (size_t)B * nchunk * C;
 }
 
-extern "C" int cvl_bn_stats(const void* x, int B, int HW, int C, double* stats, void* workspace,
+extern "C" int cvl_bn_stats(const void* x, int B, int HW, int C, uint64_t* stats, void* workspace,
                             size_t workspace_bytes, cvl_stream_t stream) {
   CVL_CHECK_ARG(x && stats && workspace && C % 8 == 0 && B > 0 && HW > 0);
   CVL_CHECK_ARG(workspace_bytes >= cvl_bn_stats_workspace_size(B, HW, C));
@@ -1574,25 +1595,25 @@ extern "C" int cvl_bn_stats(const void* x, int B, int HW, int C, double* stats, 
   float* part = reinterpret_cast<float*>(workspace);
   hipLaunchKernelGGL(bn_bwd_kernel<2>, dim3(nchunk, B), dim3(NT), 0, S_, (const cvl_bf16*)x,
                      (const cvl_bf16*)nullptr, (const cvl_bf16*)nullptr, (const float*)nullptr, (const float*)nullptr,
-                     (const double*)nullptr, (cvl_bf16*)nullptr, (cvl_bf16*)nullptr, part, C, HW, rpb, 1, 0.f, BnPG{},
+                     (const acc_u64*)nullptr, (cvl_bf16*)nullptr, (cvl_bf16*)nullptr, part, C, HW, rpb, 1, 0.f, BnPG{},
                      (const float*)nullptr, INFINITY);
   hipLaunchKernelGGL(bn_colsum_kernel, dim3((C + 31) / 32, B), dim3(NT), 0, S_, (const float*)part, nchunk, C,
-                     stats);
+                     (acc_u64*)stats);
   return cvl_launch_status();
 }
 
-extern "C" int cvl_bn_finalize_grouped(const double* stats, float* mean_rstd, float* run_mean, float* run_var,
+extern "C" int cvl_bn_finalize_grouped(const uint64_t* stats, float* mean_rstd, float* run_mean, float* run_var,
                                        int B, int C, int HW, int group, float eps, float momentum,
                                        cvl_stream_t stream) {
   CVL_CHECK_ARG(stats && mean_rstd && B > 0 && C > 0 && HW > 0 && group > 0);
-  hipLaunchKernelGGL(bn_finalize_grouped_kernel, dim3((C + NT - 1) / NT), dim3(NT), 0, S_, stats, mean_rstd,
+  hipLaunchKernelGGL(bn_finalize_grouped_kernel, dim3((C + NT - 1) / NT), dim3(NT), 0, S_, (const acc_u64*)stats, mean_rstd,
                      run_mean, run_var, B, C, HW, group, eps, momentum);
   return cvl_launch_status();
 }
 
 extern "C" size_t cvl_bn_backward_grouped_workspace_size(int B, int HW, int C) {
   if (B <= 0 || HW <= 0 || C <= 0) return 0;
-  return cvl_bn_backward_workspace_size(B, HW, C) + sizeof(double) * 2 * (size_t)B * C;
+  return cvl_bn_backward_workspace_size(B, HW, C) + sizeof(acc_u64) * 2 * kAccSlots * (size_t)B * C;
 }
 
 extern "C" int cvl_bn_backward_grouped(const void* dy, const void* y_relu, const void* z, const float* mean_rstd,
@@ -1604,22 +1625,22 @@ extern "C" int cvl_bn_backward_grouped(const void* dy, const void* y_relu, const
   CVL_CHECK_ARG(workspace_bytes >= cvl_bn_backward_grouped_workspace_size(B, HW, C));
   const int rpb = bn_bwd_rows_per_blk(B, HW, C);
   const int nchunk = (HW + rpb - 1) / rpb;
-  // workspace: sums [B][C][2] f64 | [C][2] f64 | partials [B][nchunk][C][2] f32 | group sums [B][C][2] f64
-  double* sums = reinterpret_cast<double*>(workspace);
-  double* dbsum = sums + 2 * (size_t)B * C;
+  // workspace: sums [B][C][2][8] | [C][2] f64 | partials [B][nchunk][C][2] f32 | group sums [B][C][2][8]
+  acc_u64* sums = reinterpret_cast<acc_u64*>(workspace);
+  double* dbsum = reinterpret_cast<double*>(sums + 2 * kAccSlots * (size_t)B * C);
   float* part0 = reinterpret_cast<float*>(dbsum + 2 * (size_t)C);
-  double* gsums = reinterpret_cast<double*>(reinterpret_cast<char*>(workspace) +
-                                            cvl_bn_backward_workspace_size(B, HW, C));
+  acc_u64* gsums = reinterpret_cast<acc_u64*>(reinterpret_cast<char*>(workspace) +
+                                              cvl_bn_backward_workspace_size(B, HW, C));
   dim3 g1(nchunk, B);
   hipLaunchKernelGGL(bn_bwd_kernel<0>, g1, dim3(NT), 0, S_, (const cvl_bf16*)dy, (const cvl_bf16*)y_relu,
-                     (const cvl_bf16*)z, mean_rstd, gamma, (const double*)nullptr, (cvl_bf16*)nullptr,
+                     (const cvl_bf16*)z, mean_rstd, gamma, (const acc_u64*)nullptr, (cvl_bf16*)nullptr,
                      (cvl_bf16*)nullptr, part0, C, HW, rpb, group, 0.f, BnPG{}, (const float*)nullptr, INFINITY);
   hipLaunchKernelGGL(bn_colsum_kernel, dim3((C + 31) / 32, B), dim3(NT), 0, S_, (const float*)part0, nchunk, C,
                      sums);
-  const double* use = sums;
+  const acc_u64* use = sums;
   if (group > 1) {
     hipLaunchKernelGGL(bn_group_sum_kernel, dim3((int)(((long)B * C + NT - 1) / NT)), dim3(NT), 0, S_,
-                       (const double*)sums, gsums, B, C, group);
+                       (const acc_u64*)sums, gsums, B, C, group);
     use = gsums;
   }
   hipLaunchKernelGGL(bn_bwd_kernel<1>, g1, dim3(NT), 0, S_, (const cvl_bf16*)dy, (const cvl_bf16*)y_relu,

@@ -141,9 +141,10 @@ __global__ void __launch_bounds__(NT) conv_stats_f32_kernel(ConvArgs a) {
   if (rg == 0 && c < a.n_store) {
     double t1 = 0.0, t2 = 0.0;
     for (int k = 0; k < 4; ++k) { t1 += red[k][cl][0]; t2 += red[k][cl][1]; }
-    double* st = a.stats + ((long)img * a.n_store + c) * 2;
-    st[0] += t1;
-    st[1] += t2;
+    acc_u64* st = a.stats + acc_idx((long)img * a.n_store + c, 0);
+    AccLocal l1, l2;                    // one writer per (image, channel): add onto what is there
+    l1.zero(); l1.add(st); l1.add_f64(t1); l1.store(st);
+    l2.zero(); l2.add(st + kAccSlots); l2.add_f64(t2); l2.store(st + kAccSlots);
   }
 }
 
@@ -482,7 +483,7 @@ __global__ void __launch_bounds__(NT) bias_grad_f32_kernel(BiasF32 m) {
 }  // namespace
 
 // ---- conv entry points (dispatched from cvl_conv_igemm / cvl_conv_wgrad_grouped on prec) ------
-int cvl_conv_f32(const cvl_conv_desc* d, const void* src, void* dst, double* bn_stats, hipStream_t s) {
+int cvl_conv_f32(const cvl_conv_desc* d, const void* src, void* dst, acc_u64* bn_stats, hipStream_t s) {
   ConvArgs a;
   int st = cvl_conv_prepare(d, FT, &a);
   if (st) return st;
@@ -543,7 +544,7 @@ extern "C" int cvl_bn_apply_f32(const float* z, const float* mean_rstd, const fl
   return cvl_launch_status();
 }
 
-extern "C" int cvl_bn_finalize_apply_f32(const double* stats, float* mean_rstd, float* run_mean, float* run_var,
+extern "C" int cvl_bn_finalize_apply_f32(const uint64_t* stats, float* mean_rstd, float* run_mean, float* run_var,
                                          const float* z, const float* gamma, const float* beta, const float* residual,
                                          float* y, int B, int HW, int C, int relu, float eps, float momentum,
                                          cvl_stream_t stream) {

@@ -183,7 +183,7 @@ def _bn_forward(bn, t, B, HW, group, train, relu=False):
     c = bn.c
     mr = torch.empty((B, c, 2), dtype=torch.float32, device=t.device)
     if train:
-        stats = torch.empty((B, c, 2), dtype=torch.float64, device=t.device)
+        stats = nn.bn_acc(B, c, t.device, zero=False)
         nn.bn_stats(t, B, HW, c, stats)
         nn.bn_finalize_grouped(stats, mr, bn.run_mean, bn.run_var, B, c, HW, group, bn.eps, bn.momentum)
     else:                                        # Keras inference: moving statistics

@@ -234,7 +234,7 @@ class Conv(object):
         y = bn_next[5] if len(bn_next) > 5 else None       # residual unit: mask y > 0 (bn_res_ctx)
         zero = sums is None
         if zero:
-            sums = torch.empty((B, self.cin, 2), dtype=torch.float64, device=dy.device)
+            sums = nn.bn_acc(B, self.cin, dy.device, zero=False)
         if y is not None:
             fused = nn.conv_igemm_dgrad_bnsum_res(d, dy, out, y, z, mr, ga, be, sums, zero=zero)
         else:
@@ -249,17 +249,18 @@ FUSE_BNSUM = os.environ.get("CVL_NO_BNSUM_FUSE", "0") != "1"
 FUSE_BNSUM_RES = FUSE_BNSUM and os.environ.get("CVL_NO_BNSUM_RES", "0") != "1"
 
 class StatsArena(object):
-    """One zeroed float64 buffer holding the (sum, sumsq) BN statistics of every conv of a forward
-    pass (one memset per step instead of one per BN)."""
+    """One zeroed buffer holding the (sum, sumsq) BN statistics of every conv of a forward pass as
+    exact accumulators (nn.bn_acc: [B][C][2][8] uint64, order-independent), one memset per step
+    instead of one per BN.  n_stats = statistics (2 per image and channel) it can hand out."""
 
-    def __init__(self, n_doubles, device):
-        self.buf = torch.zeros(n_doubles, dtype=torch.float64, device=device)
+    def __init__(self, n_stats, device):
+        self.buf = torch.zeros(n_stats * nn.ACC_SLOTS, dtype=torch.int64, device=device)
         self.off = 0
 
     def take(self, B, c):
-        n = B * c * 2
+        n = B * c * 2 * nn.ACC_SLOTS
         assert self.off + n <= self.buf.numel(), "stats arena too small"
-        v = self.buf[self.off:self.off + n].view(B, c, 2)
+        v = self.buf[self.off:self.off + n].view(B, c, 2, nn.ACC_SLOTS)
         self.off += n
         return v
 
@@ -322,8 +323,7 @@ class ConvBN(object):
         Ho, Wo, _, _ = self.conv.out_hw(H, W)
         stats = None
         if train:
-            stats = arena.take(B, c) if arena is not None else torch.zeros((B, c, 2), dtype=torch.float64,
-                                                                             device=x.device)
+            stats = arena.take(B, c) if arena is not None else nn.bn_acc(B, c, x.device)
         z, _, _ = self.conv.fwd(x, B, H, W, stats=stats)
         y, mr = self.bn.normalize(z, stats, B, Ho * Wo, relu, residual=residual, train=train)
         return y, (x, z, y, mr, B, H, W, Ho, Wo, relu, residual is not None)

@@ -200,6 +200,55 @@ def im2col(x, KH, KW, stride, pad_t, pad_l, Ho, Wo, Kp, out):
     _lib.call("cvl_im2col", ptr(x), B, H, W, C, KH, KW, stride, pad_t, pad_l, Ho, Wo, Kp, ptr(out), stream())
 
 
+# BN statistics are exact, order-independent accumulators (include/cvlite.h "BN accumulators";
+# csrc/bn_acc.h): per statistic ACC_SLOTS uint64 (7 exponent bins + a non-finite count), a (B, C)
+# buffer is int64 [B][C][2][ACC_SLOTS]
+ACC_SLOTS = 8
+ACC_BINS, ACC_W, ACC_E0 = 7, 22, 27
+
+
+def bn_acc(B, C, device, zero=True):
+    """A (B, C) BN statistics buffer ((sum, sumsq) or (sum g, sum g*xhat)) for the producing kernels."""
+    f = torch.zeros if zero else torch.empty
+    return f((B, C, 2, ACC_SLOTS), dtype=torch.int64, device=device)
+
+
+def bn_acc_value(acc):
+    """float64 values [..., 2] of a BN accumulator buffer [..., 2, ACC_SLOTS] (cvl_bn_acc_decode)."""
+    acc = acc.contiguous()
+    out = torch.empty(acc.shape[:-1], dtype=torch.float64, device=acc.device)
+    _lib.call("cvl_bn_acc_decode", ptr(acc), ptr(out), out.numel(), stream())
+    return out
+
+
+def _acc_add_f32(bins, f):
+    """bins[..., k] += the exact integer of float32 f in bin k (bn_acc.h acc_split), torch ops."""
+    u = f.contiguous().view(torch.int32).to(torch.int64) & 0xffffffff
+    e = (u >> 23) & 0xff
+    r = e - ACC_E0
+    k = torch.div(r.clamp(min=0), ACC_W, rounding_mode="floor")
+    bad = (e == 255) | ((e != 0) & (r >= 0) & (k >= ACC_BINS))
+    ok = (e != 0) & (r >= 0) & (k < ACC_BINS)
+    m = ((u & 0x7fffff) | 0x800000) << (r - k * ACC_W).clamp(min=0)
+    v = torch.where((u >> 31) == 1, -m, m)
+    bins.scatter_add_(-1, torch.where(ok, k, 0).unsqueeze(-1), torch.where(ok, v, 0).unsqueeze(-1))
+    bins[..., ACC_BINS] += bad.to(torch.int64)
+
+
+def bn_acc_encode(values):
+    """float64 statistic values [..., 2] -> an exact accumulator buffer [..., 2, ACC_SLOTS] (each value
+    split into three float32 pieces as bn_acc.h acc_add_f64; for callers that hold the sums already)."""
+    v = values.to(torch.float64)
+    out = torch.zeros(v.shape + (ACC_SLOTS,), dtype=torch.int64, device=v.device)
+    hi = v.to(torch.float32)
+    r = v - hi.double()
+    mid = r.to(torch.float32)
+    lo = (r - mid.double()).to(torch.float32)
+    for piece in (hi, mid, lo):
+        _acc_add_f32(out, piece)
+    return out
+
+
 def bn_finalize(stats, mean_rstd, run_mean, run_var, B, C, HW, eps, momentum):
     _lib.call("cvl_bn_finalize", ptr(stats), ptr(mean_rstd), ptr(run_mean), ptr(run_var), B, C, HW,
               float(eps), float(momentum), stream())
@@ -277,7 +326,7 @@ def depthwise_wgrad(x, dy, dw, k, stride, pad_t, pad_l, beta=0.0):
 
 def conv_igemm_dgrad_bnsum(desc, src, dst, z, mean_rstd, gamma, beta, sums, act_hi=float("inf"), zero=True):
     """DGRAD conv whose epilogue also forms the next BN's backward first pass into `sums`
-    [B][C][2] float64 (zeroed here first unless zero=False: the caller's buffer is already zero).
+    (bn_acc [B][C][2][8], zeroed here first unless zero=False: the caller's buffer is already zero).
     Returns True when fused; False = the plain data gradient ran and `sums` is untouched (run the
     two-pass BN backward)."""
     _prec(desc, src)

@@ -62,8 +62,7 @@ class Stem(object):
         act = self.conv.store.act
         stats = None
         if train:
-            stats = arena.take(B, 64) if arena is not None else torch.zeros((B, 64, 2), dtype=torch.float64,
-                                                                              device=x.device)
+            stats = arena.take(B, 64) if arena is not None else nn.bn_acc(B, 64, x.device)
         z = torch.empty((B, Ho, Wo, 64), dtype=act, device=x.device)
         if act == BF16:
             A = torch.empty((B * Ho * Wo, STEM_KP), dtype=BF16, device=x.device)

@@ -117,9 +117,20 @@ int cvl_fcos_center_v1_assign(const float* boxes, const int32_t* nbox, const flo
  * Weights: FWD  -> packed [Npad][KH*KW*Cin]   (cvl_pack_conv_weights w_fwd)
  *          DGRAD-> packed [Npad=Cin_pad][KH*KW*Cout_pad] (w_dgrad); then `Cin` = Cout_pad.
  * TF "same" padding: pad_t/pad_l = floor(total/2) (asymmetric for stride 2).
- * bn_stats (nullable) receives per-(image, out channel) (sum, sumsq) in float64 (atomic adds;
+ * bn_stats (nullable) receives per-(image, out channel) (sum, sumsq) as BN accumulators (below;
  * zero it first), which requires H*W % 4 == 0.
+ *
+ * BN accumulators (cvl_bn_acc): the statistics many workgroups add into one (image, channel) --
+ * (sum, sumsq) of a conv output, (sum g, sum g*xhat) of a BN backward -- are kept EXACTLY and
+ * order-independently: each fp32 partial is added as an integer into one of 7 uint64 bins chosen
+ * by its exponent (bin k holds multiples of 2^(22k - 123); partials below 2^-100 are dropped, slot
+ * 7 counts non-finite ones), so the result is bit-identical whatever order the atomics land in.
+ * Layout: uint64 [B][C][2][CVL_BN_ACC_SLOTS]; the value of a statistic is
+ * sum_k (double)(int64)slot[k] * 2^(22k - 123) over k = 0..6 in that order (NaN if slot[7] != 0);
+ * cvl_bn_acc_decode writes those values as float64 [n].
  * ---------------------------------------------------------------------------------------- */
+#define CVL_BN_ACC_SLOTS 8
+int cvl_bn_acc_decode(const uint64_t* acc, double* out, int64_t n, cvl_stream_t stream);
 #define CVL_CONV_MAX_SEG 10
 enum { CVL_CONV_FWD = 0, CVL_CONV_DGRAD = 1 };
 
@@ -157,7 +168,7 @@ enum { CVL_PREC_BF16 = 0, CVL_PREC_F32 = 1 };
 /* workspace (optional, >= cvl_conv_igemm_workspace_size(d) bytes) enables split-K for grids too
  * small to fill the GPU (fp32 partial slabs + a finishing pass); NULL = no split. */
 size_t cvl_conv_igemm_workspace_size(const cvl_conv_desc* d);
-int cvl_conv_igemm(const cvl_conv_desc* d, const void* src, void* dst, double* bn_stats,
+int cvl_conv_igemm(const cvl_conv_desc* d, const void* src, void* dst, uint64_t* bn_stats,
                    void* workspace, size_t workspace_bytes, cvl_stream_t stream);
 
 /* Test / profiling hook: the kernel variant the last cvl_conv_igemm / cvl_conv_wgrad* call on THIS
@@ -228,16 +239,17 @@ int cvl_im2col(const float* x, int B, int H, int W, int C, int KH, int KW, int s
 /* ------------------------------------------------------------------------------------------
  * BatchNormalization in training mode with per-image statistics (the reference forwards one
  * image at a time, train_fcos.py:137-153; Keras eps 1.001e-5, momentum 0.99, running variance
- * unbiased as TF's fused kernel).  stats from cvl_conv_igemm(bn_stats); mean_rstd [B][C][2].
+ * unbiased as TF's fused kernel).  stats: BN accumulators [B][C][2][8] from cvl_conv_igemm(bn_stats)
+ * or cvl_bn_stats; mean_rstd [B][C][2].
  * ---------------------------------------------------------------------------------------- */
-int cvl_bn_finalize(const double* stats, float* mean_rstd, float* run_mean, float* run_var, int B,
+int cvl_bn_finalize(const uint64_t* stats, float* mean_rstd, float* run_mean, float* run_var, int B,
                     int C, int HW, float eps, float momentum, cvl_stream_t stream);
 int cvl_bn_apply(const void* z, const float* mean_rstd, const float* gamma, const float* beta,
                  const void* residual, void* y, int B, int HW, int C, int relu, cvl_stream_t stream);
 /* cvl_bn_finalize + cvl_bn_apply in ONE launch (bit-identical results): every block derives the
  * (mean, rstd) of its image from stats; mean_rstd is still written for the backward and the running
  * statistics advanced (run_mean/run_var NULL together: inference-style, no EMA). */
-int cvl_bn_finalize_apply(const double* stats, float* mean_rstd, float* run_mean, float* run_var,
+int cvl_bn_finalize_apply(const uint64_t* stats, float* mean_rstd, float* run_mean, float* run_var,
                           const void* z, const float* gamma, const float* beta, const void* residual, void* y,
                           int B, int HW, int C, int relu, float eps, float momentum, cvl_stream_t stream);
 /* dy: grad of y; y_relu: y when the unit ends in ReLU (mask), else NULL; writes dz (bf16),
@@ -262,17 +274,17 @@ int cvl_bn_backward_relu(const void* dy, const void* z, const float* mean_rstd, 
  * result is dy of a BN -> ReLU (act_hi = INFINITY) / ReLU6 (act_hi = 6) unit without a residual
  * (the bottleneck's conv1 / conv2 units: their dy has one producer) and, when the 256-row
  * LDS-DMA kernel takes the launch with one image per tile, adds per (image, channel)
- * (sum g, sum g*xhat), g = dy * mask(bn(z)), into sums [B][C][2] float64 (zero it first) and sets
+ * (sum g, sum g*xhat), g = dy * mask(bn(z)), into sums (BN accumulators [B][C][2][8], zero them first) and sets
  * *fused (HOST) = 1; otherwise it runs the plain data gradient and sets *fused = 0.  z / mean_rstd
  * / gamma / beta are the unit's pre-BN conv output (same layout as dst), (mean, rstd) [B][C][2]
  * and BN parameters.  cvl_bn_backward_relu_sums is cvl_bn_backward_relu's second pass from those
  * sums (the first pass and its reduction are skipped). */
 int cvl_conv_igemm_dgrad_bnsum(const cvl_conv_desc* d, const void* src, void* dst, const void* z,
                                const float* mean_rstd, const float* gamma, const float* beta, float act_hi,
-                               double* sums, int32_t* fused, void* workspace, size_t workspace_bytes,
+                               uint64_t* sums, int32_t* fused, void* workspace, size_t workspace_bytes,
                                cvl_stream_t stream);
 int cvl_bn_backward_relu_sums(const void* dy, const void* z, const float* mean_rstd, const float* gamma,
-                              const float* beta, const double* sums, void* dz, float* dgamma, float* dbeta,
+                              const float* beta, const uint64_t* sums, void* dz, float* dgamma, float* dbeta,
                               float beta_acc, float* conv_dbias, float act_hi, int B, int HW, int C,
                               cvl_stream_t stream);
 /* The residual-unit form (a bottleneck's BN3: BN -> + shortcut -> ReLU, the block output y).  The
@@ -283,10 +295,10 @@ int cvl_bn_backward_relu_sums(const void* dy, const void* z, const float* mean_r
  * backward's second pass from the sums: dz, g_out (= g, the shortcut's gradient) and dgamma/dbeta
  * (replaces cvl_bn_backward with y_relu given). */
 int cvl_conv_igemm_dgrad_bnsum_res(const cvl_conv_desc* d, const void* src, void* dst, const void* y, const void* z,
-                                   const float* mean_rstd, const float* gamma, const float* beta, double* sums,
+                                   const float* mean_rstd, const float* gamma, const float* beta, uint64_t* sums,
                                    int32_t* fused, void* workspace, size_t workspace_bytes, cvl_stream_t stream);
 int cvl_bn_backward_res_sums(const void* dy, const void* y, const void* z, const float* mean_rstd, const float* gamma,
-                             const double* sums, void* dz, void* g_out, float* dgamma, float* dbeta, float beta_acc,
+                             const uint64_t* sums, void* dz, void* g_out, float* dgamma, float* dbeta, float beta_acc,
                              float* conv_dbias, int B, int HW, int C, cvl_stream_t stream);
 
 /* BN -> ReLU6 unit without a residual (MobileNetV2: Keras ReLU(6.)): as cvl_bn_backward_relu with
@@ -350,7 +362,7 @@ int cvl_bias_grad_multi(const cvl_bias_item* items, int n, void* workspace, size
  * ---------------------------------------------------------------------------------------- */
 int cvl_bn_apply_f32(const float* z, const float* mean_rstd, const float* gamma, const float* beta,
                      const float* residual, float* y, int B, int HW, int C, int relu, cvl_stream_t stream);
-int cvl_bn_finalize_apply_f32(const double* stats, float* mean_rstd, float* run_mean, float* run_var,
+int cvl_bn_finalize_apply_f32(const uint64_t* stats, float* mean_rstd, float* run_mean, float* run_var,
                               const float* z, const float* gamma, const float* beta, const float* residual,
                               float* y, int B, int HW, int C, int relu, float eps, float momentum,
                               cvl_stream_t stream);
@@ -481,14 +493,14 @@ int cvl_soft_nms(const double* boxes, int n, const double* classes, int ncls, do
 /* BatchNormalization over sub-batches: train_step (:527-545) runs one Keras training-mode forward
  * per sub-batch of `group` images, so statistics span the sub-batch (groups [g*G, min(g*G+G, B)),
  * the last may be short); running stats are updated once per group, in order.
- * cvl_bn_stats: stats[b][c] = (sum, sum of squares) over H*W of a bf16 NHWC tensor (float64,
- *   deterministic), the input of cvl_bn_finalize[_grouped].
+ * cvl_bn_stats: stats[b][c] = (sum, sum of squares) over H*W of a bf16 NHWC tensor (BN
+ *   accumulators [B][C][2][8], deterministic), the input of cvl_bn_finalize[_grouped].
  * cvl_bn_backward_grouped: as cvl_bn_backward (no ReLU output / conv bias terms) with group
  *   statistics; dz = BN-backward + dz_beta * dz (accumulate into an existing gradient). */
 size_t cvl_bn_stats_workspace_size(int B, int HW, int C);
-int cvl_bn_stats(const void* x, int B, int HW, int C, double* stats, void* workspace, size_t workspace_bytes,
+int cvl_bn_stats(const void* x, int B, int HW, int C, uint64_t* stats, void* workspace, size_t workspace_bytes,
                  cvl_stream_t stream);
-int cvl_bn_finalize_grouped(const double* stats, float* mean_rstd, float* run_mean, float* run_var, int B, int C,
+int cvl_bn_finalize_grouped(const uint64_t* stats, float* mean_rstd, float* run_mean, float* run_var, int B, int C,
                             int HW, int group, float eps, float momentum, cvl_stream_t stream);
 size_t cvl_bn_backward_grouped_workspace_size(int B, int HW, int C);
 int cvl_bn_backward_grouped(const void* dy, const void* y_relu, const void* z, const float* mean_rstd,

@@ -356,7 +356,7 @@ def check_conv_igemm(lp, name, launch, desc, src, dst, stats=None):
         assert desc.nseg == 1 and desc.mode == 0
         s = _segs(desc)[0]
         drows = _rows(dst, desc.ld_dst)
-        got = (stats - st0).view(desc.B, desc.n_store, 2)
+        got = _acc(stats - st0, desc.B, desc.n_store)        # integer bins: the difference is exact
         HW = s["Hr"] * s["Wr"]
         for b in range(desc.B):
             z = drows[s["db"] + b * s["di"]: s["db"] + b * s["di"] + HW, desc.dst_coff:desc.dst_coff + desc.n_store]
@@ -422,7 +422,7 @@ def check_conv_wgrad_grouped(lp, name, launch, desc, x, dy, dws, beta=0.0):
 def _bnsum_ref(lp, name, detail, kern, sums, dst_rows, idx_b, z, mr, gamma, beta, act_hi, ymask, B, C, HW):
     """(sum g, sum g*xhat) per (image, channel); g = dst * mask (mask from y > 0, or rebuilt from
     z as the kernels do), computed on the launch's own stored destination."""
-    got = sums.view(B, C, 2)
+    got = _acc(sums, B, C)
     errs = []
     for b in range(B):
         zz = z.reshape(B, HW, -1)[b, :, :C]
@@ -516,15 +516,21 @@ def check_pack_conv_weights(lp, name, launch, w_hwio, KH, KW, Cin, Cout, Cin_k, 
 # ================================================================================================
 # BatchNorm
 # ================================================================================================
+def _acc(acc, B, C):
+    """float64 (B, C, 2) values of a BN accumulator buffer (ops_nn.bn_acc layout)."""
+    from cvlite import ops_nn as nn
+    return nn.bn_acc_value(acc).view(B, C, 2)
+
+
 def _moments(stats, B, C, HW, eps):
-    s = stats.view(B, C, 2).double()
+    s = _acc(stats, B, C)
     m = s[..., 0] / HW
     var = (s[..., 1] / HW - m * m).clamp_min(0)
     return m, var, 1.0 / torch.sqrt(var + float(eps))
 
 
 def _check_finalize(lp, name, detail, stats, mr, rm0, rv0, run_mean, run_var, B, C, HW, eps, momentum, group=1):
-    s = stats.view(B, C, 2).double()
+    s = _acc(stats, B, C)
     if group > 1:          # sub-batch statistics: sums of each group of `group` images
         ng = (B + group - 1) // group
         sg = torch.stack([s[g * group:(g + 1) * group].sum(0) for g in range(ng)])
@@ -602,7 +608,8 @@ def _bn_bwd_ref(dy, z, mr, gamma, B, HW, C, mask, sums=None, group=1):
     if sums is None:
         s1, s2 = g.sum(1), (g * xh).sum(1)
     else:
-        s1, s2 = sums.view(B, C, 2)[..., 0].double(), sums.view(B, C, 2)[..., 1].double()
+        sv = _acc(sums, B, C)
+        s1, s2 = sv[..., 0], sv[..., 1]
     if group > 1:
         ng = (B + group - 1) // group
         gi = torch.arange(B, device=g.device) // group
@@ -719,7 +726,7 @@ def check_bn_stats(lp, name, launch, x, B, HW, C, stats):
     xx = x.reshape(B, HW, -1)[..., :C].double()
     ref = torch.stack([xx.sum(1), (xx * xx).sum(1)], -1)
     rabs = torch.stack([xx.abs().sum(1), (xx * xx).sum(1)], -1)
-    lp.add(name, "C%d HW%d B%d" % (C, HW, B), "stats", red_err(stats.view(B, C, 2), ref, rabs), 1e-6)
+    lp.add(name, "C%d HW%d B%d" % (C, HW, B), "stats", red_err(_acc(stats, B, C), ref, rabs), 1e-6)
 
 
 def check_bn_finalize_grouped(lp, name, launch, stats, mean_rstd, run_mean, run_var, B, C, HW, group, eps, momentum):

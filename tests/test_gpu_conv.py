@@ -101,7 +101,7 @@ def test_conv_fwd(case, kern):
     xg = x.to(BF).cuda()
     # bf16 output + relu + BN stats
     out = torch.zeros((B, Ho, Wo, Cout), dtype=BF, device="cuda")
-    stats = torch.zeros((B, Cout, 2), dtype=torch.float64, device="cuda")
+    stats = nn.bn_acc(B, Cout, "cuda")
     d = nn.make_desc(nn.FWD, B, Cin, k, k, s, pt, pl, npad, Cout, Cout, [nn.seg(Ho, Wo, H, W, wf, bias)],
                      relu_out=True)
     hw = Ho * Wo
@@ -111,7 +111,7 @@ def test_conv_fwd(case, kern):
     if stats_ok:
         o = out.double().cpu()
         st = torch.stack([o.sum((1, 2)), (o * o).sum((1, 2))], -1)
-        torch.testing.assert_close(stats.cpu(), st, rtol=1e-5, atol=1e-3)
+        torch.testing.assert_close(nn.bn_acc_value(stats).cpu(), st, rtol=1e-5, atol=1e-3)
     # fp32 output into a wider buffer at a channel offset, accumulate (beta = 1), relu on load
     ld = Cout + 16
     out32 = torch.randn((B, Ho, Wo, ld), dtype=torch.float32, device="cuda")
@@ -253,14 +253,14 @@ def test_conv_splitk_matches_unsplit(case):
     outs, stats = [], []
     for split in (True, False):
         out = torch.zeros((B, Ho, Wo, Cout), dtype=BF, device="cuda")
-        st = torch.zeros((B, Cout, 2), dtype=torch.float64, device="cuda")
+        st = nn.bn_acc(B, Cout, "cuda")
         if split:
             nn.conv_igemm(d, xg, out, st)
         else:
             _lib.call("cvl_conv_igemm", ctypes.byref(d), nn.ptr(xg), nn.ptr(out), nn.ptr(st), None, 0,
                       nn.stream())
         outs.append(out.double().cpu())
-        stats.append(st.cpu())
+        stats.append(nn.bn_acc_value(st).cpu())
     torch.testing.assert_close(outs[0], ref.clamp(min=0), rtol=1e-2, atol=1e-2)
     torch.testing.assert_close(outs[0], outs[1], rtol=1e-2, atol=1e-2)
     torch.testing.assert_close(stats[0], stats[1], rtol=5e-3, atol=1e-1)  # bf16 ulp flips
@@ -487,13 +487,13 @@ def test_conv_bn_stats_maps_not_tile_aligned(B, H, Cin, Cout, k, kern):
     wf, _, npad, _, _ = packs(w)
     bias = (torch.randn(npad, generator=g) * 0.1).float().cuda()
     out = torch.zeros((B, H, H, Cout), dtype=BF, device="cuda")
-    stats = torch.zeros((B, Cout, 2), dtype=torch.float64, device="cuda")
+    stats = nn.bn_acc(B, Cout, "cuda")
     pad = (k - 1) // 2
     d = nn.make_desc(nn.FWD, B, Cin, k, k, 1, pad, pad, npad, Cout, Cout, [nn.seg(H, H, H, H, wf, bias)])
     nn.conv_igemm(d, x.to(BF).cuda(), out, stats)
     o = out.double().cpu()
     st = torch.stack([o.sum((1, 2)), (o * o).sum((1, 2))], -1)
-    torch.testing.assert_close(stats.cpu(), st, rtol=1e-5, atol=1e-3)
+    torch.testing.assert_close(nn.bn_acc_value(stats).cpu(), st, rtol=1e-5, atol=1e-3)
 
 
 @pytest.mark.gpu

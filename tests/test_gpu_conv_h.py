@@ -64,13 +64,13 @@ def test_h_fwd_dgrad(case):
     # forward: bias + ReLU + BN statistics (bf16), then fp32 into a wider buffer with beta = 1
     ref = conv3(x.detach(), w, b).clamp(min=0)
     out = torch.zeros((B, H, W, Cout), dtype=BF, device="cuda")
-    st = torch.zeros((B, Cout, 2), dtype=torch.float64, device="cuda")
+    st = nn.bn_acc(B, Cout, "cuda")
     d = nn.make_desc(nn.FWD, B, Cin, 3, 3, 1, 1, 1, npad, Cout, Cout, [nn.seg(H, W, H, W, wf, bias)], relu_out=True)
     nn.conv_igemm(d, xg, out, st)
     assert "conv_igemm_h_kernel" in last_kernel(), last_kernel()
     torch.testing.assert_close(out.double().cpu(), ref, rtol=1e-2, atol=1e-2)
     o = out.double().cpu()
-    torch.testing.assert_close(st.cpu(), torch.stack([o.sum((1, 2)), (o * o).sum((1, 2))], -1), rtol=1e-5,
+    torch.testing.assert_close(nn.bn_acc_value(st).cpu(), torch.stack([o.sum((1, 2)), (o * o).sum((1, 2))], -1), rtol=1e-5,
                                atol=1e-3)
     ld = Cout + 8
     o32 = torch.randn((B, H, W, ld), generator=g).cuda()
@@ -151,7 +151,7 @@ def test_h_split_k_small_grid():
     outs, sts = [], []
     for split in (True, False):
         out = torch.zeros((B, H, H, Cout), dtype=BF, device="cuda")
-        st = torch.zeros((B, Cout, 2), dtype=torch.float64, device="cuda")
+        st = nn.bn_acc(B, Cout, "cuda")
         if split:
             nn.conv_igemm(d, x.to(BF).cuda(), out, st)
         else:
@@ -159,7 +159,7 @@ def test_h_split_k_small_grid():
                       None, 0, _lib.stream())
         assert "conv_igemm_h_kernel" in last_kernel(), last_kernel()
         outs.append(out.double().cpu())
-        sts.append(st.cpu())
+        sts.append(nn.bn_acc_value(st).cpu())
     ref = conv3(x, w, b).clamp(min=0)
     for o, st in zip(outs, sts):
         torch.testing.assert_close(o, ref, rtol=1e-2, atol=1e-2)
@@ -190,7 +190,7 @@ def test_h_dgrad_fused_bn_backward_sums():
     beta = torch.randn(C, generator=g).to(dev) * 0.3
     d = conv.dgrad_desc(B, [nn.seg(H, H, H, H, conv.wd)], ld_dst=C)
     dx_f = torch.empty((B, H, H, C), dtype=BF, device=dev)
-    sums = torch.empty((B, C, 2), dtype=torch.float64, device=dev)
+    sums = nn.bn_acc(B, C, dev)
     assert nn.conv_igemm_dgrad_bnsum(d, dy_next, dx_f, z, mr, gamma, beta, sums)
     assert "conv_igemm_h_kernel" in last_kernel(), last_kernel()
     dx_p = torch.empty_like(dx_f)
@@ -200,7 +200,7 @@ def test_h_dgrad_fused_bn_backward_sums():
     a = gamma * xh + beta
     gm = torch.where(a > 0, dx_p.float(), torch.zeros_like(a)).double()
     ref = torch.stack([gm.sum((1, 2)), (gm * xh.double()).sum((1, 2))], -1)
-    torch.testing.assert_close(sums, ref, rtol=1e-5, atol=1e-6 * float(ref.abs().max()))
+    torch.testing.assert_close(nn.bn_acc_value(sums), ref, rtol=1e-5, atol=1e-6 * float(ref.abs().max()))
 
 
 WG_CASES = [  # (B, H, W, Cin, Cout): the 3x3 units' weight gradients (conv2_x..conv5_x), FPN c4/c5

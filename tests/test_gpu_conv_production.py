@@ -144,7 +144,7 @@ def test_wide_1x1_with_bn_stats_configs1(variant, monkeypatch):
     wf, _ = packs(w)
     d = nn.make_desc(nn.FWD, B, Cin, 1, 1, 1, 0, 0, Cout, Cout, Cout, [nn.seg(H, H, H, H, wf, bias)])
     out = torch.empty((B, H, H, Cout), dtype=BF, device="cuda")
-    stats = torch.zeros((B, Cout, 2), dtype=F64, device="cuda")
+    stats = nn.bn_acc(B, Cout, "cuda")
     nn.conv_igemm(d, x, out, stats)
     code, name = last_kernel()
     print("kernel:", name)
@@ -153,7 +153,7 @@ def test_wide_1x1_with_bn_stats_configs1(variant, monkeypatch):
     torch.testing.assert_close(out.to(F64), ref, rtol=1e-2, atol=1e-2)
     o = out.to(F64)
     exp = torch.stack([o.sum((1, 2)), (o * o).sum((1, 2))], -1)
-    torch.testing.assert_close(stats, exp, rtol=1e-5, atol=1e-3)
+    torch.testing.assert_close(nn.bn_acc_value(stats), exp, rtol=1e-5, atol=1e-3)
 
 
 @pytest.mark.parametrize("N,NP", [(720, 768), (36, 64)])
@@ -227,11 +227,11 @@ def test_x32_tile_geometries(monkeypatch, mode, B, H, W, C, N):
         d = nn.make_desc(nn.DGRAD, B, C, 3, 3, 1, 1, 1, N, N, N, [nn.seg(H, W, H, W, wd, None)])
         ref = dgrad_ref(x.to(F64), w)
     out = torch.empty((B, H, W, N), dtype=BF, device="cuda")
-    stats = torch.zeros((B, N, 2), dtype=F64, device="cuda") if mode == "fwd" else None
+    stats = nn.bn_acc(B, N, "cuda") if mode == "fwd" else None
     nn.conv_igemm(d, x, out, stats)
     code, name = last_kernel()
     assert code == 7, name
     torch.testing.assert_close(out.to(F64), ref, rtol=1e-2, atol=2e-2)
     if stats is not None:
         o = out.to(F64)
-        torch.testing.assert_close(stats, torch.stack([o.sum((1, 2)), (o * o).sum((1, 2))], -1), rtol=1e-5, atol=1e-3)
+        torch.testing.assert_close(nn.bn_acc_value(stats), torch.stack([o.sum((1, 2)), (o * o).sum((1, 2))], -1), rtol=1e-5, atol=1e-3)

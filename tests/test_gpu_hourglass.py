@@ -103,11 +103,12 @@ def test_bn_grouped_stats_and_backward(group, C):
     x = bf(torch.randn(B, H, W, C, generator=g) * 2 + 0.5).cuda()
     gamma = (torch.rand(C, generator=g) + 0.5).cuda()
     beta = torch.randn(C, generator=g).cuda()
-    stats = torch.empty((B, C, 2), dtype=torch.float64, device="cuda")
+    stats = nn.bn_acc(B, C, "cuda")
     nn.bn_stats(x, B, H * W, C, stats)
     xd = x.double().cpu()
-    assert torch.allclose(stats[:, :, 0].cpu(), xd.sum((1, 2)), rtol=1e-5)
-    assert torch.allclose(stats[:, :, 1].cpu(), (xd * xd).sum((1, 2)), rtol=1e-5)
+    sv = nn.bn_acc_value(stats).cpu()
+    assert torch.allclose(sv[:, :, 0], xd.sum((1, 2)), rtol=1e-5)
+    assert torch.allclose(sv[:, :, 1], (xd * xd).sum((1, 2)), rtol=1e-5)
     mr = torch.empty((B, C, 2), dtype=torch.float32, device="cuda")
     rm, rv = torch.zeros(C, device="cuda"), torch.ones(C, device="cuda")
     nn.bn_finalize_grouped(stats, mr, rm, rv, B, C, H * W, group, 1e-3, 0.99)

@@ -65,7 +65,7 @@ def test_bn_relu6_apply_and_backward():
     z = (torch.randn(B, H, W, C, generator=g) * 4 + 2).to(torch.bfloat16).cuda()
     gamma = (torch.rand(C, generator=g) * 2 + 0.5).cuda()
     beta = (torch.randn(C, generator=g) * 2).cuda()
-    stats = torch.empty((B, C, 2), dtype=torch.float64, device="cuda")
+    stats = nn.bn_acc(B, C, "cuda")
     nn.bn_stats(z, B, H * W, C, stats)
     mr = torch.empty((B, C, 2), device="cuda")
     rm, rv = torch.zeros(C, device="cuda"), torch.ones(C, device="cuda")

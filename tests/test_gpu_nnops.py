@@ -27,7 +27,7 @@ def test_bn_forward_backward(B, HW, C, relu, res):
     beta = torch.randn(C, generator=g, dtype=torch.float64)
     r = bfr(torch.randn(B, HW, C, generator=g, dtype=torch.float64)) if res else None
     eps = 1.001e-5
-    stats = torch.stack([z.sum(1), (z * z).sum(1)], -1).cuda()
+    stats = nn.bn_acc_encode(torch.stack([z.sum(1), (z * z).sum(1)], -1)).cuda()
     mr = torch.empty((B, C, 2), dtype=torch.float32, device="cuda")
     rm = torch.zeros(C, device="cuda")
     rv = torch.ones(C, device="cuda")
@@ -282,7 +282,7 @@ def test_dgrad_fused_bn_backward_first_pass(B, H, Cin, Cout, k, expect_fused):
     d = conv.dgrad_desc(B, [nn.seg(H, W, H, W, conv.wd)], ld_dst=C)
     # fused
     dx_f = torch.empty((B, H, W, C), dtype=BF, device=dev)
-    sums = torch.empty((B, C, 2), dtype=torch.float64, device=dev)
+    sums = nn.bn_acc(B, C, dev)
     fused = nn.conv_igemm_dgrad_bnsum(d, dy_next, dx_f, z, mr, gamma, beta, sums)
     assert fused == expect_fused
     # plain
@@ -297,7 +297,7 @@ def test_dgrad_fused_bn_backward_first_pass(B, H, Cin, Cout, k, expect_fused):
     a = gamma * xh + beta
     gm = torch.where(a > 0, dx_p.float(), torch.zeros_like(a)).double()
     ref = torch.stack([gm.sum((1, 2)), (gm * xh.double()).sum((1, 2))], -1)
-    torch.testing.assert_close(sums, ref, rtol=1e-5, atol=1e-6 * float(ref.abs().max()))
+    torch.testing.assert_close(nn.bn_acc_value(sums), ref, rtol=1e-5, atol=1e-6 * float(ref.abs().max()))
     HW = H * W
     dz_f, dz_p = torch.empty_like(z), torch.empty_like(z)
     dg_f, db_f = torch.zeros(C, device=dev), torch.zeros(C, device=dev)
@@ -342,7 +342,7 @@ def test_dgrad_fused_bn_backward_residual(B, H, Cin, Cout, monkeypatch):
     beta = torch.randn(C, generator=g).to(dev) * 0.3
     d = conv.dgrad_desc(B, [nn.seg(H, W, H, W, conv.wd)], ld_dst=C, beta=1.0)
     dx_f = old.clone()
-    sums = torch.empty((B, C, 2), dtype=torch.float64, device=dev)
+    sums = nn.bn_acc(B, C, dev)
     assert nn.conv_igemm_dgrad_bnsum_res(d, dy_next, dx_f, y, z, mr, gamma, beta, sums)
     dx_p = old.clone()
     nn.conv_igemm(d, dy_next, dx_p)
@@ -350,7 +350,7 @@ def test_dgrad_fused_bn_backward_residual(B, H, Cin, Cout, monkeypatch):
     xh = (z.float() - mr[..., 0].view(B, 1, 1, C)) * mr[..., 1].view(B, 1, 1, C)
     gm = torch.where(y.float() > 0, dx_p.float(), torch.zeros_like(xh)).double()
     ref = torch.stack([gm.sum((1, 2)), (gm * xh.double()).sum((1, 2))], -1)
-    torch.testing.assert_close(sums, ref, rtol=1e-5, atol=1e-6 * float(ref.abs().max()))
+    torch.testing.assert_close(nn.bn_acc_value(sums), ref, rtol=1e-5, atol=1e-6 * float(ref.abs().max()))
     HW = H * W
     dz_f, dz_p = torch.empty_like(z), torch.empty_like(z)
     go_f, go_p = torch.empty_like(z), torch.empty_like(z)

@@ -151,3 +151,69 @@ def test_parse_image_decodes_jpeg_and_png(tmp_path):
     g = str(tmp_path / "g.jpg")
     Image.fromarray(img[..., 0]).save(g)
     assert _parse_image(g).shape == (37, 53, 3)
+
+
+def test_bn_acc_encoding_exact_and_order_independent():
+    """BN accumulators (include/cvlite.h, csrc/bn_acc.h): the host encoder equals a plain-Python
+    restatement of the bin split; partials added in any order give identical bins; the decoded value
+    is exact for |x| in [2^-40, 2^54)."""
+    import math
+    import struct
+
+    import torch
+    from cvlite import ops_nn as nn
+
+    def split(p):
+        u = struct.unpack("<I", struct.pack("<f", p))[0]
+        e = (u >> 23) & 0xFF
+        if e == 255:
+            return 7, 1
+        r = e - 27
+        if e == 0 or r < 0:
+            return None, 0
+        k = r // 22
+        if k >= 7:
+            return 7, 1
+        m = ((u & 0x7FFFFF) | 0x800000) << (r - 22 * k)
+        return k, (-m if u >> 31 else m)
+
+    def encode(x):
+        bins = [0] * 8
+        hi = float(np.float32(x))
+        r = x - hi
+        mid = float(np.float32(r))
+        for p in (hi, mid, float(np.float32(r - mid))):
+            k, v = split(p)
+            if k is not None:
+                bins[k] += v
+        return bins
+
+    def decode(b):
+        if b[7]:
+            return float("nan")
+        t = 0.0
+        for k in range(7):
+            t += float(b[k]) * math.ldexp(1.0, 27 + 22 * k - 150)
+        return t
+
+    rng = np.random.default_rng(3)
+    vals = np.concatenate([rng.standard_normal(300) * 10.0 ** rng.integers(-12, 15, 300),
+                           [0.0, -0.0, 1e-40, 2.0 ** 60, float("inf"), float("nan")]])
+    acc = nn.bn_acc_encode(torch.tensor(vals).view(-1, 1).repeat(1, 2))
+    for i, x in enumerate(vals):
+        b = encode(float(x))
+        assert acc[i, 0].tolist() == b, (x, acc[i, 0].tolist(), b)
+        if np.isfinite(x) and 2.0 ** -40 <= abs(x) < 2.0 ** 54:
+            assert decode(b) == x
+    # fp32 partials summed in two orders: the bins (integers) agree exactly
+    parts = (rng.standard_normal(4096) * 10.0 ** rng.integers(-6, 6, 4096)).astype(np.float32)
+    b1, b2 = [0] * 8, [0] * 8
+    for p in parts:
+        k, v = split(float(p))
+        b1[k] += v
+    for p in parts[::-1][rng.permutation(len(parts))]:
+        k, v = split(float(p))
+        b2[k] += v
+    assert b1 == b2
+    exact = math.fsum(float(p) for p in parts)
+    assert abs(decode(b1) - exact) <= 1e-15 * abs(exact) + 1e-300

@@ -38,7 +38,7 @@ for B, HW, C in shapes:
     mr = torch.stack([torch.zeros(B * C, device=dev), torch.ones(B * C, device=dev)], 1).contiguous()
     ga = torch.ones(C, device=dev)
     be = torch.zeros(C, device=dev)
-    sums = torch.zeros(B * C * 2, device=dev, dtype=torch.float64)
+    sums = nn.bn_acc(B, C, dev)
     dga = torch.zeros(C, device=dev)
     dbe = torch.zeros(C, device=dev)
     t_cp = timeit(lambda: y.copy_(z))

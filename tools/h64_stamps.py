@@ -24,7 +24,7 @@ def main():
         C = conv.cin
         x = torch.randn((B, h, w, C), generator=g).to(torch.bfloat16).cuda()
         y = torch.zeros((B, h, w, conv.cout), dtype=torch.bfloat16, device="cuda")
-        st = torch.zeros((B, conv.cout, 2), dtype=torch.float64, device="cuda")
+        st = nn.bn_acc(B, conv.cout, "cuda")
         fd = conv.fwd_desc(B, [nn.seg(h, w, h, w, conv.wf, conv.bias_arg())], ld_dst=conv.cout)
         for ab in (256 | extra,):
             os.environ["CVL_X_ABLATE"] = str(ab)

@@ -38,7 +38,7 @@ def main():
         x = torch.randn((B, H, H, Cin), generator=gen).to(torch.bfloat16).cuda()
         w = (torch.randn((Cout, Cin), generator=gen) * Cin ** -0.5).to(torch.bfloat16).cuda()
         y = torch.empty((B, H, H, Cout), dtype=torch.bfloat16, device="cuda")
-        sts = torch.zeros((B, Cout, 2), dtype=torch.float64, device="cuda") if stats else None
+        sts = nn.bn_acc(B, Cout, "cuda") if stats else None
         d = nn.make_desc(nn.FWD, B, Cin, 1, 1, 1, 0, 0, Cout, Cout, Cout, [nn.seg(H, H, H, H, w, None)])
         row = ["fwd 1x1 %d->%d @ %dx%d" % (Cin, Cout, H, H)]
         mb = (x.numel() + y.numel()) * 2 / 1e6

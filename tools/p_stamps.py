@@ -18,7 +18,7 @@ def main():
         x = torch.randn((B, H, H, Cin), generator=gen).to(torch.bfloat16).cuda()
         w = (torch.randn((Cout, Cin), generator=gen) * Cin ** -0.5).to(torch.bfloat16).cuda()
         y = torch.zeros((B, H, H, Cout), dtype=torch.bfloat16, device="cuda")
-        sts = torch.zeros((B, Cout, 2), dtype=torch.float64, device="cuda")
+        sts = nn.bn_acc(B, Cout, "cuda")
         d = nn.make_desc(nn.FWD, B, Cin, 1, 1, 1, 0, 0, Cout, Cout, Cout, [nn.seg(H, H, H, H, w, None)])
         os.environ["CVL_P_ABLATE"] = str(10 | extra)
         us = timed(lambda: nn.conv_igemm(d, x, y, sts))
