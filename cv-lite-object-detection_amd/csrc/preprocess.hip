@@ -3,7 +3,9 @@
 // `random_flip_horizontal`, one launch writing straight into a slot of the device batch.
 //
 //   out[y][x][c] = y < oh && x < ow ? bilinear(src', y, x, c) / 127.5 - 1 : 0      (pad value 0)
-//   src'         = flip ? tf.image.flip_left_right(src) : src
+//   src'         = flip == 1 ? tf.image.flip_left_right(src) : src
+//   flip == 2: the resize first, then the flip of its output (preprocess_data's pad_flag=False order,
+//   :111-125): out[y][x] = resized[y][ow - 1 - x]
 //
 // bilinear = tf.image.resize(method="bilinear", antialias=False) of TF2, restated from TF's
 // published kernel (TF is absent here, so parity is pinned to the numpy restatement, not TF):
@@ -28,13 +30,14 @@ __global__ void __launch_bounds__(PT) resize_pad_kernel(const void* src, int src
     return;
   }
   const float sy = (float)H / (float)oh, sx = (float)W / (float)ow;
-  const float iny = ((float)y + 0.5f) * sy - 0.5f, inx = ((float)x + 0.5f) * sx - 0.5f;
+  const int xs = flip == 2 ? ow - 1 - x : x;
+  const float iny = ((float)y + 0.5f) * sy - 0.5f, inx = ((float)xs + 0.5f) * sx - 0.5f;
   const float fy = floorf(iny), fx = floorf(inx);
   const int y0 = fy > 0.f ? (int)fy : 0, x0 = fx > 0.f ? (int)fx : 0;
   const int y1 = (int)ceilf(iny) < H - 1 ? (int)ceilf(iny) : H - 1;
   const int x1 = (int)ceilf(inx) < W - 1 ? (int)ceilf(inx) : W - 1;
   const float yl = iny - fy, xl = inx - fx;
-  const int c0 = flip ? W - 1 - x0 : x0, c1 = flip ? W - 1 - x1 : x1;
+  const int c0 = flip == 1 ? W - 1 - x0 : x0, c1 = flip == 1 ? W - 1 - x1 : x1;
   for (int c = 0; c < C; ++c) {
     float tl, tr, bl, br;
     if (src_u8) {
@@ -57,7 +60,7 @@ __global__ void __launch_bounds__(PT) resize_pad_kernel(const void* src, int src
 
 extern "C" int cvl_resize_pad_normalize(const void* src, int src_u8, int H, int W, int C, int flip, int out_h,
                                         int out_w, int pad_h, int pad_w, float* out, cvl_stream_t stream) {
-  CVL_CHECK_ARG(src && out && H > 0 && W > 0 && C > 0 && C <= 4 && out_h > 0 && out_w > 0);
+  CVL_CHECK_ARG(src && out && H > 0 && W > 0 && C > 0 && C <= 4 && out_h > 0 && out_w > 0 && flip >= 0 && flip <= 2);
   CVL_CHECK_ARG(pad_h >= out_h && pad_w >= out_w && (long)pad_h * pad_w < (1L << 31));
   const long n = (long)pad_h * pad_w;
   hipLaunchKernelGGL(resize_pad_kernel, dim3((unsigned)((n + PT - 1) / PT)), dim3(PT), 0, (hipStream_t)stream, src,

@@ -103,8 +103,8 @@ def preprocess_data(sample, img_dims=384, pad_flag=True, rng=None, out=None):
     [N,4] (the reference's xywh of the swapped corners), class_id [N] int32, img_shp [2] fp32).
     pad_flag=True: flip + jittered resize_and_pad_image (img_shp = the unpadded resized shape);
     pad_flag=False: resize to [img_dims, img_dims] (:111-113), flip, /127.5 - 1 (:124-125),
-    img_shp = [img_dims, img_dims] -- one fused launch either way (a bilinear half-pixel resize
-    commutes with the left-right flip).  The flip draw (p = 0.5) and the jitter draw use `rng`
+    img_shp = [img_dims, img_dims] -- one fused launch either way, in the reference's order (pad_flag
+    True: flip, then resize; False: resize, then flip its output).  The flip draw (p = 0.5) and the jitter draw use `rng`
     (numpy) in the reference's order: flip first, then the jitter size."""
     rng = rng if rng is not None else np.random.default_rng()
     jitter = [sample["l_jitter"], sample["u_jitter"]]
@@ -116,16 +116,17 @@ def preprocess_data(sample, img_dims=384, pad_flag=True, rng=None, out=None):
         img, new_shape, _ = preprocess_image(image, jitter=jitter, min_side=sample["min_side"],
                                              max_side=sample["max_side"], flip=flip, out=out, rng=rng)
     else:
-        img = resize_normalize(image, int(img_dims), int(img_dims), flip=flip, out=out)
+        img = resize_normalize(image, int(img_dims), int(img_dims), flip=flip, out=out, flip_after=True)
         new_shape = np.array([img_dims, img_dims], f32)
     bbox = box_targets(sample["objects"]["bbox"], flip)
     cls = np.asarray(sample["objects"]["label"], np.int32).reshape(-1)
     return img, bbox, cls, np.asarray(new_shape, f32)
 
 
-def resize_normalize(image, oh, ow, flip=False, out=None):
-    """tf.image.resize(image, [oh, ow]) (bilinear, half-pixel) [+ flip_left_right], / 127.5 - 1,
-    no padding: one cvl_resize_pad_normalize launch (output size = padded size)."""
+def resize_normalize(image, oh, ow, flip=False, out=None, flip_after=False):
+    """tf.image.resize(image, [oh, ow]) (bilinear, half-pixel) [+ flip_left_right of the input, or of
+    the resized output with flip_after], / 127.5 - 1, no padding: one cvl_resize_pad_normalize launch
+    (output size = padded size)."""
     _lib.require_cuda()
     img = torch.as_tensor(image).cuda()
     if img.dtype not in (torch.uint8, torch.float32):
@@ -136,7 +137,7 @@ def resize_normalize(image, oh, ow, flip=False, out=None):
         out = torch.empty((oh, ow, C), dtype=torch.float32, device=img.device)
     assert tuple(out.shape) == (oh, ow, C) and out.dtype == torch.float32 and out.is_contiguous()
     _lib.call("cvl_resize_pad_normalize", _lib.ptr(img), 1 if img.dtype == torch.uint8 else 0, H, W, C,
-              1 if flip else 0, oh, ow, oh, ow, _lib.ptr(out), _lib.stream())
+              (2 if flip_after else 1) if flip else 0, oh, ow, oh, ow, _lib.ptr(out), _lib.stream())
     return out
 
 

@@ -710,8 +710,9 @@ int cvl_fcos_detect(const float* reg_pred, int ld_reg, const float* cls_pred, in
  * ========================================================================================== */
 
 /* One decoded image src [H][W][C] (uint8 when src_u8, else fp32; C <= 4) -> out [pad_h][pad_w][C]
- * fp32 = (flip ? flip_left_right(src) : src) resized to out_h x out_w by TF2's bilinear
- * tf.image.resize (half-pixel centres, antialias off; restated), then / 127.5 - 1, zero padded
+ * fp32 = (flip == 1 ? flip_left_right(src) : src) resized to out_h x out_w by TF2's bilinear
+ * tf.image.resize (half-pixel centres, antialias off; restated), flip == 2: the resized image's
+ * left-right flip (preprocess_data pad_flag=False: resize, then flip), then / 127.5 - 1, zero padded
  * bottom/right (tf.image.pad_to_bounding_box).  out may point into a batch slot. */
 int cvl_resize_pad_normalize(const void* src, int src_u8, int H, int W, int C, int flip, int out_h, int out_w,
                              int pad_h, int pad_w, float* out, cvl_stream_t stream);
