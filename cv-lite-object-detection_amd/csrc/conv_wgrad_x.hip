@@ -56,6 +56,7 @@ struct WxArgs {
   int g_m0[kMaxGroups], g_m1[kMaxGroups]; // M range of each group
   int ld_dy, dy_coff, Cout, co_tiles, tiles, nsplit, chunk, direct;
   float beta;
+  unsigned long long* stamps;             // measurement builds (CVL_WGX_STAMPS=1): u64 [grid][4], else null
 };
 
 __device__ __forceinline__ int rswz(int r) { return (r & 3) | (((r >> 3) & 1) << 2); }
@@ -66,9 +67,12 @@ __device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t r, const cvl_bf16* 
                                            0, 0);
 }
 
-template <int T, int SR = BR>
+template <int T, int SR = BR, bool ST = false>
 __global__ void __launch_bounds__(NT) conv_wgrad_x_kernel(WxArgs g) {
   using C = WxCfg<T, SR>;
+  // ST: wall-clock stamps of thread 0 (entry, prologue landed, loop done, epilogue stored)
+  unsigned long long* stamp = (ST && threadIdx.x == 0) ? g.stamps + blockIdx.x * 4 : nullptr;
+  if (stamp) stamp[0] = wall_clock64();
   constexpr int BCO = C::BCO, BKK = C::BKK, YST = C::YST, SLOT = C::SLOT, TM = C::TM, TN = C::TN;
   constexpr int J = C::J;
   __shared__ __attribute__((aligned(16))) cvl_bf16 lds[NSLOT * SLOT];
@@ -196,6 +200,7 @@ __global__ void __launch_bounds__(NT) conv_wgrad_x_kernel(WxArgs g) {
   wait_vm<2 * PW>();
   __builtin_amdgcn_s_barrier();
   asm volatile("" ::: "memory");
+  if (stamp) stamp[1] = wall_clock64();
   if (wco == 1) bar();                          // stagger: waves 4-7 run one barrier behind
 
   int rslot = 0;
@@ -245,6 +250,7 @@ __global__ void __launch_bounds__(NT) conv_wgrad_x_kernel(WxArgs g) {
   }
   if (wco == 0) bar();                          // equal barrier counts for both groups
   wait_vm<0>();
+  if (stamp) stamp[2] = wall_clock64();
 
   // ---- epilogue: C[co][k] -> out[k][co] (HWIO), 4 consecutive co per lane -------------------------
   float* out = g.out[grp] + (g.direct ? 0 : (size_t)split * a.K * g.Cout);
@@ -267,6 +273,11 @@ __global__ void __launch_bounds__(NT) conv_wgrad_x_kernel(WxArgs g) {
         }
       }
     }
+  if (ST) {
+    wait_vm<0>();
+    __syncthreads();
+    if (stamp) stamp[3] = wall_clock64();
+  }
 }
 
 struct WxPlan {
@@ -274,6 +285,11 @@ struct WxPlan {
   int g_m0[kMaxGroups], g_m1[kMaxGroups];
   size_t slab;
 };
+
+// measurement builds: CVL_WGX_STAMPS=1 stamps every launch into this buffer (cvl_debug_wgx_stamps)
+constexpr int kStampWgs = 16384;
+__device__ unsigned long long g_wgx_stamps[kStampWgs * 4];
+int g_wgx_stamp_grid = 0;
 
 // Modelled time of s splits at tile width T: rounds of 256 workgroups (one per CU; 512 for T = 128) x 32-row steps
 // per chunk (CVL_WGX_STEP, 0.01 us; ~0.8 us measured on the tower shape; CVL_WGX_STEP128 for the
@@ -377,6 +393,13 @@ int cvl_conv_wgrad_x(const cvl_conv_desc* d, int ngroups, const void* x, const v
   WxPlan p;
   if (!wx_plan(d, ngroups, &g.a, &p)) return -1;
   if (!workspace || workspace_bytes < (p.slab > 16 ? p.slab : 16)) return CVL_EINVAL;
+  static const bool stamps = cvl_env_flag("CVL_WGX_STAMPS");
+  g.stamps = nullptr;
+  if (stamps && p.tiles * p.nsplit * ngroups <= kStampWgs) {
+    void* sym = nullptr;
+    if (hipGetSymbolAddress(&sym, HIP_SYMBOL(g_wgx_stamps)) == hipSuccess) g.stamps = (unsigned long long*)sym;
+    g_wgx_stamp_grid = p.tiles * p.nsplit * ngroups;
+  }
   g.a.src = reinterpret_cast<const cvl_bf16*>(x);
   g.dy = reinterpret_cast<const cvl_bf16*>(dy);
   g.ld_dy = d->ld_dst;
@@ -401,11 +424,32 @@ int cvl_conv_wgrad_x(const cvl_conv_desc* d, int ngroups, const void* x, const v
     if (!gs && ngroups > 1) gs = cvl_wgrad_defer_guard(dw[1], s);
     if (gs) return gs;
   }
-  if (p.T == 256) hipLaunchKernelGGL(conv_wgrad_x_kernel<256>, dim3(p.tiles * p.nsplit * ngroups), dim3(NT), 0, s, g);
-  else if (p.SR == 64) hipLaunchKernelGGL((conv_wgrad_x_kernel<128, 64>), dim3(p.tiles * p.nsplit * ngroups), dim3(NT), 0, s, g);
-  else hipLaunchKernelGGL(conv_wgrad_x_kernel<128>, dim3(p.tiles * p.nsplit * ngroups), dim3(NT), 0, s, g);
+  const dim3 grid(p.tiles * p.nsplit * ngroups);
+  if (g.stamps) {
+    if (p.T == 256) hipLaunchKernelGGL((conv_wgrad_x_kernel<256, BR, true>), grid, dim3(NT), 0, s, g);
+    else if (p.SR == 64) hipLaunchKernelGGL((conv_wgrad_x_kernel<128, 64, true>), grid, dim3(NT), 0, s, g);
+    else hipLaunchKernelGGL((conv_wgrad_x_kernel<128, BR, true>), grid, dim3(NT), 0, s, g);
+  } else if (p.T == 256) {
+    hipLaunchKernelGGL(conv_wgrad_x_kernel<256>, grid, dim3(NT), 0, s, g);
+  } else if (p.SR == 64) {
+    hipLaunchKernelGGL((conv_wgrad_x_kernel<128, 64>), grid, dim3(NT), 0, s, g);
+  } else {
+    hipLaunchKernelGGL(conv_wgrad_x_kernel<128>, grid, dim3(NT), 0, s, g);
+  }
   int st = cvl_launch_status();
   if (st || g.direct) return st;
   return cvl_wgrad_reduce((const float*)workspace, dw[0], ngroups > 1 ? dw[1] : dw[0], (long)g.a.K * g.Cout / 4,
                           p.nsplit, ngroups, beta, s);
+}
+
+// Measurement hook: the stamps of the last stamped weight-gradient launch (CVL_WGX_STAMPS=1):
+// u64 [grid][4] = (entry, prologue landed, loop done, epilogue stored) wall-clock ticks per
+// workgroup, copied to host memory (at most max_wgs rows); returns the grid size (0: none).
+extern "C" int cvl_debug_wgx_stamps(uint64_t* host, int max_wgs) {
+  const int n = g_wgx_stamp_grid < max_wgs ? g_wgx_stamp_grid : max_wgs;
+  if (n <= 0 || !host) return g_wgx_stamp_grid;
+  if (hipDeviceSynchronize() != hipSuccess) return -1;
+  if (hipMemcpyFromSymbol(host, HIP_SYMBOL(g_wgx_stamps), (size_t)n * 32, 0, hipMemcpyDeviceToHost) != hipSuccess)
+    return -1;
+  return g_wgx_stamp_grid;
 }

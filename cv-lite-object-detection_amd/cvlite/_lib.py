@@ -51,6 +51,7 @@ SIGNATURES = {
                            c_int, c_int, P, P]),
     "cvl_bn_finalize": (c_int, [P, P, P, P, c_int, c_int, c_int, c_float, c_float, P]),
     "cvl_bn_acc_decode": (c_int, [P, P, ctypes.c_int64, P]),
+    "cvl_debug_wgx_stamps": (c_int, [P, c_int]),
     "cvl_bn_apply": (c_int, [P, P, P, P, P, P, c_int, c_int, c_int, c_int, P]),
     "cvl_bn_finalize_apply": (c_int, [P, P, P, P, P, P, P, P, P, c_int, c_int, c_int, c_int, c_float, c_float, P]),
     "cvl_bn_backward_workspace_size": (c_size_t, [c_int, c_int, c_int]),
