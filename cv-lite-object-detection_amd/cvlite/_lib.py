@@ -52,6 +52,9 @@ SIGNATURES = {
     "cvl_bn_finalize": (c_int, [P, P, P, P, c_int, c_int, c_int, c_float, c_float, P]),
     "cvl_bn_acc_decode": (c_int, [P, P, ctypes.c_int64, P]),
     "cvl_debug_wgx_stamps": (c_int, [P, c_int]),
+    "cvl_stem_conv7x7s2": (c_int, [P, c_int, c_int, c_int, P, P, P, P, P]),
+    "cvl_stem_wgrad_workspace_size": (c_size_t, [c_int, c_int, c_int]),
+    "cvl_stem_wgrad": (c_int, [P, c_int, c_int, c_int, P, P, c_float, P, c_size_t, P]),
     "cvl_bn_apply": (c_int, [P, P, P, P, P, P, c_int, c_int, c_int, c_int, P]),
     "cvl_bn_finalize_apply": (c_int, [P, P, P, P, P, P, P, P, P, c_int, c_int, c_int, c_int, c_float, c_float, P]),
     "cvl_bn_backward_workspace_size": (c_size_t, [c_int, c_int, c_int]),

@@ -195,6 +195,23 @@ class PackPlan(object):
         _lib.call("cvl_pack_conv_weights_multi", ptr(self.items), ptr(self.tiles), self.ntiles, stream())
 
 
+def stem_conv7x7s2(img, w_packed, bias, z, stats=None):
+    """ResNet conv1 from the fp32 NHWC image (cvl_stem_conv7x7s2): z [B][Ho][Wo][64] bf16 (+ BN stats)."""
+    B, H, W, C = img.shape
+    assert C == 3 and img.dtype == torch.float32 and img.is_contiguous()
+    _lib.call("cvl_stem_conv7x7s2", ptr(img), B, H, W, ptr(w_packed), ptr(bias), ptr(z), ptr(stats), stream())
+
+
+def stem_wgrad(img, dz, dw, beta=0.0):
+    """dw [192][64] fp32 (padded K order, cvl_stem_wgrad) = beta*dw + the stem's weight gradient."""
+    B, H, W, _ = img.shape
+    n = int(_lib.load().cvl_stem_wgrad_workspace_size(B, H, W))
+    ws = torch.empty(max(n, 16), dtype=torch.uint8, device=img.device)
+    _lib.call("cvl_stem_wgrad", ptr(img), B, H, W, ptr(dz), ptr(dw), float(beta), ptr(ws), ws.numel(), stream())
+    if _wgrad_pending is not None:
+        _wgrad_pending.append(ws)
+
+
 def im2col(x, KH, KW, stride, pad_t, pad_l, Ho, Wo, Kp, out):
     B, H, W, C = x.shape
     _lib.call("cvl_im2col", ptr(x), B, H, W, C, KH, KW, stride, pad_t, pad_l, Ho, Wo, Kp, ptr(out), stream())

@@ -18,12 +18,12 @@ from .layers import BF16, BatchNorm, Conv, ConvBN, StatsArena
 STEM_K = 7
 # the stem's BN -> ReLU -> max-pool as one pass from z (CVL_STEM_NO_FUSE_POOL=1: BN apply + pool)
 FUSE_POOL = os.environ.get("CVL_STEM_NO_FUSE_POOL", "0") != "1"
-STEM_KP = int(os.environ.get("CVL_STEM_KP", 192))   # im2col K = 7*7*3 = 147 padded: 192 = 3 x 64 lets the
-#                                                      LDS-DMA kernels take the stem (+0.6 % step vs 160)
+STEM_KP = 168                                       # cvl_stem_conv7x7s2 K: 7 kernel rows x (21 -> 24)
 
 
 class Stem(object):
-    """conv1_conv (7x7/2 after ZeroPadding2D(3)) as im2col + 1x1 MFMA GEMM, conv1_bn, ReLU, pool1."""
+    """conv1_conv (7x7/2 after ZeroPadding2D(3)) straight from the image (cvl_stem_conv7x7s2 /
+    cvl_stem_wgrad: patch tiles built in LDS, no im2col matrix in HBM), conv1_bn, ReLU, pool1."""
 
     def __init__(self, store):
         self.conv = Conv(store, "conv1_conv", STEM_K, 3, 64, stride=2, pad=3, bias=True, dgrad=False,
@@ -31,8 +31,9 @@ class Stem(object):
         self.bn = BatchNorm(store, "conv1_bn", 64)
 
     def pack_entry(self):
-        # HWIO [7][7][3][64] == [1][1][147][64]: pack as a 1x1 conv with 147 -> 192 channels (the
-        # im2col GEMM); fp32 parity mode: a direct 7x7/2 conv over the 3 image channels
+        # HWIO [7][7][3][64] == [7][1][21][64]: packed as 7 "taps" (kernel rows) of 21 channels
+        # (kx, c) padded to 24 -- the stem kernel's K order; fp32 parity mode: a direct 7x7/2 conv
+        # over the 3 image channels
         c = self.conv
         if c.store.act != BF16:
             if c.wf is None:
@@ -40,7 +41,7 @@ class Stem(object):
             return (c.w, 49, 3, 64, 3, 64, c.wf, 0, 0, None)
         if c.wf is None:
             c.wf = torch.empty((64, STEM_KP), dtype=BF16, device=c.store.flat.device)
-        return (c.w, 1, 147, 64, STEM_KP, 64, c.wf, 0, 0, None)
+        return (c.w, 7, 21, 64, 24, 64, c.wf, 0, 0, None)
 
     def _desc7(self, B, H, W, Ho, Wo):
         """fp32 parity mode: conv1 as a direct 7x7/2 conv (ZeroPadding2D(3) = explicit pad 3)."""
@@ -50,11 +51,10 @@ class Stem(object):
     def pack(self):
         c = self.conv
         self.pack_entry()
-        nn.pack_conv_weights(c.w, 1, 1, 147, 64, STEM_KP, 64, c.wf)
-
-    def _desc(self, B, Ho, Wo):
-        return nn.make_desc(nn.FWD, B, STEM_KP, 1, 1, 1, 0, 0, 64, 64, 64,
-                            [nn.seg(Ho, Wo, Ho, Wo, self.conv.wf, self.conv.b)])
+        if c.store.act != BF16:
+            nn.pack_conv_weights(c.w, 7, 7, 3, 64, 3, 64, c.wf)
+        else:
+            nn.pack_conv_weights(c.w, 7, 1, 21, 64, 24, 64, c.wf)
 
     def forward(self, x, train=True, arena=None):
         B, H, W, _ = x.shape
@@ -64,12 +64,10 @@ class Stem(object):
         if train:
             stats = arena.take(B, 64) if arena is not None else nn.bn_acc(B, 64, x.device)
         z = torch.empty((B, Ho, Wo, 64), dtype=act, device=x.device)
+        A = x                                       # the fp32 image (the weight gradient reads it)
         if act == BF16:
-            A = torch.empty((B * Ho * Wo, STEM_KP), dtype=BF16, device=x.device)
-            nn.im2col(x, STEM_K, STEM_K, 2, pt, pl, Ho, Wo, STEM_KP, A)
-            nn.conv_igemm(self._desc(B, Ho, Wo), A, z, stats)
+            nn.stem_conv7x7s2(x, self.conv.wf, self.conv.b, z, stats)
         else:
-            A = x                                   # the fp32 image itself (direct conv)
             nn.conv_igemm(self._desc7(B, H, W, Ho, Wo), x, z, stats)
         Hp, Wp = (Ho + 2 - 3) // 2 + 1, (Wo + 2 - 3) // 2 + 1
         p = torch.empty((B, Hp, Wp, 64), dtype=act, device=x.device)
@@ -97,13 +95,13 @@ class Stem(object):
         nn.maxpool3x3s2_backward(dp, arg, dy)
         nn.bn_backward_relu(dy, z, mr, self.bn.gamma, self.bn.beta, dz, st.g(self.bn.gname),
                             st.g(self.bn.bname), B, Ho * Wo, 64, conv_dbias=self.conv.db)
-        if A.dtype != BF16:                         # fp32 parity mode: 7x7 weight gradient in place
+        if z.dtype != BF16:                         # fp32 parity mode: 7x7 weight gradient in place
             nn.conv_wgrad(self._desc7(B, A.shape[1], A.shape[2], Ho, Wo), A, dz, self.conv.dw)
             return
-        dw = torch.empty((STEM_KP, 64), dtype=torch.float32, device=dp.device)
-        nn.conv_wgrad(self._desc(B, Ho, Wo), A, dz, dw)
+        dw = torch.empty((192, 64), dtype=torch.float32, device=dp.device)    # rows ky*24 + kx*3 + c
+        nn.stem_wgrad(A, dz, dw)
         nn.wgrad_flush()                             # dw is read right away (deferred reductions)
-        self.conv.dw.view(147, 64).copy_(dw[:147])
+        self.conv.dw.view(7, 21, 64).copy_(dw.view(8, 24, 64)[:7, :21])
 
 
 class Bottleneck(object):

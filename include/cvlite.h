@@ -236,6 +236,20 @@ typedef struct {
 int cvl_pack_conv_weights_multi(const cvl_pack_item* items, const int32_t* tiles, int ntiles,
                                 cvl_stream_t stream);
 
+/* ResNet stem straight from the image (Keras ResNet50 conv1: ZeroPadding2D(3) + Conv2D(64, 7,
+ * strides=2) + bias, behind FCOS/fcos.py:30-46 and RetinaNet/retinanet_module.py:39-72; no im2col
+ * matrix in HBM).  img fp32 NHWC [B][H][W][3]; Ho = (H-1)/2+1, Wo = (W-1)/2+1.  K order k = ky*24 +
+ * kx*3 + c (each kernel row's 21 taps x channels padded to 24): w_packed = cvl_pack_conv_weights of
+ * the HWIO [7][7][3][64] kernel viewed as KH=7, KW=1, Cin=21, Cin_k=24, Npad=64 ([64][168] bf16).
+ * Forward: z [B][Ho][Wo][64] bf16 = bf16(conv(bf16(img)) + bias), bn_stats (nullable) = the BN
+ * accumulators of z.  Weight gradient: dw [192][64] fp32 = beta*dw + sum over pixels, rows in the
+ * same padded K order (HWIO row ky*21+kx*3+c = dw row ky*24+kx*3+c; pad rows 0); deterministic. */
+int cvl_stem_conv7x7s2(const float* img, int B, int H, int W, const void* w_packed, const float* bias, void* z,
+                       uint64_t* bn_stats, cvl_stream_t stream);
+size_t cvl_stem_wgrad_workspace_size(int B, int H, int W);
+int cvl_stem_wgrad(const float* img, int B, int H, int W, const void* dz, float* dw, float beta, void* workspace,
+                   size_t workspace_bytes, cvl_stream_t stream);
+
 /* fp32 NHWC image -> bf16 im2col rows [B*Ho*Wo][Kp] (ResNet50 conv1 after ZeroPadding2D(3)). */
 int cvl_im2col(const float* x, int B, int H, int W, int C, int KH, int KW, int stride, int pad_t,
                int pad_l, int Ho, int Wo, int Kp, void* out, cvl_stream_t stream);

@@ -482,6 +482,51 @@ def check_im2col(lp, name, launch, x, KH, KW, stride, pad_t, pad_l, Ho, Wo, Kp, 
              out.view(-1, Kp), ref.to(torch.bfloat16))
 
 
+def _stem_cols(img, Ho, Wo):
+    """[B*Ho*Wo, 192] float64 patch rows of the bf16-rounded image in the stem kernels' K order
+    (k = ky*24 + kx*3 + c; 21..23 of each kernel row and 168..191 zero)."""
+    B = img.shape[0]
+    x = F.pad(img.to(torch.bfloat16).double().permute(0, 3, 1, 2), (3, 3, 3, 3))     # ZeroPadding2D(3)
+    cols = F.unfold(x, 7, stride=2)                                                  # [B, (c, ky, kx), L]
+    L = cols.shape[-1]
+    assert L == Ho * Wo
+    cols = cols.view(B, 3, 7, 7, L).permute(0, 4, 2, 3, 1).reshape(B * L, 7, 21)   # [px, ky, (kx, c)]
+    out = torch.zeros((B * L, 8, 24), dtype=F64, device=img.device)
+    out[:, :7, :21] = cols
+    return out.view(B * L, 192)
+
+
+def check_stem_conv(lp, name, launch, img, w_packed, bias, z, stats=None):
+    st0 = stats.clone() if stats is not None else None
+    launch(img, w_packed, bias, z, stats)
+    B, H, W, _ = img.shape
+    Ho, Wo = z.shape[1], z.shape[2]
+    cols = _stem_cols(img, Ho, Wo)
+    wk = torch.zeros((192, 64), dtype=F64, device=img.device)
+    wk[:168] = w_packed.double().t()
+    ref = cols @ wk + (bias.double() if bias is not None else 0.0)
+    detail = "stem 7x7/2 %dx%d B%d" % (H, W, B)
+    lp.cmp(name, detail, "z", z.reshape(-1, 64), ref, "STEM", tol=TOL_BF16)
+    if stats is not None:
+        got = _acc(stats - st0, B, 64)
+        zz = z.double().reshape(B, Ho * Wo, 64)
+        r = torch.stack([zz.sum(1), (zz * zz).sum(1)], -1)
+        rabs = torch.stack([zz.abs().sum(1), (zz * zz).sum(1)], -1)
+        lp.add(name, detail, "bn_stats", max(red_err(got[b], r[b], rabs[b]) for b in range(B)), 1e-6, "STEM")
+
+
+def check_stem_wgrad(lp, name, launch, img, dz, dw, beta=0.0):
+    old = dw.clone() if beta != 0.0 else None
+    launch(img, dz, dw, beta)
+    lp.flush_wgrad()
+    B, H, W, _ = img.shape
+    Ho, Wo = dz.shape[1], dz.shape[2]
+    ref = _stem_cols(img, Ho, Wo).t() @ dz.double().reshape(-1, 64)
+    if beta != 0.0:
+        ref = ref + beta * old.double()
+    lp.cmp(name, "stem wgrad 7x7/2 %dx%d B%d" % (H, W, B), "dW", dw, ref, "STEM", tol=TOL_F32)
+
+
 def check_packplan(lp, name, launch, plan):
     launch()
     for i, (w, wf, wd) in enumerate(plan._keep):
@@ -1103,6 +1148,8 @@ CHECKS = {
     "conv_igemm_dgrad_bnsum_res": check_dgrad_bnsum_res,
     "pack_conv_weights": check_pack_conv_weights,
     "im2col": check_im2col,
+    "stem_conv7x7s2": check_stem_conv,
+    "stem_wgrad": check_stem_wgrad,
     "bn_finalize": check_bn_finalize,
     "bn_apply": check_bn_apply,
     "bn_finalize_apply": check_bn_finalize_apply,
