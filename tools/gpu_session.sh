@@ -1,0 +1,30 @@
+#!/bin/bash
+# One GPU call, several measurements: tools/gpu_session.sh <tag> [steps...]
+# steps: tests bench table wgx prof ceiling (default: all).  Each step has its own time limit; a
+# fault / abort / time-out (exit 124, 134, 137, 139) ends the session there.  Output: gpurun_out/<tag>_*.
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
+mkdir -p gpurun_out
+tag=$1; shift
+steps=${*:-tests bench table wgx prof ceiling}
+run() {   # run <seconds> <log> <cmd...>
+  local t=$1 log=$2; shift 2
+  echo "== $* ($(date +%T))"
+  timeout -k 10 "$t" "$@" > "$log" 2>&1
+  local st=$?
+  echo "   exit $st"
+  case $st in 124|134|137|139) echo "   fault/timeout: stopping"; exit $st ;; esac
+  return 0
+}
+for s in $steps; do
+  case $s in
+    tests)   run 900 gpurun_out/${tag}_pytest.log python -u -m pytest tests -m gpu -q --timeout 300 --timeout-method thread
+             tail -4 gpurun_out/${tag}_pytest.log ;;
+    bench)   run 300 gpurun_out/${tag}_bench.err bash -c "python -u bench.py --steps 30 --runs 1 --no-cpu-baseline > gpurun_out/${tag}_bench.json"
+             tail -c 300 gpurun_out/${tag}_bench.json; echo ;;
+    table)   run 240 gpurun_out/${tag}_table.log python -u tools/conv_table.py --out gpurun_out/${tag}_conv_table.md
+             head -4 gpurun_out/${tag}_conv_table.md ;;
+    wgx)     run 240 gpurun_out/${tag}_wgx.md python -u tools/wgx_stamps.py ;;
+    prof)    run 300 gpurun_out/${tag}_prof.log rocprofv3 --kernel-trace --stats -d gpurun_out/${tag}_prof -o p -- python3 bench.py --steps 10 --warmup 5 --runs 1 --no-cpu-baseline ;;
+    ceiling) run 60 gpurun_out/${tag}_ceiling.json ./tools/mfma_ceiling; cat gpurun_out/${tag}_ceiling.json ;;
+  esac
+done
