@@ -1,6 +1,6 @@
 #!/bin/bash
 # One GPU call, several measurements: tools/gpu_session.sh <tag> [steps...]
-# steps: tests bench table wgx prof ceiling (default: all).  Each step has its own time limit; a
+# steps: tests bench table wgx prof ceiling (default: all; limits sum to 1080 s).  Each step has its own time limit; a
 # fault / abort / time-out (exit 124, 134, 137, 139) ends the session there.  Output: gpurun_out/<tag>_*.
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
 mkdir -p gpurun_out
@@ -17,14 +17,18 @@ run() {   # run <seconds> <log> <cmd...>
 }
 for s in $steps; do
   case $s in
-    tests)   run 900 gpurun_out/${tag}_pytest.log python -u -m pytest tests -m gpu -q --timeout 300 --timeout-method thread
+    tests)   run 540 gpurun_out/${tag}_pytest.log python -u -m pytest tests -m gpu -q --timeout 300 --timeout-method thread
              tail -4 gpurun_out/${tag}_pytest.log ;;
-    bench)   run 300 gpurun_out/${tag}_bench.err bash -c "python -u bench.py --steps 30 --runs 1 --no-cpu-baseline > gpurun_out/${tag}_bench.json"
+    bench)   run 150 gpurun_out/${tag}_bench.err bash -c "python -u bench.py --steps 30 --runs 1 --no-cpu-baseline > gpurun_out/${tag}_bench.json"
              tail -c 300 gpurun_out/${tag}_bench.json; echo ;;
-    table)   run 240 gpurun_out/${tag}_table.log python -u tools/conv_table.py --out gpurun_out/${tag}_conv_table.md
+    table)   run 120 gpurun_out/${tag}_table.log python -u tools/conv_table.py --out gpurun_out/${tag}_conv_table.md
              head -4 gpurun_out/${tag}_conv_table.md ;;
-    wgx)     run 240 gpurun_out/${tag}_wgx.md python -u tools/wgx_stamps.py ;;
-    prof)    run 300 gpurun_out/${tag}_prof.log rocprofv3 --kernel-trace --stats -d gpurun_out/${tag}_prof -o p -- python3 bench.py --steps 10 --warmup 5 --runs 1 --no-cpu-baseline ;;
-    ceiling) run 60 gpurun_out/${tag}_ceiling.json ./tools/mfma_ceiling; cat gpurun_out/${tag}_ceiling.json ;;
+    wgx)     run 90 gpurun_out/${tag}_wgx.md python -u tools/wgx_stamps.py ;;
+    prof)    run 150 gpurun_out/${tag}_prof.log rocprofv3 --kernel-trace --stats -d gpurun_out/${tag}_prof -o p -- python3 bench.py --steps 10 --warmup 5 --runs 1 --no-cpu-baseline ;;
+    ceiling) run 30 gpurun_out/${tag}_ceiling.json ./tools/mfma_ceiling; cat gpurun_out/${tag}_ceiling.json ;;
+    pprobe)  run 90 gpurun_out/${tag}_pprobe.md python -u tools/p_probe.py; cat gpurun_out/${tag}_pprobe.md ;;
+    pstamps) run 90 gpurun_out/${tag}_pstamps.txt python -u tools/p_stamps.py; cat gpurun_out/${tag}_pstamps.txt ;;
+    stem)    run 200 gpurun_out/${tag}_stem.log python -u -m pytest tests/test_gpu_stem.py tests/test_gpu_bn_acc.py -q --timeout 150 --timeout-method thread
+             tail -3 gpurun_out/${tag}_stem.log ;;
   esac
 done
