@@ -26,6 +26,7 @@ for s in $steps; do
     wgx)     run 90 gpurun_out/${tag}_wgx.md python -u tools/wgx_stamps.py ;;
     prof)    run 150 gpurun_out/${tag}_prof.log rocprofv3 --kernel-trace --stats -d gpurun_out/${tag}_prof -o p -- python3 bench.py --steps 10 --warmup 5 --runs 1 --no-cpu-baseline ;;
     ceiling) run 30 gpurun_out/${tag}_ceiling.json ./tools/mfma_ceiling; cat gpurun_out/${tag}_ceiling.json ;;
+    rowdma)  run 60 gpurun_out/${tag}_rowdma.txt ./tools/ubench_rowdma; cat gpurun_out/${tag}_rowdma.txt ;;
     pprobe)  run 90 gpurun_out/${tag}_pprobe.md python -u tools/p_probe.py; cat gpurun_out/${tag}_pprobe.md ;;
     pstamps) run 90 gpurun_out/${tag}_pstamps.txt python -u tools/p_stamps.py; cat gpurun_out/${tag}_pstamps.txt ;;
     stem)    run 200 gpurun_out/${tag}_stem.log python -u -m pytest tests/test_gpu_stem.py tests/test_gpu_bn_acc.py -q --timeout 150 --timeout-method thread
