@@ -89,9 +89,14 @@ struct AccLocal {
   }
 };
 
+// A statistic decoded IN PLACE (acc_decode_inplace) holds its float64 value in slot 0 and this
+// marker in slot 7: the hot consumers then read one double (acc_dec), and a second decode is a no-op.
+constexpr acc_u64 kAccDecoded = ~0ull;
+
 // the statistic's value: bins decoded in a fixed order (smallest first), each exact integer
 // rounded once to float64 and scaled by a power of two
 __device__ __forceinline__ double acc_value(const acc_u64* s) {
+  if (s[kAccBins] == kAccDecoded) return __longlong_as_double((long long)s[0]);
   if (s[kAccBins] != 0) return __builtin_nan("");
   double t = 0.0;
 #pragma unroll
@@ -101,3 +106,20 @@ __device__ __forceinline__ double acc_value(const acc_u64* s) {
 
 // statistic s (0 or 1) of (image b, channel c) in a [B][C][2][8] buffer
 __device__ __forceinline__ long acc_idx(long bc, int s) { return (bc * 2 + s) * kAccSlots; }
+
+// one statistic: bins -> its float64 value in slot 0 (+ the marker); a decoded one is left alone
+__device__ __forceinline__ void acc_decode_inplace(acc_u64* s) {
+  if (s[kAccBins] == kAccDecoded) return;
+  const double v = acc_value(s);
+  s[0] = (acc_u64)__double_as_longlong(v);
+  s[kAccBins] = kAccDecoded;
+}
+
+// the float64 value of statistic s of (b, c) of a buffer decoded in place
+__device__ __forceinline__ double acc_dec(const acc_u64* buf, long bc, int s) {
+  return __longlong_as_double((long long)buf[acc_idx(bc, s)]);
+}
+__device__ __forceinline__ void acc_store_dec(acc_u64* buf, long bc, int s, double v) {
+  buf[acc_idx(bc, s)] = (acc_u64)__double_as_longlong(v);
+  buf[acc_idx(bc, s) + kAccBins] = kAccDecoded;
+}

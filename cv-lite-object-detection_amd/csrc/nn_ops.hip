@@ -261,8 +261,8 @@ __device__ __forceinline__ void bn_running(const acc_u64* stats, int B, int C, i
 #pragma unroll
     for (int u = 0; u < 8; ++u) {
       const long bc = (long)min(b0 + u, B - 1) * C + c;
-      s1[u] = acc_value(stats + acc_idx(bc, 0));
-      s2[u] = acc_value(stats + acc_idx(bc, 1));
+      s1[u] = acc_dec(stats, bc, 0);
+      s2[u] = acc_dec(stats, bc, 1);
     }
 #pragma unroll
     for (int u = 0; u < 8; ++u) {
@@ -288,7 +288,7 @@ __global__ void bn_finalize_kernel(const acc_u64* stats, float* mr, float* run_m
     float mean, rstd;
     double var;
     const long bc = (long)b * C + c;
-    bn_moments(acc_value(stats + acc_idx(bc, 0)), acc_value(stats + acc_idx(bc, 1)), HW, eps, &mean, &rstd, &var);
+    bn_moments(acc_dec(stats, bc, 0), acc_dec(stats, bc, 1), HW, eps, &mean, &rstd, &var);
     mr[((long)b * C + c) * 2] = mean;
     mr[((long)b * C + c) * 2 + 1] = rstd;
   }
@@ -333,8 +333,7 @@ __global__ void __launch_bounds__(NT) bn_apply_kernel(const cvl_bf16* __restrict
       const long bc = (long)b * C + c;
       float mm, rr;
       double var;
-      bn_moments(acc_value(fin.stats + acc_idx(bc, 0)), acc_value(fin.stats + acc_idx(bc, 1)), HW, fin.eps, &mm, &rr,
-                 &var);
+      bn_moments(acc_dec(fin.stats, bc, 0), acc_dec(fin.stats, bc, 1), HW, fin.eps, &mm, &rr, &var);
       smr[c] = float2{mm, rr};
       if (blockIdx.x == 0) { fin.mr_out[bc * 2] = mm; fin.mr_out[bc * 2 + 1] = rr; }
     }
@@ -459,8 +458,8 @@ __global__ void __launch_bounds__(NT) bn_bwd_kernel(const cvl_bf16* __restrict__
       double a1 = 0.0, a2 = 0.0;
 #pragma unroll 8
       for (int bb = 0; bb < (int)gridDim.y; ++bb) {
-        a1 += acc_value(ps + acc_idx((long)bb * C + c, 0));
-        a2 += acc_value(ps + acc_idx((long)bb * C + c, 1));
+        a1 += acc_dec(ps, (long)bb * C + c, 0);
+        a2 += acc_dec(ps, (long)bb * C + c, 1);
       }
       pg.dbeta[c] = (float)a1 + (pg.beta_acc != 0.f ? pg.beta_acc * pg.dbeta[c] : 0.f);
       pg.dgamma[c] = (float)a2 + (pg.beta_acc != 0.f ? pg.beta_acc * pg.dgamma[c] : 0.f);
@@ -487,8 +486,8 @@ __global__ void __launch_bounds__(NT) bn_bwd_kernel(const cvl_bf16* __restrict__
       be[u] = zmask ? bnb[c0 + u] : 0.f;
       s1[u] = 0.f; s2[u] = 0.f;
       if (PASS == 1) {
-        k1[u] = (float)acc_value(sums + acc_idx(bc, 0)) * inv;     // mean(g)
-        k2[u] = (float)acc_value(sums + acc_idx(bc, 1)) * inv;     // mean(g * xhat)
+        k1[u] = (float)acc_dec(sums, bc, 0) * inv;     // mean(g)
+        k2[u] = (float)acc_dec(sums, bc, 1) * inv;     // mean(g * xhat)
         gm[u] = gamma[c0 + u] * rs[u];
       }
     }
@@ -578,6 +577,7 @@ __global__ void __launch_bounds__(NT) bn_bwd_kernel(const cvl_bf16* __restrict__
 // out[y][c][0..1] = sum_r part[y][r][c][0..1]: a block owns 32 channels (256 contiguous bytes per
 // row) and 8 row groups; the row groups are combined in a fixed order (deterministic, float64) and
 // the total is stored exactly as an accumulator (bn_acc.h; the format the fused producers write)
+template <bool BINS>
 __global__ void __launch_bounds__(NT) bn_colsum_kernel(const float* __restrict__ part, int R, int C,
                                                        acc_u64* __restrict__ out) {
   const int y = blockIdx.y;
@@ -606,9 +606,14 @@ __global__ void __launch_bounds__(NT) bn_colsum_kernel(const float* __restrict__
   if (rg == 0 && c < C) {
     double t1 = 0.0, t2 = 0.0;
     for (int k = 0; k < 8; ++k) { t1 += red[k][cl][0]; t2 += red[k][cl][1]; }
-    AccLocal l;
-    l.zero(); l.add_f64(t1); l.store(out + acc_idx((long)y * C + c, 0));
-    l.zero(); l.add_f64(t2); l.store(out + acc_idx((long)y * C + c, 1));
+    if (BINS) {           // a public statistics buffer (cvl_bn_stats): accumulator bins
+      AccLocal l;
+      l.zero(); l.add_f64(t1); l.store(out + acc_idx((long)y * C + c, 0));
+      l.zero(); l.add_f64(t2); l.store(out + acc_idx((long)y * C + c, 1));
+    } else {              // an internal one: already in the decoded form its consumer reads
+      acc_store_dec(out, (long)y * C + c, 0, t1);
+      acc_store_dec(out, (long)y * C + c, 1, t2);
+    }
   }
 }
 
@@ -1184,12 +1189,11 @@ __global__ void bn_finalize_grouped_kernel(const acc_u64* stats, float* mr, floa
   float rm = run_mean ? run_mean[c] : 0.f, rv = run_var ? run_var[c] : 0.f;
   for (int g0 = 0; g0 < B; g0 += group) {
     const int g1 = min(g0 + group, B);
-    AccLocal l1, l2;                // the group's images summed exactly (integer bins), then decoded
-    l1.zero(); l2.zero();
-    for (int b = g0; b < g1; ++b) { l1.add(stats + acc_idx((long)b * C + c, 0)); l2.add(stats + acc_idx((long)b * C + c, 1)); }
-    acc_u64 t1[kAccSlots], t2[kAccSlots];
-    l1.store(t1); l2.store(t2);
-    const double s1 = acc_value(t1), s2 = acc_value(t2);
+    double s1 = 0.0, s2 = 0.0;      // the group's images in order (decoded statistics)
+    for (int b = g0; b < g1; ++b) {
+      s1 += acc_value(stats + acc_idx((long)b * C + c, 0));
+      s2 += acc_value(stats + acc_idx((long)b * C + c, 1));
+    }
     const double n = (double)(g1 - g0) * HW;
     const double mean = s1 / n;
     double var = s2 / n - mean * mean;
@@ -1207,17 +1211,27 @@ __global__ void bn_acc_decode_kernel(const acc_u64* acc, double* out, long n) {
   for (long i = blockIdx.x * (long)NT + threadIdx.x; i < n; i += (long)gridDim.x * NT) out[i] = acc_value(acc + i * kAccSlots);
 }
 
-// gs[b][c] = sum over b's group of s[b'][c] (integer bin sums: exact)
+// every statistic of a buffer decoded in place (one thread each), before its consumers read it
+__global__ void bn_acc_decode_inplace_kernel(acc_u64* acc, long n) {
+  const long i = blockIdx.x * (long)NT + threadIdx.x;
+  if (i < n) acc_decode_inplace(acc + i * kAccSlots);
+}
+
+inline int acc_decode_launch(acc_u64* acc, long nstat, hipStream_t s) {
+  hipLaunchKernelGGL(bn_acc_decode_inplace_kernel, dim3((unsigned)((nstat + NT - 1) / NT)), dim3(NT), 0, s, acc, nstat);
+  return cvl_launch_status();
+}
+
+// gs[b][c] = sum over b's group of s[b'][c] (decoded statistics, fixed order: deterministic)
 __global__ void bn_group_sum_kernel(const acc_u64* s, acc_u64* gs, int B, int C, int group) {
   const long i = blockIdx.x * (long)NT + threadIdx.x;
   if (i >= (long)B * C) return;
   const int b = (int)(i / C), c = (int)(i - (long)b * C);
   const int g0 = (b / group) * group, g1 = min(g0 + group, B);
-  AccLocal a1, a2;
-  a1.zero(); a2.zero();
-  for (int k = g0; k < g1; ++k) { a1.add(s + acc_idx((long)k * C + c, 0)); a2.add(s + acc_idx((long)k * C + c, 1)); }
-  a1.store(gs + acc_idx(i, 0));
-  a2.store(gs + acc_idx(i, 1));
+  double a1 = 0.0, a2 = 0.0;
+  for (int k = g0; k < g1; ++k) { a1 += acc_dec(s, (long)k * C + c, 0); a2 += acc_dec(s, (long)k * C + c, 1); }
+  acc_store_dec(gs, i, 0, a1);
+  acc_store_dec(gs, i, 1, a2);
 }
 
 }  // namespace
@@ -1284,9 +1298,11 @@ extern "C" int cvl_bn_acc_decode(const uint64_t* acc, double* out, int64_t n, cv
   return cvl_launch_status();
 }
 
-extern "C" int cvl_bn_finalize(const uint64_t* stats, float* mean_rstd, float* run_mean, float* run_var,
+extern "C" int cvl_bn_finalize(uint64_t* stats, float* mean_rstd, float* run_mean, float* run_var,
                                int B, int C, int HW, float eps, float momentum, cvl_stream_t stream) {
   CVL_CHECK_ARG(stats && mean_rstd && B > 0 && C > 0 && HW > 0);
+  const int dst = acc_decode_launch((acc_u64*)stats, 2L * B * C, S_);
+  if (dst) return dst;
   hipLaunchKernelGGL(bn_finalize_kernel, dim3((C + NT - 1) / NT), dim3(NT), 0, S_, (const acc_u64*)stats, mean_rstd,
                      run_mean, run_var, B, C, HW, eps, momentum);
   return cvl_launch_status();
@@ -1303,13 +1319,15 @@ extern "C" int cvl_bn_apply(const void* z, const float* mean_rstd, const float* 
   return cvl_launch_status();
 }
 
-extern "C" int cvl_bn_finalize_apply(const uint64_t* stats, float* mean_rstd, float* run_mean, float* run_var,
+extern "C" int cvl_bn_finalize_apply(uint64_t* stats, float* mean_rstd, float* run_mean, float* run_var,
                                      const void* z, const float* gamma, const float* beta, const void* residual,
                                      void* y, int B, int HW, int C, int relu, float eps, float momentum,
                                      cvl_stream_t stream) {
   CVL_CHECK_ARG(stats && mean_rstd && z && gamma && beta && y && C % 8 == 0 && B > 0 && HW > 0);
   CVL_CHECK_ARG(C <= BN_FIN_MAXC);
   CVL_CHECK_ARG((run_mean == nullptr) == (run_var == nullptr));
+  const int dst = acc_decode_launch((acc_u64*)stats, 2L * B * C, S_);    // once per statistic, not per block
+  if (dst) return dst;
   const int rpb = bn_rows_per_blk(B, HW, C);
   hipLaunchKernelGGL(bn_apply_kernel<true>, dim3((HW + rpb - 1) / rpb, B), dim3(NT), 0, S_, (const cvl_bf16*)z,
                      (const float*)nullptr, gamma, beta, (const cvl_bf16*)residual, (cvl_bf16*)y, C, HW, relu, rpb,
@@ -1345,7 +1363,7 @@ static int bn_backward_impl(const void* dy, const void* y_relu, const float* bn_
   hipLaunchKernelGGL(k0, g1, dim3(NT), 0, S_, (const cvl_bf16*)dy, (const cvl_bf16*)y_relu,
                      (const cvl_bf16*)z, mean_rstd, gamma, (const acc_u64*)nullptr, (cvl_bf16*)nullptr,
                      (cvl_bf16*)nullptr, part0, C, HW, rpb, 1, 0.f, BnPG{}, bn_beta, act_hi);
-  hipLaunchKernelGGL(bn_colsum_kernel, dim3((C + 31) / 32, B), dim3(NT), 0, S_, (const float*)part0, nchunk, C,
+  hipLaunchKernelGGL(bn_colsum_kernel<false>, dim3((C + 31) / 32, B), dim3(NT), 0, S_, (const float*)part0, nchunk, C,
                      sums);
   // pass 1 is elementwise (no partials): the apply kernels' finer chunking (~2048 workgroups)
   const int rpb1 = bn_rows_per_blk(B, HW, C);
@@ -1386,11 +1404,13 @@ extern "C" int cvl_bn_backward_relu6(const void* dy, const void* z, const float*
 // epilogue formed (cvl_conv_igemm_dgrad_bnsum): BN -> ReLU (act_hi = INF) or ReLU6 (act_hi = 6)
 // unit without a residual, mask rebuilt from z.
 extern "C" int cvl_bn_backward_relu_sums(const void* dy, const void* z, const float* mean_rstd, const float* gamma,
-                                         const float* beta, const uint64_t* sums, void* dz, float* dgamma,
+                                         const float* beta, uint64_t* sums, void* dz, float* dgamma,
                                          float* dbeta, float beta_acc, float* conv_dbias, float act_hi, int B,
                                          int HW, int C, cvl_stream_t stream) {
   CVL_CHECK_ARG(dy && z && mean_rstd && gamma && beta && sums && dz && dgamma && dbeta && C % 8 == 0);
   CVL_CHECK_ARG(B > 0 && HW > 0);
+  const int dst = acc_decode_launch((acc_u64*)sums, 2L * B * C, S_);
+  if (dst) return dst;
   const int rpb = bn_rows_per_blk(B, HW, C);
   const int nchunk = (HW + rpb - 1) / rpb;
   hipLaunchKernelGGL((bn_bwd_kernel<1, 2>), dim3(nchunk, B), dim3(NT), 0, S_, (const cvl_bf16*)dy, (const cvl_bf16*)nullptr,
@@ -1402,11 +1422,13 @@ extern "C" int cvl_bn_backward_relu_sums(const void* dy, const void* z, const fl
 // Second pass only for a residual unit (mask y > 0, g_out = the masked gradient for the shortcut),
 // from the (sum g, sum g*xhat) the producing data gradient formed (cvl_conv_igemm_dgrad_bnsum_res).
 extern "C" int cvl_bn_backward_res_sums(const void* dy, const void* y, const void* z, const float* mean_rstd,
-                                        const float* gamma, const uint64_t* sums, void* dz, void* g_out,
+                                        const float* gamma, uint64_t* sums, void* dz, void* g_out,
                                         float* dgamma, float* dbeta, float beta_acc, float* conv_dbias, int B,
                                         int HW, int C, cvl_stream_t stream) {
   CVL_CHECK_ARG(dy && y && z && mean_rstd && gamma && sums && dz && dgamma && dbeta && C % 8 == 0);
   CVL_CHECK_ARG(B > 0 && HW > 0);
+  const int dst = acc_decode_launch((acc_u64*)sums, 2L * B * C, S_);
+  if (dst) return dst;
   const int rpb = bn_rows_per_blk(B, HW, C);
   const int nchunk = (HW + rpb - 1) / rpb;
   hipLaunchKernelGGL((bn_bwd_kernel<1, 1>), dim3(nchunk, B), dim3(NT), 0, S_, (const cvl_bf16*)dy, (const cvl_bf16*)y,
@@ -1597,7 +1619,7 @@ extern "C" int cvl_bn_stats(const void* x, int B, int HW, int C, uint64_t* stats
                      (const cvl_bf16*)nullptr, (const cvl_bf16*)nullptr, (const float*)nullptr, (const float*)nullptr,
                      (const acc_u64*)nullptr, (cvl_bf16*)nullptr, (cvl_bf16*)nullptr, part, C, HW, rpb, 1, 0.f, BnPG{},
                      (const float*)nullptr, INFINITY);
-  hipLaunchKernelGGL(bn_colsum_kernel, dim3((C + 31) / 32, B), dim3(NT), 0, S_, (const float*)part, nchunk, C,
+  hipLaunchKernelGGL(bn_colsum_kernel<true>, dim3((C + 31) / 32, B), dim3(NT), 0, S_, (const float*)part, nchunk, C,
                      (acc_u64*)stats);
   return cvl_launch_status();
 }
@@ -1635,7 +1657,7 @@ extern "C" int cvl_bn_backward_grouped(const void* dy, const void* y_relu, const
   hipLaunchKernelGGL(bn_bwd_kernel<0>, g1, dim3(NT), 0, S_, (const cvl_bf16*)dy, (const cvl_bf16*)y_relu,
                      (const cvl_bf16*)z, mean_rstd, gamma, (const acc_u64*)nullptr, (cvl_bf16*)nullptr,
                      (cvl_bf16*)nullptr, part0, C, HW, rpb, group, 0.f, BnPG{}, (const float*)nullptr, INFINITY);
-  hipLaunchKernelGGL(bn_colsum_kernel, dim3((C + 31) / 32, B), dim3(NT), 0, S_, (const float*)part0, nchunk, C,
+  hipLaunchKernelGGL(bn_colsum_kernel<false>, dim3((C + 31) / 32, B), dim3(NT), 0, S_, (const float*)part0, nchunk, C,
                      sums);
   const acc_u64* use = sums;
   if (group > 1) {

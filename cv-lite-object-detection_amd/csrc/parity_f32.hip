@@ -544,7 +544,7 @@ extern "C" int cvl_bn_apply_f32(const float* z, const float* mean_rstd, const fl
   return cvl_launch_status();
 }
 
-extern "C" int cvl_bn_finalize_apply_f32(const uint64_t* stats, float* mean_rstd, float* run_mean, float* run_var,
+extern "C" int cvl_bn_finalize_apply_f32(uint64_t* stats, float* mean_rstd, float* run_mean, float* run_var,
                                          const float* z, const float* gamma, const float* beta, const float* residual,
                                          float* y, int B, int HW, int C, int relu, float eps, float momentum,
                                          cvl_stream_t stream) {

@@ -127,7 +127,10 @@ int cvl_fcos_center_v1_assign(const float* boxes, const int32_t* nbox, const flo
  * 7 counts non-finite ones), so the result is bit-identical whatever order the atomics land in.
  * Layout: uint64 [B][C][2][CVL_BN_ACC_SLOTS]; the value of a statistic is
  * sum_k (double)(int64)slot[k] * 2^(22k - 123) over k = 0..6 in that order (NaN if slot[7] != 0);
- * cvl_bn_acc_decode writes those values as float64 [n].
+ * cvl_bn_acc_decode writes those values as float64 [n].  The consumers (cvl_bn_finalize[_apply],
+ * cvl_bn_backward_*_sums) first DECODE THE BUFFER IN PLACE -- slot 0 of each statistic becomes its
+ * float64 value and slot 7 the marker ~0 -- so each statistic is decoded once, not by every block
+ * that reads it; a decoded buffer stays valid input for every reader (decode is idempotent).
  * ---------------------------------------------------------------------------------------- */
 #define CVL_BN_ACC_SLOTS 8
 int cvl_bn_acc_decode(const uint64_t* acc, double* out, int64_t n, cvl_stream_t stream);
@@ -260,14 +263,14 @@ int cvl_im2col(const float* x, int B, int H, int W, int C, int KH, int KW, int s
  * unbiased as TF's fused kernel).  stats: BN accumulators [B][C][2][8] from cvl_conv_igemm(bn_stats)
  * or cvl_bn_stats; mean_rstd [B][C][2].
  * ---------------------------------------------------------------------------------------- */
-int cvl_bn_finalize(const uint64_t* stats, float* mean_rstd, float* run_mean, float* run_var, int B,
+int cvl_bn_finalize(uint64_t* stats, float* mean_rstd, float* run_mean, float* run_var, int B,
                     int C, int HW, float eps, float momentum, cvl_stream_t stream);
 int cvl_bn_apply(const void* z, const float* mean_rstd, const float* gamma, const float* beta,
                  const void* residual, void* y, int B, int HW, int C, int relu, cvl_stream_t stream);
 /* cvl_bn_finalize + cvl_bn_apply in ONE launch (bit-identical results): every block derives the
  * (mean, rstd) of its image from stats; mean_rstd is still written for the backward and the running
  * statistics advanced (run_mean/run_var NULL together: inference-style, no EMA). */
-int cvl_bn_finalize_apply(const uint64_t* stats, float* mean_rstd, float* run_mean, float* run_var,
+int cvl_bn_finalize_apply(uint64_t* stats, float* mean_rstd, float* run_mean, float* run_var,
                           const void* z, const float* gamma, const float* beta, const void* residual, void* y,
                           int B, int HW, int C, int relu, float eps, float momentum, cvl_stream_t stream);
 /* dy: grad of y; y_relu: y when the unit ends in ReLU (mask), else NULL; writes dz (bf16),
@@ -302,7 +305,7 @@ int cvl_conv_igemm_dgrad_bnsum(const cvl_conv_desc* d, const void* src, void* ds
                                uint64_t* sums, int32_t* fused, void* workspace, size_t workspace_bytes,
                                cvl_stream_t stream);
 int cvl_bn_backward_relu_sums(const void* dy, const void* z, const float* mean_rstd, const float* gamma,
-                              const float* beta, const uint64_t* sums, void* dz, float* dgamma, float* dbeta,
+                              const float* beta, uint64_t* sums, void* dz, float* dgamma, float* dbeta,
                               float beta_acc, float* conv_dbias, float act_hi, int B, int HW, int C,
                               cvl_stream_t stream);
 /* The residual-unit form (a bottleneck's BN3: BN -> + shortcut -> ReLU, the block output y).  The
@@ -316,7 +319,7 @@ int cvl_conv_igemm_dgrad_bnsum_res(const cvl_conv_desc* d, const void* src, void
                                    const float* mean_rstd, const float* gamma, const float* beta, uint64_t* sums,
                                    int32_t* fused, void* workspace, size_t workspace_bytes, cvl_stream_t stream);
 int cvl_bn_backward_res_sums(const void* dy, const void* y, const void* z, const float* mean_rstd, const float* gamma,
-                             const uint64_t* sums, void* dz, void* g_out, float* dgamma, float* dbeta, float beta_acc,
+                             uint64_t* sums, void* dz, void* g_out, float* dgamma, float* dbeta, float beta_acc,
                              float* conv_dbias, int B, int HW, int C, cvl_stream_t stream);
 
 /* BN -> ReLU6 unit without a residual (MobileNetV2: Keras ReLU(6.)): as cvl_bn_backward_relu with
@@ -380,7 +383,7 @@ int cvl_bias_grad_multi(const cvl_bias_item* items, int n, void* workspace, size
  * ---------------------------------------------------------------------------------------- */
 int cvl_bn_apply_f32(const float* z, const float* mean_rstd, const float* gamma, const float* beta,
                      const float* residual, float* y, int B, int HW, int C, int relu, cvl_stream_t stream);
-int cvl_bn_finalize_apply_f32(const uint64_t* stats, float* mean_rstd, float* run_mean, float* run_var,
+int cvl_bn_finalize_apply_f32(uint64_t* stats, float* mean_rstd, float* run_mean, float* run_var,
                               const float* z, const float* gamma, const float* beta, const float* residual,
                               float* y, int B, int HW, int C, int relu, float eps, float momentum,
                               cvl_stream_t stream);

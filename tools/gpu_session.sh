@@ -21,10 +21,12 @@ for s in $steps; do
              tail -4 gpurun_out/${tag}_pytest.log ;;
     bench)   run 150 gpurun_out/${tag}_bench.err bash -c "python -u bench.py --steps 30 --runs 1 --no-cpu-baseline > gpurun_out/${tag}_bench.json"
              tail -c 300 gpurun_out/${tag}_bench.json; echo ;;
+    benchd)  run 150 gpurun_out/${tag}_benchd.err bash -c "CVL_STEM_DIRECT=1 python -u bench.py --steps 30 --runs 1 --no-cpu-baseline > gpurun_out/${tag}_benchd.json"
+             tail -c 200 gpurun_out/${tag}_benchd.json; echo ;;
     table)   run 120 gpurun_out/${tag}_table.log python -u tools/conv_table.py --out gpurun_out/${tag}_conv_table.md
              head -4 gpurun_out/${tag}_conv_table.md ;;
     wgx)     run 90 gpurun_out/${tag}_wgx.md python -u tools/wgx_stamps.py ;;
-    prof)    run 150 gpurun_out/${tag}_prof.log rocprofv3 --kernel-trace --stats -d gpurun_out/${tag}_prof -o p -- python3 bench.py --steps 10 --warmup 5 --runs 1 --no-cpu-baseline ;;
+    prof)    run 150 gpurun_out/${tag}_prof.log rocprofv3 --kernel-trace --stats -f csv -d gpurun_out/${tag}_prof -o p -- python3 bench.py --steps 10 --warmup 5 --runs 1 --no-cpu-baseline ;;
     ceiling) run 30 gpurun_out/${tag}_ceiling.json ./tools/mfma_ceiling; cat gpurun_out/${tag}_ceiling.json ;;
     rowdma)  run 60 gpurun_out/${tag}_rowdma.txt ./tools/ubench_rowdma; cat gpurun_out/${tag}_rowdma.txt ;;
     pprobe)  run 90 gpurun_out/${tag}_pprobe.md python -u tools/p_probe.py; cat gpurun_out/${tag}_pprobe.md ;;
