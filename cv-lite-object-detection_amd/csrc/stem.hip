@@ -3,31 +3,40 @@
 // FCOS/fcos.py:30-46 and RetinaNet/retinanet_module.py:39-72.  Forward (with the conv1_bn
 // statistics) and weight gradient; the input image has no gradient.
 //
-// The generic path materialised the im2col matrix of the 7x7x3 patches ([B*Ho*Wo][192] bf16, 403 MB
-// at 512x512 bs 16), wrote it once and read it twice (forward GEMM and weight gradient).  Here each
-// workgroup builds its patch tile in LDS from the fp32 image rows (which L1/L2 serve to the ~7
-// workgroups that share them) and feeds the MFMAs from there: the HBM traffic is the image (50 MB)
-// plus z / dz (134 MB), not the patch matrix.
+// The generic path materialises the im2col matrix of the 7x7x3 patches ([B*Ho*Wo][192] bf16, 403 MB
+// at 512x512 bs 16), writes it once and reads it twice (forward GEMM and weight gradient).  Here a
+// workgroup walks a band of output rows of one image (and one 256-pixel column range) and keeps a
+// ring of the image rows they need in LDS as bf16 -- each output row needs 7 image rows, the next
+// one 2 more -- and the MFMA operands are read straight out of that ring: the patch of output pixel
+// p, kernel row ky, is the 21 consecutive values of image row 2*oy + ky - 3 starting at element
+// 6*p (pixel 2*p - 3 + 3 of the ring's row, 3 channels).  HBM traffic: the image (~1.4x, the bands'
+// overlapping first rows) plus z / dz, no patch matrix.
 //
 // K order (both kernels, and the packed weights): k = ky * 24 + kx * 3 + c for kx < 7, c < 3 -- one
-// image row's 21 consecutive floats per ky, padded to 24 -- then k in [168, 192) zero (the 32-deep
-// MFMA step).  The packed forward weights are cvl_pack_conv_weights of the HWIO kernel viewed as
-// KH = 7, KW = 1, Cin = 21, Cin_k = 24 (w_fwd [64][168]); the weight gradient is written in the same
-// padded order, dw [192][64] fp32 (rows ky * 24 + kx * 3 + c; the pad rows come out 0).
+// image row's 21 consecutive values per ky, padded to 24 -- and k in [168, 192) for the last
+// 32-deep MFMA step.  The packed forward weights are cvl_pack_conv_weights of the HWIO kernel viewed
+// as KH = 7, KW = 1, Cin = 21, Cin_k = 24 (w_fwd [64][168]): their pad columns are zero, so the
+// ring values a pad k reads (the next pixel's, or a ring row not yet loaded: finite, the ring is
+// zeroed first) add nothing.  The weight gradient is written in the same padded order, dw [192][64]
+// fp32 (rows ky * 24 + kx * 3 + c; the pad rows come out 0).
 //
 // Numerics as the im2col path: the image rounded to bf16 (round to nearest even), bf16 MFMA with
 // fp32 accumulation, bias added in fp32, the output rounded to bf16; BN statistics of the rounded
-// output as exact accumulators (bn_acc.h).  Tile = 128 output pixels of one row.
+// output as exact accumulators (bn_acc.h), one add per (workgroup, channel).
 #include "conv_common.h"
 
 namespace {
 
 constexpr int NT = 256;                  // 4 waves
-constexpr int SP = 128;                  // output pixels per tile
+constexpr int SPX = 256;                 // output pixels per column range
+constexpr int RL = 1560;                 // ring row (bf16): (2 * SPX + 6) * 3 = 1554 values, padded
+constexpr int NRING = 12;                // ring rows (7 in use + 2 prefetched + slack)
 constexpr int KR = 168, KP = 192;        // real (7 x 24) and MFMA-padded K
-constexpr int KA = 200;                  // LDS pitch (elements) of the forward A / W rows
-constexpr int PA = 136;                  // LDS pitch (elements) of the weight gradient's transposed rows
+constexpr int WA = 200;                  // LDS pitch (elements) of the weight rows (forward)
+constexpr int DP = SPX + 8;              // LDS pitch (elements) of dz^T rows (weight gradient)
 constexpr int CO = 64;
+constexpr int RPW_F = 8, RPW_W = 16;     // output rows per workgroup (forward / weight gradient)
+constexpr int RPT = (RL + NT - 1) / NT;  // ring values per thread per image row
 
 struct StemArgs {
   const float* img;       // [B][H][W][3] fp32
@@ -36,234 +45,286 @@ struct StemArgs {
   const cvl_bf16* dz;     // [B][Ho][Wo][64] bf16 (weight gradient)
   cvl_bf16* z;            // [B][Ho][Wo][64] bf16 (forward)
   acc_u64* stats;         // [B][64][2][8] or null
-  float* out;             // weight gradient: slab [wgs][192][64] or dw
-  int B, H, W, Ho, Wo, ntx, tiles, tiles_per_wg;
+  float* out;             // weight gradient: slab [units][192][64] or dw
+  int B, H, W, Ho, Wo, ntx, nbands, rpw;
   float beta;
 };
 
-__device__ __forceinline__ s16x8 pack8f(const float* f) {
-  s16x8 v;
+struct Unit {
+  int b, x0, npx, oy0, oy1;
+};
+
+__device__ __forceinline__ Unit unit_of(const StemArgs& g, int u) {
+  Unit t;
+  const int band = u % g.nbands, r = u / g.nbands;
+  const int xt = r % g.ntx;
+  t.b = r / g.ntx;
+  t.x0 = xt * SPX;
+  t.npx = g.Wo - t.x0 < SPX ? g.Wo - t.x0 : SPX;
+  t.oy0 = band * g.rpw;
+  t.oy1 = t.oy0 + g.rpw < g.Ho ? t.oy0 + g.rpw : g.Ho;
+  return t;
+}
+
+// image row iy of the unit as ring values (bf16; zero outside the image): thread part only
+__device__ __forceinline__ void row_load(const StemArgs& g, const Unit& t, int iy, float (&v)[RPT]) {
+  const int tid = threadIdx.x;
+  const bool rok = (unsigned)iy < (unsigned)g.H;
+  const long rowbase = ((long)t.b * g.H + iy) * g.W * 3;
+  const int xs0 = 2 * t.x0 - 3;
 #pragma unroll
-  for (int u = 0; u < 8; ++u) v[u] = (short)f32_to_bf16(f[u]);
+  for (int q = 0; q < RPT; ++q) {
+    const int e = tid + q * NT;
+    const int p = xs0 + e / 3;
+    v[q] = (rok && e < (2 * SPX + 6) * 3 && (unsigned)p < (unsigned)g.W) ? g.img[rowbase + (long)p * 3 + e % 3] : 0.f;
+  }
+}
+__device__ __forceinline__ void row_store(cvl_bf16* ring, int iy, const float (&v)[RPT]) {
+  cvl_bf16* r = ring + ((iy + 3) % NRING) * RL;
+#pragma unroll
+  for (int q = 0; q < RPT; ++q) {
+    const int e = threadIdx.x + q * NT;
+    if (e < RL) r[e] = f32_to_bf16(v[q]);
+  }
+}
+
+// 8 consecutive ring values (16 B at a 4-B aligned address) as an MFMA fragment
+__device__ __forceinline__ s16x8 ring8(const cvl_bf16* p) {
+  const unsigned* u = reinterpret_cast<const unsigned*>(p);
+  const unsigned a = u[0], b = u[1], c = u[2], d = u[3];
+  s16x8 v;
+  v[0] = (short)(a & 0xffff); v[1] = (short)(a >> 16);
+  v[2] = (short)(b & 0xffff); v[3] = (short)(b >> 16);
+  v[4] = (short)(c & 0xffff); v[5] = (short)(c >> 16);
+  v[6] = (short)(d & 0xffff); v[7] = (short)(d >> 16);
   return v;
 }
 
-__device__ __forceinline__ void tile_coords(const StemArgs& g, int t, int* b, int* oy, int* x0) {
-  const int xt = t % g.ntx, r = t / g.ntx;
-  *oy = r % g.Ho;
-  *b = r / g.Ho;
-  *x0 = xt * SP;
-}
-
 // ---------------------------------------------------------------------------------------------
-// forward: one workgroup per tile.  LDS: A [128 px][KA] (row = the pixel's 192 patch values) and
-// W [64 co][KA]; 4 waves x (32 px x 64 co), 6 K-steps of v_mfma_f32_16x16x32_bf16.
+// forward: swapped operands D[co][px] = W[co][k] . patch[k][px], so a lane's accumulator quad is
+// 4 consecutive channels of one pixel (8-byte stores straight from the registers).  4 waves x 64
+// pixels x 64 channels, 6 K-steps per output row.  The next row's two image rows are loaded into
+// registers before the row's MFMAs and stored to the ring after them.
 // ---------------------------------------------------------------------------------------------
-__global__ void __launch_bounds__(NT) stem_fwd_kernel(StemArgs g) {
-  __shared__ __attribute__((aligned(16))) cvl_bf16 lds[SP * KA + CO * KA];
-  cvl_bf16* A = lds;
-  cvl_bf16* Wl = lds + SP * KA;
+__global__ void __launch_bounds__(NT, 2) stem_fwd_kernel(StemArgs g) {
+  __shared__ __attribute__((aligned(16))) cvl_bf16 Wl[CO * WA];
+  __shared__ __attribute__((aligned(16))) cvl_bf16 ring[NRING * RL];
+  __shared__ float red[4][CO][2];
   const int tid = threadIdx.x;
-  int b, oy, x0;
-  tile_coords(g, blockIdx.x, &b, &oy, &x0);
-
-  // weights: 64 rows x 24 chunks of 8 (chunks 21..23 = the zero K pad)
+  const Unit t = unit_of(g, blockIdx.x);
+  if (t.oy0 >= g.Ho) return;
   for (int i = tid; i < CO * (KP / 8); i += NT) {
     const int co = i / (KP / 8), ch = i - (i / (KP / 8)) * (KP / 8);
     s16x8 v = s16x8{0, 0, 0, 0, 0, 0, 0, 0};
     if (ch < KR / 8) v = *reinterpret_cast<const s16x8*>(g.w + co * KR + ch * 8);
-    *reinterpret_cast<s16x8*>(Wl + co * KA + ch * 8) = v;
+    *reinterpret_cast<s16x8*>(Wl + co * WA + ch * 8) = v;
   }
-  // patches: item (ky, px) = 21 consecutive floats of image row 2*oy + ky - 3 from pixel 2*ox - 3
-  const float* imgb = g.img + (long)b * g.H * g.W * 3;
-  for (int it = tid; it < 7 * SP; it += NT) {
-    const int ky = it / SP, px = it - (it / SP) * SP;
-    const int iy = 2 * oy + ky - 3, ox = x0 + px;
-    const int xs = 2 * ox - 3;
-    const bool rok = (unsigned)iy < (unsigned)g.H && ox < g.Wo;
-    const float* row = imgb + (long)iy * g.W * 3;
-    float f[24];
-#pragma unroll
-    for (int j = 0; j < 21; ++j) {
-      const int xx = xs + j / 3;
-      f[j] = (rok && (unsigned)xx < (unsigned)g.W) ? row[xx * 3 + j % 3] : 0.f;
+  for (int i = tid; i < NRING * RL / 8; i += NT) reinterpret_cast<s16x8*>(ring)[i] = s16x8{0, 0, 0, 0, 0, 0, 0, 0};
+  __syncthreads();
+  {
+    float v[RPT];
+    for (int iy = 2 * t.oy0 - 3; iy <= 2 * t.oy0 + 3; ++iy) {
+      row_load(g, t, iy, v);
+      row_store(ring, iy, v);
     }
-    f[21] = f[22] = f[23] = 0.f;
-    cvl_bf16* dst = A + px * KA + ky * 24;
-#pragma unroll
-    for (int q = 0; q < 3; ++q) *reinterpret_cast<s16x8*>(dst + q * 8) = pack8f(f + q * 8);
   }
-  for (int i = tid; i < SP * 3; i += NT)           // K pad [168, 192)
-    *reinterpret_cast<s16x8*>(A + (i / 3) * KA + KR + (i % 3) * 8) = s16x8{0, 0, 0, 0, 0, 0, 0, 0};
   __syncthreads();
 
   const int wave = tid >> 6, lane = tid & 63, lr = lane & 15, lg = lane >> 4;
-  f32x4 acc[2][4];
+  float bias[4][4];
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
+  for (int i = 0; i < 4; ++i)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int e = 0; e < 4; ++e) bias[i][e] = g.bias ? g.bias[i * 16 + lg * 4 + e] : 0.f;
+  float s1[4][4], s2[4][4];
 #pragma unroll
-  for (int ks = 0; ks < KP / 32; ++ks) {
-    s16x8 fa[2], fb[4];
+  for (int i = 0; i < 4; ++i)
 #pragma unroll
-    for (int i = 0; i < 2; ++i) fa[i] = *reinterpret_cast<const s16x8*>(A + (wave * 32 + i * 16 + lr) * KA + ks * 32 + lg * 8);
-#pragma unroll
-    for (int j = 0; j < 4; ++j) fb[j] = *reinterpret_cast<const s16x8*>(Wl + (j * 16 + lr) * KA + ks * 32 + lg * 8);
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, fa[i]),
-                                                             __builtin_bit_cast(bf16x8, fb[j]), acc[i][j], 0, 0, 0);
-  }
-  // epilogue: C[px][co] (row px = wave*32 + i*16 + lg*4 + e, col co = j*16 + lr); + bias, bf16
-  const int npx = g.Wo - x0 < SP ? g.Wo - x0 : SP;
-  float s1[4], s2[4];
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const float bj = g.bias ? g.bias[j * 16 + lr] : 0.f;
-    s1[j] = 0.f;
-    s2[j] = 0.f;
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const float v = bf16_to_f32(f32_to_bf16(acc[i][j][e] + bj));
-        acc[i][j][e] = v;
-        if (wave * 32 + i * 16 + lg * 4 + e < npx) { s1[j] += v; s2[j] += v * v; }
-      }
-  }
-  __syncthreads();                                   // A / W no longer read: reuse the LDS
-  float* red = reinterpret_cast<float*>(lds + SP * 72);    // [4 waves][64 co][2]
-  if (g.stats) {
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      float a1 = s1[j], a2 = s2[j];
-      a1 += __shfl_xor(a1, 16, 64); a1 += __shfl_xor(a1, 32, 64);
-      a2 += __shfl_xor(a2, 16, 64); a2 += __shfl_xor(a2, 32, 64);
-      if (lg == 0) {
-        red[(wave * CO + j * 16 + lr) * 2] = a1;
-        red[(wave * CO + j * 16 + lr) * 2 + 1] = a2;
-      }
-    }
-  }
-  cvl_bf16* Cs = lds;                                // [128 px][72] bf16
-#pragma unroll
-  for (int i = 0; i < 2; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j)
-#pragma unroll
-      for (int e = 0; e < 4; ++e)
-        Cs[(wave * 32 + i * 16 + lg * 4 + e) * 72 + j * 16 + lr] = f32_to_bf16(acc[i][j][e]);   // exact
-  __syncthreads();
-  if (g.stats && tid < CO) {
-    float a1 = 0.f, a2 = 0.f;
-#pragma unroll
-    for (int w = 0; w < 4; ++w) { a1 += red[(w * CO + tid) * 2]; a2 += red[(w * CO + tid) * 2 + 1]; }
-    acc_u64* st = g.stats + acc_idx((long)b * CO + tid, 0);
-    acc_add(st, a1);
-    acc_add(st + kAccSlots, a2);
-  }
-  cvl_bf16* zrow = g.z + ((long)(b * g.Ho + oy) * g.Wo + x0) * CO;
-  for (int i = tid; i < npx * 8; i += NT) {
-    const int px = i >> 3, c8 = (i & 7) * 8;
-    *reinterpret_cast<s16x8*>(zrow + (long)px * CO + c8) = *reinterpret_cast<const s16x8*>(Cs + px * 72 + c8);
-  }
-}
+    for (int e = 0; e < 4; ++e) { s1[i][e] = 0.f; s2[i][e] = 0.f; }
 
-// ---------------------------------------------------------------------------------------------
-// weight gradient: dw[k][co] = sum over output pixels of A[px][k] * dz[px][co].  A workgroup loops
-// over a contiguous range of tiles; per tile it builds A^T [192 k][128 px] and dz^T [64 co][128 px]
-// in LDS (so both MFMA operands are plain 16-byte row reads), then 4 K-steps over the pixels.  4
-// waves x (48 k x 64 co) accumulators; the partial [192][64] goes to the workgroup's fp32 slab,
-// summed in a fixed order by the shared split reducer (deterministic).
-// ---------------------------------------------------------------------------------------------
-__global__ void __launch_bounds__(NT) stem_wgrad_kernel(StemArgs g) {
-  __shared__ __attribute__((aligned(16))) cvl_bf16 lds[KP * PA + CO * PA];
-  cvl_bf16* At = lds;                      // [192][PA]
-  cvl_bf16* Dt = lds + KP * PA;            // [64][PA]
-  const int tid = threadIdx.x;
-  const int wave = tid >> 6, lane = tid & 63, lr = lane & 15, lg = lane >> 4;
-  // zero K rows (the per-ky pad 21..23 and [168, 192)): never written by the builds below
-  for (int i = tid; i < KP * (SP / 8); i += NT) {
-    const int k = i / (SP / 8), pg = i - (i / (SP / 8)) * (SP / 8);
-    if (k >= KR || k % 24 >= 21) *reinterpret_cast<s16x8*>(At + k * PA + pg * 8) = s16x8{0, 0, 0, 0, 0, 0, 0, 0};
-  }
-  f32x4 acc[3][4];
-#pragma unroll
-  for (int i = 0; i < 3; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  const int t0 = blockIdx.x * g.tiles_per_wg;
-  const int t1 = t0 + g.tiles_per_wg < g.tiles ? t0 + g.tiles_per_wg : g.tiles;
-  for (int t = t0; t < t1; ++t) {
-    int b, oy, x0;
-    tile_coords(g, t, &b, &oy, &x0);
-    const float* imgb = g.img + (long)b * g.H * g.W * 3;
-    __syncthreads();                       // the previous tile's fragment reads are done
-    // A^T: item (k < 168 with k % 24 < 21, px group of 8): 8 pixels 2 apart of one image row
-    for (int it = tid; it < 7 * 21 * (SP / 8); it += NT) {
-      const int kk = it / (SP / 8), pg = it - (it / (SP / 8)) * (SP / 8);
-      const int ky = kk / 21, r = kk - (kk / 21) * 21;
-      const int kx = r / 3, c = r - (r / 3) * 3;
-      const int iy = 2 * oy + ky - 3;
-      const bool rok = (unsigned)iy < (unsigned)g.H;
-      const float* row = imgb + (long)iy * g.W * 3 + c;
-      float f[8];
-#pragma unroll
-      for (int q = 0; q < 8; ++q) {
-        const int ox = x0 + pg * 8 + q, xx = 2 * ox + kx - 3;
-        f[q] = (rok && ox < g.Wo && (unsigned)xx < (unsigned)g.W) ? row[xx * 3] : 0.f;
-      }
-      *reinterpret_cast<s16x8*>(At + (ky * 24 + r) * PA + pg * 8) = pack8f(f);
+  for (int oy = t.oy0; oy < t.oy1; ++oy) {
+    const bool more = oy + 1 < t.oy1;
+    float n0[RPT], n1[RPT];
+    if (more) {                                     // image rows 2*oy + 4, 2*oy + 5 for row oy + 1
+      row_load(g, t, 2 * oy + 4, n0);
+      row_load(g, t, 2 * oy + 5, n1);
     }
-    // dz^T: lane = co, 8 pixel rows per 16-byte store (rows of 128 B read coalesced over the lanes)
-    const cvl_bf16* dzr = g.dz + ((long)(b * g.Ho + oy) * g.Wo + x0) * CO;
-    {
-      const int co = tid & 63, pq = tid >> 6;
+    f32x4 acc[4][4];
 #pragma unroll
-      for (int gg = 0; gg < 4; ++gg) {
-        const int pg = pq * 4 + gg;
-        s16x8 v;
+    for (int i = 0; i < 4; ++i)
 #pragma unroll
-        for (int q = 0; q < 8; ++q) {
-          const int px = pg * 8 + q;
-          v[q] = x0 + px < g.Wo ? (short)dzr[(long)px * CO + co] : (short)0;
-        }
-        *reinterpret_cast<s16x8*>(Dt + co * PA + pg * 8) = v;
-      }
-    }
-    __syncthreads();
+      for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int ks = 0; ks < SP / 32; ++ks) {
-      s16x8 fa[3], fb[4];
+    for (int s = 0; s < KP / 32; ++s) {
+      const int k0 = s * 32 + lg * 8, ky = k0 / 24, off = k0 - ky * 24;
+      const cvl_bf16* rr = ring + ((2 * oy + ky) % NRING) * RL + off;
+      s16x8 fa[4], fb[4];
 #pragma unroll
-      for (int i = 0; i < 3; ++i)
-        fa[i] = *reinterpret_cast<const s16x8*>(At + (wave * 48 + i * 16 + lr) * PA + ks * 32 + lg * 8);
+      for (int i = 0; i < 4; ++i) fa[i] = *reinterpret_cast<const s16x8*>(Wl + (i * 16 + lr) * WA + k0);
 #pragma unroll
-      for (int j = 0; j < 4; ++j) fb[j] = *reinterpret_cast<const s16x8*>(Dt + (j * 16 + lr) * PA + ks * 32 + lg * 8);
+      for (int j = 0; j < 4; ++j) fb[j] = ring8(rr + 6 * (wave * 64 + j * 16 + lr));
 #pragma unroll
-      for (int i = 0; i < 3; ++i)
+      for (int i = 0; i < 4; ++i)
 #pragma unroll
         for (int j = 0; j < 4; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, fa[i]),
                                                                __builtin_bit_cast(bf16x8, fb[j]), acc[i][j], 0, 0, 0);
     }
+    // epilogue: D[co = i*16 + lg*4 + e][px = wave*64 + j*16 + lr]
+    cvl_bf16* zrow = g.z + ((long)(t.b * g.Ho + oy) * g.Wo + t.x0) * CO;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int px = wave * 64 + j * 16 + lr;
+      const bool ok = px < t.npx;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        s16x4 o;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const cvl_bf16 h = f32_to_bf16(acc[i][j][e] + bias[i][e]);
+          const float v = bf16_to_f32(h);
+          o[e] = (short)h;
+          if (ok) { s1[i][e] += v; s2[i][e] += v * v; }
+        }
+        if (ok) *reinterpret_cast<s16x4*>(zrow + (long)px * CO + i * 16 + lg * 4) = o;
+      }
+    }
+    if (more) {
+      __syncthreads();                              // (no reader of these two slots this row: safe)
+      row_store(ring, 2 * oy + 4, n0);
+      row_store(ring, 2 * oy + 5, n1);
+      __syncthreads();
+    }
   }
-  // C[k][co]: row k = wave*48 + i*16 + lg*4 + e, col co = j*16 + lr
+  if (g.stats) {              // the 16 pixel lanes, then the 4 waves, in a fixed order
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        float a1 = s1[i][e], a2 = s2[i][e];
+#pragma unroll
+        for (int m = 1; m < 16; m <<= 1) { a1 += __shfl_xor(a1, m, 64); a2 += __shfl_xor(a2, m, 64); }
+        if (lr == 0) { red[wave][i * 16 + lg * 4 + e][0] = a1; red[wave][i * 16 + lg * 4 + e][1] = a2; }
+      }
+    __syncthreads();
+    if (tid < CO) {
+      const float a1 = (red[0][tid][0] + red[1][tid][0]) + (red[2][tid][0] + red[3][tid][0]);
+      const float a2 = (red[0][tid][1] + red[1][tid][1]) + (red[2][tid][1] + red[3][tid][1]);
+      acc_u64* st = g.stats + acc_idx((long)t.b * CO + tid, 0);
+      acc_add(st, a1);
+      acc_add(st + kAccSlots, a2);
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// weight gradient: D[co][k] = sum over the band's pixels of dz^T[co][px] . patch[px][k].  Per output
+// row the dz row is transposed into LDS (dz^T[co][px]: plain 16-byte fragment reads) and the patch
+// fragments are gathered from the ring (8 pixels 2 apart = stride 6 values).  4 waves x 48 k x 64
+// co accumulators over the band, then the [192][64] partial goes to the unit's fp32 slab (summed in
+// a fixed order by the shared split reducer: deterministic).
+// ---------------------------------------------------------------------------------------------
+__global__ void __launch_bounds__(NT) stem_wgrad_kernel(StemArgs g) {
+  __shared__ __attribute__((aligned(16))) cvl_bf16 ring[NRING * RL];
+  __shared__ __attribute__((aligned(16))) cvl_bf16 dzt[CO * DP];
+  const int tid = threadIdx.x;
+  const int wave = tid >> 6, lane = tid & 63, lr = lane & 15, lg = lane >> 4;
+  const Unit t = unit_of(g, blockIdx.x);
+  f32x4 acc[4][3];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 3; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  // this lane's patch columns k = wave*48 + j*16 + lr: kernel row, offset in the ring row, valid
+  int kyj[3], offj[3];
+  bool kv[3];
+#pragma unroll
+  for (int j = 0; j < 3; ++j) {
+    const int k = wave * 48 + j * 16 + lr, r = k % 24;
+    kv[j] = k < KR && r < 21;
+    kyj[j] = k / 24;
+    offj[j] = r;                                    // kx * 3 + c
+  }
+  if (t.oy0 < g.Ho) {
+    for (int i = tid; i < NRING * RL / 8; i += NT) reinterpret_cast<s16x8*>(ring)[i] = s16x8{0, 0, 0, 0, 0, 0, 0, 0};
+    __syncthreads();
+    {
+      float v[RPT];
+      for (int iy = 2 * t.oy0 - 3; iy <= 2 * t.oy0 + 3; ++iy) {
+        row_load(g, t, iy, v);
+        row_store(ring, iy, v);
+      }
+    }
+    // dz row -> registers: thread owns 8 chunks (pixel, 8 channels) of the 256 x 64 row
+    auto dz_load = [&](int oy, s16x8 (&d)[8]) {
+      const cvl_bf16* zr = g.dz + ((long)(t.b * g.Ho + oy) * g.Wo + t.x0) * CO;
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        const int idx = tid + q * NT, px = idx >> 3, c8 = (idx & 7) * 8;
+        d[q] = px < t.npx ? *reinterpret_cast<const s16x8*>(zr + (long)px * CO + c8) : s16x8{0, 0, 0, 0, 0, 0, 0, 0};
+      }
+    };
+    s16x8 dcur[8];
+    dz_load(t.oy0, dcur);
+    for (int oy = t.oy0; oy < t.oy1; ++oy) {
+      __syncthreads();                              // the previous row's fragment reads are done
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        const int idx = tid + q * NT, px = idx >> 3, c8 = (idx & 7) * 8;
+#pragma unroll
+        for (int u = 0; u < 8; ++u) dzt[(c8 + u) * DP + px] = (cvl_bf16)dcur[q][u];
+      }
+      const bool more = oy + 1 < t.oy1;
+      float n0[RPT], n1[RPT];
+      s16x8 dnext[8];
+      if (more) {
+        row_load(g, t, 2 * oy + 4, n0);
+        row_load(g, t, 2 * oy + 5, n1);
+        dz_load(oy + 1, dnext);
+      }
+      __syncthreads();
+#pragma unroll 2
+      for (int s = 0; s < SPX / 32; ++s) {
+        const int p0 = s * 32 + lg * 8;
+        s16x8 fa[4], fb[3];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) fa[i] = *reinterpret_cast<const s16x8*>(dzt + (i * 16 + lr) * DP + p0);
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {
+          const cvl_bf16* rr = ring + ((2 * oy + kyj[j]) % NRING) * RL + offj[j] + 6 * p0;
+          s16x8 v;
+#pragma unroll
+          for (int q = 0; q < 8; ++q) v[q] = kv[j] ? (short)rr[6 * q] : (short)0;
+          fb[j] = v;
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 3; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, fa[i]),
+                                                                 __builtin_bit_cast(bf16x8, fb[j]), acc[i][j], 0, 0, 0);
+      }
+      if (more) {
+        __syncthreads();
+        row_store(ring, 2 * oy + 4, n0);
+        row_store(ring, 2 * oy + 5, n1);
+#pragma unroll
+        for (int q = 0; q < 8; ++q) dcur[q] = dnext[q];
+      }
+    }
+  }
+  // D[co = i*16 + lg*4 + e][k = wave*48 + j*16 + lr] -> out[k][co], 16 bytes per accumulator
   const bool direct = gridDim.x == 1;
   float* out = direct ? g.out : g.out + (size_t)blockIdx.x * KP * CO;
 #pragma unroll
-  for (int i = 0; i < 3; ++i)
+  for (int i = 0; i < 4; ++i)
 #pragma unroll
-    for (int j = 0; j < 4; ++j)
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        float* po = out + (size_t)(wave * 48 + i * 16 + lg * 4 + e) * CO + j * 16 + lr;
-        const float v = acc[i][j][e];
-        *po = (direct && g.beta != 0.f) ? v + g.beta * *po : v;
-      }
+    for (int j = 0; j < 3; ++j) {
+      f32x4 v = acc[i][j];
+      f32x4* po = reinterpret_cast<f32x4*>(out + (size_t)(wave * 48 + j * 16 + lr) * CO + i * 16 + lg * 4);
+      if (direct && g.beta != 0.f) v += g.beta * *po;
+      *po = v;
+    }
 }
 
 inline void stem_geometry(int H, int W, int* Ho, int* Wo) {
@@ -271,10 +332,12 @@ inline void stem_geometry(int H, int W, int* Ho, int* Wo) {
   *Wo = (W - 1) / 2 + 1;
 }
 
-inline int stem_wgrad_wgs(int tiles) {
-  static const int target = cvl_env_int("CVL_STEM_WGRAD_WGS", 512);
-  int n = target < tiles ? target : tiles;
-  return n < 1 ? 1 : n;
+inline void stem_plan(StemArgs* g, int B, int H, int W, int rpw) {
+  g->B = B; g->H = H; g->W = W;
+  stem_geometry(H, W, &g->Ho, &g->Wo);
+  g->ntx = (g->Wo + SPX - 1) / SPX;
+  g->rpw = rpw;
+  g->nbands = (g->Ho + rpw - 1) / rpw;
 }
 
 }  // namespace
@@ -289,22 +352,17 @@ extern "C" int cvl_stem_conv7x7s2(const float* img, int B, int H, int W, const v
   g.bias = bias;
   g.z = reinterpret_cast<cvl_bf16*>(z);
   g.stats = reinterpret_cast<acc_u64*>(bn_stats);
-  g.B = B; g.H = H; g.W = W;
-  stem_geometry(H, W, &g.Ho, &g.Wo);
-  g.ntx = (g.Wo + SP - 1) / SP;
-  g.tiles = B * g.Ho * g.ntx;
-  hipLaunchKernelGGL(stem_fwd_kernel, dim3(g.tiles), dim3(NT), 0, (hipStream_t)stream, g);
+  stem_plan(&g, B, H, W, RPW_F);
+  hipLaunchKernelGGL(stem_fwd_kernel, dim3(B * g.ntx * g.nbands), dim3(NT), 0, (hipStream_t)stream, g);
   return cvl_launch_status();
 }
 
 extern "C" size_t cvl_stem_wgrad_workspace_size(int B, int H, int W) {
   if (B <= 0 || H <= 0 || W <= 0) return 0;
-  int Ho, Wo;
-  stem_geometry(H, W, &Ho, &Wo);
-  const int tiles = B * Ho * ((Wo + SP - 1) / SP);
-  const int tpw = (tiles + stem_wgrad_wgs(tiles) - 1) / stem_wgrad_wgs(tiles);
-  const int wgs = (tiles + tpw - 1) / tpw;
-  return wgs > 1 ? (size_t)wgs * KP * CO * sizeof(float) : 16;
+  StemArgs g{};
+  stem_plan(&g, B, H, W, RPW_W);
+  const long units = (long)B * g.ntx * g.nbands;
+  return units > 1 ? (size_t)units * KP * CO * sizeof(float) : 16;
 }
 
 extern "C" int cvl_stem_wgrad(const float* img, int B, int H, int W, const void* dz, float* dw, float beta,
@@ -316,20 +374,16 @@ extern "C" int cvl_stem_wgrad(const float* img, int B, int H, int W, const void*
   StemArgs g{};
   g.img = img;
   g.dz = reinterpret_cast<const cvl_bf16*>(dz);
-  g.B = B; g.H = H; g.W = W;
-  stem_geometry(H, W, &g.Ho, &g.Wo);
-  g.ntx = (g.Wo + SP - 1) / SP;
-  g.tiles = B * g.Ho * g.ntx;
-  g.tiles_per_wg = (g.tiles + stem_wgrad_wgs(g.tiles) - 1) / stem_wgrad_wgs(g.tiles);
-  const int wgs = (g.tiles + g.tiles_per_wg - 1) / g.tiles_per_wg;
   g.beta = beta;
-  g.out = wgs > 1 ? reinterpret_cast<float*>(workspace) : dw;
-  if (wgs == 1) {                                   // writes dW now: a queued reduction into it first
+  stem_plan(&g, B, H, W, RPW_W);
+  const int units = B * g.ntx * g.nbands;
+  g.out = units > 1 ? reinterpret_cast<float*>(workspace) : dw;
+  if (units == 1) {                                 // writes dW now: a queued reduction into it first
     const int gs = cvl_wgrad_defer_guard(dw, s);
     if (gs) return gs;
   }
-  hipLaunchKernelGGL(stem_wgrad_kernel, dim3(wgs), dim3(NT), 0, s, g);
+  hipLaunchKernelGGL(stem_wgrad_kernel, dim3(units), dim3(NT), 0, s, g);
   const int st = cvl_launch_status();
-  if (st || wgs == 1) return st;
-  return cvl_wgrad_reduce(reinterpret_cast<const float*>(workspace), dw, dw, (long)KP * CO / 4, wgs, 1, beta, s);
+  if (st || units == 1) return st;
+  return cvl_wgrad_reduce(reinterpret_cast<const float*>(workspace), dw, dw, (long)KP * CO / 4, units, 1, beta, s);
 }
