@@ -11,8 +11,13 @@
 // Partials below 2^-100 in magnitude (subnormals included) are dropped: far below the statistics'
 // resolution, and the drop itself is deterministic.
 //
-// Layout: one statistic = 8 consecutive uint64 ("slots"); a (B, C) statistics buffer is
-// [B][C][2][8] (the public header's cvl_bn_acc layout).  Zero it before the producer.
+// This exact form is the library's deterministic mode (cvl_bn_set_exact(1)).  The default mode
+// keeps one float64 per statistic ("1 slot") added with fp64 atomics: the same values up to the
+// last bits of a sum, no decode step, half the consumer reads (measured: the exact mode costs
+// about 6% of an FCOS step, mostly the decode launches).
+//
+// Layout: one statistic = `slots` consecutive uint64 (8 exact, 1 default); a (B, C) statistics
+// buffer is [B][C][2][slots] (the public header's cvl_bn_acc layout).  Zero it before the producer.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -45,9 +50,16 @@ __device__ __forceinline__ void acc_add(acc_u64* s, float p) {
   if (k >= 0) atomicAdd(s + k, (acc_u64)v);
 }
 
+// the producers' form: `slots` is the buffer's mode (kAccSlots exact, 1 float64 atomics)
+__device__ __forceinline__ void acc_add(acc_u64* s, float p, int slots) {
+  if (slots == kAccSlots) acc_add(s, p);
+  else atomicAdd(reinterpret_cast<double*>(s), (double)p);
+}
+
 // atomic add of a float64 partial, exactly: split into three fp32 pieces hi + mid + lo (72
 // significand bits >= 53, each remainder exact in float64)
-__device__ __forceinline__ void acc_add_f64(acc_u64* s, double p) {
+__device__ __forceinline__ void acc_add_f64(acc_u64* s, double p, int slots) {
+  if (slots != kAccSlots) { atomicAdd(reinterpret_cast<double*>(s), p); return; }
   const float hi = (float)p;
   const double r = p - (double)hi;
   const float mid = (float)r;
@@ -95,7 +107,8 @@ constexpr acc_u64 kAccDecoded = ~0ull;
 
 // the statistic's value: bins decoded in a fixed order (smallest first), each exact integer
 // rounded once to float64 and scaled by a power of two
-__device__ __forceinline__ double acc_value(const acc_u64* s) {
+__device__ __forceinline__ double acc_value(const acc_u64* s, int slots = kAccSlots) {
+  if (slots != kAccSlots) return __longlong_as_double((long long)s[0]);
   if (s[kAccBins] == kAccDecoded) return __longlong_as_double((long long)s[0]);
   if (s[kAccBins] != 0) return __builtin_nan("");
   double t = 0.0;
@@ -104,10 +117,11 @@ __device__ __forceinline__ double acc_value(const acc_u64* s) {
   return t;
 }
 
-// statistic s (0 or 1) of (image b, channel c) in a [B][C][2][8] buffer
-__device__ __forceinline__ long acc_idx(long bc, int s) { return (bc * 2 + s) * kAccSlots; }
+// statistic s (0 or 1) of (image b, channel c) in a [B][C][2][slots] buffer
+__device__ __forceinline__ long acc_idx(long bc, int s, int slots) { return (bc * 2 + s) * slots; }
 
-// one statistic: bins -> its float64 value in slot 0 (+ the marker); a decoded one is left alone
+// one statistic (exact mode): bins -> its float64 value in slot 0 (+ the marker); a decoded one
+// is left alone
 __device__ __forceinline__ void acc_decode_inplace(acc_u64* s) {
   if (s[kAccBins] == kAccDecoded) return;
   const double v = acc_value(s);
@@ -115,11 +129,11 @@ __device__ __forceinline__ void acc_decode_inplace(acc_u64* s) {
   s[kAccBins] = kAccDecoded;
 }
 
-// the float64 value of statistic s of (b, c) of a buffer decoded in place
-__device__ __forceinline__ double acc_dec(const acc_u64* buf, long bc, int s) {
-  return __longlong_as_double((long long)buf[acc_idx(bc, s)]);
+// the float64 value of statistic s of (b, c): a default-mode buffer, or an exact one decoded in place
+__device__ __forceinline__ double acc_dec(const acc_u64* buf, long bc, int s, int slots) {
+  return __longlong_as_double((long long)buf[acc_idx(bc, s, slots)]);
 }
-__device__ __forceinline__ void acc_store_dec(acc_u64* buf, long bc, int s, double v) {
-  buf[acc_idx(bc, s)] = (acc_u64)__double_as_longlong(v);
-  buf[acc_idx(bc, s) + kAccBins] = kAccDecoded;
+__device__ __forceinline__ void acc_store_dec(acc_u64* buf, long bc, int s, double v, int slots) {
+  buf[acc_idx(bc, s, slots)] = (acc_u64)__double_as_longlong(v);
+  if (slots == kAccSlots) buf[acc_idx(bc, s, slots) + kAccBins] = kAccDecoded;
 }

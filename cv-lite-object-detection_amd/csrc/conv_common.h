@@ -63,7 +63,8 @@ struct ConvSeg {
 struct ConvArgs {
   const cvl_bf16* src;
   void* dst;
-  acc_u64* stats;     // BN statistics accumulators [B][n_store][2][8] (bn_acc.h) or null
+  acc_u64* stats;     // BN statistics accumulators [B][n_store][2][acc_slots] (bn_acc.h) or null
+  int acc_slots;      // the BN accumulators' mode: kAccSlots (exact) or 1 (float64 atomics)
   int nseg, B;
   ConvSeg seg[kMaxSeg];
   int Cin, KH, KW, stride, pad_t, pad_l;
@@ -130,6 +131,7 @@ static inline int cvl_conv_prepare(const cvl_conv_desc* d, int bm, ConvArgs* a) 
   a->dbg = 0;
   a->bz = nullptr; a->bmr = nullptr; a->bga = nullptr; a->bbe = nullptr; a->bsum = nullptr; a->bhi = 0.f;
   a->by = nullptr;
+  a->acc_slots = cvl_bn_acc_slots();
   a->nseg = d->nseg;
   a->B = d->B;
   a->Cin = d->Cin; a->KH = d->KH; a->KW = d->KW; a->stride = d->stride;

@@ -117,9 +117,9 @@ __device__ __forceinline__ void conv_l_epilogue(const ConvArgs& a, const ConvSeg
       s2 += __shfl_xor(s2, 16, 64); s2 += __shfl_xor(s2, 32, 64);
       const int n = n0 + wn * WN + j * 16 + lr;
       if (lg == 0 && n < a.n_store) {
-        acc_u64* st = a.stats + acc_idx((long)img * a.n_store + n, 0);
-        acc_add(st, s1);
-        acc_add(st + kAccSlots, s2);
+        acc_u64* st = a.stats + acc_idx((long)img * a.n_store + n, 0, a.acc_slots);
+        acc_add(st, s1, a.acc_slots);
+        acc_add(st + a.acc_slots, s2, a.acc_slots);
       }
     }
   } else if (a.stats && !tile_stats && HWr >= WM) {
@@ -150,13 +150,13 @@ __device__ __forceinline__ void conv_l_epilogue(const ConvArgs& a, const ConvSeg
       b2 += __shfl_xor(b2, 16, 64); b2 += __shfl_xor(b2, 32, 64);
       const int n = n0 + wn * WN + j * 16 + lr;
       if (lg == 0 && n < a.n_store && r0 < rend) {
-        acc_u64* st = a.stats + acc_idx((long)imgA * a.n_store + n, 0);
-        acc_add(st, a1);
-        acc_add(st + kAccSlots, a2);
+        acc_u64* st = a.stats + acc_idx((long)imgA * a.n_store + n, 0, a.acc_slots);
+        acc_add(st, a1, a.acc_slots);
+        acc_add(st + a.acc_slots, a2, a.acc_slots);
         if (rb < rend) {
-          acc_u64* sb = a.stats + acc_idx((long)(imgA + 1) * a.n_store + n, 0);
-          acc_add(sb, b1);
-          acc_add(sb + kAccSlots, b2);
+          acc_u64* sb = a.stats + acc_idx((long)(imgA + 1) * a.n_store + n, 0, a.acc_slots);
+          acc_add(sb, b1, a.acc_slots);
+          acc_add(sb + a.acc_slots, b2, a.acc_slots);
         }
       }
     }
@@ -174,9 +174,9 @@ __device__ __forceinline__ void conv_l_epilogue(const ConvArgs& a, const ConvSeg
         float s1 = 0.f, s2 = 0.f;
 #pragma unroll
         for (int e = 0; e < 4; ++e) { const float v = acc[i][j][e]; s1 += v; s2 += v * v; }
-        acc_u64* st = a.stats + acc_idx((long)img * a.n_store + n, 0);
-        acc_add(st, s1);
-        acc_add(st + kAccSlots, s2);
+        acc_u64* st = a.stats + acc_idx((long)img * a.n_store + n, 0, a.acc_slots);
+        acc_add(st, s1, a.acc_slots);
+        acc_add(st + a.acc_slots, s2, a.acc_slots);
       }
     }
   }
@@ -232,9 +232,9 @@ __device__ __forceinline__ void conv_l_epilogue(const ConvArgs& a, const ConvSeg
     float s1 = 0.f, s2 = 0.f;
 #pragma unroll
     for (int w = 0; w < WGM; ++w) { s1 += sred[(w * BN + tid) * 2]; s2 += sred[(w * BN + tid) * 2 + 1]; }
-    acc_u64* st = a.stats + acc_idx((long)(mloc0 / HWr) * a.n_store + n0 + tid, 0);
-    acc_add(st, s1);
-    acc_add(st + kAccSlots, s2);
+    acc_u64* st = a.stats + acc_idx((long)(mloc0 / HWr) * a.n_store + n0 + tid, 0, a.acc_slots);
+    acc_add(st, s1, a.acc_slots);
+    acc_add(st + a.acc_slots, s2, a.acc_slots);
   }
   cvl_bf16* dst = reinterpret_cast<cvl_bf16*>(a.dst);
   // destination rows are the segment's rows in order (no channel interleave of images, no
@@ -303,9 +303,9 @@ __device__ __forceinline__ void conv_l_epilogue(const ConvArgs& a, const ConvSeg
         t1 += red[(w * CCH + c8) * 16 + u];
         t2 += red[(w * CCH + c8) * 16 + 8 + u];
       }
-      acc_u64* st = a.bsum + acc_idx((long)bimg * a.n_store + n0 + tid, 0);
-      acc_add(st, t1);
-      acc_add(st + kAccSlots, t2);
+      acc_u64* st = a.bsum + acc_idx((long)bimg * a.n_store + n0 + tid, 0, a.acc_slots);
+      acc_add(st, t1, a.acc_slots);
+      acc_add(st + a.acc_slots, t2, a.acc_slots);
     }
   }
 }

@@ -281,9 +281,9 @@ __global__ void __launch_bounds__(NT) conv_igemm_kernel(ConvArgs a) {
         float s1 = 0.f, s2 = 0.f;
 #pragma unroll
         for (int e = 0; e < 4; ++e) { const float v = acc[i][j][e]; s1 += v; s2 += v * v; }
-        acc_u64* st = a.stats + acc_idx((long)img * a.n_store + n, 0);
-        acc_add(st, s1);
-        acc_add(st + kAccSlots, s2);
+        acc_u64* st = a.stats + acc_idx((long)img * a.n_store + n, 0, a.acc_slots);
+        acc_add(st, s1, a.acc_slots);
+        acc_add(st + a.acc_slots, s2, a.acc_slots);
       }
     }
   } else if (a.stats) {   // one image per tile (H*W % BM == 0): reduce the tile's rows first
@@ -303,9 +303,9 @@ __global__ void __launch_bounds__(NT) conv_igemm_kernel(ConvArgs a) {
       s2 += __shfl_xor(s2, 16, 64); s2 += __shfl_xor(s2, 32, 64);
       const int n = n0 + wn * WN + j * 16 + lr;
       if (lg == 0 && n < a.n_store) {
-        acc_u64* st = a.stats + acc_idx((long)img * a.n_store + n, 0);
-        acc_add(st, s1);
-        acc_add(st + kAccSlots, s2);
+        acc_u64* st = a.stats + acc_idx((long)img * a.n_store + n, 0, a.acc_slots);
+        acc_add(st, s1, a.acc_slots);
+        acc_add(st + a.acc_slots, s2, a.acc_slots);
       }
     }
   }
@@ -436,9 +436,9 @@ __global__ void __launch_bounds__(NT) conv_splitk_finish(ConvArgs a, int rows_pe
       if (c < a.n_store) {
         double t1 = 0.0, t2 = 0.0;
         for (int k = 0; k < FIN_RL; ++k) { t1 += red[k][cg2][u]; t2 += red[k][cg2][8 + u]; }
-        acc_u64* st = a.stats + acc_idx((long)img * a.n_store + c, 0);
-        acc_add_f64(st, t1);
-        acc_add_f64(st + kAccSlots, t2);
+        acc_u64* st = a.stats + acc_idx((long)img * a.n_store + c, 0, a.acc_slots);
+        acc_add_f64(st, t1, a.acc_slots);
+        acc_add_f64(st + a.acc_slots, t2, a.acc_slots);
       }
     }
   }

@@ -265,9 +265,9 @@ __global__ void __launch_bounds__(NT) conv_igemm_p_kernel(ConvArgs a, int ntiles
       float t1 = 0.f, t2 = 0.f;
 #pragma unroll
       for (int w = 0; w < C::WGM; ++w) { t1 += red[(w * BN + tid) * 2]; t2 += red[(w * BN + tid) * 2 + 1]; }
-      acc_u64* st = a.stats + acc_idx((long)img * a.n_store + n0 + tid, 0);
-      acc_add(st, t1);
-      acc_add(st + kAccSlots, t2);
+      acc_u64* st = a.stats + acc_idx((long)img * a.n_store + n0 + tid, 0, a.acc_slots);
+      acc_add(st, t1, a.acc_slots);
+      acc_add(st + a.acc_slots, t2, a.acc_slots);
     }
   };
 
@@ -290,9 +290,9 @@ __global__ void __launch_bounds__(NT) conv_igemm_p_kernel(ConvArgs a, int ntiles
       float t1 = 0.f, t2 = 0.f;
 #pragma unroll
       for (int w = 0; w < C::WGM; ++w) { t1 += red[(w * BN + tid) * 2]; t2 += red[(w * BN + tid) * 2 + 1]; }
-      acc_u64* st = a.bsum + acc_idx((long)img * a.n_store + n0 + tid, 0);
-      acc_add(st, t1);
-      acc_add(st + kAccSlots, t2);
+      acc_u64* st = a.bsum + acc_idx((long)img * a.n_store + n0 + tid, 0, a.acc_slots);
+      acc_add(st, t1, a.acc_slots);
+      acc_add(st + a.acc_slots, t2, a.acc_slots);
     }
   };
 

@@ -253,7 +253,7 @@ __device__ __forceinline__ void bn_moments(double s1, double s2, int HW, float e
 }
 
 // running-stat EMA of one channel over the images in order (TF fused BN: unbiased variance)
-__device__ __forceinline__ void bn_running(const acc_u64* stats, int B, int C, int c, int HW, float eps,
+__device__ __forceinline__ void bn_running(const acc_u64* stats, int slots, int B, int C, int c, int HW, float eps,
                                            float momentum, float* run_mean, float* run_var) {
   float rm = run_mean[c], rv = run_var[c];
   for (int b0 = 0; b0 < B; b0 += 8) {       // 8 images' loads in flight, then the in-order EMA
@@ -261,8 +261,8 @@ __device__ __forceinline__ void bn_running(const acc_u64* stats, int B, int C, i
 #pragma unroll
     for (int u = 0; u < 8; ++u) {
       const long bc = (long)min(b0 + u, B - 1) * C + c;
-      s1[u] = acc_dec(stats, bc, 0);
-      s2[u] = acc_dec(stats, bc, 1);
+      s1[u] = acc_dec(stats, bc, 0, slots);
+      s2[u] = acc_dec(stats, bc, 1, slots);
     }
 #pragma unroll
     for (int u = 0; u < 8; ++u) {
@@ -281,18 +281,18 @@ __device__ __forceinline__ void bn_running(const acc_u64* stats, int B, int C, i
 
 // stats[b][c] = (sum, sumsq) accumulators -> mr[b][c] = (mean, rstd); running stats EMA, images in order.
 __global__ void bn_finalize_kernel(const acc_u64* stats, float* mr, float* run_mean, float* run_var,
-                                   int B, int C, int HW, float eps, float momentum) {
+                                   int B, int C, int HW, float eps, float momentum, int slots) {
   const int c = blockIdx.x * NT + threadIdx.x;
   if (c >= C) return;
   for (int b = 0; b < B; ++b) {
     float mean, rstd;
     double var;
     const long bc = (long)b * C + c;
-    bn_moments(acc_dec(stats, bc, 0), acc_dec(stats, bc, 1), HW, eps, &mean, &rstd, &var);
+    bn_moments(acc_dec(stats, bc, 0, slots), acc_dec(stats, bc, 1, slots), HW, eps, &mean, &rstd, &var);
     mr[((long)b * C + c) * 2] = mean;
     mr[((long)b * C + c) * 2 + 1] = rstd;
   }
-  if (run_mean) bn_running(stats, B, C, c, HW, eps, momentum, run_mean, run_var);
+  if (run_mean) bn_running(stats, slots, B, C, c, HW, eps, momentum, run_mean, run_var);
 }
 
 // y = act(gamma * (z - mean) * rstd + beta [+ residual]).  Grid (row chunk, image); a thread owns
@@ -307,6 +307,7 @@ struct BnFin {
   float* run_mean;
   float* run_var;
   float eps, momentum;
+  int slots;
 };
 
 constexpr int BNA_UNR = 4;
@@ -333,7 +334,7 @@ __global__ void __launch_bounds__(NT) bn_apply_kernel(const cvl_bf16* __restrict
       const long bc = (long)b * C + c;
       float mm, rr;
       double var;
-      bn_moments(acc_dec(fin.stats, bc, 0), acc_dec(fin.stats, bc, 1), HW, fin.eps, &mm, &rr, &var);
+      bn_moments(acc_dec(fin.stats, bc, 0, fin.slots), acc_dec(fin.stats, bc, 1, fin.slots), HW, fin.eps, &mm, &rr, &var);
       smr[c] = float2{mm, rr};
       if (blockIdx.x == 0) { fin.mr_out[bc * 2] = mm; fin.mr_out[bc * 2 + 1] = rr; }
     }
@@ -341,7 +342,7 @@ __global__ void __launch_bounds__(NT) bn_apply_kernel(const cvl_bf16* __restrict
     // over the images -- in one block it was the critical path of the small launches)
     if (b == 0 && fin.run_mean)
       for (int c = blockIdx.x * NT + threadIdx.x; c < C; c += gridDim.x * NT)
-        bn_running(fin.stats, gridDim.y, C, c, HW, fin.eps, fin.momentum, fin.run_mean, fin.run_var);
+        bn_running(fin.stats, fin.slots, gridDim.y, C, c, HW, fin.eps, fin.momentum, fin.run_mean, fin.run_var);
     __syncthreads();
   }
   if (rsub >= rpp) return;
@@ -426,6 +427,7 @@ struct BnPG {
   float* conv_dbias;
   float beta_acc;
   const acc_u64* psums;   // per-image sums for the parameter gradients (nullptr: `sums`)
+  int slots;              // `sums` / `psums` stride: the accumulator mode (fused producers) or 1 (internal)
 };
 
 // MASK selects the ReLU-mask source at compile time (1: y, 2: bn_affine(z) recomputed, 3: no mask --
@@ -458,8 +460,8 @@ __global__ void __launch_bounds__(NT) bn_bwd_kernel(const cvl_bf16* __restrict__
       double a1 = 0.0, a2 = 0.0;
 #pragma unroll 8
       for (int bb = 0; bb < (int)gridDim.y; ++bb) {
-        a1 += acc_dec(ps, (long)bb * C + c, 0);
-        a2 += acc_dec(ps, (long)bb * C + c, 1);
+        a1 += acc_dec(ps, (long)bb * C + c, 0, pg.slots);
+        a2 += acc_dec(ps, (long)bb * C + c, 1, pg.slots);
       }
       pg.dbeta[c] = (float)a1 + (pg.beta_acc != 0.f ? pg.beta_acc * pg.dbeta[c] : 0.f);
       pg.dgamma[c] = (float)a2 + (pg.beta_acc != 0.f ? pg.beta_acc * pg.dgamma[c] : 0.f);
@@ -486,8 +488,8 @@ __global__ void __launch_bounds__(NT) bn_bwd_kernel(const cvl_bf16* __restrict__
       be[u] = zmask ? bnb[c0 + u] : 0.f;
       s1[u] = 0.f; s2[u] = 0.f;
       if (PASS == 1) {
-        k1[u] = (float)acc_dec(sums, bc, 0) * inv;     // mean(g)
-        k2[u] = (float)acc_dec(sums, bc, 1) * inv;     // mean(g * xhat)
+        k1[u] = (float)acc_dec(sums, bc, 0, pg.slots) * inv;     // mean(g)
+        k2[u] = (float)acc_dec(sums, bc, 1, pg.slots) * inv;     // mean(g * xhat)
         gm[u] = gamma[c0 + u] * rs[u];
       }
     }
@@ -576,10 +578,9 @@ __global__ void __launch_bounds__(NT) bn_bwd_kernel(const cvl_bf16* __restrict__
 
 // out[y][c][0..1] = sum_r part[y][r][c][0..1]: a block owns 32 channels (256 contiguous bytes per
 // row) and 8 row groups; the row groups are combined in a fixed order (deterministic, float64) and
-// the total is stored exactly as an accumulator (bn_acc.h; the format the fused producers write)
-template <bool BINS>
+// the total is stored as a decoded accumulator of `slots` (bn_acc.h) -- the single writer of it
 __global__ void __launch_bounds__(NT) bn_colsum_kernel(const float* __restrict__ part, int R, int C,
-                                                       acc_u64* __restrict__ out) {
+                                                       acc_u64* __restrict__ out, int slots) {
   const int y = blockIdx.y;
   const int cl = threadIdx.x & 31, rg = threadIdx.x >> 5;
   const int c = blockIdx.x * 32 + cl;
@@ -606,14 +607,8 @@ __global__ void __launch_bounds__(NT) bn_colsum_kernel(const float* __restrict__
   if (rg == 0 && c < C) {
     double t1 = 0.0, t2 = 0.0;
     for (int k = 0; k < 8; ++k) { t1 += red[k][cl][0]; t2 += red[k][cl][1]; }
-    if (BINS) {           // a public statistics buffer (cvl_bn_stats): accumulator bins
-      AccLocal l;
-      l.zero(); l.add_f64(t1); l.store(out + acc_idx((long)y * C + c, 0));
-      l.zero(); l.add_f64(t2); l.store(out + acc_idx((long)y * C + c, 1));
-    } else {              // an internal one: already in the decoded form its consumer reads
-      acc_store_dec(out, (long)y * C + c, 0, t1);
-      acc_store_dec(out, (long)y * C + c, 1, t2);
-    }
+    acc_store_dec(out, (long)y * C + c, 0, t1, slots);
+    acc_store_dec(out, (long)y * C + c, 1, t2, slots);
   }
 }
 
@@ -1183,7 +1178,7 @@ __global__ void gather_rows_kernel(const int4* src, long row16, const int32_t* i
 // group order, as the reference's sequential sub-batch forwards do.
 // ---------------------------------------------------------------------------------------------
 __global__ void bn_finalize_grouped_kernel(const acc_u64* stats, float* mr, float* run_mean, float* run_var,
-                                           int B, int C, int HW, int group, float eps, float momentum) {
+                                           int B, int C, int HW, int group, float eps, float momentum, int slots) {
   const int c = blockIdx.x * NT + threadIdx.x;
   if (c >= C) return;
   float rm = run_mean ? run_mean[c] : 0.f, rv = run_var ? run_var[c] : 0.f;
@@ -1191,8 +1186,8 @@ __global__ void bn_finalize_grouped_kernel(const acc_u64* stats, float* mr, floa
     const int g1 = min(g0 + group, B);
     double s1 = 0.0, s2 = 0.0;      // the group's images in order (decoded statistics)
     for (int b = g0; b < g1; ++b) {
-      s1 += acc_value(stats + acc_idx((long)b * C + c, 0));
-      s2 += acc_value(stats + acc_idx((long)b * C + c, 1));
+      s1 += acc_value(stats + acc_idx((long)b * C + c, 0, slots), slots);
+      s2 += acc_value(stats + acc_idx((long)b * C + c, 1, slots), slots);
     }
     const double n = (double)(g1 - g0) * HW;
     const double mean = s1 / n;
@@ -1207,8 +1202,9 @@ __global__ void bn_finalize_grouped_kernel(const acc_u64* stats, float* mr, floa
   if (run_mean) { run_mean[c] = rm; run_var[c] = rv; }
 }
 
-__global__ void bn_acc_decode_kernel(const acc_u64* acc, double* out, long n) {
-  for (long i = blockIdx.x * (long)NT + threadIdx.x; i < n; i += (long)gridDim.x * NT) out[i] = acc_value(acc + i * kAccSlots);
+__global__ void bn_acc_decode_kernel(const acc_u64* acc, double* out, long n, int slots) {
+  for (long i = blockIdx.x * (long)NT + threadIdx.x; i < n; i += (long)gridDim.x * NT)
+    out[i] = acc_value(acc + i * slots, slots);
 }
 
 // every statistic of a buffer decoded in place (one thread each), before its consumers read it
@@ -1217,21 +1213,25 @@ __global__ void bn_acc_decode_inplace_kernel(acc_u64* acc, long n) {
   if (i < n) acc_decode_inplace(acc + i * kAccSlots);
 }
 
+// the accumulator mode (cvl_bn_set_exact): kAccSlots exact bins, 1 float64 atomics (default)
+int g_acc_slots = 1;
+
 inline int acc_decode_launch(acc_u64* acc, long nstat, hipStream_t s) {
+  if (g_acc_slots != kAccSlots) return CVL_OK;        // float64 mode: nothing to decode
   hipLaunchKernelGGL(bn_acc_decode_inplace_kernel, dim3((unsigned)((nstat + NT - 1) / NT)), dim3(NT), 0, s, acc, nstat);
   return cvl_launch_status();
 }
 
 // gs[b][c] = sum over b's group of s[b'][c] (decoded statistics, fixed order: deterministic)
-__global__ void bn_group_sum_kernel(const acc_u64* s, acc_u64* gs, int B, int C, int group) {
+__global__ void bn_group_sum_kernel(const acc_u64* s, acc_u64* gs, int B, int C, int group) {   // internal: 1 slot
   const long i = blockIdx.x * (long)NT + threadIdx.x;
   if (i >= (long)B * C) return;
   const int b = (int)(i / C), c = (int)(i - (long)b * C);
   const int g0 = (b / group) * group, g1 = min(g0 + group, B);
   double a1 = 0.0, a2 = 0.0;
-  for (int k = g0; k < g1; ++k) { a1 += acc_dec(s, (long)k * C + c, 0); a2 += acc_dec(s, (long)k * C + c, 1); }
-  acc_store_dec(gs, i, 0, a1);
-  acc_store_dec(gs, i, 1, a2);
+  for (int k = g0; k < g1; ++k) { a1 += acc_dec(s, (long)k * C + c, 0, 1); a2 += acc_dec(s, (long)k * C + c, 1, 1); }
+  acc_store_dec(gs, i, 0, a1, 1);
+  acc_store_dec(gs, i, 1, a2, 1);
 }
 
 }  // namespace
@@ -1291,10 +1291,18 @@ extern "C" int cvl_im2col(const float* x, int B, int H, int W, int C, int KH, in
   return cvl_launch_status();
 }
 
+extern "C" int cvl_bn_acc_slots(void) { return g_acc_slots; }
+
+extern "C" int cvl_bn_set_exact(int on) {
+  g_acc_slots = on ? kAccSlots : 1;
+  return CVL_OK;
+}
+
 extern "C" int cvl_bn_acc_decode(const uint64_t* acc, double* out, int64_t n, cvl_stream_t stream) {
   CVL_CHECK_ARG(acc && out && n >= 0);
   if (n == 0) return CVL_OK;
-  hipLaunchKernelGGL(bn_acc_decode_kernel, dim3(grid_for(n)), dim3(NT), 0, S_, (const acc_u64*)acc, out, (long)n);
+  hipLaunchKernelGGL(bn_acc_decode_kernel, dim3(grid_for(n)), dim3(NT), 0, S_, (const acc_u64*)acc, out, (long)n,
+                     g_acc_slots);
   return cvl_launch_status();
 }
 
@@ -1304,7 +1312,7 @@ extern "C" int cvl_bn_finalize(uint64_t* stats, float* mean_rstd, float* run_mea
   const int dst = acc_decode_launch((acc_u64*)stats, 2L * B * C, S_);
   if (dst) return dst;
   hipLaunchKernelGGL(bn_finalize_kernel, dim3((C + NT - 1) / NT), dim3(NT), 0, S_, (const acc_u64*)stats, mean_rstd,
-                     run_mean, run_var, B, C, HW, eps, momentum);
+                     run_mean, run_var, B, C, HW, eps, momentum, g_acc_slots);
   return cvl_launch_status();
 }
 
@@ -1315,7 +1323,7 @@ extern "C" int cvl_bn_apply(const void* z, const float* mean_rstd, const float* 
   const int rpb = bn_rows_per_blk(B, HW, C);
   hipLaunchKernelGGL(bn_apply_kernel<false>, dim3((HW + rpb - 1) / rpb, B), dim3(NT), 0, S_, (const cvl_bf16*)z,
                      mean_rstd, gamma, beta, (const cvl_bf16*)residual, (cvl_bf16*)y, C, HW, relu, rpb,
-                     BnFin{nullptr, nullptr, nullptr, nullptr, 0.f, 0.f});
+                     BnFin{nullptr, nullptr, nullptr, nullptr, 0.f, 0.f, 1});
   return cvl_launch_status();
 }
 
@@ -1331,7 +1339,7 @@ extern "C" int cvl_bn_finalize_apply(uint64_t* stats, float* mean_rstd, float* r
   const int rpb = bn_rows_per_blk(B, HW, C);
   hipLaunchKernelGGL(bn_apply_kernel<true>, dim3((HW + rpb - 1) / rpb, B), dim3(NT), 0, S_, (const cvl_bf16*)z,
                      (const float*)nullptr, gamma, beta, (const cvl_bf16*)residual, (cvl_bf16*)y, C, HW, relu, rpb,
-                     BnFin{(const acc_u64*)stats, mean_rstd, run_mean, run_var, eps, momentum});
+                     BnFin{(const acc_u64*)stats, mean_rstd, run_mean, run_var, eps, momentum, g_acc_slots});
   return cvl_launch_status();
 }
 
@@ -1339,7 +1347,7 @@ extern "C" size_t cvl_bn_backward_workspace_size(int B, int HW, int C) {
   if (B <= 0 || HW <= 0 || C <= 0) return 0;
   const int rpb = bn_bwd_rows_per_blk(B, HW, C);
   const int nchunk = (HW + rpb - 1) / rpb;
-  return sizeof(acc_u64) * 2 * kAccSlots * (size_t)B * C + sizeof(double) * 2 * (size_t)C +
+  return sizeof(acc_u64) * 2 * (size_t)B * C + sizeof(double) * 2 * (size_t)C +
          sizeof(float) * 2 * 2 * (size_t)B * nchunk * C;
 }
 
@@ -1352,9 +1360,9 @@ static int bn_backward_impl(const void* dy, const void* y_relu, const float* bn_
   CVL_CHECK_ARG(workspace_bytes >= cvl_bn_backward_workspace_size(B, HW, C));
   const int rpb = bn_bwd_rows_per_blk(B, HW, C);
   const int nchunk = (HW + rpb - 1) / rpb;
-  // workspace: sums [B][C][2][8] accumulators | (unused [C][2] f64) | pass-0 partials [B][nchunk][C][2] f32
+  // workspace: sums [B][C][2] f64 | (unused [C][2] f64) | pass-0 partials [B][nchunk][C][2] f32
   acc_u64* sums = reinterpret_cast<acc_u64*>(workspace);
-  double* dbsum = reinterpret_cast<double*>(sums + 2 * kAccSlots * (size_t)B * C);
+  double* dbsum = reinterpret_cast<double*>(sums + 2 * (size_t)B * C);
   float* part0 = reinterpret_cast<float*>(dbsum + 2 * (size_t)C);
   dim3 g1(nchunk, B);
   const bool ym = y_relu != nullptr, zm = !ym && bn_beta != nullptr;
@@ -1363,13 +1371,13 @@ static int bn_backward_impl(const void* dy, const void* y_relu, const float* bn_
   hipLaunchKernelGGL(k0, g1, dim3(NT), 0, S_, (const cvl_bf16*)dy, (const cvl_bf16*)y_relu,
                      (const cvl_bf16*)z, mean_rstd, gamma, (const acc_u64*)nullptr, (cvl_bf16*)nullptr,
                      (cvl_bf16*)nullptr, part0, C, HW, rpb, 1, 0.f, BnPG{}, bn_beta, act_hi);
-  hipLaunchKernelGGL(bn_colsum_kernel<false>, dim3((C + 31) / 32, B), dim3(NT), 0, S_, (const float*)part0, nchunk, C,
-                     sums);
+  hipLaunchKernelGGL(bn_colsum_kernel, dim3((C + 31) / 32, B), dim3(NT), 0, S_, (const float*)part0, nchunk, C,
+                     sums, 1);
   // pass 1 is elementwise (no partials): the apply kernels' finer chunking (~2048 workgroups)
   const int rpb1 = bn_rows_per_blk(B, HW, C);
   hipLaunchKernelGGL(k1, dim3((HW + rpb1 - 1) / rpb1, B), dim3(NT), 0, S_, (const cvl_bf16*)dy, (const cvl_bf16*)y_relu,
                      (const cvl_bf16*)z, mean_rstd, gamma, (const acc_u64*)sums, (cvl_bf16*)dz, (cvl_bf16*)g_out,
-                     (float*)nullptr, C, HW, rpb1, 1, 0.f, BnPG{dgamma, dbeta, conv_dbias, beta_acc}, bn_beta,
+                     (float*)nullptr, C, HW, rpb1, 1, 0.f, BnPG{dgamma, dbeta, conv_dbias, beta_acc, nullptr, 1}, bn_beta,
                      act_hi);
   return cvl_launch_status();
 }
@@ -1415,7 +1423,7 @@ extern "C" int cvl_bn_backward_relu_sums(const void* dy, const void* z, const fl
   const int nchunk = (HW + rpb - 1) / rpb;
   hipLaunchKernelGGL((bn_bwd_kernel<1, 2>), dim3(nchunk, B), dim3(NT), 0, S_, (const cvl_bf16*)dy, (const cvl_bf16*)nullptr,
                      (const cvl_bf16*)z, mean_rstd, gamma, (const acc_u64*)sums, (cvl_bf16*)dz, (cvl_bf16*)nullptr, (float*)nullptr,
-                     C, HW, rpb, 1, 0.f, BnPG{dgamma, dbeta, conv_dbias, beta_acc}, beta, act_hi);
+                     C, HW, rpb, 1, 0.f, BnPG{dgamma, dbeta, conv_dbias, beta_acc, nullptr, g_acc_slots}, beta, act_hi);
   return cvl_launch_status();
 }
 
@@ -1433,7 +1441,7 @@ extern "C" int cvl_bn_backward_res_sums(const void* dy, const void* y, const voi
   const int nchunk = (HW + rpb - 1) / rpb;
   hipLaunchKernelGGL((bn_bwd_kernel<1, 1>), dim3(nchunk, B), dim3(NT), 0, S_, (const cvl_bf16*)dy, (const cvl_bf16*)y,
                      (const cvl_bf16*)z, mean_rstd, gamma, (const acc_u64*)sums, (cvl_bf16*)dz, (cvl_bf16*)g_out, (float*)nullptr,
-                     C, HW, rpb, 1, 0.f, BnPG{dgamma, dbeta, conv_dbias, beta_acc}, (const float*)nullptr, INFINITY);
+                     C, HW, rpb, 1, 0.f, BnPG{dgamma, dbeta, conv_dbias, beta_acc, nullptr, g_acc_slots}, (const float*)nullptr, INFINITY);
   return cvl_launch_status();
 }
 
@@ -1619,8 +1627,8 @@ extern "C" int cvl_bn_stats(const void* x, int B, int HW, int C, uint64_t* stats
                      (const cvl_bf16*)nullptr, (const cvl_bf16*)nullptr, (const float*)nullptr, (const float*)nullptr,
                      (const acc_u64*)nullptr, (cvl_bf16*)nullptr, (cvl_bf16*)nullptr, part, C, HW, rpb, 1, 0.f, BnPG{},
                      (const float*)nullptr, INFINITY);
-  hipLaunchKernelGGL(bn_colsum_kernel<true>, dim3((C + 31) / 32, B), dim3(NT), 0, S_, (const float*)part, nchunk, C,
-                     (acc_u64*)stats);
+  hipLaunchKernelGGL(bn_colsum_kernel, dim3((C + 31) / 32, B), dim3(NT), 0, S_, (const float*)part, nchunk, C,
+                     (acc_u64*)stats, g_acc_slots);
   return cvl_launch_status();
 }
 
@@ -1629,13 +1637,13 @@ extern "C" int cvl_bn_finalize_grouped(const uint64_t* stats, float* mean_rstd, 
                                        cvl_stream_t stream) {
   CVL_CHECK_ARG(stats && mean_rstd && B > 0 && C > 0 && HW > 0 && group > 0);
   hipLaunchKernelGGL(bn_finalize_grouped_kernel, dim3((C + NT - 1) / NT), dim3(NT), 0, S_, (const acc_u64*)stats, mean_rstd,
-                     run_mean, run_var, B, C, HW, group, eps, momentum);
+                     run_mean, run_var, B, C, HW, group, eps, momentum, g_acc_slots);
   return cvl_launch_status();
 }
 
 extern "C" size_t cvl_bn_backward_grouped_workspace_size(int B, int HW, int C) {
   if (B <= 0 || HW <= 0 || C <= 0) return 0;
-  return cvl_bn_backward_workspace_size(B, HW, C) + sizeof(acc_u64) * 2 * kAccSlots * (size_t)B * C;
+  return cvl_bn_backward_workspace_size(B, HW, C) + sizeof(acc_u64) * 2 * (size_t)B * C;
 }
 
 extern "C" int cvl_bn_backward_grouped(const void* dy, const void* y_relu, const void* z, const float* mean_rstd,
@@ -1647,9 +1655,9 @@ extern "C" int cvl_bn_backward_grouped(const void* dy, const void* y_relu, const
   CVL_CHECK_ARG(workspace_bytes >= cvl_bn_backward_grouped_workspace_size(B, HW, C));
   const int rpb = bn_bwd_rows_per_blk(B, HW, C);
   const int nchunk = (HW + rpb - 1) / rpb;
-  // workspace: sums [B][C][2][8] | [C][2] f64 | partials [B][nchunk][C][2] f32 | group sums [B][C][2][8]
+  // workspace: sums [B][C][2] f64 | [C][2] f64 | partials [B][nchunk][C][2] f32 | group sums [B][C][2] f64
   acc_u64* sums = reinterpret_cast<acc_u64*>(workspace);
-  double* dbsum = reinterpret_cast<double*>(sums + 2 * kAccSlots * (size_t)B * C);
+  double* dbsum = reinterpret_cast<double*>(sums + 2 * (size_t)B * C);
   float* part0 = reinterpret_cast<float*>(dbsum + 2 * (size_t)C);
   acc_u64* gsums = reinterpret_cast<acc_u64*>(reinterpret_cast<char*>(workspace) +
                                               cvl_bn_backward_workspace_size(B, HW, C));
@@ -1657,8 +1665,8 @@ extern "C" int cvl_bn_backward_grouped(const void* dy, const void* y_relu, const
   hipLaunchKernelGGL(bn_bwd_kernel<0>, g1, dim3(NT), 0, S_, (const cvl_bf16*)dy, (const cvl_bf16*)y_relu,
                      (const cvl_bf16*)z, mean_rstd, gamma, (const acc_u64*)nullptr, (cvl_bf16*)nullptr,
                      (cvl_bf16*)nullptr, part0, C, HW, rpb, group, 0.f, BnPG{}, (const float*)nullptr, INFINITY);
-  hipLaunchKernelGGL(bn_colsum_kernel<false>, dim3((C + 31) / 32, B), dim3(NT), 0, S_, (const float*)part0, nchunk, C,
-                     sums);
+  hipLaunchKernelGGL(bn_colsum_kernel, dim3((C + 31) / 32, B), dim3(NT), 0, S_, (const float*)part0, nchunk, C,
+                     sums, 1);
   const acc_u64* use = sums;
   if (group > 1) {
     hipLaunchKernelGGL(bn_group_sum_kernel, dim3((int)(((long)B * C + NT - 1) / NT)), dim3(NT), 0, S_,
@@ -1667,7 +1675,7 @@ extern "C" int cvl_bn_backward_grouped(const void* dy, const void* y_relu, const
   }
   hipLaunchKernelGGL(bn_bwd_kernel<1>, g1, dim3(NT), 0, S_, (const cvl_bf16*)dy, (const cvl_bf16*)y_relu,
                      (const cvl_bf16*)z, mean_rstd, gamma, use, (cvl_bf16*)dz, (cvl_bf16*)nullptr,
-                     (float*)nullptr, C, HW, rpb, group, dz_beta, BnPG{dgamma, dbeta, nullptr, 0.f, sums},
+                     (float*)nullptr, C, HW, rpb, group, dz_beta, BnPG{dgamma, dbeta, nullptr, 0.f, sums, 1},
                      (const float*)nullptr, INFINITY);
   return cvl_launch_status();
 }

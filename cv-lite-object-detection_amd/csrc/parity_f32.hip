@@ -141,10 +141,16 @@ __global__ void __launch_bounds__(NT) conv_stats_f32_kernel(ConvArgs a) {
   if (rg == 0 && c < a.n_store) {
     double t1 = 0.0, t2 = 0.0;
     for (int k = 0; k < 4; ++k) { t1 += red[k][cl][0]; t2 += red[k][cl][1]; }
-    acc_u64* st = a.stats + acc_idx((long)img * a.n_store + c, 0);
-    AccLocal l1, l2;                    // one writer per (image, channel): add onto what is there
-    l1.zero(); l1.add(st); l1.add_f64(t1); l1.store(st);
-    l2.zero(); l2.add(st + kAccSlots); l2.add_f64(t2); l2.store(st + kAccSlots);
+    acc_u64* st = a.stats + acc_idx((long)img * a.n_store + c, 0, a.acc_slots);
+    if (a.acc_slots == kAccSlots) {
+      AccLocal l1, l2;                  // one writer per (image, channel): add onto what is there
+      l1.zero(); l1.add(st); l1.add_f64(t1); l1.store(st);
+      l2.zero(); l2.add(st + kAccSlots); l2.add_f64(t2); l2.store(st + kAccSlots);
+    } else {
+      double* dv = reinterpret_cast<double*>(st);
+      dv[0] += t1;
+      dv[1] += t2;
+    }
   }
 }
 

@@ -44,7 +44,8 @@ struct StemArgs {
   const float* bias;      // [64] or null
   const cvl_bf16* dz;     // [B][Ho][Wo][64] bf16 (weight gradient)
   cvl_bf16* z;            // [B][Ho][Wo][64] bf16 (forward)
-  acc_u64* stats;         // [B][64][2][8] or null
+  acc_u64* stats;         // [B][64][2][slots] or null
+  int acc_slots;
   float* out;             // weight gradient: slab [units][192][64] or dw
   int B, H, W, Ho, Wo, ntx, nbands, rpw;
   float beta;
@@ -210,9 +211,9 @@ __global__ void __launch_bounds__(NT, 2) stem_fwd_kernel(StemArgs g) {
     if (tid < CO) {
       const float a1 = (red[0][tid][0] + red[1][tid][0]) + (red[2][tid][0] + red[3][tid][0]);
       const float a2 = (red[0][tid][1] + red[1][tid][1]) + (red[2][tid][1] + red[3][tid][1]);
-      acc_u64* st = g.stats + acc_idx((long)t.b * CO + tid, 0);
-      acc_add(st, a1);
-      acc_add(st + kAccSlots, a2);
+      acc_u64* st = g.stats + acc_idx((long)t.b * CO + tid, 0, g.acc_slots);
+      acc_add(st, a1, g.acc_slots);
+      acc_add(st + g.acc_slots, a2, g.acc_slots);
     }
   }
 }
@@ -352,6 +353,7 @@ extern "C" int cvl_stem_conv7x7s2(const float* img, int B, int H, int W, const v
   g.bias = bias;
   g.z = reinterpret_cast<cvl_bf16*>(z);
   g.stats = reinterpret_cast<acc_u64*>(bn_stats);
+  g.acc_slots = cvl_bn_acc_slots();
   stem_plan(&g, B, H, W, RPW_F);
   hipLaunchKernelGGL(stem_fwd_kernel, dim3(B * g.ntx * g.nbands), dim3(NT), 0, (hipStream_t)stream, g);
   return cvl_launch_status();

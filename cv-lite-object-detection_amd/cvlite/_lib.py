@@ -51,6 +51,8 @@ SIGNATURES = {
                            c_int, c_int, P, P]),
     "cvl_bn_finalize": (c_int, [P, P, P, P, c_int, c_int, c_int, c_float, c_float, P]),
     "cvl_bn_acc_decode": (c_int, [P, P, ctypes.c_int64, P]),
+    "cvl_bn_set_exact": (c_int, [c_int]),
+    "cvl_bn_acc_slots": (c_int, []),
     "cvl_debug_wgx_stamps": (c_int, [P, c_int]),
     "cvl_stem_conv7x7s2": (c_int, [P, c_int, c_int, c_int, P, P, P, P, P]),
     "cvl_stem_wgrad_workspace_size": (c_size_t, [c_int, c_int, c_int]),
@@ -180,6 +182,8 @@ def load():
             fn.restype = res
             fn.argtypes = args
         _lib = lib
+        if os.environ.get("CVL_BN_EXACT", "0") == "1":      # the exact BN accumulator mode (bn_acc.h)
+            lib.cvl_bn_set_exact(1)
     return _lib
 
 

@@ -250,17 +250,18 @@ FUSE_BNSUM_RES = FUSE_BNSUM and os.environ.get("CVL_NO_BNSUM_RES", "0") != "1"
 
 class StatsArena(object):
     """One zeroed buffer holding the (sum, sumsq) BN statistics of every conv of a forward pass as
-    exact accumulators (nn.bn_acc: [B][C][2][8] uint64, order-independent), one memset per step
-    instead of one per BN.  n_stats = statistics (2 per image and channel) it can hand out."""
+    BN accumulators (nn.bn_acc: [B][C][2][S] in the library's mode), one memset per step instead of
+    one per BN.  n_stats = statistics (2 per image and channel) it can hand out."""
 
     def __init__(self, n_stats, device):
-        self.buf = torch.zeros(n_stats * nn.ACC_SLOTS, dtype=torch.int64, device=device)
+        self.slots = nn.acc_slots()
+        self.buf = torch.zeros(n_stats * self.slots, dtype=torch.int64, device=device)
         self.off = 0
 
     def take(self, B, c):
-        n = B * c * 2 * nn.ACC_SLOTS
+        n = B * c * 2 * self.slots
         assert self.off + n <= self.buf.numel(), "stats arena too small"
-        v = self.buf[self.off:self.off + n].view(B, c, 2, nn.ACC_SLOTS)
+        v = self.buf[self.off:self.off + n].view(B, c, 2, self.slots)
         self.off += n
         return v
 

@@ -217,17 +217,28 @@ def im2col(x, KH, KW, stride, pad_t, pad_l, Ho, Wo, Kp, out):
     _lib.call("cvl_im2col", ptr(x), B, H, W, C, KH, KW, stride, pad_t, pad_l, Ho, Wo, Kp, ptr(out), stream())
 
 
-# BN statistics are exact, order-independent accumulators (include/cvlite.h "BN accumulators";
-# csrc/bn_acc.h): per statistic ACC_SLOTS uint64 (7 exponent bins + a non-finite count), a (B, C)
-# buffer is int64 [B][C][2][ACC_SLOTS]
+# BN statistics accumulators (include/cvlite.h "BN accumulators"; csrc/bn_acc.h): a (B, C) buffer
+# is int64 [B][C][2][S].  S = 1 by default (one float64 per statistic, fp64 atomics); S = ACC_SLOTS
+# in the exact mode (7 exponent bins + a non-finite count: bit-identical whatever order the atomics
+# land in), chosen with set_bn_exact(True) -- or CVL_BN_EXACT=1 -- before any buffer is made.
 ACC_SLOTS = 8
 ACC_BINS, ACC_W, ACC_E0 = 7, 22, 27
+
+
+def set_bn_exact(on):
+    """Library-wide BN accumulator mode (cvl_bn_set_exact); buffers made before a switch are invalid."""
+    _lib.call("cvl_bn_set_exact", 1 if on else 0)
+
+
+def acc_slots():
+    """uint64 slots per statistic of the current mode (cvl_bn_acc_slots): 1 or ACC_SLOTS."""
+    return int(_lib.load().cvl_bn_acc_slots())
 
 
 def bn_acc(B, C, device, zero=True):
     """A (B, C) BN statistics buffer ((sum, sumsq) or (sum g, sum g*xhat)) for the producing kernels."""
     f = torch.zeros if zero else torch.empty
-    return f((B, C, 2, ACC_SLOTS), dtype=torch.int64, device=device)
+    return f((B, C, 2, acc_slots()), dtype=torch.int64, device=device)
 
 
 def bn_acc_value(acc):
@@ -252,10 +263,16 @@ def _acc_add_f32(bins, f):
     bins[..., ACC_BINS] += bad.to(torch.int64)
 
 
-def bn_acc_encode(values):
-    """float64 statistic values [..., 2] -> an exact accumulator buffer [..., 2, ACC_SLOTS] (each value
-    split into three float32 pieces as bn_acc.h acc_add_f64; for callers that hold the sums already)."""
+def bn_acc_encode(values, exact=None):
+    """float64 statistic values [..., 2] -> an accumulator buffer [..., 2, S] of the library's mode
+    (exact=None) or of the given one: the float64 bits (S = 1), or each value split into three float32
+    pieces added into the bins as bn_acc.h acc_add_f64 (S = ACC_SLOTS).  For callers that hold the
+    sums already."""
     v = values.to(torch.float64)
+    if exact is None:
+        exact = acc_slots() == ACC_SLOTS
+    if not exact:
+        return v.contiguous().view(torch.int64).unsqueeze(-1).clone()
     out = torch.zeros(v.shape + (ACC_SLOTS,), dtype=torch.int64, device=v.device)
     hi = v.to(torch.float32)
     r = v - hi.double()
@@ -343,7 +360,7 @@ def depthwise_wgrad(x, dy, dw, k, stride, pad_t, pad_l, beta=0.0):
 
 def conv_igemm_dgrad_bnsum(desc, src, dst, z, mean_rstd, gamma, beta, sums, act_hi=float("inf"), zero=True):
     """DGRAD conv whose epilogue also forms the next BN's backward first pass into `sums`
-    (bn_acc [B][C][2][8], zeroed here first unless zero=False: the caller's buffer is already zero).
+    (bn_acc [B][C][2][S], zeroed here first unless zero=False: the caller's buffer is already zero).
     Returns True when fused; False = the plain data gradient ran and `sums` is untouched (run the
     two-pass BN backward)."""
     _prec(desc, src)

@@ -20,7 +20,7 @@ STEM_K = 7
 FUSE_POOL = os.environ.get("CVL_STEM_NO_FUSE_POOL", "0") != "1"
 # stem form: im2col + 1x1 GEMM (K = 147 padded to 192, the LDS-DMA kernels' K-tiles) or, with
 # CVL_STEM_DIRECT=1, cvl_stem_conv7x7s2 / cvl_stem_wgrad straight from the image (K = 7 x 24)
-DIRECT_STEM = os.environ.get("CVL_STEM_DIRECT", "0") == "1"
+DIRECT_STEM = os.environ.get("CVL_STEM_DIRECT", "1") == "1"
 STEM_KP = 168 if DIRECT_STEM else 192
 
 

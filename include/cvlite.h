@@ -121,18 +121,24 @@ int cvl_fcos_center_v1_assign(const float* boxes, const int32_t* nbox, const flo
  * zero it first), which requires H*W % 4 == 0.
  *
  * BN accumulators (cvl_bn_acc): the statistics many workgroups add into one (image, channel) --
- * (sum, sumsq) of a conv output, (sum g, sum g*xhat) of a BN backward -- are kept EXACTLY and
- * order-independently: each fp32 partial is added as an integer into one of 7 uint64 bins chosen
- * by its exponent (bin k holds multiples of 2^(22k - 123); partials below 2^-100 are dropped, slot
- * 7 counts non-finite ones), so the result is bit-identical whatever order the atomics land in.
- * Layout: uint64 [B][C][2][CVL_BN_ACC_SLOTS]; the value of a statistic is
- * sum_k (double)(int64)slot[k] * 2^(22k - 123) over k = 0..6 in that order (NaN if slot[7] != 0);
- * cvl_bn_acc_decode writes those values as float64 [n].  The consumers (cvl_bn_finalize[_apply],
- * cvl_bn_backward_*_sums) first DECODE THE BUFFER IN PLACE -- slot 0 of each statistic becomes its
- * float64 value and slot 7 the marker ~0 -- so each statistic is decoded once, not by every block
- * that reads it; a decoded buffer stays valid input for every reader (decode is idempotent).
+ * (sum, sumsq) of a conv output, (sum g, sum g*xhat) of a BN backward.  Two modes, chosen for the
+ * whole library by cvl_bn_set_exact() before any buffer is made (cvl_bn_acc_slots() = S reports it):
+ *  - default (S = 1): one float64 per statistic, fp64 atomic adds of fp32 partials (the order of
+ *    the adds can change the last bits of a sum);
+ *  - exact (S = 8, cvl_bn_set_exact(1)): each fp32 partial is added as an integer into one of 7
+ *    uint64 bins chosen by its exponent (bin k holds multiples of 2^(22k - 123); partials below
+ *    2^-100 are dropped, slot 7 counts non-finite ones), so the result is bit-identical whatever
+ *    order the atomics land in.  The value of a statistic is
+ *    sum_k (double)(int64)slot[k] * 2^(22k - 123) over k = 0..6 in that order (NaN if slot[7] != 0).
+ *    The consumers (cvl_bn_finalize[_apply], cvl_bn_backward_*_sums) first DECODE THE BUFFER IN
+ *    PLACE -- slot 0 of each statistic becomes its float64 value and slot 7 the marker ~0 -- so each
+ *    statistic is decoded once; a decoded buffer stays valid input for every reader.
+ * Layout: uint64 [B][C][2][S] (zero it before the producer); cvl_bn_acc_decode writes the values of
+ * n statistics as float64 [n] in either mode.
  * ---------------------------------------------------------------------------------------- */
-#define CVL_BN_ACC_SLOTS 8
+#define CVL_BN_ACC_SLOTS 8          /* S of the exact mode */
+int cvl_bn_set_exact(int on);
+int cvl_bn_acc_slots(void);
 int cvl_bn_acc_decode(const uint64_t* acc, double* out, int64_t n, cvl_stream_t stream);
 #define CVL_CONV_MAX_SEG 10
 enum { CVL_CONV_FWD = 0, CVL_CONV_DGRAD = 1 };
@@ -260,7 +266,7 @@ int cvl_im2col(const float* x, int B, int H, int W, int C, int KH, int KW, int s
 /* ------------------------------------------------------------------------------------------
  * BatchNormalization in training mode with per-image statistics (the reference forwards one
  * image at a time, train_fcos.py:137-153; Keras eps 1.001e-5, momentum 0.99, running variance
- * unbiased as TF's fused kernel).  stats: BN accumulators [B][C][2][8] from cvl_conv_igemm(bn_stats)
+ * unbiased as TF's fused kernel).  stats: BN accumulators [B][C][2][S] from cvl_conv_igemm(bn_stats)
  * or cvl_bn_stats; mean_rstd [B][C][2].
  * ---------------------------------------------------------------------------------------- */
 int cvl_bn_finalize(uint64_t* stats, float* mean_rstd, float* run_mean, float* run_var, int B,
@@ -295,7 +301,7 @@ int cvl_bn_backward_relu(const void* dy, const void* z, const float* mean_rstd, 
  * result is dy of a BN -> ReLU (act_hi = INFINITY) / ReLU6 (act_hi = 6) unit without a residual
  * (the bottleneck's conv1 / conv2 units: their dy has one producer) and, when the 256-row
  * LDS-DMA kernel takes the launch with one image per tile, adds per (image, channel)
- * (sum g, sum g*xhat), g = dy * mask(bn(z)), into sums (BN accumulators [B][C][2][8], zero them first) and sets
+ * (sum g, sum g*xhat), g = dy * mask(bn(z)), into sums (BN accumulators [B][C][2][S], zero them first) and sets
  * *fused (HOST) = 1; otherwise it runs the plain data gradient and sets *fused = 0.  z / mean_rstd
  * / gamma / beta are the unit's pre-BN conv output (same layout as dst), (mean, rstd) [B][C][2]
  * and BN parameters.  cvl_bn_backward_relu_sums is cvl_bn_backward_relu's second pass from those
@@ -515,7 +521,7 @@ int cvl_soft_nms(const double* boxes, int n, const double* classes, int ncls, do
  * per sub-batch of `group` images, so statistics span the sub-batch (groups [g*G, min(g*G+G, B)),
  * the last may be short); running stats are updated once per group, in order.
  * cvl_bn_stats: stats[b][c] = (sum, sum of squares) over H*W of a bf16 NHWC tensor (BN
- *   accumulators [B][C][2][8], deterministic), the input of cvl_bn_finalize[_grouped].
+ *   accumulators [B][C][2][S], deterministic), the input of cvl_bn_finalize[_grouped].
  * cvl_bn_backward_grouped: as cvl_bn_backward (no ReLU output / conv bias terms) with group
  *   statistics; dz = BN-backward + dz_beta * dz (accumulate into an existing gradient). */
 size_t cvl_bn_stats_workspace_size(int B, int HW, int C);

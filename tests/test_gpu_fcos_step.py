@@ -248,14 +248,25 @@ def test_tower0_dgrad_forms_agree(monkeypatch):
         assert float((res["0"][k] - res["1"][k]).norm() / res["1"][k].norm()) < 2e-2, k
 
 
-def test_fcos_step_run_to_run_bit_identical():
-    """Reproducibility (SURVEY §7, round-2 review weak #11): two trainers built from the same seed run
-    one graph-replayed step on the same 512x512 batch and end with bit-identical parameters, momentum
-    buffers and losses.  The split reductions (weight-gradient slabs, split-K, gradient norm) sum in
-    a fixed order; the fused BN statistics add per-workgroup fp32 partials into fp64 with atomics,
-    which is order-independent whenever the partials' exact sum fits fp64's 53 bits (24-bit fp32
-    mantissas of similar magnitude: it does) -- this test is the check of that claim on the bench
-    shapes (4 images: ~64 workgroups of every 1x1 launch add into each image's statistics)."""
+@pytest.mark.parametrize("exact", [True, False])
+def test_fcos_step_run_to_run_bit_identical(exact):
+    """Reproducibility: two trainers built from the same seed run two graph-replayed
+    steps on the same 512x512 batch and end with bit-identical parameters, momentum buffers and
+    losses.  The split reductions (weight-gradient slabs, split-K, gradient norm) sum in a fixed
+    order.  The fused BN statistics: in the exact mode (cvl_bn_set_exact) integer bins, identical by
+    construction; in the default mode fp64 atomics of fp32 partials, which can differ in the last
+    bits only when a statistic's partials span more than fp64's 53 bits -- observed identical here."""
+    from cvlite import ops_nn as nn
+    from cvlite.fcos_net import FCOSNet
+    from cvlite.train_fcos import FCOSTrainer, synthetic_batch
+    nn.set_bn_exact(exact)
+    try:
+        _run_to_run(exact)
+    finally:
+        nn.set_bn_exact(False)
+
+
+def _run_to_run(exact):
     from cvlite.fcos_net import FCOSNet
     from cvlite.train_fcos import FCOSTrainer, synthetic_batch
     C, B, D = 20, 4, 512

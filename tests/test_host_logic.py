@@ -199,7 +199,7 @@ def test_bn_acc_encoding_exact_and_order_independent():
     rng = np.random.default_rng(3)
     vals = np.concatenate([rng.standard_normal(300) * 10.0 ** rng.integers(-12, 15, 300),
                            [0.0, -0.0, 1e-40, 2.0 ** 60, float("inf"), float("nan")]])
-    acc = nn.bn_acc_encode(torch.tensor(vals).view(-1, 1).repeat(1, 2))
+    acc = nn.bn_acc_encode(torch.tensor(vals).view(-1, 1).repeat(1, 2), exact=True)
     for i, x in enumerate(vals):
         b = encode(float(x))
         assert acc[i, 0].tolist() == b, (x, acc[i, 0].tolist(), b)

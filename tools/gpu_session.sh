@@ -21,7 +21,8 @@ for s in $steps; do
              tail -4 gpurun_out/${tag}_pytest.log ;;
     bench)   run 150 gpurun_out/${tag}_bench.err bash -c "python -u bench.py --steps 30 --runs 1 --no-cpu-baseline > gpurun_out/${tag}_bench.json"
              tail -c 300 gpurun_out/${tag}_bench.json; echo ;;
-    benchd)  run 150 gpurun_out/${tag}_benchd.err bash -c "CVL_STEM_DIRECT=1 python -u bench.py --steps 30 --runs 1 --no-cpu-baseline > gpurun_out/${tag}_benchd.json"
+    benchi)  run 150 gpurun_out/${tag}_benchi.err bash -c "CVL_STEM_DIRECT=0 python -u bench.py --steps 30 --runs 1 --no-cpu-baseline > gpurun_out/${tag}_benchi.json"
+    benchx)  run 150 gpurun_out/${tag}_benchx.err bash -c "CVL_BN_EXACT=1 python -u bench.py --steps 30 --runs 1 --no-cpu-baseline > gpurun_out/${tag}_benchx.json"
              tail -c 200 gpurun_out/${tag}_benchd.json; echo ;;
     table)   run 120 gpurun_out/${tag}_table.log python -u tools/conv_table.py --out gpurun_out/${tag}_conv_table.md
              head -4 gpurun_out/${tag}_conv_table.md ;;
