@@ -318,31 +318,53 @@ __device__ __forceinline__ float bn_affine(float z, float m, float rs, float ga,
   return __builtin_fmaf(ga, (z - m) * rs, be);
 }
 constexpr int BN_FIN_MAXC = 2048;
-template <bool FIN>
+
+// RBN: the residual is itself a BN output that was never stored -- the projection shortcut's
+// z_s with its own statistics (Keras block1: BN_0(conv_0(x)) + BN_3(conv_3(...)), ReLU).  The
+// residual term is bf16(bn_affine(z_s)), rounded exactly as the stored shortcut output was, so the
+// fused unit's y is bit-identical to the two-launch form; its finalize runs in the same prologue.
+struct BnRes {
+  const cvl_bf16* z;
+  const float* gamma;
+  const float* beta;
+  BnFin fin;
+};
+
+// FIN prologue of one BN: (mean, rstd) of image b into smr, the chunk-0 blocks store them, the
+// image-0 blocks advance the running statistics
+__device__ __forceinline__ void bn_fin_prologue(const BnFin& fin, float2* smr, int b, int C, int HW) {
+  for (int c = threadIdx.x; c < C; c += NT) {
+    const long bc = (long)b * C + c;
+    float mm, rr;
+    double var;
+    bn_moments(acc_dec(fin.stats, bc, 0, fin.slots), acc_dec(fin.stats, bc, 1, fin.slots), HW, fin.eps, &mm, &rr, &var);
+    smr[c] = float2{mm, rr};
+    if (blockIdx.x == 0) { fin.mr_out[bc * 2] = mm; fin.mr_out[bc * 2 + 1] = rr; }
+  }
+  // running statistics: one channel per thread over the image-0 blocks (a serial float64 chain
+  // over the images -- in one block it was the critical path of the small launches)
+  if (b == 0 && fin.run_mean)
+    for (int c = blockIdx.x * NT + threadIdx.x; c < C; c += gridDim.x * NT)
+      bn_running(fin.stats, fin.slots, gridDim.y, C, c, HW, fin.eps, fin.momentum, fin.run_mean, fin.run_var);
+}
+
+template <bool FIN, bool RBN = false>
 __global__ void __launch_bounds__(NT) bn_apply_kernel(const cvl_bf16* __restrict__ z, const float* __restrict__ mr,
                                                       const float* __restrict__ gamma, const float* __restrict__ beta,
                                                       const cvl_bf16* __restrict__ res, cvl_bf16* __restrict__ y,
-                                                      int C, int HW, int relu, int rows_per_blk, BnFin fin) {
+                                                      int C, int HW, int relu, int rows_per_blk, BnFin fin,
+                                                      BnRes rb) {
+  static_assert(FIN || !RBN, "the BN residual form fuses both finalizes");
   const int b = blockIdx.y;
   const int C8 = C / 8;
   const int tpr = C8 < NT ? C8 : NT;
   const int rpp = NT / tpr;
   const int cg = threadIdx.x % tpr, rsub = threadIdx.x / tpr;
   __shared__ float2 smr[FIN ? BN_FIN_MAXC : 1];
+  __shared__ float2 smr2[RBN ? BN_FIN_MAXC : 1];
   if (FIN) {      // (mean, rstd) of this image, one channel per thread, shared through LDS
-    for (int c = threadIdx.x; c < C; c += NT) {
-      const long bc = (long)b * C + c;
-      float mm, rr;
-      double var;
-      bn_moments(acc_dec(fin.stats, bc, 0, fin.slots), acc_dec(fin.stats, bc, 1, fin.slots), HW, fin.eps, &mm, &rr, &var);
-      smr[c] = float2{mm, rr};
-      if (blockIdx.x == 0) { fin.mr_out[bc * 2] = mm; fin.mr_out[bc * 2 + 1] = rr; }
-    }
-    // running statistics: one channel per thread over the image-0 blocks (a serial float64 chain
-    // over the images -- in one block it was the critical path of the small launches)
-    if (b == 0 && fin.run_mean)
-      for (int c = blockIdx.x * NT + threadIdx.x; c < C; c += gridDim.x * NT)
-        bn_running(fin.stats, fin.slots, gridDim.y, C, c, HW, fin.eps, fin.momentum, fin.run_mean, fin.run_var);
+    bn_fin_prologue(fin, smr, b, C, HW);
+    if (RBN) bn_fin_prologue(rb.fin, smr2, b, C, HW);
     __syncthreads();
   }
   if (rsub >= rpp) return;
@@ -351,6 +373,7 @@ __global__ void __launch_bounds__(NT) bn_apply_kernel(const cvl_bf16* __restrict
   for (int cgb = cg; cgb < C8; cgb += tpr) {
     const int c0 = cgb * 8;
     float m[8], rs[8], ga[8], be[8];
+    float m2[8], rs2[8], ga2[8], be2[8];
 #pragma unroll
     for (int u = 0; u < 8; ++u) {
       const long bc = (long)b * C + c0 + u;
@@ -363,7 +386,14 @@ __global__ void __launch_bounds__(NT) bn_apply_kernel(const cvl_bf16* __restrict
       }
       ga[u] = gamma[c0 + u];
       be[u] = beta[c0 + u];
+      if (RBN) {
+        m2[u] = smr2[c0 + u].x;
+        rs2[u] = smr2[c0 + u].y;
+        ga2[u] = rb.gamma[c0 + u];
+        be2[u] = rb.beta[c0 + u];
+      }
     }
+    const cvl_bf16* rsrc = RBN ? rb.z : res;
     for (int r = r0 + rsub; r < r1; r += rpp * BNA_UNR) {
       s16x8 vz[BNA_UNR], vr[BNA_UNR];
       long off[BNA_UNR];
@@ -372,18 +402,25 @@ __global__ void __launch_bounds__(NT) bn_apply_kernel(const cvl_bf16* __restrict
         const int rq = min(r + q * rpp, r1 - 1);
         off[q] = ((long)b * HW + rq) * C + c0;
         vz[q] = *reinterpret_cast<const s16x8*>(z + off[q]);
-        if (res) vr[q] = *reinterpret_cast<const s16x8*>(res + off[q]);
+        if (rsrc) vr[q] = *reinterpret_cast<const s16x8*>(rsrc + off[q]);
       }
 #pragma unroll
       for (int q = 0; q < BNA_UNR; ++q) {
         if (r + q * rpp >= r1) break;
         float v[8], rr[8];
         unpack8(vz[q], v);
-        if (res) unpack8(vr[q], rr);
+        if (RBN) {                    // the shortcut's BN output, rounded to bf16 as it was stored
+          unpack8(vr[q], rr);
+#pragma unroll
+          for (int u = 0; u < 8; ++u) rr[u] = bn_affine(rr[u], m2[u], rs2[u], ga2[u], be2[u]);
+          unpack8(pack8(rr), rr);
+        } else if (res) {
+          unpack8(vr[q], rr);
+        }
 #pragma unroll
         for (int u = 0; u < 8; ++u) {
           float o = bn_affine(v[u], m[u], rs[u], ga[u], be[u]);
-          if (res) o += rr[u];
+          if (RBN || res) o += rr[u];
           if (relu) o = o > 0.f ? o : 0.f;
           if (relu == 2) o = fminf(o, 6.0f);                     // ReLU6 (MobileNetV2)
           v[u] = o;
@@ -1323,7 +1360,7 @@ extern "C" int cvl_bn_apply(const void* z, const float* mean_rstd, const float* 
   const int rpb = bn_rows_per_blk(B, HW, C);
   hipLaunchKernelGGL(bn_apply_kernel<false>, dim3((HW + rpb - 1) / rpb, B), dim3(NT), 0, S_, (const cvl_bf16*)z,
                      mean_rstd, gamma, beta, (const cvl_bf16*)residual, (cvl_bf16*)y, C, HW, relu, rpb,
-                     BnFin{nullptr, nullptr, nullptr, nullptr, 0.f, 0.f, 1});
+                     BnFin{nullptr, nullptr, nullptr, nullptr, 0.f, 0.f, 1}, BnRes{});
   return cvl_launch_status();
 }
 
@@ -1339,7 +1376,31 @@ extern "C" int cvl_bn_finalize_apply(uint64_t* stats, float* mean_rstd, float* r
   const int rpb = bn_rows_per_blk(B, HW, C);
   hipLaunchKernelGGL(bn_apply_kernel<true>, dim3((HW + rpb - 1) / rpb, B), dim3(NT), 0, S_, (const cvl_bf16*)z,
                      (const float*)nullptr, gamma, beta, (const cvl_bf16*)residual, (cvl_bf16*)y, C, HW, relu, rpb,
-                     BnFin{(const acc_u64*)stats, mean_rstd, run_mean, run_var, eps, momentum, g_acc_slots});
+                     BnFin{(const acc_u64*)stats, mean_rstd, run_mean, run_var, eps, momentum, g_acc_slots}, BnRes{});
+  return cvl_launch_status();
+}
+
+extern "C" int cvl_bn_finalize_apply_bnres(uint64_t* stats, float* mean_rstd, float* run_mean, float* run_var,
+                                           const void* z, const float* gamma, const float* beta, uint64_t* res_stats,
+                                           float* res_mean_rstd, float* res_run_mean, float* res_run_var,
+                                           const void* res_z, const float* res_gamma, const float* res_beta,
+                                           float res_eps, float res_momentum, void* y, int B, int HW, int C, int relu,
+                                           float eps, float momentum, cvl_stream_t stream) {
+  CVL_CHECK_ARG(stats && mean_rstd && z && gamma && beta && y && C % 8 == 0 && B > 0 && HW > 0);
+  CVL_CHECK_ARG(res_stats && res_mean_rstd && res_z && res_gamma && res_beta);
+  CVL_CHECK_ARG(C <= BN_FIN_MAXC);
+  CVL_CHECK_ARG((run_mean == nullptr) == (run_var == nullptr));
+  CVL_CHECK_ARG((res_run_mean == nullptr) == (res_run_var == nullptr));
+  int dst = acc_decode_launch((acc_u64*)stats, 2L * B * C, S_);
+  if (!dst) dst = acc_decode_launch((acc_u64*)res_stats, 2L * B * C, S_);
+  if (dst) return dst;
+  const int rpb = bn_rows_per_blk(B, HW, C);
+  hipLaunchKernelGGL((bn_apply_kernel<true, true>), dim3((HW + rpb - 1) / rpb, B), dim3(NT), 0, S_, (const cvl_bf16*)z,
+                     (const float*)nullptr, gamma, beta, (const cvl_bf16*)nullptr, (cvl_bf16*)y, C, HW, relu, rpb,
+                     BnFin{(const acc_u64*)stats, mean_rstd, run_mean, run_var, eps, momentum, g_acc_slots},
+                     BnRes{(const cvl_bf16*)res_z, res_gamma, res_beta,
+                           BnFin{(const acc_u64*)res_stats, res_mean_rstd, res_run_mean, res_run_var, res_eps,
+                                 res_momentum, g_acc_slots}});
   return cvl_launch_status();
 }
 

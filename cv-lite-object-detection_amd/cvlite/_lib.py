@@ -59,6 +59,8 @@ SIGNATURES = {
     "cvl_stem_wgrad": (c_int, [P, c_int, c_int, c_int, P, P, c_float, P, c_size_t, P]),
     "cvl_bn_apply": (c_int, [P, P, P, P, P, P, c_int, c_int, c_int, c_int, P]),
     "cvl_bn_finalize_apply": (c_int, [P, P, P, P, P, P, P, P, P, c_int, c_int, c_int, c_int, c_float, c_float, P]),
+    "cvl_bn_finalize_apply_bnres": (c_int, [P, P, P, P, P, P, P, P, P, P, P, P, P, P, c_float, c_float, P, c_int,
+                                            c_int, c_int, c_int, c_float, c_float, P]),
     "cvl_bn_backward_workspace_size": (c_size_t, [c_int, c_int, c_int]),
     "cvl_bn_backward": (c_int, [P, P, P, P, P, P, c_size_t, P, P, P, P, c_float, P, c_int, c_int, c_int, P]),
     "cvl_bn_backward_relu": (c_int, [P, P, P, P, P, P, c_size_t, P, P, P, c_float, P, c_int, c_int, c_int, P]),

@@ -288,11 +288,19 @@ class BatchNorm(object):
         mr[:, :, 1] = torch.rsqrt(self.run_var + self.eps)
         return mr
 
-    def normalize(self, z, stats, B, HW, relu, residual=None, train=True):
+    def normalize(self, z, stats, B, HW, relu, residual=None, train=True, residual_bn=None):
         """y = BN(z) (+ residual) (ReLU): training mode from the conv's fused per-image statistics
-        (and the moving-average update), inference mode from the moving statistics."""
+        (and the moving-average update), inference mode from the moving statistics.
+        residual_bn: a deferred unit's (z, stats, mean_rstd out, BatchNorm) -- the residual is that
+        BN's output, formed in the same launch (cvl_bn_finalize_apply_bnres), never stored."""
         y = torch.empty_like(z)
-        if train:
+        if train and residual_bn is not None:
+            rz, rstats, rmr, rbn = residual_bn
+            mr = torch.empty((B, self.c, 2), dtype=torch.float32, device=z.device)
+            nn.bn_finalize_apply_bnres(stats, mr, self.run_mean, self.run_var, z, self.gamma, self.beta, rstats, rmr,
+                                       rbn.run_mean, rbn.run_var, rz, rbn.gamma, rbn.beta, rbn.eps, rbn.momentum, y,
+                                       B, HW, self.c, relu, self.eps, self.momentum)
+        elif train:
             mr = torch.empty((B, self.c, 2), dtype=torch.float32, device=z.device)
             nn.bn_finalize_apply(stats, mr, self.run_mean, self.run_var, z, self.gamma, self.beta, residual, y, B,
                                  HW, self.c, relu, self.eps, self.momentum)
@@ -319,15 +327,24 @@ class ConvBN(object):
                          bias=True, dgrad=dgrad, cin_k=cin_k)
         self.bn = BatchNorm(store, (name + "_bn") if bn_name is None else bn_name, cout)
 
-    def forward(self, x, B, H, W, relu=True, residual=None, train=True, arena=None):
+    def forward(self, x, B, H, W, relu=True, residual=None, train=True, arena=None, defer=False,
+                residual_bn=None):
+        """defer (training, no ReLU): the BN is not applied here -- returns (pending, saved) where
+        pending = (z, stats, mean_rstd, BatchNorm) is the consumer's residual_bn, which forms this
+        unit's output and finalize inside its own BN launch (the projection shortcut)."""
         c = self.conv.cout
         Ho, Wo, _, _ = self.conv.out_hw(H, W)
         stats = None
         if train:
             stats = arena.take(B, c) if arena is not None else nn.bn_acc(B, c, x.device)
         z, _, _ = self.conv.fwd(x, B, H, W, stats=stats)
-        y, mr = self.bn.normalize(z, stats, B, Ho * Wo, relu, residual=residual, train=train)
-        return y, (x, z, y, mr, B, H, W, Ho, Wo, relu, residual is not None)
+        if defer:
+            assert train and not relu and residual is None
+            mr = torch.empty((B, c, 2), dtype=torch.float32, device=z.device)
+            return (z, stats, mr, self.bn), (x, z, None, mr, B, H, W, Ho, Wo, relu, False)
+        y, mr = self.bn.normalize(z, stats, B, Ho * Wo, relu, residual=residual, train=train,
+                                  residual_bn=residual_bn)
+        return y, (x, z, y, mr, B, H, W, Ho, Wo, relu, residual is not None or residual_bn is not None)
 
     def bn_next_ctx(self, saved, arena=None):
         """What a producer of this unit's dy needs to fuse the BN backward's first pass into its

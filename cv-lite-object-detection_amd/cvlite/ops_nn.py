@@ -299,6 +299,16 @@ def bn_finalize_apply(stats, mean_rstd, run_mean, run_var, z, gamma, beta, resid
               ptr(beta), ptr(residual), ptr(y), B, HW, C, int(relu), float(eps), float(momentum), stream())
 
 
+def bn_finalize_apply_bnres(stats, mean_rstd, run_mean, run_var, z, gamma, beta, res_stats, res_mean_rstd,
+                            res_run_mean, res_run_var, res_z, res_gamma, res_beta, res_eps, res_momentum, y, B,
+                            HW, C, relu, eps, momentum):
+    """y = act(BN(z) + BN_res(res_z)) with both finalizes in one launch (cvl_bn_finalize_apply_bnres)."""
+    _lib.call("cvl_bn_finalize_apply_bnres", ptr(stats), ptr(mean_rstd), ptr(run_mean), ptr(run_var), ptr(z),
+              ptr(gamma), ptr(beta), ptr(res_stats), ptr(res_mean_rstd), ptr(res_run_mean), ptr(res_run_var),
+              ptr(res_z), ptr(res_gamma), ptr(res_beta), float(res_eps), float(res_momentum), ptr(y), B, HW, C,
+              int(relu), float(eps), float(momentum), stream())
+
+
 def bn_backward(dy, y_relu, z, mean_rstd, gamma, dz, g_out, dgamma, dbeta, B, HW, C, beta_acc=0.0,
                 conv_dbias=None):
     if _is_f32(dy):

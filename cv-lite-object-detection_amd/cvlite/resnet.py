@@ -21,6 +21,8 @@ FUSE_POOL = os.environ.get("CVL_STEM_NO_FUSE_POOL", "0") != "1"
 # stem form: im2col + 1x1 GEMM (K = 147 padded to 192, the LDS-DMA kernels' K-tiles) or, with
 # CVL_STEM_DIRECT=1, cvl_stem_conv7x7s2 / cvl_stem_wgrad straight from the image (K = 7 x 24)
 DIRECT_STEM = os.environ.get("CVL_STEM_DIRECT", "1") == "1"
+# projection shortcut's BN applied inside conv3's BN launch (CVL_NO_SC_BN_FUSE=1: stored and re-read)
+FUSE_SC_BN = os.environ.get("CVL_NO_SC_BN_FUSE", "0") != "1"
 STEM_KP = 168 if DIRECT_STEM else 192
 
 
@@ -139,15 +141,19 @@ class Bottleneck(object):
         return [u for u in (self.sc, self.c1, self.c2, self.c3) if u is not None]
 
     def forward(self, x, B, H, W, train=True, arena=None):
-        sv_s = None
+        sv_s = s_bn = None
+        s = x
         if self.sc is not None:
-            s, sv_s = self.sc.forward(x, B, H, W, relu=False, train=train, arena=arena)
-        else:
-            s = x
+            # training, bf16: the shortcut's BN output is formed inside conv3's BN launch
+            # (cvl_bn_finalize_apply_bnres) instead of being stored and re-read
+            defer = train and FUSE_SC_BN and x.dtype == torch.bfloat16
+            s, sv_s = self.sc.forward(x, B, H, W, relu=False, train=train, arena=arena, defer=defer)
+            if defer:
+                s_bn, s = s, None
         y1, sv1 = self.c1.forward(x, B, H, W, relu=True, train=train, arena=arena)
         H1, W1 = sv1[7], sv1[8]
         y2, sv2 = self.c2.forward(y1, B, H1, W1, relu=True, train=train, arena=arena)
-        y3, sv3 = self.c3.forward(y2, B, H1, W1, relu=True, residual=s, train=train, arena=arena)
+        y3, sv3 = self.c3.forward(y2, B, H1, W1, relu=True, residual=s, train=train, arena=arena, residual_bn=s_bn)
         return y3, H1, W1, (sv_s, sv1, sv2, sv3)
 
     def backward(self, dy, saved, dx_out=None, dx_beta=0.0, arena=None, sums3=None, prev_ctx=None):

@@ -279,6 +279,18 @@ int cvl_bn_apply(const void* z, const float* mean_rstd, const float* gamma, cons
 int cvl_bn_finalize_apply(uint64_t* stats, float* mean_rstd, float* run_mean, float* run_var,
                           const void* z, const float* gamma, const float* beta, const void* residual, void* y,
                           int B, int HW, int C, int relu, float eps, float momentum, cvl_stream_t stream);
+/* cvl_bn_finalize_apply whose residual is ANOTHER BN's output that was never stored: the projection
+ * shortcut of a Keras ResNet block1, y = act(BN_3(z) + BN_0(res_z)).  Both finalizes run in the one
+ * launch (res_mean_rstd written, res running statistics advanced with res_eps / res_momentum), and the
+ * residual term is bf16(BN_0(res_z)) rounded as the stored shortcut output was: bit-identical to
+ * cvl_bn_finalize_apply(res) + cvl_bn_finalize_apply(z, residual) without writing or re-reading it.
+ * Replaces the shortcut's apply of resnet.py block1 (Keras applications, behind FCOS/fcos.py:30-35). */
+int cvl_bn_finalize_apply_bnres(uint64_t* stats, float* mean_rstd, float* run_mean, float* run_var,
+                                const void* z, const float* gamma, const float* beta, uint64_t* res_stats,
+                                float* res_mean_rstd, float* res_run_mean, float* res_run_var,
+                                const void* res_z, const float* res_gamma, const float* res_beta,
+                                float res_eps, float res_momentum, void* y, int B, int HW, int C, int relu,
+                                float eps, float momentum, cvl_stream_t stream);
 /* dy: grad of y; y_relu: y when the unit ends in ReLU (mask), else NULL; writes dz (bf16),
  * optionally g_out = masked dy (the residual branch's gradient), dgamma/dbeta (= + beta_acc*old)
  * and, if conv_dbias != NULL, the gradient of the preceding conv's bias, which is exactly 0

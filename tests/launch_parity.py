@@ -636,6 +636,22 @@ def check_bn_finalize_apply(lp, name, launch, stats, mean_rstd, run_mean, run_va
     lp.cmp(name, d, "y", y.reshape(B, HW, C), _apply_ref(zr, mean_rstd, gamma, beta, rr, relu, B, HW, C))
 
 
+def check_bn_finalize_apply_bnres(lp, name, launch, stats, mean_rstd, run_mean, run_var, z, gamma, beta, res_stats,
+                                  res_mean_rstd, res_run_mean, res_run_var, res_z, res_gamma, res_beta, res_eps,
+                                  res_momentum, y, B, HW, C, relu, eps, momentum):
+    rm0, rv0 = _clone(run_mean, run_var)
+    rrm0, rrv0 = _clone(res_run_mean, res_run_var)
+    zr, rzr = _keep_inputs(y, z, res_z)
+    launch(stats, mean_rstd, run_mean, run_var, z, gamma, beta, res_stats, res_mean_rstd, res_run_mean, res_run_var,
+           res_z, res_gamma, res_beta, res_eps, res_momentum, y, B, HW, C, relu, eps, momentum)
+    d = "C%d HW%d B%d relu%d +bn-res" % (C, HW, B, relu)
+    _check_finalize(lp, name, d, stats, mean_rstd, rm0, rv0, run_mean, run_var, B, C, HW, eps, momentum)
+    _check_finalize(lp, name, d + " (res)", res_stats, res_mean_rstd, rrm0, rrv0, res_run_mean, res_run_var, B, C,
+                    HW, res_eps, res_momentum)
+    res = _apply_ref(rzr, res_mean_rstd, res_gamma, res_beta, None, 0, B, HW, C)
+    lp.cmp(name, d, "y", y.reshape(B, HW, C), _apply_ref(zr, mean_rstd, gamma, beta, res, relu, B, HW, C))
+
+
 def check_bn_apply(lp, name, launch, z, mean_rstd, gamma, beta, residual, y, B, HW, C, relu):
     zr, rr = _keep_inputs(y, z, residual)
     launch(z, mean_rstd, gamma, beta, residual, y, B, HW, C, relu)
@@ -1154,6 +1170,7 @@ CHECKS = {
     "bn_finalize": check_bn_finalize,
     "bn_apply": check_bn_apply,
     "bn_finalize_apply": check_bn_finalize_apply,
+    "bn_finalize_apply_bnres": check_bn_finalize_apply_bnres,
     "bn_backward": check_bn_backward,
     "bn_backward_relu": check_bn_backward_relu,
     "bn_backward_relu6": check_bn_backward_relu6,

@@ -91,6 +91,39 @@ def test_bn_forward_backward(B, HW, C, relu, res):
         assert torch.equal(dgam2, dgam) and torch.equal(dbet2, dbet) and torch.count_nonzero(cdb2).item() == 0
 
 
+@pytest.mark.parametrize("B,HW,C", [(2, 64, 256), (3, 256, 2048), (1, 4096, 512)])
+def test_bn_finalize_apply_bnres_bit_identical(B, HW, C):
+    """cvl_bn_finalize_apply_bnres (projection shortcut's BN formed inside conv3's BN launch) equals
+    the two-launch form bit for bit: shortcut finalize_apply (no ReLU) stored as bf16, then conv3's
+    finalize_apply with it as the residual -- y, both (mean, rstd) and both running statistics."""
+    from cvlite import ops_nn as nn
+    g = torch.Generator().manual_seed(B * 7 + C)
+    dev = "cuda"
+    z = bfr(torch.randn(B, HW, C, generator=g, dtype=torch.float64) * 2 + 0.5)
+    zs = bfr(torch.randn(B, HW, C, generator=g, dtype=torch.float64) * 3 - 0.2)
+    ga, be = (torch.rand(C, generator=g) + 0.5).cuda(), torch.randn(C, generator=g).cuda()
+    gs, bs = (torch.rand(C, generator=g) + 0.5).cuda(), torch.randn(C, generator=g).cuda()
+    st = nn.bn_acc_encode(torch.stack([z.sum(1), (z * z).sum(1)], -1)).cuda()
+    sts = nn.bn_acc_encode(torch.stack([zs.sum(1), (zs * zs).sum(1)], -1)).cuda()
+    zg, zsg = z.to(BF).cuda(), zs.to(BF).cuda()
+    outs = []
+    for fused in (False, True):
+        mr, mrs = torch.empty((B, C, 2), device=dev), torch.empty((B, C, 2), device=dev)
+        rm, rv, rms, rvs = (torch.full((C,), v, device=dev) for v in (0.1, 1.1, -0.2, 0.9))
+        y = torch.empty_like(zg)
+        if fused:
+            nn.bn_finalize_apply_bnres(st.clone(), mr, rm, rv, zg, ga, be, sts.clone(), mrs, rms, rvs, zsg, gs, bs,
+                                       1e-3, 0.9, y, B, HW, C, 1, 1.001e-5, 0.99)
+        else:
+            s = torch.empty_like(zg)
+            nn.bn_finalize_apply(sts.clone(), mrs, rms, rvs, zsg, gs, bs, None, s, B, HW, C, 0, 1e-3, 0.9)
+            nn.bn_finalize_apply(st.clone(), mr, rm, rv, zg, ga, be, s, y, B, HW, C, 1, 1.001e-5, 0.99)
+        outs.append((y.view(torch.int16), mr, mrs, rm, rv, rms, rvs))
+    torch.cuda.synchronize()
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)
+
+
 def test_maxpool_and_upsample():
     from cvlite import ops_nn as nn
     g = torch.Generator().manual_seed(11)

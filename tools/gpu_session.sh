@@ -22,8 +22,11 @@ for s in $steps; do
     bench)   run 150 gpurun_out/${tag}_bench.err bash -c "python -u bench.py --steps 30 --runs 1 --no-cpu-baseline > gpurun_out/${tag}_bench.json"
              tail -c 300 gpurun_out/${tag}_bench.json; echo ;;
     benchi)  run 150 gpurun_out/${tag}_benchi.err bash -c "CVL_STEM_DIRECT=0 python -u bench.py --steps 30 --runs 1 --no-cpu-baseline > gpurun_out/${tag}_benchi.json"
+             tail -c 200 gpurun_out/${tag}_benchi.json; echo ;;
+    benchs)  run 150 gpurun_out/${tag}_benchs.err bash -c "CVL_NO_SC_BN_FUSE=1 python -u bench.py --steps 30 --runs 1 --no-cpu-baseline > gpurun_out/${tag}_benchs.json"
+             tail -c 200 gpurun_out/${tag}_benchs.json; echo ;;
     benchx)  run 150 gpurun_out/${tag}_benchx.err bash -c "CVL_BN_EXACT=1 python -u bench.py --steps 30 --runs 1 --no-cpu-baseline > gpurun_out/${tag}_benchx.json"
-             tail -c 200 gpurun_out/${tag}_benchd.json; echo ;;
+             tail -c 200 gpurun_out/${tag}_benchx.json; echo ;;
     table)   run 120 gpurun_out/${tag}_table.log python -u tools/conv_table.py --out gpurun_out/${tag}_conv_table.md
              head -4 gpurun_out/${tag}_conv_table.md ;;
     wgx)     run 90 gpurun_out/${tag}_wgx.md python -u tools/wgx_stamps.py ;;
