@@ -137,3 +137,57 @@ __device__ __forceinline__ void acc_store_dec(acc_u64* buf, long bc, int s, doub
   buf[acc_idx(bc, s, slots)] = (acc_u64)__double_as_longlong(v);
   if (slots == kAccSlots) buf[acc_idx(bc, s, slots) + kAccBins] = kAccDecoded;
 }
+
+// ---- BN helpers shared by the BN kernels (nn_ops.hip) and the consumers that fold a BN into their
+// operand path (conv_igemm_p.hip, conv_wgrad_x.hip): one arithmetic, so every form is bit-identical
+
+// per-image moments of one channel from its float64 (sum, sumsq); shared by the finalize kernels
+static __device__ __forceinline__ void bn_moments(double s1, double s2, int HW, float eps, float* mean, float* rstd,
+                                           double* var_out) {
+  const double m = s1 / HW;
+  double var = s2 / HW - m * m;
+  var = var > 0.0 ? var : 0.0;
+  *mean = (float)m;
+  *rstd = (float)(1.0 / sqrt(var + (double)eps));
+  *var_out = var;
+}
+
+// running-stat EMA of one channel over the images in order (TF fused BN: unbiased variance)
+static __device__ __forceinline__ void bn_running(const acc_u64* stats, int slots, int B, int C, int c, int HW, float eps,
+                                           float momentum, float* run_mean, float* run_var) {
+  float rm = run_mean[c], rv = run_var[c];
+  for (int b0 = 0; b0 < B; b0 += 8) {       // 8 images' loads in flight, then the in-order EMA
+    double s1[8], s2[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const long bc = (long)min(b0 + u, B - 1) * C + c;
+      s1[u] = acc_dec(stats, bc, 0, slots);
+      s2[u] = acc_dec(stats, bc, 1, slots);
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      if (b0 + u >= B) break;
+      float mean, rstd;
+      double var;
+      bn_moments(s1[u], s2[u], HW, eps, &mean, &rstd, &var);
+      const double uvar = HW > 1 ? var * HW / (HW - 1.0) : var;
+      rm = rm * momentum + mean * (1.f - momentum);
+      rv = rv * momentum + (float)uvar * (1.f - momentum);
+    }
+  }
+  run_mean[c] = rm;
+  run_var[c] = rv;
+}
+
+// the BN + affine output before the residual / ReLU, one explicit fma: the backward recomputes it
+// from z to rebuild the ReLU mask of non-residual units (bit-identical to the forward's value)
+static __device__ __forceinline__ float bn_affine(float z, float m, float rs, float ga, float be) {
+  return __builtin_fmaf(ga, (z - m) * rs, be);
+}
+
+// relu(bn_affine(z)) rounded to bf16 exactly as the BN apply stores it (ReLU as `o > 0 ? o : 0`:
+// -0 and NaN become +0, as there)
+static __device__ __forceinline__ float bn_relu_value(float z, float m, float rs, float ga, float be) {
+  const float o = bn_affine(z, m, rs, ga, be);
+  return o > 0.f ? o : 0.f;
+}

@@ -67,7 +67,28 @@ __device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t r, const cvl_bf16* 
                                            0, 0);
 }
 
-template <int T, int SR = BR, bool ST = false>
+typedef float wf32x2 __attribute__((ext_vector_type(2)));
+// loads the compiler does not track: issued before the prologue DMAs, so the prologue's counted
+// wait retires them (a tracked load used in the loop would make the compiler drain the ring there)
+__device__ __forceinline__ wf32x2 gload8_untracked(const void* p) {
+  wf32x2 v;
+  asm volatile("global_load_dwordx2 %0, %1, off" : "=v"(v) : "v"(p) : "memory");
+  return v;
+}
+__device__ __forceinline__ float gload4_untracked(const void* p) {
+  float v;
+  asm volatile("global_load_dword %0, %1, off" : "=v"(v) : "v"(p) : "memory");
+  return v;
+}
+constexpr int kFoldImgs = 4;              // images one workgroup's rows may span on the FOLD path
+
+// FOLD (1x1, stride 1, one segment, H*W % SR == 0): the x operand is relu(BN(z)) of the previous
+// unit (a.fold: the forward's stored (mean, rstd), gamma, beta), formed from z in registers after
+// the transposed fragment reads -- bf16(relu(fma(gamma, (z - mean) * rstd, beta))), the BN apply's
+// arithmetic, so the MFMAs see the operand the unfused form stored.  A lane's x fragment is 8 rows
+// of ONE channel (its column), so a step needs one (mean, rstd, gamma, beta) per fragment column;
+// the values for the <= kFoldImgs images of the workgroup's rows are loaded once, before the stream.
+template <int T, int SR = BR, bool ST = false, bool FOLD = false>
 __global__ void __launch_bounds__(NT) conv_wgrad_x_kernel(WxArgs g) {
   using C = WxCfg<T, SR>;
   // ST: wall-clock stamps of thread 0 (entry, prologue landed, loop done, epilogue stored)
@@ -194,10 +215,38 @@ __global__ void __launch_bounds__(NT) conv_wgrad_x_kernel(WxArgs g) {
   }
 
   constexpr int PW = 2 * J;                     // DMA pieces per wave per step
+  // FOLD parameters of this lane's TN fragment columns, images fb_lo .. fb_lo + kFoldImgs - 1
+  wf32x2 fmr[FOLD ? kFoldImgs : 1][TN];
+  float fga[TN], fbe[TN];
+  int fb_lo = 0, fhw = 1;
+  if (FOLD) {
+    fhw = a.seg[0].Hr * a.seg[0].Wr;
+    fb_lo = m_lo / fhw;
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      int kc = k0 + (wk * TN + j) * 16 + lr;
+      kc = kc < a.K ? kc : a.K - 1;
+      fga[j] = gload4_untracked(a.fold.gamma + kc);
+      fbe[j] = gload4_untracked(a.fold.beta + kc);
+#pragma unroll
+      for (int q = 0; q < kFoldImgs; ++q) {
+        const int b = min(fb_lo + q, a.B - 1);
+        fmr[q][j] = gload8_untracked(a.fold.mr + ((long)b * a.K + kc) * 2);
+      }
+    }
+  }
   issue();
   issue();
   issue();
-  wait_vm<2 * PW>();
+  wait_vm<2 * PW>();                            // (also retires the FOLD parameter loads)
+  if (FOLD) {
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      asm volatile("" : "+v"(fga[j]), "+v"(fbe[j]));
+#pragma unroll
+      for (int q = 0; q < kFoldImgs; ++q) asm volatile("" : "+v"(fmr[q][j]));
+    }
+  }
   __builtin_amdgcn_s_barrier();
   asm volatile("" ::: "memory");
   if (stamp) stamp[1] = wall_clock64();
@@ -229,6 +278,19 @@ __global__ void __launch_bounds__(NT) conv_wgrad_x_kernel(WxArgs g) {
     }
     __builtin_amdgcn_sched_barrier(0);
     __builtin_amdgcn_s_setprio(1);
+    // FOLD: this step's image (uniform; H*W % SR == 0 keeps a step inside one image)
+    float sm[TN], srs[TN];
+    if (FOLD) {
+      const int bi = (m_lo + st * SR) / fhw - fb_lo;
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        wf32x2 v = fmr[0][j];
+#pragma unroll
+        for (int q = 1; q < kFoldImgs; ++q) v = bi == q ? fmr[q][j] : v;
+        sm[j] = v.x;
+        srs[j] = v.y;
+      }
+    }
 #pragma unroll
     for (int h = 0; h < KS; ++h) {
       s16x8 fa[TM], fb[TN];
@@ -236,6 +298,13 @@ __global__ void __launch_bounds__(NT) conv_wgrad_x_kernel(WxArgs g) {
       for (int i = 0; i < TM; ++i) fa[i] = tr_join(al[h][i], ah[h][i]);
 #pragma unroll
       for (int j = 0; j < TN; ++j) fb[j] = tr_join(bl[h][j], bh[h][j]);
+      if (FOLD) {
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+#pragma unroll
+          for (int u = 0; u < 8; ++u)
+            fb[j][u] = (short)f32_to_bf16(bn_relu_value(bf16_to_f32((cvl_bf16)fb[j][u]), sm[j], srs[j], fga[j], fbe[j]));
+      }
 #pragma unroll
       for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -388,10 +457,22 @@ long cvl_conv_wgrad_x_workspace(const cvl_conv_desc* d, int ngroups) {
 
 // Returns -1 when the launch does not qualify (the caller takes another kernel), else a status.
 int cvl_conv_wgrad_x(const cvl_conv_desc* d, int ngroups, const void* x, const void* dy, float* const* dw,
-                     float beta, void* workspace, size_t workspace_bytes, hipStream_t s) {
+                     float beta, void* workspace, size_t workspace_bytes, hipStream_t s, const FoldArgs* fold = nullptr) {
   WxArgs g;
   WxPlan p;
   if (!wx_plan(d, ngroups, &g.a, &p)) return -1;
+  if (fold) {                                   // the FOLD form: 1x1, 64-row steps inside one image
+    const ConvSeg& q = g.a.seg[0];
+    const int hw = q.Hr * q.Wr;
+    if (ngroups != 1 || d->KH != 1 || d->KW != 1 || d->stride != 1 || g.a.nseg != 1 || p.T != 128 ||
+        p.SR != 64 || hw % 64 || q.src_img != (long)hw || q.Hs != q.Hr || q.Ws != q.Wr)
+      return -1;
+    for (int sp = 0; sp < p.nsplit; ++sp) {
+      const int m0 = sp * p.chunk, m1 = min(m0 + p.chunk, min(p.g_m1[0], q.rows)) - 1;
+      if (m1 >= m0 && m1 / hw - m0 / hw + 1 > kFoldImgs) return -1;
+    }
+    g.a.fold = *fold;
+  }
   if (!workspace || workspace_bytes < (p.slab > 16 ? p.slab : 16)) return CVL_EINVAL;
   static const bool stamps = cvl_env_flag("CVL_WGX_STAMPS");
   g.stamps = nullptr;
@@ -425,7 +506,9 @@ int cvl_conv_wgrad_x(const cvl_conv_desc* d, int ngroups, const void* x, const v
     if (gs) return gs;
   }
   const dim3 grid(p.tiles * p.nsplit * ngroups);
-  if (g.stamps) {
+  if (fold) {
+    hipLaunchKernelGGL((conv_wgrad_x_kernel<128, 64, false, true>), grid, dim3(NT), 0, s, g);
+  } else if (g.stamps) {
     if (p.T == 256) hipLaunchKernelGGL((conv_wgrad_x_kernel<256, BR, true>), grid, dim3(NT), 0, s, g);
     else if (p.SR == 64) hipLaunchKernelGGL((conv_wgrad_x_kernel<128, 64, true>), grid, dim3(NT), 0, s, g);
     else hipLaunchKernelGGL((conv_wgrad_x_kernel<128, BR, true>), grid, dim3(NT), 0, s, g);
@@ -452,4 +535,20 @@ extern "C" int cvl_debug_wgx_stamps(uint64_t* host, int max_wgs) {
   if (hipMemcpyFromSymbol(host, HIP_SYMBOL(g_wgx_stamps), (size_t)n * 32, 0, hipMemcpyDeviceToHost) != hipSuccess)
     return -1;
   return g_wgx_stamp_grid;
+}
+
+// The weight gradient of a 1x1 conv whose input is relu(BN(z)) of the previous unit, the BN applied
+// in the x-operand path (FOLD above) from the stored (mean, rstd); CVL_ENOTTAKEN when the X path
+// cannot take it (the caller then materialises the input and runs cvl_conv_wgrad).
+extern "C" int cvl_conv_wgrad_fold(const cvl_conv_desc* d, const void* z, const float* fold_mean_rstd,
+                                   const float* fold_gamma, const float* fold_beta, const void* dy, float* dw,
+                                   float beta, void* workspace, size_t workspace_bytes, cvl_stream_t stream) {
+  CVL_CHECK_ARG(d && z && fold_mean_rstd && fold_gamma && fold_beta && dy && dw);
+  if (d->prec != CVL_PREC_BF16) return CVL_ENOTTAKEN;
+  const int gs = cvl_wgrad_defer_guard(dw, (hipStream_t)stream);
+  if (gs) return gs;
+  FoldArgs f{nullptr, const_cast<float*>(fold_mean_rstd), nullptr, nullptr, fold_gamma, fold_beta, 0.f, 0.f, 1};
+  float* dws[1] = {dw};
+  const int st = cvl_conv_wgrad_x(d, 1, z, dy, dws, beta, workspace, workspace_bytes, (hipStream_t)stream, &f);
+  return st >= 0 ? st : CVL_ENOTTAKEN;
 }

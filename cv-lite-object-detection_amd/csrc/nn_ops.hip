@@ -241,44 +241,6 @@ __global__ void __launch_bounds__(NT) im2col_tile_kernel(const float* __restrict
 // ---------------------------------------------------------------------------------------------
 // BatchNorm (per-image statistics over H*W, Keras fused-BN semantics)
 // ---------------------------------------------------------------------------------------------
-// per-image moments of one channel from its float64 (sum, sumsq); shared by the finalize kernels
-__device__ __forceinline__ void bn_moments(double s1, double s2, int HW, float eps, float* mean, float* rstd,
-                                           double* var_out) {
-  const double m = s1 / HW;
-  double var = s2 / HW - m * m;
-  var = var > 0.0 ? var : 0.0;
-  *mean = (float)m;
-  *rstd = (float)(1.0 / sqrt(var + (double)eps));
-  *var_out = var;
-}
-
-// running-stat EMA of one channel over the images in order (TF fused BN: unbiased variance)
-__device__ __forceinline__ void bn_running(const acc_u64* stats, int slots, int B, int C, int c, int HW, float eps,
-                                           float momentum, float* run_mean, float* run_var) {
-  float rm = run_mean[c], rv = run_var[c];
-  for (int b0 = 0; b0 < B; b0 += 8) {       // 8 images' loads in flight, then the in-order EMA
-    double s1[8], s2[8];
-#pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      const long bc = (long)min(b0 + u, B - 1) * C + c;
-      s1[u] = acc_dec(stats, bc, 0, slots);
-      s2[u] = acc_dec(stats, bc, 1, slots);
-    }
-#pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      if (b0 + u >= B) break;
-      float mean, rstd;
-      double var;
-      bn_moments(s1[u], s2[u], HW, eps, &mean, &rstd, &var);
-      const double uvar = HW > 1 ? var * HW / (HW - 1.0) : var;
-      rm = rm * momentum + mean * (1.f - momentum);
-      rv = rv * momentum + (float)uvar * (1.f - momentum);
-    }
-  }
-  run_mean[c] = rm;
-  run_var[c] = rv;
-}
-
 // stats[b][c] = (sum, sumsq) accumulators -> mr[b][c] = (mean, rstd); running stats EMA, images in order.
 __global__ void bn_finalize_kernel(const acc_u64* stats, float* mr, float* run_mean, float* run_var,
                                    int B, int C, int HW, float eps, float momentum, int slots) {
@@ -312,11 +274,6 @@ struct BnFin {
 
 constexpr int BNA_UNR = 4;
 
-// the BN + affine output before the residual / ReLU, one explicit fma: the backward recomputes it
-// from z to rebuild the ReLU mask of non-residual units (bit-identical to the forward's value)
-__device__ __forceinline__ float bn_affine(float z, float m, float rs, float ga, float be) {
-  return __builtin_fmaf(ga, (z - m) * rs, be);
-}
 constexpr int BN_FIN_MAXC = 2048;
 
 // RBN: the residual is itself a BN output that was never stored -- the projection shortcut's
@@ -1329,6 +1286,9 @@ extern "C" int cvl_im2col(const float* x, int B, int H, int W, int C, int KH, in
 }
 
 extern "C" int cvl_bn_acc_slots(void) { return g_acc_slots; }
+
+// (internal) an exact-mode buffer decoded in place before a kernel outside this file reads it
+int cvl_bn_acc_prepare(uint64_t* acc, long nstat, hipStream_t s) { return acc_decode_launch((acc_u64*)acc, nstat, s); }
 
 extern "C" int cvl_bn_set_exact(int on) {
   g_acc_slots = on ? kAccSlots : 1;

@@ -357,7 +357,7 @@ def check_conv_igemm(lp, name, launch, desc, src, dst, stats=None):
         assert desc.nseg == 1 and desc.mode == 0
         s = _segs(desc)[0]
         drows = _rows(dst, desc.ld_dst)
-        got = _acc(stats - st0, desc.B, desc.n_store)        # integer bins: the difference is exact
+        got = _acc(stats, desc.B, desc.n_store) - _acc(st0, desc.B, desc.n_store)
         HW = s["Hr"] * s["Wr"]
         for b in range(desc.B):
             z = drows[s["db"] + b * s["di"]: s["db"] + b * s["di"] + HW, desc.dst_coff:desc.dst_coff + desc.n_store]
@@ -365,6 +365,55 @@ def check_conv_igemm(lp, name, launch, desc, src, dst, stats=None):
             ref = torch.stack([z.sum(0), (z * z).sum(0)], -1)
             rabs = torch.stack([z.abs().sum(0), (z * z).sum(0)], -1)
             lp.add(name, _detail(desc, s, desc.B) + " img%d" % b, "bn_stats", red_err(got[b], ref, rabs), 1e-6, kern)
+
+
+def _fold_input(z, mr, gamma, beta, B, C):
+    """relu(BN(z)) as the BN apply stores it (bf16), from the (mean, rstd) the kernel wrote."""
+    zz = z.reshape(B, -1, C)
+    mrv = mr.view(B, C, 2)
+    a, _ = bn_affine32(zz, mrv[..., 0][:, None], mrv[..., 1][:, None], gamma, beta)
+    return a.clamp_min(0).to(torch.bfloat16).reshape(z.shape)
+
+
+def check_conv_igemm_fold(lp, name, launch, desc, z, dst, stats, fold_stats, fold_mr, run_mean, run_var, gamma,
+                          beta, eps, momentum):
+    """1x1 forward with the input's BN -> ReLU finalized and applied in the operand path: the fused
+    finalize (mean / rstd / running statistics vs the statistics), then the conv and its BN
+    statistics against the input rebuilt from z with the kernel's own (mean, rstd)."""
+    rm0, rv0 = _clone(run_mean, run_var)
+    st0 = stats.clone() if stats is not None else None
+    if not launch(desc, z, dst, stats, fold_stats, fold_mr, run_mean, run_var, gamma, beta, eps, momentum):
+        return False
+    kern = lp.last_kernel()
+    HW = z.numel() // (desc.B * desc.Cin)
+    _check_finalize(lp, name, "fold C%d HW%d B%d" % (desc.Cin, HW, desc.B), fold_stats, fold_mr, rm0, rv0, run_mean,
+                    run_var, desc.B, desc.Cin, HW, eps, momentum)
+    x = _fold_input(z, fold_mr, gamma, beta, desc.B, desc.Cin)
+    _conv_check_dst(lp, name, desc, x, dst, None, kern)
+    if stats is not None:
+        s = _segs(desc)[0]
+        drows = _rows(dst, desc.ld_dst)
+        got = _acc(stats, desc.B, desc.n_store) - _acc(st0, desc.B, desc.n_store)
+        HWo = s["Hr"] * s["Wr"]
+        for b in range(desc.B):
+            zo = drows[s["db"] + b * s["di"]: s["db"] + b * s["di"] + HWo,
+                       desc.dst_coff:desc.dst_coff + desc.n_store].double()
+            ref = torch.stack([zo.sum(0), (zo * zo).sum(0)], -1)
+            rabs = torch.stack([zo.abs().sum(0), (zo * zo).sum(0)], -1)
+            lp.add(name, _detail(desc, s, desc.B) + " img%d" % b, "bn_stats", red_err(got[b], ref, rabs), 1e-6, kern)
+    return True
+
+
+def check_conv_wgrad_fold(lp, name, launch, desc, z, fold_mr, gamma, beta_bn, dy, dw, beta=0.0):
+    old = dw.clone() if beta != 0.0 else None
+    if not launch(desc, z, fold_mr, gamma, beta_bn, dy, dw, beta):
+        return False
+    kern = lp.last_kernel()
+    lp.flush_wgrad()
+    segs = _segs(desc)
+    x = _fold_input(z, fold_mr, gamma, beta_bn, desc.B, desc.Cin)
+    _check_dw(lp, name, _wgrad_detail(desc, segs) + " fold", kern, dw, old, beta, _wgrad_ref(desc, segs, x, dy))
+    return True
 
 
 def _wgrad_ref(desc, segs, x, dy):
@@ -509,7 +558,7 @@ def check_stem_conv(lp, name, launch, img, w_packed, bias, z, stats=None):
     detail = "stem 7x7/2 %dx%d B%d" % (H, W, B)
     lp.cmp(name, detail, "z", z.reshape(-1, 64), ref, "STEM", tol=TOL_BF16)
     if stats is not None:
-        got = _acc(stats - st0, B, 64)
+        got = _acc(stats, B, 64) - _acc(st0, B, 64)
         zz = z.double().reshape(B, Ho * Wo, 64)
         r = torch.stack([zz.sum(1), (zz * zz).sum(1)], -1)
         rabs = torch.stack([zz.abs().sum(1), (zz * zz).sum(1)], -1)
@@ -1171,6 +1220,8 @@ CHECKS = {
     "bn_apply": check_bn_apply,
     "bn_finalize_apply": check_bn_finalize_apply,
     "bn_finalize_apply_bnres": check_bn_finalize_apply_bnres,
+    "conv_igemm_fold": check_conv_igemm_fold,
+    "conv_wgrad_fold": check_conv_wgrad_fold,
     "bn_backward": check_bn_backward,
     "bn_backward_relu": check_bn_backward_relu,
     "bn_backward_relu6": check_bn_backward_relu6,
