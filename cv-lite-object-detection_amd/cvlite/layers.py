@@ -379,7 +379,8 @@ class ConvBN(object):
         Ho, Wo, _, _ = self.conv.out_hw(H, W)
         stats = None
         if train:
-            stats = arena.take(B, c) if arena is not None else nn.bn_acc(B, c, x.device)
+            dev = x.z.device if isinstance(x, FoldedInput) else x.device
+            stats = arena.take(B, c) if arena is not None else nn.bn_acc(B, c, dev)
         if isinstance(x, FoldedInput):        # the input's BN -> ReLU is applied in this conv's operand path
             z, x = self.conv.fwd_folded(x, B, H, W, stats=stats)
         else:

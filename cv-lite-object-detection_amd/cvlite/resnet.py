@@ -23,8 +23,11 @@ FUSE_POOL = os.environ.get("CVL_STEM_NO_FUSE_POOL", "0") != "1"
 DIRECT_STEM = os.environ.get("CVL_STEM_DIRECT", "1") == "1"
 # projection shortcut's BN applied inside conv3's BN launch (CVL_NO_SC_BN_FUSE=1: stored and re-read)
 FUSE_SC_BN = os.environ.get("CVL_NO_SC_BN_FUSE", "0") != "1"
-# conv2's BN -> ReLU folded into conv3's operand path (CVL_NO_BN_FOLD=1: stored and re-read)
-FOLD_BN2 = os.environ.get("CVL_NO_BN_FOLD", "0") != "1"
+# conv2's BN -> ReLU folded into conv3's operand path (opt-in, CVL_BN_FOLD=1).  Measured (FCOS bs 16,
+# round 4): 1143 img/s folded vs 1170 stored -- every N-tile workgroup (and both wave columns of one)
+# re-forms the same A fragments, ~15 VALU per element, which costs more than the apply pass it saves
+# (conv3 at conv5_x: 32 N tiles, 59.7 vs 21.6 us forward); see DESIGN.md section 3.
+FOLD_BN2 = os.environ.get("CVL_BN_FOLD", "0") == "1"
 STEM_KP = 168 if DIRECT_STEM else 192
 
 

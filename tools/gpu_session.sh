@@ -25,7 +25,7 @@ for s in $steps; do
              tail -c 200 gpurun_out/${tag}_benchi.json; echo ;;
     benchs)  run 150 gpurun_out/${tag}_benchs.err bash -c "CVL_NO_SC_BN_FUSE=1 python -u bench.py --steps 30 --runs 1 --no-cpu-baseline > gpurun_out/${tag}_benchs.json"
              tail -c 200 gpurun_out/${tag}_benchs.json; echo ;;
-    benchf)  run 150 gpurun_out/${tag}_benchf.err bash -c "CVL_NO_BN_FOLD=1 python -u bench.py --steps 30 --runs 1 --no-cpu-baseline > gpurun_out/${tag}_benchf.json"
+    benchf)  run 150 gpurun_out/${tag}_benchf.err bash -c "CVL_BN_FOLD=1 python -u bench.py --steps 30 --runs 1 --no-cpu-baseline > gpurun_out/${tag}_benchf.json"
              tail -c 200 gpurun_out/${tag}_benchf.json; echo ;;
     benchx)  run 150 gpurun_out/${tag}_benchx.err bash -c "CVL_BN_EXACT=1 python -u bench.py --steps 30 --runs 1 --no-cpu-baseline > gpurun_out/${tag}_benchx.json"
              tail -c 200 gpurun_out/${tag}_benchx.json; echo ;;
