@@ -34,18 +34,9 @@ __device__ __forceinline__ s16x8 relu_bf16x8(s16x8 v) {
   return v;
 }
 
-// 16 zero bytes: the LDS-DMA source of padding taps / rows past the end of a segment
-__device__ __attribute__((aligned(16))) cvl_bf16 g_zero16[8];
 
-__device__ __forceinline__ void glds16(const void* g, void* l) {
-  __builtin_amdgcn_global_load_lds((const void __attribute__((address_space(1)))*)g,
-                                   (void __attribute__((address_space(3)))*)l, 16, 0, 0);
-}
 
-// GLDS: operands go global->LDS by LDS-DMA (global_load_lds_dwordx4: no VGPR staging, no
-// ds_write), double-buffered so the next K step's DMA overlaps this step's MFMAs; the XOR swizzle
-// moves to the per-lane source address (each wave-instruction writes 1 KiB lane-linearly).
-template <int BN, int BK, bool DGRAD, bool GLDS>
+template <int BN, int BK, bool DGRAD>
 __global__ void __launch_bounds__(NT) conv_igemm_kernel(ConvArgs a) {
   constexpr int WM = BM / 2, WN = BN / 2;
   constexpr int TM = WM / 16, TN = WN / 16;
@@ -54,8 +45,7 @@ __global__ void __launch_bounds__(NT) conv_igemm_kernel(ConvArgs a) {
   constexpr int AP = BM / RPP;
   constexpr int BROWS = BN < RPP ? BN : RPP;
   constexpr int BP = BN / BROWS;
-  constexpr int NBUF = GLDS ? 2 : 1;
-  constexpr int LDS_AB = NBUF * (BM + BN) * BK;
+  constexpr int LDS_AB = (BM + BN) * BK;
   constexpr int LDS_C = BM * (BN + 8);
   constexpr int LDS_EL = LDS_AB > LDS_C ? LDS_AB : LDS_C;
   __shared__ __attribute__((aligned(16))) cvl_bf16 lds[LDS_EL];
@@ -125,42 +115,6 @@ __global__ void __launch_bounds__(NT) conv_igemm_kernel(ConvArgs a) {
         rb[p] = *reinterpret_cast<const s16x8*>(wsrc + (long)n * a.K + k0 + ch * 8);
     }
   };
-  // LDS-DMA form of load_tile + store_tile: lane (rr, ch) of the lane-linear image holds global
-  // chunk ch ^ swz(row), so the fragment reads below are unchanged
-  auto glds_tile = [&](int kt, int buf) {
-    cvl_bf16* Ab = lds + buf * (BM + BN) * BK;
-    cvl_bf16* Bb = Ab + BM * BK;
-    const int k0 = kt * BK;
-    const int tap = k0 / Cin;
-    const int cb = k0 - tap * Cin;
-    const int r = tap / a.KW, s = tap - (tap / a.KW) * a.KW;
-    const int wbase = (tid >> 6) * (64 / CPR);    // first row of this wave's 1 KiB piece
-#pragma unroll
-    for (int p = 0; p < AP; ++p) {
-      int iy, ix;
-      bool ok = a_ok[p];
-      if (DGRAD) {
-        const int ty = a_y[p] - r, tx = a_x[p] - s;
-        ok = ok && ty >= 0 && tx >= 0 && (ty % a.stride) == 0 && (tx % a.stride) == 0;
-        iy = ty / a.stride; ix = tx / a.stride;
-      } else {
-        iy = a_y[p] + r; ix = a_x[p] + s;
-      }
-      ok = ok && iy >= 0 && ix >= 0 && iy < S.Hs && ix < S.Ws;
-      const int row = p * RPP + rr;
-      const cvl_bf16* g = g_zero16;
-      if (ok) {
-        const long grow = S.src_base + (long)a_img[p] * S.src_img + (long)iy * S.Ws + ix;
-        g = src + grow * Cin + cb + ((ch ^ swz<BK>(row)) * 8);
-      }
-      glds16(g, Ab + (p * RPP + wbase) * BK);
-    }
-#pragma unroll
-    for (int p = 0; p < BP; ++p) {
-      const int row = p * BROWS + tid / CPR;
-      glds16(wsrc + (long)(n0 + row) * a.K + k0 + ((ch ^ swz<BK>(row)) * 8), Bb + (p * BROWS + wbase) * BK);
-    }
-  };
   auto store_tile = [&]() {
 #pragma unroll
     for (int p = 0; p < AP; ++p) {
@@ -190,24 +144,14 @@ __global__ void __launch_bounds__(NT) conv_igemm_kernel(ConvArgs a) {
     kt1 = min(kt1, kt0 + a.ksteps_per_split);
   }
   const int nk = kt1;
-  if (GLDS) glds_tile(kt0, 0);
-  else load_tile(kt0);
+  load_tile(kt0);
   for (int kt = kt0; kt < nk; ++kt) {
     const cvl_bf16* Ac = As;
     const cvl_bf16* Bc = Bs;
-    if (GLDS) {
-      const int buf = (kt - kt0) & 1;
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();                          // step kt landed; buffer buf^1 no longer read
-      if (kt + 1 < nk) glds_tile(kt + 1, buf ^ 1);
-      Ac = lds + buf * (BM + BN) * BK;
-      Bc = Ac + BM * BK;
-    } else {
-      __syncthreads();
-      store_tile();
-      __syncthreads();
-      if (kt + 1 < nk) load_tile(kt + 1);
-    }
+    __syncthreads();
+    store_tile();
+    __syncthreads();
+    if (kt + 1 < nk) load_tile(kt + 1);
 #pragma unroll
     for (int ks = 0; ks < BK / 32; ++ks) {
       const int chunk = ks * 4 + lg;
@@ -483,15 +427,8 @@ int launch_bn_bk(const ConvArgs& a0, bool dgrad, hipStream_t s) {
     a.splits = (nk + a.ksteps_per_split - 1) / a.ksteps_per_split;
   }
   dim3 grid(a.m_tiles, a.Npad / BN, a.splits);
-  // LDS-DMA staging measured no faster than register staging at this tile (2 blocks/CU): opt-in
-  const bool glds = BK == 64 && !a.relu_in && cvl_env_flag("CVL_CONV_GLDS");
-  if (glds) {
-    if (dgrad) hipLaunchKernelGGL((conv_igemm_kernel<BN, BK, true, true>), grid, dim3(NT), 0, s, a);
-    else hipLaunchKernelGGL((conv_igemm_kernel<BN, BK, false, true>), grid, dim3(NT), 0, s, a);
-  } else {
-    if (dgrad) hipLaunchKernelGGL((conv_igemm_kernel<BN, BK, true, false>), grid, dim3(NT), 0, s, a);
-    else hipLaunchKernelGGL((conv_igemm_kernel<BN, BK, false, false>), grid, dim3(NT), 0, s, a);
-  }
+  if (dgrad) hipLaunchKernelGGL((conv_igemm_kernel<BN, BK, true>), grid, dim3(NT), 0, s, a);
+  else hipLaunchKernelGGL((conv_igemm_kernel<BN, BK, false>), grid, dim3(NT), 0, s, a);
   int st = cvl_launch_status();
   if (st || a.splits <= 1) return st;
   return splitk_finish_launch(a, s);

@@ -17,7 +17,7 @@ static inline int cvl_launch_status() {
   return e == hipSuccess ? CVL_OK : (CVL_EHIP + (int)e);
 }
 
-// Kernel-variant switches for A/B measurement (e.g. CVL_CONV_GLDS=1); read per launch.
+// Kernel-variant switches for A/B measurement (e.g. CVL_CONV_NO_P=1); read per launch.
 static inline bool cvl_env_flag(const char* name) {
   const char* v = getenv(name);
   return v && v[0] && v[0] != '0';

@@ -33,8 +33,8 @@ constexpr int RL = 1560;                 // ring row (bf16): (2 * SPX + 6) * 3 =
 constexpr int NRING = 12;                // ring rows (7 in use + 2 prefetched + slack)
 constexpr int KR = 168, KP = 192;        // real (7 x 24) and MFMA-padded K
 constexpr int WA = 200;                  // LDS pitch (elements) of the weight rows (forward)
-constexpr int DP = SPX + 8;              // LDS pitch (elements) of dz^T rows (weight gradient)
 constexpr int CO = 64;
+constexpr int DZP = CO + 8;              // LDS pitch (elements) of the dz row image [px][co] (weight gradient)
 constexpr int RPW_F = 8, RPW_W = 16;     // output rows per workgroup (forward / weight gradient)
 constexpr int RPT = (RL + NT - 1) / NT;  // ring values per thread per image row
 
@@ -89,6 +89,15 @@ __device__ __forceinline__ void row_store(cvl_bf16* ring, int iy, const float (&
   }
 }
 
+// the unit's first 7 image rows into the ring, all loads in flight at once (one latency, not 7)
+__device__ __forceinline__ void ring_prologue(const StemArgs& g, const Unit& t, cvl_bf16* ring) {
+  float v[7][RPT];
+#pragma unroll
+  for (int r = 0; r < 7; ++r) row_load(g, t, 2 * t.oy0 - 3 + r, v[r]);
+#pragma unroll
+  for (int r = 0; r < 7; ++r) row_store(ring, 2 * t.oy0 - 3 + r, v[r]);
+}
+
 // 8 consecutive ring values (16 B at a 4-B aligned address) as an MFMA fragment
 __device__ __forceinline__ s16x8 ring8(const cvl_bf16* p) {
   const unsigned* u = reinterpret_cast<const unsigned*>(p);
@@ -122,13 +131,7 @@ __global__ void __launch_bounds__(NT, 2) stem_fwd_kernel(StemArgs g) {
   }
   for (int i = tid; i < NRING * RL / 8; i += NT) reinterpret_cast<s16x8*>(ring)[i] = s16x8{0, 0, 0, 0, 0, 0, 0, 0};
   __syncthreads();
-  {
-    float v[RPT];
-    for (int iy = 2 * t.oy0 - 3; iy <= 2 * t.oy0 + 3; ++iy) {
-      row_load(g, t, iy, v);
-      row_store(ring, iy, v);
-    }
-  }
+  ring_prologue(g, t, ring);
   __syncthreads();
 
   const int wave = tid >> 6, lane = tid & 63, lr = lane & 15, lg = lane >> 4;
@@ -227,7 +230,7 @@ __global__ void __launch_bounds__(NT, 2) stem_fwd_kernel(StemArgs g) {
 // ---------------------------------------------------------------------------------------------
 __global__ void __launch_bounds__(NT) stem_wgrad_kernel(StemArgs g) {
   __shared__ __attribute__((aligned(16))) cvl_bf16 ring[NRING * RL];
-  __shared__ __attribute__((aligned(16))) cvl_bf16 dzt[CO * DP];
+  __shared__ __attribute__((aligned(16))) cvl_bf16 dzl[SPX * DZP];
   const int tid = threadIdx.x;
   const int wave = tid >> 6, lane = tid & 63, lr = lane & 15, lg = lane >> 4;
   const Unit t = unit_of(g, blockIdx.x);
@@ -249,13 +252,7 @@ __global__ void __launch_bounds__(NT) stem_wgrad_kernel(StemArgs g) {
   if (t.oy0 < g.Ho) {
     for (int i = tid; i < NRING * RL / 8; i += NT) reinterpret_cast<s16x8*>(ring)[i] = s16x8{0, 0, 0, 0, 0, 0, 0, 0};
     __syncthreads();
-    {
-      float v[RPT];
-      for (int iy = 2 * t.oy0 - 3; iy <= 2 * t.oy0 + 3; ++iy) {
-        row_load(g, t, iy, v);
-        row_store(ring, iy, v);
-      }
-    }
+    ring_prologue(g, t, ring);
     // dz row -> registers: thread owns 8 chunks (pixel, 8 channels) of the 256 x 64 row
     auto dz_load = [&](int oy, s16x8 (&d)[8]) {
       const cvl_bf16* zr = g.dz + ((long)(t.b * g.Ho + oy) * g.Wo + t.x0) * CO;
@@ -267,13 +264,16 @@ __global__ void __launch_bounds__(NT) stem_wgrad_kernel(StemArgs g) {
     };
     s16x8 dcur[8];
     dz_load(t.oy0, dcur);
+    // A fragments dz^T[co][px] by transposed reads of the row image [px][co]: rows p0 + 8*lg + q4
+    // (+ 4), column chunk i*16 + 4*pp (the conv_wgrad_x dY pattern; padded pitch, no swizzle)
+    const int q4 = lr >> 2, pp = lr & 3;
+    const unsigned dz0 = lds_addr(dzl);
     for (int oy = t.oy0; oy < t.oy1; ++oy) {
       __syncthreads();                              // the previous row's fragment reads are done
 #pragma unroll
       for (int q = 0; q < 8; ++q) {
         const int idx = tid + q * NT, px = idx >> 3, c8 = (idx & 7) * 8;
-#pragma unroll
-        for (int u = 0; u < 8; ++u) dzt[(c8 + u) * DP + px] = (cvl_bf16)dcur[q][u];
+        *reinterpret_cast<s16x8*>(dzl + px * DZP + c8) = dcur[q];
       }
       const bool more = oy + 1 < t.oy1;
       float n0[RPT], n1[RPT];
@@ -287,9 +287,14 @@ __global__ void __launch_bounds__(NT) stem_wgrad_kernel(StemArgs g) {
 #pragma unroll 2
       for (int s = 0; s < SPX / 32; ++s) {
         const int p0 = s * 32 + lg * 8;
-        s16x8 fa[4], fb[3];
+        s16x4 al[4], ah[4];
+        s16x8 fb[3];
+        const unsigned rlo = dz0 + 2 * ((s * 32 + 8 * lg + q4) * DZP + 4 * pp);
 #pragma unroll
-        for (int i = 0; i < 4; ++i) fa[i] = *reinterpret_cast<const s16x8*>(dzt + (i * 16 + lr) * DP + p0);
+        for (int i = 0; i < 4; ++i) {
+          al[i] = ds_tr16(rlo + 2 * (i * 16));
+          ah[i] = ds_tr16(rlo + 2 * (4 * DZP + i * 16));
+        }
 #pragma unroll
         for (int j = 0; j < 3; ++j) {
           const cvl_bf16* rr = ring + ((2 * oy + kyj[j]) % NRING) * RL + offj[j] + 6 * p0;
@@ -297,6 +302,14 @@ __global__ void __launch_bounds__(NT) stem_wgrad_kernel(StemArgs g) {
 #pragma unroll
           for (int q = 0; q < 8; ++q) v[q] = kv[j] ? (short)rr[6 * q] : (short)0;
           fb[j] = v;
+        }
+        lgkm_wait();
+        s16x8 fa[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          tr_pin(al[i]);
+          tr_pin(ah[i]);
+          fa[i] = tr_join(al[i], ah[i]);
         }
 #pragma unroll
         for (int i = 0; i < 4; ++i)
