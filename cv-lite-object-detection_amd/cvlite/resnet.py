@@ -18,9 +18,6 @@ from .layers import BF16, BatchNorm, Conv, ConvBN, StatsArena
 STEM_K = 7
 # the stem's BN -> ReLU -> max-pool as one pass from z (CVL_STEM_NO_FUSE_POOL=1: BN apply + pool)
 FUSE_POOL = os.environ.get("CVL_STEM_NO_FUSE_POOL", "0") != "1"
-# stem form: im2col + 1x1 GEMM (K = 147 padded to 192, the LDS-DMA kernels' K-tiles) or, with
-# CVL_STEM_DIRECT=1, cvl_stem_conv7x7s2 / cvl_stem_wgrad straight from the image (K = 7 x 24)
-DIRECT_STEM = os.environ.get("CVL_STEM_DIRECT", "1") == "1"
 # projection shortcut's BN applied inside conv3's BN launch (CVL_NO_SC_BN_FUSE=1: stored and re-read)
 FUSE_SC_BN = os.environ.get("CVL_NO_SC_BN_FUSE", "0") != "1"
 # conv2's BN -> ReLU folded into conv3's operand path (opt-in, CVL_BN_FOLD=1).  Measured (FCOS bs 16,
@@ -28,12 +25,13 @@ FUSE_SC_BN = os.environ.get("CVL_NO_SC_BN_FUSE", "0") != "1"
 # re-forms the same A fragments, ~15 VALU per element, which costs more than the apply pass it saves
 # (conv3 at conv5_x: 32 N tiles, 59.7 vs 21.6 us forward); see DESIGN.md section 3.
 FOLD_BN2 = os.environ.get("CVL_BN_FOLD", "0") == "1"
-STEM_KP = 168 if DIRECT_STEM else 192
+STEM_KP = 168            # the stem kernels' K: 7 kernel rows x (7 x 3 values padded to 24)
 
 
 class Stem(object):
-    """conv1_conv (7x7/2 after ZeroPadding2D(3)) as im2col + 1x1 MFMA GEMM or straight from the image
-    (DIRECT_STEM: cvl_stem_conv7x7s2 / cvl_stem_wgrad), conv1_bn, ReLU, pool1."""
+    """conv1_conv (7x7/2 after ZeroPadding2D(3)) straight from the image (cvl_stem_conv7x7s2 /
+    cvl_stem_wgrad; round 4: 1.3 % faster per FCOS step than the im2col + GEMM form it replaced, whose
+    403 MB patch matrix was written once and read twice), conv1_bn, ReLU, pool1."""
 
     def __init__(self, store):
         self.conv = Conv(store, "conv1_conv", STEM_K, 3, 64, stride=2, pad=3, bias=True, dgrad=False,
@@ -51,9 +49,7 @@ class Stem(object):
             return (c.w, 49, 3, 64, 3, 64, c.wf, 0, 0, None)
         if c.wf is None:
             c.wf = torch.empty((64, STEM_KP), dtype=BF16, device=c.store.flat.device)
-        if DIRECT_STEM:
-            return (c.w, 7, 21, 64, 24, 64, c.wf, 0, 0, None)
-        return (c.w, 1, 147, 64, STEM_KP, 64, c.wf, 0, 0, None)     # HWIO == [1][1][147][64]
+        return (c.w, 7, 21, 64, 24, 64, c.wf, 0, 0, None)
 
     def _desc7(self, B, H, W, Ho, Wo):
         """fp32 parity mode: conv1 as a direct 7x7/2 conv (ZeroPadding2D(3) = explicit pad 3)."""
@@ -65,14 +61,8 @@ class Stem(object):
         self.pack_entry()
         if c.store.act != BF16:
             nn.pack_conv_weights(c.w, 7, 7, 3, 64, 3, 64, c.wf)
-        elif DIRECT_STEM:
-            nn.pack_conv_weights(c.w, 7, 1, 21, 64, 24, 64, c.wf)
         else:
-            nn.pack_conv_weights(c.w, 1, 1, 147, 64, STEM_KP, 64, c.wf)
-
-    def _desc(self, B, Ho, Wo):
-        return nn.make_desc(nn.FWD, B, STEM_KP, 1, 1, 1, 0, 0, 64, 64, 64,
-                            [nn.seg(Ho, Wo, Ho, Wo, self.conv.wf, self.conv.b)])
+            nn.pack_conv_weights(c.w, 7, 1, 21, 64, 24, 64, c.wf)
 
     def forward(self, x, train=True, arena=None):
         B, H, W, _ = x.shape
@@ -83,12 +73,8 @@ class Stem(object):
             stats = arena.take(B, 64) if arena is not None else nn.bn_acc(B, 64, x.device)
         z = torch.empty((B, Ho, Wo, 64), dtype=act, device=x.device)
         A = x                                       # the fp32 image (the weight gradient reads it)
-        if act == BF16 and DIRECT_STEM:
+        if act == BF16:
             nn.stem_conv7x7s2(x, self.conv.wf, self.conv.b, z, stats)
-        elif act == BF16:
-            A = torch.empty((B * Ho * Wo, STEM_KP), dtype=BF16, device=x.device)
-            nn.im2col(x, STEM_K, STEM_K, 2, pt, pl, Ho, Wo, STEM_KP, A)
-            nn.conv_igemm(self._desc(B, Ho, Wo), A, z, stats)
         else:
             nn.conv_igemm(self._desc7(B, H, W, Ho, Wo), x, z, stats)
         Hp, Wp = (Ho + 2 - 3) // 2 + 1, (Wo + 2 - 3) // 2 + 1
@@ -120,16 +106,10 @@ class Stem(object):
         if z.dtype != BF16:                         # fp32 parity mode: 7x7 weight gradient in place
             nn.conv_wgrad(self._desc7(B, A.shape[1], A.shape[2], Ho, Wo), A, dz, self.conv.dw)
             return
-        if DIRECT_STEM:
-            dw = torch.empty((192, 64), dtype=torch.float32, device=dp.device)    # rows ky*24 + kx*3 + c
-            nn.stem_wgrad(A, dz, dw)
-            nn.wgrad_flush()                         # dw is read right away (deferred reductions)
-            self.conv.dw.view(7, 21, 64).copy_(dw.view(8, 24, 64)[:7, :21])
-            return
-        dw = torch.empty((STEM_KP, 64), dtype=torch.float32, device=dp.device)
-        nn.conv_wgrad(self._desc(B, Ho, Wo), A, dz, dw)
+        dw = torch.empty((192, 64), dtype=torch.float32, device=dp.device)    # rows ky*24 + kx*3 + c
+        nn.stem_wgrad(A, dz, dw)
         nn.wgrad_flush()                             # dw is read right away (deferred reductions)
-        self.conv.dw.view(147, 64).copy_(dw[:147])
+        self.conv.dw.view(7, 21, 64).copy_(dw.view(8, 24, 64)[:7, :21])
 
 
 class Bottleneck(object):

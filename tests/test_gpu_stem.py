@@ -68,16 +68,13 @@ def test_stem_forward_and_weight_gradient(B, H, W):
     assert torch.equal(dw2, dw3)
 
 
-def test_stem_module_matches_direct_conv(monkeypatch):
+def test_stem_module_matches_direct_conv():
     """resnet.Stem forward / backward on the new kernels: z equals a direct 7x7/2 conv of the image
     (float64 on the bf16 operands), and conv1_conv's HWIO gradient is the padded-order result mapped
     back (rows ky*21 + kx*3 + c)."""
     import torch.nn.functional as F
-    from cvlite import resnet
     from cvlite.layers import ParamStore
     from cvlite.resnet import Stem
-    monkeypatch.setattr(resnet, "DIRECT_STEM", True)
-    monkeypatch.setattr(resnet, "STEM_KP", 168)
     st = ParamStore()
     stem = Stem(st)
     st.finalize(torch.device("cuda", 0), seed=3)

@@ -21,8 +21,6 @@ for s in $steps; do
              tail -4 gpurun_out/${tag}_pytest.log ;;
     bench)   run 150 gpurun_out/${tag}_bench.err bash -c "python -u bench.py --steps 30 --runs 1 --no-cpu-baseline > gpurun_out/${tag}_bench.json"
              tail -c 300 gpurun_out/${tag}_bench.json; echo ;;
-    benchi)  run 150 gpurun_out/${tag}_benchi.err bash -c "CVL_STEM_DIRECT=0 python -u bench.py --steps 30 --runs 1 --no-cpu-baseline > gpurun_out/${tag}_benchi.json"
-             tail -c 200 gpurun_out/${tag}_benchi.json; echo ;;
     benchs)  run 150 gpurun_out/${tag}_benchs.err bash -c "CVL_NO_SC_BN_FUSE=1 python -u bench.py --steps 30 --runs 1 --no-cpu-baseline > gpurun_out/${tag}_benchs.json"
              tail -c 200 gpurun_out/${tag}_benchs.json; echo ;;
     benchf)  run 150 gpurun_out/${tag}_benchf.err bash -c "CVL_BN_FOLD=1 python -u bench.py --steps 30 --runs 1 --no-cpu-baseline > gpurun_out/${tag}_benchf.json"
