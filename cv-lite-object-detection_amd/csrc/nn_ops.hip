@@ -729,6 +729,75 @@ __global__ void bn_relu_maxpool_kernel(const cvl_bf16* z, const float* __restric
   }
 }
 
+// The same for the stem's 64 channels, tiled: a workgroup forms relu(BN(z)) of a 9 x 33-pixel input
+// tile ONCE into LDS (bf16, padding taps 0) and pools its 4 x 16 outputs from there -- the per-tap
+// form above normalised every input pixel 2.25 times and issued nine global loads per output.
+constexpr int PTY = 4, PTX = 16, PIY = 2 * PTY + 1, PIX = 2 * PTX + 1;
+__global__ void __launch_bounds__(NT) bn_relu_maxpool64_kernel(const cvl_bf16* __restrict__ z,
+                                                               const float* __restrict__ mr,
+                                                               const float* __restrict__ gamma,
+                                                               const float* __restrict__ beta, cvl_bf16* y,
+                                                               uint8_t* arg, int H, int W, int Ho, int Wo) {
+  constexpr int C = 64;
+  __shared__ s16x8 tile[PIY * PIX * 8];
+  const int tx_n = (Wo + PTX - 1) / PTX, ty_n = (Ho + PTY - 1) / PTY;
+  const int b = blockIdx.x / (tx_n * ty_n);
+  const int r = blockIdx.x - b * tx_n * ty_n;
+  const int oy0 = (r / tx_n) * PTY, ox0 = (r - (r / tx_n) * tx_n) * PTX;
+  const int iy0 = 2 * oy0 - 1, ix0 = 2 * ox0 - 1;
+  const int c8 = threadIdx.x & 7, c0 = c8 * 8;
+  float m[8], rs[8], ga[8], be[8];
+#pragma unroll
+  for (int u = 0; u < 8; ++u) {
+    const long bc = (long)b * C + c0 + u;
+    m[u] = mr[bc * 2];
+    rs[u] = mr[bc * 2 + 1];
+    ga[u] = gamma[c0 + u];
+    be[u] = beta[c0 + u];
+  }
+  for (int p = threadIdx.x >> 3; p < PIY * PIX; p += NT / 8) {
+    const int ly = p / PIX, lx = p - (p / PIX) * PIX;
+    const int iy = iy0 + ly, ix = ix0 + lx;
+    s16x8 o = s16x8{0, 0, 0, 0, 0, 0, 0, 0};
+    if ((unsigned)iy < (unsigned)H && (unsigned)ix < (unsigned)W) {
+      float v[8];
+      unpack8(*reinterpret_cast<const s16x8*>(z + (((long)b * H + iy) * W + ix) * C + c0), v);
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const float a = bn_affine(v[u], m[u], rs[u], ga[u], be[u]);
+        v[u] = a > 0.f ? a : 0.f;
+      }
+      o = pack8(v);                                  // the bf16 value the BN output would hold
+    }
+    tile[p * 8 + c8] = o;
+  }
+  __syncthreads();
+  for (int q = threadIdx.x >> 3; q < PTY * PTX; q += NT / 8) {
+    const int qy = q / PTX, qx = q - (q / PTX) * PTX;
+    const int oy = oy0 + qy, ox = ox0 + qx;
+    if (oy >= Ho || ox >= Wo) continue;
+    float best[8];
+    unsigned long long bi = 0;
+#pragma unroll
+    for (int u = 0; u < 8; ++u) best[u] = -INFINITY;
+#pragma unroll
+    for (int t = 0; t < 9; ++t) {
+      float v[8];
+      unpack8(tile[((2 * qy + t / 3) * PIX + 2 * qx + t % 3) * 8 + c8], v);
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        if (v[u] > best[u]) {
+          best[u] = v[u];
+          bi = (bi & ~(0xffull << (8 * u))) | ((unsigned long long)t << (8 * u));
+        }
+      }
+    }
+    const long pix = ((long)b * Ho + oy) * Wo + ox;
+    *reinterpret_cast<s16x8*>(y + pix * C + c0) = pack8(best);
+    *reinterpret_cast<unsigned long long*>(arg + pix * C + c0) = bi;
+  }
+}
+
 // a thread owns 8 channels of one input pixel: the (at most 2 x 2) windows holding it are visited
 // with their dy and argmax bytes (one 8-byte load) loaded together
 __global__ void maxpool_bwd_kernel(const cvl_bf16* dy, const uint8_t* arg, cvl_bf16* dx, int B, int H,
@@ -766,6 +835,57 @@ __global__ void maxpool_bwd_kernel(const cvl_bf16* dy, const uint8_t* arg, cvl_b
         if (ok[k] && ((am[k] >> (8 * u)) & 0xff) == t) acc[u] += gv[u];
     }
     *reinterpret_cast<s16x8*>(dx + pix * C + c0) = pack8(acc);
+  }
+}
+
+// maxpool_bwd for 64 channels, tiled: a workgroup stages the dy and argmax of the 5 x 17 windows
+// that touch its 8 x 32 input pixels in LDS once (the per-pixel form above loaded up to four windows'
+// dy + argmax per input pixel), then forms dx in the same window order.
+constexpr int BTY = 8, BTX = 32, BOY = BTY / 2 + 1, BOX = BTX / 2 + 1;
+__global__ void __launch_bounds__(NT) maxpool_bwd64_kernel(const cvl_bf16* __restrict__ dy,
+                                                           const uint8_t* __restrict__ arg, cvl_bf16* dx, int H,
+                                                           int W, int Ho, int Wo) {
+  constexpr int C = 64;
+  __shared__ s16x8 sg[BOY * BOX * 8];
+  __shared__ unsigned long long sa[BOY * BOX * 8];
+  const int tx_n = (W + BTX - 1) / BTX, ty_n = (H + BTY - 1) / BTY;
+  const int b = blockIdx.x / (tx_n * ty_n);
+  const int r = blockIdx.x - b * tx_n * ty_n;
+  const int iy0 = (r / tx_n) * BTY, ix0 = (r - (r / tx_n) * tx_n) * BTX;
+  const int oy0 = iy0 >> 1, ox0 = ix0 >> 1;          // windows oy0 .. oy0 + BOY - 1 (clipped)
+  const int c8 = threadIdx.x & 7, c0 = c8 * 8;
+  for (int p = threadIdx.x >> 3; p < BOY * BOX; p += NT / 8) {
+    const int oy = oy0 + p / BOX, ox = ox0 + (p - (p / BOX) * BOX);
+    s16x8 gv = s16x8{0, 0, 0, 0, 0, 0, 0, 0};
+    unsigned long long av = ~0ull;                   // (no window: no tap index matches)
+    if (oy < Ho && ox < Wo) {
+      const long o = (((long)b * Ho + oy) * Wo + ox) * C + c0;
+      gv = *reinterpret_cast<const s16x8*>(dy + o);
+      av = *reinterpret_cast<const unsigned long long*>(arg + o);
+    }
+    sg[p * 8 + c8] = gv;
+    sa[p * 8 + c8] = av;
+  }
+  __syncthreads();
+  for (int q = threadIdx.x >> 3; q < BTY * BTX; q += NT / 8) {
+    const int iy = iy0 + q / BTX, ix = ix0 + (q - (q / BTX) * BTX);
+    if (iy >= H || ix >= W) continue;
+    const int wy0 = iy >> 1, wx0 = ix >> 1;
+    float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {       // window order (oy, ox) row-major, as maxpool_bwd_kernel
+      const int oy = wy0 + (k >> 1), ox = wx0 + (k & 1);
+      if (oy > ((iy + 1) >> 1) || ox > ((ix + 1) >> 1)) continue;
+      const int p = (oy - oy0) * BOX + (ox - ox0);
+      const unsigned t = (unsigned)((iy - (oy * 2 - 1)) * 3 + (ix - (ox * 2 - 1)));
+      const unsigned long long am = sa[p * 8 + c8];
+      float gv[8];
+      unpack8(sg[p * 8 + c8], gv);
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+        if (((am >> (8 * u)) & 0xff) == t) acc[u] += gv[u];
+    }
+    *reinterpret_cast<s16x8*>(dx + (((long)b * H + iy) * W + ix) * C + c0) = pack8(acc);
   }
 }
 
@@ -1470,6 +1590,13 @@ extern "C" int cvl_bn_relu_maxpool3x3s2(const void* z, const float* mean_rstd, c
                                         void* y, uint8_t* argmax, int B, int H, int W, int C, cvl_stream_t stream) {
   CVL_CHECK_ARG(z && mean_rstd && gamma && beta && y && argmax && C % 8 == 0 && B > 0);
   const int Ho = (H + 2 - 3) / 2 + 1, Wo = (W + 2 - 3) / 2 + 1;
+  if (C == 64) {
+    const long blocks = (long)B * ((Ho + PTY - 1) / PTY) * ((Wo + PTX - 1) / PTX);
+    CVL_CHECK_ARG(blocks < (1l << 31));
+    hipLaunchKernelGGL(bn_relu_maxpool64_kernel, dim3((unsigned)blocks), dim3(NT), 0, S_, (const cvl_bf16*)z,
+                       mean_rstd, gamma, beta, (cvl_bf16*)y, argmax, H, W, Ho, Wo);
+    return cvl_launch_status();
+  }
   const long total = (long)B * Ho * Wo * (C / 8);
   hipLaunchKernelGGL(bn_relu_maxpool_kernel, dim3(grid_for(total)), dim3(NT), 0, S_, (const cvl_bf16*)z, mean_rstd,
                      gamma, beta, (cvl_bf16*)y, argmax, B, H, W, C, Ho, Wo);
@@ -1490,6 +1617,13 @@ extern "C" int cvl_maxpool3x3s2_backward(const void* dy, const uint8_t* argmax, 
                                          int W, int C, cvl_stream_t stream) {
   CVL_CHECK_ARG(dy && dx && argmax && C % 8 == 0);
   const int Ho = (H + 2 - 3) / 2 + 1, Wo = (W + 2 - 3) / 2 + 1;
+  if (C == 64) {
+    const long blocks = (long)B * ((H + BTY - 1) / BTY) * ((W + BTX - 1) / BTX);
+    CVL_CHECK_ARG(blocks < (1l << 31));
+    hipLaunchKernelGGL(maxpool_bwd64_kernel, dim3((unsigned)blocks), dim3(NT), 0, S_, (const cvl_bf16*)dy, argmax,
+                       (cvl_bf16*)dx, H, W, Ho, Wo);
+    return cvl_launch_status();
+  }
   const long total = (long)B * H * W * (C / 8);
   hipLaunchKernelGGL(maxpool_bwd_kernel, dim3(grid_for(total)), dim3(NT), 0, S_, (const cvl_bf16*)dy,
                      argmax, (cvl_bf16*)dx, B, H, W, C, Ho, Wo);

@@ -18,14 +18,19 @@ class FCOSNet(FPNDetector):
     def __init__(self, num_classes, backbone_model="resnet50", device="cuda", seed=0, precision=None):
         """precision: "bf16" (production) / "fp32" (parity mode); None = CVL_PRECISION or bf16."""
         self._init_common(num_classes, backbone_model, device, seed, precision)
-        self.cls_ld = self.cls_heads[0].npad          # >= C, multiple of 32
+        self.cls_ld = self.cls_heads[0].cout_pad      # >= C, multiple of 32
         self.reg_ld = 8
 
     def _build_heads(self, st, num_classes):
         b_focal = math.log(0.01 / 0.99)
-        self.cls_heads = [Conv(st, "logits_output_%d" % (l + 1), 3, FPN_C, num_classes, bias_init=b_focal)
-                          for l in range(5)]
-        self.reg_heads = [Conv(st, "reg_output_%d" % (l + 1), 3, FPN_C, 5) for l in range(5)]
+        # forward weights packed 64 wide (the halo 3x3 kernel's N tile: the tower output is staged
+        # once per channel block instead of re-read per tap by the 32-wide generic kernel); the data
+        # gradient and the loss gradients keep the 32-wide channel padding
+        def pads(c):
+            return dict(npad=max(64, (c + 63) // 64 * 64), cout_pad=max(32, (c + 31) // 32 * 32))
+        self.cls_heads = [Conv(st, "logits_output_%d" % (l + 1), 3, FPN_C, num_classes, bias_init=b_focal,
+                               **pads(num_classes)) for l in range(5)]
+        self.reg_heads = [Conv(st, "reg_output_%d" % (l + 1), 3, FPN_C, 5, **pads(5)) for l in range(5)]
 
     def head_convs(self):
         return self.cls_heads + self.reg_heads
@@ -61,7 +66,7 @@ class FCOSNet(FPNDetector):
             # each with its own dw; small-N kernel conv_wgrad_sn), data grad for all levels in one launch
             d = heads[0].fwd_desc(B, [nn.seg(h, w, h, w, heads[l].wf, None, src_base=B * off[l], src_img=h * w,
                                              dst_base=off[l], dst_img=P) for l, (h, w) in enumerate(shapes)],
-                                  ld_dst=ld)
+                                  ld_dst=ld, npad=heads[0].cout_pad)
             nn.conv_wgrad_grouped(d, acts[-1], dout, [heads[l].dw for l in range(len(shapes))])
             dA = dA_pair[len(dAs)]
             segs = [nn.seg(h, w, h, w, heads[l].wd, None, src_base=off[l], src_img=P, dst_base=B * off[l],

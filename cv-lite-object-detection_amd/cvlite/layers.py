@@ -184,9 +184,12 @@ class Conv(object):
 
     # ---- descriptors ----------------------------------------------------------------------------
     def fwd_desc(self, B, segs, ld_dst=None, dst_coff=0, dst_f32=False, relu_out=False, relu_in=False,
-                 beta=0.0, n_store=None):
+                 beta=0.0, n_store=None, npad=None):
+        """npad: the GEMM's N padding when it differs from the packed weights' (a weight gradient of a
+        conv whose forward pack is wider than its dY rows, e.g. the FCOS heads)."""
         _, _, pt, pl = self.out_hw(segs[0]["Hs"], segs[0]["Ws"])
-        return nn.make_desc(nn.FWD, B, self.cin_k, self.k, self.k, self.stride, pt, pl, self.npad,
+        return nn.make_desc(nn.FWD, B, self.cin_k, self.k, self.k, self.stride, pt, pl,
+                            self.npad if npad is None else npad,
                             self.cout if n_store is None else n_store,
                             self.npad if ld_dst is None else ld_dst, segs, dst_coff=dst_coff,
                             dst_f32=dst_f32, relu_out=relu_out, relu_in=relu_in, beta=beta)

@@ -156,6 +156,37 @@ def test_maxpool_and_upsample():
     torch.testing.assert_close(db.double().cpu(), exp, rtol=1e-2, atol=2e-2)
 
 
+@pytest.mark.parametrize("B,H,W", [(2, 256, 256), (3, 37, 70)])
+def test_stem_pool_tiled_forms_match_generic(B, H, W):
+    """The 64-channel tiled kernels of the stem pool (bn_relu_maxpool64, maxpool_bwd64: one LDS tile
+    of relu(BN(z)) / of the windows' dy + argmax per workgroup) are bit-identical to the generic
+    per-output kernels, which serve any other C: the first 64 channels of a 128-channel run."""
+    from cvlite import ops_nn as nn
+    dev = torch.device("cuda")
+    g = torch.Generator(device="cpu").manual_seed(H + W)
+    z = (torch.randn(B, H, W, 128, generator=g) * 2.0).to(BF).to(dev)
+    mr = torch.stack([torch.randn(B, 128, generator=g) * 0.3, torch.rand(B, 128, generator=g) + 0.5], -1).float().to(dev)
+    gamma = (torch.rand(128, generator=g) + 0.5).to(dev)
+    beta = (torch.randn(128, generator=g) * 0.5).to(dev)
+    Ho, Wo = (H + 2 - 3) // 2 + 1, (W + 2 - 3) // 2 + 1
+    p128 = torch.empty((B, Ho, Wo, 128), dtype=BF, device=dev)
+    a128 = torch.empty((B, Ho, Wo, 128), dtype=torch.uint8, device=dev)
+    nn.bn_relu_maxpool3x3s2(z, mr, gamma, beta, p128, a128)
+    z64 = z[..., :64].contiguous()
+    mr64 = mr[:, :64].contiguous()
+    p64 = torch.empty((B, Ho, Wo, 64), dtype=BF, device=dev)
+    a64 = torch.empty((B, Ho, Wo, 64), dtype=torch.uint8, device=dev)
+    nn.bn_relu_maxpool3x3s2(z64, mr64, gamma[:64].contiguous(), beta[:64].contiguous(), p64, a64)
+    assert torch.equal(p64.view(torch.int16), p128[..., :64].contiguous().view(torch.int16))
+    assert torch.equal(a64, a128[..., :64].contiguous())
+    dy = (torch.randn(B, Ho, Wo, 128, generator=g)).to(BF).to(dev)
+    dx128 = torch.empty((B, H, W, 128), dtype=BF, device=dev)
+    nn.maxpool3x3s2_backward(dy, a128, dx128)
+    dx64 = torch.empty((B, H, W, 64), dtype=BF, device=dev)
+    nn.maxpool3x3s2_backward(dy[..., :64].contiguous(), a64, dx64)
+    assert torch.equal(dx64.view(torch.int16), dx128[..., :64].contiguous().view(torch.int16))
+
+
 def test_relu_bwd_bias_grad_sgd_lr():
     from cvlite import ops_nn as nn
     g = torch.Generator().manual_seed(5)
