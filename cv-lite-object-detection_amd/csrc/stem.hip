@@ -35,7 +35,10 @@ constexpr int KR = 168, KP = 192;        // real (7 x 24) and MFMA-padded K
 constexpr int WA = 200;                  // LDS pitch (elements) of the weight rows (forward)
 constexpr int CO = 64;
 constexpr int DZP = CO + 8;              // LDS pitch (elements) of the dz row image [px][co] (weight gradient)
-constexpr int RPW_F = 8, RPW_W = 16;     // output rows per workgroup (forward / weight gradient)
+// output rows per workgroup (forward / weight gradient): 8 gives 512 units at 512x512 bs 16, exactly
+// two resident per CU in one round (tools/stem_probe.py sweep, round 4: forward 82 us at 8 vs 101 /
+// 109 at 4 / 16; weight gradient 74 us at 8 vs 102 at 16, 95 at 4 and 12, 170 at 32)
+constexpr int RPW_F = 8, RPW_W = 8;
 constexpr int RPT = (RL + NT - 1) / NT;  // ring values per thread per image row
 
 struct StemArgs {
@@ -49,6 +52,7 @@ struct StemArgs {
   float* out;             // weight gradient: slab [units][192][64] or dw
   int B, H, W, Ho, Wo, ntx, nbands, rpw;
   float beta;
+  unsigned long long* stamps;   // measurement builds (CVL_STEM_STAMPS=1): u64 [grid][8], else null
 };
 
 struct Unit {
@@ -116,11 +120,17 @@ __device__ __forceinline__ s16x8 ring8(const cvl_bf16* p) {
 // pixels x 64 channels, 6 K-steps per output row.  The next row's two image rows are loaded into
 // registers before the row's MFMAs and stored to the ring after them.
 // ---------------------------------------------------------------------------------------------
+template <bool ST = false>
 __global__ void __launch_bounds__(NT, 2) stem_fwd_kernel(StemArgs g) {
   __shared__ __attribute__((aligned(16))) cvl_bf16 Wl[CO * WA];
   __shared__ __attribute__((aligned(16))) cvl_bf16 ring[NRING * RL];
   __shared__ float red[4][CO][2];
   const int tid = threadIdx.x;
+  // stamps (thread 0): wall clock at entry / prologue landed / rows done / exit, then shader-clock
+  // ticks spent in the rows' MFMA phase, epilogue (stores + statistics) and ring refill
+  unsigned long long* stamp = (ST && tid == 0) ? g.stamps + blockIdx.x * 8 : nullptr;
+  unsigned long long t_mma = 0, t_epi = 0, t_ref = 0, c0 = 0;
+  if (stamp) stamp[0] = wall_clock64();
   const Unit t = unit_of(g, blockIdx.x);
   if (t.oy0 >= g.Ho) return;
   for (int i = tid; i < CO * (KP / 8); i += NT) {
@@ -133,6 +143,7 @@ __global__ void __launch_bounds__(NT, 2) stem_fwd_kernel(StemArgs g) {
   __syncthreads();
   ring_prologue(g, t, ring);
   __syncthreads();
+  if (stamp) stamp[1] = wall_clock64();
 
   const int wave = tid >> 6, lane = tid & 63, lr = lane & 15, lg = lane >> 4;
   float bias[4][4];
@@ -158,6 +169,7 @@ __global__ void __launch_bounds__(NT, 2) stem_fwd_kernel(StemArgs g) {
     for (int i = 0; i < 4; ++i)
 #pragma unroll
       for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    if (stamp) c0 = __builtin_amdgcn_s_memtime();
 #pragma unroll
     for (int s = 0; s < KP / 32; ++s) {
       const int k0 = s * 32 + lg * 8, ky = k0 / 24, off = k0 - ky * 24;
@@ -173,6 +185,12 @@ __global__ void __launch_bounds__(NT, 2) stem_fwd_kernel(StemArgs g) {
         for (int j = 0; j < 4; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, fa[i]),
                                                                __builtin_bit_cast(bf16x8, fb[j]), acc[i][j], 0, 0, 0);
+    }
+    if (stamp) {
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      const unsigned long long c1 = __builtin_amdgcn_s_memtime();
+      t_mma += c1 - c0;
+      c0 = c1;
     }
     // epilogue: D[co = i*16 + lg*4 + e][px = wave*64 + j*16 + lr]
     cvl_bf16* zrow = g.z + ((long)(t.b * g.Ho + oy) * g.Wo + t.x0) * CO;
@@ -193,13 +211,20 @@ __global__ void __launch_bounds__(NT, 2) stem_fwd_kernel(StemArgs g) {
         if (ok) *reinterpret_cast<s16x4*>(zrow + (long)px * CO + i * 16 + lg * 4) = o;
       }
     }
+    if (stamp) {
+      const unsigned long long c1 = __builtin_amdgcn_s_memtime();
+      t_epi += c1 - c0;
+      c0 = c1;
+    }
     if (more) {
       __syncthreads();                              // (no reader of these two slots this row: safe)
       row_store(ring, 2 * oy + 4, n0);
       row_store(ring, 2 * oy + 5, n1);
       __syncthreads();
     }
+    if (stamp) t_ref += __builtin_amdgcn_s_memtime() - c0;
   }
+  if (stamp) { stamp[2] = wall_clock64(); stamp[4] = t_mma; stamp[5] = t_epi; stamp[6] = t_ref; }
   if (g.stats) {              // the 16 pixel lanes, then the 4 waves, in a fixed order
 #pragma unroll
     for (int i = 0; i < 4; ++i)
@@ -219,6 +244,7 @@ __global__ void __launch_bounds__(NT, 2) stem_fwd_kernel(StemArgs g) {
       acc_add(st + g.acc_slots, a2, g.acc_slots);
     }
   }
+  if (stamp) stamp[3] = wall_clock64();
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -354,7 +380,24 @@ inline void stem_plan(StemArgs* g, int B, int H, int W, int rpw) {
   g->nbands = (g->Ho + rpw - 1) / rpw;
 }
 
+// measurement builds: CVL_STEM_STAMPS=1 stamps every forward launch into this buffer
+constexpr int kStemStampWgs = 4096;
+__device__ unsigned long long g_stem_stamps[kStemStampWgs * 8];
+int g_stem_stamp_grid = 0;
+
 }  // namespace
+
+// Measurement hook: the stamps of the last stamped stem forward (CVL_STEM_STAMPS=1): u64 [grid][8] =
+// wall clock at entry / prologue landed / rows done / exit, then shader-clock ticks in the rows' MFMA
+// phase, epilogue and ring refill (thread 0 of each workgroup); returns the grid size (0: none).
+extern "C" int cvl_debug_stem_stamps(uint64_t* host, int max_wgs) {
+  const int n = g_stem_stamp_grid < max_wgs ? g_stem_stamp_grid : max_wgs;
+  if (n <= 0 || !host) return g_stem_stamp_grid;
+  if (hipDeviceSynchronize() != hipSuccess) return -1;
+  if (hipMemcpyFromSymbol(host, HIP_SYMBOL(g_stem_stamps), (size_t)n * 64, 0, hipMemcpyDeviceToHost) != hipSuccess)
+    return -1;
+  return g_stem_stamp_grid;
+}
 
 extern "C" int cvl_stem_conv7x7s2(const float* img, int B, int H, int W, const void* w_packed, const float* bias,
                                   void* z, uint64_t* bn_stats, cvl_stream_t stream) {
@@ -368,7 +411,15 @@ extern "C" int cvl_stem_conv7x7s2(const float* img, int B, int H, int W, const v
   g.stats = reinterpret_cast<acc_u64*>(bn_stats);
   g.acc_slots = cvl_bn_acc_slots();
   stem_plan(&g, B, H, W, RPW_F);
-  hipLaunchKernelGGL(stem_fwd_kernel, dim3(B * g.ntx * g.nbands), dim3(NT), 0, (hipStream_t)stream, g);
+  static const bool stamps = cvl_env_flag("CVL_STEM_STAMPS");
+  const int grid = B * g.ntx * g.nbands;
+  if (stamps && grid <= kStemStampWgs) {
+    void* sym = nullptr;
+    if (hipGetSymbolAddress(&sym, HIP_SYMBOL(g_stem_stamps)) == hipSuccess) g.stamps = (unsigned long long*)sym;
+    g_stem_stamp_grid = grid;
+  }
+  if (g.stamps) hipLaunchKernelGGL(stem_fwd_kernel<true>, dim3(grid), dim3(NT), 0, (hipStream_t)stream, g);
+  else hipLaunchKernelGGL(stem_fwd_kernel<false>, dim3(grid), dim3(NT), 0, (hipStream_t)stream, g);
   return cvl_launch_status();
 }
 
