@@ -27,6 +27,8 @@
 
 namespace {
 
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
 constexpr int NT = 256;                  // 4 waves
 constexpr int SPX = 256;                 // output pixels per column range
 constexpr int RL = 1560;                 // ring row (bf16): (2 * SPX + 6) * 3 = 1554 values, padded
@@ -133,15 +135,29 @@ __global__ void __launch_bounds__(NT, 2) stem_fwd_kernel(StemArgs g) {
   if (stamp) stamp[0] = wall_clock64();
   const Unit t = unit_of(g, blockIdx.x);
   if (t.oy0 >= g.Ho) return;
-  for (int i = tid; i < CO * (KP / 8); i += NT) {
-    const int co = i / (KP / 8), ch = i - (i / (KP / 8)) * (KP / 8);
-    s16x8 v = s16x8{0, 0, 0, 0, 0, 0, 0, 0};
-    if (ch < KR / 8) v = *reinterpret_cast<const s16x8*>(g.w + co * KR + ch * 8);
-    *reinterpret_cast<s16x8*>(Wl + co * WA + ch * 8) = v;
+  // prologue, every load in flight at once: the weights, then the first 7 image rows; the weights
+  // land in LDS and the ring is zeroed while the image rows are still in flight
+  constexpr int WQ = CO * (KP / 8) / NT;
+  s16x8 wv[WQ];
+#pragma unroll
+  for (int q = 0; q < WQ; ++q) {
+    const int i = tid + q * NT, co = i / (KP / 8), ch = i - (i / (KP / 8)) * (KP / 8);
+    wv[q] = ch < KR / 8 ? *reinterpret_cast<const s16x8*>(g.w + co * KR + ch * 8) : s16x8{0, 0, 0, 0, 0, 0, 0, 0};
   }
-  for (int i = tid; i < NRING * RL / 8; i += NT) reinterpret_cast<s16x8*>(ring)[i] = s16x8{0, 0, 0, 0, 0, 0, 0, 0};
-  __syncthreads();
-  ring_prologue(g, t, ring);
+  {
+    float v[7][RPT];
+#pragma unroll
+    for (int r = 0; r < 7; ++r) row_load(g, t, 2 * t.oy0 - 3 + r, v[r]);
+#pragma unroll
+    for (int q = 0; q < WQ; ++q) {
+      const int i = tid + q * NT, co = i / (KP / 8), ch = i - (i / (KP / 8)) * (KP / 8);
+      *reinterpret_cast<s16x8*>(Wl + co * WA + ch * 8) = wv[q];
+    }
+    for (int i = tid; i < NRING * RL / 8; i += NT) reinterpret_cast<s16x8*>(ring)[i] = s16x8{0, 0, 0, 0, 0, 0, 0, 0};
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < 7; ++r) row_store(ring, 2 * t.oy0 - 3 + r, v[r]);
+  }
   __syncthreads();
   if (stamp) stamp[1] = wall_clock64();
 
@@ -151,13 +167,17 @@ __global__ void __launch_bounds__(NT, 2) stem_fwd_kernel(StemArgs g) {
   for (int i = 0; i < 4; ++i)
 #pragma unroll
     for (int e = 0; e < 4; ++e) bias[i][e] = g.bias ? g.bias[i * 16 + lg * 4 + e] : 0.f;
-  float s1[4][4], s2[4][4];
+  f32x2 s1[4][2], s2[4][2];        // (channel i*16 + lg*4 + e) statistics, channel pairs packed
 #pragma unroll
   for (int i = 0; i < 4; ++i)
 #pragma unroll
-    for (int e = 0; e < 4; ++e) { s1[i][e] = 0.f; s2[i][e] = 0.f; }
+    for (int e = 0; e < 2; ++e) { s1[i][e] = f32x2{0.f, 0.f}; s2[i][e] = f32x2{0.f, 0.f}; }
 
+  // per row: the next row's two image rows are loaded, the MFMAs issue, the two rows go into the
+  // ring slots this row does not read ((2*oy + 7) % NRING is only its zero-weight pad K, any finite
+  // value will do) while the MFMAs run, then the epilogue; ONE barrier per row, at its top
   for (int oy = t.oy0; oy < t.oy1; ++oy) {
+    if (oy > t.oy0) __syncthreads();                // the previous row's ring stores are visible
     const bool more = oy + 1 < t.oy1;
     float n0[RPT], n1[RPT];
     if (more) {                                     // image rows 2*oy + 4, 2*oy + 5 for row oy + 1
@@ -192,6 +212,15 @@ __global__ void __launch_bounds__(NT, 2) stem_fwd_kernel(StemArgs g) {
       t_mma += c1 - c0;
       c0 = c1;
     }
+    if (more) {
+      row_store(ring, 2 * oy + 4, n0);
+      row_store(ring, 2 * oy + 5, n1);
+    }
+    if (stamp) {
+      const unsigned long long c1 = __builtin_amdgcn_s_memtime();
+      t_ref += c1 - c0;
+      c0 = c1;
+    }
     // epilogue: D[co = i*16 + lg*4 + e][px = wave*64 + j*16 + lr]
     cvl_bf16* zrow = g.z + ((long)(t.b * g.Ho + oy) * g.Wo + t.x0) * CO;
 #pragma unroll
@@ -201,28 +230,29 @@ __global__ void __launch_bounds__(NT, 2) stem_fwd_kernel(StemArgs g) {
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         s16x4 o;
+        float r[4];
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const cvl_bf16 h = f32_to_bf16(acc[i][j][e] + bias[i][e]);
-          const float v = bf16_to_f32(h);
-          o[e] = (short)h;
-          if (ok) { s1[i][e] += v; s2[i][e] += v * v; }
+        for (int e = 0; e < 4; e += 2) {            // one v_cvt_pk_bf16_f32 per channel pair (RNE)
+          const bf16x2 h = __builtin_convertvector(
+              (f32x2{acc[i][j][e] + bias[i][e], acc[i][j][e + 1] + bias[i][e + 1]}), bf16x2);
+          const unsigned u = __builtin_bit_cast(unsigned, h);
+          r[e] = __uint_as_float(u << 16);
+          r[e + 1] = __uint_as_float(u & 0xffff0000u);
+          o[e] = (short)(u & 0xffffu);
+          o[e + 1] = (short)(u >> 16);
         }
-        if (ok) *reinterpret_cast<s16x4*>(zrow + (long)px * CO + i * 16 + lg * 4) = o;
+        if (ok) {                                   // packed fp32 adds / fmas on channel pairs
+#pragma unroll
+          for (int e = 0; e < 2; ++e) {
+            const f32x2 v = f32x2{r[2 * e], r[2 * e + 1]};
+            s1[i][e] += v;
+            s2[i][e] = __builtin_elementwise_fma(v, v, s2[i][e]);
+          }
+          *reinterpret_cast<s16x4*>(zrow + (long)px * CO + i * 16 + lg * 4) = o;
+        }
       }
     }
-    if (stamp) {
-      const unsigned long long c1 = __builtin_amdgcn_s_memtime();
-      t_epi += c1 - c0;
-      c0 = c1;
-    }
-    if (more) {
-      __syncthreads();                              // (no reader of these two slots this row: safe)
-      row_store(ring, 2 * oy + 4, n0);
-      row_store(ring, 2 * oy + 5, n1);
-      __syncthreads();
-    }
-    if (stamp) t_ref += __builtin_amdgcn_s_memtime() - c0;
+    if (stamp) t_epi += __builtin_amdgcn_s_memtime() - c0;
   }
   if (stamp) { stamp[2] = wall_clock64(); stamp[4] = t_mma; stamp[5] = t_epi; stamp[6] = t_ref; }
   if (g.stats) {              // the 16 pixel lanes, then the 4 waves, in a fixed order
@@ -230,7 +260,7 @@ __global__ void __launch_bounds__(NT, 2) stem_fwd_kernel(StemArgs g) {
     for (int i = 0; i < 4; ++i)
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
-        float a1 = s1[i][e], a2 = s2[i][e];
+        float a1 = s1[i][e >> 1][e & 1], a2 = s2[i][e >> 1][e & 1];
 #pragma unroll
         for (int m = 1; m < 16; m <<= 1) { a1 += __shfl_xor(a1, m, 64); a2 += __shfl_xor(a2, m, 64); }
         if (lr == 0) { red[wave][i * 16 + lg * 4 + e][0] = a1; red[wave][i * 16 + lg * 4 + e][1] = a2; }

@@ -36,8 +36,7 @@ def main():
     dw = torch.empty((192, 64), dtype=torch.float32, device="cuda")
     f = timed(lambda: nn.stem_conv7x7s2(img, wf, bias, z, st))
     w = timed(lambda: nn.stem_wgrad(img, dz, dw))
-    print("%s stem fwd %.1f us, wgrad %.1f us (rpw_f %s, rpw_w %s)" % (
-        tag, f, w, os.environ.get("CVL_STEM_RPW_F", "8"), os.environ.get("CVL_STEM_RPW_W", "16")), flush=True)
+    print("%s stem fwd %.1f us, wgrad %.1f us" % (tag, f, w), flush=True)
 
 
 if __name__ == "__main__":

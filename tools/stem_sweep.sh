@@ -1,5 +1,6 @@
 #!/bin/bash
-# rows-per-workgroup sweep of the stem kernels (tools/stem_probe.py), one process per setting
+# stem kernel timings (tools/stem_probe.py); the round-4 rows-per-workgroup sweep ran it once per
+# CVL_STEM_RPW_F / CVL_STEM_RPW_W setting (knobs since folded into constants, stem.hip RPW_F / RPW_W)
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
 mkdir -p gpurun_out
 for cfg in "8 8"; do
