@@ -48,6 +48,12 @@ constexpr int WT_EL = 9 * BN * BK;                  // bf16 elements of a stage'
 constexpr int STAGE_EL = HALO_EL + WT_EL;
 constexpr int LDS_C = BM * (BN + 8) + WGM * BN * 2 * 2;
 constexpr int LDS_EL = 2 * STAGE_EL > LDS_C ? 2 * STAGE_EL : LDS_C;
+// WRES (weights resident): a single-N-tile launch with at most 2 channel blocks (Cin <= 64: the
+// ResNet conv2_x 3x3 units, forward and data gradient) keeps ALL its weights in LDS for the whole
+// launch and streams only the halos, double-buffered: 2 halos + 2 x 36 KiB of weights = 152 KiB
+constexpr int WRES_CB = 2;
+constexpr int LDS_WRES_EL = 2 * HALO_EL + WRES_CB * WT_EL;
+static_assert(HALO_EL >= LDS_C, "the epilogue stages its C image in a halo buffer");
 constexpr unsigned kRecords = 0x7fffffffu;
 constexpr unsigned kOOB = 0x80000000u;
 
@@ -125,9 +131,11 @@ __device__ __forceinline__ HaloPieces halo_pieces(const HGeo& G, int H, int W, i
 // issued, so that tile's halo and weights land while the current tile's epilogue runs (the
 // epilogue stages its C image in the stage buffer just consumed), and the per-tile set-up is a
 // few adds (halo_pieces is per segment).  One workgroup per CU (148 KiB of LDS).
-template <bool DGRAD, bool BSUM>
+template <bool DGRAD, bool BSUM, bool WRES = false>
 __global__ void __launch_bounds__(NT) conv_igemm_h_kernel(ConvArgs a) {
-  __shared__ __attribute__((aligned(16))) cvl_bf16 lds[LDS_EL];
+  __shared__ __attribute__((aligned(16))) cvl_bf16 lds[WRES ? LDS_WRES_EL : LDS_EL];
+  constexpr int SST = WRES ? HALO_EL : STAGE_EL;        // elements per stage buffer
+  cvl_bf16* const wres = lds + 2 * HALO_EL;             // WRES: the weights of channel block cb at cb * WT_EL
   const int tid = threadIdx.x;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
   const int ntn = a.Npad / BN;
@@ -233,9 +241,18 @@ __global__ void __launch_bounds__(NT) conv_igemm_h_kernel(ConvArgs a) {
     const unsigned cbo = (unsigned)(i_cb * BK * 2);
 #pragma unroll
     for (int j = 0; j < HPW; ++j) dma16(rsA, st + (wave + 8 * j) * 16 * BK, hoff[j] + cbo);
+    if (WRES) {                                     // every channel block's weights, once
+      for (int cbw = 0; cbw < ncb_all; ++cbw) {
+        const unsigned wo = (unsigned)(cbw * BK * 2);
 #pragma unroll
-    for (int j = 0; j < 4; ++j) dma16(rsB, st + HALO_EL + (wave + 8 * j) * 16 * BK, woff[j] + cbo);
-    if (wave < WPC - 32) dma16(rsB, st + HALO_EL + (wave + 32) * 16 * BK, woff[4] + cbo);
+        for (int j = 0; j < 4; ++j) dma16(rsB, wres + cbw * WT_EL + (wave + 8 * j) * 16 * BK, woff[j] + wo);
+        if (wave < WPC - 32) dma16(rsB, wres + cbw * WT_EL + (wave + 32) * 16 * BK, woff[4] + wo);
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) dma16(rsB, st + HALO_EL + (wave + 8 * j) * 16 * BK, woff[j] + cbo);
+      if (wave < WPC - 32) dma16(rsB, st + HALO_EL + (wave + 32) * 16 * BK, woff[4] + cbo);
+    }
     advance();
   }
   wait_vm<0>();
@@ -243,6 +260,7 @@ __global__ void __launch_bounds__(NT) conv_igemm_h_kernel(ConvArgs a) {
   asm volatile("" ::: "memory");
 
   int gb = 0;                                       // global channel-block counter (stage parity)
+  int c_cb = 0;                                     // the channel block being computed (WRES weights)
   int c_sg = -1;
   unsigned afr[TM][3];
   int HWr = 1, prow = 0;
@@ -290,7 +308,8 @@ __global__ void __launch_bounds__(NT) conv_igemm_h_kernel(ConvArgs a) {
       const int r = t / 3, sx = t - 3 * (t / 3);
       const int d = DGRAD ? 2 - sx : sx;
       const char* Hr = Hc + (DGRAD ? 1 - r : r - 1) * prow;
-      const char* Wt = Hc + HALO_EL * 2 + t * BN * BK * 2;
+      const char* Wt = WRES ? reinterpret_cast<const char*>(wres + c_cb * WT_EL) + t * BN * BK * 2
+                            : Hc + HALO_EL * 2 + t * BN * BK * 2;
 #pragma unroll
       for (int i = 0; i < TM; ++i) fa[buf][i] = *reinterpret_cast<const s16x8*>(Hr + afr[i][d]);
 #pragma unroll
@@ -305,16 +324,17 @@ __global__ void __launch_bounds__(NT) conv_igemm_h_kernel(ConvArgs a) {
                                                                __builtin_bit_cast(bf16x8, fb[buf][j]), acc[i][j], 0, 0, 0);
     };
     for (int cb = cb0; cb < cb1; ++cb) {
-      const char* Hc = reinterpret_cast<const char*>(lds + (gb & 1) * STAGE_EL);
+      const char* Hc = reinterpret_cast<const char*>(lds + (gb & 1) * SST);
+      c_cb = cb;
       const bool more = i_L < t_hi;
-      cvl_bf16* nh = lds + ((gb + 1) & 1) * STAGE_EL;
+      cvl_bf16* nh = lds + ((gb + 1) & 1) * SST;
       const unsigned cbo = (unsigned)(i_cb * BK * 2);
       read_tap(0, Hc, 0);
 #pragma unroll
       for (int t = 0; t < 9; ++t) {
         if (more && t < HPW) dma16(rsA, nh + (wave + 8 * t) * 16 * BK, hoff[t] + cbo);
-        if (more && t >= HPW && t < HPW + 4) dma16(rsB, nh + HALO_EL + (wave + 8 * (t - HPW)) * 16 * BK, woff[t - HPW] + cbo);
-        if (t == 8 && more && wave < WPC - 32) dma16(rsB, nh + HALO_EL + (wave + 32) * 16 * BK, woff[4] + cbo);
+        if (!WRES && more && t >= HPW && t < HPW + 4) dma16(rsB, nh + HALO_EL + (wave + 8 * (t - HPW)) * 16 * BK, woff[t - HPW] + cbo);
+        if (!WRES && t == 8 && more && wave < WPC - 32) dma16(rsB, nh + HALO_EL + (wave + 32) * 16 * BK, woff[4] + cbo);
         if (t < 8) read_tap((t + 1) & 1, Hc, t + 1);
         mma_tap(t & 1);
       }
@@ -341,7 +361,7 @@ __global__ void __launch_bounds__(NT) conv_igemm_h_kernel(ConvArgs a) {
     }
     // the epilogue's C image goes into the stage buffer just consumed (the other one holds the
     // next tile's first stage, in flight); the barrier after it frees that buffer for the DMA
-    conv_l_epilogue<BN, WGM, TM, TN, NT, BSUM>(a, S, acc, lds + ((gb - 1) & 1) * STAGE_EL, tid, wm, wn, n0, mloc0,
+    conv_l_epilogue<BN, WGM, TM, TN, NT, BSUM>(a, S, acc, lds + ((gb - 1) & 1) * SST, tid, wm, wn, n0, mloc0,
                                                 HWr, zpre, bpar);
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
@@ -406,9 +426,18 @@ int cvl_conv_igemm_h(const cvl_conv_desc* d, const ConvArgs& a0, hipStream_t s, 
   const int wgs = a.splits > 1 ? tiles : (tiles < ncu * per_cu ? tiles : ncu * per_cu);
   dim3 grid(wgs, 1, a.splits);
   g_cvl_conv_last_kernel = CVL_CK_H64;
-  if (dg && a.bsum) hipLaunchKernelGGL((conv_igemm_h_kernel<true, true>), grid, dim3(NT), 0, s, a);
-  else if (dg) hipLaunchKernelGGL((conv_igemm_h_kernel<true, false>), grid, dim3(NT), 0, s, a);
-  else hipLaunchKernelGGL((conv_igemm_h_kernel<false, false>), grid, dim3(NT), 0, s, a);
+  const bool wres = a.splits <= 1 && a.Npad == BN && ncb <= WRES_CB && a.nseg == 1 && !cvl_env_flag("CVL_CONV_H_NO_WRES");
+  if (wres) {
+    if (dg && a.bsum) hipLaunchKernelGGL((conv_igemm_h_kernel<true, true, true>), grid, dim3(NT), 0, s, a);
+    else if (dg) hipLaunchKernelGGL((conv_igemm_h_kernel<true, false, true>), grid, dim3(NT), 0, s, a);
+    else hipLaunchKernelGGL((conv_igemm_h_kernel<false, false, true>), grid, dim3(NT), 0, s, a);
+  } else if (dg && a.bsum) {
+    hipLaunchKernelGGL((conv_igemm_h_kernel<true, true>), grid, dim3(NT), 0, s, a);
+  } else if (dg) {
+    hipLaunchKernelGGL((conv_igemm_h_kernel<true, false>), grid, dim3(NT), 0, s, a);
+  } else {
+    hipLaunchKernelGGL((conv_igemm_h_kernel<false, false>), grid, dim3(NT), 0, s, a);
+  }
   int st = cvl_launch_status();
   if (st || a.splits <= 1) return st;
   return cvl_conv_splitk_finish(a, s);
