@@ -3,8 +3,8 @@
 // FCOS/fcos.py:30-46 and RetinaNet/retinanet_module.py:39-72.  Forward (with the conv1_bn
 // statistics) and weight gradient; the input image has no gradient.
 //
-// The generic path materialises the im2col matrix of the 7x7x3 patches ([B*Ho*Wo][192] bf16, 403 MB
-// at 512x512 bs 16), writes it once and reads it twice (forward GEMM and weight gradient).  Here a
+// The im2col form these kernels replaced materialised the 7x7x3 patch matrix ([B*Ho*Wo][192] bf16,
+// 403 MB at 512x512 bs 16), wrote it once and read it twice (forward GEMM and weight gradient).  Here a
 // workgroup walks a band of output rows of one image (and one 256-pixel column range) and keeps a
 // ring of the image rows they need in LDS as bf16 -- each output row needs 7 image rows, the next
 // one 2 more -- and the MFMA operands are read straight out of that ring: the patch of output pixel
@@ -20,9 +20,9 @@
 // zeroed first) add nothing.  The weight gradient is written in the same padded order, dw [192][64]
 // fp32 (rows ky * 24 + kx * 3 + c; the pad rows come out 0).
 //
-// Numerics as the im2col path: the image rounded to bf16 (round to nearest even), bf16 MFMA with
+// Numerics as that im2col form: the image rounded to bf16 (round to nearest even), bf16 MFMA with
 // fp32 accumulation, bias added in fp32, the output rounded to bf16; BN statistics of the rounded
-// output as exact accumulators (bn_acc.h), one add per (workgroup, channel).
+// output as BN accumulators (bn_acc.h: float64 or the exact mode's bins), one add per (workgroup, channel).
 #include "conv_common.h"
 
 namespace {
