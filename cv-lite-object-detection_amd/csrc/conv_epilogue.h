@@ -47,21 +47,35 @@ __device__ __forceinline__ void bnsum_prefetch(const ConvArgs& a, const ConvSeg&
   }
 }
 
+// the epilogue's per-column bias of this lane (TN columns), loaded where its latency hides: a
+// persistent kernel fetches it at tile start, so the epilogue does not wait a memory round trip
+template <int BN, int WGM, int TN>
+__device__ __forceinline__ void epi_bias(const ConvArgs& a, const ConvSeg& S, int n0, int wn, int lane,
+                                         float (&bcol)[TN]) {
+  constexpr int WN = BN / (8 / WGM);
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    const int n = n0 + wn * WN + j * 16 + (lane & 15);
+    bcol[j] = (S.bias && n < a.n_store) ? S.bias[n] : 0.f;
+  }
+}
+
 template <int BN, int WGM, int TM, int TN, int NT, bool BS = false>
 __device__ __forceinline__ void conv_l_epilogue(const ConvArgs& a, const ConvSeg& S, f32x4 (&acc)[TM][TN],
                                                 cvl_bf16* lds, int tid, int wm, int wn, int n0, int mloc0,
                                                 int HWr, const s16x8 (&zpre)[BnSumPre<BN, NT>::N],
-                                                const BnSumPar& par) {
+                                                const BnSumPar& par, const float* bpre = nullptr) {
   constexpr int BM = 256;
   constexpr int WGN = 8 / WGM;
   constexpr int WM = BM / WGM, WN = BN / WGN;
   const int lane = tid & 63;
   const int lr = lane & 15, lg = lane >> 4;
   float bcol[TN];
+  if (bpre) {
 #pragma unroll
-  for (int j = 0; j < TN; ++j) {
-    const int n = n0 + wn * WN + j * 16 + lr;
-    bcol[j] = (S.bias && n < a.n_store) ? S.bias[n] : 0.f;
+    for (int j = 0; j < TN; ++j) bcol[j] = bpre[j];
+  } else {
+    epi_bias<BN, WGM, TN>(a, S, n0, wn, lane, bcol);
   }
   if (a.dst_f32) {
     // fp32 destination (the head outputs the fused losses read): +bias, ReLU, unrounded 4-byte

@@ -125,19 +125,30 @@ __device__ __forceinline__ HaloPieces halo_pieces(const HGeo& G, int H, int W, i
   return P;
 }
 
+// measurement builds (CVL_H_STAMPS=1): u64 [grid][8] per launch = wall clock at entry / prologue
+// landed / last tile's loop done / exit, then shader-clock sums over the tiles: tap loops, the
+// per-block wait + barrier, epilogues (+ their barrier), and the tile count
+constexpr int kHStampWgs = 4096;
+__device__ unsigned long long g_h_stamps[kHStampWgs * 8];
+
 // H64, persistent: a workgroup runs a contiguous chunk of the launch's 256 x 64 tiles (all of
 // them when the launch is split over K: then one tile per workgroup).  The DMA stream runs across
 // tile boundaries: during the last channel block of a tile the first stage of the next tile is
 // issued, so that tile's halo and weights land while the current tile's epilogue runs (the
 // epilogue stages its C image in the stage buffer just consumed), and the per-tile set-up is a
 // few adds (halo_pieces is per segment).  One workgroup per CU (148 KiB of LDS).
-template <bool DGRAD, bool BSUM, bool WRES = false>
+template <bool DGRAD, bool BSUM, bool WRES = false, bool ST = false>
 __global__ void __launch_bounds__(NT) conv_igemm_h_kernel(ConvArgs a) {
   __shared__ __attribute__((aligned(16))) cvl_bf16 lds[WRES ? LDS_WRES_EL : LDS_EL];
   constexpr int SST = WRES ? HALO_EL : STAGE_EL;        // elements per stage buffer
   cvl_bf16* const wres = lds + 2 * HALO_EL;             // WRES: the weights of channel block cb at cb * WT_EL
   const int tid = threadIdx.x;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
+  unsigned long long* const stamp = (ST && tid == 0 && blockIdx.x < kHStampWgs && blockIdx.z == 0)
+                                        ? g_h_stamps + blockIdx.x * 8 : nullptr;
+  // (held in registers and stored at exit: a store in flight would make the next vmcnt(0) wait for it)
+  unsigned long long t_tap = 0, t_wait = 0, t_epi = 0, n_tile = 0, c0 = 0, w0 = 0, w1 = 0, w2 = 0;
+  if (ST && stamp) w0 = wall_clock64();
   const int ntn = a.Npad / BN;
   const int ntiles = a.m_tiles * ntn;
   const int G_ = gridDim.x;
@@ -241,13 +252,10 @@ __global__ void __launch_bounds__(NT) conv_igemm_h_kernel(ConvArgs a) {
     const unsigned cbo = (unsigned)(i_cb * BK * 2);
 #pragma unroll
     for (int j = 0; j < HPW; ++j) dma16(rsA, st + (wave + 8 * j) * 16 * BK, hoff[j] + cbo);
-    if (WRES) {                                     // every channel block's weights, once
-      for (int cbw = 0; cbw < ncb_all; ++cbw) {
-        const unsigned wo = (unsigned)(cbw * BK * 2);
+    if (WRES) {                                     // the first channel block's weights (the rest below)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) dma16(rsB, wres + cbw * WT_EL + (wave + 8 * j) * 16 * BK, woff[j] + wo);
-        if (wave < WPC - 32) dma16(rsB, wres + cbw * WT_EL + (wave + 32) * 16 * BK, woff[4] + wo);
-      }
+      for (int j = 0; j < 4; ++j) dma16(rsB, wres + (wave + 8 * j) * 16 * BK, woff[j]);
+      if (wave < WPC - 32) dma16(rsB, wres + (wave + 32) * 16 * BK, woff[4]);
     } else {
 #pragma unroll
       for (int j = 0; j < 4; ++j) dma16(rsB, st + HALO_EL + (wave + 8 * j) * 16 * BK, woff[j] + cbo);
@@ -258,6 +266,17 @@ __global__ void __launch_bounds__(NT) conv_igemm_h_kernel(ConvArgs a) {
   wait_vm<0>();
   __builtin_amdgcn_s_barrier();
   asm volatile("" ::: "memory");
+  if (ST && stamp) w1 = wall_clock64();
+  // WRES: the other channel blocks' weights land under block 0's taps (its end waits for vmcnt 0
+  // and barriers before block 1 reads them)
+  if (WRES) {
+    for (int cbw = 1; cbw < ncb_all; ++cbw) {
+      const unsigned wo = (unsigned)(cbw * BK * 2);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) dma16(rsB, wres + cbw * WT_EL + (wave + 8 * j) * 16 * BK, woff[j] + wo);
+      if (wave < WPC - 32) dma16(rsB, wres + cbw * WT_EL + (wave + 32) * 16 * BK, woff[4] + wo);
+    }
+  }
 
   int gb = 0;                                       // global channel-block counter (stage parity)
   int c_cb = 0;                                     // the channel block being computed (WRES weights)
@@ -292,6 +311,8 @@ __global__ void __launch_bounds__(NT) conv_igemm_h_kernel(ConvArgs a) {
     s16x8 zpre[BnSumPre<BN, NT>::N];
     BnSumPar bpar;
     if constexpr (BSUM) bnsum_prefetch<BN, NT>(a, S, tid, n0, mloc0, zpre, bpar);
+    float bcol[TN];                                 // the epilogue's bias, in flight under the taps
+    epi_bias<BN, WGM, TN>(a, S, n0, wn, lane, bcol);
     f32x4 acc[TM][TN];
 #pragma unroll
     for (int i = 0; i < TM; ++i)
@@ -329,6 +350,7 @@ __global__ void __launch_bounds__(NT) conv_igemm_h_kernel(ConvArgs a) {
       const bool more = i_L < t_hi;
       cvl_bf16* nh = lds + ((gb + 1) & 1) * SST;
       const unsigned cbo = (unsigned)(i_cb * BK * 2);
+      if (ST && stamp) c0 = __builtin_amdgcn_s_memtime();
       read_tap(0, Hc, 0);
 #pragma unroll
       for (int t = 0; t < 9; ++t) {
@@ -339,9 +361,15 @@ __global__ void __launch_bounds__(NT) conv_igemm_h_kernel(ConvArgs a) {
         mma_tap(t & 1);
       }
       if (more) advance();
+      unsigned long long c1 = 0;
+      if (ST && stamp) {
+        c1 = __builtin_amdgcn_s_memtime();
+        t_tap += c1 - c0;
+      }
       wait_vm<0>();                                 // this wave's pieces of the next block landed
       __builtin_amdgcn_s_barrier();                 // ... and everyone's; this block fully read
       asm volatile("" ::: "memory");
+      if (ST && stamp) t_wait += __builtin_amdgcn_s_memtime() - c1;
       ++gb;
     }
     if (a.splits > 1) {           // raw fp32 partials; conv_igemm.hip's finish applies the epilogue
@@ -361,17 +389,50 @@ __global__ void __launch_bounds__(NT) conv_igemm_h_kernel(ConvArgs a) {
     }
     // the epilogue's C image goes into the stage buffer just consumed (the other one holds the
     // next tile's first stage, in flight); the barrier after it frees that buffer for the DMA
+    if (ST && stamp) {
+      c0 = __builtin_amdgcn_s_memtime();
+      w2 = wall_clock64();
+    }
     conv_l_epilogue<BN, WGM, TM, TN, NT, BSUM>(a, S, acc, lds + ((gb - 1) & 1) * SST, tid, wm, wn, n0, mloc0,
-                                                HWr, zpre, bpar);
+                                                HWr, zpre, bpar, bcol);
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
+    if (ST && stamp) {
+      t_epi += __builtin_amdgcn_s_memtime() - c0;
+      ++n_tile;
+    }
   }
   wait_vm<0>();
+  if (ST && stamp) {
+    stamp[0] = w0;
+    stamp[1] = w1;
+    stamp[2] = w2;
+    stamp[3] = wall_clock64();
+    stamp[4] = t_tap;
+    stamp[5] = t_wait;
+    stamp[6] = t_epi;
+    stamp[7] = n_tile;
+  }
 }
 
 }  // namespace
 
 int cvl_conv_splitk_finish(const ConvArgs& a, hipStream_t s);
+
+int g_h_stamp_grid = 0;
+
+// Measurement hook: the stamps of the last stamped H64 launch (CVL_H_STAMPS=1): u64 [grid][8] as
+// above.  Copies min(grid, max_wgs) rows to host; returns the grid (0: none stamped).  max_wgs < 0:
+// forget the last launch (the next stamped one reports).
+extern "C" int cvl_debug_h_stamps(uint64_t* host, int max_wgs) {
+  if (max_wgs < 0) return g_h_stamp_grid = 0;
+  const int n = g_h_stamp_grid < max_wgs ? g_h_stamp_grid : max_wgs;
+  if (n <= 0 || !host) return g_h_stamp_grid;
+  if (hipDeviceSynchronize() != hipSuccess) return CVL_EHIP;
+  if (hipMemcpyFromSymbol(host, HIP_SYMBOL(g_h_stamps), (size_t)n * 64, 0, hipMemcpyDeviceToHost) != hipSuccess)
+    return CVL_EHIP;
+  return g_h_stamp_grid;
+}
 
 // Geometry H64 covers: 3x3, stride 1, pad 1, source map = output map, every segment's 256-row tiles
 // whole image rows (W | 256, H*W % 256 == 0) or whole images (H*W | 256), halo within HPX pixels.
@@ -427,7 +488,16 @@ int cvl_conv_igemm_h(const cvl_conv_desc* d, const ConvArgs& a0, hipStream_t s, 
   dim3 grid(wgs, 1, a.splits);
   g_cvl_conv_last_kernel = CVL_CK_H64;
   const bool wres = a.splits <= 1 && a.Npad == BN && ncb <= WRES_CB && a.nseg == 1 && !cvl_env_flag("CVL_CONV_H_NO_WRES");
-  if (wres) {
+  static const bool stamps = cvl_env_flag("CVL_H_STAMPS");
+  if (stamps && a.splits <= 1 && wgs <= kHStampWgs) {
+    g_h_stamp_grid = wgs;
+    if (wres && !dg) hipLaunchKernelGGL((conv_igemm_h_kernel<false, false, true, true>), grid, dim3(NT), 0, s, a);
+    else if (wres && dg && a.bsum) hipLaunchKernelGGL((conv_igemm_h_kernel<true, true, true, true>), grid, dim3(NT), 0, s, a);
+    else if (wres) hipLaunchKernelGGL((conv_igemm_h_kernel<true, false, true, true>), grid, dim3(NT), 0, s, a);
+    else if (dg && a.bsum) hipLaunchKernelGGL((conv_igemm_h_kernel<true, true, false, true>), grid, dim3(NT), 0, s, a);
+    else if (dg) hipLaunchKernelGGL((conv_igemm_h_kernel<true, false, false, true>), grid, dim3(NT), 0, s, a);
+    else hipLaunchKernelGGL((conv_igemm_h_kernel<false, false, false, true>), grid, dim3(NT), 0, s, a);
+  } else if (wres) {
     if (dg && a.bsum) hipLaunchKernelGGL((conv_igemm_h_kernel<true, true, true>), grid, dim3(NT), 0, s, a);
     else if (dg) hipLaunchKernelGGL((conv_igemm_h_kernel<true, false, true>), grid, dim3(NT), 0, s, a);
     else hipLaunchKernelGGL((conv_igemm_h_kernel<false, false, true>), grid, dim3(NT), 0, s, a);

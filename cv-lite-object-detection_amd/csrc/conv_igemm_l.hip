@@ -129,6 +129,10 @@ __global__ void __launch_bounds__(NT) conv_igemm_l_kernel(ConvArgs a) {
 
   const int wm = wave / WGN, wn = wave % WGN;
   const int lr = lane & 15, lg = lane >> 4;
+  // the epilogue's bias, in flight under the main loop (the 256-wide form runs at the register
+  // limit and loads it in the epilogue)
+  float bcol[TN];
+  if constexpr (BN <= 128) epi_bias<BN, WGM, TN>(a, S, n0, wn, lane, bcol);
   f32x4 acc[TM][TN];
 #pragma unroll
   for (int i = 0; i < TM; ++i)
@@ -186,7 +190,8 @@ __global__ void __launch_bounds__(NT) conv_igemm_l_kernel(ConvArgs a) {
     slot = slot == NST - 1 ? 0 : slot + 1;
   }
 
-  conv_l_epilogue<BN, WGM, TM, TN, NT, BSUM>(a, S, acc, lds, tid, wm, wn, n0, mloc0, HWr, zpre, bpar);
+  conv_l_epilogue<BN, WGM, TM, TN, NT, BSUM>(a, S, acc, lds, tid, wm, wn, n0, mloc0, HWr, zpre, bpar,
+                                              BN <= 128 ? bcol : nullptr);
 }
 
 }  // namespace

@@ -57,6 +57,7 @@ SIGNATURES = {
     "cvl_bn_acc_slots": (c_int, []),
     "cvl_debug_wgx_stamps": (c_int, [P, c_int]),
     "cvl_debug_stem_stamps": (c_int, [P, c_int]),
+    "cvl_debug_h_stamps": (c_int, [P, c_int]),
     "cvl_stem_conv7x7s2": (c_int, [P, c_int, c_int, c_int, P, P, P, P, P]),
     "cvl_stem_wgrad_workspace_size": (c_size_t, [c_int, c_int, c_int]),
     "cvl_stem_wgrad": (c_int, [P, c_int, c_int, c_int, P, P, c_float, P, c_size_t, P]),

@@ -35,6 +35,7 @@ for s in $steps; do
     rowdma)  run 60 gpurun_out/${tag}_rowdma.txt ./tools/ubench_rowdma; cat gpurun_out/${tag}_rowdma.txt ;;
     pprobe)  run 90 gpurun_out/${tag}_pprobe.md python -u tools/p_probe.py; cat gpurun_out/${tag}_pprobe.md ;;
     pstamps) run 90 gpurun_out/${tag}_pstamps.txt python -u tools/p_stamps.py; cat gpurun_out/${tag}_pstamps.txt ;;
+    hstamps) run 90 gpurun_out/${tag}_hstamps.md python -u tools/h64_stamps.py; cat gpurun_out/${tag}_hstamps.md ;;
     stem)    run 200 gpurun_out/${tag}_stem.log python -u -m pytest tests/test_gpu_stem.py tests/test_gpu_bn_acc.py tests/test_gpu_bn_fold.py -q --timeout 150 --timeout-method thread
              tail -3 gpurun_out/${tag}_stem.log ;;
   esac
