@@ -64,7 +64,19 @@ template <int BN, int WGM, int TM, int TN, int NT, bool BS = false>
 __device__ __forceinline__ void conv_l_epilogue(const ConvArgs& a, const ConvSeg& S, f32x4 (&acc)[TM][TN],
                                                 cvl_bf16* lds, int tid, int wm, int wn, int n0, int mloc0,
                                                 int HWr, const s16x8 (&zpre)[BnSumPre<BN, NT>::N],
-                                                const BnSumPar& par, const float* bpre = nullptr) {
+                                                const BnSumPar& par, const float* bpre = nullptr,
+                                                unsigned long long* ts = nullptr) {
+  // ts (measurement builds): shader-clock ticks accumulated per phase -- [0] bias / rounding /
+  // statistics up to the first barrier, [1] C image + statistics combine, [2] stores (+ BN-backward
+  // sums), [3] the BN-backward sums' reduction
+  unsigned long long tprev = ts ? __builtin_amdgcn_s_memtime() : 0;
+  auto tmark = [&](int k) {
+    if (ts) {
+      const unsigned long long t = __builtin_amdgcn_s_memtime();
+      ts[k] += t - tprev;
+      tprev = t;
+    }
+  };
   constexpr int BM = 256;
   constexpr int WGN = 8 / WGM;
   constexpr int WM = BM / WGM, WN = BN / WGN;
@@ -197,6 +209,7 @@ __device__ __forceinline__ void conv_l_epilogue(const ConvArgs& a, const ConvSeg
 
   wait_vm<0>();
   __syncthreads();
+  tmark(0);
   // fused BN-backward sums (a.bsum, 64/128-wide tiles only): a thread's 8-channel chunk is fixed
   // over the store loop (NT % CCH == 0) and the tile is one image (host: H*W % 256 == 0, dense
   // rows), so its per-channel parameters load once; its z chunks arrive prefetched (zpre)
@@ -250,6 +263,7 @@ __device__ __forceinline__ void conv_l_epilogue(const ConvArgs& a, const ConvSeg
     acc_add(st, s1, a.acc_slots);
     acc_add(st + a.acc_slots, s2, a.acc_slots);
   }
+  tmark(1);
   cvl_bf16* dst = reinterpret_cast<cvl_bf16*>(a.dst);
   // destination rows are the segment's rows in order (no channel interleave of images, no
   // stride-2 scatter): the row index is base + ml, no per-row division
@@ -289,6 +303,7 @@ __device__ __forceinline__ void conv_l_epilogue(const ConvArgs& a, const ConvSeg
     }
     *pd = v;
   }
+  tmark(2);
   if (bsum) {          // the NT / CCH threads of a channel chunk, summed in a fixed order:
     // lanes l, l + CCH, ... of a wave by xor shuffles, then the NT / 64 waves through LDS
 #pragma unroll
@@ -321,5 +336,6 @@ __device__ __forceinline__ void conv_l_epilogue(const ConvArgs& a, const ConvSeg
       acc_add(st, t1, a.acc_slots);
       acc_add(st + a.acc_slots, t2, a.acc_slots);
     }
+    tmark(3);
   }
 }

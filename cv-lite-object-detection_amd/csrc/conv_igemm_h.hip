@@ -126,8 +126,9 @@ __device__ __forceinline__ HaloPieces halo_pieces(const HGeo& G, int H, int W, i
 }
 
 // measurement builds (CVL_H_STAMPS=1): u64 [grid][8] per launch = wall clock at entry / prologue
-// landed / last tile's loop done / exit, then shader-clock sums over the tiles: tap loops, the
-// per-block wait + barrier, epilogues (+ their barrier), and the tile count
+// landed, the epilogue phases (conv_l_epilogue ts, 16 bits each), wall clock at exit, then
+// shader-clock sums over the tiles: tap loops, the per-block wait + barrier, epilogues (+ their
+// barrier), and the tile count
 constexpr int kHStampWgs = 4096;
 __device__ unsigned long long g_h_stamps[kHStampWgs * 8];
 
@@ -147,7 +148,8 @@ __global__ void __launch_bounds__(NT) conv_igemm_h_kernel(ConvArgs a) {
   unsigned long long* const stamp = (ST && tid == 0 && blockIdx.x < kHStampWgs && blockIdx.z == 0)
                                         ? g_h_stamps + blockIdx.x * 8 : nullptr;
   // (held in registers and stored at exit: a store in flight would make the next vmcnt(0) wait for it)
-  unsigned long long t_tap = 0, t_wait = 0, t_epi = 0, n_tile = 0, c0 = 0, w0 = 0, w1 = 0, w2 = 0;
+  unsigned long long t_tap = 0, t_wait = 0, t_epi = 0, n_tile = 0, c0 = 0, w0 = 0, w1 = 0;
+  unsigned long long te[4] = {0, 0, 0, 0};                // the epilogue's phases (conv_l_epilogue ts)
   if (ST && stamp) w0 = wall_clock64();
   const int ntn = a.Npad / BN;
   const int ntiles = a.m_tiles * ntn;
@@ -391,10 +393,9 @@ __global__ void __launch_bounds__(NT) conv_igemm_h_kernel(ConvArgs a) {
     // next tile's first stage, in flight); the barrier after it frees that buffer for the DMA
     if (ST && stamp) {
       c0 = __builtin_amdgcn_s_memtime();
-      w2 = wall_clock64();
     }
     conv_l_epilogue<BN, WGM, TM, TN, NT, BSUM>(a, S, acc, lds + ((gb - 1) & 1) * SST, tid, wm, wn, n0, mloc0,
-                                                HWr, zpre, bpar, bcol);
+                                                HWr, zpre, bpar, bcol, (ST && stamp) ? te : nullptr);
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
     if (ST && stamp) {
@@ -406,7 +407,7 @@ __global__ void __launch_bounds__(NT) conv_igemm_h_kernel(ConvArgs a) {
   if (ST && stamp) {
     stamp[0] = w0;
     stamp[1] = w1;
-    stamp[2] = w2;
+    stamp[2] = (te[0] & 0xffff) | ((te[1] & 0xffff) << 16) | ((te[2] & 0xffff) << 32) | ((te[3] & 0xffff) << 48);
     stamp[3] = wall_clock64();
     stamp[4] = t_tap;
     stamp[5] = t_wait;

@@ -63,6 +63,7 @@ def report(lib, name, launch):
         if n <= 0:
             print("%s: not an unsplit H64 launch (%.1f us)" % (name, us))
             return
+        ph = np.stack([(buf[:n, 2] >> np.uint64(16 * k)) & np.uint64(0xffff) for k in range(4)], 1).astype(np.float64)
         s = buf[:n].astype(np.float64)
         t0 = s[:, 0].min()
         span = (s[:, 3].max() - t0) / wall
@@ -75,6 +76,9 @@ def report(lib, name, launch):
               "block wait+barrier %.1f, epilogue %.1f us"
               % (name, us, n, s[:, 7].mean(), span, (s[:, 0].max() - t0) / wall, pro, loop, clk,
                  (s[:, 4] / clk).mean(), (s[:, 5] / clk).mean(), (s[:, 6] / clk).mean()))
+        tiles = np.maximum(s[:, 7], 1)[:, None]
+        print("   epilogue per tile (us): rounding+stats+barrier %.2f, C image+combine %.2f, stores(+sums) %.2f, "
+              "sums reduction %.2f" % tuple((ph / tiles / clk).mean(0)))
 
 
 if __name__ == "__main__":
