@@ -38,6 +38,7 @@ __global__ void __launch_bounds__(512) k_reg(const char* src, unsigned fmask, in
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   unsigned off = ((unsigned)blockIdx.x * 65536u + (unsigned)wave * 1024u) & fmask;
   i32x4 v[D];
+  i32x4 x = i32x4{0, 0, 0, 0};                  // every load feeds x (no dead loads)
   for (int it = 0; it < iters; it += D) {
 #pragma unroll
     for (int d = 0; d < D; ++d) {
@@ -45,11 +46,14 @@ __global__ void __launch_bounds__(512) k_reg(const char* src, unsigned fmask, in
       off = (off + 8192u) & fmask;
     }
 #pragma unroll
-    for (int d = 0; d < D; ++d)
-      *reinterpret_cast<i32x4*>(lds + ((((it + d) & 15) * 8 + wave) * 1024) + lane * 16) = v[d];
+    for (int d = 0; d < D; ++d) {             // volatile: every ds_write_b128 is kept
+      *(volatile __attribute__((address_space(3))) i32x4*)(lds + ((((it + d) & 15) * 8 + wave) * 1024) + lane * 16) = v[d];
+      x ^= v[d];
+    }
   }
   __syncthreads();
   if (threadIdx.x == 0 && lds[blockIdx.x & 1023] == 123) sink[0] = 1;
+  if (x.x == 0x12345678 && x.y == 0x9abcdef) sink[0] = x.z;
 }
 
 int main(int argc, char** argv) {
