@@ -1,6 +1,6 @@
 """Checksums of the H64 backbone 3x3 forwards (conv2_x 64->64 @ 128^2 incl. its BN statistics, conv4_x
-256->256 @ 32^2) at bs 16 from fixed inputs: run with and without CVL_H_RSTAGE=1 and compare the lines
-(register-staged halos must be bit-identical to LDS-DMA)."""
+256->256 @ 32^2) at bs 16 from fixed inputs, for bit-identity A/Bs of H64 variants: run once per
+variant (env knob / build) and compare the lines (round 4: the register-staged halo experiment)."""
 import hashlib
 import os
 import sys
