@@ -88,15 +88,26 @@ constexpr int kFoldImgs = 4;              // images one workgroup's rows may spa
 // arithmetic, so the MFMAs see the operand the unfused form stored.  A lane's x fragment is 8 rows
 // of ONE channel (its column), so a step needs one (mean, rstd, gamma, beta) per fragment column;
 // the values for the <= kFoldImgs images of the workgroup's rows are loaded once, before the stream.
-template <int T, int SR = BR, bool ST = false, bool FOLD = false>
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+
+// RG (register-staged ring, the production form): each lane loads its 16-B pieces of a step by
+// buffer_load_dwordx4 into VGPRs (two register sets, loads issued three steps ahead of their
+// step), ds_write_b128s them into a 2-slot LDS ring one step ahead, and the transposed fragment
+// reads are those of the DMA form.  The DMA form (LDS-DMA into a 5-slot ring) issues at ~100+ cycles
+// per piece and fills at ~30 GB/s per CU (profiles/r04_ubench_ldsdma.md); the register path costs
+// ~20 cycles per piece.  Same MFMA order: bit-identical results.  Measured at the DMA form's speed
+// (loop 19.1 vs 17.3 us at 1x1 1024->256 @ 32^2), so opt-in (CVL_WGX_RG=1) for diagnosis.
+template <int T, int SR = BR, bool ST = false, bool FOLD = false, bool RG = false>
 __global__ void __launch_bounds__(NT) conv_wgrad_x_kernel(WxArgs g) {
   using C = WxCfg<T, SR>;
+  static_assert(!(RG && FOLD), "the FOLD form runs on the DMA ring");
   // ST: wall-clock stamps of thread 0 (entry, prologue landed, loop done, epilogue stored)
   unsigned long long* stamp = (ST && threadIdx.x == 0) ? g.stamps + blockIdx.x * 4 : nullptr;
   if (stamp) stamp[0] = wall_clock64();
   constexpr int BCO = C::BCO, BKK = C::BKK, YST = C::YST, SLOT = C::SLOT, TM = C::TM, TN = C::TN;
   constexpr int J = C::J;
-  __shared__ __attribute__((aligned(16))) cvl_bf16 lds[NSLOT * SLOT];
+  constexpr int NSL = RG ? 2 : NSLOT;
+  __shared__ __attribute__((aligned(16))) cvl_bf16 lds[NSL * SLOT];
   const ConvArgs& a = g.a;
   const int tid = threadIdx.x;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
@@ -155,20 +166,18 @@ __global__ void __launch_bounds__(NT) conv_wgrad_x_kernel(WxArgs g) {
       cox[j] = q - coy[j] * Wr;
     }
   };
-  auto issue = [&]() {
+  // one step's pieces: put(j, dY offset, x offset) per DMA / load instruction pair (kOOB: zeros)
+  auto issue_step = [&](auto&& put) {
     const bool live = ist < nsteps;
     if (live && im >= seg_end) seek(im);
-    cvl_bf16* Yb = lds + cslot * SLOT;
-    cvl_bf16* Xb = Yb + YST;
 #pragma unroll
     for (int j = 0; j < J; ++j) {
       const bool rv = live && cml[j] < rows;
       const int drow = dbase + cimg[j] * dimg + coy[j] * Wr + cox[j];
-      dma16(rsY, Yb + (8 * C::RPI * j + C::RPI * wave) * BCO, rv && yok ? (unsigned)(drow * rowb) + ycol : kOOB);
       const int iy = coy[j] * a.stride + ry, ix = cox[j] * a.stride + rx;
       const bool xv = rv && kok && (unsigned)iy < (unsigned)Hs && (unsigned)ix < (unsigned)Ws;
       const int pix = sbase + cimg[j] * simg + iy * Ws + ix;
-      dma16(rsX, Xb + (8 * C::RPI * j + C::RPI * wave) * BKK, xv ? (unsigned)(pix * pixb) + xcol : kOOB);
+      put(j, rv && yok ? (unsigned)(drow * rowb) + ycol : kOOB, xv ? (unsigned)(pix * pixb) + xcol : kOOB);
       // advance the row by SR: (img, y, x) with one carry per level (d_ox < Wr, d_oy < Hr)
       cml[j] += SR;
       cox[j] += d_ox;
@@ -181,7 +190,33 @@ __global__ void __launch_bounds__(NT) conv_wgrad_x_kernel(WxArgs g) {
     }
     im += SR;
     ++ist;
+  };
+  auto issue = [&]() {                          // DMA form: LDS-DMA into ring slot cslot
+    cvl_bf16* Yb = lds + cslot * SLOT;
+    cvl_bf16* Xb = Yb + YST;
+    issue_step([&](int j, unsigned oy, unsigned ox) {
+      dma16(rsY, Yb + (8 * C::RPI * j + C::RPI * wave) * BCO, oy);
+      dma16(rsX, Xb + (8 * C::RPI * j + C::RPI * wave) * BKK, ox);
+    });
     cslot = cslot == NSLOT - 1 ? 0 : cslot + 1;
+  };
+  // RG form: a register set holds one step's pieces of this lane
+  struct RSet { u32x4 y[J], x[J]; };
+  auto load_set = [&](RSet& r) {
+    issue_step([&](int j, unsigned oy, unsigned ox) {
+      r.y[j] = __builtin_amdgcn_raw_buffer_load_b128(rsY, (int)oy, 0, 0);
+      r.x[j] = __builtin_amdgcn_raw_buffer_load_b128(rsX, (int)ox, 0, 0);
+    });
+  };
+  // the lane's 16 B land where LDS-DMA would have put them (lane-linear from the wave's row base)
+  auto store_set = [&](const RSet& r, int slot) {
+    char* Yb = reinterpret_cast<char*>(lds + slot * SLOT) + lane * 16;
+    char* Xb = Yb + YST * 2;
+#pragma unroll
+    for (int j = 0; j < J; ++j) {
+      *reinterpret_cast<u32x4*>(Yb + (8 * C::RPI * j + C::RPI * wave) * BCO * 2) = r.y[j];
+      *reinterpret_cast<u32x4*>(Xb + (8 * C::RPI * j + C::RPI * wave) * BKK * 2) = r.x[j];
+    }
   };
 
   const int wco = wave >> 2, wk = wave & 3;
@@ -235,27 +270,9 @@ __global__ void __launch_bounds__(NT) conv_wgrad_x_kernel(WxArgs g) {
       }
     }
   }
-  issue();
-  issue();
-  issue();
-  wait_vm<2 * PW>();                            // (also retires the FOLD parameter loads)
-  if (FOLD) {
-#pragma unroll
-    for (int j = 0; j < TN; ++j) {
-      asm volatile("" : "+v"(fga[j]), "+v"(fbe[j]));
-#pragma unroll
-      for (int q = 0; q < kFoldImgs; ++q) asm volatile("" : "+v"(fmr[q][j]));
-    }
-  }
-  __builtin_amdgcn_s_barrier();
-  asm volatile("" ::: "memory");
-  if (stamp) stamp[1] = wall_clock64();
-  if (wco == 1) bar();                          // stagger: waves 4-7 run one barrier behind
-
-  int rslot = 0;
-  for (int st = 0; st < nsteps; ++st) {
-    wait_vm<PW>();                              // step st+1 (read next phase)
-    issue();                                    // step st+3
+  // one phase's compute: this wave's fragments of step st from ring slot rslot (issued before the
+  // barrier that ends the wave's load segment), then its MFMA segment
+  auto phase = [&](int st, int rslot) {
     const unsigned base = lds0 + rslot * (SLOT * 2);
     constexpr int KS = C::KS;
     s16x4 al[KS][TM], ah[KS][TM], bl[KS][TN], bh[KS][TN];
@@ -267,8 +284,13 @@ __global__ void __launch_bounds__(NT) conv_wgrad_x_kernel(WxArgs g) {
 #pragma unroll
       for (int j = 0; j < TN; ++j) { bl[h][j] = ds_tr16(xo + xa[j]); bh[h][j] = ds_tr16(xo + xb[j]); }
     }
-    bar();
-    lgkm_wait();
+    if (RG) {                                   // the ring writes of this segment land before the barrier
+      lgkm_wait();
+      bar();
+    } else {
+      bar();
+      lgkm_wait();
+    }
 #pragma unroll
     for (int h = 0; h < KS; ++h) {
 #pragma unroll
@@ -315,7 +337,59 @@ __global__ void __launch_bounds__(NT) conv_wgrad_x_kernel(WxArgs g) {
     __builtin_amdgcn_s_setprio(0);
     __builtin_amdgcn_sched_barrier(0);
     bar();
-    rslot = rslot == NSLOT - 1 ? 0 : rslot + 1;
+  };
+
+  if constexpr (RG) {
+    // register sets: at the load segment of step t, set (t+1)&1 holds step t+1 (written into ring slot
+    // (t+1)&1, whose step t-1 both wave groups finished reading before the previous barrier) and is
+    // then reloaded with step t+3; set t&1 holds step t+2 in flight.  nsteps is even (128-row
+    // chunks), so the loop runs phase pairs with the sets fixed.
+    RSet sa, sb;
+    load_set(sa);                               // step 0
+    load_set(sb);                               // step 1
+    store_set(sa, 0);
+    load_set(sa);                               // step 2
+    lgkm_wait();
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    if (stamp) stamp[1] = wall_clock64();
+    if (wco == 1) bar();                        // stagger: waves 4-7 run one barrier behind
+    for (int st = 0; st < nsteps; st += 2) {
+      store_set(sb, 1);                         // step st+1
+      __builtin_amdgcn_sched_barrier(0);
+      load_set(sb);                             // step st+3
+      __builtin_amdgcn_sched_barrier(0);
+      phase(st, 0);
+      store_set(sa, 0);                         // step st+2
+      __builtin_amdgcn_sched_barrier(0);
+      load_set(sa);                             // step st+4
+      __builtin_amdgcn_sched_barrier(0);
+      phase(st + 1, 1);
+    }
+  } else {
+    issue();
+    issue();
+    issue();
+    wait_vm<2 * PW>();                          // (also retires the FOLD parameter loads)
+    if (FOLD) {
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        asm volatile("" : "+v"(fga[j]), "+v"(fbe[j]));
+#pragma unroll
+        for (int q = 0; q < kFoldImgs; ++q) asm volatile("" : "+v"(fmr[q][j]));
+      }
+    }
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    if (stamp) stamp[1] = wall_clock64();
+    if (wco == 1) bar();                        // stagger: waves 4-7 run one barrier behind
+    int rslot = 0;
+    for (int st = 0; st < nsteps; ++st) {
+      wait_vm<PW>();                            // step st+1 (read next phase)
+      issue();                                  // step st+3
+      phase(st, rslot);
+      rslot = rslot == NSLOT - 1 ? 0 : rslot + 1;
+    }
   }
   if (wco == 0) bar();                          // equal barrier counts for both groups
   wait_vm<0>();
@@ -506,18 +580,24 @@ int cvl_conv_wgrad_x(const cvl_conv_desc* d, int ngroups, const void* x, const v
     if (gs) return gs;
   }
   const dim3 grid(p.tiles * p.nsplit * ngroups);
+  // CVL_WGX_RG=1: the register-staged ring (measured no faster than the LDS-DMA ring: DESIGN §7)
+  static const bool dma = !cvl_env_flag("CVL_WGX_RG");
   if (fold) {
     hipLaunchKernelGGL((conv_wgrad_x_kernel<128, 64, false, true>), grid, dim3(NT), 0, s, g);
   } else if (g.stamps) {
-    if (p.T == 256) hipLaunchKernelGGL((conv_wgrad_x_kernel<256, BR, true>), grid, dim3(NT), 0, s, g);
-    else if (p.SR == 64) hipLaunchKernelGGL((conv_wgrad_x_kernel<128, 64, true>), grid, dim3(NT), 0, s, g);
-    else hipLaunchKernelGGL((conv_wgrad_x_kernel<128, BR, true>), grid, dim3(NT), 0, s, g);
+    if (p.T == 256) hipLaunchKernelGGL((conv_wgrad_x_kernel<256, BR, true, false, true>), grid, dim3(NT), 0, s, g);
+    else if (p.SR == 64) hipLaunchKernelGGL((conv_wgrad_x_kernel<128, 64, true, false, true>), grid, dim3(NT), 0, s, g);
+    else hipLaunchKernelGGL((conv_wgrad_x_kernel<128, BR, true, false, true>), grid, dim3(NT), 0, s, g);
+  } else if (dma) {
+    if (p.T == 256) hipLaunchKernelGGL((conv_wgrad_x_kernel<256, BR>), grid, dim3(NT), 0, s, g);
+    else if (p.SR == 64) hipLaunchKernelGGL((conv_wgrad_x_kernel<128, 64>), grid, dim3(NT), 0, s, g);
+    else hipLaunchKernelGGL((conv_wgrad_x_kernel<128, BR>), grid, dim3(NT), 0, s, g);
   } else if (p.T == 256) {
-    hipLaunchKernelGGL(conv_wgrad_x_kernel<256>, grid, dim3(NT), 0, s, g);
+    hipLaunchKernelGGL((conv_wgrad_x_kernel<256, BR, false, false, true>), grid, dim3(NT), 0, s, g);
   } else if (p.SR == 64) {
-    hipLaunchKernelGGL((conv_wgrad_x_kernel<128, 64>), grid, dim3(NT), 0, s, g);
+    hipLaunchKernelGGL((conv_wgrad_x_kernel<128, 64, false, false, true>), grid, dim3(NT), 0, s, g);
   } else {
-    hipLaunchKernelGGL(conv_wgrad_x_kernel<128>, grid, dim3(NT), 0, s, g);
+    hipLaunchKernelGGL((conv_wgrad_x_kernel<128, BR, false, false, true>), grid, dim3(NT), 0, s, g);
   }
   int st = cvl_launch_status();
   if (st || g.direct) return st;

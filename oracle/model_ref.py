@@ -241,15 +241,20 @@ def fcos_loss_and_grads(params, x, targets, num_classes, grad_scale=1.0, dtype=t
     return torch.stack(losses).detach(), grads, reg.detach(), cls.detach()
 
 
-def train_step_reference(params, moms, images, targets, num_classes, lr, momentum=0.9, clip=1.0):
+def train_step_reference(params, moms, images, targets, num_classes, lr, momentum=0.9, clip=1.0,
+                         dtype=torch.float32, losses_out=None):
     """FCOS/train_fcos.py:128-185 restated: per-image forward/backward (batch-1, as the reference),
-    gradient sum, /bs, clip_by_global_norm, Keras SGD (v = m v - lr g; w += v).  In place."""
+    gradient sum, /bs, clip_by_global_norm, Keras SGD (v = m v - lr g; w += v).  In place.
+    dtype: the arithmetic type (float64 for a tolerance yardstick); losses_out: a list that
+    receives each image's (cls, reg, cen) losses (train_fcos.py:157-158)."""
     bs = images.shape[0]
     acc = {k: torch.zeros_like(v) for k, v in params.items()}
     for b in range(bs):
-        _, g, _, _ = fcos_loss_and_grads(params, images[b:b + 1], targets[b:b + 1], num_classes)
+        lo, g, _, _ = fcos_loss_and_grads(params, images[b:b + 1], targets[b:b + 1], num_classes, dtype=dtype)
+        if losses_out is not None:
+            losses_out.append(lo[0])
         for k, v in g.items():
-            acc[k] += v
+            acc[k] += v.to(acc[k].dtype)
     for k in acc:
         acc[k] /= bs
     norm = math.sqrt(sum(float((v.double() ** 2).sum()) for v in acc.values()))
