@@ -57,6 +57,8 @@ struct WxArgs {
   int ld_dy, dy_coff, Cout, co_tiles, tiles, nsplit, chunk, direct;
   float beta;
   unsigned long long* stamps;             // measurement builds (CVL_WGX_STAMPS=1): u64 [grid][4], else null
+  unsigned long long* phase;              // with stamps: per-wave loop phase cycles u64 [grid][8][8], or null
+  int ablate;                             // with stamps: ablation bits (CVL_WGX_ABLATE), else 0
 };
 
 __device__ __forceinline__ int rswz(int r) { return (r & 3) | (((r >> 3) & 1) << 2); }
@@ -68,6 +70,13 @@ __device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t r, const cvl_bf16* 
 }
 
 typedef float wf32x2 __attribute__((ext_vector_type(2)));
+// shader-clock stamp (measurement builds only), waited for at once: placed only where no LDS
+// operation of the wave is in flight, so the wait costs just the stamp's own latency
+__device__ __forceinline__ unsigned long long memtime_nowait() {
+  unsigned long long t;
+  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t) :: "memory");
+  return t;
+}
 // loads the compiler does not track: issued before the prologue DMAs, so the prologue's counted
 // wait retires them (a tracked load used in the loop would make the compiler drain the ring there)
 __device__ __forceinline__ wf32x2 gload8_untracked(const void* p) {
@@ -137,33 +146,51 @@ __global__ void __launch_bounds__(NT) conv_wgrad_x_kernel(WxArgs g) {
   const __amdgpu_buffer_rsrc_t rsX = __builtin_amdgcn_make_buffer_rsrc((void*)a.src, (short)0, (int)kRecords, 0x00020000);
 
   // ---- issue cursor ----------------------------------------------------------------------------
+  // Per lane and DMA / load instruction j: the row's (local row, source iy, ix) and its two byte
+  // offsets, advanced by SR rows per step with adds only: the (img, y, x) carries of a step are
+  // uniform deltas (d_img, d_oy, d_ox < one level each) whose byte effects are precomputed per
+  // segment, so the issue path has no integer multiplies (quarter-rate on CDNA; the multiply form
+  // cost ~0.45 us per step, measured by ablation in the stamped build).
   int ist = 0, im = m_lo, cslot = 0;
   int seg_end = -1;                                       // forces a seek at the first live step
-  int Wr = 1, Hr = 1, Ws = 1, Hs = 1, rows = 0, sbase = 0, simg = 0, dbase = 0, dimg = 0;
-  int d_img = 0, d_oy = 0, d_ox = 0;
-  int cml[J], cimg[J], coy[J], cox[J];
+  int rows = 0, Hs = 1, Ws = 1;
+  int s_dx = 0, s_dy = 0, s_wr = 0, s_hr = 0, ixw = 0, iyh = 0;
+  int DY0 = 0, DYQ = 0, DX0 = 0, DXY = 0, DXQ = 0;
+  const int st_ = a.stride;
+  int cml[J], iyj[J], ixj[J], ybo[J], xbo[J];
   auto seek = [&](int m) {
     int sg = 0;
 #pragma unroll
     for (int i = 1; i < kMaxSeg; ++i)
       if (i < a.nseg && m >= a.seg[i].m_start) sg = i;
     const ConvSeg& S = a.seg[sg];
-    Wr = S.Wr; Hr = S.Hr; Ws = S.Ws; Hs = S.Hs; rows = S.rows;
-    sbase = (int)S.src_base; simg = (int)S.src_img; dbase = (int)S.dst_base; dimg = (int)S.dst_img;
+    const int Wr = S.Wr, Hr = S.Hr;
+    Ws = S.Ws; Hs = S.Hs; rows = S.rows;
+    const int sbase = (int)S.src_base, simg = (int)S.src_img, dbase = (int)S.dst_base, dimg = (int)S.dst_img;
     seg_end = sg + 1 < a.nseg ? a.seg[sg + 1].m_start : 0x7fffffff;
     const int HW = Hr * Wr;
-    d_img = SR / HW;
+    const int d_img = SR / HW;
     const int rem = SR - d_img * HW;
-    d_oy = rem / Wr;
-    d_ox = rem - d_oy * Wr;
+    const int d_oy = rem / Wr;
+    const int d_ox = rem - d_oy * Wr;
+    s_dx = d_ox * st_; s_dy = d_oy * st_; s_wr = Wr * st_; s_hr = Hr * st_;
+    ixw = s_wr + rx; iyh = s_hr + ry;
+    DY0 = (d_img * dimg + d_oy * Wr + d_ox) * rowb;
+    DYQ = (dimg - HW) * rowb;
+    DX0 = (d_img * simg + d_oy * st_ * Ws + d_ox * st_) * pixb;
+    DXY = (st_ * Ws - s_wr) * pixb;
+    DXQ = (simg - s_hr * Ws) * pixb;
 #pragma unroll
     for (int j = 0; j < J; ++j) {
       const int ml = m - S.m_start + 8 * C::RPI * j + rr;
       cml[j] = ml;
-      cimg[j] = ml / HW;
-      const int q = ml - cimg[j] * HW;
-      coy[j] = q / Wr;
-      cox[j] = q - coy[j] * Wr;
+      const int img = ml / HW;
+      const int q = ml - img * HW;
+      const int oy = q / Wr, ox = q - (q / Wr) * Wr;
+      iyj[j] = oy * st_ + ry;
+      ixj[j] = ox * st_ + rx;
+      ybo[j] = (dbase + img * dimg + oy * Wr + ox) * rowb + (int)ycol;
+      xbo[j] = (sbase + img * simg + iyj[j] * Ws + ixj[j]) * pixb + (int)xcol;
     }
   };
   // one step's pieces: put(j, dY offset, x offset) per DMA / load instruction pair (kOOB: zeros)
@@ -173,20 +200,18 @@ __global__ void __launch_bounds__(NT) conv_wgrad_x_kernel(WxArgs g) {
 #pragma unroll
     for (int j = 0; j < J; ++j) {
       const bool rv = live && cml[j] < rows;
-      const int drow = dbase + cimg[j] * dimg + coy[j] * Wr + cox[j];
-      const int iy = coy[j] * a.stride + ry, ix = cox[j] * a.stride + rx;
-      const bool xv = rv && kok && (unsigned)iy < (unsigned)Hs && (unsigned)ix < (unsigned)Ws;
-      const int pix = sbase + cimg[j] * simg + iy * Ws + ix;
-      put(j, rv && yok ? (unsigned)(drow * rowb) + ycol : kOOB, xv ? (unsigned)(pix * pixb) + xcol : kOOB);
-      // advance the row by SR: (img, y, x) with one carry per level (d_ox < Wr, d_oy < Hr)
+      const bool xv = rv && kok && (unsigned)iyj[j] < (unsigned)Hs && (unsigned)ixj[j] < (unsigned)Ws;
+      put(j, rv && yok ? (unsigned)ybo[j] : kOOB, xv ? (unsigned)xbo[j] : kOOB);
+      // advance the row by SR: one carry per level (d_ox < Wr, d_oy < Hr)
       cml[j] += SR;
-      cox[j] += d_ox;
-      const int cy = cox[j] >= Wr;
-      cox[j] -= cy ? Wr : 0;
-      coy[j] += d_oy + cy;
-      const int cq = coy[j] >= Hr;
-      coy[j] -= cq ? Hr : 0;
-      cimg[j] += d_img + cq;
+      ixj[j] += s_dx;
+      const bool cy = ixj[j] >= ixw;
+      ixj[j] -= cy ? s_wr : 0;
+      iyj[j] += s_dy + (cy ? st_ : 0);
+      const bool cq = iyj[j] >= iyh;
+      iyj[j] -= cq ? s_hr : 0;
+      ybo[j] += DY0 + (cq ? DYQ : 0);
+      xbo[j] += DX0 + (cy ? DXY : 0) + (cq ? DXQ : 0);
     }
     im += SR;
     ++ist;
@@ -202,7 +227,18 @@ __global__ void __launch_bounds__(NT) conv_wgrad_x_kernel(WxArgs g) {
   };
   // RG form: a register set holds one step's pieces of this lane
   struct RSet { u32x4 y[J], x[J]; };
+  const int abl = ST ? g.ablate : 0;           // measurement builds: CVL_WGX_ABLATE bits (launch code)
   auto load_set = [&](RSet& r) {
+    if (abl & 4) return;                        // no loads
+    if (abl & 8) {                              // loads without the address arithmetic (one hot KiB)
+#pragma unroll
+      for (int j = 0; j < J; ++j) {
+        r.y[j] = __builtin_amdgcn_raw_buffer_load_b128(rsY, lane * 16, 0, 0);
+        r.x[j] = __builtin_amdgcn_raw_buffer_load_b128(rsX, lane * 16, 0, 0);
+      }
+      ++ist;
+      return;
+    }
     issue_step([&](int j, unsigned oy, unsigned ox) {
       r.y[j] = __builtin_amdgcn_raw_buffer_load_b128(rsY, (int)oy, 0, 0);
       r.x[j] = __builtin_amdgcn_raw_buffer_load_b128(rsX, (int)ox, 0, 0);
@@ -210,6 +246,7 @@ __global__ void __launch_bounds__(NT) conv_wgrad_x_kernel(WxArgs g) {
   };
   // the lane's 16 B land where LDS-DMA would have put them (lane-linear from the wave's row base)
   auto store_set = [&](const RSet& r, int slot) {
+    if (abl & 2) return;                        // no ring writes
     char* Yb = reinterpret_cast<char*>(lds + slot * SLOT) + lane * 16;
     char* Xb = Yb + YST * 2;
 #pragma unroll
@@ -270,27 +307,42 @@ __global__ void __launch_bounds__(NT) conv_wgrad_x_kernel(WxArgs g) {
       }
     }
   }
+  unsigned long long ph[6] = {0, 0, 0, 0, 0, 0};   // ST: per-wave phase cycles (see phase())
   // one phase's compute: this wave's fragments of step st from ring slot rslot (issued before the
   // barrier that ends the wave's load segment), then its MFMA segment
-  auto phase = [&](int st, int rslot) {
+  auto phase = [&](int st, int rslot, unsigned long long t0, unsigned long long t1) {
     const unsigned base = lds0 + rslot * (SLOT * 2);
     constexpr int KS = C::KS;
     s16x4 al[KS][TM], ah[KS][TM], bl[KS][TN], bh[KS][TN];
 #pragma unroll
     for (int h = 0; h < KS; ++h) {               // sub-step h: rows h*32 .. h*32+31 of the slot images
       const unsigned yo = base + h * BR * BCO * 2, xo = base + h * BR * BKK * 2;
+      if (abl & 1) {                            // no fragment reads (operands left as they are)
+#pragma unroll
+        for (int i = 0; i < TM; ++i) { al[h][i] = s16x4{0, 0, 0, 0}; ah[h][i] = al[h][i]; }
+#pragma unroll
+        for (int j = 0; j < TN; ++j) { bl[h][j] = s16x4{0, 0, 0, 0}; bh[h][j] = bl[h][j]; }
+        continue;
+      }
 #pragma unroll
       for (int i = 0; i < TM; ++i) { al[h][i] = ds_tr16(yo + ya[i]); ah[h][i] = ds_tr16(yo + yb[i]); }
 #pragma unroll
       for (int j = 0; j < TN; ++j) { bl[h][j] = ds_tr16(xo + xa[j]); bh[h][j] = ds_tr16(xo + xb[j]); }
     }
+    unsigned long long t2 = 0, t3 = 0, t4 = 0, t5 = 0;
     if (RG) {                                   // the ring writes of this segment land before the barrier
       lgkm_wait();
+      if (ST) t2 = memtime_nowait();
       bar();
     } else {
+      if (ST) {
+        lgkm_wait();
+        t2 = memtime_nowait();
+      }
       bar();
       lgkm_wait();
     }
+    if (ST) t3 = memtime_nowait();
 #pragma unroll
     for (int h = 0; h < KS; ++h) {
 #pragma unroll
@@ -327,6 +379,10 @@ __global__ void __launch_bounds__(NT) conv_wgrad_x_kernel(WxArgs g) {
           for (int u = 0; u < 8; ++u)
             fb[j][u] = (short)f32_to_bf16(bn_relu_value(bf16_to_f32((cvl_bf16)fb[j][u]), sm[j], srs[j], fga[j], fbe[j]));
       }
+      if (abl & 16) {                           // no MFMAs (operands folded in by one add)
+        acc[0][0][0] += (float)(fa[0][0] + fb[0][0]);
+        continue;
+      }
 #pragma unroll
       for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -336,7 +392,18 @@ __global__ void __launch_bounds__(NT) conv_wgrad_x_kernel(WxArgs g) {
     }
     __builtin_amdgcn_s_setprio(0);
     __builtin_amdgcn_sched_barrier(0);
+    if (ST) t4 = memtime_nowait();
     bar();
+    if (ST) {
+      t5 = memtime_nowait();
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      ph[0] += t1 - t0;                         // load segment: wait for the step's data
+      ph[1] += t2 - t1;                         // ring writes / loads / fragment reads issued + landed
+      ph[2] += t3 - t2;                         // barrier after the load segment
+      ph[3] += t4 - t3;                         // MFMA segment (issue)
+      ph[4] += t5 - t4;                         // barrier after the MFMA segment
+      ph[5] += 1;
+    }
   };
 
   if constexpr (RG) {
@@ -354,17 +421,28 @@ __global__ void __launch_bounds__(NT) conv_wgrad_x_kernel(WxArgs g) {
     asm volatile("" ::: "memory");
     if (stamp) stamp[1] = wall_clock64();
     if (wco == 1) bar();                        // stagger: waves 4-7 run one barrier behind
+    unsigned long long t0 = 0, t1 = 0;
     for (int st = 0; st < nsteps; st += 2) {
+      if (ST) {
+        t0 = memtime_nowait();
+        wait_vm<2 * J>();
+        t1 = memtime_nowait();
+      }
       store_set(sb, 1);                         // step st+1
       __builtin_amdgcn_sched_barrier(0);
       load_set(sb);                             // step st+3
       __builtin_amdgcn_sched_barrier(0);
-      phase(st, 0);
+      phase(st, 0, t0, t1);
+      if (ST) {
+        t0 = memtime_nowait();
+        wait_vm<2 * J>();
+        t1 = memtime_nowait();
+      }
       store_set(sa, 0);                         // step st+2
       __builtin_amdgcn_sched_barrier(0);
       load_set(sa);                             // step st+4
       __builtin_amdgcn_sched_barrier(0);
-      phase(st + 1, 1);
+      phase(st + 1, 1, t0, t1);
     }
   } else {
     issue();
@@ -385,9 +463,11 @@ __global__ void __launch_bounds__(NT) conv_wgrad_x_kernel(WxArgs g) {
     if (wco == 1) bar();                        // stagger: waves 4-7 run one barrier behind
     int rslot = 0;
     for (int st = 0; st < nsteps; ++st) {
+      const unsigned long long t0 = ST ? memtime_nowait() : 0;
       wait_vm<PW>();                            // step st+1 (read next phase)
+      const unsigned long long t1 = ST ? memtime_nowait() : 0;
       issue();                                  // step st+3
-      phase(st, rslot);
+      phase(st, rslot, t0, t1);
       rslot = rslot == NSLOT - 1 ? 0 : rslot + 1;
     }
   }
@@ -417,6 +497,12 @@ __global__ void __launch_bounds__(NT) conv_wgrad_x_kernel(WxArgs g) {
       }
     }
   if (ST) {
+    if (g.phase && lane == 0) {
+      unsigned long long* q = g.phase + ((size_t)blockIdx.x * 8 + wave) * 8;
+      for (int i = 0; i < 6; ++i) q[i] = ph[i];
+      q[6] = nsteps;
+      q[7] = wco;
+    }
     wait_vm<0>();
     __syncthreads();
     if (stamp) stamp[3] = wall_clock64();
@@ -432,6 +518,8 @@ struct WxPlan {
 // measurement builds: CVL_WGX_STAMPS=1 stamps every launch into this buffer (cvl_debug_wgx_stamps)
 constexpr int kStampWgs = 16384;
 __device__ unsigned long long g_wgx_stamps[kStampWgs * 4];
+constexpr int kPhaseWgs = 2048;
+__device__ unsigned long long g_wgx_phase[kPhaseWgs * 8 * 8];
 int g_wgx_stamp_grid = 0;
 
 // Modelled time of s splits at tile width T: rounds of 256 workgroups (one per CU; 512 for T = 128) x 32-row steps
@@ -550,9 +638,14 @@ int cvl_conv_wgrad_x(const cvl_conv_desc* d, int ngroups, const void* x, const v
   if (!workspace || workspace_bytes < (p.slab > 16 ? p.slab : 16)) return CVL_EINVAL;
   static const bool stamps = cvl_env_flag("CVL_WGX_STAMPS");
   g.stamps = nullptr;
+  g.phase = nullptr;
+  g.ablate = 0;
   if (stamps && p.tiles * p.nsplit * ngroups <= kStampWgs) {
     void* sym = nullptr;
     if (hipGetSymbolAddress(&sym, HIP_SYMBOL(g_wgx_stamps)) == hipSuccess) g.stamps = (unsigned long long*)sym;
+    if (p.tiles * p.nsplit * ngroups <= kPhaseWgs && hipGetSymbolAddress(&sym, HIP_SYMBOL(g_wgx_phase)) == hipSuccess)
+      g.phase = (unsigned long long*)sym;
+    g.ablate = cvl_env_int("CVL_WGX_ABLATE", 0);
     g_wgx_stamp_grid = p.tiles * p.nsplit * ngroups;
   }
   g.a.src = reinterpret_cast<const cvl_bf16*>(x);
@@ -584,10 +677,14 @@ int cvl_conv_wgrad_x(const cvl_conv_desc* d, int ngroups, const void* x, const v
   static const bool dma = !cvl_env_flag("CVL_WGX_RG");
   if (fold) {
     hipLaunchKernelGGL((conv_wgrad_x_kernel<128, 64, false, true>), grid, dim3(NT), 0, s, g);
-  } else if (g.stamps) {
+  } else if (g.stamps && !dma) {
     if (p.T == 256) hipLaunchKernelGGL((conv_wgrad_x_kernel<256, BR, true, false, true>), grid, dim3(NT), 0, s, g);
     else if (p.SR == 64) hipLaunchKernelGGL((conv_wgrad_x_kernel<128, 64, true, false, true>), grid, dim3(NT), 0, s, g);
     else hipLaunchKernelGGL((conv_wgrad_x_kernel<128, BR, true, false, true>), grid, dim3(NT), 0, s, g);
+  } else if (g.stamps) {
+    if (p.T == 256) hipLaunchKernelGGL((conv_wgrad_x_kernel<256, BR, true>), grid, dim3(NT), 0, s, g);
+    else if (p.SR == 64) hipLaunchKernelGGL((conv_wgrad_x_kernel<128, 64, true>), grid, dim3(NT), 0, s, g);
+    else hipLaunchKernelGGL((conv_wgrad_x_kernel<128, BR, true>), grid, dim3(NT), 0, s, g);
   } else if (dma) {
     if (p.T == 256) hipLaunchKernelGGL((conv_wgrad_x_kernel<256, BR>), grid, dim3(NT), 0, s, g);
     else if (p.SR == 64) hipLaunchKernelGGL((conv_wgrad_x_kernel<128, 64>), grid, dim3(NT), 0, s, g);
@@ -631,4 +728,16 @@ extern "C" int cvl_conv_wgrad_fold(const cvl_conv_desc* d, const void* z, const 
   float* dws[1] = {dw};
   const int st = cvl_conv_wgrad_x(d, 1, z, dy, dws, beta, workspace, workspace_bytes, (hipStream_t)stream, &f);
   return st >= 0 ? st : CVL_ENOTTAKEN;
+}
+
+// Measurement hook (CVL_WGX_STAMPS=1): per-wave loop phase counters of the last stamped launch,
+// u64 [grid][8 waves][8] = shader cycles in (data wait, LDS segment, barrier 1, MFMA issue,
+// barrier 2), phase count, nsteps, wave group; returns the grid size (0: none).
+extern "C" int cvl_debug_wgx_phase(uint64_t* host, int max_wgs) {
+  const int n = g_wgx_stamp_grid < max_wgs ? g_wgx_stamp_grid : max_wgs;
+  if (n <= 0 || !host || g_wgx_stamp_grid > kPhaseWgs) return g_wgx_stamp_grid;
+  if (hipDeviceSynchronize() != hipSuccess) return -1;
+  if (hipMemcpyFromSymbol(host, HIP_SYMBOL(g_wgx_phase), (size_t)n * 8 * 8 * 8, 0, hipMemcpyDeviceToHost) != hipSuccess)
+    return -1;
+  return g_wgx_stamp_grid;
 }

@@ -51,6 +51,7 @@ def main():
     nn.conv_wgrad, nn.conv_wgrad_grouped = orig
     lib = _lib.load()
     buf = (ctypes.c_uint64 * (16384 * 4))()
+    phases = []
     print("| launch | per step | WGs | entry spread us | prologue us | loop us | epilogue us | WG total us | span us |")
     print("|---|---|---|---|---|---|---|---|---|")
     for key, (replay, d, ng) in calls.items():
@@ -70,6 +71,25 @@ def main():
                us((s[:, 1] - s[:, 0]).median()), us((s[:, 2] - s[:, 1]).median()), us((s[:, 3] - s[:, 2]).median()),
                us((s[:, 3] - s[:, 0]).median()), us(s[:, 3].max() - t0))
         print("| %s | %d | %d | %.1f | %.2f | %.1f | %.2f | %.1f | %.1f |" % row)
+        if hasattr(lib, "cvl_debug_wgx_phase"):
+            pb = (ctypes.c_uint64 * (n * 64))()
+            if lib.cvl_debug_wgx_phase(pb, n) > 0:
+                ph = torch.tensor(list(pb[:n * 64]), dtype=torch.float64).view(n, 8, 8)
+                steps = ph[:, :, 5].clamp(min=1)
+                per = ph[:, :, :5] / steps[..., None]               # cycles per step, per wave
+                for grp in (0, 1):
+                    m = per[ph[:, :, 7] == grp].median(0).values
+                    phases.append("| %s | g%d | %.0f | %.0f | %.0f | %.0f | %.0f | %.0f |" % (
+                        describe("wgrad", d, ng), grp, m[0], m[1], m[2], m[3], m[4], float(m.sum())))
+    if phases:
+        print()
+        print("Per-step loop phases (shader cycles, median wave of each group): data wait | LDS segment "
+              "(ring writes, loads, fragment reads landed) | barrier 1 | MFMA issue | barrier 2 | sum")
+        print()
+        print("| launch | group | wait | LDS | bar1 | MFMA | bar2 | sum |")
+        print("|---|---|---|---|---|---|---|---|")
+        for r in phases:
+            print(r)
 
 
 if __name__ == "__main__":
