@@ -49,10 +49,10 @@ __device__ __forceinline__ void bnsum_prefetch(const ConvArgs& a, const ConvSeg&
 
 // the epilogue's per-column bias of this lane (TN columns), loaded where its latency hides: a
 // persistent kernel fetches it at tile start, so the epilogue does not wait a memory round trip
-template <int BN, int WGM, int TN>
+template <int BN, int WGM, int TN, int NT = 512>
 __device__ __forceinline__ void epi_bias(const ConvArgs& a, const ConvSeg& S, int n0, int wn, int lane,
                                          float (&bcol)[TN]) {
-  constexpr int WN = BN / (8 / WGM);
+  constexpr int WN = BN / (NT / 64 / WGM);
 #pragma unroll
   for (int j = 0; j < TN; ++j) {
     const int n = n0 + wn * WN + j * 16 + (lane & 15);
@@ -78,7 +78,7 @@ __device__ __forceinline__ void conv_l_epilogue(const ConvArgs& a, const ConvSeg
     }
   };
   constexpr int BM = 256;
-  constexpr int WGN = 8 / WGM;
+  constexpr int WGN = NT / 64 / WGM;             // waves per tile row (NT / 64 waves as WGM x WGN)
   constexpr int WM = BM / WGM, WN = BN / WGN;
   const int lane = tid & 63;
   const int lr = lane & 15, lg = lane >> 4;
@@ -87,7 +87,7 @@ __device__ __forceinline__ void conv_l_epilogue(const ConvArgs& a, const ConvSeg
 #pragma unroll
     for (int j = 0; j < TN; ++j) bcol[j] = bpre[j];
   } else {
-    epi_bias<BN, WGM, TN>(a, S, n0, wn, lane, bcol);
+    epi_bias<BN, WGM, TN, NT>(a, S, n0, wn, lane, bcol);
   }
   if (a.dst_f32) {
     // fp32 destination (the head outputs the fused losses read): +bias, ReLU, unrounded 4-byte

@@ -11,7 +11,8 @@ import os
 import torch  # noqa: F401  (must precede the CDLL load, see module docstring)
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libcvlite_hip.so")
+# CVL_LIB: another build of the library (same-box A/B of two builds, tools/build_base.sh)
+LIB_PATH = os.environ.get("CVL_LIB") or os.path.join(_HERE, "libcvlite_hip.so")
 
 c_int, c_float, c_size_t, c_void_p = ctypes.c_int, ctypes.c_float, ctypes.c_size_t, ctypes.c_void_p
 P = c_void_p
