@@ -138,8 +138,8 @@ __device__ __forceinline__ void acc_store_dec(acc_u64* buf, long bc, int s, doub
   if (slots == kAccSlots) buf[acc_idx(bc, s, slots) + kAccBins] = kAccDecoded;
 }
 
-// ---- BN helpers shared by the BN kernels (nn_ops.hip) and the consumers that fold a BN into their
-// operand path (conv_igemm_p.hip, conv_wgrad_x.hip): one arithmetic, so every form is bit-identical
+// ---- BN helpers shared by the BN kernels (nn_ops.hip) and the fused BN-backward conv epilogues:
+// one arithmetic, so every form is bit-identical
 
 // per-image moments of one channel from its float64 (sum, sumsq); shared by the finalize kernels
 static __device__ __forceinline__ void bn_moments(double s1, double s2, int HW, float eps, float* mean, float* rstd,
@@ -183,11 +183,4 @@ static __device__ __forceinline__ void bn_running(const acc_u64* stats, int slot
 // from z to rebuild the ReLU mask of non-residual units (bit-identical to the forward's value)
 static __device__ __forceinline__ float bn_affine(float z, float m, float rs, float ga, float be) {
   return __builtin_fmaf(ga, (z - m) * rs, be);
-}
-
-// relu(bn_affine(z)) rounded to bf16 exactly as the BN apply stores it (ReLU as `o > 0 ? o : 0`:
-// -0 and NaN become +0, as there)
-static __device__ __forceinline__ float bn_relu_value(float z, float m, float rs, float ga, float be) {
-  const float o = bn_affine(z, m, rs, ga, be);
-  return o > 0.f ? o : 0.f;
 }

@@ -60,21 +60,6 @@ struct ConvSeg {
   const float* bias;
 };
 
-// A BN -> ReLU folded into a 1x1 consumer's A operand (cvl_conv_igemm_fold / cvl_conv_wgrad_fold):
-// the conv input is relu(BN(z)) of the previous unit, formed from z in registers, never stored.
-// stats non-null: the forward -- the kernel also finalizes (mean, rstd -> mr, running statistics);
-// stats null, mr non-null: a later reader (the weight gradient) of the stored mr.
-struct FoldArgs {
-  const acc_u64* stats;   // [B][K][2][slots] of the folded BN, or null
-  float* mr;              // [B][K][2] (mean, rstd)
-  float* run_mean;
-  float* run_var;
-  const float* gamma;
-  const float* beta;
-  float eps, momentum;
-  int slots;
-};
-
 struct ConvArgs {
   const cvl_bf16* src;
   void* dst;
@@ -101,7 +86,6 @@ struct ConvArgs {
   acc_u64* bsum;
   float bhi;
   const cvl_bf16* by;     // non-null: the ReLU mask comes from y > 0 (a residual unit's output), not bn(z)
-  FoldArgs fold;          // fold.mr null = off
 };
 
 // an exact-mode BN accumulator buffer decoded in place (nn_ops.hip; no-op in the float64 mode)
@@ -150,7 +134,6 @@ static inline int cvl_conv_prepare(const cvl_conv_desc* d, int bm, ConvArgs* a) 
   a->dbg = 0;
   a->bz = nullptr; a->bmr = nullptr; a->bga = nullptr; a->bbe = nullptr; a->bsum = nullptr; a->bhi = 0.f;
   a->by = nullptr;
-  a->fold = FoldArgs{};
   a->acc_slots = cvl_bn_acc_slots();
   a->nseg = d->nseg;
   a->B = d->B;

@@ -54,8 +54,6 @@ struct PCfg {
   static constexpr int DUMMY_B = BN == 64 ? 4 * 1024 : 0;  // sink of the BN = 64 filler pieces
   static constexpr int NS = (LDS_BYTES - RED_B - DUMMY_B) / SLOT_B;
   static constexpr int D = NS - 1;                         // K-tiles in flight
-  // what the ring leaves over: the folded BN's tables ([K] (gamma, beta) + [images][K] (mean, rstd))
-  static constexpr int FOLD_B = LDS_BYTES - RED_B - DUMMY_B - NS * SLOT_B;
   static_assert(D >= 2, "ring too short");
 };
 
@@ -90,18 +88,11 @@ __device__ __forceinline__ s16x8 gload16_untracked(const void* p) {
 }
 __device__ __forceinline__ void pin16(s16x8& v) { asm volatile("" : "+v"(v)); }
 
-// FOLD: the A operand is relu(BN(z)) of the previous unit (a.fold, FoldArgs), formed from z in
-// registers right after the fragment reads -- bf16(relu(fma(gamma, (z - mean) * rstd, beta))), the
-// BN apply's own arithmetic, so the MFMAs see the very operand the unfused form stored and read
-// back.  The workgroup finalizes the BN itself before its stream starts: (mean, rstd) of the images
-// its chunk touches into LDS (decoded from the statistics, bn_moments), stored to a.fold.mr once per
-// image (by the N-tile-0 workgroup holding the image's first tile), and the running statistics
-// advanced for the channels c == L (mod G).  The BN apply launch and its write + re-read are gone.
-template <int BN, bool RELU, bool F32, int BS = 0, bool ACC = false, bool FOLD = false>
+template <int BN, bool RELU, bool F32, int BS = 0, bool ACC = false>
 __global__ void __launch_bounds__(NT) conv_igemm_p_kernel(ConvArgs a, int ntiles) {
   using C = PCfg<BN>;
   constexpr int TM = C::TM, TN = C::TN, NS = C::NS, D = C::D;
-  __shared__ __attribute__((aligned(16))) char lds[C::NS * C::SLOT_B + C::RED_B + C::DUMMY_B + (FOLD ? C::FOLD_B : 0)];
+  __shared__ __attribute__((aligned(16))) char lds[C::NS * C::SLOT_B + C::RED_B + C::DUMMY_B];
   float* red = reinterpret_cast<float*>(lds + NS * C::SLOT_B);
   char* dummy = lds + NS * C::SLOT_B + C::RED_B;
 
@@ -456,34 +447,6 @@ __global__ void __launch_bounds__(NT) conv_igemm_p_kernel(ConvArgs a, int ntiles
   // prologue: K-tiles 0 .. D-1 in flight
 #pragma unroll
   for (int d = 0; d < D; ++d) issue();
-  // the folded BN's tables (while the prologue lands; the barrier's vmcnt(0) covers both)
-  float2* fgb = reinterpret_cast<float2*>(lds + NS * C::SLOT_B + C::RED_B + C::DUMMY_B);
-  float2* fmr = fgb + a.K;
-  int fb_lo = 0;
-  if (FOLD) {
-    const FoldArgs& f = a.fold;
-    const int m_first = mt0 * BM;
-    const int m_last = min((mt0 + my_tiles) * BM, S.rows) - 1;
-    fb_lo = m_first / HWr;
-    const int nimg = my_tiles > 0 ? m_last / HWr - fb_lo + 1 : 0;
-    for (int k = tid; k < a.K; k += NT) fgb[k] = float2{f.gamma[k], f.beta[k]};
-    for (int e = tid; e < nimg * a.K; e += NT) {
-      const int bi = e / a.K, k = e - bi * a.K, b = fb_lo + bi;
-      const long bc = (long)b * a.K + k;
-      float mm, rr;
-      double var;
-      bn_moments(acc_dec(f.stats, bc, 0, f.slots), acc_dec(f.stats, bc, 1, f.slots), HWr, f.eps, &mm, &rr, &var);
-      fmr[e] = float2{mm, rr};
-      if (L % ntn == 0 && (long)b * HWr >= (long)m_first) {
-        f.mr[bc * 2] = mm;
-        f.mr[bc * 2 + 1] = rr;
-      }
-    }
-    if (f.run_mean)
-      for (int c = L + tid * G; c < a.K; c += NT * G)
-        bn_running(f.stats, f.slots, a.B, a.K, c, HWr, f.eps, f.momentum, f.run_mean, f.run_var);
-    __syncthreads();
-  }
   int rslot = 0, ck = 0, ct = 0;
   for (int g = 0; g < total; ++g) {
     wait_vm<(D - 1) * C::PW>();                    // this wave's pieces of K-tile g landed
@@ -531,24 +494,6 @@ __global__ void __launch_bounds__(NT) conv_igemm_p_kernel(ConvArgs a, int ntiles
     for (int i = 0; i < TM; ++i) fa[i] = *reinterpret_cast<const s16x8*>(sl + fao[i]);
 #pragma unroll
     for (int j = 0; j < TN; ++j) fb[j] = *reinterpret_cast<const s16x8*>(sl + fbo[j]);
-    if (FOLD) {                                     // A = bf16(relu(BN(z))), channels k0 .. k0 + 7
-      const int k0 = ck * BK + lg * 8;
-      const int bi = ((mt0 + ct) * BM) / HWr - fb_lo;
-      const float4* pm = reinterpret_cast<const float4*>(fmr + bi * a.K + k0);
-      const float4* pg = reinterpret_cast<const float4*>(fgb + k0);
-      float4 m4[4], g4[4];
-#pragma unroll
-      for (int h = 0; h < 4; ++h) { m4[h] = pm[h]; g4[h] = pg[h]; }
-#pragma unroll
-      for (int i = 0; i < TM; ++i)
-#pragma unroll
-        for (int u = 0; u < 8; ++u) {
-          const float4 mq = m4[u >> 1], gq = g4[u >> 1];
-          const float mm = (u & 1) ? mq.z : mq.x, rr = (u & 1) ? mq.w : mq.y;
-          const float ga = (u & 1) ? gq.z : gq.x, be = (u & 1) ? gq.w : gq.y;
-          fa[i][u] = (short)f32_to_bf16(bn_relu_value(bf16_to_f32((cvl_bf16)fa[i][u]), mm, rr, ga, be));
-        }
-    }
 #pragma unroll
     for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -602,23 +547,6 @@ int cvl_conv_igemm_p(const cvl_conv_desc* d, const ConvArgs& a0, hipStream_t s) 
   if (grid < 1) return -1;
   ConvArgs a = a0;
   a.dbg = cvl_env_int("CVL_P_ABLATE", 0);
-  if (a.fold.mr) {                 // folded BN -> ReLU operand: plain bf16 forward, one image per tile
-    if (d->mode != CVL_CONV_FWD || a.dst_f32 || a.relu_out || a.beta != 0.f || a.bsum || a.stride != 1 ||
-        (q.Hr * q.Wr) % BM || !a.fold.stats || (use != 64 && use != 128))
-      return -1;
-    const int tpi = q.Hr * q.Wr / BM, nmc = grid / ntn, mchunk = (a.m_tiles + nmc - 1) / nmc;
-    int nimg = 0;
-    for (int c = 0; c < nmc; ++c) {
-      const int t0 = c * mchunk, t1 = min(t0 + mchunk, a.m_tiles) - 1;
-      if (t1 >= t0) nimg = max(nimg, t1 / tpi - t0 / tpi + 1);
-    }
-    const int fold_b = use == 128 ? PCfg<128>::FOLD_B : PCfg<64>::FOLD_B;
-    if ((long)(nimg + 1) * a.K * 8 > fold_b) return -1;
-    g_cvl_conv_last_kernel = CVL_CK_P;
-    if (use == 128) hipLaunchKernelGGL((conv_igemm_p_kernel<128, false, false, 0, false, true>), dim3(grid), dim3(NT), 0, s, a, ntiles);
-    else hipLaunchKernelGGL((conv_igemm_p_kernel<64, false, false, 0, false, true>), dim3(grid), dim3(NT), 0, s, a, ntiles);
-    return cvl_launch_status();
-  }
   g_cvl_conv_last_kernel = CVL_CK_P;
 #define CVL_P_LAUNCH(BN_, ACC_)                                                                                 \
   do {                                                                                                      \
@@ -642,30 +570,3 @@ int cvl_conv_igemm_p(const cvl_conv_desc* d, const ConvArgs& a0, hipStream_t s) 
   return cvl_launch_status();
 }
 
-// A 1x1 forward whose input is relu(BN(z)) of the previous unit, the BN applied in the operand path
-// (conv_igemm_p.hip FOLD) and finalized inside the launch; CVL_ENOTTAKEN when P cannot take it.
-extern "C" int cvl_conv_igemm_fold(const cvl_conv_desc* d, const void* z, void* dst, uint64_t* bn_stats,
-                                   uint64_t* fold_stats, float* fold_mean_rstd, float* fold_run_mean,
-                                   float* fold_run_var, const float* fold_gamma, const float* fold_beta,
-                                   float fold_eps, float fold_momentum, cvl_stream_t stream) {
-  hipStream_t s = (hipStream_t)stream;
-  CVL_CHECK_ARG(d && z && dst && fold_stats && fold_mean_rstd && fold_gamma && fold_beta);
-  CVL_CHECK_ARG((fold_run_mean == nullptr) == (fold_run_var == nullptr));
-  if (d->prec != CVL_PREC_BF16 || d->mode != CVL_CONV_FWD || d->KH != 1 || d->KW != 1 || d->nseg != 1)
-    return CVL_ENOTTAKEN;
-  ConvArgs a;
-  int st = cvl_conv_prepare(d, BM, &a);
-  if (st) return st;
-  if (d->dst_f32 || d->ld_dst % 8 || d->dst_coff % 8 || d->n_store % 8 || d->Cin % 32) return CVL_ENOTTAKEN;
-  if (bn_stats && (a.seg[0].Hr * a.seg[0].Wr) % BM) return CVL_ENOTTAKEN;
-  a.src = reinterpret_cast<const cvl_bf16*>(z);
-  a.dst = dst;
-  a.stats = reinterpret_cast<acc_u64*>(bn_stats);
-  a.fold = FoldArgs{reinterpret_cast<const acc_u64*>(fold_stats), fold_mean_rstd, fold_run_mean, fold_run_var,
-                    fold_gamma, fold_beta, fold_eps, fold_momentum, a.acc_slots};
-  st = cvl_bn_acc_prepare(fold_stats, 2L * d->B * d->Cin, s);
-  if (st) return st;
-  g_cvl_conv_last_kernel = CVL_CK_NONE;
-  const int pst = cvl_conv_igemm_p(d, a, s);
-  return pst >= 0 ? pst : CVL_ENOTTAKEN;
-}

@@ -286,8 +286,7 @@ int cvl_conv_wgrad_sn(const cvl_conv_desc* d, int ngroups, const void* x, const 
 
 long cvl_conv_wgrad_x_workspace(const cvl_conv_desc* d, int ngroups);
 int cvl_conv_wgrad_x(const cvl_conv_desc* d, int ngroups, const void* x, const void* dy, float* const* dw,
-                     float beta, void* workspace, size_t workspace_bytes, hipStream_t s,
-                     const FoldArgs* fold = nullptr);
+                     float beta, void* workspace, size_t workspace_bytes, hipStream_t s);
 
 namespace {
 

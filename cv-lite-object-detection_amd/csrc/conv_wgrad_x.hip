@@ -77,26 +77,6 @@ __device__ __forceinline__ unsigned long long memtime_nowait() {
   asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t) :: "memory");
   return t;
 }
-// loads the compiler does not track: issued before the prologue DMAs, so the prologue's counted
-// wait retires them (a tracked load used in the loop would make the compiler drain the ring there)
-__device__ __forceinline__ wf32x2 gload8_untracked(const void* p) {
-  wf32x2 v;
-  asm volatile("global_load_dwordx2 %0, %1, off" : "=v"(v) : "v"(p) : "memory");
-  return v;
-}
-__device__ __forceinline__ float gload4_untracked(const void* p) {
-  float v;
-  asm volatile("global_load_dword %0, %1, off" : "=v"(v) : "v"(p) : "memory");
-  return v;
-}
-constexpr int kFoldImgs = 4;              // images one workgroup's rows may span on the FOLD path
-
-// FOLD (1x1, stride 1, one segment, H*W % SR == 0): the x operand is relu(BN(z)) of the previous
-// unit (a.fold: the forward's stored (mean, rstd), gamma, beta), formed from z in registers after
-// the transposed fragment reads -- bf16(relu(fma(gamma, (z - mean) * rstd, beta))), the BN apply's
-// arithmetic, so the MFMAs see the operand the unfused form stored.  A lane's x fragment is 8 rows
-// of ONE channel (its column), so a step needs one (mean, rstd, gamma, beta) per fragment column;
-// the values for the <= kFoldImgs images of the workgroup's rows are loaded once, before the stream.
 typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 
 // RG (register-staged ring, the production form): each lane loads its 16-B pieces of a step by
@@ -106,10 +86,9 @@ typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 // per piece and fills at ~30 GB/s per CU (profiles/r04_ubench_ldsdma.md); the register path costs
 // ~20 cycles per piece.  Same MFMA order: bit-identical results.  Measured at the DMA form's speed
 // (loop 19.1 vs 17.3 us at 1x1 1024->256 @ 32^2), so opt-in (CVL_WGX_RG=1) for diagnosis.
-template <int T, int SR = BR, bool ST = false, bool FOLD = false, bool RG = false>
+template <int T, int SR = BR, bool ST = false, bool RG = false>
 __global__ void __launch_bounds__(NT) conv_wgrad_x_kernel(WxArgs g) {
   using C = WxCfg<T, SR>;
-  static_assert(!(RG && FOLD), "the FOLD form runs on the DMA ring");
   // ST: wall-clock stamps of thread 0 (entry, prologue landed, loop done, epilogue stored)
   unsigned long long* stamp = (ST && threadIdx.x == 0) ? g.stamps + blockIdx.x * 4 : nullptr;
   if (stamp) stamp[0] = wall_clock64();
@@ -287,30 +266,10 @@ __global__ void __launch_bounds__(NT) conv_wgrad_x_kernel(WxArgs g) {
   }
 
   constexpr int PW = 2 * J;                     // DMA pieces per wave per step
-  // FOLD parameters of this lane's TN fragment columns, images fb_lo .. fb_lo + kFoldImgs - 1
-  wf32x2 fmr[FOLD ? kFoldImgs : 1][TN];
-  float fga[TN], fbe[TN];
-  int fb_lo = 0, fhw = 1;
-  if (FOLD) {
-    fhw = a.seg[0].Hr * a.seg[0].Wr;
-    fb_lo = m_lo / fhw;
-#pragma unroll
-    for (int j = 0; j < TN; ++j) {
-      int kc = k0 + (wk * TN + j) * 16 + lr;
-      kc = kc < a.K ? kc : a.K - 1;
-      fga[j] = gload4_untracked(a.fold.gamma + kc);
-      fbe[j] = gload4_untracked(a.fold.beta + kc);
-#pragma unroll
-      for (int q = 0; q < kFoldImgs; ++q) {
-        const int b = min(fb_lo + q, a.B - 1);
-        fmr[q][j] = gload8_untracked(a.fold.mr + ((long)b * a.K + kc) * 2);
-      }
-    }
-  }
   unsigned long long ph[6] = {0, 0, 0, 0, 0, 0};   // ST: per-wave phase cycles (see phase())
   // one phase's compute: this wave's fragments of step st from ring slot rslot (issued before the
   // barrier that ends the wave's load segment), then its MFMA segment
-  auto phase = [&](int st, int rslot, unsigned long long t0, unsigned long long t1) {
+  auto phase = [&](unsigned long long t0, unsigned long long t1, int rslot) {
     const unsigned base = lds0 + rslot * (SLOT * 2);
     constexpr int KS = C::KS;
     s16x4 al[KS][TM], ah[KS][TM], bl[KS][TN], bh[KS][TN];
@@ -352,19 +311,6 @@ __global__ void __launch_bounds__(NT) conv_wgrad_x_kernel(WxArgs g) {
     }
     __builtin_amdgcn_sched_barrier(0);
     __builtin_amdgcn_s_setprio(1);
-    // FOLD: this step's image (uniform; H*W % SR == 0 keeps a step inside one image)
-    float sm[TN], srs[TN];
-    if (FOLD) {
-      const int bi = (m_lo + st * SR) / fhw - fb_lo;
-#pragma unroll
-      for (int j = 0; j < TN; ++j) {
-        wf32x2 v = fmr[0][j];
-#pragma unroll
-        for (int q = 1; q < kFoldImgs; ++q) v = bi == q ? fmr[q][j] : v;
-        sm[j] = v.x;
-        srs[j] = v.y;
-      }
-    }
 #pragma unroll
     for (int h = 0; h < KS; ++h) {
       s16x8 fa[TM], fb[TN];
@@ -372,13 +318,6 @@ __global__ void __launch_bounds__(NT) conv_wgrad_x_kernel(WxArgs g) {
       for (int i = 0; i < TM; ++i) fa[i] = tr_join(al[h][i], ah[h][i]);
 #pragma unroll
       for (int j = 0; j < TN; ++j) fb[j] = tr_join(bl[h][j], bh[h][j]);
-      if (FOLD) {
-#pragma unroll
-        for (int j = 0; j < TN; ++j)
-#pragma unroll
-          for (int u = 0; u < 8; ++u)
-            fb[j][u] = (short)f32_to_bf16(bn_relu_value(bf16_to_f32((cvl_bf16)fb[j][u]), sm[j], srs[j], fga[j], fbe[j]));
-      }
       if (abl & 16) {                           // no MFMAs (operands folded in by one add)
         acc[0][0][0] += (float)(fa[0][0] + fb[0][0]);
         continue;
@@ -432,7 +371,7 @@ __global__ void __launch_bounds__(NT) conv_wgrad_x_kernel(WxArgs g) {
       __builtin_amdgcn_sched_barrier(0);
       load_set(sb);                             // step st+3
       __builtin_amdgcn_sched_barrier(0);
-      phase(st, 0, t0, t1);
+      phase(t0, t1, 0);
       if (ST) {
         t0 = memtime_nowait();
         wait_vm<2 * J>();
@@ -442,21 +381,13 @@ __global__ void __launch_bounds__(NT) conv_wgrad_x_kernel(WxArgs g) {
       __builtin_amdgcn_sched_barrier(0);
       load_set(sa);                             // step st+4
       __builtin_amdgcn_sched_barrier(0);
-      phase(st + 1, 1, t0, t1);
+      phase(t0, t1, 1);
     }
   } else {
     issue();
     issue();
     issue();
-    wait_vm<2 * PW>();                          // (also retires the FOLD parameter loads)
-    if (FOLD) {
-#pragma unroll
-      for (int j = 0; j < TN; ++j) {
-        asm volatile("" : "+v"(fga[j]), "+v"(fbe[j]));
-#pragma unroll
-        for (int q = 0; q < kFoldImgs; ++q) asm volatile("" : "+v"(fmr[q][j]));
-      }
-    }
+    wait_vm<2 * PW>();
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
     if (stamp) stamp[1] = wall_clock64();
@@ -467,7 +398,7 @@ __global__ void __launch_bounds__(NT) conv_wgrad_x_kernel(WxArgs g) {
       wait_vm<PW>();                            // step st+1 (read next phase)
       const unsigned long long t1 = ST ? memtime_nowait() : 0;
       issue();                                  // step st+3
-      phase(st, rslot, t0, t1);
+      phase(t0, t1, rslot);
       rslot = rslot == NSLOT - 1 ? 0 : rslot + 1;
     }
   }
@@ -619,22 +550,10 @@ long cvl_conv_wgrad_x_workspace(const cvl_conv_desc* d, int ngroups) {
 
 // Returns -1 when the launch does not qualify (the caller takes another kernel), else a status.
 int cvl_conv_wgrad_x(const cvl_conv_desc* d, int ngroups, const void* x, const void* dy, float* const* dw,
-                     float beta, void* workspace, size_t workspace_bytes, hipStream_t s, const FoldArgs* fold = nullptr) {
+                     float beta, void* workspace, size_t workspace_bytes, hipStream_t s) {
   WxArgs g;
   WxPlan p;
   if (!wx_plan(d, ngroups, &g.a, &p)) return -1;
-  if (fold) {                                   // the FOLD form: 1x1, 64-row steps inside one image
-    const ConvSeg& q = g.a.seg[0];
-    const int hw = q.Hr * q.Wr;
-    if (ngroups != 1 || d->KH != 1 || d->KW != 1 || d->stride != 1 || g.a.nseg != 1 || p.T != 128 ||
-        p.SR != 64 || hw % 64 || q.src_img != (long)hw || q.Hs != q.Hr || q.Ws != q.Wr)
-      return -1;
-    for (int sp = 0; sp < p.nsplit; ++sp) {
-      const int m0 = sp * p.chunk, m1 = min(m0 + p.chunk, min(p.g_m1[0], q.rows)) - 1;
-      if (m1 >= m0 && m1 / hw - m0 / hw + 1 > kFoldImgs) return -1;
-    }
-    g.a.fold = *fold;
-  }
   if (!workspace || workspace_bytes < (p.slab > 16 ? p.slab : 16)) return CVL_EINVAL;
   static const bool stamps = cvl_env_flag("CVL_WGX_STAMPS");
   g.stamps = nullptr;
@@ -675,12 +594,10 @@ int cvl_conv_wgrad_x(const cvl_conv_desc* d, int ngroups, const void* x, const v
   const dim3 grid(p.tiles * p.nsplit * ngroups);
   // CVL_WGX_RG=1: the register-staged ring (measured no faster than the LDS-DMA ring: DESIGN §7)
   static const bool dma = !cvl_env_flag("CVL_WGX_RG");
-  if (fold) {
-    hipLaunchKernelGGL((conv_wgrad_x_kernel<128, 64, false, true>), grid, dim3(NT), 0, s, g);
-  } else if (g.stamps && !dma) {
-    if (p.T == 256) hipLaunchKernelGGL((conv_wgrad_x_kernel<256, BR, true, false, true>), grid, dim3(NT), 0, s, g);
-    else if (p.SR == 64) hipLaunchKernelGGL((conv_wgrad_x_kernel<128, 64, true, false, true>), grid, dim3(NT), 0, s, g);
-    else hipLaunchKernelGGL((conv_wgrad_x_kernel<128, BR, true, false, true>), grid, dim3(NT), 0, s, g);
+  if (g.stamps && !dma) {
+    if (p.T == 256) hipLaunchKernelGGL((conv_wgrad_x_kernel<256, BR, true, true>), grid, dim3(NT), 0, s, g);
+    else if (p.SR == 64) hipLaunchKernelGGL((conv_wgrad_x_kernel<128, 64, true, true>), grid, dim3(NT), 0, s, g);
+    else hipLaunchKernelGGL((conv_wgrad_x_kernel<128, BR, true, true>), grid, dim3(NT), 0, s, g);
   } else if (g.stamps) {
     if (p.T == 256) hipLaunchKernelGGL((conv_wgrad_x_kernel<256, BR, true>), grid, dim3(NT), 0, s, g);
     else if (p.SR == 64) hipLaunchKernelGGL((conv_wgrad_x_kernel<128, 64, true>), grid, dim3(NT), 0, s, g);
@@ -690,11 +607,11 @@ int cvl_conv_wgrad_x(const cvl_conv_desc* d, int ngroups, const void* x, const v
     else if (p.SR == 64) hipLaunchKernelGGL((conv_wgrad_x_kernel<128, 64>), grid, dim3(NT), 0, s, g);
     else hipLaunchKernelGGL((conv_wgrad_x_kernel<128, BR>), grid, dim3(NT), 0, s, g);
   } else if (p.T == 256) {
-    hipLaunchKernelGGL((conv_wgrad_x_kernel<256, BR, false, false, true>), grid, dim3(NT), 0, s, g);
+    hipLaunchKernelGGL((conv_wgrad_x_kernel<256, BR, false, true>), grid, dim3(NT), 0, s, g);
   } else if (p.SR == 64) {
-    hipLaunchKernelGGL((conv_wgrad_x_kernel<128, 64, false, false, true>), grid, dim3(NT), 0, s, g);
+    hipLaunchKernelGGL((conv_wgrad_x_kernel<128, 64, false, true>), grid, dim3(NT), 0, s, g);
   } else {
-    hipLaunchKernelGGL((conv_wgrad_x_kernel<128, BR, false, false, true>), grid, dim3(NT), 0, s, g);
+    hipLaunchKernelGGL((conv_wgrad_x_kernel<128, BR, false, true>), grid, dim3(NT), 0, s, g);
   }
   int st = cvl_launch_status();
   if (st || g.direct) return st;
@@ -710,34 +627,6 @@ extern "C" int cvl_debug_wgx_stamps(uint64_t* host, int max_wgs) {
   if (n <= 0 || !host) return g_wgx_stamp_grid;
   if (hipDeviceSynchronize() != hipSuccess) return -1;
   if (hipMemcpyFromSymbol(host, HIP_SYMBOL(g_wgx_stamps), (size_t)n * 32, 0, hipMemcpyDeviceToHost) != hipSuccess)
-    return -1;
-  return g_wgx_stamp_grid;
-}
-
-// The weight gradient of a 1x1 conv whose input is relu(BN(z)) of the previous unit, the BN applied
-// in the x-operand path (FOLD above) from the stored (mean, rstd); CVL_ENOTTAKEN when the X path
-// cannot take it (the caller then materialises the input and runs cvl_conv_wgrad).
-extern "C" int cvl_conv_wgrad_fold(const cvl_conv_desc* d, const void* z, const float* fold_mean_rstd,
-                                   const float* fold_gamma, const float* fold_beta, const void* dy, float* dw,
-                                   float beta, void* workspace, size_t workspace_bytes, cvl_stream_t stream) {
-  CVL_CHECK_ARG(d && z && fold_mean_rstd && fold_gamma && fold_beta && dy && dw);
-  if (d->prec != CVL_PREC_BF16) return CVL_ENOTTAKEN;
-  const int gs = cvl_wgrad_defer_guard(dw, (hipStream_t)stream);
-  if (gs) return gs;
-  FoldArgs f{nullptr, const_cast<float*>(fold_mean_rstd), nullptr, nullptr, fold_gamma, fold_beta, 0.f, 0.f, 1};
-  float* dws[1] = {dw};
-  const int st = cvl_conv_wgrad_x(d, 1, z, dy, dws, beta, workspace, workspace_bytes, (hipStream_t)stream, &f);
-  return st >= 0 ? st : CVL_ENOTTAKEN;
-}
-
-// Measurement hook (CVL_WGX_STAMPS=1): per-wave loop phase counters of the last stamped launch,
-// u64 [grid][8 waves][8] = shader cycles in (data wait, LDS segment, barrier 1, MFMA issue,
-// barrier 2), phase count, nsteps, wave group; returns the grid size (0: none).
-extern "C" int cvl_debug_wgx_phase(uint64_t* host, int max_wgs) {
-  const int n = g_wgx_stamp_grid < max_wgs ? g_wgx_stamp_grid : max_wgs;
-  if (n <= 0 || !host || g_wgx_stamp_grid > kPhaseWgs) return g_wgx_stamp_grid;
-  if (hipDeviceSynchronize() != hipSuccess) return -1;
-  if (hipMemcpyFromSymbol(host, HIP_SYMBOL(g_wgx_phase), (size_t)n * 8 * 8 * 8, 0, hipMemcpyDeviceToHost) != hipSuccess)
     return -1;
   return g_wgx_stamp_grid;
 }

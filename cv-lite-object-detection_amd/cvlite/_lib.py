@@ -30,8 +30,6 @@ SIGNATURES = {
     "cvl_fcos_v1_decode": (c_int, [P, c_int, c_int, c_int, c_float, c_float, P, P]),
     "cvl_conv_igemm_workspace_size": (c_size_t, [P]),
     "cvl_conv_igemm": (c_int, [P, P, P, P, P, c_size_t, P]),
-    "cvl_conv_igemm_fold": (c_int, [P, P, P, P, P, P, P, P, P, P, c_float, c_float, P]),
-    "cvl_conv_wgrad_fold": (c_int, [P, P, P, P, P, P, P, c_float, P, c_size_t, P]),
     "cvl_conv_igemm_last_kernel": (c_int, []),
     "cvl_conv_kernel_name": (ctypes.c_char_p, [c_int]),
     "cvl_centernet_peak_decode_workspace_size": (ctypes.c_size_t, [c_int, c_int, c_int, c_int]),
@@ -194,16 +192,9 @@ def load():
     return _lib
 
 
-ENOTTAKEN = 2       # CVL_ENOTTAKEN: a fused form that does not apply; nothing enqueued
-FUSED = {"cvl_conv_igemm_fold", "cvl_conv_wgrad_fold"}
-
-
 def call(name, *args):
-    """Calls a C entry point; raises on an error status.  The fused entry points (FUSED) return
-    False on CVL_ENOTTAKEN (nothing enqueued: run the unfused form), True when they ran."""
+    """Calls a C entry point; raises on an error status."""
     st = getattr(load(), name)(*args)
-    if st == ENOTTAKEN and name in FUSED:
-        return False
     if st != 0:
         if st >= 1000:
             raise CvlError("%s failed: hipError %d" % (name, st - 1000))

@@ -202,21 +202,6 @@ class Conv(object):
                             self.cin, self.cin if ld_dst is None else ld_dst, segs, beta=beta)
 
     # ---- plain single-map helpers -----------------------------------------------------------------
-    def fwd_folded(self, f, B, H, W, stats=None):
-        """Forward of relu(BN(z)) (f: a pending FoldedInput) with that BN finalized and applied in
-        the operand path (cvl_conv_igemm_fold); returns (out, x) where x is what the weight
-        gradient reads: f itself, or the materialised input when the fused launch does not apply."""
-        Ho, Wo, _, _ = self.out_hw(H, W)
-        out = torch.empty((B, Ho, Wo, self.cout), dtype=f.z.dtype, device=f.z.device)
-        d = self.fwd_desc(B, [nn.seg(Ho, Wo, H, W, self.wf, self.bias_arg())], ld_dst=self.cout)
-        bn = f.bn
-        if nn.conv_igemm_fold(d, f.z, out, stats, f.stats, f.mr, bn.run_mean, bn.run_var, bn.gamma, bn.beta,
-                              bn.eps, bn.momentum):
-            return out, f
-        x = f.finalize_apply(B, H * W)
-        nn.conv_igemm(d, x, out, stats)
-        return out, x
-
     def fwd(self, x, B, H, W, out=None, stats=None, relu_out=False, relu_in=False):
         Ho, Wo, _, _ = self.out_hw(H, W)
         if out is None:
@@ -227,18 +212,10 @@ class Conv(object):
         return out, Ho, Wo
 
     def wgrad(self, x, dy, B, H, W, relu_in=False, dw=None, beta=0.0, bias=True):
-        """x: the input, or a FoldedInput (relu(BN(z)) never stored: cvl_conv_wgrad_fold, else it is
-        materialised here first)."""
         Ho, Wo, _, _ = self.out_hw(H, W)
         d = self.fwd_desc(B, [nn.seg(Ho, Wo, H, W, self.wf, None)], ld_dst=self.cout_pad_ld(dy),
                           relu_in=relu_in)
-        if isinstance(x, FoldedInput):
-            if nn.conv_wgrad_fold(d, x.z, x.mr, x.bn.gamma, x.bn.beta, dy, self.dw if dw is None else dw, beta):
-                x = None
-            else:
-                x = x.materialise(B, H * W)
-        if x is not None:
-            nn.conv_wgrad(d, x, dy, self.dw if dw is None else dw, beta)
+        nn.conv_wgrad(d, x, dy, self.dw if dw is None else dw, beta)
         if self.has_bias and bias:
             nn.bias_grad(dy, self.cout_pad_ld(dy), 0, self.cout, 0, Ho * Wo, Ho * Wo, B, self.db)
 
@@ -273,26 +250,6 @@ class Conv(object):
 FUSE_BNSUM = os.environ.get("CVL_NO_BNSUM_FUSE", "0") != "1"
 # ... and a residual unit's (BN3) first pass into the next block's conv1 data gradient (CVL_NO_BNSUM_RES=1: off)
 FUSE_BNSUM_RES = FUSE_BNSUM and os.environ.get("CVL_NO_BNSUM_RES", "0") != "1"
-
-class FoldedInput(object):
-    """relu(BN(z)) of a BN -> ReLU unit that its 1x1 consumer forms in its operand path instead of
-    reading it from memory (cvl_conv_igemm_fold / cvl_conv_wgrad_fold): z, the BN statistics, the
-    (mean, rstd) buffer the consumer's forward fills, and the BatchNorm."""
-
-    def __init__(self, z, stats, mr, bn):
-        self.z, self.stats, self.mr, self.bn = z, stats, mr, bn
-
-    def finalize_apply(self, B, HW):          # the unfused forward: finalize + apply, stored
-        y = torch.empty_like(self.z)
-        nn.bn_finalize_apply(self.stats, self.mr, self.bn.run_mean, self.bn.run_var, self.z, self.bn.gamma,
-                             self.bn.beta, None, y, B, HW, self.bn.c, 1, self.bn.eps, self.bn.momentum)
-        return y
-
-    def materialise(self, B, HW):              # the input again from the stored (mean, rstd)
-        y = torch.empty_like(self.z)
-        nn.bn_apply(self.z, self.mr, self.bn.gamma, self.bn.beta, None, y, B, HW, self.bn.c, 1)
-        return y
-
 
 class StatsArena(object):
     """One zeroed buffer holding the (sum, sumsq) BN statistics of every conv of a forward pass as
@@ -377,22 +334,18 @@ class ConvBN(object):
                 residual_bn=None):
         """defer (training, no ReLU): the BN is not applied here -- returns (pending, saved) where
         pending = (z, stats, mean_rstd, BatchNorm) is the consumer's residual_bn, which forms this
-        unit's output and finalize inside its own BN launch (the projection shortcut)."""
+        unit's output and finalize inside its own BN launch (the projection shortcut).  Its saved
+        y is None: the backward of such a unit reads z only (no ReLU mask, no residual)."""
         c = self.conv.cout
         Ho, Wo, _, _ = self.conv.out_hw(H, W)
         stats = None
         if train:
-            dev = x.z.device if isinstance(x, FoldedInput) else x.device
-            stats = arena.take(B, c) if arena is not None else nn.bn_acc(B, c, dev)
-        if isinstance(x, FoldedInput):        # the input's BN -> ReLU is applied in this conv's operand path
-            z, x = self.conv.fwd_folded(x, B, H, W, stats=stats)
-        else:
-            z, _, _ = self.conv.fwd(x, B, H, W, stats=stats)
+            stats = arena.take(B, c) if arena is not None else nn.bn_acc(B, c, x.device)
+        z, _, _ = self.conv.fwd(x, B, H, W, stats=stats)
         if defer:
-            assert train and residual is None and relu in (False, True)
+            assert train and residual is None and not relu, "defer: the projection shortcut's BN only"
             mr = torch.empty((B, c, 2), dtype=torch.float32, device=z.device)
-            pending = FoldedInput(z, stats, mr, self.bn) if relu else (z, stats, mr, self.bn)
-            return pending, (x, z, None, mr, B, H, W, Ho, Wo, relu, False)
+            return (z, stats, mr, self.bn), (x, z, None, mr, B, H, W, Ho, Wo, relu, False)
         y, mr = self.bn.normalize(z, stats, B, Ho * Wo, relu, residual=residual, train=train,
                                   residual_bn=residual_bn)
         return y, (x, z, y, mr, B, H, W, Ho, Wo, relu, residual is not None or residual_bn is not None)
@@ -436,6 +389,8 @@ class ConvBN(object):
             nn.bn_backward_relu(dy, z, mr, self.bn.gamma, self.bn.beta, dz, st.g(self.bn.gname),
                                 st.g(self.bn.bname), B, Ho * Wo, c, conv_dbias=self.conv.db)
         else:
+            # the mask comes from y: a deferred unit (saved y None) has no ReLU (ConvBN.forward)
+            assert y is not None or not relu, "ReLU unit without its saved output"
             nn.bn_backward(dy, y if relu else None, z, mr, self.bn.gamma, dz, g_out, st.g(self.bn.gname),
                            st.g(self.bn.bname), B, Ho * Wo, c, conv_dbias=self.conv.db)
         self.conv.wgrad(x, dz, B, H, W, bias=False)

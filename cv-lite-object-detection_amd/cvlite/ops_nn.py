@@ -78,15 +78,6 @@ def conv_igemm(desc, src, dst, stats=None):
               n if ws is not None else 0, stream())
 
 
-def conv_igemm_fold(desc, z, dst, stats, fold_stats, fold_mr, run_mean, run_var, gamma, beta, eps, momentum):
-    """1x1 forward of relu(BN(z)) with that BN finalized and applied inside the launch
-    (cvl_conv_igemm_fold); False when it does not apply (nothing enqueued)."""
-    _prec(desc, z)
-    return _lib.call("cvl_conv_igemm_fold", ctypes.byref(desc), ptr(z), ptr(dst), ptr(stats), ptr(fold_stats),
-                     ptr(fold_mr), ptr(run_mean), ptr(run_var), ptr(gamma), ptr(beta), float(eps), float(momentum),
-                     stream())
-
-
 def probe_begin(slot):
     """Start stamp of an in-graph launch probe (slot: uint64 [3] device tensor, cvl_probe_begin)."""
     _lib.call("cvl_probe_begin", ptr(slot), stream())
@@ -144,19 +135,6 @@ def conv_wgrad(desc, x, dy, dw, beta=0.0):
               ws.numel(), stream())
     if _wgrad_pending is not None:
         _wgrad_pending.append(ws)
-
-
-def conv_wgrad_fold(desc, z, fold_mr, gamma, beta_bn, dy, dw, beta=0.0):
-    """Weight gradient of a 1x1 conv whose input is relu(BN(z)) from the stored (mean, rstd)
-    (cvl_conv_wgrad_fold); False when it does not apply (nothing enqueued)."""
-    _prec(desc, z)
-    n = int(_lib.load().cvl_conv_wgrad_workspace_size(ctypes.byref(desc)))
-    ws = torch.empty(max(n, 16), dtype=torch.uint8, device=z.device)
-    ok = _lib.call("cvl_conv_wgrad_fold", ctypes.byref(desc), ptr(z), ptr(fold_mr), ptr(gamma), ptr(beta_bn),
-                   ptr(dy), ptr(dw), float(beta), ptr(ws), ws.numel(), stream())
-    if ok and _wgrad_pending is not None:
-        _wgrad_pending.append(ws)
-    return ok
 
 
 def conv_wgrad_grouped(desc, x, dy, dws, beta=0.0):

@@ -20,11 +20,6 @@ STEM_K = 7
 FUSE_POOL = os.environ.get("CVL_STEM_NO_FUSE_POOL", "0") != "1"
 # projection shortcut's BN applied inside conv3's BN launch (CVL_NO_SC_BN_FUSE=1: stored and re-read)
 FUSE_SC_BN = os.environ.get("CVL_NO_SC_BN_FUSE", "0") != "1"
-# conv2's BN -> ReLU folded into conv3's operand path (opt-in, CVL_BN_FOLD=1).  Measured (FCOS bs 16,
-# round 4): 1143 img/s folded vs 1170 stored -- every N-tile workgroup (and both wave columns of one)
-# re-forms the same A fragments, ~15 VALU per element, which costs more than the apply pass it saves
-# (conv3 at conv5_x: 32 N tiles, 59.7 vs 21.6 us forward); see DESIGN.md section 3.
-FOLD_BN2 = os.environ.get("CVL_BN_FOLD", "0") == "1"
 STEM_KP = 168            # the stem kernels' K: 7 kernel rows x (7 x 3 values padded to 24)
 
 
@@ -137,10 +132,7 @@ class Bottleneck(object):
                 s_bn, s = s, None
         y1, sv1 = self.c1.forward(x, B, H, W, relu=True, train=train, arena=arena)
         H1, W1 = sv1[7], sv1[8]
-        # training, bf16: conv2's BN -> ReLU is applied inside conv3's operand path, forward and weight
-        # gradient (cvl_conv_igemm_fold / cvl_conv_wgrad_fold) instead of being stored and re-read
-        fold2 = train and FOLD_BN2 and x.dtype == torch.bfloat16
-        y2, sv2 = self.c2.forward(y1, B, H1, W1, relu=True, train=train, arena=arena, defer=fold2)
+        y2, sv2 = self.c2.forward(y1, B, H1, W1, relu=True, train=train, arena=arena)
         y3, sv3 = self.c3.forward(y2, B, H1, W1, relu=True, residual=s, train=train, arena=arena, residual_bn=s_bn)
         return y3, H1, W1, (sv_s, sv1, sv2, sv3)
 

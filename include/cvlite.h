@@ -27,8 +27,7 @@ extern "C" {
 
 typedef void* cvl_stream_t; /* hipStream_t */
 
-enum { CVL_OK = 0, CVL_EINVAL = 1, CVL_ENOTTAKEN = 2, CVL_EHIP = 1000 };   /* ENOTTAKEN: a fused form
-   that does not apply to this launch; nothing enqueued -- run the unfused form */
+enum { CVL_OK = 0, CVL_EINVAL = 1, CVL_EHIP = 1000 };
 
 int cvl_version(void);
 
@@ -188,24 +187,6 @@ enum { CVL_CK_NONE = 0, CVL_CK_BASE = 1, CVL_CK_BASE_SPLITK = 2, CVL_CK_L64 = 3,
        CVL_CK_L256 = 5, CVL_CK_X256 = 6, CVL_CK_X32 = 7,
        CVL_CK_WG_S = 8, CVL_CK_WG_L128 = 9, CVL_CK_WG_L256 = 10, CVL_CK_WG_X = 11, CVL_CK_X32H = 12, CVL_CK_WG_SN = 13,
        CVL_CK_H64 = 14, CVL_CK_WG_H = 15, CVL_CK_P = 16 };
-/* BN -> ReLU folded into a 1x1 consumer (Keras ResNet block1: BN_2 + ReLU feeding conv_3, behind
- * FCOS/fcos.py:30-35): the conv input x = relu(BN(z)) of the previous unit is never stored.
- * cvl_conv_igemm_fold: 1x1 FWD of desc d from z (bf16 [B][H][W][Cin]); the BN is finalized inside
- * the launch from fold_stats (BN accumulators of z) -> fold_mean_rstd [B][Cin][2] and the running
- * statistics (fold_run_mean/var NULL together: no EMA), and applied to the A operand in registers as
- * bf16(relu(fma(gamma, (z - mean) * rstd, beta))) -- cvl_bn_finalize_apply's arithmetic, so dst and
- * bn_stats are bit-identical to finalize_apply + cvl_conv_igemm.  cvl_conv_wgrad_fold: the weight
- * gradient of the same conv from z and the stored fold_mean_rstd (bit-identical to cvl_conv_wgrad on
- * the stored input).  Either returns CVL_ENOTTAKEN (nothing enqueued) when the launch does not
- * qualify (the persistent 1x1 kernels with H*W % 256 == 0 forward / % 64 == 0 weight gradient, the
- * BN tables within the kernel's spare LDS / registers); the caller then runs the unfused form. */
-int cvl_conv_igemm_fold(const cvl_conv_desc* d, const void* z, void* dst, uint64_t* bn_stats,
-                        uint64_t* fold_stats, float* fold_mean_rstd, float* fold_run_mean, float* fold_run_var,
-                        const float* fold_gamma, const float* fold_beta, float fold_eps, float fold_momentum,
-                        cvl_stream_t stream);
-int cvl_conv_wgrad_fold(const cvl_conv_desc* d, const void* z, const float* fold_mean_rstd,
-                        const float* fold_gamma, const float* fold_beta, const void* dy, float* dw, float beta,
-                        void* workspace, size_t workspace_bytes, cvl_stream_t stream);
 int cvl_conv_igemm_last_kernel(void);
 const char* cvl_conv_kernel_name(int code);
 

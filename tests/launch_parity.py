@@ -367,55 +367,6 @@ def check_conv_igemm(lp, name, launch, desc, src, dst, stats=None):
             lp.add(name, _detail(desc, s, desc.B) + " img%d" % b, "bn_stats", red_err(got[b], ref, rabs), 1e-6, kern)
 
 
-def _fold_input(z, mr, gamma, beta, B, C):
-    """relu(BN(z)) as the BN apply stores it (bf16), from the (mean, rstd) the kernel wrote."""
-    zz = z.reshape(B, -1, C)
-    mrv = mr.view(B, C, 2)
-    a, _ = bn_affine32(zz, mrv[..., 0][:, None], mrv[..., 1][:, None], gamma, beta)
-    return a.clamp_min(0).to(torch.bfloat16).reshape(z.shape)
-
-
-def check_conv_igemm_fold(lp, name, launch, desc, z, dst, stats, fold_stats, fold_mr, run_mean, run_var, gamma,
-                          beta, eps, momentum):
-    """1x1 forward with the input's BN -> ReLU finalized and applied in the operand path: the fused
-    finalize (mean / rstd / running statistics vs the statistics), then the conv and its BN
-    statistics against the input rebuilt from z with the kernel's own (mean, rstd)."""
-    rm0, rv0 = _clone(run_mean, run_var)
-    st0 = stats.clone() if stats is not None else None
-    if not launch(desc, z, dst, stats, fold_stats, fold_mr, run_mean, run_var, gamma, beta, eps, momentum):
-        return False
-    kern = lp.last_kernel()
-    HW = z.numel() // (desc.B * desc.Cin)
-    _check_finalize(lp, name, "fold C%d HW%d B%d" % (desc.Cin, HW, desc.B), fold_stats, fold_mr, rm0, rv0, run_mean,
-                    run_var, desc.B, desc.Cin, HW, eps, momentum)
-    x = _fold_input(z, fold_mr, gamma, beta, desc.B, desc.Cin)
-    _conv_check_dst(lp, name, desc, x, dst, None, kern)
-    if stats is not None:
-        s = _segs(desc)[0]
-        drows = _rows(dst, desc.ld_dst)
-        got = _acc(stats, desc.B, desc.n_store) - _acc(st0, desc.B, desc.n_store)
-        HWo = s["Hr"] * s["Wr"]
-        for b in range(desc.B):
-            zo = drows[s["db"] + b * s["di"]: s["db"] + b * s["di"] + HWo,
-                       desc.dst_coff:desc.dst_coff + desc.n_store].double()
-            ref = torch.stack([zo.sum(0), (zo * zo).sum(0)], -1)
-            rabs = torch.stack([zo.abs().sum(0), (zo * zo).sum(0)], -1)
-            lp.add(name, _detail(desc, s, desc.B) + " img%d" % b, "bn_stats", red_err(got[b], ref, rabs), 1e-6, kern)
-    return True
-
-
-def check_conv_wgrad_fold(lp, name, launch, desc, z, fold_mr, gamma, beta_bn, dy, dw, beta=0.0):
-    old = dw.clone() if beta != 0.0 else None
-    if not launch(desc, z, fold_mr, gamma, beta_bn, dy, dw, beta):
-        return False
-    kern = lp.last_kernel()
-    lp.flush_wgrad()
-    segs = _segs(desc)
-    x = _fold_input(z, fold_mr, gamma, beta_bn, desc.B, desc.Cin)
-    _check_dw(lp, name, _wgrad_detail(desc, segs) + " fold", kern, dw, old, beta, _wgrad_ref(desc, segs, x, dy))
-    return True
-
-
 def _wgrad_ref(desc, segs, x, dy):
     xrows = _rows(x, desc.Cin)
     drows = _rows(dy, desc.ld_dst)
@@ -1220,8 +1171,6 @@ CHECKS = {
     "bn_apply": check_bn_apply,
     "bn_finalize_apply": check_bn_finalize_apply,
     "bn_finalize_apply_bnres": check_bn_finalize_apply_bnres,
-    "conv_igemm_fold": check_conv_igemm_fold,
-    "conv_wgrad_fold": check_conv_wgrad_fold,
     "bn_backward": check_bn_backward,
     "bn_backward_relu": check_bn_backward_relu,
     "bn_backward_relu6": check_bn_backward_relu6,
