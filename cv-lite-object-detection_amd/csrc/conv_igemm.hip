@@ -406,14 +406,14 @@ static inline int pick_ksplit(const ConvArgs& a, int BN_, int BK_) {
   if (a.nseg != 1) return 1;
   const int tiles = a.m_tiles * (a.Npad / BN_);
   const int nk = a.K / BK_;
-  const int max_tiles = cvl_env_int("CVL_KSPLIT_MAX_TILES", 192);
-  const int target = cvl_env_int("CVL_KSPLIT_TARGET", 384);   // workgroups a split launch aims for
+  const int max_tiles = cvl_tune_int("CVL_KSPLIT_MAX_TILES", 192);
+  const int target = cvl_tune_int("CVL_KSPLIT_TARGET", 384);   // workgroups a split launch aims for
   // short-K small launches split too (>= 4 K steps, >= 2 per split): the hourglass's 16x16 / 32x32
   // levels at bs 8, CenterNet 546 -> 554 img/s (8 / 4: the previous rule; 2 / 1 and a 768 target: less)
-  const int min_nk = cvl_env_int("CVL_KSPLIT_MIN_NK", 4);     // K steps a split needs at least
+  const int min_nk = cvl_dispatch_int("ksplit_min_nk", 4);     // K steps a split needs at least
   if (tiles >= max_tiles || nk < min_nk) return 1;
   int s = (target + tiles - 1) / tiles;
-  const int per = cvl_env_int("CVL_KSPLIT_MIN_PER", 2);       // K steps per split at least
+  const int per = cvl_tune_int("CVL_KSPLIT_MIN_PER", 2);       // K steps per split at least
   if (s > nk / per) s = nk / per;
   return s < 1 ? 1 : s;
 }
@@ -459,7 +459,7 @@ int cvl_conv_splitk_finish(const ConvArgs& a, hipStream_t s) { return splitk_fin
 // (beta == 0) or keep their accumulated value (beta != 0: they receive + 0).
 static bool s2dgrad_transform(const cvl_conv_desc* d, cvl_conv_desc* out, int* up, int* upw) {
   if (d->mode != CVL_CONV_DGRAD || d->KH != 1 || d->KW != 1 || d->stride < 2 || d->nseg != 1 ||
-      d->pad_t != 0 || d->pad_l != 0 || d->relu_in || cvl_env_flag("CVL_CONV_NO_S2DG"))
+      d->pad_t != 0 || d->pad_l != 0 || d->relu_in || cvl_tune_flag("CVL_CONV_NO_S2DG"))
     return false;
   const cvl_conv_seg& q = d->seg[0];
   if ((q.Hs - 1) * d->stride >= q.Hr || (q.Ws - 1) * d->stride >= q.Wr) return false;
@@ -605,10 +605,10 @@ extern "C" int cvl_conv_igemm_dgrad_bnsum(const cvl_conv_desc* d, const void* sr
                                           cvl_stream_t stream) {
   CVL_CHECK_ARG(d && fused && z && mean_rstd && gamma && beta && sums);
   *fused = 0;
-  if (!cvl_env_flag("CVL_NO_BNSUM_FUSE") && d->prec == CVL_PREC_BF16 && d->mode == CVL_CONV_DGRAD &&
+  if (!cvl_tune_flag("CVL_NO_BNSUM_FUSE") && d->prec == CVL_PREC_BF16 && d->mode == CVL_CONV_DGRAD &&
       // (CVL_BNSUM_MIN_HW: A/B knob; unlike the residual form this one pays on every stage -- a 64x64
       // floor cost 0.6 %, 32x32 was neutral)
-      !d->dst_f32 && d->beta == 0.f && (long)d->seg[0].Hr * d->seg[0].Wr >= cvl_env_int("CVL_BNSUM_MIN_HW", 0) &&
+      !d->dst_f32 && d->beta == 0.f && (long)d->seg[0].Hr * d->seg[0].Wr >= cvl_tune_int("CVL_BNSUM_MIN_HW", 0) &&
       d->Cin % 32 == 0 && d->Npad % 32 == 0 && d->ld_dst % 8 == 0 && d->dst_coff % 8 == 0 && d->n_store % 8 == 0 &&
       src && dst) {
     cvl_conv_desc dd;
@@ -641,11 +641,11 @@ extern "C" int cvl_conv_igemm_dgrad_bnsum_res(const cvl_conv_desc* d, const void
                                               size_t workspace_bytes, cvl_stream_t stream) {
   CVL_CHECK_ARG(d && fused && y && z && mean_rstd && gamma && beta && sums);
   *fused = 0;
-  if (!cvl_env_flag("CVL_NO_BNSUM_FUSE") && !cvl_env_flag("CVL_NO_BNSUM_RES") && d->prec == CVL_PREC_BF16 &&
+  if (!cvl_tune_flag("CVL_NO_BNSUM_FUSE") && !cvl_tune_flag("CVL_NO_BNSUM_RES") && d->prec == CVL_PREC_BF16 &&
       d->mode == CVL_CONV_DGRAD && !d->dst_f32 && d->beta != 0.f && d->KH == 1 && d->KW == 1 && d->stride == 1 &&
       // small maps: the fused launch (64-wide N tiles, three prefetched operands) loses to the
       // plain one + the separate pass (A/B per stage; CVL_BNSUM_RES_MIN_HW)
-      (long)d->seg[0].Hr * d->seg[0].Wr >= cvl_env_int("CVL_BNSUM_RES_MIN_HW", 4096) &&
+      (long)d->seg[0].Hr * d->seg[0].Wr >= cvl_dispatch_int("bnsum_res_min_hw", 4096) &&
       d->Cin % 32 == 0 && d->Npad % 32 == 0 && d->ld_dst % 8 == 0 && d->dst_coff % 8 == 0 && d->n_store % 8 == 0 &&
       src && dst) {
     ConvArgs chk;

@@ -129,7 +129,11 @@ __device__ __forceinline__ HaloPieces halo_pieces(const HGeo& G, int H, int W, i
 // landed, the epilogue phases (conv_l_epilogue ts, 16 bits each), wall clock at exit, then
 // shader-clock sums over the tiles: tap loops, the per-block wait + barrier, epilogues (+ their
 // barrier), and the tile count
+#ifdef CVL_MEASURE
 constexpr int kHStampWgs = 4096;
+#else
+constexpr int kHStampWgs = 1;                           // (the stamped instantiations are not built)
+#endif
 __device__ unsigned long long g_h_stamps[kHStampWgs * 8];
 
 // H64, persistent: a workgroup runs a contiguous chunk of the launch's 256 x 64 tiles (all of
@@ -420,6 +424,7 @@ __global__ void __launch_bounds__(NT) conv_igemm_h_kernel(ConvArgs a) {
 
 int cvl_conv_splitk_finish(const ConvArgs& a, hipStream_t s);
 
+#ifdef CVL_MEASURE
 int g_h_stamp_grid = 0;
 
 // Measurement hook: the stamps of the last stamped H64 launch (CVL_H_STAMPS=1): u64 [grid][8] as
@@ -434,6 +439,7 @@ extern "C" int cvl_debug_h_stamps(uint64_t* host, int max_wgs) {
     return CVL_EHIP;
   return g_h_stamp_grid;
 }
+#endif  // CVL_MEASURE
 
 // Geometry H64 covers: 3x3, stride 1, pad 1, source map = output map, every segment's 256-row tiles
 // whole image rows (W | 256, H*W % 256 == 0) or whole images (H*W | 256), halo within HPX pixels.
@@ -458,7 +464,7 @@ bool cvl_conv_h_fits(const cvl_conv_desc* d, const ConvArgs& a) {
 // tiles); -1 when it does not apply.  `slab` / `slab_bytes`: the caller's split-K workspace (may be
 // null: no split).
 int cvl_conv_igemm_h(const cvl_conv_desc* d, const ConvArgs& a0, hipStream_t s, void* slab, size_t slab_bytes) {
-  if (cvl_env_flag("CVL_CONV_NO_H") || !cvl_conv_h_fits(d, a0)) return -1;
+  if (cvl_dispatch_flag("no_h") || !cvl_conv_h_fits(d, a0)) return -1;
   ConvArgs a = a0;
   const bool dg = d->mode == CVL_CONV_DGRAD;
   const int tiles = a.m_tiles * (a.Npad / BN);
@@ -466,7 +472,7 @@ int cvl_conv_igemm_h(const cvl_conv_desc* d, const ConvArgs& a0, hipStream_t s, 
   // split the channel blocks of grids that leave CUs idle (fp32 slabs, single segment, no fused
   // BN-backward sums: the finish kernel forms BN statistics but not those)
   int splits = 1;
-  const int target = cvl_env_int("CVL_CONV_H_SPLIT_TARGET", 256);
+  const int target = cvl_tune_int("CVL_CONV_H_SPLIT_TARGET", 256);
   if (tiles < target && a.nseg == 1 && !a.bsum && slab && d->n_store % 8 == 0 && d->dst_coff % 8 == 0 &&
       (d->dst_f32 || d->ld_dst % 8 == 0) && d->n_store / 8 <= 256) {
     splits = (target + tiles - 1) / tiles;
@@ -484,12 +490,13 @@ int cvl_conv_igemm_h(const cvl_conv_desc* d, const ConvArgs& a0, hipStream_t s, 
   // persistent: one workgroup per CU walks a contiguous chunk of tiles (split launches: one tile
   // per workgroup, the K splits on blockIdx.z)
   static const int ncu = cvl_device_cus();
-  const int per_cu = cvl_env_int("CVL_CONV_H_WG_PER_CU", 1);
+  const int per_cu = cvl_tune_int("CVL_CONV_H_WG_PER_CU", 1);
   const int wgs = a.splits > 1 ? tiles : (tiles < ncu * per_cu ? tiles : ncu * per_cu);
   dim3 grid(wgs, 1, a.splits);
   g_cvl_conv_last_kernel = CVL_CK_H64;
-  const bool wres = a.splits <= 1 && a.Npad == BN && ncb <= WRES_CB && a.nseg == 1 && !cvl_env_flag("CVL_CONV_H_NO_WRES");
-  static const bool stamps = cvl_env_flag("CVL_H_STAMPS");
+  const bool wres = a.splits <= 1 && a.Npad == BN && ncb <= WRES_CB && a.nseg == 1 && !cvl_dispatch_flag("h_no_wres");
+#ifdef CVL_MEASURE
+  static const bool stamps = cvl_tune_flag("CVL_H_STAMPS");
   if (stamps && a.splits <= 1 && wgs <= kHStampWgs) {
     g_h_stamp_grid = wgs;
     if (wres && !dg) hipLaunchKernelGGL((conv_igemm_h_kernel<false, false, true, true>), grid, dim3(NT), 0, s, a);
@@ -498,7 +505,9 @@ int cvl_conv_igemm_h(const cvl_conv_desc* d, const ConvArgs& a0, hipStream_t s, 
     else if (dg && a.bsum) hipLaunchKernelGGL((conv_igemm_h_kernel<true, true, false, true>), grid, dim3(NT), 0, s, a);
     else if (dg) hipLaunchKernelGGL((conv_igemm_h_kernel<true, false, false, true>), grid, dim3(NT), 0, s, a);
     else hipLaunchKernelGGL((conv_igemm_h_kernel<false, false, false, true>), grid, dim3(NT), 0, s, a);
-  } else if (wres) {
+  } else
+#endif
+  if (wres) {
     if (dg && a.bsum) hipLaunchKernelGGL((conv_igemm_h_kernel<true, true, true>), grid, dim3(NT), 0, s, a);
     else if (dg) hipLaunchKernelGGL((conv_igemm_h_kernel<true, false, true>), grid, dim3(NT), 0, s, a);
     else hipLaunchKernelGGL((conv_igemm_h_kernel<false, false, true>), grid, dim3(NT), 0, s, a);
@@ -518,7 +527,7 @@ int cvl_conv_igemm_h(const cvl_conv_desc* d, const ConvArgs& a0, hipStream_t s, 
 size_t cvl_conv_h_workspace(const cvl_conv_desc* d, const ConvArgs& a) {
   if (!cvl_conv_h_fits(d, a) || a.nseg != 1) return 0;
   const int tiles = a.m_tiles * (a.Npad / BN);
-  const int target = cvl_env_int("CVL_CONV_H_SPLIT_TARGET", 256);
+  const int target = cvl_tune_int("CVL_CONV_H_SPLIT_TARGET", 256);
   if (tiles >= target) return 0;
   int splits = (target + tiles - 1) / tiles;
   if (splits > (a.Cin / BK) / 2) splits = (a.Cin / BK) / 2;

@@ -204,26 +204,26 @@ int cvl_conv_igemm_p(const cvl_conv_desc* d, const ConvArgs& a, hipStream_t s);
 // it does not, so the caller falls back to the 128-row kernel.
 int cvl_conv_igemm_l(const cvl_conv_desc* d, int dst_up, int dst_w, const void* src, void* dst, acc_u64* bn_stats,
                      hipStream_t s, const BnSumArgs* bsum, void* workspace, size_t workspace_bytes) {
-  if (cvl_env_flag("CVL_CONV_NO_L")) return -1;
+  if (cvl_dispatch_flag("no_l")) return -1;
   if (bsum && (d->mode != CVL_CONV_DGRAD || d->dst_f32 || (d->beta != 0.f && !bsum->y) || dst_up != 1 || bn_stats))
     return -1;
   // the residual (y-mask) form exists on the 1x1 persistent kernel only
   if (bsum && bsum->y && (d->KH != 1 || d->KW != 1)) return -1;
   // fp32 destinations store element-wise: any n_store (the RetinaNet box heads: 9 anchors x 4 = 36)
-  const bool n_ok = d->dst_f32 ? (d->n_store % 4 == 0 && !cvl_env_flag("CVL_CONV_L_F32_N8")) : d->n_store % 8 == 0;
+  const bool n_ok = d->dst_f32 ? (d->n_store % 4 == 0 && !cvl_tune_flag("CVL_CONV_L_F32_N8")) : d->n_store % 8 == 0;
   if (d->Cin % 32 != 0 || d->relu_in || !n_ok || (d->dst_f32 && bn_stats) ||
-      (!d->dst_f32 && (d->ld_dst % 8 || d->dst_coff % 8)) || (d->dst_f32 && cvl_env_flag("CVL_CONV_L_NO_F32")))
+      (!d->dst_f32 && (d->ld_dst % 8 || d->dst_coff % 8)) || (d->dst_f32 && cvl_tune_flag("CVL_CONV_L_NO_F32")))
     return -1;
   const bool l_cin = d->Cin % 64 == 0;          // the L / X kernels: 64-channel K steps
   // 256-wide tiles (forward and data-gradient) for launches with >= CVL_CONV_L256_MIN_TILES of
   // them.  A single FCOS tower's dgrad (341 tiles) lost 35 % on them (tools/conv_ab.py); the
   // paired cls+reg tower dgrad (682 tiles) gains: whole step 813 -> 827 img/s
   // (tools/gpu_knob_sweep.sh).  CVL_CONV_NO_DGRAD_256=1 restores forward-only.
-  const bool w256 = d->Npad % 256 == 0 && !cvl_env_flag("CVL_CONV_NO_256") &&
-                    (d->mode == CVL_CONV_FWD || !cvl_env_flag("CVL_CONV_NO_DGRAD_256"));
+  const bool w256 = d->Npad % 256 == 0 && !cvl_dispatch_flag("no_256") &&
+                    (d->mode == CVL_CONV_FWD || !cvl_tune_flag("CVL_CONV_NO_DGRAD_256"));
   const int bn = w256 ? 256 : (d->Npad % 128 == 0 ? 128 : (d->Npad % 64 == 0 ? 64 : 0));
   if (!bn) return -1;
-  if (l_cin && d->KH * d->KW * d->Cin < cvl_env_int("CVL_CONV_L_MIN_K", 0) && !bsum) return -1;   // A/B knob
+  if (l_cin && d->KH * d->KW * d->Cin < cvl_tune_int("CVL_CONV_L_MIN_K", 0) && !bsum) return -1;   // A/B knob
   ConvArgs a;
   if (cvl_conv_prepare(d, BM, &a)) return -1;
   a.dst_up = dst_up;
@@ -248,25 +248,25 @@ int cvl_conv_igemm_l(const cvl_conv_desc* d, int dst_up, int dst_w, const void* 
     if (pst >= 0) return pst;
     if (bsum && bsum->y) return -1;
   }
-  const long min_tiles = cvl_env_int("CVL_CONV_L_MIN_TILES", 128);
+  const long min_tiles = cvl_dispatch_int("l_min_tiles", 128);
   int use_bn = bn;
-  if (use_bn == 256 && (long)a.m_tiles * (a.Npad / 256) < cvl_env_int("CVL_CONV_L256_MIN_TILES", 256)) use_bn = 128;
+  if (use_bn == 256 && (long)a.m_tiles * (a.Npad / 256) < cvl_dispatch_int("l256_min_tiles", 256)) use_bn = 128;
   // short-K launches are HBM-bound: 128-wide tiles (more of them) beat the 256-wide ones (FCOS +0.6 %,
   // CenterNet +0.4 % at K < 512)
-  const int w256_min_k = cvl_env_int("CVL_CONV_W256_MIN_K", 512);
+  const int w256_min_k = cvl_dispatch_int("w256_min_k", 512);
   if (use_bn == 256 && a.K < w256_min_k) use_bn = 128;
   // a launch that would leave CUs idle with 128-wide tiles takes 64-wide ones (twice the tiles),
   // also when that lifts it over min_tiles (from the split-K 128-row kernel): FCOS A/B 970 -> 983
   // img/s at 256 for the 128-tile conv4_x launches, -> 988 with the conv5_x ones (512: 966, 1024: 941)
-  const int fill = cvl_env_int("CVL_CONV_L64_FILL", 256);
-  const bool fill_pre = !cvl_env_flag("CVL_CONV_L64_NO_FILL_PRE");
+  const int fill = cvl_tune_int("CVL_CONV_L64_FILL", 256);
+  const bool fill_pre = !cvl_tune_flag("CVL_CONV_L64_NO_FILL_PRE");
   const bool to64 = fill && use_bn == 128 && (long)a.m_tiles * (a.Npad / 128) < fill && a.Npad % 64 == 0 &&
-                    !(bsum && cvl_env_flag("CVL_BSUM_NO_FILL"));
+                    !(bsum && cvl_tune_flag("CVL_BSUM_NO_FILL"));
   // 3x3 / stride 1 launches that would run 64-wide tiles: the halo-staged 256 x 64 kernel
   // (conv_igemm_h.hip), whose A traffic is one halo per channel block instead of nine im2col tiles.
   // Not where the 256 x 128 tiles fill the chip: there the L kernel reads each A tile once for 128
   // columns (128 -> 128 @ 64^2, bs 16: L 33 / 47 us fwd / dgrad vs H64 41 / 52 us)
-  const bool h_width = use_bn == 64 || to64 || !l_cin || cvl_env_flag("CVL_CONV_H_ANY_N");
+  const bool h_width = use_bn == 64 || to64 || !l_cin || cvl_tune_flag("CVL_CONV_H_ANY_N");
   if (h_width && use_bn != 256 && (!bsum || ((a.seg[0].Hr * a.seg[0].Wr) % BM == 0 && !bn_stats))) {
     ConvArgs ah = a;
     ah.dst_up = dst_up;
@@ -305,7 +305,7 @@ int cvl_conv_igemm_l(const cvl_conv_desc* d, int dst_up, int dst_w, const void* 
   a.stats = bn_stats;
   dim3 grid(a.m_tiles * (a.Npad / use_bn));
   const bool dg = d->mode == CVL_CONV_DGRAD;
-  const bool prio = !cvl_env_flag("CVL_CONV_NO_PRIO");
+  const bool prio = !cvl_tune_flag("CVL_CONV_NO_PRIO");
 #define CVL_L_LAUNCH(BN_, WGM_, NST_)                                                                          \
   do {                                                                                                         \
     if (dg && a.bsum) {                                                                                        \

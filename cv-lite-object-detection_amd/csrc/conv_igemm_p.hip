@@ -515,13 +515,13 @@ __global__ void __launch_bounds__(NT) conv_igemm_p_kernel(ConvArgs a, int ntiles
 
 // Runs a 1x1 launch on the persistent kernel; -1 when it does not apply.
 int cvl_conv_igemm_p(const cvl_conv_desc* d, const ConvArgs& a0, hipStream_t s) {
-  if (cvl_env_flag("CVL_CONV_NO_P")) return -1;
+  if (cvl_dispatch_flag("no_p")) return -1;
   if (d->KH != 1 || d->KW != 1 || d->pad_t || d->pad_l || a0.relu_in || a0.nseg != 1 || a0.K % BK) return -1;
   // bsum forms: z-mask without beta; y-mask (residual unit) with the beta accumulate
   if (a0.bsum && (d->mode != CVL_CONV_DGRAD || a0.dst_f32 || (a0.beta != 0.f) != (a0.by != nullptr) ||
                   a0.dst_up != 1 || a0.stats ||
                   (a0.seg[0].Hr * a0.seg[0].Wr) % BM || a0.seg[0].dst_img != (long)a0.seg[0].Hr * a0.seg[0].Wr ||
-                  a0.Npad % 64 || cvl_env_flag("CVL_CONV_P_NO_BSUM")))
+                  a0.Npad % 64 || cvl_tune_flag("CVL_CONV_P_NO_BSUM")))
     return -1;
   if (d->mode == CVL_CONV_DGRAD && d->stride != 1) return -1;
   const ConvSeg& q = a0.seg[0];
@@ -536,17 +536,17 @@ int cvl_conv_igemm_p(const cvl_conv_desc* d, const ConvArgs& a0, hipStream_t s) 
   // 256->1024 @ 32^2 25 -> 21), 64 for long K (1024->256 @ 32^2 20.5 vs 23, 2048->512 @ 16^2 29.5
   // vs 35; tools/p_probe.py)
   const int bn = a0.K <= 256 && a0.Npad % 128 == 0 ? 128 : (a0.Npad % 64 == 0 ? 64 : 0);
-  const int fbn = cvl_env_int("CVL_CONV_P_BN", 0);
+  const int fbn = cvl_dispatch_int("p_bn", 0);
   const int use = a0.bsum ? 64 : (fbn && a0.Npad % fbn == 0 ? fbn : bn);
   if (!use) return -1;
   const int ntiles = a0.m_tiles * (a0.Npad / use);
   const int ntn = a0.Npad / use;
-  int grid = cvl_env_int("CVL_CONV_P_WGS", 256);
+  int grid = cvl_tune_int("CVL_CONV_P_WGS", 256);
   if (grid >= ntiles) grid = ntiles;
   else grid -= grid % ntn;                      // every workgroup keeps one N tile
   if (grid < 1) return -1;
   ConvArgs a = a0;
-  a.dbg = cvl_env_int("CVL_P_ABLATE", 0);
+  a.dbg = cvl_tune_int("CVL_P_ABLATE", 0);
   g_cvl_conv_last_kernel = CVL_CK_P;
 #define CVL_P_LAUNCH(BN_, ACC_)                                                                                 \
   do {                                                                                                      \
@@ -555,7 +555,7 @@ int cvl_conv_igemm_p(const cvl_conv_desc* d, const ConvArgs& a0, hipStream_t s) 
       else hipLaunchKernelGGL((conv_igemm_p_kernel<BN_, false, true>), dim3(grid), dim3(NT), 0, s, a, ntiles);            \
     } else if (a.relu_out) {                                                                                \
       hipLaunchKernelGGL((conv_igemm_p_kernel<BN_, true, false>), dim3(grid), dim3(NT), 0, s, a, ntiles);                 \
-    } else if (a.beta != 0.f && !cvl_env_flag("CVL_P_NO_ACC")) {                                            \
+    } else if (a.beta != 0.f && !cvl_tune_flag("CVL_P_NO_ACC")) {                                            \
       hipLaunchKernelGGL((conv_igemm_p_kernel<BN_, false, false, false, ACC_>), dim3(grid), dim3(NT), 0, s, a, ntiles);   \
     } else {                                                                                                \
       hipLaunchKernelGGL((conv_igemm_p_kernel<BN_, false, false>), dim3(grid), dim3(NT), 0, s, a, ntiles);                \

@@ -223,7 +223,7 @@ __global__ void __launch_bounds__(NT) conv_igemm_x32_kernel(ConvArgs a) {
 // Called by cvl_conv_igemm_l for launches it would run on the 256 x 256 L tile; returns -1 when
 // the X kernel does not apply (the caller then launches the L kernel).
 int cvl_conv_igemm_x(const cvl_conv_desc* d, const ConvArgs& a, hipStream_t s) {
-  if (cvl_env_flag("CVL_CONV_NO_X")) return -1;
+  if (cvl_dispatch_flag("no_x")) return -1;
   const bool dg = d->mode == CVL_CONV_DGRAD;
   if (a.Npad % BN || a.Cin % BK32 || a.K / BK32 < 1 || d->KH * d->KW > 32 || a.relu_in ||
       (dg && d->stride != 1) || a.dst_up != 1)
@@ -236,12 +236,15 @@ int cvl_conv_igemm_x(const cvl_conv_desc* d, const ConvArgs& a, hipStream_t s) {
   }
   dim3 grid(a.m_tiles * (a.Npad / BN));
   ConvArgs am = a;
-  am.dbg = cvl_env_int("CVL_X_ABLATE", 0);     // measurement builds (tools/x32_*.py): ablation bits
+  am.dbg = cvl_tune_int("CVL_X_ABLATE", 0);     // measurement builds (tools/x32_*.py): ablation bits
   g_cvl_conv_last_kernel = CVL_CK_X32;
+#ifdef CVL_MEASURE
   if (am.dbg) {
     if (dg) hipLaunchKernelGGL((conv_igemm_x32_kernel<true, true>), grid, dim3(NT), 0, s, am);
     else hipLaunchKernelGGL((conv_igemm_x32_kernel<false, true>), grid, dim3(NT), 0, s, am);
-  } else if (dg) {
+  } else
+#endif
+  if (dg) {
     hipLaunchKernelGGL((conv_igemm_x32_kernel<true>), grid, dim3(NT), 0, s, am);
   } else {
     hipLaunchKernelGGL((conv_igemm_x32_kernel<false>), grid, dim3(NT), 0, s, am);

@@ -258,7 +258,7 @@ int pick_splits(int tiles, int m_total, int bco) {
   // per workgroup (~0.8 us per 64-row step) + the fp32 slab round trip; the cheapest split wins
   // rows per split at least: 128 (one BM granule) lets small-M launches (CenterNet 16x16 maps at
   // bs 8: 2048 rows) spread over more workgroups: CenterNet 488 -> 510 img/s vs 512
-  const int min_chunk = cvl_env_int("CVL_WG_MIN_CHUNK", 128);
+  const int min_chunk = cvl_tune_int("CVL_WG_MIN_CHUNK", 128);
   int max_s = m_total / min_chunk;
   if (max_s < 1) max_s = 1;
   if (max_s > 8192 / tiles) max_s = 8192 / tiles > 1 ? 8192 / tiles : 1;
@@ -351,7 +351,7 @@ int wgrad_single(const cvl_conv_desc* d, const void* x, const void* dy, float* d
   g_cvl_conv_last_kernel = CVL_CK_WG_S;
   // 128-row steps (twice the MFMA work per barrier pair and loads in flight); the chunks are
   // multiples of BM = 128, so a step never straddles a segment either way
-  const bool r128 = cvl_env_flag("CVL_WG_BR128");
+  const bool r128 = cvl_tune_flag("CVL_WG_BR128");
   if (bco == 128) {
     if (r128) hipLaunchKernelGGL((conv_wgrad_kernel<128, 128>), grid, dim3(NT), 0, s, g);
     else hipLaunchKernelGGL((conv_wgrad_kernel<128, 64>), grid, dim3(NT), 0, s, g);

@@ -227,7 +227,7 @@ struct WhPlan {
 };
 
 inline bool wh_plan(const cvl_conv_desc* d, int ngroups, WhPlan* pl) {
-  if (cvl_env_flag("CVL_WGRAD_NO_H") || ngroups != 1 || d->nseg != 1 || d->mode != CVL_CONV_FWD) return false;
+  if (cvl_dispatch_flag("wg_no_h") || ngroups != 1 || d->nseg != 1 || d->mode != CVL_CONV_FWD) return false;
   if (d->prec != CVL_PREC_BF16 || d->KH != 3 || d->KW != 3 || d->stride != 1 || d->pad_t != 1 || d->pad_l != 1 ||
       d->relu_in || d->Cin % BCI || d->n_store % BCO || d->ld_dst % 8 || d->dst_coff % 8)
     return false;
@@ -241,7 +241,7 @@ inline bool wh_plan(const cvl_conv_desc* d, int ngroups, WhPlan* pl) {
   const int tiles = (d->Cin / BCI) * (d->n_store / BCO);
   pl->steps = d->B * HW / RS;
   // one workgroup per CU (134 KiB of LDS): ~256 workgroups, >= 4 steps each
-  const int target = cvl_env_int("CVL_WGH_WGS", 256);
+  const int target = cvl_tune_int("CVL_WGH_WGS", 256);
   int ns = (target + tiles - 1) / tiles;
   if (ns > pl->steps / 4) ns = pl->steps / 4;
   if (ns < 1) ns = 1;

@@ -291,8 +291,8 @@ inline double wl_time(int tiles, int m_total, int bco, int* best_s) {
   if (max_s < 1) max_s = 1;
   if (max_s > 4096 / tiles) max_s = 4096 / tiles > 1 ? 4096 / tiles : 1;
   // sweep knobs (tools/gpu_knob_sweep.sh): slab cost in percent, block times in 0.1 us
-  const double slab_us = (double)bco * BKK * 4 * 2 / 5.0e6 * cvl_env_int("CVL_WGL_SLAB_PCT", 100) / 100.0;
-  const double blk_us = bco == 256 ? cvl_env_int("CVL_WGL_BLK256", 44) / 10.0 : cvl_env_int("CVL_WGL_BLK128", 28) / 10.0;
+  const double slab_us = (double)bco * BKK * 4 * 2 / 5.0e6 * cvl_tune_int("CVL_WGL_SLAB_PCT", 100) / 100.0;
+  const double blk_us = bco == 256 ? cvl_tune_int("CVL_WGL_BLK256", 44) / 10.0 : cvl_tune_int("CVL_WGL_BLK128", 28) / 10.0;
   double best_t = 1e30;
   *best_s = 1;
   for (int s = 1; s <= max_s; ++s) {
@@ -307,9 +307,9 @@ inline double wl_time(int tiles, int m_total, int bco, int* best_s) {
 // Npad 128 (one 128-wide co tile) runs faster on the register-staged 128 x 128 kernel
 // (tools/wgrad_sweep.py at bs 16: 3x3 128->128 @ 64x64 85 -> 72 us, 1x1 512->128 65 -> 46 us)
 inline bool wl_eligible(const cvl_conv_desc* d, const ConvArgs& a) {
-  return !cvl_env_flag("CVL_WGRAD_NO_L") && !d->relu_in && a.K >= BKK && d->Cin % 8 == 0 &&
+  return !cvl_dispatch_flag("wg_no_l") && !d->relu_in && a.K >= BKK && d->Cin % 8 == 0 &&
          d->n_store % 4 == 0 && a.m_total >= 1024 && a.Npad % 128 == 0 &&
-         a.Npad >= cvl_env_int("CVL_WGL_MIN_NPAD", 256);
+         a.Npad >= cvl_tune_int("CVL_WGL_MIN_NPAD", 256);
 }
 
 struct WlPlan {
@@ -323,7 +323,7 @@ inline bool wl_plan(const cvl_conv_desc* d, ConvArgs* a, WlPlan* p) {
   int s128 = 1, s256 = 1;
   const double t128 = wl_time((a->Npad / 128) * kt, a->m_total, 128, &s128);
   double t256 = 1e30;
-  if (a->Npad % 256 == 0 && !cvl_env_flag("CVL_WGRAD_NO_256"))
+  if (a->Npad % 256 == 0 && !cvl_tune_flag("CVL_WGRAD_NO_256"))
     t256 = wl_time((a->Npad / 256) * kt, a->m_total, 256, &s256);
   p->bco = t256 < t128 ? 256 : 128;
   p->tiles = (a->Npad / p->bco) * kt;

@@ -184,7 +184,7 @@ struct SnPlan {
 };
 
 bool sn_plan(const cvl_conv_desc* d, int ngroups, SnPlan* p) {
-  if (cvl_env_flag("CVL_WGRAD_NO_SN")) return false;
+  if (cvl_tune_flag("CVL_WGRAD_NO_SN")) return false;
   if (!d || d->mode != CVL_CONV_FWD || d->stride != 1 || d->Npad != NP || d->relu_in) return false;
   if (d->Cin % CI || d->KH * d->KW > MAXT || d->nseg < 1 || d->nseg > kMaxSeg || ngroups < 1 ||
       d->nseg % ngroups)

@@ -79,14 +79,7 @@ __device__ __forceinline__ unsigned long long memtime_nowait() {
 }
 typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 
-// RG (register-staged ring, the production form): each lane loads its 16-B pieces of a step by
-// buffer_load_dwordx4 into VGPRs (two register sets, loads issued three steps ahead of their
-// step), ds_write_b128s them into a 2-slot LDS ring one step ahead, and the transposed fragment
-// reads are those of the DMA form.  The DMA form (LDS-DMA into a 5-slot ring) issues at ~100+ cycles
-// per piece and fills at ~30 GB/s per CU (profiles/r04_ubench_ldsdma.md); the register path costs
-// ~20 cycles per piece.  Same MFMA order: bit-identical results.  Measured at the DMA form's speed
-// (loop 19.1 vs 17.3 us at 1x1 1024->256 @ 32^2), so opt-in (CVL_WGX_RG=1) for diagnosis.
-template <int T, int SR = BR, bool ST = false, bool RG = false>
+template <int T, int SR = BR, bool ST = false>
 __global__ void __launch_bounds__(NT) conv_wgrad_x_kernel(WxArgs g) {
   using C = WxCfg<T, SR>;
   // ST: wall-clock stamps of thread 0 (entry, prologue landed, loop done, epilogue stored)
@@ -94,8 +87,7 @@ __global__ void __launch_bounds__(NT) conv_wgrad_x_kernel(WxArgs g) {
   if (stamp) stamp[0] = wall_clock64();
   constexpr int BCO = C::BCO, BKK = C::BKK, YST = C::YST, SLOT = C::SLOT, TM = C::TM, TN = C::TN;
   constexpr int J = C::J;
-  constexpr int NSL = RG ? 2 : NSLOT;
-  __shared__ __attribute__((aligned(16))) cvl_bf16 lds[NSL * SLOT];
+  __shared__ __attribute__((aligned(16))) cvl_bf16 lds[NSLOT * SLOT];
   const ConvArgs& a = g.a;
   const int tid = threadIdx.x;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
@@ -204,36 +196,7 @@ __global__ void __launch_bounds__(NT) conv_wgrad_x_kernel(WxArgs g) {
     });
     cslot = cslot == NSLOT - 1 ? 0 : cslot + 1;
   };
-  // RG form: a register set holds one step's pieces of this lane
-  struct RSet { u32x4 y[J], x[J]; };
-  const int abl = ST ? g.ablate : 0;           // measurement builds: CVL_WGX_ABLATE bits (launch code)
-  auto load_set = [&](RSet& r) {
-    if (abl & 4) return;                        // no loads
-    if (abl & 8) {                              // loads without the address arithmetic (one hot KiB)
-#pragma unroll
-      for (int j = 0; j < J; ++j) {
-        r.y[j] = __builtin_amdgcn_raw_buffer_load_b128(rsY, lane * 16, 0, 0);
-        r.x[j] = __builtin_amdgcn_raw_buffer_load_b128(rsX, lane * 16, 0, 0);
-      }
-      ++ist;
-      return;
-    }
-    issue_step([&](int j, unsigned oy, unsigned ox) {
-      r.y[j] = __builtin_amdgcn_raw_buffer_load_b128(rsY, (int)oy, 0, 0);
-      r.x[j] = __builtin_amdgcn_raw_buffer_load_b128(rsX, (int)ox, 0, 0);
-    });
-  };
-  // the lane's 16 B land where LDS-DMA would have put them (lane-linear from the wave's row base)
-  auto store_set = [&](const RSet& r, int slot) {
-    if (abl & 2) return;                        // no ring writes
-    char* Yb = reinterpret_cast<char*>(lds + slot * SLOT) + lane * 16;
-    char* Xb = Yb + YST * 2;
-#pragma unroll
-    for (int j = 0; j < J; ++j) {
-      *reinterpret_cast<u32x4*>(Yb + (8 * C::RPI * j + C::RPI * wave) * BCO * 2) = r.y[j];
-      *reinterpret_cast<u32x4*>(Xb + (8 * C::RPI * j + C::RPI * wave) * BKK * 2) = r.x[j];
-    }
-  };
+  const int abl = ST ? g.ablate : 0;           // measurement builds: CVL_WGX_ABLATE bits (1 no fragment reads, 16 no MFMAs)
 
   const int wco = wave >> 2, wk = wave & 3;
   const int lr = lane & 15, lg = lane >> 4;
@@ -289,18 +252,12 @@ __global__ void __launch_bounds__(NT) conv_wgrad_x_kernel(WxArgs g) {
       for (int j = 0; j < TN; ++j) { bl[h][j] = ds_tr16(xo + xa[j]); bh[h][j] = ds_tr16(xo + xb[j]); }
     }
     unsigned long long t2 = 0, t3 = 0, t4 = 0, t5 = 0;
-    if (RG) {                                   // the ring writes of this segment land before the barrier
+    if (ST) {
       lgkm_wait();
-      if (ST) t2 = memtime_nowait();
-      bar();
-    } else {
-      if (ST) {
-        lgkm_wait();
-        t2 = memtime_nowait();
-      }
-      bar();
-      lgkm_wait();
+      t2 = memtime_nowait();
     }
+    bar();
+    lgkm_wait();
     if (ST) t3 = memtime_nowait();
 #pragma unroll
     for (int h = 0; h < KS; ++h) {
@@ -345,45 +302,7 @@ __global__ void __launch_bounds__(NT) conv_wgrad_x_kernel(WxArgs g) {
     }
   };
 
-  if constexpr (RG) {
-    // register sets: at the load segment of step t, set (t+1)&1 holds step t+1 (written into ring slot
-    // (t+1)&1, whose step t-1 both wave groups finished reading before the previous barrier) and is
-    // then reloaded with step t+3; set t&1 holds step t+2 in flight.  nsteps is even (128-row
-    // chunks), so the loop runs phase pairs with the sets fixed.
-    RSet sa, sb;
-    load_set(sa);                               // step 0
-    load_set(sb);                               // step 1
-    store_set(sa, 0);
-    load_set(sa);                               // step 2
-    lgkm_wait();
-    __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");
-    if (stamp) stamp[1] = wall_clock64();
-    if (wco == 1) bar();                        // stagger: waves 4-7 run one barrier behind
-    unsigned long long t0 = 0, t1 = 0;
-    for (int st = 0; st < nsteps; st += 2) {
-      if (ST) {
-        t0 = memtime_nowait();
-        wait_vm<2 * J>();
-        t1 = memtime_nowait();
-      }
-      store_set(sb, 1);                         // step st+1
-      __builtin_amdgcn_sched_barrier(0);
-      load_set(sb);                             // step st+3
-      __builtin_amdgcn_sched_barrier(0);
-      phase(t0, t1, 0);
-      if (ST) {
-        t0 = memtime_nowait();
-        wait_vm<2 * J>();
-        t1 = memtime_nowait();
-      }
-      store_set(sa, 0);                         // step st+2
-      __builtin_amdgcn_sched_barrier(0);
-      load_set(sa);                             // step st+4
-      __builtin_amdgcn_sched_barrier(0);
-      phase(t0, t1, 1);
-    }
-  } else {
+  {
     issue();
     issue();
     issue();
@@ -446,12 +365,14 @@ struct WxPlan {
   size_t slab;
 };
 
+#ifdef CVL_MEASURE
 // measurement builds: CVL_WGX_STAMPS=1 stamps every launch into this buffer (cvl_debug_wgx_stamps)
 constexpr int kStampWgs = 16384;
 __device__ unsigned long long g_wgx_stamps[kStampWgs * 4];
 constexpr int kPhaseWgs = 2048;
 __device__ unsigned long long g_wgx_phase[kPhaseWgs * 8 * 8];
 int g_wgx_stamp_grid = 0;
+#endif
 
 // Modelled time of s splits at tile width T: rounds of 256 workgroups (one per CU; 512 for T = 128) x 32-row steps
 // per chunk (CVL_WGX_STEP, 0.01 us; ~0.8 us measured on the tower shape; CVL_WGX_STEP128 for the
@@ -462,7 +383,7 @@ int g_wgx_stamp_grid = 0;
 // 64 MiB of slabs; 16 tiles of 128 -> 16 splits, 16 MiB).
 // K below one 256-deep tile (1x1 convs with Cin 128) leaves half of every 256 tile idle.
 inline bool wx_plan(const cvl_conv_desc* d, int ngroups, ConvArgs* a, WxPlan* p) {
-  if (cvl_env_flag("CVL_WGRAD_NO_X")) return false;
+  if (cvl_dispatch_flag("wg_no_x")) return false;
   if (cvl_conv_prepare(d, SEGM, a)) return false;
   if (ngroups < 1 || ngroups > kMaxGroups || d->nseg % ngroups || d->relu_in || a->Npad % 64 || d->Cin % 8 ||
       d->n_store % 4 || a->m_total < 1024)
@@ -483,7 +404,7 @@ inline bool wx_plan(const cvl_conv_desc* d, int ngroups, ConvArgs* a, WxPlan* p)
     mg = p->g_m1[gq] - p->g_m0[gq] > mg ? p->g_m1[gq] - p->g_m0[gq] : mg;
   }
   for (int gq = ngroups; gq < kMaxGroups; ++gq) p->g_m0[gq] = p->g_m1[gq] = 0;
-  const int forced_t = cvl_env_int("CVL_WGX_T", 0);
+  const int forced_t = cvl_tune_int("CVL_WGX_T", 0);
   double best_t = 1e30;
   int best_s = 0, best_T = 0;
   int s256 = 0, tg256 = 0;
@@ -493,14 +414,14 @@ inline bool wx_plan(const cvl_conv_desc* d, int ngroups, ConvArgs* a, WxPlan* p)
     if (forced_t && forced_t != T) continue;
     // T = 128 also takes 64-channel outputs (half of each tile idle: the stem's and the 1x1 ->64
     // weight gradients, on the generic kernel at 149 / 44 / 37 us before)
-    if ((T == 256 && a->Npad % T) || a->K < cvl_env_int(T == 256 ? "CVL_WGX_MIN_K" : "CVL_WGX_MIN_K128", T == 256 ? 256 : 64))
+    if ((T == 256 && a->Npad % T) || a->K < cvl_tune_int(T == 256 ? "CVL_WGX_MIN_K" : "CVL_WGX_MIN_K128", T == 256 ? 256 : 64))
       continue;
     const int tg = ((a->Npad + T - 1) / T) * ((a->K + T - 1) / T) * ngroups;
-    const bool sr64 = T == 128 && cvl_env_int("CVL_WGX_SR", 64) == 64;
+    const bool sr64 = T == 128 && cvl_tune_int("CVL_WGX_SR", 64) == 64;
     const double step_us =
-        T == 256 ? cvl_env_int("CVL_WGX_STEP", 80) / 100.0
-                 : (sr64 ? cvl_env_int("CVL_WGX_STEP64", 120) / 200.0 : cvl_env_int("CVL_WGX_STEP128", 80) / 100.0);
-    const double slab_us = (double)T * T * 4 * 2 / 5.0e6 * cvl_env_int("CVL_WGX_SLAB_PCT", 100) / 100.0;
+        T == 256 ? cvl_tune_int("CVL_WGX_STEP", 80) / 100.0
+                 : (sr64 ? cvl_tune_int("CVL_WGX_STEP64", 120) / 200.0 : cvl_tune_int("CVL_WGX_STEP128", 80) / 100.0);
+    const double slab_us = (double)T * T * 4 * 2 / 5.0e6 * cvl_tune_int("CVL_WGX_SLAB_PCT", 100) / 100.0;
     int max_s = mg / 512;
     if (max_s < 1) max_s = 1;
     if (max_s > 2048 / tg) max_s = 2048 / tg > 1 ? 2048 / tg : 1;
@@ -518,7 +439,7 @@ inline bool wx_plan(const cvl_conv_desc* d, int ngroups, ConvArgs* a, WxPlan* p)
   // launches, capped by the 512-row minimum chunk) loses to the 128-wide one in the per-shape
   // sweep (1x1 256->1024 @ 32x32: 38 -> 31 us; 3x3 s2 2048->256 @ 8x8: 45 -> 34 us); the tower
   // (18 tiles x 14 splits) keeps 256 (230 vs 322 us)
-  if (best_T == 256 && s128 && tg256 * s256 < 240 && !cvl_env_flag("CVL_WGX_KEEP256")) {
+  if (best_T == 256 && s128 && tg256 * s256 < 240 && !cvl_tune_flag("CVL_WGX_KEEP256")) {
     best_T = 128;
     best_s = s128;
   }
@@ -527,10 +448,10 @@ inline bool wx_plan(const cvl_conv_desc* d, int ngroups, ConvArgs* a, WxPlan* p)
   // 64-row steps on the 128-wide tile (CVL_WGX_SR=32 reverts): one workgroup per CU, half the
   // splits of the 32-row form at the same workgroup count per CU-round -- half the slab bytes (in-step
   // trace: the reductions 90 -> 63 / 133 -> 100 us per batch, the kernels +1-3 us; FCOS +0.6 %)
-  p->SR = best_T == 128 && cvl_env_int("CVL_WGX_SR", 64) == 64 ? 64 : 32;
+  p->SR = best_T == 128 && cvl_tune_int("CVL_WGX_SR", 64) == 64 ? 64 : 32;
   p->co_tiles = (a->Npad + best_T - 1) / best_T;
   p->tiles = p->co_tiles * ((a->K + best_T - 1) / best_T);
-  const int forced = cvl_env_int("CVL_WGX_SPLITS", 0);
+  const int forced = cvl_tune_int("CVL_WGX_SPLITS", 0);
   if (forced > 0) best_s = forced;
   p->chunk = ((mg + best_s - 1) / best_s + SEGM - 1) / SEGM * SEGM;
   p->nsplit = (mg + p->chunk - 1) / p->chunk;
@@ -555,18 +476,20 @@ int cvl_conv_wgrad_x(const cvl_conv_desc* d, int ngroups, const void* x, const v
   WxPlan p;
   if (!wx_plan(d, ngroups, &g.a, &p)) return -1;
   if (!workspace || workspace_bytes < (p.slab > 16 ? p.slab : 16)) return CVL_EINVAL;
-  static const bool stamps = cvl_env_flag("CVL_WGX_STAMPS");
   g.stamps = nullptr;
   g.phase = nullptr;
   g.ablate = 0;
+#ifdef CVL_MEASURE
+  static const bool stamps = cvl_tune_flag("CVL_WGX_STAMPS");
   if (stamps && p.tiles * p.nsplit * ngroups <= kStampWgs) {
     void* sym = nullptr;
     if (hipGetSymbolAddress(&sym, HIP_SYMBOL(g_wgx_stamps)) == hipSuccess) g.stamps = (unsigned long long*)sym;
     if (p.tiles * p.nsplit * ngroups <= kPhaseWgs && hipGetSymbolAddress(&sym, HIP_SYMBOL(g_wgx_phase)) == hipSuccess)
       g.phase = (unsigned long long*)sym;
-    g.ablate = cvl_env_int("CVL_WGX_ABLATE", 0);
+    g.ablate = cvl_tune_int("CVL_WGX_ABLATE", 0);
     g_wgx_stamp_grid = p.tiles * p.nsplit * ngroups;
   }
+#endif
   g.a.src = reinterpret_cast<const cvl_bf16*>(x);
   g.dy = reinterpret_cast<const cvl_bf16*>(dy);
   g.ld_dy = d->ld_dst;
@@ -592,26 +515,19 @@ int cvl_conv_wgrad_x(const cvl_conv_desc* d, int ngroups, const void* x, const v
     if (gs) return gs;
   }
   const dim3 grid(p.tiles * p.nsplit * ngroups);
-  // CVL_WGX_RG=1: the register-staged ring (measured no faster than the LDS-DMA ring: DESIGN §7)
-  static const bool dma = !cvl_env_flag("CVL_WGX_RG");
-  if (g.stamps && !dma) {
-    if (p.T == 256) hipLaunchKernelGGL((conv_wgrad_x_kernel<256, BR, true, true>), grid, dim3(NT), 0, s, g);
-    else if (p.SR == 64) hipLaunchKernelGGL((conv_wgrad_x_kernel<128, 64, true, true>), grid, dim3(NT), 0, s, g);
-    else hipLaunchKernelGGL((conv_wgrad_x_kernel<128, BR, true, true>), grid, dim3(NT), 0, s, g);
-  } else if (g.stamps) {
+#ifdef CVL_MEASURE
+  if (g.stamps) {
     if (p.T == 256) hipLaunchKernelGGL((conv_wgrad_x_kernel<256, BR, true>), grid, dim3(NT), 0, s, g);
     else if (p.SR == 64) hipLaunchKernelGGL((conv_wgrad_x_kernel<128, 64, true>), grid, dim3(NT), 0, s, g);
     else hipLaunchKernelGGL((conv_wgrad_x_kernel<128, BR, true>), grid, dim3(NT), 0, s, g);
-  } else if (dma) {
-    if (p.T == 256) hipLaunchKernelGGL((conv_wgrad_x_kernel<256, BR>), grid, dim3(NT), 0, s, g);
-    else if (p.SR == 64) hipLaunchKernelGGL((conv_wgrad_x_kernel<128, 64>), grid, dim3(NT), 0, s, g);
-    else hipLaunchKernelGGL((conv_wgrad_x_kernel<128, BR>), grid, dim3(NT), 0, s, g);
-  } else if (p.T == 256) {
-    hipLaunchKernelGGL((conv_wgrad_x_kernel<256, BR, false, true>), grid, dim3(NT), 0, s, g);
+  } else
+#endif
+  if (p.T == 256) {
+    hipLaunchKernelGGL((conv_wgrad_x_kernel<256, BR>), grid, dim3(NT), 0, s, g);
   } else if (p.SR == 64) {
-    hipLaunchKernelGGL((conv_wgrad_x_kernel<128, 64, false, true>), grid, dim3(NT), 0, s, g);
+    hipLaunchKernelGGL((conv_wgrad_x_kernel<128, 64>), grid, dim3(NT), 0, s, g);
   } else {
-    hipLaunchKernelGGL((conv_wgrad_x_kernel<128, BR, false, true>), grid, dim3(NT), 0, s, g);
+    hipLaunchKernelGGL((conv_wgrad_x_kernel<128, BR>), grid, dim3(NT), 0, s, g);
   }
   int st = cvl_launch_status();
   if (st || g.direct) return st;
@@ -619,6 +535,7 @@ int cvl_conv_wgrad_x(const cvl_conv_desc* d, int ngroups, const void* x, const v
                           p.nsplit, ngroups, beta, s);
 }
 
+#ifdef CVL_MEASURE
 // Measurement hook: the stamps of the last stamped weight-gradient launch (CVL_WGX_STAMPS=1):
 // u64 [grid][4] = (entry, prologue landed, loop done, epilogue stored) wall-clock ticks per
 // workgroup, copied to host memory (at most max_wgs rows); returns the grid size (0: none).
@@ -630,3 +547,4 @@ extern "C" int cvl_debug_wgx_stamps(uint64_t* host, int max_wgs) {
     return -1;
   return g_wgx_stamp_grid;
 }
+#endif  // CVL_MEASURE

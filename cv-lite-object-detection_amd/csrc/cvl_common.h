@@ -17,16 +17,30 @@ static inline int cvl_launch_status() {
   return e == hipSuccess ? CVL_OK : (CVL_EHIP + (int)e);
 }
 
-// Kernel-variant switches for A/B measurement (e.g. CVL_CONV_NO_P=1); read per launch.
-static inline bool cvl_env_flag(const char* name) {
+// ---- environment --------------------------------------------------------------------------------
+// The product library reads ONE environment variable on its dispatch path: CVL_DISPATCH, a comma-
+// separated list of test hooks "key" or "key=value" (read per launch) that force a kernel family off
+// or move a planner threshold, so the parity tests reach every kernel at small sizes; unset = the
+// production dispatch.  The keys are listed in INTEGRATION.md ("Environment").  Measurement builds
+// (make MEASURE=1 -> -DCVL_MEASURE, built into ab/ by tools/build_measure.sh) also honour the per-knob
+// CVL_* variables of the measurement tools (in-kernel stamps, ablation bits, planner tuning); the
+// product build compiles those reads out and keeps their defaults.
+int cvl_dispatch_int(const char* key, int dflt);     // capi.hip
+static inline bool cvl_dispatch_flag(const char* key) { return cvl_dispatch_int(key, 0) != 0; }
+
+#ifdef CVL_MEASURE
+static inline bool cvl_tune_flag(const char* name) {
   const char* v = getenv(name);
   return v && v[0] && v[0] != '0';
 }
-
-static inline int cvl_env_int(const char* name, int dflt) {
+static inline int cvl_tune_int(const char* name, int dflt) {
   const char* v = getenv(name);
   return (v && v[0]) ? atoi(v) : dflt;
 }
+#else
+static inline bool cvl_tune_flag(const char*) { return false; }
+static inline int cvl_tune_int(const char*, int dflt) { return dflt; }
+#endif
 
 // compute units of the current device (persistent kernels size their grids by it; one process
 // drives one GPU, so the first query is cached)

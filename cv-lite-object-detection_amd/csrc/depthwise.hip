@@ -268,7 +268,7 @@ __global__ void __launch_bounds__(NT) dw_wgrad_rows_kernel(const cvl_bf16* __res
 
 // row-walk plan of dw_wgrad_rows_kernel: segment length, segments per row, blocks (0 = not taken)
 inline int rows_plan(int B, int Ho, int Wo, int C, int k, int s, int* seg, int* spr) {
-  if (k != 3 || s != 1 || C / 8 > NT || cvl_env_flag("CVL_DW_NO_ROWS")) return 0;
+  if (k != 3 || s != 1 || C / 8 > NT || cvl_tune_flag("CVL_DW_NO_ROWS")) return 0;
   *seg = Wo >= 128 ? 32 : (Wo >= 32 ? 16 : 8);
   *spr = (Wo + *seg - 1) / *seg;
   const int rpp = NT / (C / 8);

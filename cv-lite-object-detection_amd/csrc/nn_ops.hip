@@ -391,7 +391,7 @@ __global__ void __launch_bounds__(NT) bn_apply_kernel(const cvl_bf16* __restrict
 // rows per block of the (row chunk, image) grids: ~2048 blocks in total, >= 4 passes per thread
 inline int bn_rows_per_blk(int B, int HW, int C) {
   const int C8 = C / 8, tpr = C8 < NT ? C8 : NT, rpp = NT / tpr;
-  static const int target = cvl_env_int("CVL_BNA_BLOCKS", 2048);     // workgroups per launch (sweep knob)
+  static const int target = cvl_tune_int("CVL_BNA_BLOCKS", 2048);     // workgroups per launch (sweep knob)
   const int chunks = (target + B - 1) / B;
   int rpb = (HW + chunks - 1) / chunks;
   const int lo = rpp * 4 * (C8 > NT ? 1 : 1);
@@ -612,7 +612,7 @@ __global__ void __launch_bounds__(NT) bn_colsum_kernel(const float* __restrict__
 inline int bn_bwd_rows_per_blk(int B, int HW, int C) {
   const int C8 = C / 8, rpp = NT / (C8 < NT ? C8 : NT);
   long want = (long)B * HW * (C8 < NT ? C8 : NT) / (NT * 16);
-  static const int lo = cvl_env_int("CVL_BNB_MIN_BLOCKS", 256), hi = cvl_env_int("CVL_BNB_MAX_BLOCKS", 2048);
+  static const int lo = cvl_tune_int("CVL_BNB_MIN_BLOCKS", 256), hi = cvl_tune_int("CVL_BNB_MAX_BLOCKS", 2048);
   want = want < lo ? lo : (want > hi ? hi : want);
   const int chunks = (int)((want + B - 1) / B);
   int rpb = (HW + chunks - 1) / chunks;

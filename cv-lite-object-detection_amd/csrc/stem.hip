@@ -26,6 +26,7 @@
 #include "conv_common.h"
 
 namespace {
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
@@ -174,8 +175,8 @@ __global__ void __launch_bounds__(NT, 2) stem_fwd_kernel(StemArgs g) {
     for (int e = 0; e < 2; ++e) { s1[i][e] = f32x2{0.f, 0.f}; s2[i][e] = f32x2{0.f, 0.f}; }
 
   // per row: the next row's two image rows are loaded, the MFMAs issue, the two rows go into the
-  // ring slots this row does not read ((2*oy + 7) % NRING is only its zero-weight pad K, any finite
-  // value will do) while the MFMAs run, then the epilogue; ONE barrier per row, at its top
+  // ring slots this row does not read ((2*oy + 7) % NRING is only its pad K, which the fragments
+  // replace by zeros) while the MFMAs run, then the epilogue; ONE barrier per row, at its top
   for (int oy = t.oy0; oy < t.oy1; ++oy) {
     if (oy > t.oy0) __syncthreads();                // the previous row's ring stores are visible
     const bool more = oy + 1 < t.oy1;
@@ -194,11 +195,22 @@ __global__ void __launch_bounds__(NT, 2) stem_fwd_kernel(StemArgs g) {
     for (int s = 0; s < KP / 32; ++s) {
       const int k0 = s * 32 + lg * 8, ky = k0 / 24, off = k0 - ky * 24;
       const cvl_bf16* rr = ring + ((2 * oy + ky) % NRING) * RL + off;
+      // pad K (kx*3 + c in 21..23 = the next pixel's values, or ky == 7 = the ring row being
+      // rewritten) enters the MFMAs as exact zeros, not as data under zero weights: a non-finite pixel
+      // then reaches only its own outputs, and the ky == 7 read's race with row_store is harmless
+      const unsigned keep_hi = off == 16 ? 0x0000ffffu : 0xffffffffu;     // elements 5..7 of the chunk
+      const bool padrow = ky >= 7;
       s16x8 fa[4], fb[4];
 #pragma unroll
       for (int i = 0; i < 4; ++i) fa[i] = *reinterpret_cast<const s16x8*>(Wl + (i * 16 + lr) * WA + k0);
 #pragma unroll
-      for (int j = 0; j < 4; ++j) fb[j] = ring8(rr + 6 * (wave * 64 + j * 16 + lr));
+      for (int j = 0; j < 4; ++j) {
+        u32x4 v = __builtin_bit_cast(u32x4, ring8(rr + 6 * (wave * 64 + j * 16 + lr)));
+        v[2] &= keep_hi;
+        v[3] = off == 16 ? 0u : v[3];
+        v = padrow ? u32x4{0u, 0u, 0u, 0u} : v;
+        fb[j] = __builtin_bit_cast(s16x8, v);
+      }
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
@@ -410,13 +422,16 @@ inline void stem_plan(StemArgs* g, int B, int H, int W, int rpw) {
   g->nbands = (g->Ho + rpw - 1) / rpw;
 }
 
+#ifdef CVL_MEASURE
 // measurement builds: CVL_STEM_STAMPS=1 stamps every forward launch into this buffer
 constexpr int kStemStampWgs = 4096;
 __device__ unsigned long long g_stem_stamps[kStemStampWgs * 8];
 int g_stem_stamp_grid = 0;
+#endif
 
 }  // namespace
 
+#ifdef CVL_MEASURE
 // Measurement hook: the stamps of the last stamped stem forward (CVL_STEM_STAMPS=1): u64 [grid][8] =
 // wall clock at entry / prologue landed / rows done / exit, then shader-clock ticks in the rows' MFMA
 // phase, epilogue and ring refill (thread 0 of each workgroup); returns the grid size (0: none).
@@ -428,6 +443,7 @@ extern "C" int cvl_debug_stem_stamps(uint64_t* host, int max_wgs) {
     return -1;
   return g_stem_stamp_grid;
 }
+#endif  // CVL_MEASURE
 
 extern "C" int cvl_stem_conv7x7s2(const float* img, int B, int H, int W, const void* w_packed, const float* bias,
                                   void* z, uint64_t* bn_stats, cvl_stream_t stream) {
@@ -441,15 +457,18 @@ extern "C" int cvl_stem_conv7x7s2(const float* img, int B, int H, int W, const v
   g.stats = reinterpret_cast<acc_u64*>(bn_stats);
   g.acc_slots = cvl_bn_acc_slots();
   stem_plan(&g, B, H, W, RPW_F);
-  static const bool stamps = cvl_env_flag("CVL_STEM_STAMPS");
   const int grid = B * g.ntx * g.nbands;
+#ifdef CVL_MEASURE
+  static const bool stamps = cvl_tune_flag("CVL_STEM_STAMPS");
   if (stamps && grid <= kStemStampWgs) {
     void* sym = nullptr;
     if (hipGetSymbolAddress(&sym, HIP_SYMBOL(g_stem_stamps)) == hipSuccess) g.stamps = (unsigned long long*)sym;
     g_stem_stamp_grid = grid;
   }
   if (g.stamps) hipLaunchKernelGGL(stem_fwd_kernel<true>, dim3(grid), dim3(NT), 0, (hipStream_t)stream, g);
-  else hipLaunchKernelGGL(stem_fwd_kernel<false>, dim3(grid), dim3(NT), 0, (hipStream_t)stream, g);
+  else
+#endif
+  hipLaunchKernelGGL(stem_fwd_kernel<false>, dim3(grid), dim3(NT), 0, (hipStream_t)stream, g);
   return cvl_launch_status();
 }
 

@@ -11,8 +11,20 @@ import os
 import torch  # noqa: F401  (must precede the CDLL load, see module docstring)
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-# CVL_LIB: another build of the library (same-box A/B of two builds, tools/build_base.sh)
+# CVL_LIB: another build of the library (same-box A/B of two builds, tools/build_base.sh; the
+# measurement build, tools/build_measure.sh)
 LIB_PATH = os.environ.get("CVL_LIB") or os.path.join(_HERE, "libcvlite_hip.so")
+
+
+def dispatch(key, default=0):
+    """The CVL_DISPATCH test hooks (cvl_common.h; INTEGRATION.md "Environment"): "key" (= 1) or
+    "key=value", comma-separated -- the Python side's fusion switches read here, the C library's
+    kernel-family and planner hooks in cvl_dispatch_int.  Unset: the production path."""
+    for tok in os.environ.get("CVL_DISPATCH", "").split(","):
+        k, _, v = tok.strip().partition("=")
+        if k == key:
+            return int(v) if v else 1
+    return default
 
 c_int, c_float, c_size_t, c_void_p = ctypes.c_int, ctypes.c_float, ctypes.c_size_t, ctypes.c_void_p
 P = c_void_p
@@ -54,9 +66,6 @@ SIGNATURES = {
     "cvl_bn_acc_decode": (c_int, [P, P, ctypes.c_int64, P]),
     "cvl_bn_set_exact": (c_int, [c_int]),
     "cvl_bn_acc_slots": (c_int, []),
-    "cvl_debug_wgx_stamps": (c_int, [P, c_int]),
-    "cvl_debug_stem_stamps": (c_int, [P, c_int]),
-    "cvl_debug_h_stamps": (c_int, [P, c_int]),
     "cvl_stem_conv7x7s2": (c_int, [P, c_int, c_int, c_int, P, P, P, P, P]),
     "cvl_stem_wgrad_workspace_size": (c_size_t, [c_int, c_int, c_int]),
     "cvl_stem_wgrad": (c_int, [P, c_int, c_int, c_int, P, P, c_float, P, c_size_t, P]),

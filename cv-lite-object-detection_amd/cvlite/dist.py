@@ -11,6 +11,7 @@ import os
 
 import torch
 import torch.distributed as tdist
+from . import _lib
 
 # 64 MiB buckets: few, large collectives (each RCCL ring step is xGMI-link bound; ~146 MB of fp32
 # gradients per FCOS-R50 step -> 3 buckets)
@@ -18,10 +19,10 @@ BUCKET_BYTES = 64 << 20
 
 
 def force_sync():
-    """CVL_DP_FORCE_SYNC=1: run the gradient all-reduce path even at world size 1 (a one-rank RCCL
+    """CVL_DISPATCH=dp_force_sync: run the gradient all-reduce path even at world size 1 (a one-rank RCCL
     group exercises ProcessGroupNCCL's stream ordering against the HIP-graph segments on a 1-GPU
     box; the SUM over one rank is the identity, so the step must be bit-identical)."""
-    return os.environ.get("CVL_DP_FORCE_SYNC", "0") == "1"
+    return bool(_lib.dispatch("dp_force_sync"))
 
 
 def init_from_env(backend=None):

@@ -19,26 +19,28 @@ from . import ops_nn as nn
 from .layers import BF16, Conv, ParamStore, act_dtype
 from .mobilenet_v2 import MobileNetV2
 from .resnet import ResNet50
+from . import _lib
 
 FPN_C = 256
 STRIDES = (8, 16, 32, 64, 128)
 
 
-# CVL_TOWER_PAIR=0 runs the two towers as separate launches (A/B only; the paired 10-segment
-# launches are the default)
-PAIR_TOWERS = os.environ.get("CVL_TOWER_PAIR", "1") != "0"
+# CVL_DISPATCH=no_tower_pair runs the two towers as separate launches (A/B only; the paired
+# 10-segment launches are the default)
+PAIR_TOWERS = not _lib.dispatch("no_tower_pair")
 
 
 def pair_tower0_dgrad():
     """Tower layer 0 reads the shared F: its two data gradients as ONE paired launch into a
-    temporary + one add (default), or (CVL_TOWER0_PAIR=0) two launches, the second accumulating
-    into dF.  Read per backward, so both forms are testable in one process."""
-    return os.environ.get("CVL_TOWER0_PAIR", "1") != "0"
+    temporary + one add (default), or (CVL_DISPATCH=no_tower0_pair) two launches, the second
+    accumulating into dF.  Read per backward, so both forms are testable in one process."""
+    return not _lib.dispatch("no_tower0_pair")
 
-# CVL_FPN_FUSE=0 runs P3..P5's 3x3 output convs as separate launches (A/B only)
-FUSE_FPN = os.environ.get("CVL_FPN_FUSE", "1") != "0"
-# weight-gradient split reductions batched per gradient group (ops_nn.deferred_wgrad)
-DEFER_WGRAD = os.environ.get("CVL_NO_WGRAD_DEFER", "0") != "1"
+# CVL_DISPATCH=no_fpn_fuse runs P3..P5's 3x3 output convs as separate launches (A/B only)
+FUSE_FPN = not _lib.dispatch("no_fpn_fuse")
+# weight-gradient split reductions batched per gradient group (ops_nn.deferred_wgrad;
+# CVL_DISPATCH=no_wgrad_defer: one reduction launch per weight gradient)
+DEFER_WGRAD = not _lib.dispatch("no_wgrad_defer")
 
 class FPNDetector(object):
     @staticmethod
@@ -243,7 +245,7 @@ class FPNDetector(object):
     # ---- backward ------------------------------------------------------------------------------------
     def backward(self, *head_grads, hook=None):
         """The split weight-gradient reductions run deferred: one batched launch before each gradient
-        group is reported final (hook) and one at the end (DEFER_WGRAD; CVL_NO_WGRAD_DEFER=1: off)."""
+        group is reported final (hook) and one at the end (DEFER_WGRAD; CVL_DISPATCH=no_wgrad_defer: off)."""
         s = self._saved
         if not DEFER_WGRAD:
             dA = self._heads_backward(head_grads, s["towers"], s["B"], s["shapes"], s["off"], s["P"])

@@ -29,6 +29,7 @@ import torch
 
 from . import ops_nn as nn
 from .layers import BF16, BatchNorm, Conv, ParamStore, constant, glorot_uniform
+from . import _lib
 
 STEM_K = 7
 STEM_KP = 160          # im2col K = 7*7*3 = 147 padded to a multiple of 32
@@ -60,8 +61,8 @@ def block_graph(n_stacks=1):
 
 # 3x3 separable convs on maps of at least this many pixels run SPLIT: depthwise kernel
 # (cvl_depthwise_*, HBM-bound) + pointwise 1x1 GEMM, instead of the dense fold whose 3x3 GEMM does
-# 9x the pointwise FLOPs; below it the fold's single launch wins (CVL_SEP_SPLIT_MIN_HW, 0 = never)
-SPLIT_MIN_HW = int(os.environ.get("CVL_SEP_SPLIT_MIN_HW", str(128 * 128)))
+# 9x the pointwise FLOPs; below it the fold's single launch wins (CVL_DISPATCH=sep_split_min_hw=<n>, 0 = never)
+SPLIT_MIN_HW = _lib.dispatch("sep_split_min_hw", 128 * 128)
 
 
 class _PointwiseOf(Conv):

@@ -14,6 +14,7 @@ import os
 import torch
 
 from . import ops_nn as nn
+from . import _lib
 
 BF16 = torch.bfloat16
 F32 = torch.float32
@@ -245,11 +246,11 @@ class Conv(object):
         return out, (sums if fused else None)
 
 
-# the BN backward's first pass fused into the producing data gradient (CVL_NO_BNSUM_FUSE=1: off,
+# the BN backward's first pass fused into the producing data gradient (CVL_DISPATCH=no_bnsum_fuse: off,
 # for A/B measurement)
-FUSE_BNSUM = os.environ.get("CVL_NO_BNSUM_FUSE", "0") != "1"
-# ... and a residual unit's (BN3) first pass into the next block's conv1 data gradient (CVL_NO_BNSUM_RES=1: off)
-FUSE_BNSUM_RES = FUSE_BNSUM and os.environ.get("CVL_NO_BNSUM_RES", "0") != "1"
+FUSE_BNSUM = not _lib.dispatch("no_bnsum_fuse")
+# ... and a residual unit's (BN3) first pass into the next block's conv1 data gradient (CVL_DISPATCH=no_bnsum_res: off)
+FUSE_BNSUM_RES = FUSE_BNSUM and not _lib.dispatch("no_bnsum_res")
 
 class StatsArena(object):
     """One zeroed buffer holding the (sum, sumsq) BN statistics of every conv of a forward pass as

@@ -74,7 +74,7 @@ def conv_igemm(desc, src, dst, stats=None):
     _prec(desc, src)
     n = int(_lib.load().cvl_conv_igemm_workspace_size(ctypes.byref(desc)))
     ws = torch.empty(n, dtype=torch.uint8, device=src.device) if n > 16 else None
-    _lib.call("cvl_conv_igemm", ctypes.byref(desc), ptr(src), ptr(dst), ptr(stats), ptr(ws),
+    _lib.call("cvl_conv_igemm", ctypes.byref(desc), ptr(src), ptr(dst), acc_ptr(stats), ptr(ws),
               n if ws is not None else 0, stream())
 
 
@@ -199,7 +199,7 @@ def stem_conv7x7s2(img, w_packed, bias, z, stats=None):
     """ResNet conv1 from the fp32 NHWC image (cvl_stem_conv7x7s2): z [B][Ho][Wo][64] bf16 (+ BN stats)."""
     B, H, W, C = img.shape
     assert C == 3 and img.dtype == torch.float32 and img.is_contiguous()
-    _lib.call("cvl_stem_conv7x7s2", ptr(img), B, H, W, ptr(w_packed), ptr(bias), ptr(z), ptr(stats), stream())
+    _lib.call("cvl_stem_conv7x7s2", ptr(img), B, H, W, ptr(w_packed), ptr(bias), ptr(z), acc_ptr(stats), stream())
 
 
 def stem_wgrad(img, dz, dw, beta=0.0):
@@ -225,14 +225,35 @@ ACC_SLOTS = 8
 ACC_BINS, ACC_W, ACC_E0 = 7, 22, 27
 
 
+_SLOTS = [None]          # cached cvl_bn_acc_slots() of the current mode
+
+
 def set_bn_exact(on):
-    """Library-wide BN accumulator mode (cvl_bn_set_exact); buffers made before a switch are invalid."""
+    """Library-wide BN accumulator mode (cvl_bn_set_exact); buffers made before a switch are invalid
+    -- and rejected: every entry point that takes a BN accumulator buffer checks its slot dimension
+    against the mode (acc_ptr)."""
     _lib.call("cvl_bn_set_exact", 1 if on else 0)
+    _SLOTS[0] = None
 
 
 def acc_slots():
     """uint64 slots per statistic of the current mode (cvl_bn_acc_slots): 1 or ACC_SLOTS."""
-    return int(_lib.load().cvl_bn_acc_slots())
+    if _SLOTS[0] is None:
+        _SLOTS[0] = int(_lib.load().cvl_bn_acc_slots())
+    return _SLOTS[0]
+
+
+def acc_ptr(t):
+    """Pointer of a BN accumulator buffer ([..., 2, S] int64, as bn_acc / StatsArena make them) after
+    checking S against the library's current mode: a buffer made in the other mode would be indexed
+    as [..][2][8] vs [..][2][1] by the kernels (out-of-bounds atomics), so it is refused here."""
+    if t is None:
+        return None
+    if t.dtype != torch.int64 or t.dim() < 2 or int(t.shape[-1]) != acc_slots():
+        raise _lib.CvlError("BN accumulator buffer of shape %s / %s does not match the current mode (%d slots "
+                            "per statistic): made before a cvl_bn_set_exact switch?" % (tuple(t.shape), t.dtype,
+                                                                                     acc_slots()))
+    return ptr(t)
 
 
 def bn_acc(B, C, device, zero=True):
@@ -245,7 +266,7 @@ def bn_acc_value(acc):
     """float64 values [..., 2] of a BN accumulator buffer [..., 2, ACC_SLOTS] (cvl_bn_acc_decode)."""
     acc = acc.contiguous()
     out = torch.empty(acc.shape[:-1], dtype=torch.float64, device=acc.device)
-    _lib.call("cvl_bn_acc_decode", ptr(acc), ptr(out), out.numel(), stream())
+    _lib.call("cvl_bn_acc_decode", acc_ptr(acc), ptr(out), out.numel(), stream())
     return out
 
 
@@ -284,7 +305,7 @@ def bn_acc_encode(values, exact=None):
 
 
 def bn_finalize(stats, mean_rstd, run_mean, run_var, B, C, HW, eps, momentum):
-    _lib.call("cvl_bn_finalize", ptr(stats), ptr(mean_rstd), ptr(run_mean), ptr(run_var), B, C, HW,
+    _lib.call("cvl_bn_finalize", acc_ptr(stats), ptr(mean_rstd), ptr(run_mean), ptr(run_var), B, C, HW,
               float(eps), float(momentum), stream())
 
 
@@ -295,7 +316,7 @@ def bn_apply(z, mean_rstd, gamma, beta, residual, y, B, HW, C, relu):
 
 def bn_finalize_apply(stats, mean_rstd, run_mean, run_var, z, gamma, beta, residual, y, B, HW, C, relu, eps,
                       momentum):
-    _lib.call("cvl_bn_finalize_apply_f32" if _is_f32(z) else "cvl_bn_finalize_apply", ptr(stats), ptr(mean_rstd), ptr(run_mean), ptr(run_var), ptr(z), ptr(gamma),
+    _lib.call("cvl_bn_finalize_apply_f32" if _is_f32(z) else "cvl_bn_finalize_apply", acc_ptr(stats), ptr(mean_rstd), ptr(run_mean), ptr(run_var), ptr(z), ptr(gamma),
               ptr(beta), ptr(residual), ptr(y), B, HW, C, int(relu), float(eps), float(momentum), stream())
 
 
@@ -303,8 +324,8 @@ def bn_finalize_apply_bnres(stats, mean_rstd, run_mean, run_var, z, gamma, beta,
                             res_run_mean, res_run_var, res_z, res_gamma, res_beta, res_eps, res_momentum, y, B,
                             HW, C, relu, eps, momentum):
     """y = act(BN(z) + BN_res(res_z)) with both finalizes in one launch (cvl_bn_finalize_apply_bnres)."""
-    _lib.call("cvl_bn_finalize_apply_bnres", ptr(stats), ptr(mean_rstd), ptr(run_mean), ptr(run_var), ptr(z),
-              ptr(gamma), ptr(beta), ptr(res_stats), ptr(res_mean_rstd), ptr(res_run_mean), ptr(res_run_var),
+    _lib.call("cvl_bn_finalize_apply_bnres", acc_ptr(stats), ptr(mean_rstd), ptr(run_mean), ptr(run_var), ptr(z),
+              ptr(gamma), ptr(beta), acc_ptr(res_stats), ptr(res_mean_rstd), ptr(res_run_mean), ptr(res_run_var),
               ptr(res_z), ptr(res_gamma), ptr(res_beta), float(res_eps), float(res_momentum), ptr(y), B, HW, C,
               int(relu), float(eps), float(momentum), stream())
 
@@ -380,7 +401,7 @@ def conv_igemm_dgrad_bnsum(desc, src, dst, z, mean_rstd, gamma, beta, sums, act_
         sums.zero_()
     flag = ctypes.c_int32(0)
     _lib.call("cvl_conv_igemm_dgrad_bnsum", ctypes.byref(desc), ptr(src), ptr(dst), ptr(z), ptr(mean_rstd), ptr(gamma),
-              ptr(beta), float(act_hi), ptr(sums), ctypes.addressof(flag), ptr(ws), n if ws is not None else 0,
+              ptr(beta), float(act_hi), acc_ptr(sums), ctypes.addressof(flag), ptr(ws), n if ws is not None else 0,
               stream())
     return bool(flag.value)
 
@@ -396,7 +417,7 @@ def conv_igemm_dgrad_bnsum_res(desc, src, dst, y, z, mean_rstd, gamma, beta, sum
         sums.zero_()
     flag = ctypes.c_int32(0)
     _lib.call("cvl_conv_igemm_dgrad_bnsum_res", ctypes.byref(desc), ptr(src), ptr(dst), ptr(y), ptr(z),
-              ptr(mean_rstd), ptr(gamma), ptr(beta), ptr(sums), ctypes.addressof(flag), ptr(ws),
+              ptr(mean_rstd), ptr(gamma), ptr(beta), acc_ptr(sums), ctypes.addressof(flag), ptr(ws),
               n if ws is not None else 0, stream())
     return bool(flag.value)
 
@@ -404,14 +425,14 @@ def conv_igemm_dgrad_bnsum_res(desc, src, dst, y, z, mean_rstd, gamma, beta, sum
 def bn_backward_res_sums(dy, y, z, mean_rstd, gamma, sums, dz, g_out, dgamma, dbeta, B, HW, C, beta_acc=0.0,
                          conv_dbias=None):
     """Second pass of a residual unit's BN backward (mask y > 0, g_out = masked dy) from the fused sums."""
-    _lib.call("cvl_bn_backward_res_sums", ptr(dy), ptr(y), ptr(z), ptr(mean_rstd), ptr(gamma), ptr(sums), ptr(dz),
+    _lib.call("cvl_bn_backward_res_sums", ptr(dy), ptr(y), ptr(z), ptr(mean_rstd), ptr(gamma), acc_ptr(sums), ptr(dz),
               ptr(g_out), ptr(dgamma), ptr(dbeta), float(beta_acc), ptr(conv_dbias), B, HW, C, stream())
 
 
 def bn_backward_relu_sums(dy, z, mean_rstd, gamma, beta, sums, dz, dgamma, dbeta, B, HW, C, beta_acc=0.0,
                           conv_dbias=None, act_hi=float("inf")):
     """Second pass of bn_backward_relu from the fused first-pass sums (conv_igemm_dgrad_bnsum)."""
-    _lib.call("cvl_bn_backward_relu_sums", ptr(dy), ptr(z), ptr(mean_rstd), ptr(gamma), ptr(beta), ptr(sums), ptr(dz),
+    _lib.call("cvl_bn_backward_relu_sums", ptr(dy), ptr(z), ptr(mean_rstd), ptr(gamma), ptr(beta), acc_ptr(sums), ptr(dz),
               ptr(dgamma), ptr(dbeta), float(beta_acc), ptr(conv_dbias), float(act_hi), B, HW, C, stream())
 
 
@@ -553,11 +574,11 @@ def gather_rows(src, idx, dst):
 def bn_stats(x, B, HW, C, stats):
     n = int(_lib.load().cvl_bn_stats_workspace_size(B, HW, C))
     ws = torch.empty(max(n, 16), dtype=torch.uint8, device=x.device)
-    _lib.call("cvl_bn_stats", ptr(x), B, HW, C, ptr(stats), ptr(ws), ws.numel(), stream())
+    _lib.call("cvl_bn_stats", ptr(x), B, HW, C, acc_ptr(stats), ptr(ws), ws.numel(), stream())
 
 
 def bn_finalize_grouped(stats, mean_rstd, run_mean, run_var, B, C, HW, group, eps, momentum):
-    _lib.call("cvl_bn_finalize_grouped", ptr(stats), ptr(mean_rstd), ptr(run_mean), ptr(run_var), B, C, HW,
+    _lib.call("cvl_bn_finalize_grouped", acc_ptr(stats), ptr(mean_rstd), ptr(run_mean), ptr(run_var), B, C, HW,
               int(group), float(eps), float(momentum), stream())
 
 

@@ -14,12 +14,13 @@ import torch
 
 from . import ops_nn as nn
 from .layers import BF16, BatchNorm, Conv, ConvBN, StatsArena
+from . import _lib
 
 STEM_K = 7
-# the stem's BN -> ReLU -> max-pool as one pass from z (CVL_STEM_NO_FUSE_POOL=1: BN apply + pool)
-FUSE_POOL = os.environ.get("CVL_STEM_NO_FUSE_POOL", "0") != "1"
-# projection shortcut's BN applied inside conv3's BN launch (CVL_NO_SC_BN_FUSE=1: stored and re-read)
-FUSE_SC_BN = os.environ.get("CVL_NO_SC_BN_FUSE", "0") != "1"
+# the stem's BN -> ReLU -> max-pool as one pass from z (CVL_DISPATCH=no_stem_pool_fuse: BN apply + pool)
+FUSE_POOL = not _lib.dispatch("no_stem_pool_fuse")
+# projection shortcut's BN applied inside conv3's BN launch (CVL_DISPATCH=no_sc_bn_fuse: stored and re-read)
+FUSE_SC_BN = not _lib.dispatch("no_sc_bn_fuse")
 STEM_KP = 168            # the stem kernels' K: 7 kernel rows x (7 x 3 values padded to 24)
 
 

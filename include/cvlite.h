@@ -195,12 +195,6 @@ const char* cvl_conv_kernel_name(int code);
  * = start stamp, slot[1] += elapsed ticks, slot[2] += 1 (uint64 x3 device buffer, zero it first).
  * cvl_probe_clock_hz = ticks per second of the GPU wall clock. */
 int cvl_probe_begin(uint64_t* slot, cvl_stream_t stream);
-/* Measurement hook (tools/wgx_stamps.py): with CVL_WGX_STAMPS=1 in the environment, the 2-D weight
- * gradient kernel stamps (entry, prologue landed, loop done, epilogue stored) per workgroup; this
- * copies the last stamped launch's u64 [grid][4] to host memory (<= max_wgs rows), returns grid. */
-int cvl_debug_wgx_stamps(uint64_t* host, int max_wgs);
-int cvl_debug_stem_stamps(uint64_t* host, int max_wgs);   /* CVL_STEM_STAMPS=1 builds: stem forward stamps */
-int cvl_debug_h_stamps(uint64_t* host, int max_wgs);      /* CVL_H_STAMPS=1 builds: H64 (3x3) launch stamps */
 int cvl_probe_end(uint64_t* slot, cvl_stream_t stream);
 double cvl_probe_clock_hz(void);
 

@@ -17,6 +17,17 @@ def pytest_configure(config):
     config.addinivalue_line("markers", "slow: long-running CPU test")
 
 
+@pytest.fixture
+def dispatch(monkeypatch):
+    """Sets CVL_DISPATCH test hooks (cvl_common.h; INTEGRATION.md "Environment") for one test:
+    dispatch("no_h", "l_min_tiles=1"); a key given again replaces its earlier value."""
+    def add(*items):
+        keys = {i.split("=")[0] for i in items}
+        cur = [k for k in os.environ.get("CVL_DISPATCH", "").split(",") if k and k.split("=")[0] not in keys]
+        monkeypatch.setenv("CVL_DISPATCH", ",".join(cur + list(items)))
+    return add
+
+
 @pytest.fixture(scope="session")
 def golden():
     import numpy as np

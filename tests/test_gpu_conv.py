@@ -30,28 +30,27 @@ def ref_conv(x, w, b, stride, pad):
 
 
 @pytest.fixture(params=["base", "l", "l256", "x32"])
-def kern(request, monkeypatch):
+def kern(request, dispatch):
     """Run a test through the 128-row register-staged kernel ("base"), the 256-row LDS-DMA kernel
     ("l", normally taken only by launches with >= 128 tiles; 128/64-wide N tiles), its
     256x256-tile form ("l256", Npad % 256 == 0 only) and the 256x256 32-deep-K ring kernel ("x32",
     the default for those launches).  Weight gradients: "base" runs the 128-wide k-tile kernel,
     "l"/"l256" the row-table LDS-DMA kernel (conv_wgrad_l.hip), "x32" the default dispatch
     (conv_wgrad_x.hip where Npad % 256 == 0)."""
-    monkeypatch.setenv("CVL_CONV_NO_H", "1")      # the halo kernels have their own tests (test_gpu_conv_h.py)
-    monkeypatch.setenv("CVL_WGRAD_NO_H", "1")
-    if request.param in ("l", "l256", "x32"):
-        monkeypatch.setenv("CVL_CONV_L_MIN_TILES", "1")
-    if request.param == "l":
-        monkeypatch.setenv("CVL_CONV_NO_256", "1")
-    if request.param in ("l256", "x32"):
-        monkeypatch.setenv("CVL_CONV_L256_MIN_TILES", "1")
-    if request.param == "l256":
-        monkeypatch.setenv("CVL_CONV_NO_X", "1")
-    if request.param != "x32":
-        monkeypatch.setenv("CVL_WGRAD_NO_X", "1")
-    if request.param not in ("l256", "x", "x32"):
-        monkeypatch.setenv("CVL_CONV_NO_L", "1")
-        monkeypatch.setenv("CVL_WGRAD_NO_L", "1")
+    p = request.param
+    dispatch("no_h", "wg_no_h")        # the halo kernels have their own tests (test_gpu_conv_h.py)
+    if p in ("l", "l256", "x32"):
+        dispatch("l_min_tiles=1")
+    if p == "l":
+        dispatch("no_256")
+    if p in ("l256", "x32"):
+        dispatch("l256_min_tiles=1")
+    if p == "l256":
+        dispatch("no_x")
+    if p != "x32":
+        dispatch("wg_no_x")
+    if p == "base":
+        dispatch("no_l", "wg_no_l")
     return request.param
 
 
@@ -348,14 +347,14 @@ def _tower_pair_case(B, C, shapes, seed):
 
 @pytest.mark.parametrize("shared_x", [False, True])
 @pytest.mark.parametrize("variant", ["wx", "fallback"])
-def test_conv_wgrad_grouped_tower_pair(shared_x, variant, monkeypatch):
+def test_conv_wgrad_grouped_tower_pair(shared_x, variant, dispatch):
     """cvl_conv_wgrad_grouped in the paired-tower form (fcos.py:16-27, 76-101): 10 segments = 2 towers
     x 5 levels, group g -> dW_g, dY rows of tower t at t*B*P; the source is either the paired
     activation buffer (layers 1-3) or one map both towers read (layer 0, shared_x).  "fallback"
     runs one single-group launch per group.  Reference: per level and tower, torch fp64 autograd."""
     from cvlite import _lib, ops_nn as nn
     if variant == "fallback":
-        monkeypatch.setenv("CVL_WGRAD_NO_X", "1")
+        dispatch("wg_no_x")
     B, C = 4, 256
     shapes = [(24, 20), (12, 10), (6, 5), (3, 3), (2, 2)]
     off, P, xs, dys = _tower_pair_case(B, C, shapes, 21)

@@ -102,9 +102,9 @@ def test_h_fwd_dgrad(case):
 
 
 @pytest.mark.parametrize("B,H,Cin", [(4, 128, 64), (3, 8, 32), (16, 128, 64)])
-def test_h_resident_weights_bit_identical(B, H, Cin, monkeypatch):
+def test_h_resident_weights_bit_identical(B, H, Cin, dispatch):
     """WRES (weights resident in LDS for single-N-tile launches with Cin <= 64: the conv2_x 3x3 units,
-    halos streamed alone) gives the same bits as the per-block weight staging (CVL_CONV_H_NO_WRES=1):
+    halos streamed alone) gives the same bits as the per-block weight staging (CVL_DISPATCH=h_no_wres):
     forward with bias / ReLU / BN statistics, data gradient, and the data gradient with the fused
     BN-backward first pass (the step's form), including the bs 16 128x128 geometry."""
     from cvlite import ops_nn as nn
@@ -121,7 +121,7 @@ def test_h_resident_weights_bit_identical(B, H, Cin, monkeypatch):
     ga, be = (torch.rand(Cin, generator=g) + 0.5).cuda(), torch.randn(Cin, generator=g).cuda()
     res = []
     for off in ("1", "0"):
-        monkeypatch.setenv("CVL_CONV_H_NO_WRES", off)
+        dispatch("h_no_wres=" + off)
         out = torch.empty((B, H, H, Cout), dtype=BF, device="cuda")
         st = nn.bn_acc(B, Cout, "cuda")
         d = nn.make_desc(nn.FWD, B, Cin, 3, 3, 1, 1, 1, npad, Cout, Cout, [nn.seg(H, H, H, H, wf, bias)], relu_out=True)
@@ -145,7 +145,7 @@ def test_h_resident_weights_bit_identical(B, H, Cin, monkeypatch):
         torch.testing.assert_close(a[4], b2[4], rtol=1e-12, atol=1e-9 * float(a[4].abs().max()))
 
 
-def test_h_segments_fpn_trio():
+def test_h_segments_fpn_trio(dispatch):
     """The FPN's three 3x3 output convs (fcos.py:62-66: P3r, P4r, P5 -> P3, P4, P5, own weights and
     biases) as ONE 3-segment launch from one packed source buffer into the level-major F buffer."""
     from cvlite import ops_nn as nn
@@ -165,12 +165,8 @@ def test_h_segments_fpn_trio():
             for l, (h, w) in enumerate(shapes)]
     out = torch.empty_like(src)
     # 256-wide tiles would go to the 256 x 256 kernels; force the narrow path for the trio
-    import os
-    os.environ["CVL_CONV_NO_256"] = "1"
-    try:
-        nn.conv_igemm(nn.make_desc(nn.FWD, B, C, 3, 3, 1, 1, 1, C, C, C, segs), src, out)
-    finally:
-        del os.environ["CVL_CONV_NO_256"]
+    dispatch("no_256")
+    nn.conv_igemm(nn.make_desc(nn.FWD, B, C, 3, 3, 1, 1, 1, C, C, C, segs), src, out)
     assert "conv_igemm_h_kernel" in last_kernel(), last_kernel()
     for l, (h, w) in enumerate(shapes):
         got = out[base[l]:base[l] + B * h * w].reshape(B, h, w, C).double().cpu()

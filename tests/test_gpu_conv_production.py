@@ -123,19 +123,19 @@ def test_tower_pair_fwd_dgrad_configs1_layout():
 
 
 @pytest.mark.parametrize("variant", ["p", "p64", "p256", "l128", "wide"])
-def test_wide_1x1_with_bn_stats_configs1(variant, monkeypatch):
+def test_wide_1x1_with_bn_stats_configs1(variant, dispatch):
     """conv2_block1_3 (1x1 64 -> 256 at 128x128, bs 16: 1,024 M tiles) with the fused per-image BN
     statistics epilogue, as ConvBN.forward runs it: on the persistent 1x1 kernel (default; also
     forced to its 64- and 256-wide tiles), and with it off on the one-tile-per-workgroup L kernel's
-    256x128 tile and forced onto the 256-wide tiles (CVL_CONV_W256_MIN_K=0)."""
+    256x128 tile and forced onto the 256-wide tiles (CVL_DISPATCH=w256_min_k=0)."""
     from cvlite import ops_nn as nn
     wide = variant == "wide"
     if variant in ("l128", "wide"):
-        monkeypatch.setenv("CVL_CONV_NO_P", "1")
+        dispatch("no_p")
     if variant in ("p64", "p256"):
-        monkeypatch.setenv("CVL_CONV_P_BN", variant[1:])
+        dispatch("p_bn=" + variant[1:])
     if wide:
-        monkeypatch.setenv("CVL_CONV_W256_MIN_K", "0")
+        dispatch("w256_min_k=0")
     B, H, Cin, Cout = 16, 128, 64, 256
     g = torch.Generator(device="cuda").manual_seed(12)
     x = rnd((B, H, H, Cin), 1.0, g)
@@ -204,15 +204,13 @@ def test_retina_cls_head_f32_epilogue_configs4(N, NP):
 @pytest.mark.parametrize("mode,B,H,W,C,N", [("fwd", 2, 64, 64, 256, 256), ("dgrad", 3, 32, 32, 512, 256),
                                            ("fwd", 3, 8, 8, 256, 256), ("dgrad", 5, 4, 4, 256, 512),
                                            ("fwd", 2, 16, 16, 256, 256), ("fwd", 1, 64, 64, 64, 256)])
-def test_x32_tile_geometries(monkeypatch, mode, B, H, W, C, N):
+def test_x32_tile_geometries(dispatch, mode, B, H, W, C, N):
     """The 256x256 ring kernel (X32) on 3x3 tile geometries: R image rows of one image (W = 64 / 32 /
     16), several whole images per tile (8x8: 4, 4x4: 16 per tile, batches that leave the last
     tile's images partly absent), Cin 64 / 256 / 512, fwd with bias + ReLU + BN statistics and
     dgrad, against fp64."""
     from cvlite import ops_nn as nn
-    monkeypatch.setenv("CVL_CONV_L_MIN_TILES", "1")
-    monkeypatch.setenv("CVL_CONV_L256_MIN_TILES", "1")
-    monkeypatch.setenv("CVL_CONV_NO_H", "1")
+    dispatch("l_min_tiles=1", "l256_min_tiles=1", "no_h")
     g = torch.Generator(device="cuda").manual_seed(B * 1000 + H + C)
     x = rnd((B, H, W, C), 1.0, g)
     if mode == "fwd":

@@ -98,7 +98,7 @@ def _nccl_worker(rank, port, out):
     all-reduces on ProcessGroupNCCL's stream between the segment replays (the N>1 bench path)."""
     sys.path[:0] = [ROOT, PKG]
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK="0", WORLD_SIZE="1",
-                      CVL_DP_FORCE_SYNC="1")
+                      CVL_DISPATCH="dp_force_sync")
     import torch.distributed as tdist
     from cvlite import dist
     from cvlite.fcos_net import FCOSNet

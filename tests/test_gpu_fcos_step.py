@@ -187,9 +187,9 @@ def test_jitter_trainer_dataset_with_many_boxes():
 
 
 @pytest.mark.parametrize("case", [(2, 8, 8, 256, 256, 3), (2, 16, 16, 128, 128, 3), (4, 8, 8, 512, 512, 3)])
-def test_split_k_matches_unsplit(case, monkeypatch):
-    """The split-K accumulation (small grids; CVL_KSPLIT_MIN_NK = 4, the default) vs the same launch
-    unsplit (CVL_KSPLIT_MIN_NK huge): fp32 destinations agree to accumulation-order rounding
+def test_split_k_matches_unsplit(case, dispatch):
+    """The split-K accumulation (small grids; CVL_DISPATCH ksplit_min_nk = 4, the default) vs the same launch
+    unsplit (ksplit_min_nk huge): fp32 destinations agree to accumulation-order rounding
     (rel-L2 <= 1e-6) and both match the fp64 convolution of the same bf16 operands at 1e-5."""
     import torch.nn.functional as F
     from cvlite import ops_nn as nn
@@ -204,7 +204,7 @@ def test_split_k_matches_unsplit(case, monkeypatch):
                    padding=k // 2).permute(0, 2, 3, 1)
     outs = []
     for min_nk in ("4", "100000"):
-        monkeypatch.setenv("CVL_KSPLIT_MIN_NK", min_nk)
+        dispatch("ksplit_min_nk=" + min_nk)
         out = torch.zeros((B, H, W, Cout), dtype=torch.float32, device="cuda")
         d = nn.make_desc(nn.FWD, B, Cin, k, k, 1, k // 2, k // 2, npad, Cout, Cout, [nn.seg(H, W, H, W, wf, None)],
                          dst_f32=True)
@@ -218,16 +218,16 @@ def test_split_k_matches_unsplit(case, monkeypatch):
         assert float((o - ref).norm() / ref.norm()) <= 1e-5
 
 
-def test_tower0_dgrad_forms_agree(monkeypatch):
+def test_tower0_dgrad_forms_agree(dispatch):
     """Tower layer 0's two data gradients (both towers read the shared F): the paired launch into a
-    temporary + one add (CVL_TOWER0_PAIR=1, default) and two launches accumulating into dF
-    (CVL_TOWER0_PAIR=0) give dF within bf16 rounding, and the whole trunk backward agrees."""
+    temporary + one add (default) and two launches accumulating into dF
+    (CVL_DISPATCH=no_tower0_pair) give dF within bf16 rounding, and the whole trunk backward agrees."""
     from cvlite.fcos_net import FCOSNet
     from cvlite.train_fcos import synthetic_batch
     C, B, D = 20, 2, 128
     res = {}
     for flag in ("1", "0"):
-        monkeypatch.setenv("CVL_TOWER0_PAIR", flag)
+        dispatch("no_tower0_pair=" + ("0" if flag == "1" else "1"))
         net = FCOSNet(C, seed=5)
         imgs, _, _ = synthetic_batch(B, D, D, C, seed=1)
         reg, cls = net.forward(imgs)

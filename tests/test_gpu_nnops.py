@@ -378,14 +378,14 @@ def test_dgrad_fused_bn_backward_first_pass(B, H, Cin, Cout, k, expect_fused):
     (8, 32, 256, 1024),      # conv4_x
     (4, 16, 512, 2048),      # conv5_x: one tile per image
 ])
-def test_dgrad_fused_bn_backward_residual(B, H, Cin, Cout, monkeypatch):
+def test_dgrad_fused_bn_backward_residual(B, H, Cin, Cout, dispatch):
     """cvl_conv_igemm_dgrad_bnsum_res + cvl_bn_backward_res_sums (a bottleneck's conv3 BN, whose dy the
     next block's conv1 data gradient completes by accumulating onto the shortcut gradient) against the
     plain accumulating data gradient + two-pass cvl_bn_backward with the y mask: dX bit-identical,
     first-pass sums within fp32 summation order, dz / g_out / dgamma / dbeta as the two-pass form."""
     from cvlite import ops_nn as nn
     from cvlite.layers import Conv, ParamStore
-    monkeypatch.setenv("CVL_BNSUM_RES_MIN_HW", "0")     # production fuses only maps >= 64x64
+    dispatch("bnsum_res_min_hw=0")     # production fuses only maps >= 64x64
     W = H
     C = Cout                     # block width: the BN3 channels = the next conv1's input channels
     dev = torch.device("cuda")
@@ -427,7 +427,7 @@ def test_dgrad_fused_bn_backward_residual(B, H, Cin, Cout, monkeypatch):
     torch.testing.assert_close(dg_f, dg_p, rtol=1e-5, atol=1e-5 * float(dg_p.abs().max()))
     torch.testing.assert_close(db_f, db_p, rtol=1e-5, atol=1e-5 * float(db_p.abs().max()))
     if H * W < 4096:             # the production threshold: the plain path, sums untouched
-        monkeypatch.delenv("CVL_BNSUM_RES_MIN_HW")
+        dispatch("bnsum_res_min_hw=4096")
         sums2 = torch.zeros_like(sums)
         dx_2 = old.clone()
         assert not nn.conv_igemm_dgrad_bnsum_res(d, dy_next, dx_2, y, z, mr, gamma, beta, sums2)

@@ -109,3 +109,32 @@ def test_stem_module_matches_direct_conv():
                     stride=1, dilation=2)                       # [3, 64, 7(+), 7(+)]
     refw = refw[:, :, :7, :7].permute(2, 3, 0, 1)             # [ky, kx, c, co]
     assert rel_l2(stem.conv.dw.view(7, 7, 3, 64), refw) < 1e-5
+
+
+@pytest.mark.parametrize("bad", [float("nan"), float("inf")])
+def test_stem_forward_nonfinite_pixel_stays_local(bad):
+    """A non-finite image value reaches only the outputs whose 7x7/2 window (ZeroPadding2D(3)) holds
+    it: the stem kernel's pad K (the 3 values after each 21-value kernel row, and the 8th kernel row)
+    enters the MFMAs as exact zeros, not as neighbouring image data under zero weights (0 * NaN).
+    Every other output is bit-identical to the clean run."""
+    from cvlite import ops_nn as nn
+    B, H, W = 1, 64, 80
+    g = torch.Generator(device="cpu").manual_seed(5)
+    img = (torch.rand((B, H, W, 3), generator=g) * 2 - 1).cuda()
+    w = (torch.randn((7, 7, 3, 64), generator=g) * 0.1).cuda()
+    bias = (torch.randn(64, generator=g) * 0.1).cuda()
+    wf = _w_packed(w)
+    Ho, Wo = (H - 1) // 2 + 1, (W - 1) // 2 + 1
+    z0 = torch.empty((B, Ho, Wo, 64), dtype=BF, device="cuda")
+    nn.stem_conv7x7s2(img, wf, bias, z0, nn.bn_acc(B, 64, "cuda"))
+    for (y, x) in ((10, 20), (31, 0), (63, 79)):
+        bad_img = img.clone()
+        bad_img[0, y, x, 1] = bad
+        z = torch.empty_like(z0)
+        nn.stem_conv7x7s2(bad_img, wf, bias, z, nn.bn_acc(B, 64, "cuda"))
+        torch.cuda.synchronize()
+        oy = torch.arange(Ho, device="cuda")[:, None]
+        ox = torch.arange(Wo, device="cuda")[None, :]
+        hit = ((2 * oy - y).abs() <= 3) & ((2 * ox - x).abs() <= 3)
+        assert torch.equal(z[0][~hit], z0[0][~hit]), (y, x)
+        assert not torch.isfinite(z[0][hit].float()).all(), (y, x)

@@ -21,10 +21,8 @@ for s in $steps; do
              tail -4 gpurun_out/${tag}_pytest.log ;;
     bench)   run 150 gpurun_out/${tag}_bench.err bash -c "python -u bench.py --steps 30 --runs 1 --no-cpu-baseline > gpurun_out/${tag}_bench.json"
              tail -c 300 gpurun_out/${tag}_bench.json; echo ;;
-    benchs)  run 150 gpurun_out/${tag}_benchs.err bash -c "CVL_NO_SC_BN_FUSE=1 python -u bench.py --steps 30 --runs 1 --no-cpu-baseline > gpurun_out/${tag}_benchs.json"
+    benchs)  run 150 gpurun_out/${tag}_benchs.err bash -c "CVL_DISPATCH=no_sc_bn_fuse python -u bench.py --steps 30 --runs 1 --no-cpu-baseline > gpurun_out/${tag}_benchs.json"
              tail -c 200 gpurun_out/${tag}_benchs.json; echo ;;
-    benchf)  run 150 gpurun_out/${tag}_benchf.err bash -c "CVL_BN_FOLD=1 python -u bench.py --steps 30 --runs 1 --no-cpu-baseline > gpurun_out/${tag}_benchf.json"
-             tail -c 200 gpurun_out/${tag}_benchf.json; echo ;;
     benchx)  run 150 gpurun_out/${tag}_benchx.err bash -c "CVL_BN_EXACT=1 python -u bench.py --steps 30 --runs 1 --no-cpu-baseline > gpurun_out/${tag}_benchx.json"
              tail -c 200 gpurun_out/${tag}_benchx.json; echo ;;
     table)   run 120 gpurun_out/${tag}_table.log python -u tools/conv_table.py --out gpurun_out/${tag}_conv_table.md
@@ -36,7 +34,7 @@ for s in $steps; do
     pprobe)  run 90 gpurun_out/${tag}_pprobe.md python -u tools/p_probe.py; cat gpurun_out/${tag}_pprobe.md ;;
     pstamps) run 90 gpurun_out/${tag}_pstamps.txt python -u tools/p_stamps.py; cat gpurun_out/${tag}_pstamps.txt ;;
     hstamps) run 90 gpurun_out/${tag}_hstamps.md python -u tools/h64_stamps.py; cat gpurun_out/${tag}_hstamps.md ;;
-    stem)    run 200 gpurun_out/${tag}_stem.log python -u -m pytest tests/test_gpu_stem.py tests/test_gpu_bn_acc.py tests/test_gpu_bn_fold.py -q --timeout 150 --timeout-method thread
+    stem)    run 200 gpurun_out/${tag}_stem.log python -u -m pytest tests/test_gpu_stem.py tests/test_gpu_bn_acc.py -q --timeout 150 --timeout-method thread
              tail -3 gpurun_out/${tag}_stem.log ;;
   esac
 done

@@ -9,6 +9,7 @@ import sys
 
 os.environ["CVL_STEM_STAMPS"] = "1"
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+os.environ.setdefault("CVL_LIB", os.path.join(ROOT, "ab", "libcvlite_measure.so"))  # tools/build_measure.sh
 sys.path[:0] = [ROOT, os.path.join(ROOT, "cv-lite-object-detection_amd")]
 import numpy as np  # noqa: E402
 import torch  # noqa: E402

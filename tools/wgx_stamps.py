@@ -10,6 +10,7 @@ import sys
 
 os.environ["CVL_WGX_STAMPS"] = "1"
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+os.environ.setdefault("CVL_LIB", os.path.join(ROOT, "ab", "libcvlite_measure.so"))  # tools/build_measure.sh
 sys.path[:0] = [ROOT, os.path.join(ROOT, "cv-lite-object-detection_amd"), os.path.join(ROOT, "tools")]
 import torch  # noqa: E402
 

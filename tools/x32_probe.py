@@ -3,6 +3,7 @@ import os
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+os.environ.setdefault("CVL_LIB", os.path.join(ROOT, "ab", "libcvlite_measure.so"))  # tools/build_measure.sh
 sys.path[:0] = [ROOT, os.path.join(ROOT, "cv-lite-object-detection_amd")]
 import torch  # noqa: E402
 
