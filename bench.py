@@ -247,6 +247,22 @@ def _cores():
     return cores
 
 
+def _spread(rates):
+    """The spread a CPU baseline carries beside its median: the timed samples' min / max and the
+    host it ran on (the GPU boxes differ in CPU model and in co-tenant load, so the same bounded
+    sample has measured 2.0-3.0 img/s box to box)."""
+    cpu = ""
+    try:
+        with open("/proc/cpuinfo") as f:
+            cpu = next((l.split(":", 1)[1].strip() for l in f if l.startswith("model name")), "")
+    except OSError:
+        pass
+    lo, hi = min(rates), max(rates)
+    med = sorted(rates)[len(rates) // 2]
+    return {"min": round(lo, 4), "max": round(hi, 4), "rel_range": round((hi - lo) / med, 4) if med else None,
+            "loadavg_1m": round(os.getloadavg()[0], 2), "host_cpu": cpu}
+
+
 def cpu_baseline(H, W, cfg1_images=8, bs=16, timed_images=(8, 8, 8)):
     """The torch-CPU restatement of the reference step (oracle/model_ref.py: batch-1 forwards,
     per-image BN, gradient sum, /bs, clip, Keras SGD), SURVEY.md §8d protocol on a bounded sample:
@@ -282,6 +298,7 @@ def cpu_baseline(H, W, cfg1_images=8, bs=16, timed_images=(8, 8, 8)):
         print("[bench] cpu_baseline timed step: %.3f img/s" % rates[-1], file=sys.stderr, flush=True)
     return {"value": round(sorted(rates)[len(rates) // 2], 4), "unit": "images/s", "cores": cores,
             "kind": "port", "configs0_step_s": round(cfg1_s, 3), "timed_img_s": [round(r, 4) for r in rates],
+            "spread": _spread(rates),
             "sample": "torch-CPU fp32 restatement of the train_fcos.py step (oracle/model_ref.py): configs[0] "
                       "(one step, %d synthetic %dx%d images, %.1f s) as warm-up, then 3 timed steps of 8 images "
                       "of the bs=%d workload (per-image fwd+bwd, clip, SGD), median img/s, %d threads"
@@ -320,6 +337,7 @@ def cpu_baseline_retina(S, C, timed_images=2):
             rates.append(1.0 / (time.time() - t0))
         print("[bench] cpu_baseline retinanet image %d: %.1f s" % (i, time.time() - t0), file=sys.stderr, flush=True)
     return {"value": round(sorted(rates)[len(rates) // 2], 4), "unit": "images/s", "cores": cores, "kind": "port",
+            "spread": _spread(rates),
             "sample": "torch-CPU fp32 restatement of RetinaNet.train_loss fwd+bwd + clip/SGD (oracle/model_ref.py), "
                       "%dx%d C=%d, 1 warm-up + %d timed single-image steps, median, %d threads" % (S, S, C, timed_images,
                                                                                            cores)}
@@ -352,6 +370,7 @@ def cpu_baseline_centernet(S, C, timed_batches=2, sub_batch=2):
             rates.append(sub_batch / (time.time() - t0))
         print("[bench] cpu_baseline centernet step %d: %.1f s" % (i, time.time() - t0), file=sys.stderr, flush=True)
     return {"value": round(sorted(rates)[len(rates) // 2], 4), "unit": "images/s", "cores": cores, "kind": "port",
+            "spread": _spread(rates),
             "sample": "torch-CPU fp32 restatement of tf_centernet_hourglass.train_step (oracle/centernet_model_ref.py),"
                       " %dx%d C=%d, sub-batch %d: 1 warm-up + %d timed steps of %d images, median, %d threads"
                       % (S, S, C, sub_batch, timed_batches, sub_batch, cores)}
@@ -380,7 +399,9 @@ def dominant_conv_roofline(run_step, iters=10):
         rows = sum(d.B * d.seg[i].Hr * d.seg[i].Wr for i in range(d.nseg))
         srows = sum(d.B * d.seg[i].Hs * d.seg[i].Ws for i in range(d.nseg))
         K = d.KH * d.KW * d.Cin
-        fl = 2.0 * rows * K * d.n_store
+        # FLOPs over the forward output pixels: a data gradient's source (Hs, Ws) is dY, its result
+        # (Hr, Wr) the forward input -- s^2 times as many pixels for stride s
+        fl = 2.0 * (srows if kind == "igemm" and d.mode == 1 else rows) * K * d.n_store
         if kind == "igemm":
             by = srows * d.Cin * 2 + rows * d.n_store * (4 if d.dst_f32 else 2) + d.nseg * d.Npad * K * 2
         else:
@@ -584,6 +605,31 @@ def launch_ranks(n, argv):
     return subprocess.call(cmd, env=env)
 
 
+def dp_timeline(tr, batch):
+    """The gradient all-reduce plan of the step (dist.GradSync): per gradient group, in the order
+    the backward finalises them, its bucket bytes; when the all-reduce path is live (world > 1, or
+    one rank with CVL_DISPATCH=dp_force_sync under a process group) also one traced step's enqueue
+    point (device ms from step start at the group's ready point, i.e. after the graph segment that
+    finalises it) and the time its all-reduces completed.  Runs on every rank (collectives);
+    outside the timed region."""
+    sync = tr.sync
+    if sync is None or not sync.active:
+        plan = dist.GradSync(tr.net.store, tr.net.grad_groups()).plan()
+        return {"live": False, "bucket_bytes": dist.BUCKET_BYTES,
+                "groups": [{"group": n, "bucket_mb": [round(b / 2 ** 20, 2) for b in bs]} for n, bs in plan]}
+    tr.load_batch(*batch)
+    torch.cuda.synchronize()
+    end = torch.cuda.Event(enable_timing=True)
+    sync.begin_trace()
+    t0 = sync.trace["t0"]
+    tr.step()
+    end.record()
+    rows = sync.end_trace()
+    return {"live": True, "bucket_bytes": dist.BUCKET_BYTES, "traced_step_ms": round(t0.elapsed_time(end), 3),
+            "groups": [{"group": n, "bucket_mb": [round(b / 2 ** 20, 2) for b in bs], "ready_ms": round(r, 3),
+                        "allreduce_done_ms": None if d is None else round(d, 3)} for n, bs, r, d in rows]}
+
+
 def dist_info(world):
     import torch.distributed as tdist
     if tdist.is_available() and tdist.is_initialized():
@@ -646,10 +692,11 @@ def main():
     losses = tr.losses.detach().double().sum(0).cpu().tolist()
     img_s = world * B * args.steps / _median_run(times)
     fl_img = train_flops_per_image(H, W)
+    in_s, in_n = nn.probe_seconds(net.tower_probe)     # the timed steps' tower launches only
+    grad_ar = dp_timeline(tr, pool[0])                  # (replays the graph: the probe buffer stays live)
     if rank != 0:
         dist.barrier()
         return
-    in_s, in_n = nn.probe_seconds(net.tower_probe)
     net.tower_probe = None
     roof = tower_roofline(net, B, H, W, in_s, in_n, pmc=(B, H, W) == (16, 512, 512))
     roof["backbone_3x3"] = measure_backbone_3x3(net, B, H, W)
@@ -661,7 +708,7 @@ def main():
                    "model": "FCOS-ResNet50-FPN", "global_batch": B * world, "image_size": H,
                    "parallelism": "dp%d" % world},
         "roofline": roof,
-        "dist": dist_info(world),
+        "dist": dict(dist_info(world), grad_allreduce=grad_ar),
         "model_flops_per_image": fl_img,
         "step_mfma_frac": round(img_s / world * fl_img / 1e12 / PEAK_BF16_TFLOPS, 4),
         "last_step_losses_cls_reg_cen": [round(x, 3) for x in losses]})

@@ -155,6 +155,8 @@ SIGNATURES = {
     "cvl_fcos_center_assign": (c_int, [P, P, P, c_int, c_int, c_int, c_int, c_int, P, P, c_int, P, P, P]),
     "cvl_fcos_center_v1_assign": (c_int, [P, P, P, c_int, c_int, c_int, c_int, c_int, P, P, P, P, P]),
     "cvl_resize_pad_normalize": (c_int, [P, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, P, P]),
+    "cvl_image_augment_workspace_size": (c_size_t, [c_int, c_int]),
+    "cvl_image_augment": (c_int, [P, P, P, P, P, P, c_int, c_int, c_int, c_int, P, c_size_t, P]),
     "cvl_fcos_detect_workspace_size": (c_size_t, [c_int, c_int, c_int, c_int]),
     "cvl_fcos_detect": (c_int, [P, c_int, P, c_int, c_int, P, P, c_int, c_int, c_float, c_float, c_int, c_int, P, P,
                                 P, P, P, c_size_t, P]),

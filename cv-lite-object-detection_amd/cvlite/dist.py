@@ -96,13 +96,46 @@ class GradSync(object):
             "gradient groups must cover every parameter exactly once"
         self.works = []
         self.active = tdist.is_initialized() and (tdist.get_world_size(group) > 1 or force_sync())
+        self.trace = None
+
+    def plan(self):
+        """[(group, [bucket bytes])] in enqueue order (bench.py's dist block)."""
+        return [(n, [(b - a) * self.grad.element_size() for a, b in self.ranges[n]]) for n in self.order]
+
+    def begin_trace(self):
+        """Time the next step's enqueue points: a HIP event on the compute stream at step start and
+        at each group's ready point, and one after the group's all-reduces (recorded on a side
+        stream made to wait for RCCL's, so the compute stream is not held).  Read by end_trace()."""
+        self.trace = {"t0": torch.cuda.Event(enable_timing=True), "groups": []}
+        self.trace["t0"].record()
+
+    def end_trace(self):
+        """Per group: (name, bucket bytes, ready ms, all-reduce done ms) from the traced step's start."""
+        tr, self.trace = self.trace, None
+        torch.cuda.synchronize()
+        t0 = tr["t0"]
+        return [(n, by, t0.elapsed_time(r), t0.elapsed_time(d) if d is not None else None)
+                for n, by, r, d in tr["groups"]]
 
     def ready(self, name):
         if not self.active:
             return
-        for a, b in self.ranges[name]:
-            self.works.append(tdist.all_reduce(self.grad[a:b], op=tdist.ReduceOp.SUM, group=self.pg,
-                                               async_op=True))
+        ev_r = ev_d = None
+        if self.trace is not None:
+            ev_r = torch.cuda.Event(enable_timing=True)
+            ev_r.record()
+        new = [tdist.all_reduce(self.grad[a:b], op=tdist.ReduceOp.SUM, group=self.pg, async_op=True)
+               for a, b in self.ranges[name]]
+        self.works += new
+        if self.trace is not None:
+            side = self.trace.setdefault("side", torch.cuda.Stream())
+            with torch.cuda.stream(side):
+                for w in new:
+                    w.wait()
+                ev_d = torch.cuda.Event(enable_timing=True)
+                ev_d.record()
+            self.trace["groups"].append((name, [(b - a) * self.grad.element_size() for a, b in self.ranges[name]],
+                                         ev_r, ev_d))
 
     def finish(self):
         for w in self.works:

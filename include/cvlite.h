@@ -752,6 +752,20 @@ int cvl_fcos_detect(const float* reg_pred, int ld_reg, const float* cls_pred, in
 int cvl_resize_pad_normalize(const void* src, int src_u8, int H, int W, int C, int flip, int out_h, int out_w,
                              int pad_h, int pad_w, float* out, cvl_stream_t stream);
 
+/* CenterNet/train_hourglass_voc.py:24-67 image_augment over a batch, the draws made by the caller
+ * (cvlite.train_hourglass_v2.draw_augment): ops[b] / params[b] DEVICE int32 / fp32 per image,
+ * 0 none, 1 brightness (x + params[b]), 2 contrast ((x - mean_c) * params[b] + mean_c, mean over
+ * the N x N pixels of channel c), 3 flip left-right, 4 transpose (90 degrees), 5 transpose + flip
+ * up-down (270 degrees); other codes copy.  img [B][N][N][3] fp32 (square padded images); tgt
+ * [B][S][S][4][T] fp32 target maps (T = 5 + C), moved with the image (3: channel 1 := 1 - v;
+ * 4 / 5: channels 0 := 1 and 2 := 3 of the transposed cell, the reference's aliased swap; 5: then
+ * channel 0 := 1 - v) -- tgt_src = tgt_dst = NULL skips them.  src and dst must not overlap.
+ * workspace: cvl_image_augment_workspace_size(B, N) bytes.  Two launches, deterministic. */
+size_t cvl_image_augment_workspace_size(int B, int N);
+int cvl_image_augment(const float* img_src, float* img_dst, const float* tgt_src, float* tgt_dst,
+                      const int32_t* ops, const float* params, int B, int N, int S, int T, void* workspace,
+                      size_t workspace_bytes, cvl_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

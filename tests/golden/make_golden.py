@@ -535,6 +535,69 @@ def work_loss_kwargs(out_path):
 WORKERS["loss_kwargs"] = work_loss_kwargs
 
 
+def work_image_augment(out_path):
+    """CenterNet v2 `image_augment` (train_hourglass_voc.py:24-67): the REFERENCE's own function (its
+    definition executed from the file; module-level code is not) on random padded images and
+    float64 target maps.  The TF image ops it calls are given here: tf.transpose; random_brightness
+    = x + delta and random_contrast = (x - mean) * f + mean (per-channel mean over the pixels), the
+    magnitudes drawn from a recorded second generator.  Per case: the numpy seed set before the
+    call (its np.random.uniform() draws pick the branch), the second generator's seed, inputs and
+    outputs."""
+    import ast
+    import types
+    tf = _child_setup("CenterNet")
+    path = os.path.join(REF, "CenterNet", "train_hourglass_voc.py")
+    tree = ast.parse(open(path).read())
+    tree.body = [n for n in tree.body if isinstance(n, ast.FunctionDef) and n.name == "image_augment"]
+    ns = {"np": np, "tf": tf}
+    exec(compile(tree, path, "exec"), ns)
+    state = {}
+
+    def random_brightness(img, max_delta):
+        d = np.float32(state["tf_rng"].uniform(-max_delta, max_delta))
+        return tf.Tensor((np.asarray(img.numpy(), np.float32) + d).astype(np.float32))
+
+    def random_contrast(img, lower, upper):
+        f = np.float32(state["tf_rng"].uniform(lower, upper))
+        a = np.asarray(img.numpy(), np.float32)
+        m = a.astype(np.float64).mean(axis=(0, 1)).astype(np.float32)
+        return tf.Tensor(((a - m) * f + m).astype(np.float32))
+    tf.image = types.SimpleNamespace(random_brightness=random_brightness, random_contrast=random_contrast)
+    tf.transpose = lambda x, perm: tf.Tensor(np.transpose(x.numpy() if isinstance(x, tf.Tensor) else x, perm))
+    rng = np.random.default_rng(2402)
+    C = 3
+    arrays = {}
+    k = 0
+    for N in [20] * 18 + [36] * 6:
+        S = (N + 7) // 8
+        img = np.zeros((N, N, 3), np.float32)
+        pad = int(rng.integers(0, 4))
+        img[pad:N - pad, pad:N - pad] = rng.uniform(0, 1, (N - 2 * pad, N - 2 * pad, 3)).astype(np.float32)
+        bbox = np.zeros((S, S, 4, 5 + C))
+        for _ in range(int(rng.integers(1, 6))):
+            y, x, sc = int(rng.integers(0, S)), int(rng.integers(0, S)), int(rng.integers(0, 4))
+            bbox[y, x, sc, :4] = [rng.uniform(), rng.uniform(), rng.uniform(0.1, 2), rng.uniform(0.1, 2)]
+            bbox[y, x, sc, 4] = 1.0
+            bbox[y, x, sc, 5 + int(rng.integers(0, C))] = 1.0
+        seed_np, seed_tf = 1000 + k, 5000 + k
+        state["tf_rng"] = np.random.RandomState(seed_tf)
+        np.random.seed(seed_np)
+        out_img, out_bbox = ns["image_augment"](tf.constant(img), bbox.copy())
+        arrays["case_%d_seeds" % k] = np.array([seed_np, seed_tf], np.int64)
+        arrays["case_%d_img" % k] = img
+        arrays["case_%d_bbox" % k] = bbox
+        arrays["case_%d_out_img" % k] = np.asarray(out_img.numpy() if hasattr(out_img, "numpy") else out_img,
+                                                   np.float32)
+        arrays["case_%d_out_bbox" % k] = np.asarray(out_bbox.numpy() if hasattr(out_bbox, "numpy") else out_bbox,
+                                                    np.float64)
+        k += 1
+    arrays["n_cases"] = np.int32(k)
+    np.savez_compressed(out_path, **arrays)
+
+
+WORKERS["image_augment"] = work_image_augment
+
+
 def main():
     if len(sys.argv) == 3 and sys.argv[1] in WORKERS:
         WORKERS[sys.argv[1]](sys.argv[2])

@@ -69,6 +69,13 @@ def _worker(rank, world, port, out_path):
         sync.ready(name)
     sync.finish()
     assert torch.equal(st.grad, expect)
+    # the plan bench.py's dist block prints: groups in enqueue order, buckets within the cap, the
+    # whole flat buffer covered up to alignment gaps
+    plan = sync.plan()
+    assert [n for n, _ in plan] == sync.order
+    assert all(0 < b <= 1 << 20 for _, bs in plan for b in bs)
+    used = sum(st.offsets[k][1] for k in st.offsets) * 4
+    assert used <= sum(b for _, bs in plan for b in bs) <= st.grad.numel() * 4
     # 3) DP training step
     params = FCOSNet.param_dict(C, seed=0)                 # identical init on every rank
     imgs, tg = _batch(world * BS, seed=11)

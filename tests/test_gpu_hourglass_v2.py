@@ -9,7 +9,10 @@
     fp32 reference on the same operands);
   * whole graph (64x64, B = 4, BN sub-batches of 2) vs the torch restatement storing bf16 where the
     GPU path does (oracle/hourglass_v2_ref.py), rel-L2 bounds as test_gpu_hourglass.py;
-  * train steps through the captured graph: targets, losses vs the oracle, Adam update direction.
+  * train steps through the captured graph: targets, losses vs the oracle, Adam update direction;
+  * image_augment (train_hourglass_voc.py:24-67, cvl_image_augment): every case of the reference's
+    own outputs (golden_image_augment.npz) and mixed-op batches at loop sizes vs the numpy
+    restatement (oracle/augment_ref.py); the loop's draws leave numpy's stream as the reference's.
 """
 import math
 
@@ -279,3 +282,99 @@ def test_hourglass_v2_train_steps_vs_oracle():
     print("update sign agreement %.4f" % (agree / tot))
     assert agree / tot > 0.8
     assert torch.isfinite(net.store.flat).all()
+
+
+# image_augment tolerances: pixels of the geometric ops and brightness are bit-exact; contrast's
+# per-channel mean is a float64 sum in a different order than numpy's (rounded to the same fp32
+# almost always) -> 2e-7 absolute on [0, 1] pixels.  Target offsets 1 - v are formed in fp32 from
+# the fp32 map the GPU holds, the reference forms them in float64 before its fp32 cast: <= 1 ulp.
+AUG_PIX_ATOL = 2e-7
+AUG_TGT_ATOL = 1.2e-7
+
+
+def _aug_check(op, got_img, got_tgt, ref_img, ref_tgt):
+    ri = torch.from_numpy(np.ascontiguousarray(ref_img, np.float32))
+    rt = torch.from_numpy(np.ascontiguousarray(ref_tgt).astype(np.float32))
+    if op == 2:
+        torch.testing.assert_close(got_img.cpu(), ri, rtol=0, atol=AUG_PIX_ATOL)
+    else:
+        assert torch.equal(got_img.cpu(), ri), op
+    if op in (3, 5):
+        torch.testing.assert_close(got_tgt.cpu(), rt, rtol=0, atol=AUG_TGT_ATOL)
+    else:
+        assert torch.equal(got_tgt.cpu(), rt), op
+
+
+def test_image_augment_vs_reference_golden(golden):
+    """Each golden case (the reference's image_augment on a padded N x N image, N = 20 / 36: partial
+    32-pixel tiles) through cvl_image_augment with the restated draw for its numpy seed; then all
+    cases of one size as ONE batch (mixed ops in one launch)."""
+    from oracle import augment_ref as A
+    from cvlite.train_hourglass_v2 import augment_batch
+    z = golden("image_augment")
+    by_n = {}
+    for k in range(int(z["n_cases"])):
+        sn, st = (int(v) for v in z["case_%d_seeds" % k])
+        op, prm = A.draw_augment(rng=np.random.RandomState(sn), tf_rng=np.random.RandomState(st))
+        img = torch.from_numpy(z["case_%d_img" % k]).cuda()
+        tgt = torch.from_numpy(z["case_%d_bbox" % k].astype(np.float32)).cuda()
+        gi, gt = augment_batch(img[None].contiguous(), tgt[None].contiguous(), [op], [prm])
+        _aug_check(op, gi[0], gt[0], z["case_%d_out_img" % k], z["case_%d_out_bbox" % k])
+        by_n.setdefault(img.shape[0], []).append((k, op, prm, img, tgt))
+    for n, cases in by_n.items():
+        imgs = torch.stack([c[3] for c in cases])
+        tgts = torch.stack([c[4] for c in cases])
+        gi, gt = augment_batch(imgs, tgts, [c[1] for c in cases], [c[2] for c in cases])
+        for j, (k, op, _, _, _) in enumerate(cases):
+            _aug_check(op, gi[j], gt[j], z["case_%d_out_img" % k], z["case_%d_out_bbox" % k])
+
+
+@pytest.mark.parametrize("N", [384, 200])
+def test_image_augment_loop_sizes_vs_restatement(N):
+    """A batch holding every op (twice), N = 384 (the loop's jittered img_dims are multiples of 64)
+    and 200 (ragged tiles), C = 20 targets, vs oracle/augment_ref.image_augment_ref; images only
+    (targets NULL) gives the same pixels."""
+    from oracle import augment_ref as A
+    from cvlite.train_hourglass_v2 import augment_batch
+    C, S = 20, (N + 7) // 8
+    ops = [0, 1, 2, 3, 4, 5, 5, 4, 3, 2, 1, 0]
+    prm = [0.0, 0.21, 0.8, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 1.2, -0.17, 0.0]
+    g = torch.Generator().manual_seed(N)
+    imgs = torch.rand(len(ops), N, N, 3, generator=g)
+    tg = torch.zeros(len(ops), S, S, 4, 5 + C)
+    m = torch.rand(len(ops), S, S, 4, generator=g) < 0.05
+    tg[..., :4] = torch.rand(len(ops), S, S, 4, 4, generator=g) * m[..., None]
+    tg[..., 4] = m.float()
+    tg[..., 5:] = torch.nn.functional.one_hot(torch.randint(0, C, (len(ops), S, S, 4), generator=g), C) * m[..., None]
+    gi, gt = augment_batch(imgs.cuda(), tg.cuda(), ops, prm)
+    gi2, none = augment_batch(imgs.cuda(), None, ops, prm)
+    assert none is None and torch.equal(gi, gi2)
+    for b, op in enumerate(ops):
+        ri, rt = A.image_augment_ref(imgs[b].numpy(), tg[b].numpy(), op, prm[b])
+        _aug_check(op, gi[b], gt[b], ri, rt)
+
+
+def test_train_loop_augment_keeps_reference_numpy_stream():
+    """train(..., augment=True) (2 steps, tiny data): the loop's numpy draws -- batch choice,
+    rnd_scale, then image_augment's per image -- leave np.random in the state a replay of the
+    reference's draw sequence reaches, and the steps run finite."""
+    from cvlite import train_hourglass_v2 as T
+    C, n_data, B = 20, 6, 2
+    net = _small_net(C, seed=3)
+    rng = np.random.default_rng(5)
+    data = []
+    for i in range(n_data):
+        cen = rng.uniform(0.2, 0.8, (3, 2))
+        data.append({"image": rng.uniform(0, 1, (64, 64, 3)).astype(np.float32),
+                     "objects": {"bbox": np.concatenate([cen - 0.1, cen + 0.1], 1).astype(np.float32),
+                                 "label": rng.integers(0, C, 3)}})
+    losses = T.train(net, C, 2, B, data, [], 0, 2, display_step=1, base_rows=64, seed=17, print_fn=lambda *a: None)
+    after = np.random.uniform()
+    np.random.seed(17)
+    for _ in range(2):
+        np.random.choice(n_data, size=B, replace=False)
+        np.random.uniform(low=0.6, high=1.3)
+        for _ in range(B):
+            T.draw_augment(0.5, tf_rng=np.random.RandomState(0))
+    assert np.random.uniform() == after
+    assert len(losses) == 2 and all(np.isfinite(v) for row in losses for v in row)

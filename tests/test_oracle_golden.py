@@ -278,3 +278,32 @@ def test_centernet_peak_decode_restatement_known_answer():
     np.testing.assert_allclose(rows[:, 4], 1 / (1 + np.exp(-np.array([2.0, 2.0, 0.5, 0.5]))), rtol=1e-6)
     assert len(peak_decode(pred, C, 8, 0.3, K=1)) == 1
     assert len(peak_decode(pred, C, 8, 0.99, K=10)) == 0
+
+
+def test_image_augment_restatement_vs_reference(golden):
+    """oracle/augment_ref.py vs the reference's own image_augment (train_hourglass_voc.py:24-67, run by
+    make_golden.py): with the same numpy seed the restated draws take the same branch, and the
+    transformed image and float64 target map are bit-identical (all six branches occur)."""
+    from oracle import augment_ref as A
+    z = golden("image_augment")
+    seen = set()
+    for k in range(int(z["n_cases"])):
+        sn, st = (int(v) for v in z["case_%d_seeds" % k])
+        op, prm = A.draw_augment(rng=np.random.RandomState(sn), tf_rng=np.random.RandomState(st))
+        seen.add(op)
+        im, bb = A.image_augment_ref(z["case_%d_img" % k], z["case_%d_bbox" % k], op, prm)
+        assert np.array_equal(im, z["case_%d_out_img" % k]), (k, op)
+        assert np.array_equal(bb, z["case_%d_out_bbox" % k]), (k, op)
+    assert seen == set(range(6)), seen
+
+
+def test_image_augment_product_draws_match_restatement():
+    """cvlite.train_hourglass_v2.draw_augment consumes the numpy stream exactly as the reference's
+    image_augment does (same branch, same state afterwards) over many seeds."""
+    from oracle import augment_ref as A
+    from cvlite.train_hourglass_v2 import draw_augment
+    for s in range(300):
+        r1, r2 = np.random.RandomState(s), np.random.RandomState(s)
+        t1, t2 = np.random.RandomState(s + 7), np.random.RandomState(s + 7)
+        assert draw_augment(0.5, rng=r1, tf_rng=t1) == A.draw_augment(0.5, rng=r2, tf_rng=t2)
+        assert r1.uniform() == r2.uniform()

@@ -30,17 +30,19 @@ def describe(kind, d, ngroups=1):
     s0 = d.seg[0]
     mode = {0: "fwd", 1: "dgrad"}[d.mode] if kind == "igemm" else "wgrad"
     geo = "%dx%d" % (d.KH, d.KW) + (" s%d" % d.stride if d.stride > 1 else "")
-    if kind == "igemm" and d.mode == 1:
-        chans = "%d->%d" % (d.Cin, d.n_store)
-    else:
-        chans = "%d->%d" % (d.Cin, d.n_store)
+    chans = "%d->%d" % (d.Cin, d.n_store)
     lv = "%dx%d" % (s0.Hr, s0.Wr) + (" +%d seg" % (d.nseg - 1) if d.nseg > 1 else "")
     g = " (%d groups)" % ngroups if ngroups > 1 else ""
     return "%s %s %s @ %s%s" % (mode, geo, chans, lv, g)
 
 
 def flops(kind, d):
-    rows = sum(d.B * d.seg[i].Hr * d.seg[i].Wr for i in range(d.nseg))
+    """Algorithmic FLOPs: 2 x (forward output pixels) x KH*KW*Cin_fwd x Cout_fwd for all three
+    passes.  A data-gradient descriptor's result map (Hr, Wr) is the forward INPUT and its source
+    (Hs, Ws) the forward output (dY), so its rows are B*Hs*Ws -- for stride s the dX map has s^2 as
+    many pixels, and counting those would over-state a strided dgrad's work s^2-fold."""
+    dgrad = kind == "igemm" and d.mode == 1
+    rows = sum(d.B * (d.seg[i].Hs * d.seg[i].Ws if dgrad else d.seg[i].Hr * d.seg[i].Wr) for i in range(d.nseg))
     K = d.KH * d.KW * d.Cin
     return 2.0 * rows * K * d.n_store
 
