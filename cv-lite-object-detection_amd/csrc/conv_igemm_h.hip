@@ -32,7 +32,14 @@
 //   dx = -1, 0, +1.
 // * Small grids split the channel blocks over blockIdx.z (fp32 slabs + conv_igemm.hip's finish).
 // * Epilogue (bias, ReLU, BN statistics, the fused BN-backward first pass, fp32 / bf16, beta):
-//   conv_epilogue.h, the L kernel's 256 x 64 form.
+//   conv_epilogue.h, the L kernel's 256 x 64 form -- or, for the launches whose tiles each lie in
+//   one image (H*W % 256 == 0, bf16, beta 0: the backbone 3x3 units and the FPN 3x3 convs), the SW
+//   form (round 5): the MFMA operands are swapped (D = W.X^T) so that a lane's accumulator quad is
+//   4 consecutive output channels of one pixel; bias / ReLU / bf16 rounding in registers, one
+//   v_permlane16_swap regroup to 8 channels per lane, 16-B stores straight from the registers (no LDS
+//   C image, no barrier), and the BN statistics / BN-backward sums kept as per-lane partials across
+//   the workgroup's tiles of one (image, N tile): DPP row sums + one LDS combine + one fp64 atomic
+//   pair per channel only when the (image, N tile) changes or the workgroup ends.
 #include "conv_common.h"
 #include "conv_epilogue.h"
 
@@ -58,6 +65,10 @@ constexpr unsigned kRecords = 0x7fffffffu;
 constexpr unsigned kOOB = 0x80000000u;
 
 __device__ __forceinline__ int swz4(int r) { return (r >> 1) & 3; }
+
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 
 __device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t r, const cvl_bf16* lds_dst, unsigned voff) {
   __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)lds_dst, 16, (int)voff, 0,
@@ -142,9 +153,12 @@ __device__ unsigned long long g_h_stamps[kHStampWgs * 8];
 // issued, so that tile's halo and weights land while the current tile's epilogue runs (the
 // epilogue stages its C image in the stage buffer just consumed), and the per-tile set-up is a
 // few adds (halo_pieces is per segment).  One workgroup per CU (148 KiB of LDS).
-template <bool DGRAD, bool BSUM, bool WRES = false, bool ST = false>
+template <bool DGRAD, bool BSUM, bool WRES = false, bool ST = false, bool SW = false>
 __global__ void __launch_bounds__(NT) conv_igemm_h_kernel(ConvArgs a) {
-  __shared__ __attribute__((aligned(16))) cvl_bf16 lds[WRES ? LDS_WRES_EL : LDS_EL];
+  constexpr int MAIN_EL = WRES ? LDS_WRES_EL : LDS_EL;
+  // SW: + the [WGM][BN][2] fp32 combine buffer of the statistics flush
+  __shared__ __attribute__((aligned(16))) cvl_bf16 lds[MAIN_EL + (SW ? WGM * BN * 2 * 2 : 0)];
+  float* const red = reinterpret_cast<float*>(lds + MAIN_EL);
   constexpr int SST = WRES ? HALO_EL : STAGE_EL;        // elements per stage buffer
   cvl_bf16* const wres = lds + 2 * HALO_EL;             // WRES: the weights of channel block cb at cb * WT_EL
   const int tid = threadIdx.x;
@@ -252,6 +266,72 @@ __global__ void __launch_bounds__(NT) conv_igemm_h_kernel(ConvArgs a) {
     bfr[j] = (unsigned)(rr * BK * 2 + ((lg ^ swz4(rr)) * 16));
   }
 
+  // SW epilogue state: per-lane partial sums of the current (image, N tile) -- BN statistics of
+  // the lane's 4 channels per column block (forward), or the BN-backward sums of its 8 regrouped
+  // channels (BSUM) with those channels' (mean, rstd, gamma, beta)
+  const int lgo = ((lg & 1) ? 16 : 0) + ((lg & 2) ? 8 : 0);
+  float ss1[SW ? TN : 1][4], ss2[SW ? TN : 1][4];
+  float bs1[8], bs2[8], pm[8], prs[8], pga[8], pbe[8];
+  int k_img = -1, k_n0 = 0;
+  if constexpr (SW) {
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) { ss1[j][e] = 0.f; ss2[j][e] = 0.f; }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) { bs1[u] = 0.f; bs2[u] = 0.f; }
+  }
+  auto row16_sum = [](float v) {         // the 16-lane row sum, left in every lane of the row
+    v += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0xB1, 0xF, 0xF, false));   // quad xor 1
+    v += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x4E, 0xF, 0xF, false));   // quad xor 2
+    v += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x141, 0xF, 0xF, false));  // row half mirror
+    v += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x140, 0xF, 0xF, false));  // row mirror
+    return v;
+  };
+  // one flush: the WGM waves of a column combined in a fixed order, one fp64 atomic pair per channel
+  auto sw_flush = [&]() {
+    if constexpr (SW) {
+      if (k_img < 0) return;
+      if (BSUM) {
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          const float t1 = row16_sum(bs1[u]), t2 = row16_sum(bs2[u]);
+          bs1[u] = 0.f;
+          bs2[u] = 0.f;
+          if (lr == 0) {
+            const int c = wn * WN + lgo + u;
+            red[(wm * BN + c) * 2] = t1;
+            red[(wm * BN + c) * 2 + 1] = t2;
+          }
+        }
+      } else {
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const float t1 = row16_sum(ss1[j][e]), t2 = row16_sum(ss2[j][e]);
+            ss1[j][e] = 0.f;
+            ss2[j][e] = 0.f;
+            if (lr == 0) {
+              const int c = wn * WN + j * 16 + 4 * lg + e;
+              red[(wm * BN + c) * 2] = t1;
+              red[(wm * BN + c) * 2 + 1] = t2;
+            }
+          }
+      }
+      __syncthreads();
+      if (tid < BN && k_n0 + tid < a.n_store) {
+        float t1 = 0.f, t2 = 0.f;
+#pragma unroll
+        for (int w = 0; w < WGM; ++w) { t1 += red[(w * BN + tid) * 2]; t2 += red[(w * BN + tid) * 2 + 1]; }
+        acc_u64* st = (BSUM ? a.bsum : a.stats) + acc_idx((long)k_img * a.n_store + k_n0 + tid, 0, a.acc_slots);
+        acc_add(st, t1, a.acc_slots);
+        acc_add(st + a.acc_slots, t2, a.acc_slots);
+      }
+      __syncthreads();                   // red is free again
+    }
+  };
+
   // prologue: the first channel block's stage complete everywhere
   {
     cvl_bf16* st = lds;
@@ -316,9 +396,45 @@ __global__ void __launch_bounds__(NT) conv_igemm_h_kernel(ConvArgs a) {
     }
     s16x8 zpre[BnSumPre<BN, NT>::N];
     BnSumPar bpar;
-    if constexpr (BSUM) bnsum_prefetch<BN, NT>(a, S, tid, n0, mloc0, zpre, bpar);
     float bcol[TN];                                 // the epilogue's bias, in flight under the taps
-    epi_bias<BN, WGM, TN>(a, S, n0, wn, lane, bcol);
+    float bq[SW ? TN : 1][4];                       // SW: the bias of the lane's 4 channels per column block
+    s16x8 zq[SW && BSUM ? TM : 1];                  // SW + BSUM: z of the lane's pixel, its 8 regrouped channels
+    if constexpr (SW) {
+      const int img = mloc0 / HWr;                  // the tile lies in one image (host: H*W % 256 == 0)
+      if ((a.stats || BSUM) && (img != k_img || n0 != k_n0)) {
+        sw_flush();
+        k_img = img;
+        k_n0 = n0;
+        if (BSUM) {
+#pragma unroll
+          for (int u = 0; u < 8; ++u) {
+            const int c = min(n0 + wn * WN + lgo + u, a.n_store - 1);
+            const long bc = (long)img * a.n_store + c;
+            pm[u] = a.bmr[bc * 2];
+            prs[u] = a.bmr[bc * 2 + 1];
+            pga[u] = a.bga[c];
+            pbe[u] = a.bbe[c];
+          }
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int n = n0 + wn * WN + j * 16 + 4 * lg + e;
+          bq[j][e] = (S.bias && n < a.n_store) ? S.bias[n] : 0.f;
+        }
+      if (BSUM) {
+#pragma unroll
+        for (int i = 0; i < TM; ++i) {
+          const long row = S.dst_base + mloc0 + wm * WM + i * 16 + lr;
+          zq[i] = *reinterpret_cast<const s16x8*>(a.bz + row * a.ld_dst + a.dst_coff + n0 + wn * WN + lgo);
+        }
+      }
+    } else {
+      if constexpr (BSUM) bnsum_prefetch<BN, NT>(a, S, tid, n0, mloc0, zpre, bpar);
+      epi_bias<BN, WGM, TN>(a, S, n0, wn, lane, bcol);
+    }
     f32x4 acc[TM][TN];
 #pragma unroll
     for (int i = 0; i < TM; ++i)
@@ -347,8 +463,10 @@ __global__ void __launch_bounds__(NT) conv_igemm_h_kernel(ConvArgs a) {
       for (int i = 0; i < TM; ++i)
 #pragma unroll
         for (int j = 0; j < TN; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, fa[buf][i]),
-                                                               __builtin_bit_cast(bf16x8, fb[buf][j]), acc[i][j], 0, 0, 0);
+          acc[i][j] = SW ? __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, fb[buf][j]),
+                                                                    __builtin_bit_cast(bf16x8, fa[buf][i]), acc[i][j], 0, 0, 0)
+                         : __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, fa[buf][i]),
+                                                                    __builtin_bit_cast(bf16x8, fb[buf][j]), acc[i][j], 0, 0, 0);
     };
     for (int cb = cb0; cb < cb1; ++cb) {
       const char* Hc = reinterpret_cast<const char*>(lds + (gb & 1) * SST);
@@ -393,6 +511,69 @@ __global__ void __launch_bounds__(NT) conv_igemm_h_kernel(ConvArgs a) {
           }
       continue;
     }
+    if constexpr (SW) {
+      // acc[i][j] = D^T: lane (lr, lg) holds channels j*16 + 4*lg + e of pixel i*16 + lr of its wave's
+      // 64 rows.  bf16 pairs by one v_cvt_pk_bf16_f32 (the statistics take the rounded values), then
+      // one v_permlane16_swap per packed register regroups column blocks 0 / 1 so a lane holds 8
+      // consecutive channels (wn*32 + lgo ..): one 16-B store per pixel.
+      if (ST && stamp) c0 = __builtin_amdgcn_s_memtime();
+      const bool dense = S.dst_img == (long)HWr;
+      const int n = n0 + wn * WN + lgo;
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const int ml = mloc0 + wm * WM + i * 16 + lr;
+        long drow;
+        if (dense) {
+          drow = S.dst_base + ml;
+        } else {
+          const int img = ml / HWr, q = ml - img * HWr;
+          drow = conv_dst_row(a, S, img, q);
+        }
+        unsigned pk[2][2];
+#pragma unroll
+        for (int jj = 0; jj < 2; ++jj)
+#pragma unroll
+          for (int h = 0; h < 2; ++h) {
+            float v0 = acc[i][jj][2 * h] + bq[jj][2 * h];
+            float v1 = acc[i][jj][2 * h + 1] + bq[jj][2 * h + 1];
+            if (a.relu_out) { v0 = fmaxf(v0, 0.f); v1 = fmaxf(v1, 0.f); }
+            const unsigned u = __builtin_bit_cast(unsigned, __builtin_convertvector((f32x2){v0, v1}, bf16x2));
+            pk[jj][h] = u;
+            if (!BSUM && a.stats) {
+              const float r0 = __uint_as_float(u << 16), r1 = __uint_as_float(u & 0xffff0000u);
+              ss1[jj][2 * h] += r0;
+              ss2[jj][2 * h] = __builtin_fmaf(r0, r0, ss2[jj][2 * h]);
+              ss1[jj][2 * h + 1] += r1;
+              ss2[jj][2 * h + 1] = __builtin_fmaf(r1, r1, ss2[jj][2 * h + 1]);
+            }
+          }
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const auto sw = __builtin_amdgcn_permlane16_swap(pk[0][h], pk[1][h], false, false);
+          pk[0][h] = sw[0];
+          pk[1][h] = sw[1];
+        }
+        if (n >= a.n_store) continue;
+        const s16x8 o = __builtin_bit_cast(s16x8, (u32x4){pk[0][0], pk[0][1], pk[1][0], pk[1][1]});
+        if (BSUM) {        // g = dy * ReLU mask rebuilt from z (exactly the forward's bn_affine value)
+#pragma unroll
+          for (int u = 0; u < 8; ++u) {
+            const float zf = bf16_to_f32((cvl_bf16)zq[i][u]);
+            const float xh = (zf - pm[u]) * prs[u];
+            const float af = __builtin_fmaf(pga[u], xh, pbe[u]);
+            const float g = (af > 0.f && af < a.bhi) ? bf16_to_f32((cvl_bf16)o[u]) : 0.f;
+            bs1[u] += g;
+            bs2[u] = __builtin_fmaf(g, xh, bs2[u]);
+          }
+        }
+        *reinterpret_cast<s16x8*>(reinterpret_cast<cvl_bf16*>(a.dst) + drow * a.ld_dst + a.dst_coff + n) = o;
+      }
+      if (ST && stamp) {
+        t_epi += __builtin_amdgcn_s_memtime() - c0;
+        ++n_tile;
+      }
+      continue;
+    }
     // the epilogue's C image goes into the stage buffer just consumed (the other one holds the
     // next tile's first stage, in flight); the barrier after it frees that buffer for the DMA
     if (ST && stamp) {
@@ -407,6 +588,7 @@ __global__ void __launch_bounds__(NT) conv_igemm_h_kernel(ConvArgs a) {
       ++n_tile;
     }
   }
+  sw_flush();                                       // SW: the last (image, N tile)'s partial sums
   wait_vm<0>();
   if (ST && stamp) {
     stamp[0] = w0;
@@ -495,29 +677,45 @@ int cvl_conv_igemm_h(const cvl_conv_desc* d, const ConvArgs& a0, hipStream_t s, 
   dim3 grid(wgs, 1, a.splits);
   g_cvl_conv_last_kernel = CVL_CK_H64;
   const bool wres = a.splits <= 1 && a.Npad == BN && ncb <= WRES_CB && a.nseg == 1 && !cvl_dispatch_flag("h_no_wres");
+  // SW epilogue (registers -> 16-B stores, statistics per (image, N tile)): every tile inside one
+  // image, bf16 destination in 8-channel chunks, no beta, statistics OR fused BN sums
+  bool sw = a.splits <= 1 && !d->dst_f32 && d->beta == 0.f && d->n_store % 8 == 0 && d->ld_dst % 8 == 0 &&
+            d->dst_coff % 8 == 0 && !(a.stats && a.bsum) && !cvl_dispatch_flag("h_no_sw");
+  for (int i = 0; sw && i < a.nseg; ++i) {
+    const ConvSeg& q = a.seg[i];
+    const long hw = (long)q.Hr * q.Wr;
+    if (hw % BM || (a.bsum && q.dst_img != hw)) sw = false;
+  }
+  const bool bs = dg && a.bsum;
+#define CVL_H_LAUNCH(ST_)                                                                                             \
+  do {                                                                                                               \
+    if (sw) {                                                                                                        \
+      if (wres && !dg) hipLaunchKernelGGL((conv_igemm_h_kernel<false, false, true, ST_, true>), grid, dim3(NT), 0, s, a); \
+      else if (wres && bs) hipLaunchKernelGGL((conv_igemm_h_kernel<true, true, true, ST_, true>), grid, dim3(NT), 0, s, a); \
+      else if (wres) hipLaunchKernelGGL((conv_igemm_h_kernel<true, false, true, ST_, true>), grid, dim3(NT), 0, s, a);    \
+      else if (bs) hipLaunchKernelGGL((conv_igemm_h_kernel<true, true, false, ST_, true>), grid, dim3(NT), 0, s, a);      \
+      else if (dg) hipLaunchKernelGGL((conv_igemm_h_kernel<true, false, false, ST_, true>), grid, dim3(NT), 0, s, a);     \
+      else hipLaunchKernelGGL((conv_igemm_h_kernel<false, false, false, ST_, true>), grid, dim3(NT), 0, s, a);            \
+    } else {                                                                                                         \
+      if (wres && !dg) hipLaunchKernelGGL((conv_igemm_h_kernel<false, false, true, ST_>), grid, dim3(NT), 0, s, a);       \
+      else if (wres && bs) hipLaunchKernelGGL((conv_igemm_h_kernel<true, true, true, ST_>), grid, dim3(NT), 0, s, a);     \
+      else if (wres) hipLaunchKernelGGL((conv_igemm_h_kernel<true, false, true, ST_>), grid, dim3(NT), 0, s, a);          \
+      else if (bs) hipLaunchKernelGGL((conv_igemm_h_kernel<true, true, false, ST_>), grid, dim3(NT), 0, s, a);            \
+      else if (dg) hipLaunchKernelGGL((conv_igemm_h_kernel<true, false, false, ST_>), grid, dim3(NT), 0, s, a);           \
+      else hipLaunchKernelGGL((conv_igemm_h_kernel<false, false, false, ST_>), grid, dim3(NT), 0, s, a);                  \
+    }                                                                                                                \
+  } while (0)
 #ifdef CVL_MEASURE
   static const bool stamps = cvl_tune_flag("CVL_H_STAMPS");
   if (stamps && a.splits <= 1 && wgs <= kHStampWgs) {
     g_h_stamp_grid = wgs;
-    if (wres && !dg) hipLaunchKernelGGL((conv_igemm_h_kernel<false, false, true, true>), grid, dim3(NT), 0, s, a);
-    else if (wres && dg && a.bsum) hipLaunchKernelGGL((conv_igemm_h_kernel<true, true, true, true>), grid, dim3(NT), 0, s, a);
-    else if (wres) hipLaunchKernelGGL((conv_igemm_h_kernel<true, false, true, true>), grid, dim3(NT), 0, s, a);
-    else if (dg && a.bsum) hipLaunchKernelGGL((conv_igemm_h_kernel<true, true, false, true>), grid, dim3(NT), 0, s, a);
-    else if (dg) hipLaunchKernelGGL((conv_igemm_h_kernel<true, false, false, true>), grid, dim3(NT), 0, s, a);
-    else hipLaunchKernelGGL((conv_igemm_h_kernel<false, false, false, true>), grid, dim3(NT), 0, s, a);
+    CVL_H_LAUNCH(true);
   } else
 #endif
-  if (wres) {
-    if (dg && a.bsum) hipLaunchKernelGGL((conv_igemm_h_kernel<true, true, true>), grid, dim3(NT), 0, s, a);
-    else if (dg) hipLaunchKernelGGL((conv_igemm_h_kernel<true, false, true>), grid, dim3(NT), 0, s, a);
-    else hipLaunchKernelGGL((conv_igemm_h_kernel<false, false, true>), grid, dim3(NT), 0, s, a);
-  } else if (dg && a.bsum) {
-    hipLaunchKernelGGL((conv_igemm_h_kernel<true, true>), grid, dim3(NT), 0, s, a);
-  } else if (dg) {
-    hipLaunchKernelGGL((conv_igemm_h_kernel<true, false>), grid, dim3(NT), 0, s, a);
-  } else {
-    hipLaunchKernelGGL((conv_igemm_h_kernel<false, false>), grid, dim3(NT), 0, s, a);
+  {
+    CVL_H_LAUNCH(false);
   }
+#undef CVL_H_LAUNCH
   int st = cvl_launch_status();
   if (st || a.splits <= 1) return st;
   return cvl_conv_splitk_finish(a, s);

@@ -187,16 +187,21 @@ __global__ void __launch_bounds__(NT) conv_wgrad_x_kernel(WxArgs g) {
     im += SR;
     ++ist;
   };
+  // measurement builds: CVL_WGX_ABLATE bits (1 no fragment reads, 2 no memory traffic, 4 an
+  // L2-hot source window, 8 no x traffic, 16 no MFMAs)
+  const int abl = ST ? g.ablate : 0;
   auto issue = [&]() {                          // DMA form: LDS-DMA into ring slot cslot
     cvl_bf16* Yb = lds + cslot * SLOT;
     cvl_bf16* Xb = Yb + YST;
     issue_step([&](int j, unsigned oy, unsigned ox) {
+      if (ST && (abl & 2)) { oy = kOOB; ox = kOOB; }            // no memory traffic (zeros)
+      if (ST && (abl & 4)) { oy &= 0x3fff0u; ox &= 0x3fff0u; }   // an L2-hot 256 KiB window
+      if (ST && (abl & 8)) ox = kOOB;                            // no x traffic
       dma16(rsY, Yb + (8 * C::RPI * j + C::RPI * wave) * BCO, oy);
       dma16(rsX, Xb + (8 * C::RPI * j + C::RPI * wave) * BKK, ox);
     });
     cslot = cslot == NSLOT - 1 ? 0 : cslot + 1;
   };
-  const int abl = ST ? g.ablate : 0;           // measurement builds: CVL_WGX_ABLATE bits (1 no fragment reads, 16 no MFMAs)
 
   const int wco = wave >> 2, wk = wave & 3;
   const int lr = lane & 15, lg = lane >> 4;
@@ -546,5 +551,16 @@ extern "C" int cvl_debug_wgx_stamps(uint64_t* host, int max_wgs) {
   if (hipMemcpyFromSymbol(host, HIP_SYMBOL(g_wgx_stamps), (size_t)n * 32, 0, hipMemcpyDeviceToHost) != hipSuccess)
     return -1;
   return g_wgx_stamp_grid;
+}
+
+// The per-wave loop phase cycles of the last stamped launch: u64 [grid][8 waves][8] = (data wait,
+// LDS segment, barrier 1, MFMA issue, barrier 2, steps, nsteps, wave group); at most max_wgs rows.
+extern "C" int cvl_debug_wgx_phase(uint64_t* host, int max_wgs) {
+  const int n = g_wgx_stamp_grid < max_wgs ? g_wgx_stamp_grid : max_wgs;
+  if (n <= 0 || !host || g_wgx_stamp_grid > kPhaseWgs) return 0;
+  if (hipDeviceSynchronize() != hipSuccess) return -1;
+  if (hipMemcpyFromSymbol(host, HIP_SYMBOL(g_wgx_phase), (size_t)n * 512, 0, hipMemcpyDeviceToHost) != hipSuccess)
+    return -1;
+  return n;
 }
 #endif  // CVL_MEASURE

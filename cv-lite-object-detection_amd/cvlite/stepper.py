@@ -56,6 +56,8 @@ class GraphStepper(object):
 
             def split(name):
                 nonlocal g
+                if not self.sync.is_boundary(name):      # merged into a later group's launch
+                    return
                 g.capture_end()
                 segs.append((g, name))
                 g = torch.cuda.CUDAGraph()

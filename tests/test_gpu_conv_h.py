@@ -145,6 +145,53 @@ def test_h_resident_weights_bit_identical(B, H, Cin, dispatch):
         torch.testing.assert_close(a[4], b2[4], rtol=1e-12, atol=1e-9 * float(a[4].abs().max()))
 
 
+@pytest.mark.parametrize("B,H,Cin,Cout", [(16, 128, 64, 64), (4, 64, 128, 128), (4, 32, 256, 256), (2, 16, 512, 512),
+                                          (3, 8, 32, 64)])
+def test_h_register_epilogue_matches_c_image(B, H, Cin, Cout, dispatch):
+    """The SW epilogue (swapped MFMA operands, 16-B stores straight from registers, BN statistics /
+    BN-backward sums kept per (image, N tile) and flushed once per change) against the LDS C-image
+    epilogue (CVL_DISPATCH=h_no_sw): forward with bias / ReLU / BN statistics, data gradient, data
+    gradient with the fused BN-backward first pass, at the backbone 3x3 geometries (conv2_x..conv5_x,
+    bs 16 / 4 / 2: one or several tiles and N tiles per workgroup) and a mosaic map (8x8: SW does
+    not apply, both runs take the C-image form).  Outputs bit-identical (the MFMA forms the same dot
+    products); the sums differ only in fp32 summation order."""
+    from cvlite import ops_nn as nn
+    g = torch.Generator().manual_seed(B * 7 + H + Cin)
+    x = rnd(B, H, H, Cin, gen=g)
+    w = rnd(3, 3, Cin, Cout, scale=(9 * Cin) ** -0.5, gen=g)
+    wf, wd, npad, cin_pad = packs(w)
+    bias = torch.randn(Cout, generator=g).cuda()
+    xg = x.to(BF).cuda()
+    dy = rnd(B, H, H, Cout, gen=g).to(BF).cuda()
+    z = rnd(B, H, H, Cin, gen=g).to(BF).cuda()
+    mr = torch.stack([torch.randn(B, Cin, generator=g) * 0.2, torch.rand(B, Cin, generator=g) + 0.5], -1).cuda()
+    ga, be = (torch.rand(Cin, generator=g) + 0.5).cuda(), torch.randn(Cin, generator=g).cuda()
+    res = []
+    for off in ("1", "0"):
+        dispatch("h_no_sw=" + off)
+        out = torch.empty((B, H, H, Cout), dtype=BF, device="cuda")
+        st = nn.bn_acc(B, Cout, "cuda")
+        d = nn.make_desc(nn.FWD, B, Cin, 3, 3, 1, 1, 1, npad, Cout, Cout, [nn.seg(H, H, H, H, wf, bias)], relu_out=True)
+        nn.conv_igemm(d, xg, out, st)
+        k_fwd = last_kernel()
+        dx = torch.empty((B, H, H, Cin), dtype=BF, device="cuda")
+        dd = nn.make_desc(nn.DGRAD, B, npad, 3, 3, 1, 1, 1, cin_pad, Cin, Cin, [nn.seg(H, H, H, H, wd)])
+        nn.conv_igemm(dd, dy, dx)
+        dx2 = torch.empty_like(dx)
+        sums = nn.bn_acc(B, Cin, "cuda")
+        fused = nn.conv_igemm_dgrad_bnsum(dd, dy, dx2, z, mr, ga, be, sums)
+        torch.cuda.synchronize()
+        res.append((out.view(torch.int16), dx.view(torch.int16), dx2.view(torch.int16), nn.bn_acc_value(st),
+                    nn.bn_acc_value(sums) if fused else None, k_fwd))
+    a, b2 = res
+    assert "conv_igemm_h_kernel" in a[5] and "conv_igemm_h_kernel" in b2[5], (a[5], b2[5])
+    for name, u, v in zip(("fwd", "dgrad", "dgrad+bnsum"), a[:3], b2[:3]):
+        assert torch.equal(u, v), name
+    torch.testing.assert_close(a[3], b2[3], rtol=2e-5, atol=1e-3)
+    if a[4] is not None:
+        torch.testing.assert_close(a[4], b2[4], rtol=2e-5, atol=2e-5 * float(a[4].abs().max()))
+
+
 def test_h_segments_fpn_trio(dispatch):
     """The FPN's three 3x3 output convs (fcos.py:62-66: P3r, P4r, P5 -> P3, P4, P5, own weights and
     biases) as ONE 3-segment launch from one packed source buffer into the level-major F buffer."""

@@ -30,6 +30,7 @@ for s in $steps; do
     wgx)     run 90 gpurun_out/${tag}_wgx.md python -u tools/wgx_stamps.py ;;
     prof)    run 150 gpurun_out/${tag}_prof.log rocprofv3 --kernel-trace --stats -f csv -d gpurun_out/${tag}_prof -o p -- python3 bench.py --steps 10 --warmup 5 --runs 1 --no-cpu-baseline ;;
     hash)    run 120 gpurun_out/${tag}_hash.txt python -u tools/step_hash.py; cat gpurun_out/${tag}_hash.txt ;;
+    dp)      run 700 gpurun_out/${tag}_dp.txt bash tools/dp_overhead.sh; cat gpurun_out/${tag}_dp.txt ;;
     ceiling) run 30 gpurun_out/${tag}_ceiling.json ./tools/mfma_ceiling; cat gpurun_out/${tag}_ceiling.json ;;
     rowdma)  run 60 gpurun_out/${tag}_rowdma.txt ./tools/ubench_rowdma; cat gpurun_out/${tag}_rowdma.txt ;;
     pprobe)  run 90 gpurun_out/${tag}_pprobe.md python -u tools/p_probe.py; cat gpurun_out/${tag}_pprobe.md ;;
