@@ -339,3 +339,123 @@ __device__ __forceinline__ void conv_l_epilogue(const ConvArgs& a, const ConvSeg
     tmark(3);
   }
 }
+
+// ---------------------------------------------------------------------------------------------
+// SW epilogue pieces (round 5; conv_igemm_h.hip / conv_igemm_x.hip / conv_igemm_l.hip): with the
+// MFMA operands swapped (D = W.X^T), acc[i][j] holds, in lane (lr, lg), output channels
+// j*16 + 4*lg + e of pixel i*16 + lr of the wave's rows.  Column blocks 2jp / 2jp + 1 are packed to
+// bf16 and regrouped by one v_permlane16_swap per register so a lane stores 8 CONSECUTIVE channels
+// (wn*WN + jp*32 + sw_lgo(lg) ..) of its pixel with one 16-B store.  BN statistics of the rounded
+// values go into per-lane partials ss1 / ss2[TN][4] that sw_flush_stats() combines.
+typedef __bf16 sw_bf16x2 __attribute__((ext_vector_type(2)));
+typedef float sw_f32x2 __attribute__((ext_vector_type(2)));
+typedef unsigned sw_u32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ int sw_lgo(int lg) { return ((lg & 1) ? 16 : 0) + ((lg & 2) ? 8 : 0); }
+
+// the bias of the lane's 4 channels per column block (fetch where its latency hides)
+template <int TN>
+__device__ __forceinline__ void sw_bias(const ConvArgs& a, const ConvSeg& S, int nw, int lg, float (&bq)[TN][4]) {
+#pragma unroll
+  for (int j = 0; j < TN; ++j)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int n = nw + j * 16 + 4 * lg + e;
+      bq[j][e] = (S.bias && n < a.n_store) ? S.bias[n] : 0.f;
+    }
+}
+
+// stores of one tile (bf16 destination, beta 0; rows past the segment skipped); nw = n0 + wn*WN,
+// r0 = the wave's first row (segment-local)
+template <int TM, int TN, bool STATS>
+__device__ __forceinline__ void sw_store(const ConvArgs& a, const ConvSeg& S, f32x4 (&acc)[TM][TN],
+                                         const float (&bq)[TN][4], int r0, int nw, int HWr, int lane,
+                                         float (&ss1)[TN][4], float (&ss2)[TN][4]) {
+  const int lr = lane & 15, lg = lane >> 4;
+  const bool dense = S.dst_img == (long)HWr;
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+    const int ml = r0 + i * 16 + lr;
+    const bool row_ok = ml < S.rows;
+    long drow;
+    if (dense || !row_ok) {
+      drow = S.dst_base + ml;
+    } else {
+      const int img = ml / HWr, q = ml - img * HWr;
+      drow = conv_dst_row(a, S, img, q);
+    }
+#pragma unroll
+    for (int jp = 0; jp < TN / 2; ++jp) {
+      unsigned pk[2][2];
+#pragma unroll
+      for (int jj = 0; jj < 2; ++jj)
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const int j = 2 * jp + jj;
+          float v0 = acc[i][j][2 * h] + bq[j][2 * h];
+          float v1 = acc[i][j][2 * h + 1] + bq[j][2 * h + 1];
+          if (a.relu_out) { v0 = fmaxf(v0, 0.f); v1 = fmaxf(v1, 0.f); }
+          const unsigned u = __builtin_bit_cast(unsigned, __builtin_convertvector((sw_f32x2){v0, v1}, sw_bf16x2));
+          pk[jj][h] = u;
+          if (STATS && row_ok) {
+            const float q0 = __uint_as_float(u << 16), q1 = __uint_as_float(u & 0xffff0000u);
+            ss1[j][2 * h] += q0;
+            ss2[j][2 * h] = __builtin_fmaf(q0, q0, ss2[j][2 * h]);
+            ss1[j][2 * h + 1] += q1;
+            ss2[j][2 * h + 1] = __builtin_fmaf(q1, q1, ss2[j][2 * h + 1]);
+          }
+        }
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const auto sw = __builtin_amdgcn_permlane16_swap(pk[0][h], pk[1][h], false, false);
+        pk[0][h] = sw[0];
+        pk[1][h] = sw[1];
+      }
+      const int n = nw + jp * 32 + sw_lgo(lg);
+      if (!row_ok || n >= a.n_store) continue;
+      *reinterpret_cast<s16x8*>(reinterpret_cast<cvl_bf16*>(a.dst) + drow * a.ld_dst + a.dst_coff + n) =
+          __builtin_bit_cast(s16x8, (sw_u32x4){pk[0][0], pk[0][1], pk[1][0], pk[1][1]});
+    }
+  }
+}
+
+// the 16-lane row sum, left in every lane of the row (DPP: quad xor 1, quad xor 2, half-row and row mirror)
+__device__ __forceinline__ float sw_row16_sum(float v) {
+  v += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0xB1, 0xF, 0xF, false));
+  v += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x4E, 0xF, 0xF, false));
+  v += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x141, 0xF, 0xF, false));
+  v += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x140, 0xF, 0xF, false));
+  return v;
+}
+
+// statistics flush of image img, columns n0 ..: the WGM waves of a column combined in a fixed
+// order through red ([WGM][BN][2] floats), one fp64 atomic pair per channel; partials reset.
+// Contains two workgroup barriers (every thread must call it).
+template <int BN, int WGM, int TN>
+__device__ __forceinline__ void sw_flush_stats(const ConvArgs& a, float* red, int tid, int wm, int wn_off, int img,
+                                               int n0, float (&ss1)[TN][4], float (&ss2)[TN][4]) {
+  const int lane = tid & 63, lr = lane & 15, lg = lane >> 4;
+#pragma unroll
+  for (int j = 0; j < TN; ++j)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const float t1 = sw_row16_sum(ss1[j][e]), t2 = sw_row16_sum(ss2[j][e]);
+      ss1[j][e] = 0.f;
+      ss2[j][e] = 0.f;
+      if (lr == 0) {
+        const int c = wn_off + j * 16 + 4 * lg + e;
+        red[(wm * BN + c) * 2] = t1;
+        red[(wm * BN + c) * 2 + 1] = t2;
+      }
+    }
+  __syncthreads();
+  if (tid < BN && n0 + tid < a.n_store) {
+    float t1 = 0.f, t2 = 0.f;
+#pragma unroll
+    for (int w = 0; w < WGM; ++w) { t1 += red[(w * BN + tid) * 2]; t2 += red[(w * BN + tid) * 2 + 1]; }
+    acc_u64* st = a.stats + acc_idx((long)img * a.n_store + n0 + tid, 0, a.acc_slots);
+    acc_add(st, t1, a.acc_slots);
+    acc_add(st + a.acc_slots, t2, a.acc_slots);
+  }
+  __syncthreads();
+}

@@ -33,8 +33,12 @@ __device__ __forceinline__ void glds16(const void* g, void* l) {
 // BN x WGM x NST: 128/64-wide tiles run 8 waves as 4 (M) x 2 (N) with a 3-deep ring; the
 // 256-wide tile runs them as 2 x 4 (each wave 128 x 64: a quarter fewer LDS bytes per MFMA and
 // half the DMA issues per FLOP) with a 2-deep ring (2 x 64 KiB).
-template <int BN, int WGM, int NST, bool DGRAD, bool PRIO, bool BSUM = false>
+// SW (round 5): swapped MFMA operands and conv_epilogue.h's register epilogue (sw_store: 16-B
+// stores straight from the registers, BN statistics by DPP + one LDS combine) instead of the LDS C
+// image; bf16 destination, no beta, no fused BN sums, tiles inside one image when statistics are on.
+template <int BN, int WGM, int NST, bool DGRAD, bool PRIO, bool BSUM = false, bool SW = false>
 __global__ void __launch_bounds__(NT) conv_igemm_l_kernel(ConvArgs a) {
+  static_assert(!(SW && BSUM), "the fused BN sums keep the C-image epilogue");
   constexpr int WGN = 8 / WGM;
   constexpr int WM = BM / WGM, WN = BN / WGN;
   constexpr int TM = WM / 16, TN = WN / 16;
@@ -43,7 +47,7 @@ __global__ void __launch_bounds__(NT) conv_igemm_l_kernel(ConvArgs a) {
   constexpr int GPW = AP + BP;                   // LDS-DMA instructions per wave per K step
   constexpr int STAGE = (BM + BN) * BK;          // bf16 elements per ring slot
   constexpr int LDS_C = BM * (BN + 8) + (WGM > 2 ? WGM * BN * 2 * 2 : 0);   // C image + per-wave stats
-  constexpr int LDS_EL = NST * STAGE > LDS_C ? NST * STAGE : LDS_C;
+  constexpr int LDS_EL = SW ? NST * STAGE + WGM * BN * 4 : (NST * STAGE > LDS_C ? NST * STAGE : LDS_C);
   __shared__ __attribute__((aligned(16))) cvl_bf16 lds[LDS_EL];
 
   const int tid = threadIdx.x;
@@ -132,7 +136,9 @@ __global__ void __launch_bounds__(NT) conv_igemm_l_kernel(ConvArgs a) {
   // the epilogue's bias, in flight under the main loop (the 256-wide form runs at the register
   // limit and loads it in the epilogue)
   float bcol[TN];
-  if constexpr (BN <= 128) epi_bias<BN, WGM, TN>(a, S, n0, wn, lane, bcol);
+  float bq[SW ? TN : 1][4];
+  if constexpr (SW) sw_bias<TN>(a, S, n0 + wn * WN, lg, bq);
+  else if constexpr (BN <= 128) epi_bias<BN, WGM, TN>(a, S, n0, wn, lane, bcol);
   f32x4 acc[TM][TN];
 #pragma unroll
   for (int i = 0; i < TM; ++i)
@@ -172,8 +178,10 @@ __global__ void __launch_bounds__(NT) conv_igemm_l_kernel(ConvArgs a) {
       for (int i = 0; i < TM; ++i)
 #pragma unroll
         for (int j = 0; j < TN; ++j) {
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
-              __builtin_bit_cast(bf16x8, fa[i]), __builtin_bit_cast(bf16x8, fb[j]), acc[i][j], 0, 0, 0);
+          acc[i][j] = SW ? __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, fb[j]),
+                                                                    __builtin_bit_cast(bf16x8, fa[i]), acc[i][j], 0, 0, 0)
+                         : __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, fa[i]),
+                                                                    __builtin_bit_cast(bf16x8, fb[j]), acc[i][j], 0, 0, 0);
           if (PRIO && i == 0 && j == 0) {            // keep the MFMA cluster together (T5)
             __builtin_amdgcn_sched_barrier(0);
             __builtin_amdgcn_s_setprio(1);
@@ -190,6 +198,21 @@ __global__ void __launch_bounds__(NT) conv_igemm_l_kernel(ConvArgs a) {
     slot = slot == NST - 1 ? 0 : slot + 1;
   }
 
+  if constexpr (SW) {
+    float ss1[TN][4], ss2[TN][4];
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) { ss1[j][e] = 0.f; ss2[j][e] = 0.f; }
+    if (a.stats) {
+      sw_store<TM, TN, true>(a, S, acc, bq, mloc0 + wm * WM, n0 + wn * WN, HWr, lane, ss1, ss2);
+      sw_flush_stats<BN, WGM, TN>(a, reinterpret_cast<float*>(lds + NST * STAGE), tid, wm, wn * WN, mloc0 / HWr, n0,
+                                  ss1, ss2);
+    } else {
+      sw_store<TM, TN, false>(a, S, acc, bq, mloc0 + wm * WM, n0 + wn * WN, HWr, lane, ss1, ss2);
+    }
+    return;
+  }
   conv_l_epilogue<BN, WGM, TM, TN, NT, BSUM>(a, S, acc, lds, tid, wm, wn, n0, mloc0, HWr, zpre, bpar,
                                               BN <= 128 ? bcol : nullptr);
 }
@@ -306,9 +329,18 @@ int cvl_conv_igemm_l(const cvl_conv_desc* d, int dst_up, int dst_w, const void* 
   dim3 grid(a.m_tiles * (a.Npad / use_bn));
   const bool dg = d->mode == CVL_CONV_DGRAD;
   const bool prio = !cvl_tune_flag("CVL_CONV_NO_PRIO");
+  // SW epilogue: bf16 destination in 8-channel chunks, no beta / scatter / fused sums; with BN
+  // statistics every tile inside one image
+  bool sw = !a.dst_f32 && a.beta == 0.f && !a.bsum && a.dst_up == 1 && a.n_store % 8 == 0 && a.ld_dst % 8 == 0 &&
+            a.dst_coff % 8 == 0 && !cvl_dispatch_flag("l_no_sw");
+  for (int i = 0; sw && a.stats && i < a.nseg; ++i)
+    if ((a.seg[i].Hr * a.seg[i].Wr) % BM) sw = false;
 #define CVL_L_LAUNCH(BN_, WGM_, NST_)                                                                          \
   do {                                                                                                         \
-    if (dg && a.bsum) {                                                                                        \
+    if (sw && BN_ <= 128) {                                                                                     \
+      if (dg) hipLaunchKernelGGL((conv_igemm_l_kernel<BN_, WGM_, NST_, true, true, false, true>), grid, dim3(NT), 0, s, a); \
+      else hipLaunchKernelGGL((conv_igemm_l_kernel<BN_, WGM_, NST_, false, true, false, true>), grid, dim3(NT), 0, s, a);  \
+    } else if (dg && a.bsum) {                                                                                 \
       hipLaunchKernelGGL((conv_igemm_l_kernel<BN_, WGM_, NST_, true, true, true>), grid, dim3(NT), 0, s, a);     \
     } else if (dg) {                                                                                           \
       if (prio) hipLaunchKernelGGL((conv_igemm_l_kernel<BN_, WGM_, NST_, true, true>), grid, dim3(NT), 0, s, a);   \

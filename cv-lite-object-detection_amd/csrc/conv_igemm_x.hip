@@ -13,7 +13,11 @@
 // * Operand LDS images are row-major 64-B rows with an XOR swizzle on the 16-B chunk, applied to
 //   the per-lane SOURCE offset (LDS-DMA writes lane-linear): the ds_read_b128 fragment reads are
 //   bank-conflict free.
-// The epilogue (bias, ReLU, BN statistics, bf16 / fp32 destination, beta) is conv_epilogue.h's.
+// The epilogue (bias, ReLU, BN statistics, bf16 / fp32 destination, beta) is conv_epilogue.h's --
+// or, for launches without BN statistics into a bf16 destination (the towers), the SW form (round
+// 5, as conv_igemm_h.hip): swapped MFMA operands, so a lane's accumulator quad is 4 consecutive
+// channels of one pixel, and 16-B stores straight from the registers after one v_permlane16_swap
+// per packed pair -- no 132 KiB LDS C image (128 ds_write_b16 per thread) and no barrier.
 #include "conv_common.h"
 #include "conv_epilogue.h"
 
@@ -47,7 +51,11 @@ constexpr int LDS32_EL = NSLOT * SLOT > LDS_C ? NSLOT * SLOT : LDS_C;
 
 __device__ __forceinline__ int swz4(int r) { return (r >> 1) & 3; }
 
-template <bool DGRAD, bool DBG = false>
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+
+template <bool DGRAD, bool DBG = false, bool SW = false>
 __global__ void __launch_bounds__(NT) conv_igemm_x32_kernel(ConvArgs a) {
   // DBG: ablation switches (a.dbg bits, CVL_X_ABLATE) for measurement builds only: 1 no A traffic,
   // 2 no B traffic, 4 no MFMA, 8 no epilogue, 16 no vmcnt waits, 32 no DMA instructions, 64 no LDS
@@ -142,6 +150,17 @@ __global__ void __launch_bounds__(NT) conv_igemm_x32_kernel(ConvArgs a) {
 
   const int wm = wave >> 2, wn = wave & 3;
   const int lr = lane & 15, lg = lane >> 4;
+  // SW: the bias of the lane's 4 channels per column block, fetched before the stream
+  float bq[SW ? TN : 1][4];
+  if constexpr (SW) {
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int n = n0 + wn * WN + j * 16 + 4 * lg + e;
+        bq[j][e] = (S.bias && n < a.n_store) ? S.bias[n] : 0.f;
+      }
+  }
   f32x4 acc[TM][TN];
 #pragma unroll
   for (int i = 0; i < TM; ++i)
@@ -197,8 +216,10 @@ __global__ void __launch_bounds__(NT) conv_igemm_x32_kernel(ConvArgs a) {
       for (int i = 0; i < TM; ++i) {
 #pragma unroll
         for (int j = 0; j < TN; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, fa[i]),
-                                                               __builtin_bit_cast(bf16x8, fb[j]), acc[i][j], 0, 0, 0);
+          acc[i][j] = SW ? __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, fb[j]),
+                                                                    __builtin_bit_cast(bf16x8, fa[i]), acc[i][j], 0, 0, 0)
+                         : __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, fa[i]),
+                                                                    __builtin_bit_cast(bf16x8, fb[j]), acc[i][j], 0, 0, 0);
       }
     }
     __builtin_amdgcn_s_setprio(0);
@@ -212,6 +233,48 @@ __global__ void __launch_bounds__(NT) conv_igemm_x32_kernel(ConvArgs a) {
   if (stamp) { stamp[2] = wall_clock64(); stamp[3] = __builtin_amdgcn_s_memtime() - clk0; }
   if (dbg & 8) {
     if (acc[0][0][0] == 12345.f) reinterpret_cast<float*>(a.dst)[1] = 1.f;     // keep the accumulators live
+    return;
+  }
+  if constexpr (SW) {
+    // acc[i][j] = D^T: lane (lr, lg) holds channels j*16 + 4*lg + e of pixel i*16 + lr of its wave's
+    // 128 rows; column blocks 2jp / 2jp+1 regrouped so a lane stores 8 consecutive channels
+    const int lgo = ((lg & 1) ? 16 : 0) + ((lg & 2) ? 8 : 0);
+    const bool dense = S.dst_img == (long)HWr;
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      const int ml = mloc0 + wm * WM + i * 16 + lr;
+      if (ml >= S.rows) continue;
+      long drow;
+      if (dense) {
+        drow = S.dst_base + ml;
+      } else {
+        const int img = ml / HWr, q = ml - img * HWr;
+        drow = conv_dst_row(a, S, img, q);
+      }
+#pragma unroll
+      for (int jp = 0; jp < TN / 2; ++jp) {
+        unsigned pk[2][2];
+#pragma unroll
+        for (int jj = 0; jj < 2; ++jj)
+#pragma unroll
+          for (int h = 0; h < 2; ++h) {
+            float v0 = acc[i][2 * jp + jj][2 * h] + bq[2 * jp + jj][2 * h];
+            float v1 = acc[i][2 * jp + jj][2 * h + 1] + bq[2 * jp + jj][2 * h + 1];
+            if (a.relu_out) { v0 = fmaxf(v0, 0.f); v1 = fmaxf(v1, 0.f); }
+            pk[jj][h] = __builtin_bit_cast(unsigned, __builtin_convertvector((f32x2){v0, v1}, bf16x2));
+          }
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const auto sw = __builtin_amdgcn_permlane16_swap(pk[0][h], pk[1][h], false, false);
+          pk[0][h] = sw[0];
+          pk[1][h] = sw[1];
+        }
+        const int n = n0 + wn * WN + jp * 32 + lgo;
+        if (n >= a.n_store) continue;
+        *reinterpret_cast<s16x8*>(reinterpret_cast<cvl_bf16*>(a.dst) + drow * a.ld_dst + a.dst_coff + n) =
+            __builtin_bit_cast(s16x8, (u32x4){pk[0][0], pk[0][1], pk[1][0], pk[1][1]});
+      }
+    }
     return;
   }
   const s16x8 znone[1] = {s16x8{0, 0, 0, 0, 0, 0, 0, 0}};     // (256-wide tiles: no fused BN sums)
@@ -238,13 +301,20 @@ int cvl_conv_igemm_x(const cvl_conv_desc* d, const ConvArgs& a, hipStream_t s) {
   ConvArgs am = a;
   am.dbg = cvl_tune_int("CVL_X_ABLATE", 0);     // measurement builds (tools/x32_*.py): ablation bits
   g_cvl_conv_last_kernel = CVL_CK_X32;
+  // SW epilogue: bf16 destination in 8-channel chunks, no BN statistics, no beta
+  const bool sw = !a.dst_f32 && !a.stats && a.beta == 0.f && a.n_store % 8 == 0 && a.ld_dst % 8 == 0 &&
+                  a.dst_coff % 8 == 0 && !cvl_dispatch_flag("x_no_sw");
 #ifdef CVL_MEASURE
   if (am.dbg) {
     if (dg) hipLaunchKernelGGL((conv_igemm_x32_kernel<true, true>), grid, dim3(NT), 0, s, am);
     else hipLaunchKernelGGL((conv_igemm_x32_kernel<false, true>), grid, dim3(NT), 0, s, am);
   } else
 #endif
-  if (dg) {
+  if (sw && dg) {
+    hipLaunchKernelGGL((conv_igemm_x32_kernel<true, false, true>), grid, dim3(NT), 0, s, am);
+  } else if (sw) {
+    hipLaunchKernelGGL((conv_igemm_x32_kernel<false, false, true>), grid, dim3(NT), 0, s, am);
+  } else if (dg) {
     hipLaunchKernelGGL((conv_igemm_x32_kernel<true>), grid, dim3(NT), 0, s, am);
   } else {
     hipLaunchKernelGGL((conv_igemm_x32_kernel<false>), grid, dim3(NT), 0, s, am);

@@ -111,6 +111,10 @@ class GradSync(object):
                 pend, pend_bytes = [], 0
         self.works = []
         self.active = tdist.is_initialized() and (tdist.get_world_size(group) > 1 or force_sync())
+        # measurement hook (one rank only): keep the segmented graphs, issue no collective -- the
+        # segmentation's share of the one-rank overhead (tools/dp_overhead.sh)
+        self.segments_only = bool(_lib.dispatch("dp_segments_only")) and self.active and \
+            tdist.get_world_size(group) == 1
         self.trace = None
 
     def is_boundary(self, name):
@@ -138,7 +142,7 @@ class GradSync(object):
                 for n, by, r, d in tr["groups"]]
 
     def ready(self, name):
-        if not self.active or name not in self.launch_at:
+        if not self.active or name not in self.launch_at or self.segments_only:
             return
         ev_r = ev_d = None
         if self.trace is not None:

@@ -233,3 +233,77 @@ def test_x32_tile_geometries(dispatch, mode, B, H, W, C, N):
     if stats is not None:
         o = out.to(F64)
         torch.testing.assert_close(nn.bn_acc_value(stats), torch.stack([o.sum((1, 2)), (o * o).sum((1, 2))], -1), rtol=1e-5, atol=1e-3)
+
+
+@pytest.mark.parametrize("mode,B,H,W,C,N", [("fwd", 2, 64, 64, 256, 256), ("dgrad", 3, 32, 32, 512, 256),
+                                           ("fwd", 3, 8, 8, 256, 256), ("dgrad", 5, 4, 4, 256, 512),
+                                           ("fwd", 2, 16, 16, 256, 512)])
+def test_x32_register_epilogue_matches_c_image(dispatch, mode, B, H, W, C, N):
+    """X32's SW epilogue (swapped MFMA operands, 16-B stores straight from the registers; taken by
+    launches without BN statistics into bf16, the towers) against the LDS C-image epilogue
+    (CVL_DISPATCH=x_no_sw) on the same tile geometries incl. mosaic tiles of whole 8x8 / 4x4 images
+    and partly absent last tiles: bit-identical outputs, and both within bf16 rounding of fp64."""
+    from cvlite import ops_nn as nn
+    dispatch("l_min_tiles=1", "l256_min_tiles=1", "no_h")
+    g = torch.Generator(device="cuda").manual_seed(B * 1000 + H + C + 7)
+    x = rnd((B, H, W, C), 1.0, g)
+    if mode == "fwd":
+        w = rnd((3, 3, C, N), (9 * C) ** -0.5, g).to(F64)
+        wf, _ = packs(w)
+        bias = torch.randn(N, generator=g, device="cuda")
+        d = nn.make_desc(nn.FWD, B, C, 3, 3, 1, 1, 1, N, N, N, [nn.seg(H, W, H, W, wf, bias)], relu_out=True)
+        ref = torch.relu(conv_ref(x.to(F64), w) + bias.to(F64))
+    else:
+        w = rnd((3, 3, N, C), (9 * C) ** -0.5, g).to(F64)
+        _, wd = packs(w)
+        d = nn.make_desc(nn.DGRAD, B, C, 3, 3, 1, 1, 1, N, N, N, [nn.seg(H, W, H, W, wd, None)])
+        ref = dgrad_ref(x.to(F64), w)
+    outs = []
+    for off in ("1", "0"):
+        dispatch("x_no_sw=" + off)
+        out = torch.full((B, H, W, N), 7.0, dtype=BF, device="cuda")
+        nn.conv_igemm(d, x, out)
+        code, name = last_kernel()
+        assert code == 7, name
+        outs.append(out)
+    assert torch.equal(outs[0].view(torch.int16), outs[1].view(torch.int16))
+    torch.testing.assert_close(outs[1].to(F64), ref, rtol=1e-2, atol=2e-2)
+
+
+@pytest.mark.parametrize("mode,B,H,C,N,stats", [("fwd", 4, 64, 128, 128, True), ("dgrad", 4, 64, 128, 128, False),
+                                                ("fwd", 6, 8, 128, 128, False), ("fwd", 2, 32, 64, 128, True)])
+def test_l_register_epilogue_matches_c_image(dispatch, mode, B, H, C, N, stats):
+    """The L kernel's SW epilogue (128-wide tiles: swapped MFMA operands, 16-B stores from registers,
+    per-tile BN statistics by DPP + one LDS combine) against its LDS C-image epilogue
+    (CVL_DISPATCH=l_no_sw): the 3x3 128 -> 128 geometry of ResNet conv3_x (fwd with BN statistics,
+    dgrad), whole 8x8 images per tile (no statistics) and Cin 64; outputs bit-identical, the
+    statistics within fp32 summation order."""
+    from cvlite import ops_nn as nn
+    dispatch("no_h", "no_256", "l_min_tiles=1")
+    g = torch.Generator(device="cuda").manual_seed(B * 100 + H + C + N)
+    x = rnd((B, H, H, C), 1.0, g)
+    if mode == "fwd":
+        w = rnd((3, 3, C, N), (9 * C) ** -0.5, g).to(F64)
+        wf, _ = packs(w)
+        bias = torch.randn(N, generator=g, device="cuda")
+        d = nn.make_desc(nn.FWD, B, C, 3, 3, 1, 1, 1, N, N, N, [nn.seg(H, H, H, H, wf, bias)], relu_out=True)
+        ref = torch.relu(conv_ref(x.to(F64), w) + bias.to(F64))
+    else:
+        w = rnd((3, 3, N, C), (9 * C) ** -0.5, g).to(F64)
+        _, wd = packs(w)
+        d = nn.make_desc(nn.DGRAD, B, C, 3, 3, 1, 1, 1, N, N, N, [nn.seg(H, H, H, H, wd, None)])
+        ref = dgrad_ref(x.to(F64), w)
+    res = []
+    for off in ("1", "0"):
+        dispatch("l_no_sw=" + off)
+        out = torch.full((B, H, H, N), 3.0, dtype=BF, device="cuda")
+        st = nn.bn_acc(B, N, "cuda") if stats else None
+        nn.conv_igemm(d, x, out, st)
+        code, name = last_kernel()
+        assert "L" in name or "conv_igemm_l" in name, name
+        torch.cuda.synchronize()
+        res.append((out, nn.bn_acc_value(st) if stats else None))
+    assert torch.equal(res[0][0].view(torch.int16), res[1][0].view(torch.int16))
+    torch.testing.assert_close(res[1][0].to(F64), ref, rtol=1e-2, atol=2e-2)
+    if stats:
+        torch.testing.assert_close(res[0][1], res[1][1], rtol=2e-5, atol=1e-3)
