@@ -79,7 +79,12 @@ __device__ __forceinline__ unsigned long long memtime_nowait() {
 }
 typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 
-template <int T, int SR = BR, bool ST = false>
+// PF (round 5): the fragments of step t+1 are read from LDS inside step t's MFMA segment (into a
+// second register set), so a wave's load segment is its DMA issues alone; every wave waits for its
+// pieces of step t+1 at the END of its MFMA segment t-1, so with the groups one barrier apart all
+// pieces of t+1 have landed before the barrier that opens either group's MFMA segment t (the
+// X32 kernel's SW form, conv_igemm_x.hip).
+template <int T, int SR = BR, bool ST = false, bool PF = false>
 __global__ void __launch_bounds__(NT) conv_wgrad_x_kernel(WxArgs g) {
   using C = WxCfg<T, SR>;
   // ST: wall-clock stamps of thread 0 (entry, prologue landed, loop done, epilogue stored)
@@ -307,7 +312,82 @@ __global__ void __launch_bounds__(NT) conv_wgrad_x_kernel(WxArgs g) {
     }
   };
 
-  {
+  if constexpr (PF) {
+    constexpr int KS = C::KS;
+    issue();
+    issue();
+    issue();
+    wait_vm<2 * PW>();
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    // one set of dY (A) fragments, re-read row by row right after a row's last MFMA; two sets of
+    // x (B) fragments (every row uses all of them)
+    s16x4 al[KS][TM], ah[KS][TM], bl[2][KS][TN], bh[2][KS][TN];
+    auto rd_a = [&](unsigned base, int h, int i) {
+      const unsigned yo = base + h * BR * BCO * 2;
+      al[h][i] = ds_tr16(yo + ya[i]);
+      ah[h][i] = ds_tr16(yo + yb[i]);
+    };
+    auto rd_b = [&](unsigned base, int b) {
+#pragma unroll
+      for (int h = 0; h < KS; ++h) {
+        const unsigned xo = base + h * BR * BKK * 2;
+#pragma unroll
+        for (int j = 0; j < TN; ++j) { bl[b][h][j] = ds_tr16(xo + xa[j]); bh[b][h][j] = ds_tr16(xo + xb[j]); }
+      }
+    };
+#pragma unroll
+    for (int h = 0; h < KS; ++h)
+#pragma unroll
+      for (int i = 0; i < TM; ++i) rd_a(lds0, h, i);
+    rd_b(lds0, 0);
+    wait_vm<PW>();                              // this wave's pieces of step 1
+    if (stamp) stamp[1] = wall_clock64();
+    if (wco == 1) bar();                        // stagger: waves 4-7 run one barrier behind
+    int rslot = 0;
+    auto pstep = [&](int b) {
+      issue();                                  // step t+3 (out-of-range pieces past the end)
+      bar();
+      lgkm_wait();                              // step t's fragments (read in the previous MFMA segment)
+#pragma unroll
+      for (int h = 0; h < KS; ++h) {
+#pragma unroll
+        for (int i = 0; i < TM; ++i) { tr_pin(al[h][i]); tr_pin(ah[h][i]); }
+#pragma unroll
+        for (int j = 0; j < TN; ++j) { tr_pin(bl[b][h][j]); tr_pin(bh[b][h][j]); }
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_s_setprio(1);
+      const int ns = rslot == NSLOT - 1 ? 0 : rslot + 1;
+      const unsigned nbase = lds0 + ns * (SLOT * 2);
+#pragma unroll
+      for (int h = 0; h < KS; ++h) {
+        s16x8 fb[TN];
+#pragma unroll
+        for (int j = 0; j < TN; ++j) fb[j] = tr_join(bl[b][h][j], bh[b][h][j]);
+#pragma unroll
+        for (int i = 0; i < TM; ++i) {
+          const s16x8 fa = tr_join(al[h][i], ah[h][i]);
+#pragma unroll
+          for (int j = 0; j < TN; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, fa),
+                                                                 __builtin_bit_cast(bf16x8, fb[j]), acc[i][j], 0, 0, 0);
+          __builtin_amdgcn_sched_barrier(0);
+          if (h == 0 && i == 0) rd_b(nbase, b ^ 1);   // step t+1's x fragments, under the MFMAs
+          rd_a(nbase, h, i);                          // step t+1's dY fragments of this row
+          __builtin_amdgcn_sched_barrier(0);
+        }
+      }
+      __builtin_amdgcn_s_setprio(0);
+      wait_vm<PW>();                            // this wave's pieces of step t+2
+      bar();
+      rslot = ns;
+    };
+    for (int st = 0; st < nsteps; st += 2) {
+      pstep(0);
+      if (st + 1 < nsteps) pstep(1);
+    }
+  } else {
     issue();
     issue();
     issue();
@@ -528,9 +608,11 @@ int cvl_conv_wgrad_x(const cvl_conv_desc* d, int ngroups, const void* x, const v
   } else
 #endif
   if (p.T == 256) {
-    hipLaunchKernelGGL((conv_wgrad_x_kernel<256, BR>), grid, dim3(NT), 0, s, g);
+    if (!cvl_dispatch_flag("wg_no_pf")) hipLaunchKernelGGL((conv_wgrad_x_kernel<256, BR, false, true>), grid, dim3(NT), 0, s, g);
+    else hipLaunchKernelGGL((conv_wgrad_x_kernel<256, BR>), grid, dim3(NT), 0, s, g);
   } else if (p.SR == 64) {
-    hipLaunchKernelGGL((conv_wgrad_x_kernel<128, 64>), grid, dim3(NT), 0, s, g);
+    if (!cvl_dispatch_flag("wg_no_pf")) hipLaunchKernelGGL((conv_wgrad_x_kernel<128, 64, false, true>), grid, dim3(NT), 0, s, g);
+    else hipLaunchKernelGGL((conv_wgrad_x_kernel<128, 64>), grid, dim3(NT), 0, s, g);
   } else {
     hipLaunchKernelGGL((conv_wgrad_x_kernel<128, BR>), grid, dim3(NT), 0, s, g);
   }
