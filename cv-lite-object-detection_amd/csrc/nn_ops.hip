@@ -971,96 +971,39 @@ __global__ void add_kernel(const cvl_bf16* a, const cvl_bf16* b, cvl_bf16* out, 
   }
 }
 
-// bias gradient, pass 1: a block sums rows [r0, r1) of the segment; a thread owns 8 columns (one
-// 16-byte load per row), rows UNR at a time with the loads issued first; per-block partials
-// part[blk][ncol8*8] (no atomics: deterministic)
-constexpr int CS_UNR = 4;
-__global__ void __launch_bounds__(NT) colsum8_kernel(const cvl_bf16* __restrict__ dy, int ld, int coff, int ncol8,
-                                                     long base, long img_stride, int HW, long nrows,
-                                                     int rows_per_blk, float* __restrict__ part) {
-  const int tpr = ncol8;
-  const int rpp = NT / tpr;
-  const int cg = threadIdx.x % tpr, rsub = threadIdx.x / tpr;
-  const long r0 = (long)blockIdx.x * rows_per_blk;
-  const long r1 = r0 + rows_per_blk < nrows ? r0 + rows_per_blk : nrows;
-  float s[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-  if (rsub < rpp) {
-    for (long r = r0 + rsub; r < r1; r += (long)rpp * CS_UNR) {
-      s16x8 v[CS_UNR];
-#pragma unroll
-      for (int q = 0; q < CS_UNR; ++q) {
-        long rq = r + (long)q * rpp;
-        rq = rq < r1 ? rq : r1 - 1;                 // clamped: loads stay unconditional
-        const int b = (int)(rq / HW);
-        const long row = base + (long)b * img_stride + (rq - (long)b * HW);
-        v[q] = *reinterpret_cast<const s16x8*>(dy + row * ld + coff + cg * 8);
-      }
-#pragma unroll
-      for (int q = 0; q < CS_UNR; ++q) {
-        if (r + (long)q * rpp >= r1) break;
-        float f[8];
-        unpack8(v[q], f);
-#pragma unroll
-        for (int u = 0; u < 8; ++u) s[u] += f[u];
-      }
-    }
-  }
-  __shared__ float red[NT][9];
-#pragma unroll
-  for (int u = 0; u < 8; ++u) red[threadIdx.x][u] = s[u];
-  __syncthreads();
-  if (rsub == 0) {
-    float* pp = part + (long)blockIdx.x * ncol8 * 8 + cg * 8;
-#pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      float a = 0.f;
-      for (int k = 0; k < rpp; ++k) a += red[k * tpr + cg][u];
-      pp[u] = a;
-    }
-  }
-}
+// Bias gradients (cvl_bias_grad, cvl_bias_grad_multi): column sums of bf16 rows, deterministic.
+// Pass 1: block -> (item, image, row chunk) through the per-item block prefix (rows of a block lie
+// in one image).  A thread owns 8 columns (one 16-B load per row); tpr = 2^lt >= ncol8 threads per
+// row, rpp = NT / tpr rows per pass; the main loop issues CS_UNR row loads before any add (the
+// loop bound covers all CS_UNR rows, so nothing sits between the loads and the compiler keeps them
+// in flight), a tail loop finishes the chunk.  The rows of a thread's column group are combined
+// within the wave by an xor-shuffle tree and across the waves in LDS in wave order; one fp32
+// partial row per block.  Pass 2 (colsum_multi_finish_kernel): per (item, 32-column tile), 32 row
+// groups sum the partial rows k = rg (mod 32) in float64, then combine in row-group order.
+constexpr int CS_UNR = 8;
+constexpr int CS_ROUNDS = 4;        // >= CS_ROUNDS main-loop rounds per block
+constexpr int CS_MAX_PART = 256;    // partial rows per item at most (beyond: longer chunks)
+constexpr int CSF_Q = 8;            // finish: float4 column quads per block (32 columns)
+constexpr int CSF_RG = NT / CSF_Q;  // finish: row groups
 
-// pass 2: db[c] = beta*db + sum_blk part[blk][c] (float64, fixed order); 32 columns x 8 row groups
-__global__ void __launch_bounds__(NT) colsum8_finish_kernel(const float* __restrict__ part, int nblk, int ldp,
-                                                            int ncol, float* db, float beta) {
-  const int cl = threadIdx.x & 31, rg = threadIdx.x >> 5;
-  const int c = blockIdx.x * 32 + cl;
-  __shared__ double red[8][32];
-  double a = 0.0;
-  if (c < ncol)
-    for (int r = rg; r < nblk; r += 8) a += part[(long)r * ldp + c];
-  red[rg][cl] = a;
-  __syncthreads();
-  if (rg == 0 && c < ncol) {
-    double t = 0.0;
-    for (int k = 0; k < 8; ++k) t += red[k][cl];
-    db[c] = (float)t + (beta != 0.f ? beta * db[c] : 0.f);
-  }
-}
-
-inline void colsum8_geometry(int ncol, long nrows, int* ncol8, int* rows_per_blk, int* nblk) {
-  *ncol8 = (ncol + 7) / 8;
-  const int rpp = NT / *ncol8;
-  long rpb = (nrows + 511) / 512;                       // <= 512 partial rows
-  const long lo = (long)rpp * CS_UNR * 2;
-  rpb = rpb < lo ? lo : rpb;
-  rpb = (rpb + rpp - 1) / rpp * rpp;
-  *rows_per_blk = (int)rpb;
-  *nblk = (int)((nrows + rpb - 1) / rpb);
-}
-
-// Batched bias gradients (cvl_bias_grad_multi): block -> (item, image, row chunk) through the
-// per-item block prefix; rows of a block lie in one image (no per-row division).  Pass 1 writes
-// per-block column partials, pass 2 (one block per item) sums them in block order in float64.
 struct BiasMulti {
   cvl_bias_item it[CVL_BIAS_MAX_ITEMS];
-  int blk0[CVL_BIAS_MAX_ITEMS + 1];   // first block of each item (prefix), blk0[n] = grid
+  int blk0[CVL_BIAS_MAX_ITEMS + 1];   // first pass-1 block of each item (prefix), blk0[n] = grid
+  int fblk0[CVL_BIAS_MAX_ITEMS + 1];  // first finish block of each item (prefix)
   int chunks[CVL_BIAS_MAX_ITEMS];     // row chunks per image
-  int rpb[CVL_BIAS_MAX_ITEMS];        // rows per chunk (multiple of the item's rows per pass)
+  int rpb[CVL_BIAS_MAX_ITEMS];        // rows per chunk (multiple of rpp * CS_UNR)
+  int lt[CVL_BIAS_MAX_ITEMS];         // log2 threads per row
   long poff[CVL_BIAS_MAX_ITEMS];      // float offset of the item's partials in the workspace
   int n;
   float* part;
 };
+
+__device__ __forceinline__ void colsum_add8(float* s, s16x8 v) {
+  float f[8];
+  unpack8(v, f);
+#pragma unroll
+  for (int u = 0; u < 8; ++u) s[u] += f[u];
+}
 
 __global__ void __launch_bounds__(NT) colsum_multi_kernel(BiasMulti m) {
   int i = 0;
@@ -1069,84 +1012,126 @@ __global__ void __launch_bounds__(NT) colsum_multi_kernel(BiasMulti m) {
   const cvl_bias_item& it = m.it[i];
   const int local = blockIdx.x - m.blk0[i];
   const int b = local / m.chunks[i], chunk = local - b * m.chunks[i];
-  const int ncol8 = (it.ncol + 7) / 8, tpr = ncol8, rpp = NT / tpr;
-  const int cg = threadIdx.x % tpr, rsub = threadIdx.x / tpr;
+  const int ncol8 = (it.ncol + 7) / 8, lt = m.lt[i], tpr = 1 << lt, rpp = NT >> lt;
+  const int cg = threadIdx.x & (tpr - 1), rsub = threadIdx.x >> lt;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int r0 = chunk * m.rpb[i];
   const int r1 = min(r0 + m.rpb[i], it.HW);
-  const cvl_bf16* dy = reinterpret_cast<const cvl_bf16*>(it.dy) + (it.base + (long)b * it.img_stride) * it.ld +
-                       it.coff + cg * 8;
+  const long ld = it.ld;
   float s[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-  if (rsub < rpp) {
-    for (int r = r0 + rsub; r < r1; r += rpp * CS_UNR) {
+  if (cg < ncol8) {
+    const cvl_bf16* dy = reinterpret_cast<const cvl_bf16*>(it.dy) + (it.base + (long)b * it.img_stride) * ld +
+                         it.coff + cg * 8;
+    int r = r0 + rsub;
+    for (; r + (CS_UNR - 1) * rpp < r1; r += CS_UNR * rpp) {
       s16x8 v[CS_UNR];
 #pragma unroll
-      for (int q = 0; q < CS_UNR; ++q) {
-        const int rq = min(r + q * rpp, r1 - 1);        // clamped: loads stay unconditional
-        v[q] = *reinterpret_cast<const s16x8*>(dy + (long)rq * it.ld);
-      }
+      for (int q = 0; q < CS_UNR; ++q) v[q] = *reinterpret_cast<const s16x8*>(dy + (long)(r + q * rpp) * ld);
 #pragma unroll
-      for (int q = 0; q < CS_UNR; ++q) {
-        if (r + q * rpp >= r1) break;
-        float f[8];
-        unpack8(v[q], f);
-#pragma unroll
-        for (int u = 0; u < 8; ++u) s[u] += f[u];
-      }
+      for (int q = 0; q < CS_UNR; ++q) colsum_add8(s, v[q]);
     }
+    for (; r < r1; r += rpp) colsum_add8(s, *reinterpret_cast<const s16x8*>(dy + (long)r * ld));
   }
-  __shared__ float red[NT][9];
+  // rows of one column group within a wave: xor tree over the lane bits above lt (both lanes of a
+  // pair form the same sum)
+  for (int o = tpr; o < 64; o <<= 1)
 #pragma unroll
-  for (int u = 0; u < 8; ++u) red[threadIdx.x][u] = s[u];
+    for (int u = 0; u < 8; ++u) s[u] += __shfl_xor(s[u], o, 64);
+  __shared__ f32x4 red[NT * 2];
+  const int slot = lt < 6 ? wave : rsub, nslot = lt < 6 ? NT / 64 : rpp;
+  if (lt >= 6 || lane < tpr) {
+    red[(slot * tpr + cg) * 2] = f32x4{s[0], s[1], s[2], s[3]};
+    red[(slot * tpr + cg) * 2 + 1] = f32x4{s[4], s[5], s[6], s[7]};
+  }
   __syncthreads();
-  if (rsub == 0) {
-    float* pp = m.part + m.poff[i] + (long)local * ncol8 * 8 + cg * 8;
+  if ((int)threadIdx.x < tpr && (int)threadIdx.x < ncol8) {
+    const int c = threadIdx.x;
+    f32x4 a0 = red[c * 2], a1 = red[c * 2 + 1];
+    for (int k = 1; k < nslot; ++k) {
+      a0 += red[(k * tpr + c) * 2];
+      a1 += red[(k * tpr + c) * 2 + 1];
+    }
+    f32x4* pp = reinterpret_cast<f32x4*>(m.part + m.poff[i] + ((long)local * ncol8 + c) * 8);
+    pp[0] = a0;
+    pp[1] = a1;
+  }
+}
+
+__global__ void __launch_bounds__(NT) colsum_multi_finish_kernel(BiasMulti m) {
+  int i = 0;
+  for (int k = 1; k < m.n; ++k)
+    if ((int)blockIdx.x >= m.fblk0[k]) i = k;
+  const cvl_bias_item& it = m.it[i];
+  const int nblk = m.blk0[i + 1] - m.blk0[i], ld8 = (it.ncol + 7) / 8 * 8;
+  const int q = threadIdx.x % CSF_Q, rg = threadIdx.x / CSF_Q;
+  const int c = (blockIdx.x - m.fblk0[i]) * (CSF_Q * 4) + q * 4;
+  double a[4] = {0.0, 0.0, 0.0, 0.0};
+  if (c < ld8) {
+    const float* p = m.part + m.poff[i] + c;
+    int k = rg;
+    for (; k + 7 * CSF_RG < nblk; k += 8 * CSF_RG) {
+      f32x4 v[8];
 #pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      float a = 0.f;
-      for (int k = 0; k < rpp; ++k) a += red[k * tpr + cg][u];
-      pp[u] = a;
+      for (int u = 0; u < 8; ++u) v[u] = *reinterpret_cast<const f32x4*>(p + (long)(k + u * CSF_RG) * ld8);
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) a[j] += v[u][j];
+    }
+    for (; k < nblk; k += CSF_RG) {
+      const f32x4 v = *reinterpret_cast<const f32x4*>(p + (long)k * ld8);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) a[j] += v[j];
+    }
+  }
+  __shared__ double red[CSF_RG][CSF_Q * 4 + 1];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) red[rg][q * 4 + j] = a[j];
+  __syncthreads();
+  if (threadIdx.x < CSF_Q * 4) {
+    const int cc = (blockIdx.x - m.fblk0[i]) * (CSF_Q * 4) + threadIdx.x;
+    if (cc < it.ncol) {
+      double t = 0.0;
+      for (int k = 0; k < CSF_RG; ++k) t += red[k][threadIdx.x];
+      it.db[cc] = (float)t + (it.beta != 0.f ? it.beta * it.db[cc] : 0.f);
     }
   }
 }
 
-__global__ void __launch_bounds__(256) colsum_multi_finish_kernel(BiasMulti m) {
-  const int i = blockIdx.x;
-  const cvl_bias_item& it = m.it[i];
-  const int nblk = m.blk0[i + 1] - m.blk0[i], ld = (it.ncol + 7) / 8 * 8;
-  for (int c = threadIdx.x; c < it.ncol; c += 256) {
-    double a = 0.0;
-    const float* p = m.part + m.poff[i] + c;
-    for (int k = 0; k < nblk; ++k) a += p[(long)k * ld];
-    it.db[c] = (float)a + (it.beta != 0.f ? it.beta * it.db[c] : 0.f);
-  }
-}
-
-// per-item geometry: ~16+ passes of rows per block, chunks per image so the launch has work for
-// every CU without tiny blocks
+// per-item geometry: chunks of >= CS_ROUNDS main-loop rounds, at most CS_MAX_PART partial rows per
+// item; a chunk never crosses an image
 inline bool bias_multi_plan(const cvl_bias_item* items, int n, BiasMulti* m, long* total_floats) {
   if (n <= 0 || n > CVL_BIAS_MAX_ITEMS) return false;
-  int blk = 0;
+  int blk = 0, fblk = 0;
   long off = 0;
   for (int i = 0; i < n; ++i) {
     const cvl_bias_item& it = items[i];
     if (!it.dy || !it.db || it.ncol <= 0 || it.ncol > 8 * NT || it.HW <= 0 || it.B <= 0 || it.ld % 8 ||
         it.coff % 8 || it.coff + (it.ncol + 7) / 8 * 8 > it.ld)
       return false;
-    const int ncol8 = (it.ncol + 7) / 8, rpp = NT / ncol8;
-    int rpb = rpp * CS_UNR * 4;
-    const long want = (long)it.B * it.HW / 96 + 1;      // ~96 blocks of rows per item at most
-    if (want > rpb) rpb = (int)((want + rpp - 1) / rpp * rpp);
-    if (rpb > it.HW) rpb = (it.HW + rpp - 1) / rpp * rpp;
+    const int ncol8 = (it.ncol + 7) / 8;
+    int lt = 0;
+    while ((1 << lt) < ncol8) ++lt;
+    const int rpp = NT >> lt, step = rpp * CS_UNR;
+    long rpb = (long)step * CS_ROUNDS;
+    const long want = ((long)it.B * it.HW + CS_MAX_PART - 1) / CS_MAX_PART;
+    if (want > rpb) rpb = want;
+    if (rpb > it.HW) rpb = it.HW;
+    rpb = (rpb + step - 1) / step * step;
     m->it[i] = it;
-    m->rpb[i] = rpb;
-    m->chunks[i] = (it.HW + rpb - 1) / rpb;
+    m->rpb[i] = (int)rpb;
+    m->lt[i] = lt;
+    m->chunks[i] = (int)((it.HW + rpb - 1) / rpb);
     m->blk0[i] = blk;
+    m->fblk0[i] = fblk;
     m->poff[i] = off;
     const int nb = it.B * m->chunks[i];
     blk += nb;
+    fblk += (ncol8 * 8 + CSF_Q * 4 - 1) / (CSF_Q * 4);
     off += (long)nb * ncol8 * 8;
   }
   m->blk0[n] = blk;
+  m->fblk0[n] = fblk;
   m->n = n;
   m->part = nullptr;
   *total_floats = off;
@@ -1663,30 +1648,6 @@ extern "C" int cvl_add(const void* a, const void* b, void* out, long n, cvl_stre
   return cvl_launch_status();
 }
 
-extern "C" size_t cvl_bias_grad_workspace_size(int ncol, int HW, int B) {
-  if (ncol <= 0 || HW <= 0 || B <= 0) return 0;
-  int ncol8, rpb, nblk;
-  colsum8_geometry(ncol, (long)B * HW, &ncol8, &rpb, &nblk);
-  return sizeof(float) * (size_t)nblk * ncol8 * 8;
-}
-
-extern "C" int cvl_bias_grad(const void* dy, int ld, int coff, int ncol, int64_t base, int64_t img_stride,
-                             int HW, int B, void* workspace, size_t workspace_bytes, float* db, float beta,
-                             cvl_stream_t stream) {
-  CVL_CHECK_ARG(dy && workspace && db && ncol > 0 && ncol <= 8 * NT && HW > 0 && B > 0);
-  CVL_CHECK_ARG(ld % 8 == 0 && coff % 8 == 0 && coff + (ncol + 7) / 8 * 8 <= ld);
-  CVL_CHECK_ARG(workspace_bytes >= cvl_bias_grad_workspace_size(ncol, HW, B));
-  int ncol8, rpb, nblk;
-  const long nrows = (long)B * HW;
-  colsum8_geometry(ncol, nrows, &ncol8, &rpb, &nblk);
-  float* part = reinterpret_cast<float*>(workspace);
-  hipLaunchKernelGGL(colsum8_kernel, dim3(nblk), dim3(NT), 0, S_, (const cvl_bf16*)dy, ld, coff, ncol8,
-                     (long)base, (long)img_stride, HW, nrows, rpb, part);
-  hipLaunchKernelGGL(colsum8_finish_kernel, dim3((ncol + 31) / 32), dim3(NT), 0, S_, (const float*)part, nblk,
-                     ncol8 * 8, ncol, db, beta);
-  return cvl_launch_status();
-}
-
 extern "C" size_t cvl_bias_grad_multi_workspace_size(const cvl_bias_item* items, int n) {
   BiasMulti m;
   long tot = 0;
@@ -1702,9 +1663,41 @@ extern "C" int cvl_bias_grad_multi(const cvl_bias_item* items, int n, void* work
   CVL_CHECK_ARG(workspace_bytes >= sizeof(float) * (size_t)tot);
   m.part = reinterpret_cast<float*>(workspace);
   hipLaunchKernelGGL(colsum_multi_kernel, dim3(m.blk0[n]), dim3(NT), 0, S_, m);
-  hipLaunchKernelGGL(colsum_multi_finish_kernel, dim3(n), dim3(256), 0, S_, m);
+  hipLaunchKernelGGL(colsum_multi_finish_kernel, dim3(m.fblk0[n]), dim3(NT), 0, S_, m);
   return cvl_launch_status();
 }
+
+// the single-item forms: one cvl_bias_item through the batched kernels (the plan depends on ncol,
+// HW and B only, so the workspace size needs no pointers)
+extern "C" size_t cvl_bias_grad_workspace_size(int ncol, int HW, int B) {
+  if (ncol <= 0 || HW <= 0 || B <= 0) return 0;
+  cvl_bias_item it = {};
+  it.dy = &it;
+  it.db = reinterpret_cast<float*>(&it);
+  it.ld = (ncol + 7) / 8 * 8;
+  it.ncol = ncol;
+  it.HW = HW;
+  it.B = B;
+  return cvl_bias_grad_multi_workspace_size(&it, 1);
+}
+
+extern "C" int cvl_bias_grad(const void* dy, int ld, int coff, int ncol, int64_t base, int64_t img_stride,
+                             int HW, int B, void* workspace, size_t workspace_bytes, float* db, float beta,
+                             cvl_stream_t stream) {
+  cvl_bias_item it = {};
+  it.dy = dy;
+  it.db = db;
+  it.base = base;
+  it.img_stride = img_stride;
+  it.ld = ld;
+  it.coff = coff;
+  it.ncol = ncol;
+  it.HW = HW;
+  it.B = B;
+  it.beta = beta;
+  return cvl_bias_grad_multi(&it, 1, workspace, workspace_bytes, stream);
+}
+
 
 extern "C" int cvl_sgd_clip_update(float* w, const float* g, float* v, int64_t n, const float* lr_dev,
                                    float momentum, float inv_bs, float clip, double* sumsq_ws,

@@ -108,3 +108,28 @@ def test_struct_layouts_match_header(tmp_path):
         assert int(got["%s size" % cname]) == ctypes.sizeof(cls), cname
         for f in cls._fields_:
             assert int(got["%s.%s" % (cname, f[0])]) == getattr(cls, f[0]).offset, (cname, f[0])
+
+
+def test_bias_grad_plan_workspace_sizes():
+    """The bias-gradient partial-row plan (host code, nn_ops.hip bias_multi_plan): chunks of
+    >= 4 rounds of 8 rows per thread, <= 256 partial rows per item, never across an image; the
+    workspace is one fp32 row of round_up(ncol, 8) per partial row.  Invalid items size to 0."""
+    from cvlite import _lib
+    from cvlite import ops_nn as nn
+    lib = _lib.load()
+    ws = lambda ncol, HW, B: int(lib.cvl_bias_grad_workspace_size(ncol, HW, B))
+    # FPN level 0 at 512 / bs 16: 8 rows per pass, 64-row rounds -> 256-row chunks, 16 per image
+    assert ws(256, 4096, 16) == 4 * 256 * 256
+    # FCOS cls head (20 -> 24 columns, 4 threads per row, 64 rows per pass): 2048-row chunks
+    assert ws(20, 4096, 16) == 4 * (16 * 2) * 24
+    # the 256-partial-row cap: chunks grow beyond the minimum for large levels
+    assert ws(256, 16384, 16) == 4 * (16 * 16) * 256
+    # single-row images: one chunk per image
+    assert ws(516, 1, 3) == 4 * 3 * 520
+    assert ws(0, 10, 1) == 0 and ws(8, 0, 1) == 0
+    arr = (nn.BiasItem * 2)()
+    for i in range(2):
+        arr[i] = nn.BiasItem(16, 16, 0, 4096, 256, 0, 256, 4096, 16, 0.0)
+    assert int(lib.cvl_bias_grad_multi_workspace_size(arr, 2)) == 2 * 4 * 256 * 256
+    arr[1] = nn.BiasItem(16, 16, 0, 4096, 256, 8, 256, 4096, 16, 0.0)      # coff + 256 > ld
+    assert int(lib.cvl_bias_grad_multi_workspace_size(arr, 2)) == 0

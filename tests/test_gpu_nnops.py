@@ -226,6 +226,16 @@ def test_relu_bwd_bias_grad_sgd_lr():
     db = torch.zeros(720, device="cuda")
     items.append((dr, 736, 0, 720, 17, 300, 250, 2, db, 0.0))
     exps.append((db, d_ret[:, 17:267, :720].sum((0, 1))))
+    # the widest item (2048 columns: one row per pass), single-row images, a partly filled
+    # column-group tile (65 groups of 8 -> 128 threads per row)
+    wide = bfr(torch.randn(2, 40, 2048, generator=g, dtype=torch.float64))
+    db = torch.zeros(2048, device="cuda")
+    items.append((wide.to(BF).cuda(), 2048, 0, 2048, 3, 40, 33, 2, db, 0.0))
+    exps.append((db, wide[:, 3:36].sum((0, 1))))
+    one = bfr(torch.randn(3, 2, 528, generator=g, dtype=torch.float64))
+    db = torch.zeros(520, device="cuda")
+    items.append((one.to(BF).cuda(), 528, 8, 520, 1, 2, 1, 3, db, 0.0))
+    exps.append((db, one[:, 1, 8:528].sum(0)))
     db = torch.full((256,), 2.0, device="cuda")
     items.append((df, 256, 0, 256, 37, 100, 100, B, db, 0.5))
     exps.append((db, 1.0 + fpn[37:].reshape(B, 100, 256).sum((0, 1))))
