@@ -86,7 +86,35 @@ struct ConvArgs {
   acc_u64* bsum;
   float bhi;
   const cvl_bf16* by;     // non-null: the ReLU mask comes from y > 0 (a residual unit's output), not bn(z)
+  unsigned long long* probe;   // cvl_probe_arm slot of this launch (kernels that support it), or null
 };
+
+// cvl_probe_arm (probe.hip): the slot armed for the current cvl_conv_igemm call (taken at its entry;
+// take = clear it, so one armed slot times at most one launch)
+uint64_t* cvl_probe_current(bool take);
+void cvl_probe_enter_call();
+
+// In-kernel launch timing into a cvl_probe_arm slot (u64 [4]: start, sum of ticks, launches, done
+// workgroups): workgroup 0 stamps the start; every workgroup counts itself done after a barrier;
+// the last one adds (now - start) and resets the counter.  Relaxed device-scope atomics only (no
+// fences: a release fence at agent scope writes the L2 back and cost the tower launch ~15 %);
+// workgroup 0 stores the start at its entry and counts itself done at its end, so the last
+// workgroup reads a start stamp written long before.
+__device__ __forceinline__ void probe_enter(unsigned long long* p) {
+  if (blockIdx.x == 0 && threadIdx.x == 0) __hip_atomic_store(p, wall_clock64(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void probe_leave(unsigned long long* p) {
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    if (atomicAdd(p + 3, 1ull) == (unsigned long long)gridDim.x - 1) {
+      const unsigned long long t = wall_clock64();
+      const unsigned long long t0 = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      atomicAdd(p + 1, t - t0);
+      atomicAdd(p + 2, 1ull);
+      __hip_atomic_store(p + 3, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+}
 
 // an exact-mode BN accumulator buffer decoded in place (nn_ops.hip; no-op in the float64 mode)
 int cvl_bn_acc_prepare(uint64_t* acc, long nstat, hipStream_t s);
@@ -134,6 +162,7 @@ static inline int cvl_conv_prepare(const cvl_conv_desc* d, int bm, ConvArgs* a) 
   a->dbg = 0;
   a->bz = nullptr; a->bmr = nullptr; a->bga = nullptr; a->bbe = nullptr; a->bsum = nullptr; a->bhi = 0.f;
   a->by = nullptr;
+  a->probe = nullptr;
   a->acc_slots = cvl_bn_acc_slots();
   a->nseg = d->nseg;
   a->B = d->B;

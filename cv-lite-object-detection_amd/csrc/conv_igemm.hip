@@ -540,6 +540,7 @@ extern "C" int cvl_conv_igemm(const cvl_conv_desc* d, const void* src, void* dst
   acc_u64* bn_stats = reinterpret_cast<acc_u64*>(bn_stats_acc);
   hipStream_t s = (hipStream_t)stream;
   g_cvl_conv_last_kernel = CVL_CK_NONE;
+  cvl_probe_enter_call();
   CVL_CHECK_ARG(d);
   if (d->prec == CVL_PREC_F32) return cvl_conv_f32(d, src, dst, bn_stats, s);    // parity mode
   CVL_CHECK_ARG(d->prec == CVL_PREC_BF16);

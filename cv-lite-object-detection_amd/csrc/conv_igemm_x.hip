@@ -55,8 +55,8 @@ typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 
-template <bool DGRAD, bool DBG = false, bool SW = false>
-__global__ void __launch_bounds__(NT) conv_igemm_x32_kernel(ConvArgs a) {
+template <bool DGRAD, bool DBG, bool SW>
+__device__ __forceinline__ void x32_body(const ConvArgs& a) {
   // DBG: ablation switches (a.dbg bits, CVL_X_ABLATE) for measurement builds only: 1 no A traffic,
   // 2 no B traffic, 4 no MFMA, 8 no epilogue, 16 no vmcnt waits, 32 no DMA instructions, 64 no LDS
   // reads, 512 no barriers
@@ -281,6 +281,13 @@ __global__ void __launch_bounds__(NT) conv_igemm_x32_kernel(ConvArgs a) {
   conv_l_epilogue<BN, WGM, TM, TN, NT>(a, S, acc, lds, tid, wm, wn, n0, mloc0, HWr, znone, BnSumPar{});
 }
 
+template <bool DGRAD, bool DBG = false, bool SW = false>
+__global__ void __launch_bounds__(NT) conv_igemm_x32_kernel(ConvArgs a) {
+  if (a.probe) probe_enter(a.probe);
+  x32_body<DGRAD, DBG, SW>(a);
+  if (a.probe) probe_leave(a.probe);
+}
+
 }  // namespace
 
 // Called by cvl_conv_igemm_l for launches it would run on the 256 x 256 L tile; returns -1 when
@@ -300,6 +307,7 @@ int cvl_conv_igemm_x(const cvl_conv_desc* d, const ConvArgs& a, hipStream_t s) {
   dim3 grid(a.m_tiles * (a.Npad / BN));
   ConvArgs am = a;
   am.dbg = cvl_tune_int("CVL_X_ABLATE", 0);     // measurement builds (tools/x32_*.py): ablation bits
+  am.probe = reinterpret_cast<unsigned long long*>(cvl_probe_current(true));   // bench.py's in-step timing
   g_cvl_conv_last_kernel = CVL_CK_X32;
   // SW epilogue: bf16 destination in 8-channel chunks, no BN statistics, no beta
   const bool sw = !a.dst_f32 && !a.stats && a.beta == 0.f && a.n_store % 8 == 0 && a.ld_dst % 8 == 0 &&

@@ -1,39 +1,31 @@
-// In-graph launch timing: a timestamp launch before and after a kernel on the same stream, both
-// captured into the training step's HIP graph with it, so the kernel's duration is measured inside
-// the timed replays (torch's timing events cannot be recorded inside a HIP graph on ROCm).  The
-// counter is the GPU's constant-rate wall clock (s_memrealtime, cvl_probe_clock_hz); the interval
-// also holds the two inter-kernel gaps of the graph (a few us), so it bounds the kernel from above.
-#include "cvl_common.h"
+// In-graph launch timing: cvl_probe_arm hands a device slot to the next cvl_conv_igemm call; the
+// tower kernel it launches (X32) stamps itself from inside (conv_common.h probe_enter / probe_leave:
+// workgroup 0's entry to the last workgroup's exit on the GPU's constant-rate wall clock,
+// s_memrealtime, cvl_probe_clock_hz).  The launch arguments carry the slot, so the timing is
+// captured into the training step's HIP graph and measured inside the timed replays (torch's timing
+// events cannot be recorded inside a HIP graph on ROCm) with no extra dispatch in the step.
+#include "conv_common.h"
 
 namespace {
-
-// slot[0] = start stamp, slot[1] += end - start, slot[2] += 1 (one lane; plain vector stores)
-__global__ void probe_begin_kernel(unsigned long long* slot) {
-  if (threadIdx.x == 0) slot[0] = wall_clock64();
-}
-
-__global__ void probe_end_kernel(unsigned long long* slot) {
-  if (threadIdx.x == 0) {
-    const unsigned long long t = wall_clock64();
-    slot[1] += t - slot[0];
-    slot[2] += 1ull;
-  }
-}
-
+uint64_t* g_armed = nullptr;     // cvl_probe_arm: for the next cvl_conv_igemm call
+uint64_t* g_current = nullptr;   // the current call's slot (moved from g_armed at the call's entry)
 }  // namespace
 
-extern "C" int cvl_probe_begin(uint64_t* slot, cvl_stream_t stream) {
-  CVL_CHECK_ARG(slot);
-  hipLaunchKernelGGL(probe_begin_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream,
-                     reinterpret_cast<unsigned long long*>(slot));
-  return cvl_launch_status();
+void cvl_probe_enter_call() {
+  g_current = g_armed;
+  g_armed = nullptr;
 }
 
-extern "C" int cvl_probe_end(uint64_t* slot, cvl_stream_t stream) {
-  CVL_CHECK_ARG(slot);
-  hipLaunchKernelGGL(probe_end_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream,
-                     reinterpret_cast<unsigned long long*>(slot));
-  return cvl_launch_status();
+uint64_t* cvl_probe_current(bool take) {
+  uint64_t* p = g_current;
+  if (take) g_current = nullptr;
+  return p;
+}
+
+extern "C" int cvl_probe_arm(uint64_t* slot) {
+  CVL_CHECK_ARG(slot && reinterpret_cast<uintptr_t>(slot) % 8 == 0);
+  g_armed = slot;
+  return CVL_OK;
 }
 
 extern "C" double cvl_probe_clock_hz(void) {

@@ -200,10 +200,8 @@ class FPNDetector(object):
                                                relu_out=(i == 3))
                 probe = getattr(self, "tower_probe", None)      # bench.py: in-step launch timing
                 if probe is not None:
-                    nn.probe_begin(probe)
+                    nn.probe_arm(probe)
                 nn.conv_igemm(d, src, out)
-                if probe is not None:
-                    nn.probe_end(probe)
             else:                                   # A/B reference: one launch per tower
                 for t, tw in enumerate((self.cls_tower, self.reg_tower)):
                     d = tw[i].fwd_desc(B, self._tower_segs(tw[i], B, shapes, off), ld_dst=FPN_C, relu_out=(i == 3))

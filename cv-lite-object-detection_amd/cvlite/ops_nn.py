@@ -78,13 +78,10 @@ def conv_igemm(desc, src, dst, stats=None):
               n if ws is not None else 0, stream())
 
 
-def probe_begin(slot):
-    """Start stamp of an in-graph launch probe (slot: uint64 [3] device tensor, cvl_probe_begin)."""
-    _lib.call("cvl_probe_begin", ptr(slot), stream())
-
-
-def probe_end(slot):
-    _lib.call("cvl_probe_end", ptr(slot), stream())
+def probe_arm(slot):
+    """Time the next conv_igemm launch from inside if it runs the tower kernel (slot: uint64 [4]
+    device tensor, zeroed; cvl_probe_arm)."""
+    _lib.call("cvl_probe_arm", ptr(slot))
 
 
 def probe_seconds(slot):

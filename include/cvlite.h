@@ -190,12 +190,14 @@ enum { CVL_CK_NONE = 0, CVL_CK_BASE = 1, CVL_CK_BASE_SPLITK = 2, CVL_CK_L64 = 3,
 int cvl_conv_igemm_last_kernel(void);
 const char* cvl_conv_kernel_name(int code);
 
-/* Measurement hook (no reference counterpart: bench.py's in-step roofline timing).  Launch
- * cvl_probe_begin / cvl_probe_end around a kernel on the same stream (graph-capturable): slot[0]
- * = start stamp, slot[1] += elapsed ticks, slot[2] += 1 (uint64 x3 device buffer, zero it first).
- * cvl_probe_clock_hz = ticks per second of the GPU wall clock. */
-int cvl_probe_begin(uint64_t* slot, cvl_stream_t stream);
-int cvl_probe_end(uint64_t* slot, cvl_stream_t stream);
+/* Measurement hook (no reference counterpart: bench.py's in-step roofline timing).  cvl_probe_arm
+ * hands slot (uint64 x4 device buffer, zero it first) to the NEXT cvl_conv_igemm call: when that
+ * call runs the tower kernel (cvl_conv_igemm_last_kernel() == CVL_CK_X32) the kernel times itself
+ * (workgroup 0's start to the last workgroup's end): slot[1] += elapsed ticks, slot[2] += 1 (slot[0]
+ * / slot[3]: start stamp / workgroup counter); any other kernel leaves the slot untouched.  The slot
+ * travels in the launch arguments, so graph capture keeps it.  cvl_probe_clock_hz = ticks per
+ * second of the GPU wall clock. */
+int cvl_probe_arm(uint64_t* slot);
 double cvl_probe_clock_hz(void);
 
 /* Weight gradient (replaces Conv2DBackpropFilter + the per-image gradient accumulation of

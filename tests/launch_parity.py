@@ -37,7 +37,7 @@ TOL_BF16, TOL_F32 = 1e-2, 1e-4
 
 # entry points that launch nothing, or only size / configure (not compute on tensors)
 NON_COMPUTE = {
-    "cvl_wgrad_defer", "cvl_wgrad_flush", "cvl_probe_begin", "cvl_probe_end",
+    "cvl_wgrad_defer", "cvl_wgrad_flush", "cvl_probe_arm",
     "cvl_bn_acc_decode",          # the harness's own reads of BN accumulator buffers
 }
 CK_NAMES = {0: "none", 1: "BASE", 2: "BASE_SPLITK", 3: "L64", 4: "L128", 5: "L256", 6: "X256", 7: "X32",

@@ -307,3 +307,42 @@ def test_l_register_epilogue_matches_c_image(dispatch, mode, B, H, C, N, stats):
     torch.testing.assert_close(res[1][0].to(F64), ref, rtol=1e-2, atol=2e-2)
     if stats:
         torch.testing.assert_close(res[0][1], res[1][1], rtol=2e-5, atol=1e-3)
+
+
+def test_probe_arm_times_one_tower_launch(dispatch):
+    """cvl_probe_arm (bench.py's in-step roofline timing): the armed X32 launch times itself from
+    inside (slot[2] = 1 launch, slot[1] > 0 ticks, the workgroup counter slot[3] back at 0, the
+    output bit-identical to an unarmed launch); the arm is consumed by the next conv_igemm call, so
+    a launch on another kernel leaves the slot untouched and the X32 launch after it is not timed."""
+    from cvlite import ops_nn as nn
+    dispatch("l_min_tiles=1", "l256_min_tiles=1", "no_h")
+    B, H, C, N = 2, 64, 256, 256
+    g = torch.Generator(device="cuda").manual_seed(77)
+    x = rnd((B, H, H, C), 1.0, g)
+    w = rnd((3, 3, C, N), (9 * C) ** -0.5, g).to(F64)
+    wf, _ = packs(w)
+    d = nn.make_desc(nn.FWD, B, C, 3, 3, 1, 1, 1, N, N, N, [nn.seg(H, H, H, H, wf, None)])
+    slot = torch.zeros(4, dtype=torch.int64, device="cuda")
+    ref = torch.empty((B, H, H, N), dtype=BF, device="cuda")
+    nn.conv_igemm(d, x, ref)
+    out = torch.empty_like(ref)
+    for _ in range(3):
+        nn.probe_arm(slot)
+        nn.conv_igemm(d, x, out)
+        assert last_kernel()[0] == 7
+    torch.cuda.synchronize()
+    assert torch.equal(out.view(torch.int16), ref.view(torch.int16))
+    s = slot.cpu().tolist()
+    assert s[2] == 3 and s[1] > 0 and s[3] == 0, s
+    sec, n = nn.probe_seconds(slot)
+    assert n == 3 and 0 < sec < 0.05
+    # a 1x1 launch (not X32) consumes the arm and leaves the slot as it was
+    w1 = rnd((1, 1, C, N), C ** -0.5, g).to(F64)
+    wf1, _ = packs(w1)
+    d1 = nn.make_desc(nn.FWD, B, C, 1, 1, 1, 0, 0, N, N, N, [nn.seg(H, H, H, H, wf1, None)])
+    nn.probe_arm(slot)
+    nn.conv_igemm(d1, x, out)
+    assert last_kernel()[0] != 7
+    nn.conv_igemm(d, x, out)
+    torch.cuda.synchronize()
+    assert slot.cpu().tolist() == s
