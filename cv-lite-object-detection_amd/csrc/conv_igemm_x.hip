@@ -314,7 +314,9 @@ int cvl_conv_igemm_x(const cvl_conv_desc* d, const ConvArgs& a, hipStream_t s) {
                   a.dst_coff % 8 == 0 && !cvl_dispatch_flag("x_no_sw");
 #ifdef CVL_MEASURE
   if (am.dbg) {
-    if (dg) hipLaunchKernelGGL((conv_igemm_x32_kernel<true, true>), grid, dim3(NT), 0, s, am);
+    if (dg && sw) hipLaunchKernelGGL((conv_igemm_x32_kernel<true, true, true>), grid, dim3(NT), 0, s, am);
+    else if (sw) hipLaunchKernelGGL((conv_igemm_x32_kernel<false, true, true>), grid, dim3(NT), 0, s, am);
+    else if (dg) hipLaunchKernelGGL((conv_igemm_x32_kernel<true, true>), grid, dim3(NT), 0, s, am);
     else hipLaunchKernelGGL((conv_igemm_x32_kernel<false, true>), grid, dim3(NT), 0, s, am);
   } else
 #endif
