@@ -25,7 +25,7 @@ constexpr int NT = 256;
 
 template <int BK>
 __device__ __forceinline__ int swz(int r) {
-  return BK == 64 ? ((r >> 1) & 7) : ((r >> 2) & 3);
+  return BK == 128 ? (r & 15) : (BK == 64 ? ((r >> 1) & 7) : ((r >> 2) & 3));
 }
 
 __device__ __forceinline__ s16x8 relu_bf16x8(s16x8 v) {
@@ -335,9 +335,21 @@ __global__ void __launch_bounds__(NT) conv_splitk_finish(ConvArgs a, int rows_pe
       float v[8];
 #pragma unroll
       for (int u = 0; u < 8; ++u) v[u] = bb[u];
-      for (int z = 0; z < a.splits; ++z) {
-        const f32x4* p = reinterpret_cast<const f32x4*>(a.slab + ((size_t)z * a.m_total + ml) * a.Npad + c0);
-        const f32x4 x0 = p[0], x1 = p[1];
+      const f32x4* p = reinterpret_cast<const f32x4*>(a.slab + (size_t)ml * a.Npad + c0);
+      const size_t zs = (size_t)a.m_total * a.Npad / 4;     // one split's slab, in float4s
+      int z = 0;
+      for (; z + 4 <= a.splits; z += 4) {                  // 8 loads in flight, then the adds in split order
+        f32x4 x[4][2];
+#pragma unroll
+        for (int t = 0; t < 4; ++t) { x[t][0] = p[(z + t) * zs]; x[t][1] = p[(z + t) * zs + 1]; }
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+          v[0] += x[t][0][0]; v[1] += x[t][0][1]; v[2] += x[t][0][2]; v[3] += x[t][0][3];
+          v[4] += x[t][1][0]; v[5] += x[t][1][1]; v[6] += x[t][1][2]; v[7] += x[t][1][3];
+        }
+      }
+      for (; z < a.splits; ++z) {
+        const f32x4 x0 = p[z * zs], x1 = p[z * zs + 1];
         v[0] += x0[0]; v[1] += x0[1]; v[2] += x0[2]; v[3] += x0[3];
         v[4] += x1[0]; v[5] += x1[1]; v[6] += x1[2]; v[7] += x1[3];
       }
@@ -388,13 +400,14 @@ __global__ void __launch_bounds__(NT) conv_splitk_finish(ConvArgs a, int rows_pe
   }
 }
 
-// launch geometry of the finish: (row parts, images, 64-channel chunks), ~512 workgroups, >= 64 rows each
+// launch geometry of the finish: (row parts, images, 64-channel chunks), ~512 workgroups, >= 16 rows each
+// (the 8x8 maps of P6 at bs 16 gave 64 workgroups of 64 rows with a 64-row floor: 15 us)
 static int splitk_finish_launch(const ConvArgs& a, hipStream_t s) {
   const ConvSeg& S = a.seg[0];
   const int HW = S.Hr * S.Wr;
   const int nch = (a.n_store + 63) / 64;
   int parts = 512 / (a.B * nch);
-  if (parts > HW / 64) parts = HW / 64;
+  if (parts > HW / 16) parts = HW / 16;
   if (parts < 1) parts = 1;
   const int rpb = (HW + parts - 1) / parts;
   hipLaunchKernelGGL(conv_splitk_finish, dim3((HW + rpb - 1) / rpb, a.B, nch), dim3(NT), 0, s, a, rpb);
@@ -436,6 +449,9 @@ int launch_bn_bk(const ConvArgs& a0, bool dgrad, hipStream_t s) {
 
 template <int BN>
 int launch_bn(const ConvArgs& a, bool dgrad, hipStream_t s) {
+  // narrow outputs (the FCOS / RetinaNet heads, N <= 64): 128-deep K steps -- twice the bytes per
+  // register-staged load round in flight (these launches are bound by the load latency, not MFMA)
+  if (BN <= 64 && a.Cin % 128 == 0 && cvl_dispatch_int("base_bk128", 1)) return launch_bn_bk<BN, 128>(a, dgrad, s);
   if (a.Cin % 64 == 0) return launch_bn_bk<BN, 64>(a, dgrad, s);
   return launch_bn_bk<BN, 32>(a, dgrad, s);
 }

@@ -10,7 +10,8 @@ import torch  # noqa: E402
 from cvlite import ops_nn as nn, _lib  # noqa: E402
 
 CASES = [(16, 128, 64, 256, 1, True), (16, 128, 256, 64, 1, True), (16, 64, 128, 512, 1, True),
-         (16, 32, 256, 1024, 1, True), (16, 32, 1024, 256, 1, True), (16, 16, 2048, 512, 1, True)]
+         (16, 32, 256, 1024, 1, True), (16, 32, 1024, 256, 1, True), (16, 16, 2048, 512, 1, True),
+         (16, 16, 512, 2048, 1, True), (16, 16, 2048, 256, 1, False)]
 
 
 def timed(fn, iters=20):
