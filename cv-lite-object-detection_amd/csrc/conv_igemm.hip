@@ -489,6 +489,75 @@ static bool s2dgrad_transform(const cvl_conv_desc* d, cvl_conv_desc* out, int* u
   return true;
 }
 
+// 3x3 / stride-2 data gradient with zero leading pads on an even map (TF 'same': the FPN's P6 / P7
+// convs, fcos.py:66-72; conv2d_backprop_input of a stride-2 kernel) as ONE 4-segment forward launch
+// over the dY map.  Input pixel (2k + py, 2k' + px) receives dY[k - 1 + r'][k' - 1 + s'] through
+// the 2x2 sub-kernel of its parity class: tap r' = 1 is r = 0 (py even) / r = 1 (odd), r' = 0 is
+// r = 2 (even) / nothing (odd) -- the same along x.  The four sub-kernels are gathered from the
+// dgrad pack into the workspace (missing taps zero) and the results scatter by dst_up = 2 at offset
+// py * W + px.  K = 4 * Cout instead of the 9 * Cout of the direct form, most of whose taps meet dY
+// rows that do not exist at the pixel's parity (c6 dgrad 256 -> 2048 @ 16^2: 82 us).
+static int grid_for_n(long n) {
+  const long b = (n + NT - 1) / NT;
+  return (int)(b > 4096 ? 4096 : (b < 1 ? 1 : b));
+}
+
+static bool s2dgrad3_ok(const cvl_conv_desc* d) {
+  if (!d || d->mode != CVL_CONV_DGRAD || d->KH != 3 || d->KW != 3 || d->stride != 2 || d->pad_t || d->pad_l ||
+      d->nseg != 1 || d->relu_in || d->prec != CVL_PREC_BF16 || d->Cin % 32 || d->Npad % 32 ||
+      cvl_dispatch_flag("no_s2dg3"))
+    return false;
+  const cvl_conv_seg& q = d->seg[0];
+  // small maps (P7's 8x8 at bs 16: 1024 rows) keep the direct form, whose split-K fills the GPU
+  // (the 4-segment launch has no split-K: 16 workgroups, 22 -> 37 us)
+  return q.Hr == 2 * q.Hs && q.Wr == 2 * q.Ws && q.w &&
+         (long)d->B * q.Hr * q.Wr >= cvl_dispatch_int("s2dg3_min_rows", 4096);
+}
+
+static size_t s2dgrad3_pack_bytes(const cvl_conv_desc* d) {
+  return ((size_t)4 * d->Npad * 4 * d->Cin * sizeof(cvl_bf16) + 255) / 256 * 256;
+}
+
+// sub[cls][n][t' = 2 r' + s'][c] from wd[n][(3 r + s) * Cin + c], 16-B chunks
+__global__ void s2dgrad3_pack_kernel(const cvl_bf16* __restrict__ wd, cvl_bf16* __restrict__ sub, int Npad, int Cin) {
+  const int c8n = Cin / 8;
+  const long total = 16L * Npad * c8n;
+  for (long i = blockIdx.x * (long)NT + threadIdx.x; i < total; i += (long)gridDim.x * NT) {
+    const int c8 = (int)(i % c8n);
+    const long r1 = i / c8n;
+    const int t = (int)(r1 & 3);
+    const long r2 = r1 >> 2;
+    const int n = (int)(r2 % Npad), cls = (int)(r2 / Npad);
+    const int py = cls >> 1, px = cls & 1, rp = t >> 1, sp = t & 1;
+    const int r = py ? (rp ? 1 : -1) : (rp ? 0 : 2);
+    const int sx = px ? (sp ? 1 : -1) : (sp ? 0 : 2);
+    s16x8 v = s16x8{0, 0, 0, 0, 0, 0, 0, 0};
+    if (r >= 0 && sx >= 0) v = *reinterpret_cast<const s16x8*>(wd + (long)n * 9 * Cin + (r * 3 + sx) * Cin + c8 * 8);
+    *reinterpret_cast<s16x8*>(sub + i * 8) = v;
+  }
+}
+
+// the 4-segment forward descriptor over the packs at `sub`
+static cvl_conv_desc s2dgrad3_desc(const cvl_conv_desc* d, const cvl_bf16* sub) {
+  cvl_conv_desc dd = *d;
+  const cvl_conv_seg q = d->seg[0];
+  dd.mode = CVL_CONV_FWD;
+  dd.KH = dd.KW = 2;
+  dd.stride = 1;
+  dd.pad_t = dd.pad_l = 1;
+  dd.nseg = 4;
+  for (int cls = 0; cls < 4; ++cls) {
+    cvl_conv_seg& g = dd.seg[cls];
+    g = q;
+    g.Hr = q.Hs;
+    g.Wr = q.Ws;
+    g.w = sub + (size_t)cls * d->Npad * 4 * d->Cin;
+    g.bias = nullptr;
+    g.dst_base = q.dst_base + (long)(cls >> 1) * q.Wr + (cls & 1);
+  }
+  return dd;
+}
+
 __global__ void zero_gaps_kernel(void* dst, int is_f32, long dst_base, long dst_img, int ld, int coff, int n,
                                  int B, int H, int W, int s) {
   const long rows = (long)B * H * W;
@@ -536,6 +605,10 @@ int cvl_conv_f32(const cvl_conv_desc* d, const void* src, void* dst, acc_u64* bn
 
 extern "C" size_t cvl_conv_igemm_workspace_size(const cvl_conv_desc* d) {
   if (d && d->prec == CVL_PREC_F32) return 16;
+  if (s2dgrad3_ok(d)) {            // the sub-kernel packs, then the 4-segment launch's own needs
+    const cvl_conv_desc dd = s2dgrad3_desc(d, reinterpret_cast<const cvl_bf16*>(16));
+    return s2dgrad3_pack_bytes(d) + cvl_conv_igemm_workspace_size(&dd);
+  }
   cvl_conv_desc dd;
   int up = 1, upw = 0;
   if (s2dgrad_transform(d, &dd, &up, &upw)) d = &dd;
@@ -562,7 +635,23 @@ extern "C" int cvl_conv_igemm(const cvl_conv_desc* d, const void* src, void* dst
   CVL_CHECK_ARG(d->prec == CVL_PREC_BF16);
   cvl_conv_desc dd;
   int up = 1, upw = 0;
-  if (s2dgrad_transform(d, &dd, &up, &upw)) {
+  if (s2dgrad3_ok(d) && workspace && workspace_bytes >= s2dgrad3_pack_bytes(d)) {
+    CVL_CHECK_ARG(src && dst && !bn_stats);
+    CVL_CHECK_ARG(d->dst_f32 || (d->ld_dst % 8 == 0 && d->dst_coff % 8 == 0 && d->n_store % 8 == 0));
+    cvl_bf16* sub = reinterpret_cast<cvl_bf16*>(workspace);
+    const long total = 16L * d->Npad * (d->Cin / 8);
+    hipLaunchKernelGGL(s2dgrad3_pack_kernel, dim3(grid_for_n(total)), dim3(NT), 0, s,
+                       reinterpret_cast<const cvl_bf16*>(d->seg[0].w), sub, d->Npad, d->Cin);
+    const int pst = cvl_launch_status();
+    if (pst) return pst;
+    const size_t pk = s2dgrad3_pack_bytes(d);
+    up = 2;
+    upw = d->seg[0].Wr;
+    dd = s2dgrad3_desc(d, sub);
+    d = &dd;
+    workspace = reinterpret_cast<char*>(workspace) + pk;
+    workspace_bytes -= pk;
+  } else if (s2dgrad_transform(d, &dd, &up, &upw)) {
     CVL_CHECK_ARG(src && dst && !bn_stats);
     CVL_CHECK_ARG(d->dst_f32 || (d->ld_dst % 8 == 0 && d->dst_coff % 8 == 0 && d->n_store % 8 == 0));
     if (d->beta == 0.f) {

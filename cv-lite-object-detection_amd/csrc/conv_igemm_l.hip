@@ -289,6 +289,17 @@ int cvl_conv_igemm_l(const cvl_conv_desc* d, int dst_up, int dst_w, const void* 
   // (conv_igemm_h.hip), whose A traffic is one halo per channel block instead of nine im2col tiles.
   // Not where the 256 x 128 tiles fill the chip: there the L kernel reads each A tile once for 128
   // columns (128 -> 128 @ 64^2, bs 16: L 33 / 47 us fwd / dgrad vs H64 41 / 52 us)
+  // 32-channel sources into 256-wide outputs (the FCOS heads' data gradient, K = 9 x 32): the X32
+  // ring kernel reads 64-B rows, i.e. one 32-channel block per K-tile (head dgrad 44.2 -> 30.7 us
+  // per head vs the H64 halo kernel; step +0.25 %)
+  if (!l_cin && d->Cin == 32 && bn == 256 && !bsum && !bn_stats && cvl_dispatch_int("x_cin32", 1)) {
+    ConvArgs ax = a;
+    ax.src = reinterpret_cast<const cvl_bf16*>(src);
+    ax.dst = dst;
+    ax.stats = nullptr;
+    const int xst = cvl_conv_igemm_x(d, ax, s);
+    if (xst >= 0) return xst;
+  }
   const bool h_width = use_bn == 64 || to64 || !l_cin || cvl_tune_flag("CVL_CONV_H_ANY_N");
   if (h_width && use_bn != 256 && (!bsum || ((a.seg[0].Hr * a.seg[0].Wr) % BM == 0 && !bn_stats))) {
     ConvArgs ah = a;

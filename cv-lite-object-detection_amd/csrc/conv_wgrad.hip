@@ -64,9 +64,15 @@ __device__ __forceinline__ void cursor_seek(const ConvSeg& S, RowCursor& c, int 
 __device__ __forceinline__ void cursor_advance(const ConvSeg& S, RowCursor& c, int step) {
   c.ml += step;
   c.ox += step;
-  while (c.ox >= S.Wr) {
-    c.ox -= S.Wr;
-    if (++c.oy >= S.Hr) { c.oy = 0; ++c.img; }
+  if (c.ox >= S.Wr) {            // (a step spans many rows of a small map: no per-row loop)
+    const int q = c.ox / S.Wr;
+    c.ox -= q * S.Wr;
+    c.oy += q;
+    if (c.oy >= S.Hr) {
+      const int q2 = c.oy / S.Hr;
+      c.oy -= q2 * S.Hr;
+      c.img += q2;
+    }
   }
 }
 

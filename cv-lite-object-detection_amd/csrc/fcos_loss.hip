@@ -23,6 +23,8 @@
 namespace {
 
 constexpr int kThreads = 256;
+typedef short s16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 struct LossArgs {
   const float* reg;
@@ -71,100 +73,197 @@ __device__ __forceinline__ float focal_term(float y, float x, float alpha, float
   return wpos * nlp + wneg * nlq;
 }
 
-__global__ void __launch_bounds__(kThreads) fcos_loss_kernel(LossArgs a) {
-  const int b = blockIdx.y;
-  const int p = blockIdx.x * kThreads + threadIdx.x;
-  float s_cls = 0.f, s_reg = 0.f, s_cen = 0.f;
+// One cell's loss terms and gradients: t(i) targets[i], xc(c) class logit c, xr(j) box / centerness
+// prediction j; putc(c, g) / putcen(g) / putr(j, g) receive the SCALED gradients (class c, the
+// centerness column of the class rows, box j < 5).  Both kernels below run exactly this code.
+template <class TF, class XCF, class XRF, class PC, class PCEN, class PR>
+__device__ __forceinline__ void cell_loss(const LossArgs& a, TF t, XCF xc, XRF xr, PC putc, PCEN putcen, PR putr,
+                                          float& s_cls, float& s_reg, float& s_cen) {
   const int kind = a.reg_type & 3;
   const bool focal_cen = a.reg_type & 4, sig_reg = a.reg_type & 8, cen_in_cls = a.reg_type & 16;
   const int cc = (a.C + 7) / 8 * 8;                // centerness column of the class rows (CEN_IN_CLS)
-  if (p < a.P) {
-    const size_t cell = (size_t)b * a.P + p;
-    const float* t = a.tgt + cell * (5 + a.C);
-    const float* xr = a.reg + cell * a.ld_reg;
-    const float* xc = a.cls + cell * a.ld_cls;
-    float tmax = 0.f;
-    for (int c = 0; c < a.C; ++c) {
-      const float y = t[5 + c];
-      tmax = fmaxf(tmax, y);
-      float g;
-      s_cls += focal_term(y, xc[c], a.alpha, a.gamma, &g);
-      if (a.dcls) store_g(a.dcls, cell * a.ld_dcls + c, g * a.grad_scale, a.dcls_bf16);
+  float tmax = 0.f;
+  for (int c = 0; c < a.C; ++c) {
+    const float y = t(5 + c);
+    tmax = fmaxf(tmax, y);
+    float g;
+    s_cls += focal_term(y, xc(c), a.alpha, a.gamma, &g);
+    putc(c, g * a.grad_scale);
+  }
+  const float mask = (a.reg_type & 32) ? t(5) : (tmax >= 1.0f ? 1.0f : 0.0f);
+  float g[5] = {0.f, 0.f, 0.f, 0.f, 0.f};
+  // centerness: smooth-L1 on sigmoid(logit) (fcos.py:483-486) or focal (centre variants), all cells
+  {
+    const float x = cen_in_cls ? xc(cc) : xr(4);
+    float gc;
+    if (focal_cen) {
+      s_cen += focal_term(t(4), x, a.alpha, a.gamma, &gc);
+    } else {
+      const float sg = 1.0f / (1.0f + expf(-x));
+      float gd;
+      s_cen += sl1(t(4) - sg, a.delta, &gd);
+      gc = gd * sg * (1.0f - sg);
     }
-    if (a.dcls)
-      for (int c = a.C; c < a.ld_dcls; ++c) store_g(a.dcls, cell * a.ld_dcls + c, 0.f, a.dcls_bf16);
-    const float mask = (a.reg_type & 32) ? t[5] : (tmax >= 1.0f ? 1.0f : 0.0f);
-    float g[5] = {0.f, 0.f, 0.f, 0.f, 0.f};
-    // centerness: smooth-L1 on sigmoid(logit) (fcos.py:483-486) or focal (centre variants), all cells
-    {
-      const float x = cen_in_cls ? xc[cc] : xr[4];
-      float gc;
-      if (focal_cen) {
-        s_cen += focal_term(t[4], x, a.alpha, a.gamma, &gc);
-      } else {
-        const float sg = 1.0f / (1.0f + expf(-x));
-        float gd;
-        s_cen += sl1(t[4] - sg, a.delta, &gd);
-        gc = gd * sg * (1.0f - sg);
-      }
-      if (cen_in_cls) {
-        if (a.dcls) store_g(a.dcls, cell * a.ld_dcls + cc, gc * a.grad_scale, a.dcls_bf16);
-      } else {
-        g[4] = gc;
-      }
-    }
-    if (kind == 0) {
-      for (int j = 0; j < 4; ++j) {
-        float gd;
-        if (sig_reg) {                             // fcos_center_v1.py:115: reg = sigmoid(conv)
-          const float sg = 1.0f / (1.0f + expf(-xr[j]));
-          const float l = sl1(t[j] - sg, a.delta, &gd);
-          s_reg += mask * l;
-          g[j] = mask * gd * sg * (1.0f - sg);
-        } else {
-          const float l = sl1(t[j] - xr[j], a.delta, &gd);
-          s_reg += mask * l;
-          g[j] = mask * gd;
-        }
-      }
-    } else if (mask != 0.f) {
-      // IoU of ltrb boxes about the same grid point (grid offsets cancel)
-      const float t0 = t[0], t1 = t[1], t2 = t[2], t3 = t[3];
-      const float p0 = xr[0], p1 = xr[1], p2 = xr[2], p3 = xr[3];
-      const float th = t0 + t1, tw = t2 + t3, ph = p0 + p1, pw = p2 + p3;
-      const float ihr = fminf(t1, p1) + fminf(t0, p0);
-      const float iwr = fminf(t3, p3) + fminf(t2, p2);
-      const float ih = fmaxf(ihr, 0.f), iw = fmaxf(iwr, 0.f);
-      const float I = ih * iw;
-      const float Ue = th * tw + ph * pw - I + 1.0e-12f;
-      const float iou = I / Ue;
-      s_reg += -logf(iou + 1.0e-12f) * mask;
-      const float dL = -mask / (iou + 1.0e-12f);
-      const float dI = (Ue + I) / (Ue * Ue);            // d iou / d I (U depends on -I)
-      const float dph = -I * pw / (Ue * Ue), dpw = -I * ph / (Ue * Ue);
-      const float gih = ihr > 0.f ? dI * iw : 0.f;
-      const float giw = iwr > 0.f ? dI * ih : 0.f;
-      g[0] = dL * ((p0 < t0 ? gih : 0.f) + dph);
-      g[1] = dL * ((p1 < t1 ? gih : 0.f) + dph);
-      g[2] = dL * ((p2 < t2 ? giw : 0.f) + dpw);
-      g[3] = dL * ((p3 < t3 ? giw : 0.f) + dpw);
-    }
-    if (a.dreg) {
-      for (int j = 0; j < 5; ++j) store_g(a.dreg, cell * a.ld_dreg + j, g[j] * a.grad_scale, a.dreg_bf16);
-      for (int j = 5; j < a.ld_dreg; ++j) store_g(a.dreg, cell * a.ld_dreg + j, 0.f, a.dreg_bf16);
+    if (cen_in_cls) {
+      putcen(gc * a.grad_scale);
+    } else {
+      g[4] = gc;
     }
   }
-  // deterministic block reduction in float64
-  __shared__ double red[3][kThreads / 64];
+  if (kind == 0) {
+    for (int j = 0; j < 4; ++j) {
+      float gd;
+      if (sig_reg) {                             // fcos_center_v1.py:115: reg = sigmoid(conv)
+        const float sg = 1.0f / (1.0f + expf(-xr(j)));
+        const float l = sl1(t(j) - sg, a.delta, &gd);
+        s_reg += mask * l;
+        g[j] = mask * gd * sg * (1.0f - sg);
+      } else {
+        const float l = sl1(t(j) - xr(j), a.delta, &gd);
+        s_reg += mask * l;
+        g[j] = mask * gd;
+      }
+    }
+  } else if (mask != 0.f) {
+    // IoU of ltrb boxes about the same grid point (grid offsets cancel)
+    const float t0 = t(0), t1 = t(1), t2 = t(2), t3 = t(3);
+    const float p0 = xr(0), p1 = xr(1), p2 = xr(2), p3 = xr(3);
+    const float th = t0 + t1, tw = t2 + t3, ph = p0 + p1, pw = p2 + p3;
+    const float ihr = fminf(t1, p1) + fminf(t0, p0);
+    const float iwr = fminf(t3, p3) + fminf(t2, p2);
+    const float ih = fmaxf(ihr, 0.f), iw = fmaxf(iwr, 0.f);
+    const float I = ih * iw;
+    const float Ue = th * tw + ph * pw - I + 1.0e-12f;
+    const float iou = I / Ue;
+    s_reg += -logf(iou + 1.0e-12f) * mask;
+    const float dL = -mask / (iou + 1.0e-12f);
+    const float dI = (Ue + I) / (Ue * Ue);            // d iou / d I (U depends on -I)
+    const float dph = -I * pw / (Ue * Ue), dpw = -I * ph / (Ue * Ue);
+    const float gih = ihr > 0.f ? dI * iw : 0.f;
+    const float giw = iwr > 0.f ? dI * ih : 0.f;
+    g[0] = dL * ((p0 < t0 ? gih : 0.f) + dph);
+    g[1] = dL * ((p1 < t1 ? gih : 0.f) + dph);
+    g[2] = dL * ((p2 < t2 ? giw : 0.f) + dpw);
+    g[3] = dL * ((p3 < t3 ? giw : 0.f) + dpw);
+  }
+  for (int j = 0; j < 5; ++j) putr(j, g[j] * a.grad_scale);
+}
+
+// deterministic block reduction of the three sums in float64 -> partial[b][tile][3]
+template <int NTH>
+__device__ __forceinline__ void block_partials(const LossArgs& a, float s_cls, float s_reg, float s_cen) {
+  __shared__ double red[3][NTH / 64];
   double v0 = warp_sum_d((double)s_cls), v1 = warp_sum_d((double)s_reg), v2 = warp_sum_d((double)s_cen);
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
   if (lane == 0) { red[0][w] = v0; red[1][w] = v1; red[2][w] = v2; }
   __syncthreads();
   if (threadIdx.x < 3) {
     double s = 0.0;
-    for (int k = 0; k < kThreads / 64; ++k) s += red[threadIdx.x][k];
-    a.partial[((size_t)b * a.tiles + blockIdx.x) * 3 + threadIdx.x] = s;
+    for (int k = 0; k < NTH / 64; ++k) s += red[threadIdx.x][k];
+    a.partial[((size_t)blockIdx.y * a.tiles + blockIdx.x) * 3 + threadIdx.x] = s;
   }
+}
+
+// Row-pointer form (any layout): a thread walks its cell's rows in global memory.
+__global__ void __launch_bounds__(kThreads) fcos_loss_kernel(LossArgs a) {
+  const int b = blockIdx.y;
+  const int p = blockIdx.x * kThreads + threadIdx.x;
+  float s_cls = 0.f, s_reg = 0.f, s_cen = 0.f;
+  const int cc = (a.C + 7) / 8 * 8;
+  if (p < a.P) {
+    const size_t cell = (size_t)b * a.P + p;
+    const float* t = a.tgt + cell * (5 + a.C);
+    const float* xr = a.reg + cell * a.ld_reg;
+    const float* xc = a.cls + cell * a.ld_cls;
+    cell_loss(
+        a, [&](int i) { return t[i]; }, [&](int c) { return xc[c]; }, [&](int j) { return xr[j]; },
+        [&](int c, float v) {
+          if (a.dcls) store_g(a.dcls, cell * a.ld_dcls + c, v, a.dcls_bf16);
+        },
+        [&](float v) {
+          if (a.dcls) {
+            for (int c = a.C; c < a.ld_dcls; ++c) store_g(a.dcls, cell * a.ld_dcls + c, 0.f, a.dcls_bf16);
+            store_g(a.dcls, cell * a.ld_dcls + cc, v, a.dcls_bf16);
+          }
+        },
+        [&](int j, float v) {
+          if (a.dreg) store_g(a.dreg, cell * a.ld_dreg + j, v, a.dreg_bf16);
+        },
+        s_cls, s_reg, s_cen);
+    if (a.dcls && !(a.reg_type & 16))
+      for (int c = a.C; c < a.ld_dcls; ++c) store_g(a.dcls, cell * a.ld_dcls + c, 0.f, a.dcls_bf16);
+    if (a.dreg)
+      for (int j = 5; j < a.ld_dreg; ++j) store_g(a.dreg, cell * a.ld_dreg + j, 0.f, a.dreg_bf16);
+  }
+  block_partials<kThreads>(a, s_cls, s_reg, s_cen);
+}
+
+// LDS-staged form: the block's NTH cells' target, class and box rows are loaded cooperatively (every
+// global load coalesced and issued before any math), each thread runs its cell from LDS (row pitch R
+// odd: conflict-free) writing the scaled gradients back in place, and the gradient rows leave as
+// 16-byte stores of whole rows (padding columns zero).  Same cell_loss, same per-thread and block
+// sum order as fcos_loss_kernel at NTH = 256: bit-identical results.
+template <int NTH>
+__global__ void __launch_bounds__(NTH) fcos_loss_lds_kernel(LossArgs a, int R) {
+  extern __shared__ float rows[];
+  const int b = blockIdx.y, p0 = blockIdx.x * NTH;
+  const int ncell = min(NTH, a.P - p0);
+  const bool cen_in_cls = a.reg_type & 16;
+  const int cc = (a.C + 7) / 8 * 8;
+  const int T5 = 5 + a.C, ncc = cen_in_cls ? cc + 1 : a.C, nrg = cen_in_cls ? 4 : 5;
+  const int OC = T5, OR = T5 + ncc;                   // row: targets | class logits | box (5 slots)
+  const size_t cell0 = (size_t)b * a.P + p0;
+  {
+    const float* tg = a.tgt + cell0 * T5;
+    for (int i = threadIdx.x; i < ncell * T5; i += NTH) {
+      const int r = i / T5;
+      rows[r * R + (i - r * T5)] = tg[i];
+    }
+    const float* cg = a.cls + cell0 * a.ld_cls;
+    for (int i = threadIdx.x; i < ncell * ncc; i += NTH) {
+      const int r = i / ncc, c = i - r * ncc;
+      rows[r * R + OC + c] = cg[(size_t)r * a.ld_cls + c];
+    }
+    const float* rg = a.reg + cell0 * a.ld_reg;
+    for (int i = threadIdx.x; i < ncell * nrg; i += NTH) {
+      const int r = i / nrg, j = i - r * nrg;
+      rows[r * R + OR + j] = rg[(size_t)r * a.ld_reg + j];
+    }
+  }
+  __syncthreads();
+  float s_cls = 0.f, s_reg = 0.f, s_cen = 0.f;
+  if ((int)threadIdx.x < ncell) {
+    float* row = rows + threadIdx.x * R;
+    cell_loss(
+        a, [&](int i) { return row[i]; }, [&](int c) { return row[OC + c]; }, [&](int j) { return row[OR + j]; },
+        [&](int c, float v) { row[OC + c] = v; }, [&](float v) { row[OC + cc] = v; },
+        [&](int j, float v) { row[OR + j] = v; }, s_cls, s_reg, s_cen);
+  }
+  __syncthreads();
+  // gradient rows: whole rows in 16-byte pieces (8 bf16 or 4 fp32 columns), padding columns zero
+  auto grad_rows = [&](void* dst, int ld, int is_bf16, int base, int ncol, int extra) {
+    const int w = is_bf16 ? 8 : 4, npc = ld / w;
+    for (int i = threadIdx.x; i < ncell * npc; i += NTH) {
+      const int r = i / npc, c0 = (i - r * npc) * w;
+      float v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int c = c0 + u;
+        v[u] = (u < w && (c < ncol || c == extra)) ? rows[r * R + base + c] : 0.f;
+      }
+      if (is_bf16) {
+        s16x8 o;
+#pragma unroll
+        for (int u = 0; u < 8; ++u) o[u] = (short)f32_to_bf16(v[u]);
+        *reinterpret_cast<s16x8*>(reinterpret_cast<cvl_bf16*>(dst) + (cell0 + r) * ld + c0) = o;
+      } else {
+        *reinterpret_cast<f32x4*>(reinterpret_cast<float*>(dst) + (cell0 + r) * ld + c0) = f32x4{v[0], v[1], v[2], v[3]};
+      }
+    }
+  };
+  if (a.dcls) grad_rows(a.dcls, a.ld_dcls, a.dcls_bf16, OC, a.C, cen_in_cls ? cc : -1);
+  if (a.dreg) grad_rows(a.dreg, a.ld_dreg, a.dreg_bf16, OR, 5, -1);
+  block_partials<NTH>(a, s_cls, s_reg, s_cen);
 }
 
 __global__ void fcos_loss_finalize(const double* partial, float* losses, int tiles) {
@@ -180,7 +279,7 @@ __global__ void fcos_loss_finalize(const double* partial, float* losses, int til
 }  // namespace
 
 extern "C" size_t cvl_fcos_loss_workspace_size(int B, int P) {
-  const size_t tiles = (size_t)(P + kThreads - 1) / kThreads;
+  const size_t tiles = (size_t)(P + 63) / 64;        // per-tile partials of the smallest (64-cell) tiles
   return (size_t)B * tiles * 3 * sizeof(double);
 }
 
@@ -207,8 +306,22 @@ extern "C" int cvl_fcos_loss_ex(const float* reg_pred, int ld_reg, const float* 
   a.dreg_bf16 = dreg_dtype; a.dcls_bf16 = dcls_dtype;
   a.P = P; a.C = num_classes; a.reg_type = reg_type; a.grad_scale = grad_scale;
   a.alpha = alpha; a.gamma = gamma; a.delta = delta;
-  a.tiles = (P + kThreads - 1) / kThreads;
-  hipLaunchKernelGGL(fcos_loss_kernel, dim3(a.tiles, B), dim3(kThreads), 0, (hipStream_t)stream, a);
+  // the LDS-staged form when its rows fit (pitch R floats, odd) and the gradient rows take 16-B stores
+  const int ncc = cen_in_cls ? (num_classes + 7) / 8 * 8 + 1 : num_classes;
+  const int R = (5 + num_classes + ncc + 5) | 1;
+  auto vec_ok = [](const void* p, int ld, int bf16) {
+    return !p || ((reinterpret_cast<uintptr_t>(p) & 15) == 0 && ld % (bf16 ? 8 : 4) == 0);
+  };
+  int nth = 0;
+  if (vec_ok(d_reg, ld_dreg, dreg_dtype) && vec_ok(d_cls, ld_dcls, dcls_dtype) && !cvl_dispatch_flag("loss_rows"))
+    for (int n = 256; n >= 64 && !nth; n /= 2)
+      if ((size_t)n * R * sizeof(float) <= 64 * 1024) nth = n;
+  a.tiles = (P + (nth ? nth : kThreads) - 1) / (nth ? nth : kThreads);
+  const size_t lds = (size_t)nth * R * sizeof(float);
+  if (nth == 256) hipLaunchKernelGGL((fcos_loss_lds_kernel<256>), dim3(a.tiles, B), dim3(256), lds, (hipStream_t)stream, a, R);
+  else if (nth == 128) hipLaunchKernelGGL((fcos_loss_lds_kernel<128>), dim3(a.tiles, B), dim3(128), lds, (hipStream_t)stream, a, R);
+  else if (nth == 64) hipLaunchKernelGGL((fcos_loss_lds_kernel<64>), dim3(a.tiles, B), dim3(64), lds, (hipStream_t)stream, a, R);
+  else hipLaunchKernelGGL(fcos_loss_kernel, dim3(a.tiles, B), dim3(kThreads), 0, (hipStream_t)stream, a);
   int st = cvl_launch_status();
   if (st) return st;
   hipLaunchKernelGGL(fcos_loss_finalize, dim3(B), dim3(64), 0, (hipStream_t)stream,

@@ -36,8 +36,14 @@ class FCOSNet(FPNDetector):
     def _heads_forward(self, towers, B, shapes, off, P):
         """Returns reg [B,P,8] fp32 (t,b,l,r,centerness), cls [B,P,ld] fp32."""
         dev = towers[0][0].device
-        cls_out = torch.zeros((B, P, self.cls_ld), dtype=torch.float32, device=dev)
-        reg_out = torch.zeros((B, P, self.reg_ld), dtype=torch.float32, device=dev)
+        # the trainer's persistent output pair (FCOSTrainer: allocated zeroed once; the heads write
+        # only their n_store columns, so the padding columns stay zero) -- else fresh zeroed buffers
+        buf = getattr(self, "head_out", None)
+        if buf is not None and tuple(buf[1].shape) == (B, P, self.cls_ld) and buf[1].device == dev:
+            reg_out, cls_out = buf
+        else:
+            cls_out = torch.zeros((B, P, self.cls_ld), dtype=torch.float32, device=dev)
+            reg_out = torch.zeros((B, P, self.reg_ld), dtype=torch.float32, device=dev)
         for heads, acts, out, ld in ((self.cls_heads, towers[0], cls_out, self.cls_ld),
                                      (self.reg_heads, towers[1], reg_out, self.reg_ld)):
             segs = [nn.seg(h, w, h, w, heads[l].wf, heads[l].bias_arg(), src_base=B * off[l], src_img=h * w,

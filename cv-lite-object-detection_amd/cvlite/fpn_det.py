@@ -274,8 +274,14 @@ class FPNDetector(object):
         paired = PAIR_TOWERS and (dAs[1].data_ptr() - dAs[0].data_ptr() == BP * FPN_C * dAs[0].element_size()
                   and dAs[0].is_contiguous() and dAs[1].is_contiguous())
         pair0 = pair_tower0_dgrad()
-        for t in range(2):
-            nn.relu_backward(dAs[t], towers[t][-1], dAs[t])         # the tower's final ReLU
+        # the towers' final ReLU: one launch over both halves when they are one buffer
+        y_top = s["tower_bufs"][-1]
+        if paired and towers[1][-1].data_ptr() - towers[0][-1].data_ptr() == BP * FPN_C * y_top.element_size():
+            dA_all = torch.as_strided(dAs[0], (2 * BP, FPN_C), (FPN_C, 1))
+            nn.relu_backward(dA_all, y_top, dA_all)
+        else:
+            for t in range(2):
+                nn.relu_backward(dAs[t], towers[t][-1], dAs[t])
         for i in range(3, -1, -1):
             if paired:      # both towers' weight gradients: ONE launch, 2 groups x 5 levels
                 d = self.cls_tower[i].fwd_desc(B, self._pair_segs(i, B, shapes, off, P, fwd=True), ld_dst=FPN_C)

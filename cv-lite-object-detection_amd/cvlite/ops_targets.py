@@ -73,14 +73,15 @@ def fcos_center_v1_assign(boxes, nbox, img_dim, pad_hw, num_classes, strides=FCO
 
 def fcos_loss(reg_pred, cls_pred, targets, num_classes, reg_type="l1", grad_scale=1.0,
               with_grad=True, grad_dtype=torch.float32, d_reg=None, d_cls=None, cen_type="l1",
-              reg_sigmoid=False, cen_in_cls=False, alpha=0.25, gamma=2.0, delta=1.0, float_mask=False):
+              reg_sigmoid=False, cen_in_cls=False, alpha=0.25, gamma=2.0, delta=1.0, float_mask=False,
+              losses=None):
     """Fused focal + smooth-L1/IoU + centerness forward and backward.
     reg_pred [B,P,ld_reg>=5] f32, cls_pred [B,P,ld_cls>=C] f32, targets [B,P,5+C] f32.
     Centre variants (fcos_center / fcos_center_v1): cen_type "focal", reg_sigmoid (v1's sigmoid
     reg head), cen_in_cls (centerness logit in class column round_up(C, 8)).
     alpha / gamma / delta: the focal_loss / smooth_l1_loss keywords (fcos.py:380, 443-444);
-    float_mask: the regression mask is targets[..., 5] itself (C = 1).
-    Returns (losses [B,3] f32 = (cls, reg, cen) per image, d_reg, d_cls)."""
+    float_mask: the regression mask is targets[..., 5] itself (C = 1).  losses: optional [B,3] f32
+    output buffer.  Returns (losses [B,3] f32 = (cls, reg, cen) per image, d_reg, d_cls)."""
     _lib.require_cuda(reg_pred, cls_pred, targets)
     B, P = int(targets.shape[0]), int(targets.shape[1])
     assert reg_pred.shape[:2] == (B, P) and cls_pred.shape[:2] == (B, P)
@@ -88,7 +89,9 @@ def fcos_loss(reg_pred, cls_pred, targets, num_classes, reg_type="l1", grad_scal
     rt |= (4 if cen_type.lower() == "focal" else 0) | (8 if reg_sigmoid else 0) | (16 if cen_in_cls else 0)
     rt |= 32 if float_mask else 0
     dev = targets.device
-    losses = torch.empty((B, 3), device=dev, dtype=torch.float32)
+    if losses is None:
+        losses = torch.empty((B, 3), device=dev, dtype=torch.float32)
+    assert losses.shape == (B, 3) and losses.dtype == torch.float32 and losses.is_contiguous()
     ws = torch.empty(int(_lib.load().cvl_fcos_loss_workspace_size(B, P)), device=dev, dtype=torch.uint8)
     if with_grad:
         if d_reg is None:

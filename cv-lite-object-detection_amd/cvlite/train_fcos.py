@@ -89,6 +89,11 @@ class FCOSTrainer(GraphStepper):
         self.d_reg = torch.zeros((B, self.P, 32), dtype=act, device=dev)
         self.d_cls = torch.zeros((B, self.P, net.cls_ld), dtype=act, device=dev)
         self.losses = torch.zeros((B, 3), dtype=torch.float32, device=dev)
+        # the heads' fp32 outputs, zeroed once (FCOSNet writes only the used columns; see
+        # FCOSNet._heads_forward) -- lent to the network for the step's forward only
+        self._head_out = ((torch.zeros((B, self.P, net.reg_ld), dtype=torch.float32, device=dev),
+                           torch.zeros((B, self.P, net.cls_ld), dtype=torch.float32, device=dev))
+                          if hasattr(net, "reg_ld") and not centre else None)
         if self.adam is not None:
             self.lr = self.adam.lr_dev
             self.lr.fill_(init_lr)
@@ -111,11 +116,14 @@ class FCOSTrainer(GraphStepper):
         else:
             tg, _ = ot.fcos_assign(self.boxes, self.nbox, self.img_dim, (self.H, self.W), self.C,
                                    out=self.targets, num_targets=self.ntgt)
-        reg, cls = self.net.forward(self.images)
+        self.net.head_out = self._head_out
+        try:
+            reg, cls = self.net.forward(self.images)
+        finally:
+            self.net.head_out = None
         self.outputs = (reg, cls)                 # head outputs of the last step (graph memory)
-        losses, _, _ = ot.fcos_loss(reg, cls, tg, self.C, reg_type=self.reg_type, grad_scale=1.0,
-                                    d_reg=self.d_reg, d_cls=self.d_cls, **self.loss_flags)
-        self.losses.copy_(losses)
+        ot.fcos_loss(reg, cls, tg, self.C, reg_type=self.reg_type, grad_scale=1.0, d_reg=self.d_reg,
+                     d_cls=self.d_cls, losses=self.losses, **self.loss_flags)
         self.net.backward(self.d_reg, self.d_cls, hook=hook)
 
     def _update(self):

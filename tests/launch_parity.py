@@ -1126,10 +1126,10 @@ PASSTHROUGH_TESTS = {
 
 def check_fcos_loss(lp, name, launch, reg_pred, cls_pred, targets, num_classes, reg_type="l1", grad_scale=1.0,
                     with_grad=True, grad_dtype=torch.float32, d_reg=None, d_cls=None, cen_type="l1",
-                    reg_sigmoid=False, cen_in_cls=False):
+                    reg_sigmoid=False, cen_in_cls=False, losses=None):
     out = launch(reg_pred, cls_pred, targets, num_classes, reg_type=reg_type, grad_scale=grad_scale,
                  with_grad=with_grad, grad_dtype=grad_dtype, d_reg=d_reg, d_cls=d_cls, cen_type=cen_type,
-                 reg_sigmoid=reg_sigmoid, cen_in_cls=cen_in_cls)
+                 reg_sigmoid=reg_sigmoid, cen_in_cls=cen_in_cls, losses=losses)
     losses, gr, gc = out
     if cen_type != "l1" or reg_sigmoid or cen_in_cls or not isinstance(reg_type, str):
         lp.add(name, "centre variant: test_gpu_fcos_center", "-", 0.0, 0.0)

@@ -579,3 +579,75 @@ def test_conv_wgrad_deferred_then_direct_writer():
     imm, dfr = run(False), run(True)
     assert kinds[0] == 11 and kinds[1] != 11, kinds        # split wgrad_x first, a non-split writer second
     assert torch.equal(imm, dfr)
+
+
+@pytest.mark.parametrize("case", [(16, 16, 2048, 256), (16, 8, 256, 256), (3, 12, 64, 96)])
+def test_s2_3x3_dgrad_parity_form(dispatch, case):
+    """3x3 stride-2 data gradient on even maps (TF 'same', zero leading pad: the FPN P6 / P7 convs)
+    through the 4-segment parity form (2x2 sub-kernels gathered from the dgrad pack, dst_up = 2
+    scatter) vs the direct 9-tap form (CVL_DISPATCH=no_s2dg3) and fp64 autograd; into a wider
+    destination at a channel offset with beta = 1 as well (s2dg3_min_rows=1: the small maps too)."""
+    import ctypes
+    from cvlite import _lib, ops_nn as nn
+    B, H, Cin, Cout = case
+    dispatch("s2dg3_min_rows=1")
+    g = torch.Generator().manual_seed(H * 7 + Cin)
+    x = rnd(B, H, H, Cin, gen=g).cuda().requires_grad_(True)
+    w = rnd(3, 3, Cin, Cout, scale=(9 * Cin) ** -0.5, gen=g).cuda().requires_grad_(True)
+    xn = x.permute(0, 3, 1, 2)
+    y = F.conv2d(F.pad(xn, (0, 1, 0, 1)), w.permute(3, 2, 0, 1), None, 2).permute(0, 2, 3, 1)
+    Ho = y.shape[1]
+    dy = rnd(*y.shape, gen=g).cuda()
+    y.backward(dy)
+    _, wd, _, cout_pad, cin_pad = packs(w.detach().cpu())
+    dyg = torch.zeros((B, Ho, Ho, cout_pad), dtype=BF, device="cuda")
+    dyg[..., :Cout] = dy.to(BF)
+    ld = Cin + 16
+    old = torch.randn((B, H, H, ld), generator=g).to(BF).cuda()
+    outs = []
+    for off in ("0", "1"):
+        dispatch("no_s2dg3=" + off)
+        d = nn.make_desc(nn.DGRAD, B, cout_pad, 3, 3, 2, 0, 0, cin_pad, Cin, Cin, [nn.seg(H, H, Ho, Ho, wd)])
+        if off == "0":
+            assert _lib.load().cvl_conv_igemm_workspace_size(ctypes.byref(d)) >= 16 * cin_pad * cout_pad * 2
+        dx = torch.empty((B, H, H, Cin), dtype=BF, device="cuda")
+        nn.conv_igemm(d, dyg, dx)
+        d2 = nn.make_desc(nn.DGRAD, B, cout_pad, 3, 3, 2, 0, 0, cin_pad, Cin, ld, [nn.seg(H, H, Ho, Ho, wd)],
+                          dst_coff=8, beta=1.0)
+        dx2 = old.clone()
+        nn.conv_igemm(d2, dyg, dx2)
+        outs.append((dx.double(), dx2.double()))
+    for dx, dx2 in outs:
+        torch.testing.assert_close(dx, x.grad, rtol=1e-2, atol=2e-2)
+        exp = old.double().clone()
+        exp[..., 8:8 + Cin] += x.grad
+        torch.testing.assert_close(dx2, exp, rtol=1e-2, atol=3e-2)
+    torch.testing.assert_close(outs[0][0], outs[1][0], rtol=1e-2, atol=1e-2)
+
+
+@pytest.mark.parametrize("B,H", [(4, 64), (3, 20)])
+def test_head_dgrad_cin32_on_x32(dispatch, B, H):
+    """The heads' data gradient (3x3, 32 gradient channels -> 256, K = 288) on the X32 ring kernel
+    (CVL_DISPATCH=x_cin32) and on the default path, both against fp64 autograd."""
+    from cvlite import ops_nn as nn
+    g = torch.Generator().manual_seed(B * 100 + H)
+    Cin, Cout = 256, 32
+    x = rnd(B, H, H, Cin, gen=g).cuda().requires_grad_(True)
+    w = rnd(3, 3, Cin, Cout, scale=(9 * Cin) ** -0.5, gen=g).cuda().requires_grad_(True)
+    y = F.conv2d(x.permute(0, 3, 1, 2), w.permute(3, 2, 0, 1), None, 1, 1).permute(0, 2, 3, 1)
+    dy = rnd(*y.shape, gen=g).cuda()
+    y.backward(dy)
+    _, wd, _, cout_pad, cin_pad = packs(w.detach().cpu())
+    dyg = dy.to(BF).contiguous()
+    outs = []
+    for on in ("1", "0"):
+        dispatch("x_cin32=" + on)
+        dx = torch.empty((B, H, H, Cin), dtype=BF, device="cuda")
+        d = nn.make_desc(nn.DGRAD, B, cout_pad, 3, 3, 1, 1, 1, cin_pad, Cin, Cin, [nn.seg(H, H, H, H, wd)])
+        nn.conv_igemm(d, dyg, dx)
+        if on == "1":
+            from cvlite import _lib
+            assert _lib.load().cvl_conv_igemm_last_kernel() == 7
+        outs.append(dx.double())
+    for o in outs:
+        torch.testing.assert_close(o, x.grad, rtol=1e-2, atol=2e-2)

@@ -158,3 +158,42 @@ def test_fused_loss_general_gamma_grad_vs_autograd():
         np.testing.assert_allclose(losses[0, 0].item(), lc.item(), rtol=2e-5)
         np.testing.assert_allclose(dcls[0, :, :C].cpu().numpy(), x.grad.numpy(), rtol=1e-4, atol=1e-6)
         np.testing.assert_allclose(dreg[0, :, :4].cpu().numpy(), r.grad.numpy(), rtol=1e-4, atol=1e-6)
+
+
+@pytest.mark.parametrize("C,P,ld_cls,ld_reg,gdt,flags", [
+    (20, 5456, 32, 8, torch.bfloat16, {}),                                 # FCOS production (256-cell tiles)
+    (20, 5456, 32, 8, torch.float32, {"reg_type": "iou"}),                 # fp32 gradients, IoU
+    (20, 1000, 32, 8, torch.bfloat16, {"cen_type": "focal", "reg_sigmoid": True, "cen_in_cls": True}),
+    (80, 777, 96, 8, torch.bfloat16, {}),                                  # COCO classes: 64-cell tiles
+    (1, 300, 8, 8, torch.float32, {"float_mask": True}),                   # float-mask drop-in form
+    (20, 333, 24, 6, torch.bfloat16, {"alpha": 0.4, "gamma": 1.5, "delta": 0.5})])
+def test_fcos_loss_lds_form_bit_identical_to_row_form(dispatch, C, P, ld_cls, ld_reg, gdt, flags):
+    """The LDS-staged loss kernel (cooperative coalesced loads, 16-B gradient-row stores) against the
+    row-pointer kernel (CVL_DISPATCH=loss_rows): identical per-cell arithmetic and sum order, so
+    losses and both gradients (padding columns zero) must match bit for bit -- incl. partial last
+    tiles, the centre variants' centerness column, 80 classes and fp32 gradients."""
+    from cvlite import ops_targets as ot
+    g = torch.Generator().manual_seed(C * 1000 + P)
+    B = 3
+    ld_g = (ld_cls + 7) // 8 * 8
+    reg = (torch.randn(B, P, ld_reg, generator=g) * 2).cuda()
+    cls = (torch.randn(B, P, ld_cls, generator=g) * 3).cuda()
+    tg = torch.zeros(B, P, 5 + C)
+    tg[..., :4] = torch.rand(B, P, 4, generator=g) * 5
+    tg[..., 4] = torch.rand(B, P, generator=g)
+    hot = torch.rand(B, P, generator=g) < 0.1
+    cidx = torch.randint(0, C, (B, P), generator=g)
+    tg[..., 5:].scatter_(2, cidx[..., None], hot[..., None].float())
+    if flags.get("float_mask"):
+        tg[..., 5] = torch.rand(B, P, generator=g)
+    tg = tg.cuda()
+    outs = []
+    for rows in ("1", "0"):
+        dispatch("loss_rows=" + rows)
+        d_reg = torch.full((B, P, 8), 7.0, dtype=gdt, device="cuda")
+        d_cls = torch.full((B, P, ld_g), 7.0, dtype=gdt, device="cuda")
+        outs.append(ot.fcos_loss(reg, cls, tg, C, grad_scale=0.37, grad_dtype=gdt, d_reg=d_reg, d_cls=d_cls,
+                                 **flags))
+    for x, y in zip(outs[0], outs[1]):
+        assert torch.equal(x, y), float((x.double() - y.double()).abs().max())
+    assert torch.isfinite(outs[1][0]).all() and bool((outs[1][2][..., C + (8 if flags.get("cen_in_cls") else 0) + 1:] == 0).all())
