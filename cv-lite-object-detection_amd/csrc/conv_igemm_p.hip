@@ -535,7 +535,10 @@ int cvl_conv_igemm_p(const cvl_conv_desc* d, const ConvArgs& a0, hipStream_t s) 
   // N tile: 128 for short K (<= 256: fwd 1x1 64->256 @ 128^2 44 -> 36 us, 128->512 @ 64^2 31 -> 26,
   // 256->1024 @ 32^2 25 -> 21), 64 for long K (1024->256 @ 32^2 20.5 vs 23, 2048->512 @ 16^2 29.5
   // vs 35; tools/p_probe.py)
-  const int bn = a0.K <= 256 && a0.Npad % 128 == 0 ? 128 : (a0.Npad % 64 == 0 ? 64 : 0);
+  // ... and 128 where the output is much wider than K (512->2048 @ 16^2 fwd 22.4 -> 18.9 us; the
+  // same GEMM shape as conv5_x's 2048->512 data gradient), 64 for the long-K narrow ones
+  const bool wide = a0.K <= 256 || (a0.Npad >= 2 * a0.K && cvl_dispatch_int("p_wide128", 1));
+  const int bn = wide && a0.Npad % 128 == 0 ? 128 : (a0.Npad % 64 == 0 ? 64 : 0);
   const int fbn = cvl_dispatch_int("p_bn", 0);
   const int use = a0.bsum ? 64 : (fbn && a0.Npad % fbn == 0 ? fbn : bn);
   if (!use) return -1;
