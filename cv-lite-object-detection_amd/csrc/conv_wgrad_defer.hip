@@ -31,6 +31,7 @@ struct RedBatch {
   float beta[kMaxRed];
   int blk0[kMaxRed + 1];
   int n;
+  int nt;                                    // nontemporal slab loads
 };
 
 __global__ void __launch_bounds__(256) wgrad_reduce_batch_kernel(RedBatch rb) {
@@ -48,14 +49,27 @@ __global__ void __launch_bounds__(256) wgrad_reduce_batch_kernel(RedBatch rb) {
   const f32x4* sl = reinterpret_cast<const f32x4*>(rb.slab[it]) + (long)gq * splits * n4;
   f32x4 s = f32x4{0.f, 0.f, 0.f, 0.f};
   int k = j;
-  for (; k + 7 * P < splits; k += 8 * P) {
-    f32x4 v[8];
+  // the slabs are read exactly once: nontemporal loads (reducer 49.5 -> 39.9 us per launch, step
+  // +0.7 %; CVL_DISPATCH=wgr_nt=0 for the default-policy loads)
+  if (rb.nt) {
+    for (; k + 7 * P < splits; k += 8 * P) {
+      f32x4 v[8];
 #pragma unroll
-    for (int u = 0; u < 8; ++u) v[u] = sl[(long)(k + u * P) * n4 + i];
+      for (int u = 0; u < 8; ++u) v[u] = __builtin_nontemporal_load(&sl[(long)(k + u * P) * n4 + i]);
 #pragma unroll
-    for (int u = 0; u < 8; ++u) s += v[u];
+      for (int u = 0; u < 8; ++u) s += v[u];
+    }
+    for (; k < splits; k += P) s += __builtin_nontemporal_load(&sl[(long)k * n4 + i]);
+  } else {
+    for (; k + 7 * P < splits; k += 8 * P) {
+      f32x4 v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = sl[(long)(k + u * P) * n4 + i];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) s += v[u];
+    }
+    for (; k < splits; k += P) s += sl[(long)k * n4 + i];
   }
-  for (; k < splits; k += P) s += sl[(long)k * n4 + i];
   for (int m = 1; m < P; m <<= 1) {
 #pragma unroll
     for (int c = 0; c < 4; ++c) s[c] += __shfl_xor(s[c], m);
@@ -85,6 +99,7 @@ int flush_pending(hipStream_t s) {
   while (at < g_pending.size()) {
     RedBatch rb;
     rb.n = 0;
+    rb.nt = cvl_dispatch_int("wgr_nt", 1);
     int blocks = 0;
     for (; at < g_pending.size() && rb.n < kMaxRed; ++at) {
       const Pending& p = g_pending[at];

@@ -1183,6 +1183,7 @@ __global__ void __launch_bounds__(64) sumsq_final_kernel(double* ws, int nblk) {
 }
 
 // 16-B lanes; sgd_tail_kernel covers the n % 4 last elements
+template <bool NTL>
 __global__ void __launch_bounds__(NT) sgd_kernel(float* __restrict__ w, const float* __restrict__ g,
                                                  float* __restrict__ v, long n4, const float* lr_dev,
                                                  float momentum, float inv_bs, float clip, const double* gsumsq) {
@@ -1194,7 +1195,9 @@ __global__ void __launch_bounds__(NT) sgd_kernel(float* __restrict__ w, const fl
   f32x4* v4 = reinterpret_cast<f32x4*>(v);
   const f32x4* g4 = reinterpret_cast<const f32x4*>(g);
   for (long i = blockIdx.x * (long)NT + threadIdx.x; i < n4; i += (long)gridDim.x * NT) {
-    const f32x4 gg = g4[i] * scale, vo = v4[i], wo = w4[i];
+    const f32x4 gg = (NTL ? __builtin_nontemporal_load(&g4[i]) : g4[i]) * scale;
+    const f32x4 vo = NTL ? __builtin_nontemporal_load(&v4[i]) : v4[i];
+    const f32x4 wo = w4[i];
     f32x4 vv;
 #pragma unroll
     for (int e = 0; e < 4; ++e) vv[e] = momentum * vo[e] - lr * gg[e];
@@ -1710,9 +1713,15 @@ extern "C" int cvl_sgd_clip_update(float* w, const float* g, float* v, int64_t n
   hipLaunchKernelGGL(sumsq_kernel, dim3(nb), dim3(NT), 0, S_, g, (long)n, sumsq_ws);
   hipLaunchKernelGGL(sumsq_final_kernel, dim3(1), dim3(64), 0, S_, sumsq_ws, nb);
   const long n4 = n / 4;
-  if (n4 > 0)
-    hipLaunchKernelGGL(sgd_kernel, dim3(grid_for(n4, NT * 4, 4096)), dim3(NT), 0, S_, w, g, v, n4, lr_dev,
-                       momentum, inv_bs, clip, (const double*)sumsq_ws);
+  {
+    // g and v are read once per step (w is re-read right away by the weight packing): nontemporal
+    if (n4 > 0 && cvl_dispatch_int("sgd_nt", 1))
+      hipLaunchKernelGGL(sgd_kernel<true>, dim3(grid_for(n4, NT * 4, 4096)), dim3(NT), 0, S_, w, g, v, n4, lr_dev,
+                         momentum, inv_bs, clip, (const double*)sumsq_ws);
+    else if (n4 > 0)
+      hipLaunchKernelGGL(sgd_kernel<false>, dim3(grid_for(n4, NT * 4, 4096)), dim3(NT), 0, S_, w, g, v, n4, lr_dev,
+                         momentum, inv_bs, clip, (const double*)sumsq_ws);
+  }
   if (n % 4)
     hipLaunchKernelGGL(sgd_tail_kernel, dim3(1), dim3(64), 0, S_, w, g, v, n4 * 4, (long)n, lr_dev, momentum,
                        inv_bs, clip, (const double*)sumsq_ws);
