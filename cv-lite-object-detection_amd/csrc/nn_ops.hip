@@ -21,6 +21,16 @@ __device__ __forceinline__ s16x8 pack8(const float* f) {
   return v;
 }
 
+// BN kernels' row streams (z, dy, y, residual) are read once per launch: nontemporal loads
+// (BN_NT=0 builds the default-policy form for an A/B)
+#ifndef BN_NT
+#define BN_NT 1
+#endif
+__device__ __forceinline__ s16x8 ld_rows(const cvl_bf16* p) {
+  if (BN_NT) return __builtin_nontemporal_load(reinterpret_cast<const s16x8*>(p));
+  return *reinterpret_cast<const s16x8*>(p);
+}
+
 inline int grid_for(long n, int per_block = NT, int cap = 8192) {
   long b = (n + per_block - 1) / per_block;
   return (int)(b > cap ? cap : (b < 1 ? 1 : b));
@@ -358,8 +368,8 @@ __global__ void __launch_bounds__(NT) bn_apply_kernel(const cvl_bf16* __restrict
       for (int q = 0; q < BNA_UNR; ++q) {
         const int rq = min(r + q * rpp, r1 - 1);
         off[q] = ((long)b * HW + rq) * C + c0;
-        vz[q] = *reinterpret_cast<const s16x8*>(z + off[q]);
-        if (rsrc) vr[q] = *reinterpret_cast<const s16x8*>(rsrc + off[q]);
+        vz[q] = ld_rows(z + off[q]);
+        if (rsrc) vr[q] = ld_rows(rsrc + off[q]);
       }
 #pragma unroll
       for (int q = 0; q < BNA_UNR; ++q) {
@@ -498,9 +508,9 @@ __global__ void __launch_bounds__(NT) bn_bwd_kernel(const cvl_bf16* __restrict__
         for (int q = 0; q < BN_UNR; ++q) {
           const int rq = min(r + q * rpp, r1 - 1);       // clamped: loads stay unconditional
           off[q] = ((long)b * HW + rq) * C + c0;
-          vg[q] = *reinterpret_cast<const s16x8*>(dy + off[q]);
-          if (PASS != 2) vz[q] = *reinterpret_cast<const s16x8*>(z + off[q]);
-          if (use_y) vy[q] = *reinterpret_cast<const s16x8*>(y + off[q]);
+          vg[q] = ld_rows(dy + off[q]);
+          if (PASS != 2) vz[q] = ld_rows(z + off[q]);
+          if (use_y) vy[q] = ld_rows(y + off[q]);
         }
 #pragma unroll
         for (int q = 0; q < BN_UNR; ++q) {
