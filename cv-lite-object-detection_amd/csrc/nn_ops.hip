@@ -938,7 +938,7 @@ __global__ void upsample_bwd_kernel(const cvl_bf16* dout, cvl_bf16* db, int B, i
     for (int dy = 0; dy < 2; ++dy)
       for (int dx = 0; dx < 2; ++dx) {
         float v[8];
-        unpack8(*reinterpret_cast<const s16x8*>(dout + (((long)n * H + 2 * y + dy) * W + 2 * x + dx) * C + c0), v);
+        unpack8(ld_rows(dout + (((long)n * H + 2 * y + dy) * W + 2 * x + dx) * C + c0), v);
 #pragma unroll
         for (int u = 0; u < 8; ++u) s[u] += v[u];
       }
@@ -956,8 +956,8 @@ __global__ void upsample_bwd_kernel(const cvl_bf16* dout, cvl_bf16* db, int B, i
 __global__ void relu_bwd_kernel(const cvl_bf16* dy, const cvl_bf16* y, cvl_bf16* dx, long n8, float beta) {
   for (long i = blockIdx.x * (long)NT + threadIdx.x; i < n8; i += (long)gridDim.x * NT) {
     float g[8], yy[8];
-    unpack8(reinterpret_cast<const s16x8*>(dy)[i], g);
-    unpack8(reinterpret_cast<const s16x8*>(y)[i], yy);
+    unpack8(ld_rows(dy + i * 8), g);
+    unpack8(ld_rows(y + i * 8), yy);
     if (beta != 0.f) {
       float o[8];
       unpack8(reinterpret_cast<const s16x8*>(dx)[i], o);
@@ -975,8 +975,8 @@ __global__ void relu_bwd_kernel(const cvl_bf16* dy, const cvl_bf16* y, cvl_bf16*
 __global__ void add_kernel(const cvl_bf16* a, const cvl_bf16* b, cvl_bf16* out, long n8) {
   for (long i = blockIdx.x * (long)NT + threadIdx.x; i < n8; i += (long)gridDim.x * NT) {
     float x[8], y[8];
-    unpack8(reinterpret_cast<const s16x8*>(a)[i], x);
-    unpack8(reinterpret_cast<const s16x8*>(b)[i], y);
+    unpack8(ld_rows(a + i * 8), x);
+    unpack8(ld_rows(b + i * 8), y);
 #pragma unroll
     for (int u = 0; u < 8; ++u) x[u] += y[u];
     reinterpret_cast<s16x8*>(out)[i] = pack8(x);
