@@ -767,13 +767,29 @@ __global__ void __launch_bounds__(NT) bn_relu_maxpool64_kernel(const cvl_bf16* _
     ga[u] = gamma[c0 + u];
     be[u] = beta[c0 + u];
   }
-  for (int p = threadIdx.x >> 3; p < PIY * PIX; p += NT / 8) {
+  // every load of the thread's (at most 5) tile pixels issued before any use: one memory latency
+  // per workgroup instead of one per pixel pass
+  constexpr int NPP = (PIY * PIX + NT / 8 - 1) / (NT / 8);
+  s16x8 raw[NPP];
+#pragma unroll
+  for (int k = 0; k < NPP; ++k) {
+    const int p = (threadIdx.x >> 3) + k * (NT / 8);
+    const int ly = p / PIX, lx = p - (p / PIX) * PIX;
+    const int iy = iy0 + ly, ix = ix0 + lx;
+    raw[k] = s16x8{0, 0, 0, 0, 0, 0, 0, 0};
+    if (p < PIY * PIX && (unsigned)iy < (unsigned)H && (unsigned)ix < (unsigned)W)
+      raw[k] = *reinterpret_cast<const s16x8*>(z + (((long)b * H + iy) * W + ix) * C + c0);
+  }
+#pragma unroll
+  for (int k = 0; k < NPP; ++k) {
+    const int p = (threadIdx.x >> 3) + k * (NT / 8);
+    if (p >= PIY * PIX) break;
     const int ly = p / PIX, lx = p - (p / PIX) * PIX;
     const int iy = iy0 + ly, ix = ix0 + lx;
     s16x8 o = s16x8{0, 0, 0, 0, 0, 0, 0, 0};
     if ((unsigned)iy < (unsigned)H && (unsigned)ix < (unsigned)W) {
       float v[8];
-      unpack8(*reinterpret_cast<const s16x8*>(z + (((long)b * H + iy) * W + ix) * C + c0), v);
+      unpack8(raw[k], v);
 #pragma unroll
       for (int u = 0; u < 8; ++u) {
         const float a = bn_affine(v[u], m[u], rs[u], ga[u], be[u]);
@@ -866,17 +882,27 @@ __global__ void __launch_bounds__(NT) maxpool_bwd64_kernel(const cvl_bf16* __res
   const int iy0 = (r / tx_n) * BTY, ix0 = (r - (r / tx_n) * tx_n) * BTX;
   const int oy0 = iy0 >> 1, ox0 = ix0 >> 1;          // windows oy0 .. oy0 + BOY - 1 (clipped)
   const int c8 = threadIdx.x & 7, c0 = c8 * 8;
-  for (int p = threadIdx.x >> 3; p < BOY * BOX; p += NT / 8) {
+  constexpr int NPB = (BOY * BOX + NT / 8 - 1) / (NT / 8);   // window pixels per thread, loads first
+  s16x8 gv[NPB];
+  unsigned long long av[NPB];
+#pragma unroll
+  for (int k = 0; k < NPB; ++k) {
+    const int p = (threadIdx.x >> 3) + k * (NT / 8);
     const int oy = oy0 + p / BOX, ox = ox0 + (p - (p / BOX) * BOX);
-    s16x8 gv = s16x8{0, 0, 0, 0, 0, 0, 0, 0};
-    unsigned long long av = ~0ull;                   // (no window: no tap index matches)
-    if (oy < Ho && ox < Wo) {
+    gv[k] = s16x8{0, 0, 0, 0, 0, 0, 0, 0};
+    av[k] = ~0ull;                                   // (no window: no tap index matches)
+    if (p < BOY * BOX && oy < Ho && ox < Wo) {
       const long o = (((long)b * Ho + oy) * Wo + ox) * C + c0;
-      gv = *reinterpret_cast<const s16x8*>(dy + o);
-      av = *reinterpret_cast<const unsigned long long*>(arg + o);
+      gv[k] = *reinterpret_cast<const s16x8*>(dy + o);
+      av[k] = *reinterpret_cast<const unsigned long long*>(arg + o);
     }
-    sg[p * 8 + c8] = gv;
-    sa[p * 8 + c8] = av;
+  }
+#pragma unroll
+  for (int k = 0; k < NPB; ++k) {
+    const int p = (threadIdx.x >> 3) + k * (NT / 8);
+    if (p >= BOY * BOX) break;
+    sg[p * 8 + c8] = gv[k];
+    sa[p * 8 + c8] = av[k];
   }
   __syncthreads();
   for (int q = threadIdx.x >> 3; q < BTY * BTX; q += NT / 8) {
