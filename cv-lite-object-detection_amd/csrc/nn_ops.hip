@@ -282,7 +282,10 @@ struct BnFin {
   int slots;
 };
 
-constexpr int BNA_UNR = 4;
+#ifndef BNA_UNR_V
+#define BNA_UNR_V 4
+#endif
+constexpr int BNA_UNR = BNA_UNR_V;
 
 constexpr int BN_FIN_MAXC = 2048;
 
