@@ -770,8 +770,8 @@ __global__ void __launch_bounds__(NT) bn_relu_maxpool64_kernel(const cvl_bf16* _
     ga[u] = gamma[c0 + u];
     be[u] = beta[c0 + u];
   }
-  // every load of the thread's (at most 5) tile pixels issued before any use: one memory latency
-  // per workgroup instead of one per pixel pass
+  // every load of the thread's tile pixels (NPP = 10 at 256 threads) issued before any use: one
+  // memory latency per workgroup instead of one per pixel pass
   constexpr int NPP = (PIY * PIX + NT / 8 - 1) / (NT / 8);
   s16x8 raw[NPP];
 #pragma unroll
