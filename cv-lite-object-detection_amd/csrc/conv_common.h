@@ -93,6 +93,7 @@ struct ConvArgs {
 // take = clear it, so one armed slot times at most one launch)
 uint64_t* cvl_probe_current(bool take);
 void cvl_probe_enter_call();
+void cvl_probe_leave_call();
 
 // In-kernel launch timing into a cvl_probe_arm slot (u64 [4]: start, sum of ticks, launches, done
 // workgroups): workgroup 0 stamps the start; every workgroup counts itself done after a barrier;

@@ -624,12 +624,25 @@ extern "C" size_t cvl_conv_igemm_workspace_size(const cvl_conv_desc* d) {
   return n;
 }
 
+namespace {
+int conv_igemm_call(const cvl_conv_desc* d, const void* src, void* dst, uint64_t* bn_stats_acc, void* workspace,
+                    size_t workspace_bytes, cvl_stream_t stream);
+}  // namespace
+
 extern "C" int cvl_conv_igemm(const cvl_conv_desc* d, const void* src, void* dst, uint64_t* bn_stats_acc,
                               void* workspace, size_t workspace_bytes, cvl_stream_t stream) {
+  cvl_probe_enter_call();            // an armed probe slot belongs to this call and leaves with it
+  const int st = conv_igemm_call(d, src, dst, bn_stats_acc, workspace, workspace_bytes, stream);
+  cvl_probe_leave_call();
+  return st;
+}
+
+namespace {
+int conv_igemm_call(const cvl_conv_desc* d, const void* src, void* dst, uint64_t* bn_stats_acc, void* workspace,
+                    size_t workspace_bytes, cvl_stream_t stream) {
   acc_u64* bn_stats = reinterpret_cast<acc_u64*>(bn_stats_acc);
   hipStream_t s = (hipStream_t)stream;
   g_cvl_conv_last_kernel = CVL_CK_NONE;
-  cvl_probe_enter_call();
   CVL_CHECK_ARG(d);
   if (d->prec == CVL_PREC_F32) return cvl_conv_f32(d, src, dst, bn_stats, s);    // parity mode
   CVL_CHECK_ARG(d->prec == CVL_PREC_BF16);
@@ -700,6 +713,7 @@ extern "C" int cvl_conv_igemm(const cvl_conv_desc* d, const void* src, void* dst
   if (bn == 64) return launch_bn<64>(a, dg, s);
   return launch_bn<32>(a, dg, s);
 }
+}  // namespace
 
 // Data gradient whose epilogue also forms the first pass of the NEXT BN's backward (the dgrad
 // result is dy of a BN -> ReLU unit without a residual): sums[img][c] += (sum g, sum g*xhat).

@@ -287,9 +287,10 @@ extern "C" int cvl_fcos_loss_ex(const float* reg_pred, int ld_reg, const float* 
                                 const float* targets, int B, int P, int num_classes, int reg_type,
                                 float grad_scale, float alpha, float gamma, float delta, float* losses,
                                 void* d_reg, int ld_dreg, int dreg_dtype, void* d_cls, int ld_dcls, int dcls_dtype,
-                                void* workspace, cvl_stream_t stream) {
+                                void* workspace, size_t workspace_bytes, cvl_stream_t stream) {
   CVL_CHECK_ARG(reg_pred && cls_pred && targets && losses && workspace);
   CVL_CHECK_ARG(B > 0 && P > 0 && num_classes > 0);
+  CVL_CHECK_ARG(workspace_bytes >= cvl_fcos_loss_workspace_size(B, P));
   const int kind = reg_type & 3, cen_in_cls = (reg_type & 16) ? 1 : 0;
   CVL_CHECK_ARG((kind == 0 || kind == 1) && (reg_type & ~63) == 0 && !(kind == 1 && (reg_type & 8)));
   CVL_CHECK_ARG(!(reg_type & 32) || num_classes == 1);
@@ -333,11 +334,11 @@ extern "C" int cvl_fcos_loss(const float* reg_pred, int ld_reg, const float* cls
                              const float* targets, int B, int P, int num_classes, int reg_type,
                              float grad_scale, float* losses, void* d_reg, int ld_dreg,
                              int dreg_dtype, void* d_cls, int ld_dcls, int dcls_dtype,
-                             void* workspace, cvl_stream_t stream) {
+                             void* workspace, size_t workspace_bytes, cvl_stream_t stream) {
   CVL_CHECK_ARG((reg_type & 32) == 0);
   return cvl_fcos_loss_ex(reg_pred, ld_reg, cls_pred, ld_cls, targets, B, P, num_classes, reg_type, grad_scale,
                           0.25f, 2.0f, 1.0f, losses, d_reg, ld_dreg, dreg_dtype, d_cls, ld_dcls, dcls_dtype,
-                          workspace, stream);
+                          workspace, workspace_bytes, stream);
 }
 
 // ---------------------------------------------------------------------------------------------

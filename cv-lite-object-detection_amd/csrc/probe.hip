@@ -7,14 +7,19 @@
 #include "conv_common.h"
 
 namespace {
-uint64_t* g_armed = nullptr;     // cvl_probe_arm: for the next cvl_conv_igemm call
-uint64_t* g_current = nullptr;   // the current call's slot (moved from g_armed at the call's entry)
+// per host thread (a slot armed on one thread is never taken by another thread's launch)
+thread_local uint64_t* g_armed = nullptr;     // cvl_probe_arm: for the next cvl_conv_igemm call
+thread_local uint64_t* g_current = nullptr;   // the current call's slot (moved from g_armed at its entry)
 }  // namespace
 
 void cvl_probe_enter_call() {
   g_current = g_armed;
   g_armed = nullptr;
 }
+
+// cvl_conv_igemm's exit: a slot its launch did not take is dropped, so no later launch that reaches
+// the tower kernel by another entry point (the fused dgrad + BN-sum forms) can stamp into it
+void cvl_probe_leave_call() { g_current = nullptr; }
 
 uint64_t* cvl_probe_current(bool take) {
   uint64_t* p = g_current;

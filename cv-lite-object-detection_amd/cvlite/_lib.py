@@ -35,9 +35,9 @@ SIGNATURES = {
     "cvl_fcos_assign": (c_int, [P, P, P, c_int, c_int, c_int, c_int, c_int, P, P, P, P, P]),
     "cvl_fcos_loss_workspace_size": (c_size_t, [c_int, c_int]),
     "cvl_fcos_loss": (c_int, [P, c_int, P, c_int, P, c_int, c_int, c_int, c_int, c_float, P,
-                              P, c_int, c_int, P, c_int, c_int, P, P]),
+                              P, c_int, c_int, P, c_int, c_int, P, c_size_t, P]),
     "cvl_fcos_loss_ex": (c_int, [P, c_int, P, c_int, P, c_int, c_int, c_int, c_int, c_float, c_float, c_float,
-                                 c_float, P, P, c_int, c_int, P, c_int, c_int, P, P]),
+                                 c_float, P, P, c_int, c_int, P, c_int, c_int, P, c_size_t, P]),
     "cvl_fcos_decode": (c_int, [P, c_int, c_int, c_int, ctypes.c_double, P, P]),
     "cvl_fcos_v1_decode": (c_int, [P, c_int, c_int, c_int, c_float, c_float, P, P]),
     "cvl_conv_igemm_workspace_size": (c_size_t, [P]),

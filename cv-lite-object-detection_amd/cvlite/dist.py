@@ -110,6 +110,7 @@ class GradSync(object):
                 self.launch_at[n] = param_ranges(store, pend, bucket_bytes)
                 pend, pend_bytes = [], 0
         self.works = []
+        self._cursor = -1                       # ready(): the last group reported this step (order check)
         self.active = tdist.is_initialized() and (tdist.get_world_size(group) > 1 or force_sync())
         # measurement hook (one rank only): keep the segmented graphs, issue no collective -- the
         # segmentation's share of the one-rank overhead (tools/dp_overhead.sh)
@@ -142,6 +143,12 @@ class GradSync(object):
                 for n, by, r, d in tr["groups"]]
 
     def ready(self, name):
+        # a merged group launches at its LAST member's ready point, which is only right when the
+        # backward reports groups in grad_groups() order: check it (the cursor resets in finish())
+        i = self.order.index(name)
+        assert i > self._cursor, "gradient group %r reported out of grad_groups() order (after %r)" % (
+            name, self.order[self._cursor])
+        self._cursor = i
         if not self.active or name not in self.launch_at or self.segments_only:
             return
         ev_r = ev_d = None
@@ -165,6 +172,7 @@ class GradSync(object):
         for w in self.works:
             w.wait()
         self.works = []
+        self._cursor = -1
 
 
 def max_over_ranks(value, device):

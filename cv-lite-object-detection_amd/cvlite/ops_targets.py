@@ -101,7 +101,8 @@ def fcos_loss(reg_pred, cls_pred, targets, num_classes, reg_type="l1", grad_scal
     dt = lambda t: 0 if t is None or t.dtype == torch.float32 else 1  # noqa: E731
     dflt = alpha == 0.25 and gamma == 2.0 and delta == 1.0 and not float_mask
     tail = (ptr(d_reg), int(d_reg.shape[2]) if d_reg is not None else 0, dt(d_reg),
-            ptr(d_cls), int(d_cls.shape[2]) if d_cls is not None else 0, dt(d_cls), ptr(ws), _lib.stream())
+            ptr(d_cls), int(d_cls.shape[2]) if d_cls is not None else 0, dt(d_cls), ptr(ws), ws.numel(),
+            _lib.stream())
     head = (ptr(reg_pred), int(reg_pred.shape[2]), ptr(cls_pred), int(cls_pred.shape[2]), ptr(targets), B, P,
             int(num_classes), rt, float(grad_scale))
     if dflt:

@@ -177,6 +177,10 @@ def train(net, n_classes, sub_batch_sz, batch_size, train_data, training_loss, s
     reference's order, after the batch's targets; augment=False skips it).  Returns training_loss."""
     if seed is not None:
         np.random.seed(seed)
+    # the brightness / contrast amounts (tf.random draws in the reference, which tf.random.set_seed
+    # controls): a generator owned by this call, seeded from `seed`, so two train() calls with one
+    # seed draw the same amounts; the numpy branch-draw stream stays np.random, as the reference's
+    tf_rng = np.random.RandomState(None if seed is None else (int(seed) * 1000003 + 12345) % (1 << 32))
     n_data = len(train_data)
     opt = (optimizer or Adam()).bind(net.store)
     trainers = {}
@@ -208,7 +212,7 @@ def train(net, n_classes, sub_batch_sz, batch_size, train_data, training_loss, s
             nbox[j] = n
         aug = None
         if augment:
-            d = [draw_augment(0.5) for _ in range(batch_size)]
+            d = [draw_augment(0.5, tf_rng=tf_rng) for _ in range(batch_size)]
             aug = ([o for o, _ in d], [p for _, p in d])
         tr.load_batch(torch.from_numpy(imgs).to(net.device), torch.from_numpy(boxes).to(net.device),
                       torch.from_numpy(nbox).to(net.device), raw, augment=aug)

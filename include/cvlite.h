@@ -59,13 +59,16 @@ int cvl_fcos_assign(const float* boxes, const int32_t* nbox, const float* img_di
  * centerness (fcos_center.py:386-389 cen_type="focal", fcos_center_v1.py:305-307), +8 smooth-L1 on
  * sigmoid(reg[:4]) (fcos_center_v1.py:115, l1 only), +16 the centerness logit / gradient is column
  * round_up(C, 8) of the class rows (cen_output_l lives on the cls tower).
- * `workspace` >= cvl_fcos_loss_workspace_size(B, P).
+ * `workspace` >= cvl_fcos_loss_workspace_size(B, P) bytes, passed as `workspace_bytes`
+ * (CVL_EINVAL when smaller: the size grew in round 5 to 64-cell tiles, so a buffer sized by an
+ * older formula is rejected instead of overrun).
  * ---------------------------------------------------------------------------------------- */
 size_t cvl_fcos_loss_workspace_size(int B, int P);
 int cvl_fcos_loss(const float* reg_pred, int ld_reg, const float* cls_pred, int ld_cls,
                   const float* targets, int B, int P, int num_classes, int reg_type,
                   float grad_scale, float* losses, void* d_reg, int ld_dreg, int dreg_dtype,
-                  void* d_cls, int ld_dcls, int dcls_dtype, void* workspace, cvl_stream_t stream);
+                  void* d_cls, int ld_dcls, int dcls_dtype, void* workspace, size_t workspace_bytes,
+                  cvl_stream_t stream);
 /* cvl_fcos_loss with the loss keywords of FCOS/fcos.py:380 smooth_l1_loss(delta) and :443-444
  * focal_loss(alpha, gamma) (RetinaNet/retinanet_module.py:367-401 has the same two), and one more
  * reg_type flag: +32 the regression mask is the float value targets[5] itself instead of
@@ -75,7 +78,7 @@ int cvl_fcos_loss_ex(const float* reg_pred, int ld_reg, const float* cls_pred, i
                      const float* targets, int B, int P, int num_classes, int reg_type,
                      float grad_scale, float alpha, float gamma, float delta, float* losses, void* d_reg,
                      int ld_dreg, int dreg_dtype, void* d_cls, int ld_dcls, int dcls_dtype, void* workspace,
-                     cvl_stream_t stream);
+                     size_t workspace_bytes, cvl_stream_t stream);
 
 /* FCOS/fcos.py:112-134 prediction_to_corners: pred [S0][S1][ld>=4] (t, b, l, r) fp32 ->
  * out [S0][S1][4] float64 = stride * (y_lo, x_lo, y_hi, x_hi) around cell centres (fp32 math). */

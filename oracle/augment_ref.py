@@ -43,7 +43,12 @@ def draw_augment(p=0.5, rng=np.random, tf_rng=None):
 
 def adjust_contrast(img, factor):
     """tf.image.adjust_contrast of one [N, N, 3] fp32 image: per-channel mean over the pixels, then
-    (x - mean) * factor + mean, each op rounded to fp32."""
+    (x - mean) * factor + mean, each op rounded to fp32.
+
+    The mean is a RESTATEMENT: it is summed in float64 and rounded once to fp32 (as is the golden's
+    numpy TF stub and cvl_image_augment's fixed-order partials), whereas TF's kernel reduces in fp32
+    in its own order.  TF is not importable here, so the contrast mean's rounding is parity
+    unpinned: contrast outputs are tolerance-equal (a few ulp of the mean), not bit-equal, to TF."""
     a = np.asarray(img, np.float32)
     m = a.astype(np.float64).mean(axis=(0, 1)).astype(np.float32)
     return ((a - m) * np.float32(factor) + m).astype(np.float32)
