@@ -801,6 +801,98 @@ __global__ void __launch_bounds__(1024) centernet_decode_kernel(const float* pre
   if (threadIdx.x == 0) *count = base_s;
 }
 
+// The per-scale decodes of the two variant CenterNets' obj_detect_results (the parts before the
+// plotting; one image, scales in order, cells in np.nonzero (row-major) order within a scale):
+// * mode 1, CenterNet/tf_centernet_resnet_s8.py:446-547: prediction_to_corners (:210-241: fp32
+//   centre (grid + offset) * stride, size * box_scales[s] with the scale as an fp32 operand, corners
+//   +- size / 2 in fp32, stored into float64), then the ltrb post-processing of :524-547 (image
+//   ratios in float64, w / h clamps, x / y floors) -> the rows `nms` takes;
+// * mode 2, CenterNet/tf_hourglass_net.py:517-578: centroid = ratio * (cell + offset) * 8 in float64
+//   (np.nonzero's int64 index + a float32 output), size = float32(ratio * box_scale) * output in
+//   fp32 (a python float times a numpy float32: NumPy >= 2 promotion, NEP 50, the numpy the goldens
+//   ran under), clamps to the image size, corner = centroid - size / 2 floored at 0 -> the drawn
+//   rectangles (no NMS in that decode).
+// Probabilities: fp32 sigmoid of the class logits (float64, rounded), max / first argmax over the
+// classes [cls0, cls0 + C) of the scale, kept when >= thresh; int(prob * 100) in fp32.
+struct ScaleDecodeArgs {
+  const float* pred;
+  double* rows;
+  int32_t* count;
+  int ld, H, W, ns, chs, cls0, C, mode;
+  float stride, thresh;
+  double w_ratio, h_ratio, img_w, img_h;
+  double scale[16];
+};
+
+__global__ void __launch_bounds__(1024) centernet_scale_decode_kernel(ScaleDecodeArgs a) {
+  __shared__ int wtot[16];
+  __shared__ int base_s;
+  if (threadIdx.x == 0) base_s = 0;
+  __syncthreads();
+  const int n = a.H * a.W;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  for (int s = 0; s < a.ns; ++s) {
+    for (int c0 = 0; c0 < n; c0 += 1024) {
+      const int cell = c0 + threadIdx.x;
+      bool keep = false;
+      float pmax = 0.f;
+      int lab = 0;
+      const float* p = a.pred + (size_t)cell * a.ld + s * a.chs;
+      if (cell < n) {
+        for (int c = 0; c < a.C; ++c) {
+          const float pr = (float)(1.0 / (1.0 + exp(-(double)p[a.cls0 + c])));
+          if (c == 0 || pr > pmax) { pmax = pr; lab = c; }
+        }
+        keep = pmax >= a.thresh;
+      }
+      const unsigned long long m = __ballot(keep);
+      const int pre = __popcll(m & ((1ull << lane) - 1ull));
+      if (lane == 0) wtot[wv] = __popcll(m);
+      __syncthreads();
+      int off = 0, tot = 0;
+      for (int k = 0; k < 16; ++k) { off += k < wv ? wtot[k] : 0; tot += wtot[k]; }
+      if (keep) {
+        const int y = cell / a.W, x = cell - (cell / a.W) * a.W;
+        double r0, r1, r2, r3;
+        if (a.mode == 1) {
+          const float sc = (float)a.scale[s];
+          const float yc = ((float)y + p[0]) * a.stride, xc = ((float)x + p[1]) * a.stride;
+          const float bh = p[2] * sc, bw = p[3] * sc;
+          const double b0 = (double)(yc - bh / 2.0f), b2 = (double)(yc + bh / 2.0f);
+          const double b1 = (double)(xc - bw / 2.0f), b3 = (double)(xc + bw / 2.0f);
+          double x_low = a.h_ratio * b1, y_low = a.w_ratio * b0;
+          const double x_upp = a.h_ratio * b3, y_upp = a.w_ratio * b2;
+          double bw_ = x_upp - x_low, bh_ = y_upp - y_low;
+          if (bw_ > a.img_w) bw_ = a.img_w;
+          if (bh_ > a.img_h) bh_ = a.img_h;
+          if (x_low < 0.0) x_low = 0.0;
+          if (y_low < 0.0) y_low = 0.0;
+          r0 = x_low; r1 = y_low; r2 = bw_; r3 = bh_;
+        } else {
+          const double xcen = a.w_ratio * ((double)y + (double)p[0]) * 8.0;
+          const double ycen = a.h_ratio * ((double)x + (double)p[1]) * 8.0;
+          const float bwf = (float)(a.w_ratio * a.scale[s]) * p[2];
+          const float bhf = (float)(a.h_ratio * a.scale[s]) * p[3];
+          const double bw_ = bwf > (float)a.img_w ? a.img_w : (double)bwf;
+          const double bh_ = bhf > (float)a.img_h ? a.img_h : (double)bhf;
+          double x_low = xcen - bw_ / 2.0, y_low = ycen - bh_ / 2.0;
+          if (x_low < 0.0) x_low = 0.0;
+          if (y_low < 0.0) y_low = 0.0;
+          r0 = x_low; r1 = y_low; r2 = bw_; r3 = bh_;
+        }
+        double* r = a.rows + (size_t)(base_s + off + pre) * 6;
+        r[0] = r0; r[1] = r1; r[2] = r2; r[3] = r3;
+        r[4] = (double)(int)(pmax * 100.0f);
+        r[5] = (double)lab;
+      }
+      __syncthreads();
+      if (threadIdx.x == 0) base_s += tot;
+      __syncthreads();
+    }
+  }
+  if (threadIdx.x == 0) *a.count = base_s;
+}
+
 // RetinaNet.train_loss (retinanet_module.py:403-426) over every (level, anchor) at once, fwd + bwd.
 // Predictions come straight from the grouped head convs: row (level offset + cell) of [B][P][ld],
 // class channels a*C + c, box channels a*4 + j.  Targets are cvl_retina_assign's [B][A*P][4+C] in
@@ -1269,6 +1361,24 @@ extern "C" int cvl_centernet_decode(const float* pred, int ld, int H, int W, int
   CVL_CHECK_ARG(pred && rows && count && H > 0 && W > 0 && num_classes > 0 && ld >= 4 + num_classes);
   hipLaunchKernelGGL(centernet_decode_kernel, dim3(1), dim3(1024), 0, S_, pred, ld, H, W, num_classes, stride, thresh,
                      w_ratio, h_ratio, img_width, img_height, rows, count);
+  return cvl_launch_status();
+}
+
+extern "C" int cvl_centernet_scale_decode(const float* pred, int ld, int H, int W, int n_scales, int ch_per_scale,
+                                          int cls0, int num_classes, int box_mode, const double* box_scales,
+                                          float stride, float thresh, double w_ratio, double h_ratio,
+                                          double img_width, double img_height, double* rows, int32_t* count,
+                                          cvl_stream_t stream) {
+  CVL_CHECK_ARG(pred && rows && count && box_scales && H > 0 && W > 0 && num_classes > 0);
+  CVL_CHECK_ARG(n_scales > 0 && n_scales <= 16 && (box_mode == 1 || box_mode == 2));
+  CVL_CHECK_ARG(cls0 >= 4 && ch_per_scale >= cls0 + num_classes && ld >= n_scales * ch_per_scale);
+  ScaleDecodeArgs a;
+  a.pred = pred; a.rows = rows; a.count = count;
+  a.ld = ld; a.H = H; a.W = W; a.ns = n_scales; a.chs = ch_per_scale; a.cls0 = cls0; a.C = num_classes;
+  a.mode = box_mode; a.stride = stride; a.thresh = thresh;
+  a.w_ratio = w_ratio; a.h_ratio = h_ratio; a.img_w = img_width; a.img_h = img_height;
+  for (int s = 0; s < 16; ++s) a.scale[s] = s < n_scales ? box_scales[s] : 0.0;
+  hipLaunchKernelGGL(centernet_scale_decode_kernel, dim3(1), dim3(1024), 0, S_, a);
   return cvl_launch_status();
 }
 

@@ -141,6 +141,9 @@ SIGNATURES = {
                                      P, P]),
     "cvl_centernet_decode": (c_int, [P, c_int, c_int, c_int, c_int, ctypes.c_double, c_float, ctypes.c_double,
                                      ctypes.c_double, ctypes.c_double, ctypes.c_double, P, P, P]),
+    "cvl_centernet_scale_decode": (c_int, [P, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, P, c_float,
+                                           c_float, ctypes.c_double, ctypes.c_double, ctypes.c_double,
+                                           ctypes.c_double, P, P, P]),
     "cvl_nms_workspace_size": (c_size_t, [c_int, c_int]),
     "cvl_nms": (c_int, [P, c_int, P, c_int, ctypes.c_double, P, P, P, P]),
     "cvl_soft_nms_workspace_size": (c_size_t, [c_int, c_int]),

@@ -116,6 +116,24 @@ def decode_detections(pred, thresh=0.50, downsample=8, iou_thresh=0.213, img_row
     return raw, np.array(nms(raw.copy(), iou_thresh), np.float64).reshape(-1, 6)
 
 
+def scale_decode(pred, n_scales, ch_per_scale, cls0, num_classes, box_mode, box_scales, stride, thresh, img_rows,
+                 img_cols, img_shape=None):
+    """cvl_centernet_scale_decode: one image's per-scale decode of the variant CenterNets
+    (box_mode 1: tf_centernet_resnet_s8, 2: tf_hourglass_net) -> float64 rows [n, 6] (host)."""
+    _lib.require_cuda()
+    p = torch.as_tensor(pred, dtype=torch.float32).cuda().contiguous()
+    H, W = int(p.shape[0]), int(p.shape[1])
+    ld = int(p[0, 0].numel())
+    img_w, img_h = (img_rows, img_cols) if img_shape is None else (img_shape[0], img_shape[1])
+    rows = torch.empty((n_scales * H * W, 6), dtype=torch.float64, device="cuda")
+    cnt = torch.zeros(1, dtype=torch.int32, device="cuda")
+    sc = (_lib.ctypes.c_double * n_scales)(*[float(v) for v in box_scales])
+    _lib.call("cvl_centernet_scale_decode", _lib.ptr(p), ld, H, W, int(n_scales), int(ch_per_scale), int(cls0),
+              int(num_classes), int(box_mode), sc, float(stride), float(thresh), float(img_w / img_rows),
+              float(img_h / img_cols), float(img_w), float(img_h), _lib.ptr(rows), _lib.ptr(cnt), _lib.stream())
+    return rows[:int(cnt.item())].cpu().numpy()
+
+
 def peak_detections(pred, thresh=0.3, K=100, downsample=8, num_classes=None):
     """CenterNet 3x3 max-pool peak decode (cvl_centernet_peak_decode): pred [B, H, W, 4+C] or
     [H, W, 4+C] model output (device or host) -> one float64 array [n <= K, 6] per image of

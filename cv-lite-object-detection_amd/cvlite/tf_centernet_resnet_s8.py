@@ -10,8 +10,11 @@ train_centernet_crowdhuman.py) on MI355X.
   model_loss(y_true, y_pred)                                   :368-385 (read-out on the model output)
   train_step(model, sub_batch_sz, images, bboxes, optimizer, cls_lambda, reg_lambda, learning_rate,
              grad_clip)                                        :387-444 -> S8Trainer
-nms: tf_centernet_hourglass's (identical code, cvlite.centernet_hourglass); plotting and
-_parse_image are outside this tier.
+  decode_detections(output, box_scales, thresh, downsample, iou_thresh, img_rows, img_cols, img_shape)
+      the numeric part of obj_detect_results (:446-547): cvl_centernet_scale_decode (box_mode 1) +
+      nms (:44-85, cvl_nms)
+nms: tf_centernet_hourglass's (identical code, cvlite.centernet_hourglass); the plotting and
+_parse_image of obj_detect_results are outside this tier.
 """
 import ctypes
 
@@ -20,7 +23,7 @@ import torch
 
 from . import _lib
 from . import ops_targets as ot
-from .centernet_hourglass import nms  # noqa: F401
+from .centernet_hourglass import nms, scale_decode
 from .centernet_s8_net import CenterNetS8Net
 from .train_centernet_s8 import S8Trainer
 
@@ -62,6 +65,21 @@ def prediction_to_corners(xy_pred, box_scales, stride=8):
         _lib.call("cvl_fcos_v1_decode", ctypes.c_void_p(p[:, :, s].data_ptr()), ld, S0, S1,
                   ctypes.c_float(float(box_scales[s])), ctypes.c_float(float(stride)), _lib.ptr(out[s]), _lib.stream())
     return out.permute(1, 2, 0, 3).cpu().numpy()
+
+
+def decode_detections(output, box_scales, thresh=0.50, downsample=8, iou_thresh=0.213, img_rows=448, img_cols=448,
+                      img_shape=None):
+    """obj_detect_results (:446-547) without the plotting: output = one image of the model output
+    [S0, S1, n_scales, 4 + C] (device or host) -> (bboxes_raw [n, 6] = (x_low, y_low, w, h, int(100 p),
+    class) in the reference's (scale, np.nonzero) order, bboxes_nms [m, 6] corner rows from `nms`).
+    img_shape = the source image's (shape[0], shape[1]) (default (img_rows, img_cols))."""
+    o = torch.as_tensor(output, dtype=torch.float32)
+    ns, ch = int(o.shape[2]), int(o.shape[3])
+    raw = scale_decode(o, ns, ch, 4, ch - 4, 1, list(box_scales)[:ns], downsample, thresh, img_rows, img_cols,
+                       img_shape)
+    if len(raw) == 0:
+        return raw, np.zeros((0, 6))
+    return raw, np.array(nms(raw.copy(), iou_thresh, method="nms"), np.float64).reshape(-1, 6)
 
 
 def format_data(gt_labels, box_scales, img_dim, num_classes, img_pad=None, stride=8):

@@ -9,12 +9,15 @@ on MI355X.
   train_step(voc_model, sub_batch_sz, images, bboxes, masks, optimizer, learning_rate, grad_clip,
              cls_lambda, reg_lambda, loss_type)                  :415-447
       -> cvlite.train_hourglass_v2.HourglassV2Trainer (one captured step per (batch, size))
-obj_detect_results / show_object_boxes / _parse_image / bbox_flip90 (plotting and file IO) are
-outside this tier.
+  decode_detections(output, thresh, img_rows, img_cols, img_scale, img_shape)
+      the numeric part of obj_detect_results (:451-548): cvl_centernet_scale_decode (box_mode 2)
+The plotting of obj_detect_results and show_object_boxes / _parse_image / bbox_flip90 (file IO)
+are outside this tier.
 """
 import torch
 
 from . import ops_targets as ot
+from .centernet_hourglass import scale_decode
 from .hourglass_v2_net import HourglassV2Net
 from .train_centernet import Adam
 from .train_hourglass_v2 import HourglassV2Trainer
@@ -39,6 +42,34 @@ class HourglassV2Model(object):
     def trainable_variables(self):
         st = self.net.store
         return [st.p(k) for k in st.offsets]
+
+
+def box_scales(img_rows=448, img_cols=448, img_scale=None):
+    """The four per-scale box scales of obj_detect_results (:457-465, :517-524)."""
+    if img_scale is None:
+        img_scale = [64, 128, 256, max(img_rows, img_cols) if max(img_rows, img_cols) < 512 else 512]
+    elif len(img_scale) != 4:
+        raise ValueError("img_scale must be size 4.")
+    out = list(img_scale[:3])
+    out.append(max(img_rows, img_cols) if max(img_rows, img_cols) <= img_scale[3] else img_scale[3])
+    return out
+
+
+def decode_detections(output, thresh=0.50, img_rows=448, img_cols=448, img_scale=None, img_shape=None):
+    """obj_detect_results (:451-548, transpose=False) without the plotting: output = one image of the
+    model output [S, S, 4, 5 + C] (device or host) -> float64 rows [n, 6] = (x_lower, y_lower,
+    box_width, box_height, int(100 p), class index) of every drawn rectangle, in the reference's
+    (scale, np.nonzero) order (x = the row axis, as the reference names it; the rectangle is drawn at
+    (y_lower, x_lower)).  Classes: the channels after the first when the model has more than one
+    class channel (cls_probs[..., 1:]), else channel 0.  img_shape = the source image's (shape[0],
+    shape[1]) (default (img_rows, img_cols))."""
+    o = torch.as_tensor(output, dtype=torch.float32)
+    ns, ch = int(o.shape[2]), int(o.shape[3])
+    assert ns == 4, "the v2 decode reads four scales"
+    ncls = ch - 4
+    cls0, C = (5, ncls - 1) if ncls > 1 else (4, 1)
+    return scale_decode(o, ns, ch, cls0, C, 2, box_scales(img_rows, img_cols, img_scale), 8, thresh, img_rows,
+                        img_cols, img_shape)
 
 
 def build_model(n_filters, n_classes, tmp_pi=0.99, n_repeats=2, n_features=256, seperable=True, batch_norm=True,

@@ -678,6 +678,24 @@ int cvl_centernet_decode(const float* pred, int ld, int H, int W, int num_classe
                          double w_ratio, double h_ratio, double img_width, double img_height, double* rows,
                          int32_t* count, cvl_stream_t stream);
 
+/* The variant CenterNets' obj_detect_results decodes (one image, before any plotting): pred
+ * [H][W][ld] fp32 with scale s's channels at s*ch_per_scale (4 box channels, the class logits at
+ * cls0 .. cls0+num_classes-1); rows [n][6] float64 for every (scale, cell) whose max sigmoid class
+ * probability >= thresh, scale-major and np.nonzero order within a scale; *count = n (<= n_scales*H*W).
+ * box_mode 1 = CenterNet/tf_centernet_resnet_s8.py:446-547 (prediction_to_corners :210-241 with
+ *   box_scales[s] and `stride` = downsample, then (x_low, y_low, w, h, int(100 p), argmax class):
+ *   the input of `nms` :44-85, iou 0.213);
+ * box_mode 2 = CenterNet/tf_hourglass_net.py:517-578 (stride 8, box_scales[s] = the per-scale box
+ *   scale of :518-524): (x_lower, y_lower, box_width, box_height, int(100 p), class index) of the
+ *   drawn rectangles (x = the row axis, as the reference names it; cls0 = 5 skips channel 4 when the
+ *   model has more than one class channel).
+ * w_ratio = img_width / img_rows, h_ratio = img_height / img_cols (the source image's shape[0] /
+ * shape[1], as the reference names them).  n_scales <= 16. */
+int cvl_centernet_scale_decode(const float* pred, int ld, int H, int W, int n_scales, int ch_per_scale, int cls0,
+                               int num_classes, int box_mode, const double* box_scales /*host[n_scales]*/,
+                               float stride, float thresh, double w_ratio, double h_ratio, double img_width,
+                               double img_height, double* rows, int32_t* count, cvl_stream_t stream);
+
 /* CenterNet 3x3 max-pool peak decode (the north_star's peak decode; the reference's own decode is
  * cvl_centernet_decode above): pred [B][H][W][ld] fp32 (ltrb 0..3, class logits 4..4+C).  A
  * (cell, class) is a peak when sigmoid(logit) equals the 3x3 max-pool of its class map (-inf

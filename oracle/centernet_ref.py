@@ -245,3 +245,81 @@ def decode_cells(pred, thresh=0.5, downsample=8, img_rows=448, img_cols=448, img
             y_low = 0
         rows.append(np.array([x_low, y_low, bw, bh, p, lab[xc, yc]], np.float64))
     return np.array(rows, np.float64).reshape(-1, 6)
+
+
+def decode_s8_cells(output, box_scales, thresh=0.5, downsample=8, img_rows=448, img_cols=448, img_width=448,
+                    img_height=448):
+    """The numeric part of tf_centernet_resnet_s8.obj_detect_results (CenterNet/
+    tf_centernet_resnet_s8.py:455-547): output [S0, S1, ns, 4 + C] -> the rows (x_low, y_low, w, h,
+    int(100 p), label) it hands to `nms`, scale-major, np.nonzero order within a scale.  Corners as
+    prediction_to_corners (:210-241): fp32 (grid + offset) * stride and size * box_scale (the scale an
+    fp32 operand), corners +- size / 2 in fp32, then float64."""
+    o = np.asarray(output, np.float32)
+    S0, S1, ns, ch = o.shape
+    C = ch - 4
+    w_ratio, h_ratio = img_width / img_rows, img_height / img_cols
+    gy, gx = np.meshgrid(np.arange(S0, dtype=np.float32), np.arange(S1, dtype=np.float32), indexing="ij")
+    rows = []
+    for s in range(ns):
+        sc = np.float32(box_scales[s])
+        st = np.float32(downsample)
+        xc = (gx + o[:, :, s, 1]) * st
+        yc = (gy + o[:, :, s, 0]) * st
+        bw = o[:, :, s, 3] * sc
+        bh = o[:, :, s, 2] * sc
+        two = np.float32(2.0)
+        corners = np.stack([yc - bh / two, xc - bw / two, yc + bh / two, xc + bw / two], -1).astype(np.float64)
+        probs = sigmoid32(o[:, :, s, 4:])
+        pmax = probs.max(axis=2) if C > 1 else probs[:, :, 0]
+        lab = probs.argmax(axis=2) if C > 1 else np.zeros((S0, S1), np.int64)
+        xs, ys = np.nonzero(np.where(pmax >= thresh, 1, 0))
+        for xi, yi in zip(xs, ys):
+            b = corners[xi, yi]
+            p = int(pmax[xi, yi] * np.float32(100))
+            x_low, y_low = h_ratio * b[1], w_ratio * b[0]
+            x_upp, y_upp = h_ratio * b[3], w_ratio * b[2]
+            bw_, bh_ = x_upp - x_low, y_upp - y_low
+            if bw_ > img_width:
+                bw_ = img_width
+            if bh_ > img_height:
+                bh_ = img_height
+            if x_low < 0:
+                x_low = 0
+            if y_low < 0:
+                y_low = 0
+            rows.append([x_low, y_low, bw_, bh_, p, lab[xi, yi]])
+    return np.array(rows, np.float64).reshape(-1, 6)
+
+
+def decode_hg2_cells(output, thresh=0.5, img_rows=448, img_cols=448, box_scales=(64, 128, 256, 448), img_width=448,
+                     img_height=448):
+    """The numeric part of tf_hourglass_net.obj_detect_results (CenterNet/tf_hourglass_net.py:
+    486-548, transpose=False): output [S, S, 4, 5 + C] -> the drawn rectangles as rows (x_lower,
+    y_lower, box_width, box_height, int(100 p), class index), scale-major, np.nonzero order.
+    Types as the reference's with NumPy >= 2 (NEP 50): centroid = ratio * (int64 cell + float32
+    offset) * 8 in float64; size = python-float (ratio * box_scale) times a float32 output -> float32."""
+    o = np.asarray(output, np.float32)
+    S0, S1, ns, ch = o.shape
+    n_classes = ch - 4
+    w_ratio, h_ratio = img_width / img_rows, img_height / img_cols
+    rows = []
+    for s in range(4):
+        bs = box_scales[s]
+        probs = sigmoid32(o[:, :, s, 4:])
+        if n_classes > 1:
+            pmax, lab = probs[:, :, 1:].max(axis=2), probs[:, :, 1:].argmax(axis=2)
+        else:
+            pmax, lab = probs[:, :, 0], np.zeros((S0, S1), np.int64)
+        xs, ys = np.nonzero(np.where(pmax >= thresh, 1, 0))
+        for xi, yi in zip(xs, ys):
+            b = o[xi, yi, s, :4]
+            p = int(pmax[xi, yi] * np.float32(100))
+            xcen = w_ratio * (float(xi) + float(b[0])) * 8
+            ycen = h_ratio * (float(yi) + float(b[1])) * 8
+            bw = np.float32(w_ratio * bs) * b[2]
+            bh = np.float32(h_ratio * bs) * b[3]
+            bw = float(img_width) if bw > img_width else float(bw)
+            bh = float(img_height) if bh > img_height else float(bh)
+            x_lower, y_lower = xcen - bw / 2, ycen - bh / 2
+            rows.append([x_lower if x_lower >= 0 else 0.0, y_lower if y_lower >= 0 else 0.0, bw, bh, p, lab[xi, yi]])
+    return np.array(rows, np.float64).reshape(-1, 6)

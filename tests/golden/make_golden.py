@@ -598,6 +598,108 @@ def work_image_augment(out_path):
 WORKERS["image_augment"] = work_image_augment
 
 
+def work_variant_decode(out_path):
+    """The numeric part of the variant CenterNets' `obj_detect_results`: the REFERENCE's own functions
+    (CenterNet/tf_centernet_resnet_s8.py:446-600 with its prediction_to_corners and nms;
+    CenterNet/tf_hourglass_net.py:451-600), called with a model whose predict() returns a fixed
+    random head, the image reader / PIL / matplotlib replaced by recording stand-ins (heatmap=False).
+    Recorded per case: the head, the call's arguments, the rows the s8 function hands to `nms` and
+    what `nms` returns, and the v2 function's drawn rectangles + texts as (x_lower, y_lower,
+    box_width, box_height, prob %, label index) rows.  tf.nn.sigmoid is evaluated in float64 and
+    rounded to fp32 (TF's fp32 kernel is not available: its last ulp is unpinned either way)."""
+    import types
+    tf = _child_setup("CenterNet")
+    tf.nn.sigmoid = staticmethod(lambda x: tf.Tensor(
+        (1.0 / (1.0 + np.exp(-np.asarray(x.numpy() if isinstance(x, tf.Tensor) else x, np.float64))))
+        .astype(np.float32)))
+    import tf_centernet_resnet_s8 as s8
+    import tf_hourglass_net as hg
+    state = {}
+
+    class _Ax(object):
+        def imshow(self, *a, **k):
+            return None
+
+        def add_patch(self, p):
+            state["rects"].append(p)
+
+        def text(self, x, y, t, **k):
+            state["texts"].append((x, y, t))
+
+    class _Fig(object):
+        def colorbar(self, *a, **k):
+            pass
+
+        def suptitle(self, *a, **k):
+            pass
+
+        def savefig(self, *a, **k):
+            pass
+    plt = types.SimpleNamespace(subplots=lambda n: (_Fig(), _Ax()), close=lambda: None,
+                                Rectangle=lambda xy, w, h, **k: (float(xy[0]), float(xy[1]), float(w), float(h)))
+    image = types.SimpleNamespace(open=lambda f: np.zeros(state["img_shape"] + (3,), np.uint8))
+    ref_nms = s8.nms
+
+    def nms_rec(bboxes, iou_threshold, sigma=0.3, method="nms"):
+        state["nms_in"] = np.array(bboxes, np.float64).copy()
+        out = ref_nms(bboxes, iou_threshold, sigma, method)
+        state["nms_out"] = np.array(out, np.float64).reshape(-1, 6)
+        return out
+    for mod in (s8, hg):
+        mod.plt = plt
+        mod.Image = image
+        mod._parse_image = lambda f, img_rows=448, img_cols=448: np.zeros((img_rows, img_cols, 3), np.float32)
+    s8.nms = nms_rec
+
+    class _Model(object):
+        def predict(self, x):
+            return state["head"][None]
+    rng = np.random.default_rng(4471)
+    arrays = {}
+    # s8: (S, n_scales, C, thresh, downsample, img rows/cols, source image shape)
+    s8_cases = [(24, 5, 3, 0.5, 8, (192, 192), (375, 500)), (28, 3, 1, 0.4, 8, (224, 224), (224, 224)),
+                (16, 5, 6, 0.6, 8, (128, 128), (640, 427)), (20, 2, 2, 0.99, 8, (160, 160), (160, 160))]
+    for i, (S, ns, C, thr, ds, (ir, ic), shp) in enumerate(s8_cases):
+        head = np.zeros((S, S, ns, 4 + C), np.float32)
+        head[..., :2] = rng.uniform(-0.3, 1.3, (S, S, ns, 2))
+        head[..., 2:4] = rng.uniform(0.0, 1.2, (S, S, ns, 2))
+        head[..., 4:] = rng.normal(-3.5, 2.0, (S, S, ns, C))
+        scales = [16.0, 32.0, 64.0, 128.0, 256.0][:ns]
+        state.update(head=head, img_shape=shp, rects=[], texts=[], nms_in=np.zeros((0, 6)), nms_out=np.zeros((0, 6)))
+        s8.obj_detect_results("img.jpg", _Model(), scales, ["c%d" % k for k in range(C)], heatmap=False, thresh=thr,
+                              downsample=ds, iou_thresh=0.213, img_rows=ir, img_cols=ic)
+        arrays["s8_%d_head" % i] = head
+        arrays["s8_%d_args" % i] = np.array([thr, ds, ir, ic, shp[0], shp[1]], np.float64)
+        arrays["s8_%d_scales" % i] = np.array(scales, np.float64)
+        arrays["s8_%d_raw" % i] = state["nms_in"]
+        arrays["s8_%d_nms" % i] = state["nms_out"]
+    # v2: (S, C classes incl. channel 0, thresh, img rows/cols, img_scale, source image shape)
+    hg_cases = [(24, 4, 0.5, (192, 192), None, (375, 500)), (28, 1, 0.45, (224, 224), None, (224, 224)),
+                (16, 6, 0.6, (128, 128), [32, 64, 96, 100], (640, 427)), (40, 3, 0.55, (320, 320), None, (512, 512))]
+    for i, (S, C, thr, (ir, ic), isc, shp) in enumerate(hg_cases):
+        head = np.zeros((S, S, 4, 4 + C), np.float32)
+        head[..., :2] = rng.uniform(-0.2, 1.2, (S, S, 4, 2))
+        head[..., 2:4] = rng.uniform(0.0, 3.0, (S, S, 4, 2))
+        head[..., 4:] = rng.normal(-3.5, 2.0, (S, S, 4, C))
+        state.update(head=head, img_shape=shp, rects=[], texts=[])
+        labels = ["c%d" % k for k in range(C)]
+        hg.obj_detect_results("img.jpg", _Model(), labels, heatmap=False, thresh=thr, img_rows=ir, img_cols=ic,
+                              img_scale=isc)
+        rows = []
+        for (y_lo, x_lo, bh, bw), (_, _, t) in zip(state["rects"], state["texts"]):
+            lab, pr = t.split(": ")
+            rows.append([x_lo, y_lo, bw, bh, float(pr.rstrip("%")), float(labels.index(lab))])
+        arrays["hg_%d_head" % i] = head
+        arrays["hg_%d_args" % i] = np.array([thr, ir, ic, shp[0], shp[1]], np.float64)
+        arrays["hg_%d_scale" % i] = np.array(isc if isc is not None else [], np.float64)
+        arrays["hg_%d_rows" % i] = np.array(rows, np.float64).reshape(-1, 6)
+    arrays["n_s8"], arrays["n_hg"] = np.int32(len(s8_cases)), np.int32(len(hg_cases))
+    np.savez_compressed(out_path, **arrays)
+
+
+WORKERS["variant_decode"] = work_variant_decode
+
+
 def main():
     if len(sys.argv) == 3 and sys.argv[1] in WORKERS:
         WORKERS[sys.argv[1]](sys.argv[2])

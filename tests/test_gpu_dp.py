@@ -92,7 +92,7 @@ def test_dp_overlapped_allreduce_matches_single_process():
     assert e < 1e-5
 
 
-def _nccl_worker(rank, port, out):
+def _nccl_worker(rank, port, out, D=D, BS=BS):
     """One rank on an RCCL ("nccl") process group with the gradient all-reduce forced on: the
     trainer captures its backward in hook-split graph segments and GradSync queues async RCCL
     all-reduces on ProcessGroupNCCL's stream between the segment replays (the N>1 bench path)."""
@@ -119,13 +119,16 @@ def _nccl_worker(rank, port, out):
     tdist.destroy_process_group()
 
 
-def test_rccl_segmented_allreduce_matches_plain_step():
+@pytest.mark.parametrize("D,BS", [(D, BS), (512, 16)], ids=["256_bs2", "512_bs16"])
+def test_rccl_segmented_allreduce_matches_plain_step(D, BS):
     """The RCCL branch of dist.init_from_env + GradSync against HIP-graph segment replay (one GPU per
     box, so one rank: the SUM all-reduce is the identity and the two steps must be bit-identical to
-    the same trainer without the collective path)."""
+    the same trainer without the collective path).  512 / bs 16 is configs[2]'s per-rank workload:
+    the production dispatch (split-K plans, X32 tower segments, deferred weight-gradient reductions
+    flushed at each group's hook) under the segmented DP graphs."""
     with tempfile.TemporaryDirectory() as td:
         out = os.path.join(td, "nccl.pt")
-        mp.start_processes(_nccl_worker, args=(_port(), out), nprocs=1, join=True, start_method="spawn")
+        mp.start_processes(_nccl_worker, args=(_port(), out, D, BS), nprocs=1, join=True, start_method="spawn")
         got = torch.load(out, weights_only=True)
     from cvlite.fcos_net import FCOSNet
     from cvlite.train_fcos import FCOSTrainer, synthetic_batch

@@ -155,3 +155,24 @@ def test_centernet_decode_matches_restatement():
     pred = np.full((16, 16, 24), -9.0, np.float32)
     raw, kept = hg.decode_detections(pred)
     assert raw.shape == (0, 6) and kept.shape == (0, 6)
+
+
+def test_variant_decodes_bit_exact_vs_reference_goldens(golden):
+    """cvl_centernet_scale_decode (+ cvl_nms for the s8 form) vs goldens produced by the reference's
+    own obj_detect_results (CenterNet/tf_centernet_resnet_s8.py:446-547 and its nms :44-85;
+    CenterNet/tf_hourglass_net.py:451-548): bit-exact rows, incl. size clamps and an empty result."""
+    from cvlite import tf_centernet_resnet_s8 as s8
+    from cvlite import tf_hourglass_net as hg2
+    d = golden("variant_decode")
+    for i in range(int(d["n_s8"])):
+        thr, ds, ir, ic, w, h = d["s8_%d_args" % i]
+        raw, kept = s8.decode_detections(d["s8_%d_head" % i], d["s8_%d_scales" % i], thresh=thr, downsample=int(ds),
+                                         img_rows=int(ir), img_cols=int(ic), img_shape=(int(w), int(h)))
+        np.testing.assert_array_equal(raw, d["s8_%d_raw" % i])
+        np.testing.assert_array_equal(kept, d["s8_%d_nms" % i])
+    for i in range(int(d["n_hg"])):
+        thr, ir, ic, w, h = d["hg_%d_args" % i]
+        isc = list(d["hg_%d_scale" % i]) or None
+        rows = hg2.decode_detections(torch.from_numpy(d["hg_%d_head" % i]).cuda(), thresh=thr, img_rows=int(ir),
+                                     img_cols=int(ic), img_scale=isc, img_shape=(int(w), int(h)))
+        np.testing.assert_array_equal(rows, d["hg_%d_rows" % i])

@@ -307,3 +307,29 @@ def test_image_augment_product_draws_match_restatement():
         t1, t2 = np.random.RandomState(s + 7), np.random.RandomState(s + 7)
         assert draw_augment(0.5, rng=r1, tf_rng=t1) == A.draw_augment(0.5, rng=r2, tf_rng=t2)
         assert r1.uniform() == r2.uniform()
+
+
+def _hg2_box_scales(ir, ic, isc):
+    if not len(isc):
+        isc = [64, 128, 256, max(ir, ic) if max(ir, ic) < 512 else 512]
+    return list(isc[:3]) + [max(ir, ic) if max(ir, ic) <= isc[3] else isc[3]]
+
+
+def test_variant_decode_oracle(golden):
+    """The variant CenterNets' obj_detect_results decodes (tf_centernet_resnet_s8.py:446-547 incl. its
+    nms; tf_hourglass_net.py:451-548): the restatements vs goldens produced by the reference's own
+    functions (plotting recorded, not drawn) -- bit-exact rows, incl. size clamps and an empty case."""
+    d = golden("variant_decode")
+    for i in range(int(d["n_s8"])):
+        thr, ds, ir, ic, w, h = d["s8_%d_args" % i]
+        raw = centernet_ref.decode_s8_cells(d["s8_%d_head" % i], d["s8_%d_scales" % i], thr, int(ds), int(ir),
+                                            int(ic), int(w), int(h))
+        np.testing.assert_array_equal(raw, d["s8_%d_raw" % i])
+        if len(raw):
+            np.testing.assert_array_equal(np.array(centernet_ref.nms(raw.copy(), 0.213)).reshape(-1, 6),
+                                          d["s8_%d_nms" % i])
+    for i in range(int(d["n_hg"])):
+        thr, ir, ic, w, h = d["hg_%d_args" % i]
+        bs = _hg2_box_scales(int(ir), int(ic), list(d["hg_%d_scale" % i]))
+        rows = centernet_ref.decode_hg2_cells(d["hg_%d_head" % i], thr, int(ir), int(ic), bs, int(w), int(h))
+        np.testing.assert_array_equal(rows, d["hg_%d_rows" % i])
