@@ -45,22 +45,15 @@
 
 namespace {
 
-constexpr int BM = 256, BN = 64, NT = 512, BK = 32;
-constexpr int WGM = 4, WM = 64, WN = 32, TM = 4, TN = 2;
+constexpr int BM = 256, BN = 64, NT = 512, BK = 32;   // BN: the default (64-wide) N tile
+constexpr int WGM = 4, WM = 64, TM = 4;
 constexpr int HPX = 640;                            // halo pixels per stage
 constexpr int HPW = HPX / 16 / 8;                   // halo DMA pieces (16 pixels each) per wave: 5
-constexpr int WPC = 9 * BN * BK * 2 / 1024;         // weight DMA pieces per stage: 36 (4 or 5 per wave)
 constexpr int HALO_EL = HPX * BK;                   // bf16 elements of a halo image (40,960 B)
-constexpr int WT_EL = 9 * BN * BK;                  // bf16 elements of a stage's weights (36,864 B)
-constexpr int STAGE_EL = HALO_EL + WT_EL;
-constexpr int LDS_C = BM * (BN + 8) + WGM * BN * 2 * 2;
-constexpr int LDS_EL = 2 * STAGE_EL > LDS_C ? 2 * STAGE_EL : LDS_C;
 // WRES (weights resident): a single-N-tile launch with at most 2 channel blocks (Cin <= 64: the
 // ResNet conv2_x 3x3 units, forward and data gradient) keeps ALL its weights in LDS for the whole
 // launch and streams only the halos, double-buffered: 2 halos + 2 x 36 KiB of weights = 152 KiB
 constexpr int WRES_CB = 2;
-constexpr int LDS_WRES_EL = 2 * HALO_EL + WRES_CB * WT_EL;
-static_assert(HALO_EL >= LDS_C, "the epilogue stages its C image in a halo buffer");
 constexpr unsigned kRecords = 0x7fffffffu;
 constexpr unsigned kOOB = 0x80000000u;
 
@@ -153,8 +146,20 @@ __device__ unsigned long long g_h_stamps[kHStampWgs * 8];
 // issued, so that tile's halo and weights land while the current tile's epilogue runs (the
 // epilogue stages its C image in the stage buffer just consumed), and the per-tile set-up is a
 // few adds (halo_pieces is per segment).  One workgroup per CU (148 KiB of LDS).
-template <bool DGRAD, bool BSUM, bool WRES = false, bool ST = false, bool SW = false>
+template <bool DGRAD, bool BSUM, bool WRES = false, bool ST = false, bool SW = false, int BNT = 64>
 __global__ void __launch_bounds__(NT) conv_igemm_h_kernel(ConvArgs a) {
+  // BNT: the N tile, 64 (the backbone / FPN launches) or 32 (round 6: the FCOS heads' forward, 3x3
+  // 256 -> 20 / 5 over the five levels; Npad 32); the constants below shadow the 64-wide ones
+  constexpr int BN = BNT, TN = BN / 32, WN = BN / 2;
+  constexpr int WPC = 9 * BN * BK * 2 / 1024;          // weight DMA pieces per stage: 36 / 18
+  constexpr int WJ = WPC / 8, WR = WPC % 8;             // full rounds of 8 waves + the remainder
+  constexpr int PPT = BN / 16;                          // pieces per tap (16 rows x 64 B each)
+  constexpr int WT_EL = 9 * BN * BK;
+  constexpr int STAGE_EL = HALO_EL + WT_EL;
+  constexpr int LDS_C = BM * (BN + 8) + WGM * BN * 2 * 2;
+  constexpr int LDS_EL = 2 * STAGE_EL > LDS_C ? 2 * STAGE_EL : LDS_C;
+  constexpr int LDS_WRES_EL = 2 * HALO_EL + WRES_CB * WT_EL;
+  static_assert(HALO_EL >= LDS_C && HPW + WJ <= 9 && BN % 32 == 0, "H64 stage layout");
   constexpr int MAIN_EL = WRES ? LDS_WRES_EL : LDS_EL;
   // SW: + the [WGM][BN][2] fp32 combine buffer of the statistics flush
   __shared__ __attribute__((aligned(16))) cvl_bf16 lds[MAIN_EL + (SW ? WGM * BN * 2 * 2 : 0)];
@@ -203,7 +208,7 @@ __global__ void __launch_bounds__(NT) conv_igemm_h_kernel(ConvArgs a) {
   // ---- issue cursor: the channel block whose stage the next issue slots load ------------------
   const int hch = lane & 3;
   int i_L = next_tile(t_lo), i_cb = cb0, i_sg = -1;
-  unsigned hoff[HPW], woff[5];
+  unsigned hoff[HPW], woff[WJ + (WR ? 1 : 0)];
   HaloPieces HP;
   HP.valid = 0;
   auto cursor_tile = [&]() {               // hoff / woff of the cursor's tile
@@ -235,9 +240,9 @@ __global__ void __launch_bounds__(NT) conv_igemm_h_kernel(ConvArgs a) {
       hoff[j] = ok ? (unsigned)(pix * Cin * 2) + (unsigned)((hch ^ swz4(hp)) * 16) : kOOB;
     }
 #pragma unroll
-    for (int j = 0; j < 5; ++j) {
-      const int w = (wave + 8 * j) % WPC, tap = w >> 2;
-      const int row = (w & 3) * 16 + (lane >> 2);
+    for (int j = 0; j < WJ + (WR ? 1 : 0); ++j) {
+      const int w = (wave + 8 * j) % WPC, tap = w / PPT;
+      const int row = (w % PPT) * 16 + (lane >> 2);
       woff[j] = (unsigned)(((n0 + row) * Kdim + tap * Cin) * 2) + (unsigned)((hch ^ swz4(row)) * 16);
     }
   };
@@ -340,12 +345,12 @@ __global__ void __launch_bounds__(NT) conv_igemm_h_kernel(ConvArgs a) {
     for (int j = 0; j < HPW; ++j) dma16(rsA, st + (wave + 8 * j) * 16 * BK, hoff[j] + cbo);
     if (WRES) {                                     // the first channel block's weights (the rest below)
 #pragma unroll
-      for (int j = 0; j < 4; ++j) dma16(rsB, wres + (wave + 8 * j) * 16 * BK, woff[j]);
-      if (wave < WPC - 32) dma16(rsB, wres + (wave + 32) * 16 * BK, woff[4]);
+      for (int j = 0; j < WJ; ++j) dma16(rsB, wres + (wave + 8 * j) * 16 * BK, woff[j]);
+      if (WR && wave < WR) dma16(rsB, wres + (wave + 8 * WJ) * 16 * BK, woff[WJ]);
     } else {
 #pragma unroll
-      for (int j = 0; j < 4; ++j) dma16(rsB, st + HALO_EL + (wave + 8 * j) * 16 * BK, woff[j] + cbo);
-      if (wave < WPC - 32) dma16(rsB, st + HALO_EL + (wave + 32) * 16 * BK, woff[4] + cbo);
+      for (int j = 0; j < WJ; ++j) dma16(rsB, st + HALO_EL + (wave + 8 * j) * 16 * BK, woff[j] + cbo);
+      if (WR && wave < WR) dma16(rsB, st + HALO_EL + (wave + 8 * WJ) * 16 * BK, woff[WJ] + cbo);
     }
     advance();
   }
@@ -359,8 +364,8 @@ __global__ void __launch_bounds__(NT) conv_igemm_h_kernel(ConvArgs a) {
     for (int cbw = 1; cbw < ncb_all; ++cbw) {
       const unsigned wo = (unsigned)(cbw * BK * 2);
 #pragma unroll
-      for (int j = 0; j < 4; ++j) dma16(rsB, wres + cbw * WT_EL + (wave + 8 * j) * 16 * BK, woff[j] + wo);
-      if (wave < WPC - 32) dma16(rsB, wres + cbw * WT_EL + (wave + 32) * 16 * BK, woff[4] + wo);
+      for (int j = 0; j < WJ; ++j) dma16(rsB, wres + cbw * WT_EL + (wave + 8 * j) * 16 * BK, woff[j] + wo);
+      if (WR && wave < WR) dma16(rsB, wres + cbw * WT_EL + (wave + 8 * WJ) * 16 * BK, woff[WJ] + wo);
     }
   }
 
@@ -479,8 +484,8 @@ __global__ void __launch_bounds__(NT) conv_igemm_h_kernel(ConvArgs a) {
 #pragma unroll
       for (int t = 0; t < 9; ++t) {
         if (more && t < HPW) dma16(rsA, nh + (wave + 8 * t) * 16 * BK, hoff[t] + cbo);
-        if (!WRES && more && t >= HPW && t < HPW + 4) dma16(rsB, nh + HALO_EL + (wave + 8 * (t - HPW)) * 16 * BK, woff[t - HPW] + cbo);
-        if (!WRES && t == 8 && more && wave < WPC - 32) dma16(rsB, nh + HALO_EL + (wave + 32) * 16 * BK, woff[4] + cbo);
+        if (!WRES && more && t >= HPW && t < HPW + WJ) dma16(rsB, nh + HALO_EL + (wave + 8 * (t - HPW)) * 16 * BK, woff[t - HPW] + cbo);
+        if (!WRES && WR && t == 8 && more && wave < WR) dma16(rsB, nh + HALO_EL + (wave + 8 * WJ) * 16 * BK, woff[WJ] + cbo);
         if (t < 8) read_tap((t + 1) & 1, Hc, t + 1);
         mma_tap(t & 1);
       }
@@ -627,8 +632,10 @@ extern "C" int cvl_debug_h_stamps(uint64_t* host, int max_wgs) {
 // whole image rows (W | 256, H*W % 256 == 0) or whole images (H*W | 256), halo within HPX pixels.
 bool cvl_conv_h_fits(const cvl_conv_desc* d, const ConvArgs& a) {
   if (d->KH != 3 || d->KW != 3 || d->stride != 1 || d->pad_t != 1 || d->pad_l != 1 || a.Cin % BK ||
-      a.Npad % BN || a.relu_in || a.dst_up != 1)
+      (a.Npad % BN && a.Npad != 32) || a.relu_in || a.dst_up != 1)
     return false;
+  // the 32-wide form serves fp32 forwards without statistics only (the FCOS heads)
+  if (a.Npad == 32 && (d->mode != CVL_CONV_FWD || !d->dst_f32)) return false;
   for (int i = 0; i < a.nseg; ++i) {
     const ConvSeg& q = a.seg[i];
     if (q.Hr != q.Hs || q.Wr != q.Ws) return false;
@@ -649,6 +656,16 @@ int cvl_conv_igemm_h(const cvl_conv_desc* d, const ConvArgs& a0, hipStream_t s, 
   if (cvl_dispatch_flag("no_h") || !cvl_conv_h_fits(d, a0)) return -1;
   ConvArgs a = a0;
   const bool dg = d->mode == CVL_CONV_DGRAD;
+  if (a.Npad == 32) {          // 256 x 32 tiles (the FCOS heads' forward): persistent, no split, fp32 epilogue
+    if (a.stats || a.bsum) return -1;
+    static const int ncu32 = cvl_device_cus();
+    const int t32 = a.m_tiles;
+    a.splits = 1;
+    g_cvl_conv_last_kernel = CVL_CK_H64;
+    hipLaunchKernelGGL((conv_igemm_h_kernel<false, false, false, false, false, 32>), dim3(t32 < ncu32 ? t32 : ncu32),
+                       dim3(NT), 0, s, a);
+    return cvl_launch_status();
+  }
   const int tiles = a.m_tiles * (a.Npad / BN);
   const int ncb = a.Cin / BK;
   // split the channel blocks of grids that leave CUs idle (fp32 slabs, single segment, no fused
@@ -723,7 +740,7 @@ int cvl_conv_igemm_h(const cvl_conv_desc* d, const ConvArgs& a0, hipStream_t s, 
 
 // split-K workspace H64 would use for this descriptor (0: none)
 size_t cvl_conv_h_workspace(const cvl_conv_desc* d, const ConvArgs& a) {
-  if (!cvl_conv_h_fits(d, a) || a.nseg != 1) return 0;
+  if (!cvl_conv_h_fits(d, a) || a.nseg != 1 || a.Npad % BN) return 0;
   const int tiles = a.m_tiles * (a.Npad / BN);
   const int target = cvl_tune_int("CVL_CONV_H_SPLIT_TARGET", 256);
   if (tiles >= target) return 0;

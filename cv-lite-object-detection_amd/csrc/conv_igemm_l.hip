@@ -232,6 +232,18 @@ int cvl_conv_igemm_l(const cvl_conv_desc* d, int dst_up, int dst_w, const void* 
     return -1;
   // the residual (y-mask) form exists on the 1x1 persistent kernel only
   if (bsum && bsum->y && (d->KH != 1 || d->KW != 1)) return -1;
+  // 3x3 / stride 1 forwards 32 wide into fp32 (the FCOS heads, 256 -> 20 / 5 over the five levels,
+  // fcos.py:85-88, 99-101): the halo kernel with 256 x 32 tiles -- one halo stage per 32-channel
+  // block feeds all nine taps, where the 128-row generic kernel re-gathers nine im2col tiles
+  if (d->Npad == 32 && d->KH == 3 && d->KW == 3 && d->mode == CVL_CONV_FWD && d->dst_f32 && !bn_stats &&
+      !bsum && dst_up == 1 && d->Cin % 32 == 0 && !d->relu_in && !cvl_dispatch_flag("no_h32")) {
+    ConvArgs ah;
+    if (cvl_conv_prepare(d, BM, &ah)) return -1;
+    ah.src = reinterpret_cast<const cvl_bf16*>(src);
+    ah.dst = dst;
+    ah.stats = nullptr;
+    return cvl_conv_igemm_h(d, ah, s, nullptr, 0);
+  }
   // fp32 destinations store element-wise: any n_store (the RetinaNet box heads: 9 anchors x 4 = 36)
   const bool n_ok = d->dst_f32 ? (d->n_store % 4 == 0 && !cvl_tune_flag("CVL_CONV_L_F32_N8")) : d->n_store % 8 == 0;
   if (d->Cin % 32 != 0 || d->relu_in || !n_ok || (d->dst_f32 && bn_stats) ||

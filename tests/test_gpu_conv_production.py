@@ -201,6 +201,42 @@ def test_retina_cls_head_f32_epilogue_configs4(N, NP):
         torch.testing.assert_close(got, ref, rtol=1e-2, atol=2e-2, msg=lambda m: "dgrad level %d: %s" % (l, m))
 
 
+@pytest.mark.parametrize("N,LD", [(20, 32), (5, 8)], ids=["cls20", "reg5"])
+def test_fcos_heads_forward_h32_configs1(N, LD, dispatch):
+    """FCOS cls / reg head forward (fcos.py:85-88, 99-101: 3x3 256 -> 20 / 5, per-level weights and
+    bias, five segments) at bs 16 / 512 into the image-major fp32 head output [B, P, LD], on the
+    halo kernel's 256 x 32 tile (round 6; was the 128-row generic kernel); the same launch with the
+    32-wide form off (CVL_DISPATCH=no_h32) must agree to fp32 accumulation-order noise."""
+    from cvlite import ops_nn as nn
+    B, S, C = 16, 512, 256
+    shapes, off, P = fpn_layout(B, S)
+    g = torch.Generator(device="cuda").manual_seed(17)
+    act = rnd((B * P, C), 0.5, g)
+    ws = [rnd((3, 3, C, N), 0.02, g).to(F64) for _ in shapes]
+    bs = [torch.randn(N, generator=g, device="cuda") for _ in shapes]
+    pk = [packs(w) for w in ws]
+    segs = [nn.seg(h, w, h, w, pk[l][0], bs[l], src_base=B * off[l], src_img=h * w, dst_base=off[l], dst_img=P)
+            for l, (h, w) in enumerate(shapes)]
+    d = nn.make_desc(nn.FWD, B, C, 3, 3, 1, 1, 1, 32, N, LD, segs, dst_f32=True)
+    out = torch.full((B, P, LD), 7.0, dtype=torch.float32, device="cuda")
+    nn.conv_igemm(d, act, out)
+    code, name = last_kernel()
+    print("head kernel:", name)
+    assert code == 14, name                 # H64 (its 256 x 32 form)
+    a64 = act.to(F64)
+    for l, (h, w) in enumerate(shapes):
+        x = a64[B * off[l]:B * (off[l] + h * w)].view(B, h, w, C)
+        ref = conv_ref(x, ws[l]) + bs[l].to(F64)
+        got = out[:, off[l]:off[l] + h * w, :N].reshape(B, h, w, N).to(F64)
+        torch.testing.assert_close(got, ref, rtol=1e-4, atol=1e-4, msg=lambda m: "level %d: %s" % (l, m))
+    assert torch.all(out[..., N:] == 7.0), "columns past n_store must not be written"
+    dispatch("no_h32")
+    out2 = torch.full((B, P, LD), 7.0, dtype=torch.float32, device="cuda")
+    nn.conv_igemm(d, act, out2)
+    assert last_kernel()[0] != 14
+    torch.testing.assert_close(out2, out, rtol=1e-5, atol=1e-5)
+
+
 @pytest.mark.parametrize("mode,B,H,W,C,N", [("fwd", 2, 64, 64, 256, 256), ("dgrad", 3, 32, 32, 512, 256),
                                            ("fwd", 3, 8, 8, 256, 256), ("dgrad", 5, 4, 4, 256, 512),
                                            ("fwd", 2, 16, 16, 256, 256), ("fwd", 1, 64, 64, 64, 256)])
