@@ -25,6 +25,8 @@
 // * The reduction range of a group is split over workgroups to fill the GPU; partial tiles go to
 //   fp32 slabs summed in a fixed order by cvl_wgrad_reduce (conv_wgrad_defer.hip; deterministic), or straight to dW
 //   (with beta) when one split covers the range.
+#include <type_traits>
+
 #include "conv_common.h"
 
 namespace {
@@ -46,6 +48,9 @@ struct WxCfg {
   static constexpr int KS = SR / BR;      // 32-deep MFMA sub-steps per step
 };
 constexpr int kMaxGroups = 2;
+#ifndef CVL_WGX_ABL
+#define CVL_WGX_ABL 0                     // measurement variants only (ablation bits, see issue())
+#endif
 constexpr unsigned kRecords = 0x7fffffffu;
 constexpr unsigned kOOB = 0x80000000u;
 
@@ -59,6 +64,34 @@ struct WxArgs {
   unsigned long long* stamps;             // measurement builds (CVL_WGX_STAMPS=1): u64 [grid][4], else null
   unsigned long long* phase;              // with stamps: per-wave loop phase cycles u64 [grid][8][8], or null
   int ablate;                             // with stamps: ablation bits (CVL_WGX_ABLATE), else 0
+};
+
+// Batched form (round 6, cvl_conv_wgrad_batch): up to kMaxProb independent 1x1 weight gradients in
+// ONE launch, each problem a single segment (pad 0, stride 1 or 2) with its own x / dY / dW and its own
+// (tile, split) grid; workgroup L (after the XCD remap) belongs to the problem whose [wg0, wg0 +
+// tiles * nsplit) range holds it.  One launch per ResNet stage instead of one per conv: the per-launch
+// fixed cost (~7 us: prologue, epilogue, the grid's ramp) is paid once, and with the grid filled by
+// several problems each one needs fewer splits (fewer fp32 slab bytes to reduce).
+constexpr int kMaxProb = 16;
+struct WxProb {
+  const cvl_bf16* x;
+  const cvl_bf16* dy;
+  float* out;                             // fp32 slab [nsplit][K][Cout], or dW (direct)
+  int Hr, Wr, Hs, Ws, B, Cin, stride;     // output map (rows), input map, images, channels, stride
+  int Cout, ld_dy, dy_coff, co_tiles, tiles, nsplit, chunk, direct, wg0, m_total;
+  float beta;
+};
+struct WxBatchArgs {
+  WxProb p[kMaxProb];
+  int n;
+  unsigned long long* stamps;             // (measurement fields: as WxArgs, unused by the batch)
+  unsigned long long* phase;
+  int ablate;
+};
+// geometry of one segment as the cursor sees it
+struct WxSeg {
+  int Hr, Wr, Hs, Ws, rows, m_start;
+  long src_base, src_img, dst_base, dst_img;
 };
 
 __device__ __forceinline__ int rswz(int r) { return (r & 3) | (((r >> 3) & 1) << 2); }
@@ -84,8 +117,9 @@ typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 // pieces of step t+1 at the END of its MFMA segment t-1, so with the groups one barrier apart all
 // pieces of t+1 have landed before the barrier that opens either group's MFMA segment t (the
 // X32 kernel's SW form, conv_igemm_x.hip).
-template <int T, int SR = BR, bool ST = false, bool PF = false>
-__global__ void __launch_bounds__(NT) conv_wgrad_x_kernel(WxArgs g) {
+template <int T, int SR = BR, bool ST = false, bool PF = false, typename Args = WxArgs>
+__global__ void __launch_bounds__(NT) conv_wgrad_x_kernel(Args g) {
+  constexpr bool MP = !std::is_same<Args, WxArgs>::value;   // a batch of problems (WxBatchArgs)
   using C = WxCfg<T, SR>;
   // ST: wall-clock stamps of thread 0 (entry, prologue landed, loop done, epilogue stored)
   unsigned long long* stamp = (ST && threadIdx.x == 0) ? g.stamps + blockIdx.x * 4 : nullptr;
@@ -93,33 +127,86 @@ __global__ void __launch_bounds__(NT) conv_wgrad_x_kernel(WxArgs g) {
   constexpr int BCO = C::BCO, BKK = C::BKK, YST = C::YST, SLOT = C::SLOT, TM = C::TM, TN = C::TN;
   constexpr int J = C::J;
   __shared__ __attribute__((aligned(16))) cvl_bf16 lds[NSLOT * SLOT];
-  const ConvArgs& a = g.a;
+  // measurement: ablation bits (issue()); un-stamped launches take the compile-time -DCVL_WGX_ABL
+  // (tools/wgx_probe.sh's variant libraries), 0 in the product build
+  const int abl = ST ? g.ablate : CVL_WGX_ABL;
   const int tid = threadIdx.x;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
   // logical id: the (co, k) tiles of one (group, split) are consecutive, i.e. on one XCD's L2
-  const int L = xcd_remap(blockIdx.x, gridDim.x);
-  const int tile = L % g.tiles, rest = L / g.tiles;
-  const int split = rest % g.nsplit, grp = rest / g.nsplit;
-  const int co0 = (tile % g.co_tiles) * BCO, k0 = (tile / g.co_tiles) * BKK;
-  const int m_lo = g.g_m0[grp] + split * g.chunk;
-  const int m_hi = min(m_lo + g.chunk, g.g_m1[grp]);
+  int L = xcd_remap(blockIdx.x, gridDim.x);
+  // ---- the problem this workgroup works on: its geometry (segments), operands and grid --------------
+  const cvl_bf16* src_;
+  const cvl_bf16* dyp;
+  float* outp;
+  int Cin_, K_, KW_, pad_t_, pad_l_, st_, nseg_, ld_dy_, dy_coff_, Cout_, tiles_, co_tiles_, nsplit_, chunk_, direct_;
+  int gm0, gm1, grp = 0;
+  float beta_;
+  WxSeg seg1;                                             // MP: the problem's single segment
+  if constexpr (MP) {
+    int pi = 0;
+#pragma unroll
+    for (int i = 1; i < kMaxProb; ++i)
+      if (i < g.n && L >= g.p[i].wg0) pi = i;
+    const WxProb& P = g.p[pi];
+    L -= P.wg0;
+    src_ = P.x; dyp = P.dy; outp = P.out;
+    Cin_ = P.Cin; K_ = P.Cin; KW_ = 1; pad_t_ = 0; pad_l_ = 0; st_ = P.stride; nseg_ = 1;
+    ld_dy_ = P.ld_dy; dy_coff_ = P.dy_coff; Cout_ = P.Cout; tiles_ = P.tiles; co_tiles_ = P.co_tiles;
+    nsplit_ = P.nsplit; chunk_ = P.chunk; direct_ = P.direct; beta_ = P.beta;
+    gm0 = 0; gm1 = P.m_total;
+    seg1.Hr = P.Hr; seg1.Wr = P.Wr; seg1.Hs = P.Hs; seg1.Ws = P.Ws; seg1.rows = P.B * P.Hr * P.Wr; seg1.m_start = 0;
+    seg1.src_base = 0; seg1.src_img = (long)P.Hs * P.Ws; seg1.dst_base = 0; seg1.dst_img = (long)P.Hr * P.Wr;
+  } else {
+    const ConvArgs& a = g.a;
+    src_ = a.src; dyp = g.dy; outp = nullptr;
+    Cin_ = a.Cin; K_ = a.K; KW_ = a.KW; pad_t_ = a.pad_t; pad_l_ = a.pad_l; st_ = a.stride; nseg_ = a.nseg;
+    ld_dy_ = g.ld_dy; dy_coff_ = g.dy_coff; Cout_ = g.Cout; tiles_ = g.tiles; co_tiles_ = g.co_tiles;
+    nsplit_ = g.nsplit; chunk_ = g.chunk; direct_ = g.direct; beta_ = g.beta;
+    gm0 = gm1 = 0;
+  }
+  auto seg_of = [&](int i) {
+    if constexpr (MP) {
+      return seg1;
+    } else {
+      const ConvSeg& q = g.a.seg[i];
+      WxSeg v;
+      v.Hr = q.Hr; v.Wr = q.Wr; v.Hs = q.Hs; v.Ws = q.Ws; v.rows = q.rows; v.m_start = q.m_start;
+      v.src_base = q.src_base; v.src_img = q.src_img; v.dst_base = q.dst_base; v.dst_img = q.dst_img;
+      return v;
+    }
+  };
+  auto seg_start = [&](int i) {
+    if constexpr (MP) return 0;
+    else return g.a.seg[i].m_start;
+  };
+  const int tile = L % tiles_, rest = L / tiles_;
+  const int split = rest % nsplit_;
+  if constexpr (!MP) {
+    grp = rest / nsplit_;
+    gm0 = g.g_m0[grp];
+    gm1 = g.g_m1[grp];
+    outp = g.out[grp];
+  }
+  const int co0 = (tile % co_tiles_) * BCO, k0 = (tile / co_tiles_) * BKK;
+  const int m_lo = gm0 + split * chunk_;
+  const int m_hi = min(m_lo + chunk_, gm1);
   const int nsteps = m_hi > m_lo ? (m_hi - m_lo) / SR : 0;
 
   // ---- per-lane DMA constants: rows rr + 8 RPI j of each step, 16-B piece pc of the row ---------
   const int rr = C::RPI * wave + lane / C::LPR, pc = lane % C::LPR;
   const int lp = pc ^ (rswz(rr) << 1);                    // logical piece (rswz(rr + 16) == rswz(rr))
-  const unsigned ycol = (unsigned)((g.dy_coff + co0 + lp * 8) * 2);
-  const bool yok = co0 + lp * 8 < g.Cout;                 // a 128-wide tile over a 64-channel output
+  const unsigned ycol = (unsigned)((dy_coff_ + co0 + lp * 8) * 2);
+  const bool yok = co0 + lp * 8 < Cout_;                  // a 128-wide tile over a 64-channel output
   const int kx = k0 + lp * 8;
-  const bool kok = kx < a.K;
-  const int tap = kok ? kx / a.Cin : 0;
-  const int ci = kx - tap * a.Cin;
-  const int tr_ = tap / a.KW, ts_ = tap - (tap / a.KW) * a.KW;
-  const int ry = tr_ - a.pad_t, rx = ts_ - a.pad_l;       // iy = oy * stride + ry
+  const bool kok = kx < K_;
+  const int tap = kok ? kx / Cin_ : 0;
+  const int ci = kx - tap * Cin_;
+  const int tr_ = tap / KW_, ts_ = tap - (tap / KW_) * KW_;
+  const int ry = tr_ - pad_t_, rx = ts_ - pad_l_;         // iy = oy * stride + ry
   const unsigned xcol = (unsigned)(ci * 2);
-  const int rowb = g.ld_dy * 2, pixb = a.Cin * 2;
-  const __amdgpu_buffer_rsrc_t rsY = __builtin_amdgcn_make_buffer_rsrc((void*)g.dy, (short)0, (int)kRecords, 0x00020000);
-  const __amdgpu_buffer_rsrc_t rsX = __builtin_amdgcn_make_buffer_rsrc((void*)a.src, (short)0, (int)kRecords, 0x00020000);
+  const int rowb = ld_dy_ * 2, pixb = Cin_ * 2;
+  const __amdgpu_buffer_rsrc_t rsY = __builtin_amdgcn_make_buffer_rsrc((void*)dyp, (short)0, (int)kRecords, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rsX = __builtin_amdgcn_make_buffer_rsrc((void*)src_, (short)0, (int)kRecords, 0x00020000);
 
   // ---- issue cursor ----------------------------------------------------------------------------
   // Per lane and DMA / load instruction j: the row's (local row, source iy, ix) and its two byte
@@ -132,18 +219,19 @@ __global__ void __launch_bounds__(NT) conv_wgrad_x_kernel(WxArgs g) {
   int rows = 0, Hs = 1, Ws = 1;
   int s_dx = 0, s_dy = 0, s_wr = 0, s_hr = 0, ixw = 0, iyh = 0;
   int DY0 = 0, DYQ = 0, DX0 = 0, DXY = 0, DXQ = 0;
-  const int st_ = a.stride;
   int cml[J], iyj[J], ixj[J], ybo[J], xbo[J];
   auto seek = [&](int m) {
     int sg = 0;
+    if constexpr (!MP) {
 #pragma unroll
-    for (int i = 1; i < kMaxSeg; ++i)
-      if (i < a.nseg && m >= a.seg[i].m_start) sg = i;
-    const ConvSeg& S = a.seg[sg];
+      for (int i = 1; i < kMaxSeg; ++i)
+        if (i < nseg_ && m >= seg_start(i)) sg = i;
+    }
+    const WxSeg S = seg_of(sg);
     const int Wr = S.Wr, Hr = S.Hr;
     Ws = S.Ws; Hs = S.Hs; rows = S.rows;
     const int sbase = (int)S.src_base, simg = (int)S.src_img, dbase = (int)S.dst_base, dimg = (int)S.dst_img;
-    seg_end = sg + 1 < a.nseg ? a.seg[sg + 1].m_start : 0x7fffffff;
+    seg_end = sg + 1 < nseg_ ? seg_start(sg + 1) : 0x7fffffff;
     const int HW = Hr * Wr;
     const int d_img = SR / HW;
     const int rem = SR - d_img * HW;
@@ -171,6 +259,12 @@ __global__ void __launch_bounds__(NT) conv_wgrad_x_kernel(WxArgs g) {
   };
   // one step's pieces: put(j, dY offset, x offset) per DMA / load instruction pair (kOOB: zeros)
   auto issue_step = [&](auto&& put) {
+    if (abl & 64) {                             // (measurement variant: no cursor arithmetic)
+#pragma unroll
+      for (int j = 0; j < J; ++j) put(j, kOOB, kOOB);
+      ++ist;
+      return;
+    }
     const bool live = ist < nsteps;
     if (live && im >= seg_end) seek(im);
 #pragma unroll
@@ -193,15 +287,16 @@ __global__ void __launch_bounds__(NT) conv_wgrad_x_kernel(WxArgs g) {
     ++ist;
   };
   // measurement builds: CVL_WGX_ABLATE bits (1 no fragment reads, 2 no memory traffic, 4 an
-  // L2-hot source window, 8 no x traffic, 16 no MFMAs)
-  const int abl = ST ? g.ablate : 0;
+  // L2-hot source window, 8 no x traffic, 16 no MFMAs, 32 no DMA instructions, 64 no cursor arithmetic,
+  // 128 no loop barriers)
   auto issue = [&]() {                          // DMA form: LDS-DMA into ring slot cslot
     cvl_bf16* Yb = lds + cslot * SLOT;
     cvl_bf16* Xb = Yb + YST;
     issue_step([&](int j, unsigned oy, unsigned ox) {
-      if (ST && (abl & 2)) { oy = kOOB; ox = kOOB; }            // no memory traffic (zeros)
-      if (ST && (abl & 4)) { oy &= 0x3fff0u; ox &= 0x3fff0u; }   // an L2-hot 256 KiB window
-      if (ST && (abl & 8)) ox = kOOB;                            // no x traffic
+      if (abl & 2) { oy = kOOB; ox = kOOB; }            // no memory traffic (zeros)
+      if (abl & 4) { oy &= 0x3fff0u; ox &= 0x3fff0u; }   // an L2-hot 256 KiB window
+      if (abl & 8) ox = kOOB;                            // no x traffic
+      if (abl & 32) return;                              // no DMA instructions at all
       dma16(rsY, Yb + (8 * C::RPI * j + C::RPI * wave) * BCO, oy);
       dma16(rsX, Xb + (8 * C::RPI * j + C::RPI * wave) * BKK, ox);
     });
@@ -217,6 +312,7 @@ __global__ void __launch_bounds__(NT) conv_wgrad_x_kernel(WxArgs g) {
 #pragma unroll
     for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
   auto bar = [&]() {
+    if (abl & 128) return;                      // (measurement variant: no barriers)
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
   };
@@ -324,11 +420,13 @@ __global__ void __launch_bounds__(NT) conv_wgrad_x_kernel(WxArgs g) {
     // x (B) fragments (every row uses all of them)
     s16x4 al[KS][TM], ah[KS][TM], bl[2][KS][TN], bh[2][KS][TN];
     auto rd_a = [&](unsigned base, int h, int i) {
+      if (abl & 1) return;
       const unsigned yo = base + h * BR * BCO * 2;
       al[h][i] = ds_tr16(yo + ya[i]);
       ah[h][i] = ds_tr16(yo + yb[i]);
     };
     auto rd_b = [&](unsigned base, int b) {
+      if (abl & 1) return;
 #pragma unroll
       for (int h = 0; h < KS; ++h) {
         const unsigned xo = base + h * BR * BKK * 2;
@@ -370,7 +468,8 @@ __global__ void __launch_bounds__(NT) conv_wgrad_x_kernel(WxArgs g) {
           const s16x8 fa = tr_join(al[h][i], ah[h][i]);
 #pragma unroll
           for (int j = 0; j < TN; ++j)
-            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, fa),
+            if (abl & 16) acc[i][j][0] += (float)(fa[0] + fb[j][0]);
+            else acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, fa),
                                                                  __builtin_bit_cast(bf16x8, fb[j]), acc[i][j], 0, 0, 0);
           __builtin_amdgcn_sched_barrier(0);
           if (h == 0 && i == 0) rd_b(nbase, b ^ 1);   // step t+1's x fragments, under the MFMAs
@@ -411,23 +510,23 @@ __global__ void __launch_bounds__(NT) conv_wgrad_x_kernel(WxArgs g) {
   if (stamp) stamp[2] = wall_clock64();
 
   // ---- epilogue: C[co][k] -> out[k][co] (HWIO), 4 consecutive co per lane -------------------------
-  float* out = g.out[grp] + (g.direct ? 0 : (size_t)split * a.K * g.Cout);
+  float* out = outp + (direct_ ? 0 : (size_t)split * K_ * Cout_);
 #pragma unroll
   for (int i = 0; i < TM; ++i)
 #pragma unroll
     for (int j = 0; j < TN; ++j) {
       const int k = k0 + wk * (BKK / 4) + j * 16 + lr;
       const int co = co0 + wco * (BCO / 2) + i * 16 + 4 * lg;
-      if (k >= a.K || co >= g.Cout) continue;
+      if (k >= K_ || co >= Cout_) continue;
       f32x4 v = acc[i][j];
-      if (co + 3 < g.Cout && (g.Cout & 3) == 0) {
-        f32x4* po = reinterpret_cast<f32x4*>(out + (size_t)k * g.Cout + co);
-        if (g.direct && g.beta != 0.f) v += g.beta * *po;
+      if (co + 3 < Cout_ && (Cout_ & 3) == 0) {
+        f32x4* po = reinterpret_cast<f32x4*>(out + (size_t)k * Cout_ + co);
+        if (direct_ && beta_ != 0.f) v += beta_ * *po;
         *po = v;
       } else {
-        for (int e = 0; e < 4 && co + e < g.Cout; ++e) {
-          float* po = out + (size_t)k * g.Cout + co + e;
-          *po = (g.direct && g.beta != 0.f) ? v[e] + g.beta * *po : v[e];
+        for (int e = 0; e < 4 && co + e < Cout_; ++e) {
+          float* po = out + (size_t)k * Cout_ + co + e;
+          *po = (direct_ && beta_ != 0.f) ? v[e] + beta_ * *po : v[e];
         }
       }
     }
@@ -620,6 +719,204 @@ int cvl_conv_wgrad_x(const cvl_conv_desc* d, int ngroups, const void* x, const v
   if (st || g.direct) return st;
   return cvl_wgrad_reduce((const float*)workspace, dw[0], ngroups > 1 ? dw[1] : dw[0], (long)g.a.K * g.Cout / 4,
                           p.nsplit, ngroups, beta, s);
+}
+
+// ---- batched 1x1 weight gradients (cvl_conv_wgrad_batch) -------------------------------------------
+namespace {
+
+// tile width of a batched problem: 256 (the tower kernel's tile, ~2x its MFMA rate per CU) when
+// both GEMM sides fill it (Npad % 256 == 0, Cin >= 256: the conv4_x / conv5_x 1x1 convs and the
+// 256 -> 512 projections), else 128; one launch per tile width
+inline int wx_batch_t(const cvl_conv_desc* d, const ConvArgs& a) {
+  return (a.Npad % 256 == 0 && d->Cin >= 256 && !cvl_dispatch_flag("wgb_no_256")) ? 256 : 128;
+}
+
+// a problem the batched kernel takes: bf16, one dense segment (bases 0, rows = images x map), 1x1,
+// pad 0, stride 1 or 2, the wgrad_x operand constraints (16-B dY / x pieces, 32-bit offsets)
+bool wx_batch_ok(const cvl_conv_desc* d, ConvArgs* a) {
+  if (!d || d->prec != CVL_PREC_BF16 || d->mode != CVL_CONV_FWD || d->nseg != 1 || d->KH != 1 || d->KW != 1 ||
+      d->pad_t || d->pad_l || (d->stride != 1 && d->stride != 2) || d->relu_in)
+    return false;
+  if (cvl_conv_prepare(d, SEGM, a)) return false;
+  const cvl_conv_seg& q = d->seg[0];
+  if (a->Npad % 64 || d->Cin % 8 || d->n_store % 4 || d->ld_dst % 8 || d->dst_coff % 8 || a->m_total < 1024)
+    return false;
+  if (q.src_base || q.dst_base || q.src_img != (int64_t)q.Hs * q.Ws || q.dst_img != (int64_t)q.Hr * q.Wr) return false;
+  if (q.Hr != (q.Hs + d->stride - 1) / d->stride || q.Wr != (q.Ws + d->stride - 1) / d->stride) return false;
+  const long dy_end = (long)d->B * q.dst_img * d->ld_dst * 2, src_end = (long)d->B * q.src_img * d->Cin * 2;
+  return dy_end < (long)kRecords - 65536 && src_end < (long)kRecords - 65536;
+}
+
+// Plan of one launch over problems idx[0..n): a common chunk length (rows per workgroup) for all of
+// them, chosen by the same cost model as wx_plan -- rounds of one workgroup per CU x (fixed cost +
+// 64-row steps) + the fp32 slab round trip of split problems.  Measured (round 6, 1x1 1024->256 @
+// 32x32 at 16 / 8 / 4 / 2 / 1 splits: 20.6 / 29.5 / 48.2 / 89.1 / 171 us): ~7.2 us per workgroup
+// round + ~0.64 us per step.
+struct WxBatchPlan {
+  WxBatchArgs g;
+  size_t slab_off[kMaxProb];               // byte offset of problem i's slab in the workspace
+  size_t bytes;                            // workspace bytes of the slabs
+  int wgs;
+};
+
+void wx_batch_plan(const cvl_conv_desc* const* d, const int* idx, int n, int T, WxBatchPlan* pl) {
+  ConvArgs a[kMaxProb];
+  int tiles[kMaxProb], mt[kMaxProb], maxm = 0;
+  for (int i = 0; i < n; ++i) {
+    wx_batch_ok(d[idx[i]], &a[i]);
+    tiles[i] = ((a[i].Npad + T - 1) / T) * ((a[i].K + T - 1) / T);
+    mt[i] = a[i].m_total;
+    maxm = mt[i] > maxm ? mt[i] : maxm;
+  }
+  static const int ncu = cvl_device_cus();
+  // per-row costs: 128-wide tile ~0.64 us per 64-row step; 256-wide ~0.54 us per 32-row step (the
+  // tower's weight gradient: 390 steps in ~210 us)
+  const double fix = cvl_tune_int("CVL_WGB_FIX", 720) / 100.0;
+  const double step = T == 256 ? cvl_tune_int("CVL_WGB_STEP256", 54) / 100.0 : cvl_tune_int("CVL_WGB_STEP", 64) / 100.0;
+  const int srows = T == 256 ? BR : 64;
+  const double slab_us = (double)T * T * 4 * 2 / 5.0e6;
+  int best_c = maxm;
+  double best_t = 1e30;
+  for (int c = SEGM; ; c *= 2) {
+    const int cc = c < maxm ? c : maxm;
+    long w = 0, sl = 0;
+    for (int i = 0; i < n; ++i) {
+      const int sp = (mt[i] + cc - 1) / cc;
+      w += (long)tiles[i] * sp;
+      if (sp > 1) sl += (long)tiles[i] * sp;
+    }
+    const double t = (double)((w + ncu - 1) / ncu) * (fix + (cc / srows) * step) + sl * slab_us;
+    if (t < best_t) {
+      best_t = t;
+      best_c = cc;
+    }
+    if (cc >= maxm) break;
+  }
+  const int forced = cvl_tune_int("CVL_WGB_CHUNK", 0);   // measurement: rows per workgroup
+  if (forced > 0) best_c = (forced + SEGM - 1) / SEGM * SEGM;
+  pl->g.n = n;
+  pl->g.stamps = nullptr;
+  pl->g.phase = nullptr;
+  pl->g.ablate = 0;
+  size_t off = 0;
+  int wg = 0;
+  for (int i = 0; i < n; ++i) {
+    const cvl_conv_desc* q = d[idx[i]];
+    WxProb& P = pl->g.p[i];
+    P.Hr = q->seg[0].Hr; P.Wr = q->seg[0].Wr; P.Hs = q->seg[0].Hs; P.Ws = q->seg[0].Ws;
+    P.B = q->B; P.Cin = q->Cin; P.stride = q->stride;
+    P.Cout = q->n_store; P.ld_dy = q->ld_dst; P.dy_coff = q->dst_coff;
+    P.co_tiles = (a[i].Npad + T - 1) / T;
+    P.tiles = tiles[i];
+    P.chunk = best_c;
+    P.nsplit = (mt[i] + best_c - 1) / best_c;
+    P.direct = P.nsplit == 1;
+    P.m_total = mt[i];
+    P.wg0 = wg;
+    wg += P.tiles * P.nsplit;
+    pl->slab_off[i] = off;
+    if (!P.direct) off += ((size_t)P.nsplit * a[i].K * P.Cout * sizeof(float) + 255) & ~(size_t)255;
+  }
+  for (int i = n; i < kMaxProb; ++i) pl->g.p[i].wg0 = 0x7fffffff;
+  pl->bytes = off;
+  pl->wgs = wg;
+}
+
+// problems of the batch in launch groups of <= kMaxProb eligible ones of one tile width (256-wide
+// groups first), the rest individually (f(nullptr, {i}, 1, 0)); the workspace holds each launch
+// group's slabs, then each individual problem's own workspace, in this order
+template <typename F>
+int wx_batch_walk(const cvl_conv_desc* const* d, int n, F&& f) {
+  ConvArgs a;
+  for (int T = 256; T >= 128; T /= 2) {
+    int idx[kMaxProb], k = 0;
+    for (int i = 0; i < n; ++i) {
+      if (!wx_batch_ok(d[i], &a) || wx_batch_t(d[i], a) != T) continue;
+      idx[k++] = i;
+      if (k == kMaxProb) {
+        const int st = f(d, idx, k, T);
+        if (st) return st;
+        k = 0;
+      }
+    }
+    if (k) {
+      const int st = f(d, idx, k, T);
+      if (st) return st;
+    }
+  }
+  for (int i = 0; i < n; ++i) {
+    if (wx_batch_ok(d[i], &a)) continue;
+    const int st = f(nullptr, &i, 1, 0);           // individual
+    if (st) return st;
+  }
+  return CVL_OK;
+}
+
+}  // namespace
+
+extern "C" size_t cvl_conv_wgrad_batch_workspace_size(const cvl_conv_desc* const* d, int n) {
+  if (!d || n < 1) return 16;
+  size_t total = 0;
+  wx_batch_walk(d, n, [&](const cvl_conv_desc* const* dd, const int* idx, int k, int T) {
+    if (!dd) {
+      total += (cvl_conv_wgrad_workspace_size(d[idx[0]]) + 255) & ~(size_t)255;
+    } else {
+      WxBatchPlan pl;
+      wx_batch_plan(dd, idx, k, T, &pl);
+      total += pl.bytes;
+    }
+    return CVL_OK;
+  });
+  return total > 16 ? total : 16;
+}
+
+extern "C" int cvl_conv_wgrad_batch(const cvl_conv_desc* const* d, int n, const void* const* x, const void* const* dy,
+                                    float* const* dw, float beta, void* workspace, size_t workspace_bytes,
+                                    cvl_stream_t stream) {
+  CVL_CHECK_ARG(d && x && dy && dw && n >= 1);
+  for (int i = 0; i < n; ++i) {
+    CVL_CHECK_ARG(d[i] && x[i] && dy[i] && dw[i]);
+    for (int j = 0; j < i; ++j) CVL_CHECK_ARG(dw[j] != dw[i]);
+  }
+  CVL_CHECK_ARG(workspace && workspace_bytes >= cvl_conv_wgrad_batch_workspace_size(d, n));
+  hipStream_t s = (hipStream_t)stream;
+  for (int i = 0; i < n; ++i) {                   // a pending reduction into one of these dW lands first
+    const int gs = cvl_wgrad_defer_guard(dw[i], s);
+    if (gs) return gs;
+  }
+  char* ws = reinterpret_cast<char*>(workspace);
+  size_t used = 0;
+  return wx_batch_walk(d, n, [&](const cvl_conv_desc* const* dd, const int* idx, int k, int T) {
+    const int i0 = idx[0];
+    if (!dd) {                                    // a problem the batched kernel does not take
+      const size_t w = cvl_conv_wgrad_workspace_size(d[i0]);
+      const int st = cvl_conv_wgrad(d[i0], x[i0], dy[i0], dw[i0], beta, ws + used, w, stream);
+      used += (w + 255) & ~(size_t)255;
+      return st;
+    }
+    WxBatchPlan pl;
+    wx_batch_plan(dd, idx, k, T, &pl);
+    for (int i = 0; i < k; ++i) {
+      WxProb& P = pl.g.p[i];
+      P.x = reinterpret_cast<const cvl_bf16*>(x[idx[i]]);
+      P.dy = reinterpret_cast<const cvl_bf16*>(dy[idx[i]]);
+      P.out = P.direct ? dw[idx[i]] : reinterpret_cast<float*>(ws + used + pl.slab_off[i]);
+      P.beta = beta;
+    }
+    g_cvl_conv_last_kernel = CVL_CK_WG_X;
+    if (T == 256)
+      hipLaunchKernelGGL((conv_wgrad_x_kernel<256, BR, false, true, WxBatchArgs>), dim3(pl.wgs), dim3(NT), 0, s, pl.g);
+    else
+      hipLaunchKernelGGL((conv_wgrad_x_kernel<128, 64, false, true, WxBatchArgs>), dim3(pl.wgs), dim3(NT), 0, s, pl.g);
+    int st = cvl_launch_status();
+    for (int i = 0; !st && i < k; ++i) {
+      const WxProb& P = pl.g.p[i];
+      if (P.direct) continue;
+      st = cvl_wgrad_reduce(P.out, dw[idx[i]], dw[idx[i]], (long)P.Cin * P.Cout / 4, P.nsplit, 1, beta, s);
+    }
+    used += pl.bytes;
+    return st;
+  });
 }
 
 #ifdef CVL_MEASURE

@@ -57,6 +57,8 @@ SIGNATURES = {
     "cvl_conv_wgrad": (c_int, [P, P, P, P, c_float, P, c_size_t, P]),
     "cvl_conv_wgrad_grouped_workspace_size": (c_size_t, [P, c_int]),
     "cvl_conv_wgrad_grouped": (c_int, [P, c_int, P, P, P, c_float, P, c_size_t, P]),
+    "cvl_conv_wgrad_batch_workspace_size": (c_size_t, [P, c_int]),
+    "cvl_conv_wgrad_batch": (c_int, [P, c_int, P, P, P, c_float, P, c_size_t, P]),
     "cvl_pack_conv_weights": (c_int, [P, c_int, c_int, c_int, c_int, c_int, c_int, P, c_int, c_int, P, P]),
     "cvl_pack_conv_weights_multi": (c_int, [P, P, c_int, P]),
     "cvl_im2col": (c_int, [P, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int,

@@ -216,7 +216,10 @@ class Conv(object):
         Ho, Wo, _, _ = self.out_hw(H, W)
         d = self.fwd_desc(B, [nn.seg(Ho, Wo, H, W, self.wf, None)], ld_dst=self.cout_pad_ld(dy),
                           relu_in=relu_in)
-        nn.conv_wgrad(d, x, dy, self.dw if dw is None else dw, beta)
+        if _wgb is not None and self.k == 1 and beta == 0.0 and not relu_in and x.dtype == BF16:
+            _wgb.append((d, x, dy, self.dw if dw is None else dw))     # launched by flush_wgrad_batch()
+        else:
+            nn.conv_wgrad(d, x, dy, self.dw if dw is None else dw, beta)
         if self.has_bias and bias:
             nn.bias_grad(dy, self.cout_pad_ld(dy), 0, self.cout, 0, Ho * Wo, Ho * Wo, B, self.db)
 
@@ -251,6 +254,42 @@ class Conv(object):
 FUSE_BNSUM = not _lib.dispatch("no_bnsum_fuse")
 # ... and a residual unit's (BN3) first pass into the next block's conv1 data gradient (CVL_DISPATCH=no_bnsum_res: off)
 FUSE_BNSUM_RES = FUSE_BNSUM and not _lib.dispatch("no_bnsum_res")
+
+# Batched 1x1 weight gradients (round 6; CVL_DISPATCH=no_wgrad_batch: off).  Inside `with
+# wgrad_batch():` Conv.wgrad collects its 1x1 bf16 problems (keeping their x / dy alive) instead of
+# launching them; the exit (or flush_wgrad_batch()) hands all of them to ONE cvl_conv_wgrad_batch call:
+# one launch per ResNet stage instead of one per conv, with fewer splits per problem.
+WGRAD_BATCH = not _lib.dispatch("no_wgrad_batch")
+_wgb = None
+
+
+class wgrad_batch(object):
+    def __enter__(self):
+        global _wgb
+        self.own = _wgb is None and WGRAD_BATCH
+        if self.own:
+            _wgb = []
+        return self
+
+    def __exit__(self, exc_type, *exc):
+        global _wgb
+        if self.own:
+            try:
+                if exc_type is None:
+                    flush_wgrad_batch()
+            finally:
+                _wgb = None
+        return False
+
+
+def flush_wgrad_batch():
+    """Launch the collected weight gradients (no-op outside wgrad_batch / when none)."""
+    if _wgb:
+        items = list(_wgb)
+        del _wgb[:]
+        nn.conv_wgrad_batch([i[0] for i in items], [i[1] for i in items], [i[2] for i in items],
+                            [i[3] for i in items])
+
 
 class StatsArena(object):
     """One zeroed buffer holding the (sum, sumsq) BN statistics of every conv of a forward pass as

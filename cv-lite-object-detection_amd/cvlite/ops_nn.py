@@ -148,6 +148,26 @@ def conv_wgrad_grouped(desc, x, dy, dws, beta=0.0):
         _wgrad_pending.append(ws)
 
 
+def conv_wgrad_batch(descs, xs, dys, dws, beta=0.0):
+    """Weight gradients of several convolutions in one call (cvl_conv_wgrad_batch): every 1x1 bf16
+    problem of the list shares one launch, the rest run one by one -- as conv_wgrad for each."""
+    n = len(descs)
+    if n == 0:
+        return
+    for d, x in zip(descs, xs):
+        _prec(d, x)
+    lib = _lib.load()
+    darr = (c_void_p * n)(*[ctypes.addressof(d) for d in descs])
+    nb = int(lib.cvl_conv_wgrad_batch_workspace_size(darr, n))
+    ws = torch.empty(max(nb, 16), dtype=torch.uint8, device=xs[0].device)
+    xa = (c_void_p * n)(*[t.data_ptr() for t in xs])
+    ya = (c_void_p * n)(*[t.data_ptr() for t in dys])
+    wa = (c_void_p * n)(*[t.data_ptr() for t in dws])
+    _lib.call("cvl_conv_wgrad_batch", darr, n, xa, ya, wa, float(beta), ptr(ws), ws.numel(), stream())
+    if _wgrad_pending is not None:
+        _wgrad_pending.append(ws)
+
+
 def pack_conv_weights(w_hwio, KH, KW, Cin, Cout, Cin_k, Npad, w_fwd, Cin_pad=0, Cout_pad=0, w_dgrad=None):
     _lib.call("cvl_pack_conv_weights", ptr(w_hwio), KH, KW, Cin, Cout, Cin_k, Npad, ptr(w_fwd),
               Cin_pad, Cout_pad, ptr(w_dgrad), stream())

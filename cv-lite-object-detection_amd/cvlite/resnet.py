@@ -13,7 +13,7 @@ import os
 import torch
 
 from . import ops_nn as nn
-from .layers import BF16, BatchNorm, Conv, ConvBN, StatsArena
+from .layers import BF16, BatchNorm, Conv, ConvBN, StatsArena, wgrad_batch
 from . import _lib
 
 STEM_K = 7
@@ -256,16 +256,18 @@ class ResNet50(object):
         for si in range(3, -1, -1):
             st = self.stages[si]
             pending = None          # the next-processed block's conv3 BN first pass, fused upstream
-            for bi in range(len(st) - 1, -1, -1):
-                # an identity predecessor's conv3 BN first pass rides on this block's conv1 dgrad
-                prev = st[bi - 1].c3.bn_res_ctx(ssv[si][bi - 1][3], arena) if bi >= 1 else None
-                if bi == 0 and (si - 1) in dC:
-                    # this block's input is the previous stage's tap (C3 / C4), whose buffer
-                    # already holds the FPN lateral's gradient: accumulate into it
-                    dh, pending = st[bi].backward(dh, ssv[si][bi], dx_out=dC[si - 1], dx_beta=1.0, arena=arena,
-                                                  sums3=pending, prev_ctx=prev)
-                else:
-                    dh, pending = st[bi].backward(dh, ssv[si][bi], arena=arena, sums3=pending, prev_ctx=prev)
+            # the stage's 1x1 weight gradients: one batched launch at the stage's end (layers.wgrad_batch)
+            with wgrad_batch():
+                for bi in range(len(st) - 1, -1, -1):
+                    # an identity predecessor's conv3 BN first pass rides on this block's conv1 dgrad
+                    prev = st[bi - 1].c3.bn_res_ctx(ssv[si][bi - 1][3], arena) if bi >= 1 else None
+                    if bi == 0 and (si - 1) in dC:
+                        # this block's input is the previous stage's tap (C3 / C4), whose buffer
+                        # already holds the FPN lateral's gradient: accumulate into it
+                        dh, pending = st[bi].backward(dh, ssv[si][bi], dx_out=dC[si - 1], dx_beta=1.0, arena=arena,
+                                                      sums3=pending, prev_ctx=prev)
+                    else:
+                        dh, pending = st[bi].backward(dh, ssv[si][bi], arena=arena, sums3=pending, prev_ctx=prev)
             if si > 0:
                 hook("conv%d" % (si + 2))     # this stage's weight gradients are final
         self.stem.backward(dh, sv_stem)

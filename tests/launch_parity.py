@@ -420,6 +420,18 @@ def check_conv_wgrad_grouped(lp, name, launch, desc, x, dy, dws, beta=0.0):
                   _wgrad_ref(desc, sg, x, dy))
 
 
+def check_conv_wgrad_batch(lp, name, launch, descs, xs, dys, dws, beta=0.0):
+    """cvl_conv_wgrad_batch: every problem's dW against its own float64 restatement."""
+    olds = [d.clone() for d in dws] if beta != 0.0 else [None] * len(dws)
+    launch(descs, xs, dys, dws, beta)
+    kern = lp.last_kernel()
+    lp.flush_wgrad()
+    for i, (desc, x, dy, dw) in enumerate(zip(descs, xs, dys, dws)):
+        segs = _segs(desc)
+        _check_dw(lp, name, _wgrad_detail(desc, segs) + " batch%d/%d" % (i, len(descs)), kern, dw, olds[i], beta,
+                  _wgrad_ref(desc, segs, x, dy))
+
+
 def _bnsum_ref(lp, name, detail, kern, sums, dst_rows, idx_b, z, mr, gamma, beta, act_hi, ymask, B, C, HW):
     """(sum g, sum g*xhat) per (image, channel); g = dst * mask (mask from y > 0, or rebuilt from
     z as the kernels do), computed on the launch's own stored destination."""
@@ -1161,6 +1173,7 @@ CHECKS = {
     "conv_igemm": check_conv_igemm,
     "conv_wgrad": check_conv_wgrad,
     "conv_wgrad_grouped": check_conv_wgrad_grouped,
+    "conv_wgrad_batch": check_conv_wgrad_batch,
     "conv_igemm_dgrad_bnsum": check_dgrad_bnsum,
     "conv_igemm_dgrad_bnsum_res": check_dgrad_bnsum_res,
     "pack_conv_weights": check_pack_conv_weights,
