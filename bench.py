@@ -31,6 +31,7 @@ import torch  # noqa: E402
 from cvlite import dist  # noqa: E402
 from cvlite import ops_nn as nn  # noqa: E402
 from cvlite.fcos_net import FCOSNet  # noqa: E402
+from cvlite.layers import WGRAD_BATCH  # noqa: E402
 from cvlite.train_fcos import FCOSTrainer, synthetic_batch  # noqa: E402
 
 METRIC = "training images/sec (whole node), FCOS-VOC 512x512 bs=16/GPU"
@@ -167,16 +168,20 @@ def measure_backbone_3x3(net, B, H, W, iters=20, eager=False):
         mr[..., 0] = 0.0
         mr[..., 1] = 1.0
         sums = nn.bn_acc(B, C, dev)
-        dwb = torch.zeros_like(conv.dw)
+        n = len(stage)
+        dwb = [torch.zeros_like(conv.dw) for _ in range(n)]
         fd = conv.fwd_desc(B, [nn.seg(h, w, h, w, conv.wf, conv.bias_arg())], ld_dst=conv.cout)
         dd = conv.dgrad_desc(B, [nn.seg(h, w, h, w, conv.wd)], ld_dst=C)
         wd = conv.fwd_desc(B, [nn.seg(h, w, h, w, conv.wf, None)], ld_dst=conv.cout_pad)
         flops = 2.0 * B * h * w * 9 * C * conv.cout
-        for kind, fn in (("fwd", lambda: nn.conv_igemm(fd, x, y, st)),
-                         ("dgrad", lambda: nn.conv_igemm_dgrad_bnsum(dd, dy, dx, x, mr, bn.gamma, bn.beta, sums)),
-                         ("wgrad", lambda: nn.conv_wgrad(wd, x, dy, dwb))):
+        # the weight gradients as the step runs them (round 6): the stage's n units in one batched call
+        # (cvl_conv_wgrad_batch, one launch + the split reductions), timed per unit
+        for kind, fn, per in (("fwd", lambda: nn.conv_igemm(fd, x, y, st), 1),
+                              ("dgrad", lambda: nn.conv_igemm_dgrad_bnsum(dd, dy, dx, x, mr, bn.gamma, bn.beta, sums), 1),
+                              ("wgrad", (lambda: nn.conv_wgrad_batch([wd] * n, [x] * n, [dy] * n, dwb)) if WGRAD_BATCH
+                               else (lambda: nn.conv_wgrad(wd, x, dy, dwb[0])), n if WGRAD_BATCH else 1)):
             t, kname = timed(fn)
-            n = len(stage)
+            t /= per
             rows.append({"shape": "%s 3x3 %d->%d @ %dx%d" % (kind, C, conv.cout, h, w), "count": n,
                          "us": round(t * 1e6, 2), "frac": round(flops / t / 1e12 / PEAK_BF16_TFLOPS, 4),
                          "kernel": kname.split(" (")[0]})
@@ -186,7 +191,8 @@ def measure_backbone_3x3(net, B, H, W, iters=20, eager=False):
             "unit": "TFLOP/s", "peak": PEAK_BF16_TFLOPS, "launches": 48, "ms_per_step": round(tot_t * 1e3, 4),
             "gflop_per_step": round(tot_f / 1e9, 2),
             "timing": "each distinct launch captured 20x into a HIP graph and the graph replayed alone (HIP events "
-                      "on its stream) after the timed steps; "
+                      "on its stream) after the timed steps; the weight gradients as the step runs them: a stage's "
+                      "units in one batched call (cvl_conv_wgrad_batch), time per unit; "
                       "counts from the ResNet-50 stage depths (3/4/6/3)", "per_shape": rows}
 
 

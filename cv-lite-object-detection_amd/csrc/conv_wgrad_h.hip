@@ -19,6 +19,8 @@
 //   every 32-lane transposed read conflict-free under any tap shift.
 // * Chunks of steps are spread over workgroups to fill the GPU; partial tiles go to fp32 slabs
 //   summed in a fixed order (deterministic), or straight into dW (with beta) for one chunk.
+#include <type_traits>
+
 #include "conv_common.h"
 
 namespace {
@@ -50,12 +52,34 @@ struct WhArgs {
   float beta;
 };
 
-__global__ void __launch_bounds__(NT) conv_wgrad_h_kernel(WhArgs g) {
+// Batched form (round 6, cvl_conv_wgrad_batch): the 3x3 weight gradients of a ResNet stage's
+// units in ONE launch; workgroup L (after the XCD remap) works on the problem whose [wg0, wg0 +
+// tiles * nsplit) range holds it, with that problem's own arguments.
+constexpr int kMaxWhProb = 12;
+struct WhBatch {
+  WhArgs p[kMaxWhProb];
+  int wg0[kMaxWhProb];
+  int n;
+};
+
+template <typename Args>
+__global__ void __launch_bounds__(NT) conv_wgrad_h_kernel(Args ga) {
   __shared__ __attribute__((aligned(16))) char lds[2 * STAGE_B];
   const int tid = threadIdx.x;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
+  int L = xcd_remap(blockIdx.x, gridDim.x);
+  WhArgs g;
+  if constexpr (std::is_same<Args, WhBatch>::value) {
+    int pi = 0;
+#pragma unroll
+    for (int i = 1; i < kMaxWhProb; ++i)
+      if (i < ga.n && L >= ga.wg0[i]) pi = i;
+    L -= ga.wg0[pi];
+    g = ga.p[pi];
+  } else {
+    g = ga;
+  }
   const int tiles = g.ci_tiles * g.co_tiles;
-  const int L = xcd_remap(blockIdx.x, gridDim.x);
   const int tile = L % tiles, split = L / tiles;      // the tiles of one chunk share an XCD's L2
   const int ci0 = (tile % g.ci_tiles) * BCI, co0 = (tile / g.ci_tiles) * BCO;
   const int s0 = split * g.chunk, s1 = min(s0 + g.chunk, g.steps);
@@ -282,8 +306,112 @@ int cvl_conv_wgrad_h(const cvl_conv_desc* d, int ngroups, const void* x, const v
     const int gs = cvl_wgrad_defer_guard(dw[0], s);
     if (gs) return gs;
   }
-  hipLaunchKernelGGL(conv_wgrad_h_kernel, dim3(g.ci_tiles * g.co_tiles * pl.nsplit), dim3(NT), 0, s, g);
+  hipLaunchKernelGGL(conv_wgrad_h_kernel<WhArgs>, dim3(g.ci_tiles * g.co_tiles * pl.nsplit), dim3(NT), 0, s, g);
   int st = cvl_launch_status();
   if (st || g.direct) return st;
   return cvl_wgrad_reduce((const float*)workspace, dw[0], dw[0], 9L * d->Cin * d->n_store / 4, pl.nsplit, 1, beta, s);
+}
+
+// ---- batched 3x3 weight gradients (cvl_conv_wgrad_batch) --------------------------------------------
+// problems wh_plan takes; a common chunk (128-row steps per workgroup) for the launch from the cost
+// model rounds x (fixed + chunk x step) + slab round trips (defaults: CVL_WGHB_FIX / _STEP, us x 100)
+bool cvl_wgrad_h_batch_ok(const cvl_conv_desc* d) {
+  WhPlan pl;
+  return d && wh_plan(d, 1, &pl);
+}
+
+int cvl_wgrad_h_batch_max() { return kMaxWhProb; }
+
+namespace {
+struct WhBatchPlan {
+  WhBatch b;
+  size_t slab_off[kMaxWhProb];
+  size_t bytes;
+  int wgs;
+};
+
+void wh_batch_plan(const cvl_conv_desc* const* d, const int* idx, int n, WhBatchPlan* pl) {
+  int tiles[kMaxWhProb], steps[kMaxWhProb], maxs = 1;
+  for (int i = 0; i < n; ++i) {
+    const cvl_conv_desc* q = d[idx[i]];
+    tiles[i] = (q->Cin / BCI) * (q->n_store / BCO);
+    steps[i] = q->B * q->seg[0].Hr * q->seg[0].Wr / RS;
+    maxs = steps[i] > maxs ? steps[i] : maxs;
+  }
+  static const int ncu = cvl_device_cus();
+  const double fix = cvl_tune_int("CVL_WGHB_FIX", 800) / 100.0, step = cvl_tune_int("CVL_WGHB_STEP", 300) / 100.0;
+  const double slab_us = (double)9 * BCI * BCO * 4 * 2 / 5.0e6;
+  int best_c = maxs;
+  double best_t = 1e30;
+  for (int c = 1;; c *= 2) {
+    const int cc = c < maxs ? c : maxs;
+    long w = 0, sl = 0;
+    for (int i = 0; i < n; ++i) {
+      const int sp = (steps[i] + cc - 1) / cc;
+      w += (long)tiles[i] * sp;
+      if (sp > 1) sl += (long)tiles[i] * sp;
+    }
+    const double t = (double)((w + ncu - 1) / ncu) * (fix + cc * step) + sl * slab_us;
+    if (t < best_t) {
+      best_t = t;
+      best_c = cc;
+    }
+    if (cc >= maxs) break;
+  }
+  const int forced = cvl_tune_int("CVL_WGHB_CHUNK", 0);
+  if (forced > 0) best_c = forced;
+  size_t off = 0;
+  int wg = 0;
+  for (int i = 0; i < n; ++i) {
+    const cvl_conv_desc* q = d[idx[i]];
+    const cvl_conv_seg& sq = q->seg[0];
+    WhArgs& g = pl->b.p[i];
+    g.src_base = sq.src_base; g.src_img = sq.src_img; g.dst_base = sq.dst_base; g.dst_img = sq.dst_img;
+    g.B = q->B; g.H = sq.Hr; g.W = sq.Wr; g.Cin = q->Cin; g.Cout = q->n_store;
+    g.ld_dy = q->ld_dst; g.dy_coff = q->dst_coff;
+    g.ci_tiles = q->Cin / BCI; g.co_tiles = q->n_store / BCO;
+    g.steps = steps[i];
+    g.chunk = best_c < steps[i] ? best_c : steps[i];
+    g.nsplit = (steps[i] + g.chunk - 1) / g.chunk;
+    g.direct = g.nsplit == 1;
+    pl->b.wg0[i] = wg;
+    wg += tiles[i] * g.nsplit;
+    pl->slab_off[i] = off;
+    if (!g.direct) off += ((size_t)g.nsplit * 9 * q->Cin * q->n_store * sizeof(float) + 255) & ~(size_t)255;
+  }
+  for (int i = n; i < kMaxWhProb; ++i) pl->b.wg0[i] = 0x7fffffff;
+  pl->b.n = n;
+  pl->bytes = off;
+  pl->wgs = wg;
+}
+}  // namespace
+
+size_t cvl_wgrad_h_batch_workspace(const cvl_conv_desc* const* d, const int* idx, int n) {
+  WhBatchPlan pl;
+  wh_batch_plan(d, idx, n, &pl);
+  return pl.bytes;
+}
+
+// n problems (all cvl_wgrad_h_batch_ok) in one launch; slabs in workspace (>= the size above)
+int cvl_wgrad_h_batch(const cvl_conv_desc* const* d, const int* idx, int n, const void* const* x, const void* const* dy,
+                      float* const* dw, float beta, void* workspace, hipStream_t s) {
+  WhBatchPlan pl;
+  wh_batch_plan(d, idx, n, &pl);
+  char* ws = reinterpret_cast<char*>(workspace);
+  for (int i = 0; i < n; ++i) {
+    WhArgs& g = pl.b.p[i];
+    g.x = reinterpret_cast<const cvl_bf16*>(x[idx[i]]);
+    g.dy = reinterpret_cast<const cvl_bf16*>(dy[idx[i]]);
+    g.out = g.direct ? dw[idx[i]] : reinterpret_cast<float*>(ws + pl.slab_off[i]);
+    g.beta = beta;
+  }
+  g_cvl_conv_last_kernel = CVL_CK_WG_H;
+  hipLaunchKernelGGL(conv_wgrad_h_kernel<WhBatch>, dim3(pl.wgs), dim3(NT), 0, s, pl.b);
+  int st = cvl_launch_status();
+  for (int i = 0; !st && i < n; ++i) {
+    const WhArgs& g = pl.b.p[i];
+    if (g.direct) continue;
+    st = cvl_wgrad_reduce(g.out, dw[idx[i]], dw[idx[i]], 9L * g.Cin * g.Cout / 4, g.nsplit, 1, beta, s);
+  }
+  return st;
 }

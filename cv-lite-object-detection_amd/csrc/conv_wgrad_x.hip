@@ -822,12 +822,44 @@ void wx_batch_plan(const cvl_conv_desc* const* d, const int* idx, int n, int T, 
   pl->wgs = wg;
 }
 
-// problems of the batch in launch groups of <= kMaxProb eligible ones of one tile width (256-wide
-// groups first), the rest individually (f(nullptr, {i}, 1, 0)); the workspace holds each launch
+}  // namespace
+
+bool cvl_wgrad_h_batch_ok(const cvl_conv_desc* d);            // conv_wgrad_h.hip
+int cvl_wgrad_h_batch_max();
+size_t cvl_wgrad_h_batch_workspace(const cvl_conv_desc* const* d, const int* idx, int n);
+int cvl_wgrad_h_batch(const cvl_conv_desc* const* d, const int* idx, int n, const void* const* x, const void* const* dy,
+                      float* const* dw, float beta, void* workspace, hipStream_t s);
+
+namespace {
+
+// problems of the batch in launch groups: <= kMaxProb 1x1 problems of one tile width (256-wide
+// groups first; f(d, idx, k, T)), then the 3x3 problems the halo weight-gradient kernel takes
+// (f(d, idx, k, 3)), the rest individually (f(nullptr, {i}, 1, 0)); the workspace holds each launch
 // group's slabs, then each individual problem's own workspace, in this order
+bool wx_batch_wh(const cvl_conv_desc* d) {
+  return !cvl_dispatch_flag("wgb_no_h") && d->prec == CVL_PREC_BF16 && cvl_wgrad_h_batch_ok(d);
+}
+
 template <typename F>
 int wx_batch_walk(const cvl_conv_desc* const* d, int n, F&& f) {
   ConvArgs a;
+  {
+    const int mh = cvl_wgrad_h_batch_max();
+    int idx[kMaxProb], k = 0;
+    for (int i = 0; i < n; ++i) {
+      if (wx_batch_ok(d[i], &a) || !wx_batch_wh(d[i])) continue;
+      idx[k++] = i;
+      if (k == mh) {
+        const int st = f(d, idx, k, 3);
+        if (st) return st;
+        k = 0;
+      }
+    }
+    if (k) {
+      const int st = f(d, idx, k, 3);
+      if (st) return st;
+    }
+  }
   for (int T = 256; T >= 128; T /= 2) {
     int idx[kMaxProb], k = 0;
     for (int i = 0; i < n; ++i) {
@@ -845,7 +877,7 @@ int wx_batch_walk(const cvl_conv_desc* const* d, int n, F&& f) {
     }
   }
   for (int i = 0; i < n; ++i) {
-    if (wx_batch_ok(d[i], &a)) continue;
+    if (wx_batch_ok(d[i], &a) || wx_batch_wh(d[i])) continue;
     const int st = f(nullptr, &i, 1, 0);           // individual
     if (st) return st;
   }
@@ -860,6 +892,8 @@ extern "C" size_t cvl_conv_wgrad_batch_workspace_size(const cvl_conv_desc* const
   wx_batch_walk(d, n, [&](const cvl_conv_desc* const* dd, const int* idx, int k, int T) {
     if (!dd) {
       total += (cvl_conv_wgrad_workspace_size(d[idx[0]]) + 255) & ~(size_t)255;
+    } else if (T == 3) {
+      total += cvl_wgrad_h_batch_workspace(dd, idx, k);
     } else {
       WxBatchPlan pl;
       wx_batch_plan(dd, idx, k, T, &pl);
@@ -892,6 +926,11 @@ extern "C" int cvl_conv_wgrad_batch(const cvl_conv_desc* const* d, int n, const 
       const size_t w = cvl_conv_wgrad_workspace_size(d[i0]);
       const int st = cvl_conv_wgrad(d[i0], x[i0], dy[i0], dw[i0], beta, ws + used, w, stream);
       used += (w + 255) & ~(size_t)255;
+      return st;
+    }
+    if (T == 3) {                                 // 3x3 problems on the halo weight-gradient kernel
+      const int st = cvl_wgrad_h_batch(dd, idx, k, x, dy, dw, beta, ws + used, s);
+      used += cvl_wgrad_h_batch_workspace(dd, idx, k);
       return st;
     }
     WxBatchPlan pl;

@@ -16,7 +16,8 @@ import os
 import torch
 
 from . import ops_nn as nn
-from .layers import BF16, Conv, ParamStore, act_dtype
+from .layers import BF16, Conv, ParamStore, act_dtype, wgrad_batch
+from .layers import conv_wgrad as wgrad_collect
 from .mobilenet_v2 import MobileNetV2
 from .resnet import ResNet50
 from . import _lib
@@ -321,57 +322,60 @@ class FPNDetector(object):
         p3r, p4r = s["p"]
         h6, w6 = shapes[3]
         h7, w7 = shapes[4]
-        # P7 = c7(relu(P6)): weights (relu on load), then d relu(P6) -> dP6 (masked, accumulated)
-        d = self.c7_3x3.fwd_desc(B, [nn.seg(h7, w7, h6, w6, self.c7_3x3.wf, None, src_base=B * off[3],
-                                            dst_base=B * off[4])], ld_dst=FPN_C, relu_in=True)
-        nn.conv_wgrad(d, F, dF, self.c7_3x3.dw)
-        # bias gradients of the eight FPN convs: collected, then one batched launch pair
-        bias_items = [(dF, FPN_C, 0, FPN_C, B * off[4], h7 * w7, h7 * w7, B, self.c7_3x3.db, 0.0)]
-        dr6 = torch.empty((B, h6, w6, FPN_C), dtype=self.store.act, device=dev)
-        dd = self.c7_3x3.dgrad_desc(B, [nn.seg(h6, w6, h7, w7, self.c7_3x3.wd, None, src_base=B * off[4])],
-                                    ld_dst=FPN_C)
-        nn.conv_igemm(dd, dF, dr6)
-        dP6 = dF[B * off[3]:B * off[4]]
-        P6 = F[B * off[3]:B * off[4]]
-        nn.relu_backward(dr6, P6, dP6, beta=1.0)
-        # c6 (stride 2 on C5), c5_3x3, c4_3x3, c3_3x3: weight/bias grads and data grads
-        dC5 = torch.empty_like(c5)
-        n3, n4 = p3r.numel() // FPN_C, p4r.numel() // FPN_C
-        dPR = torch.empty_like(s["PR"])
-        dp3r = dPR[:n3].view(p3r.shape)
-        dp4r = dPR[n3:n3 + n4].view(p4r.shape)
-        dl5 = dPR[n3 + n4:].view(l5.shape)
-        pr_base = (0, n3, n3 + n4)
-        trio = []
-        for l, (conv, src, h, w, dsrc) in enumerate(((self.c3_3x3, p3r, H3, W3, dp3r),
-                                                     (self.c4_3x3, p4r, H4, W4, dp4r),
-                                                     (self.c5_3x3, l5, H5, W5, dl5),
-                                                     (self.c6_3x3, c5, H5, W5, dC5))):
-            Ho, Wo = shapes[l]
-            d = conv.fwd_desc(B, [nn.seg(Ho, Wo, h, w, conv.wf, None, dst_base=B * off[l])], ld_dst=FPN_C)
-            nn.conv_wgrad(d, src, dF, conv.dw)
-            bias_items.append((dF, FPN_C, 0, FPN_C, B * off[l], Ho * Wo, Ho * Wo, B, conv.db, 0.0))
-            if FUSE_FPN and l < 3:            # P3..P5 data gradients: one 3-segment launch below
-                trio.append(nn.seg(h, w, Ho, Wo, conv.wd, None, src_base=B * off[l], dst_base=pr_base[l]))
-                continue
-            dd = conv.dgrad_desc(B, [nn.seg(h, w, Ho, Wo, conv.wd, None, src_base=B * off[l])],
-                                 ld_dst=conv.cin)
-            nn.conv_igemm(dd, dF, dsrc)
-        if trio:
-            nn.conv_igemm(self.c3_3x3.dgrad_desc(B, trio, ld_dst=FPN_C), dF, dPR)
-        # top-down adds: p4r = l4 + up(l5); p3r = l3 + up(l4)
-        nn.upsample2x_backward(dp4r, dl5, B, H4, W4, FPN_C, beta=1.0)   # dl5 += up^T(dp4r)
-        dl4 = dp4r
-        nn.upsample2x_backward(dp3r, dl4, B, H3, W3, FPN_C, beta=1.0)   # dl4 += up^T(dp3r)
-        dl3 = dp3r
-        dC3 = torch.empty_like(c3)
-        dC4 = torch.empty_like(c4)
-        for conv, src, h, w, dl, dC, beta in ((self.c3_1x1, c3, H3, W3, dl3, dC3, 0.0),
-                                              (self.c4_1x1, c4, H4, W4, dl4, dC4, 0.0),
-                                              (self.c5_1x1, c5, H5, W5, dl5, dC5, 1.0)):
-            conv.wgrad(src, dl, B, h, w, bias=False)
-            bias_items.append((dl, FPN_C, 0, FPN_C, 0, h * w, h * w, B, conv.db, 0.0))
-            conv.dgrad(dl, B, h, w, out=dC, beta=beta)
+        # the FPN's weight gradients (3x3 outputs, 1x1 laterals): one batched call before the "fpn" hook
+        # (layers.wgrad_batch: the laterals share a 256-wide launch, the stride-1 3x3 outputs a halo one)
+        with wgrad_batch():
+            # P7 = c7(relu(P6)): weights (relu on load), then d relu(P6) -> dP6 (masked, accumulated)
+            d = self.c7_3x3.fwd_desc(B, [nn.seg(h7, w7, h6, w6, self.c7_3x3.wf, None, src_base=B * off[3],
+                                                dst_base=B * off[4])], ld_dst=FPN_C, relu_in=True)
+            wgrad_collect(d, F, dF, self.c7_3x3.dw)
+            # bias gradients of the eight FPN convs: collected, then one batched launch pair
+            bias_items = [(dF, FPN_C, 0, FPN_C, B * off[4], h7 * w7, h7 * w7, B, self.c7_3x3.db, 0.0)]
+            dr6 = torch.empty((B, h6, w6, FPN_C), dtype=self.store.act, device=dev)
+            dd = self.c7_3x3.dgrad_desc(B, [nn.seg(h6, w6, h7, w7, self.c7_3x3.wd, None, src_base=B * off[4])],
+                                        ld_dst=FPN_C)
+            nn.conv_igemm(dd, dF, dr6)
+            dP6 = dF[B * off[3]:B * off[4]]
+            P6 = F[B * off[3]:B * off[4]]
+            nn.relu_backward(dr6, P6, dP6, beta=1.0)
+            # c6 (stride 2 on C5), c5_3x3, c4_3x3, c3_3x3: weight/bias grads and data grads
+            dC5 = torch.empty_like(c5)
+            n3, n4 = p3r.numel() // FPN_C, p4r.numel() // FPN_C
+            dPR = torch.empty_like(s["PR"])
+            dp3r = dPR[:n3].view(p3r.shape)
+            dp4r = dPR[n3:n3 + n4].view(p4r.shape)
+            dl5 = dPR[n3 + n4:].view(l5.shape)
+            pr_base = (0, n3, n3 + n4)
+            trio = []
+            for l, (conv, src, h, w, dsrc) in enumerate(((self.c3_3x3, p3r, H3, W3, dp3r),
+                                                         (self.c4_3x3, p4r, H4, W4, dp4r),
+                                                         (self.c5_3x3, l5, H5, W5, dl5),
+                                                         (self.c6_3x3, c5, H5, W5, dC5))):
+                Ho, Wo = shapes[l]
+                d = conv.fwd_desc(B, [nn.seg(Ho, Wo, h, w, conv.wf, None, dst_base=B * off[l])], ld_dst=FPN_C)
+                wgrad_collect(d, src, dF, conv.dw)
+                bias_items.append((dF, FPN_C, 0, FPN_C, B * off[l], Ho * Wo, Ho * Wo, B, conv.db, 0.0))
+                if FUSE_FPN and l < 3:            # P3..P5 data gradients: one 3-segment launch below
+                    trio.append(nn.seg(h, w, Ho, Wo, conv.wd, None, src_base=B * off[l], dst_base=pr_base[l]))
+                    continue
+                dd = conv.dgrad_desc(B, [nn.seg(h, w, Ho, Wo, conv.wd, None, src_base=B * off[l])],
+                                     ld_dst=conv.cin)
+                nn.conv_igemm(dd, dF, dsrc)
+            if trio:
+                nn.conv_igemm(self.c3_3x3.dgrad_desc(B, trio, ld_dst=FPN_C), dF, dPR)
+            # top-down adds: p4r = l4 + up(l5); p3r = l3 + up(l4)
+            nn.upsample2x_backward(dp4r, dl5, B, H4, W4, FPN_C, beta=1.0)   # dl5 += up^T(dp4r)
+            dl4 = dp4r
+            nn.upsample2x_backward(dp3r, dl4, B, H3, W3, FPN_C, beta=1.0)   # dl4 += up^T(dp3r)
+            dl3 = dp3r
+            dC3 = torch.empty_like(c3)
+            dC4 = torch.empty_like(c4)
+            for conv, src, h, w, dl, dC, beta in ((self.c3_1x1, c3, H3, W3, dl3, dC3, 0.0),
+                                                  (self.c4_1x1, c4, H4, W4, dl4, dC4, 0.0),
+                                                  (self.c5_1x1, c5, H5, W5, dl5, dC5, 1.0)):
+                conv.wgrad(src, dl, B, h, w, bias=False)
+                bias_items.append((dl, FPN_C, 0, FPN_C, 0, h * w, h * w, B, conv.db, 0.0))
+                conv.dgrad(dl, B, h, w, out=dC, beta=beta)
         nn.bias_grad_multi(bias_items)
         hook("fpn")
         self.backbone.backward([dC3, dC4, dC5], s["bsv"], hook=hook)

@@ -216,7 +216,7 @@ class Conv(object):
         Ho, Wo, _, _ = self.out_hw(H, W)
         d = self.fwd_desc(B, [nn.seg(Ho, Wo, H, W, self.wf, None)], ld_dst=self.cout_pad_ld(dy),
                           relu_in=relu_in)
-        if _wgb is not None and self.k == 1 and beta == 0.0 and not relu_in and x.dtype == BF16:
+        if _wgb is not None and self.k in (1, 3) and beta == 0.0 and not relu_in and x.dtype == BF16:
             _wgb.append((d, x, dy, self.dw if dw is None else dw))     # launched by flush_wgrad_batch()
         else:
             nn.conv_wgrad(d, x, dy, self.dw if dw is None else dw, beta)
@@ -255,10 +255,10 @@ FUSE_BNSUM = not _lib.dispatch("no_bnsum_fuse")
 # ... and a residual unit's (BN3) first pass into the next block's conv1 data gradient (CVL_DISPATCH=no_bnsum_res: off)
 FUSE_BNSUM_RES = FUSE_BNSUM and not _lib.dispatch("no_bnsum_res")
 
-# Batched 1x1 weight gradients (round 6; CVL_DISPATCH=no_wgrad_batch: off).  Inside `with
-# wgrad_batch():` Conv.wgrad collects its 1x1 bf16 problems (keeping their x / dy alive) instead of
-# launching them; the exit (or flush_wgrad_batch()) hands all of them to ONE cvl_conv_wgrad_batch call:
-# one launch per ResNet stage instead of one per conv, with fewer splits per problem.
+# Batched weight gradients (round 6; CVL_DISPATCH=no_wgrad_batch: off).  Inside `with wgrad_batch():`
+# Conv.wgrad collects its 1x1 / 3x3 bf16 problems (keeping their x / dy alive) instead of launching
+# them; the exit (or flush_wgrad_batch()) hands all of them to ONE cvl_conv_wgrad_batch call: one
+# launch per ResNet stage and kernel instead of one per conv, with fewer splits per problem.
 WGRAD_BATCH = not _lib.dispatch("no_wgrad_batch")
 _wgb = None
 
@@ -280,6 +280,14 @@ class wgrad_batch(object):
             finally:
                 _wgb = None
         return False
+
+
+def conv_wgrad(d, x, dy, dw):
+    """nn.conv_wgrad (beta 0), collected instead while a wgrad_batch is open (bf16 operands)."""
+    if _wgb is not None and x.dtype == BF16:
+        _wgb.append((d, x, dy, dw))
+    else:
+        nn.conv_wgrad(d, x, dy, dw)
 
 
 def flush_wgrad_batch():

@@ -230,9 +230,10 @@ int cvl_conv_wgrad_grouped(const cvl_conv_desc* d, int ngroups, const void* x, c
 /* Batched weight gradients (round 6): the weight gradients of n independent convolutions, d / x /
  * dy / dw HOST arrays of n entries (dw pairwise distinct), each as cvl_conv_wgrad(d[i], x[i], dy[i],
  * dw[i], beta) would form it -- the per-image gradient accumulation of FCOS/train_fcos.py:173-176 for
- * every 1x1 conv of a ResNet stage at once.  The 1x1 bf16 single-segment problems (pad 0, stride 1
- * or 2, dense rows) share ONE launch per <= 16 (each problem its own tile grid, a common rows-per-
- * workgroup chunk chosen for the whole launch), with their split reductions deferred as by
+ * every 1x1 and 3x3 conv of a ResNet stage at once.  The 1x1 bf16 single-segment problems (pad 0,
+ * stride 1 or 2, dense rows) share ONE launch per <= 16 and tile width, the 3x3 stride-1 problems the
+ * halo weight-gradient kernel takes ONE launch per <= 12 (each problem its own tile grid, a common
+ * rows-per-workgroup chunk chosen for the whole launch), with their split reductions deferred as by
  * cvl_wgrad_defer; any other problem runs as its own cvl_conv_wgrad.  Sums are fixed-order
  * (deterministic); the chunking differs from the one-conv calls, so results agree with them to fp32
  * rounding, not bit for bit.  workspace >= cvl_conv_wgrad_batch_workspace_size(d, n). */

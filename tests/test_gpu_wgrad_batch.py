@@ -15,11 +15,13 @@ pytestmark = pytest.mark.gpu
 BF = torch.bfloat16
 F64 = torch.float64
 
-# (B, input H = W, stride, Cin, Cout): the ResNet-50 1x1 shapes at reduced batch, a 64-channel K
-# (half of the 128-wide tile idle), a 64-wide output, stride-2 projections, and a 3x3 problem (not
-# batched: it runs as its own cvl_conv_wgrad inside the call)
+# (B, input H = W, stride, Cin, Cout[, k]): the ResNet-50 1x1 shapes at reduced batch, a 64-channel K
+# (half of the 128-wide tile idle), a 64-wide output, stride-2 projections, the ResNet 3x3 unit shapes
+# (batched on the halo weight-gradient kernel) and a 3x3 stride-2 problem (neither batched kernel
+# takes it: it runs as its own cvl_conv_wgrad inside the call)
 PROBLEMS = [(4, 32, 1, 1024, 256), (4, 32, 1, 256, 1024), (4, 64, 2, 512, 1024), (2, 128, 1, 64, 256),
-            (2, 128, 1, 64, 64), (8, 16, 1, 2048, 512), (4, 64, 2, 256, 128), (2, 32, 1, 256, 256, 3)]
+            (2, 128, 1, 64, 64), (8, 16, 1, 2048, 512), (4, 64, 2, 256, 128), (2, 32, 1, 256, 256, 3),
+            (4, 16, 1, 512, 512, 3), (2, 64, 1, 128, 128, 3), (2, 128, 1, 64, 64, 3), (2, 16, 2, 256, 256, 3)]
 
 
 def build(seed=0):
@@ -55,7 +57,14 @@ def close(got, ref):
     return err <= 2e-5 * float(ref.abs().max()), err
 
 
-def test_wgrad_batch_matches_float64_and_single_calls():
+@pytest.fixture(params=["", "wgb_no_h,wgb_no_256"])
+def dispatch(request, monkeypatch):
+    """'' the production form; the 128-wide-only / unbatched-3x3 forms"""
+    monkeypatch.setenv("CVL_DISPATCH", request.param)
+    return request.param
+
+
+def test_wgrad_batch_matches_float64_and_single_calls(dispatch):
     from cvlite import _lib, ops_nn as nn
     descs, xs, dys, dws, refs = build()
     nn.conv_wgrad_batch(descs, xs, dys, dws)
@@ -73,7 +82,7 @@ def test_wgrad_batch_matches_float64_and_single_calls():
         assert err <= 2e-5 * float(ref.abs().max()), "problem %d: batch vs single %.3g" % (i, err)
 
 
-def test_wgrad_batch_deterministic_and_deferral_invariant():
+def test_wgrad_batch_deterministic_and_deferral_invariant(dispatch):
     from cvlite import ops_nn as nn
     descs, xs, dys, dws, refs = build(seed=3)
     nn.conv_wgrad_batch(descs, xs, dys, dws)
@@ -100,7 +109,7 @@ def test_wgrad_batch_beta_accumulates():
         assert ok, "problem %d: max err %.3g" % (i, err)
 
 
-def test_wgrad_batch_more_than_one_launch_group():
+def test_wgrad_batch_more_than_one_launch_group(dispatch):
     """More eligible problems than one launch takes (16): several launches, same results."""
     from cvlite import ops_nn as nn
     descs, xs, dys, dws, refs = build(seed=7)
