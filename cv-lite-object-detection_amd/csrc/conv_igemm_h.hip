@@ -274,7 +274,10 @@ __global__ void __launch_bounds__(NT) conv_igemm_h_kernel(ConvArgs a) {
   // SW epilogue state: per-lane partial sums of the current (image, N tile) -- BN statistics of
   // the lane's 4 channels per column block (forward), or the BN-backward sums of its 8 regrouped
   // channels (BSUM) with those channels' (mean, rstd, gamma, beta)
-  const int lgo = ((lg & 1) ? 16 : 0) + ((lg & 2) ? 8 : 0);
+  // channels a lane holds after the regroup: 8 (TN 2: v_permlane16_swap of the two column blocks)
+  // or 4 (TN 1, the 32-wide tile: the lane's own quad)
+  constexpr int CPL = TN == 2 ? 8 : 4;
+  const int lgo = TN == 2 ? ((lg & 1) ? 16 : 0) + ((lg & 2) ? 8 : 0) : 4 * lg;
   float ss1[SW ? TN : 1][4], ss2[SW ? TN : 1][4];
   float bs1[8], bs2[8], pm[8], prs[8], pga[8], pbe[8];
   int k_img = -1, k_n0 = 0;
@@ -299,7 +302,7 @@ __global__ void __launch_bounds__(NT) conv_igemm_h_kernel(ConvArgs a) {
       if (k_img < 0) return;
       if (BSUM) {
 #pragma unroll
-        for (int u = 0; u < 8; ++u) {
+        for (int u = 0; u < CPL; ++u) {
           const float t1 = row16_sum(bs1[u]), t2 = row16_sum(bs2[u]);
           bs1[u] = 0.f;
           bs2[u] = 0.f;
@@ -412,7 +415,7 @@ __global__ void __launch_bounds__(NT) conv_igemm_h_kernel(ConvArgs a) {
         k_n0 = n0;
         if (BSUM) {
 #pragma unroll
-          for (int u = 0; u < 8; ++u) {
+          for (int u = 0; u < CPL; ++u) {
             const int c = min(n0 + wn * WN + lgo + u, a.n_store - 1);
             const long bc = (long)img * a.n_store + c;
             pm[u] = a.bmr[bc * 2];
@@ -433,7 +436,13 @@ __global__ void __launch_bounds__(NT) conv_igemm_h_kernel(ConvArgs a) {
 #pragma unroll
         for (int i = 0; i < TM; ++i) {
           const long row = S.dst_base + mloc0 + wm * WM + i * 16 + lr;
-          zq[i] = *reinterpret_cast<const s16x8*>(a.bz + row * a.ld_dst + a.dst_coff + n0 + wn * WN + lgo);
+          const cvl_bf16* zp = a.bz + row * a.ld_dst + a.dst_coff + n0 + wn * WN + lgo;
+          if constexpr (TN == 2) {
+            zq[i] = *reinterpret_cast<const s16x8*>(zp);
+          } else {
+            const s16x4 z4 = *reinterpret_cast<const s16x4*>(zp);
+            zq[i] = s16x8{z4[0], z4[1], z4[2], z4[3], 0, 0, 0, 0};
+          }
         }
       }
     } else {
@@ -536,7 +545,7 @@ __global__ void __launch_bounds__(NT) conv_igemm_h_kernel(ConvArgs a) {
         }
         unsigned pk[2][2];
 #pragma unroll
-        for (int jj = 0; jj < 2; ++jj)
+        for (int jj = 0; jj < TN; ++jj)
 #pragma unroll
           for (int h = 0; h < 2; ++h) {
             float v0 = acc[i][jj][2 * h] + bq[jj][2 * h];
@@ -552,17 +561,21 @@ __global__ void __launch_bounds__(NT) conv_igemm_h_kernel(ConvArgs a) {
               ss2[jj][2 * h + 1] = __builtin_fmaf(r1, r1, ss2[jj][2 * h + 1]);
             }
           }
+        if constexpr (TN == 2) {
 #pragma unroll
-        for (int h = 0; h < 2; ++h) {
-          const auto sw = __builtin_amdgcn_permlane16_swap(pk[0][h], pk[1][h], false, false);
-          pk[0][h] = sw[0];
-          pk[1][h] = sw[1];
+          for (int h = 0; h < 2; ++h) {
+            const auto sw = __builtin_amdgcn_permlane16_swap(pk[0][h], pk[1][h], false, false);
+            pk[0][h] = sw[0];
+            pk[1][h] = sw[1];
+          }
+        } else {
+          pk[1][0] = pk[1][1] = 0u;
         }
         if (n >= a.n_store) continue;
         const s16x8 o = __builtin_bit_cast(s16x8, (u32x4){pk[0][0], pk[0][1], pk[1][0], pk[1][1]});
         if (BSUM) {        // g = dy * ReLU mask rebuilt from z (exactly the forward's bn_affine value)
 #pragma unroll
-          for (int u = 0; u < 8; ++u) {
+          for (int u = 0; u < CPL; ++u) {
             const float zf = bf16_to_f32((cvl_bf16)zq[i][u]);
             const float xh = (zf - pm[u]) * prs[u];
             const float af = __builtin_fmaf(pga[u], xh, pbe[u]);
@@ -571,7 +584,12 @@ __global__ void __launch_bounds__(NT) conv_igemm_h_kernel(ConvArgs a) {
             bs2[u] = __builtin_fmaf(g, xh, bs2[u]);
           }
         }
-        *reinterpret_cast<s16x8*>(reinterpret_cast<cvl_bf16*>(a.dst) + drow * a.ld_dst + a.dst_coff + n) = o;
+        cvl_bf16* op = reinterpret_cast<cvl_bf16*>(a.dst) + drow * a.ld_dst + a.dst_coff + n;
+        if constexpr (TN == 2) {
+          *reinterpret_cast<s16x8*>(op) = o;
+        } else {
+          *reinterpret_cast<s16x4*>(op) = s16x4{o[0], o[1], o[2], o[3]};
+        }
       }
       if (ST && stamp) {
         t_epi += __builtin_amdgcn_s_memtime() - c0;
@@ -665,6 +683,32 @@ int cvl_conv_igemm_h(const cvl_conv_desc* d, const ConvArgs& a0, hipStream_t s, 
     hipLaunchKernelGGL((conv_igemm_h_kernel<false, false, false, false, false, 32>), dim3(t32 < ncu32 ? t32 : ncu32),
                        dim3(NT), 0, s, a);
     return cvl_launch_status();
+  }
+  // 32-wide tiles (round 6) for the SW-epilogue launches whose 64-wide grid fills at most half of the
+  // CUs (the conv5_x 3x3 units at 512 / bs 16, forward and data gradient: 128 tiles -> 256): every CU
+  // gets a tile and no launch splits its channel blocks into fp32 slabs
+  {
+    static const int ncu0 = cvl_device_cus();
+    const int t64 = a.m_tiles * (a.Npad / BN);
+    bool n32 = !cvl_dispatch_flag("h_no_n32") && a.Npad % BN == 0 && 2 * t64 <= ncu0 && !d->dst_f32 &&
+               d->beta == 0.f && d->n_store % 8 == 0 && d->ld_dst % 8 == 0 && d->dst_coff % 8 == 0 && !(a.stats && a.bsum);
+    for (int i = 0; n32 && i < a.nseg; ++i) {
+      const ConvSeg& q = a.seg[i];
+      const long hw = (long)q.Hr * q.Wr;
+      if (hw % BM || (a.bsum && q.dst_img != hw)) n32 = false;
+    }
+    if (n32) {
+      a.splits = 1;
+      g_cvl_conv_last_kernel = CVL_CK_H64;
+      const dim3 g32(2 * t64);
+      if (d->mode == CVL_CONV_DGRAD && a.bsum)
+        hipLaunchKernelGGL((conv_igemm_h_kernel<true, true, false, false, true, 32>), g32, dim3(NT), 0, s, a);
+      else if (d->mode == CVL_CONV_DGRAD)
+        hipLaunchKernelGGL((conv_igemm_h_kernel<true, false, false, false, true, 32>), g32, dim3(NT), 0, s, a);
+      else
+        hipLaunchKernelGGL((conv_igemm_h_kernel<false, false, false, false, true, 32>), g32, dim3(NT), 0, s, a);
+      return cvl_launch_status();
+    }
   }
   const int tiles = a.m_tiles * (a.Npad / BN);
   const int ncb = a.Cin / BK;

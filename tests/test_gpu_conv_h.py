@@ -255,6 +255,45 @@ def test_h_split_k_small_grid():
     torch.testing.assert_close(outs[0], outs[1], rtol=1e-2, atol=1e-2)
 
 
+def test_h_32_wide_tiles_conv5(dispatch):
+    """conv5_x 3x3 (512 -> 512 @ 16x16, bs 16: 128 tiles of 256 x 64) on 256 x 32 tiles (round 6:
+    every CU a tile, no split-K slabs): forward with bias / ReLU / BN statistics vs float64, the data
+    gradient with the fused BN-backward first pass bit-identical to the 64-wide launch (same MFMA dot
+    products; the sums to fp32 order)."""
+    from cvlite import ops_nn as nn
+    B, H, C = 16, 16, 512
+    g = torch.Generator().manual_seed(21)
+    x = rnd(B, H, H, C, gen=g)
+    w = rnd(3, 3, C, C, scale=(9 * C) ** -0.5, gen=g)
+    b = torch.randn(C, generator=g, dtype=torch.float64)
+    wf, wd, npad, cin_pad = packs(w)
+    xg = x.to(BF).cuda()
+    dy = rnd(B, H, H, C, gen=g).to(BF).cuda()
+    z = rnd(B, H, H, C, gen=g).to(BF).cuda()
+    mr = torch.stack([torch.randn(B, C, generator=g) * 0.2, torch.rand(B, C, generator=g) + 0.5], -1).cuda()
+    ga, be = (torch.rand(C, generator=g) + 0.5).cuda(), torch.randn(C, generator=g).cuda()
+    out = torch.empty((B, H, H, C), dtype=BF, device="cuda")
+    st = nn.bn_acc(B, C, "cuda")
+    d = nn.make_desc(nn.FWD, B, C, 3, 3, 1, 1, 1, npad, C, C, [nn.seg(H, H, H, H, wf, b.float().cuda())], relu_out=True)
+    nn.conv_igemm(d, xg, out, st)
+    assert "conv_igemm_h_kernel" in last_kernel(), last_kernel()
+    o = out.double().cpu()
+    torch.testing.assert_close(o, conv3(x, w, b).clamp(min=0), rtol=1e-2, atol=1e-2)
+    torch.testing.assert_close(nn.bn_acc_value(st).cpu(), torch.stack([o.sum((1, 2)), (o * o).sum((1, 2))], -1),
+                               rtol=1e-4, atol=1e-2)
+    dd = nn.make_desc(nn.DGRAD, B, npad, 3, 3, 1, 1, 1, cin_pad, C, C, [nn.seg(H, H, H, H, wd)])
+    res = []
+    for off in ("0", "1"):
+        dispatch("h_no_n32=" + off)
+        dx = torch.empty((B, H, H, C), dtype=BF, device="cuda")
+        sums = nn.bn_acc(B, C, "cuda")
+        assert nn.conv_igemm_dgrad_bnsum(dd, dy, dx, z, mr, ga, be, sums)
+        assert "conv_igemm_h_kernel" in last_kernel(), last_kernel()
+        res.append((dx.view(torch.int16), nn.bn_acc_value(sums)))
+    assert torch.equal(res[0][0], res[1][0])
+    torch.testing.assert_close(res[0][1], res[1][1], rtol=2e-5, atol=2e-5 * float(res[1][1].abs().max()))
+
+
 def test_h_dgrad_fused_bn_backward_sums():
     """conv2_x's 3x3 data gradient with the conv1 unit's BN-backward first pass in the epilogue
     (cvl_conv_igemm_dgrad_bnsum on H64): dX identical to the plain launch, sums vs float64."""
