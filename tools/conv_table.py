@@ -1,6 +1,8 @@
 """Per-shape table of every conv launch of one FCOS training step (configs[1]: 512x512, bs 16):
 the launches are recorded during one eager step (ops_nn.conv_igemm / conv_wgrad /
-conv_wgrad_grouped), then each distinct launch is replayed alone with HIP events on its stream.
+conv_wgrad_grouped / conv_wgrad_batch -- a batched call is one row: the problems it launched
+together, with their summed FLOPs), then each distinct launch is replayed alone with HIP events on
+its stream.
 Prints a markdown table (kernel chosen, us per launch, TFLOP/s, fraction of the 2.5 PF bf16 dense
 peak, ms per step) sorted by time per step.
 usage: conv_table.py [--bs 16] [--size 512] [--iters 10] [--out file.md]"""
@@ -77,7 +79,7 @@ def main():
     torch.cuda.synchronize()
     calls = collections.OrderedDict()
     counts = collections.Counter()
-    orig = (nn.conv_igemm, nn.conv_wgrad, nn.conv_wgrad_grouped)
+    orig = (nn.conv_igemm, nn.conv_wgrad, nn.conv_wgrad_grouped, nn.conv_wgrad_batch)
 
     def rec(key, replay, d, kind, ng=1):
         counts[key] += 1
@@ -96,12 +98,17 @@ def main():
         rec(desc_key("wgrad_g", desc), lambda: orig[2](desc, x, dy, dws, beta), desc, "wgrad", len(dws))
         return orig[2](desc, x, dy, dws, beta)
 
-    nn.conv_igemm, nn.conv_wgrad, nn.conv_wgrad_grouped = igemm, wgrad, wgrad_g
+    def wgrad_b(descs, xs, dys, dws, beta=0.0):
+        key = ("wgrad_b",) + tuple(desc_key("wgrad", d) for d in descs)
+        rec(key, lambda: orig[3](descs, xs, dys, dws, beta), list(descs), "wgrad_b", len(descs))
+        return orig[3](descs, xs, dys, dws, beta)
+
+    nn.conv_igemm, nn.conv_wgrad, nn.conv_wgrad_grouped, nn.conv_wgrad_batch = igemm, wgrad, wgrad_g, wgrad_b
     if args.model == "fcos":
         tr.load_batch(*synthetic_batch(B, H, H, 20, seed=77, device="cuda"))
     tr.step()
     torch.cuda.synchronize()
-    nn.conv_igemm, nn.conv_wgrad, nn.conv_wgrad_grouped = orig
+    nn.conv_igemm, nn.conv_wgrad, nn.conv_wgrad_grouped, nn.conv_wgrad_batch = orig
     lib = _lib.load()
     rows = []
     s = torch.cuda.current_stream()
@@ -117,8 +124,15 @@ def main():
         e1.record(s)
         e1.synchronize()
         us = e0.elapsed_time(e1) / args.iters * 1e3
-        fl = flops(kind, d)
         n = counts[key]
+        if kind == "wgrad_b":      # one batched call: its problems' summed FLOPs, shapes listed
+            fl = sum(flops("wgrad", q) for q in d)
+            shapes = collections.Counter(describe("wgrad", q)[6:] for q in d)
+            label = "wgrad batch of %d: %s" % (ng, ", ".join("%s%s" % ("%dx " % c if c > 1 else "", sh)
+                                                              for sh, c in shapes.items()))
+            rows.append((us * n / 1e3, label, kname + " (batched)", n, us, fl / us / 1e6))
+            continue
+        fl = flops(kind, d)
         rows.append((us * n / 1e3, describe(kind, d, ng), kname, n, us, fl / us / 1e6))
     rows.sort(key=lambda r: -r[0])
     tot = sum(r[0] for r in rows)
