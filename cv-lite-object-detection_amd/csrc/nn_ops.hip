@@ -272,7 +272,7 @@ __global__ void bn_finalize_kernel(const acc_u64* stats, float* mr, float* run_m
 // all 16-byte loads issued before use.
 // FIN: the finalize is fused in -- every block derives (mean, rstd) of its image from the float64
 // stats (same arithmetic as bn_finalize_kernel), chunk-0 blocks store them for the backward and
-// block (0, 0) advances the running statistics.
+// an extra leading block row advances the running statistics.
 struct BnFin {
   const acc_u64* stats;
   float* mr_out;
@@ -300,8 +300,7 @@ struct BnRes {
   BnFin fin;
 };
 
-// FIN prologue of one BN: (mean, rstd) of image b into smr, the chunk-0 blocks store them, the
-// image-0 blocks advance the running statistics
+// FIN prologue of one BN: (mean, rstd) of image b into smr, the chunk-0 blocks store them
 __device__ __forceinline__ void bn_fin_prologue(const BnFin& fin, float2* smr, int b, int C, int HW) {
   for (int c = threadIdx.x; c < C; c += NT) {
     const long bc = (long)b * C + c;
@@ -311,11 +310,15 @@ __device__ __forceinline__ void bn_fin_prologue(const BnFin& fin, float2* smr, i
     smr[c] = float2{mm, rr};
     if (blockIdx.x == 0) { fin.mr_out[bc * 2] = mm; fin.mr_out[bc * 2 + 1] = rr; }
   }
-  // running statistics: one channel per thread over the image-0 blocks (a serial float64 chain
-  // over the images -- in one block it was the critical path of the small launches)
-  if (b == 0 && fin.run_mean)
+}
+
+// running statistics: one channel per thread over the extra leading block row of a FIN launch (a
+// serial float64 chain over the images -- in one block it was the critical path of the small
+// launches, in the image-0 blocks it delayed their rows)
+__device__ __forceinline__ void bn_fin_running(const BnFin& fin, int nimg, int C, int HW) {
+  if (fin.run_mean)
     for (int c = blockIdx.x * NT + threadIdx.x; c < C; c += gridDim.x * NT)
-      bn_running(fin.stats, fin.slots, gridDim.y, C, c, HW, fin.eps, fin.momentum, fin.run_mean, fin.run_var);
+      bn_running(fin.stats, fin.slots, nimg, C, c, HW, fin.eps, fin.momentum, fin.run_mean, fin.run_var);
 }
 
 template <bool FIN, bool RBN = false>
@@ -325,13 +328,18 @@ __global__ void __launch_bounds__(NT) bn_apply_kernel(const cvl_bf16* __restrict
                                                       int C, int HW, int relu, int rows_per_blk, BnFin fin,
                                                       BnRes rb) {
   static_assert(FIN || !RBN, "the BN residual form fuses both finalizes");
-  const int b = blockIdx.y;
+  const int b = FIN ? (int)blockIdx.y - 1 : (int)blockIdx.y;     // FIN: row 0 advances the running stats
   const int C8 = C / 8;
   const int tpr = C8 < NT ? C8 : NT;
   const int rpp = NT / tpr;
   const int cg = threadIdx.x % tpr, rsub = threadIdx.x / tpr;
   __shared__ float2 smr[FIN ? BN_FIN_MAXC : 1];
   __shared__ float2 smr2[RBN ? BN_FIN_MAXC : 1];
+  if (FIN && b < 0) {
+    bn_fin_running(fin, (int)gridDim.y - 1, C, HW);
+    if (RBN) bn_fin_running(rb.fin, (int)gridDim.y - 1, C, HW);
+    return;
+  }
   if (FIN) {      // (mean, rstd) of this image, one channel per thread, shared through LDS
     bn_fin_prologue(fin, smr, b, C, HW);
     if (RBN) bn_fin_prologue(rb.fin, smr2, b, C, HW);
@@ -450,7 +458,11 @@ __global__ void __launch_bounds__(NT) bn_bwd_kernel(const cvl_bf16* __restrict__
                                                     float* __restrict__ part, int C, int HW, int rows_per_blk,
                                                     int group, float dz_beta, BnPG pg,
                                                     const float* __restrict__ bnb, float act_hi) {
-  const int b = blockIdx.y;
+  // pass 1 launches one extra block row in front (grid.y = images + 1): row 0 forms the parameter
+  // gradients while the other rows stream, so the serial per-channel image chain is off every
+  // streaming block's path (in the image-0 blocks it delayed their rows and set the launch's tail)
+  const int nimg = PASS == 1 ? (int)gridDim.y - 1 : (int)gridDim.y;
+  const int b = PASS == 1 ? (int)blockIdx.y - 1 : (int)blockIdx.y;
   const int C8 = C / 8;
   const int tpr = C8 < NT ? C8 : NT;
   const int rpp = NT / tpr;
@@ -459,22 +471,24 @@ __global__ void __launch_bounds__(NT) bn_bwd_kernel(const cvl_bf16* __restrict__
   const int r1 = min(r0 + rows_per_blk, HW);
   // BN over a sub-batch of `group` images (the last group may be short): sums hold group totals
   const int g0 = (b / group) * group;
-  const int gsz = min(g0 + group, (int)gridDim.y) - g0;
+  const int gsz = min(g0 + group, nimg) - g0;
   const float inv = 1.0f / ((float)HW * (float)gsz);
   __shared__ float red[NT][17];
-  if (PASS == 1 && pg.dgamma && b == 0) {          // spread over the image-0 blocks, a channel per thread
+  if (PASS == 1 && b < 0) {                        // the parameter-gradient row, a channel per thread
+    if (!pg.dgamma) return;
     const acc_u64* ps = pg.psums ? pg.psums : sums;
     for (int c = blockIdx.x * NT + threadIdx.x; c < C; c += gridDim.x * NT) {
       if (pg.conv_dbias) pg.conv_dbias[c] = 0.f;
       double a1 = 0.0, a2 = 0.0;
 #pragma unroll 8
-      for (int bb = 0; bb < (int)gridDim.y; ++bb) {
+      for (int bb = 0; bb < nimg; ++bb) {
         a1 += acc_dec(ps, (long)bb * C + c, 0, pg.slots);
         a2 += acc_dec(ps, (long)bb * C + c, 1, pg.slots);
       }
       pg.dbeta[c] = (float)a1 + (pg.beta_acc != 0.f ? pg.beta_acc * pg.dbeta[c] : 0.f);
       pg.dgamma[c] = (float)a2 + (pg.beta_acc != 0.f ? pg.beta_acc * pg.dgamma[c] : 0.f);
     }
+    return;
   }
   // uniform trip count over the channel groups (the reduction below synchronises the block):
   // threads past the last group clamp their parameter loads and neither stream rows nor store
@@ -1483,7 +1497,7 @@ extern "C" int cvl_bn_finalize_apply(uint64_t* stats, float* mean_rstd, float* r
   const int dst = acc_decode_launch((acc_u64*)stats, 2L * B * C, S_);    // once per statistic, not per block
   if (dst) return dst;
   const int rpb = bn_rows_per_blk(B, HW, C);
-  hipLaunchKernelGGL(bn_apply_kernel<true>, dim3((HW + rpb - 1) / rpb, B), dim3(NT), 0, S_, (const cvl_bf16*)z,
+  hipLaunchKernelGGL(bn_apply_kernel<true>, dim3((HW + rpb - 1) / rpb, B + 1), dim3(NT), 0, S_, (const cvl_bf16*)z,
                      (const float*)nullptr, gamma, beta, (const cvl_bf16*)residual, (cvl_bf16*)y, C, HW, relu, rpb,
                      BnFin{(const acc_u64*)stats, mean_rstd, run_mean, run_var, eps, momentum, g_acc_slots}, BnRes{});
   return cvl_launch_status();
@@ -1504,7 +1518,7 @@ extern "C" int cvl_bn_finalize_apply_bnres(uint64_t* stats, float* mean_rstd, fl
   if (!dst) dst = acc_decode_launch((acc_u64*)res_stats, 2L * B * C, S_);
   if (dst) return dst;
   const int rpb = bn_rows_per_blk(B, HW, C);
-  hipLaunchKernelGGL((bn_apply_kernel<true, true>), dim3((HW + rpb - 1) / rpb, B), dim3(NT), 0, S_, (const cvl_bf16*)z,
+  hipLaunchKernelGGL((bn_apply_kernel<true, true>), dim3((HW + rpb - 1) / rpb, B + 1), dim3(NT), 0, S_, (const cvl_bf16*)z,
                      (const float*)nullptr, gamma, beta, (const cvl_bf16*)nullptr, (cvl_bf16*)y, C, HW, relu, rpb,
                      BnFin{(const acc_u64*)stats, mean_rstd, run_mean, run_var, eps, momentum, g_acc_slots},
                      BnRes{(const cvl_bf16*)res_z, res_gamma, res_beta,
@@ -1545,7 +1559,7 @@ static int bn_backward_impl(const void* dy, const void* y_relu, const float* bn_
                      sums, 1);
   // pass 1 is elementwise (no partials): the apply kernels' finer chunking (~2048 workgroups)
   const int rpb1 = bn_rows_per_blk(B, HW, C);
-  hipLaunchKernelGGL(k1, dim3((HW + rpb1 - 1) / rpb1, B), dim3(NT), 0, S_, (const cvl_bf16*)dy, (const cvl_bf16*)y_relu,
+  hipLaunchKernelGGL(k1, dim3((HW + rpb1 - 1) / rpb1, B + 1), dim3(NT), 0, S_, (const cvl_bf16*)dy, (const cvl_bf16*)y_relu,
                      (const cvl_bf16*)z, mean_rstd, gamma, (const acc_u64*)sums, (cvl_bf16*)dz, (cvl_bf16*)g_out,
                      (float*)nullptr, C, HW, rpb1, 1, 0.f, BnPG{dgamma, dbeta, conv_dbias, beta_acc, nullptr, 1}, bn_beta,
                      act_hi);
@@ -1591,7 +1605,7 @@ extern "C" int cvl_bn_backward_relu_sums(const void* dy, const void* z, const fl
   if (dst) return dst;
   const int rpb = bn_rows_per_blk(B, HW, C);
   const int nchunk = (HW + rpb - 1) / rpb;
-  hipLaunchKernelGGL((bn_bwd_kernel<1, 2>), dim3(nchunk, B), dim3(NT), 0, S_, (const cvl_bf16*)dy, (const cvl_bf16*)nullptr,
+  hipLaunchKernelGGL((bn_bwd_kernel<1, 2>), dim3(nchunk, B + 1), dim3(NT), 0, S_, (const cvl_bf16*)dy, (const cvl_bf16*)nullptr,
                      (const cvl_bf16*)z, mean_rstd, gamma, (const acc_u64*)sums, (cvl_bf16*)dz, (cvl_bf16*)nullptr, (float*)nullptr,
                      C, HW, rpb, 1, 0.f, BnPG{dgamma, dbeta, conv_dbias, beta_acc, nullptr, g_acc_slots}, beta, act_hi);
   return cvl_launch_status();
@@ -1609,7 +1623,7 @@ extern "C" int cvl_bn_backward_res_sums(const void* dy, const void* y, const voi
   if (dst) return dst;
   const int rpb = bn_rows_per_blk(B, HW, C);
   const int nchunk = (HW + rpb - 1) / rpb;
-  hipLaunchKernelGGL((bn_bwd_kernel<1, 1>), dim3(nchunk, B), dim3(NT), 0, S_, (const cvl_bf16*)dy, (const cvl_bf16*)y,
+  hipLaunchKernelGGL((bn_bwd_kernel<1, 1>), dim3(nchunk, B + 1), dim3(NT), 0, S_, (const cvl_bf16*)dy, (const cvl_bf16*)y,
                      (const cvl_bf16*)z, mean_rstd, gamma, (const acc_u64*)sums, (cvl_bf16*)dz, (cvl_bf16*)g_out, (float*)nullptr,
                      C, HW, rpb, 1, 0.f, BnPG{dgamma, dbeta, conv_dbias, beta_acc, nullptr, g_acc_slots}, (const float*)nullptr, INFINITY);
   return cvl_launch_status();
@@ -1871,7 +1885,7 @@ extern "C" int cvl_bn_backward_grouped(const void* dy, const void* y_relu, const
                        (const acc_u64*)sums, gsums, B, C, group);
     use = gsums;
   }
-  hipLaunchKernelGGL(bn_bwd_kernel<1>, g1, dim3(NT), 0, S_, (const cvl_bf16*)dy, (const cvl_bf16*)y_relu,
+  hipLaunchKernelGGL(bn_bwd_kernel<1>, dim3(nchunk, B + 1), dim3(NT), 0, S_, (const cvl_bf16*)dy, (const cvl_bf16*)y_relu,
                      (const cvl_bf16*)z, mean_rstd, gamma, use, (cvl_bf16*)dz, (cvl_bf16*)nullptr,
                      (float*)nullptr, C, HW, rpb, group, dz_beta, BnPG{dgamma, dbeta, nullptr, 0.f, sums, 1},
                      (const float*)nullptr, INFINITY);
