@@ -9,9 +9,17 @@
 //   dW[t = (r, s)][ci][n] = sum_p x[p][ci] * dY[p + (pad_t - r, pad_l - s)][n]     (0 off the map)
 // so each source row is read once per 128-channel tile, and the 9 shifted copies are taken of the
 // small dY rows (9 x 64 B per pixel, L2-resident).  One GEMM per workgroup chunk of source rows:
-//   C[ci][(t, n)] (128 x 9*32) = X[rows][ci]^T * Ytap[rows][(t, n)],
-// both operands staged row-major in LDS and read column-wise with ds_read_b64_tr_b16 into
-// v_mfma_f32_16x16x32_bf16 fragments (the reduction index is the row index of both).
+//   C[(t, n)][ci] (9*32 x 128) = Ytap[rows][(t, n)]^T * X[rows][ci],
+// Round 6 form: both operands move global -> LDS by buffer_load ... lds (LDS-DMA) into a 3-slot
+// ring (64 source rows per slot: x [64][128] = 16 KiB + the T shifted dY rows [64][T][32] = 36 KiB;
+// the whole 156 KiB LDS), two steps in flight, ONE barrier per step; out-of-map taps and rows past
+// the chunk get an out-of-range buffer offset and the DMA writes zeros.  Row images are XOR-swizzled
+// (applied to the lane's SOURCE offset, the DMA writes lane-linearly) so the transposed fragment
+// reads (ds_read_b64_tr_b16) are conflict-free.  8 waves as 4 (ci) x 2 (tap columns), swapped MFMA
+// operands (A = the dY columns, B = x) so a lane's accumulator quad is 4 consecutive outputs n of
+// one ci: 16-B slab stores.  The per-lane row cursor is advanced by carries (no divisions in the loop).
+// (The round-5 form staged both operands through registers with one step in flight and two
+// barriers per step: 48 us per FCOS head at 512 / bs 16.)
 // Every segment (= one head level with its own weights) is cut into row chunks; each chunk writes
 // its partial dW to an fp32 slab and a second pass sums a group's chunks in a fixed order
 // (deterministic), adding beta * dw.
@@ -19,42 +27,63 @@
 
 namespace {
 
-constexpr int NT = 256;
+constexpr int NT = 512;
 constexpr int BR = 64;          // source rows per step (two MFMA K-steps of 32)
 constexpr int CI = 128;         // input channels per workgroup
 constexpr int NP = 32;          // output columns per tap (Npad)
 constexpr int MAXT = 9;         // taps (KH*KW <= 9)
-constexpr int PITCH_X = CI + 16;
-constexpr int PITCH_Y = MAXT * NP + 16;
+constexpr int NSLOT = 3;
+constexpr unsigned kRecords = 0x7fffffffu;
+constexpr unsigned kOOB = 0x80000000u;
+#ifndef CVL_SN_ABL
+#define CVL_SN_ABL 0            // measurement variants only: 1 no DMA, 2 no fragment reads, 4 no MFMAs, 8 no stores, 16 no loop
+#endif
+
+template <int T>
+struct SnCfg {
+  static constexpr int XB = BR * CI * 2;          // x image of a slot (bytes)
+  static constexpr int YB = BR * T * NP * 2;      // dY image: T taps x 64 B per source row
+  static constexpr int SLOTB = XB + YB;
+  static constexpr int XI = XB / 1024;            // 1-KiB DMA instructions per step: x 16
+  static constexpr int YI = YB / 1024;            // dY: 36 (T 9), 4 (T 1)
+  static constexpr int XJ = XI / 8;               // per wave
+  static constexpr int YJ = (YI + 7) / 8;         // per wave (the first YI % 8 waves; the others one fewer)
+  static constexpr int YW = YI % 8 ? YI % 8 : 8;  // waves that issue YJ dY instructions
+};
 
 struct SnArgs {
   const cvl_bf16* x;
   const cvl_bf16* dy;
-  float* slab;                  // [chunks][T][Cin][NP]
-  int Cin, KH, KW, T, pad_t, pad_l, ld_dy, dy_coff, nseg, B, CH;
+  float* slab;                  // [chunks][T][Cin][nw]
+  int Cin, KH, KW, T, pad_t, pad_l, ld_dy, dy_coff, nseg, B, CH, ci_tiles, nw;
   int cbase[kMaxSeg + 1];       // first chunk of each segment (cbase[nseg] = total chunks)
   int H[kMaxSeg], W[kMaxSeg];
   long src_base[kMaxSeg], src_img[kMaxSeg], dst_base[kMaxSeg], dst_img[kMaxSeg];
 };
 
-typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
-
-__device__ __forceinline__ s16x8 tr_frag_sn(const cvl_bf16* lo, const cvl_bf16* hi) {
-  s16x4 a = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)lo);
-  s16x4 b = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)hi);
-  return s16x8{a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
+__device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t r, const char* lds_dst, unsigned voff) {
+  if (CVL_SN_ABL & 1) return;
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)lds_dst, 16, (int)voff, 0,
+                                           0, 0);
 }
+__device__ __forceinline__ int rswz(int r) { return (r & 3) | (((r >> 3) & 1) << 2); }   // x rows: 32-B chunk xor
+__device__ __forceinline__ int yswz(int r) { return ((r >> 3) & 1) << 1; }              // dY rows: 16-B chunk xor
+
+// a source row's position, advanced by BR rows per step with carries (d_x < W, d_y < H)
+struct RowPos {
+  int p, img, y, x;
+};
 
 template <int T>
 __global__ void __launch_bounds__(NT) conv_wgrad_sn_kernel(SnArgs g) {
-  constexpr int TC = T * NP;              // GEMM columns (tap, n)
-  constexpr int TJ = TC / 16;             // 16-wide column tiles
-  __shared__ __attribute__((aligned(16))) cvl_bf16 Xs[BR * PITCH_X];
-  __shared__ __attribute__((aligned(16))) cvl_bf16 Ys[BR * PITCH_Y];
-
+  using C = SnCfg<T>;
+  __shared__ __attribute__((aligned(16))) char lds[NSLOT * C::SLOTB];
   const int tid = threadIdx.x;
-  const int ci0 = blockIdx.x * CI;
-  const int chunk = blockIdx.y;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
+  // the ci tiles of one chunk are consecutive logical ids: one XCD's L2 serves their dY rows
+  const int L = xcd_remap(blockIdx.x, gridDim.x);
+  const int ci0 = (L % g.ci_tiles) * CI;
+  const int chunk = L / g.ci_tiles;
   int sg = 0;
 #pragma unroll
   for (int i = 1; i < kMaxSeg; ++i)
@@ -63,116 +92,206 @@ __global__ void __launch_bounds__(NT) conv_wgrad_sn_kernel(SnArgs g) {
   const int rows = g.B * HW;
   const int lo = (chunk - g.cbase[sg]) * g.CH;
   const int hi = min(lo + g.CH, rows);
-  const long sbase = g.src_base[sg], simg = g.src_img[sg], dbase = g.dst_base[sg], dimg = g.dst_img[sg];
+  const int nsteps = (CVL_SN_ABL & 16) ? 0 : (hi - lo + BR - 1) / BR;
+  const int sbase = (int)g.src_base[sg], simg = (int)g.src_img[sg];
+  const int dbase = (int)g.dst_base[sg], dimg = (int)g.dst_img[sg];
+  // one step in (img, y, x) units
+  const int d_img = BR / HW, d_rem = BR - d_img * HW, d_y = d_rem / Ws, d_x = d_rem - d_y * Ws;
+  auto pos_of = [&](int p) {
+    RowPos r;
+    r.p = p;
+    r.img = p / HW;
+    const int q = p - r.img * HW;
+    r.y = q / Ws;
+    r.x = q - r.y * Ws;
+    return r;
+  };
+  auto advance = [&](RowPos& r) {
+    r.p += BR;
+    r.x += d_x;
+    const bool cx = r.x >= Ws;
+    r.x -= cx ? Ws : 0;
+    r.y += d_y + (cx ? 1 : 0);
+    const bool cy = r.y >= Hs;
+    r.y -= cy ? Hs : 0;
+    r.img += d_img + (cy ? 1 : 0);
+  };
 
-  // x operand: 16-B chunk xc of rows xr + 16 h;  dY operand: 16-B chunk yc of row yr, all taps
-  const int xc = tid & 15, xr = tid >> 4;
-  const int yc = tid & 3, yr = tid >> 2;
-  s16x8 vx[4], vy[T];
-  auto load_step = [&](int m) {
+  // ---- per-lane DMA roles ------------------------------------------------------------------
+  // x: instruction j covers rows 4k .. 4k+3 (k = wave + 8j), lane = (row, 16-B piece)
+  RowPos xp[C::XJ];
+  unsigned xcol[C::XJ];
 #pragma unroll
-    for (int h = 0; h < 4; ++h) {
-      const int p = m + xr + 16 * h;
-      vx[h] = s16x8{0, 0, 0, 0, 0, 0, 0, 0};
-      if (p < hi) vx[h] = *reinterpret_cast<const s16x8*>(g.x + (sbase + (long)(p / HW) * simg + p % HW) * g.Cin +
-                                                          ci0 + xc * 8);
+  for (int j = 0; j < C::XJ; ++j) {
+    const int k = wave + 8 * j, rr = 4 * k + (lane >> 4), pc = lane & 15;
+    const int lp = pc ^ (rswz(rr) << 1);
+    xp[j] = pos_of(lo + rr);
+    xcol[j] = (unsigned)((ci0 + lp * 8) * 2);
+  }
+  // dY: instruction j covers the 64-B units u = 16k .. 16k+15 (unit = (row, tap)), lane = (unit, chunk)
+  RowPos yp[C::YJ];
+  int yoy[C::YJ], yox[C::YJ];
+  unsigned ycol[C::YJ];
+#pragma unroll
+  for (int j = 0; j < C::YJ; ++j) {
+    const int k = wave + 8 * j;
+    const int u = 16 * min(k, C::YI - 1) + (lane >> 2);
+    const int rr = u / T, t = u - (u / T) * T;
+    const int r = t / g.KW, s = t - (t / g.KW) * g.KW;
+    yoy[j] = g.pad_t - r;
+    yox[j] = g.pad_l - s;
+    yp[j] = pos_of(lo + rr);
+    ycol[j] = (unsigned)((g.dy_coff + ((lane & 3) ^ yswz(rr)) * 8) * 2);
+  }
+  const __amdgpu_buffer_rsrc_t rsX = __builtin_amdgcn_make_buffer_rsrc((void*)g.x, (short)0, (int)kRecords, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rsY = __builtin_amdgcn_make_buffer_rsrc((void*)g.dy, (short)0, (int)kRecords, 0x00020000);
+  const bool yfull = wave < C::YW;        // issues YJ dY instructions (else YJ - 1)
+  auto issue = [&](int slot) {
+    const char* base = lds + slot * C::SLOTB;
+#pragma unroll
+    for (int j = 0; j < C::XJ; ++j) {
+      const RowPos& r = xp[j];
+      const unsigned off = r.p < hi ? (unsigned)((sbase + r.img * simg + r.y * Ws + r.x) * g.Cin * 2) + xcol[j] : kOOB;
+      dma16(rsX, base + (wave + 8 * j) * 1024, off);
+      advance(xp[j]);
     }
-    const int p = m + yr;
-    const bool pin = p < hi;
-    const int img = pin ? p / HW : 0, q = pin ? p % HW : 0;
-    const int iy = q / Ws, ix = q - (q / Ws) * Ws;
 #pragma unroll
-    for (int t = 0; t < T; ++t) {
-      const int r = t / g.KW, s = t - (t / g.KW) * g.KW;
-      const int oy = iy + g.pad_t - r, ox = ix + g.pad_l - s;
-      vy[t] = s16x8{0, 0, 0, 0, 0, 0, 0, 0};
-      if (pin && oy >= 0 && oy < Hs && ox >= 0 && ox < Ws)
-        vy[t] = *reinterpret_cast<const s16x8*>(g.dy + (dbase + (long)img * dimg + (long)oy * Ws + ox) * g.ld_dy +
-                                                g.dy_coff + yc * 8);
+    for (int j = 0; j < C::YJ; ++j) {
+      if (j == C::YJ - 1 && !yfull) break;
+      const RowPos& r = yp[j];
+      const int oy = r.y + yoy[j], ox = r.x + yox[j];
+      const bool ok = r.p < hi && (unsigned)oy < (unsigned)Hs && (unsigned)ox < (unsigned)Ws;
+      const unsigned off = ok ? (unsigned)((dbase + r.img * dimg + oy * Ws + ox) * g.ld_dy * 2) + ycol[j] : kOOB;
+      dma16(rsY, base + C::XB + (wave + 8 * j) * 1024, off);
+      advance(yp[j]);
     }
   };
 
-  const int wave = tid >> 6, lane = tid & 63;
+  // ---- fragment addresses (byte offsets inside a slot) ------------------------------------------
+  const int wci = wave & 3, wc = wave >> 2;
   const int lr = lane & 15, lg = lane >> 4;
   const int q4 = lr >> 2, p4 = lr & 3;
-  f32x4 acc[2][TJ];
+  // rows r0 + q4 and r0 + 4 + q4 of sub-step ks: r0 = 32 ks + 8 lg (the swizzles depend on rows mod 16 only)
+  const int rlo = 8 * lg + q4, rhi = rlo + 4;
+  unsigned xa[2], xb[2];
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
+  for (int b = 0; b < 2; ++b) {
+    const int c0 = wci * 32 + b * 16 + 4 * p4, lp = c0 >> 3, wb = (c0 & 7) * 2;
+    xa[b] = (unsigned)(rlo * CI * 2 + ((lp ^ (rswz(rlo) << 1)) << 4) + wb);
+    xb[b] = (unsigned)(rhi * CI * 2 + ((lp ^ (rswz(rhi) << 1)) << 4) + wb);
+  }
+  unsigned ya[T], yb[T];
 #pragma unroll
-    for (int j = 0; j < TJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int a = 0; a < T; ++a) {
+    const int ct = wc * T + a;                      // 16-column tile of the (t, n) columns
+    const int t = ct >> 1, n = (ct & 1) * 16 + 4 * p4, gc = n >> 3, wb = (n & 7) * 2;
+    ya[a] = (unsigned)(C::XB + rlo * T * NP * 2 + t * NP * 2 + ((gc ^ yswz(rlo)) << 4) + wb);
+    yb[a] = (unsigned)(C::XB + rhi * T * NP * 2 + t * NP * 2 + ((gc ^ yswz(rhi)) << 4) + wb);
+  }
+  f32x4 acc[T][2];
+#pragma unroll
+  for (int a = 0; a < T; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  if (lo < hi) load_step(lo);
-  for (int m = lo; m < hi; m += BR) {
-    __syncthreads();
+  const unsigned lds0 = lds_addr(lds);
+  constexpr int PWF = C::XJ + C::YJ;                // DMA instructions per step of a full wave
+  issue(0);
+  issue(1);
+  int slot = 0;
+  for (int st = 0; st < nsteps; ++st) {
+    if (yfull) wait_vm<PWF>();                      // this wave's pieces of step st landed
+    else wait_vm<PWF - 1>();
+    __builtin_amdgcn_s_barrier();                   // everyone's; and step st-1's slot is free
+    asm volatile("" ::: "memory");
+    issue(slot == 0 ? 2 : slot - 1);                // step st+2 into the slot step st-1 used
+    const unsigned sb = lds0 + slot * C::SLOTB;
 #pragma unroll
-    for (int h = 0; h < 4; ++h) *reinterpret_cast<s16x8*>(Xs + (xr + 16 * h) * PITCH_X + xc * 8) = vx[h];
+    for (int ks = 0; ks < 2; ++ks) {
+      const unsigned kb = sb + ks * 32 * CI * 2, kyb = sb + ks * 32 * T * NP * 2;
+      s16x4 al[T], ah[T], bl[2], bh[2];
+      if (CVL_SN_ABL & 2) {
 #pragma unroll
-    for (int t = 0; t < T; ++t) *reinterpret_cast<s16x8*>(Ys + yr * PITCH_Y + t * NP + yc * 8) = vy[t];
-    __syncthreads();
-    if (m + BR < hi) load_step(m + BR);      // next step's loads in flight during this step's MFMAs
+        for (int b = 0; b < 2; ++b) { bl[b] = s16x4{0, 0, 0, 0}; bh[b] = bl[b]; }
 #pragma unroll
-    for (int ks = 0; ks < BR / 32; ++ks) {
-      const int r0 = ks * 32 + 8 * lg;
-      s16x8 fa[2];
+        for (int a = 0; a < T; ++a) { al[a] = s16x4{0, 0, 0, (short)a}; ah[a] = al[a]; }
+      } else {
 #pragma unroll
-      for (int i = 0; i < 2; ++i) {
-        const int col = wave * 32 + i * 16 + 4 * p4;
-        fa[i] = tr_frag_sn(Xs + (r0 + q4) * PITCH_X + col, Xs + (r0 + 4 + q4) * PITCH_X + col);
+        for (int b = 0; b < 2; ++b) { bl[b] = ds_tr16(kb + xa[b]); bh[b] = ds_tr16(kb + xb[b]); }
+#pragma unroll
+        for (int a = 0; a < T; ++a) { al[a] = ds_tr16(kyb + ya[a]); ah[a] = ds_tr16(kyb + yb[a]); }
       }
+      lgkm_wait();
 #pragma unroll
-      for (int j = 0; j < TJ; ++j) {
-        const int col = j * 16 + 4 * p4;
-        const s16x8 fb = tr_frag_sn(Ys + (r0 + q4) * PITCH_Y + col, Ys + (r0 + 4 + q4) * PITCH_Y + col);
+      for (int b = 0; b < 2; ++b) { tr_pin(bl[b]); tr_pin(bh[b]); }
 #pragma unroll
-        for (int i = 0; i < 2; ++i)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, fa[i]),
-                                                             __builtin_bit_cast(bf16x8, fb), acc[i][j], 0, 0, 0);
+      for (int a = 0; a < T; ++a) { tr_pin(al[a]); tr_pin(ah[a]); }
+      s16x8 fb[2];
+#pragma unroll
+      for (int b = 0; b < 2; ++b) fb[b] = tr_join(bl[b], bh[b]);
+#pragma unroll
+      for (int a = 0; a < T; ++a) {
+        const s16x8 fa = tr_join(al[a], ah[a]);
+#pragma unroll
+        for (int b = 0; b < 2; ++b)
+          if (CVL_SN_ABL & 4) acc[a][b][0] += __builtin_bit_cast(float, (int)(fa[0] ^ fb[b][1]));
+          else acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, fa),
+                                                             __builtin_bit_cast(bf16x8, fb[b]), acc[a][b], 0, 0, 0);
       }
+    }
+    slot = slot == NSLOT - 1 ? 0 : slot + 1;
+  }
+  wait_vm<0>();                                     // the out-of-range tail pieces (nothing reads them)
+
+  // D[(t, n)][ci]: element e of acc[a][b] is column 4 lg + e of tile ct = wc*T + a, ci = lr of block b.
+  // Slab layout [chunk][t][ci][NW], NW = n_store rounded up to 4: only the stored columns travel
+  // (the slab writes and the reducer's reads are the launch's largest HBM streams: 37.7 MB per FCOS
+  // head at NW = 32, 23.6 / 9.4 MB for the class / box head at NW = 20 / 8)
+  const int NW = g.nw;
+  float* out = g.slab + (size_t)chunk * T * g.Cin * NW;
+#pragma unroll
+  for (int a = 0; a < T; ++a) {
+    const int ct = wc * T + a, t = ct >> 1, n = (ct & 1) * 16 + 4 * lg;
+#pragma unroll
+    for (int b = 0; b < 2; ++b) {
+      const int ci = ci0 + wci * 32 + b * 16 + lr;
+      if (CVL_SN_ABL & 8) { if (acc[a][b][0] == 1.2345f) out[0] = 0.f; }
+      else if (n < NW) *reinterpret_cast<f32x4*>(out + ((size_t)t * g.Cin + ci) * NW + n) = acc[a][b];
     }
   }
-
-  // C[ci][(t, n)] -> slab[chunk][t][ci][n]: element e of acc[i][j] is ci = 4*lg + e (+ tile), col = lr
-  float* out = g.slab + (size_t)chunk * T * g.Cin * NP;
-#pragma unroll
-  for (int i = 0; i < 2; ++i)
-#pragma unroll
-    for (int j = 0; j < TJ; ++j) {
-      const int col = j * 16 + lr;
-      const int t = col / NP, n = col % NP;
-      const int ci = ci0 + wave * 32 + i * 16 + 4 * lg;
-#pragma unroll
-      for (int e = 0; e < 4; ++e) out[((size_t)t * g.Cin + ci + e) * NP + n] = acc[i][j][e];
-    }
 }
 
 struct SnReduce {
   const float* slab;
   float* dw[kMaxSeg];
   int cb[kMaxSeg + 1];          // group g sums chunks [cb[g], cb[g+1])
-  int n_store;
-  long per;                     // T * Cin * NP slab elements per chunk
+  int n_store, nw;
+  long per;                     // T * Cin * NW slab elements per chunk
   float beta;
 };
 
-// dw_g[t][ci][n] (HWIO, n < n_store) = sum over the group's chunks in order (+ beta * dw_g)
+// dw_g[t][ci][n] (HWIO, n < n_store) = sum over the group's chunks in order (+ beta * dw_g); slab
+// element i = (t * Cin + ci) * NW + n
 __global__ void __launch_bounds__(256) wgrad_sn_reduce_kernel(SnReduce r) {
   const long i = (long)blockIdx.x * 256 + threadIdx.x;
   const int gq = blockIdx.y;
   if (i >= r.per) return;
-  const int n = (int)(i % NP);
+  const int n = (int)(i % r.nw);
   if (n >= r.n_store) return;
-  float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;       // 4 loads in flight, fixed summation order
+  const long tci = i / r.nw;
+  float a[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};   // 8 loads in flight, fixed summation order
   int c = r.cb[gq];
   const int ce = r.cb[gq + 1];
-  for (; c + 3 < ce; c += 4) {
-    a0 += r.slab[(long)c * r.per + i];
-    a1 += r.slab[(long)(c + 1) * r.per + i];
-    a2 += r.slab[(long)(c + 2) * r.per + i];
-    a3 += r.slab[(long)(c + 3) * r.per + i];
+  for (; c + 7 < ce; c += 8) {
+    float v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) v[u] = r.slab[(long)(c + u) * r.per + i];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) a[u] += v[u];
   }
-  for (; c < ce; ++c) a0 += r.slab[(long)c * r.per + i];
-  float s = (a0 + a1) + (a2 + a3);
-  float* o = r.dw[gq] + (i / NP) * r.n_store + n;
+  for (int u = 0; c < ce; ++c, ++u) a[u] += r.slab[(long)c * r.per + i];
+  float s = ((a[0] + a[1]) + (a[2] + a[3])) + ((a[4] + a[5]) + (a[6] + a[7]));
+  float* o = r.dw[gq] + tci * r.n_store + n;
   if (r.beta != 0.f) s += r.beta * *o;
   *o = s;
 }
@@ -196,10 +315,18 @@ bool sn_plan(const cvl_conv_desc* d, int ngroups, SnPlan* p) {
     if (s.Hr != s.Hs || s.Wr != s.Ws) return false;     // "same" geometry: dY and x share the map
     rows += (long)d->B * s.Hr * s.Wr;
   }
+  // 32-bit buffer offsets (the DMA's voffset)
+  for (int i = 0; i < d->nseg; ++i) {
+    const cvl_conv_seg& s = d->seg[i];
+    const long simg = s.src_img ? s.src_img : (long)s.Hs * s.Ws, dimg = s.dst_img ? s.dst_img : (long)s.Hr * s.Wr;
+    if ((s.src_base + d->B * simg) * d->Cin * 2 >= (1l << 31) || (s.dst_base + d->B * dimg) * d->ld_dst * 2 >= (1l << 31))
+      return false;
+  }
   p->T = d->KH * d->KW;
   p->ci_tiles = d->Cin / CI;
-  // ~256 workgroups (one round at two per CU leaves room for the slab pass); chunk = whole steps
-  const long want = 256 / p->ci_tiles;
+  // ~256 workgroups (one per CU: the 156-KiB LDS ring); chunk = whole steps
+  static const int wgs = cvl_tune_int("CVL_SN_WGS", 256);
+  const long want = wgs / p->ci_tiles;
   long ch = (rows + want - 1) / want;
   ch = ((ch + BR - 1) / BR) * BR;
   if (ch < 4 * BR) ch = 4 * BR;
@@ -212,7 +339,7 @@ bool sn_plan(const cvl_conv_desc* d, int ngroups, SnPlan* p) {
   }
   p->cbase[d->nseg] = c;
   p->nch = c;
-  p->slab = (size_t)c * p->T * d->Cin * NP * sizeof(float);
+  p->slab = (size_t)c * p->T * d->Cin * ((d->n_store + 3) & ~3) * sizeof(float);
   return true;
 }
 
@@ -236,6 +363,8 @@ int cvl_conv_wgrad_sn(const cvl_conv_desc* d, int ngroups, const void* x, const 
   g.slab = reinterpret_cast<float*>(workspace);
   g.Cin = d->Cin; g.KH = d->KH; g.KW = d->KW; g.T = p.T; g.pad_t = d->pad_t; g.pad_l = d->pad_l;
   g.ld_dy = d->ld_dst; g.dy_coff = d->dst_coff; g.nseg = d->nseg; g.B = d->B; g.CH = p.CH;
+  g.ci_tiles = p.ci_tiles;
+  g.nw = (d->n_store + 3) & ~3;
   for (int i = 0; i <= kMaxSeg; ++i) g.cbase[i] = i <= d->nseg ? p.cbase[i] : p.nch;
   for (int i = 0; i < kMaxSeg; ++i) {
     const cvl_conv_seg& q = d->seg[i < d->nseg ? i : 0];
@@ -244,7 +373,7 @@ int cvl_conv_wgrad_sn(const cvl_conv_desc* d, int ngroups, const void* x, const 
     g.dst_base[i] = q.dst_base; g.dst_img[i] = q.dst_img ? q.dst_img : (long)q.Hr * q.Wr;
   }
   g_cvl_conv_last_kernel = CVL_CK_WG_SN;
-  const dim3 grid(p.ci_tiles, p.nch);
+  const dim3 grid(p.ci_tiles * p.nch);
   switch (p.T) {
     case 9: hipLaunchKernelGGL(conv_wgrad_sn_kernel<9>, grid, dim3(NT), 0, s, g); break;
     case 1: hipLaunchKernelGGL(conv_wgrad_sn_kernel<1>, grid, dim3(NT), 0, s, g); break;
@@ -258,7 +387,8 @@ int cvl_conv_wgrad_sn(const cvl_conv_desc* d, int ngroups, const void* x, const 
   for (int gq = 0; gq < kMaxSeg; ++gq) r.dw[gq] = gq < ngroups ? dw[gq] : nullptr;
   for (int gq = 0; gq <= kMaxSeg; ++gq) r.cb[gq] = gq <= ngroups ? p.cbase[gq * spg] : p.nch;
   r.n_store = d->n_store;
-  r.per = (long)p.T * d->Cin * NP;
+  r.nw = g.nw;
+  r.per = (long)p.T * d->Cin * g.nw;
   r.beta = beta;
   hipLaunchKernelGGL(wgrad_sn_reduce_kernel, dim3((unsigned)((r.per + 255) / 256), ngroups), dim3(256), 0, s, r);
   return cvl_launch_status();

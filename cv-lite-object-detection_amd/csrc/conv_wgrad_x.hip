@@ -190,7 +190,7 @@ __global__ void __launch_bounds__(NT) conv_wgrad_x_kernel(Args g) {
   const int co0 = (tile % co_tiles_) * BCO, k0 = (tile / co_tiles_) * BKK;
   const int m_lo = gm0 + split * chunk_;
   const int m_hi = min(m_lo + chunk_, gm1);
-  const int nsteps = m_hi > m_lo ? (m_hi - m_lo) / SR : 0;
+  const int nsteps = (abl & 256) ? 0 : m_hi > m_lo ? (m_hi - m_lo) / SR : 0;   // (256: measurement, no loop)
 
   // ---- per-lane DMA constants: rows rr + 8 RPI j of each step, 16-B piece pc of the row ---------
   const int rr = C::RPI * wave + lane / C::LPR, pc = lane % C::LPR;
@@ -512,7 +512,7 @@ __global__ void __launch_bounds__(NT) conv_wgrad_x_kernel(Args g) {
   // ---- epilogue: C[co][k] -> out[k][co] (HWIO), 4 consecutive co per lane -------------------------
   float* out = outp + (direct_ ? 0 : (size_t)split * K_ * Cout_);
 #pragma unroll
-  for (int i = 0; i < TM; ++i)
+  for (int i = 0; i < ((abl & 512) ? 0 : TM); ++i)      // (512: measurement, no stores)
 #pragma unroll
     for (int j = 0; j < TN; ++j) {
       const int k = k0 + wk * (BKK / 4) + j * 16 + lr;
