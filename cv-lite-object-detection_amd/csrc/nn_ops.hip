@@ -887,12 +887,29 @@ __global__ void maxpool_bwd_kernel(const cvl_bf16* dy, const uint8_t* arg, cvl_b
 // that touch its 8 x 32 input pixels in LDS once (the per-pixel form above loaded up to four windows'
 // dy + argmax per input pixel), then forms dx in the same window order.
 constexpr int BTY = 8, BTX = 32, BOY = BTY / 2 + 1, BOX = BTX / 2 + 1;
+// BNS: the stem's BN -> ReLU backward first pass fused in (cvl_maxpool3x3s2_backward_bn_relu): the
+// pixel's gradient dy (the value stored, rounded to bf16) meets its z, g = dy * (0 < bn(z) < hi), and
+// the block's (sum g, sum g * xhat) per channel go to part[b][tile][64][2] (bn_colsum_kernel reduces
+// the tiles in a fixed order) -- the separate first pass re-read the 134 MB dy and z at 512 / bs 16
+struct PoolBn {
+  const cvl_bf16* z;
+  const float* mr;
+  const float* gamma;
+  const float* beta;
+  float* part;
+  float act_hi;
+};
+
+template <bool BNS>
 __global__ void __launch_bounds__(NT) maxpool_bwd64_kernel(const cvl_bf16* __restrict__ dy,
                                                            const uint8_t* __restrict__ arg, cvl_bf16* dx, int H,
-                                                           int W, int Ho, int Wo) {
+                                                           int W, int Ho, int Wo, PoolBn pb) {
   constexpr int C = 64;
+  constexpr int NQ = BTY * BTX / (NT / 8);             // output pixels per thread
+  static_assert(BTY * BTX % (NT / 8) == 0, "pool tile");
   __shared__ s16x8 sg[BOY * BOX * 8];
   __shared__ unsigned long long sa[BOY * BOX * 8];
+  __shared__ float red[BNS ? NT / 8 * C * 2 : 1];
   const int tx_n = (W + BTX - 1) / BTX, ty_n = (H + BTY - 1) / BTY;
   const int b = blockIdx.x / (tx_n * ty_n);
   const int r = blockIdx.x - b * tx_n * ty_n;
@@ -914,6 +931,26 @@ __global__ void __launch_bounds__(NT) maxpool_bwd64_kernel(const cvl_bf16* __res
       av[k] = *reinterpret_cast<const unsigned long long*>(arg + o);
     }
   }
+  s16x8 zv[BNS ? NQ : 1];
+  float m[8], rs[8], ga[8], be[8], s1[8], s2[8];
+  if constexpr (BNS) {                               // z of this thread's pixels, in flight with the windows
+#pragma unroll
+    for (int k = 0; k < NQ; ++k) {
+      const int q = (threadIdx.x >> 3) + k * (NT / 8);
+      const int iy = iy0 + q / BTX, ix = ix0 + (q - (q / BTX) * BTX);
+      zv[k] = s16x8{0, 0, 0, 0, 0, 0, 0, 0};
+      if (iy < H && ix < W) zv[k] = ld_rows(pb.z + (((long)b * H + iy) * W + ix) * C + c0);
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      m[u] = pb.mr[((long)b * C + c0 + u) * 2];
+      rs[u] = pb.mr[((long)b * C + c0 + u) * 2 + 1];
+      ga[u] = pb.gamma[c0 + u];
+      be[u] = pb.beta[c0 + u];
+      s1[u] = 0.f;
+      s2[u] = 0.f;
+    }
+  }
 #pragma unroll
   for (int k = 0; k < NPB; ++k) {
     const int p = (threadIdx.x >> 3) + k * (NT / 8);
@@ -922,25 +959,59 @@ __global__ void __launch_bounds__(NT) maxpool_bwd64_kernel(const cvl_bf16* __res
     sa[p * 8 + c8] = av[k];
   }
   __syncthreads();
-  for (int q = threadIdx.x >> 3; q < BTY * BTX; q += NT / 8) {
+#pragma unroll
+  for (int k = 0; k < NQ; ++k) {
+    const int q = (threadIdx.x >> 3) + k * (NT / 8);
     const int iy = iy0 + q / BTX, ix = ix0 + (q - (q / BTX) * BTX);
     if (iy >= H || ix >= W) continue;
     const int wy0 = iy >> 1, wx0 = ix >> 1;
     float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {       // window order (oy, ox) row-major, as maxpool_bwd_kernel
-      const int oy = wy0 + (k >> 1), ox = wx0 + (k & 1);
+    for (int w = 0; w < 4; ++w) {       // window order (oy, ox) row-major, as maxpool_bwd_kernel
+      const int oy = wy0 + (w >> 1), ox = wx0 + (w & 1);
       if (oy > ((iy + 1) >> 1) || ox > ((ix + 1) >> 1)) continue;
       const int p = (oy - oy0) * BOX + (ox - ox0);
       const unsigned t = (unsigned)((iy - (oy * 2 - 1)) * 3 + (ix - (ox * 2 - 1)));
       const unsigned long long am = sa[p * 8 + c8];
-      float gv[8];
-      unpack8(sg[p * 8 + c8], gv);
+      float g[8];
+      unpack8(sg[p * 8 + c8], g);
 #pragma unroll
       for (int u = 0; u < 8; ++u)
-        if (((am >> (8 * u)) & 0xff) == t) acc[u] += gv[u];
+        if (((am >> (8 * u)) & 0xff) == t) acc[u] += g[u];
     }
-    *reinterpret_cast<s16x8*>(dx + (((long)b * H + iy) * W + ix) * C + c0) = pack8(acc);
+    const s16x8 o = pack8(acc);
+    *reinterpret_cast<s16x8*>(dx + (((long)b * H + iy) * W + ix) * C + c0) = o;
+    if constexpr (BNS) {                 // bn_bwd_kernel's pass 0 (mask rebuilt from z) on the stored value
+      float g[8], zz[8];
+      unpack8(o, g);
+      unpack8(zv[k], zz);
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const float a = bn_affine(zz[u], m[u], rs[u], ga[u], be[u]);
+        const float gg = (a > 0.f && a < pb.act_hi) ? g[u] : 0.f;
+        s1[u] += gg;
+        s2[u] += gg * ((zz[u] - m[u]) * rs[u]);
+      }
+    }
+  }
+  if constexpr (BNS) {                   // the block's partials: the NT / 8 pixel slots in a fixed order
+    const int slot = threadIdx.x >> 3;
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      red[(slot * C + c0 + u) * 2] = s1[u];
+      red[(slot * C + c0 + u) * 2 + 1] = s2[u];
+    }
+    __syncthreads();
+    if (threadIdx.x < C) {
+      float t1 = 0.f, t2 = 0.f;
+      for (int k = 0; k < NT / 8; ++k) {
+        t1 += red[(k * C + threadIdx.x) * 2];
+        t2 += red[(k * C + threadIdx.x) * 2 + 1];
+      }
+      float* pp = pb.part + ((long)blockIdx.x * C + threadIdx.x) * 2;    // [b][tile][C][2]: block id order
+      pp[0] = t1;
+      pp[1] = t2;
+    }
   }
 }
 
@@ -1663,13 +1734,50 @@ extern "C" int cvl_maxpool3x3s2_backward(const void* dy, const uint8_t* argmax, 
   if (C == 64) {
     const long blocks = (long)B * ((H + BTY - 1) / BTY) * ((W + BTX - 1) / BTX);
     CVL_CHECK_ARG(blocks < (1l << 31));
-    hipLaunchKernelGGL(maxpool_bwd64_kernel, dim3((unsigned)blocks), dim3(NT), 0, S_, (const cvl_bf16*)dy, argmax,
-                       (cvl_bf16*)dx, H, W, Ho, Wo);
+    hipLaunchKernelGGL(maxpool_bwd64_kernel<false>, dim3((unsigned)blocks), dim3(NT), 0, S_, (const cvl_bf16*)dy, argmax,
+                       (cvl_bf16*)dx, H, W, Ho, Wo, PoolBn{});
     return cvl_launch_status();
   }
   const long total = (long)B * H * W * (C / 8);
   hipLaunchKernelGGL(maxpool_bwd_kernel, dim3(grid_for(total)), dim3(NT), 0, S_, (const cvl_bf16*)dy,
                      argmax, (cvl_bf16*)dx, B, H, W, C, Ho, Wo);
+  return cvl_launch_status();
+}
+
+// The stem's backward front (Keras ResNet50 pool1 -> conv1_relu -> conv1_bn behind fcos.py:30):
+// max-pool backward with the BN -> ReLU backward's first pass fused in (PoolBn), the fixed-order
+// column reduction of the tiles' partials, then the BN backward's second pass (dz, dgamma, dbeta).
+// dy (the pool's input gradient) is still stored: the second pass reads it.
+extern "C" size_t cvl_maxpool3x3s2_backward_bn_relu_workspace_size(int B, int H, int W, int C) {
+  if (B <= 0 || H <= 0 || W <= 0 || C != 64) return 0;
+  const size_t tiles = (size_t)((H + BTY - 1) / BTY) * ((W + BTX - 1) / BTX);
+  return sizeof(acc_u64) * 2 * (size_t)B * C + sizeof(float) * 2 * (size_t)B * tiles * C;
+}
+
+extern "C" int cvl_maxpool3x3s2_backward_bn_relu(const void* dp, const uint8_t* argmax, const void* z,
+                                                 const float* mean_rstd, const float* gamma, const float* beta,
+                                                 void* workspace, size_t workspace_bytes, void* dy, void* dz,
+                                                 float* dgamma, float* dbeta, float beta_acc, float* conv_dbias,
+                                                 int B, int H, int W, int C, cvl_stream_t stream) {
+  CVL_CHECK_ARG(dp && argmax && z && mean_rstd && gamma && beta && workspace && dy && dz && dgamma && dbeta);
+  CVL_CHECK_ARG(C == 64 && B > 0 && H > 0 && W > 0);
+  CVL_CHECK_ARG(workspace_bytes >= cvl_maxpool3x3s2_backward_bn_relu_workspace_size(B, H, W, C));
+  const int Ho = (H + 2 - 3) / 2 + 1, Wo = (W + 2 - 3) / 2 + 1;
+  const int tiles = ((H + BTY - 1) / BTY) * ((W + BTX - 1) / BTX);
+  const long blocks = (long)B * tiles;
+  CVL_CHECK_ARG(blocks < (1l << 31) && (long)H * W < (1l << 31));
+  acc_u64* sums = reinterpret_cast<acc_u64*>(workspace);
+  float* part = reinterpret_cast<float*>(sums + 2 * (size_t)B * C);
+  hipLaunchKernelGGL(maxpool_bwd64_kernel<true>, dim3((unsigned)blocks), dim3(NT), 0, S_, (const cvl_bf16*)dp, argmax,
+                     (cvl_bf16*)dy, H, W, Ho, Wo,
+                     PoolBn{(const cvl_bf16*)z, mean_rstd, gamma, beta, part, INFINITY});
+  hipLaunchKernelGGL(bn_colsum_kernel, dim3((C + 31) / 32, B), dim3(NT), 0, S_, (const float*)part, tiles, C, sums, 1);
+  const int HW = H * W;
+  const int rpb1 = bn_rows_per_blk(B, HW, C);
+  hipLaunchKernelGGL((bn_bwd_kernel<1, 2>), dim3((HW + rpb1 - 1) / rpb1, B + 1), dim3(NT), 0, S_, (const cvl_bf16*)dy,
+                     (const cvl_bf16*)nullptr, (const cvl_bf16*)z, mean_rstd, gamma, (const acc_u64*)sums, (cvl_bf16*)dz,
+                     (cvl_bf16*)nullptr, (float*)nullptr, C, HW, rpb1, 1, 0.f,
+                     BnPG{dgamma, dbeta, conv_dbias, beta_acc, nullptr, 1}, beta, INFINITY);
   return cvl_launch_status();
 }
 

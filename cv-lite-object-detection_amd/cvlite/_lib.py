@@ -80,6 +80,9 @@ SIGNATURES = {
     "cvl_maxpool3x3s2": (c_int, [P, P, P, c_int, c_int, c_int, c_int, P]),
     "cvl_bn_relu_maxpool3x3s2": (c_int, [P, P, P, P, P, P, c_int, c_int, c_int, c_int, P]),
     "cvl_maxpool3x3s2_backward": (c_int, [P, P, P, c_int, c_int, c_int, c_int, P]),
+    "cvl_maxpool3x3s2_backward_bn_relu_workspace_size": (c_size_t, [c_int, c_int, c_int, c_int]),
+    "cvl_maxpool3x3s2_backward_bn_relu": (c_int, [P, P, P, P, P, P, P, c_size_t, P, P, P, P, c_float, P, c_int, c_int,
+                                                  c_int, c_int, P]),
     "cvl_upsample2x_add": (c_int, [P, P, P, c_int, c_int, c_int, c_int, P]),
     "cvl_upsample2x_backward": (c_int, [P, P, c_int, c_int, c_int, c_int, c_float, P]),
     "cvl_relu_backward": (c_int, [P, P, P, ctypes.c_long, c_float, P]),

@@ -481,6 +481,18 @@ def maxpool3x3s2_backward(dy, argmax, dx):
     _lib.call("cvl_maxpool3x3s2_backward_f32" if _is_f32(dy) else "cvl_maxpool3x3s2_backward", ptr(dy), ptr(argmax), ptr(dx), B, H, W, C, stream())
 
 
+def maxpool3x3s2_backward_bn_relu(dp, argmax, z, mean_rstd, gamma, beta, dy, dz, dgamma, dbeta, beta_acc=0.0,
+                                  conv_dbias=None):
+    """maxpool3x3s2_backward + bn_backward_relu of the ResNet stem (C = 64, bf16) with the BN
+    backward's first pass fused into the pool kernel; dy is the pool's input gradient (stored)."""
+    B, H, W, C = z.shape
+    n = int(_lib.load().cvl_maxpool3x3s2_backward_bn_relu_workspace_size(B, H, W, C))
+    ws = torch.empty(n, dtype=torch.uint8, device=z.device)
+    _lib.call("cvl_maxpool3x3s2_backward_bn_relu", ptr(dp), ptr(argmax), ptr(z), ptr(mean_rstd), ptr(gamma),
+              ptr(beta), ptr(ws), n, ptr(dy), ptr(dz), ptr(dgamma), ptr(dbeta), float(beta_acc), ptr(conv_dbias),
+              B, H, W, C, stream())
+
+
 def upsample2x_add(a, b, out, B, H, W, C):
     _lib.call("cvl_upsample2x_add_f32" if _is_f32(a) else "cvl_upsample2x_add", ptr(a), ptr(b), ptr(out), B, H, W, C, stream())
 

@@ -19,6 +19,8 @@ from . import _lib
 STEM_K = 7
 # the stem's BN -> ReLU -> max-pool as one pass from z (CVL_DISPATCH=no_stem_pool_fuse: BN apply + pool)
 FUSE_POOL = not _lib.dispatch("no_stem_pool_fuse")
+# backward: the BN -> ReLU first pass inside the max-pool backward kernel (cvl_maxpool3x3s2_backward_bn_relu)
+FUSE_POOL_BWD = not _lib.dispatch("no_stem_pool_bwd_fuse")
 # projection shortcut's BN applied inside conv3's BN launch (CVL_DISPATCH=no_sc_bn_fuse: stored and re-read)
 FUSE_SC_BN = not _lib.dispatch("no_sc_bn_fuse")
 STEM_KP = 168            # the stem kernels' K: 7 kernel rows x (7 x 3 values padded to 24)
@@ -96,9 +98,13 @@ class Stem(object):
         dz = torch.empty_like(z)
         st = self.bn.store
         dy = torch.empty_like(z)
-        nn.maxpool3x3s2_backward(dp, arg, dy)
-        nn.bn_backward_relu(dy, z, mr, self.bn.gamma, self.bn.beta, dz, st.g(self.bn.gname),
-                            st.g(self.bn.bname), B, Ho * Wo, 64, conv_dbias=self.conv.db)
+        if z.dtype == BF16 and FUSE_POOL_BWD:
+            nn.maxpool3x3s2_backward_bn_relu(dp, arg, z, mr, self.bn.gamma, self.bn.beta, dy, dz, st.g(self.bn.gname),
+                                             st.g(self.bn.bname), conv_dbias=self.conv.db)
+        else:
+            nn.maxpool3x3s2_backward(dp, arg, dy)
+            nn.bn_backward_relu(dy, z, mr, self.bn.gamma, self.bn.beta, dz, st.g(self.bn.gname),
+                                st.g(self.bn.bname), B, Ho * Wo, 64, conv_dbias=self.conv.db)
         if z.dtype != BF16:                         # fp32 parity mode: 7x7 weight gradient in place
             nn.conv_wgrad(self._desc7(B, A.shape[1], A.shape[2], Ho, Wo), A, dz, self.conv.dw)
             return

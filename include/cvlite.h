@@ -372,6 +372,17 @@ int cvl_maxpool3x3s2(const void* x, void* y, uint8_t* argmax, int B, int H, int 
                      cvl_stream_t stream);
 int cvl_maxpool3x3s2_backward(const void* dy, const uint8_t* argmax, void* dx, int B, int H, int W,
                               int C, cvl_stream_t stream);
+/* The stem's backward front (pool1_pool -> conv1_relu -> conv1_bn backward, the TF gradient of
+ * Keras ResNet50's first block behind FCOS/fcos.py:30): max-pool backward of dp [B,Ho,Wo,64] through
+ * argmax into dy [B,H,W,64] (bit-identical to cvl_maxpool3x3s2_backward) with the BN -> ReLU
+ * backward's first pass (mask rebuilt from z) fused into that kernel, then the second pass as
+ * cvl_bn_backward_relu (dz, dgamma, dbeta, conv_dbias = 0).  C = 64 (ResNet conv1) only. */
+size_t cvl_maxpool3x3s2_backward_bn_relu_workspace_size(int B, int H, int W, int C);
+int cvl_maxpool3x3s2_backward_bn_relu(const void* dp, const uint8_t* argmax, const void* z, const float* mean_rstd,
+                                      const float* gamma, const float* beta, void* workspace,
+                                      size_t workspace_bytes, void* dy, void* dz, float* dgamma, float* dbeta,
+                                      float beta_acc, float* conv_dbias, int B, int H, int W, int C,
+                                      cvl_stream_t stream);
 /* FPN top-down (fcos.py:57-60): out[B,H,W,C] = a + nearest_up2(b[B,H/2,W/2,C]); backward:
  * db = sum of dout over each 2x2 block (+ beta*db). */
 int cvl_upsample2x_add(const void* a, const void* b, void* out, int B, int H, int W, int C,

@@ -468,3 +468,44 @@ def test_bn_relu_maxpool_matches_apply_then_pool(B, H, W):
     nn.bn_relu_maxpool3x3s2(z, mr, gamma, beta, p, a)
     assert torch.equal(p.view(torch.int16), p_ref.view(torch.int16))
     assert torch.equal(a, a_ref)
+
+
+@pytest.mark.parametrize("B,H,W", [(2, 256, 256), (3, 17, 23)])
+def test_maxpool_backward_bn_relu_fused(B, H, W):
+    """cvl_maxpool3x3s2_backward_bn_relu (the stem's pool1 -> conv1_relu -> conv1_bn backward with the
+    BN first pass inside the pool kernel) vs cvl_maxpool3x3s2_backward + cvl_bn_backward_relu: the
+    pool gradient dy bit-exact, dz / dgamma / dbeta equal up to the order of the first-pass sums
+    (fp32 partials over pool tiles instead of row chunks), conv_dbias zeroed; run to run bit-identical."""
+    from cvlite import ops_nn as nn
+    C = 64
+    dev = torch.device("cuda")
+    g = torch.Generator(device="cpu").manual_seed(B * H + W + 1)
+    z = (torch.randn(B, H, W, C, generator=g) * 2.0).to(BF).to(dev)
+    mr = torch.stack([torch.randn(B, C, generator=g) * 0.3, torch.rand(B, C, generator=g) + 0.5], -1).float().to(dev)
+    gamma = (torch.rand(C, generator=g) + 0.5).to(dev)
+    beta = (torch.randn(C, generator=g) * 0.5).to(dev)
+    Ho, Wo = (H + 2 - 3) // 2 + 1, (W + 2 - 3) // 2 + 1
+    p = torch.empty((B, Ho, Wo, C), dtype=BF, device=dev)
+    a = torch.empty((B, Ho, Wo, C), dtype=torch.uint8, device=dev)
+    nn.bn_relu_maxpool3x3s2(z, mr, gamma, beta, p, a)
+    dp = torch.randn((B, Ho, Wo, C), generator=g).to(BF).to(dev)
+    dy_r, dz_r = torch.empty_like(z), torch.empty_like(z)
+    dg_r, db_r = torch.zeros(C, device=dev), torch.zeros(C, device=dev)
+    nn.maxpool3x3s2_backward(dp, a, dy_r)
+    nn.bn_backward_relu(dy_r, z, mr, gamma, beta, dz_r, dg_r, db_r, B, H * W, C)
+    outs = []
+    for _ in range(2):
+        dy, dz = torch.full_like(z, 7.0), torch.full_like(z, 7.0)
+        dg, db, cb = torch.zeros(C, device=dev), torch.zeros(C, device=dev), torch.full((C,), 3.0, device=dev)
+        nn.maxpool3x3s2_backward_bn_relu(dp, a, z, mr, gamma, beta, dy, dz, dg, db, conv_dbias=cb)
+        outs.append((dy, dz, dg, db, cb))
+    dy, dz, dg, db, cb = outs[0]
+    assert torch.equal(dy.view(torch.int16), dy_r.view(torch.int16))
+    for x0, x1 in zip(outs[0], outs[1]):
+        assert torch.equal(x0, x1)
+    assert float(cb.abs().max()) == 0.0
+    torch.testing.assert_close(dg, dg_r, rtol=1e-4, atol=1e-4 * float(dg_r.abs().max()))
+    torch.testing.assert_close(db, db_r, rtol=1e-4, atol=1e-4 * float(db_r.abs().max()))
+    d = (dz.float() - dz_r.float()).abs()
+    assert float(d.max()) <= 2 ** -6 * float(dz_r.float().abs().max()), float(d.max())
+    assert float((d > 0).float().mean()) < 0.02

@@ -97,11 +97,15 @@ def test_stem_module_matches_direct_conv():
     from cvlite import ops_nn as nn
     dw = torch.empty((192, 64), dtype=torch.float32, device="cuda")
     # recompute dz exactly as the module did (maxpool backward + BN backward are checked elsewhere)
+    from cvlite.resnet import FUSE_POOL_BWD
     dy = torch.empty_like(z)
-    nn.maxpool3x3s2_backward(dp, saved[4], dy)
     dz = torch.empty_like(z)
     gb, bb = torch.zeros(64, device="cuda"), torch.zeros(64, device="cuda")
-    nn.bn_backward_relu(dy, z, saved[3], stem.bn.gamma, stem.bn.beta, dz, gb, bb, B, z.shape[1] * z.shape[2], 64)
+    if FUSE_POOL_BWD:
+        nn.maxpool3x3s2_backward_bn_relu(dp, saved[4], z, saved[3], stem.bn.gamma, stem.bn.beta, dy, dz, gb, bb)
+    else:
+        nn.maxpool3x3s2_backward(dp, saved[4], dy)
+        nn.bn_backward_relu(dy, z, saved[3], stem.bn.gamma, stem.bn.beta, dz, gb, bb, B, z.shape[1] * z.shape[2], 64)
     nn.stem_wgrad(x, dz, dw)
     torch.cuda.synchronize()
     assert torch.equal(stem.conv.dw.view(7, 21, 64), dw.view(8, 24, 64)[:7, :21])
