@@ -870,6 +870,22 @@ def check_maxpool3x3s2_backward(lp, name, launch, dy, argmax, dx):
     lp.cmp(name, "3x3/2 bwd %dx%dx%d B%d" % (H, W, C, B), "dx", dx, _pool3_bwd_ref(dy, argmax, H, W))
 
 
+def check_maxpool3x3s2_backward_bn_relu(lp, name, launch, dp, argmax, z, mean_rstd, gamma, beta, dy, dz, dgamma, dbeta,
+                                        beta_acc=0.0, conv_dbias=None):
+    """The stem's fused pool1 / conv1_relu / conv1_bn backward: dy against the pool reference, then dz /
+    dgamma / dbeta / conv_dbias as check_bn_backward_relu on that dy."""
+    dg0, db0 = _clone(dgamma, dbeta)
+    (zr,) = _keep_inputs(dz, z)
+    launch(dp, argmax, z, mean_rstd, gamma, beta, dy, dz, dgamma, dbeta, beta_acc=beta_acc, conv_dbias=conv_dbias)
+    B, H, W, C = z.shape
+    HW = H * W
+    lp.cmp(name, "3x3/2 bwd %dx%dx%d B%d" % (H, W, C, B), "dy", dy, _pool3_bwd_ref(dp, argmax, H, W))
+    dyr = dy.clone()
+    mask = _mask_relu_z(zr, mean_rstd, gamma, beta, B, HW, C)
+    _check_bn_bwd(lp, name, "C%d HW%d B%d pool relu(z)" % (C, HW, B), dyr, zr, mean_rstd, gamma, dz, None, 0.0, None,
+                  dgamma, dbeta, dg0, db0, beta_acc, conv_dbias, B, HW, C, mask)
+
+
 def _up2(b):
     return b.repeat_interleave(2, 1).repeat_interleave(2, 2)
 
@@ -1192,6 +1208,7 @@ CHECKS = {
     "bn_relu_maxpool3x3s2": check_bn_relu_maxpool,
     "maxpool3x3s2": check_maxpool3x3s2,
     "maxpool3x3s2_backward": check_maxpool3x3s2_backward,
+    "maxpool3x3s2_backward_bn_relu": check_maxpool3x3s2_backward_bn_relu,
     "upsample2x_add": check_upsample2x_add,
     "upsample2x_backward": check_upsample2x_backward,
     "relu_backward": check_relu_backward,
