@@ -233,15 +233,18 @@ __global__ void __launch_bounds__(NT, 2) stem_fwd_kernel(StemArgs g) {
       t_ref += c1 - c0;
       c0 = c1;
     }
-    // epilogue: D[co = i*16 + lg*4 + e][px = wave*64 + j*16 + lr]
+    // epilogue: D[co = i*16 + lg*4 + e][px = wave*64 + j*16 + lr]; one v_permlane16_swap per packed
+    // register regroups channel blocks (2m, 2m+1) so a lane holds 8 consecutive channels of its pixel
+    // (32 m + lgo ..): two 16-B stores per pixel instead of four 8-B ones
     cvl_bf16* zrow = g.z + ((long)(t.b * g.Ho + oy) * g.Wo + t.x0) * CO;
+    const int lgo = ((lg & 1) ? 16 : 0) + ((lg & 2) ? 8 : 0);
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const int px = wave * 64 + j * 16 + lr;
       const bool ok = px < t.npx;
+      unsigned pk[4][2];
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        s16x4 o;
         float r[4];
 #pragma unroll
         for (int e = 0; e < 4; e += 2) {            // one v_cvt_pk_bf16_f32 per channel pair (RNE)
@@ -250,8 +253,7 @@ __global__ void __launch_bounds__(NT, 2) stem_fwd_kernel(StemArgs g) {
           const unsigned u = __builtin_bit_cast(unsigned, h);
           r[e] = __uint_as_float(u << 16);
           r[e + 1] = __uint_as_float(u & 0xffff0000u);
-          o[e] = (short)(u & 0xffffu);
-          o[e + 1] = (short)(u >> 16);
+          pk[i][e >> 1] = u;
         }
         if (ok) {                                   // packed fp32 adds / fmas on channel pairs
 #pragma unroll
@@ -260,8 +262,19 @@ __global__ void __launch_bounds__(NT, 2) stem_fwd_kernel(StemArgs g) {
             s1[i][e] += v;
             s2[i][e] = __builtin_elementwise_fma(v, v, s2[i][e]);
           }
-          *reinterpret_cast<s16x4*>(zrow + (long)px * CO + i * 16 + lg * 4) = o;
         }
+      }
+#pragma unroll
+      for (int m = 0; m < 2; ++m) {
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const auto sw = __builtin_amdgcn_permlane16_swap(pk[2 * m][h], pk[2 * m + 1][h], false, false);
+          pk[2 * m][h] = sw[0];
+          pk[2 * m + 1][h] = sw[1];
+        }
+        if (ok)
+          *reinterpret_cast<u32x4*>(zrow + (long)px * CO + 32 * m + lgo) =
+              u32x4{pk[2 * m][0], pk[2 * m][1], pk[2 * m + 1][0], pk[2 * m + 1][1]};
       }
     }
     if (stamp) t_epi += __builtin_amdgcn_s_memtime() - c0;
