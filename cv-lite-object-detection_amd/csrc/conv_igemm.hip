@@ -558,20 +558,23 @@ static cvl_conv_desc s2dgrad3_desc(const cvl_conv_desc* d, const cvl_bf16* sub) 
   return dd;
 }
 
+// the pixels a strided data gradient's scatter does not reach, zeroed: one block row per (image,
+// map row) -- rows with y % s != 0 are all gaps, the others every x % s != 0 -- and threads over
+// (x, 16-B column chunk), 32-bit index math (the flat 64-bit-division form was VALU-bound)
 __global__ void zero_gaps_kernel(void* dst, int is_f32, long dst_base, long dst_img, int ld, int coff, int n,
                                  int B, int H, int W, int s) {
-  const long rows = (long)B * H * W;
   const int n8 = is_f32 ? n : n / 8;
-  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < rows * n8; i += (long)gridDim.x * blockDim.x) {
-    const long r = i / n8;
-    const int c = (int)(i - r * n8);
-    const int img = (int)(r / ((long)H * W));
-    const int q = (int)(r - (long)img * H * W);
-    const int y = q / W, x = q - (q / W) * W;
-    if (y % s == 0 && x % s == 0) continue;
-    const long row = dst_base + (long)img * dst_img + q;
-    if (is_f32) reinterpret_cast<float*>(dst)[row * ld + coff + c] = 0.f;
-    else *reinterpret_cast<s16x8*>(reinterpret_cast<cvl_bf16*>(dst) + row * ld + coff + c * 8) = s16x8{0, 0, 0, 0, 0, 0, 0, 0};
+  for (int line = blockIdx.y; line < B * H; line += gridDim.y) {
+    const int img = line / H, y = line - img * H;
+    const bool full = y % s != 0;
+    const long base = dst_base + (long)img * dst_img + (long)y * W;
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < W * n8; i += gridDim.x * blockDim.x) {
+      const int x = i / n8, c = i - x * n8;
+      if (!full && x % s == 0) continue;
+      const long row = base + x;
+      if (is_f32) reinterpret_cast<float*>(dst)[row * ld + coff + c] = 0.f;
+      else *reinterpret_cast<s16x8*>(reinterpret_cast<cvl_bf16*>(dst) + row * ld + coff + c * 8) = s16x8{0, 0, 0, 0, 0, 0, 0, 0};
+    }
   }
 }
 
@@ -669,11 +672,13 @@ int conv_igemm_call(const cvl_conv_desc* d, const void* src, void* dst, uint64_t
     CVL_CHECK_ARG(d->dst_f32 || (d->ld_dst % 8 == 0 && d->dst_coff % 8 == 0 && d->n_store % 8 == 0));
     if (d->beta == 0.f) {
       const cvl_conv_seg& q = d->seg[0];
-      const long work = (long)d->B * q.Hr * q.Wr * (d->dst_f32 ? d->n_store : d->n_store / 8);
-      int blocks = (int)((work + NT - 1) / NT);
-      blocks = blocks > 8192 ? 8192 : (blocks < 1 ? 1 : blocks);
-      hipLaunchKernelGGL(zero_gaps_kernel, dim3(blocks), dim3(NT), 0, s, dst, d->dst_f32, q.dst_base, q.dst_img,
-                         d->ld_dst, d->dst_coff, d->n_store, d->B, q.Hr, q.Wr, d->stride);
+      const long line = (long)q.Wr * (d->dst_f32 ? d->n_store : d->n_store / 8);
+      CVL_CHECK_ARG(line < (1l << 31) && (long)d->B * q.Hr < (1l << 31));
+      const int bx = (int)((line + NT - 1) / NT);
+      const int by = d->B * q.Hr < 65535 ? d->B * q.Hr : 65535;
+      hipLaunchKernelGGL(zero_gaps_kernel, dim3(bx < 1 ? 1 : bx, by), dim3(NT), 0, s, dst, d->dst_f32,
+                         q.dst_base, q.dst_img, d->ld_dst, d->dst_coff, d->n_store,
+                         d->B, q.Hr, q.Wr, d->stride);
       const int zst = cvl_launch_status();
       if (zst) return zst;
     }
