@@ -87,7 +87,13 @@ struct ConvArgs {
   float bhi;
   const cvl_bf16* by;     // non-null: the ReLU mask comes from y > 0 (a residual unit's output), not bn(z)
   unsigned long long* probe;   // cvl_probe_arm slot of this launch (kernels that support it), or null
+  const cvl_bf16* ymask;       // data gradient through a ReLU: outputs where ymask <= 0 stored as 0 (X32 SW only)
 };
+
+// cvl_conv_igemm_relu_mask: the ReLU output whose mask the next launch's epilogue may apply; a kernel
+// that applies it sets g_cvl_ymask_used (else the caller runs the separate ReLU backward)
+extern thread_local const void* g_cvl_ymask;
+extern thread_local int g_cvl_ymask_used;
 
 // cvl_probe_arm (probe.hip): the slot armed for the current cvl_conv_igemm call (taken at its entry;
 // take = clear it, so one armed slot times at most one launch)
@@ -164,6 +170,7 @@ static inline int cvl_conv_prepare(const cvl_conv_desc* d, int bm, ConvArgs* a) 
   a->bz = nullptr; a->bmr = nullptr; a->bga = nullptr; a->bbe = nullptr; a->bsum = nullptr; a->bhi = 0.f;
   a->by = nullptr;
   a->probe = nullptr;
+  a->ymask = nullptr;
   a->acc_slots = cvl_bn_acc_slots();
   a->nseg = d->nseg;
   a->B = d->B;

@@ -579,6 +579,8 @@ __global__ void zero_gaps_kernel(void* dst, int is_f32, long dst_base, long dst_
 }
 
 thread_local int g_cvl_conv_last_kernel = CVL_CK_NONE;
+thread_local const void* g_cvl_ymask = nullptr;
+thread_local int g_cvl_ymask_used = 0;
 
 extern "C" int cvl_conv_igemm_last_kernel(void) { return g_cvl_conv_last_kernel; }
 
@@ -638,6 +640,35 @@ extern "C" int cvl_conv_igemm(const cvl_conv_desc* d, const void* src, void* dst
   const int st = conv_igemm_call(d, src, dst, bn_stats_acc, workspace, workspace_bytes, stream);
   cvl_probe_leave_call();
   return st;
+}
+
+int cvl_relu_backward(const void* dy, const void* y, void* dx, long n, float beta, cvl_stream_t stream);
+
+// A data gradient through a ReLU (FPNDetector.trunk_backward: the heads' data gradients into the
+// towers' ReLU outputs, fcos.py:16-27 / 76-101): dst = dgrad(src) * (y > 0), y laid out as dst.  The
+// X32 register epilogue applies the mask; any other kernel's launch is followed by the separate
+// ReLU backward (then dst must be dense: ld_dst == n_store, dst_coff 0).  Bit-identical to
+// cvl_conv_igemm + cvl_relu_backward either way.
+extern "C" int cvl_conv_igemm_relu_mask(const cvl_conv_desc* d, const void* src, void* dst, const void* y,
+                                        void* workspace, size_t workspace_bytes, cvl_stream_t stream) {
+  CVL_CHECK_ARG(d && src && dst && y && d->mode == CVL_CONV_DGRAD && d->prec == CVL_PREC_BF16 && !d->dst_f32 &&
+                d->beta == 0.f && !d->relu_out);
+  g_cvl_ymask = cvl_dispatch_flag("no_relu_mask_fuse") ? nullptr : y;
+  g_cvl_ymask_used = 0;
+  cvl_probe_enter_call();
+  const int st = conv_igemm_call(d, src, dst, nullptr, workspace, workspace_bytes, stream);
+  cvl_probe_leave_call();
+  const int used = g_cvl_ymask_used;
+  g_cvl_ymask = nullptr;
+  g_cvl_ymask_used = 0;
+  if (st || used) return st;
+  CVL_CHECK_ARG(d->ld_dst == d->n_store && d->dst_coff == 0);
+  long rows = 0;
+  for (int i = 0; i < d->nseg; ++i) {
+    const long e = d->seg[i].dst_base + (long)d->B * (d->seg[i].dst_img ? d->seg[i].dst_img : (long)d->seg[i].Hr * d->seg[i].Wr);
+    rows = e > rows ? e : rows;
+  }
+  return cvl_relu_backward(dst, y, dst, rows * d->n_store, 0.f, stream);
 }
 
 namespace {

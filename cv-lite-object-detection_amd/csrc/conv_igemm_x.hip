@@ -251,6 +251,14 @@ __device__ __forceinline__ void x32_body(const ConvArgs& a) {
         const int img = ml / HWr, q = ml - img * HWr;
         drow = conv_dst_row(a, S, img, q);
       }
+      s16x8 ym[TN / 2];                         // ReLU mask rows (data gradient through a ReLU)
+      if (a.ymask) {
+#pragma unroll
+        for (int jp = 0; jp < TN / 2; ++jp) {
+          const int n = min(n0 + wn * WN + jp * 32 + lgo, a.n_store - 8);
+          ym[jp] = *reinterpret_cast<const s16x8*>(a.ymask + drow * a.ld_dst + a.dst_coff + n);
+        }
+      }
 #pragma unroll
       for (int jp = 0; jp < TN / 2; ++jp) {
         unsigned pk[2][2];
@@ -271,8 +279,12 @@ __device__ __forceinline__ void x32_body(const ConvArgs& a) {
         }
         const int n = n0 + wn * WN + jp * 32 + lgo;
         if (n >= a.n_store) continue;
-        *reinterpret_cast<s16x8*>(reinterpret_cast<cvl_bf16*>(a.dst) + drow * a.ld_dst + a.dst_coff + n) =
-            __builtin_bit_cast(s16x8, (u32x4){pk[0][0], pk[0][1], pk[1][0], pk[1][1]});
+        s16x8 o = __builtin_bit_cast(s16x8, (u32x4){pk[0][0], pk[0][1], pk[1][0], pk[1][1]});
+        if (a.ymask) {                          // relu_bwd_kernel's g = y > 0 ? g : 0 on the stored value
+#pragma unroll
+          for (int u = 0; u < 8; ++u) o[u] = bf16_to_f32((cvl_bf16)ym[jp][u]) > 0.f ? o[u] : (short)0;
+        }
+        *reinterpret_cast<s16x8*>(reinterpret_cast<cvl_bf16*>(a.dst) + drow * a.ld_dst + a.dst_coff + n) = o;
       }
     }
     return;
@@ -312,6 +324,10 @@ int cvl_conv_igemm_x(const cvl_conv_desc* d, const ConvArgs& a, hipStream_t s) {
   // SW epilogue: bf16 destination in 8-channel chunks, no BN statistics, no beta
   const bool sw = !a.dst_f32 && !a.stats && a.beta == 0.f && a.n_store % 8 == 0 && a.ld_dst % 8 == 0 &&
                   a.dst_coff % 8 == 0 && !cvl_dispatch_flag("x_no_sw");
+  if (sw && g_cvl_ymask && !a.relu_out) {          // the ReLU mask in the register epilogue
+    am.ymask = reinterpret_cast<const cvl_bf16*>(g_cvl_ymask);
+    g_cvl_ymask_used = 1;
+  }
 #ifdef CVL_MEASURE
   if (am.dbg) {
     if (dg && sw) hipLaunchKernelGGL((conv_igemm_x32_kernel<true, true, true>), grid, dim3(NT), 0, s, am);

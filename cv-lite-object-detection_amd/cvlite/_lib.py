@@ -42,6 +42,7 @@ SIGNATURES = {
     "cvl_fcos_v1_decode": (c_int, [P, c_int, c_int, c_int, c_float, c_float, P, P]),
     "cvl_conv_igemm_workspace_size": (c_size_t, [P]),
     "cvl_conv_igemm": (c_int, [P, P, P, P, P, c_size_t, P]),
+    "cvl_conv_igemm_relu_mask": (c_int, [P, P, P, P, P, c_size_t, P]),
     "cvl_conv_igemm_last_kernel": (c_int, []),
     "cvl_conv_kernel_name": (ctypes.c_char_p, [c_int]),
     "cvl_centernet_peak_decode_workspace_size": (ctypes.c_size_t, [c_int, c_int, c_int, c_int]),

@@ -9,9 +9,12 @@ import math
 
 import torch
 
-from . import ops_nn as nn
+from . import _lib, ops_nn as nn
 from .fpn_det import FPN_C, STRIDES, FPNDetector  # noqa: F401
 from .layers import Conv
+
+# the towers' final ReLU backward inside the heads' data-gradient epilogue (cvl_conv_igemm_relu_mask)
+FUSE_TOP_RELU = not _lib.dispatch("no_top_relu_fuse")
 
 
 class FCOSNet(FPNDetector):
@@ -76,6 +79,11 @@ class FCOSNet(FPNDetector):
             segs = [nn.seg(h, w, h, w, heads[l].wd, None, src_base=off[l], src_img=P, dst_base=B * off[l],
                            dst_img=h * w) for l, (h, w) in enumerate(shapes)]
             d = heads[0].dgrad_desc(B, segs, ld_dst=FPN_C)
-            nn.conv_igemm(d, dout, dA)
+            fuse = FUSE_TOP_RELU and dA.dtype == torch.bfloat16      # (fp32 parity mode: two launches)
+            if fuse:                  # the towers' final ReLU backward in the data gradient's epilogue
+                nn.conv_igemm_relu_mask(d, dout, dA, acts[-1])
+            else:
+                nn.conv_igemm(d, dout, dA)
             dAs.append(dA)
+        self._top_relu_done = fuse
         return dAs

@@ -275,9 +275,12 @@ class FPNDetector(object):
         paired = PAIR_TOWERS and (dAs[1].data_ptr() - dAs[0].data_ptr() == BP * FPN_C * dAs[0].element_size()
                   and dAs[0].is_contiguous() and dAs[1].is_contiguous())
         pair0 = pair_tower0_dgrad()
-        # the towers' final ReLU: one launch over both halves when they are one buffer
+        # the towers' final ReLU: one launch over both halves when they are one buffer (skipped when
+        # the heads' data gradients applied it in their epilogues: FCOSNet._heads_backward)
         y_top = s["tower_bufs"][-1]
-        if paired and towers[1][-1].data_ptr() - towers[0][-1].data_ptr() == BP * FPN_C * y_top.element_size():
+        if self.__dict__.pop("_top_relu_done", False):
+            pass
+        elif paired and towers[1][-1].data_ptr() - towers[0][-1].data_ptr() == BP * FPN_C * y_top.element_size():
             dA_all = torch.as_strided(dAs[0], (2 * BP, FPN_C), (FPN_C, 1))
             nn.relu_backward(dA_all, y_top, dA_all)
         else:

@@ -78,6 +78,17 @@ def conv_igemm(desc, src, dst, stats=None):
               n if ws is not None else 0, stream())
 
 
+def conv_igemm_relu_mask(desc, src, dst, y):
+    """Data gradient through a ReLU: dst = dgrad(src) * (y > 0), y laid out as dst (the X32 register
+    epilogue applies the mask; other kernels get the separate ReLU backward).  Bit-identical to
+    conv_igemm + relu_backward."""
+    _prec(desc, src)
+    n = int(_lib.load().cvl_conv_igemm_workspace_size(ctypes.byref(desc)))
+    ws = torch.empty(n, dtype=torch.uint8, device=src.device) if n > 16 else None
+    _lib.call("cvl_conv_igemm_relu_mask", ctypes.byref(desc), ptr(src), ptr(dst), ptr(y), ptr(ws),
+              n if ws is not None else 0, stream())
+
+
 def probe_arm(slot):
     """Time the next conv_igemm launch from inside if it runs the tower kernel (slot: uint64 [4]
     device tensor, zeroed; cvl_probe_arm)."""

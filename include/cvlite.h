@@ -182,6 +182,13 @@ enum { CVL_PREC_BF16 = 0, CVL_PREC_F32 = 1 };
 size_t cvl_conv_igemm_workspace_size(const cvl_conv_desc* d);
 int cvl_conv_igemm(const cvl_conv_desc* d, const void* src, void* dst, uint64_t* bn_stats,
                    void* workspace, size_t workspace_bytes, cvl_stream_t stream);
+/* A data gradient through a ReLU (the TF gradient of the FCOS towers' final ReLU behind the heads,
+ * FCOS/fcos.py:16-27, 76-101): dst = conv data gradient of src (mode CVL_CONV_DGRAD, prec bf16, beta 0,
+ * no relu_out) masked by y > 0, y [rows][ld_dst] laid out as dst.  The tower kernel applies the mask
+ * in its register epilogue; otherwise the plain launch is followed by cvl_relu_backward (then dst
+ * must be dense: ld_dst == n_store, dst_coff 0).  Bit-identical to cvl_conv_igemm + cvl_relu_backward. */
+int cvl_conv_igemm_relu_mask(const cvl_conv_desc* d, const void* src, void* dst, const void* y, void* workspace,
+                             size_t workspace_bytes, cvl_stream_t stream);
 
 /* Test / profiling hook: the kernel variant the last cvl_conv_igemm / cvl_conv_wgrad* call on THIS
  * host thread launched.  CVL_CK_* codes; cvl_conv_kernel_name(code) is a static string.  Codes 6

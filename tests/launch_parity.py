@@ -262,6 +262,13 @@ class LaunchParity(object):
             return run
         return wrap
 
+    def orig(self, name):
+        """The unwrapped ops_nn function (a check may run a reference launch with it)."""
+        for mod, n, fn in self._saved:
+            if mod is self.nn and n == name:
+                return fn
+        return getattr(self.nn, name)
+
     def last_kernel(self):
         """Short name of the conv kernel the last launch used (include/cvlite.h CVL_CK_*)."""
         return CK_NAMES.get(int(self.lib.load().cvl_conv_igemm_last_kernel()), "?")
@@ -365,6 +372,18 @@ def check_conv_igemm(lp, name, launch, desc, src, dst, stats=None):
             ref = torch.stack([z.sum(0), (z * z).sum(0)], -1)
             rabs = torch.stack([z.abs().sum(0), (z * z).sum(0)], -1)
             lp.add(name, _detail(desc, s, desc.B) + " img%d" % b, "bn_stats", red_err(got[b], ref, rabs), 1e-6, kern)
+
+
+def check_conv_igemm_relu_mask(lp, name, launch, desc, src, dst, y):
+    """The data gradient with the ReLU mask in its epilogue: the plain launch (checked against the
+    float64 restatement as conv_igemm) masked by y > 0 must equal it bit for bit."""
+    launch(desc, src, dst, y)
+    kern = lp.last_kernel()
+    plain = torch.empty_like(dst)
+    lp.orig("conv_igemm")(desc, src, plain)
+    _conv_check_dst(lp, name, desc, src, plain, None, lp.last_kernel())
+    exp = torch.where(y.reshape(plain.shape).float() > 0, plain, torch.zeros_like(plain))
+    lp.exact(name, _detail(desc, _segs(desc)[0], desc.B) + " relu(y)", "dst", dst, exp, kern)
 
 
 def _wgrad_ref(desc, segs, x, dy):
@@ -1187,6 +1206,7 @@ def check_fcos_loss(lp, name, launch, reg_pred, cls_pred, targets, num_classes, 
 
 CHECKS = {
     "conv_igemm": check_conv_igemm,
+    "conv_igemm_relu_mask": check_conv_igemm_relu_mask,
     "conv_wgrad": check_conv_wgrad,
     "conv_wgrad_grouped": check_conv_wgrad_grouped,
     "conv_wgrad_batch": check_conv_wgrad_batch,

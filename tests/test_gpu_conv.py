@@ -651,3 +651,37 @@ def test_head_dgrad_cin32_on_x32(dispatch, B, H):
         outs.append(dx.double())
     for o in outs:
         torch.testing.assert_close(o, x.grad, rtol=1e-2, atol=2e-2)
+
+
+@pytest.mark.parametrize("fuse", [True, False], ids=["epilogue", "fallback"])
+def test_conv_igemm_relu_mask_matches_dgrad_then_relu(dispatch, fuse):
+    """cvl_conv_igemm_relu_mask (the FCOS heads' data gradients into the towers' final ReLU output,
+    fcos.py:16-27 / 76-101): bit-identical to cvl_conv_igemm + cvl_relu_backward, through the tower
+    kernel's register epilogue (bench geometry: the five levels at bs 16) and through the fallback
+    (CVL_DISPATCH=no_relu_mask_fuse: the plain launch, then the separate ReLU backward)."""
+    from cvlite import _lib, ops_nn as nn
+    if not fuse:
+        dispatch("no_relu_mask_fuse")
+    B, C, NS = 16, 256, 32
+    shapes = [(64, 64), (32, 32), (16, 16), (8, 8), (4, 4)]
+    off, o = [], 0
+    for h, w in shapes:
+        off.append(o)
+        o += h * w
+    P = o
+    g = torch.Generator().manual_seed(31)
+    dout = rnd(B * P, NS, gen=g).to(BF).cuda()                     # head gradients [B, P, 32] image-major
+    y = torch.relu(rnd(B * P, C, gen=g)).to(BF).cuda()             # tower ReLU output, level-major
+    y[::7, ::3] = 0.0
+    wd = [rnd(C, 9 * NS, scale=0.05, gen=g).to(BF).cuda() for _ in shapes]
+    segs = [nn.seg(h, w, h, w, wd[l], None, src_base=off[l], src_img=P, dst_base=B * off[l], dst_img=h * w)
+            for l, (h, w) in enumerate(shapes)]
+    d = nn.make_desc(nn.DGRAD, B, NS, 3, 3, 1, 1, 1, C, C, C, segs)
+    ref = torch.empty((B * P, C), dtype=BF, device="cuda")
+    nn.conv_igemm(d, dout, ref)
+    nn.relu_backward(ref, y, ref)
+    got = torch.full((B * P, C), 3.0, dtype=BF, device="cuda")
+    nn.conv_igemm_relu_mask(d, dout, got, y)
+    name = _lib.load().cvl_conv_kernel_name(_lib.load().cvl_conv_igemm_last_kernel()).decode()
+    assert torch.equal(got.view(torch.int16), ref.view(torch.int16)), name
+    assert float(got[y == 0].abs().max()) == 0.0
