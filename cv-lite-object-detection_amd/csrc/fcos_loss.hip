@@ -76,21 +76,13 @@ __device__ __forceinline__ float focal_term(float y, float x, float alpha, float
 // One cell's loss terms and gradients: t(i) targets[i], xc(c) class logit c, xr(j) box / centerness
 // prediction j; putc(c, g) / putcen(g) / putr(j, g) receive the SCALED gradients (class c, the
 // centerness column of the class rows, box j < 5).  Both kernels below run exactly this code.
-template <class TF, class XCF, class XRF, class PC, class PCEN, class PR>
-__device__ __forceinline__ void cell_loss(const LossArgs& a, TF t, XCF xc, XRF xr, PC putc, PCEN putcen, PR putr,
-                                          float& s_cls, float& s_reg, float& s_cen) {
+// everything after the class loop: centerness and box terms of one cell, given its positive mask
+template <class TF, class XCF, class XRF, class PCEN, class PR>
+__device__ __forceinline__ void cell_rest(const LossArgs& a, TF t, XCF xc, XRF xr, PCEN putcen, PR putr, float mask,
+                                          float& s_reg, float& s_cen) {
   const int kind = a.reg_type & 3;
   const bool focal_cen = a.reg_type & 4, sig_reg = a.reg_type & 8, cen_in_cls = a.reg_type & 16;
   const int cc = (a.C + 7) / 8 * 8;                // centerness column of the class rows (CEN_IN_CLS)
-  float tmax = 0.f;
-  for (int c = 0; c < a.C; ++c) {
-    const float y = t(5 + c);
-    tmax = fmaxf(tmax, y);
-    float g;
-    s_cls += focal_term(y, xc(c), a.alpha, a.gamma, &g);
-    putc(c, g * a.grad_scale);
-  }
-  const float mask = (a.reg_type & 32) ? t(5) : (tmax >= 1.0f ? 1.0f : 0.0f);
   float g[5] = {0.f, 0.f, 0.f, 0.f, 0.f};
   // centerness: smooth-L1 on sigmoid(logit) (fcos.py:483-486) or focal (centre variants), all cells
   {
@@ -147,6 +139,21 @@ __device__ __forceinline__ void cell_loss(const LossArgs& a, TF t, XCF xc, XRF x
     g[3] = dL * ((p3 < t3 ? giw : 0.f) + dpw);
   }
   for (int j = 0; j < 5; ++j) putr(j, g[j] * a.grad_scale);
+}
+
+template <class TF, class XCF, class XRF, class PC, class PCEN, class PR>
+__device__ __forceinline__ void cell_loss(const LossArgs& a, TF t, XCF xc, XRF xr, PC putc, PCEN putcen, PR putr,
+                                          float& s_cls, float& s_reg, float& s_cen) {
+  float tmax = 0.f;
+  for (int c = 0; c < a.C; ++c) {
+    const float y = t(5 + c);
+    tmax = fmaxf(tmax, y);
+    float g;
+    s_cls += focal_term(y, xc(c), a.alpha, a.gamma, &g);
+    putc(c, g * a.grad_scale);
+  }
+  const float mask = (a.reg_type & 32) ? t(5) : (tmax >= 1.0f ? 1.0f : 0.0f);
+  cell_rest(a, t, xc, xr, putcen, putr, mask, s_reg, s_cen);
 }
 
 // deterministic block reduction of the three sums in float64 -> partial[b][tile][3]
@@ -214,21 +221,31 @@ __global__ void __launch_bounds__(NTH) fcos_loss_lds_kernel(LossArgs a, int R) {
   const int OC = T5, OR = T5 + ncc;                   // row: targets | class logits | box (5 slots)
   const size_t cell0 = (size_t)b * a.P + p0;
   {
+    // every global load of a batch issued before its LDS stores (a load -> store loop waited for
+    // each load in turn): batches of 8 per thread
     const float* tg = a.tgt + cell0 * T5;
-    for (int i = threadIdx.x; i < ncell * T5; i += NTH) {
-      const int r = i / T5;
-      rows[r * R + (i - r * T5)] = tg[i];
-    }
     const float* cg = a.cls + cell0 * a.ld_cls;
-    for (int i = threadIdx.x; i < ncell * ncc; i += NTH) {
-      const int r = i / ncc, c = i - r * ncc;
-      rows[r * R + OC + c] = cg[(size_t)r * a.ld_cls + c];
-    }
     const float* rg = a.reg + cell0 * a.ld_reg;
-    for (int i = threadIdx.x; i < ncell * nrg; i += NTH) {
-      const int r = i / nrg, j = i - r * nrg;
-      rows[r * R + OR + j] = rg[(size_t)r * a.ld_reg + j];
-    }
+    auto stage = [&](int n, int width, int ld, const float* src, int col0) {
+      for (int base = 0; base < n; base += 8 * NTH) {
+        float v[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          const int i = base + (int)threadIdx.x + u * NTH;
+          const int r = i / width;
+          v[u] = i < n ? src[(size_t)r * ld + (i - r * width)] : 0.f;
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          const int i = base + (int)threadIdx.x + u * NTH;
+          const int r = i / width;
+          if (i < n) rows[r * R + col0 + (i - r * width)] = v[u];
+        }
+      }
+    };
+    stage(ncell * T5, T5, T5, tg, 0);
+    stage(ncell * ncc, ncc, a.ld_cls, cg, OC);
+    stage(ncell * nrg, nrg, a.ld_reg, rg, OR);
   }
   __syncthreads();
   float s_cls = 0.f, s_reg = 0.f, s_cen = 0.f;
@@ -264,6 +281,101 @@ __global__ void __launch_bounds__(NTH) fcos_loss_lds_kernel(LossArgs a, int R) {
   if (a.dcls) grad_rows(a.dcls, a.ld_dcls, a.dcls_bf16, OC, a.C, cen_in_cls ? cc : -1);
   if (a.dreg) grad_rows(a.dreg, a.ld_dreg, a.dreg_bf16, OR, 5, -1);
   block_partials<NTH>(a, s_cls, s_reg, s_cen);
+}
+
+// Four lanes per cell (round 6): the class terms -- 20 focal terms per cell, the kernel's VALU work --
+// spread over the cell's 4 lanes (class c on lane c % 4), each term parked in the cell's target slot
+// 5 + c once read, then the cell's owner lane sums them in class order (the same fp32 sequence as
+// cell_loss) and runs the rest of the cell; the block's partial sums take the 256 owners' values in
+// the fcos_loss_kernel lane order.  Bit-identical to fcos_loss_lds_kernel<256>; 4x the waves (one
+// thread per cell left 1.4 waves per SIMD at 512 / bs 16).
+template <int CPB>
+__global__ void __launch_bounds__(4 * CPB) fcos_loss_lds4_kernel(LossArgs a, int R) {
+  constexpr int NTH = 4 * CPB;
+  extern __shared__ float rows[];
+  float* csum = rows + CPB * R;                       // per-cell (s_cls, s_reg, s_cen)
+  const int b = blockIdx.y, p0 = blockIdx.x * CPB;
+  const int ncell = min(CPB, a.P - p0);
+  const bool cen_in_cls = a.reg_type & 16;
+  const int cc = (a.C + 7) / 8 * 8;
+  const int T5 = 5 + a.C, ncc = cen_in_cls ? cc + 1 : a.C, nrg = cen_in_cls ? 4 : 5;
+  const int OC = T5, OR = T5 + ncc;
+  const size_t cell0 = (size_t)b * a.P + p0;
+  {
+    const float* tg = a.tgt + cell0 * T5;
+    for (int i = threadIdx.x; i < ncell * T5; i += NTH) {
+      const int r = i / T5;
+      rows[r * R + (i - r * T5)] = tg[i];
+    }
+    const float* cg = a.cls + cell0 * a.ld_cls;
+    for (int i = threadIdx.x; i < ncell * ncc; i += NTH) {
+      const int r = i / ncc, c = i - r * ncc;
+      rows[r * R + OC + c] = cg[(size_t)r * a.ld_cls + c];
+    }
+    const float* rg = a.reg + cell0 * a.ld_reg;
+    for (int i = threadIdx.x; i < ncell * nrg; i += NTH) {
+      const int r = i / nrg, j = i - r * nrg;
+      rows[r * R + OR + j] = rg[(size_t)r * a.ld_reg + j];
+    }
+  }
+  __syncthreads();
+  const int cell = threadIdx.x >> 2, sub = threadIdx.x & 3;
+  float tmax = 0.f, y0 = 0.f;
+  if (cell < ncell) {
+    float* row = rows + cell * R;
+    y0 = row[5];
+    for (int c = sub; c < a.C; c += 4) {
+      const float y = row[5 + c];
+      tmax = fmaxf(tmax, y);
+      float g;
+      row[5 + c] = focal_term(y, row[OC + c], a.alpha, a.gamma, &g);   // the term, in its target slot
+      row[OC + c] = g * a.grad_scale;
+    }
+  }
+  tmax = fmaxf(tmax, __shfl_xor(tmax, 1, 64));
+  tmax = fmaxf(tmax, __shfl_xor(tmax, 2, 64));
+  __syncthreads();
+  if (sub == 0) {
+    float s_cls = 0.f, s_reg = 0.f, s_cen = 0.f;
+    if (cell < ncell) {
+      float* row = rows + cell * R;
+      for (int c = 0; c < a.C; ++c) s_cls += row[5 + c];
+      const float mask = (a.reg_type & 32) ? y0 : (tmax >= 1.0f ? 1.0f : 0.0f);
+      cell_rest(
+          a, [&](int i) { return row[i]; }, [&](int c) { return row[OC + c]; }, [&](int j) { return row[OR + j]; },
+          [&](float v) { row[OC + cc] = v; }, [&](int j, float v) { row[OR + j] = v; }, mask, s_reg, s_cen);
+    }
+    csum[cell * 3] = s_cls;
+    csum[cell * 3 + 1] = s_reg;
+    csum[cell * 3 + 2] = s_cen;
+  }
+  __syncthreads();
+  auto grad_rows = [&](void* dst, int ld, int is_bf16, int base, int ncol, int extra) {
+    const int w = is_bf16 ? 8 : 4, npc = ld / w;
+    for (int i = threadIdx.x; i < ncell * npc; i += NTH) {
+      const int r = i / npc, c0 = (i - r * npc) * w;
+      float v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int c = c0 + u;
+        v[u] = (u < w && (c < ncol || c == extra)) ? rows[r * R + base + c] : 0.f;
+      }
+      if (is_bf16) {
+        s16x8 o;
+#pragma unroll
+        for (int u = 0; u < 8; ++u) o[u] = (short)f32_to_bf16(v[u]);
+        *reinterpret_cast<s16x8*>(reinterpret_cast<cvl_bf16*>(dst) + (cell0 + r) * ld + c0) = o;
+      } else {
+        *reinterpret_cast<f32x4*>(reinterpret_cast<float*>(dst) + (cell0 + r) * ld + c0) = f32x4{v[0], v[1], v[2], v[3]};
+      }
+    }
+  };
+  if (a.dcls) grad_rows(a.dcls, a.ld_dcls, a.dcls_bf16, OC, a.C, cen_in_cls ? cc : -1);
+  if (a.dreg) grad_rows(a.dreg, a.ld_dreg, a.dreg_bf16, OR, 5, -1);
+  // lanes 0 .. CPB-1 carry cells 0 .. CPB-1 as fcos_loss_kernel's threads do; the other waves add zeros
+  const bool own = (int)threadIdx.x < CPB;
+  block_partials<NTH>(a, own ? csum[threadIdx.x * 3] : 0.f, own ? csum[threadIdx.x * 3 + 1] : 0.f,
+                      own ? csum[threadIdx.x * 3 + 2] : 0.f);
 }
 
 __global__ void fcos_loss_finalize(const double* partial, float* losses, int tiles) {
@@ -319,7 +431,10 @@ extern "C" int cvl_fcos_loss_ex(const float* reg_pred, int ld_reg, const float* 
       if ((size_t)n * R * sizeof(float) <= 64 * 1024) nth = n;
   a.tiles = (P + (nth ? nth : kThreads) - 1) / (nth ? nth : kThreads);
   const size_t lds = (size_t)nth * R * sizeof(float);
-  if (nth == 256) hipLaunchKernelGGL((fcos_loss_lds_kernel<256>), dim3(a.tiles, B), dim3(256), lds, (hipStream_t)stream, a, R);
+  if (nth == 256 && !cvl_dispatch_flag("loss_lds1") && lds + 256 * 3 * sizeof(float) <= 64 * 1024)
+    hipLaunchKernelGGL((fcos_loss_lds4_kernel<256>), dim3(a.tiles, B), dim3(1024), lds + 256 * 3 * sizeof(float),
+                       (hipStream_t)stream, a, R);
+  else if (nth == 256) hipLaunchKernelGGL((fcos_loss_lds_kernel<256>), dim3(a.tiles, B), dim3(256), lds, (hipStream_t)stream, a, R);
   else if (nth == 128) hipLaunchKernelGGL((fcos_loss_lds_kernel<128>), dim3(a.tiles, B), dim3(128), lds, (hipStream_t)stream, a, R);
   else if (nth == 64) hipLaunchKernelGGL((fcos_loss_lds_kernel<64>), dim3(a.tiles, B), dim3(64), lds, (hipStream_t)stream, a, R);
   else hipLaunchKernelGGL(fcos_loss_kernel, dim3(a.tiles, B), dim3(kThreads), 0, (hipStream_t)stream, a);
