@@ -445,12 +445,17 @@ struct BnPG {
   float beta_acc;
   const acc_u64* psums;   // per-image sums for the parameter gradients (nullptr: `sums`)
   int slots;              // `sums` / `psums` stride: the accumulator mode (fused producers) or 1 (internal)
+  // SC (pass 1 of a projection block's residual unit): the first pass of the SHORTCUT's BN backward
+  // on the same masked gradient g (its dy = g_out), from the shortcut's pre-BN z and (mean, rstd),
+  // into `part` as pass 0 would form it
+  const cvl_bf16* sc_z = nullptr;
+  const float* sc_mr = nullptr;
 };
 
 // MASK selects the ReLU-mask source at compile time (1: y, 2: bn_affine(z) recomputed, 3: no mask --
 // BN without ReLU; 0: decided at run time from y / bnb) -- the run-time form holds the registers of both paths (pass 0: 215 VGPRs,
 // 2 waves/SIMD; pass 1: 141, 3 waves), the specialised ones fit 4-5 waves
-template <int PASS, int MASK = 0>
+template <int PASS, int MASK = 0, bool SC = false>
 __global__ void __launch_bounds__(NT) bn_bwd_kernel(const cvl_bf16* __restrict__ dy, const cvl_bf16* __restrict__ y,
                                                     const cvl_bf16* __restrict__ z, const float* __restrict__ mr,
                                                     const float* __restrict__ gamma, const acc_u64* __restrict__ sums,
@@ -498,6 +503,7 @@ __global__ void __launch_bounds__(NT) bn_bwd_kernel(const cvl_bf16* __restrict__
     const bool act = cgb < C8;
     const int c0 = (act ? cgb : C8 - 1) * 8;
     float m[8], rs[8], s1[8], s2[8], k1[8], k2[8], gm[8], ga[8], be[8];
+    float msc[8], rssc[8];                          // SC: the shortcut BN's (mean, rstd)
     // mask source: y (relu output, residual units) or, when y is null and bnb is given, the
     // ReLU of bn_affine(z) recomputed (non-residual units: one tensor fewer to read)
     const bool use_y = PASS != 2 && (MASK == 0 ? y != nullptr : MASK == 1);
@@ -515,11 +521,15 @@ __global__ void __launch_bounds__(NT) bn_bwd_kernel(const cvl_bf16* __restrict__
         k2[u] = (float)acc_dec(sums, bc, 1, pg.slots) * inv;     // mean(g * xhat)
         gm[u] = gamma[c0 + u] * rs[u];
       }
+      if (SC) {
+        msc[u] = pg.sc_mr[bc * 2];
+        rssc[u] = pg.sc_mr[bc * 2 + 1];
+      }
     }
 
     if (rsub < rpp && act) {
       for (int r = r0 + rsub; r < r1; r += rpp * BN_UNR) {
-        s16x8 vg[BN_UNR], vz[BN_UNR], vy[BN_UNR];
+        s16x8 vg[BN_UNR], vz[BN_UNR], vy[BN_UNR], vs[SC ? BN_UNR : 1];
         long off[BN_UNR];
 #pragma unroll
         for (int q = 0; q < BN_UNR; ++q) {
@@ -528,6 +538,7 @@ __global__ void __launch_bounds__(NT) bn_bwd_kernel(const cvl_bf16* __restrict__
           vg[q] = ld_rows(dy + off[q]);
           if (PASS != 2) vz[q] = ld_rows(z + off[q]);
           if (use_y) vy[q] = ld_rows(y + off[q]);
+          if (SC) vs[q] = ld_rows(pg.sc_z + off[q]);
         }
 #pragma unroll
         for (int q = 0; q < BN_UNR; ++q) {
@@ -564,6 +575,15 @@ __global__ void __launch_bounds__(NT) bn_bwd_kernel(const cvl_bf16* __restrict__
             }
           } else if (ok) {
             if (g_out) *reinterpret_cast<s16x8*>(g_out + off[q]) = pack8(g);
+            if (SC) {                                // the shortcut BN's first pass on g (= its dy)
+              float zs[8];
+              unpack8(vs[q], zs);
+#pragma unroll
+              for (int u = 0; u < 8; ++u) {
+                s1[u] += g[u];
+                s2[u] += g[u] * ((zs[u] - msc[u]) * rssc[u]);
+              }
+            }
             float o[8];
 #pragma unroll
             for (int u = 0; u < 8; ++u) {
@@ -581,7 +601,7 @@ __global__ void __launch_bounds__(NT) bn_bwd_kernel(const cvl_bf16* __restrict__
         }
       }
     }
-    if (PASS == 1) continue;                         // pass 1 only writes dz
+    if (PASS == 1 && !SC) continue;                  // pass 1 only writes dz (SC: + the shortcut's partials)
     __syncthreads();
 #pragma unroll
     for (int u = 0; u < 8; ++u) { red[threadIdx.x][u] = s1[u]; red[threadIdx.x][8 + u] = s2[u]; }
@@ -1697,6 +1717,57 @@ extern "C" int cvl_bn_backward_res_sums(const void* dy, const void* y, const voi
   hipLaunchKernelGGL((bn_bwd_kernel<1, 1>), dim3(nchunk, B + 1), dim3(NT), 0, S_, (const cvl_bf16*)dy, (const cvl_bf16*)y,
                      (const cvl_bf16*)z, mean_rstd, gamma, (const acc_u64*)sums, (cvl_bf16*)dz, (cvl_bf16*)g_out, (float*)nullptr,
                      C, HW, rpb, 1, 0.f, BnPG{dgamma, dbeta, conv_dbias, beta_acc, nullptr, g_acc_slots}, (const float*)nullptr, INFINITY);
+  return cvl_launch_status();
+}
+
+// A projection block's residual unit (Keras block1 conv3 BN -> + shortcut BN -> ReLU): the second pass
+// of cvl_bn_backward_res_sums, which also forms the SHORTCUT BN backward's first pass on the same
+// masked gradient (its dy is g_out) from the shortcut's z_sc and (mean, rstd): per-block partials,
+// then the fixed-order column sum into sc_sums [B][C][2] (float64 values, slot mode 1) for
+// cvl_bn_backward_sums.  The shortcut's own first pass -- a re-read of g_out and z_sc -- is gone.
+extern "C" size_t cvl_bn_backward_res_sums_sc_workspace_size(int B, int HW, int C) {
+  if (B <= 0 || HW <= 0 || C <= 0) return 0;
+  const int rpb = bn_rows_per_blk(B, HW, C);
+  return sizeof(float) * 2 * (size_t)B * ((HW + rpb - 1) / rpb) * C;
+}
+
+extern "C" int cvl_bn_backward_res_sums_sc(const void* dy, const void* y, const void* z, const float* mean_rstd,
+                                           const float* gamma, uint64_t* sums, void* dz, void* g_out,
+                                           float* dgamma, float* dbeta, float beta_acc, float* conv_dbias,
+                                           const void* z_sc, const float* mean_rstd_sc, void* workspace,
+                                           size_t workspace_bytes, uint64_t* sc_sums, int B, int HW, int C,
+                                           cvl_stream_t stream) {
+  CVL_CHECK_ARG(dy && y && z && mean_rstd && gamma && sums && dz && g_out && dgamma && dbeta && C % 8 == 0);
+  CVL_CHECK_ARG(z_sc && mean_rstd_sc && workspace && sc_sums && B > 0 && HW > 0);
+  CVL_CHECK_ARG(workspace_bytes >= cvl_bn_backward_res_sums_sc_workspace_size(B, HW, C));
+  const int dst = acc_decode_launch((acc_u64*)sums, 2L * B * C, S_);
+  if (dst) return dst;
+  const int rpb = bn_rows_per_blk(B, HW, C);
+  const int nchunk = (HW + rpb - 1) / rpb;
+  float* part = reinterpret_cast<float*>(workspace);
+  BnPG pg{dgamma, dbeta, conv_dbias, beta_acc, nullptr, g_acc_slots};
+  pg.sc_z = (const cvl_bf16*)z_sc;
+  pg.sc_mr = mean_rstd_sc;
+  hipLaunchKernelGGL((bn_bwd_kernel<1, 1, true>), dim3(nchunk, B + 1), dim3(NT), 0, S_, (const cvl_bf16*)dy,
+                     (const cvl_bf16*)y, (const cvl_bf16*)z, mean_rstd, gamma, (const acc_u64*)sums, (cvl_bf16*)dz,
+                     (cvl_bf16*)g_out, part, C, HW, rpb, 1, 0.f, pg, (const float*)nullptr, INFINITY);
+  hipLaunchKernelGGL(bn_colsum_kernel, dim3((C + 31) / 32, B), dim3(NT), 0, S_, (const float*)part, nchunk, C,
+                     (acc_u64*)sc_sums, 1);
+  return cvl_launch_status();
+}
+
+// Second pass only of a BN WITHOUT ReLU (the projection shortcut's BN) from first-pass sums [B][C][2]
+// in slot mode 1 (cvl_bn_backward_res_sums_sc): dz, dgamma, dbeta (+ conv_dbias = 0).
+extern "C" int cvl_bn_backward_sums(const void* dy, const void* z, const float* mean_rstd, const float* gamma,
+                                    const uint64_t* sums, void* dz, float* dgamma, float* dbeta, float beta_acc,
+                                    float* conv_dbias, int B, int HW, int C, cvl_stream_t stream) {
+  CVL_CHECK_ARG(dy && z && mean_rstd && gamma && sums && dz && dgamma && dbeta && C % 8 == 0 && B > 0 && HW > 0);
+  const int rpb = bn_rows_per_blk(B, HW, C);
+  const int nchunk = (HW + rpb - 1) / rpb;
+  hipLaunchKernelGGL((bn_bwd_kernel<1, 3>), dim3(nchunk, B + 1), dim3(NT), 0, S_, (const cvl_bf16*)dy,
+                     (const cvl_bf16*)nullptr, (const cvl_bf16*)z, mean_rstd, gamma, (const acc_u64*)sums, (cvl_bf16*)dz,
+                     (cvl_bf16*)nullptr, (float*)nullptr, C, HW, rpb, 1, 0.f,
+                     BnPG{dgamma, dbeta, conv_dbias, beta_acc, nullptr, 1}, (const float*)nullptr, INFINITY);
   return cvl_launch_status();
 }
 

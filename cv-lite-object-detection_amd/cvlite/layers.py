@@ -254,6 +254,8 @@ class Conv(object):
 FUSE_BNSUM = not _lib.dispatch("no_bnsum_fuse")
 # ... and a residual unit's (BN3) first pass into the next block's conv1 data gradient (CVL_DISPATCH=no_bnsum_res: off)
 FUSE_BNSUM_RES = FUSE_BNSUM and not _lib.dispatch("no_bnsum_res")
+# ... and a projection shortcut BN's first pass into the residual unit's second pass (no_sc_bnsum: off)
+FUSE_SC_BNSUM = FUSE_BNSUM_RES and not _lib.dispatch("no_sc_bnsum")
 
 # Batched weight gradients (round 6; CVL_DISPATCH=no_wgrad_batch: off).  Inside `with wgrad_batch():`
 # Conv.wgrad collects its 1x1 / 3x3 bf16 problems (keeping their x / dy alive) instead of launching
@@ -416,19 +418,33 @@ class ConvBN(object):
             return None
         return (z, mr, self.bn.gamma, self.bn.beta, arena.take(B, self.bn.c) if arena is not None else None, y)
 
-    def backward(self, dy, saved, dx_out=None, dx_beta=0.0, g_out=None, need_dx=True, sums=None, bn_next=None):
+    def backward(self, dy, saved, dx_out=None, dx_beta=0.0, g_out=None, need_dx=True, sums=None, bn_next=None,
+                 sc_fuse=None):
         """dz = BN backward of dy, the conv's weight gradient, and (need_dx) its data gradient.
         sums: this unit's BN-backward first pass, already formed by the producer of dy (skip it).
         bn_next: the NEXT unit's bn_next_ctx -- the data gradient then also forms that unit's first
-        pass, and the return value is (dx, sums or None) instead of dx."""
+        pass, and the return value is (dx, sums or None) instead of dx.
+        sc_fuse: (z_sc, mean_rstd_sc, sc_sums) of a projection shortcut whose dy is g_out: with the
+        fused first pass (sums given) the second pass also forms the shortcut BN's first pass into
+        sc_sums; self.sc_fused then says whether it did."""
         x, z, y, mr, B, H, W, Ho, Wo, relu, has_res = saved
         c = self.conv.cout
         dz = torch.empty_like(z)
         st = self.bn.store
-        if sums is not None and has_res:                 # residual unit, first pass fused upstream
+        self.sc_fused = False
+        if sums is not None and has_res and sc_fuse is not None and g_out is not None:
+            assert relu                                  # + the projection shortcut BN's first pass
+            nn.bn_backward_res_sums_sc(dy, y, z, mr, self.bn.gamma, sums, dz, g_out, st.g(self.bn.gname),
+                                       st.g(self.bn.bname), sc_fuse[0], sc_fuse[1], sc_fuse[2], B, Ho * Wo, c,
+                                       conv_dbias=self.conv.db)
+            self.sc_fused = True
+        elif sums is not None and has_res:               # residual unit, first pass fused upstream
             assert relu
             nn.bn_backward_res_sums(dy, y, z, mr, self.bn.gamma, sums, dz, g_out, st.g(self.bn.gname),
                                     st.g(self.bn.bname), B, Ho * Wo, c, conv_dbias=self.conv.db)
+        elif sums is not None and not relu:              # BN without ReLU (the shortcut), first pass done
+            nn.bn_backward_sums(dy, z, mr, self.bn.gamma, sums, dz, st.g(self.bn.gname), st.g(self.bn.bname),
+                                B, Ho * Wo, c, conv_dbias=self.conv.db)
         elif sums is not None:                           # first pass fused upstream
             assert relu and not has_res and g_out is None
             nn.bn_backward_relu_sums(dy, z, mr, self.bn.gamma, self.bn.beta, sums, dz, st.g(self.bn.gname),

@@ -13,7 +13,7 @@ import os
 import torch
 
 from . import ops_nn as nn
-from .layers import BF16, BatchNorm, Conv, ConvBN, StatsArena, wgrad_batch
+from .layers import BF16, FUSE_SC_BNSUM, BatchNorm, Conv, ConvBN, StatsArena, wgrad_batch
 from . import _lib
 
 STEM_K = 7
@@ -161,16 +161,22 @@ class Bottleneck(object):
         # also forms their BN backward's first pass (sums), so that pass is skipped
         ctx2, ctx1 = self.c2.bn_next_ctx(sv2, arena), self.c1.bn_next_ctx(sv1, arena)
         s2 = s1 = None
+        # projection blocks: the shortcut BN's first pass rides on conv3's fused second pass
+        sc_fuse = None
+        if self.sc is not None and sums3 is not None and FUSE_SC_BNSUM and dy.dtype == torch.bfloat16:
+            zs, mrs = sv_s[1], sv_s[3]
+            sc_fuse = (zs, mrs, torch.empty((zs.shape[0], self.sc.bn.c, 2), dtype=torch.float64, device=zs.device))
         if ctx2 is not None:
-            dy2, s2 = self.c3.backward(dy, sv3, g_out=g, bn_next=ctx2, sums=sums3)
+            dy2, s2 = self.c3.backward(dy, sv3, g_out=g, bn_next=ctx2, sums=sums3, sc_fuse=sc_fuse)
         else:
-            dy2 = self.c3.backward(dy, sv3, g_out=g, sums=sums3)
+            dy2 = self.c3.backward(dy, sv3, g_out=g, sums=sums3, sc_fuse=sc_fuse)
+        sc_sums = sc_fuse[2] if (sc_fuse is not None and self.c3.sc_fused) else None
         if ctx1 is not None:
             dy1, s1 = self.c2.backward(dy2, sv2, sums=s2, bn_next=ctx1)
         else:
             dy1 = self.c2.backward(dy2, sv2, sums=s2)
         if self.sc is not None:
-            self.sc.backward(g, sv_s, dx_out=dx_out, dx_beta=dx_beta)
+            self.sc.backward(g, sv_s, dx_out=dx_out, dx_beta=dx_beta, sums=sc_sums)
         if prev_ctx is not None and self.c1.conv.stride == 1:
             _, s_prev = self.c1.backward(dy1, sv1, dx_out=dx_out, dx_beta=1.0, sums=s1, bn_next=prev_ctx)
             return dx_out, s_prev

@@ -361,6 +361,22 @@ int cvl_conv_igemm_dgrad_bnsum_res(const cvl_conv_desc* d, const void* src, void
 int cvl_bn_backward_res_sums(const void* dy, const void* y, const void* z, const float* mean_rstd, const float* gamma,
                              uint64_t* sums, void* dz, void* g_out, float* dgamma, float* dbeta, float beta_acc,
                              float* conv_dbias, int B, int HW, int C, cvl_stream_t stream);
+/* A projection block's residual unit (Keras ResNet50 block1: conv3 BN -> + shortcut BN -> ReLU, the
+ * TF gradient through both BNs behind FCOS/fcos.py:30-35): cvl_bn_backward_res_sums that also forms
+ * the shortcut BN backward's first pass on the same masked gradient (the shortcut's dy is g_out) from
+ * the shortcut's pre-BN z_sc and (mean, rstd) -- per-block partials in `workspace`, then a fixed-order
+ * column sum into sc_sums [B][C][2] (float64 values, slot mode 1); cvl_bn_backward_sums then runs the
+ * shortcut's second pass.  The separate first pass over g_out and z_sc is gone. */
+size_t cvl_bn_backward_res_sums_sc_workspace_size(int B, int HW, int C);
+int cvl_bn_backward_res_sums_sc(const void* dy, const void* y, const void* z, const float* mean_rstd,
+                                const float* gamma, uint64_t* sums, void* dz, void* g_out, float* dgamma,
+                                float* dbeta, float beta_acc, float* conv_dbias, const void* z_sc,
+                                const float* mean_rstd_sc, void* workspace, size_t workspace_bytes,
+                                uint64_t* sc_sums, int B, int HW, int C, cvl_stream_t stream);
+/* Second pass only of a BN without ReLU from first-pass sums [B][C][2] (slot mode 1). */
+int cvl_bn_backward_sums(const void* dy, const void* z, const float* mean_rstd, const float* gamma,
+                         const uint64_t* sums, void* dz, float* dgamma, float* dbeta, float beta_acc,
+                         float* conv_dbias, int B, int HW, int C, cvl_stream_t stream);
 
 /* BN -> ReLU6 unit without a residual (MobileNetV2: Keras ReLU(6.)): as cvl_bn_backward_relu with
  * the TF Relu6Grad mask 0 < bn(z) < 6 rebuilt from z in fp32 (the forward's exact pre-clamp value);

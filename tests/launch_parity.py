@@ -700,8 +700,8 @@ def _bn_bwd_ref(dy, z, mr, gamma, B, HW, C, mask, sums=None, group=1):
     xh = ((z.reshape(B, HW, C).float() - m[:, None].float()) * rs[:, None].float()).double()
     if sums is None:
         s1, s2 = g.sum(1), (g * xh).sum(1)
-    else:
-        sv = _acc(sums, B, C)
+    else:                                   # accumulator buffer, or plain float64 [B][C][2] values
+        sv = sums.view(B, C, 2).double() if sums.dtype == F64 else _acc(sums, B, C)
         s1, s2 = sv[..., 0], sv[..., 1]
     if group > 1:
         ng = (B + group - 1) // group
@@ -812,6 +812,36 @@ def check_bn_backward_res_sums(lp, name, launch, dy, y, z, mean_rstd, gamma, sum
     mask = yr.reshape(B, HW, C).float() > 0
     _check_bn_bwd(lp, name, "C%d HW%d B%d res sums" % (C, HW, B), dyr, zr, mean_rstd, gamma, dz, None, 0.0, g_out,
                   dgamma, dbeta, dg0, db0, beta_acc, conv_dbias, B, HW, C, mask, sums=sums)
+
+
+def check_bn_backward_res_sums_sc(lp, name, launch, dy, y, z, mean_rstd, gamma, sums, dz, g_out, dgamma, dbeta,
+                                  z_sc, mean_rstd_sc, sc_sums, B, HW, C, beta_acc=0.0, conv_dbias=None):
+    """check_bn_backward_res_sums, plus the projection shortcut BN's first pass formed on the way:
+    sc_sums = per-image (sum g_out, sum g_out * xhat_sc) against float64."""
+    dg0, db0 = _clone(dgamma, dbeta)
+    dyr, zr = _keep_inputs(dz, dy, z)
+    (yr,) = _keep_inputs(dz, y)
+    launch(dy, y, z, mean_rstd, gamma, sums, dz, g_out, dgamma, dbeta, z_sc, mean_rstd_sc, sc_sums, B, HW, C,
+           beta_acc=beta_acc, conv_dbias=conv_dbias)
+    mask = yr.reshape(B, HW, C).float() > 0
+    d = "C%d HW%d B%d res sums +sc" % (C, HW, B)
+    _check_bn_bwd(lp, name, d, dyr, zr, mean_rstd, gamma, dz, None, 0.0, g_out, dgamma, dbeta, dg0, db0, beta_acc,
+                  conv_dbias, B, HW, C, mask, sums=sums)
+    g = g_out.reshape(B, HW, C).double()
+    ms, rss = mean_rstd_sc.view(B, C, 2)[..., 0], mean_rstd_sc.view(B, C, 2)[..., 1]
+    xh = ((z_sc.reshape(B, HW, C).float() - ms[:, None].float()) * rss[:, None].float()).double()
+    ref = torch.stack([g.sum(1), (g * xh).sum(1)], -1)
+    rabs = torch.stack([g.abs().sum(1), (g * xh).abs().sum(1)], -1)
+    lp.add(name, d, "sc_sums", red_err(sc_sums.view(B, C, 2).double(), ref, rabs), 1e-6)
+
+
+def check_bn_backward_sums(lp, name, launch, dy, z, mean_rstd, gamma, sums, dz, dgamma, dbeta, B, HW, C, beta_acc=0.0,
+                           conv_dbias=None):
+    dg0, db0 = _clone(dgamma, dbeta)
+    dyr, zr = _keep_inputs(dz, dy, z)
+    launch(dy, z, mean_rstd, gamma, sums, dz, dgamma, dbeta, B, HW, C, beta_acc=beta_acc, conv_dbias=conv_dbias)
+    _check_bn_bwd(lp, name, "C%d HW%d B%d sums, no mask" % (C, HW, B), dyr, zr, mean_rstd, gamma, dz, None, 0.0,
+                  None, dgamma, dbeta, dg0, db0, beta_acc, conv_dbias, B, HW, C, None, sums=sums)
 
 
 def check_bn_stats(lp, name, launch, x, B, HW, C, stats):
@@ -1225,6 +1255,8 @@ CHECKS = {
     "bn_backward_relu6": check_bn_backward_relu6,
     "bn_backward_relu_sums": check_bn_backward_relu_sums,
     "bn_backward_res_sums": check_bn_backward_res_sums,
+    "bn_backward_res_sums_sc": check_bn_backward_res_sums_sc,
+    "bn_backward_sums": check_bn_backward_sums,
     "bn_relu_maxpool3x3s2": check_bn_relu_maxpool,
     "maxpool3x3s2": check_maxpool3x3s2,
     "maxpool3x3s2_backward": check_maxpool3x3s2_backward,
