@@ -798,19 +798,31 @@ extern "C" int cvl_conv_igemm_dgrad_bnsum_res(const cvl_conv_desc* d, const void
   CVL_CHECK_ARG(d && fused && y && z && mean_rstd && gamma && beta && sums);
   *fused = 0;
   if (!cvl_tune_flag("CVL_NO_BNSUM_FUSE") && !cvl_tune_flag("CVL_NO_BNSUM_RES") && d->prec == CVL_PREC_BF16 &&
-      d->mode == CVL_CONV_DGRAD && !d->dst_f32 && d->beta != 0.f && d->KH == 1 && d->KW == 1 && d->stride == 1 &&
+      d->mode == CVL_CONV_DGRAD && !d->dst_f32 && d->beta != 0.f && d->KH == 1 && d->KW == 1 &&
+      (d->stride == 1 || !cvl_dispatch_flag("no_bnsum_res_s2")) &&
       // small maps: the fused launch (64-wide N tiles, three prefetched operands) loses to the
       // plain one + the separate pass (A/B per stage; CVL_BNSUM_RES_MIN_HW)
       (long)d->seg[0].Hr * d->seg[0].Wr >= cvl_dispatch_int("bnsum_res_min_hw", 4096) &&
       d->Cin % 32 == 0 && d->Npad % 32 == 0 && d->ld_dst % 8 == 0 && d->dst_coff % 8 == 0 && d->n_store % 8 == 0 &&
       src && dst) {
+    // a strided 1x1 data gradient (a stage's first block accumulating onto its shortcut's) runs as the
+    // dense GEMM over the dY grid with the scatter (dst_up); it accumulates (beta 1), so the gaps keep
+    // the zeros the first launch wrote and contribute nothing to the sums
+    cvl_conv_desc dd;
+    int up = 1, upw = 0;
+    const cvl_conv_desc* dp = d;
+    bool ok = true;
+    if (d->stride != 1) {
+      ok = s2dgrad_transform(d, &dd, &up, &upw);
+      dp = &dd;
+    }
     ConvArgs chk;
-    if (cvl_conv_prepare(d, BM, &chk) == CVL_OK) {
+    if (ok && cvl_conv_prepare(dp, BM, &chk) == CVL_OK) {
       BnSumArgs b{reinterpret_cast<const cvl_bf16*>(z), mean_rstd, gamma, beta, reinterpret_cast<acc_u64*>(sums),
                   INFINITY};
       b.y = reinterpret_cast<const cvl_bf16*>(y);
       g_cvl_conv_last_kernel = CVL_CK_NONE;
-      const int lst = cvl_conv_igemm_l(d, 1, 0, src, dst, nullptr, (hipStream_t)stream, &b, workspace,
+      const int lst = cvl_conv_igemm_l(dp, up, upw, src, dst, nullptr, (hipStream_t)stream, &b, workspace,
                                        workspace_bytes);
       if (lst >= 0) {
         *fused = lst == CVL_OK ? 1 : 0;

@@ -478,11 +478,18 @@ __global__ void __launch_bounds__(NT) conv_igemm_p_kernel(ConvArgs a, int ntiles
     }
     if (BS && ck == 0) {                           // z chunks of tile ct for the epilogue
       const int m0 = (mt0 + ct) * BM;
+      const bool dense_dst = a.dst_up == 1 && S.dst_img == (long)HWr;
 #pragma unroll
       for (int i = 0; i < TM; ++i)
 #pragma unroll
         for (int jp = 0; jp < NJP; ++jp) {
-          const long row = S.dst_base + m0 + wm * C::WM + i * 16 + lr;
+          // (the strided data gradient's scatter: z / y at the output pixel's full-map row)
+          const int ml = m0 + wm * C::WM + i * 16 + lr;
+          long row = S.dst_base + ml;
+          if (!dense_dst && ml < S.rows) {
+            const int img = ml / HWr, q = ml - img * HWr;
+            row = conv_dst_row(a, S, img, q);
+          }
           zv[i][jp] = gload16_untracked(a.bz + row * a.ld_dst + a.dst_coff + n0 + wn * C::WN + jp * 32 + lgo);
           if (BS == 2)
             yv[i][jp] = gload16_untracked(a.by + row * a.ld_dst + a.dst_coff + n0 + wn * C::WN + jp * 32 + lgo);
@@ -518,9 +525,11 @@ int cvl_conv_igemm_p(const cvl_conv_desc* d, const ConvArgs& a0, hipStream_t s) 
   if (cvl_dispatch_flag("no_p")) return -1;
   if (d->KH != 1 || d->KW != 1 || d->pad_t || d->pad_l || a0.relu_in || a0.nseg != 1 || a0.K % BK) return -1;
   // bsum forms: z-mask without beta; y-mask (residual unit) with the beta accumulate
-  if (a0.bsum && (d->mode != CVL_CONV_DGRAD || a0.dst_f32 || (a0.beta != 0.f) != (a0.by != nullptr) ||
-                  a0.dst_up != 1 || a0.stats ||
-                  (a0.seg[0].Hr * a0.seg[0].Wr) % BM || a0.seg[0].dst_img != (long)a0.seg[0].Hr * a0.seg[0].Wr ||
+  // (the residual form also on the strided data gradient's scatter, dst_up 2: the gap pixels' dy is 0,
+  // so the scattered rows' sums are the map's)
+  if (a0.bsum && ((d->mode != CVL_CONV_DGRAD && a0.dst_up == 1) || a0.dst_f32 || (a0.beta != 0.f) != (a0.by != nullptr) ||
+                  (a0.dst_up != 1 && !a0.by) || a0.stats || (a0.seg[0].Hr * a0.seg[0].Wr) % BM ||
+                  (a0.dst_up == 1 && a0.seg[0].dst_img != (long)a0.seg[0].Hr * a0.seg[0].Wr) ||
                   a0.Npad % 64 || cvl_tune_flag("CVL_CONV_P_NO_BSUM")))
     return -1;
   if (d->mode == CVL_CONV_DGRAD && d->stride != 1) return -1;

@@ -23,6 +23,10 @@ FUSE_POOL = not _lib.dispatch("no_stem_pool_fuse")
 FUSE_POOL_BWD = not _lib.dispatch("no_stem_pool_bwd_fuse")
 # projection shortcut's BN applied inside conv3's BN launch (CVL_DISPATCH=no_sc_bn_fuse: stored and re-read)
 FUSE_SC_BN = not _lib.dispatch("no_sc_bn_fuse")
+# a stage's last conv3 BN first pass formed by the next stage's strided conv1 data gradient: opt-in
+# (CVL_DISPATCH=bnsum_res_s2) -- measured neutral to -0.1 % (the fused launch's 64-wide N tiles and
+# three prefetched operands cost what the removed pass saved)
+FUSE_BNSUM_RES_S2 = _lib.dispatch("bnsum_res_s2")
 STEM_KP = 168            # the stem kernels' K: 7 kernel rows x (7 x 3 values padded to 24)
 
 
@@ -177,7 +181,7 @@ class Bottleneck(object):
             dy1 = self.c2.backward(dy2, sv2, sums=s2)
         if self.sc is not None:
             self.sc.backward(g, sv_s, dx_out=dx_out, dx_beta=dx_beta, sums=sc_sums)
-        if prev_ctx is not None and self.c1.conv.stride == 1:
+        if prev_ctx is not None:      # (stride 2: the scattered data gradient, cvl_conv_igemm_dgrad_bnsum_res)
             _, s_prev = self.c1.backward(dy1, sv1, dx_out=dx_out, dx_beta=1.0, sums=s1, bn_next=prev_ctx)
             return dx_out, s_prev
         self.c1.backward(dy1, sv1, dx_out=dx_out, dx_beta=1.0, sums=s1)
@@ -265,14 +269,21 @@ class ResNet50(object):
         arena = saved[2] if len(saved) > 2 else None
         dC = {1: d_taps[0], 2: d_taps[1], 3: d_taps[2]}
         dh = dC[3]
+        pending = None              # the next-processed block's conv3 BN first pass, fused upstream
         for si in range(3, -1, -1):
             st = self.stages[si]
-            pending = None          # the next-processed block's conv3 BN first pass, fused upstream
             # the stage's 1x1 weight gradients: one batched launch at the stage's end (layers.wgrad_batch)
             with wgrad_batch():
                 for bi in range(len(st) - 1, -1, -1):
-                    # an identity predecessor's conv3 BN first pass rides on this block's conv1 dgrad
-                    prev = st[bi - 1].c3.bn_res_ctx(ssv[si][bi - 1][3], arena) if bi >= 1 else None
+                    # the predecessor's conv3 BN first pass rides on this block's conv1 dgrad -- across
+                    # a stage boundary too (a stage's first block: the strided, scattered data gradient
+                    # that completes the previous stage's output gradient)
+                    if bi >= 1:
+                        prev = st[bi - 1].c3.bn_res_ctx(ssv[si][bi - 1][3], arena)
+                    elif si >= 1 and FUSE_BNSUM_RES_S2:
+                        prev = self.stages[si - 1][-1].c3.bn_res_ctx(ssv[si - 1][-1][3], arena)
+                    else:
+                        prev = None
                     if bi == 0 and (si - 1) in dC:
                         # this block's input is the previous stage's tap (C3 / C4), whose buffer
                         # already holds the FPN lateral's gradient: accumulate into it

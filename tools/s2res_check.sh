@@ -1,0 +1,8 @@
+#!/bin/bash
+# stage-boundary residual BN-sum fusion (strided conv1 dgrad): tests + A/B
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"; mkdir -p gpurun_out
+timeout -k 10 600 python3 -u -m pytest -x -q --timeout 200 --timeout-method thread -m gpu tests/test_gpu_launch_parity.py tests/test_gpu_fcos_step.py tests/test_gpu_model.py tests/test_gpu_configs0.py tests/test_gpu_dp.py tests/test_gpu_nnops.py > gpurun_out/s2_pytest.log 2>&1 || { tail -40 gpurun_out/s2_pytest.log; exit 1; }
+tail -1 gpurun_out/s2_pytest.log
+grep -h "dgrad_bnsum_res" gpurun_out/launch_parity_fcos_512_bs16.txt | grep " s2\|/2" | head -6
+head -1 gpurun_out/launch_parity_fcos_512_bs16.txt
+bash tools/bench_ab.sh "" "CVL_DISPATCH=no_bnsum_res_s2"
