@@ -146,25 +146,34 @@ __device__ unsigned long long g_h_stamps[kHStampWgs * 8];
 // issued, so that tile's halo and weights land while the current tile's epilogue runs (the
 // epilogue stages its C image in the stage buffer just consumed), and the per-tile set-up is a
 // few adds (halo_pieces is per segment).  One workgroup per CU (148 KiB of LDS).
-template <bool DGRAD, bool BSUM, bool WRES = false, bool ST = false, bool SW = false, int BNT = 64>
+template <bool DGRAD, bool BSUM, bool WRES = false, bool ST = false, bool SW = false, int BNT = 64, int NSTG = 2>
 __global__ void __launch_bounds__(NT) conv_igemm_h_kernel(ConvArgs a) {
   // BNT: the N tile, 64 (the backbone / FPN launches) or 32 (round 6: the FCOS heads' forward, 3x3
   // 256 -> 20 / 5 over the five levels; Npad 32); the constants below shadow the 64-wide ones
   constexpr int BN = BNT, TN = BN / 32, WN = BN / 2;
+  // NSTG 3 (the 32-wide tiles): halos of at most 512 pixels, so THREE stages fit the LDS and the DMA
+  // of block cb + 2 is issued during block cb (two blocks of latency cover instead of one)
+  static_assert(NSTG == 2 || (NSTG == 3 && BNT == 32 && !WRES), "three stages: 32-wide tiles only");
+  constexpr int HPXk = NSTG == 3 ? 512 : HPX;
+  constexpr int HPWk = HPXk / 16 / 8;                   // halo pieces per wave: 5 (640 px) or 4 (512)
+  constexpr int HALO_ELk = HPXk * BK;
   constexpr int WPC = 9 * BN * BK * 2 / 1024;          // weight DMA pieces per stage: 36 / 18
   constexpr int WJ = WPC / 8, WR = WPC % 8;             // full rounds of 8 waves + the remainder
   constexpr int PPT = BN / 16;                          // pieces per tap (16 rows x 64 B each)
   constexpr int WT_EL = 9 * BN * BK;
-  constexpr int STAGE_EL = HALO_EL + WT_EL;
+  constexpr int STAGE_EL = HALO_ELk + WT_EL;
   constexpr int LDS_C = BM * (BN + 8) + WGM * BN * 2 * 2;
-  constexpr int LDS_EL = 2 * STAGE_EL > LDS_C ? 2 * STAGE_EL : LDS_C;
+  constexpr int LDS_EL = NSTG * STAGE_EL > LDS_C ? NSTG * STAGE_EL : LDS_C;
   constexpr int LDS_WRES_EL = 2 * HALO_EL + WRES_CB * WT_EL;
-  static_assert(HALO_EL >= LDS_C && HPW + WJ <= 9 && BN % 32 == 0, "H64 stage layout");
+  static_assert(HALO_ELk >= LDS_C && HPWk + WJ <= 9 && BN % 32 == 0, "H64 stage layout");
   constexpr int MAIN_EL = WRES ? LDS_WRES_EL : LDS_EL;
   // SW: + the [WGM][BN][2] fp32 combine buffer of the statistics flush
   __shared__ __attribute__((aligned(16))) cvl_bf16 lds[MAIN_EL + (SW ? WGM * BN * 2 * 2 : 0)];
   float* const red = reinterpret_cast<float*>(lds + MAIN_EL);
   constexpr int SST = WRES ? HALO_EL : STAGE_EL;        // elements per stage buffer
+  // DMA pieces a wave issues per channel block (NSTG 3: every issue slot is used, out-of-range when
+  // the stream has ended, so the counted waits are exact)
+  const int pw_blk = HPWk + WJ + ((WR && (int)(threadIdx.x >> 6) < WR) ? 1 : 0);
   cvl_bf16* const wres = lds + 2 * HALO_EL;             // WRES: the weights of channel block cb at cb * WT_EL
   const int tid = threadIdx.x;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
@@ -340,24 +349,40 @@ __global__ void __launch_bounds__(NT) conv_igemm_h_kernel(ConvArgs a) {
     }
   };
 
-  // prologue: the first channel block's stage complete everywhere
+  // prologue: the first channel block's stage complete everywhere (NSTG 3: the second one issued too)
   {
     cvl_bf16* st = lds;
     const unsigned cbo = (unsigned)(i_cb * BK * 2);
 #pragma unroll
-    for (int j = 0; j < HPW; ++j) dma16(rsA, st + (wave + 8 * j) * 16 * BK, hoff[j] + cbo);
+    for (int j = 0; j < HPWk; ++j) dma16(rsA, st + (wave + 8 * j) * 16 * BK, hoff[j] + cbo);
     if (WRES) {                                     // the first channel block's weights (the rest below)
 #pragma unroll
       for (int j = 0; j < WJ; ++j) dma16(rsB, wres + (wave + 8 * j) * 16 * BK, woff[j]);
       if (WR && wave < WR) dma16(rsB, wres + (wave + 8 * WJ) * 16 * BK, woff[WJ]);
     } else {
 #pragma unroll
-      for (int j = 0; j < WJ; ++j) dma16(rsB, st + HALO_EL + (wave + 8 * j) * 16 * BK, woff[j] + cbo);
-      if (WR && wave < WR) dma16(rsB, st + HALO_EL + (wave + 8 * WJ) * 16 * BK, woff[WJ] + cbo);
+      for (int j = 0; j < WJ; ++j) dma16(rsB, st + HALO_ELk + (wave + 8 * j) * 16 * BK, woff[j] + cbo);
+      if (WR && wave < WR) dma16(rsB, st + HALO_ELk + (wave + 8 * WJ) * 16 * BK, woff[WJ] + cbo);
     }
     advance();
+    if constexpr (NSTG == 3) {                      // block 1 into stage buffer 1 (out of range past the end)
+      const bool m1 = i_L < t_hi;
+      cvl_bf16* s1 = lds + SST;
+      const unsigned cb1o = (unsigned)(i_cb * BK * 2);
+#pragma unroll
+      for (int j = 0; j < HPWk; ++j) dma16(rsA, s1 + (wave + 8 * j) * 16 * BK, m1 ? hoff[j] + cb1o : kOOB);
+#pragma unroll
+      for (int j = 0; j < WJ; ++j) dma16(rsB, s1 + HALO_ELk + (wave + 8 * j) * 16 * BK, m1 ? woff[j] + cb1o : kOOB);
+      if (WR && wave < WR) dma16(rsB, s1 + HALO_ELk + (wave + 8 * WJ) * 16 * BK, m1 ? woff[WJ] + cb1o : kOOB);
+      if (m1) advance();
+    }
   }
-  wait_vm<0>();
+  if constexpr (NSTG == 3) {                        // block 0 landed (block 1's pieces may be in flight)
+    if (pw_blk == HPWk + WJ + 1) wait_vm<HPWk + WJ + 1>();
+    else wait_vm<HPWk + WJ>();
+  } else {
+    wait_vm<0>();
+  }
   __builtin_amdgcn_s_barrier();
   asm volatile("" ::: "memory");
   if (ST && stamp) w1 = wall_clock64();
@@ -466,7 +491,7 @@ __global__ void __launch_bounds__(NT) conv_igemm_h_kernel(ConvArgs a) {
       const int d = DGRAD ? 2 - sx : sx;
       const char* Hr = Hc + (DGRAD ? 1 - r : r - 1) * prow;
       const char* Wt = WRES ? reinterpret_cast<const char*>(wres + c_cb * WT_EL) + t * BN * BK * 2
-                            : Hc + HALO_EL * 2 + t * BN * BK * 2;
+                            : Hc + HALO_ELk * 2 + t * BN * BK * 2;
 #pragma unroll
       for (int i = 0; i < TM; ++i) fa[buf][i] = *reinterpret_cast<const s16x8*>(Hr + afr[i][d]);
 #pragma unroll
@@ -483,18 +508,20 @@ __global__ void __launch_bounds__(NT) conv_igemm_h_kernel(ConvArgs a) {
                                                                     __builtin_bit_cast(bf16x8, fb[buf][j]), acc[i][j], 0, 0, 0);
     };
     for (int cb = cb0; cb < cb1; ++cb) {
-      const char* Hc = reinterpret_cast<const char*>(lds + (gb & 1) * SST);
+      const char* Hc = reinterpret_cast<const char*>(lds + (gb % NSTG) * SST);
       c_cb = cb;
       const bool more = i_L < t_hi;
-      cvl_bf16* nh = lds + ((gb + 1) & 1) * SST;
+      cvl_bf16* nh = lds + ((gb + NSTG - 1) % NSTG) * SST;   // the block issued now: gb + NSTG - 1
       const unsigned cbo = (unsigned)(i_cb * BK * 2);
       if (ST && stamp) c0 = __builtin_amdgcn_s_memtime();
       read_tap(0, Hc, 0);
 #pragma unroll
       for (int t = 0; t < 9; ++t) {
-        if (more && t < HPW) dma16(rsA, nh + (wave + 8 * t) * 16 * BK, hoff[t] + cbo);
-        if (!WRES && more && t >= HPW && t < HPW + WJ) dma16(rsB, nh + HALO_EL + (wave + 8 * (t - HPW)) * 16 * BK, woff[t - HPW] + cbo);
-        if (!WRES && WR && t == 8 && more && wave < WR) dma16(rsB, nh + HALO_EL + (wave + 8 * WJ) * 16 * BK, woff[WJ] + cbo);
+        const bool iss = NSTG == 3 || more;         // NSTG 3: every slot issued (out of range past the end)
+        if (iss && t < HPWk) dma16(rsA, nh + (wave + 8 * t) * 16 * BK, more ? hoff[t] + cbo : kOOB);
+        if (!WRES && iss && t >= HPWk && t < HPWk + WJ)
+          dma16(rsB, nh + HALO_ELk + (wave + 8 * (t - HPWk)) * 16 * BK, more ? woff[t - HPWk] + cbo : kOOB);
+        if (!WRES && WR && t == 8 && iss && wave < WR) dma16(rsB, nh + HALO_ELk + (wave + 8 * WJ) * 16 * BK, more ? woff[WJ] + cbo : kOOB);
         if (t < 8) read_tap((t + 1) & 1, Hc, t + 1);
         mma_tap(t & 1);
       }
@@ -504,7 +531,12 @@ __global__ void __launch_bounds__(NT) conv_igemm_h_kernel(ConvArgs a) {
         c1 = __builtin_amdgcn_s_memtime();
         t_tap += c1 - c0;
       }
-      wait_vm<0>();                                 // this wave's pieces of the next block landed
+      if constexpr (NSTG == 3) {                    // block cb + 1 landed (cb + 2's pieces may be in flight)
+        if (pw_blk == HPWk + WJ + 1) wait_vm<HPWk + WJ + 1>();
+        else wait_vm<HPWk + WJ>();
+      } else {
+        wait_vm<0>();                               // this wave's pieces of the next block landed
+      }
       __builtin_amdgcn_s_barrier();                 // ... and everyone's; this block fully read
       asm volatile("" ::: "memory");
       if (ST && stamp) t_wait += __builtin_amdgcn_s_memtime() - c1;
@@ -602,7 +634,7 @@ __global__ void __launch_bounds__(NT) conv_igemm_h_kernel(ConvArgs a) {
     if (ST && stamp) {
       c0 = __builtin_amdgcn_s_memtime();
     }
-    conv_l_epilogue<BN, WGM, TM, TN, NT, BSUM>(a, S, acc, lds + ((gb - 1) & 1) * SST, tid, wm, wn, n0, mloc0,
+    conv_l_epilogue<BN, WGM, TM, TN, NT, BSUM>(a, S, acc, lds + ((gb + NSTG - 1) % NSTG) * SST, tid, wm, wn, n0, mloc0,
                                                 HWr, zpre, bpar, bcol, (ST && stamp) ? te : nullptr);
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
@@ -674,14 +706,21 @@ int cvl_conv_igemm_h(const cvl_conv_desc* d, const ConvArgs& a0, hipStream_t s, 
   if (cvl_dispatch_flag("no_h") || !cvl_conv_h_fits(d, a0)) return -1;
   ConvArgs a = a0;
   const bool dg = d->mode == CVL_CONV_DGRAD;
+  // three stages for the 32-wide tiles when every segment's halo fits 512 pixels (CVL_DISPATCH=h_no_3stage: two)
+  bool stg3 = !cvl_dispatch_flag("h_no_3stage");
+  for (int i = 0; stg3 && i < a.nseg; ++i) {
+    const HGeo g = h_geo(a.seg[i].Hr, a.seg[i].Wr);
+    if (g.rows * g.pitch > 512) stg3 = false;
+  }
   if (a.Npad == 32) {          // 256 x 32 tiles (the FCOS heads' forward): persistent, no split, fp32 epilogue
     if (a.stats || a.bsum) return -1;
     static const int ncu32 = cvl_device_cus();
     const int t32 = a.m_tiles;
     a.splits = 1;
     g_cvl_conv_last_kernel = CVL_CK_H64;
-    hipLaunchKernelGGL((conv_igemm_h_kernel<false, false, false, false, false, 32>), dim3(t32 < ncu32 ? t32 : ncu32),
-                       dim3(NT), 0, s, a);
+    const dim3 gh(t32 < ncu32 ? t32 : ncu32);
+    if (stg3) hipLaunchKernelGGL((conv_igemm_h_kernel<false, false, false, false, false, 32, 3>), gh, dim3(NT), 0, s, a);
+    else hipLaunchKernelGGL((conv_igemm_h_kernel<false, false, false, false, false, 32>), gh, dim3(NT), 0, s, a);
     return cvl_launch_status();
   }
   // 32-wide tiles (round 6) for the SW-epilogue launches whose 64-wide grid fills at most half of the
@@ -701,7 +740,13 @@ int cvl_conv_igemm_h(const cvl_conv_desc* d, const ConvArgs& a0, hipStream_t s, 
       a.splits = 1;
       g_cvl_conv_last_kernel = CVL_CK_H64;
       const dim3 g32(2 * t64);
-      if (d->mode == CVL_CONV_DGRAD && a.bsum)
+      if (stg3 && d->mode == CVL_CONV_DGRAD && a.bsum)
+        hipLaunchKernelGGL((conv_igemm_h_kernel<true, true, false, false, true, 32, 3>), g32, dim3(NT), 0, s, a);
+      else if (stg3 && d->mode == CVL_CONV_DGRAD)
+        hipLaunchKernelGGL((conv_igemm_h_kernel<true, false, false, false, true, 32, 3>), g32, dim3(NT), 0, s, a);
+      else if (stg3)
+        hipLaunchKernelGGL((conv_igemm_h_kernel<false, false, false, false, true, 32, 3>), g32, dim3(NT), 0, s, a);
+      else if (d->mode == CVL_CONV_DGRAD && a.bsum)
         hipLaunchKernelGGL((conv_igemm_h_kernel<true, true, false, false, true, 32>), g32, dim3(NT), 0, s, a);
       else if (d->mode == CVL_CONV_DGRAD)
         hipLaunchKernelGGL((conv_igemm_h_kernel<true, false, false, false, true, 32>), g32, dim3(NT), 0, s, a);
