@@ -1756,6 +1756,46 @@ extern "C" int cvl_bn_backward_res_sums_sc(const void* dy, const void* y, const 
   return cvl_launch_status();
 }
 
+// The same for a residual unit whose first pass is NOT fused upstream (the small-map projection
+// blocks): cvl_bn_backward's two passes (mask y > 0, g_out), the second one also forming the shortcut
+// BN's first pass into sc_sums.  Workspace: cvl_bn_backward's, then the shortcut partials.
+extern "C" size_t cvl_bn_backward_sc_workspace_size(int B, int HW, int C) {
+  if (B <= 0 || HW <= 0 || C <= 0) return 0;
+  return cvl_bn_backward_workspace_size(B, HW, C) + cvl_bn_backward_res_sums_sc_workspace_size(B, HW, C);
+}
+
+extern "C" int cvl_bn_backward_sc(const void* dy, const void* y, const void* z, const float* mean_rstd,
+                                  const float* gamma, void* workspace, size_t workspace_bytes, void* dz, void* g_out,
+                                  float* dgamma, float* dbeta, float beta_acc, float* conv_dbias, const void* z_sc,
+                                  const float* mean_rstd_sc, uint64_t* sc_sums, int B, int HW, int C,
+                                  cvl_stream_t stream) {
+  CVL_CHECK_ARG(dy && y && z && mean_rstd && gamma && workspace && dz && g_out && dgamma && dbeta && C % 8 == 0);
+  CVL_CHECK_ARG(z_sc && mean_rstd_sc && sc_sums && B > 0 && HW > 0);
+  CVL_CHECK_ARG(workspace_bytes >= cvl_bn_backward_sc_workspace_size(B, HW, C));
+  const int rpb = bn_bwd_rows_per_blk(B, HW, C);
+  const int nchunk = (HW + rpb - 1) / rpb;
+  acc_u64* sums = reinterpret_cast<acc_u64*>(workspace);
+  double* dbsum = reinterpret_cast<double*>(sums + 2 * (size_t)B * C);
+  float* part0 = reinterpret_cast<float*>(dbsum + 2 * (size_t)C);
+  float* part_sc = reinterpret_cast<float*>(reinterpret_cast<char*>(workspace) + cvl_bn_backward_workspace_size(B, HW, C));
+  hipLaunchKernelGGL((bn_bwd_kernel<0, 1>), dim3(nchunk, B), dim3(NT), 0, S_, (const cvl_bf16*)dy, (const cvl_bf16*)y,
+                     (const cvl_bf16*)z, mean_rstd, gamma, (const acc_u64*)nullptr, (cvl_bf16*)nullptr,
+                     (cvl_bf16*)nullptr, part0, C, HW, rpb, 1, 0.f, BnPG{}, (const float*)nullptr, INFINITY);
+  hipLaunchKernelGGL(bn_colsum_kernel, dim3((C + 31) / 32, B), dim3(NT), 0, S_, (const float*)part0, nchunk, C,
+                     sums, 1);
+  const int rpb1 = bn_rows_per_blk(B, HW, C);
+  const int nchunk1 = (HW + rpb1 - 1) / rpb1;
+  BnPG pg{dgamma, dbeta, conv_dbias, beta_acc, nullptr, 1};
+  pg.sc_z = (const cvl_bf16*)z_sc;
+  pg.sc_mr = mean_rstd_sc;
+  hipLaunchKernelGGL((bn_bwd_kernel<1, 1, true>), dim3(nchunk1, B + 1), dim3(NT), 0, S_, (const cvl_bf16*)dy,
+                     (const cvl_bf16*)y, (const cvl_bf16*)z, mean_rstd, gamma, (const acc_u64*)sums, (cvl_bf16*)dz,
+                     (cvl_bf16*)g_out, part_sc, C, HW, rpb1, 1, 0.f, pg, (const float*)nullptr, INFINITY);
+  hipLaunchKernelGGL(bn_colsum_kernel, dim3((C + 31) / 32, B), dim3(NT), 0, S_, (const float*)part_sc, nchunk1, C,
+                     (acc_u64*)sc_sums, 1);
+  return cvl_launch_status();
+}
+
 // Second pass only of a BN WITHOUT ReLU (the projection shortcut's BN) from first-pass sums [B][C][2]
 // in slot mode 1 (cvl_bn_backward_res_sums_sc): dz, dgamma, dbeta (+ conv_dbias = 0).
 extern "C" int cvl_bn_backward_sums(const void* dy, const void* z, const float* mean_rstd, const float* gamma,

@@ -56,6 +56,8 @@ SIGNATURES = {
     "cvl_bn_backward_res_sums_sc": (c_int, [P, P, P, P, P, P, P, P, P, P, c_float, P, P, P, P, c_size_t, P, c_int,
                                             c_int, c_int, P]),
     "cvl_bn_backward_sums": (c_int, [P, P, P, P, P, P, P, P, c_float, P, c_int, c_int, c_int, P]),
+    "cvl_bn_backward_sc_workspace_size": (c_size_t, [c_int, c_int, c_int]),
+    "cvl_bn_backward_sc": (c_int, [P, P, P, P, P, P, c_size_t, P, P, P, P, c_float, P, P, P, P, c_int, c_int, c_int, P]),
     "cvl_probe_arm": (c_int, [P]),
     "cvl_probe_clock_hz": (ctypes.c_double, []),
     "cvl_conv_wgrad_workspace_size": (c_size_t, [P]),

@@ -452,6 +452,11 @@ class ConvBN(object):
         elif relu and not has_res and g_out is None:    # ReLU mask rebuilt from z: y is not read
             nn.bn_backward_relu(dy, z, mr, self.bn.gamma, self.bn.beta, dz, st.g(self.bn.gname),
                                 st.g(self.bn.bname), B, Ho * Wo, c, conv_dbias=self.conv.db)
+        elif sc_fuse is not None and relu and has_res and g_out is not None and y is not None:
+            # both passes here, the second one also forming the projection shortcut BN's first pass
+            nn.bn_backward_sc(dy, y, z, mr, self.bn.gamma, dz, g_out, st.g(self.bn.gname), st.g(self.bn.bname),
+                              sc_fuse[0], sc_fuse[1], sc_fuse[2], B, Ho * Wo, c, conv_dbias=self.conv.db)
+            self.sc_fused = True
         else:
             # the mask comes from y: a deferred unit (saved y None) has no ReLU (ConvBN.forward)
             assert y is not None or not relu, "ReLU unit without its saved output"

@@ -468,6 +468,17 @@ def bn_backward_res_sums_sc(dy, y, z, mean_rstd, gamma, sums, dz, g_out, dgamma,
               ptr(mean_rstd_sc), ptr(ws), n, ptr(sc_sums), B, HW, C, stream())
 
 
+def bn_backward_sc(dy, y, z, mean_rstd, gamma, dz, g_out, dgamma, dbeta, z_sc, mean_rstd_sc, sc_sums, B, HW, C,
+                   beta_acc=0.0, conv_dbias=None):
+    """bn_backward (mask y > 0, g_out) whose second pass also forms the projection shortcut BN's first
+    pass into sc_sums [B][C][2] (float64 values)."""
+    n = int(_lib.load().cvl_bn_backward_sc_workspace_size(B, HW, C))
+    ws = torch.empty(n, dtype=torch.uint8, device=dy.device)
+    _lib.call("cvl_bn_backward_sc", ptr(dy), ptr(y), ptr(z), ptr(mean_rstd), ptr(gamma), ptr(ws), n, ptr(dz),
+              ptr(g_out), ptr(dgamma), ptr(dbeta), float(beta_acc), ptr(conv_dbias), ptr(z_sc), ptr(mean_rstd_sc),
+              ptr(sc_sums), B, HW, C, stream())
+
+
 def bn_backward_sums(dy, z, mean_rstd, gamma, sums, dz, dgamma, dbeta, B, HW, C, beta_acc=0.0, conv_dbias=None):
     """Second pass of a BN without ReLU from first-pass sums [B][C][2] (float64 values)."""
     _lib.call("cvl_bn_backward_sums", ptr(dy), ptr(z), ptr(mean_rstd), ptr(gamma), ptr(sums), ptr(dz), ptr(dgamma),

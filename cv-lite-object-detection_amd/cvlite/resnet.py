@@ -167,7 +167,7 @@ class Bottleneck(object):
         s2 = s1 = None
         # projection blocks: the shortcut BN's first pass rides on conv3's fused second pass
         sc_fuse = None
-        if self.sc is not None and sums3 is not None and FUSE_SC_BNSUM and dy.dtype == torch.bfloat16:
+        if self.sc is not None and FUSE_SC_BNSUM and dy.dtype == torch.bfloat16:
             zs, mrs = sv_s[1], sv_s[3]
             sc_fuse = (zs, mrs, torch.empty((zs.shape[0], self.sc.bn.c, 2), dtype=torch.float64, device=zs.device))
         if ctx2 is not None:

@@ -373,6 +373,13 @@ int cvl_bn_backward_res_sums_sc(const void* dy, const void* y, const void* z, co
                                 float* dbeta, float beta_acc, float* conv_dbias, const void* z_sc,
                                 const float* mean_rstd_sc, void* workspace, size_t workspace_bytes,
                                 uint64_t* sc_sums, int B, int HW, int C, cvl_stream_t stream);
+/* The same when the residual unit's first pass is not fused upstream: cvl_bn_backward (mask y > 0,
+ * g_out) whose second pass also forms the shortcut BN's first pass into sc_sums. */
+size_t cvl_bn_backward_sc_workspace_size(int B, int HW, int C);
+int cvl_bn_backward_sc(const void* dy, const void* y, const void* z, const float* mean_rstd, const float* gamma,
+                       void* workspace, size_t workspace_bytes, void* dz, void* g_out, float* dgamma, float* dbeta,
+                       float beta_acc, float* conv_dbias, const void* z_sc, const float* mean_rstd_sc,
+                       uint64_t* sc_sums, int B, int HW, int C, cvl_stream_t stream);
 /* Second pass only of a BN without ReLU from first-pass sums [B][C][2] (slot mode 1). */
 int cvl_bn_backward_sums(const void* dy, const void* z, const float* mean_rstd, const float* gamma,
                          const uint64_t* sums, void* dz, float* dgamma, float* dbeta, float beta_acc,

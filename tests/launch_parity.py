@@ -835,6 +835,26 @@ def check_bn_backward_res_sums_sc(lp, name, launch, dy, y, z, mean_rstd, gamma, 
     lp.add(name, d, "sc_sums", red_err(sc_sums.view(B, C, 2).double(), ref, rabs), 1e-6)
 
 
+def check_bn_backward_sc(lp, name, launch, dy, y, z, mean_rstd, gamma, dz, g_out, dgamma, dbeta, z_sc, mean_rstd_sc,
+                         sc_sums, B, HW, C, beta_acc=0.0, conv_dbias=None):
+    """check_bn_backward (mask y > 0, g_out), plus the projection shortcut BN's first-pass sums."""
+    dg0, db0 = _clone(dgamma, dbeta)
+    dyr, zr = _keep_inputs(dz, dy, z)
+    (yr,) = _keep_inputs(dz, y)
+    launch(dy, y, z, mean_rstd, gamma, dz, g_out, dgamma, dbeta, z_sc, mean_rstd_sc, sc_sums, B, HW, C,
+           beta_acc=beta_acc, conv_dbias=conv_dbias)
+    mask = yr.reshape(B, HW, C).float() > 0
+    d = "C%d HW%d B%d relu(y) +sc" % (C, HW, B)
+    _check_bn_bwd(lp, name, d, dyr, zr, mean_rstd, gamma, dz, None, 0.0, g_out, dgamma, dbeta, dg0, db0, beta_acc,
+                  conv_dbias, B, HW, C, mask)
+    g = g_out.reshape(B, HW, C).double()
+    ms, rss = mean_rstd_sc.view(B, C, 2)[..., 0], mean_rstd_sc.view(B, C, 2)[..., 1]
+    xh = ((z_sc.reshape(B, HW, C).float() - ms[:, None].float()) * rss[:, None].float()).double()
+    ref = torch.stack([g.sum(1), (g * xh).sum(1)], -1)
+    rabs = torch.stack([g.abs().sum(1), (g * xh).abs().sum(1)], -1)
+    lp.add(name, d, "sc_sums", red_err(sc_sums.view(B, C, 2).double(), ref, rabs), 1e-6)
+
+
 def check_bn_backward_sums(lp, name, launch, dy, z, mean_rstd, gamma, sums, dz, dgamma, dbeta, B, HW, C, beta_acc=0.0,
                            conv_dbias=None):
     dg0, db0 = _clone(dgamma, dbeta)
@@ -1257,6 +1277,7 @@ CHECKS = {
     "bn_backward_res_sums": check_bn_backward_res_sums,
     "bn_backward_res_sums_sc": check_bn_backward_res_sums_sc,
     "bn_backward_sums": check_bn_backward_sums,
+    "bn_backward_sc": check_bn_backward_sc,
     "bn_relu_maxpool3x3s2": check_bn_relu_maxpool,
     "maxpool3x3s2": check_maxpool3x3s2,
     "maxpool3x3s2_backward": check_maxpool3x3s2_backward,

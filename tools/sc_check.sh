@@ -6,3 +6,4 @@ tail -1 gpurun_out/sc_pytest.log
 grep -h "res_sums_sc\|bn_backward_sums " gpurun_out/launch_parity_fcos_512_bs16.txt | head -8
 head -1 gpurun_out/launch_parity_fcos_512_bs16.txt
 bash tools/bench_ab.sh "" "CVL_DISPATCH=no_sc_bnsum"
+grep -c "bn_backward_sc " gpurun_out/launch_parity_fcos_512_bs16.txt
