@@ -422,6 +422,20 @@ inline int bn_rows_per_blk(int B, int HW, int C) {
   return (rpb + rpp - 1) / rpp * rpp;
 }
 
+// the BN backward sums pass's chunking: its own workgroup target, fewer and longer blocks than the
+// apply (each block also reduces its partials once; round-6 sweep, FCOS step, same box: 256 / 384 /
+// 512 / 640 / 768 / 1024 / 1536 blocks -> 1388.0 / 1383.2 / 1397.9 / 1382.7 / 1389.3 / 1390.8 /
+// 1379.0 img/s)
+inline int bn1_rows_per_blk(int B, int HW, int C) {
+  const int C8 = C / 8, tpr = C8 < NT ? C8 : NT, rpp = NT / tpr;
+  static const int target = cvl_tune_int("CVL_BNB1_BLOCKS", 512);     // workgroups per launch
+  const int chunks = (target + B - 1) / B;
+  int rpb = (HW + chunks - 1) / chunks;
+  const int lo = rpp * 4;
+  rpb = rpb < lo ? lo : rpb;
+  return (rpb + rpp - 1) / rpp * rpp;
+}
+
 // BN backward over one (image, row-chunk) block; threads own 8 channels (tpr threads per row,
 // rpp rows per pass), rows taken UNR at a time with all loads issued before any use (the loop is
 // latency-bound otherwise).  No atomics: each block writes its per-channel partial sums to
@@ -1649,7 +1663,7 @@ static int bn_backward_impl(const void* dy, const void* y_relu, const float* bn_
   hipLaunchKernelGGL(bn_colsum_kernel, dim3((C + 31) / 32, B), dim3(NT), 0, S_, (const float*)part0, nchunk, C,
                      sums, 1);
   // pass 1 is elementwise (no partials): the apply kernels' finer chunking (~2048 workgroups)
-  const int rpb1 = bn_rows_per_blk(B, HW, C);
+  const int rpb1 = bn1_rows_per_blk(B, HW, C);
   hipLaunchKernelGGL(k1, dim3((HW + rpb1 - 1) / rpb1, B + 1), dim3(NT), 0, S_, (const cvl_bf16*)dy, (const cvl_bf16*)y_relu,
                      (const cvl_bf16*)z, mean_rstd, gamma, (const acc_u64*)sums, (cvl_bf16*)dz, (cvl_bf16*)g_out,
                      (float*)nullptr, C, HW, rpb1, 1, 0.f, BnPG{dgamma, dbeta, conv_dbias, beta_acc, nullptr, 1}, bn_beta,
@@ -1694,7 +1708,7 @@ extern "C" int cvl_bn_backward_relu_sums(const void* dy, const void* z, const fl
   CVL_CHECK_ARG(B > 0 && HW > 0);
   const int dst = acc_decode_launch((acc_u64*)sums, 2L * B * C, S_);
   if (dst) return dst;
-  const int rpb = bn_rows_per_blk(B, HW, C);
+  const int rpb = bn1_rows_per_blk(B, HW, C);
   const int nchunk = (HW + rpb - 1) / rpb;
   hipLaunchKernelGGL((bn_bwd_kernel<1, 2>), dim3(nchunk, B + 1), dim3(NT), 0, S_, (const cvl_bf16*)dy, (const cvl_bf16*)nullptr,
                      (const cvl_bf16*)z, mean_rstd, gamma, (const acc_u64*)sums, (cvl_bf16*)dz, (cvl_bf16*)nullptr, (float*)nullptr,
@@ -1712,7 +1726,7 @@ extern "C" int cvl_bn_backward_res_sums(const void* dy, const void* y, const voi
   CVL_CHECK_ARG(B > 0 && HW > 0);
   const int dst = acc_decode_launch((acc_u64*)sums, 2L * B * C, S_);
   if (dst) return dst;
-  const int rpb = bn_rows_per_blk(B, HW, C);
+  const int rpb = bn1_rows_per_blk(B, HW, C);
   const int nchunk = (HW + rpb - 1) / rpb;
   hipLaunchKernelGGL((bn_bwd_kernel<1, 1>), dim3(nchunk, B + 1), dim3(NT), 0, S_, (const cvl_bf16*)dy, (const cvl_bf16*)y,
                      (const cvl_bf16*)z, mean_rstd, gamma, (const acc_u64*)sums, (cvl_bf16*)dz, (cvl_bf16*)g_out, (float*)nullptr,
@@ -1727,7 +1741,7 @@ extern "C" int cvl_bn_backward_res_sums(const void* dy, const void* y, const voi
 // cvl_bn_backward_sums.  The shortcut's own first pass -- a re-read of g_out and z_sc -- is gone.
 extern "C" size_t cvl_bn_backward_res_sums_sc_workspace_size(int B, int HW, int C) {
   if (B <= 0 || HW <= 0 || C <= 0) return 0;
-  const int rpb = bn_rows_per_blk(B, HW, C);
+  const int rpb = bn1_rows_per_blk(B, HW, C);
   return sizeof(float) * 2 * (size_t)B * ((HW + rpb - 1) / rpb) * C;
 }
 
@@ -1742,7 +1756,7 @@ extern "C" int cvl_bn_backward_res_sums_sc(const void* dy, const void* y, const 
   CVL_CHECK_ARG(workspace_bytes >= cvl_bn_backward_res_sums_sc_workspace_size(B, HW, C));
   const int dst = acc_decode_launch((acc_u64*)sums, 2L * B * C, S_);
   if (dst) return dst;
-  const int rpb = bn_rows_per_blk(B, HW, C);
+  const int rpb = bn1_rows_per_blk(B, HW, C);
   const int nchunk = (HW + rpb - 1) / rpb;
   float* part = reinterpret_cast<float*>(workspace);
   BnPG pg{dgamma, dbeta, conv_dbias, beta_acc, nullptr, g_acc_slots};
@@ -1783,7 +1797,7 @@ extern "C" int cvl_bn_backward_sc(const void* dy, const void* y, const void* z, 
                      (cvl_bf16*)nullptr, part0, C, HW, rpb, 1, 0.f, BnPG{}, (const float*)nullptr, INFINITY);
   hipLaunchKernelGGL(bn_colsum_kernel, dim3((C + 31) / 32, B), dim3(NT), 0, S_, (const float*)part0, nchunk, C,
                      sums, 1);
-  const int rpb1 = bn_rows_per_blk(B, HW, C);
+  const int rpb1 = bn1_rows_per_blk(B, HW, C);
   const int nchunk1 = (HW + rpb1 - 1) / rpb1;
   BnPG pg{dgamma, dbeta, conv_dbias, beta_acc, nullptr, 1};
   pg.sc_z = (const cvl_bf16*)z_sc;
@@ -1802,7 +1816,7 @@ extern "C" int cvl_bn_backward_sums(const void* dy, const void* z, const float* 
                                     const uint64_t* sums, void* dz, float* dgamma, float* dbeta, float beta_acc,
                                     float* conv_dbias, int B, int HW, int C, cvl_stream_t stream) {
   CVL_CHECK_ARG(dy && z && mean_rstd && gamma && sums && dz && dgamma && dbeta && C % 8 == 0 && B > 0 && HW > 0);
-  const int rpb = bn_rows_per_blk(B, HW, C);
+  const int rpb = bn1_rows_per_blk(B, HW, C);
   const int nchunk = (HW + rpb - 1) / rpb;
   hipLaunchKernelGGL((bn_bwd_kernel<1, 3>), dim3(nchunk, B + 1), dim3(NT), 0, S_, (const cvl_bf16*)dy,
                      (const cvl_bf16*)nullptr, (const cvl_bf16*)z, mean_rstd, gamma, (const acc_u64*)sums, (cvl_bf16*)dz,
@@ -1884,7 +1898,7 @@ extern "C" int cvl_maxpool3x3s2_backward_bn_relu(const void* dp, const uint8_t* 
                      PoolBn{(const cvl_bf16*)z, mean_rstd, gamma, beta, part, INFINITY});
   hipLaunchKernelGGL(bn_colsum_kernel, dim3((C + 31) / 32, B), dim3(NT), 0, S_, (const float*)part, tiles, C, sums, 1);
   const int HW = H * W;
-  const int rpb1 = bn_rows_per_blk(B, HW, C);
+  const int rpb1 = bn1_rows_per_blk(B, HW, C);
   hipLaunchKernelGGL((bn_bwd_kernel<1, 2>), dim3((HW + rpb1 - 1) / rpb1, B + 1), dim3(NT), 0, S_, (const cvl_bf16*)dy,
                      (const cvl_bf16*)nullptr, (const cvl_bf16*)z, mean_rstd, gamma, (const acc_u64*)sums, (cvl_bf16*)dz,
                      (cvl_bf16*)nullptr, (float*)nullptr, C, HW, rpb1, 1, 0.f,
