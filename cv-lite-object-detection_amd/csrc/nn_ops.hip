@@ -422,8 +422,9 @@ inline int bn_rows_per_blk(int B, int HW, int C) {
   return (rpb + rpp - 1) / rpp * rpp;
 }
 
-// the BN backward sums pass's chunking: its own workgroup target, fewer and longer blocks than the
-// apply (each block also reduces its partials once; round-6 sweep, FCOS step, same box: 256 / 384 /
+// the BN backward second (elementwise dz) pass's chunking: its own workgroup target, fewer and longer
+// blocks than the apply (each block first re-forms its image's per-channel coefficients from the
+// sums and the BN parameters; round-6 sweep, FCOS step, same box: 256 / 384 /
 // 512 / 640 / 768 / 1024 / 1536 blocks -> 1388.0 / 1383.2 / 1397.9 / 1382.7 / 1389.3 / 1390.8 /
 // 1379.0 img/s)
 inline int bn1_rows_per_blk(int B, int HW, int C) {
@@ -1662,7 +1663,7 @@ static int bn_backward_impl(const void* dy, const void* y_relu, const float* bn_
                      (cvl_bf16*)nullptr, part0, C, HW, rpb, 1, 0.f, BnPG{}, bn_beta, act_hi);
   hipLaunchKernelGGL(bn_colsum_kernel, dim3((C + 31) / 32, B), dim3(NT), 0, S_, (const float*)part0, nchunk, C,
                      sums, 1);
-  // pass 1 is elementwise (no partials): the apply kernels' finer chunking (~2048 workgroups)
+  // pass 1 is elementwise (no partials): its own chunking (~512 workgroups, bn1_rows_per_blk)
   const int rpb1 = bn1_rows_per_blk(B, HW, C);
   hipLaunchKernelGGL(k1, dim3((HW + rpb1 - 1) / rpb1, B + 1), dim3(NT), 0, S_, (const cvl_bf16*)dy, (const cvl_bf16*)y_relu,
                      (const cvl_bf16*)z, mean_rstd, gamma, (const acc_u64*)sums, (cvl_bf16*)dz, (cvl_bf16*)g_out,
