@@ -800,9 +800,10 @@ extern "C" int cvl_conv_igemm_dgrad_bnsum_res(const cvl_conv_desc* d, const void
   if (!cvl_tune_flag("CVL_NO_BNSUM_FUSE") && !cvl_tune_flag("CVL_NO_BNSUM_RES") && d->prec == CVL_PREC_BF16 &&
       d->mode == CVL_CONV_DGRAD && !d->dst_f32 && d->beta != 0.f && d->KH == 1 && d->KW == 1 &&
       (d->stride == 1 || !cvl_dispatch_flag("no_bnsum_res_s2")) &&
-      // small maps: the fused launch (64-wide N tiles, three prefetched operands) loses to the
-      // plain one + the separate pass (A/B per stage; CVL_BNSUM_RES_MIN_HW)
-      (long)d->seg[0].Hr * d->seg[0].Wr >= cvl_dispatch_int("bnsum_res_min_hw", 4096) &&
+      // map-size floor (dispatch knob bnsum_res_min_hw): 4096 kept conv4_x / conv5_x on the plain
+      // launch + separate pass in round 5; after round 6's kernel changes 256 (all ResNet-50 stages at
+      // 512 px) wins, FCOS step same box 1381.1-1382.8 -> 1385.2-1388.6 img/s over 6 alternating runs
+      (long)d->seg[0].Hr * d->seg[0].Wr >= cvl_dispatch_int("bnsum_res_min_hw", 256) &&
       d->Cin % 32 == 0 && d->Npad % 32 == 0 && d->ld_dst % 8 == 0 && d->dst_coff % 8 == 0 && d->n_store % 8 == 0 &&
       src && dst) {
     // a strided 1x1 data gradient (a stage's first block accumulating onto its shortcut's) runs as the
