@@ -395,7 +395,7 @@ def test_dgrad_fused_bn_backward_residual(B, H, Cin, Cout, dispatch):
     first-pass sums within fp32 summation order, dz / g_out / dgamma / dbeta as the two-pass form."""
     from cvlite import ops_nn as nn
     from cvlite.layers import Conv, ParamStore
-    dispatch("bnsum_res_min_hw=0")     # production fuses only maps >= 64x64
+    dispatch("bnsum_res_min_hw=0")     # every map size (production floor: 256 px, i.e. conv5_x's 16x16 at 512)
     W = H
     C = Cout                     # block width: the BN3 channels = the next conv1's input channels
     dev = torch.device("cuda")
@@ -436,7 +436,7 @@ def test_dgrad_fused_bn_backward_residual(B, H, Cin, Cout, dispatch):
     torch.testing.assert_close(dz_f.float(), dz_p.float(), rtol=1e-2, atol=1e-2 * float(dz_p.float().abs().max()))
     torch.testing.assert_close(dg_f, dg_p, rtol=1e-5, atol=1e-5 * float(dg_p.abs().max()))
     torch.testing.assert_close(db_f, db_p, rtol=1e-5, atol=1e-5 * float(db_p.abs().max()))
-    if H * W < 4096:             # the production threshold: the plain path, sums untouched
+    if H * W < 4096:             # under a raised floor (round 5's 4096): the plain path, sums untouched
         dispatch("bnsum_res_min_hw=4096")
         sums2 = torch.zeros_like(sums)
         dx_2 = old.clone()
