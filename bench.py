@@ -196,7 +196,7 @@ def measure_backbone_3x3(net, B, H, W, iters=20, eager=False):
                       "counts from the ResNet-50 stage depths (3/4/6/3)", "per_shape": rows}
 
 
-PMC_FILE = "profiles/r06p_pmc_tower_conv.json"
+PMC_FILE = "profiles/r06z2_pmc_tower_conv.json"
 
 
 def pmc_traffic(kname):
